@@ -1,0 +1,313 @@
+#!/usr/bin/env python3
+"""nutexec benchmark — BASELINE.json metric:
+   "rows/sec filter->group-by on 1e9-row i64/f64; achieved HBM GB/s vs peak"
+
+Default workload (N=1): BASELINE config 4, the TPC-H Q1-shape filter -> group-by
+  SELECT l_returnflag, l_linestatus, sum(l_quantity), sum(l_extendedprice),
+         sum(l_extendedprice*(1-l_discount)), count(*)
+  FROM lineitem WHERE l_shipdate <= 10471 GROUP BY l_returnflag, l_linestatus
+on 1e9 rows per GPU (6 x 8 B columns = 48 GB resident in HBM).  With --gpus N
+(torchrun, one rank per GPU) every rank scans its own 1e9-row shard (weak scaling),
+pre-aggregates locally, exchanges partial groups by key hash with one RCCL
+all-to-all and merges the groups it owns; rank 0 gathers the final result.
+
+A "step" = one complete query over the resident columns (kernels + exchange + result
+to host).  Other configs: --workload groupby (config 3), filter (config 2).
+
+Prints ONE JSON line on rank 0 (contract in the task statement), with
+  roofline     — the dominant kernel's algorithmic bytes / its mean device time
+                 (hipEvents on the launch stream, via nut_ctx_kernel_time)
+  cpu_baseline — the C oracle (oracle/, OpenMP over the host cores) on a bounded
+                 sample of the same workload, rank 0 at N=1 only.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+METRIC = "rows/sec filter->group-by on 1e9-row i64/f64; achieved HBM GB/s vs peak"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--workload", default="q1", choices=["q1", "groupby", "filter"])
+    p.add_argument("--rows", type=float, default=None, help="rows per GPU (default: config size)")
+    p.add_argument("--groups", type=int, default=1000, help="groupby: distinct keys")
+    p.add_argument("--selectivity", type=float, default=0.5, help="filter: fraction selected")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline work")
+    return p.parse_args()
+
+
+# ------------------------------------------------------------------ workloads
+class Q1:
+    name = "tpch_q1_shape_filter_groupby"
+    cols_bytes = 48
+
+    def __init__(self, ex, rows, row0):
+        from nutdb_amd.workloads import Q1_COLS, Q1_DATE_K, gen
+        self.ex = ex
+        self.k = Q1_DATE_K
+        self.cols = [gen(ex, spec, rows, row0=row0) for spec in Q1_COLS]
+        self.rows = rows
+
+    def local(self):
+        return self.ex.q1(*self.cols, date_k=self.k)
+
+    def merge_query(self, seg):
+        from nutdb_amd import Agg, AggQuery
+        # partial record: rf, ls, sum_qty, sum_price, sum_disc_price, count
+        return AggQuery(keys=[seg[0].contiguous(), seg[1].contiguous()],
+                        values=[seg[2].contiguous().view(torch.float64), seg[3].contiguous().view(torch.float64),
+                                seg[4].contiguous().view(torch.float64), seg[5].contiguous()],
+                        aggs=[Agg("sum", "col", (0,)), Agg("sum", "col", (1,)), Agg("sum", "col", (2,)),
+                              Agg("sum", "col", (3,))])
+
+    kernel_kind = 1
+    groups_hint = 8
+
+    def config(self):
+        return {"workload": self.name, "query": "TPC-H Q1 shape: WHERE l_shipdate <= 10471, GROUP BY "
+                "l_returnflag, l_linestatus, 3 x SUM(f64) + COUNT(*)", "columns": "6 x 8 B (i64/f64)",
+                "groups": 6, "selectivity": 0.973, "bytes_per_row": 48}
+
+
+class GroupBy:
+    name = "groupby_i64_sum_f64"
+    cols_bytes = 16
+    kernel_kind = 1
+
+    def __init__(self, ex, rows, row0, groups):
+        from nutdb_amd.workloads import groupby_cols, gen
+        self.ex = ex
+        self.G = groups
+        self.groups_hint = groups
+        self.key, self.val = [gen(ex, spec, rows, row0=row0) for spec in groupby_cols(groups, dyadic=True)]
+        self.rows = rows
+
+    def local(self):
+        from nutdb_amd import Agg, AggQuery
+        return self.ex.groupby(AggQuery(keys=[self.key], values=[self.val], aggs=[Agg("sum", "col", (0,))]),
+                               group_hint=self.G)
+
+    def merge_query(self, seg):
+        from nutdb_amd import Agg, AggQuery
+        return AggQuery(keys=[seg[0].contiguous()], values=[seg[1].contiguous().view(torch.float64)],
+                        aggs=[Agg("sum", "col", (0,))])
+
+    def config(self):
+        return {"workload": self.name, "query": "SELECT key, SUM(val) FROM t GROUP BY key", "groups": self.G,
+                "columns": "i64 key + f64 val (dyadic)", "bytes_per_row": 16}
+
+
+class Filter:
+    name = "filter_i64_compaction"
+    kernel_kind = 0
+
+    def __init__(self, ex, rows, row0, sel):
+        from nutdb_amd.workloads import FILTER_COL, filter_k, gen
+        self.ex = ex
+        self.col = gen(ex, FILTER_COL, rows, row0=row0)
+        self.k = filter_k(sel)
+        self.sel = sel
+        self.out = torch.empty(rows, dtype=torch.int64, device=ex.device)
+        self.out_n = torch.zeros(1, dtype=torch.int64, device=ex.device)
+        self.rows = rows
+        self.cols_bytes = 8 + 8 * sel
+
+    def run(self):
+        self.ex.filter_i64_async(self.col, "<", self.k, self.out, self.out_n)
+
+    def config(self):
+        return {"workload": self.name, "query": "SELECT col FROM t WHERE col < k", "selectivity": self.sel,
+                "bytes_per_row": 8 + 8 * self.sel}
+
+
+# ------------------------------------------------------------------ one step
+def groupby_step(w, rank, world, group):
+    """Local scan -> (N>1) all-to-all of partial groups by owner -> owner merge ->
+    gather to rank 0.  Returns the number of result groups on rank 0."""
+    g = w.local()
+    if world == 1:
+        keys, _ = g.to_host_words()
+        n = len(keys)
+        g.free()
+        return n
+    ex = w.ex
+    buf, counts = g.partition(world)
+    width = g.nkeys + g.naggs
+    g.free()
+    send = torch.tensor(counts, dtype=torch.int64, device=ex.device)
+    recv = torch.empty_like(send)
+    dist.all_to_all_single(recv, send, group=group)
+    rc = recv.tolist()
+    out = torch.empty(width * sum(rc), dtype=torch.int64, device=ex.device)
+    dist.all_to_all_single(out, buf, [width * c for c in rc], [width * c for c in counts], group=group)
+    owner = None
+    off = 0
+    for c in rc:
+        if c:
+            seg = out[width * off: width * (off + c)].view(width, c)
+            q = w.merge_query(seg)
+            if owner is None:
+                owner = ex.groupby(q, group_hint=w.groups_hint)
+            else:
+                ex.accumulate(q, owner)
+        off += c
+    mine = owner.to_device() if owner is not None else torch.empty((width, 0), dtype=torch.int64,
+                                                                    device=ex.device)
+    if owner is not None:
+        owner.free()
+    # gather the owners' groups to rank 0 (padded all_gather: groups are few)
+    cnt = torch.tensor([mine.shape[1]], dtype=torch.int64, device=ex.device)
+    cnts = [torch.empty_like(cnt) for _ in range(world)]
+    dist.all_gather(cnts, cnt, group=group)
+    mx = max(int(c.item()) for c in cnts)
+    pad = torch.zeros((width, max(mx, 1)), dtype=torch.int64, device=ex.device)
+    pad[:, : mine.shape[1]] = mine
+    bufs = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(bufs, pad, group=group)
+    total = sum(int(c.item()) for c in cnts)
+    return total
+
+
+# ------------------------------------------------------------------ CPU baseline
+def cpu_baseline(args, workload: str, target_s: float):
+    from oracle import oracle as orc
+    from nutdb_amd.workloads import FILTER_COL, Q1_COLS, Q1_DATE_K, filter_k, groupby_cols
+    threads = orc.max_threads()
+
+    def run(n):
+        if workload == "q1":
+            sd, rf, ls, qty, price, disc = [orc.gen(s, n) for s in Q1_COLS]
+            t0 = time.perf_counter()
+            orc.groupby([rf, ls], [(0, 0, (0,)), (0, 0, (1,)), (0, 4, (1, 2)), (1, 0, ())],
+                        values=[qty, price, disc], preds=[(sd, 1, Q1_DATE_K)], cap=64)
+            return time.perf_counter() - t0
+        if workload == "groupby":
+            key, val = [orc.gen(s, n) for s in groupby_cols(args.groups, dyadic=True)]
+            t0 = time.perf_counter()
+            orc.groupby([key], [(0, 0, (0,))], values=[val], cap=max(args.groups, 1))
+            return time.perf_counter() - t0
+        col = orc.gen(FILTER_COL, n)
+        t0 = time.perf_counter()
+        orc.filter_i64(col, 0, filter_k(args.selectivity))
+        return time.perf_counter() - t0
+
+    n = 4_000_000
+    dt = run(n)
+    per_row = dt / n
+    sample = int(min(max(target_s / max(per_row, 1e-12), n), 1e9 if workload != "filter" else 1e8, 6e8))
+    dt = run(sample)
+    return {"value": sample / dt, "unit": "rows/s", "cores": threads, "kind": "port",
+            "sample": f"{sample:.3g} rows of the same synthetic workload, C oracle (oracle/oracle.c) "
+                      f"with OpenMP over {threads} host threads, generation excluded, {dt:.2f} s"}
+
+
+# ------------------------------------------------------------------ main
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            print("bench.py: --gpus N>1 must be launched with torch.distributed.run", file=sys.stderr)
+            sys.exit(2)
+    torch.cuda.set_device(local_rank)
+    group = None
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        group = dist.group.WORLD
+    from nutdb_amd import Executor
+    ex = Executor(local_rank)
+    default_rows = {"q1": 1e9, "groupby": 1e9, "filter": 1e8}[args.workload]
+    rows = int(args.rows or default_rows)
+    row0 = rank * rows
+    if args.workload == "q1":
+        w = Q1(ex, rows, row0)
+    elif args.workload == "groupby":
+        w = GroupBy(ex, rows, row0, args.groups)
+    else:
+        w = Filter(ex, rows, row0, args.selectivity)
+    torch.cuda.synchronize()
+
+    def step():
+        if args.workload == "filter":
+            w.run()
+        else:
+            groupby_step(w, rank, world, group)
+
+    for _ in range(args.warmup):
+        step()
+    ex.enable_timing(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms, launches = ex.kernel_time(w.kernel_kind)
+    ex.enable_timing(False)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=ex.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_step = elapsed * 1e3 / args.steps
+    total_rows = rows * world * args.steps
+    value = total_rows / elapsed
+    avg_kernel_ms = kern_ms / max(launches, 1)
+    bytes_per_launch = w.cols_bytes * rows
+    achieved = bytes_per_launch / (avg_kernel_ms * 1e-3) / 1e9 if launches else None
+    # PMC-measured HBM traffic of the same kernel/config, if profiled (profiles/pmc_*.json)
+    traffic = None
+    pmc = ROOT / "profiles" / f"pmc_{w.name}.json"
+    if pmc.exists():
+        try:
+            d = json.loads(pmc.read_text())
+            if int(d.get("rows", -1)) == rows:
+                traffic = d.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    if rank == 0:
+        cfg = w.config()
+        cfg.update({"rows_per_gpu": rows, "parallelism": f"dp{world} (row shards; key-hash all-to-all of "
+                    "partial groups over RCCL)" if world > 1 else "single GPU", "gpu": ex.info()["name"],
+                    "kernel_launches": launches, "avg_kernel_ms": avg_kernel_ms})
+        line = {
+            "metric": METRIC, "value": value, "unit": "rows/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "i64+f64", "data": "synthetic (counter-based splitmix64 columns "
+            "generated in HBM)", "config": cfg,
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(args, args.workload, args.cpu_seconds)
+        print(json.dumps(line), flush=True)
+    ex.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,208 @@
+/*
+ * nutexec.h — C ABI of the MI355X-native columnar executor for NutDB.
+ *
+ * Drop-in boundary.  The reference crate (nutdb v0.1.0) stops at
+ * `Parser::parse(sql) -> Result<Statement, ParseError>` (src/parser/mod.rs:26-29) and
+ * has NO executor, plugin registry or FFI to slot behind; its AST nodes
+ *   QueryBody.r#where   src/parser/ast/query.rs:30   (WhereClause, :68-72)
+ *   QueryBody.group_by  src/parser/ast/query.rs:31   (GroupByClause, :74-78)
+ *   QueryBody.columns   src/parser/ast/query.rs:25   (FnCall sum/count/min/max, expr.rs:32-36)
+ *   QueryBody.order_by  src/parser/ast/query.rs:33   (OrderByClause, :86-90)
+ * are what an executor lowers from.  Every entry point below is therefore the
+ * replacement for an interface the reference does not yet have; each names the
+ * AST node(s) it executes.  The Rust binding a maintainer would add is in
+ * INTEGRATION.md.
+ *
+ * Conventions
+ *  - Plain C: no C++ or torch types cross this boundary.
+ *  - Column pointers are DEVICE pointers (HBM-resident columns; hipMalloc'd or
+ *    torch-allocated) unless a parameter says "_host".
+ *  - The caller owns column and output buffers; the library owns its scratch and
+ *    the nut_groups result objects (freed by nut_groups_free).
+ *  - Calls are ordered on the context's stream (nut_ctx_set_stream; default: a
+ *    stream the context creates).  Entry points that return a host-visible value
+ *    synchronise that stream before returning; "_async" variants do not.
+ *  - Status is an int enum (0 = NUT_OK); nut_last_error() is a thread-local
+ *    message describing the last failure on this thread (like the reference's
+ *    thiserror messages, src/parser/error.rs:8-57).
+ *  - One context per host thread per device.
+ */
+#ifndef NUTEXEC_H
+#define NUTEXEC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NUTEXEC_ABI_VERSION 1
+
+typedef enum {
+  NUT_OK = 0,
+  NUT_ERR_INVALID_ARG = 1,
+  NUT_ERR_HIP = 2,          /* HIP runtime / launch failure */
+  NUT_ERR_OOM = 3,
+  NUT_ERR_UNSUPPORTED = 4,  /* valid request outside what the kernels implement */
+  NUT_ERR_CAPACITY = 5,     /* caller-provided output too small */
+  NUT_ERR_PARSE = 6,        /* SQL rejected by the front end (LexError/SyntaxError) */
+  NUT_ERR_PLAN = 7,         /* SQL parsed but cannot be lowered to an executor plan */
+  NUT_ERR_TIMEOUT = 8       /* a bounded device-side spin expired (never expected) */
+} nut_status;
+
+typedef struct nut_ctx nut_ctx;
+typedef struct nut_groups nut_groups;
+
+int nut_abi_version(void);
+const char *nut_last_error(void);
+
+nut_status nut_ctx_create(int device, nut_ctx **out);
+void nut_ctx_destroy(nut_ctx *ctx);
+/* hip_stream is a hipStream_t (e.g. torch.cuda.current_stream().cuda_stream); NULL
+ * restores the context's own stream. */
+nut_status nut_ctx_set_stream(nut_ctx *ctx, void *hip_stream);
+nut_status nut_ctx_sync(nut_ctx *ctx);
+/* number of CUs and device name, for reports */
+nut_status nut_ctx_info(nut_ctx *ctx, int *num_cus, char *name, size_t name_len);
+
+/* Device-side timing of the hot kernels (hipEvents recorded on the context's
+ * stream around each launch), for benchmarks and roofline reports.
+ * nut_ctx_kernel_time returns the total ms and launch count of one kernel kind
+ * since the previous call (or since timing was enabled) and resets them. */
+typedef enum {
+  NUT_KERNEL_FILTER = 0,     /* filter scan + compaction          */
+  NUT_KERNEL_AGGREGATE = 1,  /* fused filter/group-by/aggregate   */
+  NUT_KERNEL_SORT = 2        /* all radix-sort passes of one sort */
+} nut_kernel_kind;
+nut_status nut_ctx_enable_timing(nut_ctx *ctx, int enable);
+nut_status nut_ctx_kernel_time(nut_ctx *ctx, int kind, double *total_ms, uint64_t *launches);
+
+/* ------------------------------------------------------------------------
+ * Synthetic columns (bench / tests): counter-based splitmix64 generator,
+ * bit-identical to oracle/oracle.c orc_gen_column and numpy
+ * (tests/golden/make_golden.py).  u = mix64(seed + (row0+i+1) * 0x9E3779B97F4A7C15).
+ * ------------------------------------------------------------------------ */
+typedef enum {
+  NUT_GEN_U62 = 0,       /* int64: u >> 2                         */
+  NUT_GEN_FULL_I64 = 1,  /* int64: u                              */
+  NUT_GEN_POOL_KEY = 2,  /* int64: mix64((u % a) ^ 0x5DEECE66D2545F49) — a distinct keys */
+  NUT_GEN_DYADIC = 3,    /* f64: (u >> 44) / 64                   */
+  NUT_GEN_UNIT_F64 = 4,  /* f64: (u >> 11) * 2^-53                */
+  NUT_GEN_RANGE_I64 = 5, /* int64: a + u % b                      */
+  NUT_GEN_RANGE_F64 = 6  /* f64: (double)(a + u % b) / c          */
+} nut_gen_kind;
+
+nut_status nut_gen_column(nut_ctx *ctx, int kind, uint64_t seed, int64_t a, int64_t b,
+                          double c, uint64_t row0, uint64_t n, void *out);
+
+/* ------------------------------------------------------------------------
+ * Filter scan + selection-vector compaction (BASELINE config 2)
+ *   SELECT col FROM t WHERE col <cmp> k
+ * Lowered from WhereClause{BinaryOp{Identifier, op, Literal::Integer}}
+ * (src/parser/ast/query.rs:68-72, expr.rs:25-30, item.rs:89-101).
+ * Output keeps row order.  `out` must hold n elements (worst case).
+ * ------------------------------------------------------------------------ */
+typedef enum { NUT_LT = 0, NUT_LE = 1, NUT_GT = 2, NUT_GE = 3, NUT_EQ = 4, NUT_NE = 5 } nut_cmp;
+
+nut_status nut_filter_i64(nut_ctx *ctx, const int64_t *col, uint64_t n, int cmp, int64_t k,
+                          int64_t *out, uint64_t *out_n_host);
+/* as above; the count is written to device memory out_n_dev, no synchronisation */
+nut_status nut_filter_i64_async(nut_ctx *ctx, const int64_t *col, uint64_t n, int cmp,
+                                int64_t k, int64_t *out, uint64_t *out_n_dev);
+
+/* ------------------------------------------------------------------------
+ * Fused filter -> hash group-by -> aggregate (BASELINE configs 3 and 4)
+ *   SELECT k1[,k2], agg(expr)... FROM t WHERE p1 AND p2 ... GROUP BY k1[,k2]
+ * Lowered from WhereClause (AND-chain of `col op literal`), GroupByClause.keys
+ * (identifiers) and the SELECT list's FnCall{Others("sum"|"count"|"min"|"max")}.
+ * ------------------------------------------------------------------------ */
+typedef enum { NUT_T_I64 = 0, NUT_T_F64 = 1 } nut_type;
+typedef enum { NUT_AGG_SUM = 0, NUT_AGG_COUNT = 1, NUT_AGG_MIN = 2, NUT_AGG_MAX = 3 } nut_agg_op;
+typedef enum {
+  NUT_EX_COL = 0,       /* v[a]                      (i64 or f64 column) */
+  NUT_EX_MUL = 1,       /* v[a] * v[b]               (f64)               */
+  NUT_EX_ADD = 2,       /* v[a] + v[b]                                   */
+  NUT_EX_SUB = 3,       /* v[a] - v[b]                                   */
+  NUT_EX_MUL_1M = 4,    /* v[a] * (1 - v[b])         (TPC-H disc_price)  */
+  NUT_EX_MUL_1M_1P = 5  /* v[a] * (1 - v[b]) * (1 + v[c])  (charge)      */
+} nut_expr;
+
+#define NUT_MAX_KEYS 2
+#define NUT_MAX_PRED 4
+#define NUT_MAX_VALS 4
+#define NUT_MAX_AGGS 8
+
+typedef struct {
+  uint64_t n;                          /* rows */
+  int32_t nkeys;                       /* 1..2 int64 key columns */
+  const int64_t *keys[NUT_MAX_KEYS];
+  int32_t npred;                       /* conjunction of npred terms (0 = no WHERE) */
+  const void *pred_col[NUT_MAX_PRED];
+  int32_t pred_type[NUT_MAX_PRED];     /* nut_type */
+  int32_t pred_op[NUT_MAX_PRED];       /* nut_cmp */
+  int64_t pred_i64[NUT_MAX_PRED];      /* constant when pred_type == NUT_T_I64 */
+  double pred_f64[NUT_MAX_PRED];       /* constant when pred_type == NUT_T_F64 */
+  int32_t nvals;                       /* value columns referenced by expressions */
+  const void *val_col[NUT_MAX_VALS];
+  int32_t val_type[NUT_MAX_VALS];      /* nut_type; expressions other than COL need f64 */
+  int32_t naggs;
+  int32_t agg_op[NUT_MAX_AGGS];        /* nut_agg_op */
+  int32_t agg_expr[NUT_MAX_AGGS];      /* nut_expr (ignored for COUNT) */
+  int32_t agg_arg[NUT_MAX_AGGS][3];    /* value-column indices of the expression */
+} nut_agg_spec;
+
+/* Result word per aggregate: f64 bits for SUM/MIN/MAX of an f64 expression,
+ * int64 for COUNT and for SUM/MIN/MAX of an int64 column (SUM wraps).
+ * MIN/MAX order f64 by the IEEE total order (-0 < +0).
+ *
+ * group_hint: expected number of groups (0 = unknown).  It sizes the on-chip
+ * table; a wrong hint costs speed, never correctness. */
+nut_status nut_groupby(nut_ctx *ctx, const nut_agg_spec *spec, uint64_t group_hint,
+                       nut_groups **out);
+/* Aggregate more rows (same spec shape) into an existing result, e.g. to merge
+ * the partial groups received from other ranks (NUT_AGG_COUNT partials are merged
+ * with NUT_AGG_SUM over an int64 column). */
+nut_status nut_groupby_accumulate(nut_ctx *ctx, const nut_agg_spec *spec, nut_groups *acc);
+
+nut_status nut_groups_size(nut_groups *g, uint64_t *n_groups);
+/* Copy to host sorted ascending by key tuple.  keys[g*nkeys+j], aggs[g*naggs+a].
+ * cap = capacity in groups; NUT_ERR_CAPACITY if too small. */
+nut_status nut_groups_to_host(nut_groups *g, int64_t *keys, uint64_t *aggs, uint64_t cap);
+/* Dense device copy, column-major: out_dev[w * n + g], w = 0..nkeys-1 keys then
+ * naggs aggregate words; needs (nkeys+naggs)*n words.  Unordered. */
+nut_status nut_groups_to_device(nut_groups *g, uint64_t *out_dev, uint64_t cap);
+/* Partition the groups by owner rank = mix64(key tuple) % nparts for the
+ * multi-GPU exchange: segment p (counts_host[p] groups) is stored column-major
+ * like nut_groups_to_device at word offset (nkeys+naggs) * sum_{q<p} counts[q]. */
+nut_status nut_groups_partition(nut_groups *g, int nparts, uint64_t *out_dev, uint64_t cap,
+                                uint64_t *counts_host);
+void nut_groups_free(nut_groups *g);
+
+/* Convenience forms named in SURVEY.md §8(b). */
+#define NUT_AGGMASK_SUM 1u
+#define NUT_AGGMASK_COUNT 2u
+#define NUT_AGGMASK_MIN 4u
+#define NUT_AGGMASK_MAX 8u
+/* SELECT key, [sum(val)], [count(*)], [min(val)], [max(val)] FROM t GROUP BY key */
+nut_status nut_groupby_i64_f64(nut_ctx *ctx, const int64_t *key, const double *val,
+                               uint64_t n, uint32_t agg_mask, uint64_t group_hint,
+                               nut_groups **out);
+/* TPC-H Q1 shape: SELECT returnflag, linestatus, sum(qty), sum(price),
+ *   sum(price*(1-disc)), count(*) FROM lineitem WHERE shipdate <= date_k
+ *   GROUP BY returnflag, linestatus */
+nut_status nut_q1(nut_ctx *ctx, const int64_t *shipdate, const int64_t *returnflag,
+                  const int64_t *linestatus, const double *qty, const double *price,
+                  const double *disc, uint64_t n, int64_t date_k, nut_groups **out);
+
+/* ------------------------------------------------------------------------
+ * Sort (BASELINE config 5): SELECT k FROM t ORDER BY k  (ascending int64)
+ * Lowered from OrderByClause (src/parser/ast/query.rs:86-90).  in and out may
+ * not alias.  Scratch is owned by the context.
+ * ------------------------------------------------------------------------ */
+nut_status nut_sort_i64(nut_ctx *ctx, const int64_t *in, int64_t *out, uint64_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NUTEXEC_H */

@@ -1,0 +1,121 @@
+"""ctypes binding of libnutexec.so — the C ABI declared in include/nutexec.h.
+
+This is the same binding a Rust host would write with `extern "C"`:
+plain integers, doubles and pointers.  The library is REQUIRED: if it is missing or
+fails to load, importing nutdb_amd raises — there is no CPU fallback anywhere in the
+product path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+# torch must own the HIP runtime before libnutexec.so resolves libamdhip64.so.7, so
+# that torch-allocated device pointers and the library share one runtime/context.
+import torch  # noqa: F401
+
+LIB_PATH = Path(os.environ.get("NUTEXEC_LIB", Path(__file__).resolve().parent / "libnutexec.so"))
+
+NUT_MAX_KEYS = 2
+NUT_MAX_PRED = 4
+NUT_MAX_VALS = 4
+NUT_MAX_AGGS = 8
+
+# nut_status
+NUT_OK = 0
+STATUS_NAMES = {
+    0: "NUT_OK", 1: "NUT_ERR_INVALID_ARG", 2: "NUT_ERR_HIP", 3: "NUT_ERR_OOM",
+    4: "NUT_ERR_UNSUPPORTED", 5: "NUT_ERR_CAPACITY", 6: "NUT_ERR_PARSE", 7: "NUT_ERR_PLAN",
+    8: "NUT_ERR_TIMEOUT",
+}
+
+# enums (include/nutexec.h)
+GEN_U62, GEN_FULL_I64, GEN_POOL_KEY, GEN_DYADIC, GEN_UNIT_F64, GEN_RANGE_I64, GEN_RANGE_F64 = range(7)
+LT, LE, GT, GE, EQ, NE = range(6)
+T_I64, T_F64 = 0, 1
+KERNEL_FILTER, KERNEL_AGGREGATE, KERNEL_SORT = 0, 1, 2
+AGG_SUM, AGG_COUNT, AGG_MIN, AGG_MAX = range(4)
+EX_COL, EX_MUL, EX_ADD, EX_SUB, EX_MUL_1M, EX_MUL_1M_1P = range(6)
+
+
+class NutAggSpec(C.Structure):
+    _fields_ = [
+        ("n", C.c_uint64),
+        ("nkeys", C.c_int32),
+        ("keys", C.c_void_p * NUT_MAX_KEYS),
+        ("npred", C.c_int32),
+        ("pred_col", C.c_void_p * NUT_MAX_PRED),
+        ("pred_type", C.c_int32 * NUT_MAX_PRED),
+        ("pred_op", C.c_int32 * NUT_MAX_PRED),
+        ("pred_i64", C.c_int64 * NUT_MAX_PRED),
+        ("pred_f64", C.c_double * NUT_MAX_PRED),
+        ("nvals", C.c_int32),
+        ("val_col", C.c_void_p * NUT_MAX_VALS),
+        ("val_type", C.c_int32 * NUT_MAX_VALS),
+        ("naggs", C.c_int32),
+        ("agg_op", C.c_int32 * NUT_MAX_AGGS),
+        ("agg_expr", C.c_int32 * NUT_MAX_AGGS),
+        ("agg_arg", (C.c_int32 * 3) * NUT_MAX_AGGS),
+    ]
+
+
+class NutError(RuntimeError):
+    def __init__(self, status: int, where: str, message: str):
+        self.status = status
+        self.name = STATUS_NAMES.get(status, f"status {status}")
+        super().__init__(f"{where}: {self.name}: {message}")
+
+
+# name -> (restype, argtypes)
+_P = C.c_void_p
+_U64 = C.c_uint64
+_I64 = C.c_int64
+_I32 = C.c_int
+SIGNATURES = {
+    "nut_abi_version": (_I32, []),
+    "nut_last_error": (C.c_char_p, []),
+    "nut_ctx_create": (_I32, [_I32, C.POINTER(_P)]),
+    "nut_ctx_destroy": (None, [_P]),
+    "nut_ctx_set_stream": (_I32, [_P, _P]),
+    "nut_ctx_sync": (_I32, [_P]),
+    "nut_ctx_info": (_I32, [_P, C.POINTER(_I32), C.c_char_p, C.c_size_t]),
+    "nut_ctx_enable_timing": (_I32, [_P, _I32]),
+    "nut_ctx_kernel_time": (_I32, [_P, _I32, C.POINTER(C.c_double), C.POINTER(_U64)]),
+    "nut_gen_column": (_I32, [_P, _I32, _U64, _I64, _I64, C.c_double, _U64, _U64, _P]),
+    "nut_filter_i64": (_I32, [_P, _P, _U64, _I32, _I64, _P, C.POINTER(_U64)]),
+    "nut_filter_i64_async": (_I32, [_P, _P, _U64, _I32, _I64, _P, _P]),
+    "nut_groupby": (_I32, [_P, C.POINTER(NutAggSpec), _U64, C.POINTER(_P)]),
+    "nut_groupby_accumulate": (_I32, [_P, C.POINTER(NutAggSpec), _P]),
+    "nut_groups_size": (_I32, [_P, C.POINTER(_U64)]),
+    "nut_groups_to_host": (_I32, [_P, _P, _P, _U64]),
+    "nut_groups_to_device": (_I32, [_P, _P, _U64]),
+    "nut_groups_partition": (_I32, [_P, _I32, _P, _U64, C.POINTER(_U64)]),
+    "nut_groups_free": (None, [_P]),
+    "nut_groupby_i64_f64": (_I32, [_P, _P, _P, _U64, C.c_uint32, _U64, C.POINTER(_P)]),
+    "nut_q1": (_I32, [_P, _P, _P, _P, _P, _P, _P, _U64, _I64, C.POINTER(_P)]),
+    "nut_sort_i64": (_I32, [_P, _P, _P, _U64]),
+}
+
+
+def _load() -> C.CDLL:
+    if not LIB_PATH.exists():
+        raise ImportError(
+            f"nutdb_amd: {LIB_PATH} is missing — build it with `python -m nutdb_amd.build` "
+            "(hipcc --offload-arch=gfx950). There is no CPU fallback."
+        )
+    lib = C.CDLL(str(LIB_PATH), mode=C.RTLD_GLOBAL)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)  # AttributeError here = ABI mismatch, fail loudly
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+def check(status: int, where: str) -> None:
+    if status != NUT_OK:
+        msg = lib.nut_last_error()
+        raise NutError(status, where, msg.decode() if msg else "")

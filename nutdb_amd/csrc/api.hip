@@ -1,0 +1,227 @@
+// api.hip — context lifecycle, error reporting and the synthetic column source.
+#include <stdio.h>
+#include <string.h>
+
+#include "common.hpp"
+
+namespace nut {
+
+static thread_local std::string g_last_error;
+
+void set_error(const std::string &msg) { g_last_error = msg; }
+
+nut_status fail(nut_status st, const std::string &msg) {
+  g_last_error = msg;
+  return st;
+}
+
+nut_status hip_fail(hipError_t e, const char *what) {
+  g_last_error = std::string(what) + ": " + hipGetErrorName(e) + " (" + hipGetErrorString(e) + ")";
+  return e == hipErrorOutOfMemory ? NUT_ERR_OOM : NUT_ERR_HIP;
+}
+
+nut_status Scratch::reserve(size_t need) {
+  if (need <= bytes) return NUT_OK;
+  if (ptr) (void)hipFree(ptr);
+  ptr = nullptr;
+  bytes = 0;
+  size_t want = need + need / 4;
+  hipError_t e = hipMalloc(&ptr, want);
+  if (e != hipSuccess) {
+    ptr = nullptr;
+    return hip_fail(e, "hipMalloc(scratch)");
+  }
+  bytes = want;
+  return NUT_OK;
+}
+
+void Scratch::release() {
+  if (ptr) (void)hipFree(ptr);
+  ptr = nullptr;
+  bytes = 0;
+}
+
+// ------------------------------------------------------------ kernel timer
+hipEvent_t KernelTimer::get() {
+  if (!pool.empty()) {
+    hipEvent_t e = pool.back();
+    pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+
+void KernelTimer::begin(hipStream_t s, int kind) {
+  if (!enabled) return;
+  Pair p{get(), get(), kind};
+  if (p.a) (void)hipEventRecord(p.a, s);
+  pending.push_back(p);
+}
+
+void KernelTimer::end(hipStream_t s) {
+  if (!enabled || pending.empty()) return;
+  if (pending.back().b) (void)hipEventRecord(pending.back().b, s);
+}
+
+nut_status KernelTimer::drain() {
+  for (auto &p : pending) {
+    if (p.a && p.b) {
+      NUT_HIP(hipEventSynchronize(p.b));
+      float ms = 0.f;
+      NUT_HIP(hipEventElapsedTime(&ms, p.a, p.b));
+      total_ms[p.kind] += ms;
+      launches[p.kind] += 1;
+    }
+    if (p.a) pool.push_back(p.a);
+    if (p.b) pool.push_back(p.b);
+  }
+  pending.clear();
+  return NUT_OK;
+}
+
+void KernelTimer::release() {
+  (void)drain();
+  for (auto e : pool) (void)hipEventDestroy(e);
+  pool.clear();
+}
+
+// ------------------------------------------------------------ generator kernel
+__global__ void gen_column_kernel(int kind, uint64_t seed, int64_t a, int64_t b, double c,
+                                  uint64_t row0, uint64_t n, void *out) {
+  uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  int64_t *oi = (int64_t *)out;
+  double *od = (double *)out;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    uint64_t u = gen_u64(seed, row0 + i);
+    switch (kind) {
+      case NUT_GEN_U62: oi[i] = (int64_t)(u >> 2); break;
+      case NUT_GEN_FULL_I64: oi[i] = (int64_t)u; break;
+      case NUT_GEN_POOL_KEY: oi[i] = (int64_t)mix64((u % (uint64_t)a) ^ kPoolSalt); break;
+      case NUT_GEN_DYADIC: od[i] = (double)(u >> 44) / 64.0; break;
+      case NUT_GEN_UNIT_F64: od[i] = (double)(u >> 11) * 0x1p-53; break;
+      case NUT_GEN_RANGE_I64: oi[i] = a + (int64_t)(u % (uint64_t)b); break;
+      default: od[i] = (double)(a + (int64_t)(u % (uint64_t)b)) / c; break;
+    }
+  }
+}
+
+}  // namespace nut
+
+using namespace nut;
+
+extern "C" {
+
+int nut_abi_version(void) { return NUTEXEC_ABI_VERSION; }
+
+const char *nut_last_error(void) { return g_last_error.c_str(); }
+
+nut_status nut_ctx_create(int device, nut_ctx **out) {
+  if (!out) return fail(NUT_ERR_INVALID_ARG, "nut_ctx_create: out is NULL");
+  *out = nullptr;
+  int ndev = 0;
+  NUT_HIP(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev)
+    return fail(NUT_ERR_INVALID_ARG, "nut_ctx_create: device " + std::to_string(device) +
+                                         " out of range (" + std::to_string(ndev) + " devices)");
+  DeviceGuard g(device);
+  hipDeviceProp_t prop;
+  NUT_HIP(hipGetDeviceProperties(&prop, device));
+  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(NUT_ERR_UNSUPPORTED, std::string("nutexec is built for gfx950 (MI355X); device is ") +
+                                         prop.gcnArchName);
+  nut_ctx *c = new nut_ctx();
+  c->device = device;
+  c->num_cus = prop.multiProcessorCount;
+  snprintf(c->name, sizeof(c->name), "%s", prop.name);
+  hipError_t e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    delete c;
+    return hip_fail(e, "hipStreamCreate");
+  }
+  c->stream = c->own_stream;
+  e = hipHostMalloc((void **)&c->host_pinned, 4096, hipHostMallocDefault);
+  if (e != hipSuccess) {
+    (void)hipStreamDestroy(c->own_stream);
+    delete c;
+    return hip_fail(e, "hipHostMalloc");
+  }
+  *out = c;
+  return NUT_OK;
+}
+
+void nut_ctx_destroy(nut_ctx *c) {
+  if (!c) return;
+  DeviceGuard g(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  c->filter_state.release();
+  c->sort_tmp.release();
+  c->misc.release();
+  c->timer.release();
+  if (c->host_pinned) (void)hipHostFree(c->host_pinned);
+  if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+  delete c;
+}
+
+nut_status nut_ctx_set_stream(nut_ctx *c, void *s) {
+  if (!c) return fail(NUT_ERR_INVALID_ARG, "nut_ctx_set_stream: ctx is NULL");
+  c->stream = s ? (hipStream_t)s : c->own_stream;
+  return NUT_OK;
+}
+
+nut_status nut_ctx_sync(nut_ctx *c) {
+  if (!c) return fail(NUT_ERR_INVALID_ARG, "nut_ctx_sync: ctx is NULL");
+  DeviceGuard g(c->device);
+  NUT_HIP(hipStreamSynchronize(c->stream));
+  return NUT_OK;
+}
+
+nut_status nut_ctx_enable_timing(nut_ctx *c, int enable) {
+  if (!c) return fail(NUT_ERR_INVALID_ARG, "nut_ctx_enable_timing: ctx is NULL");
+  DeviceGuard g(c->device);
+  nut_status st = c->timer.drain();
+  c->timer.enabled = enable != 0;
+  for (int k = 0; k < 4; ++k) c->timer.total_ms[k] = 0, c->timer.launches[k] = 0;
+  return st;
+}
+
+nut_status nut_ctx_kernel_time(nut_ctx *c, int kind, double *total_ms, uint64_t *launches) {
+  if (!c || kind < 0 || kind > 3) return fail(NUT_ERR_INVALID_ARG, "nut_ctx_kernel_time: bad argument");
+  DeviceGuard g(c->device);
+  nut_status st = c->timer.drain();
+  if (st) return st;
+  if (total_ms) *total_ms = c->timer.total_ms[kind];
+  if (launches) *launches = c->timer.launches[kind];
+  c->timer.total_ms[kind] = 0;
+  c->timer.launches[kind] = 0;
+  return NUT_OK;
+}
+
+nut_status nut_ctx_info(nut_ctx *c, int *num_cus, char *name, size_t name_len) {
+  if (!c) return fail(NUT_ERR_INVALID_ARG, "nut_ctx_info: ctx is NULL");
+  if (num_cus) *num_cus = c->num_cus;
+  if (name && name_len) snprintf(name, name_len, "%s", c->name);
+  return NUT_OK;
+}
+
+nut_status nut_gen_column(nut_ctx *c, int kind, uint64_t seed, int64_t a, int64_t b, double cc,
+                          uint64_t row0, uint64_t n, void *out) {
+  if (!c || (!out && n)) return fail(NUT_ERR_INVALID_ARG, "nut_gen_column: NULL argument");
+  if (kind < NUT_GEN_U62 || kind > NUT_GEN_RANGE_F64)
+    return fail(NUT_ERR_INVALID_ARG, "nut_gen_column: unknown kind " + std::to_string(kind));
+  if ((kind == NUT_GEN_POOL_KEY && a <= 0) ||
+      ((kind == NUT_GEN_RANGE_I64 || kind == NUT_GEN_RANGE_F64) && b <= 0))
+    return fail(NUT_ERR_INVALID_ARG, "nut_gen_column: empty range");
+  if (n == 0) return NUT_OK;
+  DeviceGuard g(c->device);
+  uint64_t blocks = (n + 255) / 256;
+  uint64_t cap = (uint64_t)c->num_cus * 16;
+  if (blocks > cap) blocks = cap;
+  hipLaunchKernelGGL(gen_column_kernel, dim3((unsigned)blocks), dim3(256), 0, c->stream, kind,
+                     seed, a, b, cc, row0, n, out);
+  NUT_HIP(hipGetLastError());
+  return NUT_OK;
+}
+
+}  // extern "C"

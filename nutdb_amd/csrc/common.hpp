@@ -1,0 +1,168 @@
+// common.hpp — device helpers and host-side context shared by the nutexec kernels.
+// MI355X (gfx950, CDNA4) only: wave64, 256 CUs in 8 XCDs, 160 KiB LDS per CU.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/nutexec.h"
+
+namespace nut {
+
+// ---------------------------------------------------------------- constants
+constexpr int kWave = 64;
+constexpr uint64_t kGolden = 0x9E3779B97F4A7C15ull;
+constexpr uint64_t kPoolSalt = 0x5DEECE66D2545F49ull;
+constexpr uint64_t kEmpty = 0x8000000000000000ull;  // hash-table empty fingerprint
+
+// ---------------------------------------------------------------- hashing
+__host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__host__ __device__ __forceinline__ uint64_t gen_u64(uint64_t seed, uint64_t row) {
+  return mix64(seed + (row + 1) * kGolden);
+}
+// owner rank of a group for the multi-GPU exchange
+__host__ __device__ __forceinline__ uint64_t owner_hash(uint64_t k1, uint64_t k2, int nk) {
+  uint64_t h = mix64(k1 ^ 0x6A09E667F3BCC908ull);
+  if (nk == 2) h = mix64(h ^ k2);
+  return h;
+}
+// 2-key fingerprint (not injective: the table verifies the tuple)
+__device__ __forceinline__ uint64_t fp2(uint64_t k1, uint64_t k2) {
+  uint64_t f = mix64(k1 ^ mix64(k2 + kGolden));
+  return f == kEmpty ? (kEmpty ^ 1ull) : f;
+}
+// multiply-shift slot index
+__device__ __forceinline__ uint32_t slot_of(uint64_t fp, int log2cap) {
+  return (uint32_t)((fp * kGolden) >> (64 - log2cap));
+}
+
+// IEEE total order on f64 bit patterns, mapped to an unsigned integer order
+__host__ __device__ __forceinline__ uint64_t f64_to_ord(uint64_t b) {
+  return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+__host__ __device__ __forceinline__ uint64_t ord_to_f64(uint64_t o) {
+  return (o >> 63) ? (o & 0x7FFFFFFFFFFFFFFFull) : ~o;
+}
+
+__device__ __forceinline__ double as_f64(uint64_t b) { return __longlong_as_double((long long)b); }
+__device__ __forceinline__ uint64_t as_u64(double d) { return (uint64_t)__double_as_longlong(d); }
+
+// number of set bits of `mask` below this lane (v_mbcnt)
+__device__ __forceinline__ uint32_t lane_rank(uint64_t mask) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                   __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// relaxed agent-scope atomics (global_load/store ... sc1): single 8-byte granules
+__device__ __forceinline__ uint64_t ld_agent(const uint64_t *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent(uint64_t *p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ bool cmp_i64(int64_t v, int op, int64_t k) {
+  switch (op) {
+    case NUT_LT: return v < k;
+    case NUT_LE: return v <= k;
+    case NUT_GT: return v > k;
+    case NUT_GE: return v >= k;
+    case NUT_EQ: return v == k;
+    default: return v != k;
+  }
+}
+__device__ __forceinline__ bool cmp_f64(double v, int op, double k) {
+  switch (op) {
+    case NUT_LT: return v < k;
+    case NUT_LE: return v <= k;
+    case NUT_GT: return v > k;
+    case NUT_GE: return v >= k;
+    case NUT_EQ: return v == k;
+    default: return v != k;
+  }
+}
+
+typedef int64_t i64x2 __attribute__((ext_vector_type(2)));
+typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+
+// ---------------------------------------------------------------- host side
+void set_error(const std::string &msg);
+nut_status fail(nut_status st, const std::string &msg);
+nut_status hip_fail(hipError_t e, const char *what);
+
+#define NUT_HIP(call)                                  \
+  do {                                                 \
+    hipError_t e_ = (call);                            \
+    if (e_ != hipSuccess) return ::nut::hip_fail(e_, #call); \
+  } while (0)
+
+// Device scratch that only grows; reused across calls (no malloc in steady state).
+struct Scratch {
+  void *ptr = nullptr;
+  size_t bytes = 0;
+  nut_status reserve(size_t need);
+  void release();
+};
+
+}  // namespace nut
+
+namespace nut {
+// hipEvent pairs around hot-kernel launches (only while timing is enabled)
+struct KernelTimer {
+  struct Pair {
+    hipEvent_t a, b;
+    int kind;
+  };
+  bool enabled = false;
+  std::vector<Pair> pending;
+  std::vector<hipEvent_t> pool;
+  double total_ms[4] = {0, 0, 0, 0};
+  uint64_t launches[4] = {0, 0, 0, 0};
+  hipEvent_t get();
+  void begin(hipStream_t s, int kind);
+  void end(hipStream_t s);
+  nut_status drain();
+  void release();
+};
+}  // namespace nut
+
+struct nut_ctx {
+  int device = 0;
+  int num_cus = 256;
+  char name[64] = {0};
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  nut::Scratch filter_state;  // tile counter + look-back status words
+  nut::Scratch sort_tmp;      // sort ping-pong + histograms
+  nut::Scratch misc;
+  uint64_t *host_pinned = nullptr;  // small pinned staging for counts/flags
+  nut::KernelTimer timer;
+};
+
+namespace nut {
+// RAII device guard: switch to ctx->device for the call, restore afterwards.
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+}  // namespace nut

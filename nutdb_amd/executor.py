@@ -1,0 +1,293 @@
+"""Host-side executor API over the nutexec C ABI.
+
+Mirrors what the reference's AST hands an executor:
+  WhereClause      (src/parser/ast/query.rs:68-72)  -> predicates  [(column, op, literal)]
+  GroupByClause    (src/parser/ast/query.rs:74-78)  -> keys        [column, column]
+  SELECT FnCall    (src/parser/ast/expr.rs:32-36)   -> aggregates  [(op, expr, args)]
+  OrderByClause    (src/parser/ast/query.rs:86-90)  -> sort_i64
+Columns are torch tensors resident on the GPU (HBM); torch is only the allocator and
+stream provider.  Every operator runs a hand-written HIP kernel in libnutexec.so.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+from typing import Sequence
+
+import numpy as np
+import torch
+
+from . import _lib as L
+from ._lib import check, lib
+
+CMP = {"<": L.LT, "<=": L.LE, ">": L.GT, ">=": L.GE, "=": L.EQ, "==": L.EQ, "!=": L.NE, "<>": L.NE}
+AGG = {"sum": L.AGG_SUM, "count": L.AGG_COUNT, "min": L.AGG_MIN, "max": L.AGG_MAX}
+EXPR = {"col": L.EX_COL, "mul": L.EX_MUL, "add": L.EX_ADD, "sub": L.EX_SUB,
+        "mul_1m": L.EX_MUL_1M, "mul_1m_1p": L.EX_MUL_1M_1P}
+
+
+def _dtype_code(t: torch.Tensor) -> int:
+    if t.dtype == torch.int64:
+        return L.T_I64
+    if t.dtype == torch.float64:
+        return L.T_F64
+    raise TypeError(f"nutexec columns are int64 or float64, got {t.dtype}")
+
+
+def _col(t: torch.Tensor, dev: torch.device) -> int:
+    if t.device != dev:
+        raise ValueError(f"column on {t.device}, executor on {dev}")
+    if not t.is_contiguous() or t.dim() != 1:
+        raise ValueError("columns must be contiguous 1-D tensors")
+    return t.data_ptr()
+
+
+@dataclass
+class Agg:
+    op: str                      # sum | count | min | max
+    expr: str = "col"            # col | mul | add | sub | mul_1m | mul_1m_1p
+    args: Sequence[int] = ()     # indices into AggQuery.values
+
+
+@dataclass
+class AggQuery:
+    """SELECT keys..., aggs... FROM t WHERE preds... GROUP BY keys..."""
+    keys: list
+    aggs: list
+    values: list = field(default_factory=list)
+    preds: list = field(default_factory=list)   # (column, op, literal)
+
+    def to_spec(self, dev: torch.device) -> L.NutAggSpec:
+        s = L.NutAggSpec()
+        n = int(self.keys[0].numel())
+        s.n = n
+        if not 1 <= len(self.keys) <= L.NUT_MAX_KEYS:
+            raise ValueError("1 or 2 group keys")
+        s.nkeys = len(self.keys)
+        for i, k in enumerate(self.keys):
+            if k.dtype != torch.int64:
+                raise TypeError("group keys are int64 columns")
+            if k.numel() != n:
+                raise ValueError("ragged columns")
+            s.keys[i] = _col(k, dev)
+        if len(self.preds) > L.NUT_MAX_PRED:
+            raise ValueError("too many predicate terms")
+        s.npred = len(self.preds)
+        for i, (col, op, lit) in enumerate(self.preds):
+            if col.numel() != n:
+                raise ValueError("ragged columns")
+            s.pred_col[i] = _col(col, dev)
+            s.pred_type[i] = _dtype_code(col)
+            s.pred_op[i] = CMP[op] if isinstance(op, str) else int(op)
+            if s.pred_type[i] == L.T_I64:
+                s.pred_i64[i] = int(lit)
+            else:
+                s.pred_f64[i] = float(lit)
+        if len(self.values) > L.NUT_MAX_VALS:
+            raise ValueError("too many value columns")
+        s.nvals = len(self.values)
+        for i, v in enumerate(self.values):
+            if v.numel() != n:
+                raise ValueError("ragged columns")
+            s.val_col[i] = _col(v, dev)
+            s.val_type[i] = _dtype_code(v)
+        if len(self.aggs) > L.NUT_MAX_AGGS:
+            raise ValueError("too many aggregates")
+        s.naggs = len(self.aggs)
+        for i, a in enumerate(self.aggs):
+            s.agg_op[i] = AGG[a.op]
+            s.agg_expr[i] = EXPR[a.expr]
+            for j, x in enumerate(a.args):
+                s.agg_arg[i][j] = int(x)
+        return s
+
+    def result_types(self) -> list:
+        """numpy dtype of each aggregate word (matches nutexec.h result words)."""
+        out = []
+        for a in self.aggs:
+            if a.op == "count":
+                out.append(np.int64)
+            elif a.expr == "col" and self.values[a.args[0]].dtype == torch.int64:
+                out.append(np.int64)
+            else:
+                out.append(np.float64)
+        return out
+
+
+class Groups:
+    """Library-owned group-by result (nut_groups*)."""
+
+    def __init__(self, ex: "Executor", handle: int, nkeys: int, types: list):
+        self.ex = ex
+        self.h = C.c_void_p(handle)
+        self.nkeys = nkeys
+        self.types = types
+
+    @property
+    def naggs(self) -> int:
+        return len(self.types)
+
+    def __len__(self) -> int:
+        n = C.c_uint64()
+        check(lib.nut_groups_size(self.h, C.byref(n)), "nut_groups_size")
+        return n.value
+
+    def to_host_words(self):
+        """(keys int64 [n, nkeys], aggs uint64 [n, naggs]) sorted by key tuple."""
+        n = len(self)
+        keys = np.zeros((n, self.nkeys), dtype=np.int64)
+        aggs = np.zeros((n, max(self.naggs, 1)), dtype=np.uint64)
+        check(lib.nut_groups_to_host(self.h, keys.ctypes.data, aggs.ctypes.data, n), "nut_groups_to_host")
+        return keys, aggs[:, : self.naggs]
+
+    def to_host(self):
+        """(keys int64 [n, nkeys], [per-aggregate numpy column with its natural dtype])."""
+        keys, words = self.to_host_words()
+        cols = [np.ascontiguousarray(words[:, i]).view(t) for i, t in enumerate(self.types)]
+        return keys, cols
+
+    def to_device(self) -> torch.Tensor:
+        """uint64-as-int64 tensor [nkeys+naggs, n] on the device, unordered."""
+        n = len(self)
+        w = self.nkeys + self.naggs
+        out = torch.empty((w, max(n, 1)), dtype=torch.int64, device=self.ex.device)
+        check(lib.nut_groups_to_device(self.h, out.data_ptr(), max(n, 1)), "nut_groups_to_device")
+        return out[:, :n] if n else out[:, :0]
+
+    def partition(self, nparts: int):
+        """Device buffer of nparts column-major segments + per-part group counts."""
+        n = len(self)
+        w = self.nkeys + self.naggs
+        buf = torch.empty(max(w * n, 1), dtype=torch.int64, device=self.ex.device)
+        counts = (C.c_uint64 * nparts)()
+        check(lib.nut_groups_partition(self.h, nparts, buf.data_ptr(), max(n, 1), counts), "nut_groups_partition")
+        return buf[: w * n], [int(x) for x in counts]
+
+    def free(self) -> None:
+        if self.h:
+            lib.nut_groups_free(self.h)
+            self.h = C.c_void_p(None)
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class Executor:
+    """One nut_ctx bound to a GPU and to torch's current stream on it."""
+
+    def __init__(self, device: int | torch.device = 0):
+        dev = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
+        if dev.type != "cuda":
+            raise ValueError("nutexec runs on a GPU device (torch 'cuda' = HIP)")
+        if not torch.cuda.is_available():
+            raise RuntimeError("nutdb_amd: no GPU visible — the executor has no CPU fallback")
+        self.device = dev
+        h = C.c_void_p()
+        check(lib.nut_ctx_create(dev.index or 0, C.byref(h)), "nut_ctx_create")
+        self.ctx = h
+        self._bind_stream()
+
+    def _bind_stream(self):
+        s = torch.cuda.current_stream(self.device)
+        check(lib.nut_ctx_set_stream(self.ctx, C.c_void_p(s.cuda_stream)), "nut_ctx_set_stream")
+
+    def close(self):
+        if self.ctx:
+            lib.nut_ctx_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def info(self):
+        ncu = C.c_int()
+        name = C.create_string_buffer(64)
+        check(lib.nut_ctx_info(self.ctx, C.byref(ncu), name, 64), "nut_ctx_info")
+        return {"num_cus": ncu.value, "name": name.value.decode()}
+
+    def enable_timing(self, on: bool = True) -> None:
+        check(lib.nut_ctx_enable_timing(self.ctx, int(on)), "nut_ctx_enable_timing")
+
+    def kernel_time(self, kind: int):
+        """(total_ms, launches) of one hot-kernel kind since the last call (device events)."""
+        ms = C.c_double()
+        cnt = C.c_uint64()
+        check(lib.nut_ctx_kernel_time(self.ctx, kind, C.byref(ms), C.byref(cnt)), "nut_ctx_kernel_time")
+        return ms.value, cnt.value
+
+    def sync(self):
+        check(lib.nut_ctx_sync(self.ctx), "nut_ctx_sync")
+
+    # ---------------------------------------------------------------- data
+    def gen_column(self, kind: int, seed: int, n: int, row0: int = 0, a: int = 0, b: int = 0,
+                   c: float = 1.0, out: torch.Tensor | None = None) -> torch.Tensor:
+        dt = torch.float64 if kind in (L.GEN_DYADIC, L.GEN_UNIT_F64, L.GEN_RANGE_F64) else torch.int64
+        if out is None:
+            out = torch.empty(n, dtype=dt, device=self.device)
+        self._bind_stream()
+        check(lib.nut_gen_column(self.ctx, kind, seed & (2**64 - 1), a, b, c, row0, n,
+                                 C.c_void_p(out.data_ptr() if n else None)), "nut_gen_column")
+        return out
+
+    # ---------------------------------------------------------------- filter
+    def filter_i64(self, col: torch.Tensor, op: str | int, k: int, out: torch.Tensor | None = None) -> torch.Tensor:
+        if col.dtype != torch.int64:
+            raise TypeError("filter_i64 takes an int64 column")
+        n = col.numel()
+        if out is None:
+            out = torch.empty(max(n, 1), dtype=torch.int64, device=self.device)
+        self._bind_stream()
+        cnt = C.c_uint64()
+        check(lib.nut_filter_i64(self.ctx, C.c_void_p(_col(col, self.device) if n else None), n,
+                                 CMP[op] if isinstance(op, str) else int(op), int(k),
+                                 C.c_void_p(out.data_ptr()), C.byref(cnt)), "nut_filter_i64")
+        return out[: cnt.value]
+
+    def filter_i64_async(self, col: torch.Tensor, op, k: int, out: torch.Tensor, out_n: torch.Tensor) -> None:
+        self._bind_stream()
+        check(lib.nut_filter_i64_async(self.ctx, C.c_void_p(col.data_ptr()), col.numel(),
+                                       CMP[op] if isinstance(op, str) else int(op), int(k),
+                                       C.c_void_p(out.data_ptr()), C.c_void_p(out_n.data_ptr())),
+              "nut_filter_i64_async")
+
+    # ---------------------------------------------------------------- group-by
+    def groupby(self, q: AggQuery, group_hint: int = 0) -> Groups:
+        spec = q.to_spec(self.device)
+        self._bind_stream()
+        h = C.c_void_p()
+        check(lib.nut_groupby(self.ctx, C.byref(spec), group_hint, C.byref(h)), "nut_groupby")
+        return Groups(self, h.value, spec.nkeys, q.result_types())
+
+    def accumulate(self, q: AggQuery, acc: Groups) -> None:
+        spec = q.to_spec(self.device)
+        self._bind_stream()
+        check(lib.nut_groupby_accumulate(self.ctx, C.byref(spec), acc.h), "nut_groupby_accumulate")
+
+    def q1(self, shipdate, returnflag, linestatus, qty, price, disc, date_k: int = 10471) -> Groups:
+        n = shipdate.numel()
+        for t in (returnflag, linestatus, qty, price, disc):
+            if t.numel() != n:
+                raise ValueError("ragged columns")
+        self._bind_stream()
+        h = C.c_void_p()
+        ptrs = [C.c_void_p(_col(t, self.device)) for t in (shipdate, returnflag, linestatus, qty, price, disc)]
+        check(lib.nut_q1(self.ctx, *ptrs, n, int(date_k), C.byref(h)), "nut_q1")
+        return Groups(self, h.value, 2, [np.float64, np.float64, np.float64, np.int64])
+
+    # ---------------------------------------------------------------- sort
+    def sort_i64(self, col: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        if col.dtype != torch.int64:
+            raise TypeError("sort_i64 takes an int64 column")
+        n = col.numel()
+        if out is None:
+            out = torch.empty(n, dtype=torch.int64, device=self.device)
+        self._bind_stream()
+        check(lib.nut_sort_i64(self.ctx, C.c_void_p(_col(col, self.device) if n else None),
+                               C.c_void_p(out.data_ptr() if n else None), n), "nut_sort_i64")
+        return out

@@ -1,0 +1,50 @@
+"""Synthetic workloads of BASELINE.json configs 2-5.
+
+Every column is a pure function of (seed, global row index) through the counter-based
+splitmix64 generator, so any rank / shard / sample regenerates identical bits on the
+device (nut_gen_column), in the C oracle (orc_gen_column) and in numpy
+(tests/golden/make_golden.py).  Each entry: (name, nut_gen_kind, seed, a, b, c).
+"""
+from __future__ import annotations
+
+from . import _lib as L
+
+# config 2: SELECT col FROM t WHERE col < k     col uniform [0, 2^62)
+FILTER_COL = ("col", L.GEN_U62, 0x2A, 0, 0, 1.0)
+
+
+def filter_k(selectivity: float) -> int:
+    return int(selectivity * 2**62)
+
+
+# config 3: SELECT key, sum(val) ... GROUP BY key   key from a pool of G distinct i64
+GB_KEY_SEED = 0x51
+GB_VAL_SEED = 0x52
+
+
+def groupby_cols(groups: int, dyadic: bool = True):
+    return [
+        ("key", L.GEN_POOL_KEY, GB_KEY_SEED, groups, 0, 1.0),
+        ("val", L.GEN_DYADIC if dyadic else L.GEN_UNIT_F64, GB_VAL_SEED, 0, 0, 1.0),
+    ]
+
+
+# config 4: TPC-H Q1 shape (lineitem columns as i64 / f64)
+Q1_DATE_K = 10471  # l_shipdate <= date '1998-12-01' - interval '90' day, as days since 1970
+Q1_COLS = [
+    ("l_shipdate", L.GEN_RANGE_I64, 0x41, 8036, 2526, 1.0),        # [8036, 10561]
+    ("l_returnflag", L.GEN_RANGE_I64, 0x42, 0, 3, 1.0),             # {0,1,2} = A,N,R
+    ("l_linestatus", L.GEN_RANGE_I64, 0x43, 0, 2, 1.0),             # {0,1}   = F,O
+    ("l_quantity", L.GEN_RANGE_F64, 0x44, 1, 50, 1.0),              # 1..50
+    ("l_extendedprice", L.GEN_RANGE_F64, 0x45, 90000, 10404901, 100.0),  # 900.00..104949.00
+    ("l_discount", L.GEN_RANGE_F64, 0x46, 0, 11, 100.0),            # 0.00..0.10
+]
+
+# config 5: SELECT k FROM t ORDER BY k     full-range random i64
+SORT_COL = ("k", L.GEN_FULL_I64, 0x50, 0, 0, 1.0)
+
+
+def gen(ex, spec, n: int, row0: int = 0):
+    """Generate one column on ex's device."""
+    _, kind, seed, a, b, c = spec
+    return ex.gen_column(kind, seed, n, row0=row0, a=a, b=b, c=c)

@@ -1,0 +1,427 @@
+/*
+ * oracle.c — CPU restatement of the nutexec hot path.  TEST INFRASTRUCTURE ONLY
+ * (see oracle.h for who may load it and how it is pinned).
+ *
+ * Written as the plainest correct loops: one pass per operator, OpenMP over row
+ * chunks, per-thread hash tables merged at the end, Neumaier-compensated f64 sums.
+ * Nothing here shares code with nutdb_amd/csrc (the HIP product path).
+ *
+ * Anchors in the reference (the AST the executor consumes; /root/reference):
+ *   WHERE  -> src/parser/ast/query.rs:68-72 (WhereClause{condition: Expr})
+ *   GROUP  -> src/parser/ast/query.rs:74-78 (GroupByClause{keys})
+ *   SELECT -> src/parser/ast/query.rs:25 (columns) with FnCall sum/count/min/max
+ *             (src/parser/ast/expr.rs:32-36; names are FnName::Others, item.rs:164-179)
+ *   ORDER  -> src/parser/ast/query.rs:86-90 (OrderByClause)
+ * The operators themselves have no reference implementation.
+ */
+#include "oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+int orc_max_threads(void) {
+#ifdef _OPENMP
+  return omp_get_max_threads();
+#else
+  return 1;
+#endif
+}
+
+/* counter-based splitmix64 — identical bits in C, numpy, HIP. */
+uint64_t orc_mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+uint64_t orc_gen_u64(uint64_t seed, uint64_t row) {
+  return orc_mix64(seed + (row + 1) * 0x9E3779B97F4A7C15ull);
+}
+
+void orc_gen_column(int kind, uint64_t seed, int64_t a, int64_t b, double c,
+                    uint64_t row0, uint64_t n, void *out) {
+  int64_t *oi = (int64_t *)out;
+  double *od = (double *)out;
+#pragma omp parallel for schedule(static)
+  for (int64_t i = 0; i < (int64_t)n; ++i) {
+    uint64_t u = orc_gen_u64(seed, row0 + (uint64_t)i);
+    switch (kind) {
+      case ORC_GEN_U62: oi[i] = (int64_t)(u >> 2); break;
+      case ORC_GEN_FULL_I64: oi[i] = (int64_t)u; break;
+      case ORC_GEN_POOL_KEY: oi[i] = (int64_t)orc_mix64((u % (uint64_t)a) ^ ORC_POOL_SALT); break;
+      case ORC_GEN_DYADIC: od[i] = (double)(u >> 44) / 64.0; break;
+      case ORC_GEN_UNIT_F64: od[i] = (double)(u >> 11) * 0x1p-53; break;
+      case ORC_GEN_RANGE_I64: oi[i] = a + (int64_t)(u % (uint64_t)b); break;
+      case ORC_GEN_RANGE_F64: od[i] = (double)(a + (int64_t)(u % (uint64_t)b)) / c; break;
+      default: oi[i] = 0;
+    }
+  }
+}
+
+/* ------------------------------------------------------------------ filter */
+static int cmp_i64(int64_t v, int op, int64_t k) {
+  switch (op) {
+    case ORC_LT: return v < k;
+    case ORC_LE: return v <= k;
+    case ORC_GT: return v > k;
+    case ORC_GE: return v >= k;
+    case ORC_EQ: return v == k;
+    default: return v != k;
+  }
+}
+static int cmp_f64(double v, int op, double k) {
+  switch (op) {
+    case ORC_LT: return v < k;
+    case ORC_LE: return v <= k;
+    case ORC_GT: return v > k;
+    case ORC_GE: return v >= k;
+    case ORC_EQ: return v == k;
+    default: return v != k;
+  }
+}
+
+uint64_t orc_filter_i64(const int64_t *col, uint64_t n, int op, int64_t k, int64_t *out) {
+  int nt = orc_max_threads();
+  uint64_t *cnt = (uint64_t *)calloc((size_t)nt + 1, sizeof(uint64_t));
+  uint64_t chunk = (n + (uint64_t)nt - 1) / (uint64_t)nt;
+#pragma omp parallel num_threads(nt)
+  {
+#ifdef _OPENMP
+    int t = omp_get_thread_num();
+#else
+    int t = 0;
+#endif
+    uint64_t lo = (uint64_t)t * chunk, hi = lo + chunk > n ? n : lo + chunk;
+    uint64_t c = 0;
+    for (uint64_t i = lo; i < hi; ++i) c += (uint64_t)cmp_i64(col[i], op, k);
+    cnt[t + 1] = c;
+#pragma omp barrier
+#pragma omp single
+    for (int j = 0; j < nt; ++j) cnt[j + 1] += cnt[j];
+    uint64_t w = cnt[t];
+    if (out)
+      for (uint64_t i = lo; i < hi; ++i)
+        if (cmp_i64(col[i], op, k)) out[w++] = col[i];
+  }
+  uint64_t total = cnt[nt];
+  free(cnt);
+  return total;
+}
+
+/* ----------------------------------------------------------------- group-by */
+/* total order on f64 bit patterns (-0 < +0; NaN above +inf) — the documented
+ * MIN/MAX semantics of nutexec */
+static uint64_t f64_ord(double d) {
+  uint64_t b;
+  memcpy(&b, &d, 8);
+  return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+
+typedef struct {
+  int64_t k[2];
+  uint64_t w[8];   /* aggregate words */
+  double comp[8];  /* Neumaier compensation for f64 sums */
+  double sumf[8];  /* running f64 sum (kept as double to compensate) */
+} grp_t;
+
+typedef struct {
+  uint64_t cap, n;
+  int64_t *slot;   /* index into g, -1 empty */
+  grp_t *g;
+  uint64_t gcap;
+} table_t;
+
+static uint64_t hash_keys(const int64_t *k, int nk) {
+  uint64_t h = orc_mix64((uint64_t)k[0] ^ 0x243F6A8885A308D3ull);
+  if (nk == 2) h = orc_mix64(h ^ (uint64_t)k[1]);
+  return h;
+}
+
+static void tbl_init(table_t *t, uint64_t cap) {
+  t->cap = cap;
+  t->n = 0;
+  t->slot = (int64_t *)malloc(cap * sizeof(int64_t));
+  memset(t->slot, 0xff, cap * sizeof(int64_t));
+  t->gcap = cap / 2 + 1;
+  t->g = (grp_t *)malloc(t->gcap * sizeof(grp_t));
+}
+static void tbl_free(table_t *t) {
+  free(t->slot);
+  free(t->g);
+}
+
+static void grp_init(grp_t *g, const orc_agg_spec *s, const int64_t *k) {
+  g->k[0] = k[0];
+  g->k[1] = s->nkeys == 2 ? k[1] : 0;
+  for (int a = 0; a < s->naggs; ++a) {
+    g->comp[a] = 0.0;
+    g->sumf[a] = 0.0;
+    int isf = s->agg_op[a] != ORC_AGG_COUNT &&
+              !(s->agg_expr[a] == ORC_EX_COL && s->val_type[s->agg_arg[a][0]] == ORC_T_I64);
+    switch (s->agg_op[a]) {
+      case ORC_AGG_SUM: g->w[a] = 0; break;
+      case ORC_AGG_COUNT: g->w[a] = 0; break;
+      case ORC_AGG_MIN: g->w[a] = isf ? ~0ull : (uint64_t)INT64_MAX; break;
+      default: g->w[a] = isf ? 0ull : (uint64_t)INT64_MIN; break;
+    }
+  }
+}
+
+static grp_t *tbl_find(table_t *t, const orc_agg_spec *s, const int64_t *k);
+
+static void tbl_grow(table_t *t, const orc_agg_spec *s) {
+  uint64_t ncap = t->cap * 2;
+  int64_t *ns = (int64_t *)malloc(ncap * sizeof(int64_t));
+  memset(ns, 0xff, ncap * sizeof(int64_t));
+  for (uint64_t i = 0; i < t->n; ++i) {
+    uint64_t h = hash_keys(t->g[i].k, s->nkeys) & (ncap - 1);
+    while (ns[h] >= 0) h = (h + 1) & (ncap - 1);
+    ns[h] = (int64_t)i;
+  }
+  free(t->slot);
+  t->slot = ns;
+  t->cap = ncap;
+  t->gcap = ncap / 2 + 1;
+  t->g = (grp_t *)realloc(t->g, t->gcap * sizeof(grp_t));
+}
+
+static grp_t *tbl_find(table_t *t, const orc_agg_spec *s, const int64_t *k) {
+  uint64_t h = hash_keys(k, s->nkeys) & (t->cap - 1);
+  for (;;) {
+    int64_t idx = t->slot[h];
+    if (idx < 0) break;
+    grp_t *g = &t->g[idx];
+    if (g->k[0] == k[0] && (s->nkeys == 1 || g->k[1] == k[1])) return g;
+    h = (h + 1) & (t->cap - 1);
+  }
+  if (t->n + 1 > t->cap / 2) {
+    tbl_grow(t, s);
+    return tbl_find(t, s, k);
+  }
+  t->slot[h] = (int64_t)t->n;
+  grp_t *g = &t->g[t->n++];
+  grp_init(g, s, k);
+  return g;
+}
+
+static void neumaier_add(double *sum, double *comp, double x) {
+  double t = *sum + x;
+  if (fabs(*sum) >= fabs(x))
+    *comp += (*sum - t) + x;
+  else
+    *comp += (x - t) + *sum;
+  *sum = t;
+}
+
+static double eval_f64(const orc_agg_spec *s, int a, uint64_t i) {
+  const double *c0 = (const double *)s->val_col[s->agg_arg[a][0]];
+  double x = c0[i];
+  switch (s->agg_expr[a]) {
+    case ORC_EX_COL: return x;
+    case ORC_EX_MUL: return x * ((const double *)s->val_col[s->agg_arg[a][1]])[i];
+    case ORC_EX_ADD: return x + ((const double *)s->val_col[s->agg_arg[a][1]])[i];
+    case ORC_EX_SUB: return x - ((const double *)s->val_col[s->agg_arg[a][1]])[i];
+    case ORC_EX_MUL_1M: {
+      double b = ((const double *)s->val_col[s->agg_arg[a][1]])[i];
+      volatile double t = 1.0 - b; /* no contraction: exactly two roundings */
+      return x * t;
+    }
+    default: {
+      double b = ((const double *)s->val_col[s->agg_arg[a][1]])[i];
+      double c = ((const double *)s->val_col[s->agg_arg[a][2]])[i];
+      volatile double t1 = 1.0 - b;
+      volatile double t2 = x * t1;
+      volatile double t3 = 1.0 + c;
+      return t2 * t3;
+    }
+  }
+}
+
+static int row_passes(const orc_agg_spec *s, uint64_t i) {
+  for (int p = 0; p < s->npred; ++p) {
+    if (s->pred_type[p] == ORC_T_I64) {
+      if (!cmp_i64(((const int64_t *)s->pred_col[p])[i], s->pred_op[p], s->pred_i64[p])) return 0;
+    } else {
+      if (!cmp_f64(((const double *)s->pred_col[p])[i], s->pred_op[p], s->pred_f64[p])) return 0;
+    }
+  }
+  return 1;
+}
+
+static int agg_is_i64(const orc_agg_spec *s, int a) {
+  return s->agg_op[a] != ORC_AGG_COUNT && s->agg_expr[a] == ORC_EX_COL &&
+         s->val_type[s->agg_arg[a][0]] == ORC_T_I64;
+}
+
+static void grp_update(grp_t *g, const orc_agg_spec *s, uint64_t i) {
+  for (int a = 0; a < s->naggs; ++a) {
+    int op = s->agg_op[a];
+    if (op == ORC_AGG_COUNT) {
+      g->w[a] += 1;
+      continue;
+    }
+    if (agg_is_i64(s, a)) {
+      int64_t v = ((const int64_t *)s->val_col[s->agg_arg[a][0]])[i];
+      if (op == ORC_AGG_SUM) g->w[a] = g->w[a] + (uint64_t)v; /* wraps */
+      else if (op == ORC_AGG_MIN) { if (v < (int64_t)g->w[a]) g->w[a] = (uint64_t)v; }
+      else { if (v > (int64_t)g->w[a]) g->w[a] = (uint64_t)v; }
+      continue;
+    }
+    double v = eval_f64(s, a, i);
+    if (op == ORC_AGG_SUM) neumaier_add(&g->sumf[a], &g->comp[a], v);
+    else if (op == ORC_AGG_MIN) { uint64_t o = f64_ord(v); if (o < g->w[a]) g->w[a] = o; }
+    else { uint64_t o = f64_ord(v); if (o > g->w[a]) g->w[a] = o; }
+  }
+}
+
+static void grp_merge(grp_t *dst, const grp_t *src, const orc_agg_spec *s) {
+  for (int a = 0; a < s->naggs; ++a) {
+    int op = s->agg_op[a];
+    if (op == ORC_AGG_COUNT) { dst->w[a] += src->w[a]; continue; }
+    if (agg_is_i64(s, a)) {
+      if (op == ORC_AGG_SUM) dst->w[a] += src->w[a];
+      else if (op == ORC_AGG_MIN) { if ((int64_t)src->w[a] < (int64_t)dst->w[a]) dst->w[a] = src->w[a]; }
+      else { if ((int64_t)src->w[a] > (int64_t)dst->w[a]) dst->w[a] = src->w[a]; }
+      continue;
+    }
+    if (op == ORC_AGG_SUM) {
+      neumaier_add(&dst->sumf[a], &dst->comp[a], src->sumf[a]);
+      dst->comp[a] += src->comp[a];
+    } else if (op == ORC_AGG_MIN) { if (src->w[a] < dst->w[a]) dst->w[a] = src->w[a]; }
+    else { if (src->w[a] > dst->w[a]) dst->w[a] = src->w[a]; }
+  }
+}
+
+static int cmp_grp(const void *pa, const void *pb, void *nkp) {
+  const grp_t *a = (const grp_t *)pa, *b = (const grp_t *)pb;
+  int nk = *(int *)nkp;
+  if (a->k[0] != b->k[0]) return a->k[0] < b->k[0] ? -1 : 1;
+  if (nk == 2 && a->k[1] != b->k[1]) return a->k[1] < b->k[1] ? -1 : 1;
+  return 0;
+}
+
+static int g_sort_nk;
+static int cmp_grp_q(const void *a, const void *b) { return cmp_grp(a, b, &g_sort_nk); }
+
+uint64_t orc_groupby(const orc_agg_spec *s, uint64_t cap, int64_t *out_keys,
+                     uint64_t *out_aggs, int nthreads) {
+  int nt = nthreads > 0 ? nthreads : orc_max_threads();
+  table_t *tl = (table_t *)calloc((size_t)nt, sizeof(table_t));
+  uint64_t n = s->n, chunk = (n + (uint64_t)nt - 1) / (uint64_t)nt;
+#pragma omp parallel num_threads(nt)
+  {
+#ifdef _OPENMP
+    int t = omp_get_thread_num();
+#else
+    int t = 0;
+#endif
+    table_t *T = &tl[t];
+    tbl_init(T, 1024);
+    uint64_t lo = (uint64_t)t * chunk, hi = lo + chunk > n ? n : lo + chunk;
+    int64_t k[2] = {0, 0};
+    for (uint64_t i = lo; i < hi; ++i) {
+      if (!row_passes(s, i)) continue;
+      k[0] = s->keys[0][i];
+      if (s->nkeys == 2) k[1] = s->keys[1][i];
+      grp_update(tbl_find(T, s, k), s, i);
+    }
+  }
+  table_t *G = &tl[0];
+  for (int t = 1; t < nt; ++t) {
+    for (uint64_t i = 0; i < tl[t].n; ++i) {
+      grp_t *src = &tl[t].g[i];
+      /* find-or-create in G, then merge */
+      uint64_t before = G->n;
+      grp_t *dst = tbl_find(G, s, src->k);
+      (void)before;
+      grp_merge(dst, src, s);
+    }
+    tbl_free(&tl[t]);
+  }
+  uint64_t ng = G->n;
+  if (ng > cap) {
+    tbl_free(G);
+    free(tl);
+    return UINT64_MAX;
+  }
+  g_sort_nk = s->nkeys;
+  qsort(G->g, ng, sizeof(grp_t), cmp_grp_q);
+  for (uint64_t i = 0; i < ng; ++i) {
+    grp_t *g = &G->g[i];
+    out_keys[i * (uint64_t)s->nkeys] = g->k[0];
+    if (s->nkeys == 2) out_keys[i * 2 + 1] = g->k[1];
+    for (int a = 0; a < s->naggs; ++a) {
+      uint64_t w = g->w[a];
+      int op = s->agg_op[a];
+      if (op != ORC_AGG_COUNT && !agg_is_i64(s, a)) {
+        double d;
+        if (op == ORC_AGG_SUM) {
+          d = g->sumf[a] + g->comp[a];
+        } else {
+          uint64_t b = (w >> 63) ? (w & 0x7FFFFFFFFFFFFFFFull) : ~w;
+          memcpy(&d, &b, 8);
+        }
+        memcpy(&w, &d, 8);
+      }
+      out_aggs[i * (uint64_t)s->naggs + a] = w;
+    }
+  }
+  tbl_free(G);
+  free(tl);
+  return ng;
+}
+
+/* --------------------------------------------------------------------- sort */
+void orc_sort_i64(const int64_t *in, int64_t *out, uint64_t n, int nthreads) {
+  int nt = nthreads > 0 ? nthreads : orc_max_threads();
+  uint64_t *a = (uint64_t *)malloc(n * sizeof(uint64_t));
+  uint64_t *b = (uint64_t *)malloc(n * sizeof(uint64_t));
+#pragma omp parallel for num_threads(nt)
+  for (int64_t i = 0; i < (int64_t)n; ++i) a[i] = (uint64_t)in[i] ^ 0x8000000000000000ull;
+  uint64_t *hist = (uint64_t *)malloc((size_t)nt * 256 * sizeof(uint64_t));
+  uint64_t chunk = (n + (uint64_t)nt - 1) / (uint64_t)nt;
+  for (int pass = 0; pass < 8; ++pass) {
+    int sh = pass * 8;
+#pragma omp parallel num_threads(nt)
+    {
+#ifdef _OPENMP
+      int t = omp_get_thread_num();
+#else
+      int t = 0;
+#endif
+      uint64_t *h = hist + (size_t)t * 256;
+      memset(h, 0, 256 * sizeof(uint64_t));
+      uint64_t lo = (uint64_t)t * chunk, hi = lo + chunk > n ? n : lo + chunk;
+      for (uint64_t i = lo; i < hi; ++i) h[(a[i] >> sh) & 255]++;
+#pragma omp barrier
+#pragma omp single
+      {
+        uint64_t run = 0;
+        for (int d = 0; d < 256; ++d)
+          for (int tt = 0; tt < nt; ++tt) {
+            uint64_t c = hist[(size_t)tt * 256 + d];
+            hist[(size_t)tt * 256 + d] = run;
+            run += c;
+          }
+      }
+      for (uint64_t i = lo; i < hi; ++i) b[h[(a[i] >> sh) & 255]++] = a[i];
+    }
+    uint64_t *tmp = a; a = b; b = tmp;
+  }
+#pragma omp parallel for num_threads(nt)
+  for (int64_t i = 0; i < (int64_t)n; ++i) out[i] = (int64_t)(a[i] ^ 0x8000000000000000ull);
+  free(hist);
+  free(a);
+  free(b);
+}
+
+uint64_t orc_multiset_hash_i64(const int64_t *v, uint64_t n) {
+  uint64_t h = 0;
+#pragma omp parallel for reduction(+ : h)
+  for (int64_t i = 0; i < (int64_t)n; ++i) h += orc_mix64((uint64_t)v[i] ^ 0xA0761D6478BD642Full);
+  return h;
+}

@@ -1,0 +1,97 @@
+/*
+ * oracle.h — CPU restatement of the nutexec hot path.  TEST INFRASTRUCTURE ONLY.
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load
+ * liboracle.so.  It is the checker, never the thing measured or shipped: the
+ * product path (nutdb_amd/, libnutexec.so) never links or calls it.
+ *
+ * Parity anchor.  The reference (nutdb v0.1.0, /root/reference) is a SQL front end
+ * only: there is NO scan / filter / group-by / sort implementation in it
+ * (SURVEY.md §0, §2 "ABSENT → build from scratch").  The semantics below are
+ * therefore defined by this build and pinned against independent
+ * third-party oracles run in the build container — numpy 2.2 (boolean-mask
+ * filter, np.sort), pyarrow 25 (Table.group_by().aggregate) and math.fsum
+ * (correctly-rounded f64 sums) — whose outputs are committed as fixtures under
+ * tests/golden/ by tests/golden/make_golden.py.  With respect to the reference
+ * itself, executor parity is "unpinned by construction" (SURVEY.md §8(c)).
+ *
+ * The literal inputs the reference does hand to the path (the WHERE constant of
+ * TPC-H Q1, AST shapes) are pinned by the front-end tests against the reference's
+ * own fixtures (tests/golden/sql/N.sql = /root/reference/tests/sql/N.sql).
+ */
+#ifndef NUT_ORACLE_H
+#define NUT_ORACLE_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- counter-based synthetic data (SURVEY.md §8(d) "splitmix64(seed ⊕ row)") ---- */
+uint64_t orc_mix64(uint64_t z);
+uint64_t orc_gen_u64(uint64_t seed, uint64_t row);
+
+/* column kinds, identical to include/nutexec.h nut_gen_kind */
+enum {
+  ORC_GEN_U62 = 0,       /* (int64) (u >> 2)                       uniform [0, 2^62)      */
+  ORC_GEN_FULL_I64 = 1,  /* (int64) u                              full-range i64        */
+  ORC_GEN_POOL_KEY = 2,  /* pool[u % a], pool[g] = (int64) mix64(g ^ POOL_SALT)         */
+  ORC_GEN_DYADIC = 3,    /* (double)(u >> 44) / 64.0               exact-sum f64         */
+  ORC_GEN_UNIT_F64 = 4,  /* (double)(u >> 11) * 2^-53              uniform [0,1) f64     */
+  ORC_GEN_RANGE_I64 = 5, /* a + (int64)(u % b)                     uniform [a, a+b)      */
+  ORC_GEN_RANGE_F64 = 6, /* (double)(a + (int64)(u % b)) / c       decimal-like f64      */
+};
+#define ORC_POOL_SALT 0x5DEECE66D2545F49ull
+void orc_gen_column(int kind, uint64_t seed, int64_t a, int64_t b, double c,
+                    uint64_t row0, uint64_t n, void *out);
+
+/* ---- filter: SELECT col FROM t WHERE col <op> k (row order preserved) ---- */
+enum { ORC_LT = 0, ORC_LE = 1, ORC_GT = 2, ORC_GE = 3, ORC_EQ = 4, ORC_NE = 5 };
+uint64_t orc_filter_i64(const int64_t *col, uint64_t n, int op, int64_t k, int64_t *out);
+
+/* ---- fused filter -> hash group-by -> aggregate (configs 3, 4) ----
+ * Mirrors include/nutexec.h nut_agg_spec field-for-field (plain ints + pointers). */
+enum { ORC_T_I64 = 0, ORC_T_F64 = 1 };
+enum { ORC_AGG_SUM = 0, ORC_AGG_COUNT = 1, ORC_AGG_MIN = 2, ORC_AGG_MAX = 3 };
+enum { ORC_EX_COL = 0, ORC_EX_MUL = 1, ORC_EX_ADD = 2, ORC_EX_SUB = 3,
+       ORC_EX_MUL_1M = 4,    /* a * (1 - b)           */
+       ORC_EX_MUL_1M_1P = 5  /* a * (1 - b) * (1 + c) */ };
+
+typedef struct {
+  uint64_t n;
+  int nkeys;                 /* 1 or 2 int64 key columns */
+  const int64_t *keys[2];
+  int npred;                 /* conjunction of npred terms */
+  const void *pred_col[4];
+  int pred_type[4];          /* ORC_T_* */
+  int pred_op[4];            /* ORC_LT.. */
+  int64_t pred_i64[4];
+  double pred_f64[4];
+  int nvals;                 /* value columns referenced by expressions */
+  const void *val_col[4];
+  int val_type[4];
+  int naggs;
+  int agg_op[8];             /* ORC_AGG_* */
+  int agg_expr[8];           /* ORC_EX_* */
+  int agg_arg[8][3];         /* value-column indices */
+} orc_agg_spec;
+
+/* Result: groups sorted ascending by key tuple.  Each aggregate is one 64-bit
+ * word: f64 bits for SUM/MIN/MAX over f64, int64 for COUNT and i64 SUM/MIN/MAX
+ * (i64 SUM wraps two's complement).  out_keys[g*nkeys + j], out_aggs[g*naggs + a].
+ * Returns number of groups, or UINT64_MAX if cap is too small.
+ * f64 sums are Neumaier-compensated (≈ correctly rounded). nthreads<=0: all cores. */
+uint64_t orc_groupby(const orc_agg_spec *spec, uint64_t cap, int64_t *out_keys,
+                     uint64_t *out_aggs, int nthreads);
+
+/* ---- sort: ascending int64 ---- */
+void orc_sort_i64(const int64_t *in, int64_t *out, uint64_t n, int nthreads);
+
+/* order-independent multiset hash (sum of mix64 of each element), for sort parity */
+uint64_t orc_multiset_hash_i64(const int64_t *v, uint64_t n);
+
+int orc_max_threads(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

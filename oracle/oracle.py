@@ -1,0 +1,156 @@
+"""ctypes binding of oracle/liboracle.so — TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this.
+It checks (or times, as the CPU baseline) the HIP product path; it never replaces it.
+See oracle/oracle.h for the semantics and how they are pinned.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+LIB_PATH = HERE / "liboracle.so"
+
+
+def build(force: bool = False) -> Path:
+    src = [HERE / "oracle.c", HERE / "oracle.h"]
+    if force or not LIB_PATH.exists() or any(p.stat().st_mtime > LIB_PATH.stat().st_mtime for p in src):
+        subprocess.run(["make", "-s", "-C", str(HERE)] + (["-B"] if force else []), check=True)
+    return LIB_PATH
+
+
+class OrcAggSpec(C.Structure):
+    _fields_ = [
+        ("n", C.c_uint64),
+        ("nkeys", C.c_int),
+        ("keys", C.c_void_p * 2),
+        ("npred", C.c_int),
+        ("pred_col", C.c_void_p * 4),
+        ("pred_type", C.c_int * 4),
+        ("pred_op", C.c_int * 4),
+        ("pred_i64", C.c_int64 * 4),
+        ("pred_f64", C.c_double * 4),
+        ("nvals", C.c_int),
+        ("val_col", C.c_void_p * 4),
+        ("val_type", C.c_int * 4),
+        ("naggs", C.c_int),
+        ("agg_op", C.c_int * 8),
+        ("agg_expr", C.c_int * 8),
+        ("agg_arg", (C.c_int * 3) * 8),
+    ]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = C.CDLL(str(LIB_PATH))
+        L.orc_mix64.restype = C.c_uint64
+        L.orc_mix64.argtypes = [C.c_uint64]
+        L.orc_gen_u64.restype = C.c_uint64
+        L.orc_gen_u64.argtypes = [C.c_uint64, C.c_uint64]
+        L.orc_gen_column.restype = None
+        L.orc_gen_column.argtypes = [C.c_int, C.c_uint64, C.c_int64, C.c_int64, C.c_double, C.c_uint64,
+                                     C.c_uint64, C.c_void_p]
+        L.orc_filter_i64.restype = C.c_uint64
+        L.orc_filter_i64.argtypes = [C.c_void_p, C.c_uint64, C.c_int, C.c_int64, C.c_void_p]
+        L.orc_groupby.restype = C.c_uint64
+        L.orc_groupby.argtypes = [C.POINTER(OrcAggSpec), C.c_uint64, C.c_void_p, C.c_void_p, C.c_int]
+        L.orc_sort_i64.restype = None
+        L.orc_sort_i64.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_int]
+        L.orc_multiset_hash_i64.restype = C.c_uint64
+        L.orc_multiset_hash_i64.argtypes = [C.c_void_p, C.c_uint64]
+        L.orc_max_threads.restype = C.c_int
+        _lib = L
+    return _lib
+
+
+F64_KINDS = (3, 4, 6)  # GEN_DYADIC, GEN_UNIT_F64, GEN_RANGE_F64
+
+
+def gen_column(kind, seed, n, row0=0, a=0, b=0, c=1.0) -> np.ndarray:
+    out = np.empty(n, dtype=np.float64 if kind in F64_KINDS else np.int64)
+    lib().orc_gen_column(kind, seed & (2**64 - 1), a, b, c, row0, n, out.ctypes.data if n else None)
+    return out
+
+
+def gen(spec, n, row0=0):
+    _, kind, seed, a, b, c = spec
+    return gen_column(kind, seed, n, row0=row0, a=a, b=b, c=c)
+
+
+def filter_i64(col: np.ndarray, op: int, k: int) -> np.ndarray:
+    col = np.ascontiguousarray(col, dtype=np.int64)
+    out = np.empty(max(len(col), 1), dtype=np.int64)
+    cnt = lib().orc_filter_i64(col.ctypes.data, len(col), op, k, out.ctypes.data)
+    return out[:cnt]
+
+
+def groupby(keys, aggs, values=(), preds=(), nthreads=0, cap=None):
+    """keys: list of int64 arrays; values: list of arrays; preds: (array, op_int, literal);
+    aggs: (op_int, expr_int, args).  Returns (keys [n, nk] int64, words [n, na] uint64)
+    sorted by key tuple."""
+    keep = []
+    s = OrcAggSpec()
+    n = len(keys[0])
+    s.n = n
+    s.nkeys = len(keys)
+    for i, k in enumerate(keys):
+        k = np.ascontiguousarray(k, dtype=np.int64)
+        keep.append(k)
+        s.keys[i] = k.ctypes.data
+    s.npred = len(preds)
+    for i, (col, op, lit) in enumerate(preds):
+        col = np.ascontiguousarray(col)
+        keep.append(col)
+        s.pred_col[i] = col.ctypes.data
+        s.pred_op[i] = op
+        if col.dtype == np.int64:
+            s.pred_type[i] = 0
+            s.pred_i64[i] = int(lit)
+        else:
+            s.pred_type[i] = 1
+            s.pred_f64[i] = float(lit)
+    s.nvals = len(values)
+    for i, v in enumerate(values):
+        v = np.ascontiguousarray(v)
+        keep.append(v)
+        s.val_col[i] = v.ctypes.data
+        s.val_type[i] = 0 if v.dtype == np.int64 else 1
+    s.naggs = len(aggs)
+    for i, (op, ex, args) in enumerate(aggs):
+        s.agg_op[i] = op
+        s.agg_expr[i] = ex
+        for j, x in enumerate(args):
+            s.agg_arg[i][j] = x
+    cap = cap if cap is not None else max(n, 1)
+    ok = np.empty((cap, s.nkeys), dtype=np.int64)
+    ow = np.empty((cap, max(s.naggs, 1)), dtype=np.uint64)
+    g = lib().orc_groupby(C.byref(s), cap, ok.ctypes.data, ow.ctypes.data, nthreads)
+    if g == 2**64 - 1:
+        raise ValueError("oracle group capacity too small")
+    return ok[:g], ow[:g, : s.naggs]
+
+
+def sort_i64(col: np.ndarray, nthreads=0) -> np.ndarray:
+    col = np.ascontiguousarray(col, dtype=np.int64)
+    out = np.empty_like(col)
+    if len(col):
+        lib().orc_sort_i64(col.ctypes.data, out.ctypes.data, len(col), nthreads)
+    return out
+
+
+def multiset_hash(v: np.ndarray) -> int:
+    v = np.ascontiguousarray(v, dtype=np.int64)
+    return int(lib().orc_multiset_hash_i64(v.ctypes.data if len(v) else None, len(v)))
+
+
+def max_threads() -> int:
+    return int(lib().orc_max_threads())

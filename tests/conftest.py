@@ -1,0 +1,51 @@
+import os
+import sys
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "tests"))
+
+
+def _build_native():
+    """Build libnutexec.so (hipcc, gfx950) and liboracle.so if missing or stale.
+    nutdb_amd/build.py is loaded by path: importing the package needs the library."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("_nut_build", ROOT / "nutdb_amd" / "build.py")
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    mod.build()
+    from oracle import oracle
+    oracle.build()
+
+
+def pytest_configure(config):
+    _build_native()
+    config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU; runs the HIP kernels")
+    config.addinivalue_line("markers", "slow: long-running")
+
+
+@pytest.fixture(scope="session")
+def golden():
+    import json
+    return json.loads((ROOT / "tests" / "golden" / "executor_golden.json").read_text())
+
+
+@pytest.fixture(scope="session")
+def orc():
+    from oracle import oracle
+    oracle.build()
+    return oracle
+
+
+@pytest.fixture(scope="session")
+def ex():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("GPU test selected but no GPU is visible")
+    from nutdb_amd import Executor
+    e = Executor(0)
+    yield e
+    e.close()

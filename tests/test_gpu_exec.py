@@ -1,0 +1,267 @@
+"""GPU parity: the HIP kernels (through the C ABI) vs the C oracle and the golden fixtures.
+
+Bit-exact for integer / index / count / min / max results and for f64 sums of dyadic
+values; f64 sums of non-dyadic values within F64_SUM_RTOL = 1e-12 relative
+(BASELINE.json north_star).
+"""
+import numpy as np
+import pytest
+import torch
+
+from helpers import F64_SUM_RTOL, OPCODE, fromhex, pos_hash, rel_err, wsum
+
+pytestmark = pytest.mark.gpu
+
+I64_MIN = np.iinfo(np.int64).min
+I64_MAX = np.iinfo(np.int64).max
+
+
+def dev(x, ex):
+    return torch.from_numpy(np.ascontiguousarray(x)).to(ex.device)
+
+
+def host(t):
+    return t.cpu().numpy()
+
+
+# ----------------------------------------------------------------------------- generator
+def test_generator(golden, ex):
+    for case in golden["generator"]:
+        v = host(ex.gen_column(case["kind"], case["seed"], case["n"], row0=case["row0"], a=case["a"],
+                               b=case["b"], c=case["c"]))
+        assert [int(x) for x in v[:8].view(np.uint64)] == case["head"]
+        assert wsum(v) == case["wsum"]
+
+
+# ----------------------------------------------------------------------------- filter
+def test_filter_golden(golden, ex):
+    n = golden["filter"][0]["n"]
+    col = ex.gen_column(0, 0x2A, n)
+    for case in golden["filter"]:
+        out = host(ex.filter_i64(col, case["op"], case["k"]))
+        assert len(out) == case["count"], case
+        assert [int(x) for x in out[:8]] == case["head"]
+        assert [int(x) for x in out[-8:]] == case["tail"]
+        assert pos_hash(out) == case["pos_hash"]
+
+
+@pytest.mark.parametrize("n", [0, 1, 2, 3, 511, 4095, 4096, 4097, 8191, 65536 + 3, 1_000_003])
+def test_filter_sizes_vs_oracle(ex, orc, n):
+    col = orc.gen_column(0, 0x2A, n)
+    d = dev(col, ex)
+    for s in (0.0, 0.3, 1.0):
+        k = int(s * 2**62)
+        for op in ("<", ">="):
+            got = host(ex.filter_i64(d, op, k))
+            want = orc.filter_i64(col, OPCODE[op], k)
+            assert np.array_equal(got, want), (n, s, op)
+
+
+def test_filter_extremes_and_unaligned(ex, orc):
+    rng = np.random.default_rng(7)
+    v = rng.integers(I64_MIN, I64_MAX, size=50_001, dtype=np.int64)
+    v[::97] = I64_MIN
+    v[::89] = I64_MAX
+    v[::5] = 42
+    d = dev(v, ex)
+    for op in OPCODE:
+        for k in (I64_MIN, -1, 0, 42, I64_MAX):
+            assert np.array_equal(host(ex.filter_i64(d, op, k)), orc.filter_i64(v, OPCODE[op], k)), (op, k)
+    # 8-byte aligned but not 16-byte aligned column (slice) takes the scalar-load path
+    got = host(ex.filter_i64(d[1:], "==", 42))
+    assert np.array_equal(got, orc.filter_i64(v[1:], OPCODE["=="], 42))
+
+
+def test_filter_large_property(ex, orc):
+    n = 100_000_000  # BASELINE config 2 size
+    col = ex.gen_column(0, 0x2A, n)
+    k = int(0.5 * 2**62)
+    out = ex.filter_i64(col, "<", k)
+    ref = orc.filter_i64(orc.gen_column(0, 0x2A, n), OPCODE["<"], k)
+    assert out.numel() == len(ref)
+    o = host(out)
+    assert np.array_equal(o, ref)
+
+
+# ----------------------------------------------------------------------------- group-by
+def gb_query(key, val, preds=()):
+    from nutdb_amd import Agg, AggQuery
+    return AggQuery(keys=[key], values=[val], preds=list(preds),
+                    aggs=[Agg("sum", "col", (0,)), Agg("count"), Agg("min", "col", (0,)), Agg("max", "col", (0,))])
+
+
+@pytest.mark.parametrize("idx", range(5))
+def test_groupby_golden(golden, ex, idx):
+    case = golden["groupby"][idx]
+    n, G = case["n"], case["G"]
+    key = ex.gen_column(2, 0x51, n, a=G)
+    val = ex.gen_column(3 if case["dyadic"] else 4, 0x52, n)
+    preds = [(val, "<", case["pred_val_lt"])] if case["pred_val_lt"] is not None else []
+    g = ex.groupby(gb_query(key, val, preds), group_hint=G)
+    keys, words = g.to_host_words()
+    assert [int(k) for k in keys[:, 0]] == case["keys"]
+    s = words[:, 0].view(np.float64)
+    fs = fromhex(case["sum_fsum"])
+    if case["dyadic"]:
+        assert np.array_equal(s, fs)
+    assert rel_err(s, fs) <= F64_SUM_RTOL
+    assert [int(x) for x in words[:, 1]] == case["count"]
+    assert np.array_equal(words[:, 2].view(np.float64), fromhex(case["min"]))
+    assert np.array_equal(words[:, 3].view(np.float64), fromhex(case["max"]))
+
+
+def check_vs_oracle(g, okeys, owords, types):
+    keys, words = g.to_host_words()
+    assert np.array_equal(keys, okeys)
+    for j, t in enumerate(types):
+        if t == "sum_f64":
+            assert rel_err(words[:, j].view(np.float64), owords[:, j].view(np.float64)) <= F64_SUM_RTOL
+        else:
+            assert np.array_equal(words[:, j], owords[:, j]), t
+
+
+AGGS4 = [(0, 0, (0,)), (1, 0, ()), (2, 0, (0,)), (3, 0, (0,))]
+
+
+@pytest.mark.parametrize("G,hint", [(1, 1), (16, 0), (1000, 1000), (1000, 0), (100_000, 100_000),
+                                    (100_000, 1000), (2_000_000, 2_000_000)])
+def test_groupby_cardinalities(ex, orc, G, hint):
+    n = 3_000_017
+    key = orc.gen_column(2, 0x51, n, a=G)
+    val = orc.gen_column(4, 0x52, n)
+    g = ex.groupby(gb_query(dev(key, ex), dev(val, ex)), group_hint=hint)
+    ok, ow = orc.groupby([key], AGGS4, values=[val])
+    assert len(g) == len(ok)
+    check_vs_oracle(g, ok, ow, ["sum_f64", "i", "i", "i"])
+
+
+def test_groupby_sentinel_and_extreme_keys(ex, orc):
+    rng = np.random.default_rng(3)
+    n = 200_000
+    pool = np.array([I64_MIN, I64_MAX, 0, -1, 1, 12345], dtype=np.int64)
+    key = pool[rng.integers(0, len(pool), n)]
+    val = rng.standard_normal(n)
+    val[::1000] = -0.0
+    g = ex.groupby(gb_query(dev(key, ex), dev(val, ex)), group_hint=8)
+    ok, ow = orc.groupby([key], AGGS4, values=[val])
+    check_vs_oracle(g, ok, ow, ["sum_f64", "i", "i", "i"])
+
+
+def test_groupby_i64_values_wrap(ex, orc):
+    from nutdb_amd import Agg, AggQuery
+    rng = np.random.default_rng(5)
+    n = 500_003
+    key = rng.integers(0, 37, n).astype(np.int64)
+    v = rng.integers(I64_MIN, I64_MAX, n, dtype=np.int64)
+    q = AggQuery(keys=[dev(key, ex)], values=[dev(v, ex)],
+                 aggs=[Agg("sum", "col", (0,)), Agg("min", "col", (0,)), Agg("max", "col", (0,)), Agg("count")])
+    g = ex.groupby(q, group_hint=37)
+    ok, ow = orc.groupby([key], [(0, 0, (0,)), (2, 0, (0,)), (3, 0, (0,)), (1, 0, ())], values=[v])
+    check_vs_oracle(g, ok, ow, ["i", "i", "i", "i"])
+
+
+def test_groupby_two_keys_preds_exprs(ex, orc):
+    from nutdb_amd import Agg, AggQuery
+    rng = np.random.default_rng(11)
+    n = 1_000_001
+    k1 = rng.integers(-3, 40, n).astype(np.int64)
+    k2 = rng.integers(0, 7, n).astype(np.int64) * 1_000_000_007
+    a = rng.random(n)
+    b = rng.random(n)
+    c = rng.random(n)
+    f = rng.integers(0, 100, n).astype(np.int64)
+    q = AggQuery(keys=[dev(k1, ex), dev(k2, ex)], values=[dev(a, ex), dev(b, ex), dev(c, ex)],
+                 preds=[(dev(f, ex), ">=", 10), (dev(a, ex), "<", 0.9)],
+                 aggs=[Agg("sum", "mul", (0, 1)), Agg("sum", "mul_1m_1p", (0, 1, 2)), Agg("min", "sub", (1, 2)),
+                       Agg("max", "add", (0, 2)), Agg("count"), Agg("sum", "mul_1m", (2, 0))])
+    g = ex.groupby(q, group_hint=300)
+    ok, ow = orc.groupby([k1, k2], [(0, 1, (0, 1)), (0, 5, (0, 1, 2)), (2, 3, (1, 2)), (3, 2, (0, 2)), (1, 0, ()),
+                                    (0, 4, (2, 0))],
+                         values=[a, b, c], preds=[(f, OPCODE[">="], 10), (a, OPCODE["<"], 0.9)])
+    check_vs_oracle(g, ok, ow, ["sum_f64", "sum_f64", "i", "i", "i", "sum_f64"])
+
+
+def test_groupby_empty_and_tiny(ex, orc):
+    for n in (0, 1, 2, 3):
+        key = np.arange(n, dtype=np.int64) % 2
+        val = np.arange(n, dtype=np.float64)
+        g = ex.groupby(gb_query(dev(key, ex), dev(val, ex)))
+        if n == 0:
+            assert len(g) == 0
+            continue
+        ok, ow = orc.groupby([key], AGGS4, values=[val])
+        check_vs_oracle(g, ok, ow, ["sum_f64", "i", "i", "i"])
+    # predicate that rejects everything
+    key = np.arange(1000, dtype=np.int64)
+    val = np.ones(1000)
+    g = ex.groupby(gb_query(dev(key, ex), dev(val, ex), [(dev(key, ex), "<", -5)]))
+    assert len(g) == 0
+
+
+def test_groupby_accumulate_and_partition(ex, orc):
+    """N virtual ranks on one GPU: local partials -> owner partition -> per-owner merge."""
+    from nutdb_amd import Agg, AggQuery
+    G, n, P = 5000, 2_000_003, 4
+    key = orc.gen_column(2, 0x51, n, a=G)
+    val = orc.gen_column(4, 0x52, n)
+    ok, ow = orc.groupby([key], AGGS4, values=[val])
+    shards = np.array_split(np.arange(n), P)
+    owners = [None] * P
+    for r in range(P):  # rank r's local pre-aggregation, partitioned by owner
+        sl = shards[r]
+        g = ex.groupby(gb_query(dev(key[sl], ex), dev(val[sl], ex)), group_hint=G)
+        buf, counts = g.partition(P)
+        w = 1 + 4
+        off = 0
+        for p in range(P):
+            seg = buf[w * off: w * (off + counts[p])].view(w, counts[p]) if counts[p] else None
+            off += counts[p]
+            if seg is None:
+                continue
+            kcol = seg[0].contiguous()
+            sums = seg[1].contiguous().view(torch.float64)
+            cnts = seg[2].contiguous()
+            mins = seg[3].contiguous().view(torch.float64)
+            maxs = seg[4].contiguous().view(torch.float64)
+            q = AggQuery(keys=[kcol], values=[sums, cnts, mins, maxs],
+                         aggs=[Agg("sum", "col", (0,)), Agg("sum", "col", (1,)), Agg("min", "col", (2,)),
+                               Agg("max", "col", (3,))])
+            if owners[p] is None:
+                owners[p] = ex.groupby(q, group_hint=G)
+            else:
+                ex.accumulate(q, owners[p])
+    parts = [o.to_host_words() for o in owners if o is not None]
+    keys = np.concatenate([p[0] for p in parts])
+    words = np.concatenate([p[1] for p in parts])
+    order = np.argsort(keys[:, 0], kind="stable")
+    keys, words = keys[order], words[order]
+    assert np.array_equal(keys, ok)
+    assert rel_err(words[:, 0].view(np.float64), ow[:, 0].view(np.float64)) <= F64_SUM_RTOL
+    assert np.array_equal(words[:, 1:], ow[:, 1:])
+
+
+# ----------------------------------------------------------------------------- Q1
+@pytest.mark.parametrize("idx", range(2))
+def test_q1_golden(golden, ex, idx):
+    from nutdb_amd.workloads import Q1_COLS, Q1_DATE_K, gen
+    case = golden["q1"][idx]
+    cols = [gen(ex, spec, case["n"], row0=case["row0"]) for spec in Q1_COLS]
+    g = ex.q1(*cols, date_k=Q1_DATE_K)
+    keys, words = g.to_host_words()
+    assert len(keys) == len(case["groups"])
+    for k, w, ref in zip(keys, words, case["groups"]):
+        assert (int(k[0]), int(k[1])) == (ref["returnflag"], ref["linestatus"])
+        assert int(w[3]) == ref["count"]
+        for j, name in enumerate(["sum_qty", "sum_price", "sum_disc_price"]):
+            assert rel_err([w[j:j + 1].view(np.float64)[0]], [float.fromhex(ref[name])]) <= F64_SUM_RTOL
+
+
+def test_q1_vs_oracle_large(ex, orc):
+    from nutdb_amd.workloads import Q1_COLS, Q1_DATE_K, gen
+    n = 20_000_011
+    cols_d = [gen(ex, spec, n) for spec in Q1_COLS]
+    g = ex.q1(*cols_d, date_k=Q1_DATE_K)
+    sd, rf, ls, qty, price, disc = [orc.gen(spec, n) for spec in Q1_COLS]
+    ok, ow = orc.groupby([rf, ls], [(0, 0, (0,)), (0, 0, (1,)), (0, 4, (1, 2)), (1, 0, ())],
+                         values=[qty, price, disc], preds=[(sd, OPCODE["<="], Q1_DATE_K)])
+    check_vs_oracle(g, ok, ow, ["sum_f64", "sum_f64", "sum_f64", "i"])
