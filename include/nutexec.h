@@ -60,7 +60,8 @@ const char *nut_last_error(void);
 nut_status nut_ctx_create(int device, nut_ctx **out);
 void nut_ctx_destroy(nut_ctx *ctx);
 /* hip_stream is a hipStream_t (e.g. torch.cuda.current_stream().cuda_stream); NULL
- * restores the context's own stream. */
+ * selects the device's default (null) stream.  A new context starts on a stream of
+ * its own. */
 nut_status nut_ctx_set_stream(nut_ctx *ctx, void *hip_stream);
 nut_status nut_ctx_sync(nut_ctx *ctx);
 /* number of CUs and device name, for reports */

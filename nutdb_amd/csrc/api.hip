@@ -166,7 +166,7 @@ void nut_ctx_destroy(nut_ctx *c) {
 
 nut_status nut_ctx_set_stream(nut_ctx *c, void *s) {
   if (!c) return fail(NUT_ERR_INVALID_ARG, "nut_ctx_set_stream: ctx is NULL");
-  c->stream = s ? (hipStream_t)s : c->own_stream;
+  c->stream = (hipStream_t)s;  // NULL is the device's default (null) stream, a valid target
   return NUT_OK;
 }
 

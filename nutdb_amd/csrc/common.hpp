@@ -74,6 +74,20 @@ __device__ __forceinline__ void st_agent(uint64_t *p, uint64_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Coherent read of a word that other workgroups update with memory-side atomics.
+// A plain or sc1 load can be served by this XCD's L2 from a line cached before the
+// update (measured: a spin on `atomicAdd(p, 0)`, which LLVM folds into a
+// `global_load sc1`, never saw another XCD's atomic swap).  A volatile RMW cannot be
+// folded and executes at the memory side.  (LLVM folds an idempotent fetch_or/add
+// into a load even through a volatile pointer; a compare-exchange whose swap value
+// equals its compare value is left alone and returns the current word unchanged.)
+__device__ __forceinline__ uint32_t rmw_load(uint32_t *p) {
+  return atomicCAS((unsigned int *)p, 0u, 0u);
+}
+__device__ __forceinline__ uint64_t rmw_load(uint64_t *p) {
+  return (uint64_t)atomicCAS((unsigned long long *)p, 0ull, 0ull);
+}
+
 __device__ __forceinline__ bool cmp_i64(int64_t v, int op, int64_t k) {
   switch (op) {
     case NUT_LT: return v < k;

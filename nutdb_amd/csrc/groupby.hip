@@ -157,7 +157,7 @@ __device__ __forceinline__ int64_t g_find(const GTable t, uint64_t fp, int64_t k
       if (NK == 1) return (int64_t)s;
       uint32_t spins = 0;
       bool timeout = false;
-      while (atomicAdd(&t.ready[s], 0u) == 0u) {
+      while (rmw_load(&t.ready[s]) == 0u) {
         __builtin_amdgcn_s_sleep(2);
         if (++spins > G_SPIN_LIMIT) {
           timeout = true;
@@ -168,8 +168,8 @@ __device__ __forceinline__ int64_t g_find(const GTable t, uint64_t fp, int64_t k
         atomicOr(&t.ctl[1], 2u);
         return -1;
       }
-      int64_t a = (int64_t)atomicAdd((unsigned long long *)&t.k1[s], 0ull);
-      int64_t b = (int64_t)atomicAdd((unsigned long long *)&t.k2[s], 0ull);
+      int64_t a = (int64_t)rmw_load((uint64_t *)&t.k1[s]);
+      int64_t b = (int64_t)rmw_load((uint64_t *)&t.k2[s]);
       if (a == k1 && b == k2) return (int64_t)s;
     }
     s = (s + 1) & (t.cap - 1);
