@@ -81,6 +81,7 @@ struct AggArgs {
   uint32_t lds_limit;
   uint32_t lds_arena;
   int32_t lds_log2;
+  int32_t vec;          // all columns 16-B aligned: vector loads
   const GTable *gt;     // device copy of the global table descriptor
 };
 
@@ -298,8 +299,13 @@ __device__ __forceinline__ bool row_pass(const AggArgs &p, const uint64_t (&pv)[
   return ok;
 }
 
-__device__ __forceinline__ u64x2 ld2(const void *col, uint64_t i) {
-  return *reinterpret_cast<const u64x2 *>((const uint64_t *)col + i);
+__device__ __forceinline__ u64x2 ld2(const void *col, uint64_t i, bool vec) {
+  const uint64_t *c = (const uint64_t *)col + i;
+  if (vec) return *reinterpret_cast<const u64x2 *>(c);  // uniform branch: 16-B aligned columns
+  u64x2 r;
+  r.x = c[0];
+  r.y = c[1];
+  return r;
 }
 __device__ __forceinline__ u64x2 ld2_tail(const void *col, uint64_t i, uint64_t n) {
   const uint64_t *c = (const uint64_t *)col;
@@ -319,12 +325,12 @@ template <int NK, bool TAIL>
 __device__ __forceinline__ void load_pair(const AggArgs &p, uint64_t i, Pair<NK> &x) {
 #pragma unroll
   for (int t = 0; t < NUT_MAX_PRED; ++t)
-    if (t < p.npred) x.pv[t] = TAIL ? ld2_tail(p.pred_col[t], i, p.n) : ld2(p.pred_col[t], i);
-  x.k1 = TAIL ? ld2_tail(p.keys[0], i, p.n) : ld2(p.keys[0], i);
-  if (NK == 2) x.k2 = TAIL ? ld2_tail(p.keys[1], i, p.n) : ld2(p.keys[1], i);
+    if (t < p.npred) x.pv[t] = TAIL ? ld2_tail(p.pred_col[t], i, p.n) : ld2(p.pred_col[t], i, p.vec);
+  x.k1 = TAIL ? ld2_tail(p.keys[0], i, p.n) : ld2(p.keys[0], i, p.vec);
+  if (NK == 2) x.k2 = TAIL ? ld2_tail(p.keys[1], i, p.n) : ld2(p.keys[1], i, p.vec);
 #pragma unroll
   for (int c = 0; c < NUT_MAX_VALS; ++c)
-    if (c < p.nvals) x.vv[c] = TAIL ? ld2_tail(p.val_col[c], i, p.n) : ld2(p.val_col[c], i);
+    if (c < p.nvals) x.vv[c] = TAIL ? ld2_tail(p.val_col[c], i, p.n) : ld2(p.val_col[c], i, p.vec);
 }
 
 template <int NK, bool TAIL>
@@ -591,7 +597,9 @@ size_t lds_bytes(uint32_t cap, int nk, int naggs) {
 // (re)allocate the global table for `cap` slots and initialise it on the stream
 nut_status alloc_table(nut_groups *g, uint64_t cap) {
   const uint64_t stride = cap + 1;
-  const uint64_t arena = g->nk == 2 ? cap : 0;
+  // two-key arena: one entry per claimable slot plus slack for claim races lost by
+  // concurrent inserters of the same key (each loser leaks at most one entry)
+  const uint64_t arena = g->nk == 2 ? cap + 65536 : 0;
   size_t off = 0;
   auto carve = [&](size_t bytes) {
     size_t o = off;
@@ -676,7 +684,7 @@ nut_status launch_agg(nut_groups *g, const nut_agg_spec *s, uint64_t group_hint,
   bool bad = misaligned(a.keys[0]) || misaligned(a.keys[1]);
   for (int t = 0; t < a.npred; ++t) bad |= misaligned(a.pred_col[t]);
   for (int v = 0; v < a.nvals; ++v) bad |= misaligned(a.val_col[v]);
-  if (bad) return fail(NUT_ERR_UNSUPPORTED, "nut_groupby: columns must be 16-byte aligned");
+  a.vec = bad ? 0 : 1;  // 8-B aligned columns (e.g. slices) take two 8-B loads per pair
 
   // on-chip table: 2x the expected groups within the LDS budget
   const size_t lds_max = 160 * 1024;
