@@ -1,0 +1,436 @@
+// agg_kernel.hpp — the streaming filter -> group-by -> aggregate kernel.
+//
+//   * grid-stride over row pairs; each lane holds FOUR rows per step (two 16-B loads per
+//     column) and the loads of the NEXT step are issued before the current step is
+//     folded (register double buffer), so a wave keeps HBM requests in flight while it
+//     computes — the Q1 kernel runs at 8 waves/CU (private accumulators take the LDS);
+//   * per-workgroup hash table in LDS; the home of a key is a 2-slot bucket read with one
+//     ds_read_b128, so most rows resolve without entering the probe loop;
+//   * keys are found lock-free; NEW keys of tables that publish more than the slot word
+//     (two-key tuples, private ids) are inserted under a block-level LDS lock, so nothing
+//     is half-published and nothing is wasted; single-key shared tables claim by CAS;
+//   * PRIV: the first P groups of a block fold into per-thread private accumulators
+//     laid out [group][agg][thread] (plain read-modify-write, conflict-free), reduced
+//     once per block;
+//   * rows of keys the block table does not admit fold into the global table (g_row);
+//     at block end the LDS table is merged into the global (HBM) table.
+#pragma once
+
+#include "agg_ops.hpp"
+
+namespace nut {
+
+// ------------------------------------------------------------------ LDS table
+// Layout (dynamic LDS, this order, 16-B aligned):
+//   slot[cap+1] u64 | agg[na][cap+1] u64 | k12[cap+1] {i64,i64} (NK=2) | did[cap+1] u32
+//   (PRIV) | dslot[kPrivMax] u32 (PRIV) | ctl[4] u32 | priv[P][na][BD] u64 (PRIV)
+enum { CTL_CLAIMED = 0, CTL_SPECIAL = 1, CTL_LOCK = 2, CTL_NDENSE = 3 };
+constexpr uint32_t kNoDense = 0xFFFFFFFFu;
+
+struct LTable {
+  uint64_t *slot, *agg;
+  i64x2 *k12;
+  uint32_t *did, *dslot, *ctl;
+  uint64_t *priv;
+};
+
+__host__ __device__ inline size_t lds_layout(uint32_t cap, int nk, int na, bool privm, int P, int bd,
+                                             size_t *o_k12, size_t *o_did, size_t *o_dslot, size_t *o_ctl,
+                                             size_t *o_priv) {
+  const size_t stride = cap + 1;
+  size_t o = stride * 8 * (1 + (size_t)na);
+  o = (o + 15) & ~size_t(15);
+  *o_k12 = o;
+  if (nk == 2) o += stride * 16;
+  *o_did = o;
+  if (privm) o += stride * 4;
+  *o_dslot = o;
+  if (privm) o += kPrivMax * 4;
+  *o_ctl = o;
+  o += 16;
+  o = (o + 15) & ~size_t(15);
+  *o_priv = o;
+  if (privm) o += (size_t)P * na * bd * 8;
+  return (o + 15) & ~size_t(15);
+}
+
+// slot word of a key: the key itself (one key) or a 64-bit hash nudged off the empty
+// marker (two keys; the tuple is verified against k12)
+template <int NK>
+__device__ __forceinline__ uint64_t lkey(uint64_t k1, uint64_t k2) {
+  if (NK == 1) return k1;
+  uint64_t h = k1 * kGolden ^ ((k2 + 0x632BE59BD9B4E019ull) * 0xC2B2AE3D27D4EB4Full);
+  h ^= h >> 29;
+  return h == kEmpty ? h ^ 1ull : h;
+}
+// home bucket (even slot) of a slot word
+__device__ __forceinline__ uint32_t lhome(uint64_t w, int log2cap) { return slot_of(w, log2cap) & ~1u; }
+
+template <int NK>
+__device__ __forceinline__ bool keys_match(const LTable &t, uint32_t s, uint64_t k1, uint64_t k2) {
+  if (NK == 1) return true;
+  const i64x2 kk = t.k12[s];
+  return (uint64_t)kk.x == k1 && (uint64_t)kk.y == k2;
+}
+
+// Lock-free walk from the home bucket: slot index, or -1 (reached an empty slot, at
+// `empty_at`) or -2 (chain exhausted).
+template <int NK>
+__device__ __forceinline__ int32_t l_walk(const LTable &t, uint32_t cap, int log2cap, uint64_t w, uint64_t k1,
+                                          uint64_t k2, uint32_t &empty_at) {
+  uint32_t s = lhome(w, log2cap);
+  for (uint32_t probe = 0; probe < cap; ++probe) {
+    const uint64_t cur = __hip_atomic_load(&t.slot[s], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (cur == w && keys_match<NK>(t, s, k1, k2)) return (int32_t)s;
+    if (cur == kEmpty) {
+      empty_at = s;
+      return -1;
+    }
+    s = (s + 1) & (cap - 1);
+  }
+  return -2;
+}
+
+// Slow path of the lookup (home bucket missed): find or insert; returns the slot (>= 0)
+// or -1 (not admitted: the row goes to the global table).
+template <int NK, bool LOCKED>
+__device__ __noinline__ int32_t l_find_slow(const LTable t, const uint32_t cap, const uint32_t limit,
+                                            const int log2cap, const int priv, const uint64_t w, const uint64_t k1,
+                                            const uint64_t k2) {
+  if (NK == 1 && w == kEmpty) {
+    t.ctl[CTL_SPECIAL] = 1u;
+    return (int32_t)cap;
+  }
+  uint32_t e = 0;
+  int32_t s = l_walk<NK>(t, cap, log2cap, w, k1, k2, e);
+  if (s >= 0) return s;
+  if (s == -2) return -1;
+  if (!LOCKED) {
+    // claim by CAS along the chain from the first empty slot
+    for (uint32_t probe = 0; probe < cap; ++probe) {
+      uint64_t cur = t.slot[e];
+      if (cur == w) return (int32_t)e;
+      if (cur == kEmpty) {
+        if (*(volatile uint32_t *)&t.ctl[CTL_CLAIMED] >= limit) return -1;
+        cur = atomicCAS((unsigned long long *)&t.slot[e], (unsigned long long)kEmpty, (unsigned long long)w);
+        if (cur == kEmpty) {
+          atomicAdd(&t.ctl[CTL_CLAIMED], 1u);
+          return (int32_t)e;
+        }
+        if (cur == w) return (int32_t)e;
+      }
+      e = (e + 1) & (cap - 1);
+    }
+    return -1;
+  }
+  // Locked insert.  Every waiting lane of the wave retries until it has run its own
+  // critical section; the lock holder's section runs in the same pass (no SIMT
+  // deadlock); other waves retry.  The slot word is published last (release).
+  int32_t res = -1;
+  bool done = false;
+  for (uint32_t spins = 0;; ++spins) {
+    if (!done) {
+      if (__hip_atomic_exchange(&t.ctl[CTL_LOCK], 1u, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u) {
+        uint32_t e2 = 0;
+        res = l_walk<NK>(t, cap, log2cap, w, k1, k2, e2);
+        if (res == -1) {
+          if (t.ctl[CTL_CLAIMED] < limit) {
+            if (NK == 2) t.k12[e2] = i64x2{(int64_t)k1, (int64_t)k2};
+            if (t.did) {
+              uint32_t d = t.ctl[CTL_NDENSE];
+              if (d < (uint32_t)priv) {
+                t.dslot[d] = e2;
+                t.ctl[CTL_NDENSE] = d + 1;
+              } else {
+                d = kNoDense;
+              }
+              t.did[e2] = d;
+            }
+            t.ctl[CTL_CLAIMED] += 1u;
+            __hip_atomic_store(&t.slot[e2], w, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            res = (int32_t)e2;
+          }
+        } else if (res == -2) {
+          res = -1;
+        }
+        __hip_atomic_store(&t.ctl[CTL_LOCK], 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        done = true;
+      }
+    }
+    if (__all(done) || spins > (1u << 20)) break;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  return done ? res : -1;
+}
+
+// ------------------------------------------------------------------ row loads
+template <class S>
+struct Rows {
+  uint64_t k1[4], k2[4];
+  uint64_t pv[S::MP > 0 ? S::MP : 1][4];
+  uint64_t vv[S::MV > 0 ? S::MV : 1][4];
+};
+
+// VEC: 1 = all columns 16-B aligned (vector loads), 0 = decided at run time (p.vec)
+template <int VEC>
+__device__ __forceinline__ void load2(const AggArgs &p, const uint64_t *col, uint64_t i, uint64_t &x, uint64_t &y) {
+  if (VEC == 1 || p.vec) {
+    const u64x2 v = *reinterpret_cast<const u64x2 *>(col + i);
+    x = v.x;
+    y = v.y;
+  } else {
+    x = col[i];
+    y = col[i + 1];
+  }
+}
+
+// rows {i0, i0+1, i1, i1+1}; TAIL: guard every row against n
+template <int NK, class S, int VEC, bool TAIL>
+__device__ __forceinline__ void load_rows(const AggArgs &p, uint64_t i0, uint64_t i1, Rows<S> &x) {
+  auto ld = [&](const uint64_t *col, uint64_t (&d)[4]) {
+    if (TAIL) {
+      d[0] = i0 < p.n ? col[i0] : 0;
+      d[1] = i0 + 1 < p.n ? col[i0 + 1] : 0;
+      d[2] = i1 < p.n ? col[i1] : 0;
+      d[3] = i1 + 1 < p.n ? col[i1 + 1] : 0;
+    } else {
+      load2<VEC>(p, col, i0, d[0], d[1]);
+      load2<VEC>(p, col, i1, d[2], d[3]);
+    }
+  };
+#pragma unroll
+  for (int t = 0; t < S::MP; ++t)
+    if (t < S::np(p)) ld(p.pred_col[t], x.pv[t]);
+  ld(p.keys[0], x.k1);
+  if (NK == 2) ld(p.keys[1], x.k2);
+#pragma unroll
+  for (int c = 0; c < S::MV; ++c)
+    if (c < S::nv(p)) ld(p.val_col[c], x.vv[c]);
+}
+
+// ------------------------------------------------------------------ fold four rows
+template <int NK, bool PRIV, int BD, class S, bool TAIL>
+__device__ __forceinline__ void consume_rows(const AggArgs &p, const LTable &lt, uint64_t i0, uint64_t i1,
+                                             const Rows<S> &x) {
+  constexpr int R = 4;
+  constexpr bool LOCKED = NK == 2 || PRIV;
+  bool ok[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) ok[r] = !TAIL || ((r < 2 ? i0 : i1) + (r & 1)) < p.n;
+  // WHERE: one decision per term per four rows
+#pragma unroll
+  for (int t = 0; t < S::MP; ++t) {
+    if (t < S::np(p)) {
+      const uint64_t k = p.pred_k[t];
+      with_pred(S::ptype(p, t), S::pop(p, t), [&](auto OPC, auto TYC) {
+        constexpr int OP = decltype(OPC)::value, TY = decltype(TYC)::value;
+#pragma unroll
+        for (int r = 0; r < R; ++r) ok[r] = ok[r] && pred1<OP, TY>(x.pv[t][r], k);
+      });
+    }
+  }
+  // GROUP BY: home-bucket lookup of all four rows (four ds_read_b128 in flight), then
+  // the probe loop only for rows that missed
+  const uint32_t cap = p.lds_cap;
+  int32_t sl[R];
+  uint64_t w[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    w[r] = lkey<NK>(x.k1[r], x.k2[r]);
+    sl[r] = -2;
+  }
+  if (cap) {
+    u64x2 bk[R];
+    uint32_t hb[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      hb[r] = lhome(w[r], p.lds_log2);
+      bk[r] = *reinterpret_cast<const u64x2 *>(&lt.slot[hb[r]]);
+    }
+    if (LOCKED) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if (ok[r]) {
+        int32_t s = bk[r].x == w[r] ? (int32_t)hb[r] : bk[r].y == w[r] ? (int32_t)hb[r] + 1 : -1;
+        if (NK == 2 && s >= 0 && !keys_match<NK>(lt, (uint32_t)s, x.k1[r], x.k2[r])) s = -1;
+        if (s < 0 || (NK == 1 && w[r] == kEmpty))
+          s = l_find_slow<NK, LOCKED>(lt, cap, p.lds_limit, p.lds_log2, p.priv, w[r], x.k1[r], x.k2[r]);
+        sl[r] = s;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < R; ++r) sl[r] = ok[r] ? -1 : -2;
+  }
+  uint32_t dd[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) dd[r] = (PRIV && sl[r] >= 0 && sl[r] < (int32_t)cap) ? lt.did[sl[r]] : kNoDense;
+
+  // aggregate inputs
+  uint64_t av[S::MA][R];
+#pragma unroll
+  for (int a = 0; a < S::MA; ++a) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) av[a][r] = 0;
+    if (a < S::na(p) && S::kind(p, a) != AK_COUNT) {
+      const int a0 = S::arg(p, a, 0), a1 = S::arg(p, a, 1), a2 = S::arg(p, a, 2);
+      with_expr(S::expr(p, a), [&](auto EC) {
+        constexpr int E = decltype(EC)::value;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          auto pick = [&](int c) {
+            uint64_t v = x.vv[0][r];
+#pragma unroll
+            for (int q = 1; q < S::MV; ++q) v = c == q ? x.vv[q][r] : v;
+            return v;
+          };
+          av[a][r] = eval<E>(pick(a0), pick(a1), pick(a2));
+        }
+      });
+    }
+  }
+  // fold
+  const uint32_t stride = cap + 1;
+#pragma unroll
+  for (int a = 0; a < S::MA; ++a) {
+    if (a < S::na(p)) {
+      with_kind(S::kind(p, a), [&](auto KC) {
+        constexpr int K = decltype(KC)::value;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          if (sl[r] >= 0) {
+            if (PRIV && dd[r] != kNoDense) {
+              uint64_t *pw = &lt.priv[((size_t)dd[r] * S::na(p) + a) * BD + threadIdx.x];
+              *pw = fold<K>(*pw, av[a][r]);
+            } else {
+              fold_atomic<K>(&lt.agg[a * stride + sl[r]], av[a][r]);
+            }
+          }
+        }
+      });
+    }
+  }
+  // rows the block table did not admit
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    if (sl[r] == -1) {
+      uint64_t g[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+      for (int a = 0; a < S::MA && a < 8; ++a) g[a] = av[a][r];
+      g_row<NK>(p.gt, (int64_t)x.k1[r], (int64_t)x.k2[r], g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7]);
+    }
+  }
+}
+
+// ------------------------------------------------------------------ the kernel
+template <int NK, bool PRIV, int BD, class S, int VEC>
+__global__ __launch_bounds__(BD) void agg_kernel(AggArgs p) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
+  const uint32_t cap = p.lds_cap;
+  const uint32_t stride = cap + 1;
+  const int na = S::na(p);
+  LTable lt;
+  {
+    size_t o_k12, o_did, o_dslot, o_ctl, o_priv;
+    lds_layout(cap, NK, na, PRIV, p.priv, BD, &o_k12, &o_did, &o_dslot, &o_ctl, &o_priv);
+    char *b = (char *)smem;
+    lt.slot = (uint64_t *)b;
+    lt.agg = lt.slot + stride;
+    lt.k12 = (i64x2 *)(b + o_k12);
+    lt.did = PRIV ? (uint32_t *)(b + o_did) : nullptr;
+    lt.dslot = (uint32_t *)(b + o_dslot);
+    lt.ctl = (uint32_t *)(b + o_ctl);
+    lt.priv = (uint64_t *)(b + o_priv);
+  }
+  if (cap) {
+    for (uint32_t s = threadIdx.x; s < stride; s += BD) {
+      lt.slot[s] = kEmpty;
+#pragma unroll
+      for (int a = 0; a < S::MA; ++a)
+        if (a < na) lt.agg[a * stride + s] = agg_init(S::kind(p, a));
+      if (PRIV) lt.did[s] = kNoDense;
+    }
+    if (threadIdx.x < 4) lt.ctl[threadIdx.x] = 0;
+    if (PRIV) {
+#pragma unroll
+      for (int a = 0; a < S::MA; ++a)
+        if (a < na) {
+          const uint64_t init = agg_init(S::kind(p, a));
+          for (int d = 0; d < p.priv; ++d) lt.priv[((size_t)d * na + a) * BD + threadIdx.x] = init;
+        }
+    }
+    __syncthreads();
+  }
+
+  // grid-stride over row pairs; a step takes pairs q and q + gstride (four rows) and
+  // the next step's loads are issued before this step is folded
+  const uint64_t npairs = (p.n + 1) / 2;
+  const uint64_t full_pairs = p.n / 2;
+  const uint64_t gstride = (uint64_t)gridDim.x * BD;
+  uint64_t q = (uint64_t)blockIdx.x * BD + threadIdx.x;
+  if (q + gstride < full_pairs) {
+    Rows<S> cur;
+    load_rows<NK, S, VEC, false>(p, 2 * q, 2 * (q + gstride), cur);
+    for (;;) {
+      const uint64_t qn = q + 2 * gstride;
+      const bool more = qn + gstride < full_pairs;
+      Rows<S> nxt;
+      if (more) load_rows<NK, S, VEC, false>(p, 2 * qn, 2 * (qn + gstride), nxt);
+      consume_rows<NK, PRIV, BD, S, false>(p, lt, 2 * q, 2 * (q + gstride), cur);
+      q = qn;
+      if (!more) break;
+      cur = nxt;
+    }
+  }
+  if (q < npairs) {  // last partial step: at most two pairs left for this lane
+    const uint64_t q1 = q + gstride < npairs ? q + gstride : q;
+    Rows<S> x;
+    load_rows<NK, S, VEC, true>(p, 2 * q, 2 * q1, x);
+    // a duplicate second pair (q1 == q) is masked out by placing it past the end
+    consume_rows<NK, PRIV, BD, S, true>(p, lt, 2 * q, q1 == q ? p.n : 2 * q1, x);
+  }
+
+  if (!cap) return;
+  __syncthreads();
+  if (PRIV) {
+    // reduce each (group, aggregate) column of the private accumulators: 8 threads per
+    // column, fixed order, then one LDS atomic merge into the shared slot
+    const uint32_t nd = min(lt.ctl[CTL_NDENSE], (uint32_t)p.priv);
+    const int part = threadIdx.x & 7;
+    for (uint32_t pi = threadIdx.x >> 3; pi < nd * (uint32_t)na; pi += BD / 8) {
+      const uint32_t d = pi / na, a = pi % na;
+      const uint64_t *col = &lt.priv[(size_t)pi * BD];
+#pragma unroll
+      for (int aa = 0; aa < S::MA; ++aa) {
+        if ((int)a == aa) {
+          with_kind(S::kind(p, aa), [&](auto KC) {
+            constexpr int K = decltype(KC)::value;
+            uint64_t acc = col[part];
+            for (int j = part + 8; j < BD; j += 8) acc = combine<K>(acc, col[j]);
+#pragma unroll
+            for (int off = 4; off >= 1; off >>= 1) acc = combine<K>(acc, __shfl_xor(acc, off, 8));
+            if (part == 0) agg_merge_word(&lt.agg[aa * stride + lt.dslot[d]], K, acc);
+          });
+        }
+      }
+    }
+    __syncthreads();
+  }
+  // merge the block's table into the global table
+  const GTable t = *p.gt;
+  const uint64_t gstr = t.cap + 1;
+  for (uint32_t s = threadIdx.x; s < stride; s += BD) {
+    const uint64_t wd = lt.slot[s];
+    const bool occ = s < cap ? wd != kEmpty : lt.ctl[CTL_SPECIAL] != 0u;
+    if (!occ) continue;
+    const int64_t k1 = NK == 1 ? (int64_t)(s < cap ? wd : kEmpty) : lt.k12[s].x;
+    const int64_t k2 = NK == 1 ? 0 : lt.k12[s].y;
+    const int64_t gs = g_find<NK>(t, key_hash<NK>(k1, k2), k1, k2);
+    if (gs < 0) continue;
+#pragma unroll
+    for (int a = 0; a < S::MA; ++a)
+      if (a < na) agg_merge_word(&t.agg[a * gstr + gs], S::kind(p, a), lt.agg[a * stride + s]);
+  }
+}
+
+}  // namespace nut

@@ -1,13 +1,13 @@
 // aggregate.hip — host side of the fused  WHERE -> GROUP BY -> SUM/COUNT/MIN/MAX
 // executor (BASELINE configs 3, 4): table lifecycle, kernel dispatch and the
 // nut_groupby* / nut_groups_* / nut_q1 entry points of include/nutexec.h.
-// Device code: agg_stream.hpp (streaming kernel), gtable.hpp (global table).
+// Device code: agg_kernel.hpp + agg_ops.hpp (streaming kernel), gtable.hpp (global table).
 #include <string.h>
 
 #include <algorithm>
 #include <vector>
 
-#include "agg_stream.hpp"
+#include "agg_kernel.hpp"
 
 // ============================================================== host side
 using namespace nut;
@@ -182,18 +182,21 @@ int detect_shape(const nut_agg_spec *s, const int32_t *kinds, const AggArgs &a) 
 constexpr int kBdShared = 512;
 constexpr int kBdPriv = 256;
 
-KernelFn pick_kernel(int nk, bool priv, int shape) {
+// Compiled shapes assume 16-B aligned columns (vector loads); anything else runs the
+// generic kernel, which decides the load width at run time.
+KernelFn pick_kernel(int nk, bool priv, int shape, bool vec) {
+  if (!vec) shape = SHAPE_GENERIC;
   if (priv) {
-    if (shape == SHAPE_Q1) return agg_kernel<2, true, kBdPriv, ShapeQ1>;
-    if (shape == SHAPE_SUM) return agg_kernel<1, true, kBdPriv, ShapeSum>;
-    if (shape == SHAPE_ALL4) return agg_kernel<1, true, kBdPriv, ShapeAll4>;
-    return nk == 1 ? agg_kernel<1, true, kBdPriv, Generic> : agg_kernel<2, true, kBdPriv, Generic>;
+    if (shape == SHAPE_Q1) return agg_kernel<2, true, kBdPriv, ShapeQ1, 1>;
+    if (shape == SHAPE_SUM) return agg_kernel<1, true, kBdPriv, ShapeSum, 1>;
+    if (shape == SHAPE_ALL4) return agg_kernel<1, true, kBdPriv, ShapeAll4, 1>;
+    return nk == 1 ? agg_kernel<1, true, kBdPriv, Generic, 0> : agg_kernel<2, true, kBdPriv, Generic, 0>;
   }
-  if (shape == SHAPE_Q1) return agg_kernel<2, false, kBdShared, ShapeQ1>;
-  if (shape == SHAPE_SUM) return agg_kernel<1, false, kBdShared, ShapeSum>;
-  if (shape == SHAPE_SUMCOUNT) return agg_kernel<1, false, kBdShared, ShapeSumCount>;
-  if (shape == SHAPE_ALL4) return agg_kernel<1, false, kBdShared, ShapeAll4>;
-  return nk == 1 ? agg_kernel<1, false, kBdShared, Generic> : agg_kernel<2, false, kBdShared, Generic>;
+  if (shape == SHAPE_Q1) return agg_kernel<2, false, kBdShared, ShapeQ1, 1>;
+  if (shape == SHAPE_SUM) return agg_kernel<1, false, kBdShared, ShapeSum, 1>;
+  if (shape == SHAPE_SUMCOUNT) return agg_kernel<1, false, kBdShared, ShapeSumCount, 1>;
+  if (shape == SHAPE_ALL4) return agg_kernel<1, false, kBdShared, ShapeAll4, 1>;
+  return nk == 1 ? agg_kernel<1, false, kBdShared, Generic, 0> : agg_kernel<2, false, kBdShared, Generic, 0>;
 }
 
 size_t lds_bytes(uint32_t cap, int nk, int na, bool priv, int P, int bd) {
@@ -256,7 +259,7 @@ nut_status launch_agg(nut_groups *g, const nut_agg_spec *s, uint64_t group_hint,
   a.gt = g->dev_gt;
   const size_t lb = lds_bytes(lcap, g->nk, na, priv, P, bd);
   const int shape = detect_shape(s, kinds, a);
-  KernelFn fn = pick_kernel(g->nk, priv, shape);
+  KernelFn fn = pick_kernel(g->nk, priv, shape, a.vec != 0);
   NUT_HIP(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_max));
   int blocks_per_cu = lb ? (int)std::max<size_t>(1, std::min<size_t>(bd == 512 ? 4 : 8, lds_max / lb)) : 4;
   uint64_t pairs = (s->n + 1) / 2;
