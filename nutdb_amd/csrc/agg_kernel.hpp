@@ -63,8 +63,9 @@ __device__ __forceinline__ uint64_t lkey(uint64_t k1, uint64_t k2) {
   h ^= h >> 29;
   return h == kEmpty ? h ^ 1ull : h;
 }
-// home bucket (even slot) of a slot word
-__device__ __forceinline__ uint32_t lhome(uint64_t w, int log2cap) { return slot_of(w, log2cap) & ~1u; }
+// home bucket (4 slots, 32-B aligned) of a slot word
+constexpr uint32_t kBucket = 4;
+__device__ __forceinline__ uint32_t lhome(uint64_t w, int log2cap) { return slot_of(w, log2cap) & ~(kBucket - 1); }
 
 template <int NK>
 __device__ __forceinline__ bool keys_match(const LTable &t, uint32_t s, uint64_t k1, uint64_t k2) {
@@ -240,21 +241,46 @@ __device__ __forceinline__ void consume_rows(const AggArgs &p, const LTable &lt,
     sl[r] = -2;
   }
   if (cap) {
-    u64x2 bk[R];
+    u64x2 b0[R], b1[R];
     uint32_t hb[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       hb[r] = lhome(w[r], p.lds_log2);
-      bk[r] = *reinterpret_cast<const u64x2 *>(&lt.slot[hb[r]]);
+      b0[r] = *reinterpret_cast<const u64x2 *>(&lt.slot[hb[r]]);
+      b1[r] = *reinterpret_cast<const u64x2 *>(&lt.slot[hb[r] + 2]);
     }
     if (LOCKED) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       if (ok[r]) {
-        int32_t s = bk[r].x == w[r] ? (int32_t)hb[r] : bk[r].y == w[r] ? (int32_t)hb[r] + 1 : -1;
-        if (NK == 2 && s >= 0 && !keys_match<NK>(lt, (uint32_t)s, x.k1[r], x.k2[r])) s = -1;
-        if (s < 0 || (NK == 1 && w[r] == kEmpty))
-          s = l_find_slow<NK, LOCKED>(lt, cap, p.lds_limit, p.lds_log2, p.priv, w[r], x.k1[r], x.k2[r]);
+        // home bucket: the first slot holding w, or the first empty slot ends the chain
+        int32_t s = -1;
+        bool end = false;
+        const uint64_t c[4] = {b0[r].x, b0[r].y, b1[r].x, b1[r].y};
+#pragma unroll
+        for (int j = 3; j >= 0; --j) {
+          if (c[j] == w[r]) s = (int32_t)hb[r] + j;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) end = end || (c[j] == kEmpty && (s < 0 || j < s - (int32_t)hb[r]));
+        if (NK == 2 && s >= 0 && !keys_match<NK>(lt, (uint32_t)s, x.k1[r], x.k2[r])) s = -1, end = false;
+        if (NK == 1 && w[r] == kEmpty) s = -1, end = true;
+        if (s < 0 && !end) {
+          // continue the probe chain past the bucket (inline: a few slots at most)
+          uint32_t e = (hb[r] + kBucket) & (cap - 1);
+          for (uint32_t probe = kBucket; probe < cap; ++probe) {
+            const uint64_t cur =
+                LOCKED ? __hip_atomic_load(&lt.slot[e], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) : lt.slot[e];
+            if (cur == w[r] && keys_match<NK>(lt, e, x.k1[r], x.k2[r])) {
+              s = (int32_t)e;
+              break;
+            }
+            if (cur == kEmpty) break;
+            e = (e + 1) & (cap - 1);
+          }
+        }
+        // not present: insert (or find a concurrent insert) out of line
+        if (s < 0) s = l_find_slow<NK, LOCKED>(lt, cap, p.lds_limit, p.lds_log2, p.priv, w[r], x.k1[r], x.k2[r]);
         sl[r] = s;
       }
     }

@@ -237,12 +237,13 @@ nut_status launch_agg(nut_groups *g, const nut_agg_spec *s, uint64_t group_hint,
   for (int v = 0; v < a.nvals; ++v) bad |= misaligned(a.val_col[v]);
   a.vec = bad ? 0 : 1;  // 8-B aligned columns (e.g. slices) take two 8-B loads per pair
 
-  // on-chip table: 2x the expected groups within the LDS budget
+  // on-chip table: 4x the expected groups (load <= 1/4: a key almost always sits in
+  // its 4-slot home bucket) within the LDS budget
   const size_t lds_max = 160 * 1024;
   const int na = s->naggs;
-  uint64_t want = group_hint ? 2 * group_hint : 4096;
+  uint64_t want = group_hint ? 4 * group_hint : 4096;
   uint32_t lcap = 64;
-  while (lcap < want && lds_bytes(lcap * 2, g->nk, na, false, 0, kBdShared) <= lds_max / 2) lcap *= 2;
+  while (lcap < want && lds_bytes(lcap * 2, g->nk, na, false, 0, kBdShared) <= lds_max) lcap *= 2;
   if (group_hint > 8ull * lcap) lcap = 0;  // hot keys cannot fit on chip: straight to HBM
   // private accumulators when every expected group fits P per thread, 2 blocks per CU
   int P = 0;
