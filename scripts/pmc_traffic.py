@@ -1,0 +1,45 @@
+#!/usr/bin/env python3
+"""Turn a scripts/round_profile.sh directory into profiles/-ready summaries:
+  summary.json       per-kernel trace stats (calls, avg ns) + per-dispatch PMC means
+  pmc_<workload>.json HBM bytes per launch of the dominant kernel, read by bench.py
+gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE reports half the bytes of a
+wide coalesced streaming read, so read bytes = 2 x FETCH_SIZE x 1024; WRITE_SIZE is
+exact for 16-B streaming stores and atomics (x 1024)."""
+import json
+import sys
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parent))
+from prof_summary import summarize  # noqa: E402
+
+WORKLOAD_KERNEL = {"q1": ("tpch_q1_shape_filter_groupby", "agg_kernel"),
+                   "groupby": ("groupby_i64_sum_f64", "agg_kernel"),
+                   "filter": ("filter_i64_compaction", "filter_i64_kernel"),
+                   "sort": ("sort_i64_radix", "radix")}
+
+
+def main():
+    d = Path(sys.argv[1])
+    args = sys.argv[2:]
+    wl = args[args.index("--workload") + 1] if "--workload" in args else "q1"
+    rows = float(args[args.index("--rows") + 1]) if "--rows" in args else {"q1": 1e9, "groupby": 1e9, "filter": 1e8,
+                                                                           "sort": 1e9}[wl]
+    name, match = WORKLOAD_KERNEL[wl]
+    s = summarize(d, match)
+    c = s["counters"]
+    traffic = None
+    if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+        traffic = c["FETCH_SIZE"] * 1024 * 2 + c["WRITE_SIZE"] * 1024
+    s["workload"] = name
+    s["rows"] = int(rows)
+    s["hbm_bytes_per_launch"] = traffic
+    (d / "summary.json").write_text(json.dumps(s, indent=1))
+    (d / f"pmc_{name}.json").write_text(json.dumps({
+        "workload": name, "rows": int(rows), "kernel_match": match, "hbm_bytes_per_launch": traffic,
+        "fetch_size_kb": c.get("FETCH_SIZE"), "write_size_kb": c.get("WRITE_SIZE"),
+        "correction": "read = 2 x FETCH_SIZE (gfx950 wide-stream halving), write = WRITE_SIZE"}, indent=1))
+    print(json.dumps({"workload": name, "traffic": traffic, "kernels": s["kernels"][:3]}))
+
+
+if __name__ == "__main__":
+    main()
