@@ -188,35 +188,43 @@ def groupby_step(w, rank, world, group):
 
 # ------------------------------------------------------------------ CPU baseline
 def cpu_baseline(args, workload: str, target_s: float):
+    """The C oracle on the host cores, same synthetic workload.  Columns are generated
+    once (not timed); the scan is timed repeatedly up to ~target_s and the best run is
+    reported."""
     from oracle import oracle as orc
     from nutdb_amd.workloads import FILTER_COL, Q1_COLS, Q1_DATE_K, filter_k, groupby_cols
     threads = orc.max_threads()
 
-    def run(n):
+    def prepare(n):
         if workload == "q1":
             sd, rf, ls, qty, price, disc = [orc.gen(s, n) for s in Q1_COLS]
-            t0 = time.perf_counter()
-            orc.groupby([rf, ls], [(0, 0, (0,)), (0, 0, (1,)), (0, 4, (1, 2)), (1, 0, ())],
-                        values=[qty, price, disc], preds=[(sd, 1, Q1_DATE_K)], cap=64)
-            return time.perf_counter() - t0
+            return lambda: orc.groupby([rf, ls], [(0, 0, (0,)), (0, 0, (1,)), (0, 4, (1, 2)), (1, 0, ())],
+                                       values=[qty, price, disc], preds=[(sd, 1, Q1_DATE_K)], cap=64)
         if workload == "groupby":
             key, val = [orc.gen(s, n) for s in groupby_cols(args.groups, dyadic=True)]
-            t0 = time.perf_counter()
-            orc.groupby([key], [(0, 0, (0,))], values=[val], cap=max(args.groups, 1))
-            return time.perf_counter() - t0
+            return lambda: orc.groupby([key], [(0, 0, (0,))], values=[val], cap=max(args.groups, 1))
         col = orc.gen(FILTER_COL, n)
+        k = filter_k(args.selectivity)
+        return lambda: orc.filter_i64(col, 0, k)
+
+    def timed(fn):
         t0 = time.perf_counter()
-        orc.filter_i64(col, 0, filter_k(args.selectivity))
+        fn()
         return time.perf_counter() - t0
 
-    n = 4_000_000
-    dt = run(n)
-    per_row = dt / n
-    sample = int(min(max(target_s / max(per_row, 1e-12), n), 1e9 if workload != "filter" else 1e8, 6e8))
-    dt = run(sample)
+    full = int(args.rows) if args.rows else {"q1": 10**9, "groupby": 10**9, "filter": 10**8}[workload]
+    probe = min(full, 4_000_000)
+    per_row = timed(prepare(probe)) / probe
+    sample = int(min(full, max(probe, target_s / max(per_row, 1e-12))))
+    fn = prepare(sample)
+    times = [timed(fn)]
+    while sum(times) < target_s and len(times) < 10:
+        times.append(timed(fn))
+    dt = min(times)
     return {"value": sample / dt, "unit": "rows/s", "cores": threads, "kind": "port",
-            "sample": f"{sample:.3g} rows of the same synthetic workload, C oracle (oracle/oracle.c) "
-                      f"with OpenMP over {threads} host threads, generation excluded, {dt:.2f} s"}
+            "sample": f"{sample:.3g} rows of the same synthetic workload ({sample / full:.2f} of one GPU's "
+                      f"rows), C oracle (oracle/oracle.c), OpenMP over {threads} host threads, generation "
+                      f"excluded, best of {len(times)} timed scans = {dt:.3f} s"}
 
 
 # ------------------------------------------------------------------ main
