@@ -141,49 +141,16 @@ class Filter:
 # ------------------------------------------------------------------ one step
 def groupby_step(w, rank, world, group):
     """Local scan -> (N>1) all-to-all of partial groups by owner -> owner merge ->
-    gather to rank 0.  Returns the number of result groups on rank 0."""
+    gather to rank 0 (nutdb_amd/dist.py).  Returns the number of result groups on rank 0."""
     g = w.local()
     if world == 1:
         keys, _ = g.to_host_words()
-        n = len(keys)
         g.free()
-        return n
-    ex = w.ex
-    buf, counts = g.partition(world)
-    width = g.nkeys + g.naggs
+        return len(keys)
+    from nutdb_amd.dist import distributed_groupby
+    res = distributed_groupby(w.ex, g, w.merge_query, w.groups_hint, group)
     g.free()
-    send = torch.tensor(counts, dtype=torch.int64, device=ex.device)
-    recv = torch.empty_like(send)
-    dist.all_to_all_single(recv, send, group=group)
-    rc = recv.tolist()
-    out = torch.empty(width * sum(rc), dtype=torch.int64, device=ex.device)
-    dist.all_to_all_single(out, buf, [width * c for c in rc], [width * c for c in counts], group=group)
-    owner = None
-    off = 0
-    for c in rc:
-        if c:
-            seg = out[width * off: width * (off + c)].view(width, c)
-            q = w.merge_query(seg)
-            if owner is None:
-                owner = ex.groupby(q, group_hint=w.groups_hint)
-            else:
-                ex.accumulate(q, owner)
-        off += c
-    mine = owner.to_device() if owner is not None else torch.empty((width, 0), dtype=torch.int64,
-                                                                    device=ex.device)
-    if owner is not None:
-        owner.free()
-    # gather the owners' groups to rank 0 (padded all_gather: groups are few)
-    cnt = torch.tensor([mine.shape[1]], dtype=torch.int64, device=ex.device)
-    cnts = [torch.empty_like(cnt) for _ in range(world)]
-    dist.all_gather(cnts, cnt, group=group)
-    mx = max(int(c.item()) for c in cnts)
-    pad = torch.zeros((width, max(mx, 1)), dtype=torch.int64, device=ex.device)
-    pad[:, : mine.shape[1]] = mine
-    bufs = [torch.empty_like(pad) for _ in range(world)]
-    dist.all_gather(bufs, pad, group=group)
-    total = sum(int(c.item()) for c in cnts)
-    return total
+    return res.shape[1] if res is not None else 0
 
 
 # ------------------------------------------------------------------ CPU baseline

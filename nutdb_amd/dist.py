@@ -1,0 +1,107 @@
+"""Multi-GPU group-by: key-hash exchange of partial groups over torch.distributed.
+
+One process per GPU; backend "nccl" is RCCL over xGMI on ROCm ("gloo" on CPU for tests).
+Each rank pre-aggregates its row shard on its GPU (nut_groupby), partitions the partial
+groups by owner = mix64(key tuple) % P on the device (nut_groups_partition), and the
+ranks exchange them with ONE all-to-all of counts and ONE all-to-all of records.  Each
+owner merges what it received (nut_groupby_accumulate: SUM/COUNT partials add, MIN/MAX
+re-min/max) and rank 0 gathers the owners' final groups.  xGMI is a full point-to-point
+mesh, so the all-to-all uses every link directly.
+
+The record layout is the library's column-major segment format: segment p holds
+counts[p] groups as (nkeys + naggs) consecutive 64-bit columns.
+"""
+from __future__ import annotations
+
+from typing import Callable, List, Optional
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+MASK64 = (1 << 64) - 1
+
+
+def owner_of(k1: np.ndarray, k2: Optional[np.ndarray], nparts: int) -> np.ndarray:
+    """Host restatement of the device owner hash (csrc/common.hpp owner_hash) for tests
+    and host-side tooling: mix64(k1 ^ 0x6A09E667F3BCC908) [then mix64(h ^ k2)] % P."""
+    def mix(z):
+        z = z.astype(np.uint64)
+        with np.errstate(over="ignore"):
+            z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+            z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+    h = mix(k1.view(np.uint64) ^ np.uint64(0x6A09E667F3BCC908))
+    if k2 is not None:
+        h = mix(h ^ k2.view(np.uint64))
+    return (h % np.uint64(nparts)).astype(np.int64)
+
+
+def exchange_partials(buf: torch.Tensor, counts: List[int], width: int, group=None) -> List[torch.Tensor]:
+    """All-to-all of partitioned partial groups.  `buf` holds P column-major segments
+    (segment p: counts[p] groups x `width` int64 words).  Returns the P segments this
+    rank receives, each a [width, c] int64 view (c may be 0)."""
+    world = dist.get_world_size(group)
+    dev = buf.device
+    send = torch.tensor(counts, dtype=torch.int64, device=dev)
+    recv = torch.empty_like(send)
+    dist.all_to_all_single(recv, send, group=group)
+    rc = [int(x) for x in recv.tolist()]
+    out = torch.empty(width * sum(rc), dtype=torch.int64, device=dev)
+    dist.all_to_all_single(out, buf.reshape(-1)[: width * sum(counts)].contiguous(),
+                           [width * c for c in rc], [width * c for c in counts], group=group)
+    segs, off = [], 0
+    for c in rc:
+        segs.append(out[width * off: width * (off + c)].view(width, c))
+        off += c
+    assert len(segs) == world
+    return segs
+
+
+def gather_groups(mine: torch.Tensor, group=None, dst: int = 0) -> Optional[torch.Tensor]:
+    """Collect every owner's [width, n_r] groups on rank `dst` (padded all_gather: the
+    final group count is small).  Returns [width, sum n_r] on dst, None elsewhere."""
+    world = dist.get_world_size(group)
+    width = mine.shape[0]
+    dev = mine.device
+    cnt = torch.tensor([mine.shape[1]], dtype=torch.int64, device=dev)
+    cnts = [torch.empty_like(cnt) for _ in range(world)]
+    dist.all_gather(cnts, cnt, group=group)
+    ns = [int(c.item()) for c in cnts]
+    mx = max(max(ns), 1)
+    pad = torch.zeros((width, mx), dtype=torch.int64, device=dev)
+    pad[:, : mine.shape[1]] = mine
+    bufs = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(bufs, pad, group=group)
+    if dist.get_rank(group) != dst:
+        return None
+    return torch.cat([b[:, :n] for b, n in zip(bufs, ns)], dim=1)
+
+
+def distributed_groupby(ex, local, merge_query: Callable[[torch.Tensor], "object"], group_hint: int,
+                        group=None) -> Optional[torch.Tensor]:
+    """Full multi-GPU group-by step after the local scan.
+
+    `local` is this rank's nut_groups result (Groups); `merge_query(seg)` builds the
+    AggQuery that merges one received [width, c] segment.  Returns the final groups as a
+    [width, G] int64 tensor on rank 0 (unordered; f64 words as bits), None elsewhere."""
+    world = dist.get_world_size(group)
+    width = local.nkeys + local.naggs
+    buf, counts = local.partition(world)
+    segs = exchange_partials(buf, counts, width, group)
+    owner = None
+    for seg in segs:
+        if seg.shape[1] == 0:
+            continue
+        q = merge_query(seg)
+        if owner is None:
+            owner = ex.groupby(q, group_hint=group_hint)
+        else:
+            ex.accumulate(q, owner)
+    if owner is not None:
+        mine = owner.to_device()
+        owner.free()
+    else:
+        mine = torch.empty((width, 0), dtype=torch.int64, device=ex.device)
+    return gather_groups(mine, group)

@@ -1,0 +1,96 @@
+"""The N>1 group-by exchange on CPU: world_size 2 over gloo.
+
+Each rank pre-aggregates its row shard with the C oracle (standing in for its GPU),
+partitions the partial groups by the device owner hash (nutdb_amd.dist.owner_of), runs
+the SAME exchange / gather code bench.py runs over RCCL (nutdb_amd.dist), merges its
+owned groups, and rank 0 checks the union against a single-process oracle result.
+"""
+import os
+import socket
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+ROOT = Path(__file__).resolve().parent.parent
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _segments(keys, words, owners, P):
+    """column-major segment buffer in nut_groups_partition's layout"""
+    width = keys.shape[1] + words.shape[1]
+    counts, cols = [], []
+    for p in range(P):
+        m = owners == p
+        counts.append(int(m.sum()))
+        block = np.concatenate([keys[m].T, words[m].T.view(np.int64)], axis=0)  # [width, c]
+        cols.append(block.reshape(-1))
+    buf = np.concatenate(cols) if cols else np.zeros(0, np.int64)
+    return torch.from_numpy(np.ascontiguousarray(buf)), counts, width
+
+
+def _worker(rank, world, port, n, G, q):
+    sys.path.insert(0, str(ROOT))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    from oracle import oracle as orc
+    from nutdb_amd.dist import exchange_partials, gather_groups, owner_of
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        rows = n // world
+        key = orc.gen_column(2, 0x51, rows, row0=rank * rows, a=G)
+        val = orc.gen_column(4, 0x52, rows, row0=rank * rows)
+        aggs = [(0, 0, (0,)), (1, 0, ()), (2, 0, (0,)), (3, 0, (0,))]
+        k, w = orc.groupby([key], aggs, values=[val])
+        buf, counts, width = _segments(k, w, owner_of(k[:, 0], None, world), world)
+        segs = exchange_partials(buf, counts, width)
+        recv = torch.cat(segs, dim=1).numpy()
+        # owner merge: SUM of sums, SUM of counts (i64), MIN of mins, MAX of maxes
+        mk, mw = orc.groupby([recv[0]], [(0, 0, (0,)), (0, 0, (1,)), (2, 0, (2,)), (3, 0, (3,))],
+                             values=[recv[1].view(np.float64), recv[2], recv[3].view(np.float64),
+                                     recv[4].view(np.float64)])
+        # every received key must be owned by this rank
+        assert np.all(owner_of(mk[:, 0], None, world) == rank)
+        mine = torch.from_numpy(np.ascontiguousarray(np.concatenate([mk.T, mw.T.view(np.int64)], axis=0)))
+        allg = gather_groups(mine)
+        if rank == 0:
+            q.put(allg.numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("G", [7, 1000])
+def test_exchange_world2(G, orc):
+    n = 400_000
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, G, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    order = np.argsort(got[0], kind="stable")
+    got = got[:, order]
+    key = orc.gen_column(2, 0x51, n, a=G)
+    val = orc.gen_column(4, 0x52, n)
+    ok, ow = orc.groupby([key], [(0, 0, (0,)), (1, 0, ()), (2, 0, (0,)), (3, 0, (0,))], values=[val])
+    assert np.array_equal(got[0], ok[:, 0])
+    s = got[1].view(np.float64)
+    assert np.max(np.abs(s - ow[:, 0].view(np.float64)) / np.abs(ow[:, 0].view(np.float64))) <= 1e-12
+    assert np.array_equal(got[2], ow[:, 1].view(np.int64))
+    assert np.array_equal(got[3], ow[:, 2].view(np.int64))
+    assert np.array_equal(got[4], ow[:, 3].view(np.int64))

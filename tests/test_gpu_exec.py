@@ -265,3 +265,29 @@ def test_q1_vs_oracle_large(ex, orc):
     ok, ow = orc.groupby([rf, ls], [(0, 0, (0,)), (0, 0, (1,)), (0, 4, (1, 2)), (1, 0, ())],
                          values=[qty, price, disc], preds=[(sd, OPCODE["<="], Q1_DATE_K)])
     check_vs_oracle(g, ok, ow, ["sum_f64", "sum_f64", "sum_f64", "i"])
+
+
+def test_partition_owner_matches_host_hash(ex, orc):
+    """Device owner partition (nut_groups_partition) == nutdb_amd.dist.owner_of, for one
+    and two keys: the CPU gloo exchange test and the GPU path route identically."""
+    from nutdb_amd import Agg, AggQuery
+    from nutdb_amd.dist import owner_of
+    rng = np.random.default_rng(2)
+    n = 300_000
+    k1 = rng.integers(I64_MIN, I64_MAX, 5000, dtype=np.int64)[rng.integers(0, 5000, n)]
+    k2 = rng.integers(-5, 5, n).astype(np.int64)
+    v = rng.random(n)
+    for keys in ([k1], [k1, k2]):
+        q = AggQuery(keys=[dev(k, ex) for k in keys], values=[dev(v, ex)], aggs=[Agg("count")])
+        g = ex.groupby(q, group_hint=6000)
+        for P in (2, 3, 8):
+            buf, counts = g.partition(P)
+            b = host(buf)
+            w = len(keys) + 1
+            off = 0
+            for p in range(P):
+                seg = b[w * off: w * (off + counts[p])].reshape(w, counts[p])
+                off += counts[p]
+                own = owner_of(seg[0], seg[1] if len(keys) == 2 else None, P)
+                assert np.all(own == p)
+            assert sum(counts) == len(g)
