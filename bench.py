@@ -45,7 +45,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--workload", default="q1", choices=["q1", "groupby", "filter"])
+    p.add_argument("--workload", default="q1", choices=["q1", "groupby", "filter", "sort"])
     p.add_argument("--rows", type=float, default=None, help="rows per GPU (default: config size)")
     p.add_argument("--groups", type=int, default=1000, help="groupby: distinct keys")
     p.add_argument("--selectivity", type=float, default=0.5, help="filter: fraction selected")
@@ -138,6 +138,29 @@ class Filter:
                 "bytes_per_row": 8 + 8 * self.sel}
 
 
+class Sort:
+    """config 5 per GPU: ORDER BY a full-range i64 key (local LSD radix sort)."""
+    name = "sort_i64_radix"
+    kernel_kind = 2
+
+    def __init__(self, ex, rows, row0):
+        from nutdb_amd.workloads import SORT_COL, gen
+        self.ex = ex
+        self.col = gen(ex, SORT_COL, rows, row0=row0)
+        self.out = torch.empty_like(self.col)
+        self.rows = rows
+        self.passes = 8  # full-range keys: no digit pass is constant
+        self.cols_bytes = 8 + 16 * self.passes
+
+    def run(self):
+        self.ex.sort_i64(self.col, out=self.out)
+
+    def config(self):
+        return {"workload": self.name, "query": "SELECT k FROM t ORDER BY k (full-range i64)",
+                "algorithm": "LSD radix, 8 x 8-bit passes, onesweep look-back",
+                "bytes_per_row": self.cols_bytes, "hbm_lower_bound_bytes_per_row": 16}
+
+
 # ------------------------------------------------------------------ one step
 def groupby_step(w, rank, world, group):
     """Local scan -> (N>1) all-to-all of partial groups by owner -> owner merge ->
@@ -159,7 +182,7 @@ def cpu_baseline(args, workload: str, target_s: float):
     once (not timed); the scan is timed repeatedly up to ~target_s and the best run is
     reported."""
     from oracle import oracle as orc
-    from nutdb_amd.workloads import FILTER_COL, Q1_COLS, Q1_DATE_K, filter_k, groupby_cols
+    from nutdb_amd.workloads import FILTER_COL, Q1_COLS, Q1_DATE_K, SORT_COL, filter_k, groupby_cols
     threads = orc.max_threads()
 
     def prepare(n):
@@ -170,6 +193,9 @@ def cpu_baseline(args, workload: str, target_s: float):
         if workload == "groupby":
             key, val = [orc.gen(s, n) for s in groupby_cols(args.groups, dyadic=True)]
             return lambda: orc.groupby([key], [(0, 0, (0,))], values=[val], cap=max(args.groups, 1))
+        if workload == "sort":
+            col = orc.gen(SORT_COL, n)
+            return lambda: orc.sort_i64(col)
         col = orc.gen(FILTER_COL, n)
         k = filter_k(args.selectivity)
         return lambda: orc.filter_i64(col, 0, k)
@@ -179,7 +205,8 @@ def cpu_baseline(args, workload: str, target_s: float):
         fn()
         return time.perf_counter() - t0
 
-    full = int(args.rows) if args.rows else {"q1": 10**9, "groupby": 10**9, "filter": 10**8}[workload]
+    full = int(args.rows) if args.rows else {"q1": 10**9, "groupby": 10**9, "filter": 10**8,
+                                             "sort": 1_250_000_000}[workload]
     probe = min(full, 4_000_000)
     per_row = timed(prepare(probe)) / probe
     sample = int(min(full, max(probe, target_s / max(per_row, 1e-12))))
@@ -211,19 +238,21 @@ def main():
         group = dist.group.WORLD
     from nutdb_amd import Executor
     ex = Executor(local_rank)
-    default_rows = {"q1": 1e9, "groupby": 1e9, "filter": 1e8}[args.workload]
+    default_rows = {"q1": 1e9, "groupby": 1e9, "filter": 1e8, "sort": 1.25e9}[args.workload]
     rows = int(args.rows or default_rows)
     row0 = rank * rows
     if args.workload == "q1":
         w = Q1(ex, rows, row0)
     elif args.workload == "groupby":
         w = GroupBy(ex, rows, row0, args.groups)
+    elif args.workload == "sort":
+        w = Sort(ex, rows, row0)
     else:
         w = Filter(ex, rows, row0, args.selectivity)
     torch.cuda.synchronize()
 
     def step():
-        if args.workload == "filter":
+        if args.workload in ("filter", "sort"):
             w.run()
         else:
             groupby_step(w, rank, world, group)

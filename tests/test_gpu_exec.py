@@ -291,3 +291,51 @@ def test_partition_owner_matches_host_hash(ex, orc):
                 own = owner_of(seg[0], seg[1] if len(keys) == 2 else None, P)
                 assert np.all(own == p)
             assert sum(counts) == len(g)
+
+
+# ----------------------------------------------------------------------------- sort
+def test_sort_golden(golden, ex):
+    case = golden["sort"][0]
+    keys = ex.gen_column(1, 0x50, case["n"])
+    out = host(ex.sort_i64(keys))
+    assert [int(x) for x in out[:8]] == case["head"]
+    assert [int(x) for x in out[-8:]] == case["tail"]
+    assert pos_hash(out) == case["pos_hash"]
+
+
+@pytest.mark.parametrize("n", [0, 1, 2, 3, 63, 64, 65, 4095, 4096, 4097, 12289, 1_000_003])
+def test_sort_sizes_vs_oracle(ex, orc, n):
+    col = orc.gen_column(1, 0x50, n)
+    got = host(ex.sort_i64(dev(col, ex)))
+    assert np.array_equal(got, orc.sort_i64(col))
+
+
+@pytest.mark.parametrize("kind", ["dups", "const", "small_range", "extremes", "negative", "unaligned"])
+def test_sort_distributions(ex, orc, kind):
+    rng = np.random.default_rng(9)
+    n = 300_007
+    if kind == "dups":
+        v = rng.integers(-50, 50, n).astype(np.int64)
+    elif kind == "const":
+        v = np.full(n, -7, dtype=np.int64)
+    elif kind == "small_range":
+        v = rng.integers(0, 1 << 20, n).astype(np.int64)      # 5 of 8 digit passes trivial
+    elif kind == "extremes":
+        v = rng.choice(np.array([I64_MIN, I64_MAX, 0, -1, 1], dtype=np.int64), n)
+    elif kind == "negative":
+        v = -rng.integers(0, I64_MAX, n, dtype=np.int64)
+    else:
+        v = rng.integers(I64_MIN, I64_MAX, n + 1, dtype=np.int64)
+    d = dev(v, ex)
+    src = d[1:] if kind == "unaligned" else d
+    want = orc.sort_i64(v[1:] if kind == "unaligned" else v)
+    assert np.array_equal(host(ex.sort_i64(src)), want)
+
+
+def test_sort_large_property(ex, orc):
+    n = 200_000_000
+    keys = ex.gen_column(1, 0x50, n)
+    out = ex.sort_i64(keys)
+    o = host(out)
+    assert np.all(o[1:] >= o[:-1])
+    assert orc.multiset_hash(o) == orc.multiset_hash(orc.gen_column(1, 0x50, n))
