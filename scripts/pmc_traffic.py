@@ -15,7 +15,7 @@ from prof_summary import summarize  # noqa: E402
 WORKLOAD_KERNEL = {"q1": ("tpch_q1_shape_filter_groupby", "agg_kernel"),
                    "groupby": ("groupby_i64_sum_f64", "agg_kernel"),
                    "filter": ("filter_i64_compaction", "filter_i64_kernel"),
-                   "sort": ("sort_i64_radix", "radix")}
+                   "sort": ("sort_i64_radix", "rs_pass")}
 
 
 def main():
