@@ -45,7 +45,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--workload", default="q1", choices=["q1", "groupby", "filter", "sort"])
+    p.add_argument("--workload", default="q1", choices=["q1", "groupby", "filter", "sort", "parse"])
     p.add_argument("--rows", type=float, default=None, help="rows per GPU (default: config size)")
     p.add_argument("--groups", type=int, default=1000, help="groupby: distinct keys")
     p.add_argument("--selectivity", type=float, default=0.5, help="filter: fraction selected")
@@ -222,8 +222,49 @@ def cpu_baseline(args, workload: str, target_s: float):
 
 
 # ------------------------------------------------------------------ main
+def parse_bench(args):
+    """BASELINE config 1: parse-only over the reference's SQL fixtures (tests/golden/sql:
+    tests/sql/1..14.sql + the two criterion bench statements), CPU only, through the C ABI
+    (nut_sql_parse + nut_stmt_free per statement; ctypes call overhead included)."""
+    import ctypes as C
+    from nutdb_amd._lib import lib
+    files = sorted((ROOT / "tests" / "golden" / "sql").glob("*.sql"))
+    stmts = [f.read_bytes() for f in files]
+    iters = max(args.steps, 1) * 100
+    h = C.c_void_p()
+    for s in stmts * max(args.warmup, 1):
+        assert lib.nut_sql_parse(s, len(s), C.byref(h)) == 0
+        lib.nut_stmt_free(h)
+    per = {}
+    t_all = 0.0
+    for f, s in zip(files, stmts):
+        n = len(s)
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            lib.nut_sql_parse(s, n, C.byref(h))
+            lib.nut_stmt_free(h)
+        dt = time.perf_counter() - t0
+        t_all += dt
+        per[f.name] = round(dt / iters * 1e6, 3)
+    total = iters * len(stmts)
+    line = {
+        "metric": "statements/sec parse-only over tests/sql fixtures (CPU)", "value": total / t_all,
+        "unit": "statements/s", "n_gpus": 0, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": t_all * 1e3 / max(args.steps, 1), "higher_is_better": True, "scaling": "none",
+        "vs_baseline": None, "dtype": "utf8", "data": "reference fixtures (tests/golden/sql)",
+        "config": {"workload": "parse", "statements": len(stmts), "iterations_each": iters,
+                   "us_per_statement": per, "bytes_total": sum(len(s) for s in stmts),
+                   "note": "single host thread; includes ctypes call overhead (~0.5 us/call)"},
+        "roofline": None, "cpu_baseline": None,
+    }
+    print(json.dumps(line), flush=True)
+
+
 def main():
     args = parse()
+    if args.workload == "parse":
+        parse_bench(args)
+        return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))

@@ -202,6 +202,94 @@ nut_status nut_q1(nut_ctx *ctx, const int64_t *shipdate, const int64_t *returnfl
  * not alias.  Scratch is owned by the context.
  * ------------------------------------------------------------------------ */
 nut_status nut_sort_i64(nut_ctx *ctx, const int64_t *in, int64_t *out, uint64_t n);
+/* ORDER BY k DESC (the same passes with the key order complemented; no extra pass) */
+nut_status nut_sort_i64_desc(nut_ctx *ctx, const int64_t *in, int64_t *out, uint64_t n);
+
+/* ========================================================================
+ * SQL front end (CPU) — restatement of the reference's only public API,
+ *   nutdb::parser::Parser::parse(&str) -> Result<Statement, ParseError>
+ *   (src/lib.rs:3-4, src/parser/mod.rs:26-29)
+ * Accept/reject behaviour, error texts (src/parser/error.rs:8-57) and constant
+ * folding (src/parser/simplify.rs) follow the reference, quirks included
+ * (SURVEY.md §8(a) A8).  These entry points never touch a GPU.
+ * Errors: NUT_ERR_PARSE with nut_last_error() = the ParseError Display text
+ * ("Lex Error: ..." / "Syntax Error: ...").
+ * ======================================================================== */
+typedef struct nut_stmt nut_stmt;
+
+/* Statement variants, in the order of src/parser/ast/mod.rs:13-24 */
+typedef enum {
+  NUT_STMT_SELECT = 0, NUT_STMT_INSERT = 1, NUT_STMT_EXPLAIN = 2, NUT_STMT_ALTER = 3,
+  NUT_STMT_CREATE = 4, NUT_STMT_DESCRIBE = 5, NUT_STMT_DROP = 6, NUT_STMT_TRUNCATE = 7,
+  NUT_STMT_OPTIMIZE = 8, NUT_STMT_SET = 9
+} nut_stmt_kind;
+
+/* Parser::parse.  `sql` need not be NUL-terminated; it must be valid UTF-8 (the
+ * reference takes &str).  The statement keeps its own copy of the text. */
+nut_status nut_sql_parse(const char *sql, size_t len, nut_stmt **out);
+int nut_stmt_kind_of(const nut_stmt *stmt);
+/* S-expression of the tree (grammar in nutdb_amd/csrc/sql_dump.cpp).  Writes at
+ * most cap-1 bytes + NUL; *len (optional) = full length, so a too-small buffer
+ * returns NUT_ERR_CAPACITY with the size needed. */
+nut_status nut_stmt_dump(const nut_stmt *stmt, char *buf, size_t cap, size_t *len);
+void nut_stmt_free(nut_stmt *stmt);
+
+/* Tokenizer::next_token (src/parser/tokenizer/mod.rs:66-112) until EOF, whitespace
+ * and comment tokens included.  types[i] = TokenType index (token.rs:5-91 order,
+ * KeywordOrIdentifier = 0 ... EOF = 39); spans[2i], spans[2i+1] = byte offsets.
+ * *ntok = tokens produced (EOF included).  NUT_ERR_PARSE on a lexical error
+ * (the tokens before it are still written), NUT_ERR_CAPACITY if cap is short. */
+nut_status nut_sql_tokenize(const char *sql, size_t len, int32_t *types, uint64_t *spans, size_t cap,
+                            size_t *ntok);
+/* unescape_{single,double}_quoted_string (src/parser/literal.rs:36-103); quote is
+ * '\'' or '"'.  Output is not NUL-terminated; *out_len = bytes. */
+nut_status nut_sql_unescape(const char *s, size_t len, int quote, char *out, size_t cap, size_t *out_len);
+
+/* ========================================================================
+ * Plan lowering and execution.  A plan is lowered from the
+ * statement tree — QueryBody.r#where / group_by / columns / order_by / limit
+ * (src/parser/ast/query.rs:21-35) — and executed on the kernels above with the
+ * plan's column names bound to device columns at execute time.
+ *   FILTER : SELECT c FROM t [WHERE c <cmp> const]          [LIMIT]
+ *   GROUPBY: SELECT k.., agg(expr).. FROM t [WHERE conj] GROUP BY k1[,k2]
+ *            [ORDER BY outputs] [LIMIT]; agg in sum/count/min/max/avg
+ *   SORT   : SELECT c FROM t [WHERE c <cmp> const] ORDER BY c [DESC] [LIMIT]
+ * Constants may be integer/float literals, toDate('YYYY-MM-DD') and date +/-
+ * interval n day|month|year (days since 1970-01-01).
+ * Lowering failures return NUT_ERR_PLAN with a message naming the construct.
+ * ======================================================================== */
+typedef struct nut_plan nut_plan;
+typedef struct nut_result nut_result;
+
+typedef enum { NUT_PLAN_FILTER = 0, NUT_PLAN_GROUPBY = 1, NUT_PLAN_SORT = 2 } nut_plan_kind;
+
+typedef struct {
+  const char *name;   /* column name as written in the SQL (ASCII case-insensitive match) */
+  const void *data;   /* device pointer, nrows elements */
+  int32_t type;       /* nut_type */
+} nut_column;
+
+nut_status nut_sql_plan(const char *sql, size_t len, nut_plan **out);
+int nut_plan_kind_of(const nut_plan *plan);
+/* JSON description of the plan (columns, predicates, aggregates, outputs); same
+ * buffer convention as nut_stmt_dump */
+nut_status nut_plan_describe(const nut_plan *plan, char *buf, size_t cap, size_t *len);
+void nut_plan_free(nut_plan *plan);
+
+/* Execute on nrows rows of the bound columns (every column the plan names must be
+ * bound).  group_hint as for nut_groupby.  Synchronous. */
+nut_status nut_plan_execute(nut_ctx *ctx, const nut_plan *plan, const nut_column *cols, int ncols,
+                            uint64_t nrows, uint64_t group_hint, nut_result **out);
+/* Result = ncols output columns (the SELECT list, in order) x nrows rows. */
+nut_status nut_result_shape(const nut_result *res, uint64_t *nrows, int *ncols);
+/* type: nut_type of output column j; name: alias or expression text (owned by res) */
+nut_status nut_result_column(const nut_result *res, int j, int *type, const char **name);
+/* copy output column j to host (int64 or double; cap in elements) */
+nut_status nut_result_to_host(const nut_result *res, int j, void *dst, uint64_t cap);
+/* FILTER/SORT results stay in HBM: device pointer of the nrows output values.
+ * NUT_ERR_UNSUPPORTED for GROUPBY results (those are materialised on the host). */
+nut_status nut_result_device(const nut_result *res, const void **dev);
+void nut_result_free(nut_result *res);
 
 #ifdef __cplusplus
 }

@@ -60,6 +60,23 @@ class NutAggSpec(C.Structure):
     ]
 
 
+class NutColumn(C.Structure):
+    """nut_column: a named device column bound to a plan at execute time."""
+    _fields_ = [("name", C.c_char_p), ("data", C.c_void_p), ("type", C.c_int32)]
+
+
+PLAN_FILTER, PLAN_GROUPBY, PLAN_SORT = 0, 1, 2
+STMT_KINDS = ["Select", "Insert", "Explain", "Alter", "Create", "Describe", "Drop", "Truncate", "Optimize", "Set"]
+# TokenType order (reference src/parser/tokenizer/token.rs:5-91)
+TOKEN_TYPES = [
+    "KeywordOrIdentifier", "DelimitedIdentifier", "ConfigIdentifier", "QueryParameter", "RawStringLiteral",
+    "EscapedSQStringLiteral", "EscapedDQStringLiteral", "IntegerLiteral", "FloatLiteral", "HexLiteral", "Comma",
+    "Dot", "Colon", "SemiColon", "Plus", "Minus", "Mul", "Div", "Mod", "Eq", "NotEq", "Lt", "Gt", "LtEq", "GtEq",
+    "LParen", "RParen", "LBracket", "RBracket", "LBrace", "RBrace", "BitAnd", "BitOr", "BitXor", "BitNot",
+    "BitLShift", "BitRShift", "Comment", "Whitespace", "EOF",
+]
+
+
 class NutError(RuntimeError):
     def __init__(self, status: int, where: str, message: str):
         self.status = status
@@ -95,6 +112,25 @@ SIGNATURES = {
     "nut_groupby_i64_f64": (_I32, [_P, _P, _P, _U64, C.c_uint32, _U64, C.POINTER(_P)]),
     "nut_q1": (_I32, [_P, _P, _P, _P, _P, _P, _P, _U64, _I64, C.POINTER(_P)]),
     "nut_sort_i64": (_I32, [_P, _P, _P, _U64]),
+    "nut_sort_i64_desc": (_I32, [_P, _P, _P, _U64]),
+    # SQL front end (CPU) and plan lowering / execution
+    "nut_sql_parse": (_I32, [C.c_char_p, C.c_size_t, C.POINTER(_P)]),
+    "nut_stmt_kind_of": (_I32, [_P]),
+    "nut_stmt_dump": (_I32, [_P, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
+    "nut_stmt_free": (None, [_P]),
+    "nut_sql_tokenize": (_I32, [C.c_char_p, C.c_size_t, C.POINTER(C.c_int32), C.POINTER(_U64), C.c_size_t,
+                                C.POINTER(C.c_size_t)]),
+    "nut_sql_unescape": (_I32, [C.c_char_p, C.c_size_t, _I32, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
+    "nut_sql_plan": (_I32, [C.c_char_p, C.c_size_t, C.POINTER(_P)]),
+    "nut_plan_kind_of": (_I32, [_P]),
+    "nut_plan_describe": (_I32, [_P, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
+    "nut_plan_free": (None, [_P]),
+    "nut_plan_execute": (_I32, [_P, _P, _P, _I32, _U64, _U64, C.POINTER(_P)]),
+    "nut_result_shape": (_I32, [_P, C.POINTER(_U64), C.POINTER(_I32)]),
+    "nut_result_column": (_I32, [_P, _I32, C.POINTER(_I32), C.POINTER(C.c_char_p)]),
+    "nut_result_to_host": (_I32, [_P, _I32, _P, _U64]),
+    "nut_result_device": (_I32, [_P, C.POINTER(_P)]),
+    "nut_result_free": (None, [_P]),
 }
 
 

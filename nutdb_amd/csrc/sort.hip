@@ -26,14 +26,15 @@ constexpr int RS_WAVES = RS_THREADS / kWave;
 constexpr int RS_ITEMS = 16;
 constexpr int RS_TILE = RS_THREADS * RS_ITEMS;  // 4096 keys
 constexpr int RS_BINS = 256;
-constexpr uint64_t RS_FLIP = 0x8000000000000000ull;
+constexpr uint64_t RS_FLIP = 0x8000000000000000ull;      // ascending: signed order -> unsigned order
+constexpr uint64_t RS_FLIP_DESC = 0x7FFFFFFFFFFFFFFFull; // descending: the complement of the above
 constexpr uint64_t RS_AGG = 1ull << 62;
 constexpr uint64_t RS_INC = 2ull << 62;
 constexpr uint64_t RS_VAL = (1ull << 62) - 1;
 constexpr uint32_t RS_SPIN_LIMIT = 1u << 24;
 
 // ---------------------------------------------------------------- histograms
-__global__ __launch_bounds__(RS_THREADS) void rs_hist_kernel(const int64_t *__restrict__ in, uint64_t n,
+__global__ __launch_bounds__(RS_THREADS) void rs_hist_kernel(const int64_t *__restrict__ in, uint64_t n, uint64_t flip,
                                                              unsigned long long *__restrict__ hist) {
   __shared__ uint32_t h[8][RS_BINS];
   for (int i = threadIdx.x; i < 8 * RS_BINS; i += RS_THREADS) (&h[0][0])[i] = 0;
@@ -50,8 +51,8 @@ __global__ __launch_bounds__(RS_THREADS) void rs_hist_kernel(const int64_t *__re
       a = (uint64_t)in[i];
       b = two ? (uint64_t)in[i + 1] : 0;
     }
-    a ^= RS_FLIP;
-    b ^= RS_FLIP;
+    a ^= flip;
+    b ^= flip;
 #pragma unroll
     for (int p = 0; p < 8; ++p) {
       atomicAdd(&h[p][(a >> (8 * p)) & 255], 1u);
@@ -104,7 +105,7 @@ __device__ __forceinline__ uint64_t digit_peers(uint32_t d, bool valid) {
 // FIRST: input is raw int64 (flip on load); LAST: write int64 (flip back)
 template <bool FIRST, bool LAST>
 __global__ __launch_bounds__(RS_THREADS) void rs_pass_kernel(const uint64_t *__restrict__ in, uint64_t *__restrict__ out,
-                                                             uint64_t n, int shift,
+                                                             uint64_t n, int shift, uint64_t flip,
                                                              const uint64_t *__restrict__ dbase,
                                                              uint64_t *__restrict__ status,
                                                              uint32_t *__restrict__ ticket,
@@ -130,7 +131,7 @@ __global__ __launch_bounds__(RS_THREADS) void rs_pass_kernel(const uint64_t *__r
   for (int i = 0; i < RS_ITEMS; ++i) {
     const uint64_t idx = wbase + (uint64_t)i * kWave + lane;
     uint64_t k = idx < n ? in[idx] : 0;
-    if (FIRST) k ^= RS_FLIP;
+    if (FIRST) k ^= flip;
     key[i] = k;
   }
   // stable in-wave ranking, items in order
@@ -221,7 +222,7 @@ __global__ __launch_bounds__(RS_THREADS) void rs_pass_kernel(const uint64_t *__r
     if (j < valid_n) {
       const uint64_t k = s_keys[j];
       const uint32_t dd = (uint32_t)(k >> shift) & 255u;
-      out[s_gbase[dd] + (j - s_tex[dd])] = LAST ? (k ^ RS_FLIP) : k;
+      out[s_gbase[dd] + (j - s_tex[dd])] = LAST ? (k ^ flip) : k;
     }
   }
 }
@@ -235,7 +236,7 @@ __global__ void rs_copy_kernel(const uint64_t *__restrict__ in, uint64_t *__rest
 
 using namespace nut;
 
-extern "C" nut_status nut_sort_i64(nut_ctx *c, const int64_t *in, int64_t *out, uint64_t n) {
+static nut_status sort_i64(nut_ctx *c, const int64_t *in, int64_t *out, uint64_t n, uint64_t flip) {
   if (!c || (n && (!in || !out))) return fail(NUT_ERR_INVALID_ARG, "nut_sort_i64: NULL argument");
   if (n && (uintptr_t)in == (uintptr_t)out) return fail(NUT_ERR_INVALID_ARG, "nut_sort_i64: in and out alias");
   if (n == 0) return NUT_OK;
@@ -265,7 +266,7 @@ extern "C" nut_status nut_sort_i64(nut_ctx *c, const int64_t *in, int64_t *out, 
   NUT_HIP(hipMemsetAsync(hist, 0, 8 * RS_BINS * 8, st));
   NUT_HIP(hipMemsetAsync(err, 0, 4, st));
   uint64_t hblocks = std::min<uint64_t>((n + 2 * RS_THREADS - 1) / (2 * RS_THREADS), (uint64_t)c->num_cus * 4);
-  hipLaunchKernelGGL(rs_hist_kernel, dim3((unsigned)hblocks), dim3(RS_THREADS), 0, st, in, n, hist);
+  hipLaunchKernelGGL(rs_hist_kernel, dim3((unsigned)hblocks), dim3(RS_THREADS), 0, st, in, n, flip, hist);
   hipLaunchKernelGGL(rs_scan_kernel, dim3(8), dim3(RS_BINS), 0, st, (const unsigned long long *)hist, n, base, triv);
   NUT_HIP(hipGetLastError());
   // which passes run is decided on the host (8 flags)
@@ -292,7 +293,7 @@ extern "C" nut_status nut_sort_i64(nut_ctx *c, const int64_t *in, int64_t *out, 
     const uint64_t *db = base + p * RS_BINS;
     auto kern = first ? (last ? rs_pass_kernel<true, true> : rs_pass_kernel<true, false>)
                       : (last ? rs_pass_kernel<false, true> : rs_pass_kernel<false, false>);
-    hipLaunchKernelGGL(kern, dim3((unsigned)ntiles), dim3(RS_THREADS), 0, st, src, dst, n, 8 * p, db, status, ticket,
+    hipLaunchKernelGGL(kern, dim3((unsigned)ntiles), dim3(RS_THREADS), 0, st, src, dst, n, 8 * p, flip, db, status, ticket,
                        err);
     NUT_HIP(hipGetLastError());
     src = dst;
@@ -302,4 +303,12 @@ extern "C" nut_status nut_sort_i64(nut_ctx *c, const int64_t *in, int64_t *out, 
   NUT_HIP(hipStreamSynchronize(st));
   if (htriv[0]) return fail(NUT_ERR_TIMEOUT, "nut_sort_i64: look-back spin limit hit");
   return NUT_OK;
+}
+
+extern "C" nut_status nut_sort_i64(nut_ctx *c, const int64_t *in, int64_t *out, uint64_t n) {
+  return sort_i64(c, in, out, n, RS_FLIP);
+}
+
+extern "C" nut_status nut_sort_i64_desc(nut_ctx *c, const int64_t *in, int64_t *out, uint64_t n) {
+  return sort_i64(c, in, out, n, RS_FLIP_DESC);
 }

@@ -1,0 +1,1079 @@
+// sql_plan.cpp — SQL C ABI (parse / tokenize / unescape) and plan lowering + execution
+// (SURVEY.md §8(a) B1).
+//
+// The reference stops at the statement tree; what an executor lowers from is
+//   QueryBody { columns, from, r#where, group_by, order_by, limit }  (ast/query.rs:21-35)
+// with WHERE already constant-folded by the parser (simplify.rs), so a WHERE may arrive
+// as a bare Literal::Boolean.  Lowering rules (DESIGN.md "Plan lowering"):
+//   * WHERE: AND-chain of  col <cmp> const | const <cmp> col | col BETWEEN c1 AND c2 |
+//     Boolean(true) (dropped) | Boolean(false) (empty result).  Comparisons are exact
+//     in the column's type: against an int64 column a non-integral constant moves the
+//     bound (x < 2.5 -> x <= 2) and an out-of-range constant folds to true/false.
+//   * constants: Literal::Integer(u128, sign) and Literal::Float(BigDecimal) (exact,
+//     converted with correct rounding for f64 columns), toDate('YYYY-MM-DD') and
+//     date +/- interval n day|month|year, as days since 1970-01-01.
+//   * SELECT-list FnCall Others(name): sum/count/min/max/avg, case-insensitive
+//     (the parser keeps the original case, mod.rs:1305); count(*) is the wildcard
+//     Identifier (mod.rs:1271); avg = sum / count.  Arguments: a column or one of the
+//     fused expression shapes of nut_expr (a*b, a+b, a-b, a*(1-b), a*(1-b)*(1+c)).
+//   * GROUP BY: 1-2 column identifiers; ORDER BY/LIMIT over the (small) group result
+//     run on the host after the device aggregation.
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+
+#include "common.hpp"
+#include "sql_ast.hpp"
+#include "sql_lexer.hpp"
+
+using namespace nut;
+using namespace nut::sql;
+
+struct nut_stmt {
+  std::string sql;   // the tree's views point into this copy
+  Statement st;
+};
+
+namespace {
+
+typedef __int128 i128;
+
+bool ieq(sv a, sv b) {
+  if (a.size() != b.size()) return false;
+  for (size_t i = 0; i < a.size(); ++i) {
+    char x = a[i], y = b[i];
+    if (x >= 'A' && x <= 'Z') x = (char)(x + 32);
+    if (y >= 'A' && y <= 'Z') y = (char)(y + 32);
+    if (x != y) return false;
+  }
+  return true;
+}
+
+std::string i128_str(i128 v) {
+  if (v == 0) return "0";
+  bool neg = v < 0;
+  unsigned __int128 m = neg ? (unsigned __int128)(-(v + 1)) + 1 : (unsigned __int128)v;
+  char buf[64];
+  int i = 63;
+  buf[i] = 0;
+  while (m) {
+    buf[--i] = (char)('0' + (int)(m % 10));
+    m /= 10;
+  }
+  if (neg) buf[--i] = '-';
+  return std::string(buf + i);
+}
+
+void json_str(std::string &o, sv s) {
+  o += '"';
+  for (unsigned char c : s) {
+    if (c == '"' || c == '\\') {
+      o += '\\';
+      o += (char)c;
+    } else if (c < 0x20) {
+      char b[8];
+      snprintf(b, sizeof b, "\\u%04x", c);
+      o += b;
+    } else {
+      o += (char)c;
+    }
+  }
+  o += '"';
+}
+
+// ------------------------------------------------------------------ constants
+constexpr i128 kHuge = (i128)1 << 100;  // saturation bound: anything beyond is "out of every range"
+
+struct CVal {
+  bool is_int = true;
+  i128 v = 0;        // integer value (saturated to +/-kHuge)
+  Decimal dec;       // float value
+};
+
+i128 sat_from_u128(u128 m, bool neg) {
+  i128 v = m > (u128)kHuge ? kHuge : (i128)m;
+  return neg ? -v : v;
+}
+
+// days since 1970-01-01 of a proleptic Gregorian date (civil-from-days inverse)
+int64_t days_from_civil(int64_t y, unsigned m, unsigned d) {
+  y -= m <= 2;
+  const int64_t era = (y >= 0 ? y : y - 399) / 400;
+  const unsigned yoe = (unsigned)(y - era * 400);
+  const unsigned doy = (153 * (m + (m > 2 ? -3 : 9)) + 2) / 5 + d - 1;
+  const unsigned doe = yoe * 365 + yoe / 4 - yoe / 100 + doy;
+  return era * 146097 + (int64_t)doe - 719468;
+}
+void civil_from_days(int64_t z, int64_t &y, unsigned &m, unsigned &d) {
+  z += 719468;
+  const int64_t era = (z >= 0 ? z : z - 146096) / 146097;
+  const unsigned doe = (unsigned)(z - era * 146097);
+  const unsigned yoe = (doe - doe / 1460 + doe / 36524 - doe / 146096) / 365;
+  y = (int64_t)yoe + era * 400;
+  const unsigned doy = doe - (365 * yoe + yoe / 4 - yoe / 100);
+  const unsigned mp = (5 * doy + 2) / 153;
+  d = doy - (153 * mp + 2) / 5 + 1;
+  m = mp + (mp < 10 ? 3 : -9);
+  y += m <= 2;
+}
+bool leap(int64_t y) { return (y % 4 == 0 && y % 100 != 0) || y % 400 == 0; }
+unsigned month_days(int64_t y, unsigned m) {
+  static const unsigned md[] = {31, 28, 31, 30, 31, 30, 31, 31, 30, 31, 30, 31};
+  return m == 2 && leap(y) ? 29 : md[m - 1];
+}
+
+bool parse_date(sv s, int64_t &days) {
+  if (s.size() != 10 || s[4] != '-' || s[7] != '-') return false;
+  auto num = [&](size_t a, size_t n, int64_t &out) {
+    out = 0;
+    for (size_t i = a; i < a + n; ++i) {
+      if (s[i] < '0' || s[i] > '9') return false;
+      out = out * 10 + (s[i] - '0');
+    }
+    return true;
+  };
+  int64_t y, m, d;
+  if (!num(0, 4, y) || !num(5, 2, m) || !num(8, 2, d)) return false;
+  if (m < 1 || m > 12 || d < 1 || d > (int64_t)month_days(y, (unsigned)m)) return false;
+  days = days_from_civil(y, (unsigned)m, (unsigned)d);
+  return true;
+}
+
+// date +/- n months, clamping the day to the target month's length
+int64_t add_months(int64_t days, i128 months) {
+  int64_t y;
+  unsigned m, d;
+  civil_from_days(days, y, m, d);
+  i128 t = (i128)y * 12 + (m - 1) + months;
+  int64_t ny = (int64_t)(t >= 0 ? t / 12 : -((-t + 11) / 12));
+  unsigned nm = (unsigned)(t - (i128)ny * 12) + 1;
+  unsigned nd = std::min(d, month_days(ny, nm));
+  return days_from_civil(ny, nm, nd);
+}
+
+struct Lowering {
+  std::string err;
+  bool fail(const std::string &m) {
+    if (err.empty()) err = m;
+    return false;
+  }
+};
+
+bool const_eval(const Expr &e, CVal &out, Lowering &L) {
+  if (e.k == EK::Literal) {
+    const Literal &l = *e.lit;
+    if (l.k == LitKind::Integer) {
+      out.is_int = true;
+      out.v = sat_from_u128(l.mag, !l.positive);
+      return true;
+    }
+    if (l.k == LitKind::Float) {
+      out.is_int = false;
+      out.dec = l.dec;
+      return true;
+    }
+    return false;
+  }
+  if (e.k == EK::FnCall && e.fn() == FnKind::Others && ieq(e.id.name, "todate") && e.kids.size() == 1 &&
+      e.kids[0].k == EK::Literal && e.kids[0].lit->k == LitKind::String) {
+    int64_t days;
+    if (!parse_date(e.kids[0].lit->str, days)) return L.fail("toDate: '" + e.kids[0].lit->str + "' is not YYYY-MM-DD");
+    out.is_int = true;
+    out.v = days;
+    return true;
+  }
+  if (e.k == EK::BinaryOp && (e.bop() == BinOp::Plus || e.bop() == BinOp::Minus)) {
+    const Expr &a = e.kids[0], &b = e.kids[1];
+    const i128 sign = e.bop() == BinOp::Plus ? 1 : -1;
+    CVal x;
+    if (b.k == EK::Literal && b.lit->k == LitKind::Interval) {
+      if (!const_eval(a, x, L) || !x.is_int) return false;
+      const i128 n = sign * (i128)b.lit->interval;
+      if (x.v > INT64_MAX || x.v < INT64_MIN) return false;
+      switch (b.lit->unit) {
+        case IntervalUnit::Day: out.v = x.v + n; break;
+        case IntervalUnit::Month: out.v = add_months((int64_t)x.v, n); break;
+        case IntervalUnit::Year: out.v = add_months((int64_t)x.v, 12 * n); break;
+        default: return L.fail("interval units below a day do not apply to day-number columns");
+      }
+      out.is_int = true;
+      return true;
+    }
+    CVal y;
+    if (const_eval(a, x, L) && const_eval(b, y, L) && x.is_int && y.is_int) {
+      i128 r = x.v + sign * y.v;
+      out.is_int = true;
+      out.v = r > kHuge ? kHuge : r < -kHuge ? -kHuge : r;
+      return true;
+    }
+  }
+  return false;
+}
+
+std::string cval_str(const CVal &c) { return c.is_int ? i128_str(c.v) : c.dec.str(); }
+
+// floor of an exact decimal, saturated; frac = true if it had a fractional part
+i128 dec_floor(const Decimal &d, bool &frac) {
+  const std::string &dg = d.digits;
+  const int64_t sc = d.scale;
+  const int64_t nint = (int64_t)dg.size() - sc;
+  frac = false;
+  i128 v = 0;
+  for (int64_t i = 0; i < nint; ++i) {
+    if (v > kHuge) break;
+    v = v * 10 + (i < (int64_t)dg.size() ? dg[(size_t)i] - '0' : 0);
+  }
+  if (v > kHuge) v = kHuge;
+  for (int64_t i = std::max<int64_t>(nint, 0); i < (int64_t)dg.size(); ++i)
+    if (dg[(size_t)i] != '0') frac = true;
+  if (d.neg) v = frac ? -v - 1 : -v;
+  return v;
+}
+
+// ------------------------------------------------------------------ plan
+const char *kCmpText[] = {"<", "<=", ">", ">=", "=", "!="};
+int cmp_of(BinOp op) {
+  switch (op) {
+    case BinOp::Lt: return NUT_LT;
+    case BinOp::LtEq: return NUT_LE;
+    case BinOp::Gt: return NUT_GT;
+    case BinOp::GtEq: return NUT_GE;
+    case BinOp::Eq: return NUT_EQ;
+    case BinOp::NotEq: return NUT_NE;
+    default: return -1;
+  }
+}
+int mirror(int op) { return op == NUT_LT ? NUT_GT : op == NUT_GT ? NUT_LT : op == NUT_LE ? NUT_GE : op == NUT_GE ? NUT_LE : op; }
+
+struct PlanPred {
+  int col, op;
+  CVal c;
+};
+struct PlanAgg {
+  int op, expr;
+  int arg[3];
+};
+enum OutKind { OUT_KEY, OUT_AGG, OUT_AVG };
+struct PlanOut {
+  int kind, a, b;
+  std::string name, text;
+};
+
+}  // namespace
+
+struct nut_plan {
+  int kind = NUT_PLAN_FILTER;
+  std::string table;
+  std::vector<std::string> cols;  // names the plan binds
+  bool never = false;             // WHERE folded to false
+  std::vector<PlanPred> preds;
+  int proj = -1;                  // FILTER/SORT column
+  bool desc = false;              // SORT direction
+  std::vector<int> keys, vals;    // GROUPBY key / value columns (indices into cols)
+  std::vector<PlanAgg> aggs;
+  std::vector<PlanOut> outs;
+  std::vector<std::pair<int, bool>> order;  // GROUPBY: (output, desc)
+  bool has_limit = false;
+  uint64_t limit = 0, offset = 0;
+};
+
+struct nut_result {
+  int kind = NUT_PLAN_FILTER;
+  int device = 0;
+  uint64_t nrows = 0;
+  std::vector<std::string> names;
+  std::vector<int> types;
+  void *dev = nullptr;  // FILTER/SORT: owned device buffer
+  uint64_t dev_off = 0;
+  std::vector<std::vector<uint64_t>> host;  // GROUPBY: output columns (int64 / f64 bits)
+};
+
+namespace {
+
+int col_index(nut_plan &p, sv name) {
+  for (size_t i = 0; i < p.cols.size(); ++i)
+    if (ieq(p.cols[i], name)) return (int)i;
+  p.cols.emplace_back(name);
+  return (int)p.cols.size() - 1;
+}
+
+bool column_ref(const Expr &e, sv &name) {
+  if (e.k != EK::Identifier || e.id.wildcard) return false;
+  name = e.id.name;
+  return true;
+}
+
+std::string expr_text(const Expr &e) {
+  static const char *bin[] = {"+", "-", "*", "/", "%", ">", "<", ">=", "<=", "=", "!=", "and", "or",
+                              "xor", "like", "not like", "ilike", "not ilike", "in", "not in", "[]",
+                              "|", "&", "^", "<<", ">>"};
+  switch (e.k) {
+    case EK::Identifier: {
+      std::string s;
+      if (e.id.qualified) s = std::string(e.id.qualifier) + ".";
+      return s + (e.id.wildcard ? std::string("*") : std::string(e.id.name));
+    }
+    case EK::Literal: {
+      const Literal &l = *e.lit;
+      if (l.k == LitKind::Integer) return (l.positive ? "" : "-") + i128_str((i128)l.mag);
+      if (l.k == LitKind::Float) return l.dec.str();
+      if (l.k == LitKind::String) return "'" + l.str + "'";
+      if (l.k == LitKind::Boolean) return l.positive ? "true" : "false";
+      return dump(e);
+    }
+    case EK::BinaryOp: {
+      auto side = [](const Expr &x) {
+        std::string t = expr_text(x);
+        return x.k == EK::BinaryOp ? "(" + t + ")" : t;
+      };
+      return side(e.kids[0]) + " " + bin[e.op] + " " + side(e.kids[1]);
+    }
+    case EK::FnCall:
+      if (e.fn() == FnKind::Others) {
+        std::string s = std::string(e.id.name) + "(";
+        for (size_t i = 0; i < e.kids.size(); ++i) s += (i ? ", " : "") + expr_text(e.kids[i]);
+        return s + ")";
+      }
+      return dump(e);
+    default: return dump(e);
+  }
+}
+
+bool is_one(const Expr &e) {
+  if (e.k != EK::Literal) return false;
+  const Literal &l = *e.lit;
+  if (l.k == LitKind::Integer) return l.positive && l.mag == 1;
+  if (l.k == LitKind::Float) {
+    Decimal one;
+    one.digits = "1";
+    return l.dec == one;
+  }
+  return false;
+}
+
+// SELECT-list aggregate argument -> fused expression shape (nut_expr)
+bool lower_agg_expr(nut_plan &p, const Expr &e, PlanAgg &a, Lowering &L) {
+  sv n0, n1, n2;
+  auto val = [&](sv n) {
+    int c = col_index(p, n);
+    for (size_t i = 0; i < p.vals.size(); ++i)
+      if (p.vals[i] == c) return (int)i;
+    p.vals.push_back(c);
+    return (int)p.vals.size() - 1;
+  };
+  a.arg[0] = a.arg[1] = a.arg[2] = 0;
+  if (column_ref(e, n0)) {
+    a.expr = NUT_EX_COL;
+    a.arg[0] = val(n0);
+    return true;
+  }
+  if (e.k == EK::BinaryOp) {
+    const Expr &l = e.kids[0], &r = e.kids[1];
+    if (column_ref(l, n0) && column_ref(r, n1)) {
+      BinOp op = e.bop();
+      if (op == BinOp::Multi || op == BinOp::Plus || op == BinOp::Minus) {
+        a.expr = op == BinOp::Multi ? NUT_EX_MUL : op == BinOp::Plus ? NUT_EX_ADD : NUT_EX_SUB;
+        a.arg[0] = val(n0);
+        a.arg[1] = val(n1);
+        return true;
+      }
+    }
+    // a * (1 - b)
+    if (e.bop() == BinOp::Multi && column_ref(l, n0) && r.k == EK::BinaryOp && r.bop() == BinOp::Minus &&
+        is_one(r.kids[0]) && column_ref(r.kids[1], n1)) {
+      a.expr = NUT_EX_MUL_1M;
+      a.arg[0] = val(n0);
+      a.arg[1] = val(n1);
+      return true;
+    }
+    // a * (1 - b) * (1 + c)
+    if (e.bop() == BinOp::Multi && l.k == EK::BinaryOp && l.bop() == BinOp::Multi && column_ref(l.kids[0], n0) &&
+        l.kids[1].k == EK::BinaryOp && l.kids[1].bop() == BinOp::Minus && is_one(l.kids[1].kids[0]) &&
+        column_ref(l.kids[1].kids[1], n1) && r.k == EK::BinaryOp && r.bop() == BinOp::Plus && is_one(r.kids[0]) &&
+        column_ref(r.kids[1], n2)) {
+      a.expr = NUT_EX_MUL_1M_1P;
+      a.arg[0] = val(n0);
+      a.arg[1] = val(n1);
+      a.arg[2] = val(n2);
+      return true;
+    }
+  }
+  return L.fail("aggregate argument '" + expr_text(e) +
+                "' is not a column or a fused expression shape (a*b, a+b, a-b, a*(1-b), a*(1-b)*(1+c))");
+}
+
+int add_agg(nut_plan &p, const PlanAgg &a) {
+  for (size_t i = 0; i < p.aggs.size(); ++i) {
+    const PlanAgg &b = p.aggs[i];
+    if (b.op == a.op && (a.op == NUT_AGG_COUNT ||
+                         (b.expr == a.expr && !memcmp(b.arg, a.arg, sizeof a.arg))))
+      return (int)i;
+  }
+  p.aggs.push_back(a);
+  return (int)p.aggs.size() - 1;
+}
+
+bool lower_pred_term(nut_plan &p, const Expr &e, Lowering &L) {
+  bool b;
+  if (e.is_bool_lit(&b)) {
+    if (!b) p.never = true;
+    return true;
+  }
+  sv name;
+  CVal c;
+  if (e.k == EK::BinaryOp && cmp_of(e.bop()) >= 0) {
+    int op = cmp_of(e.bop());
+    const Expr &l = e.kids[0], &r = e.kids[1];
+    if (column_ref(l, name) && const_eval(r, c, L)) {
+      p.preds.push_back({col_index(p, name), op, c});
+      return true;
+    }
+    if (column_ref(r, name) && const_eval(l, c, L)) {
+      p.preds.push_back({col_index(p, name), mirror(op), c});
+      return true;
+    }
+  }
+  if (e.k == EK::FnCall && e.fn() == FnKind::Between && e.kids.size() == 3 && column_ref(e.kids[0], name)) {
+    CVal lo, hi;
+    if (const_eval(e.kids[1], lo, L) && const_eval(e.kids[2], hi, L)) {
+      int ci = col_index(p, name);
+      p.preds.push_back({ci, NUT_GE, lo});
+      p.preds.push_back({ci, NUT_LE, hi});
+      return true;
+    }
+  }
+  return L.fail("unsupported WHERE term '" + expr_text(e) + "' (expected column <cmp> constant)");
+}
+
+bool lower_where(nut_plan &p, const Expr &e, Lowering &L) {
+  if (e.k == EK::BinaryOp && e.bop() == BinOp::And)
+    return lower_where(p, e.kids[0], L) && lower_where(p, e.kids[1], L);
+  return lower_pred_term(p, e, L);
+}
+
+bool lower(const Statement &st, nut_plan &p, Lowering &L) {
+  if (st.k != StmtKind::Select) return L.fail("only SELECT statements execute");
+  if (st.query.is_union) return L.fail("UNION/INTERSECT/EXCEPT are not executed (one query body per plan)");
+  const QueryBody &b = *st.query.body;
+  if (b.with) return L.fail("WITH is not executed");
+  if (b.distinct) return L.fail("DISTINCT is not executed");
+  if (!b.from || b.from->k != SourceKind::Table) return L.fail("FROM must name one table");
+  if (!b.joins.empty()) return L.fail("JOIN is not executed");
+  if (b.having) return L.fail("HAVING is not executed");
+  p.table = std::string(b.from->table);
+  if (b.where && !lower_where(p, *b.where, L)) return false;
+  if (p.preds.size() > NUT_MAX_PRED) return L.fail("more than 4 WHERE terms");
+  if (b.limit) {
+    p.has_limit = true;
+    p.limit = b.limit->size;
+    p.offset = b.limit->offset;
+    if (b.limit->with_ties) return L.fail("LIMIT ... WITH TIES is not executed");
+  }
+
+  if (b.group_by) {
+    p.kind = NUT_PLAN_GROUPBY;
+    for (const QueryExpr &k : *b.group_by) {
+      sv name;
+      if (!column_ref(k.e, name)) return L.fail("GROUP BY keys must be columns");
+      p.keys.push_back(col_index(p, name));
+    }
+    if (p.keys.empty() || p.keys.size() > NUT_MAX_KEYS) return L.fail("GROUP BY takes 1 or 2 key columns");
+    int count_idx = -1;
+    for (const QueryExpr &q : b.columns) {
+      PlanOut o;
+      o.text = expr_text(q.e);
+      o.name = q.alias ? std::string(*q.alias) : o.text;
+      sv name;
+      if (column_ref(q.e, name)) {
+        int c = col_index(p, name), j = -1;
+        for (size_t i = 0; i < p.keys.size(); ++i)
+          if (p.keys[i] == c) j = (int)i;
+        if (j < 0) return L.fail("column '" + std::string(name) + "' is neither a GROUP BY key nor aggregated");
+        o.kind = OUT_KEY;
+        o.a = j;
+      } else if (q.e.k == EK::FnCall && q.e.fn() == FnKind::Others) {
+        sv fn = q.e.id.name;
+        int op = ieq(fn, "sum") ? NUT_AGG_SUM : ieq(fn, "count") ? NUT_AGG_COUNT : ieq(fn, "min") ? NUT_AGG_MIN
+                 : ieq(fn, "max") ? NUT_AGG_MAX : ieq(fn, "avg") ? 100 : -1;
+        if (op < 0) return L.fail("function '" + std::string(fn) + "' is not an executed aggregate (sum/count/min/max/avg)");
+        PlanAgg a{};
+        if (op == NUT_AGG_COUNT) {
+          if (q.e.kids.size() > 1) return L.fail("count takes at most one argument");
+          if (q.e.kids.size() == 1 && !(q.e.kids[0].k == EK::Identifier)) return L.fail("count argument must be * or a column");
+          a.op = NUT_AGG_COUNT;
+          a.expr = NUT_EX_COL;
+          o.kind = OUT_AGG;
+          o.a = add_agg(p, a);
+        } else {
+          if (q.e.kids.size() != 1) return L.fail(std::string(fn) + " takes one argument");
+          if (!lower_agg_expr(p, q.e.kids[0], a, L)) return false;
+          if (op == 100) {
+            a.op = NUT_AGG_SUM;
+            o.kind = OUT_AVG;
+            o.a = add_agg(p, a);
+            PlanAgg c{};
+            c.op = NUT_AGG_COUNT;
+            o.b = add_agg(p, c);
+          } else {
+            a.op = op;
+            o.kind = OUT_AGG;
+            o.a = add_agg(p, a);
+          }
+        }
+      } else {
+        return L.fail("SELECT item '" + o.text + "' is not a key column or an aggregate");
+      }
+      p.outs.push_back(std::move(o));
+    }
+    (void)count_idx;
+    if (p.aggs.size() > NUT_MAX_AGGS) return L.fail("more than 8 aggregates");
+    if (p.vals.size() > NUT_MAX_VALS) return L.fail("aggregates reference more than 4 value columns");
+    if (b.order_by) {
+      for (const OrderKey &k : *b.order_by) {
+        int idx = -1;
+        sv name;
+        std::string text = expr_text(k.e.e);
+        for (size_t i = 0; i < p.outs.size() && idx < 0; ++i) {
+          const PlanOut &o = p.outs[i];
+          if (ieq(o.name, text) || ieq(o.text, text)) idx = (int)i;
+          if (idx < 0 && column_ref(k.e.e, name) && o.kind == OUT_KEY && ieq(p.cols[p.keys[o.a]], name)) idx = (int)i;
+        }
+        if (idx < 0) return L.fail("ORDER BY '" + text + "' is not an output column");
+        p.order.push_back({idx, k.desc});
+      }
+    }
+    return true;
+  }
+
+  // no GROUP BY: one projected column
+  for (const QueryExpr &q : b.columns)
+    if (q.e.k == EK::FnCall) return L.fail("aggregates without GROUP BY are not executed");
+  sv name;
+  if (b.columns.size() != 1 || !column_ref(b.columns[0].e, name))
+    return L.fail("a plan without GROUP BY projects exactly one column");
+  p.proj = col_index(p, name);
+  PlanOut o;
+  o.kind = OUT_KEY;
+  o.a = 0;
+  o.text = std::string(name);
+  o.name = b.columns[0].alias ? std::string(*b.columns[0].alias) : o.text;
+  p.outs.push_back(o);
+  for (const PlanPred &pr : p.preds)
+    if (pr.col != p.proj) return L.fail("WHERE must test the projected column (single-column scan)");
+  if (p.preds.size() > 1) return L.fail("a scan takes one comparison");
+  if (b.order_by) {
+    if (b.order_by->size() != 1) return L.fail("ORDER BY takes one key");
+    const OrderKey &k = (*b.order_by)[0];
+    sv oname;
+    if (!column_ref(k.e.e, oname) || !(ieq(oname, p.cols[p.proj]) || ieq(oname, p.outs[0].name)))
+      return L.fail("ORDER BY must name the projected column");
+    p.kind = NUT_PLAN_SORT;
+    p.desc = k.desc;
+  } else {
+    p.kind = NUT_PLAN_FILTER;
+  }
+  return true;
+}
+
+std::string describe(const nut_plan &p) {
+  static const char *kinds[] = {"filter", "groupby", "sort"};
+  static const char *aggs[] = {"sum", "count", "min", "max"};
+  static const char *exprs[] = {"col", "mul", "add", "sub", "mul_1m", "mul_1m_1p"};
+  static const int nargs[] = {1, 2, 2, 2, 2, 3};
+  std::string o = "{\"kind\":\"";
+  o += kinds[p.kind];
+  o += "\",\"table\":";
+  json_str(o, p.table);
+  o += ",\"columns\":[";
+  for (size_t i = 0; i < p.cols.size(); ++i) {
+    if (i) o += ',';
+    json_str(o, p.cols[i]);
+  }
+  o += "],\"never\":";
+  o += p.never ? "true" : "false";
+  o += ",\"where\":[";
+  for (size_t i = 0; i < p.preds.size(); ++i) {
+    const PlanPred &pr = p.preds[i];
+    if (i) o += ',';
+    o += "{\"col\":";
+    json_str(o, p.cols[pr.col]);
+    o += ",\"op\":\"";
+    o += kCmpText[pr.op];
+    o += "\",\"value\":\"" + cval_str(pr.c) + "\",\"value_kind\":\"" + (pr.c.is_int ? "int" : "decimal") + "\"}";
+  }
+  o += "]";
+  if (p.kind == NUT_PLAN_GROUPBY) {
+    o += ",\"keys\":[";
+    for (size_t i = 0; i < p.keys.size(); ++i) {
+      if (i) o += ',';
+      json_str(o, p.cols[p.keys[i]]);
+    }
+    o += "],\"values\":[";
+    for (size_t i = 0; i < p.vals.size(); ++i) {
+      if (i) o += ',';
+      json_str(o, p.cols[p.vals[i]]);
+    }
+    o += "],\"aggs\":[";
+    for (size_t i = 0; i < p.aggs.size(); ++i) {
+      const PlanAgg &a = p.aggs[i];
+      if (i) o += ',';
+      o += "{\"op\":\"";
+      o += aggs[a.op];
+      o += "\"";
+      if (a.op != NUT_AGG_COUNT) {
+        o += ",\"expr\":\"";
+        o += exprs[a.expr];
+        o += "\",\"args\":[";
+        for (int j = 0; j < nargs[a.expr]; ++j) {
+          if (j) o += ',';
+          json_str(o, p.cols[p.vals[a.arg[j]]]);
+        }
+        o += "]";
+      }
+      o += "}";
+    }
+    o += "]";
+  } else {
+    o += ",\"column\":";
+    json_str(o, p.cols[p.proj]);
+  }
+  if (p.kind == NUT_PLAN_SORT) o += p.desc ? ",\"desc\":true" : ",\"desc\":false";
+  o += ",\"outputs\":[";
+  for (size_t i = 0; i < p.outs.size(); ++i) {
+    const PlanOut &u = p.outs[i];
+    if (i) o += ',';
+    o += "{\"name\":";
+    json_str(o, u.name);
+    o += u.kind == OUT_KEY ? ",\"from\":\"key\",\"index\":" + std::to_string(u.a)
+         : u.kind == OUT_AGG ? ",\"from\":\"agg\",\"index\":" + std::to_string(u.a)
+                             : ",\"from\":\"avg\",\"sum\":" + std::to_string(u.a) + ",\"count\":" + std::to_string(u.b);
+    o += "}";
+  }
+  o += "],\"order\":[";
+  for (size_t i = 0; i < p.order.size(); ++i) {
+    if (i) o += ',';
+    o += "{\"output\":" + std::to_string(p.order[i].first) + ",\"desc\":" + (p.order[i].second ? "true" : "false") + "}";
+  }
+  o += "],\"limit\":";
+  o += p.has_limit ? std::to_string(p.limit) : "null";
+  o += ",\"offset\":" + std::to_string(p.offset) + "}";
+  return o;
+}
+
+nut_status put_text(const std::string &s, char *buf, size_t cap, size_t *len) {
+  if (len) *len = s.size();
+  if (buf && cap) {
+    size_t n = std::min(cap - 1, s.size());
+    memcpy(buf, s.data(), n);
+    buf[n] = 0;
+  }
+  if (cap < s.size() + 1) return fail(NUT_ERR_CAPACITY, "buffer of " + std::to_string(cap) + " bytes < " +
+                                                         std::to_string(s.size() + 1) + " needed");
+  return NUT_OK;
+}
+
+nut_status parse_into(const char *sql, size_t len, nut_stmt *s) {
+  size_t bad = 0;
+  if (!valid_utf8(sql, len, &bad))
+    return fail(NUT_ERR_INVALID_ARG, "sql is not valid UTF-8 (byte " + std::to_string(bad) + ")");
+  s->sql.assign(sql, len);
+  ParseError pe;
+  if (!parse(sv(s->sql), s->st, pe)) return fail(NUT_ERR_PARSE, pe.str());
+  return NUT_OK;
+}
+
+// ------------------------------------------------------------------ predicate resolution
+enum Verdict { V_PRED, V_TRUE, V_FALSE };
+
+Verdict resolve_i64(int op, const CVal &c, int &out_op, int64_t &k) {
+  i128 v;
+  bool frac = false;
+  if (c.is_int)
+    v = c.v;
+  else
+    v = dec_floor(c.dec, frac);
+  out_op = op;
+  if (frac) {  // x <cmp> v with floor(v) < v < floor(v)+1
+    switch (op) {
+      case NUT_LT:
+      case NUT_LE: out_op = NUT_LE; break;
+      case NUT_GT:
+      case NUT_GE: out_op = NUT_GT; break;
+      case NUT_EQ: return V_FALSE;
+      default: return V_TRUE;
+    }
+  }
+  if (v > INT64_MAX) return (out_op == NUT_LT || out_op == NUT_LE || out_op == NUT_NE) ? V_TRUE : V_FALSE;
+  if (v < INT64_MIN) return (out_op == NUT_GT || out_op == NUT_GE || out_op == NUT_NE) ? V_TRUE : V_FALSE;
+  k = (int64_t)v;
+  return V_PRED;
+}
+
+double resolve_f64(const CVal &c) { return c.is_int ? (double)c.v : c.dec.to_f64(); }
+
+const nut_column *bind(const nut_plan &p, int ci, const nut_column *cols, int ncols) {
+  for (int i = 0; i < ncols; ++i)
+    if (cols[i].name && ieq(cols[i].name, p.cols[ci])) return &cols[i];
+  return nullptr;
+}
+
+struct DevBuf {
+  void *p = nullptr;
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+};
+
+nut_status exec_scan(nut_ctx *c, const nut_plan &p, const nut_column *const *bound, uint64_t n, nut_result *r) {
+  const nut_column *col = bound[p.proj];
+  if (col->type != NUT_T_I64) return fail(NUT_ERR_PLAN, "column '" + p.cols[p.proj] + "' must be int64 for a scan/sort");
+  r->names.push_back(p.outs[0].name);
+  r->types.push_back(NUT_T_I64);
+  int op = NUT_GE;
+  int64_t k = INT64_MIN;  // no predicate: every row passes
+  bool none = p.never || n == 0;
+  if (!none && !p.preds.empty()) {
+    Verdict v = resolve_i64(p.preds[0].op, p.preds[0].c, op, k);
+    if (v == V_FALSE) none = true;
+    if (v == V_TRUE) {
+      op = NUT_GE;
+      k = INT64_MIN;
+    }
+  }
+  uint64_t cnt = 0;
+  if (!none) {
+    NUT_HIP(hipMalloc(&r->dev, n * 8));
+    if (p.kind == NUT_PLAN_FILTER) {
+      nut_status s = nut_filter_i64(c, (const int64_t *)col->data, n, op, k, (int64_t *)r->dev, &cnt);
+      if (s) return s;
+    } else {
+      const int64_t *src = (const int64_t *)col->data;
+      DevBuf tmp;
+      cnt = n;
+      if (!p.preds.empty() && !(op == NUT_GE && k == INT64_MIN)) {
+        NUT_HIP(hipMalloc(&tmp.p, n * 8));
+        nut_status s = nut_filter_i64(c, src, n, op, k, (int64_t *)tmp.p, &cnt);
+        if (s) return s;
+        src = (const int64_t *)tmp.p;
+      }
+      nut_status s = p.desc ? nut_sort_i64_desc(c, src, (int64_t *)r->dev, cnt)
+                            : nut_sort_i64(c, src, (int64_t *)r->dev, cnt);
+      if (s) return s;
+      s = nut_ctx_sync(c);
+      if (s) return s;
+    }
+  }
+  uint64_t off = p.has_limit ? std::min(p.offset, cnt) : 0;
+  uint64_t rows = cnt - off;
+  if (p.has_limit) rows = std::min(rows, p.limit);
+  r->dev_off = off;
+  r->nrows = rows;
+  return NUT_OK;
+}
+
+nut_status exec_groupby(nut_ctx *c, const nut_plan &p, const nut_column *const *bound, uint64_t n, uint64_t hint,
+                        nut_result *r) {
+  nut_agg_spec s;
+  memset(&s, 0, sizeof s);
+  s.n = p.never ? 0 : n;
+  s.nkeys = (int32_t)p.keys.size();
+  for (size_t j = 0; j < p.keys.size(); ++j) {
+    const nut_column *k = bound[p.keys[j]];
+    if (k->type != NUT_T_I64) return fail(NUT_ERR_PLAN, "GROUP BY column '" + p.cols[p.keys[j]] + "' must be int64");
+    s.keys[j] = (const int64_t *)k->data;
+  }
+  for (const PlanPred &pr : p.preds) {
+    const nut_column *col = bound[pr.col];
+    if (col->type == NUT_T_I64) {
+      int op;
+      int64_t k;
+      Verdict v = resolve_i64(pr.op, pr.c, op, k);
+      if (v == V_TRUE) continue;
+      if (v == V_FALSE) {
+        s.n = 0;
+        continue;
+      }
+      s.pred_col[s.npred] = col->data;
+      s.pred_type[s.npred] = NUT_T_I64;
+      s.pred_op[s.npred] = op;
+      s.pred_i64[s.npred] = k;
+    } else {
+      s.pred_col[s.npred] = col->data;
+      s.pred_type[s.npred] = NUT_T_F64;
+      s.pred_op[s.npred] = pr.op;
+      s.pred_f64[s.npred] = resolve_f64(pr.c);
+    }
+    s.npred++;
+  }
+  s.nvals = (int32_t)p.vals.size();
+  for (size_t v = 0; v < p.vals.size(); ++v) {
+    s.val_col[v] = bound[p.vals[v]]->data;
+    s.val_type[v] = bound[p.vals[v]]->type;
+  }
+  std::vector<int> agg_f64(p.aggs.size(), 0);
+  s.naggs = (int32_t)p.aggs.size();
+  for (size_t a = 0; a < p.aggs.size(); ++a) {
+    const PlanAgg &g = p.aggs[a];
+    s.agg_op[a] = g.op;
+    s.agg_expr[a] = g.expr;
+    for (int j = 0; j < 3; ++j) s.agg_arg[a][j] = g.arg[j];
+    if (g.op != NUT_AGG_COUNT) {
+      bool f = s.val_type[g.arg[0]] == NUT_T_F64;
+      if (g.expr != NUT_EX_COL) {
+        static const int nargs[] = {1, 2, 2, 2, 2, 3};
+        for (int j = 0; j < nargs[g.expr]; ++j)
+          if (s.val_type[g.arg[j]] != NUT_T_F64)
+            return fail(NUT_ERR_PLAN, "fused aggregate expressions need float64 columns ('" +
+                                          p.cols[p.vals[g.arg[j]]] + "' is int64)");
+        f = true;
+      }
+      agg_f64[a] = f;
+    }
+  }
+  if (s.n == 0) {  // keep the kernels' pointer checks happy for an empty scan
+    s.npred = 0;
+  }
+  nut_groups *g = nullptr;
+  nut_status st = nut_groupby(c, &s, hint, &g);
+  if (st) return st;
+  uint64_t ng = 0;
+  st = nut_groups_size(g, &ng);
+  std::vector<int64_t> keys(ng * p.keys.size() + 1);
+  std::vector<uint64_t> words(ng * p.aggs.size() + 1);
+  if (!st) st = nut_groups_to_host(g, keys.data(), words.data(), ng);
+  nut_groups_free(g);
+  if (st) return st;
+  const size_t nk = p.keys.size(), na = p.aggs.size();
+  // output columns in SELECT order
+  r->host.resize(p.outs.size());
+  for (size_t j = 0; j < p.outs.size(); ++j) {
+    const PlanOut &o = p.outs[j];
+    std::vector<uint64_t> &col = r->host[j];
+    col.resize(ng);
+    int type = NUT_T_I64;
+    if (o.kind == OUT_KEY) {
+      for (uint64_t i = 0; i < ng; ++i) col[i] = (uint64_t)keys[i * nk + o.a];
+    } else if (o.kind == OUT_AGG) {
+      type = agg_f64[o.a] ? NUT_T_F64 : NUT_T_I64;
+      for (uint64_t i = 0; i < ng; ++i) col[i] = words[i * na + o.a];
+    } else {
+      type = NUT_T_F64;
+      for (uint64_t i = 0; i < ng; ++i) {
+        uint64_t sw = words[i * na + o.a];
+        double sum;
+        if (agg_f64[o.a])
+          memcpy(&sum, &sw, 8);
+        else
+          sum = (double)(int64_t)sw;
+        double avg = sum / (double)(int64_t)words[i * na + o.b];
+        memcpy(&col[i], &avg, 8);
+      }
+    }
+    r->names.push_back(o.name);
+    r->types.push_back(type);
+  }
+  // ORDER BY over outputs (groups arrive sorted by key tuple), then LIMIT
+  std::vector<uint64_t> idx(ng);
+  for (uint64_t i = 0; i < ng; ++i) idx[i] = i;
+  if (!p.order.empty()) {
+    std::stable_sort(idx.begin(), idx.end(), [&](uint64_t x, uint64_t y) {
+      for (const auto &ok : p.order) {
+        const std::vector<uint64_t> &col = r->host[ok.first];
+        int cmp;
+        if (r->types[ok.first] == NUT_T_F64) {
+          double a, b;
+          memcpy(&a, &col[x], 8);
+          memcpy(&b, &col[y], 8);
+          cmp = a < b ? -1 : a > b ? 1 : 0;
+        } else {
+          int64_t a = (int64_t)col[x], b = (int64_t)col[y];
+          cmp = a < b ? -1 : a > b ? 1 : 0;
+        }
+        if (cmp) return ok.second ? cmp > 0 : cmp < 0;
+      }
+      return false;
+    });
+  }
+  uint64_t off = p.has_limit ? std::min(p.offset, ng) : 0;
+  uint64_t rows = ng - off;
+  if (p.has_limit) rows = std::min(rows, p.limit);
+  for (auto &col : r->host) {
+    std::vector<uint64_t> out(rows);
+    for (uint64_t i = 0; i < rows; ++i) out[i] = col[idx[off + i]];
+    col.swap(out);
+  }
+  r->nrows = rows;
+  return NUT_OK;
+}
+
+}  // namespace
+
+// ====================================================================== C ABI
+extern "C" {
+
+nut_status nut_sql_parse(const char *sql, size_t len, nut_stmt **out) {
+  if (!out || (!sql && len)) return fail(NUT_ERR_INVALID_ARG, "nut_sql_parse: NULL argument");
+  *out = nullptr;
+  nut_stmt *s = new (std::nothrow) nut_stmt;
+  if (!s) return fail(NUT_ERR_OOM, "nut_sql_parse: out of host memory");
+  nut_status st = parse_into(sql ? sql : "", len, s);
+  if (st) {
+    delete s;
+    return st;
+  }
+  *out = s;
+  return NUT_OK;
+}
+
+int nut_stmt_kind_of(const nut_stmt *s) { return s ? (int)s->st.k : -1; }
+
+nut_status nut_stmt_dump(const nut_stmt *s, char *buf, size_t cap, size_t *len) {
+  if (!s) return fail(NUT_ERR_INVALID_ARG, "nut_stmt_dump: NULL statement");
+  return put_text(dump(s->st), buf, cap, len);
+}
+
+void nut_stmt_free(nut_stmt *s) { delete s; }
+
+nut_status nut_sql_tokenize(const char *sql, size_t len, int32_t *types, uint64_t *spans, size_t cap, size_t *ntok) {
+  if (!ntok || (!sql && len) || (cap && (!types || !spans)))
+    return fail(NUT_ERR_INVALID_ARG, "nut_sql_tokenize: NULL argument");
+  size_t bad = 0;
+  if (!valid_utf8(sql, len, &bad))
+    return fail(NUT_ERR_INVALID_ARG, "sql is not valid UTF-8 (byte " + std::to_string(bad) + ")");
+  Tokenizer tz(sql ? sql : "", len);
+  size_t n = 0;
+  for (;;) {
+    Token t;
+    LexError le;
+    if (!tz.next_token(t, le)) {
+      *ntok = n;
+      return fail(NUT_ERR_PARSE, le.str());
+    }
+    if (n >= cap) {
+      *ntok = n;
+      return fail(NUT_ERR_CAPACITY, "nut_sql_tokenize: more than " + std::to_string(cap) + " tokens");
+    }
+    types[n] = (int32_t)t.t;
+    spans[2 * n] = t.span.start;
+    spans[2 * n + 1] = t.span.end;
+    ++n;
+    if (t.t == Tok::Eof) break;
+  }
+  *ntok = n;
+  return NUT_OK;
+}
+
+nut_status nut_sql_unescape(const char *s, size_t len, int quote, char *out, size_t cap, size_t *out_len) {
+  if (!out_len || (!s && len) || (quote != '\'' && quote != '"'))
+    return fail(NUT_ERR_INVALID_ARG, "nut_sql_unescape: bad argument");
+  size_t bad = 0;
+  if (!valid_utf8(s, len, &bad)) return fail(NUT_ERR_INVALID_ARG, "nut_sql_unescape: input is not valid UTF-8");
+  std::string r;
+  ParseError pe;
+  if (!unescape(sv(s ? s : "", len), (char)quote, r, pe)) return fail(NUT_ERR_PARSE, pe.msg);  // SyntaxError Display
+  *out_len = r.size();
+  if (r.size() > cap) return fail(NUT_ERR_CAPACITY, "nut_sql_unescape: output needs " + std::to_string(r.size()) + " bytes");
+  if (!r.empty()) memcpy(out, r.data(), r.size());
+  return NUT_OK;
+}
+
+nut_status nut_sql_plan(const char *sql, size_t len, nut_plan **out) {
+  if (!out || (!sql && len)) return fail(NUT_ERR_INVALID_ARG, "nut_sql_plan: NULL argument");
+  *out = nullptr;
+  nut_stmt s;
+  nut_status st = parse_into(sql ? sql : "", len, &s);
+  if (st) return st;
+  nut_plan *p = new (std::nothrow) nut_plan;
+  if (!p) return fail(NUT_ERR_OOM, "nut_sql_plan: out of host memory");
+  Lowering L;
+  if (!lower(s.st, *p, L)) {
+    delete p;
+    return fail(NUT_ERR_PLAN, "cannot lower to an executor plan: " + L.err);
+  }
+  *out = p;
+  return NUT_OK;
+}
+
+int nut_plan_kind_of(const nut_plan *p) { return p ? p->kind : -1; }
+
+nut_status nut_plan_describe(const nut_plan *p, char *buf, size_t cap, size_t *len) {
+  if (!p) return fail(NUT_ERR_INVALID_ARG, "nut_plan_describe: NULL plan");
+  return put_text(describe(*p), buf, cap, len);
+}
+
+void nut_plan_free(nut_plan *p) { delete p; }
+
+nut_status nut_plan_execute(nut_ctx *c, const nut_plan *p, const nut_column *cols, int ncols, uint64_t nrows,
+                            uint64_t group_hint, nut_result **out) {
+  if (!c || !p || !out || (ncols && !cols) || ncols < 0) return fail(NUT_ERR_INVALID_ARG, "nut_plan_execute: NULL argument");
+  *out = nullptr;
+  std::vector<const nut_column *> bound(p->cols.size());
+  for (size_t i = 0; i < p->cols.size(); ++i) {
+    bound[i] = bind(*p, (int)i, cols, ncols);
+    if (!bound[i]) return fail(NUT_ERR_INVALID_ARG, "nut_plan_execute: column '" + p->cols[i] + "' is not bound");
+    if (bound[i]->type != NUT_T_I64 && bound[i]->type != NUT_T_F64)
+      return fail(NUT_ERR_INVALID_ARG, "nut_plan_execute: column '" + p->cols[i] + "' has an unknown type");
+    if (nrows && !bound[i]->data) return fail(NUT_ERR_INVALID_ARG, "nut_plan_execute: column '" + p->cols[i] + "' is NULL");
+  }
+  nut_result *r = new (std::nothrow) nut_result;
+  if (!r) return fail(NUT_ERR_OOM, "nut_plan_execute: out of host memory");
+  r->kind = p->kind;
+  r->device = c->device;
+  DeviceGuard g(c->device);
+  nut_status st = p->kind == NUT_PLAN_GROUPBY ? exec_groupby(c, *p, bound.data(), nrows, group_hint, r)
+                                              : exec_scan(c, *p, bound.data(), nrows, r);
+  if (st) {
+    nut_result_free(r);
+    return st;
+  }
+  *out = r;
+  return NUT_OK;
+}
+
+nut_status nut_result_shape(const nut_result *r, uint64_t *nrows, int *ncols) {
+  if (!r) return fail(NUT_ERR_INVALID_ARG, "nut_result_shape: NULL result");
+  if (nrows) *nrows = r->nrows;
+  if (ncols) *ncols = (int)r->names.size();
+  return NUT_OK;
+}
+
+nut_status nut_result_column(const nut_result *r, int j, int *type, const char **name) {
+  if (!r || j < 0 || j >= (int)r->names.size()) return fail(NUT_ERR_INVALID_ARG, "nut_result_column: bad column");
+  if (type) *type = r->types[j];
+  if (name) *name = r->names[j].c_str();
+  return NUT_OK;
+}
+
+nut_status nut_result_to_host(const nut_result *r, int j, void *dst, uint64_t cap) {
+  if (!r || j < 0 || j >= (int)r->names.size()) return fail(NUT_ERR_INVALID_ARG, "nut_result_to_host: bad column");
+  if (r->nrows > cap) return fail(NUT_ERR_CAPACITY, "nut_result_to_host: capacity < " + std::to_string(r->nrows));
+  if (r->nrows == 0) return NUT_OK;
+  if (!dst) return fail(NUT_ERR_INVALID_ARG, "nut_result_to_host: NULL dst");
+  if (r->kind == NUT_PLAN_GROUPBY) {
+    memcpy(dst, r->host[j].data(), r->nrows * 8);
+    return NUT_OK;
+  }
+  DeviceGuard g(r->device);
+  NUT_HIP(hipMemcpy(dst, (const int64_t *)r->dev + r->dev_off, r->nrows * 8, hipMemcpyDeviceToHost));
+  return NUT_OK;
+}
+
+nut_status nut_result_device(const nut_result *r, const void **dev) {
+  if (!r || !dev) return fail(NUT_ERR_INVALID_ARG, "nut_result_device: NULL argument");
+  if (r->kind == NUT_PLAN_GROUPBY) return fail(NUT_ERR_UNSUPPORTED, "nut_result_device: group results live on the host");
+  *dev = r->dev ? (const void *)((const int64_t *)r->dev + r->dev_off) : nullptr;
+  return NUT_OK;
+}
+
+void nut_result_free(nut_result *r) {
+  if (!r) return;
+  if (r->dev) {
+    DeviceGuard g(r->device);
+    (void)hipFree(r->dev);
+  }
+  delete r;
+}
+
+}  // extern "C"

@@ -281,13 +281,21 @@ class Executor:
         return Groups(self, h.value, 2, [np.float64, np.float64, np.float64, np.int64])
 
     # ---------------------------------------------------------------- sort
-    def sort_i64(self, col: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    def sort_i64(self, col: torch.Tensor, out: torch.Tensor | None = None, descending: bool = False) -> torch.Tensor:
         if col.dtype != torch.int64:
             raise TypeError("sort_i64 takes an int64 column")
         n = col.numel()
         if out is None:
             out = torch.empty(n, dtype=torch.int64, device=self.device)
         self._bind_stream()
-        check(lib.nut_sort_i64(self.ctx, C.c_void_p(_col(col, self.device) if n else None),
-                               C.c_void_p(out.data_ptr() if n else None), n), "nut_sort_i64")
+        fn = lib.nut_sort_i64_desc if descending else lib.nut_sort_i64
+        check(fn(self.ctx, C.c_void_p(_col(col, self.device) if n else None),
+                 C.c_void_p(out.data_ptr() if n else None), n), fn.__name__)
         return out
+
+    # ---------------------------------------------------------------- SQL
+    def sql(self, query: str, columns: dict, group_hint: int = 0) -> dict:
+        """Parse + lower `query` (nut_sql_plan) and run it on `columns` = {name: CUDA
+        tensor}.  Returns {output name: numpy array} in SELECT-list order."""
+        from .sql import Plan
+        return Plan(query).execute(self, columns, group_hint=group_hint)

@@ -1,0 +1,206 @@
+"""SQL front end and plan execution — Python mirror of the reference's interface.
+
+The reference's only public API is ``nutdb::parser::Parser::parse(&str) ->
+Result<Statement, ParseError>`` (src/lib.rs:3-4, src/parser/mod.rs:26-29).  Here the same
+call goes through the C ABI (``nut_sql_parse``) into the C++ restatement of the
+tokenizer/parser (nutdb_amd/csrc/sql_*.cpp):
+
+    >>> Parser.parse("select a from t where a < 5").kind
+    'Select'
+    >>> Parser.parse("select a from t order by a asc")   # A8(i): ASC is never consumed
+    Traceback (most recent call last):
+    ParseError: Syntax Error: fail to parse (more than one statement) at line 1 col 28
+
+``ParseError`` carries the reference's Display text ("Lex Error: ..." / "Syntax Error:
+...", src/parser/error.rs:8-57) and ``lex`` (LexError vs SyntaxError).  Everything in
+this module except ``execute`` runs on the CPU.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import json
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+
+from ._lib import (NUT_OK, STMT_KINDS, TOKEN_TYPES, NutColumn, NutError, T_F64, T_I64, check, lib)
+
+NUT_ERR_PARSE = 6
+NUT_ERR_CAPACITY = 5
+
+
+class ParseError(Exception):
+    """ParseError::{LexError, SyntaxError} (src/parser/error.rs:8-14)."""
+
+    def __init__(self, message: str):
+        super().__init__(message)
+        self.message = message
+        self.lex = message.startswith("Lex Error: ")
+
+
+def _last_error() -> str:
+    m = lib.nut_last_error()
+    return m.decode() if m else ""
+
+
+def _text(fn, handle) -> str:
+    need = C.c_size_t(0)
+    fn(handle, None, 0, C.byref(need))
+    buf = C.create_string_buffer(need.value + 1)
+    check(fn(handle, buf, len(buf), C.byref(need)), fn.__name__)
+    return buf.value.decode()
+
+
+class Statement:
+    """A parsed statement (ast::Statement, src/parser/ast/mod.rs:13-24)."""
+
+    def __init__(self, handle: int):
+        self._h = C.c_void_p(handle)
+
+    @property
+    def kind(self) -> str:
+        return STMT_KINDS[lib.nut_stmt_kind_of(self._h)]
+
+    def dump(self) -> str:
+        """S-expression of the tree (grammar: nutdb_amd/csrc/sql_dump.cpp)."""
+        return _text(lib.nut_stmt_dump, self._h)
+
+    def __repr__(self) -> str:
+        return f"Statement({self.dump()})"
+
+    def __del__(self):
+        h, self._h = getattr(self, "_h", None), None
+        if h:
+            lib.nut_stmt_free(h)
+
+
+class Parser:
+    @staticmethod
+    def parse(sql: str) -> Statement:
+        """Parser::parse (src/parser/mod.rs:26-29): raises ParseError on rejection."""
+        b = sql.encode("utf-8")
+        h = C.c_void_p()
+        st = lib.nut_sql_parse(b, len(b), C.byref(h))
+        if st == NUT_ERR_PARSE:
+            raise ParseError(_last_error())
+        check(st, "nut_sql_parse")
+        return Statement(h.value)
+
+
+def tokenize(sql: str) -> List[Tuple[str, str]]:
+    """Tokenizer::next_token until EOF (src/parser/tokenizer/mod.rs:66-112), whitespace and
+    comment tokens included: [(TokenType name, token text)].  Raises ParseError on a
+    lexical error."""
+    b = sql.encode("utf-8")
+    cap = len(b) + 2
+    types = (C.c_int32 * cap)()
+    spans = (C.c_uint64 * (2 * cap))()
+    n = C.c_size_t(0)
+    st = lib.nut_sql_tokenize(b, len(b), types, spans, cap, C.byref(n))
+    if st == NUT_ERR_PARSE:
+        raise ParseError("Lex Error: " + _last_error())
+    check(st, "nut_sql_tokenize")
+    return [(TOKEN_TYPES[types[i]], b[spans[2 * i]:spans[2 * i + 1]].decode()) for i in range(n.value)]
+
+
+def _unescape(s: str, quote: str) -> str:
+    b = s.encode("utf-8")
+    cap = len(b) * 4 + 4
+    out = C.create_string_buffer(cap)
+    n = C.c_size_t(0)
+    st = lib.nut_sql_unescape(b, len(b), ord(quote), out, cap, C.byref(n))
+    if st == NUT_ERR_PARSE:
+        raise ParseError(_last_error())
+    check(st, "nut_sql_unescape")
+    return out.raw[: n.value].decode()
+
+
+def unescape_single_quoted_string(s: str) -> str:
+    """src/parser/literal.rs:102"""
+    return _unescape(s, "'")
+
+
+def unescape_double_quoted_string(s: str) -> str:
+    """src/parser/literal.rs:103"""
+    return _unescape(s, '"')
+
+
+class Plan:
+    """An executor plan lowered from a SELECT."""
+
+    KINDS = ["filter", "groupby", "sort"]
+
+    def __init__(self, sql: str):
+        b = sql.encode("utf-8")
+        h = C.c_void_p()
+        st = lib.nut_sql_plan(b, len(b), C.byref(h))
+        if st == NUT_ERR_PARSE:
+            raise ParseError(_last_error())
+        check(st, "nut_sql_plan")
+        self._h = h
+
+    @property
+    def kind(self) -> str:
+        return self.KINDS[lib.nut_plan_kind_of(self._h)]
+
+    def describe(self) -> dict:
+        return json.loads(_text(lib.nut_plan_describe, self._h))
+
+    @property
+    def columns(self) -> List[str]:
+        return self.describe()["columns"]
+
+    def execute(self, ex, columns: Dict[str, "object"], nrows: Optional[int] = None,
+                group_hint: int = 0) -> Dict[str, np.ndarray]:
+        """Run on the GPU of executor `ex` with `columns` = {name: 1-D int64/float64 CUDA
+        tensor}.  Returns {output name: numpy array} in SELECT-list order."""
+        import torch
+        names = self.columns
+        arr = (NutColumn * max(len(columns), 1))()
+        keep = []
+        n = None
+        for i, (name, t) in enumerate(columns.items()):
+            if not isinstance(t, torch.Tensor) or not t.is_cuda or t.dim() != 1 or not t.is_contiguous():
+                raise ValueError(f"column {name!r} must be a contiguous 1-D CUDA tensor")
+            if t.dtype == torch.int64:
+                typ = T_I64
+            elif t.dtype == torch.float64:
+                typ = T_F64
+            else:
+                raise ValueError(f"column {name!r}: dtype {t.dtype} is not int64/float64")
+            nb = name.encode()
+            keep.append(nb)
+            arr[i] = NutColumn(nb, t.data_ptr(), typ)
+            if any(name.lower() == c.lower() for c in names):
+                n = t.numel() if n is None else n
+                if t.numel() != n:
+                    raise ValueError("bound columns differ in length")
+        rows = nrows if nrows is not None else (n or 0)
+        res = C.c_void_p()
+        ex._bind_stream()
+        check(lib.nut_plan_execute(ex.ctx, self._h, arr, len(columns), rows, group_hint, C.byref(res)),
+              "nut_plan_execute")
+        try:
+            nr = C.c_uint64(0)
+            nc = C.c_int(0)
+            check(lib.nut_result_shape(res, C.byref(nr), C.byref(nc)), "nut_result_shape")
+            out = {}
+            for j in range(nc.value):
+                typ = C.c_int(0)
+                nm = C.c_char_p()
+                check(lib.nut_result_column(res, j, C.byref(typ), C.byref(nm)), "nut_result_column")
+                a = np.empty(nr.value, dtype=np.float64 if typ.value == T_F64 else np.int64)
+                check(lib.nut_result_to_host(res, j, a.ctypes.data_as(C.c_void_p), nr.value), "nut_result_to_host")
+                out[nm.value.decode()] = a
+            return out
+        finally:
+            lib.nut_result_free(res)
+
+    def __del__(self):
+        h, self._h = getattr(self, "_h", None), None
+        if h:
+            lib.nut_plan_free(h)
+
+
+__all__ = ["ParseError", "Parser", "Plan", "Statement", "tokenize", "unescape_single_quoted_string",
+           "unescape_double_quoted_string", "NutError", "NUT_OK"]

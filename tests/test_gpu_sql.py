@@ -1,0 +1,137 @@
+"""GPU: SQL text -> nut_sql_plan -> HIP kernels, checked against the C oracle / numpy.
+
+Covers the plan lowering row end to end: the TPC-H Q1 text of the
+reference's fixture family (toDate/interval constants, fused expressions, avg), the
+filter / sort / group-by plan kinds, constant-comparison folding against int64 columns,
+ORDER BY / LIMIT over group results, and the binding errors.
+Tolerances: integer results bit-exact; f64 sums of non-dyadic values <= 1e-12 relative.
+"""
+import numpy as np
+import pytest
+import torch
+
+from helpers import F64_SUM_RTOL, OPCODE, rel_err
+
+pytestmark = pytest.mark.gpu
+
+LINEITEM_TAX = ("l_tax", 6, 0x47, 0, 9, 100.0)  # RANGE_F64: 0.00..0.08
+
+
+def dev(x, ex):
+    return torch.from_numpy(np.ascontiguousarray(x)).to(ex.device)
+
+
+def test_sql_tpch_q1(ex, orc):
+    from nutdb_amd.workloads import Q1_COLS, gen
+    n = 2_000_003
+    specs = Q1_COLS + [LINEITEM_TAX]
+    cols = {s[0]: gen(ex, s, n) for s in specs}
+    sql = """select l_returnflag, l_linestatus, sum(l_quantity) as sum_qty, sum(l_extendedprice) as sum_base_price,
+        sum(l_extendedprice * (1 - l_discount)) as sum_disc_price,
+        sum(l_extendedprice * (1 - l_discount) * (1 + l_tax)) as sum_charge,
+        avg(l_quantity) as avg_qty, avg(l_extendedprice) as avg_price, avg(l_discount) as avg_disc,
+        count(*) as count_order
+      from lineitem
+      where l_shipdate <= toDate('1998-12-01') - interval 90 day
+      group by l_returnflag, l_linestatus
+      order by l_returnflag, l_linestatus"""
+    got = ex.sql(sql, cols, group_hint=6)
+    sd, rf, ls, qty, price, disc, tax = [orc.gen(s, n) for s in specs]
+    ok, ow = orc.groupby([rf, ls], [(0, 0, (0,)), (0, 0, (1,)), (0, 4, (1, 2)), (0, 5, (1, 2, 3)), (1, 0, ()),
+                                    (0, 0, (2,))],
+                         values=[qty, price, disc, tax], preds=[(sd, OPCODE["<="], 10471)])
+    f = ow.view(np.float64)
+    cnt = ow[:, 4].astype(np.int64)
+    assert list(got) == ["l_returnflag", "l_linestatus", "sum_qty", "sum_base_price", "sum_disc_price",
+                         "sum_charge", "avg_qty", "avg_price", "avg_disc", "count_order"]
+    assert np.array_equal(got["l_returnflag"], ok[:, 0]) and np.array_equal(got["l_linestatus"], ok[:, 1])
+    assert np.array_equal(got["count_order"], cnt)
+    for name, j in (("sum_qty", 0), ("sum_base_price", 1), ("sum_disc_price", 2), ("sum_charge", 3)):
+        assert rel_err(got[name], f[:, j]) <= F64_SUM_RTOL, name
+    for name, j in (("avg_qty", 0), ("avg_price", 1), ("avg_disc", 5)):
+        assert rel_err(got[name], f[:, j] / cnt) <= 2 * F64_SUM_RTOL, name
+
+
+def test_sql_filter_plans(ex, orc):
+    from nutdb_amd.workloads import FILTER_COL, filter_k, gen
+    n = 3_000_017
+    col = gen(ex, FILTER_COL, n)
+    h = orc.gen(FILTER_COL, n)
+    k = filter_k(0.3)
+    want = orc.filter_i64(h, OPCODE["<"], k)
+    t = {"col": col}
+    assert np.array_equal(ex.sql(f"select col from t where col < {k}", t)["col"], want)
+    assert np.array_equal(ex.sql(f"select col from t where {k} > col", t)["col"], want)
+    # a non-integral constant moves the bound: col <= k.5  ==  col <= k
+    assert np.array_equal(ex.sql(f"select col from t where col <= {k}.5", t)["col"], h[h <= k])
+    assert np.array_equal(ex.sql(f"select col from t where col >= {k}.5", t)["col"], h[h > k])
+    # constants outside int64 fold to all/none
+    assert len(ex.sql("select col from t where col < 99999999999999999999999", t)["col"]) == n
+    assert len(ex.sql("select col from t where col > -1.5", t)["col"]) == n
+    assert len(ex.sql("select col from t where col = 3.5", t)["col"]) == 0
+    assert len(ex.sql("select col from t where 1 = 0", t)["col"]) == 0
+    assert np.array_equal(ex.sql("select col from t", t)["col"], h)
+    got = ex.sql(f"select col as c from t where col < {k} limit 10 offset 5", t)
+    assert list(got) == ["c"] and np.array_equal(got["c"], want[5:15])
+
+
+def test_sql_sort_plans(ex, orc):
+    from nutdb_amd.workloads import SORT_COL, gen
+    n = 1_000_003
+    key = gen(ex, SORT_COL, n)
+    h = orc.gen(SORT_COL, n)
+    s = np.sort(h)
+    t = {"k": key}
+    assert np.array_equal(ex.sql("select k from t order by k", t)["k"], s)
+    assert np.array_equal(ex.sql("select k from t order by k desc", t)["k"], s[::-1])
+    assert np.array_equal(ex.sql("select k from t where k < 0 order by k desc limit 100", t)["k"],
+                          np.sort(h[h < 0])[::-1][:100])
+    # direct descending entry point, including duplicates and extremes
+    v = np.concatenate([h[:1000], np.repeat(h[:10], 50), [np.iinfo(np.int64).min, np.iinfo(np.int64).max, 0, -1]])
+    out = ex.sort_i64(dev(v, ex), descending=True).cpu().numpy()
+    assert np.array_equal(out, np.sort(v)[::-1])
+
+
+def test_sql_groupby_order_limit(ex, orc):
+    from nutdb_amd import _lib as L
+    n = 1_500_007
+    G = 50
+    kspec = ("k", L.GEN_POOL_KEY, 0x61, G, 0, 1.0)
+    vspec = ("v", L.GEN_DYADIC, 0x62, 0, 0, 1.0)
+    ispec = ("i", L.GEN_FULL_I64, 0x63, 0, 0, 1.0)
+    cols = {s[0]: ex.gen_column(s[1], s[2], n, a=s[3], b=s[4], c=s[5]) for s in (kspec, vspec, ispec)}
+    k, v, i = (orc.gen(s, n) for s in (kspec, vspec, ispec))
+    got = ex.sql("select k, sum(v) as s, count(*) as c, min(v), max(v), avg(v) as a, sum(i) as si from t "
+                 "where v > 0.25 and v <= 8000 group by k order by c desc, k limit 7 offset 2", cols)
+    m = (v > 0.25) & (v <= 8000)
+    uk, inv = np.unique(k[m], return_inverse=True)
+    cnt = np.bincount(inv)
+    sums = np.bincount(inv, weights=v[m])  # dyadic values: exact in any order
+    mins = np.full(len(uk), np.inf)
+    maxs = np.full(len(uk), -np.inf)
+    np.minimum.at(mins, inv, v[m])
+    np.maximum.at(maxs, inv, v[m])
+    isum = np.zeros(len(uk), dtype=np.uint64)
+    np.add.at(isum, inv, i[m].view(np.uint64))  # two's-complement wrap
+    order = np.lexsort((uk, -cnt))[2:9]
+    assert list(got) == ["k", "s", "c", "min(v)", "max(v)", "a", "si"]
+    assert np.array_equal(got["k"], uk[order])
+    assert np.array_equal(got["c"], cnt[order])
+    assert np.array_equal(got["s"], sums[order])
+    assert np.array_equal(got["min(v)"], mins[order]) and np.array_equal(got["max(v)"], maxs[order])
+    assert np.array_equal(got["a"], sums[order] / cnt[order])
+    assert np.array_equal(got["si"], isum[order].view(np.int64))
+
+
+def test_sql_binding_errors(ex):
+    from nutdb_amd import NutError
+    a = torch.zeros(10, dtype=torch.int64, device=ex.device)
+    with pytest.raises(NutError) as e:
+        ex.sql("select k, sum(v) from t group by k", {"k": a})
+    assert e.value.status == 1 and "'v' is not bound" in str(e.value)
+    with pytest.raises(NutError) as e:
+        ex.sql("select k, sum(v * w) from t group by k", {"k": a, "v": a, "w": a})
+    assert e.value.status == 7 and "float64" in str(e.value)
+    with pytest.raises(NutError) as e:
+        ex.sql("select k from t group by k", {"k": a.double()})
+    assert e.value.status == 7

@@ -1,0 +1,460 @@
+"""CPU tests of the SQL front end and plan lowering (B1),
+through the C ABI (nut_sql_parse / nut_sql_tokenize / nut_sql_unescape / nut_sql_plan).
+
+Pins:
+  * every reference fixture parses Ok (reference tests/parser_test.rs:19-34), plus the
+    two criterion bench statements (benches/parser_bench.rs:5,8-46);
+  * the reference's tokenizer unit vectors (src/parser/tokenizer/mod.rs:576-782), its
+    Utf8Iter position vectors (utf8_iter.rs:284-307, observed through error positions)
+    and its unescape vectors (literal.rs:122-151);
+  * the A8 quirks as negative/positive cases, constant folding (simplify.rs) and the
+    error Display formats (error.rs:8-57).
+Expected tree shapes and error texts below were derived by hand from the reference's
+mod.rs; none of them is read from this implementation.
+"""
+from pathlib import Path
+
+import pytest
+
+from nutdb_amd.sql import (ParseError, Parser, Plan, tokenize, unescape_double_quoted_string,
+                           unescape_single_quoted_string)
+from nutdb_amd._lib import NutError
+
+SQL_DIR = Path(__file__).resolve().parent / "golden" / "sql"
+FIXTURES = sorted(SQL_DIR.glob("*.sql"), key=lambda p: p.name)
+
+
+def dump(sql):
+    return Parser.parse(sql).dump()
+
+
+def err(sql):
+    with pytest.raises(ParseError) as e:
+        Parser.parse(sql)
+    return e.value.message
+
+
+# ------------------------------------------------------------------ fixtures (A1)
+def test_fixture_set_is_complete():
+    names = {p.name for p in FIXTURES}
+    assert {f"{i}.sql" for i in range(1, 15)} <= names
+    assert {"bench_short.sql", "bench_long.sql"} <= names
+
+
+@pytest.mark.parametrize("path", FIXTURES, ids=lambda p: p.name)
+def test_reference_fixture_parses(path):
+    st = Parser.parse(path.read_text())
+    want = {"11.sql": "Create", "12.sql": "Create", "13.sql": "Insert"}.get(path.name, "Select")
+    assert st.kind == want
+
+
+def test_fixture_14_constant_folding():
+    # tests/sql/14.sql: every SELECT folds (simplify.rs); UNION ALL is left-associative
+    b = {
+        "t": "(body (columns (bool true)))", "f": "(body (columns (bool false)))",
+        "isnull": "(body (columns (is-null (id col))))",
+        "xor": "(body (columns (not (call random))))",
+    }
+    seq = ["t", "f", "t", "f", "t", "isnull", "f", "xor", "f"]
+    q = b[seq[0]]
+    for s in seq[1:]:
+        q = f"(union-all {q} {b[s]})"
+    assert dump((SQL_DIR / "14.sql").read_text()) == f"(select {q})"
+
+
+# ------------------------------------------------------------------ tokenizer (A2)
+def first(sql):
+    return tokenize(sql)[0]
+
+
+def test_tokenize_whitespaces():
+    toks = tokenize(" ".join(["    ", "\t\t", "\n", "\r\n", "\r"]))
+    assert [t for t, _ in toks] == ["Whitespace", "EOF"]
+
+
+@pytest.mark.parametrize("sql,kind", [("510", "IntegerLiteral"), ("0.123", "FloatLiteral"),
+                                      (".123", "FloatLiteral"), ("1.", "FloatLiteral"), ("0x123", "HexLiteral")])
+def test_tokenize_numerics(sql, kind):
+    assert first(sql)[0] == kind
+
+
+@pytest.mark.parametrize("sql", ["1d", "1好", "1.d", "0d", "1(", "1.(", "1.."])
+def test_tokenize_numerics_fail(sql):
+    with pytest.raises(ParseError):
+        tokenize(sql)
+
+
+@pytest.mark.parametrize("sql,text,kind", [
+    ('"hello"', "hello", "RawStringLiteral"),
+    ("'hello'", "hello", "RawStringLiteral"),
+    ("'he''llo'", "he''llo", "EscapedSQStringLiteral"),
+    ('"he""llo"', 'he""llo', "EscapedDQStringLiteral"),
+    ("'h\\t i\\r\\n'", "h\\t i\\r\\n", "EscapedSQStringLiteral"),
+    ("\"\\\n\"", "\\\n", "EscapedDQStringLiteral"),
+])
+def test_tokenize_strings(sql, text, kind):
+    assert first(sql) == (kind, text)
+
+
+@pytest.mark.parametrize("sql", ['"hello\'', '"\n"', '"\r"'])
+def test_tokenize_strings_fail(sql):
+    with pytest.raises(ParseError):
+        tokenize(sql)
+
+
+@pytest.mark.parametrize("sql,text,kind", [
+    ("hello_world", "hello_world", "KeywordOrIdentifier"),
+    ("`select`", "select", "DelimitedIdentifier"),
+    ("`你 好`", "你 好", "DelimitedIdentifier"),
+    ("@a", "a", "ConfigIdentifier"),
+])
+def test_tokenize_identifiers(sql, text, kind):
+    assert first(sql) == (kind, text)
+
+
+@pytest.mark.parametrize("sql", ["``", "@", "你好", "@你好", "hello_你好", "@1a", "a:"])
+def test_tokenize_identifiers_fail(sql):
+    with pytest.raises(ParseError):
+        tokenize(sql)
+
+
+@pytest.mark.parametrize("sql,text", [("$0", "0"), ("$01", "01"), ("$9", "9")])
+def test_tokenize_query_parameter(sql, text):
+    assert first(sql) == ("QueryParameter", text)
+
+
+@pytest.mark.parametrize("sql", ["$", "$a", "$0a", "$_0"])
+def test_tokenize_query_parameter_fail(sql):
+    with pytest.raises(ParseError):
+        tokenize(sql)
+
+
+@pytest.mark.parametrize("sql,idx,text", [("hello -- world", 2, "world"), ("/* hello */", 0, " hello "),
+                                          ("hello /* \n */world", 2, " \n ")])
+def test_tokenize_comment(sql, idx, text):
+    toks = tokenize(sql)
+    assert toks[idx] == ("Comment", text)
+
+
+@pytest.mark.parametrize("sql", ["/*", "/* /"])
+def test_tokenize_comment_fail(sql):
+    with pytest.raises(ParseError):
+        tokenize(sql)
+
+
+@pytest.mark.parametrize("sql,kind", [
+    (".", "Dot"), ("+", "Plus"), ("-", "Minus"), ("*", "Mul"), ("/", "Div"), ("%", "Mod"), ("&", "BitAnd"),
+    ("|", "BitOr"), ("^", "BitXor"), (">>", "BitRShift"), ("<<", "BitLShift"), ("=", "Eq"), ("!=", "NotEq"),
+    ("<>", "NotEq"), (">", "Gt"), (">=", "GtEq"), ("<", "Lt"), ("<=", "LtEq"), (":", "Colon"), (",", "Comma"),
+    (";", "SemiColon"), ("[", "LBracket"), ("]", "RBracket"), ("{", "LBrace"), ("}", "RBrace"), ("(", "LParen"),
+    (")", "RParen"), ("~", "BitNot"),
+])
+def test_tokenize_symbols(sql, kind):
+    assert first(sql)[0] == kind
+
+
+def test_tokenize_symbol_fail():
+    with pytest.raises(ParseError) as e:
+        tokenize("!")
+    assert e.value.message == "Lex Error: Unexpected Char: '!' can only be used with '=' near line 1 col 2"
+
+
+def test_tokenize_simple_query():
+    sql = "\nSELECT *\nFROM\n(\n    SELECT count() AS `c`\n    FROM events\n    WHERE event_type = $0\n" \
+          "    GROUP BY name\n)"
+    kinds = [t for t, _ in tokenize(sql) if t not in ("Whitespace", "EOF")]
+    K = "KeywordOrIdentifier"
+    assert kinds == [K, "Mul", K, "LParen", K, K, "LParen", "RParen", K, "DelimitedIdentifier", K, K, K, K, "Eq",
+                     "QueryParameter", K, K, K, "RParen"]
+
+
+# ------------------------------------------------------------------ positions (utf8_iter.rs:284-307)
+def test_positions_count_chars_tabs_and_crlf():
+    assert err("select * \n\t你好") == \
+        "Lex Error: Unexpected Char: '你' is invalid outside string literal near line 2 col 5"
+    assert err("select \n\tab + ❤") == \
+        "Lex Error: Unexpected Char: '❤' is invalid outside string literal near line 2 col 10"
+    assert err("select \n\tab❤") == \
+        "Lex Error: Unexpected Char: '❤' cannot be a part of identifier or keyword near line 2 col 7"
+    assert err("select 1\r\n$") == \
+        "Lex Error: Incomplete Token: query parameter should have an index near line 2 col 2"
+    assert err("select 1\r\r$") == \
+        "Lex Error: Incomplete Token: query parameter should have an index near line 3 col 2"
+
+
+# ------------------------------------------------------------------ unescape (literal.rs:122-151)
+@pytest.mark.parametrize("raw,want", [("'", "'"), ("'hello'", "'hello'"), ('h""i', 'h"i'),
+                                      ("\\r\\n\\t\\\\hello 你好", "\r\n\t\\hello 你好"), ("\\u{767D}", "白"),
+                                      ("\\\r\\\n", "\r\n")])
+def test_unescape_double_quoted(raw, want):
+    assert unescape_double_quoted_string(raw) == want
+
+
+@pytest.mark.parametrize("raw,want", [('"', '"'), ('"hello"', '"hello"'), ("h''i", "h'i"),
+                                      ("\\r\\n\\t\\\\hello 你好", "\r\n\t\\hello 你好"), ("\\u{767D}", "白"),
+                                      ("\\\r\\\n", "\r\n")])
+def test_unescape_single_quoted(raw, want):
+    assert unescape_single_quoted_string(raw) == want
+
+
+def test_unescape_edge_cases():
+    # '\u' not followed by '{' keeps 'u' and drops the char it consumed (literal.rs:70-90)
+    assert unescape_single_quoted_string("\\uab") == "ub"
+    assert unescape_single_quoted_string("\\q") == "q"
+    for bad in ("\\u{D800}", "\\u{110000}", "\\u{}", "\\u{zz}"):
+        with pytest.raises(ParseError) as e:
+            unescape_single_quoted_string(bad)
+        assert e.value.message.startswith("invalid escaped unicode '\\u{")
+    assert err("select '\\u{D800}'") == "Syntax Error: invalid escaped unicode '\\u{D800}' in string literal"
+
+
+# ------------------------------------------------------------------ expressions (A4) and literals (A6)
+@pytest.mark.parametrize("sql,tree", [
+    ("select a + b * c - d", "(- (+ (id a) (* (id b) (id c))) (id d))"),
+    ("select a or b and c xor d", "(or (id a) (xor (and (id b) (id c)) (id d)))"),
+    ("select a between 1 and 2 and b", "(and (between (id a) (int 1) (int 2)) (id b))"),
+    ("select a not between 1 and 2", "(not-between (id a) (int 1) (int 2))"),
+    ("select a not in (1, 2)", "(not-in (id a) (tuple (int 1) (int 2)))"),
+    ("select a not like 'x%'", "(not-like (id a) (str \"x%\"))"),
+    ("select a ilike 'x'", "(ilike (id a) (str \"x\"))"),
+    ("select x[1]", "(index (id x) (int 1))"),
+    ("select a | b & c", "(| (id a) (& (id b) (id c)))"),
+    ("select a << 1 + 2", "(<< (id a) (+ (int 1) (int 2)))"),
+    ("select ~a", "(bitnot (id a))"),
+    ("select a is not null", "(is-not-null (id a))"),
+    ("select not a = b", "(= (not (id a)) (id b))"),
+    ("select not exists(select 1)", "(not (call exists (subquery (body (columns (int 1))))))"),
+    ("select a not exists (select 1)", "(not-exists (subquery (body (columns (int 1)))))"),
+    ("select count(*)", "(call count (id *))"),
+    ("select t.*, t.`a b`", "(id t.*) (id t.`a b`)"),
+    ("select [1, 2], {1: 'a'}", "(array (int 1) (int 2)) (map (int 1) (str \"a\"))"),
+    ("select if a then 1 else 2 end", "(if (id a) (int 1) (int 2))"),
+    ("select case when a then 1 end", "(multi-if (id a) (int 1) null)"),
+    ("select case a when 1 then 2 else 3 end", "(case-when (id a) (int 1) (int 2) (int 3))"),
+    ("select -5, -0x10, -1.50, +3, .5, 1.", "(int -5) (int -16) (float -1.50) (int 3) (float 0.5) (float 1)"),
+    ("select 0.0001000000", "(float 0.0001000000)"),
+    ("select 340282366920938463463374607431768211455", "(int 340282366920938463463374607431768211455)"),
+    ("select interval 90 day", "(interval 90 day)"),
+    ("select $1 2", "(param 2)"),
+    ("select 1 = 1.0, -0 = 0, 1.0 = 1.00, null = null, 'a' != 'b'",
+     "(bool false) (bool false) (bool true) (bool true) (bool true)"),
+    ("select x and true, x and false, x or true, x or false, x xor false, not false, 1 is null",
+     "(id x) (bool false) (bool true) (id x) (id x) (bool true) (bool false)"),
+])
+def test_expression_trees(sql, tree):
+    assert dump(sql) == f"(select (body (columns {tree})))"
+
+
+def test_expression_trees_exact():
+    assert dump("select a + b * c - d from t") == \
+        "(select (body (columns (- (+ (id a) (* (id b) (id c))) (id d))) (from (table t))))"
+    assert dump("select k, sum(v) as s from t where k > 1 and v < 2.5 group by k order by s desc, k limit 3, 10") == \
+        ("(select (body (columns (id k) (as (call sum (id v)) s)) (from (table t)) "
+         "(where (and (> (id k) (int 1)) (< (id v) (float 2.5)))) (group-by (id k)) "
+         "(order-by (desc (id s)) (asc (id k))) (limit 10 3)))")
+    assert dump("select a from t limit 5 offset 2 with ties") == \
+        "(select (body (columns (id a)) (from (table t)) (limit 5 2 ties)))"
+
+
+# ------------------------------------------------------------------ A8 quirks
+def test_order_by_asc_is_rejected():
+    assert err("select a from t order by a asc") == \
+        "Syntax Error: fail to parse (more than one statement) at line 1 col 28"
+    assert "(order-by (desc (id a)))" in dump("select a from t order by a desc")
+    assert "(order-by (asc (id a)))" in dump("select a from t order by a")
+
+
+def test_query_parameter_needs_a_further_integer():
+    assert err("select $1") == "Syntax Error: expected token (IntegerLiteral, HexLiteral) but found token EOF " \
+                               "at line 1 col 10"
+
+
+def test_minus_only_before_numeric_literals():
+    assert err("select -col") == "Syntax Error: expected token (IntegerLiteral, HexLiteral, FloatLiteral) but found " \
+                                 "token KeywordOrIdentifier at line 1 col 9"
+
+
+def test_text_after_semicolon_is_never_read():
+    assert dump("select 1; this is 'not even lexed") == "(select (body (columns (int 1))))"
+
+
+def test_add_column_position_is_unreachable():
+    # column_def's attribute loop (mod.rs:941-969) consumes every keyword that follows the
+    # type, so FIRST/AFTER after a column definition is rejected
+    assert err("alter table t add column c Int8 after b") == \
+        "Syntax Error: expected keyword (default, comment) but found token after at line 1 col 33"
+
+
+def test_map_type_is_stored_value_first():
+    assert dump("create table t (m Map(Int8, String))") == \
+        "(create (table t (columns (column m (Map (String 0) Int8))) (constraints) (indexes)))"
+
+
+# ------------------------------------------------------------------ statements (A3)
+@pytest.mark.parametrize("sql,tree", [
+    ("insert into t (a, b) values (1, 2), (3, 4)",
+     "(insert t (columns a b) (rows 2 (int 1) (int 2) (int 3) (int 4)))"),
+    ("insert into t select 1", "(insert t (query (body (columns (int 1)))))"),
+    ("insert into t from input('a Int8')", "(insert t (fn (call input (str \"a Int8\"))))"),
+    ("explain select 1", "(explain (body (columns (int 1))))"),
+    ("alter table t add if not exists column c Int8", "(alter t (add if-not-exists (column c Int8)))"),
+    ("alter table t add constraint c check a > 0 after b", "(alter t (add (constraint c (> (id a) (int 0))) (after b)))"),
+    ("alter table t add index i f(a) first", "(alter t (add (index i (call f (id a))) first))"),
+    ("alter table t drop if exists partition '2020'", "(alter t (drop if-exists partition \"2020\"))"),
+    ("alter table t rename table u", "(alter t (rename table u))"),
+    ("alter table t rename column a b", "(alter t (rename column a b))"),
+    ("describe database", "(describe database)"),
+    ("describe view v", "(describe view v)"),
+    ("drop view if exists v", "(drop view if-exists v)"),
+    ("truncate table t", "(truncate table t)"),
+    ("optimize table t", "(optimize t)"),
+    ("optimize table t on partition 1", "(optimize t (int 1))"),
+    ("set @max_threads = 8", "(set max_threads (int 8))"),
+    ("create table if not exists t (a Int8 default 1 comment 'x', index i f(a), constraint c check a > 0) "
+     "primary key a order by a partition by a comment 'tbl'",
+     "(create if-not-exists (table t (columns (column a Int8 (default (int 1)) (comment \"x\"))) "
+     "(constraints (constraint c (> (id a) (int 0)))) (indexes (index i (call f (id a)))) (primary-key (id a)) "
+     "(order-by (id a)) (partition-by (id a)) (comment \"tbl\")))"),
+    ("create view v update by Summing order by a as select a from t",
+     "(create (view v (update-by Summing) (order-by (id a)) (body (columns (id a)) (from (table t)))))"),
+    ("create table t (e Enum('a', 'b' = 5, 'c'), d Decimal64(4), c Chars(3), n Nullable(Array(UInt8)))",
+     "(create (table t (columns (column e (Enum (\"a\" 0) (\"b\" 5) (\"c\" 6))) (column d (Decimal64 4)) "
+     "(column c (Chars 3)) (column n (Nullable (Array UInt8)))) (constraints) (indexes)))"),
+])
+def test_statement_trees(sql, tree):
+    assert dump(sql) == tree
+
+
+# ------------------------------------------------------------------ error formats (error.rs)
+@pytest.mark.parametrize("sql,msg", [
+    ("", "Syntax Error: empty query"),
+    (" ; select 1", "Syntax Error: empty query"),
+    ("update t", "Syntax Error: fail to parse (cannot recognize statement) at line 1 col 1"),
+    ("(select 1)", "Syntax Error: fail to parse (statements should start with a keyword) at line 1 col 1"),
+    ("select 'abc", "Lex Error: Unexpected EOF: string literal is not complete near line 1 col 12"),
+    ("select 1 from t where a !b", "Lex Error: Unexpected Char: '!' can only be used with '=' near line 1 col 26"),
+    ("select 340282366920938463463374607431768211456",
+     "Syntax Error: invalid integer '340282366920938463463374607431768211456'"),
+    ("select a from t limit 18446744073709551616", "Syntax Error: invalid integer '18446744073709551616'"),
+    ("create table t (a Decimal32(256))", "Syntax Error: invalid integer '256'"),
+    ("select 0x", "Syntax Error: invalid hex '0x'"),
+    ("select 0x100000000000000000000000000000000", "Syntax Error: invalid hex '0x100000000000000000000000000000000'"),
+    ("insert into t values (1, 2), (3)",
+     "Syntax Error: (row has 1 column(s)) conflicts with (previous rows have 2 column(s)) near line 1 col 32"),
+    ("select a from t join u",
+     "Syntax Error: expected token (KeywordOrIdentifier) but found token EOF at line 1 col 23"),
+    ("select a from 1",
+     "Syntax Error: fail to parse (query source must be a subquery, a table function or a table) at line 1 col 15"),
+    ("create view v as select 1", "Syntax Error: expected keyword (update) but found token as at line 1 col 15"),
+    ("create table t (a Int8) order by a order by a",
+     "Syntax Error: (order by) conflicts with (order by) near line 1 col 36"),
+    ("select a b", "Syntax Error: fail to parse (more than one statement) at line 1 col 10"),
+    ("select a from t where a not foo",
+     "Syntax Error: expected keyword (in, like, ilike, between, exists) but found token foo at line 1 col 29"),
+    ("select a from t where a is foo",
+     "Syntax Error: expected keyword (not, null) but found token foo at line 1 col 28"),
+    ("select a not exists",
+     "Syntax Error: fail to parse (`not exists` should have arguments) at line 1 col 10"),
+    ("with x as 1 select 1", "Syntax Error: fail to parse (not a subquery) at line 1 col 11"),
+    ("select )", "Syntax Error: expected token (RawStringLiteral, EscapedSingleQuotedStringLiteral, "
+                 "EscapedDoubleQuotedStringLiteral, FloatLiteral, HexLiteral, IntegerLiteral, QueryParameter, "
+                 "KeywordOrIdentifier, DelimitedIdentifier, LParen, LBracket, LBrace, Minus, Plus, BitNot, Mul) "
+                 "but found token RParen at line 1 col 8"),
+    ("select 1 union", "Syntax Error: expected token (KeywordOrIdentifier) but found token EOF at line 1 col 15"),
+    ("select 1 union select 2", "Syntax Error: expected keyword (all, distinct) but found token select at line 1 "
+                                "col 16"),
+])
+def test_error_messages(sql, msg):
+    m = err(sql)
+    assert m == msg
+    assert ParseError(m).lex == m.startswith("Lex Error")
+
+
+def test_invalid_utf8_is_rejected_at_the_boundary():
+    import ctypes as C
+    from nutdb_amd._lib import lib
+    h = C.c_void_p()
+    bad = b"select '\xff'"
+    assert lib.nut_sql_parse(bad, len(bad), C.byref(h)) == 1
+    assert b"UTF-8" in lib.nut_last_error()
+
+
+# ------------------------------------------------------------------ plan lowering (B1)
+Q1 = """select l_returnflag, l_linestatus, sum(l_quantity) as sum_qty, sum(l_extendedprice) as sum_base_price,
+  sum(l_extendedprice * (1 - l_discount)) as sum_disc_price,
+  sum(l_extendedprice * (1 - l_discount) * (1 + l_tax)) as sum_charge,
+  avg(l_quantity) as avg_qty, avg(l_extendedprice) as avg_price, avg(l_discount) as avg_disc,
+  count(*) as count_order
+from lineitem
+where l_shipdate <= toDate('1998-12-01') - interval 90 day
+group by l_returnflag, l_linestatus
+order by l_returnflag, l_linestatus"""
+
+
+def test_plan_tpch_q1():
+    p = Plan(Q1)
+    d = p.describe()
+    assert p.kind == "groupby" and d["table"] == "lineitem"
+    assert d["where"] == [{"col": "l_shipdate", "op": "<=", "value": "10471", "value_kind": "int"}]
+    assert d["keys"] == ["l_returnflag", "l_linestatus"]
+    assert d["values"] == ["l_quantity", "l_extendedprice", "l_discount", "l_tax"]
+    ops = [(a["op"], a.get("expr"), tuple(a.get("args", ()))) for a in d["aggs"]]
+    assert ops == [("sum", "col", ("l_quantity",)), ("sum", "col", ("l_extendedprice",)),
+                   ("sum", "mul_1m", ("l_extendedprice", "l_discount")),
+                   ("sum", "mul_1m_1p", ("l_extendedprice", "l_discount", "l_tax")),
+                   ("count", None, ()), ("sum", "col", ("l_discount",))]
+    outs = [(o["name"], o["from"]) for o in d["outputs"]]
+    assert outs == [("l_returnflag", "key"), ("l_linestatus", "key"), ("sum_qty", "agg"), ("sum_base_price", "agg"),
+                    ("sum_disc_price", "agg"), ("sum_charge", "agg"), ("avg_qty", "avg"), ("avg_price", "avg"),
+                    ("avg_disc", "avg"), ("count_order", "agg")]
+    assert d["outputs"][6] == {"name": "avg_qty", "from": "avg", "sum": 0, "count": 4}
+    assert d["order"] == [{"output": 0, "desc": False}, {"output": 1, "desc": False}]
+
+
+@pytest.mark.parametrize("sql,days", [
+    ("toDate('1998-12-01') - interval 90 day", 10471),
+    ("toDate('1970-01-01')", 0),
+    ("toDate('2000-03-01') - interval 1 month", 10988),
+    ("toDate('2000-03-31') - interval 1 month", 11016),
+    ("toDate('2001-02-28') + interval 1 year", 11746),
+    ("toDate('1969-12-31')", -1),
+])
+def test_plan_date_constants(sql, days):
+    d = Plan(f"select x from t where x >= {sql}").describe()
+    assert d["where"][0]["value"] == str(days)
+
+
+def test_plan_filter_sort_shapes():
+    d = Plan("select x from t where x < 2.5").describe()
+    assert d["kind"] == "filter" and d["where"] == [{"col": "x", "op": "<", "value": "2.5", "value_kind": "decimal"}]
+    d = Plan("select x from t where 5 > x").describe()
+    assert d["where"][0]["op"] == "<" and d["where"][0]["value"] == "5"
+    d = Plan("select x from t where 1 = 0").describe()
+    assert d["never"] is True and d["where"] == []
+    d = Plan("select x from t where 1 = 1").describe()
+    assert d["never"] is False and d["where"] == []
+    d = Plan("select x as y from t order by y desc limit 10").describe()
+    assert d["kind"] == "sort" and d["desc"] is True and d["limit"] == 10
+    d = Plan("select K, SUM(v), Count(*), min(v), max(v) from t where v between 1 and 2 group by K").describe()
+    assert d["where"] == [{"col": "v", "op": ">=", "value": "1", "value_kind": "int"},
+                          {"col": "v", "op": "<=", "value": "2", "value_kind": "int"}]
+    assert [a["op"] for a in d["aggs"]] == ["sum", "count", "min", "max"]
+
+
+@pytest.mark.parametrize("sql,frag", [
+    ("insert into t values (1)", "only SELECT"),
+    ("select a, b from t", "exactly one column"),
+    ("select k, sum(v) from t group by k having sum(v) > 1", "HAVING"),
+    ("select k, median(v) from t group by k", "median"),
+    ("select x from t where x < y", "unsupported WHERE term"),
+    ("select k, sum(v) from t join u on a = b group by k", "JOIN"),
+    ("select k, v from t group by k", "neither a GROUP BY key"),
+    ("select k, sum(v * w * z) from t group by k", "fused expression shape"),
+    ("select count(*) from t", "without GROUP BY"),
+    ("select x from t where x < 1 union all select x from t", "UNION"),
+    ("select x from t where x >= toDate('1998-13-01')", "toDate"),
+])
+def test_plan_lowering_errors(sql, frag):
+    with pytest.raises(NutError) as e:
+        Plan(sql)
+    assert e.value.status == 7 and frag in str(e.value)
