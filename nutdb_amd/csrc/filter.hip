@@ -1,10 +1,14 @@
 // filter.hip — SELECT col FROM t WHERE col <op> k  (BASELINE config 2)
 //
 // One pass over the column, order-preserving stream compaction:
-//   * 256-thread workgroups, one 4096-row tile each; tile order comes from an atomic
-//     ticket so a tile only ever waits on tiles that are already running.
-//   * loads: 8 stripes x 16 B per lane (a wave instruction reads 1 KiB contiguous).
-//   * in-wave rank: __ballot + v_mbcnt (no shuffles); cross-wave: 32 counts in LDS.
+//   * 512-thread workgroups, one 16384-row tile each (16 stripes x 16 B per lane, a
+//     wave instruction reads 1 KiB contiguous; non-temporal loads: the column is
+//     streamed once).  Tile = blockIdx.x: workgroups are dispatched in ID order, so a
+//     tile only waits on tiles that were dispatched before it (the lowest unfinished
+//     tile never waits).  A global atomic ticket was measured to cost 0.11 ms of 0.39
+//     at N = 1e8 — every workgroup serialised on one address.
+//   * in-wave rank: __ballot + v_mbcnt (no shuffles); cross-wave: 16x8 counts in LDS.
+//   * the comparison is a template parameter (no per-row switch).
 //   * global offset: single-pass decoupled look-back.  Each tile publishes ONE 8-byte
 //     granule {flag:2 | count:62} with a relaxed agent-scope (sc1) store; predecessors
 //     are read by one wave, 64 tiles per step, with relaxed agent-scope loads — the
@@ -16,11 +20,11 @@
 
 namespace nut {
 
-constexpr int FT_THREADS = 256;
-constexpr int FT_WAVES = FT_THREADS / kWave;
-constexpr int FT_STRIPES = 8;
-constexpr int FT_STRIPE_ROWS = FT_THREADS * 2;            // 512
-constexpr int FT_TILE = FT_STRIPE_ROWS * FT_STRIPES;       // 4096 rows
+constexpr int FT_THREADS = 512;
+constexpr int FT_WAVES = FT_THREADS / kWave;               // 8
+constexpr int FT_STRIPES = 16;                             // <= 16: selection bits fit a u32
+constexpr int FT_STRIPE_ROWS = FT_THREADS * 2;             // 1024
+constexpr int FT_TILE = FT_STRIPE_ROWS * FT_STRIPES;       // 16384 rows
 constexpr uint64_t FLAG_AGG = 1ull << 62;
 constexpr uint64_t FLAG_INC = 2ull << 62;
 constexpr uint64_t VAL_MASK = (1ull << 62) - 1;
@@ -30,7 +34,7 @@ template <bool FULL, bool ALIGNED>
 __device__ __forceinline__ void load_stripe(const int64_t *__restrict__ col, uint64_t idx, uint64_t n,
                                             int64_t &a, int64_t &b) {
   if (FULL && ALIGNED) {
-    i64x2 v = *reinterpret_cast<const i64x2 *>(col + idx);
+    i64x2 v = __builtin_nontemporal_load(reinterpret_cast<const i64x2 *>(col + idx));
     a = v.x;
     b = v.y;
   } else {
@@ -74,19 +78,22 @@ __device__ uint64_t lookback(uint64_t *__restrict__ status, uint32_t tile, uint6
   return excl;
 }
 
-template <bool ALIGNED>
+template <int OP>
+__device__ __forceinline__ bool cmp_op(int64_t v, int64_t k) {
+  return OP == NUT_LT ? v < k : OP == NUT_LE ? v <= k : OP == NUT_GT ? v > k : OP == NUT_GE ? v >= k
+       : OP == NUT_EQ ? v == k : v != k;
+}
+
+template <bool ALIGNED, int OP>
 __global__ __launch_bounds__(FT_THREADS) void filter_i64_kernel(
-    const int64_t *__restrict__ col, uint64_t n, int op, int64_t k, int64_t *__restrict__ out,
-    uint64_t *__restrict__ out_n, uint32_t *__restrict__ ticket, uint64_t *__restrict__ status,
-    uint32_t ntiles, uint32_t *__restrict__ err) {
-  __shared__ uint32_t s_tile;
+    const int64_t *__restrict__ col, uint64_t n, int64_t k, int64_t *__restrict__ out,
+    uint64_t *__restrict__ out_n, uint64_t *__restrict__ status, uint32_t ntiles,
+    uint32_t *__restrict__ err) {
   __shared__ uint32_t s_cnt[FT_STRIPES][FT_WAVES];
   __shared__ uint64_t s_excl;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (tid == 0) s_tile = atomicAdd(ticket, 1u);
-  __syncthreads();
-  const uint32_t tile = s_tile;
+  const uint32_t tile = blockIdx.x;
   const uint64_t base = (uint64_t)tile * FT_TILE;
   const bool full = base + FT_TILE <= n;
 
@@ -107,8 +114,8 @@ __global__ __launch_bounds__(FT_THREADS) void filter_i64_kernel(
 #pragma unroll
   for (int j = 0; j < FT_STRIPES; ++j) {
     uint64_t idx = base + j * FT_STRIPE_ROWS + 2 * tid;
-    bool p0 = cmp_i64(v0[j], op, k) && (full || idx < n);
-    bool p1 = cmp_i64(v1[j], op, k) && (full || idx + 1 < n);
+    bool p0 = cmp_op<OP>(v0[j], k) && (full || idx < n);
+    bool p1 = cmp_op<OP>(v1[j], k) && (full || idx + 1 < n);
     uint64_t b0 = __ballot(p0), b1 = __ballot(p1);
     r0[j] = lane_rank(b0) + lane_rank(b1);
     sel |= (p0 ? 1u : 0u) << (2 * j);
@@ -118,7 +125,9 @@ __global__ __launch_bounds__(FT_THREADS) void filter_i64_kernel(
   __syncthreads();
 
   if (wave == 0) {
-    uint32_t c = lane < FT_STRIPES * FT_WAVES ? (&s_cnt[0][0])[lane] : 0u;
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = lane; i < FT_STRIPES * FT_WAVES; i += kWave) c += (&s_cnt[0][0])[i];
     uint64_t total = wave_sum_u64(c);
     uint64_t excl = lookback(status, tile, total, err, lane);
     if (lane == 0) {
@@ -158,24 +167,25 @@ extern "C" nut_status nut_filter_i64_async(nut_ctx *c, const int64_t *col, uint6
   }
   uint64_t ntiles = (n + FT_TILE - 1) / FT_TILE;
   if (ntiles > 0xFFFFFFF0ull) return fail(NUT_ERR_UNSUPPORTED, "nut_filter_i64: n too large");
-  // [ticket u32, err u32, pad 8][status u64 x ntiles] — zeroed each call as one block
+  // [pad u32, err u32, pad 8][status u64 x ntiles] — zeroed each call as one block
   size_t state = 16 + ntiles * 8;
   state = (state + 15) & ~size_t(15);
   nut_status st = c->filter_state.reserve(state);
   if (st) return st;
   char *base = (char *)c->filter_state.ptr;
-  uint32_t *ticket = (uint32_t *)base;
-  uint32_t *err = ticket + 1;
+  uint32_t *err = (uint32_t *)base + 1;
   uint64_t *status = (uint64_t *)(base + 16);
   NUT_HIP(hipMemsetAsync(base, 0, state, c->stream));
   bool aligned = ((uintptr_t)col & 15) == 0;
   c->timer.begin(c->stream, NUT_KERNEL_FILTER);
-  if (aligned)
-    hipLaunchKernelGGL(filter_i64_kernel<true>, dim3((unsigned)ntiles), dim3(FT_THREADS), 0,
-                       c->stream, col, n, op, k, out, out_n_dev, ticket, status, (uint32_t)ntiles, err);
-  else
-    hipLaunchKernelGGL(filter_i64_kernel<false>, dim3((unsigned)ntiles), dim3(FT_THREADS), 0,
-                       c->stream, col, n, op, k, out, out_n_dev, ticket, status, (uint32_t)ntiles, err);
+  using K = void (*)(const int64_t *, uint64_t, int64_t, int64_t *, uint64_t *, uint64_t *, uint32_t, uint32_t *);
+  static const K kern[2][6] = {
+      {filter_i64_kernel<false, NUT_LT>, filter_i64_kernel<false, NUT_LE>, filter_i64_kernel<false, NUT_GT>,
+       filter_i64_kernel<false, NUT_GE>, filter_i64_kernel<false, NUT_EQ>, filter_i64_kernel<false, NUT_NE>},
+      {filter_i64_kernel<true, NUT_LT>, filter_i64_kernel<true, NUT_LE>, filter_i64_kernel<true, NUT_GT>,
+       filter_i64_kernel<true, NUT_GE>, filter_i64_kernel<true, NUT_EQ>, filter_i64_kernel<true, NUT_NE>}};
+  hipLaunchKernelGGL(kern[aligned ? 1 : 0][op], dim3((unsigned)ntiles), dim3(FT_THREADS), 0, c->stream, col, n, k,
+                     out, out_n_dev, status, (uint32_t)ntiles, err);
   c->timer.end(c->stream);
   NUT_HIP(hipGetLastError());
   return NUT_OK;
@@ -190,7 +200,7 @@ extern "C" nut_status nut_filter_i64(nut_ctx *c, const int64_t *col, uint64_t n,
   uint64_t *dev_n = (uint64_t *)c->misc.ptr;
   st = nut_filter_i64_async(c, col, n, op, k, out, dev_n);
   if (st) return st;
-  // err flag lives right after the ticket in filter_state (only if n > 0)
+  // err flag is the second word of filter_state (only if n > 0)
   if (n) NUT_HIP(hipMemcpyAsync(c->host_pinned + 1, (char *)c->filter_state.ptr + 4, 4,
                                 hipMemcpyDeviceToHost, c->stream));
   NUT_HIP(hipMemcpyAsync(c->host_pinned, dev_n, 8, hipMemcpyDeviceToHost, c->stream));

@@ -32,6 +32,7 @@ constexpr uint64_t RS_AGG = 1ull << 62;
 constexpr uint64_t RS_INC = 2ull << 62;
 constexpr uint64_t RS_VAL = (1ull << 62) - 1;
 constexpr uint32_t RS_SPIN_LIMIT = 1u << 24;
+constexpr int RS_LBW = 8;  // predecessor granules per look-back round trip
 
 // ---------------------------------------------------------------- histograms
 __global__ __launch_bounds__(RS_THREADS) void rs_hist_kernel(const int64_t *__restrict__ in, uint64_t n, uint64_t flip,
@@ -108,19 +109,18 @@ __global__ __launch_bounds__(RS_THREADS) void rs_pass_kernel(const uint64_t *__r
                                                              uint64_t n, int shift, uint64_t flip,
                                                              const uint64_t *__restrict__ dbase,
                                                              uint64_t *__restrict__ status,
-                                                             uint32_t *__restrict__ ticket,
                                                              uint32_t *__restrict__ err) {
   __shared__ uint64_t s_keys[RS_TILE];             // tile staged in digit order
   __shared__ uint32_t s_wcnt[RS_WAVES][RS_BINS];    // per-wave digit counters -> wave prefixes
   __shared__ uint32_t s_tex[RS_BINS];              // exclusive digit offsets inside the tile
   __shared__ uint64_t s_gbase[RS_BINS];            // global position of the tile's first key of digit d
-  __shared__ uint32_t s_tile;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   for (int i = tid; i < RS_WAVES * RS_BINS; i += RS_THREADS) (&s_wcnt[0][0])[i] = 0;
-  if (tid == 0) s_tile = atomicAdd(ticket, 1u);
-  __syncthreads();
-  const uint32_t tile = s_tile;
+  // tile = blockIdx.x: workgroups are dispatched in ID order, so a tile only waits on
+  // tiles dispatched before it (no global ticket: one contended atomic per tile cost
+  // more than the look-back itself, see filter.hip)
+  const uint32_t tile = blockIdx.x;
   const uint64_t tbase = (uint64_t)tile * RS_TILE;
   // wave w owns keys [w*ITEMS*64, (w+1)*ITEMS*64) of the tile; item i, lane l -> +i*64+l
   const uint64_t wbase = tbase + (uint64_t)wave * RS_ITEMS * kWave;
@@ -182,22 +182,31 @@ __global__ __launch_bounds__(RS_THREADS) void rs_pass_kernel(const uint64_t *__r
       st_agent(my, RS_INC | tot);
     } else {
       st_agent(my, RS_AGG | tot);
+      // walk back RS_LBW predecessors per round trip (loads issued together)
       int64_t j = (int64_t)tile - 1;
       uint32_t spins = 0;
-      while (j >= 0) {
-        const uint64_t s = ld_agent(&status[(uint64_t)j * RS_BINS + d]);
-        const uint64_t flag = s >> 62;
-        if (flag == 0) {
-          __builtin_amdgcn_s_sleep(1);
-          if (++spins > RS_SPIN_LIMIT) {
-            atomicOr(err, 1u);
-            break;
+      bool done = false;
+      while (!done) {
+        uint64_t sv[RS_LBW];
+#pragma unroll
+        for (int m = 0; m < RS_LBW; ++m)
+          sv[m] = j - m >= 0 ? ld_agent(&status[(uint64_t)(j - m) * RS_BINS + d]) : RS_INC;
+#pragma unroll
+        for (int m = 0; m < RS_LBW; ++m) {
+          if (done) break;
+          uint64_t sm = sv[m];
+          while ((sm >> 62) == 0) {
+            __builtin_amdgcn_s_sleep(1);
+            sm = ld_agent(&status[(uint64_t)(j - m) * RS_BINS + d]);
+            if (++spins > RS_SPIN_LIMIT) {
+              atomicOr(err, 1u);
+              sm = RS_INC;
+            }
           }
-          continue;
+          excl += sm & RS_VAL;
+          if ((sm >> 62) == 2) done = true;
         }
-        excl += s & RS_VAL;
-        if (flag == 2) break;
-        --j;
+        j -= RS_LBW;
       }
       st_agent(my, RS_INC | (excl + tot));
     }
@@ -243,7 +252,7 @@ static nut_status sort_i64(nut_ctx *c, const int64_t *in, int64_t *out, uint64_t
   DeviceGuard g(c->device);
   const uint64_t ntiles = (n + RS_TILE - 1) / RS_TILE;
   if (ntiles > 0xFFFFFFF0ull) return fail(NUT_ERR_UNSUPPORTED, "nut_sort_i64: n too large");
-  // scratch: [ticket+err 16 B | status ntiles*256*8 | hist 8*256*8 | base 8*256*8 | trivial 8*4
+  // scratch: [pad+err 16 B | status ntiles*256*8 | hist 8*256*8 | base 8*256*8 | trivial 8*4
   //           | ping-pong buffer n*8]
   const size_t st_bytes = 16 + ntiles * RS_BINS * 8;
   const size_t o_hist = (st_bytes + 255) & ~size_t(255);
@@ -253,7 +262,6 @@ static nut_status sort_i64(nut_ctx *c, const int64_t *in, int64_t *out, uint64_t
   nut_status s = c->sort_tmp.reserve(o_tmp + n * 8);
   if (s) return s;
   char *b = (char *)c->sort_tmp.ptr;
-  uint32_t *ticket = (uint32_t *)b;
   uint32_t *err = (uint32_t *)(b + o_triv + 32);  // survives the per-pass memset
   uint64_t *status = (uint64_t *)(b + 16);
   unsigned long long *hist = (unsigned long long *)(b + o_hist);
@@ -293,7 +301,7 @@ static nut_status sort_i64(nut_ctx *c, const int64_t *in, int64_t *out, uint64_t
     const uint64_t *db = base + p * RS_BINS;
     auto kern = first ? (last ? rs_pass_kernel<true, true> : rs_pass_kernel<true, false>)
                       : (last ? rs_pass_kernel<false, true> : rs_pass_kernel<false, false>);
-    hipLaunchKernelGGL(kern, dim3((unsigned)ntiles), dim3(RS_THREADS), 0, st, src, dst, n, 8 * p, flip, db, status, ticket,
+    hipLaunchKernelGGL(kern, dim3((unsigned)ntiles), dim3(RS_THREADS), 0, st, src, dst, n, 8 * p, flip, db, status,
                        err);
     NUT_HIP(hipGetLastError());
     src = dst;
