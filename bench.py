@@ -139,26 +139,39 @@ class Filter:
 
 
 class Sort:
-    """config 5 per GPU: ORDER BY a full-range i64 key (local LSD radix sort)."""
+    """config 5: ORDER BY a full-range i64 key.  N=1: local LSD radix sort.  N>1: sample
+    sort — splitters from an all_gather'd sample, local stable partition into P buckets
+    (nut_partition_i64), ONE RCCL all-to-all of keys, local radix sort of the received
+    range (nutdb_amd/dist.py distributed_sort).  Rank r ends with the r-th key range."""
     name = "sort_i64_radix"
     kernel_kind = 2
 
-    def __init__(self, ex, rows, row0):
+    def __init__(self, ex, rows, row0, world=1, group=None):
         from nutdb_amd.workloads import SORT_COL, gen
         self.ex = ex
         self.col = gen(ex, SORT_COL, rows, row0=row0)
         self.out = torch.empty_like(self.col)
         self.rows = rows
+        self.world = world
+        self.group = group
         self.passes = 8  # full-range keys: no digit pass is constant
-        self.cols_bytes = 8 + 16 * self.passes
+        # histogram read + 16 B per pass; N>1 adds the partition (8 B histogram + 16 B pass)
+        self.cols_bytes = 8 + 16 * self.passes + (24 if world > 1 else 0)
 
     def run(self):
-        self.ex.sort_i64(self.col, out=self.out)
+        if self.world == 1:
+            self.ex.sort_i64(self.col, out=self.out)
+            return
+        from nutdb_amd.dist import distributed_sort
+        self.out = distributed_sort(self.col, self.ex.partition_i64, self.ex.sort_i64, self.group)
 
     def config(self):
         return {"workload": self.name, "query": "SELECT k FROM t ORDER BY k (full-range i64)",
-                "algorithm": "LSD radix, 8 x 8-bit passes, onesweep look-back",
-                "bytes_per_row": self.cols_bytes, "hbm_lower_bound_bytes_per_row": 16}
+                "algorithm": "LSD radix, 8 x 8-bit passes, onesweep look-back" +
+                ("; sample sort across ranks: partition by P-1 splitters + RCCL all-to-all" if self.world > 1
+                 else ""),
+                "bytes_per_row": self.cols_bytes, "hbm_lower_bound_bytes_per_row": 16,
+                "xgmi_bytes_per_row": 8.0 * (self.world - 1) / self.world}
 
 
 # ------------------------------------------------------------------ one step
@@ -287,7 +300,7 @@ def main():
     elif args.workload == "groupby":
         w = GroupBy(ex, rows, row0, args.groups)
     elif args.workload == "sort":
-        w = Sort(ex, rows, row0)
+        w = Sort(ex, rows, row0, world, group)
     else:
         w = Filter(ex, rows, row0, args.selectivity)
     torch.cuda.synchronize()
@@ -320,9 +333,11 @@ def main():
     ms_step = elapsed * 1e3 / args.steps
     total_rows = rows * world * args.steps
     value = total_rows / elapsed
-    avg_kernel_ms = kern_ms / max(launches, 1)
-    bytes_per_launch = w.cols_bytes * rows
-    achieved = bytes_per_launch / (avg_kernel_ms * 1e-3) / 1e9 if launches else None
+    # per step: the step's algorithmic bytes over its device time in the hot kernels
+    # (one launch per step except the multi-GPU merge / sample-sort partition)
+    avg_kernel_ms = kern_ms / args.steps
+    bytes_per_step = w.cols_bytes * rows
+    achieved = bytes_per_step / (avg_kernel_ms * 1e-3) / 1e9 if launches else None
     # PMC-measured HBM traffic of the same kernel/config, if profiled (profiles/pmc_*.json)
     traffic = None
     pmc = ROOT / "profiles" / f"pmc_{w.name}.json"
@@ -337,7 +352,7 @@ def main():
         cfg = w.config()
         cfg.update({"rows_per_gpu": rows, "parallelism": f"dp{world} (row shards; key-hash all-to-all of "
                     "partial groups over RCCL)" if world > 1 else "single GPU", "gpu": ex.info()["name"],
-                    "kernel_launches": launches, "avg_kernel_ms": avg_kernel_ms})
+                    "kernel_launches": launches, "kernel_ms_per_step": avg_kernel_ms})
         line = {
             "metric": METRIC, "value": value, "unit": "rows/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True, "scaling": "weak",

@@ -204,6 +204,13 @@ nut_status nut_q1(nut_ctx *ctx, const int64_t *shipdate, const int64_t *returnfl
 nut_status nut_sort_i64(nut_ctx *ctx, const int64_t *in, int64_t *out, uint64_t n);
 /* ORDER BY k DESC (the same passes with the key order complemented; no extra pass) */
 nut_status nut_sort_i64_desc(nut_ctx *ctx, const int64_t *in, int64_t *out, uint64_t n);
+/* Stable partition of int64 keys into nsplit+1 buckets, bucket(k) = #{i : splitters[i] <= k}
+ * (splitters_host ascending, 0 <= nsplit < 64).  Bucket b is written to out at offset
+ * sum_{c<b} counts_host[c]; counts_host receives nsplit+1 counts.  The local step of the
+ * multi-GPU sample sort: partition by splitters, all-to-all,
+ * local nut_sort_i64. */
+nut_status nut_partition_i64(nut_ctx *ctx, const int64_t *in, uint64_t n, const int64_t *splitters_host,
+                             int nsplit, int64_t *out, uint64_t *counts_host);
 
 /* ========================================================================
  * SQL front end (CPU) — restatement of the reference's only public API,

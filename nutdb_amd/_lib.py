@@ -113,6 +113,7 @@ SIGNATURES = {
     "nut_q1": (_I32, [_P, _P, _P, _P, _P, _P, _P, _U64, _I64, C.POINTER(_P)]),
     "nut_sort_i64": (_I32, [_P, _P, _P, _U64]),
     "nut_sort_i64_desc": (_I32, [_P, _P, _P, _U64]),
+    "nut_partition_i64": (_I32, [_P, _P, _U64, _P, _I32, _P, _P]),
     # SQL front end (CPU) and plan lowering / execution
     "nut_sql_parse": (_I32, [C.c_char_p, C.c_size_t, C.POINTER(_P)]),
     "nut_stmt_kind_of": (_I32, [_P]),

@@ -157,6 +157,7 @@ void nut_ctx_destroy(nut_ctx *c) {
   (void)hipStreamSynchronize(c->stream);
   c->filter_state.release();
   c->sort_tmp.release();
+  c->sort_status.release();
   c->misc.release();
   c->timer.release();
   if (c->host_pinned) (void)hipHostFree(c->host_pinned);

@@ -161,6 +161,10 @@ struct nut_ctx {
   hipStream_t stream = nullptr;
   nut::Scratch filter_state;  // tile counter + look-back status words
   nut::Scratch sort_tmp;      // sort ping-pong + histograms
+  nut::Scratch sort_status;   // radix-pass look-back granules, epoch-tagged (sort.hip)
+  void *sort_status_seen = nullptr;
+  size_t sort_status_clean = 0;
+  uint32_t sort_epoch = 0;
   nut::Scratch misc;
   uint64_t *host_pinned = nullptr;  // small pinned staging for counts/flags
   nut::KernelTimer timer;

@@ -1,17 +1,24 @@
-// sort.hip — SELECT k FROM t ORDER BY k  (BASELINE config 5): LSD radix sort of int64.
+// sort.hip — SELECT k FROM t ORDER BY k  (BASELINE config 5): LSD radix sort of int64,
+// and the stable bucket partition that is the local step of the multi-GPU sample sort.
 //
 // Onesweep-style:
-//   * keys are mapped to u64 with the sign bit flipped (order-preserving); 8 passes of
-//     8-bit digits, least significant first; a pass whose digit is constant over all
-//     keys (one histogram bin = n) is skipped;
+//   * keys are mapped to u64 with the sign bit flipped (order-preserving; DESC uses the
+//     complement); 8 passes of 8-bit digits, least significant first; a pass whose digit
+//     is constant over all keys (one histogram bin = n) is skipped;
 //   * ONE upfront read computes all eight 256-bin histograms (LDS per block, then
 //     global atomics); a tiny kernel turns them into per-pass digit bases;
-//   * per pass ONE kernel: a 4096-key tile (256 threads = 4 waves x 16 items) is ranked
+//   * per pass ONE kernel: an 8192-key tile (512 threads = 8 waves x 16 items) is ranked
 //     stably in registers — peers of a key within its wave from 8 ballots over the
 //     digit bits, running per-wave digit counters in LDS — then every digit's tile
-//     offset comes from a decoupled look-back (thread t owns digit t; 8-B {flag|count}
-//     granules, relaxed agent-scope stores/loads, no fence), and the tile is staged in
-//     LDS in digit order so consecutive threads write consecutive addresses of a bucket.
+//     offset comes from a decoupled look-back (thread t < 256 owns digit t; 8-B
+//     {epoch|flag|count} granules, relaxed agent-scope stores/loads, no fence), and the
+//     tile is staged in LDS in digit order so consecutive threads write consecutive
+//     addresses of a bucket;
+//   * tile = blockIdx.x (in-order dispatch; no contended ticket atomic) and the status
+//     granules carry the pass epoch, so no per-pass memset of the status array
+//     (312 MB per pass at 1.25e9 keys otherwise).
+// Measured (scripts/tune/sort_tune.hip, one pass, 2.5e8 keys): 256x16 tiles 1.72 ms,
+// 512x16 tiles 1.40 ms; without the look-back 0.91 ms.
 // Algorithmic bytes: 8 B/key histogram read + 16 B/key per executed pass.
 #include <string.h>
 
@@ -21,31 +28,58 @@
 
 namespace nut {
 
-constexpr int RS_THREADS = 256;
-constexpr int RS_WAVES = RS_THREADS / kWave;
+constexpr int RS_THREADS = 512;
+constexpr int RS_WAVES = RS_THREADS / kWave;     // 8
 constexpr int RS_ITEMS = 16;
-constexpr int RS_TILE = RS_THREADS * RS_ITEMS;  // 4096 keys
+constexpr int RS_TILE = RS_THREADS * RS_ITEMS;   // 8192 keys
 constexpr int RS_BINS = 256;
+constexpr int RS_HIST_THREADS = 256;
 constexpr uint64_t RS_FLIP = 0x8000000000000000ull;      // ascending: signed order -> unsigned order
 constexpr uint64_t RS_FLIP_DESC = 0x7FFFFFFFFFFFFFFFull; // descending: the complement of the above
-constexpr uint64_t RS_AGG = 1ull << 62;
-constexpr uint64_t RS_INC = 2ull << 62;
-constexpr uint64_t RS_VAL = (1ull << 62) - 1;
+// status granule: [epoch:8 | flag:2 | count:54]
+constexpr int RS_EPOCH_SHIFT = 56;
+constexpr uint64_t RS_AGG = 1ull << 54;
+constexpr uint64_t RS_INC = 2ull << 54;
+constexpr uint64_t RS_VAL = (1ull << 54) - 1;
 constexpr uint32_t RS_SPIN_LIMIT = 1u << 24;
-constexpr int RS_LBW = 8;  // predecessor granules per look-back round trip
+constexpr int RS_MAX_BUCKETS = 64;  // nut_partition_i64: up to 63 splitters
+
+static_assert(RS_THREADS >= RS_BINS, "one thread per digit in the scan / look-back");
+
+// ---------------------------------------------------------------- digits
+struct RadixDigit {  // bits [shift, shift+8) of the (flipped) key
+  int shift;
+  static constexpr int BITS = 8;
+  __device__ __forceinline__ uint32_t operator()(uint64_t k, const int64_t *) const {
+    return (uint32_t)(k >> shift) & 255u;
+  }
+};
+
+struct BucketDigit {  // #splitters <= key (signed), splitters ascending in LDS
+  int nsplit;
+  static constexpr int BITS = 6;
+  __device__ __forceinline__ uint32_t operator()(uint64_t k, const int64_t *spl) const {
+    // branch-free lower bound over <= 63 splitters
+    uint32_t lo = 0;
+#pragma unroll
+    for (int step = RS_MAX_BUCKETS / 2; step >= 1; step >>= 1)
+      if (lo + step <= (uint32_t)nsplit && spl[lo + step - 1] <= (int64_t)k) lo += step;
+    return lo;
+  }
+};
 
 // ---------------------------------------------------------------- histograms
-__global__ __launch_bounds__(RS_THREADS) void rs_hist_kernel(const int64_t *__restrict__ in, uint64_t n, uint64_t flip,
-                                                             unsigned long long *__restrict__ hist) {
+__global__ __launch_bounds__(RS_HIST_THREADS) void rs_hist_kernel(const int64_t *__restrict__ in, uint64_t n,
+                                                                  uint64_t flip, unsigned long long *__restrict__ hist) {
   __shared__ uint32_t h[8][RS_BINS];
-  for (int i = threadIdx.x; i < 8 * RS_BINS; i += RS_THREADS) (&h[0][0])[i] = 0;
+  for (int i = threadIdx.x; i < 8 * RS_BINS; i += RS_HIST_THREADS) (&h[0][0])[i] = 0;
   __syncthreads();
-  const uint64_t stride = (uint64_t)gridDim.x * RS_THREADS * 2;
-  for (uint64_t i = ((uint64_t)blockIdx.x * RS_THREADS + threadIdx.x) * 2; i < n; i += stride) {
+  const uint64_t stride = (uint64_t)gridDim.x * RS_HIST_THREADS * 2;
+  for (uint64_t i = ((uint64_t)blockIdx.x * RS_HIST_THREADS + threadIdx.x) * 2; i < n; i += stride) {
     uint64_t a, b;
     bool two = i + 1 < n;
     if (two && ((((uintptr_t)(in + i)) & 15) == 0)) {
-      const u64x2 v = *reinterpret_cast<const u64x2 *>(in + i);
+      const u64x2 v = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(in + i));
       a = v.x;
       b = v.y;
     } else {
@@ -61,10 +95,28 @@ __global__ __launch_bounds__(RS_THREADS) void rs_hist_kernel(const int64_t *__re
     }
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < 8 * RS_BINS; i += RS_THREADS) {
+  for (int i = threadIdx.x; i < 8 * RS_BINS; i += RS_HIST_THREADS) {
     uint32_t c = (&h[0][0])[i];
     if (c) atomicAdd(&hist[i], (unsigned long long)c);
   }
+}
+
+// bucket histogram for nut_partition_i64
+__global__ __launch_bounds__(RS_HIST_THREADS) void pt_hist_kernel(const int64_t *__restrict__ in, uint64_t n,
+                                                                  BucketDigit dig, const int64_t *__restrict__ splitters,
+                                                                  unsigned long long *__restrict__ hist) {
+  __shared__ uint32_t h[RS_MAX_BUCKETS];
+  __shared__ int64_t spl[RS_MAX_BUCKETS];
+  for (int i = threadIdx.x; i < RS_MAX_BUCKETS; i += RS_HIST_THREADS) {
+    h[i] = 0;
+    spl[i] = i < dig.nsplit ? splitters[i] : INT64_MAX;
+  }
+  __syncthreads();
+  for (uint64_t i = (uint64_t)blockIdx.x * RS_HIST_THREADS + threadIdx.x; i < n; i += (uint64_t)gridDim.x * RS_HIST_THREADS)
+    atomicAdd(&h[dig((uint64_t)in[i], spl)], 1u);
+  __syncthreads();
+  for (int i = threadIdx.x; i <= dig.nsplit; i += RS_HIST_THREADS)
+    if (h[i]) atomicAdd(&hist[i], (unsigned long long)h[i]);
 }
 
 // exclusive scan of each pass's 256 bins -> digit bases; flags passes whose digit is
@@ -93,30 +145,35 @@ __global__ __launch_bounds__(RS_BINS) void rs_scan_kernel(const unsigned long lo
 
 // ---------------------------------------------------------------- one pass
 // lanes of this wave holding the same digit (valid lanes only)
+template <int BITS>
 __device__ __forceinline__ uint64_t digit_peers(uint32_t d, bool valid) {
   uint64_t m = __ballot(valid);
 #pragma unroll
-  for (int b = 0; b < 8; ++b) {
+  for (int b = 0; b < BITS; ++b) {
     const uint64_t bb = __ballot((d >> b) & 1u);
     m &= ((d >> b) & 1u) ? bb : ~bb;
   }
   return m;
 }
 
-// FIRST: input is raw int64 (flip on load); LAST: write int64 (flip back)
-template <bool FIRST, bool LAST>
+// FIRST: input is raw int64 (flip on load); LAST: write int64 (flip back).
+// nbins: digits in use (256 for radix passes, #buckets for a partition).
+template <bool FIRST, bool LAST, class Digit>
 __global__ __launch_bounds__(RS_THREADS) void rs_pass_kernel(const uint64_t *__restrict__ in, uint64_t *__restrict__ out,
-                                                             uint64_t n, int shift, uint64_t flip,
-                                                             const uint64_t *__restrict__ dbase,
-                                                             uint64_t *__restrict__ status,
+                                                             uint64_t n, Digit dig, const int64_t *__restrict__ splitters,
+                                                             int nbins, uint64_t flip, const uint64_t *__restrict__ dbase,
+                                                             uint64_t *__restrict__ status, uint32_t epoch,
                                                              uint32_t *__restrict__ err) {
   __shared__ uint64_t s_keys[RS_TILE];             // tile staged in digit order
   __shared__ uint32_t s_wcnt[RS_WAVES][RS_BINS];    // per-wave digit counters -> wave prefixes
   __shared__ uint32_t s_tex[RS_BINS];              // exclusive digit offsets inside the tile
   __shared__ uint64_t s_gbase[RS_BINS];            // global position of the tile's first key of digit d
+  __shared__ uint32_t s_wsum[RS_BINS / kWave];
+  __shared__ int64_t s_spl[RS_MAX_BUCKETS];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   for (int i = tid; i < RS_WAVES * RS_BINS; i += RS_THREADS) (&s_wcnt[0][0])[i] = 0;
+  if (splitters && tid < RS_MAX_BUCKETS) s_spl[tid] = tid < nbins - 1 ? splitters[tid] : INT64_MAX;
   // tile = blockIdx.x: workgroups are dispatched in ID order, so a tile only waits on
   // tiles dispatched before it (no global ticket: one contended atomic per tile cost
   // more than the look-back itself, see filter.hip)
@@ -134,13 +191,14 @@ __global__ __launch_bounds__(RS_THREADS) void rs_pass_kernel(const uint64_t *__r
     if (FIRST) k ^= flip;
     key[i] = k;
   }
+  __syncthreads();  // s_wcnt zeroed, s_spl loaded
   // stable in-wave ranking, items in order
 #pragma unroll
   for (int i = 0; i < RS_ITEMS; ++i) {
     const uint64_t idx = wbase + (uint64_t)i * kWave + lane;
     const bool valid = idx < n;
-    const uint32_t d = (uint32_t)(key[i] >> shift) & 255u;
-    const uint64_t peers = digit_peers(d, valid);
+    const uint32_t d = dig(key[i], s_spl);
+    const uint64_t peers = digit_peers<Digit::BITS>(d, valid);
     const uint32_t before = lane_rank(peers);
     const uint32_t cnt = (uint32_t)__popcll(peers);
     uint32_t prior = valid ? s_wcnt[wave][d] : 0u;  // all peers read before the leader writes
@@ -148,69 +206,60 @@ __global__ __launch_bounds__(RS_THREADS) void rs_pass_kernel(const uint64_t *__r
     if (valid && before == 0) s_wcnt[wave][d] = prior + cnt;
   }
   __syncthreads();
-  // per digit (thread t = digit): tile count, wave prefixes, tile-internal offsets
-  const int d = tid;
-  uint32_t tot = 0;
+  // per digit (thread t < 256 = digit): tile count and wave prefixes
+  uint32_t tot = 0, incl = 0;
+  if (tid < RS_BINS) {
 #pragma unroll
-  for (int w = 0; w < RS_WAVES; ++w) {
-    const uint32_t c = s_wcnt[w][d];
-    s_wcnt[w][d] = tot;  // exclusive prefix over waves
-    tot += c;
-  }
-  // exclusive scan of tile counts over digits (block scan of 256 values)
-  {
-    uint32_t v = tot;
-    // inclusive wave scan
+    for (int w = 0; w < RS_WAVES; ++w) {
+      const uint32_t c = s_wcnt[w][tid];
+      s_wcnt[w][tid] = tot;  // exclusive prefix over waves
+      tot += c;
+    }
+    // inclusive scan of tile counts over digits: waves 0..3, then across them
+    incl = tot;
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
-      uint32_t y = __shfl_up(v, off, 64);
-      if (lane >= off) v += y;
+      uint32_t y = __shfl_up(incl, off, 64);
+      if (lane >= off) incl += y;
     }
-    __shared__ uint32_t s_wsum[RS_WAVES];
-    if (lane == 63) s_wsum[wave] = v;
-    __syncthreads();
+    if (lane == 63) s_wsum[wave] = incl;
+  }
+  __syncthreads();
+  if (tid < RS_BINS) {
+    const int d = tid;
     uint32_t add = 0;
 #pragma unroll
-    for (int w = 0; w < RS_WAVES; ++w) add += (w < wave) ? s_wsum[w] : 0u;
-    s_tex[d] = v - tot + add;
-  }
-  // decoupled look-back, thread d walks back through predecessors' digit-d granules
-  {
-    uint64_t *my = &status[(uint64_t)tile * RS_BINS + d];
+    for (int w = 0; w < RS_BINS / kWave; ++w) add += (w < wave) ? s_wsum[w] : 0u;
+    s_tex[d] = incl - tot + add;
+    // decoupled look-back, thread d walks back through predecessors' digit-d granules
     uint64_t excl = 0;
-    if (tile == 0) {
-      st_agent(my, RS_INC | tot);
-    } else {
-      st_agent(my, RS_AGG | tot);
-      // walk back RS_LBW predecessors per round trip (loads issued together)
-      int64_t j = (int64_t)tile - 1;
-      uint32_t spins = 0;
-      bool done = false;
-      while (!done) {
-        uint64_t sv[RS_LBW];
-#pragma unroll
-        for (int m = 0; m < RS_LBW; ++m)
-          sv[m] = j - m >= 0 ? ld_agent(&status[(uint64_t)(j - m) * RS_BINS + d]) : RS_INC;
-#pragma unroll
-        for (int m = 0; m < RS_LBW; ++m) {
-          if (done) break;
-          uint64_t sm = sv[m];
-          while ((sm >> 62) == 0) {
+    if (d < nbins) {
+      const uint64_t ep = (uint64_t)epoch << RS_EPOCH_SHIFT;
+      uint64_t *my = &status[(uint64_t)tile * RS_BINS + d];
+      if (tile == 0) {
+        st_agent(my, ep | RS_INC | tot);
+      } else {
+        st_agent(my, ep | RS_AGG | tot);
+        int64_t j = (int64_t)tile - 1;
+        uint32_t spins = 0;
+        for (;;) {
+          uint64_t s = ld_agent(&status[(uint64_t)j * RS_BINS + d]);
+          while ((s >> RS_EPOCH_SHIFT) != epoch) {  // not yet published in this pass
             __builtin_amdgcn_s_sleep(1);
-            sm = ld_agent(&status[(uint64_t)(j - m) * RS_BINS + d]);
+            s = ld_agent(&status[(uint64_t)j * RS_BINS + d]);
             if (++spins > RS_SPIN_LIMIT) {
               atomicOr(err, 1u);
-              sm = RS_INC;
+              s = ep | RS_INC;
             }
           }
-          excl += sm & RS_VAL;
-          if ((sm >> 62) == 2) done = true;
+          excl += s & RS_VAL;
+          if (s & RS_INC) break;
+          --j;
         }
-        j -= RS_LBW;
+        st_agent(my, ep | RS_INC | (excl + tot));
       }
-      st_agent(my, RS_INC | (excl + tot));
     }
-    s_gbase[d] = dbase[d] + excl;
+    s_gbase[d] = d < nbins ? dbase[d] + excl : 0;
   }
   __syncthreads();
   // stage in digit order
@@ -218,7 +267,7 @@ __global__ __launch_bounds__(RS_THREADS) void rs_pass_kernel(const uint64_t *__r
   for (int i = 0; i < RS_ITEMS; ++i) {
     const uint64_t idx = wbase + (uint64_t)i * kWave + lane;
     if (idx < n) {
-      const uint32_t dd = (uint32_t)(key[i] >> shift) & 255u;
+      const uint32_t dd = dig(key[i], s_spl);
       s_keys[s_tex[dd] + s_wcnt[wave][dd] + rank[i]] = key[i];
     }
   }
@@ -230,7 +279,7 @@ __global__ __launch_bounds__(RS_THREADS) void rs_pass_kernel(const uint64_t *__r
     const uint32_t j = (uint32_t)i * RS_THREADS + tid;
     if (j < valid_n) {
       const uint64_t k = s_keys[j];
-      const uint32_t dd = (uint32_t)(k >> shift) & 255u;
+      const uint32_t dd = dig(k, s_spl);
       out[s_gbase[dd] + (j - s_tex[dd])] = LAST ? (k ^ flip) : k;
     }
   }
@@ -239,6 +288,23 @@ __global__ __launch_bounds__(RS_THREADS) void rs_pass_kernel(const uint64_t *__r
 __global__ void rs_copy_kernel(const uint64_t *__restrict__ in, uint64_t *__restrict__ out, uint64_t n) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
     out[i] = in[i];
+}
+
+// Status granules for `ntiles` tiles, tagged with a fresh pass epoch.  The array is
+// cleared only when it is (re)allocated or the 8-bit epoch wraps.
+nut_status next_status(nut_ctx *c, uint64_t ntiles, uint64_t **status, uint32_t *epoch) {
+  const size_t need = ntiles * RS_BINS * 8;
+  nut_status s = c->sort_status.reserve(need);
+  if (s) return s;
+  if (c->sort_status.ptr != c->sort_status_seen || need > c->sort_status_clean || c->sort_epoch >= 255) {
+    NUT_HIP(hipMemsetAsync(c->sort_status.ptr, 0, c->sort_status.bytes, c->stream));
+    c->sort_status_seen = c->sort_status.ptr;
+    c->sort_status_clean = c->sort_status.bytes;
+    c->sort_epoch = 0;
+  }
+  *epoch = ++c->sort_epoch;
+  *status = (uint64_t *)c->sort_status.ptr;
+  return NUT_OK;
 }
 
 }  // namespace nut
@@ -251,19 +317,16 @@ static nut_status sort_i64(nut_ctx *c, const int64_t *in, int64_t *out, uint64_t
   if (n == 0) return NUT_OK;
   DeviceGuard g(c->device);
   const uint64_t ntiles = (n + RS_TILE - 1) / RS_TILE;
-  if (ntiles > 0xFFFFFFF0ull) return fail(NUT_ERR_UNSUPPORTED, "nut_sort_i64: n too large");
-  // scratch: [pad+err 16 B | status ntiles*256*8 | hist 8*256*8 | base 8*256*8 | trivial 8*4
-  //           | ping-pong buffer n*8]
-  const size_t st_bytes = 16 + ntiles * RS_BINS * 8;
-  const size_t o_hist = (st_bytes + 255) & ~size_t(255);
+  if (ntiles > 0x7FFFFFF0ull || n > RS_VAL) return fail(NUT_ERR_UNSUPPORTED, "nut_sort_i64: n too large");
+  // scratch: [err 16 B | hist 8*256*8 | base 8*256*8 | trivial 8*4 | ping-pong buffer n*8]
+  const size_t o_hist = 256;
   const size_t o_base = o_hist + 8 * RS_BINS * 8;
   const size_t o_triv = o_base + 8 * RS_BINS * 8;
   const size_t o_tmp = (o_triv + 64 + 255) & ~size_t(255);
   nut_status s = c->sort_tmp.reserve(o_tmp + n * 8);
   if (s) return s;
   char *b = (char *)c->sort_tmp.ptr;
-  uint32_t *err = (uint32_t *)(b + o_triv + 32);  // survives the per-pass memset
-  uint64_t *status = (uint64_t *)(b + 16);
+  uint32_t *err = (uint32_t *)b;
   unsigned long long *hist = (unsigned long long *)(b + o_hist);
   uint64_t *base = (uint64_t *)(b + o_base);
   uint32_t *triv = (uint32_t *)(b + o_triv);
@@ -271,10 +334,9 @@ static nut_status sort_i64(nut_ctx *c, const int64_t *in, int64_t *out, uint64_t
   hipStream_t st = c->stream;
 
   c->timer.begin(st, NUT_KERNEL_SORT);
-  NUT_HIP(hipMemsetAsync(hist, 0, 8 * RS_BINS * 8, st));
-  NUT_HIP(hipMemsetAsync(err, 0, 4, st));
-  uint64_t hblocks = std::min<uint64_t>((n + 2 * RS_THREADS - 1) / (2 * RS_THREADS), (uint64_t)c->num_cus * 4);
-  hipLaunchKernelGGL(rs_hist_kernel, dim3((unsigned)hblocks), dim3(RS_THREADS), 0, st, in, n, flip, hist);
+  NUT_HIP(hipMemsetAsync(b, 0, o_base, st));  // err + histograms
+  uint64_t hblocks = std::min<uint64_t>((n + 2 * RS_HIST_THREADS - 1) / (2 * RS_HIST_THREADS), (uint64_t)c->num_cus * 4);
+  hipLaunchKernelGGL(rs_hist_kernel, dim3((unsigned)hblocks), dim3(RS_HIST_THREADS), 0, st, in, n, flip, hist);
   hipLaunchKernelGGL(rs_scan_kernel, dim3(8), dim3(RS_BINS), 0, st, (const unsigned long long *)hist, n, base, triv);
   NUT_HIP(hipGetLastError());
   // which passes run is decided on the host (8 flags)
@@ -296,13 +358,16 @@ static nut_status sort_i64(nut_ctx *c, const int64_t *in, int64_t *out, uint64_t
   for (int k = 0; k < np; ++k) {
     const bool first = k == 0, last = k == np - 1;
     uint64_t *dst = ((np - 1 - k) % 2 == 0) ? (uint64_t *)out : tmp;
-    NUT_HIP(hipMemsetAsync(b, 0, st_bytes, st));
+    uint64_t *status;
+    uint32_t epoch;
+    s = next_status(c, ntiles, &status, &epoch);
+    if (s) return s;
     const int p = passes[k];
     const uint64_t *db = base + p * RS_BINS;
-    auto kern = first ? (last ? rs_pass_kernel<true, true> : rs_pass_kernel<true, false>)
-                      : (last ? rs_pass_kernel<false, true> : rs_pass_kernel<false, false>);
-    hipLaunchKernelGGL(kern, dim3((unsigned)ntiles), dim3(RS_THREADS), 0, st, src, dst, n, 8 * p, flip, db, status,
-                       err);
+    auto kern = first ? (last ? rs_pass_kernel<true, true, RadixDigit> : rs_pass_kernel<true, false, RadixDigit>)
+                      : (last ? rs_pass_kernel<false, true, RadixDigit> : rs_pass_kernel<false, false, RadixDigit>);
+    hipLaunchKernelGGL(kern, dim3((unsigned)ntiles), dim3(RS_THREADS), 0, st, src, dst, n, RadixDigit{8 * p},
+                       (const int64_t *)nullptr, RS_BINS, flip, db, status, epoch, err);
     NUT_HIP(hipGetLastError());
     src = dst;
   }
@@ -319,4 +384,61 @@ extern "C" nut_status nut_sort_i64(nut_ctx *c, const int64_t *in, int64_t *out, 
 
 extern "C" nut_status nut_sort_i64_desc(nut_ctx *c, const int64_t *in, int64_t *out, uint64_t n) {
   return sort_i64(c, in, out, n, RS_FLIP_DESC);
+}
+
+extern "C" nut_status nut_partition_i64(nut_ctx *c, const int64_t *in, uint64_t n, const int64_t *splitters_host,
+                                        int nsplit, int64_t *out, uint64_t *counts_host) {
+  if (!c || !counts_host || (n && (!in || !out)) || (nsplit && !splitters_host))
+    return fail(NUT_ERR_INVALID_ARG, "nut_partition_i64: NULL argument");
+  if (nsplit < 0 || nsplit >= RS_MAX_BUCKETS)
+    return fail(NUT_ERR_INVALID_ARG, "nut_partition_i64: 0 <= nsplit < 64 required");
+  for (int i = 1; i < nsplit; ++i)
+    if (splitters_host[i] < splitters_host[i - 1])
+      return fail(NUT_ERR_INVALID_ARG, "nut_partition_i64: splitters must be ascending");
+  if (n && (uintptr_t)in == (uintptr_t)out) return fail(NUT_ERR_INVALID_ARG, "nut_partition_i64: in and out alias");
+  const int nb = nsplit + 1;
+  for (int i = 0; i < nb; ++i) counts_host[i] = 0;
+  if (n == 0) return NUT_OK;
+  DeviceGuard g(c->device);
+  const uint64_t ntiles = (n + RS_TILE - 1) / RS_TILE;
+  if (ntiles > 0x7FFFFFF0ull || n > RS_VAL) return fail(NUT_ERR_UNSUPPORTED, "nut_partition_i64: n too large");
+  // misc scratch: [err 16 | hist 64*8 | splitters 64*8 | base 64*8]
+  nut_status s = c->misc.reserve(16 + 3 * RS_MAX_BUCKETS * 8 + 64);
+  if (s) return s;
+  char *b = (char *)c->misc.ptr;
+  uint32_t *err = (uint32_t *)b;
+  unsigned long long *hist = (unsigned long long *)(b + 16);
+  int64_t *spl = (int64_t *)(b + 16 + RS_MAX_BUCKETS * 8);
+  uint64_t *base = (uint64_t *)(b + 16 + 2 * RS_MAX_BUCKETS * 8);
+  hipStream_t st = c->stream;
+  BucketDigit dig{nsplit};
+  c->timer.begin(st, NUT_KERNEL_SORT);
+  NUT_HIP(hipMemsetAsync(b, 0, 16 + RS_MAX_BUCKETS * 8, st));
+  if (nsplit) NUT_HIP(hipMemcpyAsync(spl, splitters_host, nsplit * 8, hipMemcpyHostToDevice, st));
+  uint64_t hblocks = std::min<uint64_t>((n + RS_HIST_THREADS - 1) / RS_HIST_THREADS, (uint64_t)c->num_cus * 4);
+  hipLaunchKernelGGL(pt_hist_kernel, dim3((unsigned)hblocks), dim3(RS_HIST_THREADS), 0, st, in, n, dig,
+                     (const int64_t *)spl, hist);
+  NUT_HIP(hipGetLastError());
+  NUT_HIP(hipMemcpyAsync(counts_host, hist, nb * 8, hipMemcpyDeviceToHost, st));
+  NUT_HIP(hipStreamSynchronize(st));
+  uint64_t hbase[RS_MAX_BUCKETS], run = 0;
+  for (int i = 0; i < nb; ++i) {
+    hbase[i] = run;
+    run += counts_host[i];
+  }
+  NUT_HIP(hipMemcpyAsync(base, hbase, nb * 8, hipMemcpyHostToDevice, st));
+  uint64_t *status;
+  uint32_t epoch;
+  s = next_status(c, ntiles, &status, &epoch);
+  if (s) return s;
+  hipLaunchKernelGGL((rs_pass_kernel<false, false, BucketDigit>), dim3((unsigned)ntiles), dim3(RS_THREADS), 0, st,
+                     (const uint64_t *)in, (uint64_t *)out, n, dig, (const int64_t *)spl, nb, (uint64_t)0,
+                     (const uint64_t *)base, status, epoch, err);
+  NUT_HIP(hipGetLastError());
+  c->timer.end(st);
+  uint32_t herr = 0;
+  NUT_HIP(hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, st));
+  NUT_HIP(hipStreamSynchronize(st));
+  if (herr) return fail(NUT_ERR_TIMEOUT, "nut_partition_i64: look-back spin limit hit");
+  return NUT_OK;
 }

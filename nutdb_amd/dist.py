@@ -1,4 +1,5 @@
-"""Multi-GPU group-by: key-hash exchange of partial groups over torch.distributed.
+"""Multi-GPU group-by (key-hash exchange of partial groups) and sample sort over
+torch.distributed.
 
 One process per GPU; backend "nccl" is RCCL over xGMI on ROCm ("gloo" on CPU for tests).
 Each rank pre-aggregates its row shard on its GPU (nut_groupby), partitions the partial
@@ -105,3 +106,59 @@ def distributed_groupby(ex, local, merge_query: Callable[[torch.Tensor], "object
     else:
         mine = torch.empty((width, 0), dtype=torch.int64, device=ex.device)
     return gather_groups(mine, group)
+
+
+# ---------------------------------------------------------------------------- sample sort
+def choose_splitters(local: torch.Tensor, group=None, samples_per_rank: int = 4096) -> np.ndarray:
+    """Regular sample of the local keys -> all_gather -> P-1 splitters at the global
+    sample's quantiles (host array, ascending).  The sample is a strided read of
+    `samples_per_rank` keys (with repetition when the shard is smaller); a rank with no
+    keys contributes nothing (its sample slots are masked by a gathered count)."""
+    world = dist.get_world_size(group)
+    n = local.numel()
+    dev = local.device
+    S = samples_per_rank
+    if n:
+        idx = (torch.arange(S, device=dev, dtype=torch.int64) * n) // S
+        sample = local[idx].contiguous()
+    else:
+        sample = torch.zeros(S, dtype=torch.int64, device=dev)
+    have = torch.tensor([1 if n else 0], dtype=torch.int64, device=dev)
+    samples = [torch.empty_like(sample) for _ in range(world)]
+    haves = [torch.empty_like(have) for _ in range(world)]
+    dist.all_gather(samples, sample, group=group)
+    dist.all_gather(haves, have, group=group)
+    pool = np.concatenate([s.cpu().numpy() for s, h in zip(samples, haves) if int(h.item())] or
+                          [np.zeros(0, np.int64)])
+    if len(pool) == 0:
+        return np.zeros(world - 1, dtype=np.int64)
+    pool.sort()
+    m = len(pool)
+    return np.array([pool[(i * m) // world] for i in range(1, world)], dtype=np.int64)
+
+
+def exchange_keys(part: torch.Tensor, counts: List[int], group=None) -> torch.Tensor:
+    """All-to-all of the bucket-partitioned keys: segment p (counts[p] keys) goes to rank p.
+    Returns this rank's received keys, concatenated in source-rank order."""
+    dev = part.device
+    send = torch.tensor(counts, dtype=torch.int64, device=dev)
+    recv = torch.empty_like(send)
+    dist.all_to_all_single(recv, send, group=group)
+    rc = [int(x) for x in recv.tolist()]
+    out = torch.empty(sum(rc), dtype=torch.int64, device=dev)
+    dist.all_to_all_single(out, part[: sum(counts)].contiguous(), rc, list(counts), group=group)
+    return out
+
+
+def distributed_sort(local: torch.Tensor, partition: Callable, sort: Callable, group=None,
+                     samples_per_rank: int = 4096) -> torch.Tensor:
+    """Multi-GPU ORDER BY k (BASELINE config 5): sample -> splitters ->
+    local stable partition into P buckets (`partition(keys, splitters) -> (keys, counts)`,
+    nut_partition_i64 on a GPU) -> ONE all-to-all of keys over RCCL -> local radix sort
+    (`sort(keys) -> keys`, nut_sort_i64).  Rank r returns the r-th range of the global
+    order: every key on rank r is <= every key on rank r+1 (keys equal to a splitter all
+    land on the higher rank)."""
+    splitters = choose_splitters(local, group, samples_per_rank)
+    part, counts = partition(local, splitters)
+    recv = exchange_keys(part, counts, group)
+    return sort(recv)

@@ -293,6 +293,22 @@ class Executor:
                  C.c_void_p(out.data_ptr() if n else None), n), fn.__name__)
         return out
 
+    def partition_i64(self, col: torch.Tensor, splitters, out: torch.Tensor | None = None):
+        """Stable partition by bucket(k) = #{splitters <= k} (nut_partition_i64).  Returns
+        (partitioned tensor, per-bucket counts)."""
+        if col.dtype != torch.int64:
+            raise TypeError("partition_i64 takes an int64 column")
+        spl = np.ascontiguousarray(np.asarray(splitters, dtype=np.int64))
+        n = col.numel()
+        if out is None:
+            out = torch.empty(max(n, 1), dtype=torch.int64, device=self.device)
+        counts = (C.c_uint64 * (len(spl) + 1))()
+        self._bind_stream()
+        check(lib.nut_partition_i64(self.ctx, C.c_void_p(_col(col, self.device) if n else None), n,
+                                    spl.ctypes.data_as(C.c_void_p) if len(spl) else None, len(spl),
+                                    C.c_void_p(out.data_ptr()), counts), "nut_partition_i64")
+        return out[:n], [int(c) for c in counts]
+
     # ---------------------------------------------------------------- SQL
     def sql(self, query: str, columns: dict, group_hint: int = 0) -> dict:
         """Parse + lower `query` (nut_sql_plan) and run it on `columns` = {name: CUDA

@@ -94,3 +94,51 @@ def test_exchange_world2(G, orc):
     assert np.array_equal(got[2], ow[:, 1].view(np.int64))
     assert np.array_equal(got[3], ow[:, 2].view(np.int64))
     assert np.array_equal(got[4], ow[:, 3].view(np.int64))
+
+
+# ---------------------------------------------------------------------------- sample sort
+def _np_partition(keys, splitters):
+    """stands in for nut_partition_i64: stable, bucket = #splitters <= key"""
+    k = keys.numpy()
+    b = np.searchsorted(splitters, k, side="right")
+    order = np.argsort(b, kind="stable")
+    counts = np.bincount(b, minlength=len(splitters) + 1)
+    return torch.from_numpy(np.ascontiguousarray(k[order])), [int(c) for c in counts]
+
+
+def _sort_worker(rank, world, port, n, kind, q):
+    sys.path.insert(0, str(ROOT))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    from oracle import oracle as orc
+    from nutdb_amd.dist import distributed_sort, gather_groups
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        rows = n // world
+        a, b = (0, 0) if kind == 1 else (-3, 7)  # kind 5 (RANGE_I64): heavy duplicates, splitter ties
+        local = torch.from_numpy(orc.gen_column(kind, 0x50, rows, row0=rank * rows, a=a, b=b))
+        out = distributed_sort(local, _np_partition, lambda t: torch.from_numpy(np.sort(t.numpy())),
+                               samples_per_rank=256)
+        allg = gather_groups(out.view(1, -1))
+        if rank == 0:
+            q.put(allg.numpy()[0])
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,kind", [(2, 1), (3, 1), (2, 5)])
+def test_sample_sort(world, kind, orc):
+    n = 300_000 - (300_000 % world)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sort_worker, args=(r, world, port, n, kind, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    a, b = (0, 0) if kind == 1 else (-3, 7)
+    want = np.sort(orc.gen_column(kind, 0x50, n, a=a, b=b))
+    assert np.array_equal(got, want)

@@ -339,3 +339,43 @@ def test_sort_large_property(ex, orc):
     o = host(out)
     assert np.all(o[1:] >= o[:-1])
     assert orc.multiset_hash(o) == orc.multiset_hash(orc.gen_column(1, 0x50, n))
+
+
+# ----------------------------------------------------------------------------- partition / sample sort
+@pytest.mark.parametrize("nsplit", [0, 1, 7, 63])
+def test_partition_i64(ex, nsplit):
+    rng = np.random.default_rng(nsplit)
+    n = 1_000_003
+    keys = rng.integers(-50, 50, n, dtype=np.int64) if nsplit == 7 else rng.integers(I64_MIN, I64_MAX, n,
+                                                                                        dtype=np.int64)
+    keys[:3] = [I64_MIN, I64_MAX, 0]
+    spl = np.sort(rng.choice(keys, nsplit, replace=False)) if nsplit else np.zeros(0, np.int64)
+    if nsplit == 7:
+        spl = np.array([-40, -10, -10, 0, 5, 5, 49], dtype=np.int64)  # repeated splitters: empty buckets
+    got, counts = ex.partition_i64(dev(keys, ex), spl)
+    b = np.searchsorted(spl, keys, side="right")
+    want = keys[np.argsort(b, kind="stable")]
+    assert counts == [int(c) for c in np.bincount(b, minlength=nsplit + 1)]
+    assert np.array_equal(host(got), want)
+
+
+def test_sample_sort_virtual_ranks(ex, orc):
+    """The multi-GPU sample sort's data path with P virtual ranks on one GPU: every shard
+    is partitioned on the device by the same splitters, bucket p of every shard goes to
+    'rank' p, each rank radix-sorts what it received; the concatenation is the sort."""
+    from nutdb_amd.workloads import SORT_COL
+    P, n = 5, 2_000_000
+    keys = orc.gen(SORT_COL, n)
+    shards = np.array_split(keys, P)
+    sample = np.sort(np.concatenate([s[(np.arange(256) * len(s)) // 256] for s in shards]))
+    spl = np.array([sample[(i * len(sample)) // P] for i in range(1, P)], dtype=np.int64)
+    received = [[] for _ in range(P)]
+    for s in shards:
+        part, counts = ex.partition_i64(dev(s, ex), spl)
+        off = 0
+        for p, c in enumerate(counts):
+            received[p].append(part[off:off + c])
+            off += c
+    out = [host(ex.sort_i64(torch.cat(r))) for r in received]
+    assert np.array_equal(np.concatenate(out), orc.sort_i64(keys))
+    assert all(o[-1] <= out[i + 1][0] for i, o in enumerate(out[:-1]) if len(o) and len(out[i + 1]))
