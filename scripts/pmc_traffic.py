@@ -15,7 +15,9 @@ from prof_summary import summarize  # noqa: E402
 WORKLOAD_KERNEL = {"q1": ("tpch_q1_shape_filter_groupby", "agg_kernel"),
                    "groupby": ("groupby_i64_sum_f64", "agg_kernel"),
                    "filter": ("filter_i64_compaction", "filter_i64_kernel"),
-                   "sort": ("sort_i64_radix", "rs_pass")}
+                   "sort": ("sort_i64_radix", "rs_")}
+# sort: one step = histogram kernel + every radix pass; traffic is summed per step
+STEP_KERNEL = {"sort": "rs_hist_kernel"}
 
 
 def main():
@@ -23,9 +25,9 @@ def main():
     args = sys.argv[2:]
     wl = args[args.index("--workload") + 1] if "--workload" in args else "q1"
     rows = float(args[args.index("--rows") + 1]) if "--rows" in args else {"q1": 1e9, "groupby": 1e9, "filter": 1e8,
-                                                                           "sort": 1e9}[wl]
+                                                                           "sort": 1.25e9}[wl]
     name, match = WORKLOAD_KERNEL[wl]
-    s = summarize(d, match)
+    s = summarize(d, match, STEP_KERNEL.get(wl, ""))
     c = s["counters"]
     traffic = None
     if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
@@ -37,6 +39,7 @@ def main():
     (d / f"pmc_{name}.json").write_text(json.dumps({
         "workload": name, "rows": int(rows), "kernel_match": match, "hbm_bytes_per_launch": traffic,
         "fetch_size_kb": c.get("FETCH_SIZE"), "write_size_kb": c.get("WRITE_SIZE"),
+        "per": "step (all rs_* kernels of one sort)" if wl == "sort" else "launch of " + match,
         "correction": "read = 2 x FETCH_SIZE (gfx950 wide-stream halving), write = WRITE_SIZE"}, indent=1))
     print(json.dumps({"workload": name, "traffic": traffic, "kernels": s["kernels"][:3]}))
 

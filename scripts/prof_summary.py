@@ -11,7 +11,7 @@ import sys
 from pathlib import Path
 
 
-def summarize(d: Path, match: str = "agg_kernel"):
+def summarize(d: Path, match: str = "agg_kernel", step_match: str = ""):
     out = {"kernels": [], "counters": {}}
     for f in glob.glob(str(d / "trace" / "*_kernel_stats.csv")):
         for row in csv.DictReader(open(f)):
@@ -25,6 +25,20 @@ def summarize(d: Path, match: str = "agg_kernel"):
         for k, v in vals.items():
             out["counters"][k] = sum(v) / len(v)
     c = out["counters"]
+    if step_match:
+        # totals per step: every dispatch matching `match`, divided by the number of
+        # dispatches of the once-per-step kernel `step_match`
+        for f in glob.glob(str(d / "*" / "*_counter_collection.csv")):
+            tot = collections.defaultdict(float)
+            steps = collections.defaultdict(set)
+            for row in csv.DictReader(open(f)):
+                if match in row["Kernel_Name"]:
+                    tot[row["Counter_Name"]] += float(row["Counter_Value"])
+                if step_match in row["Kernel_Name"]:
+                    steps[row["Counter_Name"]].add(row.get("Dispatch_Id", row.get("Correlation_Id", len(steps))))
+            for k, v in tot.items():
+                if steps[k]:
+                    c[k] = v / len(steps[k])
     if "FETCH_SIZE" in c:
         c["HBM_READ_BYTES_x2corr"] = c["FETCH_SIZE"] * 1024 * 2
     if "WRITE_SIZE" in c:
