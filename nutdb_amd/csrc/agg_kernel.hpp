@@ -65,7 +65,12 @@ __device__ __forceinline__ uint64_t lkey(uint64_t k1, uint64_t k2) {
 }
 // home bucket (4 slots, 32-B aligned) of a slot word
 constexpr uint32_t kBucket = 4;
-__device__ __forceinline__ uint32_t lhome(uint64_t w, int log2cap) { return slot_of(w, log2cap) & ~(kBucket - 1); }
+// on-chip table home: Fibonacci hash of the xor-folded key (3 VALU ops; the table has
+// at most 2^15 slots, so 32 product bits are plenty)
+__device__ __forceinline__ uint32_t lhome(uint64_t w, int log2cap) {
+  const uint32_t f = (uint32_t)w ^ (uint32_t)(w >> 32);
+  return ((f * 0x9E3779B1u) >> (32 - log2cap)) & ~(kBucket - 1);
+}
 
 template <int NK>
 __device__ __forceinline__ bool keys_match(const LTable &t, uint32_t s, uint64_t k1, uint64_t k2) {
@@ -253,16 +258,13 @@ __device__ __forceinline__ void consume_rows(const AggArgs &p, const LTable &lt,
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       if (ok[r]) {
-        // home bucket: the first slot holding w, or the first empty slot ends the chain
+        // home bucket: the first slot holding w; no match and an empty slot in the
+        // bucket ends the chain (no deletes: a key never sits behind an empty slot)
         int32_t s = -1;
-        bool end = false;
         const uint64_t c[4] = {b0[r].x, b0[r].y, b1[r].x, b1[r].y};
 #pragma unroll
-        for (int j = 3; j >= 0; --j) {
-          if (c[j] == w[r]) s = (int32_t)hb[r] + j;
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) end = end || (c[j] == kEmpty && (s < 0 || j < s - (int32_t)hb[r]));
+        for (int j = 3; j >= 0; --j) s = c[j] == w[r] ? (int32_t)hb[r] + j : s;
+        bool end = (c[0] == kEmpty) | (c[1] == kEmpty) | (c[2] == kEmpty) | (c[3] == kEmpty);
         if (NK == 2 && s >= 0 && !keys_match<NK>(lt, (uint32_t)s, x.k1[r], x.k2[r])) s = -1, end = false;
         if (NK == 1 && w[r] == kEmpty) s = -1, end = true;
         if (s < 0 && !end) {

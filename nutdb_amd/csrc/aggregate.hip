@@ -241,8 +241,10 @@ nut_status launch_agg(nut_groups *g, const nut_agg_spec *s, uint64_t group_hint,
   // its 4-slot home bucket) within the LDS budget
   const size_t lds_max = 160 * 1024;
   const int na = s->naggs;
+  // (32 slots = 8 buckets x 32 B = one pass over the 64 LDS banks: for <= 8 groups two
+  // home buckets never conflict — distinct buckets hit distinct banks, equal ones broadcast)
   uint64_t want = group_hint ? 4 * group_hint : 4096;
-  uint32_t lcap = 64;
+  uint32_t lcap = 32;
   while (lcap < want && lds_bytes(lcap * 2, g->nk, na, false, 0, kBdShared) <= lds_max) lcap *= 2;
   if (group_hint > 8ull * lcap) lcap = 0;  // hot keys cannot fit on chip: straight to HBM
   // private accumulators when every expected group fits P per thread, 2 blocks per CU

@@ -3,10 +3,11 @@
 // One pass over the column, order-preserving stream compaction:
 //   * 512-thread workgroups, one 16384-row tile each (16 stripes x 16 B per lane, a
 //     wave instruction reads 1 KiB contiguous; non-temporal loads: the column is
-//     streamed once).  Tile = blockIdx.x: workgroups are dispatched in ID order, so a
-//     tile only waits on tiles that were dispatched before it (the lowest unfinished
-//     tile never waits).  A global atomic ticket was measured to cost 0.11 ms of 0.39
-//     at N = 1e8 — every workgroup serialised on one address.
+//     streamed once).  Tile order comes from an atomic ticket taken at workgroup start,
+//     so a tile only ever waits on tiles that are already running, whatever the dispatch
+//     order (cdna_hip_programming.md §6 G16: no dependence on dispatch order).  The
+//     ticket serialises on one address: 0.11 ms at 24414 tiles, hence the large tiles
+//     (6104 tiles at N = 1e8; ~5 % of the kernel, scripts/tune/filter_tune.hip).
 //   * in-wave rank: __ballot + v_mbcnt (no shuffles); cross-wave: 16x8 counts in LDS.
 //   * the comparison is a template parameter (no per-row switch).
 //   * global offset: single-pass decoupled look-back.  Each tile publishes ONE 8-byte
@@ -87,13 +88,16 @@ __device__ __forceinline__ bool cmp_op(int64_t v, int64_t k) {
 template <bool ALIGNED, int OP>
 __global__ __launch_bounds__(FT_THREADS) void filter_i64_kernel(
     const int64_t *__restrict__ col, uint64_t n, int64_t k, int64_t *__restrict__ out,
-    uint64_t *__restrict__ out_n, uint64_t *__restrict__ status, uint32_t ntiles,
-    uint32_t *__restrict__ err) {
+    uint64_t *__restrict__ out_n, uint32_t *__restrict__ ticket, uint64_t *__restrict__ status,
+    uint32_t ntiles, uint32_t *__restrict__ err) {
   __shared__ uint32_t s_cnt[FT_STRIPES][FT_WAVES];
   __shared__ uint64_t s_excl;
+  __shared__ uint32_t s_tile;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const uint32_t tile = blockIdx.x;
+  if (tid == 0) s_tile = atomicAdd(ticket, 1u);
+  __syncthreads();
+  const uint32_t tile = s_tile;
   const uint64_t base = (uint64_t)tile * FT_TILE;
   const bool full = base + FT_TILE <= n;
 
@@ -167,25 +171,27 @@ extern "C" nut_status nut_filter_i64_async(nut_ctx *c, const int64_t *col, uint6
   }
   uint64_t ntiles = (n + FT_TILE - 1) / FT_TILE;
   if (ntiles > 0xFFFFFFF0ull) return fail(NUT_ERR_UNSUPPORTED, "nut_filter_i64: n too large");
-  // [pad u32, err u32, pad 8][status u64 x ntiles] — zeroed each call as one block
+  // [ticket u32, err u32, pad 8][status u64 x ntiles] — zeroed each call as one block
   size_t state = 16 + ntiles * 8;
   state = (state + 15) & ~size_t(15);
   nut_status st = c->filter_state.reserve(state);
   if (st) return st;
   char *base = (char *)c->filter_state.ptr;
-  uint32_t *err = (uint32_t *)base + 1;
+  uint32_t *ticket = (uint32_t *)base;
+  uint32_t *err = ticket + 1;
   uint64_t *status = (uint64_t *)(base + 16);
   NUT_HIP(hipMemsetAsync(base, 0, state, c->stream));
   bool aligned = ((uintptr_t)col & 15) == 0;
   c->timer.begin(c->stream, NUT_KERNEL_FILTER);
-  using K = void (*)(const int64_t *, uint64_t, int64_t, int64_t *, uint64_t *, uint64_t *, uint32_t, uint32_t *);
+  using K = void (*)(const int64_t *, uint64_t, int64_t, int64_t *, uint64_t *, uint32_t *, uint64_t *, uint32_t,
+                     uint32_t *);
   static const K kern[2][6] = {
       {filter_i64_kernel<false, NUT_LT>, filter_i64_kernel<false, NUT_LE>, filter_i64_kernel<false, NUT_GT>,
        filter_i64_kernel<false, NUT_GE>, filter_i64_kernel<false, NUT_EQ>, filter_i64_kernel<false, NUT_NE>},
       {filter_i64_kernel<true, NUT_LT>, filter_i64_kernel<true, NUT_LE>, filter_i64_kernel<true, NUT_GT>,
        filter_i64_kernel<true, NUT_GE>, filter_i64_kernel<true, NUT_EQ>, filter_i64_kernel<true, NUT_NE>}};
   hipLaunchKernelGGL(kern[aligned ? 1 : 0][op], dim3((unsigned)ntiles), dim3(FT_THREADS), 0, c->stream, col, n, k,
-                     out, out_n_dev, status, (uint32_t)ntiles, err);
+                     out, out_n_dev, ticket, status, (uint32_t)ntiles, err);
   c->timer.end(c->stream);
   NUT_HIP(hipGetLastError());
   return NUT_OK;
@@ -200,7 +206,7 @@ extern "C" nut_status nut_filter_i64(nut_ctx *c, const int64_t *col, uint64_t n,
   uint64_t *dev_n = (uint64_t *)c->misc.ptr;
   st = nut_filter_i64_async(c, col, n, op, k, out, dev_n);
   if (st) return st;
-  // err flag is the second word of filter_state (only if n > 0)
+  // err flag is the word after the ticket in filter_state (only if n > 0)
   if (n) NUT_HIP(hipMemcpyAsync(c->host_pinned + 1, (char *)c->filter_state.ptr + 4, 4,
                                 hipMemcpyDeviceToHost, c->stream));
   NUT_HIP(hipMemcpyAsync(c->host_pinned, dev_n, 8, hipMemcpyDeviceToHost, c->stream));

@@ -14,9 +14,9 @@
 //     {epoch|flag|count} granules, relaxed agent-scope stores/loads, no fence), and the
 //     tile is staged in LDS in digit order so consecutive threads write consecutive
 //     addresses of a bucket;
-//   * tile = blockIdx.x (in-order dispatch; no contended ticket atomic) and the status
-//     granules carry the pass epoch, so no per-pass memset of the status array
-//     (312 MB per pass at 1.25e9 keys otherwise).
+//   * tile order comes from a per-pass atomic ticket (progress never depends on dispatch
+//     order, cdna_hip_programming.md §6 G16) and the status granules carry the pass
+//     epoch, so no per-pass memset of the status array (312 MB per pass at 1.25e9 keys).
 // Measured (scripts/tune/sort_tune.hip, one pass, 2.5e8 keys): 256x16 tiles 1.72 ms,
 // 512x16 tiles 1.40 ms; without the look-back 0.91 ms.
 // Algorithmic bytes: 8 B/key histogram read + 16 B/key per executed pass.
@@ -163,6 +163,7 @@ __global__ __launch_bounds__(RS_THREADS) void rs_pass_kernel(const uint64_t *__r
                                                              uint64_t n, Digit dig, const int64_t *__restrict__ splitters,
                                                              int nbins, uint64_t flip, const uint64_t *__restrict__ dbase,
                                                              uint64_t *__restrict__ status, uint32_t epoch,
+                                                             uint32_t *__restrict__ ticket,
                                                              uint32_t *__restrict__ err) {
   __shared__ uint64_t s_keys[RS_TILE];             // tile staged in digit order
   __shared__ uint32_t s_wcnt[RS_WAVES][RS_BINS];    // per-wave digit counters -> wave prefixes
@@ -170,14 +171,15 @@ __global__ __launch_bounds__(RS_THREADS) void rs_pass_kernel(const uint64_t *__r
   __shared__ uint64_t s_gbase[RS_BINS];            // global position of the tile's first key of digit d
   __shared__ uint32_t s_wsum[RS_BINS / kWave];
   __shared__ int64_t s_spl[RS_MAX_BUCKETS];
+  __shared__ uint32_t s_tile;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   for (int i = tid; i < RS_WAVES * RS_BINS; i += RS_THREADS) (&s_wcnt[0][0])[i] = 0;
   if (splitters && tid < RS_MAX_BUCKETS) s_spl[tid] = tid < nbins - 1 ? splitters[tid] : INT64_MAX;
-  // tile = blockIdx.x: workgroups are dispatched in ID order, so a tile only waits on
-  // tiles dispatched before it (no global ticket: one contended atomic per tile cost
-  // more than the look-back itself, see filter.hip)
-  const uint32_t tile = blockIdx.x;
+  // ticket: a tile only waits on tiles that already hold a ticket (running or done)
+  if (tid == 0) s_tile = atomicAdd(ticket, 1u);
+  __syncthreads();
+  const uint32_t tile = s_tile;
   const uint64_t tbase = (uint64_t)tile * RS_TILE;
   // wave w owns keys [w*ITEMS*64, (w+1)*ITEMS*64) of the tile; item i, lane l -> +i*64+l
   const uint64_t wbase = tbase + (uint64_t)wave * RS_ITEMS * kWave;
@@ -191,7 +193,6 @@ __global__ __launch_bounds__(RS_THREADS) void rs_pass_kernel(const uint64_t *__r
     if (FIRST) k ^= flip;
     key[i] = k;
   }
-  __syncthreads();  // s_wcnt zeroed, s_spl loaded
   // stable in-wave ranking, items in order
 #pragma unroll
   for (int i = 0; i < RS_ITEMS; ++i) {
@@ -318,7 +319,8 @@ static nut_status sort_i64(nut_ctx *c, const int64_t *in, int64_t *out, uint64_t
   DeviceGuard g(c->device);
   const uint64_t ntiles = (n + RS_TILE - 1) / RS_TILE;
   if (ntiles > 0x7FFFFFF0ull || n > RS_VAL) return fail(NUT_ERR_UNSUPPORTED, "nut_sort_i64: n too large");
-  // scratch: [err 16 B | hist 8*256*8 | base 8*256*8 | trivial 8*4 | ping-pong buffer n*8]
+  // scratch: [err 4 B, pad | tickets 8 x 4 B at +16 | hist 8*256*8 at +256 | base 8*256*8 |
+  //           trivial 8*4 | ping-pong buffer n*8]
   const size_t o_hist = 256;
   const size_t o_base = o_hist + 8 * RS_BINS * 8;
   const size_t o_triv = o_base + 8 * RS_BINS * 8;
@@ -327,6 +329,7 @@ static nut_status sort_i64(nut_ctx *c, const int64_t *in, int64_t *out, uint64_t
   if (s) return s;
   char *b = (char *)c->sort_tmp.ptr;
   uint32_t *err = (uint32_t *)b;
+  uint32_t *tickets = (uint32_t *)(b + 16);
   unsigned long long *hist = (unsigned long long *)(b + o_hist);
   uint64_t *base = (uint64_t *)(b + o_base);
   uint32_t *triv = (uint32_t *)(b + o_triv);
@@ -334,7 +337,7 @@ static nut_status sort_i64(nut_ctx *c, const int64_t *in, int64_t *out, uint64_t
   hipStream_t st = c->stream;
 
   c->timer.begin(st, NUT_KERNEL_SORT);
-  NUT_HIP(hipMemsetAsync(b, 0, o_base, st));  // err + histograms
+  NUT_HIP(hipMemsetAsync(b, 0, o_base, st));  // err + tickets + histograms
   uint64_t hblocks = std::min<uint64_t>((n + 2 * RS_HIST_THREADS - 1) / (2 * RS_HIST_THREADS), (uint64_t)c->num_cus * 4);
   hipLaunchKernelGGL(rs_hist_kernel, dim3((unsigned)hblocks), dim3(RS_HIST_THREADS), 0, st, in, n, flip, hist);
   hipLaunchKernelGGL(rs_scan_kernel, dim3(8), dim3(RS_BINS), 0, st, (const unsigned long long *)hist, n, base, triv);
@@ -367,7 +370,7 @@ static nut_status sort_i64(nut_ctx *c, const int64_t *in, int64_t *out, uint64_t
     auto kern = first ? (last ? rs_pass_kernel<true, true, RadixDigit> : rs_pass_kernel<true, false, RadixDigit>)
                       : (last ? rs_pass_kernel<false, true, RadixDigit> : rs_pass_kernel<false, false, RadixDigit>);
     hipLaunchKernelGGL(kern, dim3((unsigned)ntiles), dim3(RS_THREADS), 0, st, src, dst, n, RadixDigit{8 * p},
-                       (const int64_t *)nullptr, RS_BINS, flip, db, status, epoch, err);
+                       (const int64_t *)nullptr, RS_BINS, flip, db, status, epoch, tickets + k, err);
     NUT_HIP(hipGetLastError());
     src = dst;
   }
@@ -402,11 +405,12 @@ extern "C" nut_status nut_partition_i64(nut_ctx *c, const int64_t *in, uint64_t 
   DeviceGuard g(c->device);
   const uint64_t ntiles = (n + RS_TILE - 1) / RS_TILE;
   if (ntiles > 0x7FFFFFF0ull || n > RS_VAL) return fail(NUT_ERR_UNSUPPORTED, "nut_partition_i64: n too large");
-  // misc scratch: [err 16 | hist 64*8 | splitters 64*8 | base 64*8]
+  // misc scratch: [err 4, ticket 4, pad 8 | hist 64*8 | splitters 64*8 | base 64*8]
   nut_status s = c->misc.reserve(16 + 3 * RS_MAX_BUCKETS * 8 + 64);
   if (s) return s;
   char *b = (char *)c->misc.ptr;
   uint32_t *err = (uint32_t *)b;
+  uint32_t *ticket = err + 1;
   unsigned long long *hist = (unsigned long long *)(b + 16);
   int64_t *spl = (int64_t *)(b + 16 + RS_MAX_BUCKETS * 8);
   uint64_t *base = (uint64_t *)(b + 16 + 2 * RS_MAX_BUCKETS * 8);
@@ -433,7 +437,7 @@ extern "C" nut_status nut_partition_i64(nut_ctx *c, const int64_t *in, uint64_t 
   if (s) return s;
   hipLaunchKernelGGL((rs_pass_kernel<false, false, BucketDigit>), dim3((unsigned)ntiles), dim3(RS_THREADS), 0, st,
                      (const uint64_t *)in, (uint64_t *)out, n, dig, (const int64_t *)spl, nb, (uint64_t)0,
-                     (const uint64_t *)base, status, epoch, err);
+                     (const uint64_t *)base, status, epoch, ticket, err);
   NUT_HIP(hipGetLastError());
   c->timer.end(st);
   uint32_t herr = 0;
