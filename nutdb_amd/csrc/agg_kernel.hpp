@@ -181,7 +181,9 @@ struct Rows {
 template <int VEC>
 __device__ __forceinline__ void load2(const AggArgs &p, const uint64_t *col, uint64_t i, uint64_t &x, uint64_t &y) {
   if (VEC == 1 || p.vec) {
-    const u64x2 v = *reinterpret_cast<const u64x2 *>(col + i);
+    // non-temporal: the columns stream through once (measured A/B on one box: config 3
+    // 2.98 -> 2.63 ms, Q1 7.95 -> 7.42 ms)
+    const u64x2 v = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(col + i));
     x = v.x;
     y = v.y;
   } else {
