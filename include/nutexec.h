@@ -130,13 +130,14 @@ typedef enum {
 } nut_expr;
 
 #define NUT_MAX_KEYS 2
-#define NUT_MAX_PRED 4
+#define NUT_MAX_PRED 6
 #define NUT_MAX_VALS 4
 #define NUT_MAX_AGGS 8
 
 typedef struct {
   uint64_t n;                          /* rows */
-  int32_t nkeys;                       /* 1..2 int64 key columns */
+  int32_t nkeys;                       /* 1..2 int64 key columns; 0 = global aggregate
+                                          (no GROUP BY: at most one group, key word 0) */
   const int64_t *keys[NUT_MAX_KEYS];
   int32_t npred;                       /* conjunction of npred terms (0 = no WHERE) */
   const void *pred_col[NUT_MAX_PRED];

@@ -18,7 +18,7 @@ import torch  # noqa: F401
 LIB_PATH = Path(os.environ.get("NUTEXEC_LIB", Path(__file__).resolve().parent / "libnutexec.so"))
 
 NUT_MAX_KEYS = 2
-NUT_MAX_PRED = 4
+NUT_MAX_PRED = 6
 NUT_MAX_VALS = 4
 NUT_MAX_AGGS = 8
 

@@ -209,7 +209,12 @@ __device__ __forceinline__ void load_rows(const AggArgs &p, uint64_t i0, uint64_
 #pragma unroll
   for (int t = 0; t < S::MP; ++t)
     if (t < S::np(p)) ld(p.pred_col[t], x.pv[t]);
-  ld(p.keys[0], x.k1);
+  if (NK == 1 && p.nokey) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) x.k1[r] = 0;
+  } else {
+    ld(p.keys[0], x.k1);
+  }
   if (NK == 2) ld(p.keys[1], x.k2);
 #pragma unroll
   for (int c = 0; c < S::MV; ++c)

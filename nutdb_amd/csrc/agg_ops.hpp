@@ -41,6 +41,7 @@ struct AggArgs {
   int32_t lds_log2;
   int32_t priv;                   // private groups per thread (PRIV kernels)
   int32_t vec;                    // all columns 16-B aligned: vector loads
+  int32_t nokey;                  // global aggregate: no key column, every key is 0
   const GTable *gt;               // device copy of the global table descriptor
 };
 

@@ -40,7 +40,7 @@ uint32_t pack_kinds(const int32_t *k, int n) {
 
 nut_status validate(const nut_agg_spec *s) {
   if (!s) return fail(NUT_ERR_INVALID_ARG, "nut_groupby: spec is NULL");
-  if (s->nkeys < 1 || s->nkeys > 2) return fail(NUT_ERR_UNSUPPORTED, "nut_groupby: 1 or 2 key columns supported");
+  if (s->nkeys < 0 || s->nkeys > 2) return fail(NUT_ERR_UNSUPPORTED, "nut_groupby: 0, 1 or 2 key columns supported");
   if (s->npred < 0 || s->npred > NUT_MAX_PRED) return fail(NUT_ERR_UNSUPPORTED, "nut_groupby: too many predicate terms");
   if (s->nvals < 0 || s->nvals > NUT_MAX_VALS) return fail(NUT_ERR_UNSUPPORTED, "nut_groupby: too many value columns");
   if (s->naggs < 0 || s->naggs > NUT_MAX_AGGS) return fail(NUT_ERR_UNSUPPORTED, "nut_groupby: too many aggregates");
@@ -213,8 +213,10 @@ nut_status launch_agg(nut_groups *g, const nut_agg_spec *s, uint64_t group_hint,
   AggArgs a;
   memset(&a, 0, sizeof(a));
   a.n = s->n;
-  a.keys[0] = (const uint64_t *)s->keys[0];
-  a.keys[1] = (const uint64_t *)(s->nkeys == 2 ? s->keys[1] : s->keys[0]);
+  // nkeys == 0 (global aggregate) runs the one-key kernels with every key = 0
+  a.nokey = s->nkeys == 0 ? 1 : 0;
+  a.keys[0] = (const uint64_t *)(s->nkeys ? s->keys[0] : nullptr);
+  a.keys[1] = s->nkeys == 2 ? (const uint64_t *)s->keys[1] : a.keys[0];
   a.npred = s->npred;
   for (int t = 0; t < s->npred; ++t) {
     a.pred_col[t] = (const uint64_t *)s->pred_col[t];
@@ -231,7 +233,7 @@ nut_status launch_agg(nut_groups *g, const nut_agg_spec *s, uint64_t group_hint,
     a.expr[i] = s->agg_op[i] == NUT_AGG_COUNT ? NUT_EX_COL : s->agg_expr[i];
     for (int j = 0; j < 3; ++j) a.arg[i][j] = s->agg_op[i] == NUT_AGG_COUNT ? 0 : s->agg_arg[i][j];
   }
-  auto misaligned = [](const void *ptr) { return ((uintptr_t)ptr & 15) != 0; };
+  auto misaligned = [](const void *ptr) { return ptr && ((uintptr_t)ptr & 15) != 0; };
   bool bad = misaligned(a.keys[0]) || misaligned(a.keys[1]);
   for (int t = 0; t < a.npred; ++t) bad |= misaligned(a.pred_col[t]);
   for (int v = 0; v < a.nvals; ++v) bad |= misaligned(a.val_col[v]);
@@ -325,9 +327,10 @@ nut_status nut_groupby(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hint, n
   DeviceGuard dg(c->device);
   nut_groups *g = new nut_groups();
   g->ctx = c;
-  g->nk = s->nkeys;
+  g->nk = s->nkeys ? s->nkeys : 1;  // a global aggregate is one group with key 0
   g->naggs = s->naggs;
   for (int a = 0; a < s->naggs; ++a) g->kinds[a] = kind_of(s, a);
+  if (s->nkeys == 0) group_hint = 1;
   uint64_t cap = table_cap_for(group_hint ? group_hint : 8192);
   for (int attempt = 0;; ++attempt) {
     st = alloc_table(g, cap);
@@ -355,7 +358,7 @@ nut_status nut_groupby_accumulate(nut_ctx *c, const nut_agg_spec *s, nut_groups 
   if (!c || !g) return fail(NUT_ERR_INVALID_ARG, "nut_groupby_accumulate: NULL argument");
   nut_status st = validate(s);
   if (st) return st;
-  if (s->nkeys != g->nk || s->naggs != g->naggs)
+  if ((s->nkeys ? s->nkeys : 1) != g->nk || s->naggs != g->naggs)
     return fail(NUT_ERR_INVALID_ARG, "nut_groupby_accumulate: spec shape differs from the result");
   int32_t kinds[NUT_MAX_AGGS];
   for (int a = 0; a < s->naggs; ++a) {

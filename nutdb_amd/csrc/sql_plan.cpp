@@ -464,7 +464,7 @@ bool lower(const Statement &st, nut_plan &p, Lowering &L) {
   if (b.having) return L.fail("HAVING is not executed");
   p.table = std::string(b.from->table);
   if (b.where && !lower_where(p, *b.where, L)) return false;
-  if (p.preds.size() > NUT_MAX_PRED) return L.fail("more than 4 WHERE terms");
+  if (p.preds.size() > NUT_MAX_PRED) return L.fail("more than " + std::to_string(NUT_MAX_PRED) + " WHERE terms");
   if (b.limit) {
     p.has_limit = true;
     p.limit = b.limit->size;
@@ -472,14 +472,20 @@ bool lower(const Statement &st, nut_plan &p, Lowering &L) {
     if (b.limit->with_ties) return L.fail("LIMIT ... WITH TIES is not executed");
   }
 
-  if (b.group_by) {
+  bool has_agg = false;
+  for (const QueryExpr &q : b.columns)
+    if (q.e.k == EK::FnCall && q.e.fn() == FnKind::Others) has_agg = true;
+  if (b.group_by || has_agg) {
+    // GROUP BY, or aggregates over the whole table (a global aggregate: no keys)
     p.kind = NUT_PLAN_GROUPBY;
-    for (const QueryExpr &k : *b.group_by) {
-      sv name;
-      if (!column_ref(k.e, name)) return L.fail("GROUP BY keys must be columns");
-      p.keys.push_back(col_index(p, name));
+    if (b.group_by) {
+      for (const QueryExpr &k : *b.group_by) {
+        sv name;
+        if (!column_ref(k.e, name)) return L.fail("GROUP BY keys must be columns");
+        p.keys.push_back(col_index(p, name));
+      }
+      if (p.keys.empty() || p.keys.size() > NUT_MAX_KEYS) return L.fail("GROUP BY takes 1 or 2 key columns");
     }
-    if (p.keys.empty() || p.keys.size() > NUT_MAX_KEYS) return L.fail("GROUP BY takes 1 or 2 key columns");
     int count_idx = -1;
     for (const QueryExpr &q : b.columns) {
       PlanOut o;
@@ -490,7 +496,9 @@ bool lower(const Statement &st, nut_plan &p, Lowering &L) {
         int c = col_index(p, name), j = -1;
         for (size_t i = 0; i < p.keys.size(); ++i)
           if (p.keys[i] == c) j = (int)i;
-        if (j < 0) return L.fail("column '" + std::string(name) + "' is neither a GROUP BY key nor aggregated");
+        if (j < 0)
+          return L.fail("column '" + std::string(name) + "' is neither a GROUP BY key nor aggregated" +
+                        (p.keys.empty() ? " (no GROUP BY)" : ""));
         o.kind = OUT_KEY;
         o.a = j;
       } else if (q.e.k == EK::FnCall && q.e.fn() == FnKind::Others) {
@@ -547,9 +555,7 @@ bool lower(const Statement &st, nut_plan &p, Lowering &L) {
     return true;
   }
 
-  // no GROUP BY: one projected column
-  for (const QueryExpr &q : b.columns)
-    if (q.e.k == EK::FnCall) return L.fail("aggregates without GROUP BY are not executed");
+  // no GROUP BY, no aggregate: one projected column
   sv name;
   if (b.columns.size() != 1 || !column_ref(b.columns[0].e, name))
     return L.fail("a plan without GROUP BY projects exactly one column");
@@ -840,12 +846,19 @@ nut_status exec_groupby(nut_ctx *c, const nut_plan &p, const nut_column *const *
   if (st) return st;
   uint64_t ng = 0;
   st = nut_groups_size(g, &ng);
-  std::vector<int64_t> keys(ng * p.keys.size() + 1);
+  std::vector<int64_t> keys(ng * std::max<size_t>(p.keys.size(), 1) + 1);
   std::vector<uint64_t> words(ng * p.aggs.size() + 1);
   if (!st) st = nut_groups_to_host(g, keys.data(), words.data(), ng);
   nut_groups_free(g);
   if (st) return st;
-  const size_t nk = p.keys.size(), na = p.aggs.size();
+  const size_t nk = std::max<size_t>(p.keys.size(), 1), na = p.aggs.size();
+  if (p.keys.empty() && ng == 0) {
+    // a global aggregate over no rows is still one row: counts and sums 0, min/max 0,
+    // avg NaN (ClickHouse's non-Nullable results)
+    ng = 1;
+    keys.assign(1, 0);
+    words.assign(na + 1, 0);
+  }
   // output columns in SELECT order
   r->host.resize(p.outs.size());
   for (size_t j = 0; j < p.outs.size(); ++j) {

@@ -51,18 +51,21 @@ class Agg:
 
 @dataclass
 class AggQuery:
-    """SELECT keys..., aggs... FROM t WHERE preds... GROUP BY keys..."""
+    """SELECT keys..., aggs... FROM t WHERE preds... GROUP BY keys...  (no keys: a global
+    aggregate, one group with key 0)"""
     keys: list
     aggs: list
     values: list = field(default_factory=list)
     preds: list = field(default_factory=list)   # (column, op, literal)
+    rows: int | None = None                     # row count when there is no column at all
 
     def to_spec(self, dev: torch.device) -> L.NutAggSpec:
         s = L.NutAggSpec()
-        n = int(self.keys[0].numel())
+        cols = list(self.keys) + list(self.values) + [c for c, _, _ in self.preds]
+        n = int(cols[0].numel()) if cols else int(self.rows or 0)
         s.n = n
-        if not 1 <= len(self.keys) <= L.NUT_MAX_KEYS:
-            raise ValueError("1 or 2 group keys")
+        if not 0 <= len(self.keys) <= L.NUT_MAX_KEYS:
+            raise ValueError("0, 1 or 2 group keys")
         s.nkeys = len(self.keys)
         for i, k in enumerate(self.keys):
             if k.dtype != torch.int64:
@@ -262,7 +265,7 @@ class Executor:
         self._bind_stream()
         h = C.c_void_p()
         check(lib.nut_groupby(self.ctx, C.byref(spec), group_hint, C.byref(h)), "nut_groupby")
-        return Groups(self, h.value, spec.nkeys, q.result_types())
+        return Groups(self, h.value, max(spec.nkeys, 1), q.result_types())
 
     def accumulate(self, q: AggQuery, acc: Groups) -> None:
         spec = q.to_spec(self.device)

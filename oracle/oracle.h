@@ -61,11 +61,11 @@ typedef struct {
   int nkeys;                 /* 1 or 2 int64 key columns */
   const int64_t *keys[2];
   int npred;                 /* conjunction of npred terms */
-  const void *pred_col[4];
-  int pred_type[4];          /* ORC_T_* */
-  int pred_op[4];            /* ORC_LT.. */
-  int64_t pred_i64[4];
-  double pred_f64[4];
+  const void *pred_col[6];
+  int pred_type[6];          /* ORC_T_* */
+  int pred_op[6];            /* ORC_LT.. */
+  int64_t pred_i64[6];
+  double pred_f64[6];
   int nvals;                 /* value columns referenced by expressions */
   const void *val_col[4];
   int val_type[4];

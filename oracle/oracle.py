@@ -29,11 +29,11 @@ class OrcAggSpec(C.Structure):
         ("nkeys", C.c_int),
         ("keys", C.c_void_p * 2),
         ("npred", C.c_int),
-        ("pred_col", C.c_void_p * 4),
-        ("pred_type", C.c_int * 4),
-        ("pred_op", C.c_int * 4),
-        ("pred_i64", C.c_int64 * 4),
-        ("pred_f64", C.c_double * 4),
+        ("pred_col", C.c_void_p * 6),
+        ("pred_type", C.c_int * 6),
+        ("pred_op", C.c_int * 6),
+        ("pred_i64", C.c_int64 * 6),
+        ("pred_f64", C.c_double * 6),
         ("nvals", C.c_int),
         ("val_col", C.c_void_p * 4),
         ("val_type", C.c_int * 4),

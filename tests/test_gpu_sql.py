@@ -135,3 +135,38 @@ def test_sql_binding_errors(ex):
     with pytest.raises(NutError) as e:
         ex.sql("select k from t group by k", {"k": a.double()})
     assert e.value.status == 7
+
+
+def test_sql_tpch_q6_global_aggregate(ex, orc):
+    """TPC-H Q6: five predicates (BETWEEN + date interval) and SUM(a*b) without GROUP BY."""
+    import math
+    from nutdb_amd.workloads import Q1_COLS, gen
+    n = 3_000_001
+    cols = {s[0]: gen(ex, s, n) for s in Q1_COLS}
+    got = ex.sql("""select sum(l_extendedprice * l_discount) as revenue, count(*) as n from lineitem
+        where l_shipdate >= toDate('1994-01-01') and l_shipdate < toDate('1994-01-01') + interval 1 year
+          and l_discount between 0.05 and 0.07 and l_quantity < 24""", cols)
+    sd, _, _, qty, price, disc = [orc.gen(s, n) for s in Q1_COLS]
+    m = (sd >= 8766) & (sd < 9131) & (disc >= 0.05) & (disc <= 0.07) & (qty < 24)
+    assert list(got) == ["revenue", "n"]
+    assert got["n"].tolist() == [int(m.sum())]
+    want = math.fsum((price[m] * disc[m]).tolist())
+    assert rel_err(got["revenue"], [want]) <= F64_SUM_RTOL
+
+
+def test_sql_global_aggregates_and_empty(ex):
+    rng = np.random.default_rng(11)
+    n = 1_000_003
+    v = rng.integers(0, 1 << 20, n) / 64.0  # dyadic: exact sums
+    i = rng.integers(-1000, 1000, n).astype(np.int64)
+    t = {"v": dev(v, ex), "i": dev(i, ex)}
+    got = ex.sql("select count(*), sum(v), min(v), max(v), avg(v), sum(i), min(i) from t where v > 4096", t)
+    m = v > 4096
+    assert got["count(*)"].tolist() == [int(m.sum())]
+    assert got["sum(v)"].tolist() == [float(v[m].sum())]
+    assert got["min(v)"].tolist() == [float(v[m].min())] and got["max(v)"].tolist() == [float(v[m].max())]
+    assert got["avg(v)"].tolist() == [float(v[m].sum()) / int(m.sum())]
+    assert got["sum(i)"].tolist() == [int(i[m].sum())] and got["min(i)"].tolist() == [int(i[m].min())]
+    empty = ex.sql("select count(*), sum(v), avg(v) from t where 1 = 0", t)
+    assert empty["count(*)"].tolist() == [0] and empty["sum(v)"].tolist() == [0.0]
+    assert np.isnan(empty["avg(v)"][0])

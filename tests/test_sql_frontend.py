@@ -441,6 +441,21 @@ def test_plan_filter_sort_shapes():
     assert [a["op"] for a in d["aggs"]] == ["sum", "count", "min", "max"]
 
 
+Q6 = """select sum(l_extendedprice * l_discount) as revenue from lineitem
+where l_shipdate >= toDate('1994-01-01') and l_shipdate < toDate('1994-01-01') + interval 1 year
+  and l_discount between 0.05 and 0.07 and l_quantity < 24"""
+
+
+def test_plan_tpch_q6_global_aggregate():
+    d = Plan(Q6).describe()
+    assert d["kind"] == "groupby" and d["keys"] == []
+    assert [(w["col"], w["op"], w["value"]) for w in d["where"]] == [
+        ("l_shipdate", ">=", "8766"), ("l_shipdate", "<", "9131"), ("l_discount", ">=", "0.05"),
+        ("l_discount", "<=", "0.07"), ("l_quantity", "<", "24")]
+    assert d["aggs"] == [{"op": "sum", "expr": "mul", "args": ["l_extendedprice", "l_discount"]}]
+    assert d["outputs"] == [{"name": "revenue", "from": "agg", "index": 0}]
+
+
 @pytest.mark.parametrize("sql,frag", [
     ("insert into t values (1)", "only SELECT"),
     ("select a, b from t", "exactly one column"),
@@ -450,7 +465,9 @@ def test_plan_filter_sort_shapes():
     ("select k, sum(v) from t join u on a = b group by k", "JOIN"),
     ("select k, v from t group by k", "neither a GROUP BY key"),
     ("select k, sum(v * w * z) from t group by k", "fused expression shape"),
-    ("select count(*) from t", "without GROUP BY"),
+    ("select count(*), v from t", "no GROUP BY"),
+    ("select x from t where x > 1 and x < 9 and x != 3 and x != 4 and x != 5 and x != 6 and x != 7 order by x",
+     "more than 6 WHERE terms"),
     ("select x from t where x < 1 union all select x from t", "UNION"),
     ("select x from t where x >= toDate('1998-13-01')", "toDate"),
 ])
