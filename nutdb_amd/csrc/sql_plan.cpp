@@ -259,6 +259,19 @@ enum OutKind { OUT_KEY, OUT_AGG, OUT_AVG };
 struct PlanOut {
   int kind, a, b;
   std::string name, text;
+  bool hidden = false;  // computed for HAVING only, not part of the result
+};
+
+// HAVING, evaluated on the host over the (small) group result
+enum HKind { H_CONST, H_OUT, H_CMP, H_AND, H_OR, H_NOT, H_BOOL };
+struct HNode {
+  int k = H_BOOL;
+  int op = 0;        // H_CMP: nut_cmp
+  int out = -1;      // H_OUT: output index
+  bool is_int = false, b = true;
+  int64_t i = 0;
+  double f = 0;
+  std::vector<HNode> kids;
 };
 
 }  // namespace
@@ -275,6 +288,8 @@ struct nut_plan {
   std::vector<PlanAgg> aggs;
   std::vector<PlanOut> outs;
   std::vector<std::pair<int, bool>> order;  // GROUPBY: (output, desc)
+  bool has_having = false;
+  HNode having;
   bool has_limit = false;
   uint64_t limit = 0, offset = 0;
 };
@@ -453,6 +468,134 @@ bool lower_where(nut_plan &p, const Expr &e, Lowering &L) {
   return lower_pred_term(p, e, L);
 }
 
+// one SELECT-list item of an aggregate plan: a GROUP BY key or sum/count/min/max/avg
+bool lower_output(nut_plan &p, const Expr &e, PlanOut &o, Lowering &L) {
+  sv name;
+  if (column_ref(e, name)) {
+    int c = col_index(p, name), j = -1;
+    for (size_t i = 0; i < p.keys.size(); ++i)
+      if (p.keys[i] == c) j = (int)i;
+    if (j < 0)
+      return L.fail("column '" + std::string(name) + "' is neither a GROUP BY key nor aggregated" +
+                    (p.keys.empty() ? " (no GROUP BY)" : ""));
+    o.kind = OUT_KEY;
+    o.a = j;
+    return true;
+  }
+  if (!(e.k == EK::FnCall && e.fn() == FnKind::Others))
+    return L.fail("SELECT item '" + o.text + "' is not a key column or an aggregate");
+  sv fn = e.id.name;
+  int op = ieq(fn, "sum") ? NUT_AGG_SUM : ieq(fn, "count") ? NUT_AGG_COUNT : ieq(fn, "min") ? NUT_AGG_MIN
+           : ieq(fn, "max") ? NUT_AGG_MAX : ieq(fn, "avg") ? 100 : -1;
+  if (op < 0) return L.fail("function '" + std::string(fn) + "' is not an executed aggregate (sum/count/min/max/avg)");
+  PlanAgg a{};
+  if (op == NUT_AGG_COUNT) {
+    if (e.kids.size() > 1) return L.fail("count takes at most one argument");
+    if (e.kids.size() == 1 && !(e.kids[0].k == EK::Identifier)) return L.fail("count argument must be * or a column");
+    a.op = NUT_AGG_COUNT;
+    a.expr = NUT_EX_COL;
+    o.kind = OUT_AGG;
+    o.a = add_agg(p, a);
+    return true;
+  }
+  if (e.kids.size() != 1) return L.fail(std::string(fn) + " takes one argument");
+  if (!lower_agg_expr(p, e.kids[0], a, L)) return false;
+  if (op == 100) {
+    a.op = NUT_AGG_SUM;
+    o.kind = OUT_AVG;
+    o.a = add_agg(p, a);
+    PlanAgg c{};
+    c.op = NUT_AGG_COUNT;
+    o.b = add_agg(p, c);
+  } else {
+    a.op = op;
+    o.kind = OUT_AGG;
+    o.a = add_agg(p, a);
+  }
+  return true;
+}
+
+// an output for a HAVING operand: reuse a SELECT item with the same text, else add a
+// hidden one
+bool having_output(nut_plan &p, const Expr &e, int &out, Lowering &L) {
+  const std::string text = expr_text(e);
+  for (size_t i = 0; i < p.outs.size(); ++i)
+    if (ieq(p.outs[i].text, text) || (!p.outs[i].hidden && ieq(p.outs[i].name, text))) {
+      out = (int)i;
+      return true;
+    }
+  PlanOut o;
+  o.text = o.name = text;
+  o.hidden = true;
+  if (!lower_output(p, e, o, L)) return false;
+  p.outs.push_back(std::move(o));
+  out = (int)p.outs.size() - 1;
+  return true;
+}
+
+// HAVING: AND/OR/NOT of comparisons between aggregates, keys and constants
+bool lower_having(nut_plan &p, const Expr &e, HNode &h, Lowering &L) {
+  bool bv;
+  if (e.is_bool_lit(&bv)) {
+    h.k = H_BOOL;
+    h.b = bv;
+    return true;
+  }
+  if (e.k == EK::UnaryOp && e.uop() == UnOp::Not) {
+    h.k = H_NOT;
+    h.kids.resize(1);
+    return lower_having(p, e.kids[0], h.kids[0], L);
+  }
+  if (e.k == EK::BinaryOp && (e.bop() == BinOp::And || e.bop() == BinOp::Or)) {
+    h.k = e.bop() == BinOp::And ? H_AND : H_OR;
+    h.kids.resize(2);
+    return lower_having(p, e.kids[0], h.kids[0], L) && lower_having(p, e.kids[1], h.kids[1], L);
+  }
+  auto operand = [&](const Expr &x, HNode &o) {
+    CVal c;
+    Lowering quiet;
+    if (const_eval(x, c, quiet)) {
+      o.k = H_CONST;
+      if (c.is_int && c.v <= INT64_MAX && c.v >= INT64_MIN) {
+        o.is_int = true;
+        o.i = (int64_t)c.v;
+      } else {
+        o.f = c.is_int ? (double)c.v : c.dec.to_f64();
+      }
+      return true;
+    }
+    o.k = H_OUT;
+    return having_output(p, x, o.out, L);
+  };
+  if (e.k == EK::BinaryOp && cmp_of(e.bop()) >= 0) {
+    h.k = H_CMP;
+    h.op = cmp_of(e.bop());
+    h.kids.resize(2);
+    return operand(e.kids[0], h.kids[0]) && operand(e.kids[1], h.kids[1]);
+  }
+  if (e.k == EK::FnCall && (e.fn() == FnKind::Between || e.fn() == FnKind::NotBetween) && e.kids.size() == 3) {
+    HNode lo, hi, x;
+    if (!operand(e.kids[0], x) || !operand(e.kids[1], lo) || !operand(e.kids[2], hi)) return false;
+    HNode ge, le;
+    ge.k = le.k = H_CMP;
+    ge.op = NUT_GE;
+    le.op = NUT_LE;
+    ge.kids = {x, lo};
+    le.kids = {x, hi};
+    HNode both;
+    both.k = H_AND;
+    both.kids = {ge, le};
+    if (e.fn() == FnKind::Between) {
+      h = std::move(both);
+    } else {
+      h.k = H_NOT;
+      h.kids = {both};
+    }
+    return true;
+  }
+  return L.fail("unsupported HAVING term '" + expr_text(e) + "'");
+}
+
 bool lower(const Statement &st, nut_plan &p, Lowering &L) {
   if (st.k != StmtKind::Select) return L.fail("only SELECT statements execute");
   if (st.query.is_union) return L.fail("UNION/INTERSECT/EXCEPT are not executed (one query body per plan)");
@@ -461,7 +604,7 @@ bool lower(const Statement &st, nut_plan &p, Lowering &L) {
   if (b.distinct) return L.fail("DISTINCT is not executed");
   if (!b.from || b.from->k != SourceKind::Table) return L.fail("FROM must name one table");
   if (!b.joins.empty()) return L.fail("JOIN is not executed");
-  if (b.having) return L.fail("HAVING is not executed");
+  if (b.having && !b.group_by) return L.fail("HAVING needs GROUP BY");
   p.table = std::string(b.from->table);
   if (b.where && !lower_where(p, *b.where, L)) return false;
   if (p.preds.size() > NUT_MAX_PRED) return L.fail("more than " + std::to_string(NUT_MAX_PRED) + " WHERE terms");
@@ -486,72 +629,37 @@ bool lower(const Statement &st, nut_plan &p, Lowering &L) {
       }
       if (p.keys.empty() || p.keys.size() > NUT_MAX_KEYS) return L.fail("GROUP BY takes 1 or 2 key columns");
     }
-    int count_idx = -1;
     for (const QueryExpr &q : b.columns) {
       PlanOut o;
       o.text = expr_text(q.e);
       o.name = q.alias ? std::string(*q.alias) : o.text;
-      sv name;
-      if (column_ref(q.e, name)) {
-        int c = col_index(p, name), j = -1;
-        for (size_t i = 0; i < p.keys.size(); ++i)
-          if (p.keys[i] == c) j = (int)i;
-        if (j < 0)
-          return L.fail("column '" + std::string(name) + "' is neither a GROUP BY key nor aggregated" +
-                        (p.keys.empty() ? " (no GROUP BY)" : ""));
-        o.kind = OUT_KEY;
-        o.a = j;
-      } else if (q.e.k == EK::FnCall && q.e.fn() == FnKind::Others) {
-        sv fn = q.e.id.name;
-        int op = ieq(fn, "sum") ? NUT_AGG_SUM : ieq(fn, "count") ? NUT_AGG_COUNT : ieq(fn, "min") ? NUT_AGG_MIN
-                 : ieq(fn, "max") ? NUT_AGG_MAX : ieq(fn, "avg") ? 100 : -1;
-        if (op < 0) return L.fail("function '" + std::string(fn) + "' is not an executed aggregate (sum/count/min/max/avg)");
-        PlanAgg a{};
-        if (op == NUT_AGG_COUNT) {
-          if (q.e.kids.size() > 1) return L.fail("count takes at most one argument");
-          if (q.e.kids.size() == 1 && !(q.e.kids[0].k == EK::Identifier)) return L.fail("count argument must be * or a column");
-          a.op = NUT_AGG_COUNT;
-          a.expr = NUT_EX_COL;
-          o.kind = OUT_AGG;
-          o.a = add_agg(p, a);
-        } else {
-          if (q.e.kids.size() != 1) return L.fail(std::string(fn) + " takes one argument");
-          if (!lower_agg_expr(p, q.e.kids[0], a, L)) return false;
-          if (op == 100) {
-            a.op = NUT_AGG_SUM;
-            o.kind = OUT_AVG;
-            o.a = add_agg(p, a);
-            PlanAgg c{};
-            c.op = NUT_AGG_COUNT;
-            o.b = add_agg(p, c);
-          } else {
-            a.op = op;
-            o.kind = OUT_AGG;
-            o.a = add_agg(p, a);
-          }
-        }
-      } else {
-        return L.fail("SELECT item '" + o.text + "' is not a key column or an aggregate");
-      }
+      if (!lower_output(p, q.e, o, L)) return false;
       p.outs.push_back(std::move(o));
     }
-    (void)count_idx;
+    if (b.having) {
+      if (!lower_having(p, *b.having, p.having, L)) return false;
+      p.has_having = true;
+    }
     if (p.aggs.size() > NUT_MAX_AGGS) return L.fail("more than 8 aggregates");
     if (p.vals.size() > NUT_MAX_VALS) return L.fail("aggregates reference more than 4 value columns");
     if (b.order_by) {
       for (const OrderKey &k : *b.order_by) {
         int idx = -1;
         sv name;
-        std::string text = expr_text(k.e.e);
+        const std::string text = expr_text(k.e.e);
         for (size_t i = 0; i < p.outs.size() && idx < 0; ++i) {
           const PlanOut &o = p.outs[i];
-          if (ieq(o.name, text) || ieq(o.text, text)) idx = (int)i;
-          if (idx < 0 && column_ref(k.e.e, name) && o.kind == OUT_KEY && ieq(p.cols[p.keys[o.a]], name)) idx = (int)i;
+          if (!o.hidden && (ieq(o.name, text) || ieq(o.text, text))) idx = (int)i;
+          if (idx < 0 && !o.hidden && column_ref(k.e.e, name) && o.kind == OUT_KEY && ieq(p.cols[p.keys[o.a]], name))
+            idx = (int)i;
         }
-        if (idx < 0) return L.fail("ORDER BY '" + text + "' is not an output column");
+        if (idx < 0 && !having_output(p, k.e.e, idx, L))
+          return L.fail("ORDER BY '" + text + "' is neither an output column nor an aggregate");
         p.order.push_back({idx, k.desc});
       }
     }
+    if (p.aggs.size() > NUT_MAX_AGGS) return L.fail("more than 8 aggregates (HAVING / ORDER BY included)");
+    if (p.vals.size() > NUT_MAX_VALS) return L.fail("aggregates reference more than 4 value columns");
     return true;
   }
 
@@ -652,12 +760,15 @@ std::string describe(const nut_plan &p) {
     if (i) o += ',';
     o += "{\"name\":";
     json_str(o, u.name);
+    if (u.hidden) o += ",\"hidden\":true";
     o += u.kind == OUT_KEY ? ",\"from\":\"key\",\"index\":" + std::to_string(u.a)
          : u.kind == OUT_AGG ? ",\"from\":\"agg\",\"index\":" + std::to_string(u.a)
                              : ",\"from\":\"avg\",\"sum\":" + std::to_string(u.a) + ",\"count\":" + std::to_string(u.b);
     o += "}";
   }
-  o += "],\"order\":[";
+  o += "],\"having\":";
+  o += p.has_having ? "true" : "false";
+  o += ",\"order\":[";
   for (size_t i = 0; i < p.order.size(); ++i) {
     if (i) o += ',';
     o += "{\"output\":" + std::to_string(p.order[i].first) + ",\"desc\":" + (p.order[i].second ? "true" : "false") + "}";
@@ -779,6 +890,52 @@ nut_status exec_scan(nut_ctx *c, const nut_plan &p, const nut_column *const *bou
   return NUT_OK;
 }
 
+// HAVING evaluation for group i: operands are int64 or f64 output words / constants;
+// int-int comparisons are exact, anything else compares as f64
+struct HVal {
+  bool is_int;
+  int64_t i;
+  double f;
+};
+HVal having_val(const HNode &h, const std::vector<std::vector<uint64_t>> &cols, const std::vector<int> &types,
+                uint64_t g) {
+  if (h.k == H_CONST) return HVal{h.is_int, h.i, h.f};
+  const uint64_t w = cols[h.out][g];
+  if (types[h.out] == NUT_T_I64) return HVal{true, (int64_t)w, 0.0};
+  double f;
+  memcpy(&f, &w, 8);
+  return HVal{false, 0, f};
+}
+bool having_true(const HNode &h, const std::vector<std::vector<uint64_t>> &cols, const std::vector<int> &types,
+                 uint64_t g) {
+  switch (h.k) {
+    case H_BOOL: return h.b;
+    case H_NOT: return !having_true(h.kids[0], cols, types, g);
+    case H_AND: return having_true(h.kids[0], cols, types, g) && having_true(h.kids[1], cols, types, g);
+    case H_OR: return having_true(h.kids[0], cols, types, g) || having_true(h.kids[1], cols, types, g);
+    case H_CMP: {
+      const HVal a = having_val(h.kids[0], cols, types, g), b = having_val(h.kids[1], cols, types, g);
+      int c;
+      if (a.is_int && b.is_int) {
+        c = a.i < b.i ? -1 : a.i > b.i ? 1 : 0;
+      } else {
+        const double x = a.is_int ? (double)a.i : a.f, y = b.is_int ? (double)b.i : b.f;
+        if (x != x || y != y) return h.op == NUT_NE;  // NaN compares unequal
+        c = x < y ? -1 : x > y ? 1 : 0;
+      }
+      switch (h.op) {
+        case NUT_LT: return c < 0;
+        case NUT_LE: return c <= 0;
+        case NUT_GT: return c > 0;
+        case NUT_GE: return c >= 0;
+        case NUT_EQ: return c == 0;
+        default: return c != 0;
+      }
+    }
+    default: return false;
+  }
+}
+
 nut_status exec_groupby(nut_ctx *c, const nut_plan &p, const nut_column *const *bound, uint64_t n, uint64_t hint,
                         nut_result *r) {
   nut_agg_spec s;
@@ -887,9 +1044,12 @@ nut_status exec_groupby(nut_ctx *c, const nut_plan &p, const nut_column *const *
     r->names.push_back(o.name);
     r->types.push_back(type);
   }
-  // ORDER BY over outputs (groups arrive sorted by key tuple), then LIMIT
-  std::vector<uint64_t> idx(ng);
-  for (uint64_t i = 0; i < ng; ++i) idx[i] = i;
+  // HAVING, then ORDER BY over outputs (groups arrive sorted by key tuple), then LIMIT
+  std::vector<uint64_t> idx;
+  idx.reserve(ng);
+  for (uint64_t i = 0; i < ng; ++i)
+    if (!p.has_having || having_true(p.having, r->host, r->types, i)) idx.push_back(i);
+  const uint64_t kept = idx.size();
   if (!p.order.empty()) {
     std::stable_sort(idx.begin(), idx.end(), [&](uint64_t x, uint64_t y) {
       for (const auto &ok : p.order) {
@@ -909,14 +1069,23 @@ nut_status exec_groupby(nut_ctx *c, const nut_plan &p, const nut_column *const *
       return false;
     });
   }
-  uint64_t off = p.has_limit ? std::min(p.offset, ng) : 0;
-  uint64_t rows = ng - off;
+  uint64_t off = p.has_limit ? std::min(p.offset, kept) : 0;
+  uint64_t rows = kept - off;
   if (p.has_limit) rows = std::min(rows, p.limit);
-  for (auto &col : r->host) {
+  std::vector<std::vector<uint64_t>> vis;
+  std::vector<std::string> names;
+  std::vector<int> types;
+  for (size_t j = 0; j < p.outs.size(); ++j) {
+    if (p.outs[j].hidden) continue;
     std::vector<uint64_t> out(rows);
-    for (uint64_t i = 0; i < rows; ++i) out[i] = col[idx[off + i]];
-    col.swap(out);
+    for (uint64_t i = 0; i < rows; ++i) out[i] = r->host[j][idx[off + i]];
+    vis.push_back(std::move(out));
+    names.push_back(r->names[j]);
+    types.push_back(r->types[j]);
   }
+  r->host.swap(vis);
+  r->names.swap(names);
+  r->types.swap(types);
   r->nrows = rows;
   return NUT_OK;
 }

@@ -170,3 +170,24 @@ def test_sql_global_aggregates_and_empty(ex):
     empty = ex.sql("select count(*), sum(v), avg(v) from t where 1 = 0", t)
     assert empty["count(*)"].tolist() == [0] and empty["sum(v)"].tolist() == [0.0]
     assert np.isnan(empty["avg(v)"][0])
+
+
+def test_sql_having_and_order_by_aggregate(ex, orc):
+    from nutdb_amd import _lib as L
+    n = 1_200_007
+    kspec = ("k", L.GEN_POOL_KEY, 0x71, 300, 0, 1.0)
+    vspec = ("v", L.GEN_DYADIC, 0x72, 0, 0, 1.0)
+    cols = {s[0]: ex.gen_column(s[1], s[2], n, a=s[3], b=s[4], c=s[5]) for s in (kspec, vspec)}
+    k, v = (orc.gen(s, n) for s in (kspec, vspec))
+    got = ex.sql("select k, sum(v) as s from t group by k having count(*) >= 4000 and not s < 32000000 "
+                 "or k between -10 and 10 order by max(v) desc, k", cols, group_hint=300)
+    uk, inv = np.unique(k, return_inverse=True)
+    cnt = np.bincount(inv)
+    sums = np.bincount(inv, weights=v)
+    maxs = np.full(len(uk), -np.inf)
+    np.maximum.at(maxs, inv, v)
+    keep = ((cnt >= 4000) & ~(sums < 32000000)) | ((uk >= -10) & (uk <= 10))
+    order = np.lexsort((uk[keep], -maxs[keep]))
+    assert list(got) == ["k", "s"]
+    assert np.array_equal(got["k"], uk[keep][order])
+    assert np.array_equal(got["s"], sums[keep][order])

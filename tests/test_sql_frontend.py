@@ -441,6 +441,16 @@ def test_plan_filter_sort_shapes():
     assert [a["op"] for a in d["aggs"]] == ["sum", "count", "min", "max"]
 
 
+def test_plan_having_and_hidden_order_keys():
+    d = Plan("select k, sum(v) as s from t group by k having count(*) > 10 and s < 5.5 "
+             "order by max(v) desc").describe()
+    assert d["having"] is True
+    assert [(o["name"], o.get("hidden", False)) for o in d["outputs"]] == [
+        ("k", False), ("s", False), ("count(*)", True), ("max(v)", True)]
+    assert [a["op"] for a in d["aggs"]] == ["sum", "count", "max"]
+    assert d["order"] == [{"output": 3, "desc": True}]
+
+
 Q6 = """select sum(l_extendedprice * l_discount) as revenue from lineitem
 where l_shipdate >= toDate('1994-01-01') and l_shipdate < toDate('1994-01-01') + interval 1 year
   and l_discount between 0.05 and 0.07 and l_quantity < 24"""
@@ -459,7 +469,9 @@ def test_plan_tpch_q6_global_aggregate():
 @pytest.mark.parametrize("sql,frag", [
     ("insert into t values (1)", "only SELECT"),
     ("select a, b from t", "exactly one column"),
-    ("select k, sum(v) from t group by k having sum(v) > 1", "HAVING"),
+    ("select sum(v) from t having sum(v) > 1", "HAVING needs GROUP BY"),
+    ("select k, sum(v) from t group by k having k like 'x%'", "unsupported HAVING term"),
+    ("select k from t group by k order by median(v)", "median"),
     ("select k, median(v) from t group by k", "median"),
     ("select x from t where x < y", "unsupported WHERE term"),
     ("select k, sum(v) from t join u on a = b group by k", "JOIN"),
