@@ -179,7 +179,7 @@ def test_sql_having_and_order_by_aggregate(ex, orc):
     vspec = ("v", L.GEN_DYADIC, 0x72, 0, 0, 1.0)
     cols = {s[0]: ex.gen_column(s[1], s[2], n, a=s[3], b=s[4], c=s[5]) for s in (kspec, vspec)}
     k, v = (orc.gen(s, n) for s in (kspec, vspec))
-    got = ex.sql("select k, sum(v) as s from t group by k having count(*) >= 4000 and not s < 32000000 "
+    got = ex.sql("select k, sum(v) as s from t group by k having count(*) >= 4000 and not (s < 32000000) "
                  "or k between -10 and 10 order by max(v) desc, k", cols, group_hint=300)
     uk, inv = np.unique(k, return_inverse=True)
     cnt = np.bincount(inv)
