@@ -256,6 +256,161 @@ void run(const char *name, const uint64_t *in, uint64_t *out, uint64_t n, const 
   CK(hipMemset(g_steps, 0, sizeof hs));
 }
 
+// SUB sub-tiles of THREADS*ITEMS keys per workgroup: one look-back per SUB*THREADS*ITEMS
+// keys; ranks run across the sub-tiles; staging in LDS one sub-tile of positions at a time.
+template <int THREADS, int ITEMS, int SUB>
+__global__ __launch_bounds__(THREADS) void pass2(const uint64_t *__restrict__ in, uint64_t *__restrict__ out, uint64_t n,
+                                                 int shift, const uint64_t *__restrict__ dbase,
+                                                 uint64_t *__restrict__ status, uint32_t *__restrict__ ticket) {
+  constexpr int WAVES = THREADS / kWave;
+  constexpr int STILE = THREADS * ITEMS;
+  constexpr int TILE = STILE * SUB;
+  __shared__ uint64_t s_keys[STILE];
+  __shared__ uint32_t s_wcnt[WAVES][BINS];
+  __shared__ uint32_t s_tex[BINS];
+  __shared__ uint64_t s_gbase[BINS];
+  __shared__ uint32_t s_wsum[BINS / 64];
+  __shared__ uint32_t s_tile;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int i = tid; i < WAVES * BINS; i += THREADS) (&s_wcnt[0][0])[i] = 0;
+  if (tid == 0) s_tile = atomicAdd(ticket, 1u);
+  __syncthreads();
+  const uint32_t tile = s_tile;
+  const uint64_t tbase = (uint64_t)tile * TILE;
+  uint64_t key[SUB][ITEMS];
+  uint32_t rank[SUB][ITEMS];
+#pragma unroll
+  for (int sb = 0; sb < SUB; ++sb) {
+    const uint64_t wbase = tbase + (uint64_t)sb * STILE + (uint64_t)wave * ITEMS * kWave;
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {
+      const uint64_t idx = wbase + (uint64_t)i * kWave + lane;
+      key[sb][i] = idx < n ? in[idx] : 0;
+    }
+  }
+#pragma unroll
+  for (int sb = 0; sb < SUB; ++sb) {
+    const uint64_t wbase = tbase + (uint64_t)sb * STILE + (uint64_t)wave * ITEMS * kWave;
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {
+      const uint64_t idx = wbase + (uint64_t)i * kWave + lane;
+      const bool valid = idx < n;
+      const uint32_t d = (uint32_t)(key[sb][i] >> shift) & 255u;
+      const uint64_t pe = peers8(d, valid);
+      const uint32_t before = lane_rank(pe);
+      const uint32_t cnt = (uint32_t)__popcll(pe);
+      uint32_t prior = valid ? s_wcnt[wave][d] : 0u;
+      rank[sb][i] = prior + before;
+      if (valid && before == 0) s_wcnt[wave][d] = prior + cnt;
+    }
+  }
+  __syncthreads();
+  uint32_t v = 0, tot = 0;
+  if (tid < BINS) {
+#pragma unroll
+    for (int w = 0; w < WAVES; ++w) {
+      const uint32_t c = s_wcnt[w][tid];
+      s_wcnt[w][tid] = tot;
+      tot += c;
+    }
+    v = tot;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      uint32_t y = __shfl_up(v, off, 64);
+      if (lane >= off) v += y;
+    }
+    if (lane == 63) s_wsum[wave] = v;
+  }
+  __syncthreads();
+  if (tid < BINS) {
+    const int d = tid;
+    uint32_t add = 0;
+    for (int w = 0; w < (BINS / 64); ++w) add += (w < wave) ? s_wsum[w] : 0u;
+    s_tex[d] = v - tot + add;
+    uint64_t excl = 0;
+    uint64_t *my = &status[(uint64_t)tile * BINS + d];
+    if (tile == 0) {
+      st_agent(my, INC | tot);
+    } else {
+      st_agent(my, AGG | tot);
+      int64_t j = (int64_t)tile - 1;
+      for (;;) {
+        uint64_t sm = ld_agent(&status[(uint64_t)j * BINS + d]);
+        while ((sm >> 62) == 0) {
+          __builtin_amdgcn_s_sleep(1);
+          sm = ld_agent(&status[(uint64_t)j * BINS + d]);
+        }
+        excl += sm & VAL;
+        if ((sm >> 62) == 2) break;
+        --j;
+      }
+      st_agent(my, INC | (excl + tot));
+    }
+    s_gbase[d] = dbase[d] + excl;
+  }
+  __syncthreads();
+  const uint32_t valid_n = (uint32_t)min<uint64_t>(TILE, n - min<uint64_t>(n, tbase));
+#pragma unroll
+  for (int half = 0; half < SUB; ++half) {
+    const uint32_t lo = (uint32_t)half * STILE, hi = lo + STILE;
+#pragma unroll
+    for (int sb = 0; sb < SUB; ++sb) {
+      const uint64_t wbase = tbase + (uint64_t)sb * STILE + (uint64_t)wave * ITEMS * kWave;
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i) {
+        const uint64_t idx = wbase + (uint64_t)i * kWave + lane;
+        if (idx < n) {
+          const uint32_t dd = (uint32_t)(key[sb][i] >> shift) & 255u;
+          const uint32_t pos = s_tex[dd] + s_wcnt[wave][dd] + rank[sb][i];
+          if (pos >= lo && pos < hi) s_keys[pos - lo] = key[sb][i];
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {
+      const uint32_t j = lo + (uint32_t)i * THREADS + tid;
+      if (j < valid_n) {
+        const uint64_t k = s_keys[j - lo];
+        const uint32_t dd = (uint32_t)(k >> shift) & 255u;
+        out[s_gbase[dd] + (j - s_tex[dd])] = k;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+template <int THREADS, int ITEMS, int SUB>
+void run2(const char *name, const uint64_t *in, uint64_t *out, uint64_t n, const uint64_t *dbase, uint64_t *status,
+          unsigned long long *bad, uint32_t *ticket) {
+  constexpr int TILE = THREADS * ITEMS * SUB;
+  uint64_t ntiles = (n + TILE - 1) / TILE;
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  float tot = 0;
+  const int R = 10;
+  for (int r = 0; r < R + 2; ++r) {
+    CK(hipMemsetAsync(status, 0, ntiles * BINS * 8, 0));
+    CK(hipMemsetAsync(ticket, 0, 4, 0));
+    CK(hipEventRecord(a, 0));
+    hipLaunchKernelGGL((pass2<THREADS, ITEMS, SUB>), dim3((unsigned)ntiles), dim3(THREADS), 0, 0, in, out, n, 0, dbase,
+                       status, ticket);
+    CK(hipGetLastError());
+    CK(hipEventRecord(b, 0));
+    CK(hipEventSynchronize(b));
+    float ms;
+    CK(hipEventElapsedTime(&ms, a, b));
+    if (r >= 2) tot += ms;
+  }
+  CK(hipMemset(bad, 0, 8));
+  hipLaunchKernelGGL(check, dim3(4096), dim3(256), 0, 0, out, n, bad);
+  unsigned long long hb;
+  CK(hipMemcpy(&hb, bad, 8, hipMemcpyDeviceToHost));
+  double ms = tot / R;
+  printf("%-36s %8.3f ms  %7.1f GB/s  unsorted=%llu\n", name, ms, 16.0 * n / 1e9 / (ms * 1e-3), hb);
+}
+
 int main(int argc, char **argv) {
   setvbuf(stdout, NULL, _IONBF, 0);
   uint64_t n = argc > 1 ? strtoull(argv[1], 0, 10) : 250000000ull;
@@ -285,8 +440,16 @@ int main(int argc, char **argv) {
   int idx = 0;
 #define V(...) \
   if (v == idx++) run<__VA_ARGS__>
-  V(512, 16, 0, 1)("512x16 LBW1", in, out, n, dbase, status, bad);
-  V(256, 16, 0, 1)("256x16 LBW1", in, out, n, dbase, status, bad);
-  V(512, 16, 0, 8)("512x16 LBW8", in, out, n, dbase, status, bad);
+  uint32_t *ticket;
+  CK(hipMalloc(&ticket, 64));
+#define V2(...) \
+  if (v == idx++) run2<__VA_ARGS__>
+  V2(512, 16, 1)("T 512x16 sub1", in, out, n, dbase, status, bad, ticket);
+  V2(512, 16, 2)("T 512x16 sub2", in, out, n, dbase, status, bad, ticket);
+  V2(512, 8, 2)("T 512x8 sub2", in, out, n, dbase, status, bad, ticket);
+  V2(512, 8, 4)("T 512x8 sub4", in, out, n, dbase, status, bad, ticket);
+  V2(256, 16, 2)("T 256x16 sub2", in, out, n, dbase, status, bad, ticket);
+  V2(512, 12, 2)("T 512x12 sub2", in, out, n, dbase, status, bad, ticket);
+  V2(1024, 8, 2)("T 1024x8 sub2", in, out, n, dbase, status, bad, ticket);
   return 0;
 }
