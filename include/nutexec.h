@@ -104,7 +104,10 @@ nut_status nut_gen_column(nut_ctx *ctx, int kind, uint64_t seed, int64_t a, int6
  * (src/parser/ast/query.rs:68-72, expr.rs:25-30, item.rs:89-101).
  * Output keeps row order.  `out` must hold n elements (worst case).
  * ------------------------------------------------------------------------ */
-typedef enum { NUT_LT = 0, NUT_LE = 1, NUT_GT = 2, NUT_GE = 3, NUT_EQ = 4, NUT_NE = 5 } nut_cmp;
+typedef enum {
+  NUT_LT = 0, NUT_LE = 1, NUT_GT = 2, NUT_GE = 3, NUT_EQ = 4, NUT_NE = 5,
+  NUT_IN = 6, NUT_NOT_IN = 7  /* set membership: nut_agg_spec predicates only */
+} nut_cmp;
 
 nut_status nut_filter_i64(nut_ctx *ctx, const int64_t *col, uint64_t n, int cmp, int64_t k,
                           int64_t *out, uint64_t *out_n_host);
@@ -133,6 +136,7 @@ typedef enum {
 #define NUT_MAX_PRED 6
 #define NUT_MAX_VALS 4
 #define NUT_MAX_AGGS 8
+#define NUT_MAX_SET 16
 
 typedef struct {
   uint64_t n;                          /* rows */
@@ -152,6 +156,10 @@ typedef struct {
   int32_t agg_op[NUT_MAX_AGGS];        /* nut_agg_op */
   int32_t agg_expr[NUT_MAX_AGGS];      /* nut_expr (ignored for COUNT) */
   int32_t agg_arg[NUT_MAX_AGGS][3];    /* value-column indices of the expression */
+  /* pred_op NUT_IN / NUT_NOT_IN: `col [NOT] IN (set)` with pred_nset[t] in 1..16 values
+   * (an f64 column's values as the doubles' bits) */
+  int32_t pred_nset[NUT_MAX_PRED];
+  int64_t pred_set[NUT_MAX_PRED][NUT_MAX_SET];
 } nut_agg_spec;
 
 /* Result word per aggregate: f64 bits for SUM/MIN/MAX of an f64 expression,

@@ -21,6 +21,7 @@ NUT_MAX_KEYS = 2
 NUT_MAX_PRED = 6
 NUT_MAX_VALS = 4
 NUT_MAX_AGGS = 8
+NUT_MAX_SET = 16
 
 # nut_status
 NUT_OK = 0
@@ -32,7 +33,7 @@ STATUS_NAMES = {
 
 # enums (include/nutexec.h)
 GEN_U62, GEN_FULL_I64, GEN_POOL_KEY, GEN_DYADIC, GEN_UNIT_F64, GEN_RANGE_I64, GEN_RANGE_F64 = range(7)
-LT, LE, GT, GE, EQ, NE = range(6)
+LT, LE, GT, GE, EQ, NE, IN, NOT_IN = range(8)
 T_I64, T_F64 = 0, 1
 KERNEL_FILTER, KERNEL_AGGREGATE, KERNEL_SORT = 0, 1, 2
 AGG_SUM, AGG_COUNT, AGG_MIN, AGG_MAX = range(4)
@@ -57,6 +58,8 @@ class NutAggSpec(C.Structure):
         ("agg_op", C.c_int32 * NUT_MAX_AGGS),
         ("agg_expr", C.c_int32 * NUT_MAX_AGGS),
         ("agg_arg", (C.c_int32 * 3) * NUT_MAX_AGGS),
+        ("pred_nset", C.c_int32 * NUT_MAX_PRED),
+        ("pred_set", (C.c_int64 * NUT_MAX_SET) * NUT_MAX_PRED),
     ]
 
 

@@ -234,12 +234,28 @@ __device__ __forceinline__ void consume_rows(const AggArgs &p, const LTable &lt,
 #pragma unroll
   for (int t = 0; t < S::MP; ++t) {
     if (t < S::np(p)) {
-      const uint64_t k = p.pred_k[t];
-      with_pred(S::ptype(p, t), S::pop(p, t), [&](auto OPC, auto TYC) {
-        constexpr int OP = decltype(OPC)::value, TY = decltype(TYC)::value;
+      const int op = S::pop(p, t);
+      if (op >= NUT_IN) {
+        // [NOT] IN: uniform loop over the set (scalar loads), one compare per value
+        const int ns = p.pred_nset[t];
+        const bool f64 = S::ptype(p, t) == NUT_T_F64;
+        bool in[R] = {};
+        for (int i = 0; i < ns; ++i) {
+          const uint64_t sv = p.pred_set[t][i];
 #pragma unroll
-        for (int r = 0; r < R; ++r) ok[r] = ok[r] && pred1<OP, TY>(x.pv[t][r], k);
-      });
+          for (int r = 0; r < R; ++r)
+            in[r] = in[r] || (f64 ? as_f64(x.pv[t][r]) == as_f64(sv) : x.pv[t][r] == sv);
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) ok[r] = ok[r] && (in[r] == (op == NUT_IN));
+      } else {
+        const uint64_t k = p.pred_k[t];
+        with_pred(S::ptype(p, t), op, [&](auto OPC, auto TYC) {
+          constexpr int OP = decltype(OPC)::value, TY = decltype(TYC)::value;
+#pragma unroll
+          for (int r = 0; r < R; ++r) ok[r] = ok[r] && pred1<OP, TY>(x.pv[t][r], k);
+        });
+      }
     }
   }
   // GROUP BY: home-bucket lookup of all four rows (four ds_read_b128 in flight), then

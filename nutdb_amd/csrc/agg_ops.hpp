@@ -42,6 +42,8 @@ struct AggArgs {
   int32_t priv;                   // private groups per thread (PRIV kernels)
   int32_t vec;                    // all columns 16-B aligned: vector loads
   int32_t nokey;                  // global aggregate: no key column, every key is 0
+  int32_t pred_nset[NUT_MAX_PRED];                 // NUT_IN / NUT_NOT_IN set sizes
+  uint64_t pred_set[NUT_MAX_PRED][NUT_MAX_SET];    // set values (bits)
   const GTable *gt;               // device copy of the global table descriptor
 };
 

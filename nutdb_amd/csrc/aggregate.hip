@@ -49,7 +49,9 @@ nut_status validate(const nut_agg_spec *s) {
       if (!s->keys[k]) return fail(NUT_ERR_INVALID_ARG, "nut_groupby: NULL key column");
     for (int t = 0; t < s->npred; ++t) {
       if (!s->pred_col[t]) return fail(NUT_ERR_INVALID_ARG, "nut_groupby: NULL predicate column");
-      if (s->pred_op[t] < NUT_LT || s->pred_op[t] > NUT_NE) return fail(NUT_ERR_INVALID_ARG, "nut_groupby: bad cmp op");
+      if (s->pred_op[t] < NUT_LT || s->pred_op[t] > NUT_NOT_IN) return fail(NUT_ERR_INVALID_ARG, "nut_groupby: bad cmp op");
+      if (s->pred_op[t] >= NUT_IN && (s->pred_nset[t] < 1 || s->pred_nset[t] > NUT_MAX_SET))
+        return fail(NUT_ERR_INVALID_ARG, "nut_groupby: IN sets hold 1..16 values");
       if (s->pred_type[t] != NUT_T_I64 && s->pred_type[t] != NUT_T_F64)
         return fail(NUT_ERR_INVALID_ARG, "nut_groupby: bad predicate type");
     }
@@ -224,6 +226,10 @@ nut_status launch_agg(nut_groups *g, const nut_agg_spec *s, uint64_t group_hint,
     a.pred_op[t] = s->pred_op[t];
     if (s->pred_type[t] == NUT_T_I64) a.pred_k[t] = (uint64_t)s->pred_i64[t];
     else memcpy(&a.pred_k[t], &s->pred_f64[t], 8);
+    if (s->pred_op[t] >= NUT_IN) {
+      a.pred_nset[t] = s->pred_nset[t];
+      for (int i = 0; i < s->pred_nset[t]; ++i) a.pred_set[t][i] = (uint64_t)s->pred_set[t][i];
+    }
   }
   a.nvals = s->nvals;
   for (int v = 0; v < s->nvals; ++v) a.val_col[v] = (const uint64_t *)s->val_col[v];

@@ -233,7 +233,7 @@ i128 dec_floor(const Decimal &d, bool &frac) {
 }
 
 // ------------------------------------------------------------------ plan
-const char *kCmpText[] = {"<", "<=", ">", ">=", "=", "!="};
+const char *kCmpText[] = {"<", "<=", ">", ">=", "=", "!=", "in", "not in"};
 int cmp_of(BinOp op) {
   switch (op) {
     case BinOp::Lt: return NUT_LT;
@@ -250,6 +250,7 @@ int mirror(int op) { return op == NUT_LT ? NUT_GT : op == NUT_GT ? NUT_LT : op =
 struct PlanPred {
   int col, op;
   CVal c;
+  std::vector<CVal> set;  // NUT_IN / NUT_NOT_IN
 };
 struct PlanAgg {
   int op, expr;
@@ -449,6 +450,25 @@ bool lower_pred_term(nut_plan &p, const Expr &e, Lowering &L) {
       p.preds.push_back({col_index(p, name), mirror(op), c});
       return true;
     }
+  }
+  if (e.k == EK::BinaryOp && (e.bop() == BinOp::In || e.bop() == BinOp::NotIn) && column_ref(e.kids[0], name)) {
+    // col [NOT] IN (c1, c2, ...): a tuple of constants, or one constant
+    const Expr &r = e.kids[1];
+    PlanPred pr{col_index(p, name), e.bop() == BinOp::In ? NUT_IN : NUT_NOT_IN, CVal{}, {}};
+    if (r.k == EK::Collection && (CollType)r.op == CollType::Tuple) {
+      for (const Expr &x : r.kids) {
+        CVal v;
+        if (!const_eval(x, v, L)) return L.fail("IN list item '" + expr_text(x) + "' is not a constant");
+        pr.set.push_back(v);
+      }
+    } else {
+      CVal v;
+      if (!const_eval(r, v, L)) return L.fail("IN needs a list of constants (subqueries are not executed)");
+      pr.set.push_back(v);
+    }
+    if (pr.set.size() > NUT_MAX_SET) return L.fail("IN lists hold at most 16 values");
+    p.preds.push_back(std::move(pr));
+    return true;
   }
   if (e.k == EK::FnCall && e.fn() == FnKind::Between && e.kids.size() == 3 && column_ref(e.kids[0], name)) {
     CVal lo, hi;
@@ -715,7 +735,13 @@ std::string describe(const nut_plan &p) {
     json_str(o, p.cols[pr.col]);
     o += ",\"op\":\"";
     o += kCmpText[pr.op];
-    o += "\",\"value\":\"" + cval_str(pr.c) + "\",\"value_kind\":\"" + (pr.c.is_int ? "int" : "decimal") + "\"}";
+    if (pr.op >= NUT_IN) {
+      o += "\",\"values\":[";
+      for (size_t j = 0; j < pr.set.size(); ++j) o += (j ? ",\"" : "\"") + cval_str(pr.set[j]) + "\"";
+      o += "]}";
+    } else {
+      o += "\",\"value\":\"" + cval_str(pr.c) + "\",\"value_kind\":\"" + (pr.c.is_int ? "int" : "decimal") + "\"}";
+    }
   }
   o += "]";
   if (p.kind == NUT_PLAN_GROUPBY) {
@@ -851,6 +877,8 @@ nut_status exec_scan(nut_ctx *c, const nut_plan &p, const nut_column *const *bou
   int op = NUT_GE;
   int64_t k = INT64_MIN;  // no predicate: every row passes
   bool none = p.never || n == 0;
+  if (!p.preds.empty() && p.preds[0].op >= NUT_IN)
+    return fail(NUT_ERR_PLAN, "IN is executed in aggregate plans only (the scan kernel takes one comparison)");
   if (!none && !p.preds.empty()) {
     Verdict v = resolve_i64(p.preds[0].op, p.preds[0].c, op, k);
     if (v == V_FALSE) none = true;
@@ -949,6 +977,34 @@ nut_status exec_groupby(nut_ctx *c, const nut_plan &p, const nut_column *const *
   }
   for (const PlanPred &pr : p.preds) {
     const nut_column *col = bound[pr.col];
+    if (pr.op >= NUT_IN) {
+      // keep the set values the column type can hold (a non-integral or out-of-range
+      // constant never equals an int64)
+      std::vector<int64_t> vals;
+      for (const CVal &v : pr.set) {
+        if (col->type == NUT_T_I64) {
+          int o2;
+          int64_t k;
+          if (resolve_i64(NUT_EQ, v, o2, k) == V_PRED) vals.push_back(k);
+        } else {
+          double d = resolve_f64(v);
+          int64_t bits;
+          memcpy(&bits, &d, 8);
+          vals.push_back(bits);
+        }
+      }
+      if (vals.empty()) {
+        if (pr.op == NUT_IN) s.n = 0;  // IN () is false; NOT IN () is true
+        continue;
+      }
+      s.pred_col[s.npred] = col->data;
+      s.pred_type[s.npred] = col->type;
+      s.pred_op[s.npred] = pr.op;
+      s.pred_nset[s.npred] = (int32_t)vals.size();
+      for (size_t j = 0; j < vals.size(); ++j) s.pred_set[s.npred][j] = vals[j];
+      s.npred++;
+      continue;
+    }
     if (col->type == NUT_T_I64) {
       int op;
       int64_t k;

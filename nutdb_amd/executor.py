@@ -20,7 +20,8 @@ import torch
 from . import _lib as L
 from ._lib import check, lib
 
-CMP = {"<": L.LT, "<=": L.LE, ">": L.GT, ">=": L.GE, "=": L.EQ, "==": L.EQ, "!=": L.NE, "<>": L.NE}
+CMP = {"<": L.LT, "<=": L.LE, ">": L.GT, ">=": L.GE, "=": L.EQ, "==": L.EQ, "!=": L.NE, "<>": L.NE,
+       "in": L.IN, "not in": L.NOT_IN}
 AGG = {"sum": L.AGG_SUM, "count": L.AGG_COUNT, "min": L.AGG_MIN, "max": L.AGG_MAX}
 EXPR = {"col": L.EX_COL, "mul": L.EX_MUL, "add": L.EX_ADD, "sub": L.EX_SUB,
         "mul_1m": L.EX_MUL_1M, "mul_1m_1p": L.EX_MUL_1M_1P}
@@ -82,7 +83,17 @@ class AggQuery:
             s.pred_col[i] = _col(col, dev)
             s.pred_type[i] = _dtype_code(col)
             s.pred_op[i] = CMP[op] if isinstance(op, str) else int(op)
-            if s.pred_type[i] == L.T_I64:
+            if s.pred_op[i] in (L.IN, L.NOT_IN):  # lit: a sequence of 1..16 values
+                vals = list(lit)
+                if not 1 <= len(vals) <= L.NUT_MAX_SET:
+                    raise ValueError("IN sets hold 1..16 values")
+                s.pred_nset[i] = len(vals)
+                for j, v in enumerate(vals):
+                    if s.pred_type[i] == L.T_I64:
+                        s.pred_set[i][j] = int(v)
+                    else:
+                        s.pred_set[i][j] = int(np.array([float(v)], dtype=np.float64).view(np.int64)[0])
+            elif s.pred_type[i] == L.T_I64:
                 s.pred_i64[i] = int(lit)
             else:
                 s.pred_f64[i] = float(lit)

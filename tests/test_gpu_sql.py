@@ -191,3 +191,27 @@ def test_sql_having_and_order_by_aggregate(ex, orc):
     assert list(got) == ["k", "s"]
     assert np.array_equal(got["k"], uk[keep][order])
     assert np.array_equal(got["s"], sums[keep][order])
+
+
+def test_sql_in_lists(ex):
+    rng = np.random.default_rng(5)
+    n = 900_001
+    k = rng.integers(-20, 20, n).astype(np.int64)
+    f = (rng.integers(0, 8, n) / 4.0).astype(np.float64)
+    v = rng.integers(0, 1 << 20, n) / 64.0
+    t = {"k": dev(k, ex), "f": dev(f, ex), "v": dev(v, ex)}
+    got = ex.sql("select k, sum(v), count(*) from t where k in (-3, 0, 7, 2.5, 99999999999999999999) "
+                 "and f not in (0.25, 1.5) group by k", t)
+    m = np.isin(k, [-3, 0, 7]) & ~np.isin(f, [0.25, 1.5])
+    uk = np.unique(k[m])
+    assert got["k"].tolist() == uk.tolist()
+    assert got["count(*)"].tolist() == [int((k[m] == x).sum()) for x in uk]
+    assert got["sum(v)"].tolist() == [float(v[m][k[m] == x].sum()) for x in uk]
+    # an IN list nothing in the column can equal
+    assert ex.sql("select count(*) from t where k in (0.5, 1.5)", t)["count(*)"].tolist() == [0]
+    assert ex.sql("select count(*) from t where k not in (0.5)", t)["count(*)"].tolist() == [n]
+    # the AggQuery path
+    from nutdb_amd import Agg, AggQuery
+    g = ex.groupby(AggQuery(keys=[t["k"]], aggs=[Agg("count")], preds=[(t["k"], "in", [1, 2, 3])]))
+    keys, words = g.to_host_words()
+    assert keys[:, 0].tolist() == [1, 2, 3] and words[:, 0].tolist() == [int((k == x).sum()) for x in (1, 2, 3)]

@@ -441,6 +441,18 @@ def test_plan_filter_sort_shapes():
     assert [a["op"] for a in d["aggs"]] == ["sum", "count", "min", "max"]
 
 
+def test_plan_in_lists():
+    d = Plan("select k, count(*) from t where k in (1, -2, 3.5) and v not in (0.5) group by k").describe()
+    assert d["where"] == [{"col": "k", "op": "in", "values": ["1", "-2", "3.5"]},
+                          {"col": "v", "op": "not in", "values": ["0.5"]}]
+    with pytest.raises(NutError) as e:
+        Plan("select count(*) from t where k in (select 1)")
+    assert "constants" in str(e.value)
+    with pytest.raises(NutError) as e:
+        Plan("select count(*) from t where k in (" + ", ".join(map(str, range(17))) + ")")
+    assert "16 values" in str(e.value)
+
+
 def test_plan_having_and_hidden_order_keys():
     d = Plan("select k, sum(v) as s from t group by k having count(*) > 10 and s < 5.5 "
              "order by max(v) desc").describe()
