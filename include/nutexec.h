@@ -30,8 +30,10 @@
 #ifndef NUTEXEC_H
 #define NUTEXEC_H
 
+#ifndef __HIPCC_RTC__ /* the runtime-compiled scan kernels bring their own */
 #include <stddef.h>
 #include <stdint.h>
+#endif
 
 #ifdef __cplusplus
 extern "C" {
@@ -137,6 +139,45 @@ typedef enum {
 #define NUT_MAX_VALS 4
 #define NUT_MAX_AGGS 8
 #define NUT_MAX_SET 16
+#define NUT_MAX_PROG_COLS 16
+#define NUT_MAX_PROG_NODES 256
+
+/* Expression programs: postfix (RPN) node arrays.  Every node pops its operands and
+ * pushes one value of type int64, float64 or bool (nut_prog_type gives the result).
+ *   COL      push prog_col[arg]
+ *   I64/F64  push the constant v (F64: the double's bits)
+ *   arithmetic  i64 (+ - *) wraps; any f64 operand makes the op f64; DIV is always
+ *            f64 (int operands converted); MOD/INTDIV on ints truncate toward zero and
+ *            fail the query on a zero divisor (INT64_MIN % -1 = 0, INT64_MIN div -1
+ *            wraps); MOD on f64 is fmod
+ *   compare  bool; an int compared with an f64 converts the int to f64
+ *   AND OR XOR NOT  bool operands (ints: non-zero = true), no short circuit
+ *   BITAND BITOR BITXOR BITNOT SHL SHR  ints; shift counts outside [0, 63] give 0
+ *            (SHR of a negative value: -1); SHR is arithmetic
+ *   IF       pops cond, then, else: the chosen branch (only its errors count)
+ *   ABS, TO_F64  one operand; bool operands count as int 0/1 in arithmetic */
+typedef enum {
+  NUT_P_COL = 0, NUT_P_I64 = 1, NUT_P_F64 = 2,
+  NUT_P_ADD = 3, NUT_P_SUB = 4, NUT_P_MUL = 5, NUT_P_DIV = 6, NUT_P_MOD = 7, NUT_P_INTDIV = 8,
+  NUT_P_LT = 9, NUT_P_LE = 10, NUT_P_GT = 11, NUT_P_GE = 12, NUT_P_EQ = 13, NUT_P_NE = 14,
+  NUT_P_AND = 15, NUT_P_OR = 16, NUT_P_XOR = 17, NUT_P_NOT = 18,
+  NUT_P_BITAND = 19, NUT_P_BITOR = 20, NUT_P_BITXOR = 21, NUT_P_BITNOT = 22,
+  NUT_P_SHL = 23, NUT_P_SHR = 24,
+  NUT_P_IF = 25, NUT_P_ABS = 26, NUT_P_TO_F64 = 27
+} nut_prog_op;
+typedef enum { NUT_PT_I64 = 0, NUT_PT_F64 = 1, NUT_PT_BOOL = 2 } nut_prog_value_type;
+typedef struct {
+  int32_t op;   /* nut_prog_op */
+  int32_t arg;  /* NUT_P_COL: column index */
+  int64_t v;    /* NUT_P_I64 / NUT_P_F64 constant */
+} nut_prog_node;
+typedef struct {
+  int32_t n;                  /* 0..NUT_MAX_PROG_NODES */
+  const nut_prog_node *node;  /* host memory */
+} nut_prog;
+/* Type-check a program against column types; *type = nut_prog_value_type of the
+ * result.  NUT_ERR_INVALID_ARG (message in nut_last_error) if it is malformed. */
+nut_status nut_prog_type(const nut_prog *prog, const int32_t *col_types, int ncols, int32_t *type);
 
 typedef struct {
   uint64_t n;                          /* rows */
@@ -160,11 +201,28 @@ typedef struct {
    * (an f64 column's values as the doubles' bits) */
   int32_t pred_nset[NUT_MAX_PRED];
   int64_t pred_set[NUT_MAX_PRED][NUT_MAX_SET];
+  /* Expression mode (prog_mode = 1): WHERE and every aggregate
+   * argument are expression programs over prog_col[], compiled at run time into the
+   * same streaming kernel.  pred_*, val_* and agg_expr/agg_arg must then be unused
+   * (npred = nvals = 0).  Types follow nut_prog_type. */
+  int32_t prog_mode;
+  int32_t nprog_cols;
+  const void *prog_col[NUT_MAX_PROG_COLS];
+  int32_t prog_col_type[NUT_MAX_PROG_COLS]; /* nut_type */
+  nut_prog where;                           /* n = 0: every row */
+  nut_prog agg_val[NUT_MAX_AGGS];           /* argument of each non-COUNT aggregate */
+  nut_prog agg_mask[NUT_MAX_AGGS];          /* n = 0: every row; else the aggregate takes
+                                               only rows where it is true (SQL NULL
+                                               arguments of CASE without ELSE) */
 } nut_agg_spec;
 
 /* Result word per aggregate: f64 bits for SUM/MIN/MAX of an f64 expression,
  * int64 for COUNT and for SUM/MIN/MAX of an int64 column (SUM wraps).
- * MIN/MAX order f64 by the IEEE total order (-0 < +0).
+ * MIN/MAX order f64 by the IEEE total order (-0 < +0).  Expression mode: f64 bits
+ * when the program's type is f64, else int64 (bool = 0/1); an aggregate whose mask
+ * took no row of a group holds its identity (SUM/COUNT 0, MIN/MAX the type's
+ * largest/smallest value; f64: 0x7FFF... / 0xFFFF..., the NaN patterns at the
+ * two ends of the IEEE total order).
  *
  * group_hint: expected number of groups (0 = unknown).  It sizes the on-chip
  * table; a wrong hint costs speed, never correctness. */
@@ -174,6 +232,13 @@ nut_status nut_groupby(nut_ctx *ctx, const nut_agg_spec *spec, uint64_t group_hi
  * the partial groups received from other ranks (NUT_AGG_COUNT partials are merged
  * with NUT_AGG_SUM over an int64 column). */
 nut_status nut_groupby_accumulate(nut_ctx *ctx, const nut_agg_spec *spec, nut_groups *acc);
+
+/* Expression mode: the HIP source of the query-specific kernel shape (generated from
+ * the programs; constants travel as kernel arguments, so queries that differ only in
+ * constants share one compiled kernel), and a compile-only check of it (hipRTC,
+ * gfx950; no device needed).  The compile log of a failure is in nut_last_error. */
+nut_status nut_groupby_jit_source(const nut_agg_spec *spec, char *buf, size_t cap, size_t *len);
+nut_status nut_groupby_jit_compile(const nut_agg_spec *spec);
 
 nut_status nut_groups_size(nut_groups *g, uint64_t *n_groups);
 /* Copy to host sorted ascending by key tuple.  keys[g*nkeys+j], aggs[g*naggs+a].
@@ -292,6 +357,10 @@ int nut_plan_kind_of(const nut_plan *plan);
 nut_status nut_plan_describe(const nut_plan *plan, char *buf, size_t cap, size_t *len);
 void nut_plan_free(nut_plan *plan);
 
+/* Compile an expression-mode plan's kernel now (hipRTC; no device needed) so the first
+ * nut_plan_execute does not pay for it.  Columns bind by name like execute; only their
+ * types matter (data may be NULL).  A no-op for plans on the precompiled kernels. */
+nut_status nut_plan_prepare(const nut_plan *plan, const nut_column *cols, int ncols);
 /* Execute on nrows rows of the bound columns (every column the plan names must be
  * bound).  group_hint as for nut_groupby.  Synchronous. */
 nut_status nut_plan_execute(nut_ctx *ctx, const nut_plan *plan, const nut_column *cols, int ncols,

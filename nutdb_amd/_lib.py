@@ -22,6 +22,8 @@ NUT_MAX_PRED = 6
 NUT_MAX_VALS = 4
 NUT_MAX_AGGS = 8
 NUT_MAX_SET = 16
+NUT_MAX_PROG_COLS = 16
+NUT_MAX_PROG_NODES = 256
 
 # nut_status
 NUT_OK = 0
@@ -38,6 +40,19 @@ T_I64, T_F64 = 0, 1
 KERNEL_FILTER, KERNEL_AGGREGATE, KERNEL_SORT = 0, 1, 2
 AGG_SUM, AGG_COUNT, AGG_MIN, AGG_MAX = range(4)
 EX_COL, EX_MUL, EX_ADD, EX_SUB, EX_MUL_1M, EX_MUL_1M_1P = range(6)
+# nut_prog_op (expression programs, RPN) and nut_prog_value_type
+PROG_OPS = ["col", "i64", "f64", "add", "sub", "mul", "div", "mod", "intdiv", "lt", "le", "gt", "ge", "eq", "ne",
+            "and", "or", "xor", "not", "bitand", "bitor", "bitxor", "bitnot", "shl", "shr", "if", "abs", "to_f64"]
+P = {name: i for i, name in enumerate(PROG_OPS)}
+PT_I64, PT_F64, PT_BOOL = 0, 1, 2
+
+
+class NutProgNode(C.Structure):
+    _fields_ = [("op", C.c_int32), ("arg", C.c_int32), ("v", C.c_int64)]
+
+
+class NutProg(C.Structure):
+    _fields_ = [("n", C.c_int32), ("node", C.POINTER(NutProgNode))]
 
 
 class NutAggSpec(C.Structure):
@@ -60,6 +75,13 @@ class NutAggSpec(C.Structure):
         ("agg_arg", (C.c_int32 * 3) * NUT_MAX_AGGS),
         ("pred_nset", C.c_int32 * NUT_MAX_PRED),
         ("pred_set", (C.c_int64 * NUT_MAX_SET) * NUT_MAX_PRED),
+        ("prog_mode", C.c_int32),
+        ("nprog_cols", C.c_int32),
+        ("prog_col", C.c_void_p * NUT_MAX_PROG_COLS),
+        ("prog_col_type", C.c_int32 * NUT_MAX_PROG_COLS),
+        ("where", NutProg),
+        ("agg_val", NutProg * NUT_MAX_AGGS),
+        ("agg_mask", NutProg * NUT_MAX_AGGS),
     ]
 
 
@@ -107,6 +129,10 @@ SIGNATURES = {
     "nut_filter_i64_async": (_I32, [_P, _P, _U64, _I32, _I64, _P, _P]),
     "nut_groupby": (_I32, [_P, C.POINTER(NutAggSpec), _U64, C.POINTER(_P)]),
     "nut_groupby_accumulate": (_I32, [_P, C.POINTER(NutAggSpec), _P]),
+    "nut_prog_type": (_I32, [C.POINTER(NutProg), C.POINTER(C.c_int32), _I32, C.POINTER(C.c_int32)]),
+    "nut_groupby_jit_source": (_I32, [C.POINTER(NutAggSpec), C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
+    "nut_groupby_jit_compile": (_I32, [C.POINTER(NutAggSpec)]),
+    "nut_plan_prepare": (_I32, [_P, C.POINTER(NutColumn), _I32]),
     "nut_groups_size": (_I32, [_P, C.POINTER(_U64)]),
     "nut_groups_to_host": (_I32, [_P, _P, _P, _U64]),
     "nut_groups_to_device": (_I32, [_P, _P, _U64]),

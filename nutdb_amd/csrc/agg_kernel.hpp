@@ -224,12 +224,22 @@ __device__ __forceinline__ void load_rows(const AggArgs &p, uint64_t i0, uint64_
 // ------------------------------------------------------------------ fold four rows
 template <int NK, bool PRIV, int BD, class S, bool TAIL>
 __device__ __forceinline__ void consume_rows(const AggArgs &p, const LTable &lt, uint64_t i0, uint64_t i1,
-                                             const Rows<S> &x) {
+                                             const Rows<S> &x, bool &err) {
   constexpr int R = 4;
   constexpr bool LOCKED = NK == 2 || PRIV;
   bool ok[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) ok[r] = !TAIL || ((r < 2 ? i0 : i1) + (r & 1)) < p.n;
+  if constexpr (S::kProg) {
+    // generated WHERE program (padding rows of the tail never raise)
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      bool e = false;
+      const bool w = S::where(p, x.vv, r, e);
+      err = err || (e && ok[r]);
+      ok[r] = ok[r] && w;
+    }
+  }
   // WHERE: one decision per term per four rows
 #pragma unroll
   for (int t = 0; t < S::MP; ++t) {
@@ -319,11 +329,21 @@ __device__ __forceinline__ void consume_rows(const AggArgs &p, const LTable &lt,
 
   // aggregate inputs
   uint64_t av[S::MA][R];
+  bool vm[S::MA][R];  // row mask per aggregate (expression shapes; constant true otherwise)
 #pragma unroll
   for (int a = 0; a < S::MA; ++a) {
 #pragma unroll
-    for (int r = 0; r < R; ++r) av[a][r] = 0;
-    if (a < S::na(p) && S::kind(p, a) != AK_COUNT) {
+    for (int r = 0; r < R; ++r) av[a][r] = 0, vm[a][r] = true;
+    if constexpr (S::kProg) {
+      // errors count only for rows the aggregate actually takes
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        bool em = false, ev = false;
+        vm[a][r] = S::valid(p, a, x.vv, r, em);
+        if (S::kind(p, a) != AK_COUNT) av[a][r] = S::value(p, a, x.vv, r, ev);
+        err = err || (ok[r] && (em || (vm[a][r] && ev)));
+      }
+    } else if (a < S::na(p) && S::kind(p, a) != AK_COUNT) {
       const int a0 = S::arg(p, a, 0), a1 = S::arg(p, a, 1), a2 = S::arg(p, a, 2);
       with_expr(S::expr(p, a), [&](auto EC) {
         constexpr int E = decltype(EC)::value;
@@ -349,7 +369,7 @@ __device__ __forceinline__ void consume_rows(const AggArgs &p, const LTable &lt,
         constexpr int K = decltype(KC)::value;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-          if (sl[r] >= 0) {
+          if (sl[r] >= 0 && vm[a][r]) {
             if (PRIV && dd[r] != kNoDense) {
               uint64_t *pw = &lt.priv[((size_t)dd[r] * S::na(p) + a) * BD + threadIdx.x];
               *pw = fold<K>(*pw, av[a][r]);
@@ -366,9 +386,10 @@ __device__ __forceinline__ void consume_rows(const AggArgs &p, const LTable &lt,
   for (int r = 0; r < R; ++r) {
     if (sl[r] == -1) {
       uint64_t g[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      uint32_t m = 0;
 #pragma unroll
-      for (int a = 0; a < S::MA && a < 8; ++a) g[a] = av[a][r];
-      g_row<NK>(p.gt, (int64_t)x.k1[r], (int64_t)x.k2[r], g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7]);
+      for (int a = 0; a < S::MA && a < 8; ++a) g[a] = av[a][r], m |= vm[a][r] ? 1u << a : 0u;
+      g_row<NK>(p.gt, (int64_t)x.k1[r], (int64_t)x.k2[r], m, g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7]);
     }
   }
 }
@@ -419,6 +440,7 @@ __global__ __launch_bounds__(BD) void agg_kernel(AggArgs p) {
   const uint64_t full_pairs = p.n / 2;
   const uint64_t gstride = (uint64_t)gridDim.x * BD;
   uint64_t q = (uint64_t)blockIdx.x * BD + threadIdx.x;
+  bool err = false;  // an expression raised (integer division by zero)
   if (q + gstride < full_pairs) {
     Rows<S> cur;
     load_rows<NK, S, VEC, false>(p, 2 * q, 2 * (q + gstride), cur);
@@ -427,7 +449,7 @@ __global__ __launch_bounds__(BD) void agg_kernel(AggArgs p) {
       const bool more = qn + gstride < full_pairs;
       Rows<S> nxt;
       if (more) load_rows<NK, S, VEC, false>(p, 2 * qn, 2 * (qn + gstride), nxt);
-      consume_rows<NK, PRIV, BD, S, false>(p, lt, 2 * q, 2 * (q + gstride), cur);
+      consume_rows<NK, PRIV, BD, S, false>(p, lt, 2 * q, 2 * (q + gstride), cur, err);
       q = qn;
       if (!more) break;
       cur = nxt;
@@ -438,9 +460,12 @@ __global__ __launch_bounds__(BD) void agg_kernel(AggArgs p) {
     Rows<S> x;
     load_rows<NK, S, VEC, true>(p, 2 * q, 2 * q1, x);
     // a duplicate second pair (q1 == q) is masked out by placing it past the end
-    consume_rows<NK, PRIV, BD, S, true>(p, lt, 2 * q, q1 == q ? p.n : 2 * q1, x);
+    consume_rows<NK, PRIV, BD, S, true>(p, lt, 2 * q, q1 == q ? p.n : 2 * q1, x, err);
   }
 
+  if constexpr (S::kProg) {
+    if (err) atomicOr(&p.gt->ctl[1], 2u);  // flag 2: division by zero (query fails)
+  }
   if (!cap) return;
   __syncthreads();
   if (PRIV) {

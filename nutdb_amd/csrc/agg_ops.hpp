@@ -23,6 +23,8 @@
 namespace nut {
 
 constexpr int kPrivMax = 8;  // private groups per thread (upper bound)
+constexpr int kMaxCols = NUT_MAX_PROG_COLS;  // value columns a kernel can load
+constexpr int kMaxConst = 64;                // expression constants (kernel arguments)
 
 struct AggArgs {
   uint64_t n;
@@ -31,7 +33,7 @@ struct AggArgs {
   uint64_t pred_k[NUT_MAX_PRED];  // constant bits
   int32_t pred_type[NUT_MAX_PRED];
   int32_t pred_op[NUT_MAX_PRED];
-  const uint64_t *val_col[NUT_MAX_VALS];
+  const uint64_t *val_col[kMaxCols];  // expression shapes load every program column here
   int32_t npred, nvals, naggs;
   uint32_t kinds;                 // 4 bits per aggregate kind
   int32_t expr[NUT_MAX_AGGS];
@@ -44,12 +46,29 @@ struct AggArgs {
   int32_t nokey;                  // global aggregate: no key column, every key is 0
   int32_t pred_nset[NUT_MAX_PRED];                 // NUT_IN / NUT_NOT_IN set sizes
   uint64_t pred_set[NUT_MAX_PRED][NUT_MAX_SET];    // set values (bits)
+  uint64_t kc[kMaxConst];         // expression constants (bits), read by generated shapes
   const GTable *gt;               // device copy of the global table descriptor
 };
 
 // ------------------------------------------------------------------ query shapes
 // A shape answers what the kernel would otherwise read from AggArgs at run time.
-struct Generic {
+//
+// kProg shapes (generated per query and compiled at run time, jit.cpp) also provide
+//   where(p, v, r, err)     -> bool       the WHERE program of row r
+//   value(p, a, v, r, err)  -> u64 bits   aggregate a's argument
+//   valid(p, a, v, r, err)  -> bool       aggregate a's row mask
+// over v = the loaded columns; err is set by a failing integer division.
+struct NoProg {
+  static constexpr bool kProg = false;
+  template <class V>
+  __device__ static bool where(const AggArgs &, const V &, int, bool &) { return true; }
+  template <class V>
+  __device__ static uint64_t value(const AggArgs &, int, const V &, int, bool &) { return 0; }
+  template <class V>
+  __device__ static bool valid(const AggArgs &, int, const V &, int, bool &) { return true; }
+};
+
+struct Generic : NoProg {
   static constexpr int MP = NUT_MAX_PRED, MV = NUT_MAX_VALS, MA = NUT_MAX_AGGS;
   __device__ static int np(const AggArgs &p) { return p.npred; }
   __device__ static int nv(const AggArgs &p) { return p.nvals; }
@@ -64,7 +83,7 @@ struct Generic {
 // packed: KINDS/EXPRS 4 bits per aggregate, ARGS 6 bits (3 x 2) per aggregate,
 // PREDS 4 bits per predicate term (type << 3 | op)
 template <int NP, int NV, int NA, uint32_t KINDS, uint32_t EXPRS, uint64_t ARGS, uint32_t PREDS>
-struct Fixed {
+struct Fixed : NoProg {
   static constexpr int MP = NP, MV = NV, MA = NA;
   static constexpr uint32_t kKinds = KINDS, kExprs = EXPRS, kPreds = PREDS;
   static constexpr uint64_t kArgs = ARGS;
@@ -220,9 +239,9 @@ __device__ __forceinline__ void with_expr(int e, F &&f) {
 // ------------------------------------------------------------------ global fall-back
 // rows whose key the block table did not admit (rare; out of line keeps the loop small)
 template <int NK>
-__device__ __noinline__ void g_row(const GTable *__restrict__ gtp, int64_t k1, int64_t k2, uint64_t a0,
-                                   uint64_t a1, uint64_t a2, uint64_t a3, uint64_t a4, uint64_t a5, uint64_t a6,
-                                   uint64_t a7) {
+__device__ __noinline__ void g_row(const GTable *__restrict__ gtp, int64_t k1, int64_t k2, uint32_t amask,
+                                   uint64_t a0, uint64_t a1, uint64_t a2, uint64_t a3, uint64_t a4, uint64_t a5,
+                                   uint64_t a6, uint64_t a7) {
   const GTable t = *gtp;
   int64_t gs = g_find<NK>(t, key_hash<NK>(k1, k2), k1, k2);
   if (gs < 0) return;
@@ -230,7 +249,7 @@ __device__ __noinline__ void g_row(const GTable *__restrict__ gtp, int64_t k1, i
   const uint64_t av[8] = {a0, a1, a2, a3, a4, a5, a6, a7};
 #pragma unroll
   for (int a = 0; a < NUT_MAX_AGGS; ++a)
-    if (a < t.naggs) agg_update(&t.agg[a * stride + gs], kind_at(t.kinds, a), av[a]);
+    if (a < t.naggs && ((amask >> a) & 1u)) agg_update(&t.agg[a * stride + gs], kind_at(t.kinds, a), av[a]);
 }
 
 

@@ -8,6 +8,7 @@
 #include <vector>
 
 #include "agg_kernel.hpp"
+#include "jit.hpp"
 
 // ============================================================== host side
 using namespace nut;
@@ -58,6 +59,31 @@ nut_status validate(const nut_agg_spec *s) {
     for (int c = 0; c < s->nvals; ++c)
       if (!s->val_col[c]) return fail(NUT_ERR_INVALID_ARG, "nut_groupby: NULL value column");
   }
+  if (s->prog_mode) {
+    if (s->npred || s->nvals) return fail(NUT_ERR_INVALID_ARG, "nut_groupby: expression mode takes no pred_*/val_* terms");
+    if (s->nprog_cols < 0 || s->nprog_cols > NUT_MAX_PROG_COLS)
+      return fail(NUT_ERR_UNSUPPORTED, "nut_groupby: expression programs read at most 16 columns");
+    for (int c = 0; c < s->nprog_cols; ++c) {
+      if (s->n && !s->prog_col[c]) return fail(NUT_ERR_INVALID_ARG, "nut_groupby: NULL program column");
+      if (s->prog_col_type[c] != NUT_T_I64 && s->prog_col_type[c] != NUT_T_F64)
+        return fail(NUT_ERR_INVALID_ARG, "nut_groupby: bad program column type");
+    }
+    int32_t t;
+    for (int a = 0; a < s->naggs; ++a) {
+      int op = s->agg_op[a];
+      if (op < NUT_AGG_SUM || op > NUT_AGG_MAX) return fail(NUT_ERR_INVALID_ARG, "nut_groupby: bad aggregate op");
+      if (op != NUT_AGG_COUNT) {
+        nut_status st = prog_check(&s->agg_val[a], s->prog_col_type, s->nprog_cols, &t);
+        if (st) return st;
+      }
+      if (s->agg_mask[a].n) {
+        nut_status st = prog_check(&s->agg_mask[a], s->prog_col_type, s->nprog_cols, &t);
+        if (st) return st;
+      }
+    }
+    if (s->where.n) return prog_check(&s->where, s->prog_col_type, s->nprog_cols, &t);
+    return NUT_OK;
+  }
   for (int a = 0; a < s->naggs; ++a) {
     int op = s->agg_op[a];
     if (op < NUT_AGG_SUM || op > NUT_AGG_MAX) return fail(NUT_ERR_INVALID_ARG, "nut_groupby: bad aggregate op");
@@ -79,6 +105,11 @@ int32_t kind_of(const nut_agg_spec *s, int a) {
   int op = s->agg_op[a];
   if (op == NUT_AGG_COUNT) return AK_COUNT;
   bool i64 = s->agg_expr[a] == NUT_EX_COL && s->val_type[s->agg_arg[a][0]] == NUT_T_I64;
+  if (s->prog_mode) {  // validated: the program type-checks
+    int32_t t = NUT_PT_F64;
+    (void)prog_check(&s->agg_val[a], s->prog_col_type, s->nprog_cols, &t);
+    i64 = t != NUT_PT_F64;
+  }
   switch (op) {
     case NUT_AGG_SUM: return i64 ? AK_SUM_I64 : AK_SUM_F64;
     case NUT_AGG_MIN: return i64 ? AK_MIN_I64 : AK_MIN_F64;
@@ -233,6 +264,10 @@ nut_status launch_agg(nut_groups *g, const nut_agg_spec *s, uint64_t group_hint,
   }
   a.nvals = s->nvals;
   for (int v = 0; v < s->nvals; ++v) a.val_col[v] = (const uint64_t *)s->val_col[v];
+  if (s->prog_mode) {
+    a.nvals = s->nprog_cols;
+    for (int v = 0; v < s->nprog_cols; ++v) a.val_col[v] = (const uint64_t *)s->prog_col[v];
+  }
   a.naggs = s->naggs;
   a.kinds = pack_kinds(kinds, s->naggs);
   for (int i = 0; i < s->naggs; ++i) {
@@ -269,13 +304,33 @@ nut_status launch_agg(nut_groups *g, const nut_agg_spec *s, uint64_t group_hint,
   a.priv = P;
   a.gt = g->dev_gt;
   const size_t lb = lds_bytes(lcap, g->nk, na, priv, P, bd);
-  const int shape = detect_shape(s, kinds, a);
-  KernelFn fn = pick_kernel(g->nk, priv, shape, a.vec != 0);
-  NUT_HIP(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_max));
   int blocks_per_cu = lb ? (int)std::max<size_t>(1, std::min<size_t>(bd == 512 ? 4 : 8, lds_max / lb)) : 4;
   uint64_t pairs = (s->n + 1) / 2;
   uint64_t blocks = std::min<uint64_t>((uint64_t)c->num_cus * blocks_per_cu, (pairs + bd - 1) / bd);
   if (blocks == 0) blocks = 1;
+  if (s->prog_mode) {
+    // expression mode: the query's own kernel (jit.cpp), compiled once per shape
+    JitShape js;
+    nut_status st = jit_shape(s, kinds, js);
+    if (st) return st;
+    if (js.consts.size() > (size_t)kMaxConst)
+      return fail(NUT_ERR_UNSUPPORTED, "nut_groupby: more than 64 distinct expression constants");
+    for (size_t i = 0; i < js.consts.size(); ++i) a.kc[i] = js.consts[i];
+    hipFunction_t fn;
+    st = jit_kernel(jit_unit(js.src, g->nk, priv, bd, sizeof(AggArgs)), true, &fn);
+    if (st) return st;
+    size_t asz = sizeof(a);
+    void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &asz, HIP_LAUNCH_PARAM_END};
+    c->timer.begin(c->stream, NUT_KERNEL_AGGREGATE);
+    hipError_t e = hipModuleLaunchKernel(fn, (unsigned)blocks, 1, 1, (unsigned)bd, 1, 1, (unsigned)lb, c->stream,
+                                         nullptr, cfg);
+    c->timer.end(c->stream);
+    if (e != hipSuccess) return hip_fail(e, "hipModuleLaunchKernel (expression kernel)");
+    return NUT_OK;
+  }
+  const int shape = detect_shape(s, kinds, a);
+  KernelFn fn = pick_kernel(g->nk, priv, shape, a.vec != 0);
+  NUT_HIP(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_max));
   c->timer.begin(c->stream, NUT_KERNEL_AGGREGATE);
   hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(bd), lb, c->stream, a);
   c->timer.end(c->stream);
@@ -347,6 +402,10 @@ nut_status nut_groupby(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hint, n
       nut_groups_free(g);
       return st;
     }
+    if (ctl[1] & 2u) {
+      nut_groups_free(g);
+      return fail(NUT_ERR_INVALID_ARG, "nut_groupby: division by zero in an expression");
+    }
     if (!(ctl[1] & 1u)) break;
     // more groups than the table admits: retry with a larger table
     if (cap >= (1ull << 34) || attempt > 12) {
@@ -382,6 +441,7 @@ nut_status nut_groupby_accumulate(nut_ctx *c, const nut_agg_spec *s, nut_groups 
   uint32_t ctl[4];
   st = read_ctl(g, ctl);
   if (st) return st;
+  if (ctl[1] & 2u) return fail(NUT_ERR_INVALID_ARG, "nut_groupby_accumulate: division by zero in an expression");
   if (ctl[1]) return fail(NUT_ERR_OOM, "nut_groupby_accumulate: table overflow");
   return NUT_OK;
 }
@@ -455,6 +515,36 @@ nut_status nut_groups_partition(nut_groups *g, int nparts, uint64_t *out, uint64
   NUT_HIP(hipGetLastError());
   NUT_HIP(hipStreamSynchronize(c->stream));
   return NUT_OK;
+}
+
+nut_status nut_groupby_jit_source(const nut_agg_spec *s, char *buf, size_t cap, size_t *len) {
+  nut_status st = validate(s);
+  if (st) return st;
+  if (!s->prog_mode) return fail(NUT_ERR_INVALID_ARG, "nut_groupby_jit_source: spec is not in expression mode");
+  int32_t kinds[NUT_MAX_AGGS];
+  for (int a = 0; a < s->naggs; ++a) kinds[a] = kind_of(s, a);
+  JitShape js;
+  st = jit_shape(s, kinds, js);
+  if (st) return st;
+  if (len) *len = js.src.size();
+  if (buf && cap) {
+    size_t k = std::min(cap - 1, js.src.size());
+    memcpy(buf, js.src.data(), k);
+    buf[k] = '\0';
+  }
+  return cap && js.src.size() >= cap ? fail(NUT_ERR_CAPACITY, "nut_groupby_jit_source: buffer too small") : NUT_OK;
+}
+
+nut_status nut_groupby_jit_compile(const nut_agg_spec *s) {
+  nut_status st = validate(s);
+  if (st) return st;
+  if (!s->prog_mode) return fail(NUT_ERR_INVALID_ARG, "nut_groupby_jit_compile: spec is not in expression mode");
+  int32_t kinds[NUT_MAX_AGGS];
+  for (int a = 0; a < s->naggs; ++a) kinds[a] = kind_of(s, a);
+  JitShape js;
+  st = jit_shape(s, kinds, js);
+  if (st) return st;
+  return jit_kernel(jit_unit(js.src, s->nkeys == 2 ? 2 : 1, false, kBdShared, sizeof(AggArgs)), false, nullptr);
 }
 
 nut_status nut_groups_to_host(nut_groups *g, int64_t *keys, uint64_t *aggs, uint64_t cap) {

@@ -2,13 +2,15 @@
 // MI355X (gfx950, CDNA4) only: wave64, 256 CUs in 8 XCDs, 160 KiB LDS per CU.
 #pragma once
 
+#ifndef __HIPCC_RTC__  // also compiled at run time by hipRTC (jit.cpp): device part only
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include <string>
 #include <vector>
+#endif
 
-#include "../../include/nutexec.h"
+#include "nutexec.h"
 
 namespace nut {
 
@@ -112,6 +114,7 @@ __device__ __forceinline__ bool cmp_f64(double v, int op, double k) {
 typedef int64_t i64x2 __attribute__((ext_vector_type(2)));
 typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 
+#ifndef __HIPCC_RTC__
 // ---------------------------------------------------------------- host side
 void set_error(const std::string &msg);
 nut_status fail(nut_status st, const std::string &msg);
@@ -184,3 +187,6 @@ struct DeviceGuard {
   }
 };
 }  // namespace nut
+#else
+}  // namespace nut
+#endif  // __HIPCC_RTC__

@@ -23,6 +23,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <deque>
 
 #include "common.hpp"
 #include "sql_ast.hpp"
@@ -252,9 +253,18 @@ struct PlanPred {
   CVal c;
   std::vector<CVal> set;  // NUT_IN / NUT_NOT_IN
 };
+// expression-program node before binding (compiled mode; nut_prog_op)
+struct PNode {
+  int op = NUT_P_I64;
+  int col = -1;  // NUT_P_COL: plan column
+  CVal c;        // NUT_P_I64 / NUT_P_F64 constant
+};
+using PProg = std::vector<PNode>;
+
 struct PlanAgg {
   int op, expr;
   int arg[3];
+  PProg val, mask;  // compiled mode: argument program and row mask (empty = every row)
 };
 enum OutKind { OUT_KEY, OUT_AGG, OUT_AVG };
 struct PlanOut {
@@ -279,6 +289,8 @@ struct HNode {
 
 struct nut_plan {
   int kind = NUT_PLAN_FILTER;
+  bool compiled = false;          // expression mode: WHERE / aggregate arguments are programs
+  PProg where;                    // compiled mode WHERE (empty = every row)
   std::string table;
   std::vector<std::string> cols;  // names the plan binds
   bool never = false;             // WHERE folded to false
@@ -420,9 +432,276 @@ bool lower_agg_expr(nut_plan &p, const Expr &e, PlanAgg &a, Lowering &L) {
                 "' is not a column or a fused expression shape (a*b, a+b, a-b, a*(1-b), a*(1-b)*(1+c))");
 }
 
+bool same_prog(const PProg &x, const PProg &y) {
+  if (x.size() != y.size()) return false;
+  for (size_t i = 0; i < x.size(); ++i) {
+    const PNode &a = x[i], &b = y[i];
+    if (a.op != b.op || a.col != b.col) return false;
+    if (a.op == NUT_P_I64 && !(a.c.is_int == b.c.is_int && a.c.v == b.c.v)) return false;
+    if (a.op == NUT_P_F64 && !(a.c.dec == b.c.dec)) return false;
+  }
+  return true;
+}
+
+// ---- compiled mode: SQL expression -> RPN program (include/nutexec.h nut_prog_op)
+void emit(PProg &o, int op) {
+  PNode n;
+  n.op = op;
+  o.push_back(n);
+}
+void emit_int(PProg &o, i128 v) {
+  PNode n;
+  n.op = NUT_P_I64;
+  n.c.is_int = true;
+  n.c.v = v;
+  o.push_back(n);
+}
+void emit_bool(PProg &o, bool b) {  // (b != 0): a bool-typed constant
+  emit_int(o, b ? 1 : 0);
+  emit_int(o, 0);
+  emit(o, NUT_P_NE);
+}
+void append(PProg &o, const PProg &x) { o.insert(o.end(), x.begin(), x.end()); }
+
+int prog_binop(BinOp b) {
+  switch (b) {
+    case BinOp::Plus: return NUT_P_ADD;
+    case BinOp::Minus: return NUT_P_SUB;
+    case BinOp::Multi: return NUT_P_MUL;
+    case BinOp::Div: return NUT_P_DIV;
+    case BinOp::Mod: return NUT_P_MOD;
+    case BinOp::Gt: return NUT_P_GT;
+    case BinOp::Lt: return NUT_P_LT;
+    case BinOp::GtEq: return NUT_P_GE;
+    case BinOp::LtEq: return NUT_P_LE;
+    case BinOp::Eq: return NUT_P_EQ;
+    case BinOp::NotEq: return NUT_P_NE;
+    case BinOp::And: return NUT_P_AND;
+    case BinOp::Or: return NUT_P_OR;
+    case BinOp::Xor: return NUT_P_XOR;
+    case BinOp::BitwiseOr: return NUT_P_BITOR;
+    case BinOp::BitwiseAnd: return NUT_P_BITAND;
+    case BinOp::BitwiseXor: return NUT_P_BITXOR;
+    case BinOp::BitwiseLeftShift: return NUT_P_SHL;
+    case BinOp::BitwiseRightShift: return NUT_P_SHR;
+    default: return -1;
+  }
+}
+
+bool is_null_lit(const Expr &e) { return e.k == EK::Literal && e.lit->k == LitKind::Null; }
+bool is_agg_name(sv n) {
+  return ieq(n, "sum") || ieq(n, "count") || ieq(n, "min") || ieq(n, "max") || ieq(n, "avg");
+}
+
+// A conditional: conds[i] -> vals[i], else vals.back().  CASE WHEN / IF / multiIf and
+// CASE x WHEN v (cond x = v).  Returns false if e is not a conditional.
+bool lower_prog(nut_plan &p, const Expr &e, PProg &o, Lowering &L);
+bool conditional(nut_plan &p, const Expr &e, std::vector<PProg> &conds, std::vector<const Expr *> &vals,
+                 Lowering &L, bool &ok) {
+  ok = true;
+  if (e.k != EK::FnCall) return false;
+  const FnKind f = e.fn();
+  const bool fn_if = f == FnKind::Others && ieq(e.id.name, "if");
+  const bool fn_multi = f == FnKind::Others && ieq(e.id.name, "multiif");
+  if (f == FnKind::If || fn_if || f == FnKind::MultiIf || fn_multi) {
+    const size_t n = e.kids.size();
+    if ((f == FnKind::If || fn_if) ? n != 3 : (n < 3 || n % 2 == 0)) {
+      ok = L.fail(std::string(fn_if ? "if" : "multiIf") + " takes a condition, a value and an else value" +
+                  (fn_multi ? " (cond, value pairs, then else)" : ""));
+      return true;
+    }
+    for (size_t i = 0; i + 1 < n; i += 2) {
+      PProg c;
+      if (!lower_prog(p, e.kids[i], c, L)) return ok = false, true;
+      conds.push_back(std::move(c));
+      vals.push_back(&e.kids[i + 1]);
+    }
+    vals.push_back(&e.kids[n - 1]);
+    return true;
+  }
+  if (f == FnKind::CaseWhen) {
+    const size_t n = e.kids.size();  // x, v1, a1, ..., else
+    if (n < 4 || n % 2 != 0) return ok = L.fail("malformed CASE"), true;
+    PProg x;
+    if (!lower_prog(p, e.kids[0], x, L)) return ok = false, true;
+    for (size_t i = 1; i + 1 < n; i += 2) {
+      PProg c = x;
+      if (!lower_prog(p, e.kids[i], c, L)) return ok = false, true;
+      emit(c, NUT_P_EQ);
+      conds.push_back(std::move(c));
+      vals.push_back(&e.kids[i + 1]);
+    }
+    vals.push_back(&e.kids[n - 1]);
+    return true;
+  }
+  return false;
+}
+// c1 v1 c2 v2 ... else IF IF ... (IF pops cond, then, else)
+void chain(PProg &o, const std::vector<PProg> &conds, const std::vector<PProg> &vals) {
+  for (size_t i = 0; i < conds.size(); ++i) {
+    append(o, conds[i]);
+    append(o, vals[i]);
+  }
+  append(o, vals.back());
+  for (size_t i = 0; i < conds.size(); ++i) emit(o, NUT_P_IF);
+}
+
+bool lower_prog(nut_plan &p, const Expr &e, PProg &o, Lowering &L) {
+  CVal c;
+  if (const_eval(e, c, L)) {
+    PNode n;
+    n.op = c.is_int ? NUT_P_I64 : NUT_P_F64;
+    n.c = c;
+    o.push_back(n);
+    return true;
+  }
+  if (!L.err.empty()) return false;
+  switch (e.k) {
+    case EK::Identifier: {
+      if (e.id.wildcard) return L.fail("'*' is not a value");
+      PNode n;
+      n.op = NUT_P_COL;
+      n.col = col_index(p, e.id.name);
+      o.push_back(n);
+      return true;
+    }
+    case EK::Literal: {
+      bool b;
+      if (e.is_bool_lit(&b)) {
+        emit_bool(o, b);
+        return true;
+      }
+      if (is_null_lit(e)) return L.fail("NULL is executed only as a CASE/IF branch of an aggregate argument");
+      if (e.lit->k == LitKind::String) return L.fail("string constant '" + e.lit->str + "' (no string columns are executed)");
+      return L.fail("literal '" + expr_text(e) + "' is not executed here");
+    }
+    case EK::BinaryOp: {
+      const BinOp b = e.bop();
+      if (b == BinOp::In || b == BinOp::NotIn) {
+        const bool in = b == BinOp::In;
+        const Expr &r = e.kids[1];
+        if (r.k == EK::Subquery) return L.fail("IN (subquery) is not executed");
+        std::vector<const Expr *> items;
+        if (r.k == EK::Collection && (CollType)r.op == CollType::Tuple)
+          for (const Expr &x : r.kids) items.push_back(&x);
+        else
+          items.push_back(&r);
+        if (items.empty()) {
+          emit_bool(o, !in);
+          return true;
+        }
+        PProg x;
+        if (!lower_prog(p, e.kids[0], x, L)) return false;
+        for (size_t i = 0; i < items.size(); ++i) {
+          append(o, x);
+          if (!lower_prog(p, *items[i], o, L)) return false;
+          emit(o, in ? NUT_P_EQ : NUT_P_NE);
+          if (i) emit(o, in ? NUT_P_OR : NUT_P_AND);
+        }
+        return true;
+      }
+      const int op = prog_binop(b);
+      if (op < 0) return L.fail("operator in '" + expr_text(e) + "' is not executed (no string columns)");
+      if (!lower_prog(p, e.kids[0], o, L) || !lower_prog(p, e.kids[1], o, L)) return false;
+      emit(o, op);
+      return true;
+    }
+    case EK::UnaryOp: {
+      const UnOp u = e.uop();
+      if (u == UnOp::IsNull || u == UnOp::IsNotNull) {  // executed columns hold no NULLs
+        PProg tmp;
+        if (!lower_prog(p, e.kids[0], tmp, L)) return false;
+        emit_bool(o, u == UnOp::IsNotNull);
+        return true;
+      }
+      if (!lower_prog(p, e.kids[0], o, L)) return false;
+      emit(o, u == UnOp::Not ? NUT_P_NOT : NUT_P_BITNOT);
+      return true;
+    }
+    case EK::FnCall: {
+      std::vector<PProg> conds;
+      std::vector<const Expr *> vals;
+      bool ok;
+      if (conditional(p, e, conds, vals, L, ok)) {
+        if (!ok) return false;
+        std::vector<PProg> vp(vals.size());
+        for (size_t i = 0; i < vals.size(); ++i)
+          if (!lower_prog(p, *vals[i], vp[i], L)) return false;
+        chain(o, conds, vp);
+        return true;
+      }
+      const FnKind f = e.fn();
+      if (f == FnKind::Between || f == FnKind::NotBetween) {
+        if (e.kids.size() != 3) return L.fail("malformed BETWEEN");
+        const bool in = f == FnKind::Between;
+        for (int side = 0; side < 2; ++side) {
+          if (!lower_prog(p, e.kids[0], o, L) || !lower_prog(p, e.kids[1 + side], o, L)) return false;
+          emit(o, side == 0 ? (in ? NUT_P_GE : NUT_P_LT) : (in ? NUT_P_LE : NUT_P_GT));
+        }
+        emit(o, in ? NUT_P_AND : NUT_P_OR);
+        return true;
+      }
+      if (f != FnKind::Others) return L.fail("'" + expr_text(e) + "' (EXISTS / subqueries) is not executed");
+      const sv n = e.id.name;
+      const size_t na = e.kids.size();
+      if (is_agg_name(n)) return L.fail("aggregate '" + std::string(n) + "' nested inside an expression");
+      if ((ieq(n, "abs") || ieq(n, "tofloat64")) && na == 1) {
+        if (!lower_prog(p, e.kids[0], o, L)) return false;
+        emit(o, ieq(n, "abs") ? NUT_P_ABS : NUT_P_TO_F64);
+        return true;
+      }
+      if ((ieq(n, "intdiv") || ieq(n, "modulo")) && na == 2) {
+        if (!lower_prog(p, e.kids[0], o, L) || !lower_prog(p, e.kids[1], o, L)) return false;
+        emit(o, ieq(n, "intdiv") ? NUT_P_INTDIV : NUT_P_MOD);
+        return true;
+      }
+      if (ieq(n, "todate")) return L.fail("toDate takes one 'YYYY-MM-DD' constant");
+      return L.fail("function '" + std::string(n) + "' is not executed (executed: if, multiIf, abs, toFloat64, intDiv, modulo)");
+    }
+    default: return L.fail("'" + expr_text(e) + "' is not executed (parameters, collections, subqueries)");
+  }
+}
+
+// An aggregate argument: a NULL branch of a top-level conditional (CASE without ELSE)
+// becomes the aggregate's row mask — SQL aggregates skip NULL arguments.
+bool lower_nullable(nut_plan &p, const Expr &e, PProg &val, PProg &mask, bool &nullable, Lowering &L) {
+  nullable = false;
+  if (is_null_lit(e)) {
+    emit_int(val, 0);
+    emit_bool(mask, false);
+    nullable = true;
+    return true;
+  }
+  std::vector<PProg> conds;
+  std::vector<const Expr *> vals;
+  bool ok;
+  if (!conditional(p, e, conds, vals, L, ok)) return lower_prog(p, e, val, L);
+  if (!ok) return false;
+  std::vector<PProg> vv(vals.size()), mm(vals.size());
+  std::vector<char> nb(vals.size());
+  for (size_t i = 0; i < vals.size(); ++i) {
+    bool n;
+    if (!lower_nullable(p, *vals[i], vv[i], mm[i], n, L)) return false;
+    nb[i] = n;
+    nullable = nullable || n;
+  }
+  chain(val, conds, vv);
+  if (nullable) {
+    for (size_t i = 0; i < vals.size(); ++i)
+      if (!nb[i]) emit_bool(mm[i], true);
+    chain(mask, conds, mm);
+  }
+  return true;
+}
+
 int add_agg(nut_plan &p, const PlanAgg &a) {
   for (size_t i = 0; i < p.aggs.size(); ++i) {
     const PlanAgg &b = p.aggs[i];
+    if (p.compiled) {
+      if (b.op == a.op && same_prog(b.mask, a.mask) && (a.op == NUT_AGG_COUNT || same_prog(b.val, a.val)))
+        return (int)i;
+      continue;
+    }
     if (b.op == a.op && (a.op == NUT_AGG_COUNT ||
                          (b.expr == a.expr && !memcmp(b.arg, a.arg, sizeof a.arg))))
       return (int)i;
@@ -509,6 +788,26 @@ bool lower_output(nut_plan &p, const Expr &e, PlanOut &o, Lowering &L) {
            : ieq(fn, "max") ? NUT_AGG_MAX : ieq(fn, "avg") ? 100 : -1;
   if (op < 0) return L.fail("function '" + std::string(fn) + "' is not an executed aggregate (sum/count/min/max/avg)");
   PlanAgg a{};
+  if (p.compiled) {
+    if (op == NUT_AGG_COUNT ? e.kids.size() > 1 : e.kids.size() != 1)
+      return L.fail(std::string(fn) + (op == NUT_AGG_COUNT ? " takes at most one argument" : " takes one argument"));
+    bool nullable = false;
+    const bool star = e.kids.empty() || (e.kids[0].k == EK::Identifier && e.kids[0].id.wildcard);
+    if (!star && !lower_nullable(p, e.kids[0], a.val, a.mask, nullable, L)) return false;
+    if (op == NUT_AGG_COUNT) a.val.clear();  // count(x) counts the rows where x is not NULL
+    a.op = op == 100 ? NUT_AGG_SUM : op;
+    a.expr = NUT_EX_COL;
+    o.a = add_agg(p, a);
+    o.kind = op == 100 ? OUT_AVG : OUT_AGG;
+    if (op == 100) {
+      PlanAgg cnt{};
+      cnt.op = NUT_AGG_COUNT;
+      cnt.expr = NUT_EX_COL;
+      cnt.mask = a.mask;
+      o.b = add_agg(p, cnt);
+    }
+    return true;
+  }
   if (op == NUT_AGG_COUNT) {
     if (e.kids.size() > 1) return L.fail("count takes at most one argument");
     if (e.kids.size() == 1 && !(e.kids[0].k == EK::Identifier)) return L.fail("count argument must be * or a column");
@@ -616,7 +915,7 @@ bool lower_having(nut_plan &p, const Expr &e, HNode &h, Lowering &L) {
   return L.fail("unsupported HAVING term '" + expr_text(e) + "'");
 }
 
-bool lower(const Statement &st, nut_plan &p, Lowering &L) {
+bool lower_mode(const Statement &st, nut_plan &p, Lowering &L) {
   if (st.k != StmtKind::Select) return L.fail("only SELECT statements execute");
   if (st.query.is_union) return L.fail("UNION/INTERSECT/EXCEPT are not executed (one query body per plan)");
   const QueryBody &b = *st.query.body;
@@ -626,7 +925,16 @@ bool lower(const Statement &st, nut_plan &p, Lowering &L) {
   if (!b.joins.empty()) return L.fail("JOIN is not executed");
   if (b.having && !b.group_by) return L.fail("HAVING needs GROUP BY");
   p.table = std::string(b.from->table);
-  if (b.where && !lower_where(p, *b.where, L)) return false;
+  bool wb;
+  if (p.compiled && b.where) {
+    if (b.where->is_bool_lit(&wb)) {
+      if (!wb) p.never = true;
+    } else if (!lower_prog(p, *b.where, p.where, L)) {
+      return false;
+    }
+  } else if (b.where && !lower_where(p, *b.where, L)) {
+    return false;
+  }
   if (p.preds.size() > NUT_MAX_PRED) return L.fail("more than " + std::to_string(NUT_MAX_PRED) + " WHERE terms");
   if (b.limit) {
     p.has_limit = true;
@@ -711,6 +1019,57 @@ bool lower(const Statement &st, nut_plan &p, Lowering &L) {
   return true;
 }
 
+// Aggregate queries lower to the precompiled kernel shapes when they fit (column
+// comparisons ANDed, the fused expression shapes); anything else — arbitrary
+// expressions, OR / NOT / CASE, column-to-column comparisons, more than 6 terms — to
+// expression programs compiled for the query (jit.cpp).  Scans stay on the filter kernel.
+bool lower(const Statement &st, nut_plan &p, Lowering &L) {
+  Lowering L1;
+  if (lower_mode(st, p, L1)) return true;
+  bool agg = false;
+  if (st.k == StmtKind::Select && !st.query.is_union && st.query.body) {
+    const QueryBody &b = *st.query.body;
+    agg = b.group_by.has_value();
+    for (const QueryExpr &q : b.columns)
+      if (q.e.k == EK::FnCall && q.e.fn() == FnKind::Others) agg = true;
+  }
+  if (!agg) return L.fail(L1.err);
+  nut_plan p2;
+  p2.compiled = true;
+  Lowering L2;
+  if (!lower_mode(st, p2, L2)) return L.fail(L2.err);
+  p = std::move(p2);
+  return true;
+}
+
+// RPN -> infix text, for describe()
+std::string prog_text(const nut_plan &p, const PProg &pp) {
+  static const char *bin[] = {"", "", "", "+", "-", "*", "/", "%", "div", "<", "<=", ">", ">=", "=", "!=",
+                              "and", "or", "xor", "", "&", "|", "^", "", "<<", ">>"};
+  std::vector<std::string> st;
+  for (const PNode &n : pp) {
+    auto pop = [&]() {
+      std::string t = st.empty() ? "?" : st.back();
+      if (!st.empty()) st.pop_back();
+      return t;
+    };
+    if (n.op == NUT_P_COL) st.push_back(p.cols[n.col]);
+    else if (n.op == NUT_P_I64 || n.op == NUT_P_F64) st.push_back(cval_str(n.c));
+    else if (n.op == NUT_P_NOT || n.op == NUT_P_BITNOT || n.op == NUT_P_ABS || n.op == NUT_P_TO_F64) {
+      const char *f = n.op == NUT_P_NOT ? "not" : n.op == NUT_P_BITNOT ? "~" : n.op == NUT_P_ABS ? "abs" : "toFloat64";
+      st.push_back(std::string(f) + "(" + pop() + ")");
+    } else if (n.op == NUT_P_IF) {
+      std::string e = pop(), t = pop(), c = pop();
+      st.push_back("if(" + c + ", " + t + ", " + e + ")");
+    } else {
+      std::string r = pop(), l = pop();
+      if (n.op == NUT_P_NE && r == "0" && (l == "1" || l == "0")) st.push_back(l == "1" ? "true" : "false");
+      else st.push_back("(" + l + " " + bin[n.op] + " " + r + ")");
+    }
+  }
+  return st.empty() ? "" : st.back();
+}
+
 std::string describe(const nut_plan &p) {
   static const char *kinds[] = {"filter", "groupby", "sort"};
   static const char *aggs[] = {"sum", "count", "min", "max"};
@@ -727,6 +1086,11 @@ std::string describe(const nut_plan &p) {
   }
   o += "],\"never\":";
   o += p.never ? "true" : "false";
+  o += p.compiled ? ",\"mode\":\"compiled\"" : ",\"mode\":\"fused\"";
+  if (p.compiled) {
+    o += ",\"where_expr\":";
+    json_str(o, prog_text(p, p.where));
+  }
   o += ",\"where\":[";
   for (size_t i = 0; i < p.preds.size(); ++i) {
     const PlanPred &pr = p.preds[i];
@@ -762,7 +1126,16 @@ std::string describe(const nut_plan &p) {
       o += "{\"op\":\"";
       o += aggs[a.op];
       o += "\"";
-      if (a.op != NUT_AGG_COUNT) {
+      if (p.compiled) {
+        if (a.op != NUT_AGG_COUNT) {
+          o += ",\"expr\":";
+          json_str(o, prog_text(p, a.val));
+        }
+        if (!a.mask.empty()) {
+          o += ",\"mask\":";
+          json_str(o, prog_text(p, a.mask));
+        }
+      } else if (a.op != NUT_AGG_COUNT) {
         o += ",\"expr\":\"";
         o += exprs[a.expr];
         o += "\",\"args\":[";
@@ -964,9 +1337,9 @@ bool having_true(const HNode &h, const std::vector<std::vector<uint64_t>> &cols,
   }
 }
 
-nut_status exec_groupby(nut_ctx *c, const nut_plan &p, const nut_column *const *bound, uint64_t n, uint64_t hint,
-                        nut_result *r) {
-  nut_agg_spec s;
+// the nut_agg_spec of an aggregate plan over bound columns (program nodes live in store)
+nut_status build_spec(const nut_plan &p, const nut_column *const *bound, uint64_t n, nut_agg_spec &s,
+                      std::deque<std::vector<nut_prog_node>> &store, std::vector<int> &agg_f64) {
   memset(&s, 0, sizeof s);
   s.n = p.never ? 0 : n;
   s.nkeys = (int32_t)p.keys.size();
@@ -975,85 +1348,149 @@ nut_status exec_groupby(nut_ctx *c, const nut_plan &p, const nut_column *const *
     if (k->type != NUT_T_I64) return fail(NUT_ERR_PLAN, "GROUP BY column '" + p.cols[p.keys[j]] + "' must be int64");
     s.keys[j] = (const int64_t *)k->data;
   }
-  for (const PlanPred &pr : p.preds) {
-    const nut_column *col = bound[pr.col];
-    if (pr.op >= NUT_IN) {
-      // keep the set values the column type can hold (a non-integral or out-of-range
-      // constant never equals an int64)
-      std::vector<int64_t> vals;
-      for (const CVal &v : pr.set) {
-        if (col->type == NUT_T_I64) {
-          int o2;
-          int64_t k;
-          if (resolve_i64(NUT_EQ, v, o2, k) == V_PRED) vals.push_back(k);
-        } else {
-          double d = resolve_f64(v);
-          int64_t bits;
-          memcpy(&bits, &d, 8);
-          vals.push_back(bits);
+  agg_f64.assign(p.aggs.size(), 0);
+  if (p.compiled) {
+    // expression mode: bind the programs' columns (first use order) and constants
+    s.prog_mode = 1;
+    std::vector<int> pcol(p.cols.size(), -1);
+    auto resolve = [&](const PProg &pp, nut_prog &out, const char *what, int32_t *type) -> nut_status {
+      store.emplace_back();
+      std::vector<nut_prog_node> &v = store.back();
+      for (const PNode &n : pp) {
+        nut_prog_node q{n.op, 0, 0};
+        if (n.op == NUT_P_COL) {
+          if (pcol[n.col] < 0) {
+            if (s.nprog_cols >= NUT_MAX_PROG_COLS) return fail(NUT_ERR_PLAN, "expressions read more than 16 columns");
+            pcol[n.col] = s.nprog_cols;
+            s.prog_col[s.nprog_cols] = bound[n.col]->data;
+            s.prog_col_type[s.nprog_cols] = bound[n.col]->type;
+            s.nprog_cols++;
+          }
+          q.arg = pcol[n.col];
+        } else if (n.op == NUT_P_I64) {
+          if (n.c.v > INT64_MAX || n.c.v < INT64_MIN)
+            return fail(NUT_ERR_PLAN, "integer constant " + cval_str(n.c) + " is outside int64");
+          q.v = (int64_t)n.c.v;
+        } else if (n.op == NUT_P_F64) {
+          const double d = n.c.dec.to_f64();
+          memcpy(&q.v, &d, 8);
         }
+        v.push_back(q);
       }
-      if (vals.empty()) {
-        if (pr.op == NUT_IN) s.n = 0;  // IN () is false; NOT IN () is true
+      out.n = (int32_t)v.size();
+      out.node = v.data();
+      if (!type) return NUT_OK;
+      if (nut_prog_type(&out, s.prog_col_type, NUT_MAX_PROG_COLS, type))
+        return fail(NUT_ERR_PLAN, std::string(what) + ": " + nut_last_error());
+      return NUT_OK;
+    };
+    int32_t t;
+    nut_status st = NUT_OK;
+    if (!p.where.empty()) {
+      st = resolve(p.where, s.where, "WHERE", &t);
+      if (!st && t == NUT_PT_F64) st = fail(NUT_ERR_PLAN, "WHERE: a float64 expression is not a condition");
+    }
+    s.naggs = (int32_t)p.aggs.size();
+    for (size_t a = 0; a < p.aggs.size() && !st; ++a) {
+      const PlanAgg &g = p.aggs[a];
+      s.agg_op[a] = g.op;
+      if (g.op != NUT_AGG_COUNT) {
+        st = resolve(g.val, s.agg_val[a], "aggregate argument", &t);
+        agg_f64[a] = t == NUT_PT_F64;
+      }
+      if (!st && !g.mask.empty()) st = resolve(g.mask, s.agg_mask[a], "aggregate argument", &t);
+    }
+    if (st) return st;
+  } else {
+    for (const PlanPred &pr : p.preds) {
+      const nut_column *col = bound[pr.col];
+      if (pr.op >= NUT_IN) {
+        // keep the set values the column type can hold (a non-integral or out-of-range
+        // constant never equals an int64)
+        std::vector<int64_t> vals;
+        for (const CVal &v : pr.set) {
+          if (col->type == NUT_T_I64) {
+            int o2;
+            int64_t k;
+            if (resolve_i64(NUT_EQ, v, o2, k) == V_PRED) vals.push_back(k);
+          } else {
+            double d = resolve_f64(v);
+            int64_t bits;
+            memcpy(&bits, &d, 8);
+            vals.push_back(bits);
+          }
+        }
+        if (vals.empty()) {
+          if (pr.op == NUT_IN) s.n = 0;  // IN () is false; NOT IN () is true
+          continue;
+        }
+        s.pred_col[s.npred] = col->data;
+        s.pred_type[s.npred] = col->type;
+        s.pred_op[s.npred] = pr.op;
+        s.pred_nset[s.npred] = (int32_t)vals.size();
+        for (size_t j = 0; j < vals.size(); ++j) s.pred_set[s.npred][j] = vals[j];
+        s.npred++;
         continue;
       }
-      s.pred_col[s.npred] = col->data;
-      s.pred_type[s.npred] = col->type;
-      s.pred_op[s.npred] = pr.op;
-      s.pred_nset[s.npred] = (int32_t)vals.size();
-      for (size_t j = 0; j < vals.size(); ++j) s.pred_set[s.npred][j] = vals[j];
+      if (col->type == NUT_T_I64) {
+        int op;
+        int64_t k;
+        Verdict v = resolve_i64(pr.op, pr.c, op, k);
+        if (v == V_TRUE) continue;
+        if (v == V_FALSE) {
+          s.n = 0;
+          continue;
+        }
+        s.pred_col[s.npred] = col->data;
+        s.pred_type[s.npred] = NUT_T_I64;
+        s.pred_op[s.npred] = op;
+        s.pred_i64[s.npred] = k;
+      } else {
+        s.pred_col[s.npred] = col->data;
+        s.pred_type[s.npred] = NUT_T_F64;
+        s.pred_op[s.npred] = pr.op;
+        s.pred_f64[s.npred] = resolve_f64(pr.c);
+      }
       s.npred++;
-      continue;
     }
-    if (col->type == NUT_T_I64) {
-      int op;
-      int64_t k;
-      Verdict v = resolve_i64(pr.op, pr.c, op, k);
-      if (v == V_TRUE) continue;
-      if (v == V_FALSE) {
-        s.n = 0;
-        continue;
-      }
-      s.pred_col[s.npred] = col->data;
-      s.pred_type[s.npred] = NUT_T_I64;
-      s.pred_op[s.npred] = op;
-      s.pred_i64[s.npred] = k;
-    } else {
-      s.pred_col[s.npred] = col->data;
-      s.pred_type[s.npred] = NUT_T_F64;
-      s.pred_op[s.npred] = pr.op;
-      s.pred_f64[s.npred] = resolve_f64(pr.c);
+    s.nvals = (int32_t)p.vals.size();
+    for (size_t v = 0; v < p.vals.size(); ++v) {
+      s.val_col[v] = bound[p.vals[v]]->data;
+      s.val_type[v] = bound[p.vals[v]]->type;
     }
-    s.npred++;
-  }
-  s.nvals = (int32_t)p.vals.size();
-  for (size_t v = 0; v < p.vals.size(); ++v) {
-    s.val_col[v] = bound[p.vals[v]]->data;
-    s.val_type[v] = bound[p.vals[v]]->type;
-  }
-  std::vector<int> agg_f64(p.aggs.size(), 0);
-  s.naggs = (int32_t)p.aggs.size();
-  for (size_t a = 0; a < p.aggs.size(); ++a) {
-    const PlanAgg &g = p.aggs[a];
-    s.agg_op[a] = g.op;
-    s.agg_expr[a] = g.expr;
-    for (int j = 0; j < 3; ++j) s.agg_arg[a][j] = g.arg[j];
-    if (g.op != NUT_AGG_COUNT) {
-      bool f = s.val_type[g.arg[0]] == NUT_T_F64;
-      if (g.expr != NUT_EX_COL) {
-        static const int nargs[] = {1, 2, 2, 2, 2, 3};
-        for (int j = 0; j < nargs[g.expr]; ++j)
-          if (s.val_type[g.arg[j]] != NUT_T_F64)
-            return fail(NUT_ERR_PLAN, "fused aggregate expressions need float64 columns ('" +
-                                          p.cols[p.vals[g.arg[j]]] + "' is int64)");
-        f = true;
+    s.naggs = (int32_t)p.aggs.size();
+    for (size_t a = 0; a < p.aggs.size(); ++a) {
+      const PlanAgg &g = p.aggs[a];
+      s.agg_op[a] = g.op;
+      s.agg_expr[a] = g.expr;
+      for (int j = 0; j < 3; ++j) s.agg_arg[a][j] = g.arg[j];
+      if (g.op != NUT_AGG_COUNT) {
+        bool f = s.val_type[g.arg[0]] == NUT_T_F64;
+        if (g.expr != NUT_EX_COL) {
+          static const int nargs[] = {1, 2, 2, 2, 2, 3};
+          for (int j = 0; j < nargs[g.expr]; ++j)
+            if (s.val_type[g.arg[j]] != NUT_T_F64)
+              return fail(NUT_ERR_PLAN, "fused aggregate expressions need float64 columns ('" +
+                                            p.cols[p.vals[g.arg[j]]] + "' is int64)");
+          f = true;
+        }
+        agg_f64[a] = f;
       }
-      agg_f64[a] = f;
     }
   }
   if (s.n == 0) {  // keep the kernels' pointer checks happy for an empty scan
     s.npred = 0;
   }
+  return NUT_OK;
+}
+
+nut_status exec_groupby(nut_ctx *c, const nut_plan &p, const nut_column *const *bound, uint64_t n, uint64_t hint,
+                        nut_result *r) {
+  nut_agg_spec s;
+  std::deque<std::vector<nut_prog_node>> store;  // program nodes, alive until nut_groupby returns
+  std::vector<int> agg_f64;
+  nut_status bs = build_spec(p, bound, n, s, store, agg_f64);
+  if (bs) return bs;
   nut_groups *g = nullptr;
   nut_status st = nut_groupby(c, &s, hint, &g);
   if (st) return st;
@@ -1268,6 +1705,24 @@ nut_status nut_plan_execute(nut_ctx *c, const nut_plan *p, const nut_column *col
   }
   *out = r;
   return NUT_OK;
+}
+
+nut_status nut_plan_prepare(const nut_plan *p, const nut_column *cols, int ncols) {
+  if (!p || (ncols && !cols) || ncols < 0) return fail(NUT_ERR_INVALID_ARG, "nut_plan_prepare: NULL argument");
+  if (p->kind != NUT_PLAN_GROUPBY || !p->compiled) return NUT_OK;  // precompiled kernels only
+  std::vector<const nut_column *> bound(p->cols.size());
+  for (size_t i = 0; i < p->cols.size(); ++i) {
+    bound[i] = bind(*p, (int)i, cols, ncols);
+    if (!bound[i]) return fail(NUT_ERR_INVALID_ARG, "nut_plan_prepare: column '" + p->cols[i] + "' is not bound");
+    if (bound[i]->type != NUT_T_I64 && bound[i]->type != NUT_T_F64)
+      return fail(NUT_ERR_INVALID_ARG, "nut_plan_prepare: column '" + p->cols[i] + "' has an unknown type");
+  }
+  nut_agg_spec s;
+  std::deque<std::vector<nut_prog_node>> store;
+  std::vector<int> agg_f64;
+  nut_status st = build_spec(*p, bound.data(), 0, s, store, agg_f64);
+  if (st) return st;
+  return nut_groupby_jit_compile(&s);
 }
 
 nut_status nut_result_shape(const nut_result *r, uint64_t *nrows, int *ncols) {

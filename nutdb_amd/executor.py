@@ -128,6 +128,90 @@ class AggQuery:
         return out
 
 
+def _node(nd) -> tuple:
+    """(op, arg, v): op = nut_prog_op index or name (_lib.PROG_OPS); an "f64" constant
+    may be given as a Python float (stored as the double's bits)."""
+    op, arg, v = (tuple(nd) + (0, 0))[:3]
+    op = L.P[op] if isinstance(op, str) else int(op)
+    if op == L.P["f64"] and isinstance(v, float):
+        v = int(np.array([v], dtype=np.float64).view(np.int64)[0])
+    return op, int(arg), int(v)
+
+
+def _prog(nodes, keep: list) -> L.NutProg:
+    pr = L.NutProg()
+    if not nodes:
+        return pr
+    if len(nodes) > L.NUT_MAX_PROG_NODES:
+        raise ValueError("expression programs hold at most 256 nodes")
+    arr = (L.NutProgNode * len(nodes))()
+    for i, nd in enumerate(nodes):
+        arr[i].op, arr[i].arg, arr[i].v = _node(nd)
+    keep.append(arr)
+    pr.n = len(nodes)
+    pr.node = C.cast(arr, C.POINTER(L.NutProgNode))
+    return pr
+
+
+@dataclass
+class ProgQuery:
+    """Expression mode of nut_groupby (include/nutexec.h nut_prog): WHERE and every
+    aggregate argument are RPN programs over `cols`, compiled for the query at run time
+    (csrc/jit.cpp).  aggs = [(op, value program or None, mask program or None)]: the
+    mask keeps only rows where it is true (CASE without ELSE)."""
+    keys: list
+    cols: list
+    aggs: list
+    where: list | None = None
+    rows: int | None = None
+
+    def to_spec(self, dev: torch.device) -> L.NutAggSpec:
+        s = L.NutAggSpec()
+        keep = []
+        s._keep = keep  # node arrays live as long as the spec
+        cols = list(self.keys) + list(self.cols)
+        n = int(cols[0].numel()) if cols else int(self.rows or 0)
+        s.n = n
+        if not 0 <= len(self.keys) <= L.NUT_MAX_KEYS:
+            raise ValueError("0, 1 or 2 group keys")
+        s.nkeys = len(self.keys)
+        for i, k in enumerate(self.keys):
+            if k.dtype != torch.int64 or k.numel() != n:
+                raise ValueError("group keys are int64 columns of equal length")
+            s.keys[i] = _col(k, dev)
+        if len(self.cols) > L.NUT_MAX_PROG_COLS:
+            raise ValueError("programs read at most 16 columns")
+        s.prog_mode = 1
+        s.nprog_cols = len(self.cols)
+        for i, c in enumerate(self.cols):
+            if c.numel() != n:
+                raise ValueError("ragged columns")
+            s.prog_col[i] = _col(c, dev)
+            s.prog_col_type[i] = _dtype_code(c)
+        s.where = _prog(self.where, keep)
+        if len(self.aggs) > L.NUT_MAX_AGGS:
+            raise ValueError("too many aggregates")
+        s.naggs = len(self.aggs)
+        for i, (op, val, mask) in enumerate(self.aggs):
+            s.agg_op[i] = AGG[op] if isinstance(op, str) else int(op)
+            s.agg_val[i] = _prog(val, keep)
+            s.agg_mask[i] = _prog(mask, keep)
+        return s
+
+    def result_types(self) -> list:
+        types = (C.c_int32 * max(len(self.cols), 1))(*[_dtype_code(c) for c in self.cols])
+        out = []
+        for op, val, _ in self.aggs:
+            if (AGG[op] if isinstance(op, str) else int(op)) == L.AGG_COUNT:
+                out.append(np.int64)
+                continue
+            keep = []
+            t = C.c_int32()
+            check(lib.nut_prog_type(C.byref(_prog(val, keep)), types, len(self.cols), C.byref(t)), "nut_prog_type")
+            out.append(np.float64 if t.value == L.PT_F64 else np.int64)
+        return out
+
+
 class Groups:
     """Library-owned group-by result (nut_groups*)."""
 
@@ -271,7 +355,7 @@ class Executor:
               "nut_filter_i64_async")
 
     # ---------------------------------------------------------------- group-by
-    def groupby(self, q: AggQuery, group_hint: int = 0) -> Groups:
+    def groupby(self, q: "AggQuery | ProgQuery", group_hint: int = 0) -> Groups:
         spec = q.to_spec(self.device)
         self._bind_stream()
         h = C.c_void_p()

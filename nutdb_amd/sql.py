@@ -150,6 +150,17 @@ class Plan:
     def columns(self) -> List[str]:
         return self.describe()["columns"]
 
+    def prepare(self, types: Dict[str, str]) -> None:
+        """Compile an expression-mode plan's kernel ahead of execute (hipRTC, no GPU
+        needed); `types` = {column: "int64" | "float64"}.  No-op for fused plans."""
+        arr = (NutColumn * max(len(types), 1))()
+        names = [k.encode() for k in types]
+        for i, (name, t) in enumerate(types.items()):
+            arr[i].name = names[i]
+            arr[i].data = None
+            arr[i].type = {"int64": T_I64, "float64": T_F64}[t]
+        check(lib.nut_plan_prepare(self._h, arr, len(types)), "nut_plan_prepare")
+
     def execute(self, ex, columns: Dict[str, "object"], nrows: Optional[int] = None,
                 group_hint: int = 0) -> Dict[str, np.ndarray]:
         """Run on the GPU of executor `ex` with `columns` = {name: 1-D int64/float64 CUDA

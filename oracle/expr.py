@@ -1,0 +1,210 @@
+"""Expression-program oracle (numpy) — TEST INFRASTRUCTURE ONLY.
+
+Restates the semantics of include/nutexec.h `nut_prog` (RPN expression programs, the
+expression mode of nut_groupby; nutdb_amd/csrc/jit.cpp generates the device code)
+column-at-a-time with numpy, independently of the generated HIP code:
+
+  * i64 + - * wrap (two's complement); any f64 operand makes the op f64 (the int is
+    converted with round-to-nearest); DIV is always f64;
+  * MOD / INTDIV on ints truncate toward zero; a zero divisor is an error of the row;
+    INT64_MIN % -1 = 0 and INT64_MIN div -1 wraps; MOD on f64 is C fmod;
+  * comparisons give bool; int vs f64 compares as f64; NaN compares unequal;
+  * AND / OR / XOR / NOT over bools (ints: non-zero = true), both operands evaluated;
+  * bit ops and shifts on ints; shift counts outside [0, 63] give 0 (SHR of a
+    negative value: -1); SHR is arithmetic;
+  * IF takes the chosen branch's value and only the chosen branch's errors.
+
+Errors are tracked per row (a bool array); the group-by rule is the kernel's
+(agg_kernel.hpp consume_rows): a WHERE error counts for every row, an aggregate's mask
+error for rows passing WHERE, its value error for rows passing WHERE and its mask.
+
+The reference (nutdb v0.1.0) executes no expressions at all — it stops at the AST
+ — so these semantics are defined by this build and the oracle is
+"parity unpinned" with respect to the reference; the SQL→program lowering they are fed
+from is pinned by the front-end tests against the reference's own fixtures.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+OPS = ["col", "i64", "f64", "add", "sub", "mul", "div", "mod", "intdiv", "lt", "le", "gt", "ge", "eq", "ne",
+       "and", "or", "xor", "not", "bitand", "bitor", "bitxor", "bitnot", "shl", "shr", "if", "abs", "to_f64"]
+OP = {name: i for i, name in enumerate(OPS)}
+I64, F64, BOOL = 0, 1, 2
+_ARITY = {OP["not"]: 1, OP["bitnot"]: 1, OP["abs"]: 1, OP["to_f64"]: 1, OP["if"]: 3}
+
+
+class ProgramError(ValueError):
+    pass
+
+
+class DivisionByZero(ArithmeticError):
+    pass
+
+
+def _f(v):
+    x, t, _ = v
+    return x if t == F64 else x.astype(np.float64)
+
+
+def _i(v):
+    x, t, _ = v
+    if t == F64:
+        raise ProgramError("integer operand expected, got float64")
+    return x.astype(np.int64)
+
+
+def _b(v):
+    x, t, _ = v
+    if t == F64:
+        raise ProgramError("boolean or integer operand expected, got float64")
+    return x.astype(bool) if t == BOOL else x != 0
+
+
+def eval_prog(nodes, cols, n=None):
+    """nodes: [(op, arg, v)] (op index or name; v = int64 constant or the double's bits);
+    cols: list of int64 / float64 arrays.  Returns (values, type, err): values int64
+    (I64/BOOL as 0/1) or float64, type I64/F64/BOOL, err a bool array."""
+    if n is None:
+        n = len(cols[0]) if cols else 0
+    st = []
+    z = np.zeros(n, dtype=bool)
+    with np.errstate(all="ignore"):
+        for node in nodes:
+            op, arg, v = (tuple(node) + (0, 0))[:3]
+            op = OP[op] if isinstance(op, str) else int(op)
+            if op == OP["f64"] and isinstance(v, float):
+                v = int(np.array([v], dtype=np.float64).view(np.int64)[0])
+            k = 0 if op <= OP["f64"] else _ARITY.get(op, 2)
+            if len(st) < k:
+                raise ProgramError("stack underflow")
+            a = st[len(st) - k:]
+            del st[len(st) - k:]
+            err = z.copy()
+            for x in a:
+                err = err | x[2]
+            f = k == 2 and (a[0][1] == F64 or a[1][1] == F64)
+            if op == OP["col"]:
+                c = np.asarray(cols[arg])
+                r = (c.astype(np.float64), F64) if c.dtype == np.float64 else (c.astype(np.int64), I64)
+            elif op == OP["i64"]:
+                r = (np.full(n, v, dtype=np.int64), I64)
+            elif op == OP["f64"]:
+                r = (np.full(n, np.int64(v).view(np.float64), dtype=np.float64), F64)
+            elif op in (OP["add"], OP["sub"], OP["mul"]):
+                fn = {OP["add"]: np.add, OP["sub"]: np.subtract, OP["mul"]: np.multiply}[op]
+                r = (fn(_f(a[0]), _f(a[1])), F64) if f else (fn(_i(a[0]), _i(a[1])), I64)
+            elif op == OP["div"]:
+                r = (np.divide(_f(a[0]), _f(a[1])), F64)
+            elif op in (OP["mod"], OP["intdiv"]):
+                if f:
+                    if op == OP["intdiv"]:
+                        raise ProgramError("integer division needs integer operands")
+                    r = (np.fmod(_f(a[0]), _f(a[1])), F64)
+                else:
+                    x, y = _i(a[0]), _i(a[1])
+                    zero, m1 = y == 0, y == -1
+                    ys = np.where(zero | m1, 1, y)
+                    q = np.floor_divide(x, ys)
+                    rem = x - q * ys
+                    fix = (rem != 0) & ((x < 0) != (ys < 0))  # floor -> truncation
+                    q = np.where(fix, q + 1, q)
+                    rem = np.where(fix, rem - ys, rem)
+                    if op == OP["mod"]:
+                        out = np.where(zero | m1, 0, rem)
+                    else:
+                        out = np.where(zero, 0, np.where(m1, np.negative(x), q))
+                    r = (out.astype(np.int64), I64)
+                    err = err | zero
+            elif OP["lt"] <= op <= OP["ne"]:
+                fn = [np.less, np.less_equal, np.greater, np.greater_equal, np.equal, np.not_equal][op - OP["lt"]]
+                r = (fn(_f(a[0]), _f(a[1])) if f else fn(_i(a[0]), _i(a[1])), BOOL)
+            elif op in (OP["and"], OP["or"], OP["xor"]):
+                fn = {OP["and"]: np.logical_and, OP["or"]: np.logical_or, OP["xor"]: np.not_equal}[op]
+                r = (fn(_b(a[0]), _b(a[1])), BOOL)
+            elif op == OP["not"]:
+                r = (~_b(a[0]), BOOL)
+            elif op in (OP["bitand"], OP["bitor"], OP["bitxor"]):
+                if f:
+                    raise ProgramError("bitwise operators need integer operands")
+                fn = {OP["bitand"]: np.bitwise_and, OP["bitor"]: np.bitwise_or, OP["bitxor"]: np.bitwise_xor}[op]
+                r = (fn(_i(a[0]), _i(a[1])), I64)
+            elif op == OP["bitnot"]:
+                r = (np.invert(_i(a[0])), I64)
+            elif op in (OP["shl"], OP["shr"]):
+                if f:
+                    raise ProgramError("bitwise operators need integer operands")
+                x, y = _i(a[0]), _i(a[1])
+                ok = (y >= 0) & (y < 64)
+                ys = np.where(ok, y, 0).astype(np.uint64)
+                if op == OP["shl"]:
+                    out = np.where(ok, np.left_shift(x.view(np.uint64), ys).view(np.int64), 0)
+                else:
+                    out = np.where(ok, np.right_shift(x, ys.astype(np.int64)), np.where(x < 0, -1, 0))
+                r = (out.astype(np.int64), I64)
+            elif op == OP["if"]:
+                c = _b(a[0])
+                x, y = a[1], a[2]
+                if x[1] == BOOL and y[1] == BOOL:
+                    r = (np.where(c, _b(x), _b(y)), BOOL)
+                elif x[1] == F64 or y[1] == F64:
+                    r = (np.where(c, _f(x), _f(y)), F64)
+                else:
+                    r = (np.where(c, _i(x), _i(y)), I64)
+                err = a[0][2] | np.where(c, x[2], y[2])
+            elif op == OP["abs"]:
+                r = (np.abs(_f(a[0])), F64) if a[0][1] == F64 else (np.abs(_i(a[0])), I64)
+            elif op == OP["to_f64"]:
+                r = (_f(a[0]), F64)
+            else:
+                raise ProgramError(f"unknown op {op}")
+            st.append((r[0], r[1], err))
+    if len(st) != 1:
+        raise ProgramError(f"program leaves {len(st)} values")
+    x, t, err = st[0]
+    if t == BOOL:
+        x = x.astype(np.int64)
+    return x, t, err
+
+
+def groupby_prog(keys, cols, where, aggs, n=None):
+    """Expression-mode group-by: keys = list of int64 arrays (empty = global aggregate),
+    where = nodes or None, aggs = [(op, val_nodes or None, mask_nodes or None)] with op
+    0 SUM / 1 COUNT / 2 MIN / 3 MAX.  Returns (keys, words, types) like
+    oracle.groupby (words = result bits) plus each aggregate's value type; raises
+    DivisionByZero under the kernel's error rule."""
+    from . import oracle as orc
+
+    if n is None:
+        n = len(keys[0]) if keys else len(cols[0])
+    ok = np.ones(n, dtype=bool)
+    bad = np.zeros(n, dtype=bool)
+    if where:
+        w, t, e = eval_prog(where, cols, n)
+        if t == F64:
+            raise ProgramError("WHERE is float64")
+        ok = w != 0
+        bad |= e
+    values, masks, spec, types = [], [], [], []
+    for a, (op, val, mask) in enumerate(aggs):
+        m = None
+        if mask:
+            mv, mt, me = eval_prog(mask, cols, n)
+            m = mv != 0
+            bad |= ok & me
+        take = ok if m is None else ok & m
+        if op == 1:
+            types.append(I64)
+            spec.append((1, 0, ()))
+        else:
+            v, t, e = eval_prog(val, cols, n)
+            bad |= take & e
+            types.append(t)
+            values.append(v)
+            spec.append((op, 0, (len(values) - 1,)))
+        masks.append(m)
+    if bad.any():
+        raise DivisionByZero("division by zero in an expression")
+    kk = list(keys) if keys else [np.zeros(n, dtype=np.int64)]
+    ok_keys, words = orc.groupby(kk, spec, values=values, row_mask=ok, agg_masks=masks)
+    return ok_keys, words, types

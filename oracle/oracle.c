@@ -242,6 +242,7 @@ static double eval_f64(const orc_agg_spec *s, int a, uint64_t i) {
 }
 
 static int row_passes(const orc_agg_spec *s, uint64_t i) {
+  if (s->row_mask && !s->row_mask[i]) return 0;
   for (int p = 0; p < s->npred; ++p) {
     if (s->pred_type[p] == ORC_T_I64) {
       if (!cmp_i64(((const int64_t *)s->pred_col[p])[i], s->pred_op[p], s->pred_i64[p])) return 0;
@@ -260,6 +261,7 @@ static int agg_is_i64(const orc_agg_spec *s, int a) {
 static void grp_update(grp_t *g, const orc_agg_spec *s, uint64_t i) {
   for (int a = 0; a < s->naggs; ++a) {
     int op = s->agg_op[a];
+    if (s->agg_mask[a] && !s->agg_mask[a][i]) continue;
     if (op == ORC_AGG_COUNT) {
       g->w[a] += 1;
       continue;

@@ -67,12 +67,17 @@ typedef struct {
   int64_t pred_i64[6];
   double pred_f64[6];
   int nvals;                 /* value columns referenced by expressions */
-  const void *val_col[4];
-  int val_type[4];
+  const void *val_col[8];
+  int val_type[8];
   int naggs;
   int agg_op[8];             /* ORC_AGG_* */
   int agg_expr[8];           /* ORC_EX_* */
   int agg_arg[8][3];         /* value-column indices */
+  /* expression mode (oracle/expr.py evaluates the programs with numpy): rows pass only
+   * where row_mask[i] != 0; aggregate a takes only rows where agg_mask[a][i] != 0.
+   * NULL = every row. */
+  const uint8_t *row_mask;
+  const uint8_t *agg_mask[8];
 } orc_agg_spec;
 
 /* Result: groups sorted ascending by key tuple.  Each aggregate is one 64-bit

@@ -35,12 +35,14 @@ class OrcAggSpec(C.Structure):
         ("pred_i64", C.c_int64 * 6),
         ("pred_f64", C.c_double * 6),
         ("nvals", C.c_int),
-        ("val_col", C.c_void_p * 4),
-        ("val_type", C.c_int * 4),
+        ("val_col", C.c_void_p * 8),
+        ("val_type", C.c_int * 8),
         ("naggs", C.c_int),
         ("agg_op", C.c_int * 8),
         ("agg_expr", C.c_int * 8),
         ("agg_arg", (C.c_int * 3) * 8),
+        ("row_mask", C.c_void_p),
+        ("agg_mask", C.c_void_p * 8),
     ]
 
 
@@ -93,12 +95,22 @@ def filter_i64(col: np.ndarray, op: int, k: int) -> np.ndarray:
     return out[:cnt]
 
 
-def groupby(keys, aggs, values=(), preds=(), nthreads=0, cap=None):
+def groupby(keys, aggs, values=(), preds=(), nthreads=0, cap=None, row_mask=None, agg_masks=None):
     """keys: list of int64 arrays; values: list of arrays; preds: (array, op_int, literal);
-    aggs: (op_int, expr_int, args).  Returns (keys [n, nk] int64, words [n, na] uint64)
-    sorted by key tuple."""
+    aggs: (op_int, expr_int, args).  row_mask / agg_masks[a]: optional bool arrays (the
+    expression-mode WHERE and per-aggregate row masks, oracle/expr.py).  Returns
+    (keys [n, nk] int64, words [n, na] uint64) sorted by key tuple."""
     keep = []
     s = OrcAggSpec()
+    if row_mask is not None:
+        m = np.ascontiguousarray(row_mask, dtype=np.uint8)
+        keep.append(m)
+        s.row_mask = m.ctypes.data
+    for a, am in enumerate(agg_masks or ()):
+        if am is not None:
+            m = np.ascontiguousarray(am, dtype=np.uint8)
+            keep.append(m)
+            s.agg_mask[a] = m.ctypes.data
     n = len(keys[0])
     s.n = n
     s.nkeys = len(keys)
