@@ -45,7 +45,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--workload", default="q1", choices=["q1", "groupby", "filter", "sort", "parse"])
+    p.add_argument("--workload", default="q1", choices=["q1", "groupby", "filter", "sort", "q12expr", "parse"])
     p.add_argument("--rows", type=float, default=None, help="rows per GPU (default: config size)")
     p.add_argument("--groups", type=int, default=1000, help="groupby: distinct keys")
     p.add_argument("--selectivity", type=float, default=0.5, help="filter: fraction selected")
@@ -174,6 +174,32 @@ class Sort:
                 "xgmi_bytes_per_row": 8.0 * (self.world - 1) / self.world}
 
 
+class Q12Expr:
+    """Expression mode: the reference fixture tests/sql/5.sql (TPC-H Q12
+    shape, integer codes for its strings) through SQL -> plan -> a kernel compiled for
+    the query.  Column-vs-column predicates, IN, CASE inside SUM.  Single GPU."""
+    name = "q12_shape_expression_groupby"
+    cols_bytes = 56
+    kernel_kind = 1
+
+    def __init__(self, ex, rows, row0):
+        from nutdb_amd.sql import Plan
+        from nutdb_amd.workloads import Q12_COLS, Q12_SQL, gen
+        self.ex = ex
+        self.cols = {spec[0]: gen(ex, spec, rows, row0=row0) for spec in Q12_COLS}
+        self.plan = Plan(Q12_SQL)
+        self.rows = rows
+
+    def run(self):
+        return self.plan.execute(self.ex, self.cols, group_hint=8)
+
+    def config(self):
+        return {"workload": self.name, "query": "reference tests/sql/5.sql (TPC-H Q12 shape; integer codes for "
+                "its strings): 4 column-vs-column / IN predicates, 2 x SUM(CASE ...), GROUP BY l_shipmode",
+                "columns": "7 x 8 B (i64)", "groups": 2, "bytes_per_row": 56,
+                "kernel": "expression mode (hipRTC-compiled per query shape)"}
+
+
 # ------------------------------------------------------------------ one step
 def groupby_step(w, rank, world, group):
     """Local scan -> (N>1) all-to-all of partial groups by owner -> owner merge ->
@@ -209,6 +235,11 @@ def cpu_baseline(args, workload: str, target_s: float):
         if workload == "sort":
             col = orc.gen(SORT_COL, n)
             return lambda: orc.sort_i64(col)
+        if workload == "q12expr":
+            from nutdb_amd.workloads import Q12_AGGS, Q12_COLS, Q12_WHERE
+            from oracle.expr import groupby_prog
+            cols = [orc.gen(s, n) for s in Q12_COLS]
+            return lambda: groupby_prog([cols[2]], cols, Q12_WHERE, Q12_AGGS)
         col = orc.gen(FILTER_COL, n)
         k = filter_k(args.selectivity)
         return lambda: orc.filter_i64(col, 0, k)
@@ -219,7 +250,7 @@ def cpu_baseline(args, workload: str, target_s: float):
         return time.perf_counter() - t0
 
     full = int(args.rows) if args.rows else {"q1": 10**9, "groupby": 10**9, "filter": 10**8,
-                                             "sort": 1_250_000_000}[workload]
+                                             "sort": 1_250_000_000, "q12expr": 10**9}[workload]
     probe = min(full, 4_000_000)
     per_row = timed(prepare(probe)) / probe
     sample = int(min(full, max(probe, target_s / max(per_row, 1e-12))))
@@ -230,7 +261,9 @@ def cpu_baseline(args, workload: str, target_s: float):
     dt = min(times)
     return {"value": sample / dt, "unit": "rows/s", "cores": threads, "kind": "port",
             "sample": f"{sample:.3g} rows of the same synthetic workload ({sample / full:.2f} of one GPU's "
-                      f"rows), C oracle (oracle/oracle.c), OpenMP over {threads} host threads, generation "
+                      f"rows), " + ("numpy expression oracle (oracle/expr.py, 1 thread) + " if workload == "q12expr"
+                                    else "") +
+                      f"C oracle (oracle/oracle.c), OpenMP over {threads} host threads, generation "
                       f"excluded, best of {len(times)} timed scans = {dt:.3f} s"}
 
 
@@ -292,7 +325,7 @@ def main():
         group = dist.group.WORLD
     from nutdb_amd import Executor
     ex = Executor(local_rank)
-    default_rows = {"q1": 1e9, "groupby": 1e9, "filter": 1e8, "sort": 1.25e9}[args.workload]
+    default_rows = {"q1": 1e9, "groupby": 1e9, "filter": 1e8, "sort": 1.25e9, "q12expr": 1e9}[args.workload]
     rows = int(args.rows or default_rows)
     row0 = rank * rows
     if args.workload == "q1":
@@ -301,12 +334,17 @@ def main():
         w = GroupBy(ex, rows, row0, args.groups)
     elif args.workload == "sort":
         w = Sort(ex, rows, row0, world, group)
+    elif args.workload == "q12expr":
+        if world > 1:
+            print("bench.py: q12expr is a single-GPU workload", file=sys.stderr)
+            sys.exit(2)
+        w = Q12Expr(ex, rows, row0)
     else:
         w = Filter(ex, rows, row0, args.selectivity)
     torch.cuda.synchronize()
 
     def step():
-        if args.workload in ("filter", "sort"):
+        if args.workload in ("filter", "sort", "q12expr"):
             w.run()
         else:
             groupby_step(w, rank, world, group)

@@ -43,6 +43,44 @@ Q1_COLS = [
 # config 5: SELECT k FROM t ORDER BY k     full-range random i64
 SORT_COL = ("k", L.GEN_FULL_I64, 0x50, 0, 0, 1.0)
 
+# Expression-mode workload: the reference fixture tests/sql/5.sql (TPC-H Q12 shape) with
+# integer codes for its strings; 7 int64 columns = 56 B/row.
+Q12_COLS = [
+    ("o_orderkey", L.GEN_RANGE_I64, 0x61, 0, 4, 1.0),
+    ("l_orderkey", L.GEN_RANGE_I64, 0x62, 0, 4, 1.0),
+    ("l_shipmode", L.GEN_RANGE_I64, 0x63, 0, 7, 1.0),
+    ("o_orderpriority", L.GEN_RANGE_I64, 0x64, 1, 5, 1.0),
+    ("l_shipdate", L.GEN_RANGE_I64, 0x65, 8000, 2000, 1.0),
+    ("l_commitdate", L.GEN_RANGE_I64, 0x66, 8000, 2000, 1.0),
+    ("l_receiptdate", L.GEN_RANGE_I64, 0x67, 8000, 2000, 1.0),
+]
+Q12_SQL = """select l_shipmode,
+    sum(case when o_orderpriority = 1 or o_orderpriority = 2 then 1 else 0 end) as high_line_count,
+    sum(case when o_orderpriority <> 1 and o_orderpriority <> 2 then 1 else 0 end) as low_line_count
+  from orders
+  where o_orderkey = l_orderkey and l_shipmode in (3, 5) and l_commitdate < l_receiptdate
+    and l_shipdate < l_commitdate
+  group by l_shipmode
+  order by l_shipmode"""
+# the same query as the expression programs the planner lowers it to (column order
+# = Q12_COLS), for the CPU baseline / oracle (oracle/expr.py)
+_C = {name: i for i, (name, *_rest) in enumerate(Q12_COLS)}
+
+
+def _col(n):
+    return ("col", _C[n])
+
+
+Q12_WHERE = [_col("o_orderkey"), _col("l_orderkey"), ("eq",), _col("l_shipmode"), ("i64", 0, 3), ("eq",),
+             _col("l_shipmode"), ("i64", 0, 5), ("eq",), ("or",), ("and",), _col("l_commitdate"),
+             _col("l_receiptdate"), ("lt",), ("and",), _col("l_shipdate"), _col("l_commitdate"), ("lt",), ("and",)]
+Q12_AGGS = [
+    (0, [_col("o_orderpriority"), ("i64", 0, 1), ("eq",), _col("o_orderpriority"), ("i64", 0, 2), ("eq",), ("or",),
+         ("i64", 0, 1), ("i64", 0, 0), ("if",)], None),
+    (0, [_col("o_orderpriority"), ("i64", 0, 1), ("ne",), _col("o_orderpriority"), ("i64", 0, 2), ("ne",), ("and",),
+         ("i64", 0, 1), ("i64", 0, 0), ("if",)], None),
+]
+
 
 def gen(ex, spec, n: int, row0: int = 0):
     """Generate one column on ex's device."""

@@ -15,7 +15,8 @@ from prof_summary import summarize  # noqa: E402
 WORKLOAD_KERNEL = {"q1": ("tpch_q1_shape_filter_groupby", "agg_kernel"),
                    "groupby": ("groupby_i64_sum_f64", "agg_kernel"),
                    "filter": ("filter_i64_compaction", "filter_i64_kernel"),
-                   "sort": ("sort_i64_radix", "rs_")}
+                   "sort": ("sort_i64_radix", "rs_"),
+                   "q12expr": ("q12_shape_expression_groupby", "agg_kernel")}
 # sort: one step = histogram kernel + every radix pass; traffic is summed per step
 STEP_KERNEL = {"sort": "rs_hist_kernel"}
 
@@ -25,7 +26,7 @@ def main():
     args = sys.argv[2:]
     wl = args[args.index("--workload") + 1] if "--workload" in args else "q1"
     rows = float(args[args.index("--rows") + 1]) if "--rows" in args else {"q1": 1e9, "groupby": 1e9, "filter": 1e8,
-                                                                           "sort": 1.25e9}[wl]
+                                                                           "sort": 1.25e9, "q12expr": 1e9}[wl]
     name, match = WORKLOAD_KERNEL[wl]
     s = summarize(d, match, STEP_KERNEL.get(wl, ""))
     c = s["counters"]

@@ -258,3 +258,17 @@ def test_sql_compiled_global_aggregate(ex):
     assert vals[2].tolist() == [np.max(sel / 4)]
     empty = ex.sql("select count(*), sum(a) from t where a > 5000 or a < -1", {"a": dev(a, ex)})
     assert [v.tolist() for v in empty.values()] == [[0], [0]]
+
+
+def test_bench_q12_programs_match_sql(ex):
+    """bench.py q12expr's CPU baseline evaluates hand-written programs (workloads.py):
+    they must be the query the SQL path runs."""
+    from nutdb_amd.workloads import Q12_AGGS, Q12_COLS, Q12_SQL, Q12_WHERE, gen
+    n = 2_000_003
+    cols = {s[0]: gen(ex, s, n) for s in Q12_COLS}
+    got = ex.sql(Q12_SQL, cols, group_hint=8)
+    host = [cols[s[0]].cpu().numpy() for s in Q12_COLS]
+    ok, ow, _ = groupby_prog([host[2]], host, Q12_WHERE, Q12_AGGS)
+    assert got["l_shipmode"].tolist() == ok[:, 0].tolist() == [3, 5]
+    assert got["high_line_count"].tolist() == ow[:, 0].astype(np.int64).tolist()
+    assert got["low_line_count"].tolist() == ow[:, 1].astype(np.int64).tolist()
