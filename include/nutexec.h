@@ -123,7 +123,7 @@ nut_status nut_filter_i64_async(nut_ctx *ctx, const int64_t *col, uint64_t n, in
  * Lowered from WhereClause (AND-chain of `col op literal`), GroupByClause.keys
  * (identifiers) and the SELECT list's FnCall{Others("sum"|"count"|"min"|"max")}.
  * ------------------------------------------------------------------------ */
-typedef enum { NUT_T_I64 = 0, NUT_T_F64 = 1 } nut_type;
+typedef enum { NUT_T_I64 = 0, NUT_T_F64 = 1, NUT_T_STR = 2 /* result columns of typed tables only */ } nut_type;
 typedef enum { NUT_AGG_SUM = 0, NUT_AGG_COUNT = 1, NUT_AGG_MIN = 2, NUT_AGG_MAX = 3 } nut_agg_op;
 typedef enum {
   NUT_EX_COL = 0,       /* v[a]                      (i64 or f64 column) */
@@ -374,7 +374,47 @@ nut_status nut_result_to_host(const nut_result *res, int j, void *dst, uint64_t 
 /* FILTER/SORT results stay in HBM: device pointer of the nrows output values.
  * NUT_ERR_UNSUPPORTED for GROUPBY results (those are materialised on the host). */
 nut_status nut_result_device(const nut_result *res, const void **dev);
+/* row of a NUT_T_STR output column (a string group key of a typed table); the bytes
+ * are owned by res and not NUL-terminated */
+nut_status nut_result_string(const nut_result *res, int j, uint64_t row, const char **s, size_t *len);
 void nut_result_free(nut_result *res);
+
+/* ========================================================================
+ * Typed tables from CREATE TABLE
+ * A CREATE TABLE statement (TableDef, src/parser/ast/stmt.rs; column types
+ * ScalarDataType / CompoundDataType, ast/item.rs:14-68) gives an empty table whose
+ * columns live in HBM in the executed representation:
+ *   Int8..Int64, UInt8..UInt64, Serial*  -> int64   (UInt64 >= 2^63 rejected)
+ *   Boolean -> int64 0/1; Date / Datetime -> int64 days / seconds since 1970-01-01
+ *   Float32 / Float64 -> f64
+ *   String, Chars(n), Dictionary(String) -> int64 codes of the table's dictionary
+ *   Enum('a' = 1, ...) -> int64 declared ids;  Nullable(T) -> T (NULLs rejected)
+ * Int128/UInt128, Decimal, Uuid, Array, Tuple, Map: NUT_ERR_UNSUPPORTED at create.
+ * Plans execute against a table by column name; string constants bind to dictionary
+ * codes (= / != / IN, CASE x WHEN 'a'), string group keys come back as NUT_T_STR.
+ * ======================================================================== */
+typedef struct nut_table nut_table;
+typedef enum {
+  NUT_COL_INT = 0, NUT_COL_UINT = 1, NUT_COL_FLOAT = 2, NUT_COL_BOOL = 3,
+  NUT_COL_DATE = 4, NUT_COL_DATETIME = 5, NUT_COL_STRING = 6, NUT_COL_ENUM = 7
+} nut_col_kind;
+
+nut_status nut_table_create(const char *sql, size_t len, nut_table **out);
+nut_status nut_table_shape(const nut_table *t, int *ncols, uint64_t *nrows);
+/* kind: nut_col_kind; width: bytes per appended host value (numeric kinds) */
+nut_status nut_table_column_info(const nut_table *t, int j, const char **name, int *kind, int *width,
+                                 int *exec_type);
+/* Append n values to column j (host memory -> HBM on ctx's device; narrow integers and
+ * Float32 are widened by a GPU kernel).  Numeric kinds: `data` holds n values of the
+ * column's width (little-endian; BOOL 1 B; DATE / DATETIME int64).  STRING / ENUM:
+ * n UTF-8 strings, string i = data[offsets[i] .. offsets[i+1]).  A table's rows are the
+ * rows every column has. */
+nut_status nut_table_append(nut_ctx *ctx, nut_table *t, int j, const void *data, const int64_t *offsets,
+                            uint64_t n);
+/* Execute a plan against the table (binds every plan column by name). */
+nut_status nut_table_execute(nut_ctx *ctx, nut_table *t, const nut_plan *plan, uint64_t group_hint,
+                             nut_result **out);
+void nut_table_free(nut_table *t);
 
 #ifdef __cplusplus
 }

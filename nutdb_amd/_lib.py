@@ -36,7 +36,8 @@ STATUS_NAMES = {
 # enums (include/nutexec.h)
 GEN_U62, GEN_FULL_I64, GEN_POOL_KEY, GEN_DYADIC, GEN_UNIT_F64, GEN_RANGE_I64, GEN_RANGE_F64 = range(7)
 LT, LE, GT, GE, EQ, NE, IN, NOT_IN = range(8)
-T_I64, T_F64 = 0, 1
+T_I64, T_F64, T_STR = 0, 1, 2
+COL_KINDS = ["int", "uint", "float", "bool", "date", "datetime", "string", "enum"]
 KERNEL_FILTER, KERNEL_AGGREGATE, KERNEL_SORT = 0, 1, 2
 AGG_SUM, AGG_COUNT, AGG_MIN, AGG_MAX = range(4)
 EX_COL, EX_MUL, EX_ADD, EX_SUB, EX_MUL_1M, EX_MUL_1M_1P = range(6)
@@ -133,6 +134,14 @@ SIGNATURES = {
     "nut_groupby_jit_source": (_I32, [C.POINTER(NutAggSpec), C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
     "nut_groupby_jit_compile": (_I32, [C.POINTER(NutAggSpec)]),
     "nut_plan_prepare": (_I32, [_P, C.POINTER(NutColumn), _I32]),
+    "nut_result_string": (_I32, [_P, _I32, _U64, C.POINTER(C.c_char_p), C.POINTER(C.c_size_t)]),
+    "nut_table_create": (_I32, [C.c_char_p, C.c_size_t, C.POINTER(_P)]),
+    "nut_table_shape": (_I32, [_P, C.POINTER(_I32), C.POINTER(_U64)]),
+    "nut_table_column_info": (_I32, [_P, _I32, C.POINTER(C.c_char_p), C.POINTER(_I32), C.POINTER(_I32),
+                                     C.POINTER(_I32)]),
+    "nut_table_append": (_I32, [_P, _P, _I32, _P, _P, _U64]),
+    "nut_table_execute": (_I32, [_P, _P, _P, _U64, C.POINTER(_P)]),
+    "nut_table_free": (None, [_P]),
     "nut_groups_size": (_I32, [_P, C.POINTER(_U64)]),
     "nut_groups_to_host": (_I32, [_P, _P, _P, _U64]),
     "nut_groups_to_device": (_I32, [_P, _P, _U64]),

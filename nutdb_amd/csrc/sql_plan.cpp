@@ -28,6 +28,7 @@
 #include "common.hpp"
 #include "sql_ast.hpp"
 #include "sql_lexer.hpp"
+#include "table.hpp"
 
 using namespace nut;
 using namespace nut::sql;
@@ -91,6 +92,8 @@ struct CVal {
   bool is_int = true;
   i128 v = 0;        // integer value (saturated to +/-kHuge)
   Decimal dec;       // float value
+  bool is_str = false;  // string constant (binds to a dictionary code at execution)
+  std::string s;
 };
 
 i128 sat_from_u128(u128 m, bool neg) {
@@ -175,6 +178,12 @@ bool const_eval(const Expr &e, CVal &out, Lowering &L) {
       out.dec = l.dec;
       return true;
     }
+    if (l.k == LitKind::String) {
+      out.is_int = false;
+      out.is_str = true;
+      out.s = l.str;
+      return true;
+    }
     return false;
   }
   if (e.k == EK::FnCall && e.fn() == FnKind::Others && ieq(e.id.name, "todate") && e.kids.size() == 1 &&
@@ -213,7 +222,7 @@ bool const_eval(const Expr &e, CVal &out, Lowering &L) {
   return false;
 }
 
-std::string cval_str(const CVal &c) { return c.is_int ? i128_str(c.v) : c.dec.str(); }
+std::string cval_str(const CVal &c) { return c.is_str ? "'" + c.s + "'" : c.is_int ? i128_str(c.v) : c.dec.str(); }
 
 // floor of an exact decimal, saturated; frac = true if it had a fractional part
 i128 dec_floor(const Decimal &d, bool &frac) {
@@ -316,6 +325,7 @@ struct nut_result {
   void *dev = nullptr;  // FILTER/SORT: owned device buffer
   uint64_t dev_off = 0;
   std::vector<std::vector<uint64_t>> host;  // GROUPBY: output columns (int64 / f64 bits)
+  std::vector<std::vector<std::string>> strs;  // NUT_T_STR columns, decoded (others empty)
 };
 
 namespace {
@@ -437,7 +447,9 @@ bool same_prog(const PProg &x, const PProg &y) {
   for (size_t i = 0; i < x.size(); ++i) {
     const PNode &a = x[i], &b = y[i];
     if (a.op != b.op || a.col != b.col) return false;
-    if (a.op == NUT_P_I64 && !(a.c.is_int == b.c.is_int && a.c.v == b.c.v)) return false;
+    if (a.op == NUT_P_I64 && !(a.c.is_int == b.c.is_int && a.c.v == b.c.v && a.c.is_str == b.c.is_str &&
+                               a.c.s == b.c.s))
+      return false;
     if (a.op == NUT_P_F64 && !(a.c.dec == b.c.dec)) return false;
   }
   return true;
@@ -489,6 +501,12 @@ int prog_binop(BinOp b) {
 }
 
 bool is_null_lit(const Expr &e) { return e.k == EK::Literal && e.lit->k == LitKind::Null; }
+// a string constant compared (= / != / IN / CASE x WHEN) with a column takes that
+// column's dictionary at execution
+void bind_str(PProg &a, const PProg &other) {
+  if (a.size() == 1 && a[0].op == NUT_P_I64 && a[0].c.is_str && other.size() == 1 && other[0].op == NUT_P_COL)
+    a[0].col = other[0].col;
+}
 bool is_agg_name(sv n) {
   return ieq(n, "sum") || ieq(n, "count") || ieq(n, "min") || ieq(n, "max") || ieq(n, "avg");
 }
@@ -525,8 +543,10 @@ bool conditional(nut_plan &p, const Expr &e, std::vector<PProg> &conds, std::vec
     PProg x;
     if (!lower_prog(p, e.kids[0], x, L)) return ok = false, true;
     for (size_t i = 1; i + 1 < n; i += 2) {
-      PProg c = x;
-      if (!lower_prog(p, e.kids[i], c, L)) return ok = false, true;
+      PProg c = x, v;
+      if (!lower_prog(p, e.kids[i], v, L)) return ok = false, true;
+      bind_str(v, x);
+      append(c, v);
       emit(c, NUT_P_EQ);
       conds.push_back(std::move(c));
       vals.push_back(&e.kids[i + 1]);
@@ -550,7 +570,7 @@ bool lower_prog(nut_plan &p, const Expr &e, PProg &o, Lowering &L) {
   CVal c;
   if (const_eval(e, c, L)) {
     PNode n;
-    n.op = c.is_int ? NUT_P_I64 : NUT_P_F64;
+    n.op = c.is_int || c.is_str ? NUT_P_I64 : NUT_P_F64;
     n.c = c;
     o.push_back(n);
     return true;
@@ -572,7 +592,6 @@ bool lower_prog(nut_plan &p, const Expr &e, PProg &o, Lowering &L) {
         return true;
       }
       if (is_null_lit(e)) return L.fail("NULL is executed only as a CASE/IF branch of an aggregate argument");
-      if (e.lit->k == LitKind::String) return L.fail("string constant '" + e.lit->str + "' (no string columns are executed)");
       return L.fail("literal '" + expr_text(e) + "' is not executed here");
     }
     case EK::BinaryOp: {
@@ -594,15 +613,25 @@ bool lower_prog(nut_plan &p, const Expr &e, PProg &o, Lowering &L) {
         if (!lower_prog(p, e.kids[0], x, L)) return false;
         for (size_t i = 0; i < items.size(); ++i) {
           append(o, x);
-          if (!lower_prog(p, *items[i], o, L)) return false;
+          PProg it;
+          if (!lower_prog(p, *items[i], it, L)) return false;
+          bind_str(it, x);
+          append(o, it);
           emit(o, in ? NUT_P_EQ : NUT_P_NE);
           if (i) emit(o, in ? NUT_P_OR : NUT_P_AND);
         }
         return true;
       }
       const int op = prog_binop(b);
-      if (op < 0) return L.fail("operator in '" + expr_text(e) + "' is not executed (no string columns)");
-      if (!lower_prog(p, e.kids[0], o, L) || !lower_prog(p, e.kids[1], o, L)) return false;
+      if (op < 0) return L.fail("operator in '" + expr_text(e) + "' is not executed (LIKE, [] and friends)");
+      PProg l, r;
+      if (!lower_prog(p, e.kids[0], l, L) || !lower_prog(p, e.kids[1], r, L)) return false;
+      if (op == NUT_P_EQ || op == NUT_P_NE) {
+        bind_str(l, r);
+        bind_str(r, l);
+      }
+      append(o, l);
+      append(o, r);
       emit(o, op);
       return true;
     }
@@ -874,6 +903,7 @@ bool lower_having(nut_plan &p, const Expr &e, HNode &h, Lowering &L) {
     CVal c;
     Lowering quiet;
     if (const_eval(x, c, quiet)) {
+      if (c.is_str) return L.fail("string constants in HAVING are not executed");
       o.k = H_CONST;
       if (c.is_int && c.v <= INT64_MAX && c.v >= INT64_MIN) {
         o.is_int = true;
@@ -1104,7 +1134,7 @@ std::string describe(const nut_plan &p) {
       for (size_t j = 0; j < pr.set.size(); ++j) o += (j ? ",\"" : "\"") + cval_str(pr.set[j]) + "\"";
       o += "]}";
     } else {
-      o += "\",\"value\":\"" + cval_str(pr.c) + "\",\"value_kind\":\"" + (pr.c.is_int ? "int" : "decimal") + "\"}";
+      o += "\",\"value\":\"" + cval_str(pr.c) + "\",\"value_kind\":\"" + (pr.c.is_str ? "string" : pr.c.is_int ? "int" : "decimal") + "\"}";
     }
   }
   o += "]";
@@ -1242,8 +1272,13 @@ struct DevBuf {
   }
 };
 
-nut_status exec_scan(nut_ctx *c, const nut_plan &p, const nut_column *const *bound, uint64_t n, nut_result *r) {
+nut_status exec_scan(nut_ctx *c, const nut_plan &p, const nut_column *const *bound, const Dict *const *dicts,
+                     uint64_t n, nut_result *r) {
   const nut_column *col = bound[p.proj];
+  if (dicts && dicts[p.proj])
+    return fail(NUT_ERR_PLAN, "column '" + p.cols[p.proj] + "' holds strings: scans / sorts of strings are not executed");
+  for (const PlanPred &pr : p.preds)
+    if (pr.c.is_str) return fail(NUT_ERR_PLAN, "string constant " + cval_str(pr.c) + " compared with an int64 column");
   if (col->type != NUT_T_I64) return fail(NUT_ERR_PLAN, "column '" + p.cols[p.proj] + "' must be int64 for a scan/sort");
   r->names.push_back(p.outs[0].name);
   r->types.push_back(NUT_T_I64);
@@ -1338,8 +1373,40 @@ bool having_true(const HNode &h, const std::vector<std::vector<uint64_t>> &cols,
 }
 
 // the nut_agg_spec of an aggregate plan over bound columns (program nodes live in store)
-nut_status build_spec(const nut_plan &p, const nut_column *const *bound, uint64_t n, nut_agg_spec &s,
-                      std::deque<std::vector<nut_prog_node>> &store, std::vector<int> &agg_f64) {
+// String programs: a dictionary column or string constant may only meet another string
+// in = / != (IN and CASE x WHEN lower to those), or be a GROUP BY key.
+nut_status check_strings(const nut_plan &p, const PProg &pp, const Dict *const *dicts, const char *what) {
+  std::vector<char> st;
+  for (const PNode &n : pp) {
+    const int op = n.op;
+    const int k = op <= NUT_P_F64 ? 0 : (op == NUT_P_NOT || op == NUT_P_BITNOT || op == NUT_P_ABS ||
+                                         op == NUT_P_TO_F64) ? 1 : op == NUT_P_IF ? 3 : 2;
+    char a[3] = {0, 0, 0};
+    for (int i = k - 1; i >= 0; --i) {
+      if (st.empty()) return NUT_OK;  // malformed: nut_prog_type reports it
+      a[i] = st.back();
+      st.pop_back();
+    }
+    if (op == NUT_P_COL) {
+      st.push_back(dicts[n.col] != nullptr);
+      continue;
+    }
+    if (op == NUT_P_I64 || op == NUT_P_F64) {
+      st.push_back(n.c.is_str);
+      continue;
+    }
+    if ((op == NUT_P_EQ || op == NUT_P_NE) && a[0] != a[1])
+      return fail(NUT_ERR_PLAN, std::string(what) + ": a string compared with a number");
+    if (!(op == NUT_P_EQ || op == NUT_P_NE) && (a[0] || a[1] || a[2]))
+      return fail(NUT_ERR_PLAN, std::string(what) + ": strings are executed in = / != / IN and as GROUP BY keys only");
+    st.push_back(0);
+  }
+  if (!st.empty() && st.back()) return fail(NUT_ERR_PLAN, std::string(what) + ": a string value (only count() takes strings)");
+  return NUT_OK;
+}
+
+nut_status build_spec(const nut_plan &p, const nut_column *const *bound, const Dict *const *dicts, uint64_t n,
+                      nut_agg_spec &s, std::deque<std::vector<nut_prog_node>> &store, std::vector<int> &agg_f64) {
   memset(&s, 0, sizeof s);
   s.n = p.never ? 0 : n;
   s.nkeys = (int32_t)p.keys.size();
@@ -1367,6 +1434,17 @@ nut_status build_spec(const nut_plan &p, const nut_column *const *bound, uint64_
             s.nprog_cols++;
           }
           q.arg = pcol[n.col];
+        } else if (n.op == NUT_P_I64 && n.c.is_str) {
+          // dictionary code of the compared column (-1 = absent: equal to no row);
+          // dicts == NULL: compile-only (nut_plan_prepare), the code does not matter
+          if (dicts) {
+            if (n.col < 0 || !dicts[n.col])
+              return fail(NUT_ERR_PLAN, std::string(what) + ": string constant " + cval_str(n.c) +
+                                            " must be compared (= / != / IN) with a string column");
+            q.v = dicts[n.col]->find(n.c.s);
+          } else {
+            q.v = -1;
+          }
         } else if (n.op == NUT_P_I64) {
           if (n.c.v > INT64_MAX || n.c.v < INT64_MIN)
             return fail(NUT_ERR_PLAN, "integer constant " + cval_str(n.c) + " is outside int64");
@@ -1379,6 +1457,10 @@ nut_status build_spec(const nut_plan &p, const nut_column *const *bound, uint64_
       }
       out.n = (int32_t)v.size();
       out.node = v.data();
+      if (dicts) {
+        nut_status cs = check_strings(p, pp, dicts, what);
+        if (cs) return cs;
+      }
       if (!type) return NUT_OK;
       if (nut_prog_type(&out, s.prog_col_type, NUT_MAX_PROG_COLS, type))
         return fail(NUT_ERR_PLAN, std::string(what) + ": " + nut_last_error());
@@ -1404,6 +1486,35 @@ nut_status build_spec(const nut_plan &p, const nut_column *const *bound, uint64_
   } else {
     for (const PlanPred &pr : p.preds) {
       const nut_column *col = bound[pr.col];
+      const Dict *dc = dicts ? dicts[pr.col] : nullptr;
+      bool any_str = pr.c.is_str;
+      for (const CVal &v : pr.set) any_str = any_str || v.is_str;
+      if (dc || any_str) {
+        // strings: = / != / IN against dictionary codes (absent string: equal to no row)
+        const std::string &cn = p.cols[pr.col];
+        if (!dc) return fail(NUT_ERR_PLAN, "string constant compared with the non-string column '" + cn + "'");
+        if (pr.op != NUT_EQ && pr.op != NUT_NE && pr.op < NUT_IN)
+          return fail(NUT_ERR_PLAN, "ordering comparison on the string column '" + cn +
+                                        "' (dictionary codes are unordered)");
+        std::vector<int64_t> codes;
+        for (const CVal &v : pr.op >= NUT_IN ? pr.set : std::vector<CVal>{pr.c}) {
+          if (!v.is_str) return fail(NUT_ERR_PLAN, "string column '" + cn + "' compared with a number");
+          const int64_t code = dc->find(v.s);
+          if (code >= 0) codes.push_back(code);
+        }
+        const bool positive = pr.op == NUT_EQ || pr.op == NUT_IN;
+        if (codes.empty()) {
+          if (positive) s.n = 0;  // equal to no row; the negated form keeps every row
+          continue;
+        }
+        s.pred_col[s.npred] = col->data;
+        s.pred_type[s.npred] = NUT_T_I64;
+        s.pred_op[s.npred] = positive ? NUT_IN : NUT_NOT_IN;
+        s.pred_nset[s.npred] = (int32_t)codes.size();
+        for (size_t j = 0; j < codes.size(); ++j) s.pred_set[s.npred][j] = codes[j];
+        s.npred++;
+        continue;
+      }
       if (pr.op >= NUT_IN) {
         // keep the set values the column type can hold (a non-integral or out-of-range
         // constant never equals an int64)
@@ -1455,6 +1566,8 @@ nut_status build_spec(const nut_plan &p, const nut_column *const *bound, uint64_
     }
     s.nvals = (int32_t)p.vals.size();
     for (size_t v = 0; v < p.vals.size(); ++v) {
+      if (dicts && dicts[p.vals[v]])
+        return fail(NUT_ERR_PLAN, "aggregate over the string column '" + p.cols[p.vals[v]] + "' (only count)");
       s.val_col[v] = bound[p.vals[v]]->data;
       s.val_type[v] = bound[p.vals[v]]->type;
     }
@@ -1484,12 +1597,12 @@ nut_status build_spec(const nut_plan &p, const nut_column *const *bound, uint64_
   return NUT_OK;
 }
 
-nut_status exec_groupby(nut_ctx *c, const nut_plan &p, const nut_column *const *bound, uint64_t n, uint64_t hint,
-                        nut_result *r) {
+nut_status exec_groupby(nut_ctx *c, const nut_plan &p, const nut_column *const *bound, const Dict *const *dicts,
+                        uint64_t n, uint64_t hint, nut_result *r) {
   nut_agg_spec s;
   std::deque<std::vector<nut_prog_node>> store;  // program nodes, alive until nut_groupby returns
   std::vector<int> agg_f64;
-  nut_status bs = build_spec(p, bound, n, s, store, agg_f64);
+  nut_status bs = build_spec(p, bound, dicts, n, s, store, agg_f64);
   if (bs) return bs;
   nut_groups *g = nullptr;
   nut_status st = nut_groupby(c, &s, hint, &g);
@@ -1509,14 +1622,19 @@ nut_status exec_groupby(nut_ctx *c, const nut_plan &p, const nut_column *const *
     keys.assign(1, 0);
     words.assign(na + 1, 0);
   }
-  // output columns in SELECT order
+  // output columns in SELECT order (string keys stay codes until the end)
   r->host.resize(p.outs.size());
+  std::vector<const Dict *> out_dict(p.outs.size(), nullptr);
   for (size_t j = 0; j < p.outs.size(); ++j) {
     const PlanOut &o = p.outs[j];
     std::vector<uint64_t> &col = r->host[j];
     col.resize(ng);
     int type = NUT_T_I64;
     if (o.kind == OUT_KEY) {
+      if (dicts && dicts[p.keys[o.a]]) {
+        type = NUT_T_STR;
+        out_dict[j] = dicts[p.keys[o.a]];
+      }
       for (uint64_t i = 0; i < ng; ++i) col[i] = (uint64_t)keys[i * nk + o.a];
     } else if (o.kind == OUT_AGG) {
       type = agg_f64[o.a] ? NUT_T_F64 : NUT_T_I64;
@@ -1538,6 +1656,20 @@ nut_status exec_groupby(nut_ctx *c, const nut_plan &p, const nut_column *const *
     r->types.push_back(type);
   }
   // HAVING, then ORDER BY over outputs (groups arrive sorted by key tuple), then LIMIT
+  if (p.has_having) {
+    std::vector<const HNode *> todo{&p.having};
+    while (!todo.empty()) {
+      const HNode *h = todo.back();
+      todo.pop_back();
+      if (h->k == H_OUT && r->types[h->out] == NUT_T_STR)
+        return fail(NUT_ERR_PLAN, "HAVING on the string key '" + p.outs[h->out].name + "' is not executed");
+      for (const HNode &k : h->kids) todo.push_back(&k);
+    }
+  }
+  auto str_of = [&](size_t j, uint64_t i) -> std::string {
+    const std::string *t = out_dict[j]->decode((int64_t)r->host[j][i]);
+    return t ? *t : std::string();
+  };
   std::vector<uint64_t> idx;
   idx.reserve(ng);
   for (uint64_t i = 0; i < ng; ++i)
@@ -1548,7 +1680,10 @@ nut_status exec_groupby(nut_ctx *c, const nut_plan &p, const nut_column *const *
       for (const auto &ok : p.order) {
         const std::vector<uint64_t> &col = r->host[ok.first];
         int cmp;
-        if (r->types[ok.first] == NUT_T_F64) {
+        if (r->types[ok.first] == NUT_T_STR) {
+          const int c2 = str_of(ok.first, x).compare(str_of(ok.first, y));
+          cmp = c2 < 0 ? -1 : c2 > 0 ? 1 : 0;
+        } else if (r->types[ok.first] == NUT_T_F64) {
           double a, b;
           memcpy(&a, &col[x], 8);
           memcpy(&b, &col[y], 8);
@@ -1568,14 +1703,19 @@ nut_status exec_groupby(nut_ctx *c, const nut_plan &p, const nut_column *const *
   std::vector<std::vector<uint64_t>> vis;
   std::vector<std::string> names;
   std::vector<int> types;
+  std::vector<std::vector<std::string>> strs;
   for (size_t j = 0; j < p.outs.size(); ++j) {
     if (p.outs[j].hidden) continue;
     std::vector<uint64_t> out(rows);
     for (uint64_t i = 0; i < rows; ++i) out[i] = r->host[j][idx[off + i]];
+    strs.emplace_back();
+    if (r->types[j] == NUT_T_STR)
+      for (uint64_t i = 0; i < rows; ++i) strs.back().push_back(str_of(j, idx[off + i]));
     vis.push_back(std::move(out));
     names.push_back(r->names[j]);
     types.push_back(r->types[j]);
   }
+  r->strs.swap(strs);
   r->host.swap(vis);
   r->names.swap(names);
   r->types.swap(types);
@@ -1697,8 +1837,9 @@ nut_status nut_plan_execute(nut_ctx *c, const nut_plan *p, const nut_column *col
   r->kind = p->kind;
   r->device = c->device;
   DeviceGuard g(c->device);
-  nut_status st = p->kind == NUT_PLAN_GROUPBY ? exec_groupby(c, *p, bound.data(), nrows, group_hint, r)
-                                              : exec_scan(c, *p, bound.data(), nrows, r);
+  const std::vector<const Dict *> nodict(p->cols.size(), nullptr);  // raw columns carry no strings
+  nut_status st = p->kind == NUT_PLAN_GROUPBY ? exec_groupby(c, *p, bound.data(), nodict.data(), nrows, group_hint, r)
+                                              : exec_scan(c, *p, bound.data(), nodict.data(), nrows, r);
   if (st) {
     nut_result_free(r);
     return st;
@@ -1720,9 +1861,55 @@ nut_status nut_plan_prepare(const nut_plan *p, const nut_column *cols, int ncols
   nut_agg_spec s;
   std::deque<std::vector<nut_prog_node>> store;
   std::vector<int> agg_f64;
-  nut_status st = build_spec(*p, bound.data(), 0, s, store, agg_f64);
+  nut_status st = build_spec(*p, bound.data(), nullptr, 0, s, store, agg_f64);
   if (st) return st;
   return nut_groupby_jit_compile(&s);
+}
+
+nut_status nut_table_execute(nut_ctx *c, nut_table *t, const nut_plan *p, uint64_t group_hint, nut_result **out) {
+  if (!c || !t || !p || !out) return fail(NUT_ERR_INVALID_ARG, "nut_table_execute: NULL argument");
+  *out = nullptr;
+  if (t->ragged()) return fail(NUT_ERR_INVALID_ARG, "nut_table_execute: table '" + t->name + "' has ragged columns");
+  if (t->device >= 0 && t->device != c->device)
+    return fail(NUT_ERR_INVALID_ARG, "nut_table_execute: the table lives on another device");
+  const uint64_t nrows = t->rows();
+  std::vector<nut_column> cols(p->cols.size());
+  std::vector<const nut_column *> bound(p->cols.size());
+  std::vector<const Dict *> dicts(p->cols.size(), nullptr);
+  for (size_t i = 0; i < p->cols.size(); ++i) {
+    const TCol *tc = nullptr;
+    for (const TCol &x : t->cols)
+      if (ieq(x.name, p->cols[i])) tc = &x;
+    if (!tc) return fail(NUT_ERR_PLAN, "table '" + t->name + "' has no column '" + p->cols[i] + "'");
+    cols[i] = nut_column{tc->name.c_str(), tc->dev, tc->exec_type};
+    bound[i] = &cols[i];
+    dicts[i] = tc->dict;
+  }
+  nut_result *r = new (std::nothrow) nut_result;
+  if (!r) return fail(NUT_ERR_OOM, "nut_table_execute: out of host memory");
+  r->kind = p->kind;
+  r->device = c->device;
+  DeviceGuard g(c->device);
+  nut_status st = p->kind == NUT_PLAN_GROUPBY ? exec_groupby(c, *p, bound.data(), dicts.data(), nrows, group_hint, r)
+                                              : exec_scan(c, *p, bound.data(), dicts.data(), nrows, r);
+  if (st) {
+    nut_result_free(r);
+    return st;
+  }
+  *out = r;
+  return NUT_OK;
+}
+
+nut_status nut_result_string(const nut_result *r, int j, uint64_t row, const char **str, size_t *len) {
+  if (!r || j < 0 || j >= (int)r->names.size() || !str || !len)
+    return fail(NUT_ERR_INVALID_ARG, "nut_result_string: bad argument");
+  if (r->types[j] != NUT_T_STR || (size_t)j >= r->strs.size())
+    return fail(NUT_ERR_INVALID_ARG, "nut_result_string: column is not a string column");
+  if (row >= r->nrows) return fail(NUT_ERR_INVALID_ARG, "nut_result_string: row out of range");
+  const std::string &v = r->strs[j][row];
+  *str = v.data();
+  *len = v.size();
+  return NUT_OK;
 }
 
 nut_status nut_result_shape(const nut_result *r, uint64_t *nrows, int *ncols) {
@@ -1745,6 +1932,8 @@ nut_status nut_result_to_host(const nut_result *r, int j, void *dst, uint64_t ca
   if (r->nrows == 0) return NUT_OK;
   if (!dst) return fail(NUT_ERR_INVALID_ARG, "nut_result_to_host: NULL dst");
   if (r->kind == NUT_PLAN_GROUPBY) {
+    if (r->types[j] == NUT_T_STR)
+      return fail(NUT_ERR_INVALID_ARG, "nut_result_to_host: string column (use nut_result_string)");
     memcpy(dst, r->host[j].data(), r->nrows * 8);
     return NUT_OK;
   }

@@ -23,7 +23,7 @@ from typing import Dict, List, Optional, Tuple
 
 import numpy as np
 
-from ._lib import (NUT_OK, STMT_KINDS, TOKEN_TYPES, NutColumn, NutError, T_F64, T_I64, check, lib)
+from ._lib import (NUT_OK, STMT_KINDS, TOKEN_TYPES, NutColumn, NutError, T_F64, T_I64, T_STR, check, lib)
 
 NUT_ERR_PARSE = 6
 NUT_ERR_CAPACITY = 5
@@ -125,6 +125,33 @@ def unescape_double_quoted_string(s: str) -> str:
     return _unescape(s, '"')
 
 
+def read_result(res) -> Dict[str, np.ndarray]:
+    """nut_result -> {output name: numpy array} (NUT_T_STR columns: object arrays of str);
+    frees the result."""
+    try:
+        nr = C.c_uint64(0)
+        nc = C.c_int(0)
+        check(lib.nut_result_shape(res, C.byref(nr), C.byref(nc)), "nut_result_shape")
+        out = {}
+        for j in range(nc.value):
+            typ = C.c_int(0)
+            nm = C.c_char_p()
+            check(lib.nut_result_column(res, j, C.byref(typ), C.byref(nm)), "nut_result_column")
+            if typ.value == T_STR:
+                a = np.empty(nr.value, dtype=object)
+                sp, sl = C.c_char_p(), C.c_size_t()
+                for i in range(nr.value):
+                    check(lib.nut_result_string(res, j, i, C.byref(sp), C.byref(sl)), "nut_result_string")
+                    a[i] = C.string_at(sp, sl.value).decode("utf-8")
+            else:
+                a = np.empty(nr.value, dtype=np.float64 if typ.value == T_F64 else np.int64)
+                check(lib.nut_result_to_host(res, j, a.ctypes.data_as(C.c_void_p), nr.value), "nut_result_to_host")
+            out[nm.value.decode()] = a
+        return out
+    finally:
+        lib.nut_result_free(res)
+
+
 class Plan:
     """An executor plan lowered from a SELECT."""
 
@@ -191,21 +218,10 @@ class Plan:
         ex._bind_stream()
         check(lib.nut_plan_execute(ex.ctx, self._h, arr, len(columns), rows, group_hint, C.byref(res)),
               "nut_plan_execute")
-        try:
-            nr = C.c_uint64(0)
-            nc = C.c_int(0)
-            check(lib.nut_result_shape(res, C.byref(nr), C.byref(nc)), "nut_result_shape")
-            out = {}
-            for j in range(nc.value):
-                typ = C.c_int(0)
-                nm = C.c_char_p()
-                check(lib.nut_result_column(res, j, C.byref(typ), C.byref(nm)), "nut_result_column")
-                a = np.empty(nr.value, dtype=np.float64 if typ.value == T_F64 else np.int64)
-                check(lib.nut_result_to_host(res, j, a.ctypes.data_as(C.c_void_p), nr.value), "nut_result_to_host")
-                out[nm.value.decode()] = a
-            return out
-        finally:
-            lib.nut_result_free(res)
+        return read_result(res)
+
+    def _handle(self):
+        return self._h
 
     def __del__(self):
         h, self._h = getattr(self, "_h", None), None

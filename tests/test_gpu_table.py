@@ -1,0 +1,160 @@
+"""GPU: typed tables from CREATE TABLE — the reference's own fixture
+tests/sql/5.sql run verbatim over string columns, TPC-H Q1 over narrow / string / Date
+columns, string predicates in both lowerings, narrow-type widening, Enum / Boolean, and
+the string-misuse errors.  Ground truth: numpy over the same host data (exact: counts,
+integer sums, dyadic or float32-widened values)."""
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from nutdb_amd import NutError
+from nutdb_amd.table import Table
+
+pytestmark = pytest.mark.gpu
+GOLDEN = Path(__file__).parent / "golden" / "sql"
+
+
+def test_fixture5_verbatim(ex):
+    """/root/reference/tests/sql/5.sql (copied as data to tests/golden/sql/5.sql), string
+    constants and all, over one denormalised table."""
+    rng = np.random.default_rng(55)
+    n = 400_003
+    modes = np.array(["MAIL", "SHIP", "AIR", "RAIL", "TRUCK", "FOB", "REG AIR"], dtype=object)
+    prios = np.array(["1-URGENT", "2-HIGH", "3-MEDIUM", "4-NOT SPECIFIED", "5-LOW"], dtype=object)
+    okey = rng.integers(0, 40, n)
+    lkey = np.where(rng.random(n) < 0.6, okey, rng.integers(0, 40, n))
+    mode = modes[rng.integers(0, len(modes), n)]
+    prio = prios[rng.integers(0, len(prios), n)]
+    ship = rng.integers(8000, 10000, n)
+    commit = ship + rng.integers(-30, 30, n)
+    receipt = ship + rng.integers(-30, 30, n)
+    t = Table(ex, """CREATE TABLE orders (o_orderkey Int64, l_orderkey Int32, l_shipmode Dictionary(String),
+        o_orderpriority String, l_shipdate Date, l_commitdate Date, l_receiptdate Date)""")
+    t.append(o_orderkey=okey, l_orderkey=lkey.astype(np.int32), l_shipmode=mode, o_orderpriority=prio,
+             l_shipdate=ship, l_commitdate=commit, l_receiptdate=receipt)
+    assert t.nrows == n
+    got = t.sql((GOLDEN / "5.sql").read_text(), group_hint=8)
+    m = (okey == lkey) & np.isin(mode, ["MAIL", "SHIP"]) & (commit < receipt) & (ship < commit)
+    hi_p = (prio == "1-URGENT") | (prio == "2-HIGH")
+    assert got["l_shipmode"].tolist() == ["MAIL", "SHIP"]
+    assert got["high_line_count"].tolist() == [int(np.sum(m & (mode == s) & hi_p)) for s in ("MAIL", "SHIP")]
+    assert got["low_line_count"].tolist() == [int(np.sum(m & (mode == s) & ~hi_p)) for s in ("MAIL", "SHIP")]
+
+
+def q1_table(ex, n, seed=11):
+    rng = np.random.default_rng(seed)
+    cols = dict(
+        l_returnflag=np.array(["A", "N", "R"], dtype=object)[rng.integers(0, 3, n)],
+        l_linestatus=np.array(["F", "O"], dtype=object)[rng.integers(0, 2, n)],
+        l_quantity=rng.integers(1, 51, n).astype(np.int8),
+        l_extendedprice=rng.integers(90000, 10494900, n) / 128.0,  # dyadic: exact sums
+        l_discount=(rng.integers(0, 11, n) / 100.0).astype(np.float32),
+        l_shipdate=rng.integers(8036, 10562, n),
+    )
+    t = Table(ex, """CREATE TABLE lineitem (l_returnflag Enum('A' = 65, 'N' = 78, 'R' = 82), l_linestatus String,
+        l_quantity Int8, l_extendedprice Float64, l_discount Float32, l_shipdate Date)""")
+    t.append(**cols)
+    return t, cols
+
+
+def test_q1_typed(ex):
+    n = 300_007
+    t, c = q1_table(ex, n)
+    got = t.sql("""select l_returnflag, l_linestatus, sum(l_quantity) as sum_qty, sum(l_extendedprice) as base,
+          avg(l_quantity) as avg_qty, max(l_discount) as max_disc, count(*) as count_order
+        from lineitem where l_shipdate <= toDate('1998-12-01') - interval 90 day
+        group by l_returnflag, l_linestatus order by l_returnflag desc, l_linestatus""", group_hint=6)
+    m = c["l_shipdate"] <= 10471
+    groups = sorted({(a, b) for a, b in zip(c["l_returnflag"][m], c["l_linestatus"][m])}, key=lambda g: (-ord(g[0]), g[1]))
+    assert list(zip(got["l_returnflag"], got["l_linestatus"])) == groups
+    for i, (a, b) in enumerate(groups):
+        s = m & (c["l_returnflag"] == a) & (c["l_linestatus"] == b)
+        assert got["sum_qty"][i] == int(np.sum(c["l_quantity"][s].astype(np.int64)))
+        assert got["base"][i] == np.sum(c["l_extendedprice"][s])
+        assert got["avg_qty"][i] == np.sum(c["l_quantity"][s].astype(np.int64)) / np.sum(s)
+        assert got["max_disc"][i] == np.max(c["l_discount"][s].astype(np.float64))
+        assert got["count_order"][i] == np.sum(s)
+
+
+def test_string_predicates(ex):
+    n = 100_003
+    t, c = q1_table(ex, n, seed=3)
+    rf, ls = c["l_returnflag"], c["l_linestatus"]
+    cases = [
+        ("l_returnflag = 'R'", rf == "R"),
+        ("l_returnflag != 'R'", rf != "R"),
+        ("l_linestatus in ('O', 'X')", ls == "O"),          # 'X' is in no row
+        ("l_linestatus not in ('X')", np.ones(n, bool)),     # absent: every row
+        ("l_linestatus = 'X'", np.zeros(n, bool)),
+        ("'F' = l_linestatus", ls == "F"),
+        ("l_returnflag = 'A' or l_linestatus = 'O'", (rf == "A") | (ls == "O")),  # expression mode
+    ]
+    for where, m in cases:
+        got = t.sql(f"select count(*) as c from lineitem where {where}")
+        assert got["c"].tolist() == [int(np.sum(m))], where
+    got = t.sql("select l_linestatus, sum(case l_returnflag when 'A' then 1 when 'N' then 2 else 0 end) as s "
+                "from lineitem group by l_linestatus order by l_linestatus")
+    w = np.where(rf == "A", 1, np.where(rf == "N", 2, 0))
+    assert got["l_linestatus"].tolist() == ["F", "O"]
+    assert got["s"].tolist() == [int(np.sum(w[ls == "F"])), int(np.sum(w[ls == "O"]))]
+
+
+@pytest.mark.parametrize("sql,frag", [
+    ("select count(*) from lineitem where l_linestatus < 'G'", "ordering comparison"),
+    ("select count(*) from lineitem where l_linestatus = 3", "compared with a number"),
+    ("select count(*) from lineitem where l_quantity = 'a'", "non-string column"),
+    ("select sum(l_linestatus) from lineitem", "only count"),
+    ("select count(*) from lineitem where l_linestatus + 1 = 2 or l_quantity > 3", "= / != / IN"),
+    ("select l_linestatus, count(*) from lineitem group by l_linestatus having l_linestatus > 0", "HAVING on the string key"),
+    ("select l_linestatus from lineitem where l_linestatus = 'F'", "scans / sorts of strings"),
+    ("select count(*) from lineitem where nosuch > 1", "no column 'nosuch'"),
+])
+def test_string_errors(ex, sql, frag):
+    t, _ = q1_table(ex, 1000)
+    with pytest.raises(NutError) as e:
+        t.sql(sql)
+    assert frag in str(e.value)
+
+
+def test_widening_and_kinds(ex):
+    t = Table(ex, "CREATE TABLE w (a Int8, b Int16, c Int32, d UInt8, e UInt16, f UInt32, g Boolean, h Float32, "
+                  "i UInt64, k Int64)")
+    a = np.array([-128, 127, -1, 0, 5], np.int8)
+    b = np.array([-32768, 32767, -1, 0, 7], np.int16)
+    c = np.array([-2**31, 2**31 - 1, -1, 0, 9], np.int32)
+    d = np.array([255, 0, 1, 128, 3], np.uint8)
+    e = np.array([65535, 0, 1, 32768, 3], np.uint16)
+    f = np.array([2**32 - 1, 0, 1, 2**31, 3], np.uint32)
+    g = np.array([1, 0, 7, 0, 1], np.uint8)
+    h = np.array([0.1, -2.5, 3.0e38, -0.0, 1e-40], np.float32)
+    i = np.array([2**63 - 1, 0, 1, 5, 3], np.uint64)
+    k = np.arange(5, dtype=np.int64)
+    t.append(a=a, b=b, c=c, d=d, e=e, f=f, g=g, h=h, i=i, k=k)
+    got = t.sql("select k, min(a), max(a), sum(b), sum(c), sum(d), max(f), sum(e), sum(g), min(h), max(h), max(i) "
+                "from w group by k order by k")
+    vals = list(got.values())
+    assert vals[0].tolist() == k.tolist()
+    assert vals[1].tolist() == a.astype(np.int64).tolist() and vals[2].tolist() == a.astype(np.int64).tolist()
+    for got_col, src in zip(vals[3:8], (b, c, d, f, e)):
+        assert got_col.tolist() == src.astype(np.int64).tolist()
+    assert vals[8].tolist() == (g != 0).astype(np.int64).tolist()
+    assert vals[9].tolist() == h.astype(np.float64).tolist()
+    assert vals[11].tolist() == i.astype(np.int64).tolist()
+    with pytest.raises(NutError) as err:
+        t.append(i=np.array([2**63], np.uint64))
+    assert "2^63" in str(err.value)
+    t.append(k=np.array([9]))
+    with pytest.raises(NutError) as err:  # rows are ragged until every column matches
+        t.sql("select count(*) from w")
+    assert "ragged" in str(err.value)
+
+
+def test_enum_values(ex):
+    t = Table(ex, "CREATE TABLE e (s Enum('lo' = 1, 'hi' = 9), v Int64)")
+    t.append(s=["lo", "hi", "hi", "lo", "hi"], v=np.array([1, 2, 3, 4, 5]))
+    got = t.sql("select s, sum(v) as sv from e where s != 'mid' group by s order by s")
+    assert got["s"].tolist() == ["hi", "lo"] and got["sv"].tolist() == [10, 5]
+    with pytest.raises(NutError) as err:
+        t.append(s=["mid"])
+    assert "not a value of its Enum" in str(err.value)
