@@ -139,10 +139,13 @@ class Filter:
 
 
 class Sort:
-    """config 5: ORDER BY a full-range i64 key.  N=1: local LSD radix sort.  N>1: sample
-    sort — splitters from an all_gather'd sample, local stable partition into P buckets
-    (nut_partition_i64), ONE RCCL all-to-all of keys, local radix sort of the received
-    range (nutdb_amd/dist.py distributed_sort).  Rank r ends with the r-th key range."""
+    """config 5: ORDER BY a full-range i64 key.  N=1: local hybrid MSD radix sort
+    (msd_sort.hip: two segmented scatter levels + on-chip local sorts for 1.25e9 random
+    keys).  N>1: sample sort — splitters from an all_gather'd sample, local stable
+    partition into P buckets (nut_partition_i64), ONE RCCL all-to-all of keys, local sort
+    of the received range (nutdb_amd/dist.py distributed_sort).  Rank r ends with the r-th
+    key range.  Algorithmic bytes come from the library (nut_ctx_sort_stats): 8 B/key per
+    histogram read, 16 B/key per scatter level, local sort and copy."""
     name = "sort_i64_radix"
     kernel_kind = 2
 
@@ -154,22 +157,26 @@ class Sort:
         self.rows = rows
         self.world = world
         self.group = group
-        self.passes = 8  # full-range keys: no digit pass is constant
-        # histogram read + 16 B per pass; N>1 adds the partition (8 B histogram + 16 B pass)
-        self.cols_bytes = 8 + 16 * self.passes + (24 if world > 1 else 0)
+        self.sort_bytes, self.levels = 0, 0
+
+    @property
+    def cols_bytes(self):
+        # per row of this rank's shard; N>1 adds the partition (8 B histogram + 16 B pass)
+        return self.sort_bytes / self.rows + (24 if self.world > 1 else 0)
 
     def run(self):
         if self.world == 1:
             self.ex.sort_i64(self.col, out=self.out)
-            return
-        from nutdb_amd.dist import distributed_sort
-        self.out = distributed_sort(self.col, self.ex.partition_i64, self.ex.sort_i64, self.group)
+        else:
+            from nutdb_amd.dist import distributed_sort
+            self.out = distributed_sort(self.col, self.ex.partition_i64, self.ex.sort_i64, self.group)
+        self.sort_bytes, self.levels = self.ex.sort_stats()
 
     def config(self):
         return {"workload": self.name, "query": "SELECT k FROM t ORDER BY k (full-range i64)",
-                "algorithm": "LSD radix, 8 x 8-bit passes, onesweep look-back" +
-                ("; sample sort across ranks: partition by P-1 splitters + RCCL all-to-all" if self.world > 1
-                 else ""),
+                "algorithm": f"hybrid MSD radix: {self.levels} segmented scatter levels + on-chip local sorts"
+                + ("; sample sort across ranks: partition by P-1 splitters + RCCL all-to-all" if self.world > 1
+                   else ""),
                 "bytes_per_row": self.cols_bytes, "hbm_lower_bound_bytes_per_row": 16,
                 "xgmi_bytes_per_row": 8.0 * (self.world - 1) / self.world}
 

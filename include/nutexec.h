@@ -80,6 +80,10 @@ typedef enum {
 } nut_kernel_kind;
 nut_status nut_ctx_enable_timing(nut_ctx *ctx, int enable);
 nut_status nut_ctx_kernel_time(nut_ctx *ctx, int kind, double *total_ms, uint64_t *launches);
+/* Algorithmic HBM bytes of the last nut_sort_i64[_desc] on this context (its levels
+ * depend on the data: 8 B/key per histogram read, 16 B/key per scatter level, local sort
+ * and copy) and the number of scatter levels it ran — the roofline numerator for sorts. */
+nut_status nut_ctx_sort_stats(nut_ctx *ctx, uint64_t *bytes, uint32_t *levels);
 
 /* ------------------------------------------------------------------------
  * Synthetic columns (bench / tests): counter-based splitmix64 generator,

@@ -125,6 +125,7 @@ SIGNATURES = {
     "nut_ctx_info": (_I32, [_P, C.POINTER(_I32), C.c_char_p, C.c_size_t]),
     "nut_ctx_enable_timing": (_I32, [_P, _I32]),
     "nut_ctx_kernel_time": (_I32, [_P, _I32, C.POINTER(C.c_double), C.POINTER(_U64)]),
+    "nut_ctx_sort_stats": (_I32, [_P, C.POINTER(_U64), C.POINTER(C.c_uint32)]),
     "nut_gen_column": (_I32, [_P, _I32, _U64, _I64, _I64, C.c_double, _U64, _U64, _P]),
     "nut_filter_i64": (_I32, [_P, _P, _U64, _I32, _I64, _P, C.POINTER(_U64)]),
     "nut_filter_i64_async": (_I32, [_P, _P, _U64, _I32, _I64, _P, _P]),

@@ -158,6 +158,7 @@ void nut_ctx_destroy(nut_ctx *c) {
   c->filter_state.release();
   c->sort_tmp.release();
   c->sort_status.release();
+  c->sort_meta.release();
   c->misc.release();
   c->timer.release();
   if (c->host_pinned) (void)hipHostFree(c->host_pinned);
@@ -185,6 +186,13 @@ nut_status nut_ctx_enable_timing(nut_ctx *c, int enable) {
   c->timer.enabled = enable != 0;
   for (int k = 0; k < 4; ++k) c->timer.total_ms[k] = 0, c->timer.launches[k] = 0;
   return st;
+}
+
+nut_status nut_ctx_sort_stats(nut_ctx *c, uint64_t *bytes, uint32_t *levels) {
+  if (!c) return fail(NUT_ERR_INVALID_ARG, "nut_ctx_sort_stats: NULL context");
+  if (bytes) *bytes = c->sort_bytes;
+  if (levels) *levels = c->sort_levels;
+  return NUT_OK;
 }
 
 nut_status nut_ctx_kernel_time(nut_ctx *c, int kind, double *total_ms, uint64_t *launches) {

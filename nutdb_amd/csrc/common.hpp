@@ -168,6 +168,9 @@ struct nut_ctx {
   void *sort_status_seen = nullptr;
   size_t sort_status_clean = 0;
   uint32_t sort_epoch = 0;
+  uint64_t sort_bytes = 0;   // algorithmic bytes of the last sort (nut_ctx_sort_stats)
+  uint32_t sort_levels = 0;
+  nut::Scratch sort_meta;     // MSD sort per-level segment / tile / histogram tables (msd_sort.hip)
   nut::Scratch misc;
   uint64_t *host_pinned = nullptr;  // small pinned staging for counts/flags
   nut::KernelTimer timer;

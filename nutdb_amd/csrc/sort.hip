@@ -20,11 +20,13 @@
 // Measured (scripts/tune/sort_tune.hip, one pass, 2.5e8 keys): 256x16 tiles 1.72 ms,
 // 512x16 tiles 1.40 ms; without the look-back 0.91 ms.
 // Algorithmic bytes: 8 B/key histogram read + 16 B/key per executed pass.
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
 
 #include "common.hpp"
+#include "sort.hpp"
 
 namespace nut {
 
@@ -312,11 +314,8 @@ nut_status next_status(nut_ctx *c, uint64_t ntiles, uint64_t **status, uint32_t 
 
 using namespace nut;
 
-static nut_status sort_i64(nut_ctx *c, const int64_t *in, int64_t *out, uint64_t n, uint64_t flip) {
+nut_status nut::lsd_sort_i64(nut_ctx *c, const int64_t *in, int64_t *out, uint64_t n, uint64_t flip) {
   if (!c || (n && (!in || !out))) return fail(NUT_ERR_INVALID_ARG, "nut_sort_i64: NULL argument");
-  if (n && (uintptr_t)in == (uintptr_t)out) return fail(NUT_ERR_INVALID_ARG, "nut_sort_i64: in and out alias");
-  if (n == 0) return NUT_OK;
-  DeviceGuard g(c->device);
   const uint64_t ntiles = (n + RS_TILE - 1) / RS_TILE;
   if (ntiles > 0x7FFFFFF0ull || n > RS_VAL) return fail(NUT_ERR_UNSUPPORTED, "nut_sort_i64: n too large");
   // scratch: [err 4 B, pad | tickets 8 x 4 B at +16 | hist 8*256*8 at +256 | base 8*256*8 |
@@ -349,6 +348,8 @@ static nut_status sort_i64(nut_ctx *c, const int64_t *in, int64_t *out, uint64_t
   int passes[8], np = 0;
   for (int p = 0; p < 8; ++p)
     if (!htriv[p]) passes[np++] = p;
+  c->sort_bytes = 8 * n + 16 * n * (uint64_t)(np ? np : 1);
+  c->sort_levels = (uint32_t)np;
   if (np == 0) {  // all keys equal
     hipLaunchKernelGGL(rs_copy_kernel, dim3((unsigned)std::min<uint64_t>((n + 255) / 256, 4096)), dim3(256), 0, st,
                        (const uint64_t *)in, (uint64_t *)out, n);
@@ -379,6 +380,19 @@ static nut_status sort_i64(nut_ctx *c, const int64_t *in, int64_t *out, uint64_t
   NUT_HIP(hipStreamSynchronize(st));
   if (htriv[0]) return fail(NUT_ERR_TIMEOUT, "nut_sort_i64: look-back spin limit hit");
   return NUT_OK;
+}
+
+// NUT_SORT=lsd selects the 8-pass LSD sort above (A/B measurements); default: msd_sort.hip
+static nut_status sort_i64(nut_ctx *c, const int64_t *in, int64_t *out, uint64_t n, uint64_t flip) {
+  if (!c || (n && (!in || !out))) return fail(NUT_ERR_INVALID_ARG, "nut_sort_i64: NULL argument");
+  if (n && (uintptr_t)in == (uintptr_t)out) return fail(NUT_ERR_INVALID_ARG, "nut_sort_i64: in and out alias");
+  if (n == 0) return NUT_OK;
+  DeviceGuard g(c->device);
+  static const bool lsd = [] {
+    const char *e = getenv("NUT_SORT");
+    return e && strcmp(e, "lsd") == 0;
+  }();
+  return lsd ? lsd_sort_i64(c, in, out, n, flip) : msd_sort_i64(c, in, out, n, flip);
 }
 
 extern "C" nut_status nut_sort_i64(nut_ctx *c, const int64_t *in, int64_t *out, uint64_t n) {

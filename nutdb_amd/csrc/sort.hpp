@@ -1,0 +1,10 @@
+// sort.hpp — the two sort implementations behind nut_sort_i64 / nut_sort_i64_desc.
+// Both take validated arguments (n > 0, in != out, device set) and `flip`, the XOR that maps
+// int64 order to unsigned order (ascending) or to its reverse (descending).
+#pragma once
+#include "common.hpp"
+
+namespace nut {
+nut_status lsd_sort_i64(nut_ctx *c, const int64_t *in, int64_t *out, uint64_t n, uint64_t flip);  // sort.hip
+nut_status msd_sort_i64(nut_ctx *c, const int64_t *in, int64_t *out, uint64_t n, uint64_t flip);  // msd_sort.hip
+}  // namespace nut

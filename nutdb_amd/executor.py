@@ -319,6 +319,13 @@ class Executor:
         check(lib.nut_ctx_kernel_time(self.ctx, kind, C.byref(ms), C.byref(cnt)), "nut_ctx_kernel_time")
         return ms.value, cnt.value
 
+    def sort_stats(self):
+        """(algorithmic HBM bytes, scatter levels) of the last sort on this context."""
+        b = C.c_uint64()
+        lv = C.c_uint32()
+        check(lib.nut_ctx_sort_stats(self.ctx, C.byref(b), C.byref(lv)), "nut_ctx_sort_stats")
+        return b.value, lv.value
+
     def sync(self):
         check(lib.nut_ctx_sync(self.ctx), "nut_ctx_sync")
 

@@ -303,17 +303,22 @@ def test_sort_golden(golden, ex):
     assert pos_hash(out) == case["pos_hash"]
 
 
-@pytest.mark.parametrize("n", [0, 1, 2, 3, 63, 64, 65, 4095, 4096, 4097, 12289, 1_000_003])
+@pytest.mark.parametrize("n", [0, 1, 2, 3, 63, 64, 65, 2048, 2049, 4095, 4096, 4097, 8192, 8193, 12289,
+                               32767, 32768, 32769, 65537, 1_000_003, 9_000_011])
 def test_sort_sizes_vs_oracle(ex, orc, n):
     col = orc.gen_column(1, 0x50, n)
     got = host(ex.sort_i64(dev(col, ex)))
     assert np.array_equal(got, orc.sort_i64(col))
 
 
-@pytest.mark.parametrize("kind", ["dups", "const", "small_range", "extremes", "negative", "unaligned"])
-def test_sort_distributions(ex, orc, kind):
+@pytest.mark.parametrize("n", [300_007, 3_000_017])
+@pytest.mark.parametrize("kind", ["dups", "const", "small_range", "extremes", "negative", "unaligned",
+                                  "skewed", "sparse_digits", "top_and_bottom"])
+def test_sort_distributions(ex, orc, kind, n):
+    """Distributions that drive the MSD sort (msd_sort.hip) through every branch: segments
+    of equal keys larger than a local sort (copied), digits constant inside a segment but
+    not globally (pass-through levels), varying digits that are not adjacent."""
     rng = np.random.default_rng(9)
-    n = 300_007
     if kind == "dups":
         v = rng.integers(-50, 50, n).astype(np.int64)
     elif kind == "const":
@@ -324,6 +329,15 @@ def test_sort_distributions(ex, orc, kind):
         v = rng.choice(np.array([I64_MIN, I64_MAX, 0, -1, 1], dtype=np.int64), n)
     elif kind == "negative":
         v = -rng.integers(0, I64_MAX, n, dtype=np.int64)
+    elif kind == "skewed":  # half the keys one value, the rest full-range
+        v = rng.integers(I64_MIN, I64_MAX, n, dtype=np.int64)
+        v[rng.random(n) < 0.5] = 42
+    elif kind == "sparse_digits":  # digits 7, 6 take 4 values each, digits 5..2 constant
+        v = ((rng.integers(0, 4, n) << 56) | (rng.integers(0, 4, n) << 48) | (0x5A << 24)
+             | rng.integers(0, 1 << 16, n)).astype(np.int64)
+    elif kind == "top_and_bottom":  # only digits 7 and 0 vary
+        v = ((rng.integers(0, 256, n).astype(np.uint64) << np.uint64(56))
+             | rng.integers(0, 256, n).astype(np.uint64)).view(np.int64)
     else:
         v = rng.integers(I64_MIN, I64_MAX, n + 1, dtype=np.int64)
     d = dev(v, ex)
@@ -379,3 +393,24 @@ def test_sample_sort_virtual_ranks(ex, orc):
     out = [host(ex.sort_i64(torch.cat(r))) for r in received]
     assert np.array_equal(np.concatenate(out), orc.sort_i64(keys))
     assert all(o[-1] <= out[i + 1][0] for i, o in enumerate(out[:-1]) if len(o) and len(out[i + 1]))
+
+
+@pytest.mark.parametrize("n", [40_000, 5_000_003])
+def test_sort_desc_msd(ex, orc, n):
+    """Descending MSD sort: duplicates, extremes and a block of equal keys."""
+    rng = np.random.default_rng(11)
+    v = rng.integers(I64_MIN, I64_MAX, n, dtype=np.int64)
+    v[: n // 3] = rng.integers(-3, 3, n // 3)
+    v[-4:] = [I64_MIN, I64_MAX, 0, -1]
+    out = host(ex.sort_i64(dev(v, ex), descending=True))
+    assert np.array_equal(out, np.sort(v)[::-1])
+
+
+def test_sort_stats(ex):
+    """Algorithmic bytes reported for the roofline: full-range keys above one local sort
+    take two histogram reads, two scatter levels and the local sort (64 B/key)."""
+    n = 20_000_000
+    keys = ex.gen_column(1, 0x50, n)
+    ex.sort_i64(keys)
+    nbytes, levels = ex.sort_stats()
+    assert levels == 2 and nbytes == 64 * n
