@@ -39,7 +39,7 @@ constexpr int MS_BINS = 256;
 // local-sort classes: threads x max items per thread (ms_local_kernel)
 constexpr int LS_S_THREADS = 256, LS_S_ITEMS = 8;    // <= 2048 keys
 constexpr int LS_M_THREADS = 512, LS_M_ITEMS = 16;   // <= 8192 keys
-constexpr int LS_L_THREADS = 1024, LS_L_ITEMS = 32;  // <= 32768 keys
+constexpr int LS_L_THREADS = 512, LS_L_ITEMS = 48;   // <= 24576 keys
 constexpr uint64_t LS_S_CAP = LS_S_THREADS * LS_S_ITEMS;
 constexpr uint64_t LS_M_CAP = LS_M_THREADS * LS_M_ITEMS;
 constexpr uint64_t LS_CAP = LS_L_THREADS * LS_L_ITEMS;
@@ -116,72 +116,98 @@ __global__ __launch_bounds__(MH_THREADS) void ms_hist_kernel(MsBufs bf, const Ms
 // sub-segment (s, d) and is advanced by one atomic per (tile, digit).
 __device__ __forceinline__ uint64_t *ms_dst(const MsBufs &bf, uint32_t buf) { return buf == 2 ? bf.a : bf.b; }
 
-__global__ __launch_bounds__(MS_THREADS) void ms_scatter_kernel(MsBufs bf, const MsSeg *__restrict__ segs,
-                                                                const uint32_t *__restrict__ tile_seg, int shift,
-                                                                uint64_t flip, unsigned long long *__restrict__ cursor) {
+// Persistent: workgroup b takes tiles b, b + grid, ...; the next tile's keys are loaded into
+// the key registers as soon as the current tile is staged in LDS, so its HBM latency hides
+// behind the current tile's write-out (and the segment lookup behind the ranking).
+__global__ __launch_bounds__(MS_THREADS, 4) void ms_scatter_kernel(MsBufs bf, const MsSeg *__restrict__ segs,
+                                                                   const uint32_t *__restrict__ tile_seg, uint32_t ntiles,
+                                                                int shift, uint64_t flip,
+                                                                unsigned long long *__restrict__ cursor) {
   __shared__ uint64_t s_keys[MS_TILE];
   __shared__ uint32_t s_cnt[MS_BINS];
   __shared__ uint32_t s_tex[MS_BINS];
   __shared__ uint64_t s_gb[MS_BINS];
   __shared__ uint32_t s_wsum[MS_BINS / kWave];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (tid < MS_BINS) s_cnt[tid] = 0;
-  const uint32_t s = tile_seg[blockIdx.x];
-  const MsSeg sg = segs[s];
-  const uint64_t lo = (uint64_t)(blockIdx.x - sg.aux) * MS_TILE;
-  const uint32_t cnt = (uint32_t)min<uint64_t>(MS_TILE, sg.count - lo);
-  const uint64_t *src = ms_src(bf, sg.buf) + sg.start + lo;
-  uint64_t *dst = ms_dst(bf, sg.buf);
-  const uint64_t f = sg.buf == 0 ? flip : 0;
+  uint32_t t = blockIdx.x;
   uint64_t key[MS_ITEMS];
+  auto load = [&](uint32_t tt, const MsSeg &g) {
+    const uint64_t lo = (uint64_t)(tt - g.aux) * MS_TILE;
+    const uint32_t cn = (uint32_t)min<uint64_t>(MS_TILE, g.count - lo);
+    const uint64_t *sp = ms_src(bf, g.buf) + g.start + lo;
+    const uint64_t ff = g.buf == 0 ? flip : 0;
 #pragma unroll
-  for (int i = 0; i < MS_ITEMS; ++i) {
-    const uint32_t idx = (uint32_t)i * MS_THREADS + tid;
-    key[i] = idx < cnt ? (__builtin_nontemporal_load(src + idx) ^ f) : 0;
-  }
-  __syncthreads();
-  uint32_t rk[MS_ITEMS];
-#pragma unroll
-  for (int i = 0; i < MS_ITEMS; ++i) {
-    const uint32_t idx = (uint32_t)i * MS_THREADS + tid;
-    rk[i] = idx < cnt ? atomicAdd(&s_cnt[(key[i] >> shift) & 255], 1u) : 0u;
-  }
-  __syncthreads();
-  uint32_t c = 0, incl = 0;
-  if (tid < MS_BINS) {
-    c = s_cnt[tid];
-    incl = c;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const uint32_t y = __shfl_up(incl, off, 64);
-      if (lane >= off) incl += y;
+    for (int i = 0; i < MS_ITEMS; ++i) {
+      const uint32_t idx = (uint32_t)i * MS_THREADS + tid;
+      key[i] = idx < cn ? (__builtin_nontemporal_load(sp + idx) ^ ff) : 0;
     }
-    if (lane == 63) s_wsum[wave] = incl;
-  }
-  __syncthreads();
-  if (tid < MS_BINS) {
-    uint32_t add = 0;
+  };
+  uint32_t s = tile_seg[t];
+  MsSeg sg = segs[s];
+  load(t, sg);
+  for (;;) {
+    const uint64_t lo = (uint64_t)(t - sg.aux) * MS_TILE;
+    const uint32_t cnt = (uint32_t)min<uint64_t>(MS_TILE, sg.count - lo);
+    uint64_t *dst = ms_dst(bf, sg.buf);
+    const uint32_t next = t + gridDim.x;
+    const uint32_t ns = next < ntiles ? tile_seg[next] : 0;
+    if (tid < MS_BINS) s_cnt[tid] = 0;
+    __syncthreads();
+    uint32_t rk[MS_ITEMS / 2];  // ranks in the tile's digit run (< 8192), 16-bit pairs
 #pragma unroll
-    for (int w = 0; w < MS_BINS / kWave; ++w) add += (w < wave) ? s_wsum[w] : 0u;
-    const uint32_t tex = incl - c + add;
-    s_tex[tid] = tex;
-    const uint64_t gb = c ? (uint64_t)atomicAdd(&cursor[(uint64_t)s * MS_BINS + tid], (unsigned long long)c) : 0;
-    s_gb[tid] = gb - tex;  // out position of LDS slot j of this digit = s_gb[d] + j
-  }
-  __syncthreads();
+    for (int i = 0; i < MS_ITEMS; i += 2) rk[i / 2] = 0;
 #pragma unroll
-  for (int i = 0; i < MS_ITEMS; ++i) {
-    const uint32_t idx = (uint32_t)i * MS_THREADS + tid;
-    if (idx < cnt) s_keys[s_tex[(key[i] >> shift) & 255] + rk[i]] = key[i];
-  }
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < MS_ITEMS; ++i) {
-    const uint32_t j = (uint32_t)i * MS_THREADS + tid;
-    if (j < cnt) {
-      const uint64_t k = s_keys[j];
-      dst[s_gb[(k >> shift) & 255] + j] = k;
+    for (int i = 0; i < MS_ITEMS; ++i) {
+      const uint32_t idx = (uint32_t)i * MS_THREADS + tid;
+      if (idx < cnt) rk[i / 2] |= atomicAdd(&s_cnt[(key[i] >> shift) & 255], 1u) << (16 * (i & 1));
     }
+    __syncthreads();
+    uint32_t c = 0, incl = 0;
+    if (tid < MS_BINS) {
+      c = s_cnt[tid];
+      incl = c;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += y;
+      }
+      if (lane == 63) s_wsum[wave] = incl;
+    }
+    __syncthreads();
+    if (tid < MS_BINS) {
+      uint32_t add = 0;
+#pragma unroll
+      for (int w = 0; w < MS_BINS / kWave; ++w) add += (w < wave) ? s_wsum[w] : 0u;
+      const uint32_t tex = incl - c + add;
+      s_tex[tid] = tex;
+      const uint64_t gb = c ? (uint64_t)atomicAdd(&cursor[(uint64_t)s * MS_BINS + tid], (unsigned long long)c) : 0;
+      s_gb[tid] = gb - tex;  // out position of LDS slot j of this digit = s_gb[d] + j
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < MS_ITEMS; ++i) {
+      const uint32_t idx = (uint32_t)i * MS_THREADS + tid;
+      if (idx < cnt) s_keys[s_tex[(key[i] >> shift) & 255] + ((rk[i / 2] >> (16 * (i & 1))) & 0xFFFFu)] = key[i];
+    }
+    MsSeg nsg = sg;
+    if (next < ntiles) {  // the key registers are free: fetch the next tile now
+      nsg = segs[ns];
+      load(next, nsg);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < MS_ITEMS; ++i) {
+      const uint32_t j = (uint32_t)i * MS_THREADS + tid;
+      if (j < cnt) {
+        const uint64_t k = s_keys[j];
+        dst[s_gb[(k >> shift) & 255] + j] = k;
+      }
+    }
+    if (next >= ntiles) break;
+    __syncthreads();  // s_keys / s_gb are reused
+    t = next;
+    s = ns;
+    sg = nsg;
   }
 }
 
@@ -197,116 +223,19 @@ __global__ __launch_bounds__(MS_THREADS) void ms_scatter_kernel(MsBufs bf, const
 //      is a run of whole buckets of about WS + (one bucket) keys;
 //   3. the keys are written to LDS (8 B each) at their bucket positions, in at most two
 //      rounds of LDS_KEYS keys; every wave then takes windows, loads one into registers
-//      (64, 128 or 256 slots, padded with all-ones), sorts it with a bitonic network
+//      (64 or 128 slots, padded with all-ones), sorts it with a bitonic network
 //      (full 64-bit compares; xor partners by lane shuffles, partners >= 64 in registers)
 //      and stores it straight to out.  Sorting whole buckets in place is sorting the segment,
 //      because every key of a bucket is below every key of the next.
-// Fallback (a window > 256 keys, or no round split, e.g. heavy duplicates): the segment is
+// Fallback (a window > 128 keys, or no round split, e.g. heavy duplicates): the segment is
 // listed for ms_lsd_kernel — stable LSD passes in LDS (ballot peer ranking, per-wave digit
 // counters, exchange by 32-bit halves).
-constexpr int LS_WS = 32;           // window stride: windows hold ~WS + one bucket keys
-constexpr int LS_MAX_WINDOW = 256;  // largest bitonic network (4 registers per lane)
+constexpr int LS_WS = 24;           // window stride: windows hold ~WS +- part of a bucket
+constexpr int LS_MAX_WINDOW = 128;  // largest bitonic network (2 registers per lane)
 
-// Value of lane (lane ^ J), 64-bit.  Partners inside a 16-lane row come by DPP (a VALU
-// operand modifier, no LDS round trip): quad_perm for 1 and 2, row_ror:8 for 8, and for 4
-// the two rotations by 4 and 12 with a per-lane choice (`x4`, see xor4_sel); 16 by
-// ds_swizzle (xor mode within 32 lanes); 32 by ds_bpermute.
-template <int CTRL>
-__device__ __forceinline__ uint64_t dpp64(uint64_t v) {
-  const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, CTRL, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), CTRL, 0xF, 0xF, false);
-  return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
-}
-constexpr int DPP_QUAD_X1 = 0xB1;  // quad_perm [1,0,3,2]
-constexpr int DPP_QUAD_X2 = 0x4E;  // quad_perm [2,3,0,1]
-constexpr int DPP_ROR4 = 0x124, DPP_ROR8 = 0x128, DPP_ROR12 = 0x12C;
-// true where row_ror:4 delivers lane ^ 4 (else row_ror:12 does)
-__device__ __forceinline__ bool xor4_sel(int lane) {
-  return __builtin_amdgcn_update_dpp(0, lane, DPP_ROR4, 0xF, 0xF, false) == (lane ^ 4);
-}
-template <int J>
-__device__ __forceinline__ uint64_t lane_xor(uint64_t v, bool x4) {
-  if constexpr (J == 1) {
-    return dpp64<DPP_QUAD_X1>(v);
-  } else if constexpr (J == 2) {
-    return dpp64<DPP_QUAD_X2>(v);
-  } else if constexpr (J == 4) {
-    const uint64_t a = dpp64<DPP_ROR4>(v), b = dpp64<DPP_ROR12>(v);
-    return x4 ? a : b;
-  } else if constexpr (J == 8) {
-    return dpp64<DPP_ROR8>(v);
-  } else if constexpr (J == 16) {
-    const int lo = __builtin_amdgcn_ds_swizzle((int)(uint32_t)v, 0x401F);  // and 0x1F, xor 0x10
-    const int hi = __builtin_amdgcn_ds_swizzle((int)(uint32_t)(v >> 32), 0x401F);
-    return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
-  } else {
-    const int lo = __shfl_xor((int)(uint32_t)v, J, 64);
-    const int hi = __shfl_xor((int)(uint32_t)(v >> 32), J, 64);
-    return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
-  }
-}
-
-// one compare-exchange stage (partner lane ^ J, J < 64) over R registers
-template <int J, int R>
-__device__ __forceinline__ void cx_lanes(uint64_t (&v)[R], int lane, bool x4, int k) {
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const uint64_t p = lane_xor<J>(v[r], x4);
-    const bool up = ((((r << 6) | lane) & k) == 0);
-    const bool take_min = ((lane & J) == 0) == up;
-    const uint64_t mn = v[r] < p ? v[r] : p, mx = v[r] < p ? p : v[r];
-    v[r] = take_min ? mn : mx;
-  }
-}
-template <int J, int R>
-__device__ __forceinline__ void cx_lanes_ind(uint64_t (&v)[R], int lane, bool x4, int k) {
-  // R independent 64-element networks: direction from the lane bits only
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const uint64_t p = lane_xor<J>(v[r], x4);
-    const bool up = (lane & k) == 0 || k == 64;
-    const bool take_min = ((lane & J) == 0) == up;
-    const uint64_t mn = v[r] < p ? v[r] : p, mx = v[r] < p ? p : v[r];
-    v[r] = take_min ? mn : mx;
-  }
-}
-
-// ascending bitonic sort of the 64*R values v[r] at positions r*64 + lane
-template <int R>
-__device__ __forceinline__ void wave_bitonic(uint64_t (&v)[R], int lane, bool x4) {
-  constexpr int N = 64 * R;
-#pragma unroll
-  for (int k = 2; k <= N; k <<= 1) {
-#pragma unroll
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      if (j >= 64) {
-        const int jr = j >> 6;
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-          if (r & jr) continue;
-          const int r2 = r | jr;
-          const bool up = ((r << 6) & k) == 0;  // k >= 128: the lane bits do not matter
-          const uint64_t a = v[r], b = v[r2];
-          const bool sw = up ? (a > b) : (a < b);
-          v[r] = sw ? b : a;
-          v[r2] = sw ? a : b;
-        }
-      } else if (j == 32) {
-        cx_lanes<32, R>(v, lane, x4, k);
-      } else if (j == 16) {
-        cx_lanes<16, R>(v, lane, x4, k);
-      } else if (j == 8) {
-        cx_lanes<8, R>(v, lane, x4, k);
-      } else if (j == 4) {
-        cx_lanes<4, R>(v, lane, x4, k);
-      } else if (j == 2) {
-        cx_lanes<2, R>(v, lane, x4, k);
-      } else {
-        cx_lanes<1, R>(v, lane, x4, k);
-      }
-    }
-  }
-}
+constexpr int DPP_QUAD_X1 = 0xB1;  // quad_perm [1,0,3,2]: lane ^ 1
+constexpr int DPP_QUAD_X2 = 0x4E;  // quad_perm [2,3,0,1]: lane ^ 2
+constexpr int DPP_ROR8 = 0x128;    // row_ror:8: lane ^ 8 within 16
 
 // 32-bit DPP move (bound_ctrl: every lane is a valid source for the patterns used here)
 template <int CTRL>
@@ -378,25 +307,37 @@ __device__ __forceinline__ void wave_bitonic64_multi(uint64_t (&v)[NW], int lane
   cx64<1, 1, NW>(v, lane);
 }
 
-template <int R>
-__device__ __forceinline__ void sort_window(const uint64_t *w, uint32_t m, uint64_t *dst, uint64_t flip, int lane,
-                                            bool x4) {
-  uint64_t v[R];
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const uint32_t e = (uint32_t)(r * 64 + lane);
-    v[r] = e < m ? w[e] : ~0ull;
+// Sort one window of m <= 128 keys in place in LDS with the whole wave: m <= 64 one
+// network; otherwise two sorted 64-halves merged by the block-128 mirror stage (lane ^ 63
+// across the two registers) and the half-cleaners inside each register.
+__device__ __forceinline__ void sort_window(uint64_t *w, uint32_t m, int lane) {
+  if (m <= 64) {
+    uint64_t v[1] = {(uint32_t)lane < m ? w[lane] : ~0ull};
+    wave_bitonic64_multi<1>(v, lane);
+    if ((uint32_t)lane < m) w[lane] = v[0];
+    return;
   }
-  wave_bitonic<R>(v, lane, x4);
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const uint32_t e = (uint32_t)(r * 64 + lane);
-    if (e < m) dst[e] = v[r] ^ flip;
-  }
+  uint64_t v[2] = {w[lane], (uint32_t)(64 + lane) < m ? w[64 + lane] : ~0ull};
+  wave_bitonic64_multi<2>(v, lane);
+  const uint64_t p = lane_x64<63>(v[1]);
+  const uint64_t mn = v[0] < p ? v[0] : p, mx = v[0] < p ? p : v[0];
+  v[0] = mn;
+  v[1] = lane_x64<63>(mx);
+  cx64<32, 32, 2>(v, lane);
+  cx64<16, 16, 2>(v, lane);
+  cx64<8, 8, 2>(v, lane);
+  cx64<4, 4, 2>(v, lane);
+  cx64<2, 2, 2>(v, lane);
+  cx64<1, 1, 2>(v, lane);
+  w[lane] = v[0];
+  if ((uint32_t)(64 + lane) < m) w[64 + lane] = v[1];
 }
 
 #ifdef NUT_MSD_PROFILE_STOP
-__device__ int g_ms_stop;  // msd_tune: end ms_local_kernel after phase g_ms_stop (0 = run all)
+__device__ int g_ms_stop;  // msd_tune only: 1 load, 3 + ranks/scans/LDS, 4 + windows, 5 = all but windows
+#define MS_STOP(k) (g_ms_stop == (k))
+#else
+#define MS_STOP(k) false
 #endif
 
 template <int THREADS, int MAXK>
@@ -404,12 +345,14 @@ struct LocalCfg {
   static constexpr int WAVES = THREADS / kWave;
   static constexpr int CAP = THREADS * MAXK;
   static constexpr int LDS_KEYS = CAP < 16384 ? CAP : 16384;  // 8-B keys per round
-  static constexpr int SB = THREADS == 1024 ? 10 : (THREADS == 512 ? 9 : 8);  // bucket bits
+  static constexpr int SB = CAP > 8192 ? 11 : (CAP > 2048 ? 10 : 9);  // bucket bits: ~4-10 keys each
   static constexpr int NB = 1 << SB;
-  static_assert(NB == THREADS, "one bucket per thread");
+  static constexpr int BPT = NB / THREADS;  // buckets per thread in the scan
+  static_assert(BPT * THREADS == NB && BPT <= 4, "whole buckets per thread");
   static_assert(CAP <= 2 * LDS_KEYS, "at most two rounds");
-  static_assert(CAP / LS_WS <= THREADS, "one thread per window boundary");
-  // LDS: one round of 8-B keys, bucket starts, window starts, scan words
+  static constexpr int WPT = (CAP / LS_WS + THREADS - 1) / THREADS;  // windows per thread
+  static_assert(WPT <= 2, "at most two windows per thread");
+  // LDS: one round of 8-B keys, bucket counts -> starts, window starts, scan words
   static constexpr int BYTES = LDS_KEYS * 8 + (2 * (NB + 1) + 16 + 2) * 4;
 };
 
@@ -437,6 +380,71 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t *ws, ui
   return incl - x + add;
 }
 
+// Batcher's odd-even merge sort network on N (power of two) elements, as a compile-time
+// list of compare-exchange pairs (N = 32: 191 pairs).
+template <int N>
+struct OemNet {
+  int a[N * N], b[N * N], n = 0;
+  constexpr void merge(int lo, int cnt, int r) {
+    const int step = r * 2;
+    if (step < cnt) {
+      merge(lo, cnt, step);
+      merge(lo + r, cnt, step);
+      for (int i = lo + r; i + r < lo + cnt; i += step) {
+        a[n] = i;
+        b[n] = i + r;
+        ++n;
+      }
+    } else {
+      a[n] = lo;
+      b[n] = lo + r;
+      ++n;
+    }
+  }
+  constexpr void sort(int lo, int cnt) {
+    if (cnt > 1) {
+      sort(lo, cnt / 2);
+      sort(lo + cnt / 2, cnt / 2);
+      merge(lo, cnt, 1);
+    }
+  }
+  constexpr OemNet() : a(), b() { sort(0, N); }
+};
+constexpr OemNet<32> kOem32{};
+
+// every lane sorts its own 32 registers ascending (no cross-lane traffic: 191 independent-
+// per-stage compare-exchanges of v_cmp_lt_u64 + 4 v_cndmask)
+__device__ __forceinline__ void lane_sort32(uint64_t (&v)[32]) {
+#pragma unroll
+  for (int i = 0; i < kOem32.n; ++i) {
+    const uint64_t x = v[kOem32.a[i]], y = v[kOem32.b[i]];
+    const bool lt = x < y;
+    v[kOem32.a[i]] = lt ? x : y;
+    v[kOem32.b[i]] = lt ? y : x;
+  }
+}
+
+// Half-wave batches: register r holds window 2r in lanes 0-31 and window 2r+1 in lanes
+// 32-63; NR registers = 2*NR windows of <= 32 keys, one 15-stage network each.
+template <int NR>
+__device__ __forceinline__ void wave_bitonic32_multi(uint64_t (&v)[NR], int lane) {
+  cx64<1, 1, NR>(v, lane);
+  cx64<3, 2, NR>(v, lane);
+  cx64<1, 1, NR>(v, lane);
+  cx64<7, 4, NR>(v, lane);
+  cx64<2, 2, NR>(v, lane);
+  cx64<1, 1, NR>(v, lane);
+  cx64<15, 8, NR>(v, lane);
+  cx64<4, 4, NR>(v, lane);
+  cx64<2, 2, NR>(v, lane);
+  cx64<1, 1, NR>(v, lane);
+  cx64<31, 16, NR>(v, lane);
+  cx64<8, 8, NR>(v, lane);
+  cx64<4, 4, NR>(v, lane);
+  cx64<2, 2, NR>(v, lane);
+  cx64<1, 1, NR>(v, lane);
+}
+
 template <int THREADS, int MAXK>
 __global__ __launch_bounds__(THREADS) void ms_local_kernel(MsBufs bf, const MsSeg *__restrict__ segs, MsShifts sh,
                                                            uint64_t flip, uint32_t *__restrict__ fb) {
@@ -444,12 +452,11 @@ __global__ __launch_bounds__(THREADS) void ms_local_kernel(MsBufs bf, const MsSe
   constexpr int WAVES = C::WAVES, NB = C::NB, SB = C::SB;
   __shared__ __attribute__((aligned(16))) char lds[C::BYTES];
   uint64_t *s_keys = (uint64_t *)lds;
-  uint32_t *s_off = (uint32_t *)(lds + C::LDS_KEYS * 8);  // [NB + 1] bucket starts, then c
+  uint32_t *s_off = (uint32_t *)(lds + C::LDS_KEYS * 8);  // [NB + 1] bucket counts -> starts, then c
   uint32_t *s_win = s_off + NB + 1;                        // [NB + 1] window starts
   uint32_t *s_ws = s_win + NB + 1;                         // 16 scan words
   uint32_t *s_misc = s_ws + 16;                            // [0] max window, [1] round split
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const bool x4 = xor4_sel(lane);
   const MsSeg sg = segs[blockIdx.x];
   const uint32_t c = (uint32_t)sg.count;
   const int ndig = (int)sg.aux;
@@ -461,10 +468,8 @@ __global__ __launch_bounds__(THREADS) void ms_local_kernel(MsBufs bf, const MsSe
   uint64_t key[MAXK];
 #pragma unroll
   for (int i = 0; i < MAXK; ++i) {
-    if ((uint32_t)i < K) {
-      const uint32_t p = pw + (uint32_t)i * kWave;
-      key[i] = p < c ? (src[p] ^ f) : ~0ull;
-    }
+    const uint32_t p = pw + (uint32_t)i * kWave;
+    if ((uint32_t)i < K) key[i] = p < c ? (src[p] ^ f) : ~0ull;
   }
   if (ndig == 0) {  // every key equal: copy
 #pragma unroll
@@ -474,26 +479,25 @@ __global__ __launch_bounds__(THREADS) void ms_local_kernel(MsBufs bf, const MsSe
     }
     return;
   }
-#ifdef NUT_MSD_PROFILE_STOP
-  if (g_ms_stop == 1) {  // load only
+  if (MS_STOP(1)) {
     uint64_t x = 0;
+#pragma unroll
     for (int i = 0; i < MAXK; ++i)
       if ((uint32_t)i < K) x ^= key[i];
     dst[tid] = x;
     return;
   }
-#endif
   // ---- 1. bucket ranks: top SB remaining varying bits
   const int top = sh.s[ndig - 1];
   const int nxt = ndig >= 2 ? sh.s[ndig - 2] : -1;
   constexpr int EXTRA = SB - 8;
   auto bucket = [&](uint64_t k) -> uint32_t {
     uint32_t b = ((uint32_t)(k >> top) & 255u) << EXTRA;
-    if (EXTRA > 0 && nxt >= 0) b |= (uint32_t)(k >> (nxt + 8 - EXTRA)) & ((1u << EXTRA) - 1u);
+    if (nxt >= 0) b |= (uint32_t)(k >> (nxt + 8 - EXTRA)) & ((1u << EXTRA) - 1u);
     return b;
   };
-  uint32_t *s_cnt = s_win;  // counts live where the window table goes later
-  s_cnt[tid] = 0;
+#pragma unroll
+  for (int j = 0; j < C::BPT; ++j) s_off[C::BPT * tid + j] = 0;
   if (tid == 0) {
     s_misc[0] = 0;
     s_misc[1] = 0;
@@ -505,50 +509,62 @@ __global__ __launch_bounds__(THREADS) void ms_local_kernel(MsBufs bf, const MsSe
 #pragma unroll
   for (int i = 0; i < MAXK; ++i) {
     const uint32_t p = pw + (uint32_t)i * kWave;
-    if ((uint32_t)i < K && p < c) rk[i / 2] |= atomicAdd(&s_cnt[bucket(key[i])], 1u) << (16 * (i & 1));
+    if ((uint32_t)i < K && p < c) rk[i / 2] |= atomicAdd(&s_off[bucket(key[i])], 1u) << (16 * (i & 1));
   }
   __syncthreads();
-#ifdef NUT_MSD_PROFILE_STOP
-  if (g_ms_stop == 2) {  // + bucket ranks
-    dst[tid] = rk[0] ^ rk[MAXK / 2 - 1];
-    return;
+  // ---- 2. bucket starts (BPT consecutive buckets per thread) and windows
+  {
+    uint32_t cb[C::BPT], sum = 0;
+#pragma unroll
+    for (int j = 0; j < C::BPT; ++j) {
+      cb[j] = s_off[C::BPT * tid + j];
+      sum += cb[j];
+    }
+    uint32_t tot;
+    uint32_t e = block_excl_scan<THREADS>(sum, s_ws, &tot);
+    __syncthreads();  // every count read before the starts overwrite them
+#pragma unroll
+    for (int j = 0; j < C::BPT; ++j) {
+      s_off[C::BPT * tid + j] = e;
+      e += cb[j];
+    }
+    if (tid == 0) s_off[NB] = c;
   }
-#endif
-  // ---- 2. bucket offsets and windows
-  uint32_t tot;
-  const uint32_t off = block_excl_scan<THREADS>(s_cnt[tid], s_ws, &tot);
-  s_off[tid] = off;
-  if (tid == 0) s_off[NB] = c;
   __syncthreads();
   const uint32_t nq = (c + LS_WS - 1) / LS_WS;
-  if ((uint32_t)tid < nq) {  // first bucket start >= tid * WS
-    const uint32_t target = (uint32_t)tid * LS_WS;
-    uint32_t lo = 0;
 #pragma unroll
-    for (int step = NB / 2; step >= 1; step >>= 1)
-      if (s_off[lo + step - 1] < target) lo += step;
-    s_win[tid] = s_off[lo];  // s_off[NB] = c bounds the search
+  for (int j = 0; j < C::WPT; ++j) {
+    const uint32_t q = (uint32_t)tid + (uint32_t)j * THREADS;
+    if (q < nq) {  // first bucket start >= q * WS
+      const uint32_t target = q * LS_WS;
+      uint32_t lo = 0;
+#pragma unroll
+      for (int step = NB / 2; step >= 1; step >>= 1)
+        if (s_off[lo + step - 1] < target) lo += step;
+      s_win[q] = s_off[lo];  // s_off[NB] = c bounds the search
+    }
   }
   if (tid == 0) s_win[nq] = c;
   __syncthreads();
-  if ((uint32_t)tid < nq) {
-    const uint32_t a = s_win[tid], b = s_win[tid + 1];
-    atomicMax(&s_misc[0], b - a);
-    if (a <= (uint32_t)C::LDS_KEYS) atomicMax(&s_misc[1], (uint32_t)tid);
+#pragma unroll
+  for (int j = 0; j < C::WPT; ++j) {
+    const uint32_t q = (uint32_t)tid + (uint32_t)j * THREADS;
+    if (q < nq) {
+      const uint32_t wa = s_win[q], wb = s_win[q + 1];
+      atomicMax(&s_misc[0], wb - wa);
+      if (wa <= (uint32_t)C::LDS_KEYS) atomicMax(&s_misc[1], q);
+    }
   }
   __syncthreads();
   // rounds: windows [0, split) then [split, nq) with at most LDS_KEYS keys each
-  uint32_t split = nq;
-  if (c > (uint32_t)C::LDS_KEYS) split = s_misc[1];
+  const uint32_t split = c > (uint32_t)C::LDS_KEYS ? s_misc[1] : nq;
   const uint32_t mid = split < nq ? s_win[split] : c;
-  const bool lsd = s_misc[0] > (uint32_t)LS_MAX_WINDOW || c - mid > (uint32_t)C::LDS_KEYS;
-  if (lsd) {  // uniform: leave the segment to ms_lsd_kernel
-    if (tid == 0) fb[1 + atomicAdd(&fb[0], 1u)] = blockIdx.x;
+  if (s_misc[0] > (uint32_t)LS_MAX_WINDOW || c - mid > (uint32_t)C::LDS_KEYS) {
+    if (tid == 0) fb[1 + atomicAdd(&fb[0], 1u)] = blockIdx.x;  // uniform: to ms_lsd_kernel
     return;
   }
   // ---- 3. keys to their bucket positions: round 0's into LDS, round 1's parked in out at
-  //         their final range (L2-resident; every key is already in registers, so this is
-  //         safe in place), which frees the key registers before the networks run
+  //         their final range (L2-resident; safe in place, every key is in registers)
 #pragma unroll
   for (int i = 0; i < MAXK; ++i) {
     const uint32_t p = pw + (uint32_t)i * kWave;
@@ -560,13 +576,11 @@ __global__ __launch_bounds__(THREADS) void ms_local_kernel(MsBufs bf, const MsSe
         dst[pos] = key[i];
     }
   }
-#ifdef NUT_MSD_PROFILE_STOP
-  if (g_ms_stop == 3) {  // + scans, windows, LDS writes / parking
+  if (MS_STOP(3)) {
     __syncthreads();
     dst[tid] = s_keys[tid];
     return;
   }
-#endif
   for (int round = 0; round < 2; ++round) {
     const uint32_t base = round ? mid : 0;
     const uint32_t w0 = round ? split : 0, w1 = round ? nq : split;
@@ -576,40 +590,32 @@ __global__ __launch_bounds__(THREADS) void ms_local_kernel(MsBufs bf, const MsSe
       for (uint32_t j = tid; j < c - mid; j += THREADS) s_keys[j] = ld_agent(dst + mid + j);  // L1-bypassing
     }
     __syncthreads();
-    // this wave's windows t = w0 + wave + WAVES*j, four at a time through independent
-    // 64-element networks; a group holding a window > 64 keys goes one by one
-    for (uint32_t t = w0 + wave; t < w1; t += 4 * WAVES) {
-      uint32_t a[4], m[4];
-      bool small = true;
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const uint32_t tg = t + (uint32_t)g * WAVES;
-        a[g] = tg < w1 ? s_win[tg] : 0;
-        m[g] = tg < w1 ? s_win[tg + 1] - a[g] : 0;
-        small = small && m[g] <= 64;
-      }
-      if (small) {
-        uint64_t v[4];
-#pragma unroll
-        for (int g = 0; g < 4; ++g) v[g] = (uint32_t)lane < m[g] ? s_keys[a[g] - base + lane] : ~0ull;
-        wave_bitonic64_multi<4>(v, lane);
-#pragma unroll
-        for (int g = 0; g < 4; ++g)
-          if ((uint32_t)lane < m[g]) dst[a[g] + lane] = v[g] ^ flip;
-      } else {
+    // one window per thread (nq <= THREADS): each lane sorts its window of <= 32 keys in
+    // its own registers, the rare larger window goes through a wave-wide network; sorted
+    // windows go back to LDS, then the round is copied out coalesced
 #pragma unroll 1
-        for (int g = 0; g < 4; ++g) {
-          const uint64_t *w = s_keys + (a[g] - base);
-          if (m[g] == 0) continue;
-          if (m[g] <= 64)
-            sort_window<1>(w, m[g], dst + a[g], flip, lane, x4);
-          else if (m[g] <= 128)
-            sort_window<2>(w, m[g], dst + a[g], flip, lane, x4);
-          else
-            sort_window<4>(w, m[g], dst + a[g], flip, lane, x4);
-        }
+    for (int j = 0; j < C::WPT && !MS_STOP(5); ++j) {
+      const uint32_t t = w0 + (uint32_t)tid + (uint32_t)j * THREADS;
+      const uint32_t wa = t < w1 ? s_win[t] - base : 0, wm = t < w1 ? s_win[t + 1] - s_win[t] : 0;
+      const bool mine = wm > 1 && wm <= 32;
+      if (__ballot(mine)) {
+        uint64_t v[32];
+#pragma unroll
+        for (int i = 0; i < 32; ++i) v[i] = (mine && (uint32_t)i < wm) ? s_keys[wa + i] : ~0ull;
+        lane_sort32(v);
+#pragma unroll
+        for (int i = 0; i < 32; ++i)
+          if (mine && (uint32_t)i < wm) s_keys[wa + i] = v[i];
+      }
+      for (uint64_t big = __ballot(wm > 32); big; big &= big - 1) {
+        const int l = __builtin_ctzll(big);
+        sort_window(s_keys + __shfl(wa, l, 64), __shfl(wm, l, 64), lane);
       }
     }
+    __syncthreads();
+    if (MS_STOP(4)) continue;
+    const uint32_t rend = round ? c : mid;
+    for (uint32_t j = tid; j < rend - base; j += THREADS) dst[base + j] = s_keys[j] ^ flip;
   }
 }
 
@@ -937,8 +943,9 @@ nut_status msd_sort_i64(nut_ctx *c, const int64_t *in, int64_t *out, uint64_t n,
       if ((s = ar.upload(scat, &dsc)) || (s = ar.upload(tiles, &dt)) || (s = ar.upload(cursor, &dcur))) return s;
       for (const MsSeg &sg : scat) c->sort_bytes += 16 * sg.count;
       ++c->sort_levels;
-      hipLaunchKernelGGL(ms_scatter_kernel, dim3((unsigned)nst), dim3(MS_THREADS), 0, st, bf, (const MsSeg *)dsc,
-                         (const uint32_t *)dt, 8 * digit, flip, (unsigned long long *)dcur);
+      const unsigned sgrid = (unsigned)std::min<uint64_t>(nst, (uint64_t)c->num_cus * 2);  // persistent, 2 per CU
+      hipLaunchKernelGGL(ms_scatter_kernel, dim3(sgrid), dim3(MS_THREADS), 0, st, bf, (const MsSeg *)dsc,
+                         (const uint32_t *)dt, (uint32_t)nst, 8 * digit, flip, (unsigned long long *)dcur);
       NUT_HIP(hipGetLastError());
     }
     big.swap(next);

@@ -200,19 +200,20 @@ int main(int argc, char **argv) {
     nut::MsShifts sh{{0, 8, 16, 24, 32, 40, 48, 56}};
     // bufs: in unused, a = out, b = tmp (segment source)
     nut::MsBufs bf{nullptr, a, b};
-    for (int variant = 0; variant < 5; ++variant) {
-      const int stop = variant < 4 ? (variant == 0 ? 0 : variant) : 0;
+    const int stops[] = {0, 1, 3, 4, 5, 0};
+    for (int variant = 0; variant < 6; ++variant) {
+      const int stop = stops[variant];
       CK(hipMemcpyToSymbol(HIP_SYMBOL(nut::g_ms_stop), &stop, sizeof(int)));
       float best = 1e9;
       for (int r = 0; r < 3; ++r) {
         hipLaunchKernelGGL(gen48, dim3(4096), dim3(256), 0, 0, b, n);
         CK(hipMemset(dfb0, 0, 4));
         CK(hipEventRecord(e0));
-        if (variant < 4)
-          hipLaunchKernelGGL((nut::ms_local_kernel<1024, 32>), dim3((unsigned)nseg), dim3(1024), 0, 0, bf,
+        if (variant < 5)
+          hipLaunchKernelGGL((nut::ms_local_kernel<512, 48>), dim3((unsigned)nseg), dim3(512), 0, 0, bf,
                              (const nut::MsSeg *)dseg, sh, 0ull, dfb0);
         else
-          hipLaunchKernelGGL((nut::ms_lsd_kernel<1024, 32>), dim3((unsigned)nseg), dim3(1024), 0, 0, bf,
+          hipLaunchKernelGGL((nut::ms_lsd_kernel<512, 48>), dim3((unsigned)nseg), dim3(512), 0, 0, bf,
                              (const nut::MsSeg *)dseg, sh, 0ull, (const uint32_t *)dfb);
         CK(hipEventRecord(e1));
         best = std::min(best, time_it(e0, e1));
@@ -224,8 +225,8 @@ int main(int argc, char **argv) {
       unsigned long long hb;
       CK(hipMemcpy(&hb, bad, 8, hipMemcpyDeviceToHost));
       printf("local %s stop=%d seglen=%u: %.3f ms  (%.0f GB/s) unsorted pairs %llu fallbacks %u\n",
-             variant < 4 ? "msd+bitonic" : "lsd-ballot", stop, seglen, best, 16.0 * nseg * seglen / best / 1e6, hb,
-             variant < 4 ? nfb : 0u);
+             variant < 5 ? "msd+net" : "lsd-ballot", stop, seglen, best, 16.0 * nseg * seglen / best / 1e6, hb,
+             variant < 5 ? nfb : 0u);
     }
   }
   return 0;
