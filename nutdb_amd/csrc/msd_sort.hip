@@ -39,7 +39,7 @@ constexpr int MS_BINS = 256;
 // local-sort classes: threads x max items per thread (ms_local_kernel)
 constexpr int LS_S_THREADS = 256, LS_S_ITEMS = 8;    // <= 2048 keys
 constexpr int LS_M_THREADS = 512, LS_M_ITEMS = 16;   // <= 8192 keys
-constexpr int LS_L_THREADS = 512, LS_L_ITEMS = 48;   // <= 24576 keys
+constexpr int LS_L_THREADS = 1024, LS_L_ITEMS = 24;  // <= 24576 keys
 constexpr uint64_t LS_S_CAP = LS_S_THREADS * LS_S_ITEMS;
 constexpr uint64_t LS_M_CAP = LS_M_THREADS * LS_M_ITEMS;
 constexpr uint64_t LS_CAP = LS_L_THREADS * LS_L_ITEMS;
@@ -230,7 +230,8 @@ __global__ __launch_bounds__(MS_THREADS, 4) void ms_scatter_kernel(MsBufs bf, co
 // Fallback (a window > 128 keys, or no round split, e.g. heavy duplicates): the segment is
 // listed for ms_lsd_kernel — stable LSD passes in LDS (ballot peer ranking, per-wave digit
 // counters, exchange by 32-bit halves).
-constexpr int LS_WS = 24;           // window stride: windows hold ~WS +- part of a bucket
+constexpr int LS_WS = 12;           // window stride: windows hold ~WS +- part of a bucket
+constexpr int LS_LANE_N = 16;       // windows up to this size are sorted inside one lane
 constexpr int LS_MAX_WINDOW = 128;  // largest bitonic network (2 registers per lane)
 
 constexpr int DPP_QUAD_X1 = 0xB1;  // quad_perm [1,0,3,2]: lane ^ 1
@@ -345,7 +346,7 @@ struct LocalCfg {
   static constexpr int WAVES = THREADS / kWave;
   static constexpr int CAP = THREADS * MAXK;
   static constexpr int LDS_KEYS = CAP < 16384 ? CAP : 16384;  // 8-B keys per round
-  static constexpr int SB = CAP > 8192 ? 11 : (CAP > 2048 ? 10 : 9);  // bucket bits: ~4-10 keys each
+  static constexpr int SB = CAP > 8192 ? 12 : (CAP > 2048 ? 11 : 9);  // bucket bits: ~4-6 keys each
   static constexpr int NB = 1 << SB;
   static constexpr int BPT = NB / THREADS;  // buckets per thread in the scan
   static_assert(BPT * THREADS == NB && BPT <= 4, "whole buckets per thread");
@@ -353,7 +354,8 @@ struct LocalCfg {
   static constexpr int WPT = (CAP / LS_WS + THREADS - 1) / THREADS;  // windows per thread
   static_assert(WPT <= 2, "at most two windows per thread");
   // LDS: one round of 8-B keys, bucket counts -> starts, window starts, scan words
-  static constexpr int BYTES = LDS_KEYS * 8 + (2 * (NB + 1) + 16 + 2) * 4;
+  static constexpr int NWIN = CAP / LS_WS + 2;  // window table entries (+ end)
+  static constexpr int BYTES = LDS_KEYS * 8 + ((NB + 1) + NWIN + 16 + 2) * 4;
 };
 
 // block-wide exclusive scan of one value per thread (THREADS <= 1024); returns the prefix
@@ -410,17 +412,22 @@ struct OemNet {
   }
   constexpr OemNet() : a(), b() { sort(0, N); }
 };
-constexpr OemNet<32> kOem32{};
+template <int N>
+struct OemTable {
+  static constexpr OemNet<N> net{};
+};
 
-// every lane sorts its own 32 registers ascending (no cross-lane traffic: 191 independent-
-// per-stage compare-exchanges of v_cmp_lt_u64 + 4 v_cndmask)
-__device__ __forceinline__ void lane_sort32(uint64_t (&v)[32]) {
+// every lane sorts its own N registers ascending: no cross-lane traffic, each compare-
+// exchange is v_cmp_lt_u64 + 4 v_cndmask (N = 16: 63 of them)
+template <int N>
+__device__ __forceinline__ void lane_sort(uint64_t (&v)[N]) {
+  constexpr auto &net = OemTable<N>::net;
 #pragma unroll
-  for (int i = 0; i < kOem32.n; ++i) {
-    const uint64_t x = v[kOem32.a[i]], y = v[kOem32.b[i]];
+  for (int i = 0; i < net.n; ++i) {
+    const uint64_t x = v[net.a[i]], y = v[net.b[i]];
     const bool lt = x < y;
-    v[kOem32.a[i]] = lt ? x : y;
-    v[kOem32.b[i]] = lt ? y : x;
+    v[net.a[i]] = lt ? x : y;
+    v[net.b[i]] = lt ? y : x;
   }
 }
 
@@ -453,8 +460,8 @@ __global__ __launch_bounds__(THREADS) void ms_local_kernel(MsBufs bf, const MsSe
   __shared__ __attribute__((aligned(16))) char lds[C::BYTES];
   uint64_t *s_keys = (uint64_t *)lds;
   uint32_t *s_off = (uint32_t *)(lds + C::LDS_KEYS * 8);  // [NB + 1] bucket counts -> starts, then c
-  uint32_t *s_win = s_off + NB + 1;                        // [NB + 1] window starts
-  uint32_t *s_ws = s_win + NB + 1;                         // 16 scan words
+  uint32_t *s_win = s_off + NB + 1;                        // [NWIN] window starts
+  uint32_t *s_ws = s_win + C::NWIN;                        // 16 scan words
   uint32_t *s_misc = s_ws + 16;                            // [0] max window, [1] round split
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const MsSeg sg = segs[blockIdx.x];
@@ -597,17 +604,41 @@ __global__ __launch_bounds__(THREADS) void ms_local_kernel(MsBufs bf, const MsSe
     for (int j = 0; j < C::WPT && !MS_STOP(5); ++j) {
       const uint32_t t = w0 + (uint32_t)tid + (uint32_t)j * THREADS;
       const uint32_t wa = t < w1 ? s_win[t] - base : 0, wm = t < w1 ? s_win[t + 1] - s_win[t] : 0;
-      const bool mine = wm > 1 && wm <= 32;
+      const bool mine = wm > 1 && wm <= (uint32_t)LS_LANE_N;
       if (__ballot(mine)) {
-        uint64_t v[32];
+        uint64_t v[LS_LANE_N];
 #pragma unroll
-        for (int i = 0; i < 32; ++i) v[i] = (mine && (uint32_t)i < wm) ? s_keys[wa + i] : ~0ull;
-        lane_sort32(v);
+        for (int i = 0; i < LS_LANE_N; ++i) v[i] = (mine && (uint32_t)i < wm) ? s_keys[wa + i] : ~0ull;
+        lane_sort<LS_LANE_N>(v);
 #pragma unroll
-        for (int i = 0; i < 32; ++i)
+        for (int i = 0; i < LS_LANE_N; ++i)
           if (mine && (uint32_t)i < wm) s_keys[wa + i] = v[i];
       }
-      for (uint64_t big = __ballot(wm > 32); big; big &= big - 1) {
+      // windows of LANE_N+1 .. 32 keys: eight at a time, two per register (half-waves)
+      for (uint64_t mid32 = __ballot(wm > (uint32_t)LS_LANE_N && wm <= 32); mid32;) {
+        uint32_t ga[8], gm[8];
+#pragma unroll
+        for (int g = 0; g < 8; ++g) {
+          const int l = mid32 ? __builtin_ctzll(mid32) : 0;
+          gm[g] = mid32 ? __shfl(wm, l, 64) : 0;
+          ga[g] = mid32 ? __shfl(wa, l, 64) : 0;
+          mid32 &= mid32 - 1;
+        }
+        const uint32_t h = (uint32_t)lane & 31;
+        uint64_t v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const uint32_t mg = lane < 32 ? gm[2 * r] : gm[2 * r + 1], ag = lane < 32 ? ga[2 * r] : ga[2 * r + 1];
+          v[r] = h < mg ? s_keys[ag + h] : ~0ull;
+        }
+        wave_bitonic32_multi<4>(v, lane);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const uint32_t mg = lane < 32 ? gm[2 * r] : gm[2 * r + 1], ag = lane < 32 ? ga[2 * r] : ga[2 * r + 1];
+          if (h < mg) s_keys[ag + h] = v[r];
+        }
+      }
+      for (uint64_t big = __ballot(wm > 32); big; big &= big - 1) {  // rare: one by one
         const int l = __builtin_ctzll(big);
         sort_window(s_keys + __shfl(wa, l, 64), __shfl(wm, l, 64), lane);
       }

@@ -15,10 +15,11 @@ from prof_summary import summarize  # noqa: E402
 WORKLOAD_KERNEL = {"q1": ("tpch_q1_shape_filter_groupby", "agg_kernel"),
                    "groupby": ("groupby_i64_sum_f64", "agg_kernel"),
                    "filter": ("filter_i64_compaction", "filter_i64_kernel"),
-                   "sort": ("sort_i64_radix", "rs_"),
+                   "sort": ("sort_i64_radix", "nut::ms_"),
                    "q12expr": ("q12_shape_expression_groupby", "agg_kernel")}
-# sort: one step = histogram kernel + every radix pass; traffic is summed per step
-STEP_KERNEL = {"sort": "rs_hist_kernel"}
+# sort: one step = every kernel of one MSD sort (2 histograms, 2 scatter levels, the
+# local sort and its fallback); traffic is summed per step (one local-sort launch per step)
+STEP_KERNEL = {"sort": "ms_local_kernel"}
 
 
 def main():
@@ -40,7 +41,7 @@ def main():
     (d / f"pmc_{name}.json").write_text(json.dumps({
         "workload": name, "rows": int(rows), "kernel_match": match, "hbm_bytes_per_launch": traffic,
         "fetch_size_kb": c.get("FETCH_SIZE"), "write_size_kb": c.get("WRITE_SIZE"),
-        "per": "step (all rs_* kernels of one sort)" if wl == "sort" else "launch of " + match,
+        "per": "step (all ms_* kernels of one sort)" if wl == "sort" else "launch of " + match,
         "correction": "read = 2 x FETCH_SIZE (gfx950 wide-stream halving), write = WRITE_SIZE"}, indent=1))
     print(json.dumps({"workload": name, "traffic": traffic, "kernels": s["kernels"][:3]}))
 

@@ -210,10 +210,10 @@ int main(int argc, char **argv) {
         CK(hipMemset(dfb0, 0, 4));
         CK(hipEventRecord(e0));
         if (variant < 5)
-          hipLaunchKernelGGL((nut::ms_local_kernel<512, 48>), dim3((unsigned)nseg), dim3(512), 0, 0, bf,
+          hipLaunchKernelGGL((nut::ms_local_kernel<1024, 24>), dim3((unsigned)nseg), dim3(1024), 0, 0, bf,
                              (const nut::MsSeg *)dseg, sh, 0ull, dfb0);
         else
-          hipLaunchKernelGGL((nut::ms_lsd_kernel<512, 48>), dim3((unsigned)nseg), dim3(512), 0, 0, bf,
+          hipLaunchKernelGGL((nut::ms_lsd_kernel<1024, 24>), dim3((unsigned)nseg), dim3(1024), 0, 0, bf,
                              (const nut::MsSeg *)dseg, sh, 0ull, (const uint32_t *)dfb);
         CK(hipEventRecord(e1));
         best = std::min(best, time_it(e0, e1));
