@@ -32,6 +32,7 @@ struct LTable {
   i64x2 *k12;
   uint32_t *did, *dslot, *ctl;
   uint64_t *priv;
+  uint32_t *spill;  // spill mode: the block's append cursor (LDS)
 };
 
 __host__ __device__ inline size_t lds_layout(uint32_t cap, int nk, int na, bool privm, int P, int bd,
@@ -194,13 +195,13 @@ __device__ __forceinline__ void load2(const AggArgs &p, const uint64_t *col, uin
 
 // rows {i0, i0+1, i1, i1+1}; TAIL: guard every row against n
 template <int NK, class S, int VEC, bool TAIL>
-__device__ __forceinline__ void load_rows(const AggArgs &p, uint64_t i0, uint64_t i1, Rows<S> &x) {
+__device__ __forceinline__ void load_rows(const AggArgs &p, uint64_t i0, uint64_t i1, uint64_t nend, Rows<S> &x) {
   auto ld = [&](const uint64_t *col, uint64_t (&d)[4]) {
     if (TAIL) {
-      d[0] = i0 < p.n ? col[i0] : 0;
-      d[1] = i0 + 1 < p.n ? col[i0 + 1] : 0;
-      d[2] = i1 < p.n ? col[i1] : 0;
-      d[3] = i1 + 1 < p.n ? col[i1 + 1] : 0;
+      d[0] = i0 < nend ? col[i0] : 0;
+      d[1] = i0 + 1 < nend ? col[i0 + 1] : 0;
+      d[2] = i1 < nend ? col[i1] : 0;
+      d[3] = i1 + 1 < nend ? col[i1 + 1] : 0;
     } else {
       load2<VEC>(p, col, i0, d[0], d[1]);
       load2<VEC>(p, col, i1, d[2], d[3]);
@@ -221,15 +222,57 @@ __device__ __forceinline__ void load_rows(const AggArgs &p, uint64_t i0, uint64_
     if (c < S::nv(p)) ld(p.val_col[c], x.vv[c]);
 }
 
+// ------------------------------------------------------------------ spill (partitioned mode)
+// Append the rows with sl[r] == -1 to the staged arrays: one cursor atomic per wave and
+// row slot, on the block's LDS cursor.  A value a masked-out row does not give its aggregate is staged as the
+// aggregate's identity (f64 SUM: -0.0, which leaves every sum bit-identical), a COUNT as
+// 1 / 0 (the partition pass then sums it).
+template <int NK, class S>
+__device__ __forceinline__ void spill_rows(const AggArgs &p, const LTable &lt, const Rows<S> &x,
+                                           const int32_t (&sl)[4], const uint64_t (&av)[S::MA][4],
+                                           const bool (&vm)[S::MA][4]) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t region = (uint64_t)blockIdx.x * p.sp_region;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const bool mine = sl[r] == -1;
+    const uint64_t m = __ballot(mine);
+    if (!m) continue;
+    const int leader = __builtin_ctzll(m);
+    uint32_t b = 0;
+    if (lane == leader) b = atomicAdd(lt.spill, (uint32_t)__popcll(m));
+    b = __shfl(b, leader, 64);
+    if (mine) {
+      const uint64_t pos = region + b + lane_rank(m);
+      const uint64_t k1 = x.k1[r], k2 = NK == 2 ? x.k2[r] : 0;
+      p.sp_cols[0][pos] = owner_hash(k1, k2, NK);
+      p.sp_cols[1][pos] = k1;
+      if (NK == 2) p.sp_cols[2][pos] = k2;
+#pragma unroll
+      for (int a = 0; a < S::MA; ++a) {
+        if (a < S::na(p) && p.sp_map[a] >= 0) {
+          const int k = S::kind(p, a);
+          uint64_t v = av[a][r];
+          if (k == AK_COUNT) v = vm[a][r] ? 1ull : 0ull;
+          else if (!vm[a][r])
+            v = k == AK_SUM_F64 ? 0x8000000000000000ull
+                                : (k == AK_MIN_F64 || k == AK_MAX_F64) ? ord_to_f64(agg_init(k)) : agg_init(k);
+          p.sp_cols[3 + p.sp_map[a]][pos] = v;
+        }
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------------ fold four rows
 template <int NK, bool PRIV, int BD, class S, bool TAIL>
 __device__ __forceinline__ void consume_rows(const AggArgs &p, const LTable &lt, uint64_t i0, uint64_t i1,
-                                             const Rows<S> &x, bool &err) {
+                                             uint64_t nend, const Rows<S> &x, bool &err) {
   constexpr int R = 4;
   constexpr bool LOCKED = NK == 2 || PRIV;
   bool ok[R];
 #pragma unroll
-  for (int r = 0; r < R; ++r) ok[r] = !TAIL || ((r < 2 ? i0 : i1) + (r & 1)) < p.n;
+  for (int r = 0; r < R; ++r) ok[r] = !TAIL || ((r < 2 ? i0 : i1) + (r & 1)) < nend;
   if constexpr (S::kProg) {
     // generated WHERE program (padding rows of the tail never raise)
 #pragma unroll
@@ -382,6 +425,10 @@ __device__ __forceinline__ void consume_rows(const AggArgs &p, const LTable &lt,
     }
   }
   // rows the block table did not admit
+  if (p.sp_counts) {
+    spill_rows<NK, S>(p, lt, x, sl, av, vm);
+    return;
+  }
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     if (sl[r] == -1) {
@@ -414,6 +461,12 @@ __global__ __launch_bounds__(BD) void agg_kernel(AggArgs p) {
     lt.ctl = (uint32_t *)(b + o_ctl);
     lt.priv = (uint64_t *)(b + o_priv);
   }
+  __shared__ uint32_t s_spill;
+  lt.spill = &s_spill;
+  if (p.sp_counts) {
+    if (threadIdx.x == 0) s_spill = 0;
+    __syncthreads();
+  }
   if (cap) {
     for (uint32_t s = threadIdx.x; s < stride; s += BD) {
       lt.slot[s] = kEmpty;
@@ -435,21 +488,28 @@ __global__ __launch_bounds__(BD) void agg_kernel(AggArgs p) {
   }
 
   // grid-stride over row pairs; a step takes pairs q and q + gstride (four rows) and
-  // the next step's loads are issued before this step is folded
-  const uint64_t npairs = (p.n + 1) / 2;
-  const uint64_t full_pairs = p.n / 2;
-  const uint64_t gstride = (uint64_t)gridDim.x * BD;
-  uint64_t q = (uint64_t)blockIdx.x * BD + threadIdx.x;
+  // the next step's loads are issued before this step is folded.  Segment mode: this
+  // block's rows [seg_off[2b], seg_off[2b+1]), block-stride (row base `rb`).
+  uint64_t rb = 0, nrows = p.n, gstride = (uint64_t)gridDim.x * BD, q = (uint64_t)blockIdx.x * BD + threadIdx.x;
+  if (p.seg_off) {
+    rb = p.seg_off[2 * blockIdx.x];
+    nrows = p.seg_off[2 * blockIdx.x + 1] - rb;
+    gstride = BD;
+    q = threadIdx.x;
+  }
+  const uint64_t nend = rb + nrows;
+  const uint64_t npairs = (nrows + 1) / 2;
+  const uint64_t full_pairs = nrows / 2;
   bool err = false;  // an expression raised (integer division by zero)
   if (q + gstride < full_pairs) {
     Rows<S> cur;
-    load_rows<NK, S, VEC, false>(p, 2 * q, 2 * (q + gstride), cur);
+    load_rows<NK, S, VEC, false>(p, rb + 2 * q, rb + 2 * (q + gstride), nend, cur);
     for (;;) {
       const uint64_t qn = q + 2 * gstride;
       const bool more = qn + gstride < full_pairs;
       Rows<S> nxt;
-      if (more) load_rows<NK, S, VEC, false>(p, 2 * qn, 2 * (qn + gstride), nxt);
-      consume_rows<NK, PRIV, BD, S, false>(p, lt, 2 * q, 2 * (q + gstride), cur, err);
+      if (more) load_rows<NK, S, VEC, false>(p, rb + 2 * qn, rb + 2 * (qn + gstride), nend, nxt);
+      consume_rows<NK, PRIV, BD, S, false>(p, lt, rb + 2 * q, rb + 2 * (q + gstride), nend, cur, err);
       q = qn;
       if (!more) break;
       cur = nxt;
@@ -458,13 +518,17 @@ __global__ __launch_bounds__(BD) void agg_kernel(AggArgs p) {
   if (q < npairs) {  // last partial step: at most two pairs left for this lane
     const uint64_t q1 = q + gstride < npairs ? q + gstride : q;
     Rows<S> x;
-    load_rows<NK, S, VEC, true>(p, 2 * q, 2 * q1, x);
+    load_rows<NK, S, VEC, true>(p, rb + 2 * q, rb + 2 * q1, nend, x);
     // a duplicate second pair (q1 == q) is masked out by placing it past the end
-    consume_rows<NK, PRIV, BD, S, true>(p, lt, 2 * q, q1 == q ? p.n : 2 * q1, x, err);
+    consume_rows<NK, PRIV, BD, S, true>(p, lt, rb + 2 * q, q1 == q ? nend : rb + 2 * q1, nend, x, err);
   }
 
   if constexpr (S::kProg) {
     if (err) atomicOr(&p.gt->ctl[1], 2u);  // flag 2: division by zero (query fails)
+  }
+  if (p.sp_counts) {
+    __syncthreads();
+    if (threadIdx.x == 0) p.sp_counts[blockIdx.x] = s_spill;
   }
   if (!cap) return;
   __syncthreads();

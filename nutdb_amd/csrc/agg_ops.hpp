@@ -48,6 +48,17 @@ struct AggArgs {
   uint64_t pred_set[NUT_MAX_PRED][NUT_MAX_SET];    // set values (bits)
   uint64_t kc[kMaxConst];         // expression constants (bits), read by generated shapes
   const GTable *gt;               // device copy of the global table descriptor
+  // Partitioned aggregation (gpart.hip), for more groups than the on-chip tables hold.
+  // Spill mode (sp_counts != 0, lds_cap = 0): every row passing WHERE is appended to the
+  // staged arrays sp_cols = {hash, k1, k2, value arrays...} instead of the global table,
+  // block b at [b * sp_region, ...) (an LDS cursor; the count lands in sp_counts[b]);
+  // aggregate a's value goes to array 3 + sp_map[a] (-1: not staged).
+  uint64_t *sp_cols[3 + NUT_MAX_VALS];
+  unsigned long long *sp_counts;
+  uint64_t sp_region;
+  int32_t sp_map[NUT_MAX_AGGS];
+  // Segment mode (seg_off != 0): block b folds rows [seg_off[2b], seg_off[2b+1]) only.
+  const uint64_t *seg_off;
 };
 
 // ------------------------------------------------------------------ query shapes

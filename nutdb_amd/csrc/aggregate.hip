@@ -2,12 +2,15 @@
 // executor (BASELINE configs 3, 4): table lifecycle, kernel dispatch and the
 // nut_groupby* / nut_groups_* / nut_q1 entry points of include/nutexec.h.
 // Device code: agg_kernel.hpp + agg_ops.hpp (streaming kernel), gtable.hpp (global table).
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
 #include <vector>
 
 #include "agg_kernel.hpp"
+#include "gpart.hpp"
+#include "sort.hpp"
 #include "jit.hpp"
 
 // ============================================================== host side
@@ -136,6 +139,9 @@ nut_status alloc_table(nut_groups *g, uint64_t cap) {
   size_t o_a1 = carve(arena * 8 + 8);
   size_t o_a2 = carve(arena * 8 + 8);
   size_t o_ctl = carve(64);
+  const int nsh_log2 = cap >= (1ull << 18) ? 8 : 0;
+  const uint32_t nsh = 1u << nsh_log2;
+  size_t o_sh = carve((size_t)nsh * 2 * 16 * 4);
   size_t o_gt = carve(sizeof(GTable));
   size_t o_cur = carve(64 * 8);
   size_t o_seg = carve(128 * 8);
@@ -152,10 +158,15 @@ nut_status alloc_table(nut_groups *g, uint64_t cap) {
   t.ak1 = (int64_t *)(b + o_a1);
   t.ak2 = (int64_t *)(b + o_a2);
   t.ctl = (uint32_t *)(b + o_ctl);
+  t.shard = (uint32_t *)(b + o_sh);
+  t.nsh_log2 = nsh_log2;
   t.cap = cap;
   t.log2cap = ilog2(cap);
   t.limit = (uint32_t)std::min<uint64_t>(cap - cap / 4, 0xFFFFFFF0ull);
   t.arena_cap = (uint32_t)std::min<uint64_t>(arena, 0xFFFFFFF0ull);
+  // per shard: the claims of a uniformly hashed 1/nsh of the slots, +1/16 for variance
+  t.limit_sh = nsh == 1 ? t.limit : t.limit / nsh + t.limit / nsh / 16;
+  t.arena_sh = t.arena_cap / nsh;
   t.naggs = g->naggs;
   t.kinds = pack_kinds(g->kinds, g->naggs);
   g->dev_gt = (GTable *)(b + o_gt);
@@ -163,6 +174,7 @@ nut_status alloc_table(nut_groups *g, uint64_t cap) {
   g->dev_segbase = (uint64_t *)(b + o_seg);
   hipStream_t st = g->ctx->stream;
   NUT_HIP(hipMemsetAsync(t.ctl, 0, 64, st));
+  NUT_HIP(hipMemsetAsync(t.shard, 0, (size_t)nsh * 2 * 16 * 4, st));
   NUT_HIP(hipMemcpyAsync(g->dev_gt, &g->gt, sizeof(GTable), hipMemcpyHostToDevice, st));
   uint64_t blocks = std::min<uint64_t>((stride + 255) / 256, (uint64_t)g->ctx->num_cus * 8);
   hipLaunchKernelGGL(gtable_init_kernel, dim3((unsigned)blocks), dim3(256), 0, st, (const GTable *)g->dev_gt, g->nk);
@@ -172,6 +184,8 @@ nut_status alloc_table(nut_groups *g, uint64_t cap) {
 
 nut_status read_ctl(nut_groups *g, uint32_t *ctl4) {
   nut_ctx *c = g->ctx;
+  hipLaunchKernelGGL(gtable_sum_kernel, dim3(1), dim3(256), 0, c->stream, (const GTable *)g->dev_gt);
+  NUT_HIP(hipGetLastError());
   NUT_HIP(hipMemcpyAsync(c->host_pinned, g->gt.ctl, 16, hipMemcpyDeviceToHost, c->stream));
   NUT_HIP(hipStreamSynchronize(c->stream));
   memcpy(ctl4, c->host_pinned, 16);
@@ -238,9 +252,21 @@ size_t lds_bytes(uint32_t cap, int nk, int na, bool priv, int P, int bd) {
   return lds_layout(cap, nk, na, priv, P, bd, &a, &b, &c, &d, &e);
 }
 
+// Partitioned aggregation (gpart.hpp) drives the same kernels in two extra modes.
+struct LaunchExtra {
+  bool spill = false;                      // stage rows passing WHERE (no tables)
+  uint64_t *sp_cols[3 + NUT_MAX_VALS] = {};
+  unsigned long long *sp_counts = nullptr; // [blocks] rows staged per block
+  int32_t sp_map[NUT_MAX_AGGS] = {};
+  uint64_t blocks = 0, region = 0;         // out (spill): grid and per-block staging region
+  const uint64_t *seg_off = nullptr;       // one block per segment: [start, end) pairs, even starts
+  uint32_t nseg = 0;
+};
+
 // launch the streaming aggregation of spec's rows into g's table.  `kinds` are the
 // per-row update kinds (COUNT partials are merged as integer sums).
-nut_status launch_agg(nut_groups *g, const nut_agg_spec *s, uint64_t group_hint, const int32_t *kinds) {
+nut_status launch_agg(nut_groups *g, const nut_agg_spec *s, uint64_t group_hint, const int32_t *kinds,
+                      LaunchExtra *ex = nullptr) {
   nut_ctx *c = g->ctx;
   if (s->n == 0) return NUT_OK;
   AggArgs a;
@@ -282,7 +308,7 @@ nut_status launch_agg(nut_groups *g, const nut_agg_spec *s, uint64_t group_hint,
 
   // on-chip table: 4x the expected groups (load <= 1/4: a key almost always sits in
   // its 4-slot home bucket) within the LDS budget
-  const size_t lds_max = 160 * 1024;
+  const size_t lds_max = 160 * 1024 - 64;  // the kernel also holds a few static LDS words
   const int na = s->naggs;
   // (32 slots = 8 buckets x 32 B = one pass over the 64 LDS banks: for <= 8 groups two
   // home buckets never conflict — distinct buckets hit distinct banks, equal ones broadcast)
@@ -290,9 +316,15 @@ nut_status launch_agg(nut_groups *g, const nut_agg_spec *s, uint64_t group_hint,
   uint32_t lcap = 32;
   while (lcap < want && lds_bytes(lcap * 2, g->nk, na, false, 0, kBdShared) <= lds_max) lcap *= 2;
   if (group_hint > 8ull * lcap) lcap = 0;  // hot keys cannot fit on chip: straight to HBM
+  if (ex && ex->spill) {
+    lcap = 0;
+    a.sp_counts = ex->sp_counts;
+    for (int i = 0; i < 3 + NUT_MAX_VALS; ++i) a.sp_cols[i] = ex->sp_cols[i];
+    for (int i = 0; i < NUT_MAX_AGGS; ++i) a.sp_map[i] = ex->sp_map[i];
+  }
   // private accumulators when every expected group fits P per thread, 2 blocks per CU
   int P = 0;
-  if (lcap && group_hint && group_hint <= (uint64_t)kPrivMax && na > 0) {
+  if (lcap && group_hint && group_hint <= (uint64_t)kPrivMax && na > 0 && !(ex && ex->seg_off)) {
     P = (int)group_hint;
     if (lds_bytes(lcap, g->nk, na, true, P, kBdPriv) > lds_max / 2) P = 0;
   }
@@ -308,6 +340,15 @@ nut_status launch_agg(nut_groups *g, const nut_agg_spec *s, uint64_t group_hint,
   uint64_t pairs = (s->n + 1) / 2;
   uint64_t blocks = std::min<uint64_t>((uint64_t)c->num_cus * blocks_per_cu, (pairs + bd - 1) / bd);
   if (blocks == 0) blocks = 1;
+  if (ex && ex->seg_off) {  // one block per segment (segments start at even rows)
+    a.seg_off = ex->seg_off;
+    blocks = ex->nseg;
+  }
+  if (ex && ex->spill) {  // block b stages at most the rows it visits: 2 per pair of its lanes
+    a.sp_region = 2ull * bd * ((pairs + blocks * bd - 1) / (blocks * bd));
+    ex->blocks = blocks;
+    ex->region = a.sp_region;
+  }
   if (s->prog_mode) {
     // expression mode: the query's own kernel (jit.cpp), compiled once per shape
     JitShape js;
@@ -350,7 +391,10 @@ nut_status ensure_room(nut_groups *g, uint64_t extra) {
   nut_status st = read_ctl(g, ctl);
   if (st) return st;
   uint64_t need = (uint64_t)ctl[0] + extra + 1;
-  if (need <= g->gt.limit && (g->nk == 1 || (uint64_t)ctl[3] + extra <= g->gt.arena_cap)) return NUT_OK;
+  // sharded counters (large tables) overflow per shard: keep 1/8 of headroom for variance
+  const uint64_t slack = g->gt.nsh_log2 ? need / 8 : 0;
+  if (need + slack <= g->gt.limit && (g->nk == 1 || (uint64_t)ctl[3] + extra + slack <= g->gt.arena_cap))
+    return NUT_OK;
   nut_groups fresh;
   fresh.ctx = g->ctx;
   fresh.nk = g->nk;
@@ -376,6 +420,260 @@ nut_status ensure_room(nut_groups *g, uint64_t extra) {
   return NUT_OK;
 }
 
+// ---------------------------------------------------------------- partitioned aggregation
+// (gpart.hpp).  Used when the expected groups exceed what the on-chip tables hold.
+// NUT_GP=0 / 1 forces the path off / on, NUT_GP_LEVELS=1|2 the partition levels (tests).
+constexpr uint64_t kGpMinGroups = 1ull << 16;
+
+int env_int(const char *name, int dflt) {
+  const char *e = getenv(name);
+  return e && *e ? atoi(e) : dflt;
+}
+
+// upload host vectors into a fresh region of ctx->gp_meta (grown after a sync)
+struct GpMeta {
+  nut_ctx *c;
+  size_t off = 0;
+  std::vector<std::vector<char>> keep;
+  static size_t al(size_t x) { return (x + 255) & ~size_t(255); }
+  nut_status begin(size_t total) {
+    off = 0;
+    if (total > c->gp_meta.bytes) {
+      NUT_HIP(hipStreamSynchronize(c->stream));
+      nut_status s = c->gp_meta.reserve(total);
+      if (s) return s;
+    }
+    return NUT_OK;
+  }
+  void *alloc(size_t b) {
+    void *p = (char *)c->gp_meta.ptr + off;
+    off += al(b);
+    return p;
+  }
+  template <class T>
+  nut_status up(const std::vector<T> &v, T **d) {
+    *d = (T *)alloc(v.size() * sizeof(T) + 1);
+    if (v.empty()) return NUT_OK;
+    keep.emplace_back((const char *)v.data(), (const char *)(v.data() + v.size()));
+    NUT_HIP(hipMemcpyAsync(*d, keep.back().data(), v.size() * sizeof(T), hipMemcpyHostToDevice, c->stream));
+    return NUT_OK;
+  }
+};
+
+uint32_t gp_tiles(std::vector<GpSeg> &segs, uint32_t tile, std::vector<uint32_t> &ts) {
+  ts.clear();
+  for (uint32_t i = 0; i < segs.size(); ++i) {
+    segs[i].tile0 = (uint32_t)ts.size();
+    ts.insert(ts.end(), (segs[i].count + tile - 1) / tile, i);
+  }
+  return (uint32_t)ts.size();
+}
+
+// one partition level: histogram + scatter of every segment; returns the 256 counts per
+// segment in `hist`
+// `parts` (if not null): the output is laid out as 256 partitions per input segment, each
+// starting at an even row (16-B aligned for the aggregation's vector loads); their
+// [start, end) pairs are appended to *parts
+nut_status gp_level(nut_ctx *c, GpMeta &mm, std::vector<GpSeg> &segs, int shift, const uint64_t *const *src,
+                    uint64_t *const *dst, int first, int narr, bool gather, std::vector<uint64_t> &hist,
+                    std::vector<uint64_t> *parts = nullptr) {
+  hipStream_t st = c->stream;
+  std::vector<uint32_t> ts;
+  const uint32_t nht = gp_tiles(segs, GP_HTILE, ts);
+  const size_t nh = gather ? 1 : segs.size();  // gather: every segment into one compact range
+  const size_t hb = nh * GP_BINS * 8;
+  nut_status s = mm.begin(GpMeta::al(segs.size() * sizeof(GpSeg)) + GpMeta::al(ts.size() * 4 + 1) + GpMeta::al(hb));
+  if (s) return s;
+  GpSeg *dseg;
+  uint32_t *dts;
+  if ((s = mm.up(segs, &dseg)) || (s = mm.up(ts, &dts))) return s;
+  unsigned long long *dh = (unsigned long long *)mm.alloc(hb);
+  NUT_HIP(hipMemsetAsync(dh, 0, hb, st));
+  if (nht) hipLaunchKernelGGL(gp_hist_kernel, dim3(nht), dim3(GP_HTHREADS), 0, st, src[0], (const GpSeg *)dseg,
+                              (const uint32_t *)dts, shift, gather ? 1 : 0, dh);
+  NUT_HIP(hipGetLastError());
+  hist.resize(nh * GP_BINS);
+  NUT_HIP(hipMemcpyAsync(hist.data(), dh, hb, hipMemcpyDeviceToHost, st));
+  NUT_HIP(hipStreamSynchronize(st));
+  std::vector<uint64_t> cur(hist.size());
+  uint64_t arun = 0;  // aligned layout: one running offset over all (segment, digit)
+  for (size_t i = 0; i < nh; ++i) {
+    uint64_t run = gather ? 0 : segs[i].start;
+    for (int d = 0; d < GP_BINS; ++d) {
+      const uint64_t h = hist[i * GP_BINS + d];
+      if (parts) {
+        arun = (arun + 1) & ~1ull;
+        cur[i * GP_BINS + d] = arun;
+        if (h) {
+          parts->push_back(arun);
+          parts->push_back(arun + h);
+        }
+        arun += h;
+      } else {
+        cur[i * GP_BINS + d] = run;
+        run += h;
+      }
+    }
+  }
+  const uint32_t nst = gp_tiles(segs, GP_TILE, ts);
+  s = mm.begin(GpMeta::al(segs.size() * sizeof(GpSeg)) + GpMeta::al(ts.size() * 4 + 1) + GpMeta::al(cur.size() * 8));
+  if (s) return s;
+  uint64_t *dcur;
+  if ((s = mm.up(segs, &dseg)) || (s = mm.up(ts, &dts)) || (s = mm.up(cur, &dcur))) return s;
+  GpArrays ar;
+  for (int a = 0; a < GP_MAX_ARR; ++a) {
+    ar.src[a] = src[a];
+    ar.dst[a] = dst[a];
+  }
+  ar.first = first;
+  ar.narr = narr;
+  if (nst) hipLaunchKernelGGL(gp_scatter_kernel, dim3(nst), dim3(GP_THREADS), 0, st, ar, (const GpSeg *)dseg,
+                              (const uint32_t *)dts, shift, gather ? 1 : 0, (unsigned long long *)dcur);
+  NUT_HIP(hipGetLastError());
+  return NUT_OK;
+}
+
+// Spill -> partition -> per-partition aggregation into g's table.  *used = false when the
+// query does not fit the staged layout (more than NUT_MAX_VALS staged value arrays).
+nut_status groupby_partitioned(nut_groups *g, const nut_agg_spec *s, uint64_t group_hint, bool *used) {
+  *used = false;
+  nut_ctx *c = g->ctx;
+  hipStream_t st = c->stream;
+  const int nk = g->nk, na = g->naggs;
+  // staged value arrays: every aggregate except a COUNT that takes every row
+  LaunchExtra sp;
+  sp.spill = true;
+  int32_t kinds2[NUT_MAX_AGGS];
+  int nv = 0;
+  for (int a = 0; a < na; ++a) {
+    const bool masked = s->prog_mode && s->agg_mask[a].n;
+    const bool need = g->kinds[a] != AK_COUNT || masked;
+    sp.sp_map[a] = need ? nv++ : -1;
+    kinds2[a] = g->kinds[a] == AK_COUNT && need ? AK_SUM_I64 : g->kinds[a];
+  }
+  if (nv > NUT_MAX_VALS) return NUT_OK;
+  *used = true;
+  const int narr = 3 + nv;  // hash, k1, k2 (unused for one key), values
+  const uint64_t n = s->n;
+  // staging: every block's region (<= n + one region of slack per block) in A, the
+  // compact partitioned records in B (and A again after a second level)
+  const uint64_t maxblocks = (uint64_t)c->num_cus * 8;
+  // (+ one alignment gap per final partition; a multiple of 32 keeps every array 256-B aligned)
+  const uint64_t rows = (n + maxblocks * 2 * kBdShared + 2 * 65536 + 64 + 31) & ~31ull;
+  nut_status e = c->gp_data.reserve(2 * (size_t)narr * rows * 8 + 256);
+  if (e) return e;
+  uint64_t *A[GP_MAX_ARR] = {}, *B[GP_MAX_ARR] = {};
+  for (int i = 0; i < narr; ++i) {
+    A[i] = (uint64_t *)c->gp_data.ptr + (size_t)i * rows;
+    B[i] = (uint64_t *)c->gp_data.ptr + (size_t)(narr + i) * rows;
+  }
+  if (nk == 1) A[2] = B[2] = nullptr;
+  GpMeta mm{c};
+  // ---- 1. spill: WHERE + aggregate arguments evaluated, rows staged per block in A
+  e = mm.begin(GpMeta::al(maxblocks * 8));
+  if (e) return e;
+  unsigned long long *dcnt = (unsigned long long *)mm.alloc(maxblocks * 8);
+  sp.sp_counts = dcnt;
+  for (int i = 0; i < narr; ++i) sp.sp_cols[i] = A[i];
+  e = launch_agg(g, s, group_hint, g->kinds, &sp);
+  if (e) return e;
+  std::vector<uint64_t> cnt(sp.blocks);
+  NUT_HIP(hipMemcpyAsync(cnt.data(), dcnt, sp.blocks * 8, hipMemcpyDeviceToHost, st));
+  uint32_t ctl[4];
+  e = read_ctl(g, ctl);
+  if (e) return e;
+  if (ctl[1] & 2u) return fail(NUT_ERR_INVALID_ARG, "nut_groupby: division by zero in an expression");
+  std::vector<GpSeg> segs;
+  uint64_t nsp = 0;
+  for (uint64_t b = 0; b < sp.blocks; ++b) {
+    if (cnt[b]) segs.push_back(GpSeg{b * sp.region, cnt[b], 0, 0});
+    nsp += cnt[b];
+  }
+  if (nsp == 0) return NUT_OK;
+  // ---- 2. partition by the key hash: 256 or 65536 partitions of ~<= 1K groups
+  int levels = group_hint > 256ull * 1024 ? 2 : 1;
+  levels = env_int("NUT_GP_LEVELS", levels) == 2 ? 2 : 1;
+  c->timer.begin(st, NUT_KERNEL_AGGREGATE);
+  std::vector<uint64_t> hist, parts;  // parts: [start, end) pairs of the final partitions
+  uint64_t **fin = B;
+  if (levels == 1) {
+    e = gp_level(c, mm, segs, 56, A, B, 1, narr, true, hist, &parts);  // last level: hash dropped
+    if (e) return e;
+  } else {
+    e = gp_level(c, mm, segs, 56, A, B, 0, narr, true, hist);
+    if (e) return e;
+    std::vector<GpSeg> s2;
+    uint64_t run = 0;
+    for (int d = 0; d < GP_BINS; ++d) {
+      if (hist[d]) s2.push_back(GpSeg{run, hist[d], 0, 0});
+      run += hist[d];
+    }
+    std::vector<uint64_t> h2;
+    e = gp_level(c, mm, s2, 48, B, A, 1, narr, false, h2, &parts);
+    if (e) return e;
+    fin = A;
+  }
+  c->timer.end(st);
+  const uint32_t nparts = (uint32_t)(parts.size() / 2);
+  // split partitions into chunks (even boundaries) so that the grid fills the chip (chunks
+  // of one partition merge the same keys: a handful of extra merges per group)
+  const uint64_t k = std::max<uint64_t>(1, ((uint64_t)c->num_cus * 4 + nparts - 1) / nparts);
+  std::vector<uint64_t> off;
+  for (uint32_t p = 0; p < nparts; ++p) {
+    const uint64_t a0 = parts[2 * p], a1 = parts[2 * p + 1];
+    uint64_t prev = a0;
+    for (uint64_t j = 1; j <= k; ++j) {
+      const uint64_t cut = j == k ? a1 : std::max<uint64_t>(prev, (a0 + (a1 - a0) * j / k) & ~1ull);
+      if (cut > prev) {
+        off.push_back(prev);
+        off.push_back(cut);
+        prev = cut;
+      }
+    }
+  }
+  const uint32_t nblk = (uint32_t)(off.size() / 2);
+  // ---- 3. one workgroup per partition, its groups in LDS, merged into g's table once
+  nut_agg_spec s2;
+  memset(&s2, 0, sizeof(s2));
+  s2.n = nsp;  // (segment mode reads only the listed ranges)
+  s2.nkeys = nk;
+  s2.keys[0] = (const int64_t *)fin[1];
+  s2.keys[1] = nk == 2 ? (const int64_t *)fin[2] : nullptr;
+  s2.nvals = nv;
+  s2.naggs = na;
+  for (int a = 0; a < na; ++a) {
+    const int k = kinds2[a];
+    s2.agg_op[a] = k == AK_COUNT ? NUT_AGG_COUNT : (k == AK_SUM_F64 || k == AK_SUM_I64) ? NUT_AGG_SUM
+                   : (k == AK_MIN_F64 || k == AK_MIN_I64) ? NUT_AGG_MIN : NUT_AGG_MAX;
+    s2.agg_expr[a] = NUT_EX_COL;
+    if (sp.sp_map[a] >= 0) {
+      s2.agg_arg[a][0] = sp.sp_map[a];
+      s2.val_col[sp.sp_map[a]] = fin[3 + sp.sp_map[a]];
+      s2.val_type[sp.sp_map[a]] = (k == AK_SUM_F64 || k == AK_MIN_F64 || k == AK_MAX_F64) ? NUT_T_F64 : NUT_T_I64;
+    }
+  }
+  e = mm.begin(GpMeta::al(off.size() * 8));
+  if (e) return e;
+  uint64_t *doff;
+  if ((e = mm.up(off, &doff))) return e;
+  LaunchExtra sg;
+  sg.seg_off = doff;
+  sg.nseg = nblk;
+  const uint64_t per = std::max<uint64_t>(64, 2 * ((group_hint + nparts - 1) / nparts));
+  for (int attempt = 0;; ++attempt) {
+    e = launch_agg(g, &s2, per, kinds2, &sg);
+    if (!e) e = read_ctl(g, ctl);
+    if (e) return e;
+    if (!(ctl[1] & 1u)) break;
+    // more groups than the table admits: a larger table, then the same partitions again
+    if (g->gt.cap >= (1ull << 34) || attempt > 12) return fail(NUT_ERR_OOM, "nut_groupby: group table too large");
+    e = alloc_table(g, g->gt.cap * 4);
+    if (e) return e;
+  }
+  NUT_HIP(hipStreamSynchronize(st));  // the host tables in mm.keep outlive their copies
+  return NUT_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -393,6 +691,20 @@ nut_status nut_groupby(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hint, n
   for (int a = 0; a < s->naggs; ++a) g->kinds[a] = kind_of(s, a);
   if (s->nkeys == 0) group_hint = 1;
   uint64_t cap = table_cap_for(group_hint ? group_hint : 8192);
+  const int gp = env_int("NUT_GP", -1);
+  if (s->nkeys >= 1 && s->n && gp != 0 && (gp == 1 || (group_hint >= kGpMinGroups && s->n >= 4 * group_hint))) {
+    bool used = false;
+    st = alloc_table(g, cap);
+    if (!st) st = groupby_partitioned(g, s, group_hint, &used);
+    if (st) {
+      nut_groups_free(g);
+      return st;
+    }
+    if (used) {
+      *out = g;
+      return NUT_OK;
+    }
+  }
   for (int attempt = 0;; ++attempt) {
     st = alloc_table(g, cap);
     if (!st) st = launch_agg(g, s, group_hint, g->kinds);
@@ -547,6 +859,33 @@ nut_status nut_groupby_jit_compile(const nut_agg_spec *s) {
   return jit_kernel(jit_unit(js.src, s->nkeys == 2 ? 2 : 1, false, kBdShared, sizeof(AggArgs)), false, nullptr);
 }
 
+}  // extern "C"
+
+namespace nut {
+// Row i of the compacted columns goes to its key's rank among the (unique, sorted) keys:
+// keys_out[rank] = key, aggs_out[rank * naggs + a] = aggregate a.
+__global__ void groups_place_kernel(const uint64_t *__restrict__ cols, const int64_t *__restrict__ sorted, uint64_t n,
+                                    int naggs, int64_t *__restrict__ keys_out, uint64_t *__restrict__ aggs_out) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const int64_t k = (int64_t)cols[i];
+    uint64_t lo = 0, len = n;
+    while (len > 0) {  // lower bound
+      const uint64_t half = len >> 1;
+      if (sorted[lo + half] < k) {
+        lo += half + 1;
+        len -= half + 1;
+      } else {
+        len = half;
+      }
+    }
+    keys_out[lo] = k;
+    for (int a = 0; a < naggs; ++a) aggs_out[lo * naggs + a] = cols[(uint64_t)(1 + a) * n + i];
+  }
+}
+}  // namespace nut
+
+extern "C" {
+
 nut_status nut_groups_to_host(nut_groups *g, int64_t *keys, uint64_t *aggs, uint64_t cap) {
   if (!g) return fail(NUT_ERR_INVALID_ARG, "nut_groups_to_host: NULL argument");
   uint64_t n;
@@ -563,8 +902,40 @@ nut_status nut_groups_to_host(nut_groups *g, int64_t *keys, uint64_t *aggs, uint
   uint64_t *dev = nullptr;
   NUT_HIP(hipMallocAsync((void **)&dev, (size_t)w * n * 8, c->stream));
   st = nut_groups_to_device(g, dev, n);
+  if (st) {
+    (void)hipFreeAsync(dev, c->stream);
+    return st;
+  }
+  if (g->nk == 1 && n >= (1u << 16)) {
+    // large one-key results are ordered on the device: sort the (unique) keys, then every
+    // group finds its rank by binary search and is placed there
+    const uint64_t saved_bytes = c->sort_bytes;
+    const uint32_t saved_levels = c->sort_levels;
+    uint64_t *buf = nullptr;
+    const size_t nb = (size_t)n * 8;
+    NUT_HIP(hipMallocAsync((void **)&buf, nb * (2 + (size_t)g->naggs), c->stream));
+    int64_t *sorted = (int64_t *)buf, *dk = (int64_t *)(buf + n);
+    uint64_t *da = buf + 2 * n;
+    st = msd_sort_i64(c, (const int64_t *)dev, sorted, n, 0x8000000000000000ull);
+    c->sort_bytes = saved_bytes;
+    c->sort_levels = saved_levels;
+    if (!st) {
+      const uint64_t blocks = std::min<uint64_t>((n + 255) / 256, (uint64_t)c->num_cus * 16);
+      hipLaunchKernelGGL(groups_place_kernel, dim3((unsigned)blocks), dim3(256), 0, c->stream, (const uint64_t *)dev,
+                         (const int64_t *)sorted, n, g->naggs, dk, da);
+      hipError_t e = hipGetLastError();
+      if (e == hipSuccess) e = hipMemcpyAsync(keys, dk, nb, hipMemcpyDeviceToHost, c->stream);
+      if (e == hipSuccess && g->naggs)
+        e = hipMemcpyAsync(aggs, da, nb * g->naggs, hipMemcpyDeviceToHost, c->stream);
+      if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+      if (e != hipSuccess) st = hip_fail(e, "nut_groups_to_host (device order)");
+    }
+    (void)hipFreeAsync(buf, c->stream);
+    (void)hipFreeAsync(dev, c->stream);
+    return st;
+  }
   std::vector<uint64_t> h((size_t)w * n);
-  if (!st) {
+  {
     hipError_t e = hipMemcpyAsync(h.data(), dev, (size_t)w * n * 8, hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) st = hip_fail(e, "nut_groups_to_host copy");

@@ -159,6 +159,8 @@ void nut_ctx_destroy(nut_ctx *c) {
   c->sort_tmp.release();
   c->sort_status.release();
   c->sort_meta.release();
+  c->gp_data.release();
+  c->gp_meta.release();
   c->misc.release();
   c->timer.release();
   if (c->host_pinned) (void)hipHostFree(c->host_pinned);

@@ -171,6 +171,8 @@ struct nut_ctx {
   uint64_t sort_bytes = 0;   // algorithmic bytes of the last sort (nut_ctx_sort_stats)
   uint32_t sort_levels = 0;
   nut::Scratch sort_meta;     // MSD sort per-level segment / tile / histogram tables (msd_sort.hip)
+  nut::Scratch gp_data;       // partitioned aggregation: staged / partitioned records (aggregate.hip)
+  nut::Scratch gp_meta;       //   and their per-level tables
   nut::Scratch misc;
   uint64_t *host_pinned = nullptr;  // small pinned staging for counts/flags
   nut::KernelTimer timer;

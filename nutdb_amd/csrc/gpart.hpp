@@ -1,0 +1,149 @@
+// gpart.hpp — partitioned aggregation for more groups than the on-chip tables hold
+// (BASELINE config 3 at G = 1e5 .. 1e7).
+//
+// The streaming kernel (agg_kernel.hpp) first runs in SPILL mode: it evaluates WHERE and
+// the aggregate arguments as always, but appends every passing row to staged arrays
+// {hash, k1, [k2], value arrays} instead of hashing it into a table.  The kernels here then
+// radix-partition those records by the key hash (one or two 8-bit levels -> 256 or 65536
+// partitions of a few hundred groups each), and the streaming kernel runs again in
+// SEGMENT mode, one workgroup per partition: every group of a partition lives in that
+// workgroup's LDS table, and the block-end merge into the global table inserts each group
+// once, with no contention (partitions hold disjoint keys).
+#pragma once
+
+#include "common.hpp"
+
+namespace nut {
+
+constexpr int GP_THREADS = 512;
+constexpr int GP_ITEMS = 8;
+constexpr uint32_t GP_TILE = GP_THREADS * GP_ITEMS;  // 4096 records per scatter tile
+constexpr int GP_HTHREADS = 256;
+constexpr uint32_t GP_HTILE = 1u << 16;              // records per histogram tile
+constexpr int GP_BINS = 256;
+constexpr int GP_MAX_ARR = 3 + NUT_MAX_VALS;         // hash, k1, k2, value arrays
+
+struct GpSeg {  // records [start, start + count) of the current buffer
+  uint64_t start, count;
+  uint32_t tile0, pad;  // first tile of the segment in the launch's tile table
+};
+
+struct GpArrays {
+  const uint64_t *src[GP_MAX_ARR];
+  uint64_t *dst[GP_MAX_ARR];
+  int first, narr;  // arrays [first, narr) move; src[0] (the hash) gives the digit
+};
+
+// 256-bin histogram of (hash >> shift) & 255 per segment (gather: one for all segments)
+__global__ __launch_bounds__(GP_HTHREADS) void gp_hist_kernel(const uint64_t *__restrict__ h,
+                                                              const GpSeg *__restrict__ segs,
+                                                              const uint32_t *__restrict__ tile_seg, int shift,
+                                                              int gather, unsigned long long *__restrict__ hist) {
+  __shared__ uint32_t cnt[GP_BINS];
+  const int tid = threadIdx.x;
+  cnt[tid] = 0;
+  __syncthreads();
+  const uint32_t s = tile_seg[blockIdx.x];
+  const GpSeg sg = segs[s];
+  const uint64_t lo = sg.start + (uint64_t)(blockIdx.x - sg.tile0) * GP_HTILE;
+  const uint32_t n = (uint32_t)min<uint64_t>(GP_HTILE, sg.start + sg.count - lo);
+  for (uint32_t i = tid; i < n; i += GP_HTHREADS * 8) {
+    uint64_t v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t k = i + j * GP_HTHREADS;
+      v[j] = k < n ? __builtin_nontemporal_load(h + lo + k) : 0;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (i + j * GP_HTHREADS < n) atomicAdd(&cnt[(v[j] >> shift) & 255], 1u);
+  }
+  __syncthreads();
+  if (cnt[tid]) atomicAdd(&hist[(gather ? 0 : (uint64_t)s) * GP_BINS + tid], (unsigned long long)cnt[tid]);
+}
+
+// Unstable partition of every segment's records by (hash >> shift) & 255: a tile ranks its
+// records with LDS atomics and claims each digit's output run with one global atomic on
+// the segment's digit cursor; then every array is staged in LDS in digit order (coalesced
+// loads in, one LDS write per record) and written out in coalesced runs.
+// Gather mode: all segments share one set of 256 cursors (the spilled blocks' regions ->
+// one compact partitioned array).
+__global__ __launch_bounds__(GP_THREADS) void gp_scatter_kernel(GpArrays ar, const GpSeg *__restrict__ segs,
+                                                                const uint32_t *__restrict__ tile_seg, int shift,
+                                                                int gather, unsigned long long *__restrict__ cursor) {
+  __shared__ uint64_t s_stage[GP_TILE];
+  __shared__ uint8_t s_dig[GP_TILE];
+  __shared__ uint32_t s_cnt[GP_BINS];
+  __shared__ uint32_t s_tex[GP_BINS];
+  __shared__ uint64_t s_gb[GP_BINS];
+  __shared__ uint32_t s_wsum[GP_BINS / kWave];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid < GP_BINS) s_cnt[tid] = 0;
+  const uint32_t s = tile_seg[blockIdx.x];
+  const GpSeg sg = segs[s];
+  const uint64_t lo = sg.start + (uint64_t)(blockIdx.x - sg.tile0) * GP_TILE;
+  const uint32_t n = (uint32_t)min<uint64_t>(GP_TILE, sg.start + sg.count - lo);
+  __syncthreads();
+  uint32_t d[GP_ITEMS], slot[GP_ITEMS];
+#pragma unroll
+  for (int i = 0; i < GP_ITEMS; ++i) {
+    const uint32_t idx = (uint32_t)i * GP_THREADS + tid;
+    d[i] = idx < n ? (uint32_t)(__builtin_nontemporal_load(ar.src[0] + lo + idx) >> shift) & 255u : 0u;
+    slot[i] = idx < n ? atomicAdd(&s_cnt[d[i]], 1u) : 0u;
+  }
+  __syncthreads();
+  uint32_t c = 0, incl = 0;
+  if (tid < GP_BINS) {
+    c = s_cnt[tid];
+    incl = c;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t y = __shfl_up(incl, off, 64);
+      if (lane >= off) incl += y;
+    }
+    if (lane == 63) s_wsum[wave] = incl;
+  }
+  __syncthreads();
+  if (tid < GP_BINS) {
+    uint32_t add = 0;
+#pragma unroll
+    for (int w = 0; w < GP_BINS / kWave; ++w) add += (w < wave) ? s_wsum[w] : 0u;
+    const uint32_t tex = incl - c + add;
+    s_tex[tid] = tex;
+    const uint64_t cs = gather ? 0 : (uint64_t)s;
+    const uint64_t gb = c ? (uint64_t)atomicAdd(&cursor[cs * GP_BINS + tid], (unsigned long long)c) : 0;
+    s_gb[tid] = gb - tex;  // output position of tile slot j with digit d = s_gb[d] + j
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < GP_ITEMS; ++i) {
+    const uint32_t idx = (uint32_t)i * GP_THREADS + tid;
+    if (idx < n) {
+      slot[i] += s_tex[d[i]];
+      s_dig[slot[i]] = (uint8_t)d[i];
+    }
+  }
+  for (int a = ar.first; a < ar.narr; ++a) {
+    if (!ar.src[a]) continue;  // k2 of one-key queries
+    const uint64_t *src = ar.src[a] + lo;
+    uint64_t *dst = ar.dst[a];
+    uint64_t v[GP_ITEMS];
+#pragma unroll
+    for (int i = 0; i < GP_ITEMS; ++i) {
+      const uint32_t idx = (uint32_t)i * GP_THREADS + tid;
+      v[i] = idx < n ? __builtin_nontemporal_load(src + idx) : 0;
+    }
+    __syncthreads();  // the previous array's write-out is done with s_stage
+#pragma unroll
+    for (int i = 0; i < GP_ITEMS; ++i)
+      if ((uint32_t)i * GP_THREADS + tid < n) s_stage[slot[i]] = v[i];
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < GP_ITEMS; ++i) {
+      const uint32_t j = (uint32_t)i * GP_THREADS + tid;
+      if (j < n) dst[s_gb[s_dig[j]] + j] = s_stage[j];
+    }
+  }
+}
+
+}  // namespace nut

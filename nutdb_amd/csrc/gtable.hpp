@@ -44,7 +44,13 @@ struct GTable {
   uint64_t *agg;     // [naggs][cap + 1]
   int64_t *ak1;      // [arena_cap] two-key tables: key tuples, written before publication
   int64_t *ak2;
-  uint32_t *ctl;     // [0] claimed, [1] flags (1 overflow), [2] special used, [3] arena next
+  uint32_t *ctl;     // [0] claimed, [1] flags (1 overflow), [2] special used, [3] arena used
+                     //   ([0] and [3] are written by gtable_sum_kernel from the shards)
+  uint32_t *shard;   // claim counters at [i * 16], arena counters at [(nsh + i) * 16]: one
+                     //   64-B line each, so that inserts do not all hit one address
+  int nsh_log2;      // 0 for small tables
+  uint32_t limit_sh; // claims per shard before overflow is flagged
+  uint32_t arena_sh; // arena entries per shard
   uint64_t cap;      // power of two
   uint32_t limit;    // claims allowed before overflow is flagged
   uint32_t arena_cap;
@@ -100,7 +106,7 @@ __device__ __forceinline__ int64_t g_find(const GTable &t, uint64_t h, int64_t k
       uint64_t old = atomicCAS((unsigned long long *)&t.slot[s], (unsigned long long)kEmpty,
                                (unsigned long long)h);
       if (old == kEmpty) {
-        if (atomicAdd(&t.ctl[0], 1u) >= t.limit) atomicOr(&t.ctl[1], 1u);
+        if (atomicAdd(&t.shard[(s & ((1u << t.nsh_log2) - 1)) * 16], 1u) >= t.limit_sh) atomicOr(&t.ctl[1], 1u);
         return (int64_t)s;
       }
       if (old == h) return (int64_t)s;
@@ -108,11 +114,13 @@ __device__ __forceinline__ int64_t g_find(const GTable &t, uint64_t h, int64_t k
       uint64_t cur = rmw_load(&t.slot[s]);
       if (cur == kEmpty2) {
         if (word == kEmpty2) {
-          uint32_t idx = atomicAdd(&t.ctl[3], 1u);
-          if (idx >= t.arena_cap) {
+          const uint32_t sh = tag & ((1u << t.nsh_log2) - 1);
+          const uint32_t loc = atomicAdd(&t.shard[((1u << t.nsh_log2) + sh) * 16], 1u);
+          if (loc >= t.arena_sh) {
             atomicOr(&t.ctl[1], 1u);
             return -1;
           }
+          const uint32_t idx = sh * t.arena_sh + loc;
           // publish the tuple at the memory side before the slot word can point at it
           atomicExch((unsigned long long *)&t.ak1[idx], (unsigned long long)k1);
           atomicExch((unsigned long long *)&t.ak2[idx], (unsigned long long)k2);
@@ -123,7 +131,7 @@ __device__ __forceinline__ int64_t g_find(const GTable &t, uint64_t h, int64_t k
                   ? kEmpty2
                   : cur;
         if (cur == kEmpty2) {
-          if (atomicAdd(&t.ctl[0], 1u) >= t.limit) atomicOr(&t.ctl[1], 1u);
+          if (atomicAdd(&t.shard[(s & ((1u << t.nsh_log2) - 1)) * 16], 1u) >= t.limit_sh) atomicOr(&t.ctl[1], 1u);
           return (int64_t)s;
         }
       }
@@ -172,7 +180,29 @@ __device__ __forceinline__ bool slot_keys(const GTable &t, int nk, uint64_t s, u
   return true;
 }
 
-// dense column-major copy of the occupied slots; owner partitioning optional
+// ctl[0] = claimed groups, ctl[3] = arena entries used (sums of the shard counters)
+__global__ void gtable_sum_kernel(const GTable *__restrict__ gtp) {
+  const GTable t = *gtp;
+  const uint32_t nsh = 1u << t.nsh_log2;
+  uint32_t c = 0, a = 0;
+  for (uint32_t i = threadIdx.x; i < nsh; i += blockDim.x) {
+    c += t.shard[i * 16];
+    a += t.shard[(nsh + i) * 16];
+  }
+  __shared__ uint32_t sc[256], sa[256];
+  sc[threadIdx.x] = c;
+  sa[threadIdx.x] = a;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t tc = 0, ta = 0;
+    for (uint32_t i = 0; i < blockDim.x; ++i) tc += sc[i], ta += sa[i];
+    t.ctl[0] = tc;
+    t.ctl[3] = ta;
+  }
+}
+
+// dense column-major copy of the occupied slots; owner partitioning optional (one
+// cursor atomic per wave when not partitioned)
 __global__ void gtable_compact_kernel(const GTable *__restrict__ gtp, int nk, uint64_t *__restrict__ out,
                                       uint64_t out_cap, unsigned long long *__restrict__ cursors, int nparts,
                                       const uint64_t *__restrict__ seg_base) {
@@ -182,9 +212,21 @@ __global__ void gtable_compact_kernel(const GTable *__restrict__ gtp, int nk, ui
   for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < stride;
        s += (uint64_t)gridDim.x * blockDim.x) {
     uint64_t k1, k2;
-    if (!slot_keys(t, nk, s, k1, k2)) continue;
-    int part = nparts > 1 ? (int)(owner_hash(k1, k2, nk) % (uint64_t)nparts) : 0;
-    uint64_t pos = atomicAdd(&cursors[part], 1ull);
+    const bool occ = slot_keys(t, nk, s, k1, k2);
+    int part = 0;
+    uint64_t pos;
+    if (nparts > 1) {
+      if (!occ) continue;
+      part = (int)(owner_hash(k1, k2, nk) % (uint64_t)nparts);
+      pos = atomicAdd(&cursors[part], 1ull);
+    } else {
+      const uint64_t m = __ballot(occ);
+      if (!occ) continue;
+      const int lane = threadIdx.x & 63, leader = __builtin_ctzll(m);
+      unsigned long long b = 0;
+      if (lane == leader) b = atomicAdd(&cursors[0], (unsigned long long)__popcll(m));
+      pos = __shfl(b, leader, 64) + lane_rank(m);
+    }
     // segment `part` starts at word w*seg_base[part]; each of its columns has seg_n rows
     uint64_t seg_n = nparts > 1 ? seg_base[nparts + part] : out_cap;
     uint64_t *seg = out + (nparts > 1 ? (uint64_t)w * seg_base[part] : 0);

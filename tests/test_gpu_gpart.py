@@ -1,0 +1,130 @@
+"""GPU parity of the partitioned aggregation path (csrc/gpart.hpp): spill
+-> hash partitions (one or two 8-bit levels) -> one workgroup per partition.  NUT_GP=1
+forces the path at test sizes, NUT_GP_LEVELS the partition levels; results must equal the
+oracle exactly as the on-chip path's do (f64 sums within F64_SUM_RTOL, exact for dyadic)."""
+import numpy as np
+import pytest
+
+from helpers import F64_SUM_RTOL, OPCODE, rel_err
+from test_gpu_exec import AGGS4, check_vs_oracle, dev, gb_query
+
+pytestmark = pytest.mark.gpu
+
+I64_MIN = np.iinfo(np.int64).min
+I64_MAX = np.iinfo(np.int64).max
+
+
+@pytest.fixture(params=[1, 2], ids=["levels1", "levels2"])
+def gp(request, monkeypatch):
+    monkeypatch.setenv("NUT_GP", "1")
+    monkeypatch.setenv("NUT_GP_LEVELS", str(request.param))
+    return request.param
+
+
+@pytest.mark.parametrize("G,hint", [(1, 1), (1000, 1000), (100_000, 100_000), (2_000_000, 2_000_000),
+                                    (100_000, 0)])
+def test_gp_cardinalities(ex, orc, gp, G, hint):
+    n = 3_000_017
+    key = orc.gen_column(2, 0x51, n, a=G)
+    val = orc.gen_column(4, 0x52, n)
+    g = ex.groupby(gb_query(dev(key, ex), dev(val, ex)), group_hint=hint)
+    ok, ow = orc.groupby([key], AGGS4, values=[val])
+    assert len(g) == len(ok)
+    check_vs_oracle(g, ok, ow, ["sum_f64", "i", "i", "i"])
+
+
+def test_gp_dyadic_exact_and_predicate(ex, orc, gp):
+    n = 2_000_003
+    key = orc.gen_column(2, 0x51, n, a=300_000)
+    val = orc.gen_column(3, 0x52, n)  # dyadic: every sum exact
+    preds = [(dev(val, ex), "<", 6000.0)]
+    g = ex.groupby(gb_query(dev(key, ex), dev(val, ex), preds), group_hint=300_000)
+    ok, ow = orc.groupby([key], AGGS4, values=[val], preds=[(val, OPCODE["<"], 6000.0)])
+    keys, words = g.to_host_words()
+    assert np.array_equal(keys, ok) and np.array_equal(words, ow)
+
+
+def test_gp_extreme_keys_and_negative_zero(ex, orc, gp):
+    rng = np.random.default_rng(3)
+    n = 400_000
+    key = rng.integers(I64_MIN, I64_MAX, n, dtype=np.int64) // 1000 * 1000
+    key[::7] = I64_MIN
+    key[::11] = I64_MAX
+    key[::13] = np.int64(-9223372036854775808 + 0)  # the table's empty marker
+    val = rng.standard_normal(n)
+    val[::100] = -0.0
+    g = ex.groupby(gb_query(dev(key, ex), dev(val, ex)), group_hint=len(np.unique(key)))
+    ok, ow = orc.groupby([key], AGGS4, values=[val])
+    check_vs_oracle(g, ok, ow, ["sum_f64", "i", "i", "i"])
+
+
+def test_gp_two_keys_preds_exprs(ex, orc, gp):
+    from nutdb_amd import Agg, AggQuery
+    rng = np.random.default_rng(11)
+    n = 1_000_001
+    k1 = rng.integers(-3000, 4000, n).astype(np.int64)
+    k2 = rng.integers(0, 70, n).astype(np.int64) * 1_000_000_007
+    a = rng.random(n)
+    b = rng.random(n)
+    c = rng.random(n)
+    f = rng.integers(0, 100, n).astype(np.int64)
+    q = AggQuery(keys=[dev(k1, ex), dev(k2, ex)], values=[dev(a, ex), dev(b, ex), dev(c, ex)],
+                 preds=[(dev(f, ex), ">=", 10), (dev(a, ex), "<", 0.9)],
+                 aggs=[Agg("sum", "mul", (0, 1)), Agg("sum", "mul_1m_1p", (0, 1, 2)), Agg("min", "sub", (1, 2)),
+                       Agg("count"), Agg("max", "add", (0, 2))])
+    g = ex.groupby(q, group_hint=300_000)
+    ok, ow = orc.groupby([k1, k2], [(0, 1, (0, 1)), (0, 5, (0, 1, 2)), (2, 3, (1, 2)), (1, 0, ()), (3, 2, (0, 2))],
+                         values=[a, b, c], preds=[(f, OPCODE[">="], 10), (a, OPCODE["<"], 0.9)])
+    check_vs_oracle(g, ok, ow, ["sum_f64", "sum_f64", "i", "i", "i"])
+
+
+def test_gp_i64_wrap(ex, orc, gp):
+    from nutdb_amd import Agg, AggQuery
+    rng = np.random.default_rng(5)
+    n = 500_003
+    key = rng.integers(0, 90_000, n).astype(np.int64)
+    v = rng.integers(I64_MIN, I64_MAX, n, dtype=np.int64)
+    q = AggQuery(keys=[dev(key, ex)], values=[dev(v, ex)],
+                 aggs=[Agg("sum", "col", (0,)), Agg("min", "col", (0,)), Agg("max", "col", (0,)), Agg("count")])
+    g = ex.groupby(q, group_hint=90_000)
+    ok, ow = orc.groupby([key], [(0, 0, (0,)), (2, 0, (0,)), (3, 0, (0,)), (1, 0, ())], values=[v])
+    check_vs_oracle(g, ok, ow, ["i", "i", "i", "i"])
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_gp_expression_programs_with_masks(ex, gp, seed):
+    """Expression mode through the spill: masked COUNT is staged as 0/1, a masked-out value
+    as its aggregate's identity — the groups and words equal the numpy oracle's."""
+    from test_gpu_expr import Gen, make_table, run_both
+    rng = np.random.default_rng(2000 + seed)
+    n = 300_007
+    cols, ic, fc = make_table(rng, n)
+    g = Gen(rng, ic, fc)
+    keys = [rng.integers(0, 50_000, n).astype(np.int64)]
+    if seed % 2:
+        keys.append(rng.integers(0, 3, n).astype(np.int64))
+    where = g.bool_(2) if seed != 3 else None
+    aggs = [("sum", g.int_(3), None), ("count", None, g.bool_(2)), ("max", g.f64_(2), g.bool_(1)),
+            ("min", g.int_(2), g.bool_(1))]
+    gk, gw, ok, ow, types = run_both(ex, keys, cols, where, aggs, 50_000)
+    assert np.array_equal(gk, ok)
+    assert np.array_equal(gw, ow), (seed, np.argwhere(gw != ow)[:5])
+
+
+def test_gp_empty_and_all_rejected(ex, orc, gp):
+    key = np.arange(5000, dtype=np.int64)
+    val = np.ones(5000)
+    g = ex.groupby(gb_query(dev(key, ex), dev(val, ex), [(dev(key, ex), "<", -5)]), group_hint=5000)
+    assert len(g) == 0
+
+
+def test_gp_table_growth(ex, orc, monkeypatch):
+    """A hint far below the real group count: the partitioned pass grows the table and
+    re-runs only the per-partition aggregation."""
+    monkeypatch.setenv("NUT_GP", "1")
+    n = 2_000_000
+    key = orc.gen_column(2, 0x51, n, a=500_000)
+    val = orc.gen_column(4, 0x52, n)
+    g = ex.groupby(gb_query(dev(key, ex), dev(val, ex)), group_hint=1000)
+    ok, ow = orc.groupby([key], AGGS4, values=[val])
+    check_vs_oracle(g, ok, ow, ["sum_f64", "i", "i", "i"])
