@@ -33,6 +33,7 @@ struct LTable {
   uint32_t *did, *dslot, *ctl;
   uint64_t *priv;
   uint32_t *spill;  // spill mode: the block's append cursor (LDS)
+  uint32_t *shist;  //   and its histogram of the key hash's top byte (LDS, 256)
 };
 
 __host__ __device__ inline size_t lds_layout(uint32_t cap, int nk, int na, bool privm, int P, int bd,
@@ -245,7 +246,7 @@ __device__ __forceinline__ void spill_rows(const AggArgs &p, const LTable &lt, c
     if (mine) {
       const uint64_t pos = region + b + lane_rank(m);
       const uint64_t k1 = x.k1[r], k2 = NK == 2 ? x.k2[r] : 0;
-      p.sp_cols[0][pos] = owner_hash(k1, k2, NK);
+      atomicAdd(&lt.shist[owner_hash(k1, k2, NK) >> 56], 1u);
       p.sp_cols[1][pos] = k1;
       if (NK == 2) p.sp_cols[2][pos] = k2;
 #pragma unroll
@@ -462,9 +463,12 @@ __global__ __launch_bounds__(BD) void agg_kernel(AggArgs p) {
     lt.priv = (uint64_t *)(b + o_priv);
   }
   __shared__ uint32_t s_spill;
+  __shared__ uint32_t s_shist[256];
   lt.spill = &s_spill;
+  lt.shist = s_shist;
   if (p.sp_counts) {
     if (threadIdx.x == 0) s_spill = 0;
+    for (int i = threadIdx.x; i < 256; i += BD) s_shist[i] = 0;
     __syncthreads();
   }
   if (cap) {
@@ -529,6 +533,8 @@ __global__ __launch_bounds__(BD) void agg_kernel(AggArgs p) {
   if (p.sp_counts) {
     __syncthreads();
     if (threadIdx.x == 0) p.sp_counts[blockIdx.x] = s_spill;
+    for (int i = threadIdx.x; i < 256; i += BD)
+      if (s_shist[i]) atomicAdd(&p.sp_hist[i], (unsigned long long)s_shist[i]);
   }
   if (!cap) return;
   __syncthreads();

@@ -50,11 +50,12 @@ struct AggArgs {
   const GTable *gt;               // device copy of the global table descriptor
   // Partitioned aggregation (gpart.hip), for more groups than the on-chip tables hold.
   // Spill mode (sp_counts != 0, lds_cap = 0): every row passing WHERE is appended to the
-  // staged arrays sp_cols = {hash, k1, k2, value arrays...} instead of the global table,
+  // staged arrays sp_cols = {-, k1, k2, value arrays...} instead of the global table,
   // block b at [b * sp_region, ...) (an LDS cursor; the count lands in sp_counts[b]);
   // aggregate a's value goes to array 3 + sp_map[a] (-1: not staged).
-  uint64_t *sp_cols[3 + NUT_MAX_VALS];
+  uint64_t *sp_cols[3 + NUT_MAX_VALS];  // [0] unused (the partition hash is recomputed)
   unsigned long long *sp_counts;
+  unsigned long long *sp_hist;   // [256] histogram of the key hash's top byte (level 0)
   uint64_t sp_region;
   int32_t sp_map[NUT_MAX_AGGS];
   // Segment mode (seg_off != 0): block b folds rows [seg_off[2b], seg_off[2b+1]) only.

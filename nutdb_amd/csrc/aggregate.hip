@@ -257,6 +257,7 @@ struct LaunchExtra {
   bool spill = false;                      // stage rows passing WHERE (no tables)
   uint64_t *sp_cols[3 + NUT_MAX_VALS] = {};
   unsigned long long *sp_counts = nullptr; // [blocks] rows staged per block
+  unsigned long long *sp_hist = nullptr;   // [256] level-0 histogram (zeroed)
   int32_t sp_map[NUT_MAX_AGGS] = {};
   uint64_t blocks = 0, region = 0;         // out (spill): grid and per-block staging region
   const uint64_t *seg_off = nullptr;       // one block per segment: [start, end) pairs, even starts
@@ -308,7 +309,7 @@ nut_status launch_agg(nut_groups *g, const nut_agg_spec *s, uint64_t group_hint,
 
   // on-chip table: 4x the expected groups (load <= 1/4: a key almost always sits in
   // its 4-slot home bucket) within the LDS budget
-  const size_t lds_max = 160 * 1024 - 64;  // the kernel also holds a few static LDS words
+  const size_t lds_max = 160 * 1024 - 2048;  // the kernel also holds static LDS (spill cursor, histogram)
   const int na = s->naggs;
   // (32 slots = 8 buckets x 32 B = one pass over the 64 LDS banks: for <= 8 groups two
   // home buckets never conflict — distinct buckets hit distinct banks, equal ones broadcast)
@@ -319,6 +320,7 @@ nut_status launch_agg(nut_groups *g, const nut_agg_spec *s, uint64_t group_hint,
   if (ex && ex->spill) {
     lcap = 0;
     a.sp_counts = ex->sp_counts;
+    a.sp_hist = ex->sp_hist;
     for (int i = 0; i < 3 + NUT_MAX_VALS; ++i) a.sp_cols[i] = ex->sp_cols[i];
     for (int i = 0; i < NUT_MAX_AGGS; ++i) a.sp_map[i] = ex->sp_map[i];
   }
@@ -470,31 +472,35 @@ uint32_t gp_tiles(std::vector<GpSeg> &segs, uint32_t tile, std::vector<uint32_t>
 }
 
 // one partition level: histogram + scatter of every segment; returns the 256 counts per
-// segment in `hist`
+// segment in `hist` (gather mode: one histogram for all segments; `have_hist`: the caller
+// already holds it — the spill pass counts level 0)
 // `parts` (if not null): the output is laid out as 256 partitions per input segment, each
 // starting at an even row (16-B aligned for the aggregation's vector loads); their
 // [start, end) pairs are appended to *parts
 nut_status gp_level(nut_ctx *c, GpMeta &mm, std::vector<GpSeg> &segs, int shift, const uint64_t *const *src,
-                    uint64_t *const *dst, int first, int narr, bool gather, std::vector<uint64_t> &hist,
+                    uint64_t *const *dst, int narr, bool gather, bool have_hist, std::vector<uint64_t> &hist,
                     std::vector<uint64_t> *parts = nullptr) {
   hipStream_t st = c->stream;
   std::vector<uint32_t> ts;
-  const uint32_t nht = gp_tiles(segs, GP_HTILE, ts);
-  const size_t nh = gather ? 1 : segs.size();  // gather: every segment into one compact range
-  const size_t hb = nh * GP_BINS * 8;
-  nut_status s = mm.begin(GpMeta::al(segs.size() * sizeof(GpSeg)) + GpMeta::al(ts.size() * 4 + 1) + GpMeta::al(hb));
-  if (s) return s;
+  nut_status s;
   GpSeg *dseg;
   uint32_t *dts;
-  if ((s = mm.up(segs, &dseg)) || (s = mm.up(ts, &dts))) return s;
-  unsigned long long *dh = (unsigned long long *)mm.alloc(hb);
-  NUT_HIP(hipMemsetAsync(dh, 0, hb, st));
-  if (nht) hipLaunchKernelGGL(gp_hist_kernel, dim3(nht), dim3(GP_HTHREADS), 0, st, src[0], (const GpSeg *)dseg,
-                              (const uint32_t *)dts, shift, gather ? 1 : 0, dh);
-  NUT_HIP(hipGetLastError());
-  hist.resize(nh * GP_BINS);
-  NUT_HIP(hipMemcpyAsync(hist.data(), dh, hb, hipMemcpyDeviceToHost, st));
-  NUT_HIP(hipStreamSynchronize(st));
+  const size_t nh = gather ? 1 : segs.size();  // gather: every segment into one compact range
+  if (!have_hist) {
+    const uint32_t nht = gp_tiles(segs, GP_HTILE, ts);
+    const size_t hb = nh * GP_BINS * 8;
+    s = mm.begin(GpMeta::al(segs.size() * sizeof(GpSeg)) + GpMeta::al(ts.size() * 4 + 1) + GpMeta::al(hb));
+    if (s) return s;
+    if ((s = mm.up(segs, &dseg)) || (s = mm.up(ts, &dts))) return s;
+    unsigned long long *dh = (unsigned long long *)mm.alloc(hb);
+    NUT_HIP(hipMemsetAsync(dh, 0, hb, st));
+    if (nht) hipLaunchKernelGGL(gp_hist_kernel, dim3(nht), dim3(GP_HTHREADS), 0, st, src[1], src[2],
+                                (const GpSeg *)dseg, (const uint32_t *)dts, shift, gather ? 1 : 0, dh);
+    NUT_HIP(hipGetLastError());
+    hist.resize(nh * GP_BINS);
+    NUT_HIP(hipMemcpyAsync(hist.data(), dh, hb, hipMemcpyDeviceToHost, st));
+    NUT_HIP(hipStreamSynchronize(st));
+  }
   std::vector<uint64_t> cur(hist.size());
   uint64_t arun = 0;  // aligned layout: one running offset over all (segment, digit)
   for (size_t i = 0; i < nh; ++i) {
@@ -525,7 +531,6 @@ nut_status gp_level(nut_ctx *c, GpMeta &mm, std::vector<GpSeg> &segs, int shift,
     ar.src[a] = src[a];
     ar.dst[a] = dst[a];
   }
-  ar.first = first;
   ar.narr = narr;
   if (nst) hipLaunchKernelGGL(gp_scatter_kernel, dim3(nst), dim3(GP_THREADS), 0, st, ar, (const GpSeg *)dseg,
                               (const uint32_t *)dts, shift, gather ? 1 : 0, (unsigned long long *)dcur);
@@ -553,32 +558,38 @@ nut_status groupby_partitioned(nut_groups *g, const nut_agg_spec *s, uint64_t gr
   }
   if (nv > NUT_MAX_VALS) return NUT_OK;
   *used = true;
-  const int narr = 3 + nv;  // hash, k1, k2 (unused for one key), values
+  const int narr = 3 + nv;  // -, k1, k2 (unused for one key), values
   const uint64_t n = s->n;
   // staging: every block's region (<= n + one region of slack per block) in A, the
   // compact partitioned records in B (and A again after a second level)
   const uint64_t maxblocks = (uint64_t)c->num_cus * 8;
   // (+ one alignment gap per final partition; a multiple of 32 keeps every array 256-B aligned)
   const uint64_t rows = (n + maxblocks * 2 * kBdShared + 2 * 65536 + 64 + 31) & ~31ull;
-  nut_status e = c->gp_data.reserve(2 * (size_t)narr * rows * 8 + 256);
+  const int nstore = narr - 1 - (nk == 1 ? 1 : 0);  // k1, [k2], values
+  nut_status e = c->gp_data.reserve(2 * (size_t)nstore * rows * 8 + 256);
   if (e) return e;
   uint64_t *A[GP_MAX_ARR] = {}, *B[GP_MAX_ARR] = {};
-  for (int i = 0; i < narr; ++i) {
-    A[i] = (uint64_t *)c->gp_data.ptr + (size_t)i * rows;
-    B[i] = (uint64_t *)c->gp_data.ptr + (size_t)(narr + i) * rows;
+  for (int i = 1, k = 0; i < narr; ++i) {
+    if (i == 2 && nk == 1) continue;
+    A[i] = (uint64_t *)c->gp_data.ptr + (size_t)k * rows;
+    B[i] = (uint64_t *)c->gp_data.ptr + (size_t)(nstore + k) * rows;
+    ++k;
   }
-  if (nk == 1) A[2] = B[2] = nullptr;
   GpMeta mm{c};
   // ---- 1. spill: WHERE + aggregate arguments evaluated, rows staged per block in A
-  e = mm.begin(GpMeta::al(maxblocks * 8));
+  e = mm.begin(GpMeta::al(maxblocks * 8) + GpMeta::al(GP_BINS * 8));
   if (e) return e;
   unsigned long long *dcnt = (unsigned long long *)mm.alloc(maxblocks * 8);
+  unsigned long long *dh0 = (unsigned long long *)mm.alloc(GP_BINS * 8);
+  NUT_HIP(hipMemsetAsync(dh0, 0, GP_BINS * 8, st));
   sp.sp_counts = dcnt;
-  for (int i = 0; i < narr; ++i) sp.sp_cols[i] = A[i];
+  sp.sp_hist = dh0;
+  for (int i = 1; i < narr; ++i) sp.sp_cols[i] = A[i];
   e = launch_agg(g, s, group_hint, g->kinds, &sp);
   if (e) return e;
-  std::vector<uint64_t> cnt(sp.blocks);
+  std::vector<uint64_t> cnt(sp.blocks), hist(GP_BINS);
   NUT_HIP(hipMemcpyAsync(cnt.data(), dcnt, sp.blocks * 8, hipMemcpyDeviceToHost, st));
+  NUT_HIP(hipMemcpyAsync(hist.data(), dh0, GP_BINS * 8, hipMemcpyDeviceToHost, st));
   uint32_t ctl[4];
   e = read_ctl(g, ctl);
   if (e) return e;
@@ -594,13 +605,13 @@ nut_status groupby_partitioned(nut_groups *g, const nut_agg_spec *s, uint64_t gr
   int levels = group_hint > 256ull * 1024 ? 2 : 1;
   levels = env_int("NUT_GP_LEVELS", levels) == 2 ? 2 : 1;
   c->timer.begin(st, NUT_KERNEL_AGGREGATE);
-  std::vector<uint64_t> hist, parts;  // parts: [start, end) pairs of the final partitions
+  std::vector<uint64_t> parts;  // [start, end) pairs of the final partitions
   uint64_t **fin = B;
   if (levels == 1) {
-    e = gp_level(c, mm, segs, 56, A, B, 1, narr, true, hist, &parts);  // last level: hash dropped
+    e = gp_level(c, mm, segs, 56, A, B, narr, true, true, hist, &parts);
     if (e) return e;
   } else {
-    e = gp_level(c, mm, segs, 56, A, B, 0, narr, true, hist);
+    e = gp_level(c, mm, segs, 56, A, B, narr, true, true, hist);
     if (e) return e;
     std::vector<GpSeg> s2;
     uint64_t run = 0;
@@ -609,7 +620,7 @@ nut_status groupby_partitioned(nut_groups *g, const nut_agg_spec *s, uint64_t gr
       run += hist[d];
     }
     std::vector<uint64_t> h2;
-    e = gp_level(c, mm, s2, 48, B, A, 1, narr, false, h2, &parts);
+    e = gp_level(c, mm, s2, 48, B, A, narr, false, false, h2, &parts);
     if (e) return e;
     fin = A;
   }

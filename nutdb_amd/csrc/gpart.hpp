@@ -3,7 +3,8 @@
 //
 // The streaming kernel (agg_kernel.hpp) first runs in SPILL mode: it evaluates WHERE and
 // the aggregate arguments as always, but appends every passing row to staged arrays
-// {hash, k1, [k2], value arrays} instead of hashing it into a table.  The kernels here then
+// {k1, [k2], value arrays} instead of hashing it into a table (and counts the first
+// partition level's histogram on the way).  The kernels here then
 // radix-partition those records by the key hash (one or two 8-bit levels -> 256 or 65536
 // partitions of a few hundred groups each), and the streaming kernel runs again in
 // SEGMENT mode, one workgroup per partition: every group of a partition lives in that
@@ -29,13 +30,19 @@ struct GpSeg {  // records [start, start + count) of the current buffer
 };
 
 struct GpArrays {
-  const uint64_t *src[GP_MAX_ARR];
+  const uint64_t *src[GP_MAX_ARR];  // [0] unused, [1] k1, [2] k2 (two keys), values
   uint64_t *dst[GP_MAX_ARR];
-  int first, narr;  // arrays [first, narr) move; src[0] (the hash) gives the digit
+  int narr;
 };
 
+// the partition digit: a byte of the key tuple's owner hash (recomputed, never stored)
+__device__ __forceinline__ uint32_t gp_digit(const uint64_t *k1, const uint64_t *k2, uint64_t i, int shift) {
+  return (uint32_t)(owner_hash(k1[i], k2 ? k2[i] : 0, k2 ? 2 : 1) >> shift) & 255u;
+}
+
 // 256-bin histogram of (hash >> shift) & 255 per segment (gather: one for all segments)
-__global__ __launch_bounds__(GP_HTHREADS) void gp_hist_kernel(const uint64_t *__restrict__ h,
+__global__ __launch_bounds__(GP_HTHREADS) void gp_hist_kernel(const uint64_t *__restrict__ k1,
+                                                              const uint64_t *__restrict__ k2,
                                                               const GpSeg *__restrict__ segs,
                                                               const uint32_t *__restrict__ tile_seg, int shift,
                                                               int gather, unsigned long long *__restrict__ hist) {
@@ -47,16 +54,16 @@ __global__ __launch_bounds__(GP_HTHREADS) void gp_hist_kernel(const uint64_t *__
   const GpSeg sg = segs[s];
   const uint64_t lo = sg.start + (uint64_t)(blockIdx.x - sg.tile0) * GP_HTILE;
   const uint32_t n = (uint32_t)min<uint64_t>(GP_HTILE, sg.start + sg.count - lo);
-  for (uint32_t i = tid; i < n; i += GP_HTHREADS * 8) {
-    uint64_t v[8];
+  for (uint32_t i = tid; i < n; i += GP_HTHREADS * 4) {
+    uint32_t d[4];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
+    for (int j = 0; j < 4; ++j) {
       const uint32_t k = i + j * GP_HTHREADS;
-      v[j] = k < n ? __builtin_nontemporal_load(h + lo + k) : 0;
+      d[j] = k < n ? gp_digit(k1, k2, lo + k, shift) : 0;
     }
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
-      if (i + j * GP_HTHREADS < n) atomicAdd(&cnt[(v[j] >> shift) & 255], 1u);
+    for (int j = 0; j < 4; ++j)
+      if (i + j * GP_HTHREADS < n) atomicAdd(&cnt[d[j]], 1u);
   }
   __syncthreads();
   if (cnt[tid]) atomicAdd(&hist[(gather ? 0 : (uint64_t)s) * GP_BINS + tid], (unsigned long long)cnt[tid]);
@@ -88,7 +95,7 @@ __global__ __launch_bounds__(GP_THREADS) void gp_scatter_kernel(GpArrays ar, con
 #pragma unroll
   for (int i = 0; i < GP_ITEMS; ++i) {
     const uint32_t idx = (uint32_t)i * GP_THREADS + tid;
-    d[i] = idx < n ? (uint32_t)(__builtin_nontemporal_load(ar.src[0] + lo + idx) >> shift) & 255u : 0u;
+    d[i] = idx < n ? gp_digit(ar.src[1], ar.src[2], lo + idx, shift) : 0u;
     slot[i] = idx < n ? atomicAdd(&s_cnt[d[i]], 1u) : 0u;
   }
   __syncthreads();
@@ -123,7 +130,7 @@ __global__ __launch_bounds__(GP_THREADS) void gp_scatter_kernel(GpArrays ar, con
       s_dig[slot[i]] = (uint8_t)d[i];
     }
   }
-  for (int a = ar.first; a < ar.narr; ++a) {
+  for (int a = 1; a < ar.narr; ++a) {
     if (!ar.src[a]) continue;  // k2 of one-key queries
     const uint64_t *src = ar.src[a] + lo;
     uint64_t *dst = ar.dst[a];
