@@ -76,7 +76,8 @@ nut_status nut_ctx_info(nut_ctx *ctx, int *num_cus, char *name, size_t name_len)
 typedef enum {
   NUT_KERNEL_FILTER = 0,     /* filter scan + compaction          */
   NUT_KERNEL_AGGREGATE = 1,  /* fused filter/group-by/aggregate   */
-  NUT_KERNEL_SORT = 2        /* all radix-sort passes of one sort */
+  NUT_KERNEL_SORT = 2,       /* all radix-sort passes of one sort */
+  NUT_KERNEL_JOIN = 3        /* hash join: build, count and write passes */
 } nut_kernel_kind;
 nut_status nut_ctx_enable_timing(nut_ctx *ctx, int enable);
 nut_status nut_ctx_kernel_time(nut_ctx *ctx, int kind, double *total_ms, uint64_t *launches);
@@ -289,6 +290,33 @@ nut_status nut_sort_i64_desc(nut_ctx *ctx, const int64_t *in, int64_t *out, uint
  * local nut_sort_i64. */
 nut_status nut_partition_i64(nut_ctx *ctx, const int64_t *in, uint64_t n, const int64_t *splitters_host,
                              int nsplit, int64_t *out, uint64_t *counts_host);
+
+/* ------------------------------------------------------------------------
+ * Hash join: equi-join on one int64 key, lowered from
+ * JoinClause{typ, source, condition: On(a = b)} (src/parser/ast/query.rs:55-66,
+ * 100-117).  `build` is the joined table (the JoinClause source), `probe` the
+ * FROM table.  The result is a join index: pairs (probe row, build row) ordered
+ * by probe row; the build rows of one probe row are in unspecified order.
+ *   NUT_JOIN_INNER  every matching pair
+ *   NUT_JOIN_LEFT   LEFT OUTER: as INNER, plus (p, -1) for probe rows without a match
+ *   NUT_JOIN_SEMI   LEFT SEMI: (p, -1) once per probe row with >= 1 match
+ *   NUT_JOIN_ANTI   LEFT ANTI: (p, -1) for probe rows without a match
+ * (RIGHT variants are the LEFT ones with the tables swapped.)  Keys are device
+ * pointers; the index arrays live in HBM, owned by the nut_join.
+ * ------------------------------------------------------------------------ */
+typedef enum { NUT_JOIN_INNER = 0, NUT_JOIN_LEFT = 1, NUT_JOIN_SEMI = 2, NUT_JOIN_ANTI = 3 } nut_join_type;
+typedef struct nut_join nut_join;
+/* builds the table and counts the pairs (the key arrays must stay valid until
+ * nut_join_write); *npairs receives the result length */
+nut_status nut_join_i64(nut_ctx *ctx, const int64_t *build, uint64_t nbuild, const int64_t *probe, uint64_t nprobe,
+                        int join_type, nut_join **out, uint64_t *npairs);
+/* writes the npairs pairs into caller-owned device arrays */
+nut_status nut_join_write(nut_join *j, int64_t *probe_idx, int64_t *build_idx);
+void nut_join_free(nut_join *j);
+/* out[i] = src[idx[i]] (8-byte words), or `null_bits` where idx[i] < 0: carries any
+ * int64 / f64 column through a join index */
+nut_status nut_gather_u64(nut_ctx *ctx, const uint64_t *src, const int64_t *idx, uint64_t n, uint64_t null_bits,
+                          uint64_t *out);
 
 /* ========================================================================
  * SQL front end (CPU) — restatement of the reference's only public API,

@@ -126,6 +126,10 @@ SIGNATURES = {
     "nut_ctx_enable_timing": (_I32, [_P, _I32]),
     "nut_ctx_kernel_time": (_I32, [_P, _I32, C.POINTER(C.c_double), C.POINTER(_U64)]),
     "nut_ctx_sort_stats": (_I32, [_P, C.POINTER(_U64), C.POINTER(C.c_uint32)]),
+    "nut_join_i64": (_I32, [_P, _P, _U64, _P, _U64, _I32, C.POINTER(_P), C.POINTER(_U64)]),
+    "nut_join_write": (_I32, [_P, _P, _P]),
+    "nut_join_free": (None, [_P]),
+    "nut_gather_u64": (_I32, [_P, _P, _P, _U64, _U64, _P]),
     "nut_gen_column": (_I32, [_P, _I32, _U64, _I64, _I64, C.c_double, _U64, _U64, _P]),
     "nut_filter_i64": (_I32, [_P, _P, _U64, _I32, _I64, _P, C.POINTER(_U64)]),
     "nut_filter_i64_async": (_I32, [_P, _P, _U64, _I32, _I64, _P, _P]),

@@ -398,6 +398,48 @@ class Executor:
                  C.c_void_p(out.data_ptr() if n else None), n), fn.__name__)
         return out
 
+    # ---------------------------------------------------------------- join
+    JOIN_TYPES = {"inner": 0, "left": 1, "semi": 2, "anti": 3}
+
+    def join_i64(self, build: torch.Tensor, probe: torch.Tensor, how: str = "inner"):
+        """Hash equi-join (nut_join_i64): (probe_idx, build_idx) int64 tensors, ordered by
+        probe row; build_idx = -1 for LEFT rows without a match and for SEMI / ANTI rows.
+        Lowered from JoinClause (src/parser/ast/query.rs:55-66, 100-117)."""
+        for t in (build, probe):
+            if t.dtype != torch.int64:
+                raise TypeError("join_i64 takes int64 key columns")
+        if how not in self.JOIN_TYPES:
+            raise ValueError(f"join type {how!r} (inner, left, semi, anti)")
+        self._bind_stream()
+        h = C.c_void_p()
+        n = C.c_uint64()
+        nb, np_ = build.numel(), probe.numel()
+        check(lib.nut_join_i64(self.ctx, C.c_void_p(_col(build, self.device) if nb else None), nb,
+                               C.c_void_p(_col(probe, self.device) if np_ else None), np_, self.JOIN_TYPES[how],
+                               C.byref(h), C.byref(n)), "nut_join_i64")
+        try:
+            pi = torch.empty(n.value, dtype=torch.int64, device=self.device)
+            bi = torch.empty(n.value, dtype=torch.int64, device=self.device)
+            check(lib.nut_join_write(h, C.c_void_p(pi.data_ptr() if n.value else None),
+                                     C.c_void_p(bi.data_ptr() if n.value else None)), "nut_join_write")
+            self.sync()
+        finally:
+            lib.nut_join_free(h)
+        return pi, bi
+
+    def gather(self, col: torch.Tensor, idx: torch.Tensor, null=0) -> torch.Tensor:
+        """col[idx] for an int64 / float64 column, `null` where idx < 0 (nut_gather_u64)."""
+        if col.element_size() != 8 or idx.dtype != torch.int64:
+            raise TypeError("gather takes an 8-byte column and an int64 index")
+        n = idx.numel()
+        out = torch.empty(n, dtype=col.dtype, device=self.device)
+        nb = torch.tensor([null], dtype=col.dtype).view(torch.int64).item() & 0xFFFFFFFFFFFFFFFF
+        self._bind_stream()
+        check(lib.nut_gather_u64(self.ctx, C.c_void_p(_col(col, self.device) if col.numel() else None),
+                                 C.c_void_p(idx.data_ptr() if n else None), n, nb,
+                                 C.c_void_p(out.data_ptr() if n else None)), "nut_gather_u64")
+        return out
+
     def partition_i64(self, col: torch.Tensor, splitters, out: torch.Tensor | None = None):
         """Stable partition by bucket(k) = #{splitters <= k} (nut_partition_i64).  Returns
         (partitioned tensor, per-bucket counts)."""

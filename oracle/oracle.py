@@ -166,3 +166,26 @@ def multiset_hash(v: np.ndarray) -> int:
 
 def max_threads() -> int:
     return int(lib().orc_max_threads())
+
+
+def join_i64(build: np.ndarray, probe: np.ndarray, how: str = "inner"):
+    """Hash-join oracle (numpy, test-only): (probe_idx, build_idx) ordered by probe row,
+    build rows ascending within a probe row; -1 where the join type has no build row.
+    Semantics of include/nutexec.h nut_join_i64 (LEFT / SEMI / ANTI are left joins)."""
+    build = np.asarray(build, dtype=np.int64)
+    probe = np.asarray(probe, dtype=np.int64)
+    order = np.argsort(build, kind="stable")
+    sb = build[order]
+    lo = np.searchsorted(sb, probe, side="left")
+    hi = np.searchsorted(sb, probe, side="right")
+    m = hi - lo
+    rows = np.arange(len(probe), dtype=np.int64)
+    if how in ("semi", "anti"):
+        keep = m > 0 if how == "semi" else m == 0
+        return rows[keep], np.full(int(keep.sum()), -1, dtype=np.int64)
+    cnt = m if how == "inner" else np.maximum(m, 1)
+    pi = np.repeat(rows, cnt)
+    starts = np.repeat(lo, cnt)
+    within = np.arange(len(pi), dtype=np.int64) - np.repeat(np.cumsum(cnt) - cnt, cnt)
+    bi = np.where(np.repeat(m, cnt) > 0, order[np.minimum(starts + within, len(order) - 1)] if len(order) else -1, -1)
+    return pi, bi.astype(np.int64)

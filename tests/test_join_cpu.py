@@ -1,0 +1,45 @@
+"""CPU: the hash-join oracle (oracle/oracle.py join_i64) against a brute-force nested
+loop on small inputs, and the known answers of the join types (include/nutexec.h)."""
+import numpy as np
+import pytest
+
+from oracle.oracle import join_i64
+
+
+def brute(build, probe, how):
+    pi, bi = [], []
+    for r, k in enumerate(probe):
+        hits = [j for j, b in enumerate(build) if b == k]
+        if how == "inner":
+            pi += [r] * len(hits)
+            bi += hits
+        elif how == "left":
+            pi += [r] * max(len(hits), 1)
+            bi += hits if hits else [-1]
+        elif how == "semi" and hits:
+            pi.append(r)
+            bi.append(-1)
+        elif how == "anti" and not hits:
+            pi.append(r)
+            bi.append(-1)
+    return np.array(pi, dtype=np.int64), np.array(bi, dtype=np.int64)
+
+
+def test_join_known_answers():
+    b = np.array([5, 3, 5, 7])
+    p = np.array([5, 1, 7, 3, 5])
+    assert [x.tolist() for x in join_i64(b, p, "inner")] == [[0, 0, 2, 3, 4, 4], [0, 2, 3, 1, 0, 2]]
+    assert [x.tolist() for x in join_i64(b, p, "left")] == [[0, 0, 1, 2, 3, 4, 4], [0, 2, -1, 3, 1, 0, 2]]
+    assert join_i64(b, p, "semi")[0].tolist() == [0, 2, 3, 4]
+    assert join_i64(b, p, "anti")[0].tolist() == [1]
+
+
+@pytest.mark.parametrize("how", ["inner", "left", "semi", "anti"])
+@pytest.mark.parametrize("seed", range(6))
+def test_join_oracle_vs_nested_loop(how, seed):
+    rng = np.random.default_rng(seed)
+    nb, npr = [(0, 5), (5, 0), (30, 40), (64, 200), (200, 64), (1, 1)][seed]
+    b = rng.integers(-8, 8, nb).astype(np.int64)
+    p = rng.integers(-10, 10, npr).astype(np.int64)
+    got, want = join_i64(b, p, how), brute(b.tolist(), p.tolist(), how)
+    assert np.array_equal(got[0], want[0]) and np.array_equal(got[1], want[1])
