@@ -397,6 +397,17 @@ nut_status nut_plan_prepare(const nut_plan *plan, const nut_column *cols, int nc
  * bound).  group_hint as for nut_groupby.  Synchronous. */
 nut_status nut_plan_execute(nut_ctx *ctx, const nut_plan *plan, const nut_column *cols, int ncols,
                             uint64_t nrows, uint64_t group_hint, nut_result **out);
+/* A plan with a JOIN: `left` = the FROM table (lrows rows), `right` = the JOIN source.
+ * Every plan column is bound in exactly one of them (names unique across the two).
+ * The ON columns (int64) drive nut_join_i64 — INNER builds the smaller table; LEFT /
+ * RIGHT OUTER, SEMI and ANTI preserve their side — and the columns the plan names are
+ * gathered through the join index; the rest of the plan runs on the joined rows.  Outer
+ * joins: NULL-extended rows add nothing to an aggregate whose argument reads the other
+ * table (its aggregate mask), and the other table's columns may not appear in WHERE,
+ * GROUP BY or a scan; SEMI / ANTI expose only the preserved table. */
+nut_status nut_plan_execute2(nut_ctx *ctx, const nut_plan *plan, const nut_column *left, int nleft, uint64_t lrows,
+                             const nut_column *right, int nright, uint64_t rrows, uint64_t group_hint,
+                             nut_result **out);
 /* Result = ncols output columns (the SELECT list, in order) x nrows rows. */
 nut_status nut_result_shape(const nut_result *res, uint64_t *nrows, int *ncols);
 /* type: nut_type of output column j; name: alias or expression text (owned by res) */

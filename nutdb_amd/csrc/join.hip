@@ -206,6 +206,20 @@ __global__ __launch_bounds__(HJ_THREADS) void hj_probe_write_kernel(HjTable t, c
   }
 }
 
+__global__ void matched_kernel(const int64_t *__restrict__ bi, uint64_t n, int64_t *__restrict__ out) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    out[i] = bi[i] >= 0 ? 1 : 0;
+}
+
+// 1 where a join pair has a build row, 0 for NULL-extended rows (outer joins; sql_plan.cpp)
+nut_status join_matched(nut_ctx *c, const int64_t *bi, uint64_t n, int64_t *out) {
+  if (!n) return NUT_OK;
+  const unsigned g = (unsigned)std::min<uint64_t>((n + 255) / 256, c->num_cus * 16ull);
+  hipLaunchKernelGGL(matched_kernel, dim3(g), dim3(256), 0, c->stream, bi, n, out);
+  NUT_HIP(hipGetLastError());
+  return NUT_OK;
+}
+
 __global__ void gather_u64_kernel(const uint64_t *__restrict__ src, const int64_t *__restrict__ idx, uint64_t n,
                                   uint64_t null_bits, uint64_t *__restrict__ out) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {

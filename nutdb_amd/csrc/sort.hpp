@@ -1,4 +1,5 @@
-// sort.hpp — the two sort implementations behind nut_sort_i64 / nut_sort_i64_desc.
+// sort.hpp — internal entry points shared between translation units: the two sort
+// implementations behind nut_sort_i64 / nut_sort_i64_desc, and join helpers.
 // Both take validated arguments (n > 0, in != out, device set) and `flip`, the XOR that maps
 // int64 order to unsigned order (ascending) or to its reverse (descending).
 #pragma once
@@ -7,4 +8,5 @@
 namespace nut {
 nut_status lsd_sort_i64(nut_ctx *c, const int64_t *in, int64_t *out, uint64_t n, uint64_t flip);  // sort.hip
 nut_status msd_sort_i64(nut_ctx *c, const int64_t *in, int64_t *out, uint64_t n, uint64_t flip);  // msd_sort.hip
+nut_status join_matched(nut_ctx *c, const int64_t *bi, uint64_t n, int64_t *out);                   // join.hip
 }  // namespace nut

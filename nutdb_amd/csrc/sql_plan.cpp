@@ -27,6 +27,7 @@
 
 #include "common.hpp"
 #include "sql_ast.hpp"
+#include "sort.hpp"
 #include "sql_lexer.hpp"
 #include "table.hpp"
 
@@ -273,7 +274,8 @@ using PProg = std::vector<PNode>;
 struct PlanAgg {
   int op, expr;
   int arg[3];
-  PProg val, mask;  // compiled mode: argument program and row mask (empty = every row)
+  PProg val, mask;        // compiled mode: argument program and row mask (empty = every row)
+  std::vector<int> refs;  // compiled mode: columns the argument reads (COUNT(x) included)
 };
 enum OutKind { OUT_KEY, OUT_AGG, OUT_AVG };
 struct PlanOut {
@@ -314,6 +316,12 @@ struct nut_plan {
   HNode having;
   bool has_limit = false;
   uint64_t limit = 0, offset = 0;
+  // JOIN (one JoinClause with ON a = b), executed by nut_plan_execute2: a hash join
+  // (nut_join_i64) then gathers into the joined table the rest of the plan runs on
+  int join = -1;           // nut_join_type; -1: no JOIN
+  bool jright = false;     // RIGHT OUTER / SEMI / ANTI: the JOIN source is the preserved side
+  std::string jtable;
+  int jkey[2] = {-1, -1};  // plan columns of the ON equality
 };
 
 struct nut_result {
@@ -727,7 +735,8 @@ int add_agg(nut_plan &p, const PlanAgg &a) {
   for (size_t i = 0; i < p.aggs.size(); ++i) {
     const PlanAgg &b = p.aggs[i];
     if (p.compiled) {
-      if (b.op == a.op && same_prog(b.mask, a.mask) && (a.op == NUT_AGG_COUNT || same_prog(b.val, a.val)))
+      if (b.op == a.op && same_prog(b.mask, a.mask) && (a.op == NUT_AGG_COUNT || same_prog(b.val, a.val)) &&
+          b.refs == a.refs)  // count(x) and count(*) differ once outer joins mask x's table
         return (int)i;
       continue;
     }
@@ -823,6 +832,11 @@ bool lower_output(nut_plan &p, const Expr &e, PlanOut &o, Lowering &L) {
     bool nullable = false;
     const bool star = e.kids.empty() || (e.kids[0].k == EK::Identifier && e.kids[0].id.wildcard);
     if (!star && !lower_nullable(p, e.kids[0], a.val, a.mask, nullable, L)) return false;
+    for (const PProg *pp : {&a.val, &a.mask})
+      for (const PNode &nd : *pp)
+        if (nd.op == NUT_P_COL) a.refs.push_back(nd.col);
+    std::sort(a.refs.begin(), a.refs.end());
+    a.refs.erase(std::unique(a.refs.begin(), a.refs.end()), a.refs.end());
     if (op == NUT_AGG_COUNT) a.val.clear();  // count(x) counts the rows where x is not NULL
     a.op = op == 100 ? NUT_AGG_SUM : op;
     a.expr = NUT_EX_COL;
@@ -833,6 +847,7 @@ bool lower_output(nut_plan &p, const Expr &e, PlanOut &o, Lowering &L) {
       cnt.op = NUT_AGG_COUNT;
       cnt.expr = NUT_EX_COL;
       cnt.mask = a.mask;
+      cnt.refs = a.refs;
       o.b = add_agg(p, cnt);
     }
     return true;
@@ -952,7 +967,30 @@ bool lower_mode(const Statement &st, nut_plan &p, Lowering &L) {
   if (b.with) return L.fail("WITH is not executed");
   if (b.distinct) return L.fail("DISTINCT is not executed");
   if (!b.from || b.from->k != SourceKind::Table) return L.fail("FROM must name one table");
-  if (!b.joins.empty()) return L.fail("JOIN is not executed");
+  if (b.joins.size() > 1) return L.fail("one JOIN per plan");
+  if (!b.joins.empty()) {
+    const JoinClause &jc = b.joins[0];
+    if (jc.src.k != SourceKind::Table) return L.fail("JOIN source must be a table");
+    if (!jc.on) return L.fail("JOIN ... USING is not executed (ON a = b)");
+    const Expr &cnd = jc.cond;
+    sv ka, kb;
+    if (!(cnd.k == EK::BinaryOp && cnd.bop() == BinOp::Eq && column_ref(cnd.kids[0], ka) &&
+          column_ref(cnd.kids[1], kb)))
+      return L.fail("JOIN ON must be one equality of two columns");
+    switch (jc.t) {
+      case JoinType::Inner: p.join = NUT_JOIN_INNER; break;
+      case JoinType::LeftOuter: p.join = NUT_JOIN_LEFT; break;
+      case JoinType::RightOuter: p.join = NUT_JOIN_LEFT, p.jright = true; break;
+      case JoinType::LeftSemi: p.join = NUT_JOIN_SEMI; break;
+      case JoinType::RightSemi: p.join = NUT_JOIN_SEMI, p.jright = true; break;
+      case JoinType::LeftAnti: p.join = NUT_JOIN_ANTI; break;
+      case JoinType::RightAnti: p.join = NUT_JOIN_ANTI, p.jright = true; break;
+      default: return L.fail("FULL OUTER and ASOF JOIN are not executed");
+    }
+    p.jtable = std::string(jc.src.table);
+    p.jkey[0] = col_index(p, ka);
+    p.jkey[1] = col_index(p, kb);
+  }
   if (b.having && !b.group_by) return L.fail("HAVING needs GROUP BY");
   p.table = std::string(b.from->table);
   bool wb;
@@ -1018,6 +1056,8 @@ bool lower_mode(const Statement &st, nut_plan &p, Lowering &L) {
     }
     if (p.aggs.size() > NUT_MAX_AGGS) return L.fail("more than 8 aggregates (HAVING / ORDER BY included)");
     if (p.vals.size() > NUT_MAX_VALS) return L.fail("aggregates reference more than 4 value columns");
+    if (!p.compiled && p.join == NUT_JOIN_LEFT)  // NULL-extended rows need aggregate masks
+      return L.fail("outer-join aggregates lower to expression mode");
     return true;
   }
 
@@ -1204,6 +1244,19 @@ std::string describe(const nut_plan &p) {
   }
   o += "],\"limit\":";
   o += p.has_limit ? std::to_string(p.limit) : "null";
+  if (p.join >= 0) {
+    static const char *jn[] = {"inner", "left", "semi", "anti"};
+    o += ",\"join\":{\"type\":\"";
+    o += jn[p.join];
+    o += p.jright ? "\",\"right\":true" : "\",\"right\":false";
+    o += ",\"table\":";
+    json_str(o, p.jtable);
+    o += ",\"on\":[";
+    json_str(o, p.cols[p.jkey[0]]);
+    o += ',';
+    json_str(o, p.cols[p.jkey[1]]);
+    o += "]}";
+  }
   o += ",\"offset\":" + std::to_string(p.offset) + "}";
   return o;
 }
@@ -1726,6 +1779,124 @@ nut_status exec_groupby(nut_ctx *c, const nut_plan &p, const nut_column *const *
 }  // namespace
 
 // ====================================================================== C ABI
+namespace {
+
+// A plan with a JOIN (nut_plan_execute2): hash join on the ON columns, gathers of every
+// plan column through the join index, then the plan's scan / group-by on the joined rows.
+nut_status exec_join(nut_ctx *c, const nut_plan &p, const nut_column *lc, int nl, uint64_t lrows,
+                     const nut_column *rc, int nr, uint64_t rrows, uint64_t hint, nut_result *r) {
+  const size_t nc = p.cols.size();
+  std::vector<int> side(nc);
+  std::vector<const nut_column *> src(nc);
+  for (size_t i = 0; i < nc; ++i) {
+    const nut_column *a = bind(p, (int)i, lc, nl), *b = bind(p, (int)i, rc, nr);
+    if (a && b) return fail(NUT_ERR_INVALID_ARG, "nut_plan_execute2: column '" + p.cols[i] + "' is in both tables");
+    if (!a && !b) return fail(NUT_ERR_INVALID_ARG, "nut_plan_execute2: column '" + p.cols[i] + "' is not bound");
+    side[i] = a ? 0 : 1;
+    src[i] = a ? a : b;
+    if (src[i]->type != NUT_T_I64 && src[i]->type != NUT_T_F64)
+      return fail(NUT_ERR_INVALID_ARG, "nut_plan_execute2: column '" + p.cols[i] + "' has an unknown type");
+    if ((a ? lrows : rrows) && !src[i]->data)
+      return fail(NUT_ERR_INVALID_ARG, "nut_plan_execute2: column '" + p.cols[i] + "' is NULL");
+  }
+  const int k0 = p.jkey[0], k1 = p.jkey[1];
+  if (side[k0] == side[k1]) return fail(NUT_ERR_PLAN, "JOIN ON must compare a column of each table");
+  const nut_column *lkey = side[k0] == 0 ? src[k0] : src[k1], *rkey = side[k0] == 0 ? src[k1] : src[k0];
+  if (lkey->type != NUT_T_I64 || rkey->type != NUT_T_I64) return fail(NUT_ERR_PLAN, "JOIN keys must be int64 columns");
+  // INNER builds the smaller table; the outer / semi / anti joins preserve their side
+  const int ps = p.join == NUT_JOIN_INNER ? (lrows >= rrows ? 0 : 1) : (p.jright ? 1 : 0);
+  const nut_column *pk = ps == 0 ? lkey : rkey, *bk = ps == 0 ? rkey : lkey;
+  const uint64_t np = ps == 0 ? lrows : rrows, nb = ps == 0 ? rrows : lrows;
+  const bool outer = p.join == NUT_JOIN_LEFT;
+  // what the other (build) table may feed
+  const int bkey = side[k0] == ps ? k1 : k0, pkey = side[k0] == ps ? k0 : k1;
+  auto in_prog = [](const PProg &pp, int i) {
+    for (const PNode &nd : pp)
+      if (nd.op == NUT_P_COL && nd.col == i) return true;
+    return false;
+  };
+  for (size_t i = 0; i < nc; ++i) {
+    if (side[i] == ps) continue;
+    const int ci = (int)i;
+    bool row = ci == p.proj || in_prog(p.where, ci);  // decides or projects rows
+    for (int k : p.keys) row = row || k == ci;
+    for (const PlanPred &pr : p.preds) row = row || pr.col == ci;
+    bool agg = false;
+    for (int v : p.vals) agg = agg || v == ci;
+    for (const PlanAgg &a : p.aggs) {
+      for (int ref : a.refs) agg = agg || ref == ci;
+      agg = agg || in_prog(a.val, ci) || in_prog(a.mask, ci);
+    }
+    if (p.join == NUT_JOIN_SEMI || p.join == NUT_JOIN_ANTI) {
+      // SEMI: the other table's ON column equals the preserved one; nothing else exists
+      if ((row || agg) && !(p.join == NUT_JOIN_SEMI && ci == bkey))
+        return fail(NUT_ERR_PLAN, "SEMI / ANTI JOIN output only the preserved table's columns ('" + p.cols[i] + "')");
+    } else if (outer && row) {
+      return fail(NUT_ERR_PLAN, "outer JOIN: the NULL-extended table's column '" + p.cols[i] +
+                                    "' may only appear inside aggregates");
+    }
+  }
+  nut_join *j = nullptr;
+  uint64_t npairs = 0;
+  nut_status st = nut_join_i64(c, (const int64_t *)bk->data, nb, (const int64_t *)pk->data, np, p.join, &j, &npairs);
+  if (st) return st;
+  DevBuf idx;
+  hipError_t he = hipMalloc(&idx.p, std::max<uint64_t>(npairs, 1) * 16);
+  if (he != hipSuccess) {
+    nut_join_free(j);
+    return hip_fail(he, "hipMalloc (join index)");
+  }
+  int64_t *pi = (int64_t *)idx.p, *bi = pi + std::max<uint64_t>(npairs, 1);
+  st = nut_join_write(j, pi, bi);
+  nut_join_free(j);
+  if (st) return st;
+  // the joined table: every plan column gathered through its side's index
+  nut_plan p2 = p;
+  const bool mask_col = outer && p.kind == NUT_PLAN_GROUPBY;
+  std::vector<DevBuf> bufs(nc + 1);
+  std::vector<nut_column> jc(nc + 1);
+  for (size_t i = 0; i < nc; ++i) {
+    NUT_HIP(hipMalloc(&bufs[i].p, std::max<uint64_t>(npairs, 1) * 8));
+    // SEMI / ANTI pairs carry no build row: the other ON column reads the preserved one
+    // (outer joins: equal on matched rows; aggregates mask the NULL-extended ones)
+    const bool via_probe = side[i] == ps || (p.join != NUT_JOIN_INNER && (int)i == bkey);
+    st = nut_gather_u64(c, (const uint64_t *)src[via_probe && (int)i == bkey ? pkey : i]->data, via_probe ? pi : bi,
+                        npairs, 0, (uint64_t *)bufs[i].p);
+    if (st) return st;
+    jc[i] = nut_column{p.cols[i].c_str(), bufs[i].p, src[i]->type};
+  }
+  if (mask_col) {  // aggregates over the other table skip the NULL-extended rows
+    NUT_HIP(hipMalloc(&bufs[nc].p, std::max<uint64_t>(npairs, 1) * 8));
+    st = join_matched(c, bi, npairs, (int64_t *)bufs[nc].p);
+    if (st) return st;
+    p2.cols.push_back("__matched");
+    jc[nc] = nut_column{p2.cols[nc].c_str(), bufs[nc].p, NUT_T_I64};
+    const int m = (int)nc;
+    for (PlanAgg &a : p2.aggs) {
+      bool other = false;
+      for (int ref : a.refs) other = other || side[ref] != ps;
+      if (!other) continue;
+      const bool had = !a.mask.empty();
+      PNode col;
+      col.op = NUT_P_COL;
+      col.col = m;
+      a.mask.push_back(col);  // (__matched != 0) [AND the argument's own mask]
+      emit_int(a.mask, 0);
+      emit(a.mask, NUT_P_NE);
+      if (had) emit(a.mask, NUT_P_AND);
+    }
+  }
+  std::vector<const nut_column *> bound(p2.cols.size());
+  for (size_t i = 0; i < p2.cols.size(); ++i) bound[i] = &jc[i];
+  const std::vector<const Dict *> nodict(p2.cols.size(), nullptr);
+  st = p2.kind == NUT_PLAN_GROUPBY ? exec_groupby(c, p2, bound.data(), nodict.data(), npairs, hint, r)
+                                   : exec_scan(c, p2, bound.data(), nodict.data(), npairs, r);
+  NUT_HIP(hipStreamSynchronize(c->stream));  // the gathered columns are freed on return
+  return st;
+}
+
+}  // namespace
+
 extern "C" {
 
 nut_status nut_sql_parse(const char *sql, size_t len, nut_stmt **out) {
@@ -1824,6 +1995,7 @@ nut_status nut_plan_execute(nut_ctx *c, const nut_plan *p, const nut_column *col
                             uint64_t group_hint, nut_result **out) {
   if (!c || !p || !out || (ncols && !cols) || ncols < 0) return fail(NUT_ERR_INVALID_ARG, "nut_plan_execute: NULL argument");
   *out = nullptr;
+  if (p->join >= 0) return fail(NUT_ERR_INVALID_ARG, "nut_plan_execute: the plan has a JOIN (nut_plan_execute2)");
   std::vector<const nut_column *> bound(p->cols.size());
   for (size_t i = 0; i < p->cols.size(); ++i) {
     bound[i] = bind(*p, (int)i, cols, ncols);
@@ -1840,6 +2012,27 @@ nut_status nut_plan_execute(nut_ctx *c, const nut_plan *p, const nut_column *col
   const std::vector<const Dict *> nodict(p->cols.size(), nullptr);  // raw columns carry no strings
   nut_status st = p->kind == NUT_PLAN_GROUPBY ? exec_groupby(c, *p, bound.data(), nodict.data(), nrows, group_hint, r)
                                               : exec_scan(c, *p, bound.data(), nodict.data(), nrows, r);
+  if (st) {
+    nut_result_free(r);
+    return st;
+  }
+  *out = r;
+  return NUT_OK;
+}
+
+nut_status nut_plan_execute2(nut_ctx *c, const nut_plan *p, const nut_column *left, int nleft, uint64_t lrows,
+                             const nut_column *right, int nright, uint64_t rrows, uint64_t group_hint,
+                             nut_result **out) {
+  if (!c || !p || !out || (nleft && !left) || (nright && !right) || nleft < 0 || nright < 0)
+    return fail(NUT_ERR_INVALID_ARG, "nut_plan_execute2: NULL argument");
+  if (p->join < 0) return nut_plan_execute(c, p, left, nleft, lrows, group_hint, out);
+  *out = nullptr;
+  nut_result *r = new (std::nothrow) nut_result;
+  if (!r) return fail(NUT_ERR_OOM, "nut_plan_execute2: out of host memory");
+  r->kind = p->kind;
+  r->device = c->device;
+  DeviceGuard g(c->device);
+  nut_status st = exec_join(c, *p, left, nleft, lrows, right, nright, rrows, group_hint, r);
   if (st) {
     nut_result_free(r);
     return st;

@@ -12,7 +12,7 @@ from __future__ import annotations
 
 import ctypes as C
 from dataclasses import dataclass, field
-from typing import Sequence
+from typing import Optional, Sequence
 
 import numpy as np
 import torch
@@ -457,8 +457,12 @@ class Executor:
         return out[:n], [int(c) for c in counts]
 
     # ---------------------------------------------------------------- SQL
-    def sql(self, query: str, columns: dict, group_hint: int = 0) -> dict:
+    def sql(self, query: str, columns: dict, group_hint: int = 0, right: Optional[dict] = None) -> dict:
         """Parse + lower `query` (nut_sql_plan) and run it on `columns` = {name: CUDA
-        tensor}.  Returns {output name: numpy array} in SELECT-list order."""
+        tensor}.  Returns {output name: numpy array} in SELECT-list order.  A query with
+        a JOIN takes the JOIN source's columns as `right` (`columns` = the FROM table)."""
         from .sql import Plan
-        return Plan(query).execute(self, columns, group_hint=group_hint)
+        p = Plan(query)
+        if right is not None or "join" in p.describe():
+            return p.execute_join(self, columns, right or {}, group_hint=group_hint)
+        return p.execute(self, columns, group_hint=group_hint)

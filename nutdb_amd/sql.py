@@ -192,6 +192,28 @@ class Plan:
                 group_hint: int = 0) -> Dict[str, np.ndarray]:
         """Run on the GPU of executor `ex` with `columns` = {name: 1-D int64/float64 CUDA
         tensor}.  Returns {output name: numpy array} in SELECT-list order."""
+        arr, keep, n = self._bind(columns)
+        rows = nrows if nrows is not None else (n or 0)
+        res = C.c_void_p()
+        ex._bind_stream()
+        check(lib.nut_plan_execute(ex.ctx, self._h, arr, len(columns), rows, group_hint, C.byref(res)),
+              "nut_plan_execute")
+        return read_result(res)
+
+    def execute_join(self, ex, left: Dict[str, "object"], right: Dict[str, "object"],
+                     group_hint: int = 0) -> Dict[str, np.ndarray]:
+        """Run a plan with a JOIN (nut_plan_execute2): `left` = the FROM table's columns,
+        `right` = the JOIN source's (names unique across both).  The ON columns are
+        int64; the hash join runs on the GPU and the rest of the plan on the joined rows."""
+        la, lk, ln = self._bind(left)
+        ra, rk, rn = self._bind(right)
+        res = C.c_void_p()
+        ex._bind_stream()
+        check(lib.nut_plan_execute2(ex.ctx, self._h, la, len(left), ln or 0, ra, len(right), rn or 0,
+                                    group_hint, C.byref(res)), "nut_plan_execute2")
+        return read_result(res)
+
+    def _bind(self, columns):
         import torch
         names = self.columns
         arr = (NutColumn * max(len(columns), 1))()
@@ -213,12 +235,7 @@ class Plan:
                 n = t.numel() if n is None else n
                 if t.numel() != n:
                     raise ValueError("bound columns differ in length")
-        rows = nrows if nrows is not None else (n or 0)
-        res = C.c_void_p()
-        ex._bind_stream()
-        check(lib.nut_plan_execute(ex.ctx, self._h, arr, len(columns), rows, group_hint, C.byref(res)),
-              "nut_plan_execute")
-        return read_result(res)
+        return arr, keep, n
 
     def _handle(self):
         return self._h

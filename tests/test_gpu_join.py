@@ -77,3 +77,150 @@ def test_gather_null_and_f64(ex):
     assert out.tolist() == [4.5, -0.25, 0.0, 13.5, -0.25]
     icol = torch.tensor([I64_MIN, 7, I64_MAX], dtype=torch.int64, device=ex.device)
     assert host(ex.gather(icol, torch.tensor([2, 0, -1], device=ex.device), null=-9)).tolist() == [I64_MAX, I64_MIN, -9]
+
+
+# ------------------------------------------------------------------ SQL: JOIN plans
+# (nut_plan_execute2: hash join on the ON columns, gathers, then the plan's group-by /
+# scan on the joined rows).  Expected values: the numpy join oracle + pandas group-by.
+# The reference parses JOINs but executes none: semantics are this build's (SQL's, with
+# ClickHouse-style non-Nullable aggregate results), parity pinned by the numpy oracle.
+import pandas as pd  # noqa: E402
+
+from nutdb_amd import NutError  # noqa: E402
+
+
+def tables(seed, norders, nlines, miss=0.2):
+    rng = np.random.default_rng(seed)
+    o_okey = rng.permutation(np.arange(norders, dtype=np.int64) * 3 + 11)
+    o_cust = rng.integers(0, 50, norders).astype(np.int64)
+    hit = o_okey[rng.integers(0, norders, nlines)] if norders else np.full(nlines, 5, dtype=np.int64)
+    l_okey = np.where(rng.random(nlines) < miss, rng.integers(0, 3 * max(norders, 1), nlines) * 3 + 12, hit).astype(np.int64)
+    l_qty = rng.integers(1, 60, nlines).astype(np.int64)
+    l_price = rng.integers(-4096, 4096, nlines).astype(np.float64) / 32.0  # dyadic: sums exact
+    return ({"o_okey": o_okey, "o_cust": o_cust}, {"l_okey": l_okey, "l_qty": l_qty, "l_price": l_price})
+
+
+def joined(orc, left, lkey, right, rkey, how):
+    """numpy join of left (preserved for outer / semi / anti) with right: a DataFrame with
+    every column of both, NaN-free; `matched` marks rows with a right row."""
+    pi, bi = orc.join_i64(right[rkey], left[lkey], how)
+    d = {k: v[pi] for k, v in left.items()}
+    if how in ("inner", "left"):
+        for k, v in right.items():
+            d[k] = np.where(bi >= 0, v[np.maximum(bi, 0)], 0).astype(v.dtype)
+    d["matched"] = bi >= 0
+    return pd.DataFrame(d)
+
+
+def on_dev(ex, t):
+    return {k: dev(v, ex) for k, v in t.items()}
+
+
+@pytest.mark.parametrize("sizes", [(20_000, 100_000), (200_000, 50_000), (0, 1000), (1000, 0)])
+def test_sql_inner_join_groupby(ex, orc, sizes):
+    orders, lines = tables(1, *sizes)
+    sql = """select o_cust, sum(l_qty) as q, count(*) as c, min(l_price) as mn, max(l_qty) as mx,
+               sum(l_price) as p
+             from lineitem join orders on l_okey = o_okey where l_qty > 3 group by o_cust order by o_cust"""
+    got = ex.sql(sql, on_dev(ex, lines), right=on_dev(ex, orders))
+    j = joined(orc, lines, "l_okey", orders, "o_okey", "inner")
+    g = j[j.l_qty > 3].groupby("o_cust").agg(q=("l_qty", "sum"), c=("l_qty", "size"), mn=("l_price", "min"),
+                                            mx=("l_qty", "max"), p=("l_price", "sum"))
+    assert got["o_cust"].tolist() == g.index.tolist()
+    for c in ("q", "c", "mn", "mx", "p"):
+        assert got[c].tolist() == g[c].tolist(), c
+
+
+@pytest.mark.parametrize("right", [False, True])
+def test_sql_left_outer_join_groupby(ex, orc, right):
+    orders, lines = tables(2, 30_000, 60_000, miss=0.3)
+    orders["o_cust"][:40] = 1000  # customer 1000: orders with no line (below)
+    lines["l_okey"][np.isin(lines["l_okey"], orders["o_okey"][:40])] = -5
+    body = ("from orders left join lineitem on o_okey = l_okey" if not right
+            else "from lineitem right outer join orders on l_okey = o_okey")
+    sql = f"""select o_cust, count(*) as c, count(l_qty) as cl, sum(l_qty) as s, sum(l_price) as p,
+                avg(l_qty) as a, max(case when l_qty > 50 then l_price end) as mx
+              {body} where o_cust >= 10 group by o_cust order by o_cust"""
+    got = ex.sql(sql, on_dev(ex, lines if right else orders), right=on_dev(ex, orders if right else lines))
+    j = joined(orc, orders, "o_okey", lines, "l_okey", "left")
+    j = j[j.o_cust >= 10]
+    m = j[j.matched]
+    g = j.groupby("o_cust").size()
+    assert got["o_cust"].tolist() == g.index.tolist()
+    assert got["c"].tolist() == g.tolist()
+    cl = m.groupby("o_cust").size().reindex(g.index, fill_value=0)
+    assert got["cl"].tolist() == cl.tolist()
+    assert got["s"].tolist() == m.groupby("o_cust").l_qty.sum().reindex(g.index, fill_value=0).tolist()
+    assert got["p"].tolist() == m.groupby("o_cust").l_price.sum().reindex(g.index, fill_value=0.0).tolist()
+    i1000 = g.index.tolist().index(1000)
+    assert got["cl"][i1000] == 0 and got["s"][i1000] == 0 and got["c"][i1000] == 40
+    a = (m.groupby("o_cust").l_qty.sum() / m.groupby("o_cust").size()).reindex(g.index)
+    keep = g.index != 1000
+    assert np.array_equal(got["a"][keep], a[keep].to_numpy())
+    big = m[m.l_qty > 50].groupby("o_cust").l_price.max()
+    for i, cst in enumerate(g.index):
+        if cst in big.index:
+            assert got["mx"][i] == big[cst]
+
+
+@pytest.mark.parametrize("how", ["semi", "anti"])
+def test_sql_semi_anti_join(ex, orc, how):
+    orders, lines = tables(3, 50_000, 80_000, miss=0.5)
+    sql = f"""select o_cust, count(*) as c, sum(o_okey) as s from orders left {how} join lineitem
+              on o_okey = l_okey group by o_cust order by o_cust"""
+    got = ex.sql(sql, on_dev(ex, orders), right=on_dev(ex, lines))
+    j = joined(orc, orders, "o_okey", lines, "l_okey", how)
+    g = j.groupby("o_cust").agg(c=("o_okey", "size"), s=("o_okey", "sum"))
+    assert got["o_cust"].tolist() == g.index.tolist()
+    assert got["c"].tolist() == g.c.tolist() and got["s"].tolist() == g.s.tolist()
+    # the RIGHT form preserves the JOIN source; SEMI may read the other ON column
+    sql = f"select l_okey from lineitem right {how} join orders on l_okey = o_okey"
+    if how == "semi":
+        got = ex.sql(sql, on_dev(ex, lines), right=on_dev(ex, orders))
+        assert got["l_okey"].tolist() == j.o_okey.tolist()
+    else:
+        with pytest.raises(NutError, match="preserved table"):
+            ex.sql(sql, on_dev(ex, lines), right=on_dev(ex, orders))
+
+
+def test_sql_join_scan_and_sort(ex, orc):
+    orders, lines = tables(4, 10_000, 40_000)
+    got = ex.sql("select l_qty from lineitem join orders on l_okey = o_okey where l_qty >= 30",
+                 on_dev(ex, lines), right=on_dev(ex, orders))
+    j = joined(orc, lines, "l_okey", orders, "o_okey", "inner")
+    assert got["l_qty"].tolist() == j.l_qty[j.l_qty >= 30].tolist()  # joined rows in probe-row order
+    got = ex.sql("select o_okey from orders join lineitem on o_okey = l_okey order by o_okey desc limit 100",
+                 on_dev(ex, orders), right=on_dev(ex, lines))
+    assert got["o_okey"].tolist() == sorted(j.o_okey.tolist(), reverse=True)[:100]
+
+
+def test_sql_join_errors(ex):
+    orders, lines = tables(5, 200, 200)  # equal lengths: the binding checks pass, the plan errors
+    o, l_ = on_dev(ex, orders), on_dev(ex, lines)
+    with pytest.raises(NutError, match="may only appear inside aggregates"):
+        ex.sql("select o_cust, count(*) from orders left join lineitem on o_okey = l_okey where l_qty > 3 "
+               "group by o_cust", o, right=l_)
+    with pytest.raises(NutError, match="may only appear inside aggregates"):
+        ex.sql("select l_qty, count(*) from orders left join lineitem on o_okey = l_okey group by l_qty", o, right=l_)
+    with pytest.raises(NutError, match="in both tables"):
+        ex.sql("select o_cust, count(*) from orders join lineitem on o_okey = l_okey group by o_cust",
+               o, right={**l_, "o_cust": o["o_cust"]})
+    with pytest.raises(NutError, match="must be int64"):
+        ex.sql("select count(*) from orders join lineitem on o_okey = l_price", o, right=l_)
+    with pytest.raises(NutError, match="a column of each table"):
+        ex.sql("select count(*) from orders join lineitem on o_okey = o_cust", o, right=l_)
+    from nutdb_amd.sql import Plan
+    with pytest.raises(NutError, match="nut_plan_execute2"):
+        Plan("select count(*) from orders join lineitem on o_okey = l_okey").execute(ex, {**o, **l_})
+
+
+def test_sql_inner_join_large(ex, orc):
+    """1e6 orders x 8e6 lines: the TPC-H-shaped join + group-by (Q3/Q10 style)."""
+    orders, lines = tables(6, 1_000_000, 8_000_000)
+    sql = """select o_cust, count(*) as c, sum(l_qty) as q from lineitem join orders on l_okey = o_okey
+             group by o_cust order by o_cust"""
+    got = ex.sql(sql, on_dev(ex, lines), right=on_dev(ex, orders))
+    j = joined(orc, lines, "l_okey", orders, "o_okey", "inner")
+    g = j.groupby("o_cust").agg(c=("l_qty", "size"), q=("l_qty", "sum"))
+    assert got["o_cust"].tolist() == g.index.tolist()
+    assert got["c"].tolist() == g.c.tolist() and got["q"].tolist() == g.q.tolist()

@@ -43,3 +43,49 @@ def test_join_oracle_vs_nested_loop(how, seed):
     p = rng.integers(-10, 10, npr).astype(np.int64)
     got, want = join_i64(b, p, how), brute(b.tolist(), p.tolist(), how)
     assert np.array_equal(got[0], want[0]) and np.array_equal(got[1], want[1])
+
+
+# ------------------------------------------------------------------ SQL JOIN lowering
+JQ = "select o_cust, count(*) as c, sum(l_qty) as s from orders {} lineitem on o_okey = l_okey group by o_cust"
+
+
+@pytest.mark.parametrize("kw,typ,right,mode", [
+    ("join", "inner", False, "fused"), ("inner join", "inner", False, "fused"),
+    ("left join", "left", False, "compiled"), ("left outer join", "left", False, "compiled"),
+    ("right join", "left", True, "compiled"), ("left semi join", "semi", False, "fused"),
+    ("right semi join", "semi", True, "fused"), ("left anti join", "anti", False, "fused"),
+    ("right anti join", "anti", True, "fused")])
+def test_sql_join_lowering(kw, typ, right, mode):
+    from nutdb_amd.sql import Plan
+    d = Plan(JQ.format(kw)).describe()
+    assert d["join"] == {"type": typ, "right": right, "table": "lineitem", "on": ["o_okey", "l_okey"]}
+    assert d["table"] == "orders" and d["mode"] == mode  # outer joins mask aggregates: expression mode
+    assert set(d["columns"]) == {"o_okey", "l_okey", "o_cust", "l_qty"}
+
+
+def test_sql_no_join_has_no_join_key():
+    from nutdb_amd.sql import Plan
+    assert "join" not in Plan("select k, count(*) from t group by k").describe()
+
+
+@pytest.mark.parametrize("sql,msg", [
+    ("select count(*) from a full join b on x = y", "FULL OUTER"),
+    ("select count(*) from a join b using (x)", "USING"),
+    ("select count(*) from a join b on x < y", "one equality"),
+    ("select count(*) from a join b on x = y and u = v", "one equality"),
+    ("select count(*) from a join b on x = y join c on y = z", "one JOIN"),
+    ("select count(*) from a join (select x from b) on x = y", "must be a table")])
+def test_sql_join_rejections(sql, msg):
+    from nutdb_amd import NutError
+    from nutdb_amd.sql import Plan
+    with pytest.raises(NutError, match=msg):
+        Plan(sql)
+
+
+def test_count_star_and_count_column_stay_apart():
+    """count(l_qty) and count(*) are one aggregate without a join, two under an outer join
+    (the NULL-extended rows count for * only)."""
+    from nutdb_amd.sql import Plan
+    d = Plan("select o_cust, count(*), count(l_qty) from orders left join lineitem on o_okey = l_okey "
+             "group by o_cust").describe()
+    assert len(d["aggs"]) == 2
