@@ -12,7 +12,8 @@ pre-aggregates locally, exchanges partial groups by key hash with one RCCL
 all-to-all and merges the groups it owns; rank 0 gathers the final result.
 
 A "step" = one complete query over the resident columns (kernels + exchange + result
-to host).  Other configs: --workload groupby (config 3), filter (config 2).
+to host).  Other configs: --workload groupby (config 3), filter (config 2), sort
+(config 5), q12expr (expression mode), join (SURVEY.md §8(f)4 hash join).
 
 Prints ONE JSON line on rank 0 (contract in the task statement), with
   roofline     — the dominant kernel's algorithmic bytes / its mean device time
@@ -45,7 +46,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--workload", default="q1", choices=["q1", "groupby", "filter", "sort", "q12expr", "parse"])
+    p.add_argument("--workload", default="q1", choices=["q1", "groupby", "filter", "sort", "q12expr", "join", "parse"])
     p.add_argument("--rows", type=float, default=None, help="rows per GPU (default: config size)")
     p.add_argument("--groups", type=int, default=1000, help="groupby: distinct keys")
     p.add_argument("--selectivity", type=float, default=0.5, help="filter: fraction selected")
@@ -207,6 +208,44 @@ class Q12Expr:
                 "kernel": "expression mode (hipRTC-compiled per query shape)"}
 
 
+class Join:
+    """INNER hash equi-join on int64 keys, TPC-H orders x lineitem shape —
+    `rows` probe keys (lineitem.l_orderkey) against rows/4 unique build keys
+    (orders.o_orderkey), 90 % of probe rows matching one build row.  One step = build
+    (bucket count, scan, fill) + probe count + probe write of (probe_idx, build_idx) pairs
+    in probe-row order (join.hip).  Algorithmic bytes: build keys read once (8 B) and the
+    CSR table written once (16 B) per build row; probe keys read once (8 B) per probe row;
+    16 B per output pair.  The table's random reads (bucket offsets, keys, rows) are not
+    algorithmic bytes: they show up in the PMC traffic."""
+    name = "join_i64_hash"
+    kernel_kind = 3
+
+    def __init__(self, ex, rows, row0):
+        self.ex = ex
+        self.rows = rows
+        self.nb = rows // 4
+        self.build = ex.gen_column(0, 0x71 + row0, self.nb)  # 62-bit: unique w.h.p.
+        sel = ex.gen_column(0, 0x72 + row0, rows)
+        self.probe = torch.where(sel % 10 == 0, sel | (1 << 62), self.build[sel % self.nb])
+        del sel
+        self.npairs = 0
+
+    @property
+    def cols_bytes(self):  # per probe row
+        return (24.0 * self.nb + 8.0 * self.rows + 16.0 * self.npairs) / self.rows
+
+    def run(self):
+        pi, bi = self.ex.join_i64(self.build, self.probe, "inner")
+        self.npairs = pi.numel()
+        del pi, bi
+
+    def config(self):
+        return {"workload": self.name, "query": "SELECT ... FROM lineitem JOIN orders ON l_orderkey = o_orderkey "
+                "(join index: probe_idx, build_idx)", "build_rows": self.nb, "probe_rows": self.rows,
+                "pairs": self.npairs, "match_rate": 0.9, "bytes_per_row": self.cols_bytes,
+                "unit_rows": "probe rows"}
+
+
 # ------------------------------------------------------------------ one step
 def groupby_step(w, rank, world, group):
     """Local scan -> (N>1) all-to-all of partial groups by owner -> owner merge ->
@@ -242,6 +281,13 @@ def cpu_baseline(args, workload: str, target_s: float):
         if workload == "sort":
             col = orc.gen(SORT_COL, n)
             return lambda: orc.sort_i64(col)
+        if workload == "join":
+            rng = np.random.default_rng(0x71)
+            nb = max(n // 4, 1)
+            b = rng.permutation(nb).astype(np.int64) * 7919 + 13
+            sel = rng.integers(0, nb, n)
+            p = np.where(rng.random(n) < 0.1, -1 - sel, b[sel])
+            return lambda: orc.join_i64_c(b, p, "inner")
         if workload == "q12expr":
             from nutdb_amd.workloads import Q12_AGGS, Q12_COLS, Q12_WHERE
             from oracle.expr import groupby_prog
@@ -257,7 +303,7 @@ def cpu_baseline(args, workload: str, target_s: float):
         return time.perf_counter() - t0
 
     full = int(args.rows) if args.rows else {"q1": 10**9, "groupby": 10**9, "filter": 10**8,
-                                             "sort": 1_250_000_000, "q12expr": 10**9}[workload]
+                                             "sort": 1_250_000_000, "q12expr": 10**9, "join": 10**9}[workload]
     probe = min(full, 4_000_000)
     per_row = timed(prepare(probe)) / probe
     sample = int(min(full, max(probe, target_s / max(per_row, 1e-12))))
@@ -266,12 +312,17 @@ def cpu_baseline(args, workload: str, target_s: float):
     while sum(times) < target_s and len(times) < 10:
         times.append(timed(fn))
     dt = min(times)
-    return {"value": sample / dt, "unit": "rows/s", "cores": threads, "kind": "port",
+    if workload == "join":
+        how, cores = (f"C hash join (oracle/oracle.c orc_join_i64: CSR bucket table + two-pass probe), OpenMP "
+                      f"over {threads} host threads; probe rows, build = probe/4"), threads
+    elif workload == "q12expr":
+        how, cores = (f"numpy expression oracle (oracle/expr.py, 1 thread) + C oracle group-by (oracle/oracle.c, "
+                      f"OpenMP over {threads} host threads)"), threads
+    else:
+        how, cores = f"C oracle (oracle/oracle.c), OpenMP over {threads} host threads", threads
+    return {"value": sample / dt, "unit": "rows/s", "cores": cores, "kind": "port",
             "sample": f"{sample:.3g} rows of the same synthetic workload ({sample / full:.2f} of one GPU's "
-                      f"rows), " + ("numpy expression oracle (oracle/expr.py, 1 thread) + " if workload == "q12expr"
-                                    else "") +
-                      f"C oracle (oracle/oracle.c), OpenMP over {threads} host threads, generation "
-                      f"excluded, best of {len(times)} timed scans = {dt:.3f} s"}
+                      f"rows), {how}, generation excluded, best of {len(times)} timed runs = {dt:.3f} s"}
 
 
 # ------------------------------------------------------------------ main
@@ -332,7 +383,8 @@ def main():
         group = dist.group.WORLD
     from nutdb_amd import Executor
     ex = Executor(local_rank)
-    default_rows = {"q1": 1e9, "groupby": 1e9, "filter": 1e8, "sort": 1.25e9, "q12expr": 1e9}[args.workload]
+    default_rows = {"q1": 1e9, "groupby": 1e9, "filter": 1e8, "sort": 1.25e9, "q12expr": 1e9,
+                    "join": 1e9}[args.workload]
     rows = int(args.rows or default_rows)
     row0 = rank * rows
     if args.workload == "q1":
@@ -346,12 +398,17 @@ def main():
             print("bench.py: q12expr is a single-GPU workload", file=sys.stderr)
             sys.exit(2)
         w = Q12Expr(ex, rows, row0)
+    elif args.workload == "join":
+        if world > 1:
+            print("bench.py: join is a single-GPU workload", file=sys.stderr)
+            sys.exit(2)
+        w = Join(ex, rows, row0)
     else:
         w = Filter(ex, rows, row0, args.selectivity)
     torch.cuda.synchronize()
 
     def step():
-        if args.workload in ("filter", "sort", "q12expr"):
+        if args.workload in ("filter", "sort", "q12expr", "join"):
             w.run()
         else:
             groupby_step(w, rank, world, group)

@@ -313,6 +313,13 @@ nut_status nut_join_i64(nut_ctx *ctx, const int64_t *build, uint64_t nbuild, con
 /* writes the npairs pairs into caller-owned device arrays */
 nut_status nut_join_write(nut_join *j, int64_t *probe_idx, int64_t *build_idx);
 void nut_join_free(nut_join *j);
+/* one-pass form: builds the table and writes the pairs straight into caller-owned device
+ * arrays of `cap` entries; *npairs = the result length.  NUT_ERR_CAPACITY when it exceeds
+ * cap (no pair is valid then: call again with cap >= *npairs).  cap = nprobe always
+ * suffices for LEFT SEMI / ANTI, and for INNER / LEFT when the build keys are unique. */
+nut_status nut_join_i64_into(nut_ctx *ctx, const int64_t *build, uint64_t nbuild, const int64_t *probe,
+                             uint64_t nprobe, int join_type, int64_t *probe_idx, int64_t *build_idx, uint64_t cap,
+                             uint64_t *npairs);
 /* out[i] = src[idx[i]] (8-byte words), or `null_bits` where idx[i] < 0: carries any
  * int64 / f64 column through a join index */
 nut_status nut_gather_u64(nut_ctx *ctx, const uint64_t *src, const int64_t *idx, uint64_t n, uint64_t null_bits,

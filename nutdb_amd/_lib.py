@@ -27,6 +27,7 @@ NUT_MAX_PROG_NODES = 256
 
 # nut_status
 NUT_OK = 0
+NUT_ERR_CAPACITY = 5
 STATUS_NAMES = {
     0: "NUT_OK", 1: "NUT_ERR_INVALID_ARG", 2: "NUT_ERR_HIP", 3: "NUT_ERR_OOM",
     4: "NUT_ERR_UNSUPPORTED", 5: "NUT_ERR_CAPACITY", 6: "NUT_ERR_PARSE", 7: "NUT_ERR_PLAN",
@@ -128,6 +129,7 @@ SIGNATURES = {
     "nut_ctx_sort_stats": (_I32, [_P, C.POINTER(_U64), C.POINTER(C.c_uint32)]),
     "nut_join_i64": (_I32, [_P, _P, _U64, _P, _U64, _I32, C.POINTER(_P), C.POINTER(_U64)]),
     "nut_join_write": (_I32, [_P, _P, _P]),
+    "nut_join_i64_into": (_I32, [_P, _P, _U64, _P, _U64, _I32, _P, _P, _U64, C.POINTER(_U64)]),
     "nut_join_free": (None, [_P]),
     "nut_gather_u64": (_I32, [_P, _P, _P, _U64, _U64, _P]),
     "nut_gen_column": (_I32, [_P, _I32, _U64, _I64, _I64, C.c_double, _U64, _U64, _P]),

@@ -18,6 +18,7 @@
 //     partial lines before write-back).
 // Algorithmic bytes: 8 B/row read + 8 B/selected row written.
 #include "common.hpp"
+#include "lookback.hpp"
 
 namespace nut {
 
@@ -26,11 +27,6 @@ constexpr int FT_WAVES = FT_THREADS / kWave;               // 8
 constexpr int FT_STRIPES = 16;                             // <= 16: selection bits fit a u32
 constexpr int FT_STRIPE_ROWS = FT_THREADS * 2;             // 1024
 constexpr int FT_TILE = FT_STRIPE_ROWS * FT_STRIPES;       // 16384 rows
-constexpr uint64_t FLAG_AGG = 1ull << 62;
-constexpr uint64_t FLAG_INC = 2ull << 62;
-constexpr uint64_t VAL_MASK = (1ull << 62) - 1;
-constexpr uint32_t SPIN_LIMIT = 1u << 24;
-
 template <bool FULL, bool ALIGNED>
 __device__ __forceinline__ void load_stripe(const int64_t *__restrict__ col, uint64_t idx, uint64_t n,
                                             int64_t &a, int64_t &b) {
@@ -42,41 +38,6 @@ __device__ __forceinline__ void load_stripe(const int64_t *__restrict__ col, uin
     a = (FULL || idx < n) ? col[idx] : 0;
     b = (FULL || idx + 1 < n) ? col[idx + 1] : 0;
   }
-}
-
-// Wave 0 of the block: publish this tile's aggregate and return its exclusive prefix.
-__device__ uint64_t lookback(uint64_t *__restrict__ status, uint32_t tile, uint64_t total,
-                             uint32_t *__restrict__ err, int lane) {
-  if (tile == 0) {
-    if (lane == 0) st_agent(&status[0], FLAG_INC | total);
-    return 0;
-  }
-  if (lane == 0) st_agent(&status[tile], FLAG_AGG | total);
-  uint64_t excl = 0;
-  int64_t pred = (int64_t)tile - 1;
-  uint32_t spins = 0;
-  for (;;) {
-    int64_t idx = pred - lane;
-    uint64_t s = idx >= 0 ? ld_agent(&status[idx]) : FLAG_INC;
-    while (__any((s >> 62) == 0)) {
-      __builtin_amdgcn_s_sleep(1);
-      if ((s >> 62) == 0) s = ld_agent(&status[idx]);
-      if (++spins > SPIN_LIMIT) {  // never expected: predecessors always run ahead
-        if (lane == 0) atomicOr(err, 1u);
-        s = FLAG_INC | (s & VAL_MASK);
-      }
-    }
-    uint64_t inc = __ballot((s >> 62) == 2);
-    if (inc) {
-      int first = __builtin_ctzll(inc);
-      excl += wave_sum_u64(lane <= first ? (s & VAL_MASK) : 0);
-      break;
-    }
-    excl += wave_sum_u64(s & VAL_MASK);
-    pred -= kWave;
-  }
-  if (lane == 0) st_agent(&status[tile], FLAG_INC | (excl + total));
-  return excl;
 }
 
 template <int OP>

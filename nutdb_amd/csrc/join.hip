@@ -1,208 +1,283 @@
 // join.hip — hash equi-join on one int64 key.
 //
-// Build: the build keys are bucketed by the top bits of mix64(key) into a CSR table
-// (bucket counts -> exclusive scan -> fill), keys stored in bucket order next to their row
-// ids, so a probe scans one short contiguous run (>= 2 buckets per build row: ~0.5 keys per
-// bucket).  Probe: a tile of 4096 probe rows counts its output pairs (one bucket scan per
-// row), the tile totals are scanned, then the tile re-probes and writes its pairs at its
-// offset — pairs come out in probe-row order with no per-row count array in HBM.
+// Build: an open-addressing table of 16-byte slots {key, row} (row = -1: empty), capacity
+// the power of two >= 2 x build rows (load <= 0.5), linear probing from the top bits of
+// mix64(key).  One agent-scope CAS on the row word claims a slot (memory-side atomic:
+// coherent across the XCDs' L2s); the key is stored after the claim and the probe kernel
+// runs after the build kernel, so no reader sees a claimed slot without its key.  A probe
+// reads one 16-B slot per step: the common case — a unique build key — costs one random
+// 128-B line (its run continues in the same line), where a CSR bucket table costs two
+// (bucket offsets, then the keys).
+//
+// The same claim makes duplicate keys separate slots of one run; a check pass (each build
+// row walks to its own slot, any equal key before it = duplicates) tells the probe whether
+// it may stop at the first match (unique build keys: the PK-FK case) or must walk the run
+// to its empty slot.  SEMI / ANTI always stop at the first match.
+//
+// Probe: ONE pass in probe-row order.  A 512-thread workgroup takes a tile of 4096 probe
+// rows by atomic ticket and loads its keys (striped, coalesced).  Runs are walked in
+// lock-step rounds: each round issues one slot load for every unfinished row of the lane
+// (8 random reads in flight per lane; finished rows issue nothing), then consumes them.
+// Each row's output pairs are counted, ranked inside the tile (wave scans + one scan of
+// the wave totals) and the tile's global offset comes from decoupled look-back
+// (lookback.hpp).  A row with at most one match writes its pair from registers; rows with
+// several walk their run again while writing.  Rows come out in probe order with no
+// per-row or per-tile count array in HBM.  NUT_HJ_CFG selects another tile shape (tuning).
+//   nut_join_i64 (+ nut_join_write): a count-only pass gives the pair count first, the
+//   write pass follows (two probe passes, caller-sized output);
+//   nut_join_i64_into: the write pass alone into caller arrays of a given capacity.
+//
+// Roofline: the probe is bound by random 128-B line fetches (one slot read per probe row
+// in the common case, ~1.2 lines with run continuations), not by its sequential bytes —
+// see DESIGN.md §4.4 for the measured line rate.
 #include <algorithm>
-#include <vector>
+#include <new>
 
 #include "common.hpp"
+#include "lookback.hpp"
 
 namespace nut {
 
-constexpr int HJ_THREADS = 256;
-constexpr int HJ_ITEMS = 16;
-constexpr uint32_t HJ_TILE = HJ_THREADS * HJ_ITEMS;  // probe rows per tile
-
-__device__ __forceinline__ uint64_t hj_bucket(int64_t k, int log2b) {
-  return log2b ? mix64((uint64_t)k ^ 0x3C6EF372FE94F82Aull) >> (64 - log2b) : 0;
-}
-
-__global__ void hj_count_kernel(const int64_t *__restrict__ keys, uint64_t n, int log2b, uint32_t *__restrict__ cnt) {
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
-    atomicAdd(&cnt[hj_bucket(keys[i], log2b)], 1u);
-}
-
-// exclusive scan of u32 counts into u64 offsets: per-block sums, one-block scan of the sums,
-// per-block add (generic helpers for the two scans the join needs)
-constexpr int SC_THREADS = 1024;
-constexpr int SC_ITEMS = 8;
-constexpr uint64_t SC_TILE = SC_THREADS * SC_ITEMS;
-
-template <class T>
-__device__ __forceinline__ uint64_t block_scan_excl(uint64_t x, uint64_t *ws, uint64_t *total) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  uint64_t incl = x;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const uint64_t y = __shfl_up(incl, off, 64);
-    if (lane >= off) incl += y;
-  }
-  if (lane == 63) ws[wave] = incl;
-  __syncthreads();
-  uint64_t add = 0, tot = 0;
-  for (int w = 0; w < (int)(blockDim.x / kWave); ++w) {
-    const uint64_t sw = ws[w];
-    add += (w < wave) ? sw : 0;
-    tot += sw;
-  }
-  *total = tot;
-  return incl - x + add;
-}
-
-template <class T>
-__global__ __launch_bounds__(SC_THREADS) void scan_reduce_kernel(const T *__restrict__ in, uint64_t n,
-                                                                 uint64_t *__restrict__ sums) {
-  __shared__ uint64_t ws[SC_THREADS / kWave];
-  const uint64_t base = (uint64_t)blockIdx.x * SC_TILE + (uint64_t)threadIdx.x * SC_ITEMS;
-  uint64_t x = 0;
-#pragma unroll
-  for (int i = 0; i < SC_ITEMS; ++i)
-    if (base + i < n) x += in[base + i];
-  uint64_t tot;
-  (void)block_scan_excl<T>(x, ws, &tot);
-  if (threadIdx.x == 0) sums[blockIdx.x] = tot;
-}
-
-// one block: exclusive scan of `n` sums in place; sums[n] = total
-__global__ __launch_bounds__(SC_THREADS) void scan_sums_kernel(uint64_t *__restrict__ sums, uint64_t n) {
-  __shared__ uint64_t ws[SC_THREADS / kWave];
-  __shared__ uint64_t carry;
-  if (threadIdx.x == 0) carry = 0;
-  __syncthreads();
-  for (uint64_t b = 0; b < n; b += SC_THREADS) {
-    const uint64_t i = b + threadIdx.x;
-    const uint64_t x = i < n ? sums[i] : 0;
-    uint64_t tot;
-    const uint64_t e = block_scan_excl<uint64_t>(x, ws, &tot);
-    const uint64_t c = carry;
-    if (i < n) sums[i] = c + e;
-    __syncthreads();
-    if (threadIdx.x == 0) carry = c + tot;
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) sums[n] = carry;
-}
-
-template <class T>
-__global__ __launch_bounds__(SC_THREADS) void scan_apply_kernel(const T *__restrict__ in, uint64_t n,
-                                                                const uint64_t *__restrict__ sums,
-                                                                uint64_t *__restrict__ out) {
-  __shared__ uint64_t ws[SC_THREADS / kWave];
-  const uint64_t base = (uint64_t)blockIdx.x * SC_TILE + (uint64_t)threadIdx.x * SC_ITEMS;
-  T v[SC_ITEMS];
-  uint64_t x = 0;
-#pragma unroll
-  for (int i = 0; i < SC_ITEMS; ++i) {
-    v[i] = base + i < n ? in[base + i] : 0;
-    x += v[i];
-  }
-  uint64_t tot;
-  uint64_t run = sums[blockIdx.x] + block_scan_excl<T>(x, ws, &tot);
-#pragma unroll
-  for (int i = 0; i < SC_ITEMS; ++i) {
-    if (base + i < n) out[base + i] = run;
-    run += v[i];
-  }
-  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) out[n] = sums[gridDim.x];
-}
-
-__global__ void hj_fill_kernel(const int64_t *__restrict__ keys, uint64_t n, int log2b,
-                               unsigned long long *__restrict__ cursor, int64_t *__restrict__ bkeys,
-                               int64_t *__restrict__ brow) {
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-    const int64_t k = keys[i];
-    const uint64_t pos = atomicAdd(&cursor[hj_bucket(k, log2b)], 1ull);
-    bkeys[pos] = k;
-    brow[pos] = (int64_t)i;
-  }
-}
-
-// output pairs of one probe row
-__device__ __forceinline__ uint32_t hj_out_count(uint32_t matches, int type) {
-  switch (type) {
-    case NUT_JOIN_INNER: return matches;
-    case NUT_JOIN_LEFT: return matches ? matches : 1u;
-    case NUT_JOIN_SEMI: return matches ? 1u : 0u;
-    default: return matches ? 0u : 1u;
-  }
-}
+constexpr uint64_t HJ_EMPTY = ~0ull;
 
 struct HjTable {
-  const uint64_t *off;  // [nbuckets + 1]
-  const int64_t *bkeys, *brow;
-  int log2b;
+  i64x2 *slot;  // .x key, .y build row (-1: empty)
+  uint64_t mask;
+  int shift;  // 64 - log2(capacity)
 };
 
-__device__ __forceinline__ uint32_t hj_matches(const HjTable &t, int64_t k, uint64_t &lo, uint64_t &hi) {
-  const uint64_t b = hj_bucket(k, t.log2b);
-  lo = t.off[b];
-  hi = t.off[b + 1];
-  uint32_t m = 0;
-  for (uint64_t j = lo; j < hi; ++j) m += t.bkeys[j] == k;
-  return m;
+__device__ __forceinline__ uint64_t hj_home(int64_t k, const HjTable &t) {
+  return mix64((uint64_t)k ^ 0x3C6EF372FE94F82Aull) >> t.shift;
 }
 
-// pass 1: output pairs per probe tile
-__global__ __launch_bounds__(HJ_THREADS) void hj_probe_count_kernel(HjTable t, const int64_t *__restrict__ probe,
-                                                                    uint64_t n, int type,
-                                                                    uint64_t *__restrict__ tile_cnt) {
-  __shared__ uint64_t ws[HJ_THREADS / kWave];
-  const uint64_t base = (uint64_t)blockIdx.x * HJ_TILE + threadIdx.x;
-  uint64_t c = 0;
-#pragma unroll 4
-  for (int i = 0; i < HJ_ITEMS; ++i) {
-    const uint64_t r = base + (uint64_t)i * HJ_THREADS;
-    if (r < n) {
-      uint64_t lo, hi;
-      c += hj_out_count(hj_matches(t, probe[r], lo, hi), type);
-    }
-  }
-  uint64_t tot;
-  (void)block_scan_excl<uint64_t>(c, ws, &tot);
-  if (threadIdx.x == 0) tile_cnt[blockIdx.x] = tot;
-}
+// Build and duplicate check: HJ_BITEMS rows per lane in flight (their slot atomics /
+// loads are issued together each round, like the probe's run walks).
+constexpr int HJ_BITEMS = 4;
 
-// pass 2: the tile re-probes and writes its pairs at tile_off[tile] + (rows before, in
-// row order: row r = base + i*THREADS is the i-th row of thread t, rows ordered by (i, t))
-__global__ __launch_bounds__(HJ_THREADS) void hj_probe_write_kernel(HjTable t, const int64_t *__restrict__ probe,
-                                                                    uint64_t n, int type,
-                                                                    const uint64_t *__restrict__ tile_off,
-                                                                    int64_t *__restrict__ out_p,
-                                                                    int64_t *__restrict__ out_b) {
-  __shared__ uint64_t ws[HJ_THREADS / kWave];
-  const uint64_t base = (uint64_t)blockIdx.x * HJ_TILE + threadIdx.x;
-  uint64_t run = tile_off[blockIdx.x];
-  for (int i = 0; i < HJ_ITEMS; ++i) {  // one row per thread per step, rows in order
-    const uint64_t r = base + (uint64_t)i * HJ_THREADS;
-    uint64_t lo = 0, hi = 0;
-    int64_t k = 0;
-    uint32_t m = 0, c = 0;
-    if (r < n) {
-      k = probe[r];
-      m = hj_matches(t, k, lo, hi);
-      c = hj_out_count(m, type);
+__global__ __launch_bounds__(256) void hj_build_kernel(const int64_t *__restrict__ keys, uint64_t n, HjTable t) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < n; i0 += stride * HJ_BITEMS) {
+    int64_t k[HJ_BITEMS];
+    uint64_t s[HJ_BITEMS];
+    uint32_t act = 0;
+#pragma unroll
+    for (int j = 0; j < HJ_BITEMS; ++j) {
+      const uint64_t i = i0 + j * stride;
+      k[j] = i < n ? __builtin_nontemporal_load(keys + i) : 0;
+      s[j] = hj_home(k[j], t);
+      act |= (i < n ? 1u : 0u) << j;
     }
-    uint64_t tot;
-    uint64_t pos = run + block_scan_excl<uint64_t>(c, ws, &tot);
-    run += tot;
-    if (c) {
-      if (type == NUT_JOIN_INNER || (type == NUT_JOIN_LEFT && m)) {
-        for (uint64_t j = lo; j < hi; ++j)
-          if (t.bkeys[j] == k) {
-            out_p[pos] = (int64_t)r;
-            out_b[pos] = t.brow[j];
-            ++pos;
-          }
-      } else {
-        out_p[pos] = (int64_t)r;
-        out_b[pos] = -1;
+    while (act) {  // capacity >= 2n: every row finds an empty slot
+      // a plain read of the row words first: occupied slots are skipped without an atomic
+      unsigned long long old[HJ_BITEMS];
+#pragma unroll
+      for (int j = 0; j < HJ_BITEMS; ++j) {
+        old[j] = 0;
+        if ((act >> j) & 1u) old[j] = reinterpret_cast<const unsigned long long *>(&t.slot[s[j]])[1];
+      }
+#pragma unroll
+      for (int j = 0; j < HJ_BITEMS; ++j)
+        if (((act >> j) & 1u) && old[j] == HJ_EMPTY)
+          old[j] = atomicCAS(reinterpret_cast<unsigned long long *>(&t.slot[s[j]]) + 1, HJ_EMPTY,
+                             (unsigned long long)(i0 + j * stride));
+#pragma unroll
+      for (int j = 0; j < HJ_BITEMS; ++j) {
+        if (!((act >> j) & 1u)) continue;
+        if (old[j] == HJ_EMPTY) {
+          reinterpret_cast<int64_t *>(&t.slot[s[j]])[0] = k[j];
+          act &= ~(1u << j);
+        } else {
+          s[j] = (s[j] + 1) & t.mask;
+        }
       }
     }
-    __syncthreads();  // ws is reused by the next row's scan
+  }
+}
+
+// Duplicate build keys? Each build row walks its run up to its own slot; a slot with the
+// same key before it means the key repeats (of two equal keys, the one placed later in the
+// run meets the other).  Unique build keys let the probe stop at its first match.
+__global__ __launch_bounds__(256) void hj_dupcheck_kernel(const int64_t *__restrict__ keys, uint64_t n, HjTable t,
+                                                          uint32_t *__restrict__ dup) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  bool found = false;
+  for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < n; i0 += stride * HJ_BITEMS) {
+    int64_t k[HJ_BITEMS];
+    uint64_t s[HJ_BITEMS];
+    uint32_t act = 0;
+#pragma unroll
+    for (int j = 0; j < HJ_BITEMS; ++j) {
+      const uint64_t i = i0 + j * stride;
+      k[j] = i < n ? __builtin_nontemporal_load(keys + i) : 0;
+      s[j] = hj_home(k[j], t);
+      act |= (i < n ? 1u : 0u) << j;
+    }
+    while (act) {
+      i64x2 v[HJ_BITEMS];
+#pragma unroll
+      for (int j = 0; j < HJ_BITEMS; ++j) {
+        v[j] = i64x2{0, -1};
+        if ((act >> j) & 1u) v[j] = t.slot[s[j]];
+      }
+#pragma unroll
+      for (int j = 0; j < HJ_BITEMS; ++j) {
+        if (!((act >> j) & 1u)) continue;
+        const bool mine = v[j].y == (int64_t)(i0 + j * stride);
+        found = found || (!mine && v[j].x == k[j]);
+        if (mine || v[j].x == k[j]) act &= ~(1u << j);
+        s[j] = (s[j] + 1) & t.mask;
+      }
+    }
+  }
+  if (__any(found) && (threadIdx.x & (kWave - 1)) == 0) atomicOr(dup, 1u);
+}
+
+// output pairs of one probe row with m matches
+__device__ __forceinline__ uint32_t hj_out_count(uint32_t m, int type) {
+  switch (type) {
+    case NUT_JOIN_INNER: return m;
+    case NUT_JOIN_LEFT: return m ? m : 1u;
+    case NUT_JOIN_SEMI: return m ? 1u : 0u;
+    default: return m ? 0u : 1u;
+  }
+}
+
+// WRITE = false: count pass (tile = blockIdx.x, tile totals added to *total).
+// WRITE = true: ticket-ordered tiles, look-back offsets, pairs written below `cap`; the
+// last tile stores the grand total in *total.
+template <bool WRITE, int HJ_THREADS, int HJ_ITEMS>
+__global__ __launch_bounds__(HJ_THREADS) void hj_probe_kernel(HjTable t, const int64_t *__restrict__ probe,
+                                                              uint64_t n, int type, uint32_t *__restrict__ ticket,
+                                                              uint64_t *__restrict__ status, uint32_t ntiles,
+                                                              unsigned long long *__restrict__ total,
+                                                              int64_t *__restrict__ out_p,
+                                                              int64_t *__restrict__ out_b, uint64_t cap,
+                                                              uint32_t *__restrict__ err,
+                                                              const uint32_t *__restrict__ dup) {
+  constexpr int HJ_WAVES = HJ_THREADS / kWave;
+  constexpr uint32_t HJ_TILE = HJ_THREADS * HJ_ITEMS;
+  __shared__ uint64_t s_pre[HJ_ITEMS][HJ_WAVES];
+  __shared__ uint64_t s_excl;
+  __shared__ uint32_t s_tile;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  uint32_t tile = blockIdx.x;
+  if (WRITE) {
+    if (tid == 0) s_tile = atomicAdd(ticket, 1u);
+    __syncthreads();
+    tile = s_tile;
+  }
+  const uint64_t base = (uint64_t)tile * HJ_TILE + tid;
+  int64_t key[HJ_ITEMS];
+  uint32_t s[HJ_ITEMS], m[HJ_ITEMS], first[HJ_ITEMS];
+  uint32_t act = 0;  // bit i: item i's run not finished
+#pragma unroll
+  for (int i = 0; i < HJ_ITEMS; ++i) {
+    const uint64_t r = base + (uint64_t)i * HJ_THREADS;
+    key[i] = r < n ? __builtin_nontemporal_load(probe + r) : 0;
+    s[i] = (uint32_t)hj_home(key[i], t);
+    m[i] = 0;
+    first[i] = 0;
+    act |= (r < n ? 1u : 0u) << i;
+  }
+  // a probe row stops at its first match when the build keys are unique, and always for
+  // SEMI / ANTI (existence is all they need)
+  const bool stop_on_hit = type >= NUT_JOIN_SEMI || *dup == 0;
+  // walk every item's run in lock-step rounds: each round issues one slot load per item
+  // (unconditionally — a finished item re-reads its empty slot from cache — so all of
+  // them are in flight together), then consumes them
+  while (__any(act)) {
+    i64x2 v[HJ_ITEMS];
+#pragma unroll
+    for (int i = 0; i < HJ_ITEMS; ++i) {
+      v[i] = i64x2{0, -1};
+      if ((act >> i) & 1u) v[i] = t.slot[s[i]];  // finished items issue no request
+    }
+#pragma unroll
+    for (int i = 0; i < HJ_ITEMS; ++i) {
+      const bool occ = ((act >> i) & 1u) && v[i].y != -1;
+      const bool hit = occ && v[i].x == key[i];
+      if (hit) {
+        first[i] = m[i] ? first[i] : (uint32_t)v[i].y;
+        ++m[i];
+      }
+      const bool more = occ && !(hit && stop_on_hit);
+      s[i] = more ? (uint32_t)((s[i] + 1) & t.mask) : s[i];
+      act = more ? act : (act & ~(1u << i));
+    }
+  }
+  // ranks inside the tile, rows ordered (item, wave, lane)
+  uint64_t ex[HJ_ITEMS];
+#pragma unroll
+  for (int i = 0; i < HJ_ITEMS; ++i) {
+    const uint64_t c = base + (uint64_t)i * HJ_THREADS < n ? hj_out_count(m[i], type) : 0;
+    uint64_t incl = c;
+#pragma unroll
+    for (int off = 1; off < kWave; off <<= 1) {
+      const uint64_t y = __shfl_up(incl, off, kWave);
+      if (lane >= off) incl += y;
+    }
+    ex[i] = incl - c;
+    if (lane == kWave - 1) s_pre[i][wave] = incl;
+  }
+  __syncthreads();
+  if (wave == 0) {
+    // the ITEMS x WAVES wave totals, scanned in (item, wave) order, PER consecutive per lane
+    constexpr int E = HJ_ITEMS * HJ_WAVES, PER = E > kWave ? E / kWave : 1;
+    static_assert(E <= kWave || PER * kWave == E, "wave totals must fill the lanes");
+    uint64_t *flat = &s_pre[0][0];
+    uint64_t a[PER], sum = 0;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      a[k] = PER * lane + k < E ? flat[PER * lane + k] : 0;
+      sum += a[k];
+    }
+    uint64_t incl = sum;
+#pragma unroll
+    for (int off = 1; off < kWave; off <<= 1) {
+      const uint64_t y = __shfl_up(incl, off, kWave);
+      if (lane >= off) incl += y;
+    }
+    const uint64_t tot = __shfl(incl, kWave - 1, kWave);
+    uint64_t run = incl - sum;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      if (PER * lane + k < E) flat[PER * lane + k] = run;
+      run += a[k];
+    }
+    if (!WRITE) {
+      if (lane == 0 && tot) atomicAdd(total, (unsigned long long)tot);
+    } else {
+      const uint64_t e = lookback(status, tile, tot, err, lane);
+      if (lane == 0) {
+        s_excl = e;
+        if (tile == ntiles - 1) *total = e + tot;
+      }
+    }
+  }
+  if (!WRITE) return;
+  __syncthreads();
+  const uint64_t off0 = s_excl;
+#pragma unroll
+  for (int i = 0; i < HJ_ITEMS; ++i) {
+    const uint64_t r = base + (uint64_t)i * HJ_THREADS;
+    const uint32_t c = r < n ? hj_out_count(m[i], type) : 0;
+    if (!c) continue;
+    uint64_t pos = off0 + s_pre[i][wave] + ex[i];
+    if (pos + c > cap) continue;  // too small: the caller retries with the total
+    if (m[i] == 0 || type >= NUT_JOIN_SEMI) {
+      out_p[pos] = (int64_t)r;
+      out_b[pos] = -1;
+    } else if (m[i] == 1) {
+      out_p[pos] = (int64_t)r;
+      out_b[pos] = (int64_t)first[i];
+    } else {
+      uint64_t q = hj_home(key[i], t);
+      for (i64x2 v = t.slot[q]; v.y != -1; q = (q + 1) & t.mask, v = t.slot[q])
+        if (v.x == key[i]) {
+          out_p[pos] = (int64_t)r;
+          out_b[pos++] = v.y;
+        }
+    }
   }
 }
 
@@ -232,76 +307,113 @@ __global__ void gather_u64_kernel(const uint64_t *__restrict__ src, const int64_
 
 using namespace nut;
 
+namespace {
+
+using HjProbeFn = void (*)(HjTable, const int64_t *, uint64_t, int, uint32_t *, uint64_t *, uint32_t,
+                           unsigned long long *, int64_t *, int64_t *, uint64_t, uint32_t *, const uint32_t *);
+struct HjCfg {
+  int threads;
+  uint32_t tile;
+  HjProbeFn write, count;
+};
+template <int T, int I>
+constexpr HjCfg hj_make() {
+  return HjCfg{T, (uint32_t)(T * I), hj_probe_kernel<true, T, I>, hj_probe_kernel<false, T, I>};
+}
+// probe tile shapes (threads x rows per lane); NUT_HJ_CFG picks one for tuning runs
+const HjCfg &hj_cfg() {
+  static const HjCfg cfgs[] = {hj_make<512, 8>(), hj_make<256, 8>(), hj_make<256, 16>(), hj_make<512, 16>(),
+                               hj_make<256, 4>()};
+  static const int pick = [] {
+    const char *e = getenv("NUT_HJ_CFG");
+    const int v = e ? atoi(e) : 0;
+    return v >= 0 && v < (int)(sizeof cfgs / sizeof cfgs[0]) ? v : 0;
+  }();
+  return cfgs[pick];
+}
+
+}  // namespace
+
 struct nut_join {
   nut_ctx *ctx = nullptr;
-  void *mem = nullptr;  // table (offsets, bucket keys, row ids) + tile counts / offsets
+  void *mem = nullptr;  // table slots + probe state (status per tile, ticket, error, total)
   HjTable t{};
   const int64_t *probe = nullptr;
   uint64_t np = 0, ntiles = 0, n = 0;
   int type = 0;
-  uint64_t *toff = nullptr;
+  uint64_t *status = nullptr;
+  uint32_t *ticket = nullptr, *err = nullptr, *dup = nullptr;
+  unsigned long long *total = nullptr;
+  size_t state_bytes = 0;
 };
 
 namespace {
 
-// exclusive scan of n u32 / u64 values into out[0..n] (out[n] = total)
-template <class T>
-nut_status excl_scan(nut_ctx *c, const T *in, uint64_t n, uint64_t *out, uint64_t *sums) {
-  const uint64_t blocks = (n + SC_TILE - 1) / SC_TILE;
-  hipLaunchKernelGGL(scan_reduce_kernel<T>, dim3((unsigned)blocks), dim3(SC_THREADS), 0, c->stream, in, n, sums);
-  hipLaunchKernelGGL(scan_sums_kernel, dim3(1), dim3(SC_THREADS), 0, c->stream, sums, blocks);
-  hipLaunchKernelGGL(scan_apply_kernel<T>, dim3((unsigned)blocks), dim3(SC_THREADS), 0, c->stream, in, n,
-                     (const uint64_t *)sums, out);
+nut_status join_build(nut_ctx *c, nut_join *j, const int64_t *build, uint64_t nb) {
+  hipStream_t st = c->stream;
+  int log2c = 6;  // >= 2 slots per build row, >= 64 slots
+  while ((1ull << log2c) < 2 * nb) ++log2c;
+  const uint64_t cap = 1ull << log2c;
+  j->ntiles = (j->np + hj_cfg().tile - 1) / hj_cfg().tile;
+  if (j->ntiles > 0xFFFFFFF0ull) return fail(NUT_ERR_UNSUPPORTED, "nut_join_i64: probe side too large");
+  // [slots 16 B x cap | dup u32, pad | ticket u32, err u32, total u64 | status u64 x ntiles]
+  const size_t o_dup = cap * 16, o_state = o_dup + 16;
+  j->state_bytes = 16 + j->ntiles * 8;
+  NUT_HIP(hipMalloc(&j->mem, o_state + j->state_bytes));
+  char *b = (char *)j->mem;
+  j->t = HjTable{(i64x2 *)b, cap - 1, 64 - log2c};
+  j->ticket = (uint32_t *)(b + o_state);
+  j->err = j->ticket + 1;
+  j->total = (unsigned long long *)(b + o_state + 8);
+  j->status = (uint64_t *)(b + o_state + 16);
+  j->dup = (uint32_t *)(b + o_dup);
+  NUT_HIP(hipMemsetAsync(b, 0xFF, cap * 16, st));
+  NUT_HIP(hipMemsetAsync(j->dup, 0, 16, st));
+  if (nb) {
+    const unsigned g = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((nb + 255) / 256, c->num_cus * 16ull));
+    hipLaunchKernelGGL(hj_build_kernel, dim3(g), dim3(256), 0, st, build, nb, j->t);
+    if (j->type <= NUT_JOIN_LEFT)
+      hipLaunchKernelGGL(hj_dupcheck_kernel, dim3(g), dim3(256), 0, st, build, nb, j->t, j->dup);
+  }
   NUT_HIP(hipGetLastError());
   return NUT_OK;
 }
 
-nut_status join_build_count(nut_ctx *c, nut_join *j, const int64_t *build, uint64_t nb) {
+// one probe pass; WRITE: pairs below cap into (pi, bi).  Returns the pair count.
+nut_status join_probe(nut_join *j, bool write, int64_t *pi, int64_t *bi, uint64_t cap, uint64_t *npairs) {
+  nut_ctx *c = j->ctx;
   hipStream_t st = c->stream;
-  int log2b = 0;  // >= 2 buckets per build row
-  while ((1ull << log2b) < 2 * std::max<uint64_t>(nb, 1)) ++log2b;
-  const uint64_t nbk = 1ull << log2b;
-  const uint64_t ntiles = (j->np + HJ_TILE - 1) / HJ_TILE;
-  const uint64_t nsc = std::max<uint64_t>(nbk, ntiles);
-  // [counts u32 nbk | offsets u64 nbk+1 | cursors u64 nbk | bkeys nb | brow nb | tile counts u64 |
-  //  tile offsets u64 ntiles+1 | scan sums]
-  size_t o = 0;
-  auto carve = [&](size_t bytes) {
-    const size_t r = o;
-    o += (bytes + 255) & ~size_t(255);
-    return r;
-  };
-  const size_t o_cnt = carve(nbk * 4), o_off = carve((nbk + 1) * 8), o_cur = carve(nbk * 8), o_bk = carve(nb * 8),
-               o_br = carve(nb * 8), o_tc = carve(ntiles * 8), o_to = carve((ntiles + 1) * 8),
-               o_sm = carve(((nsc + SC_TILE - 1) / SC_TILE + 1) * 8);
-  NUT_HIP(hipMalloc(&j->mem, o));
-  char *b = (char *)j->mem;
-  uint32_t *cnt = (uint32_t *)(b + o_cnt);
-  uint64_t *off = (uint64_t *)(b + o_off), *cur = (uint64_t *)(b + o_cur);
-  int64_t *bkeys = (int64_t *)(b + o_bk), *brow = (int64_t *)(b + o_br);
-  uint64_t *tcnt = (uint64_t *)(b + o_tc), *sums = (uint64_t *)(b + o_sm);
-  j->toff = (uint64_t *)(b + o_to);
-  j->ntiles = ntiles;
-  NUT_HIP(hipMemsetAsync(cnt, 0, nbk * 4, st));
-  const unsigned g = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((nb + 255) / 256, c->num_cus * 8ull));
-  if (nb) hipLaunchKernelGGL(hj_count_kernel, dim3(g), dim3(256), 0, st, build, nb, log2b, cnt);
-  nut_status s = excl_scan<uint32_t>(c, cnt, nbk, off, sums);
-  if (s) return s;
-  NUT_HIP(hipMemcpyAsync(cur, off, nbk * 8, hipMemcpyDeviceToDevice, st));
-  if (nb) hipLaunchKernelGGL(hj_fill_kernel, dim3(g), dim3(256), 0, st, build, nb, log2b, (unsigned long long *)cur,
-                             bkeys, brow);
-  j->t = HjTable{off, bkeys, brow, log2b};
-  j->n = 0;
-  if (ntiles) {
-    hipLaunchKernelGGL(hj_probe_count_kernel, dim3((unsigned)ntiles), dim3(HJ_THREADS), 0, st, j->t, j->probe, j->np,
-                       j->type, tcnt);
-    s = excl_scan<uint64_t>(c, tcnt, ntiles, j->toff, sums);
-    if (s) return s;
-    NUT_HIP(hipMemcpyAsync(c->host_pinned, j->toff + ntiles, 8, hipMemcpyDeviceToHost, st));
-    NUT_HIP(hipStreamSynchronize(st));
-    j->n = c->host_pinned[0];
-  }
+  *npairs = 0;
+  if (!j->ntiles) return NUT_OK;
+  NUT_HIP(hipMemsetAsync(j->ticket, 0, j->state_bytes, st));
+  const HjCfg &cf = hj_cfg();
+  (write ? cf.write : cf.count)<<<dim3((unsigned)j->ntiles), dim3(cf.threads), 0, st>>>(
+      j->t, j->probe, j->np, j->type, j->ticket, j->status, (uint32_t)j->ntiles, j->total, pi, bi, cap, j->err,
+      (const uint32_t *)j->dup);
   NUT_HIP(hipGetLastError());
+  NUT_HIP(hipMemcpyAsync(c->host_pinned, j->ticket, 16, hipMemcpyDeviceToHost, st));
+  NUT_HIP(hipStreamSynchronize(st));
+  if ((uint32_t)(c->host_pinned[0] >> 32) != 0) return fail(NUT_ERR_TIMEOUT, "nut_join: look-back spin limit hit");
+  *npairs = c->host_pinned[1];
+  return NUT_OK;
+}
+
+nut_status join_begin(nut_ctx *c, const int64_t *build, uint64_t nb, const int64_t *probe, uint64_t np, int type,
+                      nut_join **out, const char *who) {
+  if (type < NUT_JOIN_INNER || type > NUT_JOIN_ANTI) return fail(NUT_ERR_INVALID_ARG, std::string(who) + ": bad join type");
+  if (nb >= (1ull << 31)) return fail(NUT_ERR_UNSUPPORTED, std::string(who) + ": build side >= 2^31 rows");
+  nut_join *j = new (std::nothrow) nut_join();
+  if (!j) return fail(NUT_ERR_OOM, std::string(who) + ": out of host memory");
+  j->ctx = c;
+  j->probe = probe;
+  j->np = np;
+  j->type = type;
+  nut_status s = join_build(c, j, build, nb);
+  if (s) {
+    nut_join_free(j);
+    return s;
+  }
+  *out = j;
   return NUT_OK;
 }
 
@@ -313,17 +425,12 @@ nut_status nut_join_i64(nut_ctx *c, const int64_t *build, uint64_t nb, const int
                         nut_join **out, uint64_t *npairs) {
   if (!c || !out || !npairs || (nb && !build) || (np && !probe))
     return fail(NUT_ERR_INVALID_ARG, "nut_join_i64: NULL argument");
-  if (type < NUT_JOIN_INNER || type > NUT_JOIN_ANTI) return fail(NUT_ERR_INVALID_ARG, "nut_join_i64: bad join type");
-  if (nb >= (1ull << 32)) return fail(NUT_ERR_UNSUPPORTED, "nut_join_i64: build side >= 2^32 rows");
   *out = nullptr;
   DeviceGuard dg(c->device);
-  nut_join *j = new nut_join();
-  j->ctx = c;
-  j->probe = probe;
-  j->np = np;
-  j->type = type;
+  nut_join *j = nullptr;
   c->timer.begin(c->stream, NUT_KERNEL_JOIN);
-  nut_status s = join_build_count(c, j, build, nb);
+  nut_status s = join_begin(c, build, nb, probe, np, type, &j, "nut_join_i64");
+  if (!s) s = join_probe(j, false, nullptr, nullptr, 0, &j->n);
   c->timer.end(c->stream);
   if (s) {
     nut_join_free(j);
@@ -339,11 +446,30 @@ nut_status nut_join_write(nut_join *j, int64_t *probe_idx, int64_t *build_idx) {
   if (!j->n) return NUT_OK;
   nut_ctx *c = j->ctx;
   DeviceGuard dg(c->device);
+  uint64_t n = 0;
   c->timer.begin(c->stream, NUT_KERNEL_JOIN);
-  hipLaunchKernelGGL(hj_probe_write_kernel, dim3((unsigned)j->ntiles), dim3(HJ_THREADS), 0, c->stream, j->t, j->probe,
-                     j->np, j->type, (const uint64_t *)j->toff, probe_idx, build_idx);
+  nut_status s = join_probe(j, true, probe_idx, build_idx, j->n, &n);
   c->timer.end(c->stream);
-  NUT_HIP(hipGetLastError());
+  if (!s && n != j->n) return fail(NUT_ERR_HIP, "nut_join_write: pair count changed between passes");
+  return s;
+}
+
+nut_status nut_join_i64_into(nut_ctx *c, const int64_t *build, uint64_t nb, const int64_t *probe, uint64_t np,
+                             int type, int64_t *probe_idx, int64_t *build_idx, uint64_t cap, uint64_t *npairs) {
+  if (!c || !npairs || (nb && !build) || (np && !probe) || (cap && (!probe_idx || !build_idx)))
+    return fail(NUT_ERR_INVALID_ARG, "nut_join_i64_into: NULL argument");
+  DeviceGuard dg(c->device);
+  nut_join *j = nullptr;
+  c->timer.begin(c->stream, NUT_KERNEL_JOIN);
+  nut_status s = join_begin(c, build, nb, probe, np, type, &j, "nut_join_i64_into");
+  uint64_t n = 0;
+  if (!s) s = join_probe(j, true, probe_idx, build_idx, cap, &n);
+  c->timer.end(c->stream);
+  nut_join_free(j);
+  if (s) return s;
+  *npairs = n;
+  if (n > cap) return fail(NUT_ERR_CAPACITY, "nut_join_i64_into: " + std::to_string(n) + " pairs > capacity " +
+                                                std::to_string(cap));
   return NUT_OK;
 }
 

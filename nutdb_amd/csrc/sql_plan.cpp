@@ -1836,20 +1836,23 @@ nut_status exec_join(nut_ctx *c, const nut_plan &p, const nut_column *lc, int nl
                                     "' may only appear inside aggregates");
     }
   }
-  nut_join *j = nullptr;
-  uint64_t npairs = 0;
-  nut_status st = nut_join_i64(c, (const int64_t *)bk->data, nb, (const int64_t *)pk->data, np, p.join, &j, &npairs);
-  if (st) return st;
+  // one pass into arrays of np pairs (enough unless the build keys repeat), else again
+  // with the exact count
   DevBuf idx;
-  hipError_t he = hipMalloc(&idx.p, std::max<uint64_t>(npairs, 1) * 16);
-  if (he != hipSuccess) {
-    nut_join_free(j);
-    return hip_fail(he, "hipMalloc (join index)");
+  uint64_t cap = std::max<uint64_t>(np, 1), npairs = 0;
+  nut_status st;
+  for (;;) {
+    hipError_t he = hipMalloc(&idx.p, cap * 16);
+    if (he != hipSuccess) return hip_fail(he, "hipMalloc (join index)");
+    st = nut_join_i64_into(c, (const int64_t *)bk->data, nb, (const int64_t *)pk->data, np, p.join,
+                           (int64_t *)idx.p, (int64_t *)idx.p + cap, cap, &npairs);
+    if (st != NUT_ERR_CAPACITY || npairs <= cap) break;
+    NUT_HIP(hipFree(idx.p));
+    idx.p = nullptr;
+    cap = npairs;
   }
-  int64_t *pi = (int64_t *)idx.p, *bi = pi + std::max<uint64_t>(npairs, 1);
-  st = nut_join_write(j, pi, bi);
-  nut_join_free(j);
   if (st) return st;
+  int64_t *pi = (int64_t *)idx.p, *bi = pi + cap;
   // the joined table: every plan column gathered through its side's index
   nut_plan p2 = p;
   const bool mask_col = outer && p.kind == NUT_PLAN_GROUPBY;

@@ -401,30 +401,50 @@ class Executor:
     # ---------------------------------------------------------------- join
     JOIN_TYPES = {"inner": 0, "left": 1, "semi": 2, "anti": 3}
 
-    def join_i64(self, build: torch.Tensor, probe: torch.Tensor, how: str = "inner"):
+    def join_i64(self, build: torch.Tensor, probe: torch.Tensor, how: str = "inner", passes: int = 1):
         """Hash equi-join (nut_join_i64): (probe_idx, build_idx) int64 tensors, ordered by
         probe row; build_idx = -1 for LEFT rows without a match and for SEMI / ANTI rows.
-        Lowered from JoinClause (src/parser/ast/query.rs:55-66, 100-117)."""
+        Lowered from JoinClause (src/parser/ast/query.rs:55-66, 100-117).  passes=1:
+        nut_join_i64_into (one probe pass into arrays of len(probe) pairs, again with the
+        exact size if the build keys repeat); passes=2: nut_join_i64 (count) +
+        nut_join_write."""
         for t in (build, probe):
             if t.dtype != torch.int64:
                 raise TypeError("join_i64 takes int64 key columns")
         if how not in self.JOIN_TYPES:
             raise ValueError(f"join type {how!r} (inner, left, semi, anti)")
         self._bind_stream()
-        h = C.c_void_p()
         n = C.c_uint64()
         nb, np_ = build.numel(), probe.numel()
-        check(lib.nut_join_i64(self.ctx, C.c_void_p(_col(build, self.device) if nb else None), nb,
-                               C.c_void_p(_col(probe, self.device) if np_ else None), np_, self.JOIN_TYPES[how],
-                               C.byref(h), C.byref(n)), "nut_join_i64")
-        try:
-            pi = torch.empty(n.value, dtype=torch.int64, device=self.device)
-            bi = torch.empty(n.value, dtype=torch.int64, device=self.device)
-            check(lib.nut_join_write(h, C.c_void_p(pi.data_ptr() if n.value else None),
-                                     C.c_void_p(bi.data_ptr() if n.value else None)), "nut_join_write")
-            self.sync()
-        finally:
-            lib.nut_join_free(h)
+        bp = C.c_void_p(_col(build, self.device) if nb else None)
+        pp = C.c_void_p(_col(probe, self.device) if np_ else None)
+        if passes == 2:
+            h = C.c_void_p()
+            check(lib.nut_join_i64(self.ctx, bp, nb, pp, np_, self.JOIN_TYPES[how], C.byref(h), C.byref(n)),
+                  "nut_join_i64")
+            try:
+                pi = torch.empty(n.value, dtype=torch.int64, device=self.device)
+                bi = torch.empty(n.value, dtype=torch.int64, device=self.device)
+                check(lib.nut_join_write(h, C.c_void_p(pi.data_ptr() if n.value else None),
+                                         C.c_void_p(bi.data_ptr() if n.value else None)), "nut_join_write")
+                self.sync()
+            finally:
+                lib.nut_join_free(h)
+            return pi, bi
+        cap = np_  # enough unless build keys repeat (INNER / LEFT): then one more pass
+        while True:
+            pi = torch.empty(cap, dtype=torch.int64, device=self.device)
+            bi = torch.empty(cap, dtype=torch.int64, device=self.device)
+            st = lib.nut_join_i64_into(self.ctx, bp, nb, pp, np_, self.JOIN_TYPES[how],
+                                       C.c_void_p(pi.data_ptr() if cap else None),
+                                       C.c_void_p(bi.data_ptr() if cap else None), cap, C.byref(n))
+            if st == L.NUT_ERR_CAPACITY and n.value > cap:
+                cap = n.value
+                continue
+            check(st, "nut_join_i64_into")
+            break
+        self.sync()
+        pi, bi = pi[:n.value], bi[:n.value]
         return pi, bi
 
     def gather(self, col: torch.Tensor, idx: torch.Tensor, null=0) -> torch.Tensor:

@@ -427,3 +427,90 @@ uint64_t orc_multiset_hash_i64(const int64_t *v, uint64_t n) {
   for (int64_t i = 0; i < (int64_t)n; ++i) h += orc_mix64((uint64_t)v[i] ^ 0xA0761D6478BD642Full);
   return h;
 }
+
+/* Hash equi-join (include/nutexec.h nut_join_i64 semantics; join types 0 INNER, 1 LEFT,
+ * 2 SEMI, 3 ANTI): a CSR bucket table over the build keys (OpenMP count / scan / fill),
+ * then an OpenMP probe in two passes per thread chunk (count pairs, write them), so the
+ * pairs come out in probe-row order.  Within a probe row the build rows are in the
+ * table's fill order (unspecified).  Writes at most `cap` pairs; returns the pair count
+ * (call again with a larger cap when it exceeds cap).  Pinned by the numpy join oracle
+ * (oracle.py join_i64) in tests/test_join_cpu.py; the CPU baseline of bench.py join. */
+static uint64_t join_bucket(int64_t k, int log2b) {
+  return log2b ? orc_mix64((uint64_t)k ^ 0x3C6EF372FE94F82Aull) >> (64 - log2b) : 0;
+}
+
+uint64_t orc_join_i64(const int64_t *build, uint64_t nb, const int64_t *probe, uint64_t np, int type,
+                      int64_t *out_p, int64_t *out_b, uint64_t cap) {
+  int log2b = 0;
+  while ((1ull << log2b) < 2 * nb) ++log2b;
+  const uint64_t nbk = 1ull << log2b;
+  uint64_t *off = calloc(nbk + 1, sizeof(uint64_t));
+  int64_t *bkeys = malloc((nb ? nb : 1) * sizeof(int64_t)), *brow = malloc((nb ? nb : 1) * sizeof(int64_t));
+#pragma omp parallel for
+  for (int64_t i = 0; i < (int64_t)nb; ++i) {
+    const uint64_t b = join_bucket(build[i], log2b);
+#pragma omp atomic
+    off[b + 1]++;
+  }
+  for (uint64_t b = 0; b < nbk; ++b) off[b + 1] += off[b];
+  uint64_t *cur = malloc(nbk * sizeof(uint64_t));
+  memcpy(cur, off, nbk * sizeof(uint64_t));
+#pragma omp parallel for
+  for (int64_t i = 0; i < (int64_t)nb; ++i) {
+    const uint64_t b = join_bucket(build[i], log2b);
+    uint64_t pos;
+#pragma omp atomic capture
+    pos = cur[b]++;
+    bkeys[pos] = build[i];
+    brow[pos] = i;
+  }
+  free(cur);
+  const int nt = omp_get_max_threads();
+  uint64_t *tcnt = calloc((size_t)nt + 1, sizeof(uint64_t));
+  uint64_t total = 0;
+#pragma omp parallel num_threads(nt)
+  {
+    const int t = omp_get_thread_num(), T = omp_get_num_threads();
+    const uint64_t chunk = (np + T - 1) / T, lo = (uint64_t)t * chunk < np ? (uint64_t)t * chunk : np;
+    const uint64_t hi = lo + chunk < np ? lo + chunk : np;
+    uint64_t c = 0;
+    for (uint64_t r = lo; r < hi; ++r) {
+      const uint64_t b = join_bucket(probe[r], log2b);
+      uint64_t m = 0;
+      for (uint64_t j = off[b]; j < off[b + 1]; ++j) m += bkeys[j] == probe[r];
+      c += type == 0 ? m : type == 1 ? (m ? m : 1) : type == 2 ? (m ? 1 : 0) : (m ? 0 : 1);
+    }
+    tcnt[t + 1] = c;
+#pragma omp barrier
+#pragma omp single
+    {
+      for (int i = 0; i < T; ++i) tcnt[i + 1] += tcnt[i];
+      total = tcnt[T];
+    }
+    if (total <= cap) {
+      uint64_t pos = tcnt[t];
+      for (uint64_t r = lo; r < hi; ++r) {
+        const int64_t k = probe[r];
+        const uint64_t b = join_bucket(k, log2b);
+        uint64_t m = 0;
+        for (uint64_t j = off[b]; j < off[b + 1]; ++j)
+          if (bkeys[j] == k) {
+            if (type <= 1) {
+              out_p[pos] = (int64_t)r;
+              out_b[pos++] = brow[j];
+            }
+            ++m;
+          }
+        if ((type == 1 && !m) || (type == 2 && m) || (type == 3 && !m)) {
+          out_p[pos] = (int64_t)r;
+          out_b[pos++] = -1;
+        }
+      }
+    }
+  }
+  free(tcnt);
+  free(off);
+  free(bkeys);
+  free(brow);
+  return total;
+}

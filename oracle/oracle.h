@@ -90,6 +90,11 @@ uint64_t orc_groupby(const orc_agg_spec *spec, uint64_t cap, int64_t *out_keys,
 
 /* ---- sort: ascending int64 ---- */
 void orc_sort_i64(const int64_t *in, int64_t *out, uint64_t n, int nthreads);
+/* Hash equi-join, nut_join_i64 semantics (type 0 INNER, 1 LEFT, 2 SEMI, 3 ANTI): pairs in
+ * probe-row order, build rows of one probe row in unspecified order, -1 = no build row.
+ * Writes at most cap pairs and returns the pair count. */
+uint64_t orc_join_i64(const int64_t *build, uint64_t nb, const int64_t *probe, uint64_t np, int type,
+                      int64_t *out_p, int64_t *out_b, uint64_t cap);
 
 /* order-independent multiset hash (sum of mix64 of each element), for sort parity */
 uint64_t orc_multiset_hash_i64(const int64_t *v, uint64_t n);

@@ -65,6 +65,9 @@ def lib():
         L.orc_filter_i64.argtypes = [C.c_void_p, C.c_uint64, C.c_int, C.c_int64, C.c_void_p]
         L.orc_groupby.restype = C.c_uint64
         L.orc_groupby.argtypes = [C.POINTER(OrcAggSpec), C.c_uint64, C.c_void_p, C.c_void_p, C.c_int]
+        L.orc_join_i64.restype = C.c_uint64
+        L.orc_join_i64.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_int, C.c_void_p,
+                                   C.c_void_p, C.c_uint64]
         L.orc_sort_i64.restype = None
         L.orc_sort_i64.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_int]
         L.orc_multiset_hash_i64.restype = C.c_uint64
@@ -189,3 +192,23 @@ def join_i64(build: np.ndarray, probe: np.ndarray, how: str = "inner"):
     within = np.arange(len(pi), dtype=np.int64) - np.repeat(np.cumsum(cnt) - cnt, cnt)
     bi = np.where(np.repeat(m, cnt) > 0, order[np.minimum(starts + within, len(order) - 1)] if len(order) else -1, -1)
     return pi, bi.astype(np.int64)
+
+
+JOIN_TYPES = {"inner": 0, "left": 1, "semi": 2, "anti": 3}
+
+
+def join_i64_c(build: np.ndarray, probe: np.ndarray, how: str = "inner"):
+    """The C hash join (oracle.c orc_join_i64, OpenMP): (probe_idx, build_idx) in probe-row
+    order, build rows of one probe row in unspecified order.  CPU baseline of bench.py's
+    join workload; pinned against join_i64 above."""
+    build = np.ascontiguousarray(build, dtype=np.int64)
+    probe = np.ascontiguousarray(probe, dtype=np.int64)
+    cap = len(probe)
+    while True:
+        pi = np.empty(max(cap, 1), dtype=np.int64)
+        bi = np.empty(max(cap, 1), dtype=np.int64)
+        n = lib().orc_join_i64(build.ctypes.data, len(build), probe.ctypes.data, len(probe), JOIN_TYPES[how],
+                               pi.ctypes.data, bi.ctypes.data, cap)
+        if n <= cap:
+            return pi[:n], bi[:n]
+        cap = n

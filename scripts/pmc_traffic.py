@@ -16,10 +16,11 @@ WORKLOAD_KERNEL = {"q1": ("tpch_q1_shape_filter_groupby", "agg_kernel"),
                    "groupby": ("groupby_i64_sum_f64", "agg_kernel"),
                    "filter": ("filter_i64_compaction", "filter_i64_kernel"),
                    "sort": ("sort_i64_radix", "nut::ms_"),
-                   "q12expr": ("q12_shape_expression_groupby", "agg_kernel")}
+                   "q12expr": ("q12_shape_expression_groupby", "agg_kernel"),
+                   "join": ("join_i64_hash", "hj_")}
 # sort: one step = every kernel of one MSD sort (2 histograms, 2 scatter levels, the
 # local sort and its fallback); traffic is summed per step (one local-sort launch per step)
-STEP_KERNEL = {"sort": "ms_local_kernel"}
+STEP_KERNEL = {"sort": "ms_local_kernel", "join": "hj_probe_kernel"}
 
 
 def main():
@@ -27,13 +28,17 @@ def main():
     args = sys.argv[2:]
     wl = args[args.index("--workload") + 1] if "--workload" in args else "q1"
     rows = float(args[args.index("--rows") + 1]) if "--rows" in args else {"q1": 1e9, "groupby": 1e9, "filter": 1e8,
-                                                                           "sort": 1.25e9, "q12expr": 1e9}[wl]
+                                                                           "sort": 1.25e9, "q12expr": 1e9,
+                                                                           "join": 1e9}[wl]
     name, match = WORKLOAD_KERNEL[wl]
     s = summarize(d, match, STEP_KERNEL.get(wl, ""))
     c = s["counters"]
     traffic = None
+    # join: the reads are dominated by random single-slot (64-B) requests, counted whole;
+    # the x2 halving correction is for wide streaming reads only
+    rmul = 1 if wl == "join" else 2
     if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
-        traffic = c["FETCH_SIZE"] * 1024 * 2 + c["WRITE_SIZE"] * 1024
+        traffic = c["FETCH_SIZE"] * 1024 * rmul + c["WRITE_SIZE"] * 1024
     s["workload"] = name
     s["rows"] = int(rows)
     s["hbm_bytes_per_launch"] = traffic
@@ -41,8 +46,12 @@ def main():
     (d / f"pmc_{name}.json").write_text(json.dumps({
         "workload": name, "rows": int(rows), "kernel_match": match, "hbm_bytes_per_launch": traffic,
         "fetch_size_kb": c.get("FETCH_SIZE"), "write_size_kb": c.get("WRITE_SIZE"),
-        "per": "step (all ms_* kernels of one sort)" if wl == "sort" else "launch of " + match,
-        "correction": "read = 2 x FETCH_SIZE (gfx950 wide-stream halving), write = WRITE_SIZE"}, indent=1))
+        "per": {"sort": "step (all ms_* kernels of one sort)", "join": "step (all hj_* kernels of one join)"}.get(
+            wl, "launch of " + match),
+        "correction": ("read = FETCH_SIZE (random 64-B slot reads dominate; the gfx950 x2 wide-stream "
+                       "correction is not applied, so the ~12 GB of streaming key reads count half)"
+                       if wl == "join" else "read = 2 x FETCH_SIZE (gfx950 wide-stream halving), write = WRITE_SIZE")},
+        indent=1))
     print(json.dumps({"workload": name, "traffic": traffic, "kernels": s["kernels"][:3]}))
 
 

@@ -18,8 +18,8 @@ def canon(pi, bi):
     return pi[o], bi[o]
 
 
-def check(ex, orc, b, p, how):
-    pi, bi = ex.join_i64(dev(b, ex), dev(p, ex), how)
+def check(ex, orc, b, p, how, passes=1):
+    pi, bi = ex.join_i64(dev(b, ex), dev(p, ex), how, passes=passes)
     pi, bi = host(pi), host(bi)
     wp, wb = orc.join_i64(b, p, how)
     assert np.all(pi[1:] >= pi[:-1]), "pairs not in probe-row order"
@@ -36,12 +36,34 @@ def test_join_unique_build(ex, orc, how, nb, np_):
     check(ex, orc, b, p, how)
 
 
+@pytest.mark.parametrize("passes", [1, 2])
 @pytest.mark.parametrize("how", HOW)
-def test_join_duplicates_both_sides(ex, orc, how):
+def test_join_duplicates_both_sides(ex, orc, how, passes):
+    """Repeated build keys: INNER / LEFT produce more pairs than probe rows, so the
+    one-pass form hits NUT_ERR_CAPACITY and runs again at the exact size."""
     rng = np.random.default_rng(5)
     b = rng.integers(0, 300, 20_000).astype(np.int64)
     p = rng.integers(-50, 350, 30_001).astype(np.int64)
-    check(ex, orc, b, p, how)
+    check(ex, orc, b, p, how, passes)
+
+
+@pytest.mark.parametrize("how", HOW)
+def test_join_two_pass_api(ex, orc, how):
+    rng = np.random.default_rng(15)
+    b = rng.permutation(np.arange(70_000, dtype=np.int64) * 5)
+    p = rng.integers(-100, 400_000, 1_000_003).astype(np.int64)
+    check(ex, orc, b, p, how, passes=2)
+
+
+def test_join_long_runs(ex, orc):
+    """Clustered hashes: 1000 copies of each of 3 keys build long probe runs; tiles mix
+    rows with thousands of matches and rows with none."""
+    rng = np.random.default_rng(21)
+    b = np.repeat(np.array([7, -7, 2**40], dtype=np.int64), 1000)
+    p = rng.choice(np.array([7, -7, 2**40, 8, 9], dtype=np.int64), 5_000)
+    check(ex, orc, b, p, "inner")
+    check(ex, orc, b, p, "left")
+    check(ex, orc, b, p, "anti")
 
 
 @pytest.mark.parametrize("how", HOW)

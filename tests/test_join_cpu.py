@@ -89,3 +89,18 @@ def test_count_star_and_count_column_stay_apart():
     d = Plan("select o_cust, count(*), count(l_qty) from orders left join lineitem on o_okey = l_okey "
              "group by o_cust").describe()
     assert len(d["aggs"]) == 2
+
+
+@pytest.mark.parametrize("how", ["inner", "left", "semi", "anti"])
+@pytest.mark.parametrize("nb,npr", [(0, 7), (7, 0), (300, 1000), (20_000, 200_000)])
+def test_c_join_oracle_matches_numpy(how, nb, npr):
+    """oracle.c orc_join_i64 (the bench's CPU baseline) against the numpy oracle; the C
+    join leaves the build rows of one probe row unordered, so pairs compare sorted."""
+    from oracle.oracle import join_i64_c
+    rng = np.random.default_rng(nb + npr)
+    b = rng.integers(-500, 500, nb).astype(np.int64)
+    p = rng.integers(-600, 600, npr).astype(np.int64)
+    a, c = join_i64(b, p, how), join_i64_c(b, p, how)
+    assert np.all(c[0][1:] >= c[0][:-1])
+    o = np.lexsort((c[1], c[0]))
+    assert np.array_equal(a[0], c[0][o]) and np.array_equal(a[1], c[1][o])
