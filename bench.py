@@ -220,10 +220,11 @@ class Join:
     name = "join_i64_hash"
     kernel_kind = 3
 
-    def __init__(self, ex, rows, row0):
+    def __init__(self, ex, rows, row0, world=1, group=None, rank=0):
         self.ex = ex
         self.rows = rows
         self.nb = rows // 4
+        self.world, self.group, self.rank = world, group, rank
         self.build = ex.gen_column(0, 0x71 + row0, self.nb)  # 62-bit: unique w.h.p.
         sel = ex.gen_column(0, 0x72 + row0, rows)
         self.probe = torch.where(sel % 10 == 0, sel | (1 << 62), self.build[sel % self.nb])
@@ -231,11 +232,16 @@ class Join:
         self.npairs = 0
 
     @property
-    def cols_bytes(self):  # per probe row
+    def cols_bytes(self):  # per probe row, of the join kernels the roofline times (N>1: local join)
         return (24.0 * self.nb + 8.0 * self.rows + 16.0 * self.npairs) / self.rows
 
     def run(self):
-        pi, bi = self.ex.join_i64(self.build, self.probe, "inner")
+        if self.world == 1:
+            pi, bi = self.ex.join_i64(self.build, self.probe, "inner")
+        else:
+            from nutdb_amd.dist import distributed_join
+            pi, bi = distributed_join(self.build, self.probe, self.ex.hash_partition_i64, self.ex.join_i64, "inner",
+                                      self.rank * self.nb, self.rank * self.rows, self.group)
         self.npairs = pi.numel()
         del pi, bi
 
@@ -243,7 +249,12 @@ class Join:
         return {"workload": self.name, "query": "SELECT ... FROM lineitem JOIN orders ON l_orderkey = o_orderkey "
                 "(join index: probe_idx, build_idx)", "build_rows": self.nb, "probe_rows": self.rows,
                 "pairs": self.npairs, "match_rate": 0.9, "bytes_per_row": self.cols_bytes,
-                "unit_rows": "probe rows"}
+                "unit_rows": "probe rows",
+                "algorithm": "open-addressing hash join, one ordered probe pass" + (
+                    "; both sides hash-partitioned by key owner + one RCCL all-to-all each, local joins"
+                    if self.world > 1 else ""),
+                "xgmi_bytes_per_row": 16.0 * (1 + self.nb / self.rows) * (self.world - 1) / self.world,
+                "partition_bytes_per_row": 48.0 * (1 + self.nb / self.rows) if self.world > 1 else 0.0}
 
 
 # ------------------------------------------------------------------ one step
@@ -399,10 +410,7 @@ def main():
             sys.exit(2)
         w = Q12Expr(ex, rows, row0)
     elif args.workload == "join":
-        if world > 1:
-            print("bench.py: join is a single-GPU workload", file=sys.stderr)
-            sys.exit(2)
-        w = Join(ex, rows, row0)
+        w = Join(ex, rows, row0, world, group, rank)
     else:
         w = Filter(ex, rows, row0, args.selectivity)
     torch.cuda.synchronize()

@@ -320,6 +320,12 @@ void nut_join_free(nut_join *j);
 nut_status nut_join_i64_into(nut_ctx *ctx, const int64_t *build, uint64_t nbuild, const int64_t *probe,
                              uint64_t nprobe, int join_type, int64_t *probe_idx, int64_t *build_idx, uint64_t cap,
                              uint64_t *npairs);
+/* The multi-GPU join's exchange step: rows go to part (owner_hash(key) >> 56) * nparts / 256
+ * (owner_hash = the group-by's; host restatement nutdb_amd/dist.py join_owner); out_keys /
+ * out_rows (row0 + row index) hold the parts one after another in part order, rows
+ * unordered within a part; counts_host[nparts] receives the part sizes.  nparts in [1, 256]. */
+nut_status nut_hash_partition_i64(nut_ctx *ctx, const int64_t *keys, uint64_t n, int nparts, int64_t row0,
+                                  int64_t *out_keys, int64_t *out_rows, uint64_t *counts_host);
 /* out[i] = src[idx[i]] (8-byte words), or `null_bits` where idx[i] < 0: carries any
  * int64 / f64 column through a join index */
 nut_status nut_gather_u64(nut_ctx *ctx, const uint64_t *src, const int64_t *idx, uint64_t n, uint64_t null_bits,

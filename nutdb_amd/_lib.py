@@ -131,6 +131,7 @@ SIGNATURES = {
     "nut_join_write": (_I32, [_P, _P, _P]),
     "nut_join_i64_into": (_I32, [_P, _P, _U64, _P, _U64, _I32, _P, _P, _U64, C.POINTER(_U64)]),
     "nut_join_free": (None, [_P]),
+    "nut_hash_partition_i64": (_I32, [_P, _P, _U64, _I32, _I64, _P, _P, C.POINTER(_U64)]),
     "nut_gather_u64": (_I32, [_P, _P, _P, _U64, _U64, _P]),
     "nut_gen_column": (_I32, [_P, _I32, _U64, _I64, _I64, C.c_double, _U64, _U64, _P]),
     "nut_filter_i64": (_I32, [_P, _P, _U64, _I32, _I64, _P, C.POINTER(_U64)]),

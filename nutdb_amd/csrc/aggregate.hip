@@ -893,9 +893,44 @@ __global__ void groups_place_kernel(const uint64_t *__restrict__ cols, const int
     for (int a = 0; a < naggs; ++a) aggs_out[lo * naggs + a] = cols[(uint64_t)(1 + a) * n + i];
   }
 }
+
+__global__ void iota_kernel(int64_t *__restrict__ out, uint64_t n, int64_t base) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    out[i] = base + (int64_t)i;
+}
 }  // namespace nut
 
 extern "C" {
+
+// The multi-GPU join's exchange step: one gp_level (gpart.hpp) over the keys with the row
+// ids as payload, 256 digits of the owner hash's top byte, parts = digit ranges.
+nut_status nut_hash_partition_i64(nut_ctx *c, const int64_t *keys, uint64_t n, int nparts, int64_t row0,
+                                  int64_t *out_keys, int64_t *out_rows, uint64_t *counts_host) {
+  if (!c || !counts_host || (n && (!keys || !out_keys || !out_rows)))
+    return fail(NUT_ERR_INVALID_ARG, "nut_hash_partition_i64: NULL argument");
+  if (nparts < 1 || nparts > GP_BINS) return fail(NUT_ERR_INVALID_ARG, "nut_hash_partition_i64: nparts not in [1, 256]");
+  for (int p = 0; p < nparts; ++p) counts_host[p] = 0;
+  if (n == 0) return NUT_OK;
+  DeviceGuard dg(c->device);
+  hipStream_t st = c->stream;
+  int64_t *rows = nullptr;
+  NUT_HIP(hipMallocAsync((void **)&rows, n * 8, st));
+  const unsigned g = (unsigned)std::min<uint64_t>((n + 255) / 256, (uint64_t)c->num_cus * 16);
+  hipLaunchKernelGGL(iota_kernel, dim3(g), dim3(256), 0, st, rows, n, row0);
+  const uint64_t *src[GP_MAX_ARR] = {nullptr, (const uint64_t *)keys, nullptr, (const uint64_t *)rows};
+  uint64_t *dst[GP_MAX_ARR] = {nullptr, (uint64_t *)out_keys, nullptr, (uint64_t *)out_rows};
+  std::vector<GpSeg> segs{GpSeg{0, n, 0, 0}};
+  std::vector<uint64_t> hist;
+  GpMeta mm{c};
+  nut_status e = gp_level(c, mm, segs, 56, src, dst, 4, false, false, hist);
+  if (!e) {
+    for (int d = 0; d < GP_BINS; ++d) counts_host[(d * nparts) >> 8] += hist[d];
+    hipError_t he = hipStreamSynchronize(st);
+    if (he != hipSuccess) e = hip_fail(he, "nut_hash_partition_i64");
+  }
+  (void)hipFreeAsync(rows, st);
+  return e;
+}
 
 nut_status nut_groups_to_host(nut_groups *g, int64_t *keys, uint64_t *aggs, uint64_t cap) {
   if (!g) return fail(NUT_ERR_INVALID_ARG, "nut_groups_to_host: NULL argument");

@@ -150,6 +150,58 @@ def exchange_keys(part: torch.Tensor, counts: List[int], group=None) -> torch.Te
     return out
 
 
+def join_owner(keys: np.ndarray, nparts: int) -> np.ndarray:
+    """Host restatement of nut_hash_partition_i64's part of a key: the top byte of the
+    group-by's owner hash, split into nparts ranges: ((owner_hash(k) >> 56) * P) >> 8."""
+    def mix(z):
+        z = z.astype(np.uint64)
+        with np.errstate(over="ignore"):
+            z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+            z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+    d = mix(np.asarray(keys, dtype=np.int64).view(np.uint64) ^ np.uint64(0x6A09E667F3BCC908)) >> np.uint64(56)
+    return ((d.astype(np.int64) * nparts) >> 8).astype(np.int64)
+
+
+def exchange_rows(keys: torch.Tensor, rows: torch.Tensor, counts: List[int], group=None):
+    """All-to-all of (key, row id) records partitioned by destination rank: segment p
+    (counts[p] records) goes to rank p.  Returns the received (keys, rows)."""
+    dev = keys.device
+    n = sum(counts)
+    send = torch.tensor(counts, dtype=torch.int64, device=dev)
+    recv = torch.empty_like(send)
+    dist.all_to_all_single(recv, send, group=group)
+    rc = [int(x) for x in recv.tolist()]
+    pack = torch.stack([keys[:n], rows[:n]], dim=1).contiguous()  # [n, 2]: one record per row
+    out = torch.empty((sum(rc), 2), dtype=torch.int64, device=dev)
+    dist.all_to_all_single(out, pack, rc, list(counts), group=group)
+    return out[:, 0].contiguous(), out[:, 1].contiguous()
+
+
+def distributed_join(build: torch.Tensor, probe: torch.Tensor, partition: Callable, join: Callable,
+                     how: str = "inner", build_row0: int = 0, probe_row0: int = 0, group=None):
+    """Multi-GPU hash join (the group-by's key-hash exchange reused):
+    both sides are partitioned by part = join_owner(key, P) (`partition(keys, row0, P) ->
+    (keys, rows, counts)`, nut_hash_partition_i64 on a GPU), ONE all-to-all per side moves
+    (key, global row) records to their owner, and each rank joins what it owns (`join(build
+    keys, probe keys, how) -> (probe_idx, build_idx)`, nut_join_i64_into).  Every key's
+    build and probe rows meet on one rank, so INNER / LEFT / SEMI / ANTI keep their global
+    meaning.  Returns this rank's pairs as GLOBAL (probe row, build row), -1 = no build row;
+    each rank's pairs are grouped by the owner's received probe order."""
+    world = dist.get_world_size(group)
+    bk, br, bc = partition(build, build_row0, world)
+    pk, pr, pc = partition(probe, probe_row0, world)
+    rbk, rbr = exchange_rows(bk, br, bc, group)
+    rpk, rpr = exchange_rows(pk, pr, pc, group)
+    pi, bi = join(rbk, rpk, how)
+    gp = rpr[pi]
+    if rbr.numel() == 0:
+        return gp, bi.clone()
+    gb = torch.where(bi >= 0, rbr[bi.clamp(min=0)], bi)
+    return gp, gb
+
+
 def distributed_sort(local: torch.Tensor, partition: Callable, sort: Callable, group=None,
                      samples_per_rank: int = 4096) -> torch.Tensor:
     """Multi-GPU ORDER BY k (BASELINE config 5): sample -> splitters ->

@@ -476,6 +476,22 @@ class Executor:
                                     C.c_void_p(out.data_ptr()), counts), "nut_partition_i64")
         return out[:n], [int(c) for c in counts]
 
+    def hash_partition_i64(self, keys: torch.Tensor, row0: int, nparts: int):
+        """The multi-GPU join's exchange step (nut_hash_partition_i64): keys and their row
+        ids (row0 + index) grouped by part = dist.join_owner(key, nparts).  Returns
+        (keys, rows, per-part counts)."""
+        if keys.dtype != torch.int64:
+            raise TypeError("hash_partition_i64 takes an int64 column")
+        n = keys.numel()
+        ok = torch.empty(max(n, 1), dtype=torch.int64, device=self.device)
+        orow = torch.empty(max(n, 1), dtype=torch.int64, device=self.device)
+        counts = (C.c_uint64 * nparts)()
+        self._bind_stream()
+        check(lib.nut_hash_partition_i64(self.ctx, C.c_void_p(_col(keys, self.device) if n else None), n, nparts,
+                                         row0, C.c_void_p(ok.data_ptr()), C.c_void_p(orow.data_ptr()), counts),
+              "nut_hash_partition_i64")
+        return ok[:n], orow[:n], [int(c) for c in counts]
+
     # ---------------------------------------------------------------- SQL
     def sql(self, query: str, columns: dict, group_hint: int = 0, right: Optional[dict] = None) -> dict:
         """Parse + lower `query` (nut_sql_plan) and run it on `columns` = {name: CUDA

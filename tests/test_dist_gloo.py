@@ -126,6 +126,73 @@ def _sort_worker(rank, world, port, n, kind, q):
         dist.destroy_process_group()
 
 
+# ---------------------------------------------------------------------------- hash join
+def _np_hash_partition(keys, row0, P):
+    """stands in for nut_hash_partition_i64: (keys, row0 + row, counts) grouped by join_owner"""
+    from nutdb_amd.dist import join_owner
+    k = keys.numpy()
+    o = join_owner(k, P)
+    order = np.argsort(o, kind="stable")
+    rows = np.arange(len(k), dtype=np.int64) + row0
+    return (torch.from_numpy(np.ascontiguousarray(k[order])), torch.from_numpy(rows[order]),
+            [int(c) for c in np.bincount(o, minlength=P)])
+
+
+def _join_tables(world, nb, npr, rank):
+    """rank's build / probe shards of one global pair of tables (keys with repeats)"""
+    rng = np.random.default_rng(77)
+    b = rng.integers(0, nb // 2, nb).astype(np.int64) * 3
+    p = rng.integers(-20, nb * 2, npr).astype(np.int64)
+    bs, ps = np.array_split(b, world), np.array_split(p, world)
+    b0 = sum(len(x) for x in bs[:rank])
+    p0 = sum(len(x) for x in ps[:rank])
+    return b, p, bs[rank], ps[rank], b0, p0
+
+
+def _join_worker(rank, world, port, nb, npr, how, q):
+    sys.path.insert(0, str(ROOT))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    from oracle import oracle as orc
+    from nutdb_amd.dist import distributed_join, gather_groups, join_owner
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        _, _, bs, ps, b0, p0 = _join_tables(world, nb, npr, rank)
+
+        def local_join(bk, pk, how_):
+            # every received key is owned by this rank
+            assert np.all(join_owner(bk.numpy(), world) == rank) and np.all(join_owner(pk.numpy(), world) == rank)
+            pi, bi = orc.join_i64(bk.numpy(), pk.numpy(), how_)
+            return torch.from_numpy(pi), torch.from_numpy(bi)
+
+        gp, gb = distributed_join(torch.from_numpy(bs), torch.from_numpy(ps), _np_hash_partition, local_join,
+                                  how, b0, p0)
+        allg = gather_groups(torch.stack([gp, gb]))
+        if rank == 0:
+            q.put(allg.numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,how", [(2, "inner"), (3, "inner"), (2, "left"), (3, "semi"), (2, "anti")])
+def test_distributed_join(world, how, orc):
+    nb, npr = 20_000, 60_001
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_join_worker, args=(r, world, port, nb, npr, how, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    b, p, *_ = _join_tables(world, nb, npr, 0)
+    wp, wb = orc.join_i64(b, p, how)
+    o = np.lexsort((got[1], got[0]))
+    assert np.array_equal(got[0][o], wp) and np.array_equal(got[1][o], wb)
+
+
 @pytest.mark.parametrize("world,kind", [(2, 1), (3, 1), (2, 5)])
 def test_sample_sort(world, kind, orc):
     n = 300_000 - (300_000 % world)

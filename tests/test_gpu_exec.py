@@ -395,6 +395,59 @@ def test_sample_sort_virtual_ranks(ex, orc):
     assert all(o[-1] <= out[i + 1][0] for i, o in enumerate(out[:-1]) if len(o) and len(out[i + 1]))
 
 
+@pytest.mark.parametrize("P", [1, 2, 3, 8, 256])
+def test_hash_partition_i64(ex, P):
+    """nut_hash_partition_i64 against the host owner function: every part holds exactly the
+    rows whose key maps to it (keys with their row ids), parts in order."""
+    from nutdb_amd.dist import join_owner
+    rng = np.random.default_rng(P)
+    n = 700_001
+    keys = rng.integers(I64_MIN, I64_MAX, n, dtype=np.int64)
+    keys[:4] = [I64_MIN, I64_MAX, 0, -1]
+    k, r, counts = ex.hash_partition_i64(dev(keys, ex), 1000, P)
+    k, r = host(k), host(r)
+    own = join_owner(keys, P)
+    assert counts == [int(c) for c in np.bincount(own, minlength=P)]
+    assert np.array_equal(np.sort(r), np.arange(n) + 1000)
+    assert np.array_equal(keys[r - 1000], k)
+    off = 0
+    for p, c in enumerate(counts):
+        assert np.all(own[r[off:off + c] - 1000] == p)
+        off += c
+
+
+def test_join_virtual_ranks(ex, orc):
+    """The multi-GPU join's data path with P virtual ranks on one GPU: both sides' shards
+    hash-partitioned on the device, part p of every shard joined on 'rank' p; the union of
+    the per-rank pairs (global rows) is the single-GPU join."""
+    P = 4
+    rng = np.random.default_rng(8)
+    b = rng.integers(0, 400_000, 500_000).astype(np.int64)
+    p = rng.integers(-1000, 500_000, 2_000_003).astype(np.int64)
+    recv = [[[], [], [], []] for _ in range(P)]  # per rank: build keys, build rows, probe keys, probe rows
+    for side, arr in ((0, b), (2, p)):
+        off = 0
+        for s in np.array_split(arr, P):
+            k, r, counts = ex.hash_partition_i64(dev(s, ex), off, P)
+            o = 0
+            for q, c in enumerate(counts):
+                recv[q][side].append(k[o:o + c])
+                recv[q][side + 1].append(r[o:o + c])
+                o += c
+            off += len(s)
+    for how in ("inner", "left", "anti"):
+        gps, gbs = [], []
+        for q in range(P):
+            bk, br, pk, pr = (torch.cat(x) for x in recv[q])
+            pi, bi = ex.join_i64(bk, pk, how)
+            gps.append(host(pr[pi]))
+            gbs.append(np.where(host(bi) >= 0, host(br)[np.maximum(host(bi), 0)], -1))
+        gp, gb = np.concatenate(gps), np.concatenate(gbs)
+        o = np.lexsort((gb, gp))
+        wp, wb = orc.join_i64(b, p, how)
+        assert np.array_equal(gp[o], wp) and np.array_equal(gb[o], wb), how
+
+
 @pytest.mark.parametrize("n", [40_000, 5_000_003])
 def test_sort_desc_msd(ex, orc, n):
     """Descending MSD sort: duplicates, extremes and a block of equal keys."""
