@@ -479,7 +479,7 @@ uint32_t gp_tiles(std::vector<GpSeg> &segs, uint32_t tile, std::vector<uint32_t>
 // [start, end) pairs are appended to *parts
 nut_status gp_level(nut_ctx *c, GpMeta &mm, std::vector<GpSeg> &segs, int shift, const uint64_t *const *src,
                     uint64_t *const *dst, int narr, bool gather, bool have_hist, std::vector<uint64_t> &hist,
-                    std::vector<uint64_t> *parts = nullptr) {
+                    std::vector<uint64_t> *parts = nullptr, uint64_t kx = 0) {
   hipStream_t st = c->stream;
   std::vector<uint32_t> ts;
   nut_status s;
@@ -495,7 +495,7 @@ nut_status gp_level(nut_ctx *c, GpMeta &mm, std::vector<GpSeg> &segs, int shift,
     unsigned long long *dh = (unsigned long long *)mm.alloc(hb);
     NUT_HIP(hipMemsetAsync(dh, 0, hb, st));
     if (nht) hipLaunchKernelGGL(gp_hist_kernel, dim3(nht), dim3(GP_HTHREADS), 0, st, src[1], src[2],
-                                (const GpSeg *)dseg, (const uint32_t *)dts, shift, gather ? 1 : 0, dh);
+                                (const GpSeg *)dseg, (const uint32_t *)dts, shift, gather ? 1 : 0, dh, kx);
     NUT_HIP(hipGetLastError());
     hist.resize(nh * GP_BINS);
     NUT_HIP(hipMemcpyAsync(hist.data(), dh, hb, hipMemcpyDeviceToHost, st));
@@ -533,7 +533,7 @@ nut_status gp_level(nut_ctx *c, GpMeta &mm, std::vector<GpSeg> &segs, int shift,
   }
   ar.narr = narr;
   if (nst) hipLaunchKernelGGL(gp_scatter_kernel, dim3(nst), dim3(GP_THREADS), 0, st, ar, (const GpSeg *)dseg,
-                              (const uint32_t *)dts, shift, gather ? 1 : 0, (unsigned long long *)dcur);
+                              (const uint32_t *)dts, shift, gather ? 1 : 0, (unsigned long long *)dcur, kx);
   NUT_HIP(hipGetLastError());
   return NUT_OK;
 }
@@ -931,6 +931,45 @@ nut_status nut_hash_partition_i64(nut_ctx *c, const int64_t *keys, uint64_t n, i
   (void)hipFreeAsync(rows, st);
   return e;
 }
+
+}  // extern "C"
+
+namespace nut {
+// The join's region build (join.hip): (key, row) records of `keys` partitioned by the top
+// 16 bits of owner_hash(key ^ kx) — two gp_levels, 8 bits each — into outk / outr; tmpk /
+// tmpr hold the first level.  counts[65536] = records per 16-bit partition, in order.
+nut_status hash_partition16(nut_ctx *c, const int64_t *keys, uint64_t n, uint64_t kx, int64_t *tmpk, int64_t *tmpr,
+                            int64_t *outk, int64_t *outr, std::vector<uint64_t> &counts) {
+  hipStream_t st = c->stream;
+  counts.assign(65536, 0);
+  if (n == 0) return NUT_OK;
+  // row ids: staged in outr, partitioned into tmpr by level 1, into outr by level 2
+  const unsigned g = (unsigned)std::min<uint64_t>((n + 255) / 256, (uint64_t)c->num_cus * 16);
+  hipLaunchKernelGGL(iota_kernel, dim3(g), dim3(256), 0, st, outr, n, (int64_t)0);
+  const uint64_t *s1[GP_MAX_ARR] = {nullptr, (const uint64_t *)keys, nullptr, (const uint64_t *)outr};
+  uint64_t *d1[GP_MAX_ARR] = {nullptr, (uint64_t *)tmpk, nullptr, (uint64_t *)tmpr};
+  std::vector<GpSeg> segs{GpSeg{0, n, 0, 0}};
+  std::vector<uint64_t> h1;
+  GpMeta mm{c};
+  nut_status e = gp_level(c, mm, segs, 56, s1, d1, 4, false, false, h1, nullptr, kx);
+  if (e) return e;
+  std::vector<GpSeg> s2;
+  uint64_t run = 0;
+  for (int d = 0; d < GP_BINS; ++d) {
+    s2.push_back(GpSeg{run, h1[d], 0, 0});  // empty segments too: one histogram row per digit
+    run += h1[d];
+  }
+  const uint64_t *src2[GP_MAX_ARR] = {nullptr, (const uint64_t *)tmpk, nullptr, (const uint64_t *)tmpr};
+  uint64_t *d2[GP_MAX_ARR] = {nullptr, (uint64_t *)outk, nullptr, (uint64_t *)outr};
+  std::vector<uint64_t> h2;
+  e = gp_level(c, mm, s2, 48, src2, d2, 4, false, false, h2, nullptr, kx);
+  if (e) return e;
+  for (size_t i = 0; i < 65536; ++i) counts[i] = h2[i];
+  return NUT_OK;
+}
+}  // namespace nut
+
+extern "C" {
 
 nut_status nut_groups_to_host(nut_groups *g, int64_t *keys, uint64_t *aggs, uint64_t cap) {
   if (!g) return fail(NUT_ERR_INVALID_ARG, "nut_groups_to_host: NULL argument");

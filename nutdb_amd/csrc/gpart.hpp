@@ -35,9 +35,12 @@ struct GpArrays {
   int narr;
 };
 
-// the partition digit: a byte of the key tuple's owner hash (recomputed, never stored)
-__device__ __forceinline__ uint32_t gp_digit(const uint64_t *k1, const uint64_t *k2, uint64_t i, int shift) {
-  return (uint32_t)(owner_hash(k1[i], k2 ? k2[i] : 0, k2 ? 2 : 1) >> shift) & 255u;
+// the partition digit: a byte of the key tuple's owner hash (recomputed, never stored);
+// kx (0 for the aggregation) re-keys the hash: the join table's home hash is
+// owner_hash(k ^ kx) with its own kx, independent of the multi-GPU owner (kx = 0)
+__device__ __forceinline__ uint32_t gp_digit(const uint64_t *k1, const uint64_t *k2, uint64_t i, int shift,
+                                             uint64_t kx) {
+  return (uint32_t)(owner_hash(k1[i] ^ kx, k2 ? k2[i] : 0, k2 ? 2 : 1) >> shift) & 255u;
 }
 
 // 256-bin histogram of (hash >> shift) & 255 per segment (gather: one for all segments)
@@ -45,7 +48,8 @@ __global__ __launch_bounds__(GP_HTHREADS) void gp_hist_kernel(const uint64_t *__
                                                               const uint64_t *__restrict__ k2,
                                                               const GpSeg *__restrict__ segs,
                                                               const uint32_t *__restrict__ tile_seg, int shift,
-                                                              int gather, unsigned long long *__restrict__ hist) {
+                                                              int gather, unsigned long long *__restrict__ hist,
+                                                              uint64_t kx) {
   __shared__ uint32_t cnt[GP_BINS];
   const int tid = threadIdx.x;
   cnt[tid] = 0;
@@ -59,7 +63,7 @@ __global__ __launch_bounds__(GP_HTHREADS) void gp_hist_kernel(const uint64_t *__
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const uint32_t k = i + j * GP_HTHREADS;
-      d[j] = k < n ? gp_digit(k1, k2, lo + k, shift) : 0;
+      d[j] = k < n ? gp_digit(k1, k2, lo + k, shift, kx) : 0;
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j)
@@ -77,7 +81,8 @@ __global__ __launch_bounds__(GP_HTHREADS) void gp_hist_kernel(const uint64_t *__
 // one compact partitioned array).
 __global__ __launch_bounds__(GP_THREADS) void gp_scatter_kernel(GpArrays ar, const GpSeg *__restrict__ segs,
                                                                 const uint32_t *__restrict__ tile_seg, int shift,
-                                                                int gather, unsigned long long *__restrict__ cursor) {
+                                                                int gather, unsigned long long *__restrict__ cursor,
+                                                                uint64_t kx) {
   __shared__ uint64_t s_stage[GP_TILE];
   __shared__ uint8_t s_dig[GP_TILE];
   __shared__ uint32_t s_cnt[GP_BINS];
@@ -95,7 +100,7 @@ __global__ __launch_bounds__(GP_THREADS) void gp_scatter_kernel(GpArrays ar, con
 #pragma unroll
   for (int i = 0; i < GP_ITEMS; ++i) {
     const uint32_t idx = (uint32_t)i * GP_THREADS + tid;
-    d[i] = idx < n ? gp_digit(ar.src[1], ar.src[2], lo + idx, shift) : 0u;
+    d[i] = idx < n ? gp_digit(ar.src[1], ar.src[2], lo + idx, shift, kx) : 0u;
     slot[i] = idx < n ? atomicAdd(&s_cnt[d[i]], 1u) : 0u;
   }
   __syncthreads();

@@ -35,6 +35,7 @@
 
 #include "common.hpp"
 #include "lookback.hpp"
+#include "sort.hpp"
 
 namespace nut {
 
@@ -42,12 +43,20 @@ constexpr uint64_t HJ_EMPTY = ~0ull;
 
 struct HjTable {
   i64x2 *slot;  // .x key, .y build row (-1: empty)
-  uint64_t mask;
-  int shift;  // 64 - log2(capacity)
+  uint64_t wmask;  // runs wrap inside aligned blocks of wmask + 1 slots (a region, or the table)
+  int shift;       // 64 - log2(capacity)
 };
 
+// home hash = mix64(key ^ 0x3C6EF372FE94F82A), written as the group-by's owner hash of a
+// re-keyed key so the partition kernels (gpart.hpp, kx) compute the same digits; it is
+// independent of the multi-GPU owner (owner_hash of the key itself)
+constexpr uint64_t HJ_KX = 0x6A09E667F3BCC908ull ^ 0x3C6EF372FE94F82Aull;
+
 __device__ __forceinline__ uint64_t hj_home(int64_t k, const HjTable &t) {
-  return mix64((uint64_t)k ^ 0x3C6EF372FE94F82Aull) >> t.shift;
+  return owner_hash((uint64_t)k ^ HJ_KX, 0, 1) >> t.shift;
+}
+__device__ __forceinline__ uint64_t hj_next(uint64_t s, const HjTable &t) {
+  return (s & ~t.wmask) | ((s + 1) & t.wmask);
 }
 
 // Build and duplicate check: HJ_BITEMS rows per lane in flight (their slot atomics /
@@ -87,7 +96,7 @@ __global__ __launch_bounds__(256) void hj_build_kernel(const int64_t *__restrict
           reinterpret_cast<int64_t *>(&t.slot[s[j]])[0] = k[j];
           act &= ~(1u << j);
         } else {
-          s[j] = (s[j] + 1) & t.mask;
+          s[j] = hj_next(s[j], t);
         }
       }
     }
@@ -125,11 +134,60 @@ __global__ __launch_bounds__(256) void hj_dupcheck_kernel(const int64_t *__restr
         const bool mine = v[j].y == (int64_t)(i0 + j * stride);
         found = found || (!mine && v[j].x == k[j]);
         if (mine || v[j].x == k[j]) act &= ~(1u << j);
-        s[j] = (s[j] + 1) & t.mask;
+        s[j] = hj_next(s[j], t);
       }
     }
   }
   if (__any(found) && (threadIdx.x & (kWave - 1)) == 0) atomicOr(dup, 1u);
+}
+
+// Region build: the table is cut into regions of HJ_RS slots (128 KB); a region's build
+// rows arrive contiguous (hash_partition16 by the home hash's top bits), one workgroup
+// builds the region in LDS with LDS atomics — runs wrap inside the region — checks it for
+// duplicate keys, and writes it out whole (the table needs no memset).
+constexpr uint32_t HJ_RS = 8192;
+constexpr int HJ_RTHREADS = 1024;
+
+__global__ __launch_bounds__(HJ_RTHREADS) void hj_region_build_kernel(const int64_t *__restrict__ keys,
+                                                                      const int64_t *__restrict__ rows,
+                                                                      const uint64_t *__restrict__ region_off,
+                                                                      HjTable t, int64_t row_base,
+                                                                      uint32_t *__restrict__ dup) {
+  __shared__ int64_t s_key[HJ_RS];
+  __shared__ unsigned long long s_row[HJ_RS];
+  const int tid = threadIdx.x;
+  const uint64_t r = blockIdx.x;
+  for (uint32_t i = tid; i < HJ_RS; i += HJ_RTHREADS) s_row[i] = HJ_EMPTY;
+  __syncthreads();
+  const uint64_t lo = region_off[r], hi = region_off[r + 1];
+  for (uint64_t i = lo + tid; i < hi; i += HJ_RTHREADS) {
+    const int64_t k = keys[i];
+    const unsigned long long row = (unsigned long long)(rows[i] + row_base);
+    uint32_t s = (uint32_t)(hj_home(k, t) & (HJ_RS - 1));
+    for (;;) {  // the host checked that the region has empty slots
+      if (s_row[s] == HJ_EMPTY && atomicCAS(&s_row[s], HJ_EMPTY, row) == HJ_EMPTY) {
+        s_key[s] = k;
+        break;
+      }
+      s = (s + 1) & (HJ_RS - 1);
+    }
+  }
+  __syncthreads();
+  bool found = false;
+  for (uint64_t i = lo + tid; i < hi; i += HJ_RTHREADS) {
+    const int64_t k = keys[i];
+    const unsigned long long row = (unsigned long long)(rows[i] + row_base);
+    for (uint32_t s = (uint32_t)(hj_home(k, t) & (HJ_RS - 1));; s = (s + 1) & (HJ_RS - 1)) {
+      if (s_row[s] == row) break;
+      if (s_key[s] == k) {
+        found = true;
+        break;
+      }
+    }
+  }
+  if (__any(found) && (tid & (kWave - 1)) == 0) atomicOr(dup, 1u);
+  i64x2 *out = t.slot + r * HJ_RS;
+  for (uint32_t i = tid; i < HJ_RS; i += HJ_RTHREADS) out[i] = i64x2{s_key[i], (int64_t)s_row[i]};
 }
 
 // output pairs of one probe row with m matches
@@ -201,7 +259,7 @@ __global__ __launch_bounds__(HJ_THREADS) void hj_probe_kernel(HjTable t, const i
         ++m[i];
       }
       const bool more = occ && !(hit && stop_on_hit);
-      s[i] = more ? (uint32_t)((s[i] + 1) & t.mask) : s[i];
+      s[i] = more ? (uint32_t)hj_next(s[i], t) : s[i];
       act = more ? act : (act & ~(1u << i));
     }
   }
@@ -272,7 +330,7 @@ __global__ __launch_bounds__(HJ_THREADS) void hj_probe_kernel(HjTable t, const i
       out_b[pos] = (int64_t)first[i];
     } else {
       uint64_t q = hj_home(key[i], t);
-      for (i64x2 v = t.slot[q]; v.y != -1; q = (q + 1) & t.mask, v = t.slot[q])
+      for (i64x2 v = t.slot[q]; v.y != -1; q = hj_next(q, t), v = t.slot[q])
         if (v.x == key[i]) {
           out_p[pos] = (int64_t)r;
           out_b[pos++] = v.y;
@@ -367,8 +425,49 @@ nut_status join_build(nut_ctx *c, nut_join *j, const int64_t *build, uint64_t nb
   j->total = (unsigned long long *)(b + o_state + 8);
   j->status = (uint64_t *)(b + o_state + 16);
   j->dup = (uint32_t *)(b + o_dup);
-  NUT_HIP(hipMemsetAsync(b, 0xFF, cap * 16, st));
   NUT_HIP(hipMemsetAsync(j->dup, 0, 16, st));
+  // region build for tables of 2^22 .. 2^29 slots (regions of 8192 slots, one 16-bit
+  // partition), unless a region would be too full (many equal keys): then global CAS
+  static const bool region_on = [] {
+    const char *e = getenv("NUT_HJ_REGION");
+    return !(e && *e == '0');
+  }();
+  if (nb && region_on && log2c >= 22 && log2c <= 29) {
+    const int rb = log2c - 13;
+    const uint64_t nreg = 1ull << rb;
+    int64_t *tmp = nullptr;
+    NUT_HIP(hipMallocAsync((void **)&tmp, nb * 32, st));
+    std::vector<uint64_t> counts;
+    nut_status e = hash_partition16(c, build, nb, HJ_KX, tmp, tmp + nb, tmp + 2 * nb, tmp + 3 * nb, counts);
+    if (e) {
+      (void)hipFreeAsync(tmp, st);
+      return e;
+    }
+    std::vector<uint64_t> off(nreg + 1, 0);
+    uint64_t mx = 0;
+    for (uint64_t r = 0; r < nreg; ++r) {
+      uint64_t cnt = 0;
+      for (uint64_t q = r << (16 - rb); q < (r + 1) << (16 - rb); ++q) cnt += counts[q];
+      off[r + 1] = off[r] + cnt;
+      mx = std::max(mx, cnt);
+    }
+    if (mx <= HJ_RS * 7 / 8) {
+      uint64_t *doff = nullptr;
+      NUT_HIP(hipMallocAsync((void **)&doff, (nreg + 1) * 8, st));
+      NUT_HIP(hipMemcpyAsync(doff, off.data(), (nreg + 1) * 8, hipMemcpyHostToDevice, st));
+      j->t.wmask = HJ_RS - 1;
+      hipLaunchKernelGGL(hj_region_build_kernel, dim3((unsigned)nreg), dim3(HJ_RTHREADS), 0, st,
+                         (const int64_t *)(tmp + 2 * nb), (const int64_t *)(tmp + 3 * nb), (const uint64_t *)doff,
+                         j->t, (int64_t)0, j->dup);
+      NUT_HIP(hipGetLastError());
+      NUT_HIP(hipStreamSynchronize(st));  // `off` is host memory of this frame
+      (void)hipFreeAsync(doff, st);
+      (void)hipFreeAsync(tmp, st);
+      return NUT_OK;
+    }
+    (void)hipFreeAsync(tmp, st);
+  }
+  NUT_HIP(hipMemsetAsync(b, 0xFF, cap * 16, st));
   if (nb) {
     const unsigned g = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((nb + 255) / 256, c->num_cus * 16ull));
     hipLaunchKernelGGL(hj_build_kernel, dim3(g), dim3(256), 0, st, build, nb, j->t);

@@ -55,6 +55,24 @@ def test_join_two_pass_api(ex, orc, how):
     check(ex, orc, b, p, how, passes=2)
 
 
+@pytest.mark.parametrize("how", HOW)
+def test_join_region_build(ex, orc, how):
+    """> 2^20 build rows: the table is built region by region in LDS (hash_partition16 +
+    hj_region_build_kernel), with repeated keys (duplicate check inside the regions)."""
+    rng = np.random.default_rng(31)
+    b = rng.integers(0, 1_500_000, 2_100_000).astype(np.int64)
+    p = rng.integers(-100_000, 1_600_000, 3_000_001).astype(np.int64)
+    check(ex, orc, b, p, how)
+
+
+def test_join_region_overflow_falls_back(ex, orc):
+    """1.2e6 copies of one key cannot fit a 8192-slot region: the global CAS build runs."""
+    b = np.concatenate([np.full(1_200_000, 42, dtype=np.int64), np.arange(1_000_000, dtype=np.int64) * 5 + 7])
+    p = np.array([42, 7, 8, 42, 12, -1], dtype=np.int64)
+    check(ex, orc, b, p, "inner")
+    check(ex, orc, b, p, "semi")
+
+
 def test_join_long_runs(ex, orc):
     """Clustered hashes: 1000 copies of each of 3 keys build long probe runs; tiles mix
     rows with thousands of matches and rows with none."""
