@@ -320,8 +320,9 @@ struct nut_plan {
   // (nut_join_i64) then gathers into the joined table the rest of the plan runs on
   int join = -1;           // nut_join_type; -1: no JOIN
   bool jright = false;     // RIGHT OUTER / SEMI / ANTI: the JOIN source is the preserved side
-  std::string jtable;
+  std::string jtable, talias, jalias;  // JOIN source; FROM / JOIN aliases (qualifiers)
   int jkey[2] = {-1, -1};  // plan columns of the ON equality
+  std::deque<std::string> qnames;  // storage of qualified column names (column_ref)
 };
 
 struct nut_result {
@@ -345,9 +346,17 @@ int col_index(nut_plan &p, sv name) {
   return (int)p.cols.size() - 1;
 }
 
-bool column_ref(const Expr &e, sv &name) {
+// A column reference.  In a JOIN plan a qualified name keeps its qualifier ("o.custkey"):
+// exec_join binds it to the table named or aliased so (and `a.k = b.k` can join two
+// columns of the same name); elsewhere the qualifier is dropped.
+bool column_ref(nut_plan &p, const Expr &e, sv &name) {
   if (e.k != EK::Identifier || e.id.wildcard) return false;
-  name = e.id.name;
+  if (p.join >= 0 && e.id.qualified) {
+    p.qnames.push_back(std::string(e.id.qualifier) + "." + std::string(e.id.name));
+    name = p.qnames.back();
+  } else {
+    name = e.id.name;
+  }
   return true;
 }
 
@@ -410,14 +419,14 @@ bool lower_agg_expr(nut_plan &p, const Expr &e, PlanAgg &a, Lowering &L) {
     return (int)p.vals.size() - 1;
   };
   a.arg[0] = a.arg[1] = a.arg[2] = 0;
-  if (column_ref(e, n0)) {
+  if (column_ref(p, e, n0)) {
     a.expr = NUT_EX_COL;
     a.arg[0] = val(n0);
     return true;
   }
   if (e.k == EK::BinaryOp) {
     const Expr &l = e.kids[0], &r = e.kids[1];
-    if (column_ref(l, n0) && column_ref(r, n1)) {
+    if (column_ref(p, l, n0) && column_ref(p, r, n1)) {
       BinOp op = e.bop();
       if (op == BinOp::Multi || op == BinOp::Plus || op == BinOp::Minus) {
         a.expr = op == BinOp::Multi ? NUT_EX_MUL : op == BinOp::Plus ? NUT_EX_ADD : NUT_EX_SUB;
@@ -427,18 +436,18 @@ bool lower_agg_expr(nut_plan &p, const Expr &e, PlanAgg &a, Lowering &L) {
       }
     }
     // a * (1 - b)
-    if (e.bop() == BinOp::Multi && column_ref(l, n0) && r.k == EK::BinaryOp && r.bop() == BinOp::Minus &&
-        is_one(r.kids[0]) && column_ref(r.kids[1], n1)) {
+    if (e.bop() == BinOp::Multi && column_ref(p, l, n0) && r.k == EK::BinaryOp && r.bop() == BinOp::Minus &&
+        is_one(r.kids[0]) && column_ref(p, r.kids[1], n1)) {
       a.expr = NUT_EX_MUL_1M;
       a.arg[0] = val(n0);
       a.arg[1] = val(n1);
       return true;
     }
     // a * (1 - b) * (1 + c)
-    if (e.bop() == BinOp::Multi && l.k == EK::BinaryOp && l.bop() == BinOp::Multi && column_ref(l.kids[0], n0) &&
+    if (e.bop() == BinOp::Multi && l.k == EK::BinaryOp && l.bop() == BinOp::Multi && column_ref(p, l.kids[0], n0) &&
         l.kids[1].k == EK::BinaryOp && l.kids[1].bop() == BinOp::Minus && is_one(l.kids[1].kids[0]) &&
-        column_ref(l.kids[1].kids[1], n1) && r.k == EK::BinaryOp && r.bop() == BinOp::Plus && is_one(r.kids[0]) &&
-        column_ref(r.kids[1], n2)) {
+        column_ref(p, l.kids[1].kids[1], n1) && r.k == EK::BinaryOp && r.bop() == BinOp::Plus && is_one(r.kids[0]) &&
+        column_ref(p, r.kids[1], n2)) {
       a.expr = NUT_EX_MUL_1M_1P;
       a.arg[0] = val(n0);
       a.arg[1] = val(n1);
@@ -589,7 +598,9 @@ bool lower_prog(nut_plan &p, const Expr &e, PProg &o, Lowering &L) {
       if (e.id.wildcard) return L.fail("'*' is not a value");
       PNode n;
       n.op = NUT_P_COL;
-      n.col = col_index(p, e.id.name);
+      sv nm;
+      column_ref(p, e, nm);
+      n.col = col_index(p, nm);
       o.push_back(n);
       return true;
     }
@@ -759,16 +770,16 @@ bool lower_pred_term(nut_plan &p, const Expr &e, Lowering &L) {
   if (e.k == EK::BinaryOp && cmp_of(e.bop()) >= 0) {
     int op = cmp_of(e.bop());
     const Expr &l = e.kids[0], &r = e.kids[1];
-    if (column_ref(l, name) && const_eval(r, c, L)) {
+    if (column_ref(p, l, name) && const_eval(r, c, L)) {
       p.preds.push_back({col_index(p, name), op, c});
       return true;
     }
-    if (column_ref(r, name) && const_eval(l, c, L)) {
+    if (column_ref(p, r, name) && const_eval(l, c, L)) {
       p.preds.push_back({col_index(p, name), mirror(op), c});
       return true;
     }
   }
-  if (e.k == EK::BinaryOp && (e.bop() == BinOp::In || e.bop() == BinOp::NotIn) && column_ref(e.kids[0], name)) {
+  if (e.k == EK::BinaryOp && (e.bop() == BinOp::In || e.bop() == BinOp::NotIn) && column_ref(p, e.kids[0], name)) {
     // col [NOT] IN (c1, c2, ...): a tuple of constants, or one constant
     const Expr &r = e.kids[1];
     PlanPred pr{col_index(p, name), e.bop() == BinOp::In ? NUT_IN : NUT_NOT_IN, CVal{}, {}};
@@ -787,7 +798,7 @@ bool lower_pred_term(nut_plan &p, const Expr &e, Lowering &L) {
     p.preds.push_back(std::move(pr));
     return true;
   }
-  if (e.k == EK::FnCall && e.fn() == FnKind::Between && e.kids.size() == 3 && column_ref(e.kids[0], name)) {
+  if (e.k == EK::FnCall && e.fn() == FnKind::Between && e.kids.size() == 3 && column_ref(p, e.kids[0], name)) {
     CVal lo, hi;
     if (const_eval(e.kids[1], lo, L) && const_eval(e.kids[2], hi, L)) {
       int ci = col_index(p, name);
@@ -808,7 +819,7 @@ bool lower_where(nut_plan &p, const Expr &e, Lowering &L) {
 // one SELECT-list item of an aggregate plan: a GROUP BY key or sum/count/min/max/avg
 bool lower_output(nut_plan &p, const Expr &e, PlanOut &o, Lowering &L) {
   sv name;
-  if (column_ref(e, name)) {
+  if (column_ref(p, e, name)) {
     int c = col_index(p, name), j = -1;
     for (size_t i = 0; i < p.keys.size(); ++i)
       if (p.keys[i] == c) j = (int)i;
@@ -973,10 +984,6 @@ bool lower_mode(const Statement &st, nut_plan &p, Lowering &L) {
     if (jc.src.k != SourceKind::Table) return L.fail("JOIN source must be a table");
     if (!jc.on) return L.fail("JOIN ... USING is not executed (ON a = b)");
     const Expr &cnd = jc.cond;
-    sv ka, kb;
-    if (!(cnd.k == EK::BinaryOp && cnd.bop() == BinOp::Eq && column_ref(cnd.kids[0], ka) &&
-          column_ref(cnd.kids[1], kb)))
-      return L.fail("JOIN ON must be one equality of two columns");
     switch (jc.t) {
       case JoinType::Inner: p.join = NUT_JOIN_INNER; break;
       case JoinType::LeftOuter: p.join = NUT_JOIN_LEFT; break;
@@ -987,7 +994,13 @@ bool lower_mode(const Statement &st, nut_plan &p, Lowering &L) {
       case JoinType::RightAnti: p.join = NUT_JOIN_ANTI, p.jright = true; break;
       default: return L.fail("FULL OUTER and ASOF JOIN are not executed");
     }
+    sv ka, kb;  // (p.join is set: qualified ON columns keep their qualifier)
+    if (!(cnd.k == EK::BinaryOp && cnd.bop() == BinOp::Eq && column_ref(p, cnd.kids[0], ka) &&
+          column_ref(p, cnd.kids[1], kb)))
+      return L.fail("JOIN ON must be one equality of two columns");
     p.jtable = std::string(jc.src.table);
+    if (jc.src.alias) p.jalias = std::string(*jc.src.alias);
+    if (b.from && b.from->alias) p.talias = std::string(*b.from->alias);
     p.jkey[0] = col_index(p, ka);
     p.jkey[1] = col_index(p, kb);
   }
@@ -1020,7 +1033,7 @@ bool lower_mode(const Statement &st, nut_plan &p, Lowering &L) {
     if (b.group_by) {
       for (const QueryExpr &k : *b.group_by) {
         sv name;
-        if (!column_ref(k.e, name)) return L.fail("GROUP BY keys must be columns");
+        if (!column_ref(p, k.e, name)) return L.fail("GROUP BY keys must be columns");
         p.keys.push_back(col_index(p, name));
       }
       if (p.keys.empty() || p.keys.size() > NUT_MAX_KEYS) return L.fail("GROUP BY takes 1 or 2 key columns");
@@ -1046,7 +1059,7 @@ bool lower_mode(const Statement &st, nut_plan &p, Lowering &L) {
         for (size_t i = 0; i < p.outs.size() && idx < 0; ++i) {
           const PlanOut &o = p.outs[i];
           if (!o.hidden && (ieq(o.name, text) || ieq(o.text, text))) idx = (int)i;
-          if (idx < 0 && !o.hidden && column_ref(k.e.e, name) && o.kind == OUT_KEY && ieq(p.cols[p.keys[o.a]], name))
+          if (idx < 0 && !o.hidden && column_ref(p, k.e.e, name) && o.kind == OUT_KEY && ieq(p.cols[p.keys[o.a]], name))
             idx = (int)i;
         }
         if (idx < 0 && !having_output(p, k.e.e, idx, L))
@@ -1063,7 +1076,7 @@ bool lower_mode(const Statement &st, nut_plan &p, Lowering &L) {
 
   // no GROUP BY, no aggregate: one projected column
   sv name;
-  if (b.columns.size() != 1 || !column_ref(b.columns[0].e, name))
+  if (b.columns.size() != 1 || !column_ref(p, b.columns[0].e, name))
     return L.fail("a plan without GROUP BY projects exactly one column");
   p.proj = col_index(p, name);
   PlanOut o;
@@ -1079,7 +1092,7 @@ bool lower_mode(const Statement &st, nut_plan &p, Lowering &L) {
     if (b.order_by->size() != 1) return L.fail("ORDER BY takes one key");
     const OrderKey &k = (*b.order_by)[0];
     sv oname;
-    if (!column_ref(k.e.e, oname) || !(ieq(oname, p.cols[p.proj]) || ieq(oname, p.outs[0].name)))
+    if (!column_ref(p, k.e.e, oname) || !(ieq(oname, p.cols[p.proj]) || ieq(oname, p.outs[0].name)))
       return L.fail("ORDER BY must name the projected column");
     p.kind = NUT_PLAN_SORT;
     p.desc = k.desc;
@@ -1251,6 +1264,11 @@ std::string describe(const nut_plan &p) {
     o += p.jright ? "\",\"right\":true" : "\",\"right\":false";
     o += ",\"table\":";
     json_str(o, p.jtable);
+    o += ",\"aliases\":[";
+    json_str(o, p.talias);
+    o += ',';
+    json_str(o, p.jalias);
+    o += ']';
     o += ",\"on\":[";
     json_str(o, p.cols[p.jkey[0]]);
     o += ',';
@@ -1788,10 +1806,28 @@ nut_status exec_join(nut_ctx *c, const nut_plan &p, const nut_column *lc, int nl
   const size_t nc = p.cols.size();
   std::vector<int> side(nc);
   std::vector<const nut_column *> src(nc);
+  auto find = [](const std::string &name, const nut_column *cols, int n) -> const nut_column * {
+    for (int i = 0; i < n; ++i)
+      if (cols[i].name && ieq(cols[i].name, name)) return &cols[i];
+    return nullptr;
+  };
+  auto names = [](const std::string &q, const std::string &t, const std::string &a) {
+    return ieq(q, t) || (!a.empty() && ieq(q, a));
+  };
   for (size_t i = 0; i < nc; ++i) {
-    const nut_column *a = bind(p, (int)i, lc, nl), *b = bind(p, (int)i, rc, nr);
-    if (a && b) return fail(NUT_ERR_INVALID_ARG, "nut_plan_execute2: column '" + p.cols[i] + "' is in both tables");
-    if (!a && !b) return fail(NUT_ERR_INVALID_ARG, "nut_plan_execute2: column '" + p.cols[i] + "' is not bound");
+    const std::string &nm = p.cols[i];
+    const nut_column *a = find(nm, lc, nl), *b = find(nm, rc, nr);
+    const size_t dot = nm.find('.');
+    if (!a && !b && dot != std::string::npos) {  // qualified: table name or alias picks the side
+      const std::string q = nm.substr(0, dot), c = nm.substr(dot + 1);
+      const bool l = names(q, p.table, p.talias), r = names(q, p.jtable, p.jalias);
+      if (l && r) return fail(NUT_ERR_PLAN, "qualifier '" + q + "' names both tables (use aliases)");
+      if (!l && !r) return fail(NUT_ERR_PLAN, "qualifier '" + q + "' names neither joined table");
+      if (l) a = find(c, lc, nl);
+      else b = find(c, rc, nr);
+    }
+    if (a && b) return fail(NUT_ERR_INVALID_ARG, "nut_plan_execute2: column '" + nm + "' is in both tables");
+    if (!a && !b) return fail(NUT_ERR_INVALID_ARG, "nut_plan_execute2: column '" + nm + "' is not bound");
     side[i] = a ? 0 : 1;
     src[i] = a ? a : b;
     if (src[i]->type != NUT_T_I64 && src[i]->type != NUT_T_F64)

@@ -231,7 +231,8 @@ class Plan:
             nb = name.encode()
             keep.append(nb)
             arr[i] = NutColumn(nb, t.data_ptr(), typ)
-            if any(name.lower() == c.lower() for c in names):
+            low = name.lower()
+            if any(low == c.lower() or c.lower().endswith("." + low) for c in names):  # JOIN plans qualify
                 n = t.numel() if n is None else n
                 if t.numel() != n:
                     raise ValueError("bound columns differ in length")

@@ -264,3 +264,24 @@ def test_sql_inner_join_large(ex, orc):
     g = j.groupby("o_cust").agg(c=("l_qty", "size"), q=("l_qty", "sum"))
     assert got["o_cust"].tolist() == g.index.tolist()
     assert got["c"].tolist() == g.c.tolist() and got["q"].tolist() == g.q.tolist()
+
+
+def test_sql_join_qualified_same_name_keys(ex, orc):
+    """`ON o.okey = l.okey`: both tables name their key `okey`; qualifiers (table names or
+    AS aliases) pick the table, unqualified names must be unique across the two."""
+    orders, lines = tables(7, 30_000, 90_000)
+    o = {"okey": dev(orders["o_okey"], ex), "cust": dev(orders["o_cust"], ex)}
+    li = {"okey": dev(lines["l_okey"], ex), "qty": dev(lines["l_qty"], ex)}
+    j = joined(orc, lines, "l_okey", orders, "o_okey", "inner")
+    g = j.groupby("o_cust").agg(c=("l_qty", "size"), q=("l_qty", "sum"))
+    for sql in ["select cust, count(*) as c, sum(qty) as q from lineitem as l join orders as o "
+                "on l.okey = o.okey group by cust order by cust",
+                "select o.cust, count(*) as c, sum(lineitem.qty) as q from lineitem join orders as o "
+                "on lineitem.okey = o.okey group by o.cust order by o.cust"]:
+        got = ex.sql(sql, li, right=o)
+        assert list(got.values())[0].tolist() == g.index.tolist()
+        assert got["c"].tolist() == g.c.tolist() and got["q"].tolist() == g.q.tolist()
+    with pytest.raises(NutError, match="names neither"):
+        ex.sql("select count(*) from lineitem as l join orders as o on x.okey = o.okey", li, right=o)
+    with pytest.raises(NutError, match="in both tables"):
+        ex.sql("select count(*) from lineitem as l join orders as o on okey = o.okey", li, right=o)

@@ -104,3 +104,12 @@ def test_c_join_oracle_matches_numpy(how, nb, npr):
     assert np.all(c[0][1:] >= c[0][:-1])
     o = np.lexsort((c[1], c[0]))
     assert np.array_equal(a[0], c[0][o]) and np.array_equal(a[1], c[1][o])
+
+
+def test_sql_join_qualified_names():
+    from nutdb_amd.sql import Plan
+    d = Plan("select o.cust, count(*) from orders as o join lineitem as l on o.okey = l.okey "
+             "group by o.cust").describe()
+    assert d["join"]["on"] == ["o.okey", "l.okey"] and d["keys"] == ["o.cust"]
+    # without a JOIN the qualifier is dropped, as before
+    assert Plan("select t.a from t where t.a > 3").describe()["columns"] == ["a"]
