@@ -58,7 +58,8 @@ JQ = "select o_cust, count(*) as c, sum(l_qty) as s from orders {} lineitem on o
 def test_sql_join_lowering(kw, typ, right, mode):
     from nutdb_amd.sql import Plan
     d = Plan(JQ.format(kw)).describe()
-    assert d["join"] == {"type": typ, "right": right, "table": "lineitem", "on": ["o_okey", "l_okey"]}
+    assert d["join"] == {"type": typ, "right": right, "table": "lineitem", "aliases": ["", ""],
+                         "on": ["o_okey", "l_okey"]}
     assert d["table"] == "orders" and d["mode"] == mode  # outer joins mask aggregates: expression mode
     assert set(d["columns"]) == {"o_okey", "l_okey", "o_cust", "l_qty"}
 
