@@ -470,6 +470,11 @@ nut_status nut_table_append(nut_ctx *ctx, nut_table *t, int j, const void *data,
 /* Execute a plan against the table (binds every plan column by name). */
 nut_status nut_table_execute(nut_ctx *ctx, nut_table *t, const nut_plan *plan, uint64_t group_hint,
                              nut_result **out);
+/* A JOIN plan over two typed tables (left = FROM, right = JOIN source; nut_plan_execute2
+ * semantics).  String columns travel through the join as codes of their own table's
+ * dictionary and decode on output; JOIN keys must be integer columns. */
+nut_status nut_table_execute2(nut_ctx *ctx, nut_table *left, nut_table *right, const nut_plan *plan,
+                              uint64_t group_hint, nut_result **out);
 void nut_table_free(nut_table *t);
 
 #ifdef __cplusplus

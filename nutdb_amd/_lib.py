@@ -149,6 +149,7 @@ SIGNATURES = {
                                      C.POINTER(_I32)]),
     "nut_table_append": (_I32, [_P, _P, _I32, _P, _P, _U64]),
     "nut_table_execute": (_I32, [_P, _P, _P, _U64, C.POINTER(_P)]),
+    "nut_table_execute2": (_I32, [_P, _P, _P, _P, _U64, C.POINTER(_P)]),
     "nut_table_free": (None, [_P]),
     "nut_groups_size": (_I32, [_P, C.POINTER(_U64)]),
     "nut_groups_to_host": (_I32, [_P, _P, _P, _U64]),

@@ -1801,11 +1801,14 @@ namespace {
 
 // A plan with a JOIN (nut_plan_execute2): hash join on the ON columns, gathers of every
 // plan column through the join index, then the plan's scan / group-by on the joined rows.
+// ldict / rdict (may be null): the dictionary of each column of lc / rc (typed tables)
 nut_status exec_join(nut_ctx *c, const nut_plan &p, const nut_column *lc, int nl, uint64_t lrows,
-                     const nut_column *rc, int nr, uint64_t rrows, uint64_t hint, nut_result *r) {
+                     const nut_column *rc, int nr, uint64_t rrows, uint64_t hint, nut_result *r,
+                     const Dict *const *ldict = nullptr, const Dict *const *rdict = nullptr) {
   const size_t nc = p.cols.size();
   std::vector<int> side(nc);
   std::vector<const nut_column *> src(nc);
+  std::vector<const Dict *> sdict(nc + 1, nullptr);
   auto find = [](const std::string &name, const nut_column *cols, int n) -> const nut_column * {
     for (int i = 0; i < n; ++i)
       if (cols[i].name && ieq(cols[i].name, name)) return &cols[i];
@@ -1830,6 +1833,7 @@ nut_status exec_join(nut_ctx *c, const nut_plan &p, const nut_column *lc, int nl
     if (!a && !b) return fail(NUT_ERR_INVALID_ARG, "nut_plan_execute2: column '" + nm + "' is not bound");
     side[i] = a ? 0 : 1;
     src[i] = a ? a : b;
+    sdict[i] = a ? (ldict ? ldict[a - lc] : nullptr) : (rdict ? rdict[b - rc] : nullptr);
     if (src[i]->type != NUT_T_I64 && src[i]->type != NUT_T_F64)
       return fail(NUT_ERR_INVALID_ARG, "nut_plan_execute2: column '" + p.cols[i] + "' has an unknown type");
     if ((a ? lrows : rrows) && !src[i]->data)
@@ -1839,6 +1843,8 @@ nut_status exec_join(nut_ctx *c, const nut_plan &p, const nut_column *lc, int nl
   if (side[k0] == side[k1]) return fail(NUT_ERR_PLAN, "JOIN ON must compare a column of each table");
   const nut_column *lkey = side[k0] == 0 ? src[k0] : src[k1], *rkey = side[k0] == 0 ? src[k1] : src[k0];
   if (lkey->type != NUT_T_I64 || rkey->type != NUT_T_I64) return fail(NUT_ERR_PLAN, "JOIN keys must be int64 columns");
+  if (sdict[k0] || sdict[k1])  // codes of two dictionaries do not compare
+    return fail(NUT_ERR_PLAN, "JOIN keys must be integer columns (string keys are not executed)");
   // INNER builds the smaller table; the outer / semi / anti joins preserve their side
   const int ps = p.join == NUT_JOIN_INNER ? (lrows >= rrows ? 0 : 1) : (p.jright ? 1 : 0);
   const nut_column *pk = ps == 0 ? lkey : rkey, *bk = ps == 0 ? rkey : lkey;
@@ -1927,9 +1933,9 @@ nut_status exec_join(nut_ctx *c, const nut_plan &p, const nut_column *lc, int nl
   }
   std::vector<const nut_column *> bound(p2.cols.size());
   for (size_t i = 0; i < p2.cols.size(); ++i) bound[i] = &jc[i];
-  const std::vector<const Dict *> nodict(p2.cols.size(), nullptr);
-  st = p2.kind == NUT_PLAN_GROUPBY ? exec_groupby(c, p2, bound.data(), nodict.data(), npairs, hint, r)
-                                   : exec_scan(c, p2, bound.data(), nodict.data(), npairs, r);
+  sdict.resize(p2.cols.size());
+  st = p2.kind == NUT_PLAN_GROUPBY ? exec_groupby(c, p2, bound.data(), sdict.data(), npairs, hint, r)
+                                   : exec_scan(c, p2, bound.data(), sdict.data(), npairs, r);
   NUT_HIP(hipStreamSynchronize(c->stream));  // the gathered columns are freed on return
   return st;
 }
@@ -2124,6 +2130,39 @@ nut_status nut_table_execute(nut_ctx *c, nut_table *t, const nut_plan *p, uint64
   DeviceGuard g(c->device);
   nut_status st = p->kind == NUT_PLAN_GROUPBY ? exec_groupby(c, *p, bound.data(), dicts.data(), nrows, group_hint, r)
                                               : exec_scan(c, *p, bound.data(), dicts.data(), nrows, r);
+  if (st) {
+    nut_result_free(r);
+    return st;
+  }
+  *out = r;
+  return NUT_OK;
+}
+
+nut_status nut_table_execute2(nut_ctx *c, nut_table *left, nut_table *right, const nut_plan *p, uint64_t group_hint,
+                              nut_result **out) {
+  if (!c || !left || !right || !p || !out) return fail(NUT_ERR_INVALID_ARG, "nut_table_execute2: NULL argument");
+  if (p->join < 0) return nut_table_execute(c, left, p, group_hint, out);
+  *out = nullptr;
+  std::vector<nut_column> cols[2];
+  std::vector<const Dict *> dicts[2];
+  nut_table *t2[2] = {left, right};
+  for (int k = 0; k < 2; ++k) {
+    nut_table *t = t2[k];
+    if (t->ragged()) return fail(NUT_ERR_INVALID_ARG, "nut_table_execute2: table '" + t->name + "' has ragged columns");
+    if (t->device >= 0 && t->device != c->device)
+      return fail(NUT_ERR_INVALID_ARG, "nut_table_execute2: table '" + t->name + "' lives on another device");
+    for (const TCol &x : t->cols) {
+      cols[k].push_back(nut_column{x.name.c_str(), x.dev, x.exec_type});
+      dicts[k].push_back(x.dict);
+    }
+  }
+  nut_result *r = new (std::nothrow) nut_result;
+  if (!r) return fail(NUT_ERR_OOM, "nut_table_execute2: out of host memory");
+  r->kind = p->kind;
+  r->device = c->device;
+  DeviceGuard g(c->device);
+  nut_status st = exec_join(c, *p, cols[0].data(), (int)cols[0].size(), left->rows(), cols[1].data(),
+                            (int)cols[1].size(), right->rows(), group_hint, r, dicts[0].data(), dicts[1].data());
   if (st) {
     nut_result_free(r);
     return st;

@@ -79,7 +79,18 @@ class Table:
               "nut_table_execute")
         return read_result(res)
 
-    def sql(self, query: str, group_hint: int = 0) -> Dict[str, np.ndarray]:
+    def execute_join(self, plan: Plan, right: "Table", group_hint: int = 0) -> Dict[str, np.ndarray]:
+        """A JOIN plan with this table as the FROM side and `right` as the JOIN source
+        (nut_table_execute2): string columns carry their own dictionaries through the join."""
+        res = C.c_void_p()
+        self.ex._bind_stream()
+        check(lib.nut_table_execute2(self.ex.ctx, self._h, right._h, plan._handle(), group_hint, C.byref(res)),
+              "nut_table_execute2")
+        return read_result(res)
+
+    def sql(self, query: str, group_hint: int = 0, right: "Table" = None) -> Dict[str, np.ndarray]:
+        if right is not None:
+            return self.execute_join(Plan(query), right, group_hint)
         return self.execute(Plan(query), group_hint)
 
     def free(self) -> None:

@@ -160,3 +160,48 @@ def test_enum_values(ex):
     with pytest.raises(NutError) as err:
         t.append(s=["mid"])
     assert "not a value of its Enum" in str(err.value)
+
+
+def test_tpch_q12_join_two_typed_tables(ex):
+    """TPC-H Q12 as written (orders JOIN lineitem ON o_orderkey = l_orderkey) over two
+    typed tables: string predicates on both sides, CASE over the other table's strings,
+    string group keys decoded from their own table's dictionary (nut_table_execute2)."""
+    rng = np.random.default_rng(12)
+    no, nl = 50_000, 200_003
+    prios = np.array(["1-URGENT", "2-HIGH", "3-MEDIUM", "4-NOT SPECIFIED", "5-LOW"], dtype=object)
+    modes = np.array(["MAIL", "SHIP", "AIR", "RAIL", "TRUCK", "FOB", "REG AIR"], dtype=object)
+    okey = rng.permutation(no).astype(np.int64) * 4 + 1
+    prio = prios[rng.integers(0, len(prios), no)]
+    lkey = np.where(rng.random(nl) < 0.9, okey[rng.integers(0, no, nl)], 2).astype(np.int64)
+    mode = modes[rng.integers(0, len(modes), nl)]
+    ship = rng.integers(8000, 10000, nl)
+    commit = ship + rng.integers(-30, 30, nl)
+    receipt = ship + rng.integers(-30, 30, nl)
+    orders = Table(ex, "CREATE TABLE orders (o_orderkey Int64, o_orderpriority String)")
+    orders.append(o_orderkey=okey, o_orderpriority=prio)
+    lineitem = Table(ex, """CREATE TABLE lineitem (l_orderkey Int64, l_shipmode Dictionary(String),
+        l_shipdate Date, l_commitdate Date, l_receiptdate Date)""")
+    lineitem.append(l_orderkey=lkey, l_shipmode=mode, l_shipdate=ship, l_commitdate=commit, l_receiptdate=receipt)
+    sql = """select l_shipmode,
+        sum(case when o_orderpriority = '1-URGENT' or o_orderpriority = '2-HIGH' then 1 else 0 end) as high_line_count,
+        sum(case when o_orderpriority <> '1-URGENT' and o_orderpriority <> '2-HIGH' then 1 else 0 end)
+          as low_line_count
+      from orders join lineitem on o_orderkey = l_orderkey
+      where l_shipmode in ('MAIL', 'SHIP') and l_commitdate < l_receiptdate and l_shipdate < l_commitdate
+      group by l_shipmode order by l_shipmode"""
+    got = orders.sql(sql, group_hint=8, right=lineitem)
+    pos = {k: i for i, k in enumerate(okey)}
+    oi = np.array([pos.get(k, -1) for k in lkey])
+    m = (oi >= 0) & np.isin(mode, ["MAIL", "SHIP"]) & (commit < receipt) & (ship < commit)
+    lp = np.where(oi >= 0, prio[np.maximum(oi, 0)], "")
+    hi = (lp == "1-URGENT") | (lp == "2-HIGH")
+    assert got["l_shipmode"].tolist() == ["MAIL", "SHIP"]
+    assert got["high_line_count"].tolist() == [int(np.sum(m & (mode == s) & hi)) for s in ("MAIL", "SHIP")]
+    assert got["low_line_count"].tolist() == [int(np.sum(m & (mode == s) & ~hi)) for s in ("MAIL", "SHIP")]
+    # a string key of the build side, grouped through the join
+    got = lineitem.sql("select o_orderpriority, count(*) as c from lineitem join orders on l_orderkey = o_orderkey "
+                       "group by o_orderpriority order by o_orderpriority", right=orders)
+    assert got["o_orderpriority"].tolist() == sorted(prios.tolist())
+    assert got["c"].tolist() == [int(np.sum((oi >= 0) & (lp == p))) for p in sorted(prios.tolist())]
+    with pytest.raises(NutError, match="string keys"):
+        lineitem.sql("select count(*) from lineitem join orders on l_shipmode = o_orderpriority", right=orders)
