@@ -1857,8 +1857,8 @@ nut_status exec_join(nut_ctx *c, const nut_plan &p, const nut_column *lc, int nl
       if (nd.op == NUT_P_COL && nd.col == i) return true;
     return false;
   };
+  std::vector<char> used(nc);  // read by the plan after the join (ON-only columns are not)
   for (size_t i = 0; i < nc; ++i) {
-    if (side[i] == ps) continue;
     const int ci = (int)i;
     bool row = ci == p.proj || in_prog(p.where, ci);  // decides or projects rows
     for (int k : p.keys) row = row || k == ci;
@@ -1869,6 +1869,8 @@ nut_status exec_join(nut_ctx *c, const nut_plan &p, const nut_column *lc, int nl
       for (int ref : a.refs) agg = agg || ref == ci;
       agg = agg || in_prog(a.val, ci) || in_prog(a.mask, ci);
     }
+    used[i] = row || agg;
+    if (side[i] == ps) continue;
     if (p.join == NUT_JOIN_SEMI || p.join == NUT_JOIN_ANTI) {
       // SEMI: the other table's ON column equals the preserved one; nothing else exists
       if ((row || agg) && !(p.join == NUT_JOIN_SEMI && ci == bkey))
@@ -1901,6 +1903,10 @@ nut_status exec_join(nut_ctx *c, const nut_plan &p, const nut_column *lc, int nl
   std::vector<DevBuf> bufs(nc + 1);
   std::vector<nut_column> jc(nc + 1);
   for (size_t i = 0; i < nc; ++i) {
+    if (!used[i]) {  // never read: bound to its source column, not gathered
+      jc[i] = nut_column{p.cols[i].c_str(), src[i]->data, src[i]->type};
+      continue;
+    }
     NUT_HIP(hipMalloc(&bufs[i].p, std::max<uint64_t>(npairs, 1) * 8));
     // SEMI / ANTI pairs carry no build row: the other ON column reads the preserved one
     // (outer joins: equal on matched rows; aggregates mask the NULL-extended ones)
