@@ -46,7 +46,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--workload", default="q1", choices=["q1", "groupby", "filter", "sort", "q12expr", "join", "parse"])
+    p.add_argument("--workload", default="q1", choices=["q1", "groupby", "filter", "scanexpr", "sort", "q12expr", "join", "parse"])
     p.add_argument("--rows", type=float, default=None, help="rows per GPU (default: config size)")
     p.add_argument("--groups", type=int, default=1000, help="groupby: distinct keys")
     p.add_argument("--selectivity", type=float, default=0.5, help="filter: fraction selected")
@@ -137,6 +137,32 @@ class Filter:
     def config(self):
         return {"workload": self.name, "query": "SELECT col FROM t WHERE col < k", "selectivity": self.sel,
                 "bytes_per_row": 8 + 8 * self.sel}
+
+
+class ScanExpr:
+    """Expression-mode scan: SELECT a FROM t WHERE a < b over two int64
+    columns (selectivity 0.5): nut_select_rows (WHERE compiled per query, row ids in row
+    order) + the gather of `a` through the ids.  Roofline on the scan kernel: 16 B read +
+    8 B per selected row id written."""
+    name = "scan_expr_i64_compaction"
+    kernel_kind = 0
+
+    def __init__(self, ex, rows, row0):
+        self.ex = ex
+        self.a = ex.gen_column(1, 0x81, rows, row0=row0)
+        self.b = ex.gen_column(1, 0x82, rows, row0=row0)
+        self.where = [("col", 0), ("col", 1), ("lt",)]
+        self.rows = rows
+        self.cols_bytes = 16 + 8 * 0.5
+
+    def run(self):  # results stay in HBM (as nut_plan_execute's scan results do)
+        ids = self.ex.select_rows([self.a, self.b], self.where)
+        return self.ex.gather(self.a, ids)
+
+    def config(self):
+        return {"workload": self.name, "query": "SELECT a FROM t WHERE a < b (expression-mode scan)",
+                "selectivity": 0.5, "bytes_per_row": self.cols_bytes,
+                "step": "select kernel (row ids) + gather of a, results in HBM"}
 
 
 class Sort:
@@ -292,6 +318,10 @@ def cpu_baseline(args, workload: str, target_s: float):
         if workload == "sort":
             col = orc.gen(SORT_COL, n)
             return lambda: orc.sort_i64(col)
+        if workload == "scanexpr":
+            from oracle.expr import eval_prog
+            a, b = orc.gen_column(1, 0x81, n), orc.gen_column(1, 0x82, n)
+            return lambda: a[eval_prog([("col", 0), ("col", 1), ("lt",)], [a, b], n)[0] != 0]
         if workload == "join":
             rng = np.random.default_rng(0x71)
             nb = max(n // 4, 1)
@@ -314,7 +344,8 @@ def cpu_baseline(args, workload: str, target_s: float):
         return time.perf_counter() - t0
 
     full = int(args.rows) if args.rows else {"q1": 10**9, "groupby": 10**9, "filter": 10**8,
-                                             "sort": 1_250_000_000, "q12expr": 10**9, "join": 10**9}[workload]
+                                             "sort": 1_250_000_000, "q12expr": 10**9, "join": 10**9,
+                                             "scanexpr": 10**8}[workload]
     probe = min(full, 4_000_000)
     per_row = timed(prepare(probe)) / probe
     sample = int(min(full, max(probe, target_s / max(per_row, 1e-12))))
@@ -326,6 +357,8 @@ def cpu_baseline(args, workload: str, target_s: float):
     if workload == "join":
         how, cores = (f"C hash join (oracle/oracle.c orc_join_i64: CSR bucket table + two-pass probe), OpenMP "
                       f"over {threads} host threads; probe rows, build = probe/4"), threads
+    elif workload == "scanexpr":
+        how, cores = "numpy expression oracle (oracle/expr.py) + boolean compaction, 1 host thread", 1
     elif workload == "q12expr":
         how, cores = (f"numpy expression oracle (oracle/expr.py, 1 thread) + C oracle group-by (oracle/oracle.c, "
                       f"OpenMP over {threads} host threads)"), threads
@@ -395,7 +428,7 @@ def main():
     from nutdb_amd import Executor
     ex = Executor(local_rank)
     default_rows = {"q1": 1e9, "groupby": 1e9, "filter": 1e8, "sort": 1.25e9, "q12expr": 1e9,
-                    "join": 1e9}[args.workload]
+                    "join": 1e9, "scanexpr": 1e8}[args.workload]
     rows = int(args.rows or default_rows)
     row0 = rank * rows
     if args.workload == "q1":
@@ -411,12 +444,14 @@ def main():
         w = Q12Expr(ex, rows, row0)
     elif args.workload == "join":
         w = Join(ex, rows, row0, world, group, rank)
+    elif args.workload == "scanexpr":
+        w = ScanExpr(ex, rows, row0)
     else:
         w = Filter(ex, rows, row0, args.selectivity)
     torch.cuda.synchronize()
 
     def step():
-        if args.workload in ("filter", "sort", "q12expr", "join"):
+        if args.workload in ("filter", "sort", "q12expr", "join", "scanexpr"):
             w.run()
         else:
             groupby_step(w, rank, world, group)

@@ -320,6 +320,14 @@ void nut_join_free(nut_join *j);
 nut_status nut_join_i64_into(nut_ctx *ctx, const int64_t *build, uint64_t nbuild, const int64_t *probe,
                              uint64_t nprobe, int join_type, int64_t *probe_idx, int64_t *build_idx, uint64_t cap,
                              uint64_t *npairs);
+/* Expression-mode scan + compaction: the row ids (ascending) of the
+ * rows where s->where holds — any program over s->prog_col, compiled for the query like
+ * the expression-mode group-by.  Reads s->n, s->where and the program columns only (keys
+ * and aggregates are ignored).  out_rows holds s->n entries (worst case); *count_host =
+ * rows selected.  Carry any column through the ids with nut_gather_u64. */
+nut_status nut_select_rows(nut_ctx *ctx, const nut_agg_spec *s, int64_t *out_rows, uint64_t *count_host);
+/* compile the scan kernel of nut_select_rows for this spec (hipRTC; no GPU needed) */
+nut_status nut_select_jit_compile(const nut_agg_spec *s);
 /* The multi-GPU join's exchange step: rows go to part (owner_hash(key) >> 56) * nparts / 256
  * (owner_hash = the group-by's; host restatement nutdb_amd/dist.py join_owner); out_keys /
  * out_rows (row0 + row index) hold the parts one after another in part order, rows

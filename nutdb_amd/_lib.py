@@ -133,6 +133,8 @@ SIGNATURES = {
     "nut_join_free": (None, [_P]),
     "nut_hash_partition_i64": (_I32, [_P, _P, _U64, _I32, _I64, _P, _P, C.POINTER(_U64)]),
     "nut_gather_u64": (_I32, [_P, _P, _P, _U64, _U64, _P]),
+    "nut_select_rows": (_I32, [_P, C.POINTER(NutAggSpec), _P, C.POINTER(_U64)]),
+    "nut_select_jit_compile": (_I32, [C.POINTER(NutAggSpec)]),
     "nut_gen_column": (_I32, [_P, _I32, _U64, _I64, _I64, C.c_double, _U64, _U64, _P]),
     "nut_filter_i64": (_I32, [_P, _P, _U64, _I32, _I64, _P, C.POINTER(_U64)]),
     "nut_filter_i64_async": (_I32, [_P, _P, _U64, _I32, _I64, _P, _P]),

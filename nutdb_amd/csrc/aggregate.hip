@@ -12,6 +12,7 @@
 #include "gpart.hpp"
 #include "sort.hpp"
 #include "jit.hpp"
+#include "select_kernel.hpp"
 
 // ============================================================== host side
 using namespace nut;
@@ -901,6 +902,76 @@ __global__ void iota_kernel(int64_t *__restrict__ out, uint64_t n, int64_t base)
 }  // namespace nut
 
 extern "C" {
+
+// Expression-mode scan (select_kernel.hpp): the row ids where the spec's WHERE program
+// holds, in row order.  Reads s->n, s->where and the program columns only.
+nut_status nut_select_rows(nut_ctx *c, const nut_agg_spec *s, int64_t *out_rows, uint64_t *count_host) {
+  if (!c || !s || !count_host || (s->n && !out_rows)) return fail(NUT_ERR_INVALID_ARG, "nut_select_rows: NULL argument");
+  if (!s->prog_mode) return fail(NUT_ERR_INVALID_ARG, "nut_select_rows: needs an expression-mode spec (prog_mode = 1)");
+  if (s->nprog_cols < 0 || s->nprog_cols > NUT_MAX_PROG_COLS)
+    return fail(NUT_ERR_INVALID_ARG, "nut_select_rows: bad program column count");
+  *count_host = 0;
+  for (int i = 0; i < s->nprog_cols; ++i)
+    if (s->n && !s->prog_col[i]) return fail(NUT_ERR_INVALID_ARG, "nut_select_rows: NULL program column");
+  nut_agg_spec q = *s;  // the WHERE program alone
+  q.naggs = 0;
+  int32_t kinds[NUT_MAX_AGGS] = {};
+  JitShape js;
+  nut_status st = jit_shape(&q, kinds, js);
+  if (st) return st;
+  if (js.consts.size() > (size_t)kMaxConst)
+    return fail(NUT_ERR_UNSUPPORTED, "nut_select_rows: more than 64 distinct expression constants");
+  if (s->n == 0) return NUT_OK;
+  const uint64_t n = s->n;
+  const uint64_t ntiles = (n + SEL_TILE - 1) / SEL_TILE;
+  if (ntiles > 0xFFFFFFF0ull) return fail(NUT_ERR_UNSUPPORTED, "nut_select_rows: n too large");
+  DeviceGuard dg(c->device);
+  hipFunction_t fn;
+  st = jit_kernel(jit_select_unit(js.src, sizeof(SelArgs)), true, &fn);
+  if (st) return st;
+  // [ticket u32, err u32, out_n u64][status u64 x ntiles], zeroed as one block
+  const size_t state = 16 + ntiles * 8;
+  st = c->filter_state.reserve(state);
+  if (st) return st;
+  char *base = (char *)c->filter_state.ptr;
+  SelArgs sa;
+  memset(&sa, 0, sizeof sa);
+  sa.a.n = n;
+  sa.a.nvals = s->nprog_cols;
+  for (int i = 0; i < s->nprog_cols; ++i) sa.a.val_col[i] = (const uint64_t *)s->prog_col[i];
+  for (size_t i = 0; i < js.consts.size(); ++i) sa.a.kc[i] = js.consts[i];
+  sa.out = out_rows;
+  sa.ticket = (uint32_t *)base;
+  sa.out_n = (unsigned long long *)(base + 8);
+  sa.status = (uint64_t *)(base + 16);
+  sa.ntiles = (uint32_t)ntiles;
+  NUT_HIP(hipMemsetAsync(base, 0, state, c->stream));
+  size_t asz = sizeof sa;
+  void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &sa, HIP_LAUNCH_PARAM_BUFFER_SIZE, &asz, HIP_LAUNCH_PARAM_END};
+  c->timer.begin(c->stream, NUT_KERNEL_FILTER);
+  hipError_t e = hipModuleLaunchKernel(fn, (unsigned)ntiles, 1, 1, SEL_THREADS, 1, 1, 0, c->stream, nullptr, cfg);
+  c->timer.end(c->stream);
+  if (e != hipSuccess) return hip_fail(e, "hipModuleLaunchKernel (select kernel)");
+  NUT_HIP(hipMemcpyAsync(c->host_pinned, base, 16, hipMemcpyDeviceToHost, c->stream));
+  NUT_HIP(hipStreamSynchronize(c->stream));
+  const uint32_t err = (uint32_t)(c->host_pinned[0] >> 32);
+  if (err & 2u) return fail(NUT_ERR_INVALID_ARG, "nut_select_rows: division by zero in an expression");
+  if (err & 1u) return fail(NUT_ERR_TIMEOUT, "nut_select_rows: look-back spin limit hit");
+  *count_host = c->host_pinned[1];
+  return NUT_OK;
+}
+
+// compile (no GPU needed) the scan kernel nut_select_rows would run for this spec
+nut_status nut_select_jit_compile(const nut_agg_spec *s) {
+  if (!s || !s->prog_mode) return fail(NUT_ERR_INVALID_ARG, "nut_select_jit_compile: needs an expression-mode spec");
+  nut_agg_spec q = *s;
+  q.naggs = 0;
+  int32_t kinds[NUT_MAX_AGGS] = {};
+  JitShape js;
+  nut_status st = jit_shape(&q, kinds, js);
+  if (st) return st;
+  return jit_kernel(jit_select_unit(js.src, sizeof(SelArgs)), false, nullptr);
+}
 
 // The multi-GPU join's exchange step: one gp_level (gpart.hpp) over the keys with the row
 // ids as payload, 256 digits of the owner hash's top byte, parts = digit ranges.

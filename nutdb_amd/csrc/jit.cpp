@@ -179,6 +179,7 @@ typedef int int32_t;
 typedef unsigned short uint16_t;
 typedef unsigned char uint8_t;
 #include "agg_kernel.hpp"
+#include "select_kernel.hpp"
 namespace nut {
 // integer helpers of the expression semantics (include/nutexec.h, nut_prog_op)
 __device__ __forceinline__ int64_t jmod(int64_t a, int64_t b, bool &err) {
@@ -322,6 +323,15 @@ std::string jit_unit(const std::string &shape_src, int nk, bool priv, int bd, si
                            std::to_string(bd) + ", nut::QShape, 0>";
   u += "template __global__ void " + inst + "(AggArgs);\n}  // namespace nut\n";
   u += "// kernel &nut::" + inst + "\n";
+  return u;
+}
+
+std::string jit_select_unit(const std::string &shape_src, size_t args_size) {
+  std::string u = kPrelude;
+  u += "static_assert(sizeof(SelArgs) == " + std::to_string(args_size) + ", \"SelArgs layout\");\n";
+  u += shape_src;
+  u += "template __global__ void select_kernel<nut::QShape>(SelArgs);\n}  // namespace nut\n";
+  u += "// kernel &nut::select_kernel<nut::QShape>\n";
   return u;
 }
 

@@ -1085,8 +1085,12 @@ bool lower_mode(const Statement &st, nut_plan &p, Lowering &L) {
   o.text = std::string(name);
   o.name = b.columns[0].alias ? std::string(*b.columns[0].alias) : o.text;
   p.outs.push_back(o);
-  for (const PlanPred &pr : p.preds)
+  // fused scans: one comparison of the projected column (nut_filter_i64); anything else
+  // is an expression-mode scan (nut_select_rows, WHERE compiled for the query)
+  for (const PlanPred &pr : p.preds) {
     if (pr.col != p.proj) return L.fail("WHERE must test the projected column (single-column scan)");
+    if (pr.op >= NUT_IN) return L.fail("IN in a single-column scan");
+  }
   if (p.preds.size() > 1) return L.fail("a scan takes one comparison");
   if (b.order_by) {
     if (b.order_by->size() != 1) return L.fail("ORDER BY takes one key");
@@ -1116,7 +1120,7 @@ bool lower(const Statement &st, nut_plan &p, Lowering &L) {
     for (const QueryExpr &q : b.columns)
       if (q.e.k == EK::FnCall && q.e.fn() == FnKind::Others) agg = true;
   }
-  if (!agg) return L.fail(L1.err);
+  (void)agg;  // aggregate plans and scans both retry in expression mode
   nut_plan p2;
   p2.compiled = true;
   Lowering L2;
@@ -1343,6 +1347,9 @@ struct DevBuf {
   }
 };
 
+nut_status build_spec(const nut_plan &p, const nut_column *const *bound, const Dict *const *dicts, uint64_t n,
+                      nut_agg_spec &s, std::deque<std::vector<nut_prog_node>> &store, std::vector<int> &agg_f64);
+
 nut_status exec_scan(nut_ctx *c, const nut_plan &p, const nut_column *const *bound, const Dict *const *dicts,
                      uint64_t n, nut_result *r) {
   const nut_column *col = bound[p.proj];
@@ -1356,9 +1363,7 @@ nut_status exec_scan(nut_ctx *c, const nut_plan &p, const nut_column *const *bou
   int op = NUT_GE;
   int64_t k = INT64_MIN;  // no predicate: every row passes
   bool none = p.never || n == 0;
-  if (!p.preds.empty() && p.preds[0].op >= NUT_IN)
-    return fail(NUT_ERR_PLAN, "IN is executed in aggregate plans only (the scan kernel takes one comparison)");
-  if (!none && !p.preds.empty()) {
+  if (!p.compiled && !none && !p.preds.empty()) {
     Verdict v = resolve_i64(p.preds[0].op, p.preds[0].c, op, k);
     if (v == V_FALSE) none = true;
     if (v == V_TRUE) {
@@ -1367,7 +1372,31 @@ nut_status exec_scan(nut_ctx *c, const nut_plan &p, const nut_column *const *bou
     }
   }
   uint64_t cnt = 0;
-  if (!none) {
+  if (!none && p.compiled) {
+    // expression-mode scan: row ids where the WHERE program holds, then the projected
+    // column gathered through them (ascending ids), then sorted for ORDER BY
+    nut_agg_spec sp;
+    std::deque<std::vector<nut_prog_node>> store;
+    std::vector<int> agg_f64;
+    nut_status s = build_spec(p, bound, dicts, n, sp, store, agg_f64);
+    if (s) return s;
+    DevBuf rows;
+    NUT_HIP(hipMalloc(&rows.p, n * 8));
+    s = nut_select_rows(c, &sp, (int64_t *)rows.p, &cnt);
+    if (s) return s;
+    NUT_HIP(hipMalloc(&r->dev, std::max<uint64_t>(cnt, 1) * 8));
+    if (p.kind == NUT_PLAN_FILTER) {
+      s = nut_gather_u64(c, (const uint64_t *)col->data, (const int64_t *)rows.p, cnt, 0, (uint64_t *)r->dev);
+    } else {
+      DevBuf vals;
+      NUT_HIP(hipMalloc(&vals.p, std::max<uint64_t>(cnt, 1) * 8));
+      s = nut_gather_u64(c, (const uint64_t *)col->data, (const int64_t *)rows.p, cnt, 0, (uint64_t *)vals.p);
+      if (!s) s = p.desc ? nut_sort_i64_desc(c, (const int64_t *)vals.p, (int64_t *)r->dev, cnt)
+                         : nut_sort_i64(c, (const int64_t *)vals.p, (int64_t *)r->dev, cnt);
+    }
+    if (!s) s = nut_ctx_sync(c);
+    if (s) return s;
+  } else if (!none) {
     NUT_HIP(hipMalloc(&r->dev, n * 8));
     if (p.kind == NUT_PLAN_FILTER) {
       nut_status s = nut_filter_i64(c, (const int64_t *)col->data, n, op, k, (int64_t *)r->dev, &cnt);
@@ -2094,7 +2123,7 @@ nut_status nut_plan_execute2(nut_ctx *c, const nut_plan *p, const nut_column *le
 
 nut_status nut_plan_prepare(const nut_plan *p, const nut_column *cols, int ncols) {
   if (!p || (ncols && !cols) || ncols < 0) return fail(NUT_ERR_INVALID_ARG, "nut_plan_prepare: NULL argument");
-  if (p->kind != NUT_PLAN_GROUPBY || !p->compiled) return NUT_OK;  // precompiled kernels only
+  if (!p->compiled) return NUT_OK;  // precompiled kernels only
   std::vector<const nut_column *> bound(p->cols.size());
   for (size_t i = 0; i < p->cols.size(); ++i) {
     bound[i] = bind(*p, (int)i, cols, ncols);
@@ -2107,7 +2136,7 @@ nut_status nut_plan_prepare(const nut_plan *p, const nut_column *cols, int ncols
   std::vector<int> agg_f64;
   nut_status st = build_spec(*p, bound.data(), nullptr, 0, s, store, agg_f64);
   if (st) return st;
-  return nut_groupby_jit_compile(&s);
+  return p->kind == NUT_PLAN_GROUPBY ? nut_groupby_jit_compile(&s) : nut_select_jit_compile(&s);
 }
 
 nut_status nut_table_execute(nut_ctx *c, nut_table *t, const nut_plan *p, uint64_t group_hint, nut_result **out) {

@@ -476,6 +476,19 @@ class Executor:
                                     C.c_void_p(out.data_ptr()), counts), "nut_partition_i64")
         return out[:n], [int(c) for c in counts]
 
+    def select_rows(self, cols: list, where: list | None) -> torch.Tensor:
+        """Expression-mode scan (nut_select_rows): ascending int64 row ids of the rows where
+        the RPN program `where` (ProgQuery node syntax, over `cols`) holds."""
+        q = ProgQuery(keys=[], cols=list(cols), aggs=[], where=where)
+        spec = q.to_spec(self.device)
+        n = int(spec.n)
+        out = torch.empty(max(n, 1), dtype=torch.int64, device=self.device)
+        cnt = C.c_uint64()
+        self._bind_stream()
+        check(lib.nut_select_rows(self.ctx, C.byref(spec), C.c_void_p(out.data_ptr()), C.byref(cnt)),
+              "nut_select_rows")
+        return out[:cnt.value]
+
     def hash_partition_i64(self, keys: torch.Tensor, row0: int, nparts: int):
         """The multi-GPU join's exchange step (nut_hash_partition_i64): keys and their row
         ids (row0 + index) grouped by part = dist.join_owner(key, nparts).  Returns

@@ -189,10 +189,26 @@ def test_plan_fused_stays_fused():
     assert d["where_expr"] == "((a >= 1) and (a <= 9))"
 
 
-def test_plan_scan_stays_on_filter_kernel():
-    with pytest.raises(NutError) as e:
-        Plan("select x from t where x < y")
-    assert "unsupported WHERE term" in str(e.value)
+def test_plan_scan_modes():
+    """one comparison of the projected column stays on the filter kernel; any other WHERE
+    makes an expression-mode scan (nut_select_rows), ORDER BY / LIMIT included"""
+    assert Plan("select x from t where x < 5").describe()["mode"] == "fused"
+    for sql, where in [("select x from t where x < y", "(x < y)"),
+                       ("select x from t where x > 1 and x < 9", "((x > 1) and (x < 9))"),
+                       ("select x from t where y in (1, 2)", "((y = 1) or (y = 2))"),
+                       ("select x from t where x % 3 = 0 order by x desc limit 4", "((x % 3) = 0)")]:
+        d = Plan(sql).describe()
+        assert d["mode"] == "compiled" and d["where_expr"] == where, sql
+    assert Plan("select x from t where x % 3 = 0 order by x desc limit 4").kind == "sort"
+
+
+@pytest.mark.parametrize("sql,types", [
+    ("select x from t where x < y", {"x": "int64", "y": "int64"}),
+    ("select x from t where y * 2.5 > 1 or not (x between 3 and 8) order by x", {"x": "int64", "y": "float64"}),
+    ("select x from t where multiIf(x = 1, y, x = 2, 2 * y, 0) > 0.5", {"x": "int64", "y": "float64"})])
+def test_scan_jit_compiles(sql, types):
+    """the scan kernel (select_kernel.hpp) of expression-mode scans compiles with hipRTC"""
+    Plan(sql).prepare(types)
 
 
 # ------------------------------------------------------------------ hipRTC

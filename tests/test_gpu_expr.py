@@ -272,3 +272,47 @@ def test_bench_q12_programs_match_sql(ex):
     assert got["l_shipmode"].tolist() == ok[:, 0].tolist() == [3, 5]
     assert got["high_line_count"].tolist() == ow[:, 0].astype(np.int64).tolist()
     assert got["low_line_count"].tolist() == ow[:, 1].astype(np.int64).tolist()
+
+
+# ------------------------------------------------------------------ expression-mode scans
+@pytest.mark.parametrize("seed", range(8))
+def test_select_rows_fuzz(ex, seed):
+    """nut_select_rows (select_kernel.hpp, WHERE compiled per query) against the numpy
+    expression oracle: the selected row ids, in order, bit-exact."""
+    from oracle.expr import eval_prog
+    rng = np.random.default_rng(2000 + seed)
+    n = [1, 4095, 4097, 300_007, 1_000_003, 77, 65536, 250_000][seed]
+    cols, ic, fc = make_table(rng, n)
+    where = Gen(rng, ic, fc).bool_(3) if seed != 5 else None
+    got = ex.select_rows([dev(c, ex) for c in cols], where).cpu().numpy()
+    if where is None:
+        want = np.arange(n)
+    else:
+        w, _, e = eval_prog(where, cols, n)
+        want = np.nonzero(w != 0)[0]
+    assert np.array_equal(got, want), (seed, len(got), len(want))
+
+
+def test_select_rows_division_by_zero(ex):
+    a = np.arange(10_000, dtype=np.int64)
+    b = a % 5
+    with pytest.raises(NutError, match="division by zero"):
+        ex.select_rows([dev(a, ex), dev(b, ex)], [("col", 0), ("col", 1), ("mod",), ("i64", 0, 1), ("eq",)])
+
+
+def test_sql_expression_scans(ex):
+    rng = np.random.default_rng(17)
+    n = 500_003
+    x = rng.integers(-1000, 1000, n).astype(np.int64)
+    y = rng.integers(-1000, 1000, n).astype(np.int64)
+    f = rng.random(n)
+    cols = {"x": dev(x, ex), "y": dev(y, ex), "f": dev(f, ex)}
+    got = ex.sql("select x from t where x < y and f > 0.25", cols)
+    assert got["x"].tolist() == x[(x < y) & (f > 0.25)].tolist()
+    got = ex.sql("select x from t where x in (1, 2, 3, 500) or y % 7 = 0", cols)
+    assert got["x"].tolist() == x[np.isin(x, [1, 2, 3, 500]) | (y % 7 == 0)].tolist()
+    got = ex.sql("select x from t where x * 2 > y order by x desc limit 10 offset 3", cols)
+    assert got["x"].tolist() == np.sort(x[x * 2 > y])[::-1][3:13].tolist()
+    got = ex.sql("select y from t where f between 0.1 and 0.2 order by y", cols)
+    assert got["y"].tolist() == np.sort(y[(f >= 0.1) & (f <= 0.2)]).tolist()
+    assert ex.sql("select x from t where x > 5000 or y > 5000", cols)["x"].tolist() == []

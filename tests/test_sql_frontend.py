@@ -485,7 +485,7 @@ def test_plan_tpch_q6_global_aggregate():
     ("select k, sum(v) from t group by k having k like 'x%'", "unsupported HAVING term"),
     ("select k from t group by k order by median(v)", "median"),
     ("select k, median(v) from t group by k", "median"),
-    ("select x from t where x < y", "unsupported WHERE term"),
+    ("select x from t where y like 'a%'", "LIKE"),
     ("select k, sum(v) from t full join u on a = b group by k", "FULL OUTER"),
     ("select k, v from t group by k", "neither a GROUP BY key"),
     ("select k, sum(v like 'x') from t group by k", "not executed"),
@@ -494,8 +494,7 @@ def test_plan_tpch_q6_global_aggregate():
     ("select k, sum(v + null) from t group by k", "NULL is executed only"),
     ("select k, sum(median(v)) from t group by k", "median"),
     ("select count(*), v from t", "no GROUP BY"),
-    ("select x from t where x > 1 and x < 9 and x != 3 and x != 4 and x != 5 and x != 6 and x != 7 order by x",
-     "more than 6 WHERE terms"),
+    ("select x, y from t where x > 1", "projects exactly one column"),
     ("select x from t where x < 1 union all select x from t", "UNION"),
     ("select x from t where x >= toDate('1998-13-01')", "toDate"),
 ])
