@@ -1830,6 +1830,82 @@ namespace {
 
 // A plan with a JOIN (nut_plan_execute2): hash join on the ON columns, gathers of every
 // plan column through the join index, then the plan's scan / group-by on the joined rows.
+// conjuncts of a boolean program: `A AND B` splits into A's and B's conjuncts
+void split_and(const PProg &pp, std::vector<PProg> &out) {
+  if (pp.empty()) return;
+  if (pp.back().op != NUT_P_AND) {
+    out.push_back(pp);
+    return;
+  }
+  // subtree starts: the AND's two operands are the last two subtrees before it
+  std::vector<size_t> st;
+  for (size_t i = 0; i + 1 < pp.size(); ++i) {
+    const int op = pp[i].op;
+    const int k = op <= NUT_P_F64 ? 0 : (op == NUT_P_NOT || op == NUT_P_BITNOT || op == NUT_P_ABS ||
+                                         op == NUT_P_TO_F64) ? 1 : op == NUT_P_IF ? 3 : 2;
+    size_t start = i;
+    for (int j = 0; j < k; ++j) {
+      start = st.back();
+      st.pop_back();
+    }
+    st.push_back(start);
+  }
+  if (st.size() != 2) {  // malformed: keep whole
+    out.push_back(pp);
+    return;
+  }
+  split_and(PProg(pp.begin(), pp.begin() + st[1]), out);
+  split_and(PProg(pp.begin() + st[1], pp.end() - 1), out);
+}
+
+PProg and_all(const std::vector<PProg> &cs) {
+  PProg r;
+  for (size_t i = 0; i < cs.size(); ++i) {
+    r.insert(r.end(), cs[i].begin(), cs[i].end());
+    if (i) {
+      PNode a;
+      a.op = NUT_P_AND;
+      r.push_back(a);
+    }
+  }
+  return r;
+}
+
+// a fused-mode predicate as a program: col <cmp> c, or an OR / AND of equalities (IN)
+PProg pred_prog(const PlanPred &pr) {
+  auto konst = [&](const CVal &c) {
+    PNode n;
+    n.op = c.is_int || c.is_str ? NUT_P_I64 : NUT_P_F64;
+    n.c = c;
+    n.col = pr.col;  // string constants take the compared column's dictionary
+    return n;
+  };
+  PNode col;
+  col.op = NUT_P_COL;
+  col.col = pr.col;
+  PProg r;
+  if (pr.op < NUT_IN) {
+    r = {col, konst(pr.c)};
+    PNode cmp;
+    cmp.op = NUT_P_LT + pr.op;
+    r.push_back(cmp);
+    return r;
+  }
+  for (size_t i = 0; i < pr.set.size(); ++i) {
+    r.push_back(col);
+    r.push_back(konst(pr.set[i]));
+    PNode cmp;
+    cmp.op = pr.op == NUT_IN ? NUT_P_EQ : NUT_P_NE;
+    r.push_back(cmp);
+    if (i) {
+      PNode j;
+      j.op = pr.op == NUT_IN ? NUT_P_OR : NUT_P_AND;
+      r.push_back(j);
+    }
+  }
+  return r;
+}
+
 // ldict / rdict (may be null): the dictionary of each column of lc / rc (typed tables)
 nut_status exec_join(nut_ctx *c, const nut_plan &p, const nut_column *lc, int nl, uint64_t lrows,
                      const nut_column *rc, int nr, uint64_t rrows, uint64_t hint, nut_result *r,
@@ -1874,31 +1950,33 @@ nut_status exec_join(nut_ctx *c, const nut_plan &p, const nut_column *lc, int nl
   if (lkey->type != NUT_T_I64 || rkey->type != NUT_T_I64) return fail(NUT_ERR_PLAN, "JOIN keys must be int64 columns");
   if (sdict[k0] || sdict[k1])  // codes of two dictionaries do not compare
     return fail(NUT_ERR_PLAN, "JOIN keys must be integer columns (string keys are not executed)");
-  // INNER builds the smaller table; the outer / semi / anti joins preserve their side
-  const int ps = p.join == NUT_JOIN_INNER ? (lrows >= rrows ? 0 : 1) : (p.jright ? 1 : 0);
-  const nut_column *pk = ps == 0 ? lkey : rkey, *bk = ps == 0 ? rkey : lkey;
-  const uint64_t np = ps == 0 ? lrows : rrows, nb = ps == 0 ? rrows : lrows;
+  // INNER builds the smaller table (decided after the pushdown below); the outer / semi /
+  // anti joins preserve their side
+  int ps = p.join == NUT_JOIN_INNER ? (lrows >= rrows ? 0 : 1) : (p.jright ? 1 : 0);
   const bool outer = p.join == NUT_JOIN_LEFT;
   // what the other (build) table may feed
-  const int bkey = side[k0] == ps ? k1 : k0, pkey = side[k0] == ps ? k0 : k1;
+  int bkey = side[k0] == ps ? k1 : k0, pkey = side[k0] == ps ? k0 : k1;
   auto in_prog = [](const PProg &pp, int i) {
     for (const PNode &nd : pp)
       if (nd.op == NUT_P_COL && nd.col == i) return true;
     return false;
   };
-  std::vector<char> used(nc);  // read by the plan after the join (ON-only columns are not)
-  for (size_t i = 0; i < nc; ++i) {
-    const int ci = (int)i;
-    bool row = ci == p.proj || in_prog(p.where, ci);  // decides or projects rows
-    for (int k : p.keys) row = row || k == ci;
-    for (const PlanPred &pr : p.preds) row = row || pr.col == ci;
-    bool agg = false;
-    for (int v : p.vals) agg = agg || v == ci;
-    for (const PlanAgg &a : p.aggs) {
+  // read by plan q after the join: as a row decider / projection, or inside an aggregate
+  auto reads = [&](const nut_plan &q, int ci, bool &row, bool &agg) {
+    row = ci == q.proj || in_prog(q.where, ci);
+    for (int k : q.keys) row = row || k == ci;
+    for (const PlanPred &pr : q.preds) row = row || pr.col == ci;
+    agg = false;
+    for (int v : q.vals) agg = agg || v == ci;
+    for (const PlanAgg &a : q.aggs) {
       for (int ref : a.refs) agg = agg || ref == ci;
       agg = agg || in_prog(a.val, ci) || in_prog(a.mask, ci);
     }
-    used[i] = row || agg;
+  };
+  for (size_t i = 0; i < nc; ++i) {
+    const int ci = (int)i;
+    bool row, agg;
+    reads(p, ci, row, agg);
     if (side[i] == ps) continue;
     if (p.join == NUT_JOIN_SEMI || p.join == NUT_JOIN_ANTI) {
       // SEMI: the other table's ON column equals the preserved one; nothing else exists
@@ -1909,6 +1987,66 @@ nut_status exec_join(nut_ctx *c, const nut_plan &p, const nut_column *lc, int nl
                                     "' may only appear inside aggregates");
     }
   }
+  // ---- predicate pushdown: WHERE conjuncts that read one table filter that table before
+  // the join (nut_select_rows -> ascending row ids; the join runs on the selected keys and
+  // its indices map back through the ids).  INNER: both tables; outer / semi / anti: the
+  // preserved one (WHERE may not read the other table there).
+  nut_plan p2 = p;
+  std::vector<PProg> push[2];
+  auto pushable = [&](int sd) { return sd >= 0 && (p.join == NUT_JOIN_INNER || sd == ps); };
+  if (p.compiled) {
+    std::vector<PProg> conj, keep;
+    split_and(p.where, conj);
+    for (PProg &cj : conj) {
+      int sd = -1;
+      for (const PNode &nd : cj)
+        if (nd.op == NUT_P_COL) sd = sd < 0 || sd == side[nd.col] ? side[nd.col] : 2;
+      (sd < 2 && pushable(sd) ? push[sd] : keep).push_back(std::move(cj));
+    }
+    p2.where = and_all(keep);
+  } else {
+    p2.preds.clear();
+    for (const PlanPred &pr : p.preds)
+      if (pushable(side[pr.col])) push[side[pr.col]].push_back(pred_prog(pr));
+      else p2.preds.push_back(pr);
+  }
+  const nut_column *keycol[2] = {lkey, rkey};
+  const int64_t *keys_s[2] = {(const int64_t *)lkey->data, (const int64_t *)rkey->data};
+  uint64_t rows_s[2] = {lrows, rrows};
+  DevBuf ids_s[2], keybuf[2];
+  for (int sd = 0; sd < 2; ++sd) {
+    if (push[sd].empty() || p.never) continue;
+    nut_plan q;
+    q.compiled = true;
+    q.cols = p.cols;
+    q.where = and_all(push[sd]);
+    nut_agg_spec spec;
+    std::deque<std::vector<nut_prog_node>> store;
+    std::vector<int> agg_f64;
+    nut_status es = build_spec(q, src.data(), sdict.data(), rows_s[sd], spec, store, agg_f64);
+    if (es) return es;
+    NUT_HIP(hipMalloc(&ids_s[sd].p, std::max<uint64_t>(rows_s[sd], 1) * 8));
+    uint64_t cnt = 0;
+    if (rows_s[sd]) es = nut_select_rows(c, &spec, (int64_t *)ids_s[sd].p, &cnt);
+    if (es) return es;
+    NUT_HIP(hipMalloc(&keybuf[sd].p, std::max<uint64_t>(cnt, 1) * 8));
+    es = nut_gather_u64(c, (const uint64_t *)keycol[sd]->data, (const int64_t *)ids_s[sd].p, cnt, 0,
+                        (uint64_t *)keybuf[sd].p);
+    if (es) return es;
+    keys_s[sd] = (const int64_t *)keybuf[sd].p;
+    rows_s[sd] = cnt;
+  }
+  if (p.join == NUT_JOIN_INNER) ps = rows_s[0] >= rows_s[1] ? 0 : 1;
+  bkey = side[k0] == ps ? k1 : k0;
+  pkey = side[k0] == ps ? k0 : k1;
+  const int64_t *pkd = keys_s[ps], *bkd = keys_s[1 - ps];
+  const uint64_t np = rows_s[ps], nb = rows_s[1 - ps];
+  std::vector<char> used(nc);  // read after the join (ON-only and pushed-down columns are not)
+  for (size_t i = 0; i < nc; ++i) {
+    bool row, agg;
+    reads(p2, (int)i, row, agg);
+    used[i] = row || agg;
+  }
   // one pass into arrays of np pairs (enough unless the build keys repeat), else again
   // with the exact count
   DevBuf idx;
@@ -1917,8 +2055,7 @@ nut_status exec_join(nut_ctx *c, const nut_plan &p, const nut_column *lc, int nl
   for (;;) {
     hipError_t he = hipMalloc(&idx.p, cap * 16);
     if (he != hipSuccess) return hip_fail(he, "hipMalloc (join index)");
-    st = nut_join_i64_into(c, (const int64_t *)bk->data, nb, (const int64_t *)pk->data, np, p.join,
-                           (int64_t *)idx.p, (int64_t *)idx.p + cap, cap, &npairs);
+    st = nut_join_i64_into(c, bkd, nb, pkd, np, p.join, (int64_t *)idx.p, (int64_t *)idx.p + cap, cap, &npairs);
     if (st != NUT_ERR_CAPACITY || npairs <= cap) break;
     NUT_HIP(hipFree(idx.p));
     idx.p = nullptr;
@@ -1926,8 +2063,16 @@ nut_status exec_join(nut_ctx *c, const nut_plan &p, const nut_column *lc, int nl
   }
   if (st) return st;
   int64_t *pi = (int64_t *)idx.p, *bi = pi + cap;
+  // indices into the pushed-down selections -> table rows (-1 stays -1)
+  if (ids_s[ps].p && npairs) {
+    st = nut_gather_u64(c, (const uint64_t *)ids_s[ps].p, pi, npairs, 0, (uint64_t *)pi);
+    if (st) return st;
+  }
+  if (ids_s[1 - ps].p && npairs) {
+    st = nut_gather_u64(c, (const uint64_t *)ids_s[1 - ps].p, bi, npairs, ~0ull, (uint64_t *)bi);
+    if (st) return st;
+  }
   // the joined table: every plan column gathered through its side's index
-  nut_plan p2 = p;
   const bool mask_col = outer && p.kind == NUT_PLAN_GROUPBY;
   std::vector<DevBuf> bufs(nc + 1);
   std::vector<nut_column> jc(nc + 1);

@@ -285,3 +285,25 @@ def test_sql_join_qualified_same_name_keys(ex, orc):
         ex.sql("select count(*) from lineitem as l join orders as o on x.okey = o.okey", li, right=o)
     with pytest.raises(NutError, match="in both tables"):
         ex.sql("select count(*) from lineitem as l join orders as o on okey = o.okey", li, right=o)
+
+
+def test_sql_join_pushdown_mixed_where(ex, orc):
+    """WHERE conjuncts on one table are pushed below the join (nut_select_rows on that
+    table); a conjunct reading both tables stays above it; OR across tables stays whole."""
+    orders, lines = tables(8, 40_000, 150_000)
+    j = joined(orc, lines, "l_okey", orders, "o_okey", "inner")
+    cases = [
+        ("l_qty > 3 and o_cust < 30 and l_qty > o_cust", (j.l_qty > 3) & (j.o_cust < 30) & (j.l_qty > j.o_cust)),
+        ("(l_qty > 50 or o_cust = 7) and l_price >= 0", ((j.l_qty > 50) | (j.o_cust == 7)) & (j.l_price >= 0)),
+        ("l_qty in (5, 6, 7) and o_cust != 3", j.l_qty.isin([5, 6, 7]) & (j.o_cust != 3)),
+    ]
+    for where, m in cases:
+        got = ex.sql(f"select o_cust, count(*) as c, sum(l_qty) as q from lineitem join orders on l_okey = o_okey "
+                     f"where {where} group by o_cust order by o_cust", on_dev(ex, lines), right=on_dev(ex, orders))
+        g = j[m].groupby("o_cust").agg(c=("l_qty", "size"), q=("l_qty", "sum"))
+        assert got["o_cust"].tolist() == g.index.tolist(), where
+        assert got["c"].tolist() == g.c.tolist() and got["q"].tolist() == g.q.tolist(), where
+    # a scan with a pushed-down predicate keeps probe-row order
+    got = ex.sql("select l_qty from lineitem join orders on l_okey = o_okey where o_cust = 4 and l_qty < 20",
+                 on_dev(ex, lines), right=on_dev(ex, orders))
+    assert got["l_qty"].tolist() == j.l_qty[(j.o_cust == 4) & (j.l_qty < 20)].tolist()
