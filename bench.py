@@ -46,7 +46,8 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--workload", default="q1", choices=["q1", "groupby", "filter", "scanexpr", "sort", "q12expr", "join", "parse"])
+    p.add_argument("--workload", default="q1", choices=["q1", "groupby", "filter", "scanexpr", "sort", "q12expr", "join", "q12join",
+                                                   "parse"])
     p.add_argument("--rows", type=float, default=None, help="rows per GPU (default: config size)")
     p.add_argument("--groups", type=int, default=1000, help="groupby: distinct keys")
     p.add_argument("--selectivity", type=float, default=0.5, help="filter: fraction selected")
@@ -283,6 +284,58 @@ class Join:
                 "partition_bytes_per_row": 48.0 * (1 + self.nb / self.rows) if self.world > 1 else 0.0}
 
 
+Q12J_SQL = """select l_shipmode,
+    sum(case when o_orderpriority = 1 or o_orderpriority = 2 then 1 else 0 end) as high_line_count,
+    sum(case when o_orderpriority <> 1 and o_orderpriority <> 2 then 1 else 0 end) as low_line_count
+  from orders join lineitem on o_orderkey = l_orderkey
+  where l_shipmode in (3, 5) and l_commitdate < l_receiptdate and l_shipdate < l_commitdate
+  group by l_shipmode order by l_shipmode"""
+
+
+def q12j_tables(gen_i, rows):
+    """orders (rows/4 unique keys, priority 1..5) and lineitem (rows, every line on an
+    order; ship mode 0..6, three dates in [8000, 10000)) from a column generator
+    gen_i(kind, seed, n, a, b) (device or oracle)."""
+    no = max(rows // 4, 1)
+    okey = gen_i(0, 0x91, no, 0, 0)
+    orders = {"o_orderkey": okey, "o_orderpriority": gen_i(5, 0x92, no, 1, 5)}
+    sel = gen_i(0, 0x93, rows, 0, 0) % no
+    lineitem = {"l_orderkey": okey[sel], "l_shipmode": gen_i(5, 0x94, rows, 0, 7),
+                "l_shipdate": gen_i(5, 0x95, rows, 8000, 2000), "l_commitdate": gen_i(5, 0x96, rows, 8000, 2000),
+                "l_receiptdate": gen_i(5, 0x97, rows, 8000, 2000)}
+    return orders, lineitem
+
+
+class Q12Join:
+    """TPC-H Q12 as written — orders JOIN lineitem ON o_orderkey = l_orderkey — through
+    SQL -> plan -> nut_plan_execute2: the lineitem-only WHERE conjuncts are pushed below the
+    join (expression-mode scan of lineitem, ~4.8 % selected), the join runs on the selected
+    lines against all orders, the priority is gathered through the join index and the
+    CASE sums run in the expression-mode group-by.  Roofline on the pushed-down scan kernel
+    (4 x 8 B lineitem columns read + 8 B per selected id)."""
+    name = "tpch_q12_join"
+    kernel_kind = 0
+
+    def __init__(self, ex, rows, row0):
+        from nutdb_amd.sql import Plan
+        self.ex = ex
+        self.rows = rows
+        self.orders, self.lineitem = q12j_tables(
+            lambda k, seed, n, a, b: ex.gen_column(k, seed, n, a=a, b=b), rows)
+        self.plan = Plan(Q12J_SQL)
+        self.cols_bytes = 32 + 8 * (2 / 7) / 6
+
+    def run(self):
+        return self.plan.execute_join(self.ex, self.orders, self.lineitem, group_hint=8)
+
+    def config(self):
+        return {"workload": self.name, "query": "TPC-H Q12 (integer codes for ship mode / priority): orders JOIN "
+                "lineitem, IN + 2 date comparisons, 2 x SUM(CASE ...) GROUP BY l_shipmode",
+                "lineitem_rows": self.rows, "orders_rows": self.rows // 4, "bytes_per_row": self.cols_bytes,
+                "plan": "WHERE pushed below the join (select kernel) -> hash join (selected lines x orders) -> "
+                        "gathers -> expression-mode group-by"}
+
+
 # ------------------------------------------------------------------ one step
 def groupby_step(w, rank, world, group):
     """Local scan -> (N>1) all-to-all of partial groups by owner -> owner merge ->
@@ -318,6 +371,18 @@ def cpu_baseline(args, workload: str, target_s: float):
         if workload == "sort":
             col = orc.gen(SORT_COL, n)
             return lambda: orc.sort_i64(col)
+        if workload == "q12join":
+            o, li = q12j_tables(lambda k, seed, m, a, b: orc.gen_column(k, seed, m, a=a, b=b), n)
+
+            def q12():
+                m = (np.isin(li["l_shipmode"], [3, 5]) & (li["l_commitdate"] < li["l_receiptdate"])
+                     & (li["l_shipdate"] < li["l_commitdate"]))
+                ids = np.nonzero(m)[0]
+                pi, bi = orc.join_i64_c(o["o_orderkey"], li["l_orderkey"][ids], "inner")
+                pr, mode = o["o_orderpriority"][bi], li["l_shipmode"][ids[pi]]
+                hi = (pr == 1) | (pr == 2)
+                return [(s_, int(np.sum(hi & (mode == s_))), int(np.sum(~hi & (mode == s_)))) for s_ in (3, 5)]
+            return q12
         if workload == "scanexpr":
             from oracle.expr import eval_prog
             a, b = orc.gen_column(1, 0x81, n), orc.gen_column(1, 0x82, n)
@@ -345,7 +410,7 @@ def cpu_baseline(args, workload: str, target_s: float):
 
     full = int(args.rows) if args.rows else {"q1": 10**9, "groupby": 10**9, "filter": 10**8,
                                              "sort": 1_250_000_000, "q12expr": 10**9, "join": 10**9,
-                                             "scanexpr": 10**8}[workload]
+                                             "scanexpr": 10**8, "q12join": 10**9}[workload]
     probe = min(full, 4_000_000)
     per_row = timed(prepare(probe)) / probe
     sample = int(min(full, max(probe, target_s / max(per_row, 1e-12))))
@@ -359,6 +424,9 @@ def cpu_baseline(args, workload: str, target_s: float):
                       f"over {threads} host threads; probe rows, build = probe/4"), threads
     elif workload == "scanexpr":
         how, cores = "numpy expression oracle (oracle/expr.py) + boolean compaction, 1 host thread", 1
+    elif workload == "q12join":
+        how, cores = (f"numpy filter (pushed down, 1 thread) + C hash join (oracle/oracle.c, OpenMP over {threads} "
+                      f"threads) + numpy CASE sums"), threads
     elif workload == "q12expr":
         how, cores = (f"numpy expression oracle (oracle/expr.py, 1 thread) + C oracle group-by (oracle/oracle.c, "
                       f"OpenMP over {threads} host threads)"), threads
@@ -428,7 +496,7 @@ def main():
     from nutdb_amd import Executor
     ex = Executor(local_rank)
     default_rows = {"q1": 1e9, "groupby": 1e9, "filter": 1e8, "sort": 1.25e9, "q12expr": 1e9,
-                    "join": 1e9, "scanexpr": 1e8}[args.workload]
+                    "join": 1e9, "scanexpr": 1e8, "q12join": 1e9}[args.workload]
     rows = int(args.rows or default_rows)
     row0 = rank * rows
     if args.workload == "q1":
@@ -446,12 +514,17 @@ def main():
         w = Join(ex, rows, row0, world, group, rank)
     elif args.workload == "scanexpr":
         w = ScanExpr(ex, rows, row0)
+    elif args.workload == "q12join":
+        if world > 1:
+            print("bench.py: q12join is a single-GPU workload", file=sys.stderr)
+            sys.exit(2)
+        w = Q12Join(ex, rows, row0)
     else:
         w = Filter(ex, rows, row0, args.selectivity)
     torch.cuda.synchronize()
 
     def step():
-        if args.workload in ("filter", "sort", "q12expr", "join", "scanexpr"):
+        if args.workload in ("filter", "sort", "q12expr", "join", "scanexpr", "q12join"):
             w.run()
         else:
             groupby_step(w, rank, world, group)

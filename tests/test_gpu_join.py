@@ -307,3 +307,26 @@ def test_sql_join_pushdown_mixed_where(ex, orc):
     got = ex.sql("select l_qty from lineitem join orders on l_okey = o_okey where o_cust = 4 and l_qty < 20",
                  on_dev(ex, lines), right=on_dev(ex, orders))
     assert got["l_qty"].tolist() == j.l_qty[(j.o_cust == 4) & (j.l_qty < 20)].tolist()
+
+
+def test_q12_join_bench_workload_parity(ex, orc):
+    """bench.py's q12join workload (TPC-H Q12 as written, pushdown + join + expression
+    group-by) on 2e6 lines against its own CPU baseline computation."""
+    import sys
+    from pathlib import Path
+    sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+    import bench
+    from nutdb_amd.sql import Plan
+    n = 2_000_000
+    od, ld = bench.q12j_tables(lambda k, seed, m, a, b: ex.gen_column(k, seed, m, a=a, b=b), n)
+    got = Plan(bench.Q12J_SQL).execute_join(ex, od, ld, group_hint=8)
+    o, li = bench.q12j_tables(lambda k, seed, m, a, b: orc.gen_column(k, seed, m, a=a, b=b), n)
+    m = (np.isin(li["l_shipmode"], [3, 5]) & (li["l_commitdate"] < li["l_receiptdate"])
+         & (li["l_shipdate"] < li["l_commitdate"]))
+    ids = np.nonzero(m)[0]
+    pi, bi = orc.join_i64(o["o_orderkey"], li["l_orderkey"][ids], "inner")
+    pr, mode = o["o_orderpriority"][bi], li["l_shipmode"][ids[pi]]
+    hi = (pr == 1) | (pr == 2)
+    assert got["l_shipmode"].tolist() == [3, 5]
+    assert got["high_line_count"].tolist() == [int(np.sum(hi & (mode == s))) for s in (3, 5)]
+    assert got["low_line_count"].tolist() == [int(np.sum(~hi & (mode == s))) for s in (3, 5)]
