@@ -438,6 +438,8 @@ nut_status nut_result_to_host(const nut_result *res, int j, void *dst, uint64_t 
 /* FILTER/SORT results stay in HBM: device pointer of the nrows output values.
  * NUT_ERR_UNSUPPORTED for GROUPBY results (those are materialised on the host). */
 nut_status nut_result_device(const nut_result *res, const void **dev);
+/* column j of a FILTER / SORT result in HBM (expression-mode scans may project several) */
+nut_status nut_result_device_column(const nut_result *r, int j, const void **dev);
 /* row of a NUT_T_STR output column (a string group key of a typed table); the bytes
  * are owned by res and not NUL-terminated */
 nut_status nut_result_string(const nut_result *res, int j, uint64_t row, const char **s, size_t *len);

@@ -181,6 +181,7 @@ SIGNATURES = {
     "nut_result_column": (_I32, [_P, _I32, C.POINTER(_I32), C.POINTER(C.c_char_p)]),
     "nut_result_to_host": (_I32, [_P, _I32, _P, _U64]),
     "nut_result_device": (_I32, [_P, C.POINTER(_P)]),
+    "nut_result_device_column": (_I32, [_P, _I32, C.POINTER(_P)]),
     "nut_result_free": (None, [_P]),
 }
 

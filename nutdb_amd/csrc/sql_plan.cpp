@@ -306,7 +306,8 @@ struct nut_plan {
   std::vector<std::string> cols;  // names the plan binds
   bool never = false;             // WHERE folded to false
   std::vector<PlanPred> preds;
-  int proj = -1;                  // FILTER/SORT column
+  int proj = -1;                  // FILTER/SORT column (the first projected one)
+  std::vector<int> projs;         // every projected column (expression-mode scans: several)
   bool desc = false;              // SORT direction
   std::vector<int> keys, vals;    // GROUPBY key / value columns (indices into cols)
   std::vector<PlanAgg> aggs;
@@ -333,6 +334,7 @@ struct nut_result {
   std::vector<int> types;
   void *dev = nullptr;  // FILTER/SORT: owned device buffer
   uint64_t dev_off = 0;
+  uint64_t dev_stride = 0;  // FILTER with several columns: column j at dev + j * dev_stride
   std::vector<std::vector<uint64_t>> host;  // GROUPBY: output columns (int64 / f64 bits)
   std::vector<std::vector<std::string>> strs;  // NUT_T_STR columns, decoded (others empty)
 };
@@ -1074,17 +1076,24 @@ bool lower_mode(const Statement &st, nut_plan &p, Lowering &L) {
     return true;
   }
 
-  // no GROUP BY, no aggregate: one projected column
+  // no GROUP BY, no aggregate: projected columns (several: expression-mode scans only)
   sv name;
-  if (b.columns.size() != 1 || !column_ref(p, b.columns[0].e, name))
-    return L.fail("a plan without GROUP BY projects exactly one column");
-  p.proj = col_index(p, name);
-  PlanOut o;
-  o.kind = OUT_KEY;
-  o.a = 0;
-  o.text = std::string(name);
-  o.name = b.columns[0].alias ? std::string(*b.columns[0].alias) : o.text;
-  p.outs.push_back(o);
+  if (b.columns.empty()) return L.fail("a plan without GROUP BY projects columns");
+  for (size_t j = 0; j < b.columns.size(); ++j) {
+    if (!column_ref(p, b.columns[j].e, name))
+      return L.fail("a plan without GROUP BY projects plain columns ('" + expr_text(b.columns[j].e) + "')");
+    p.projs.push_back(col_index(p, name));
+    PlanOut o;
+    o.kind = OUT_KEY;
+    o.a = (int)j;
+    o.text = std::string(name);
+    o.name = b.columns[j].alias ? std::string(*b.columns[j].alias) : o.text;
+    p.outs.push_back(o);
+  }
+  p.proj = p.projs[0];
+  if (p.projs.size() > 1 && !p.compiled) return L.fail("a fused scan projects one column");
+  if (p.projs.size() > 1 && b.order_by)
+    return L.fail("ORDER BY with several projected columns is not executed (keys-only sort)");
   // fused scans: one comparison of the projected column (nut_filter_i64); anything else
   // is an expression-mode scan (nut_select_rows, WHERE compiled for the query)
   for (const PlanPred &pr : p.preds) {
@@ -1238,6 +1247,14 @@ std::string describe(const nut_plan &p) {
   } else {
     o += ",\"column\":";
     json_str(o, p.cols[p.proj]);
+    if (p.projs.size() > 1) {
+      o += ",\"project\":[";
+      for (size_t j = 0; j < p.projs.size(); ++j) {
+        if (j) o += ',';
+        json_str(o, p.cols[p.projs[j]]);
+      }
+      o += ']';
+    }
   }
   if (p.kind == NUT_PLAN_SORT) o += p.desc ? ",\"desc\":true" : ",\"desc\":false";
   o += ",\"outputs\":[";
@@ -1353,13 +1370,19 @@ nut_status build_spec(const nut_plan &p, const nut_column *const *bound, const D
 nut_status exec_scan(nut_ctx *c, const nut_plan &p, const nut_column *const *bound, const Dict *const *dicts,
                      uint64_t n, nut_result *r) {
   const nut_column *col = bound[p.proj];
-  if (dicts && dicts[p.proj])
-    return fail(NUT_ERR_PLAN, "column '" + p.cols[p.proj] + "' holds strings: scans / sorts of strings are not executed");
+  for (int pj : p.projs)
+    if (dicts && dicts[pj])
+      return fail(NUT_ERR_PLAN, "column '" + p.cols[pj] + "' holds strings: scans / sorts of strings are not executed");
   for (const PlanPred &pr : p.preds)
     if (pr.c.is_str) return fail(NUT_ERR_PLAN, "string constant " + cval_str(pr.c) + " compared with an int64 column");
-  if (col->type != NUT_T_I64) return fail(NUT_ERR_PLAN, "column '" + p.cols[p.proj] + "' must be int64 for a scan/sort");
-  r->names.push_back(p.outs[0].name);
-  r->types.push_back(NUT_T_I64);
+  // fused scans and sorts: int64; expression-mode FILTER scans: int64 or float64 columns
+  for (int pj : p.projs)
+    if (bound[pj]->type != NUT_T_I64 && !(p.compiled && p.kind == NUT_PLAN_FILTER && bound[pj]->type == NUT_T_F64))
+      return fail(NUT_ERR_PLAN, "column '" + p.cols[pj] + "' must be int64 for this scan/sort");
+  for (size_t j = 0; j < p.projs.size(); ++j) {
+    r->names.push_back(p.outs[j].name);
+    r->types.push_back(bound[p.projs[j]]->type);
+  }
   int op = NUT_GE;
   int64_t k = INT64_MIN;  // no predicate: every row passes
   bool none = p.never || n == 0;
@@ -1384,9 +1407,13 @@ nut_status exec_scan(nut_ctx *c, const nut_plan &p, const nut_column *const *bou
     NUT_HIP(hipMalloc(&rows.p, n * 8));
     s = nut_select_rows(c, &sp, (int64_t *)rows.p, &cnt);
     if (s) return s;
-    NUT_HIP(hipMalloc(&r->dev, std::max<uint64_t>(cnt, 1) * 8));
+    const size_t k = p.kind == NUT_PLAN_FILTER ? p.projs.size() : 1;
+    NUT_HIP(hipMalloc(&r->dev, std::max<uint64_t>(cnt, 1) * 8 * k));
     if (p.kind == NUT_PLAN_FILTER) {
-      s = nut_gather_u64(c, (const uint64_t *)col->data, (const int64_t *)rows.p, cnt, 0, (uint64_t *)r->dev);
+      r->dev_stride = cnt;
+      for (size_t j = 0; j < k && !s; ++j)
+        s = nut_gather_u64(c, (const uint64_t *)bound[p.projs[j]]->data, (const int64_t *)rows.p, cnt, 0,
+                           (uint64_t *)r->dev + j * cnt);
     } else {
       DevBuf vals;
       NUT_HIP(hipMalloc(&vals.p, std::max<uint64_t>(cnt, 1) * 8));
@@ -1964,6 +1991,7 @@ nut_status exec_join(nut_ctx *c, const nut_plan &p, const nut_column *lc, int nl
   // read by plan q after the join: as a row decider / projection, or inside an aggregate
   auto reads = [&](const nut_plan &q, int ci, bool &row, bool &agg) {
     row = ci == q.proj || in_prog(q.where, ci);
+    for (int pj : q.projs) row = row || pj == ci;
     for (int k : q.keys) row = row || k == ci;
     for (const PlanPred &pr : q.preds) row = row || pr.col == ci;
     agg = false;
@@ -2389,7 +2417,17 @@ nut_status nut_result_to_host(const nut_result *r, int j, void *dst, uint64_t ca
     return NUT_OK;
   }
   DeviceGuard g(r->device);
-  NUT_HIP(hipMemcpy(dst, (const int64_t *)r->dev + r->dev_off, r->nrows * 8, hipMemcpyDeviceToHost));
+  NUT_HIP(hipMemcpy(dst, (const int64_t *)r->dev + (uint64_t)j * r->dev_stride + r->dev_off, r->nrows * 8,
+                    hipMemcpyDeviceToHost));
+  return NUT_OK;
+}
+
+nut_status nut_result_device_column(const nut_result *r, int j, const void **dev) {
+  if (!r || !dev || j < 0 || j >= (int)r->names.size())
+    return fail(NUT_ERR_INVALID_ARG, "nut_result_device_column: bad argument");
+  if (r->kind == NUT_PLAN_GROUPBY)
+    return fail(NUT_ERR_UNSUPPORTED, "nut_result_device_column: group results live on the host");
+  *dev = r->dev ? (const void *)((const int64_t *)r->dev + (uint64_t)j * r->dev_stride + r->dev_off) : nullptr;
   return NUT_OK;
 }
 

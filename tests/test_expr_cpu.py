@@ -278,3 +278,11 @@ def test_jit_source_independent_of_constants():
     s1, s2 = jit_source(mk(5, 2.5)), jit_source(mk(-123, 0.125))
     assert s1 == s2 and "p.kc[0]" in s1 and "p.kc[1]" in s1
     assert "5" not in s1.split("where")[1].split(";")[0].replace("p.kc", "")
+
+
+def test_plan_scan_several_columns():
+    d = Plan("select a, b as bb, c from t where a > 1 or c < 0").describe()
+    assert d["kind"] == "filter" and d["mode"] == "compiled" and d["project"] == ["a", "b", "c"]
+    assert [o["name"] for o in d["outputs"]] == ["a", "bb", "c"]
+    with pytest.raises(NutError, match="several projected columns"):
+        Plan("select a, b from t where a > 1 order by a")

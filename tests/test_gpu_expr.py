@@ -316,3 +316,20 @@ def test_sql_expression_scans(ex):
     got = ex.sql("select y from t where f between 0.1 and 0.2 order by y", cols)
     assert got["y"].tolist() == np.sort(y[(f >= 0.1) & (f <= 0.2)]).tolist()
     assert ex.sql("select x from t where x > 5000 or y > 5000", cols)["x"].tolist() == []
+
+
+def test_sql_scan_several_columns(ex):
+    """expression-mode scans project several int64 / float64 columns (one gather each)"""
+    rng = np.random.default_rng(23)
+    n = 300_001
+    x = rng.integers(-100, 100, n).astype(np.int64)
+    f = rng.random(n)
+    y = rng.integers(0, 1000, n).astype(np.int64)
+    cols = {"x": dev(x, ex), "f": dev(f, ex), "y": dev(y, ex)}
+    got = ex.sql("select y, f as ff, x from t where x > 10 and f < 0.5 limit 1000 offset 7", cols)
+    m = (x > 10) & (f < 0.5)
+    assert list(got) == ["y", "ff", "x"]
+    assert got["y"].tolist() == y[m][7:1007].tolist() and got["x"].tolist() == x[m][7:1007].tolist()
+    assert got["ff"].dtype == np.float64 and np.array_equal(got["ff"], f[m][7:1007])
+    got = ex.sql("select x, y from t", cols)
+    assert np.array_equal(got["x"], x) and np.array_equal(got["y"], y)

@@ -480,7 +480,7 @@ def test_plan_tpch_q6_global_aggregate():
 
 @pytest.mark.parametrize("sql,frag", [
     ("insert into t values (1)", "only SELECT"),
-    ("select a, b from t", "exactly one column"),
+    ("select a + 1 from t", "projects plain columns"),
     ("select sum(v) from t having sum(v) > 1", "HAVING needs GROUP BY"),
     ("select k, sum(v) from t group by k having k like 'x%'", "unsupported HAVING term"),
     ("select k from t group by k order by median(v)", "median"),
@@ -494,7 +494,7 @@ def test_plan_tpch_q6_global_aggregate():
     ("select k, sum(v + null) from t group by k", "NULL is executed only"),
     ("select k, sum(median(v)) from t group by k", "median"),
     ("select count(*), v from t", "no GROUP BY"),
-    ("select x, y from t where x > 1", "projects exactly one column"),
+    ("select x, y from t where x > 1 order by x", "several projected columns"),
     ("select x from t where x < 1 union all select x from t", "UNION"),
     ("select x from t where x >= toDate('1998-13-01')", "toDate"),
 ])
