@@ -978,7 +978,7 @@ bool lower_mode(const Statement &st, nut_plan &p, Lowering &L) {
   if (st.query.is_union) return L.fail("UNION/INTERSECT/EXCEPT are not executed (one query body per plan)");
   const QueryBody &b = *st.query.body;
   if (b.with) return L.fail("WITH is not executed");
-  if (b.distinct) return L.fail("DISTINCT is not executed");
+  if (b.distinct && b.group_by) return L.fail("DISTINCT with GROUP BY is not executed");
   if (!b.from || b.from->k != SourceKind::Table) return L.fail("FROM must name one table");
   if (b.joins.size() > 1) return L.fail("one JOIN per plan");
   if (!b.joins.empty()) {
@@ -1029,9 +1029,23 @@ bool lower_mode(const Statement &st, nut_plan &p, Lowering &L) {
   bool has_agg = false;
   for (const QueryExpr &q : b.columns)
     if (q.e.k == EK::FnCall && q.e.fn() == FnKind::Others) has_agg = true;
-  if (b.group_by || has_agg) {
-    // GROUP BY, or aggregates over the whole table (a global aggregate: no keys)
+  if (b.group_by || has_agg || b.distinct) {
+    // GROUP BY, or aggregates over the whole table (a global aggregate: no keys), or
+    // SELECT DISTINCT of 1-2 columns (= GROUP BY those columns, with a hidden COUNT)
     p.kind = NUT_PLAN_GROUPBY;
+    if (b.distinct) {
+      if (has_agg) return L.fail("DISTINCT over aggregates is not executed");
+      for (const QueryExpr &q : b.columns) {
+        sv name;
+        if (!column_ref(p, q.e, name)) return L.fail("SELECT DISTINCT takes columns");
+        p.keys.push_back(col_index(p, name));
+      }
+      if (p.keys.empty() || p.keys.size() > NUT_MAX_KEYS) return L.fail("SELECT DISTINCT takes 1 or 2 columns");
+      PlanAgg cnt{};
+      cnt.op = NUT_AGG_COUNT;
+      cnt.expr = NUT_EX_COL;
+      add_agg(p, cnt);
+    }
     if (b.group_by) {
       for (const QueryExpr &k : *b.group_by) {
         sv name;

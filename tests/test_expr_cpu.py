@@ -286,3 +286,14 @@ def test_plan_scan_several_columns():
     assert [o["name"] for o in d["outputs"]] == ["a", "bb", "c"]
     with pytest.raises(NutError, match="several projected columns"):
         Plan("select a, b from t where a > 1 order by a")
+
+
+def test_plan_select_distinct():
+    d = Plan("select distinct k, j from t where x > 3 order by k desc limit 5").describe()
+    assert d["kind"] == "groupby" and d["keys"] == ["k", "j"] and d["aggs"] == [{"op": "count"}]
+    assert [o["name"] for o in d["outputs"]] == ["k", "j"]
+    for sql, msg in [("select distinct count(*) from t", "over aggregates"),
+                     ("select distinct k from t group by k", "with GROUP BY"),
+                     ("select distinct a, b, c from t", "1 or 2 columns")]:
+        with pytest.raises(NutError, match=msg):
+            Plan(sql)

@@ -333,3 +333,19 @@ def test_sql_scan_several_columns(ex):
     assert got["ff"].dtype == np.float64 and np.array_equal(got["ff"], f[m][7:1007])
     got = ex.sql("select x, y from t", cols)
     assert np.array_equal(got["x"], x) and np.array_equal(got["y"], y)
+
+
+def test_sql_select_distinct(ex):
+    rng = np.random.default_rng(29)
+    n = 400_003
+    k = rng.integers(0, 50, n).astype(np.int64)
+    j = rng.integers(-3, 3, n).astype(np.int64)
+    x = rng.random(n)
+    cols = {"k": dev(k, ex), "j": dev(j, ex), "x": dev(x, ex)}
+    got = ex.sql("select distinct k from t where x > 0.5", cols)
+    assert got["k"].tolist() == np.unique(k[x > 0.5]).tolist()
+    got = ex.sql("select distinct k, j from t where k < 10 or x < 0.01 order by k desc", cols)
+    m = (k < 10) | (x < 0.01)
+    gk = got["k"].tolist()
+    assert gk == sorted(gk, reverse=True)
+    assert sorted(zip(gk, got["j"].tolist())) == sorted(set(zip(k[m].tolist(), j[m].tolist())))
