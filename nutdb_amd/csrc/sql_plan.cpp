@@ -1380,13 +1380,27 @@ struct DevBuf {
 
 nut_status build_spec(const nut_plan &p, const nut_column *const *bound, const Dict *const *dicts, uint64_t n,
                       nut_agg_spec &s, std::deque<std::vector<nut_prog_node>> &store, std::vector<int> &agg_f64);
+PProg and_all(const std::vector<PProg> &cs);
+PProg pred_prog(const PlanPred &pr);
 
 nut_status exec_scan(nut_ctx *c, const nut_plan &p, const nut_column *const *bound, const Dict *const *dicts,
                      uint64_t n, nut_result *r) {
   const nut_column *col = bound[p.proj];
+  if (!p.compiled && p.kind == NUT_PLAN_FILTER && dicts && dicts[p.proj]) {
+    // a string column: rerun as an expression-mode scan (codes gathered, then decoded)
+    nut_plan q = p;
+    std::vector<PProg> cs;
+    for (const PlanPred &pr : p.preds) cs.push_back(pred_prog(pr));
+    q.compiled = true;
+    q.preds.clear();
+    q.where = and_all(cs);
+    return exec_scan(c, q, bound, dicts, n, r);
+  }
+  // string columns: expression-mode FILTER scans gather their codes and decode on output
   for (int pj : p.projs)
-    if (dicts && dicts[pj])
-      return fail(NUT_ERR_PLAN, "column '" + p.cols[pj] + "' holds strings: scans / sorts of strings are not executed");
+    if (dicts && dicts[pj] && !(p.compiled && p.kind == NUT_PLAN_FILTER))
+      return fail(NUT_ERR_PLAN, "column '" + p.cols[pj] + "' holds strings: sorts and single-column fused scans of "
+                                "strings are not executed");
   for (const PlanPred &pr : p.preds)
     if (pr.c.is_str) return fail(NUT_ERR_PLAN, "string constant " + cval_str(pr.c) + " compared with an int64 column");
   // fused scans and sorts: int64; expression-mode FILTER scans: int64 or float64 columns
@@ -1395,7 +1409,7 @@ nut_status exec_scan(nut_ctx *c, const nut_plan &p, const nut_column *const *bou
       return fail(NUT_ERR_PLAN, "column '" + p.cols[pj] + "' must be int64 for this scan/sort");
   for (size_t j = 0; j < p.projs.size(); ++j) {
     r->names.push_back(p.outs[j].name);
-    r->types.push_back(bound[p.projs[j]]->type);
+    r->types.push_back(dicts && dicts[p.projs[j]] ? NUT_T_STR : bound[p.projs[j]]->type);
   }
   int op = NUT_GE;
   int64_t k = INT64_MIN;  // no predicate: every row passes
@@ -1464,6 +1478,19 @@ nut_status exec_scan(nut_ctx *c, const nut_plan &p, const nut_column *const *bou
   if (p.has_limit) rows = std::min(rows, p.limit);
   r->dev_off = off;
   r->nrows = rows;
+  for (size_t j = 0; j < p.projs.size(); ++j) {  // decode string columns (codes -> text)
+    if (r->types[j] != NUT_T_STR) continue;
+    r->strs.resize(p.projs.size());
+    std::vector<int64_t> codes(rows);
+    if (rows) NUT_HIP(hipMemcpy(codes.data(), (const int64_t *)r->dev + j * r->dev_stride + off, rows * 8,
+                                hipMemcpyDeviceToHost));
+    const Dict *d = dicts[p.projs[j]];
+    r->strs[j].reserve(rows);
+    for (int64_t cde : codes) {
+      const std::string *v = d->decode(cde);
+      r->strs[j].push_back(v ? *v : std::string());
+    }
+  }
   return NUT_OK;
 }
 
@@ -2430,6 +2457,7 @@ nut_status nut_result_to_host(const nut_result *r, int j, void *dst, uint64_t ca
     memcpy(dst, r->host[j].data(), r->nrows * 8);
     return NUT_OK;
   }
+  if (r->types[j] == NUT_T_STR) return fail(NUT_ERR_INVALID_ARG, "nut_result_to_host: string column (use nut_result_string)");
   DeviceGuard g(r->device);
   NUT_HIP(hipMemcpy(dst, (const int64_t *)r->dev + (uint64_t)j * r->dev_stride + r->dev_off, r->nrows * 8,
                     hipMemcpyDeviceToHost));
