@@ -341,6 +341,50 @@ struct nut_result {
 
 namespace {
 
+// internal program leaves (never reach nut_prog): `col [I]LIKE 'pattern'` over a
+// dictionary column, expanded at execution into equalities with the matching strings
+constexpr int P_LIKE = 1000, P_ILIKE = 1001;
+
+int pnode_arity(int op) {
+  if (op == P_LIKE || op == P_ILIKE) return 0;
+  return op <= NUT_P_F64 ? 0 : (op == NUT_P_NOT || op == NUT_P_BITNOT || op == NUT_P_ABS ||
+                                op == NUT_P_TO_F64) ? 1 : op == NUT_P_IF ? 3 : 2;
+}
+
+// SQL LIKE: % any run, _ any one byte, backslash escapes the next pattern byte;
+// ILIKE folds ASCII case
+bool like_match(const std::string &str, const std::string &pat, bool ci) {
+  auto eq = [&](char a, char b) {
+    if (ci) {
+      a = (char)tolower((unsigned char)a);
+      b = (char)tolower((unsigned char)b);
+    }
+    return a == b;
+  };
+  size_t s = 0, p = 0, star_p = std::string::npos, star_s = 0;
+  while (s < str.size()) {
+    if (p < pat.size() && pat[p] == '%') {
+      star_p = ++p;
+      star_s = s;
+      continue;
+    }
+    if (p < pat.size()) {
+      const bool esc = pat[p] == '\\' && p + 1 < pat.size();
+      const char pc = esc ? pat[p + 1] : pat[p];
+      if ((!esc && pc == '_') || eq(pc, str[s])) {
+        p += esc ? 2 : 1;
+        ++s;
+        continue;
+      }
+    }
+    if (star_p == std::string::npos) return false;
+    p = star_p;
+    s = ++star_s;
+  }
+  while (p < pat.size() && pat[p] == '%') ++p;
+  return p == pat.size();
+}
+
 int col_index(nut_plan &p, sv name) {
   for (size_t i = 0; i < p.cols.size(); ++i)
     if (ieq(p.cols[i], name)) return (int)i;
@@ -643,8 +687,21 @@ bool lower_prog(nut_plan &p, const Expr &e, PProg &o, Lowering &L) {
         }
         return true;
       }
+      if (b == BinOp::Like || b == BinOp::NotLike || b == BinOp::ILike || b == BinOp::NotILike) {
+        sv cname;
+        CVal pat;
+        if (!column_ref(p, e.kids[0], cname) || !const_eval(e.kids[1], pat, L) || !pat.is_str)
+          return L.fail("LIKE takes a column and a string pattern ('" + expr_text(e) + "')");
+        PNode n;
+        n.op = (b == BinOp::ILike || b == BinOp::NotILike) ? P_ILIKE : P_LIKE;
+        n.col = col_index(p, cname);
+        n.c = pat;
+        o.push_back(n);
+        if (b == BinOp::NotLike || b == BinOp::NotILike) emit(o, NUT_P_NOT);
+        return true;
+      }
       const int op = prog_binop(b);
-      if (op < 0) return L.fail("operator in '" + expr_text(e) + "' is not executed (LIKE, [] and friends)");
+      if (op < 0) return L.fail("operator in '" + expr_text(e) + "' is not executed ([] and friends)");
       PProg l, r;
       if (!lower_prog(p, e.kids[0], l, L) || !lower_prog(p, e.kids[1], r, L)) return false;
       if (op == NUT_P_EQ || op == NUT_P_NE) {
@@ -1163,7 +1220,9 @@ std::string prog_text(const nut_plan &p, const PProg &pp) {
       if (!st.empty()) st.pop_back();
       return t;
     };
-    if (n.op == NUT_P_COL) st.push_back(p.cols[n.col]);
+    if (n.op == P_LIKE || n.op == P_ILIKE)
+      st.push_back("(" + p.cols[n.col] + (n.op == P_LIKE ? " like " : " ilike ") + cval_str(n.c) + ")");
+    else if (n.op == NUT_P_COL) st.push_back(p.cols[n.col]);
     else if (n.op == NUT_P_I64 || n.op == NUT_P_F64) st.push_back(cval_str(n.c));
     else if (n.op == NUT_P_NOT || n.op == NUT_P_BITNOT || n.op == NUT_P_ABS || n.op == NUT_P_TO_F64) {
       const char *f = n.op == NUT_P_NOT ? "not" : n.op == NUT_P_BITNOT ? "~" : n.op == NUT_P_ABS ? "abs" : "toFloat64";
@@ -1547,8 +1606,7 @@ nut_status check_strings(const nut_plan &p, const PProg &pp, const Dict *const *
   std::vector<char> st;
   for (const PNode &n : pp) {
     const int op = n.op;
-    const int k = op <= NUT_P_F64 ? 0 : (op == NUT_P_NOT || op == NUT_P_BITNOT || op == NUT_P_ABS ||
-                                         op == NUT_P_TO_F64) ? 1 : op == NUT_P_IF ? 3 : 2;
+    const int k = pnode_arity(op);
     char a[3] = {0, 0, 0};
     for (int i = k - 1; i >= 0; --i) {
       if (st.empty()) return NUT_OK;  // malformed: nut_prog_type reports it
@@ -1588,7 +1646,63 @@ nut_status build_spec(const nut_plan &p, const nut_column *const *bound, const D
     // expression mode: bind the programs' columns (first use order) and constants
     s.prog_mode = 1;
     std::vector<int> pcol(p.cols.size(), -1);
-    auto resolve = [&](const PProg &pp, nut_prog &out, const char *what, int32_t *type) -> nut_status {
+    std::deque<PProg> expanded;
+    auto resolve = [&](const PProg &pp0, nut_prog &out, const char *what, int32_t *type) -> nut_status {
+      // [I]LIKE over a dictionary column -> OR of equalities with the matching strings
+      expanded.emplace_back();
+      PProg &pp = expanded.back();
+      for (const PNode &n : pp0) {
+        if (n.op != P_LIKE && n.op != P_ILIKE) {
+          pp.push_back(n);
+          continue;
+        }
+        PNode zero;
+        zero.op = NUT_P_I64;
+        zero.c.is_int = true;
+        zero.c.v = 0;
+        std::vector<std::string> hits;
+        if (dicts) {
+          const Dict *d = dicts[n.col];
+          if (!d) return fail(NUT_ERR_PLAN, "LIKE needs a string column ('" + p.cols[n.col] + "')");
+          auto test = [&](const std::string &v) {
+            if (like_match(v, n.c.s, n.op == P_ILIKE)) hits.push_back(v);
+          };
+          if (d->fixed) {
+            for (const auto &kv : d->codes) test(kv.first);
+          } else {
+            for (const std::string &v : d->strs) test(v);
+          }
+          if (hits.size() > 48)
+            return fail(NUT_ERR_PLAN, "LIKE " + cval_str(n.c) + " matches " + std::to_string(hits.size()) +
+                                          " strings of '" + p.cols[n.col] + "' (at most 48)");
+        }
+        if (hits.empty()) {  // false (also the compile-only shape of nut_plan_prepare)
+          pp.push_back(zero);
+          pp.push_back(zero);
+          PNode ne;
+          ne.op = NUT_P_NE;
+          pp.push_back(ne);
+          continue;
+        }
+        for (size_t h = 0; h < hits.size(); ++h) {
+          PNode col, k, eqn;
+          col.op = NUT_P_COL;
+          col.col = n.col;
+          k.op = NUT_P_I64;
+          k.col = n.col;
+          k.c.is_str = true;
+          k.c.s = hits[h];
+          eqn.op = NUT_P_EQ;
+          pp.push_back(col);
+          pp.push_back(k);
+          pp.push_back(eqn);
+          if (h) {
+            PNode orn;
+            orn.op = NUT_P_OR;
+            pp.push_back(orn);
+          }
+        }
+      }
       store.emplace_back();
       std::vector<nut_prog_node> &v = store.back();
       for (const PNode &n : pp) {
@@ -1909,8 +2023,7 @@ void split_and(const PProg &pp, std::vector<PProg> &out) {
   std::vector<size_t> st;
   for (size_t i = 0; i + 1 < pp.size(); ++i) {
     const int op = pp[i].op;
-    const int k = op <= NUT_P_F64 ? 0 : (op == NUT_P_NOT || op == NUT_P_BITNOT || op == NUT_P_ABS ||
-                                         op == NUT_P_TO_F64) ? 1 : op == NUT_P_IF ? 3 : 2;
+    const int k = pnode_arity(op);
     size_t start = i;
     for (int j = 0; j < k; ++j) {
       start = st.back();

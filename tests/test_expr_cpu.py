@@ -297,3 +297,11 @@ def test_plan_select_distinct():
                      ("select distinct a, b, c from t", "1 or 2 columns")]:
         with pytest.raises(NutError, match=msg):
             Plan(sql)
+
+
+def test_plan_like():
+    d = Plan("select count(*) from t where s like 'AB%' and not (s ilike '%x_')").describe()
+    assert d["mode"] == "compiled" and d["where_expr"] == "((s like 'AB%') and not((s ilike '%x_')))"
+    assert Plan("select s from t where s not like '%Z'").describe()["where_expr"] == "not((s like '%Z'))"
+    with pytest.raises(NutError, match="string pattern"):
+        Plan("select count(*) from t where s like 3")

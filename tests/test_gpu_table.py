@@ -225,3 +225,47 @@ def test_scans_of_string_columns(ex):
     assert got["k"].tolist() == k[m][:50].tolist() and got["s"].tolist() == s[m][:50].tolist()
     assert got["e"].tolist() == e[m][:50].tolist()
     assert t.sql("select s from t")["s"].tolist() == s.tolist()
+
+
+def _like(v, pat, ci=False):
+    import re
+    rx = ""
+    i = 0
+    while i < len(pat):
+        ch = pat[i]
+        if ch == "\\" and i + 1 < len(pat):
+            rx += re.escape(pat[i + 1])
+            i += 2
+            continue
+        rx += ".*" if ch == "%" else "." if ch == "_" else re.escape(ch)
+        i += 1
+    return re.fullmatch(rx, v, re.S | (re.I if ci else 0)) is not None
+
+
+def test_like_on_dictionary_columns(ex):
+    """[NOT] [I]LIKE over String / Enum columns: evaluated once per dictionary string (the
+    matching codes become equalities), in scans, aggregates and joins' pushed WHERE."""
+    rng = np.random.default_rng(43)
+    n = 200_003
+    types = np.array(["STANDARD POLISHED BRASS", "SMALL BRUSHED TIN", "LARGE PLATED BRASS", "ECONOMY ANODIZED STEEL",
+                      "PROMO BURNISHED COPPER", "MEDIUM POLISHED brass", "50%_OFF", "50X_OFF"], dtype=object)
+    ty = types[rng.integers(0, len(types), n)]
+    size = rng.integers(1, 50, n)
+    t = Table(ex, "CREATE TABLE part (p_type String, p_size Int64, p_e Enum('red' = 1, 'green' = 2))")
+    pe = np.array(["red", "green"], dtype=object)[rng.integers(0, 2, n)]
+    t.append(p_type=ty, p_size=size, p_e=pe)
+    for where, m in [
+        ("p_type like '%BRASS'", np.array([_like(v, "%BRASS") for v in ty])),
+        ("p_type ilike '%brass'", np.array([_like(v, "%brass", True) for v in ty])),
+        ("p_type not like 'S%'", np.array([not _like(v, "S%") for v in ty])),
+        ("p_type like '_MALL%' or p_size > 45", np.array([_like(v, "_MALL%") for v in ty]) | (size > 45)),
+        ("p_type like '50\\\\%\\\\_OFF'", ty == "50%_OFF"),
+        ("p_type like 'NOTHING%'", np.zeros(n, bool)),
+        ("p_e like 'gr%'", pe == "green"),
+    ]:
+        got = t.sql(f"select count(*) as c, sum(p_size) as s from part where {where}")
+        assert got["c"].tolist() == [int(m.sum())] and got["s"].tolist() == [int(size[m].sum())], where
+    got = t.sql("select p_size from part where p_type like '%TIN' and p_size < 10")
+    assert got["p_size"].tolist() == size[(ty == "SMALL BRUSHED TIN") & (size < 10)].tolist()
+    with pytest.raises(NutError, match="LIKE needs a string column"):
+        t.sql("select count(*) from part where p_size like '1%'")
