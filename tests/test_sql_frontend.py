@@ -485,7 +485,7 @@ def test_plan_tpch_q6_global_aggregate():
     ("select k, sum(v) from t group by k having k like 'x%'", "unsupported HAVING term"),
     ("select k from t group by k order by median(v)", "median"),
     ("select k, median(v) from t group by k", "median"),
-    ("select x from t where y like 'a%'", "LIKE"),
+    ("select x from t where y like z", "string pattern"),
     ("select k, sum(v) from t full join u on a = b group by k", "FULL OUTER"),
     ("select k, v from t group by k", "neither a GROUP BY key"),
     ("select k, sum(v like 'x') from t group by k", "not executed"),
