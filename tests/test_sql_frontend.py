@@ -488,7 +488,7 @@ def test_plan_tpch_q6_global_aggregate():
     ("select x from t where y like z", "string pattern"),
     ("select k, sum(v) from t full join u on a = b group by k", "FULL OUTER"),
     ("select k, v from t group by k", "neither a GROUP BY key"),
-    ("select k, sum(v like 'x') from t group by k", "not executed"),
+    ("select k, sum(v[1]) from t group by k", "not executed"),
     ("select k, sum(multiIf(v, 1)) from t group by k", "multiIf takes"),
     ("select k, sum(sum(v)) from t group by k", "nested inside an expression"),
     ("select k, sum(v + null) from t group by k", "NULL is executed only"),
