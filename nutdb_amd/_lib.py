@@ -177,6 +177,7 @@ SIGNATURES = {
     "nut_plan_free": (None, [_P]),
     "nut_plan_execute": (_I32, [_P, _P, _P, _I32, _U64, _U64, C.POINTER(_P)]),
     "nut_plan_execute2": (_I32, [_P, _P, _P, _I32, _U64, _P, _I32, _U64, _U64, C.POINTER(_P)]),
+    "nut_plan_executen": (_I32, [_P, _P, C.POINTER(_P), C.POINTER(_I32), C.POINTER(_U64), _I32, _U64, C.POINTER(_P)]),
     "nut_result_shape": (_I32, [_P, C.POINTER(_U64), C.POINTER(_I32)]),
     "nut_result_column": (_I32, [_P, _I32, C.POINTER(_I32), C.POINTER(C.c_char_p)]),
     "nut_result_to_host": (_I32, [_P, _I32, _P, _U64]),

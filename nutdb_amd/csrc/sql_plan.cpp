@@ -320,6 +320,12 @@ struct nut_plan {
   // JOIN (one JoinClause with ON a = b), executed by nut_plan_execute2: a hash join
   // (nut_join_i64) then gathers into the joined table the rest of the plan runs on
   int join = -1;           // nut_join_type; -1: no JOIN
+  // several INNER JoinClauses (nut_plan_executen): table k+1 joins on jn[k].key
+  struct JoinStep {
+    std::string table, alias;
+    int key[2];
+  };
+  std::vector<JoinStep> jn;
   bool jright = false;     // RIGHT OUTER / SEMI / ANTI: the JOIN source is the preserved side
   std::string jtable, talias, jalias;  // JOIN source; FROM / JOIN aliases (qualifiers)
   int jkey[2] = {-1, -1};  // plan columns of the ON equality
@@ -1037,8 +1043,31 @@ bool lower_mode(const Statement &st, nut_plan &p, Lowering &L) {
   if (b.with) return L.fail("WITH is not executed");
   if (b.distinct && b.group_by) return L.fail("DISTINCT with GROUP BY is not executed");
   if (!b.from || b.from->k != SourceKind::Table) return L.fail("FROM must name one table");
-  if (b.joins.size() > 1) return L.fail("one JOIN per plan");
-  if (!b.joins.empty()) {
+  if (b.joins.size() > 1) {  // a chain of INNER joins: FROM t0 JOIN t1 ON .. JOIN t2 ON ..
+    p.join = NUT_JOIN_INNER;
+    if (b.from->alias) p.talias = std::string(*b.from->alias);
+    for (const JoinClause &jc : b.joins) {
+      if (jc.src.k != SourceKind::Table) return L.fail("JOIN source must be a table");
+      if (!jc.on) return L.fail("JOIN ... USING is not executed (ON a = b)");
+      if (jc.t != JoinType::Inner) return L.fail("several JOINs: INNER only");
+      const Expr &cnd = jc.cond;
+      sv ka, kb;
+      if (!(cnd.k == EK::BinaryOp && cnd.bop() == BinOp::Eq && column_ref(p, cnd.kids[0], ka) &&
+            column_ref(p, cnd.kids[1], kb)))
+        return L.fail("JOIN ON must be one equality of two columns");
+      nut_plan::JoinStep js;
+      js.table = std::string(jc.src.table);
+      if (jc.src.alias) js.alias = std::string(*jc.src.alias);
+      js.key[0] = col_index(p, ka);
+      js.key[1] = col_index(p, kb);
+      p.jn.push_back(js);
+    }
+    if (p.jn.size() > 7) return L.fail("at most 8 joined tables");
+    p.jtable = p.jn[0].table;
+    p.jalias = p.jn[0].alias;
+    p.jkey[0] = p.jn[0].key[0];
+    p.jkey[1] = p.jn[0].key[1];
+  } else if (!b.joins.empty()) {
     const JoinClause &jc = b.joins[0];
     if (jc.src.k != SourceKind::Table) return L.fail("JOIN source must be a table");
     if (!jc.on) return L.fail("JOIN ... USING is not executed (ON a = b)");
@@ -1368,6 +1397,20 @@ std::string describe(const nut_plan &p) {
     o += ',';
     json_str(o, p.cols[p.jkey[1]]);
     o += "]}";
+    if (!p.jn.empty()) {
+      o += ",\"joins\":[";
+      for (size_t k = 0; k < p.jn.size(); ++k) {
+        if (k) o += ',';
+        o += "{\"table\":";
+        json_str(o, p.jn[k].table);
+        o += ",\"on\":[";
+        json_str(o, p.cols[p.jn[k].key[0]]);
+        o += ',';
+        json_str(o, p.cols[p.jn[k].key[1]]);
+        o += "]}";
+      }
+      o += ']';
+    }
   }
   o += ",\"offset\":" + std::to_string(p.offset) + "}";
   return o;
@@ -2304,6 +2347,187 @@ nut_status exec_join(nut_ctx *c, const nut_plan &p, const nut_column *lc, int nl
 
 }  // namespace
 
+namespace {
+
+// A chain of INNER joins (nut_plan_executen): FROM t0 JOIN t1 ON .. JOIN t2 ON ..  Single-
+// table WHERE conjuncts are pushed down per table; the accumulated join result is kept as
+// one row-id array per joined table (the probe side); each step builds on the next table.
+nut_status exec_joinn(nut_ctx *c, const nut_plan &p, const nut_column *const *tabs, const int *ncols,
+                      const uint64_t *nrows, int nt, uint64_t hint, nut_result *r) {
+  const size_t nc = p.cols.size();
+  if (nt != (int)p.jn.size() + 1)
+    return fail(NUT_ERR_INVALID_ARG, "nut_plan_executen: the plan joins " + std::to_string(p.jn.size() + 1) +
+                                         " tables, got " + std::to_string(nt));
+  std::vector<std::string> tname(nt), talias(nt);
+  tname[0] = p.table;
+  talias[0] = p.talias;
+  for (int k = 1; k < nt; ++k) tname[k] = p.jn[k - 1].table, talias[k] = p.jn[k - 1].alias;
+  auto find = [&](const std::string &name, int t) -> const nut_column * {
+    for (int i = 0; i < ncols[t]; ++i)
+      if (tabs[t][i].name && ieq(tabs[t][i].name, name)) return &tabs[t][i];
+    return nullptr;
+  };
+  std::vector<int> side(nc);
+  std::vector<const nut_column *> src(nc);
+  for (size_t i = 0; i < nc; ++i) {
+    const std::string &nm = p.cols[i];
+    int hit = -1, nh = 0;
+    for (int t = 0; t < nt; ++t)
+      if (find(nm, t)) hit = t, ++nh;
+    const nut_column *col = hit >= 0 ? find(nm, hit) : nullptr;
+    const size_t dot = nm.find('.');
+    if (!nh && dot != std::string::npos) {
+      const std::string q = nm.substr(0, dot), cn = nm.substr(dot + 1);
+      for (int t = 0; t < nt; ++t)
+        if (ieq(q, tname[t]) || (!talias[t].empty() && ieq(q, talias[t]))) hit = t, ++nh;
+      if (nh > 1) return fail(NUT_ERR_PLAN, "qualifier '" + q + "' names several tables (use aliases)");
+      if (nh == 0) return fail(NUT_ERR_PLAN, "qualifier '" + q + "' names no joined table");
+      col = find(cn, hit);
+      if (!col) nh = 0;
+    }
+    if (nh > 1) return fail(NUT_ERR_INVALID_ARG, "nut_plan_executen: column '" + nm + "' is in several tables");
+    if (!col) return fail(NUT_ERR_INVALID_ARG, "nut_plan_executen: column '" + nm + "' is not bound");
+    if (col->type != NUT_T_I64 && col->type != NUT_T_F64)
+      return fail(NUT_ERR_INVALID_ARG, "nut_plan_executen: column '" + nm + "' has an unknown type");
+    if (nrows[hit] && !col->data) return fail(NUT_ERR_INVALID_ARG, "nut_plan_executen: column '" + nm + "' is NULL");
+    side[i] = hit;
+    src[i] = col;
+  }
+  std::vector<int> knew(nt - 1), kold(nt - 1);
+  for (int k = 0; k + 1 < nt; ++k) {
+    const int a = p.jn[k].key[0], b = p.jn[k].key[1], t = k + 1;
+    if (side[a] == t && side[b] < t) knew[k] = a, kold[k] = b;
+    else if (side[b] == t && side[a] < t) knew[k] = b, kold[k] = a;
+    else return fail(NUT_ERR_PLAN, "JOIN " + std::to_string(t) + ": ON must compare a column of '" + tname[t] +
+                                       "' with a column of an earlier table");
+    if (src[a]->type != NUT_T_I64 || src[b]->type != NUT_T_I64) return fail(NUT_ERR_PLAN, "JOIN keys must be int64 columns");
+  }
+  nut_plan p2 = p;
+  std::vector<std::vector<PProg>> push(nt);
+  if (p.compiled) {
+    std::vector<PProg> conj, keep;
+    split_and(p.where, conj);
+    for (PProg &cj : conj) {
+      int sd = -1;
+      for (const PNode &nd : cj)
+        if (nd.op == NUT_P_COL || nd.op == P_LIKE || nd.op == P_ILIKE) sd = sd < 0 || sd == side[nd.col] ? side[nd.col] : nt;
+      (sd >= 0 && sd < nt ? push[sd] : keep).push_back(std::move(cj));
+    }
+    p2.where = and_all(keep);
+  } else {
+    p2.preds.clear();
+    for (const PlanPred &pr : p.preds) push[side[pr.col]].push_back(pred_prog(pr));
+  }
+  const std::vector<const Dict *> nodict(nc + 1, nullptr);
+  std::vector<DevBuf> ids(nt);
+  std::vector<uint64_t> rows(nrows, nrows + nt);
+  for (int t = 0; t < nt; ++t) {
+    if (push[t].empty() || p.never) continue;
+    nut_plan q;
+    q.compiled = true;
+    q.cols = p.cols;
+    q.where = and_all(push[t]);
+    nut_agg_spec spec;
+    std::deque<std::vector<nut_prog_node>> store;
+    std::vector<int> agg_f64;
+    nut_status es = build_spec(q, src.data(), nodict.data(), rows[t], spec, store, agg_f64);
+    if (es) return es;
+    NUT_HIP(hipMalloc(&ids[t].p, std::max<uint64_t>(rows[t], 1) * 8));
+    uint64_t cnt = 0;
+    if (rows[t]) es = nut_select_rows(c, &spec, (int64_t *)ids[t].p, &cnt);
+    if (es) return es;
+    rows[t] = cnt;
+  }
+  auto gather_to = [&](const void *col, const int64_t *idx, uint64_t n, DevBuf &out) -> nut_status {
+    if (hipMalloc(&out.p, std::max<uint64_t>(n, 1) * 8) != hipSuccess) return fail(NUT_ERR_OOM, "hipMalloc (join)");
+    return n ? nut_gather_u64(c, (const uint64_t *)col, idx, n, 0, (uint64_t *)out.p) : NUT_OK;
+  };
+  std::vector<DevBuf> acc(nt);
+  std::vector<const int64_t *> accp(nt, nullptr);
+  accp[0] = (const int64_t *)ids[0].p;
+  uint64_t ncur = rows[0];
+  nut_status st = NUT_OK;
+  for (int k = 0; k + 1 < nt && !st; ++k) {
+    const int t = k + 1, u = side[kold[k]];
+    DevBuf pk, bk;
+    const int64_t *pkd = (const int64_t *)src[kold[k]]->data, *bkd = (const int64_t *)src[knew[k]]->data;
+    if (accp[u]) {
+      if ((st = gather_to(pkd, accp[u], ncur, pk))) break;
+      pkd = (const int64_t *)pk.p;
+    }
+    if (ids[t].p) {
+      if ((st = gather_to(bkd, (const int64_t *)ids[t].p, rows[t], bk))) break;
+      bkd = (const int64_t *)bk.p;
+    }
+    DevBuf pairs;
+    uint64_t cap = std::max<uint64_t>(ncur, 1), m = 0;
+    for (;;) {
+      if (hipMalloc(&pairs.p, cap * 16) != hipSuccess) return fail(NUT_ERR_OOM, "hipMalloc (join index)");
+      st = nut_join_i64_into(c, bkd, rows[t], pkd, ncur, NUT_JOIN_INNER, (int64_t *)pairs.p,
+                             (int64_t *)pairs.p + cap, cap, &m);
+      if (st != NUT_ERR_CAPACITY || m <= cap) break;
+      NUT_HIP(hipFree(pairs.p));
+      pairs.p = nullptr;
+      cap = m;
+    }
+    if (st) break;
+    const int64_t *pi = (const int64_t *)pairs.p, *bi = pi + cap;
+    std::vector<DevBuf> next(nt);
+    for (int v = 0; v <= t && !st; ++v) {
+      const int64_t *base = v == t ? (const int64_t *)ids[t].p : accp[v];
+      const int64_t *through = v == t ? bi : pi;
+      if (base) {
+        st = gather_to(base, through, m, next[v]);
+      } else {
+        if (hipMalloc(&next[v].p, std::max<uint64_t>(m, 1) * 8) != hipSuccess) return fail(NUT_ERR_OOM, "hipMalloc");
+        if (m) NUT_HIP(hipMemcpyAsync(next[v].p, through, m * 8, hipMemcpyDeviceToDevice, c->stream));
+      }
+    }
+    if (st) break;
+    NUT_HIP(hipStreamSynchronize(c->stream));
+    for (int v = 0; v <= t; ++v) {
+      std::swap(acc[v].p, next[v].p);
+      accp[v] = (const int64_t *)acc[v].p;
+    }
+    ncur = m;
+  }
+  if (st) return st;
+  auto in_prog = [](const PProg &pp, int i) {
+    for (const PNode &nd : pp)
+      if ((nd.op == NUT_P_COL || nd.op == P_LIKE || nd.op == P_ILIKE) && nd.col == i) return true;
+    return false;
+  };
+  std::vector<DevBuf> bufs(nc);
+  std::vector<nut_column> jc(nc);
+  for (size_t i = 0; i < nc; ++i) {
+    const int ci = (int)i;
+    bool used = ci == p2.proj || in_prog(p2.where, ci);
+    for (int pj : p2.projs) used = used || pj == ci;
+    for (int k2 : p2.keys) used = used || k2 == ci;
+    for (const PlanPred &pr : p2.preds) used = used || pr.col == ci;
+    for (int v : p2.vals) used = used || v == ci;
+    for (const PlanAgg &a : p2.aggs) {
+      for (int ref : a.refs) used = used || ref == ci;
+      used = used || in_prog(a.val, ci) || in_prog(a.mask, ci);
+    }
+    if (!used || !accp[side[i]]) {
+      jc[i] = nut_column{p.cols[i].c_str(), src[i]->data, src[i]->type};
+      continue;
+    }
+    st = gather_to(src[i]->data, accp[side[i]], ncur, bufs[i]);
+    if (st) return st;
+    jc[i] = nut_column{p.cols[i].c_str(), bufs[i].p, src[i]->type};
+  }
+  std::vector<const nut_column *> bound(nc);
+  for (size_t i = 0; i < nc; ++i) bound[i] = &jc[i];
+  st = p2.kind == NUT_PLAN_GROUPBY ? exec_groupby(c, p2, bound.data(), nodict.data(), ncur, hint, r)
+                                   : exec_scan(c, p2, bound.data(), nodict.data(), ncur, r);
+  NUT_HIP(hipStreamSynchronize(c->stream));
+  return st;
+}
+
+}  // namespace
+
 extern "C" {
 
 nut_status nut_sql_parse(const char *sql, size_t len, nut_stmt **out) {
@@ -2433,6 +2657,7 @@ nut_status nut_plan_execute2(nut_ctx *c, const nut_plan *p, const nut_column *le
   if (!c || !p || !out || (nleft && !left) || (nright && !right) || nleft < 0 || nright < 0)
     return fail(NUT_ERR_INVALID_ARG, "nut_plan_execute2: NULL argument");
   if (p->join < 0) return nut_plan_execute(c, p, left, nleft, lrows, group_hint, out);
+  if (!p->jn.empty()) return fail(NUT_ERR_INVALID_ARG, "nut_plan_execute2: the plan joins several tables (nut_plan_executen)");
   *out = nullptr;
   nut_result *r = new (std::nothrow) nut_result;
   if (!r) return fail(NUT_ERR_OOM, "nut_plan_execute2: out of host memory");
@@ -2440,6 +2665,31 @@ nut_status nut_plan_execute2(nut_ctx *c, const nut_plan *p, const nut_column *le
   r->device = c->device;
   DeviceGuard g(c->device);
   nut_status st = exec_join(c, *p, left, nleft, lrows, right, nright, rrows, group_hint, r);
+  if (st) {
+    nut_result_free(r);
+    return st;
+  }
+  *out = r;
+  return NUT_OK;
+}
+
+nut_status nut_plan_executen(nut_ctx *c, const nut_plan *p, const nut_column *const *tables, const int *ncols,
+                             const uint64_t *nrows, int ntables, uint64_t group_hint, nut_result **out) {
+  if (!c || !p || !out || !tables || !ncols || !nrows || ntables < 1)
+    return fail(NUT_ERR_INVALID_ARG, "nut_plan_executen: NULL argument");
+  if (p->jn.empty()) {
+    if (ntables == 1) return nut_plan_execute(c, p, tables[0], ncols[0], nrows[0], group_hint, out);
+    if (ntables == 2)
+      return nut_plan_execute2(c, p, tables[0], ncols[0], nrows[0], tables[1], ncols[1], nrows[1], group_hint, out);
+    return fail(NUT_ERR_INVALID_ARG, "nut_plan_executen: the plan joins fewer tables");
+  }
+  *out = nullptr;
+  nut_result *r = new (std::nothrow) nut_result;
+  if (!r) return fail(NUT_ERR_OOM, "nut_plan_executen: out of host memory");
+  r->kind = p->kind;
+  r->device = c->device;
+  DeviceGuard g(c->device);
+  nut_status st = exec_joinn(c, *p, tables, ncols, nrows, ntables, group_hint, r);
   if (st) {
     nut_result_free(r);
     return st;

@@ -512,6 +512,8 @@ class Executor:
         a JOIN takes the JOIN source's columns as `right` (`columns` = the FROM table)."""
         from .sql import Plan
         p = Plan(query)
+        if isinstance(right, (list, tuple)):  # several JOINs: one dict per JOIN source, in order
+            return p.execute_tables(self, [columns] + list(right), group_hint=group_hint)
         if right is not None or "join" in p.describe():
             return p.execute_join(self, columns, right or {}, group_hint=group_hint)
         return p.execute(self, columns, group_hint=group_hint)

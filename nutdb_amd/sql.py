@@ -213,6 +213,19 @@ class Plan:
                                     group_hint, C.byref(res)), "nut_plan_execute2")
         return read_result(res)
 
+    def execute_tables(self, ex, tables: list, group_hint: int = 0) -> Dict[str, np.ndarray]:
+        """A plan over several tables (nut_plan_executen): `tables` = [FROM columns, first
+        JOIN source's columns, ...], each {name: CUDA tensor}."""
+        bound = [self._bind(t) for t in tables]
+        k = len(tables)
+        arrs = (C.c_void_p * k)(*[C.cast(b[0], C.c_void_p) for b in bound])
+        nco = (C.c_int * k)(*[len(t) for t in tables])
+        nro = (C.c_uint64 * k)(*[b[2] or 0 for b in bound])
+        res = C.c_void_p()
+        ex._bind_stream()
+        check(lib.nut_plan_executen(ex.ctx, self._h, arrs, nco, nro, k, group_hint, C.byref(res)), "nut_plan_executen")
+        return read_result(res)
+
     def _bind(self, columns):
         import torch
         names = self.columns

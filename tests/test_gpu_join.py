@@ -330,3 +330,22 @@ def test_q12_join_bench_workload_parity(ex, orc):
     assert got["l_shipmode"].tolist() == [3, 5]
     assert got["high_line_count"].tolist() == [int(np.sum(hi & (mode == s))) for s in (3, 5)]
     assert got["low_line_count"].tolist() == [int(np.sum(~hi & (mode == s))) for s in (3, 5)]
+
+
+def test_sql_three_table_join(ex, orc):
+    """lineitem JOIN orders JOIN customer (nut_plan_executen): pushed-down WHERE on two
+    tables, a cross-table conjunct above the joins, group-by on the third table's column."""
+    orders, lines = tables(9, 40_000, 160_000)
+    rng = np.random.default_rng(90)
+    ncust = 50
+    cust = {"c_key": rng.permutation(ncust).astype(np.int64), "c_nation": rng.integers(0, 8, ncust).astype(np.int64)}
+    j = joined(orc, lines, "l_okey", orders, "o_okey", "inner")
+    cn = dict(zip(cust["c_key"].tolist(), cust["c_nation"].tolist()))
+    j["c_nation"] = [cn[k] for k in j.o_cust.tolist()]
+    m = (j.l_qty > 10) & (j.c_nation < 6) & (j.l_qty > j.o_cust)
+    g = j[m].groupby("c_nation").agg(n=("l_qty", "size"), q=("l_qty", "sum"))
+    got = ex.sql("select c_nation, count(*) as n, sum(l_qty) as q from lineitem join orders on l_okey = o_okey "
+                 "join customer on o_cust = c_key where l_qty > 10 and c_nation < 6 and l_qty > o_cust "
+                 "group by c_nation order by c_nation", on_dev(ex, lines), right=[on_dev(ex, orders), on_dev(ex, cust)])
+    assert got["c_nation"].tolist() == g.index.tolist()
+    assert got["n"].tolist() == g.n.tolist() and got["q"].tolist() == g.q.tolist()

@@ -74,7 +74,7 @@ def test_sql_no_join_has_no_join_key():
     ("select count(*) from a join b using (x)", "USING"),
     ("select count(*) from a join b on x < y", "one equality"),
     ("select count(*) from a join b on x = y and u = v", "one equality"),
-    ("select count(*) from a join b on x = y join c on y = z", "one JOIN"),
+    ("select count(*) from a join b on x = y full join c on y = z", "INNER only"),
     ("select count(*) from a join (select x from b) on x = y", "must be a table")])
 def test_sql_join_rejections(sql, msg):
     from nutdb_amd import NutError
@@ -114,3 +114,14 @@ def test_sql_join_qualified_names():
     assert d["join"]["on"] == ["o.okey", "l.okey"] and d["keys"] == ["o.cust"]
     # without a JOIN the qualifier is dropped, as before
     assert Plan("select t.a from t where t.a > 3").describe()["columns"] == ["a"]
+
+
+def test_sql_join_chain_lowering():
+    from nutdb_amd.sql import Plan
+    d = Plan("select c_nation, count(*) from lineitem join orders on l_okey = o_okey join customer on "
+             "o_cust = c_key group by c_nation").describe()
+    assert d["joins"] == [{"table": "orders", "on": ["l_okey", "o_okey"]},
+                          {"table": "customer", "on": ["o_cust", "c_key"]}]
+    from nutdb_amd import NutError
+    with pytest.raises(NutError, match="INNER only"):
+        Plan("select count(*) from a join b on x = y left join c on y = z")
