@@ -2180,9 +2180,9 @@ nut_status exec_join(nut_ctx *c, const nut_plan &p, const nut_column *lc, int nl
   const bool outer = p.join == NUT_JOIN_LEFT;
   // what the other (build) table may feed
   int bkey = side[k0] == ps ? k1 : k0, pkey = side[k0] == ps ? k0 : k1;
-  auto in_prog = [](const PProg &pp, int i) {
+  auto in_prog = [](const PProg &pp, int i) {  // (LIKE leaves read their column too)
     for (const PNode &nd : pp)
-      if (nd.op == NUT_P_COL && nd.col == i) return true;
+      if ((nd.op == NUT_P_COL || nd.op == P_LIKE || nd.op == P_ILIKE) && nd.col == i) return true;
     return false;
   };
   // read by plan q after the join: as a row decider / projection, or inside an aggregate
@@ -2225,7 +2225,7 @@ nut_status exec_join(nut_ctx *c, const nut_plan &p, const nut_column *lc, int nl
     for (PProg &cj : conj) {
       int sd = -1;
       for (const PNode &nd : cj)
-        if (nd.op == NUT_P_COL) sd = sd < 0 || sd == side[nd.col] ? side[nd.col] : 2;
+        if (nd.op == NUT_P_COL || nd.op == P_LIKE || nd.op == P_ILIKE) sd = sd < 0 || sd == side[nd.col] ? side[nd.col] : 2;
       (sd < 2 && pushable(sd) ? push[sd] : keep).push_back(std::move(cj));
     }
     p2.where = and_all(keep);

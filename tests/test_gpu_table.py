@@ -269,3 +269,26 @@ def test_like_on_dictionary_columns(ex):
     assert got["p_size"].tolist() == size[(ty == "SMALL BRUSHED TIN") & (size < 10)].tolist()
     with pytest.raises(NutError, match="LIKE needs a string column"):
         t.sql("select count(*) from part where p_size like '1%'")
+
+
+def test_like_through_a_join(ex):
+    """LIKE on the other table's dictionary column: pushed below the join alone, and kept
+    above it inside a cross-table OR (the column is gathered through the join index)."""
+    rng = np.random.default_rng(47)
+    names = np.array(["ACME BOLT", "ACME NUT", "ZED BOLT", "ZED GEAR"], dtype=object)
+    nparts, nl = 1000, 50_003
+    pkey = rng.permutation(nparts).astype(np.int64)
+    pname = names[rng.integers(0, 4, nparts)]
+    part = Table(ex, "CREATE TABLE part (p_key Int64, p_name String)")
+    part.append(p_key=pkey, p_name=pname)
+    lk = rng.integers(0, nparts, nl).astype(np.int64)
+    qty = rng.integers(1, 50, nl).astype(np.int64)
+    li = Table(ex, "CREATE TABLE lineitem (l_part Int64, l_qty Int64)")
+    li.append(l_part=lk, l_qty=qty)
+    nm = dict(zip(pkey.tolist(), pname.tolist()))
+    ln = np.array([nm[k] for k in lk.tolist()], dtype=object)
+    for where, m in [("p_name like 'ACME%'", np.array([v.startswith("ACME") for v in ln])),
+                     ("p_name like '%BOLT' or l_qty > 45", np.array([v.endswith("BOLT") for v in ln]) | (qty > 45))]:
+        got = li.sql(f"select count(*) as c, sum(l_qty) as s from lineitem join part on l_part = p_key where {where}",
+                     right=part)
+        assert got["c"].tolist() == [int(m.sum())] and got["s"].tolist() == [int(qty[m].sum())], where
