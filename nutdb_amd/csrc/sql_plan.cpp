@@ -910,7 +910,7 @@ bool lower_output(nut_plan &p, const Expr &e, PlanOut &o, Lowering &L) {
     if (!star && !lower_nullable(p, e.kids[0], a.val, a.mask, nullable, L)) return false;
     for (const PProg *pp : {&a.val, &a.mask})
       for (const PNode &nd : *pp)
-        if (nd.op == NUT_P_COL) a.refs.push_back(nd.col);
+        if (nd.op == NUT_P_COL || nd.op == P_LIKE || nd.op == P_ILIKE) a.refs.push_back(nd.col);
     std::sort(a.refs.begin(), a.refs.end());
     a.refs.erase(std::unique(a.refs.begin(), a.refs.end()), a.refs.end());
     if (op == NUT_AGG_COUNT) a.val.clear();  // count(x) counts the rows where x is not NULL
