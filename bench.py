@@ -71,6 +71,17 @@ class Q1:
     def local(self):
         return self.ex.q1(*self.cols, date_k=self.k)
 
+    def run(self):  # single GPU step: the query and its (<= 6-group) result on the host
+        g = self.local()
+        r = g.to_host_words()
+        g.free()
+        return r
+
+    @staticmethod
+    def parity(gpu, cpu):
+        (gk, gw), (ck, cw) = gpu, cpu
+        return _cmp_groups(gk, gw, ck, cw, f64_cols=(0, 1, 2), rtol=1e-12)
+
     def merge_query(self, seg):
         from nutdb_amd import Agg, AggQuery
         # partial record: rf, ls, sum_qty, sum_price, sum_disc_price, count
@@ -107,6 +118,17 @@ class GroupBy:
         return self.ex.groupby(AggQuery(keys=[self.key], values=[self.val], aggs=[Agg("sum", "col", (0,))]),
                                group_hint=self.G)
 
+    def run(self):
+        g = self.local()
+        r = g.to_host_words()
+        g.free()
+        return r
+
+    @staticmethod
+    def parity(gpu, cpu):  # dyadic values: the f64 sums are exact, so compare bits
+        (gk, gw), (ck, cw) = gpu, cpu
+        return _cmp_groups(gk, gw, ck, cw, f64_cols=(), rtol=0.0)
+
     def merge_query(self, seg):
         from nutdb_amd import Agg, AggQuery
         return AggQuery(keys=[seg[0].contiguous()], values=[seg[1].contiguous().view(torch.float64)],
@@ -134,6 +156,12 @@ class Filter:
 
     def run(self):
         self.ex.filter_i64_async(self.col, "<", self.k, self.out, self.out_n)
+        return self.out, self.out_n
+
+    @staticmethod
+    def parity(gpu, cpu):
+        out, out_n = gpu
+        return _cmp_arrays(out[: int(out_n.item())].cpu().numpy(), cpu)
 
     def config(self):
         return {"workload": self.name, "query": "SELECT col FROM t WHERE col < k", "selectivity": self.sel,
@@ -159,6 +187,10 @@ class ScanExpr:
     def run(self):  # results stay in HBM (as nut_plan_execute's scan results do)
         ids = self.ex.select_rows([self.a, self.b], self.where)
         return self.ex.gather(self.a, ids)
+
+    @staticmethod
+    def parity(gpu, cpu):
+        return _cmp_arrays(gpu.cpu().numpy(), cpu)
 
     def config(self):
         return {"workload": self.name, "query": "SELECT a FROM t WHERE a < b (expression-mode scan)",
@@ -187,8 +219,12 @@ class Sort:
         self.group = group
         self.sort_bytes, self.levels = 0, 0
 
+    # roofline numerator: SURVEY.md §8(d)'s HBM lower bound, one read + one write of every
+    # key (16 B/key); the bytes the passes actually stream are reported beside it
+    cols_bytes = 16
+
     @property
-    def cols_bytes(self):
+    def pass_bytes(self):
         # per row of this rank's shard; N>1 adds the partition (8 B histogram + 16 B pass)
         return self.sort_bytes / self.rows + (24 if self.world > 1 else 0)
 
@@ -199,13 +235,19 @@ class Sort:
             from nutdb_amd.dist import distributed_sort
             self.out = distributed_sort(self.col, self.ex.partition_i64, self.ex.sort_i64, self.group)
         self.sort_bytes, self.levels = self.ex.sort_stats()
+        return self.out
+
+    @staticmethod
+    def parity(gpu, cpu):
+        return _cmp_arrays(gpu.cpu().numpy(), cpu)
 
     def config(self):
         return {"workload": self.name, "query": "SELECT k FROM t ORDER BY k (full-range i64)",
                 "algorithm": f"hybrid MSD radix: {self.levels} segmented scatter levels + on-chip local sorts"
                 + ("; sample sort across ranks: partition by P-1 splitters + RCCL all-to-all" if self.world > 1
                    else ""),
-                "bytes_per_row": self.cols_bytes, "hbm_lower_bound_bytes_per_row": 16,
+                "bytes_per_row": self.cols_bytes, "roofline_bytes": "16 B/key HBM lower bound (SURVEY.md §8(d))",
+                "pass_bytes_per_row": self.pass_bytes,
                 "xgmi_bytes_per_row": 8.0 * (self.world - 1) / self.world}
 
 
@@ -227,6 +269,12 @@ class Q12Expr:
 
     def run(self):
         return self.plan.execute(self.ex, self.cols, group_hint=8)
+
+    @staticmethod
+    def parity(gpu, cpu):
+        ck, cw = cpu[0], cpu[1]
+        return _cmp_groups(np.stack([gpu["l_shipmode"]], 1), np.stack([gpu["high_line_count"],
+                           gpu["low_line_count"]], 1).view(np.uint64), ck, cw, f64_cols=(), rtol=0.0)
 
     def config(self):
         return {"workload": self.name, "query": "reference tests/sql/5.sql (TPC-H Q12 shape; integer codes for "
@@ -270,7 +318,16 @@ class Join:
             pi, bi = distributed_join(self.build, self.probe, self.ex.hash_partition_i64, self.ex.join_i64, "inner",
                                       self.rank * self.nb, self.rank * self.rows, self.group)
         self.npairs = pi.numel()
-        del pi, bi
+        return pi, bi
+
+    @staticmethod
+    def parity(gpu, cpu):
+        # build keys are unique w.h.p., but the ABI leaves the build rows of one probe row
+        # unordered: compare the pair sets ordered by (probe row, build row)
+        g = [t.cpu().numpy() for t in gpu]
+        og, oc = np.lexsort((g[1], g[0])), np.lexsort((cpu[1], cpu[0]))
+        r = _cmp_arrays(g[0][og], cpu[0][oc])
+        return r if not r["ok"] else _cmp_arrays(g[1][og], cpu[1][oc])
 
     def config(self):
         return {"workload": self.name, "query": "SELECT ... FROM lineitem JOIN orders ON l_orderkey = o_orderkey "
@@ -327,6 +384,13 @@ class Q12Join:
 
     def run(self):
         return self.plan.execute_join(self.ex, self.orders, self.lineitem, group_hint=8)
+
+    @staticmethod
+    def parity(gpu, cpu):
+        got = [(int(m), int(h), int(lo)) for m, h, lo in zip(gpu["l_shipmode"], gpu["high_line_count"],
+                                                              gpu["low_line_count"])]
+        want = [r for r in cpu if r[1] + r[2] > 0]
+        return {"ok": got == want, "rows": len(got)} if got == want else {"ok": False, "got": got, "want": want}
 
     def config(self):
         return {"workload": self.name, "query": "TPC-H Q12 (integer codes for ship mode / priority): orders JOIN "
@@ -387,12 +451,12 @@ def cpu_baseline(args, workload: str, target_s: float):
             from oracle.expr import eval_prog
             a, b = orc.gen_column(1, 0x81, n), orc.gen_column(1, 0x82, n)
             return lambda: a[eval_prog([("col", 0), ("col", 1), ("lt",)], [a, b], n)[0] != 0]
-        if workload == "join":
-            rng = np.random.default_rng(0x71)
-            nb = max(n // 4, 1)
-            b = rng.permutation(nb).astype(np.int64) * 7919 + 13
-            sel = rng.integers(0, nb, n)
-            p = np.where(rng.random(n) < 0.1, -1 - sel, b[sel])
+        if workload == "join":  # the columns of bench's Join (same generator, rank 0)
+            nb = n // 4
+            b = orc.gen_column(0, 0x71, nb)
+            sel = orc.gen_column(0, 0x72, n)
+            p = np.where(sel % 10 == 0, sel | (1 << 62), b[sel % max(nb, 1)])
+            del sel
             return lambda: orc.join_i64_c(b, p, "inner")
         if workload == "q12expr":
             from nutdb_amd.workloads import Q12_AGGS, Q12_COLS, Q12_WHERE
@@ -403,12 +467,15 @@ def cpu_baseline(args, workload: str, target_s: float):
         k = filter_k(args.selectivity)
         return lambda: orc.filter_i64(col, 0, k)
 
+    last = [None]
+
     def timed(fn):
+        last[0] = None
         t0 = time.perf_counter()
-        fn()
+        last[0] = fn()
         return time.perf_counter() - t0
 
-    full = int(args.rows) if args.rows else {"q1": 10**9, "groupby": 10**9, "filter": 10**8,
+    full =int(args.rows) if args.rows else {"q1": 10**9, "groupby": 10**9, "filter": 10**8,
                                              "sort": 1_250_000_000, "q12expr": 10**9, "join": 10**9,
                                              "scanexpr": 10**8, "q12join": 10**9}[workload]
     probe = min(full, 4_000_000)
@@ -432,9 +499,43 @@ def cpu_baseline(args, workload: str, target_s: float):
                       f"OpenMP over {threads} host threads)"), threads
     else:
         how, cores = f"C oracle (oracle/oracle.c), OpenMP over {threads} host threads", threads
-    return {"value": sample / dt, "unit": "rows/s", "cores": cores, "kind": "port",
+    del fn
+    info = {"value": sample / dt, "unit": "rows/s", "cores": cores, "kind": "port",
             "sample": f"{sample:.3g} rows of the same synthetic workload ({sample / full:.2f} of one GPU's "
                       f"rows), {how}, generation excluded, best of {len(times)} timed runs = {dt:.3f} s"}
+    return info, last[0], sample
+
+
+def _cmp_arrays(got, want):
+    if got.shape != want.shape:
+        return {"ok": False, "why": f"length {got.shape} != {want.shape}"}
+    bad = np.flatnonzero(got != want)
+    if len(bad):
+        i = int(bad[0])
+        return {"ok": False, "why": f"{len(bad)} mismatches, first at {i}: {got[i]} != {want[i]}"}
+    return {"ok": True, "compare": "bit-exact"}
+
+
+def _cmp_groups(gk, gw, ck, cw, f64_cols, rtol):
+    """Group results (keys [G, nk] int64, words [G, na] uint64, both ordered by key):
+    keys and integer / count words bit-exact, f64 sum columns within rtol relative
+    (rtol 0: bit-exact)."""
+    if gk.shape != ck.shape or not np.array_equal(gk, ck):
+        return {"ok": False, "why": f"group keys differ ({len(gk)} vs {len(ck)} groups)"}
+    worst = 0.0
+    for j in range(cw.shape[1]):
+        if j in f64_cols and rtol > 0:
+            a, b = gw[:, j].view(np.float64), cw[:, j].view(np.float64)
+            err = float(np.max(np.abs(a - b) / np.maximum(np.abs(b), 1e-300))) if len(a) else 0.0
+            worst = max(worst, err)
+            if err > rtol:
+                return {"ok": False, "why": f"aggregate {j}: rel err {err:.3g} > {rtol}"}
+        elif not np.array_equal(gw[:, j], cw[:, j]):
+            return {"ok": False, "why": f"aggregate {j} differs"}
+    r = {"ok": True, "groups": int(len(gk)), "compare": "keys + integer aggregates bit-exact"}
+    r["compare"] += f", f64 sums max rel err {worst:.2g} (tol {rtol})" if f64_cols and rtol > 0 else \
+        ", f64 sums bit-exact"
+    return r
 
 
 # ------------------------------------------------------------------ main
@@ -499,33 +600,17 @@ def main():
                     "join": 1e9, "scanexpr": 1e8, "q12join": 1e9}[args.workload]
     rows = int(args.rows or default_rows)
     row0 = rank * rows
-    if args.workload == "q1":
-        w = Q1(ex, rows, row0)
-    elif args.workload == "groupby":
-        w = GroupBy(ex, rows, row0, args.groups)
-    elif args.workload == "sort":
-        w = Sort(ex, rows, row0, world, group)
-    elif args.workload == "q12expr":
-        if world > 1:
-            print("bench.py: q12expr is a single-GPU workload", file=sys.stderr)
-            sys.exit(2)
-        w = Q12Expr(ex, rows, row0)
-    elif args.workload == "join":
-        w = Join(ex, rows, row0, world, group, rank)
-    elif args.workload == "scanexpr":
-        w = ScanExpr(ex, rows, row0)
-    elif args.workload == "q12join":
-        if world > 1:
-            print("bench.py: q12join is a single-GPU workload", file=sys.stderr)
-            sys.exit(2)
-        w = Q12Join(ex, rows, row0)
-    else:
-        w = Filter(ex, rows, row0, args.selectivity)
+    if args.workload in ("q12expr", "q12join") and world > 1:
+        print(f"bench.py: {args.workload} is a single-GPU workload", file=sys.stderr)
+        sys.exit(2)
+    w = make_workload(args, ex, rows, row0, world, group, rank)
     torch.cuda.synchronize()
+    last = [None]
 
     def step():
-        if args.workload in ("filter", "sort", "q12expr", "join", "scanexpr", "q12join"):
-            w.run()
+        last[0] = None  # the previous step's result is dropped before the next one runs
+        if world == 1 or args.workload not in ("q1", "groupby"):
+            last[0] = w.run()
         else:
             groupby_step(w, rank, world, group)
 
@@ -557,15 +642,36 @@ def main():
     bytes_per_step = w.cols_bytes * rows
     achieved = bytes_per_step / (avg_kernel_ms * 1e-3) / 1e9 if launches else None
     # PMC-measured HBM traffic of the same kernel/config, if profiled (profiles/pmc_*.json)
-    traffic = None
+    # (not measured in this run: rocprofv3 --pmc cannot run under the timed bench; the
+    # source file, its commit and date travel with the number as traffic_source)
+    traffic, traffic_src = None, None
     pmc = ROOT / "profiles" / f"pmc_{w.name}.json"
     if pmc.exists():
         try:
             d = json.loads(pmc.read_text())
-            if int(d.get("rows", -1)) == rows:
+            if int(d.get("rows", -1)) == rows and (w.name != "groupby_i64_sum_f64" or
+                                                    int(d.get("groups", 1000)) == args.groups):
                 traffic = d.get("hbm_bytes_per_launch")
+                m = d.get("measured", {})
+                traffic_src = (f"profiles/{pmc.name}: {d.get('per', 'per launch')}, "
+                               f"{d.get('correction', '')}; measured {m.get('date_utc', 'round 1')} at commit "
+                               f"{m.get('commit', 'unknown')} (separate rocprofv3 --pmc passes of the same command)")
         except Exception:
             traffic = None
+    parity = None
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu, cpu_res, sample = cpu_baseline(args, args.workload, args.cpu_seconds)
+        if sample == rows:
+            how = "last timed step vs the CPU baseline's result on the same full-size input"
+            gpu_res = last[0]
+        else:  # the GPU rerun (untimed) on the CPU sample's input: the first `sample` rows
+            how = f"GPU rerun (untimed) on the CPU sample's {sample} rows vs the CPU baseline's result"
+            last[0] = None
+            gpu_res = make_workload(args, ex, sample, 0, 1, None, 0).run()
+        parity = {"rows": sample, "full_size": sample == rows, "method": how}
+        parity.update(type(w).parity(gpu_res, cpu_res))
+        del cpu_res, gpu_res
     if rank == 0:
         cfg = w.config()
         cfg.update({"rows_per_gpu": rows, "parallelism": f"dp{world} (row shards; key-hash all-to-all of "
@@ -577,14 +683,37 @@ def main():
             "vs_baseline": None, "dtype": "i64+f64", "data": "synthetic (counter-based splitmix64 columns "
             "generated in HBM)", "config": cfg,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic},
+                         "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
+                         "traffic_source": traffic_src},
         }
-        if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(args, args.workload, args.cpu_seconds)
+        if cpu is not None:
+            line["cpu_baseline"] = cpu
+            line["parity"] = parity
         print(json.dumps(line), flush=True)
     ex.close()
     if world > 1:
         dist.destroy_process_group()
+    if parity is not None and not parity["ok"]:
+        print(f"bench.py: PARITY FAILURE vs the CPU oracle: {parity}", file=sys.stderr)
+        sys.exit(1)
+
+
+def make_workload(args, ex, rows, row0, world, group, rank):
+    if args.workload == "q1":
+        return Q1(ex, rows, row0)
+    if args.workload == "groupby":
+        return GroupBy(ex, rows, row0, args.groups)
+    if args.workload == "sort":
+        return Sort(ex, rows, row0, world, group)
+    if args.workload == "q12expr":
+        return Q12Expr(ex, rows, row0)
+    if args.workload == "join":
+        return Join(ex, rows, row0, world, group, rank)
+    if args.workload == "scanexpr":
+        return ScanExpr(ex, rows, row0)
+    if args.workload == "q12join":
+        return Q12Join(ex, rows, row0)
+    return Filter(ex, rows, row0, args.selectivity)
 
 
 if __name__ == "__main__":

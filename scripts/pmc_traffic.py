@@ -6,7 +6,9 @@ gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE reports half the bytes
 wide coalesced streaming read, so read bytes = 2 x FETCH_SIZE x 1024; WRITE_SIZE is
 exact for 16-B streaming stores and atomics (x 1024)."""
 import json
+import os
 import sys
+import time
 from pathlib import Path
 
 sys.path.insert(0, str(Path(__file__).resolve().parent))
@@ -45,10 +47,15 @@ def main():
     s["hbm_bytes_per_launch"] = traffic
     (d / "summary.json").write_text(json.dumps(s, indent=1))
     (d / f"pmc_{name}.json").write_text(json.dumps({
-        "workload": name, "rows": int(rows), "kernel_match": match, "hbm_bytes_per_launch": traffic,
+        "workload": name, "rows": int(rows),
+        "groups": int(args[args.index("--groups") + 1]) if "--groups" in args else 1000, "kernel_match": match, "hbm_bytes_per_launch": traffic,
         "fetch_size_kb": c.get("FETCH_SIZE"), "write_size_kb": c.get("WRITE_SIZE"),
         "per": {"sort": "step (all ms_* kernels of one sort)", "join": "step (all hj_* kernels of one join)"}.get(
             wl, "launch of " + match),
+        "measured": {"tag": d.name, "commit": os.environ.get("NUT_COMMIT", "unknown"),
+                     "date_utc": time.strftime("%Y-%m-%dT%H:%MZ", time.gmtime()),
+                     "how": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, one pass each, over bench.py "
+                            + " ".join(args)},
         "correction": ("read = FETCH_SIZE (random 64-B slot reads dominate; the gfx950 x2 wide-stream "
                        "correction is not applied, so the ~12 GB of streaming key reads count half)"
                        if wl == "join" else "read = 2 x FETCH_SIZE (gfx950 wide-stream halving), write = WRITE_SIZE")},

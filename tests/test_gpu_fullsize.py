@@ -1,0 +1,81 @@
+"""GPU parity at the BASELINE.json sizes (VERDICT r1 "What's weak" 1): the benchmarked
+shapes themselves, not scaled-down stand-ins, checked against the C oracle.
+
+- config 5: one full 1.25e9-key sort shard (the per-GPU share of 1e10 keys on 8 GPUs).
+  At this size the hybrid MSD sort takes two scatter levels and its ~19 K-key segments
+  run through the largest local-sort class — a segment mix no smaller test drives.
+  Checked by sortedness + count + order-independent multiset hash against the oracle's
+  hash of the same generated column (a full element compare would need a 10 GB CPU sort).
+- config 3: GROUP BY key SUM(val) over 1e9 rows, G = 1000, dyadic values -> the f64 sums
+  are exact, so the comparison is bit-exact.
+- config 4: the TPC-H Q1 shape over 1e9 rows (keys / counts exact, f64 sums <= 1e-12).
+
+Host memory: at most ~50 GB at a time (the Q1 columns), freed between tests.
+"""
+import gc
+
+import numpy as np
+import pytest
+
+from helpers import F64_SUM_RTOL, OPCODE, rel_err
+
+pytestmark = pytest.mark.gpu
+
+
+def test_sort_full_config5_shard(ex, orc):
+    from nutdb_amd.workloads import SORT_COL, gen
+    n = 1_250_000_000
+    keys = gen(ex, SORT_COL, n)
+    out = ex.sort_i64(keys)
+    nbytes, levels = ex.sort_stats()
+    assert levels == 2 and nbytes >= 16 * n
+    del keys
+    o = out.cpu().numpy()
+    del out
+    assert len(o) == n
+    assert bool(np.all(o[1:] >= o[:-1])), "not sorted"
+    h = orc.multiset_hash(o)
+    del o
+    gc.collect()
+    want = orc.gen(SORT_COL, n)
+    assert h == orc.multiset_hash(want), "multiset hash differs from the generated column's"
+
+
+def test_groupby_full_config3(ex, orc):
+    from nutdb_amd import Agg, AggQuery
+    from nutdb_amd.workloads import gen, groupby_cols
+    n, G = 1_000_000_000, 1000
+    specs = groupby_cols(G, dyadic=True)
+    key, val = [gen(ex, s, n) for s in specs]
+    g = ex.groupby(AggQuery(keys=[key], values=[val], aggs=[Agg("sum", "col", (0,)), Agg("count")]),
+                   group_hint=G)
+    gk, gw = g.to_host_words()
+    g.free()
+    del key, val
+    hk, hv = [orc.gen(s, n) for s in specs]
+    ok, ow = orc.groupby([hk], [(0, 0, (0,)), (1, 0, ())], values=[hv], cap=G)
+    del hk, hv
+    gc.collect()
+    assert len(ok) == G
+    assert np.array_equal(gk, ok)
+    assert np.array_equal(gw, ow), "dyadic sums / counts must be bit-exact"
+    assert int(gw[:, 1].sum()) == n
+
+
+def test_q1_full_config4(ex, orc):
+    from nutdb_amd.workloads import Q1_COLS, Q1_DATE_K, gen
+    n = 1_000_000_000
+    cols = [gen(ex, spec, n) for spec in Q1_COLS]
+    g = ex.q1(*cols, date_k=Q1_DATE_K)
+    gk, gw = g.to_host_words()
+    g.free()
+    del cols
+    sd, rf, ls, qty, price, disc = [orc.gen(spec, n) for spec in Q1_COLS]
+    ok, ow = orc.groupby([rf, ls], [(0, 0, (0,)), (0, 0, (1,)), (0, 4, (1, 2)), (1, 0, ())],
+                         values=[qty, price, disc], preds=[(sd, OPCODE["<="], Q1_DATE_K)], cap=64)
+    del sd, rf, ls, qty, price, disc
+    gc.collect()
+    assert np.array_equal(gk, ok)
+    assert np.array_equal(gw[:, 3], ow[:, 3])
+    for j in range(3):
+        assert rel_err(gw[:, j].view(np.float64), ow[:, j].view(np.float64)) <= F64_SUM_RTOL
