@@ -66,6 +66,9 @@ void nut_ctx_destroy(nut_ctx *ctx);
  * its own. */
 nut_status nut_ctx_set_stream(nut_ctx *ctx, void *hip_stream);
 nut_status nut_ctx_sync(nut_ctx *ctx);
+/* copy `bytes` between any host / device addresses on the context's stream and wait for
+ * it (lets a host without its own HIP binding read library-owned device results) */
+nut_status nut_ctx_memcpy(nut_ctx *ctx, void *dst, const void *src, size_t bytes);
 /* number of CUs and device name, for reports */
 nut_status nut_ctx_info(nut_ctx *ctx, int *num_cus, char *name, size_t name_len);
 
@@ -338,6 +341,67 @@ nut_status nut_hash_partition_i64(nut_ctx *ctx, const int64_t *keys, uint64_t n,
  * int64 / f64 column through a join index */
 nut_status nut_gather_u64(nut_ctx *ctx, const uint64_t *src, const int64_t *idx, uint64_t n, uint64_t null_bits,
                           uint64_t *out);
+
+/* ========================================================================
+ * Multi-GPU execution over RCCL (SURVEY.md §8(b) nut_dist_*, §8(e)).
+ * A nut_dist is a group of P ranks, one GPU each; this process drives `nlocal` of them
+ * (its "local members", global ranks first_rank .. first_rank+nlocal-1), each with its
+ * own nut_ctx and RCCL communicator.  Three ways to form one:
+ *   nut_dist_create        one process drives ndev GPUs (ncclCommInitAll); the
+ *                          nut_dist_* calls run one host thread per device
+ *   nut_dist_create_rank   one process per GPU (MPI / torchrun style): rank 0 makes an
+ *                          id with nut_dist_unique_id, the host shares its
+ *                          NUT_DIST_ID_BYTES bytes with every rank (ncclCommInitRank)
+ *   nut_dist_create_virtual  P ranks on ONE device whose exchanges are device copies
+ *                          instead of RCCL: the same partition / exchange / merge code
+ *                          with P > 1 on a single GPU (tests)
+ * Every nut_dist_* call is collective: each process calls it with arrays of nlocal
+ * entries (entry l = local member l's shard; device pointers on that member's device).
+ * Rows are sharded by rank; the exchange is one all-to-all of counts (an all-gather,
+ * which also carries every rank's status so a failure on one rank fails the call on
+ * all of them instead of hanging the others) and one ncclAllToAllv of records.
+ * ======================================================================== */
+typedef struct nut_dist nut_dist;
+#define NUT_DIST_ID_BYTES 128
+nut_status nut_dist_create(int ndev, const int *devs, nut_dist **out);
+nut_status nut_dist_unique_id(void *id);
+nut_status nut_dist_create_rank(int nranks, int rank, const void *id, int device, nut_dist **out);
+nut_status nut_dist_create_virtual(int nranks, int device, nut_dist **out);
+nut_status nut_dist_info(const nut_dist *d, int *nranks, int *nlocal, int *first_rank);
+/* context of local member l (timing, synthetic columns, single-GPU calls on its shard) */
+nut_ctx *nut_dist_ctx(nut_dist *d, int local);
+/* Collective like every nut_dist call.  Free the nut_groups a nut_dist_groupby returned
+ * first: they live on a member's context, which this destroys. */
+void nut_dist_destroy(nut_dist *d);
+
+/* Group-by across ranks (configs 3, 4): local pre-aggregation of specs[l] on member l ->
+ * partial groups partitioned by owner = mix64(key tuple) % P -> ncclAllToAllv -> each
+ * owner merges what it received (SUM / COUNT add, MIN / MAX re-min/max) -> the owners'
+ * groups are gathered on rank 0.  out[l] = the global result on the member holding
+ * rank 0, NULL on every other member.  Every rank's spec has the same shape. */
+nut_status nut_dist_groupby(nut_dist *d, const nut_agg_spec *specs, uint64_t group_hint, nut_groups **out);
+/* ORDER BY k across ranks (config 5), sample sort: 4096 strided samples per rank ->
+ * all-gather -> P-1 splitters at the pooled sample's quantiles -> nut_partition_i64 ->
+ * ncclAllToAllv of keys -> local nut_sort_i64.  Member l ends with out_n[l] keys at
+ * out[l] (device memory owned by the member, valid until its next nut_dist_* call):
+ * the r-th key range of the global order, so the ranks' outputs concatenated in rank
+ * order are sorted.  Keys equal to a splitter go to the higher rank.  P <= 64. */
+nut_status nut_dist_sort_i64(nut_dist *d, const int64_t *const *in, const uint64_t *n, const int64_t **out,
+                             uint64_t *out_n);
+/* SELECT col FROM t WHERE col <cmp> k over row shards (config 2): no data exchange;
+ * out_n[l] = rows member l selected (into its caller-owned out[l], n[l] entries),
+ * out_offset[l] = their position in the global result (the rank-ordered concatenation). */
+nut_status nut_dist_filter_i64(nut_dist *d, const int64_t *const *col, const uint64_t *n, int cmp, int64_t k,
+                               int64_t *const *out, uint64_t *out_n, uint64_t *out_offset);
+/* Hash join across ranks (§8(f) 4): both sides hash-partitioned by key owner
+ * (nut_hash_partition_i64), one ncclAllToAllv of (key, global row) records per side, a
+ * local nut_join_i64 on every rank.  Global row ids: build_row0[l] / probe_row0[l] = the
+ * global index of member l's first row.  Member l ends with npairs[l] pairs of GLOBAL
+ * (probe row, build row) at probe_idx[l] / build_idx[l] (member-owned, valid until its
+ * next nut_dist_* call; -1 = no build row), nut_join_i64 semantics per key. */
+nut_status nut_dist_join_i64(nut_dist *d, const int64_t *const *build, const uint64_t *nbuild, const int64_t *build_row0,
+                             const int64_t *const *probe, const uint64_t *nprobe, const int64_t *probe_row0,
+                             int join_type, const int64_t **probe_idx, const int64_t **build_idx, uint64_t *npairs);
 
 /* ========================================================================
  * SQL front end (CPU) — restatement of the reference's only public API,

@@ -184,7 +184,23 @@ SIGNATURES = {
     "nut_result_device": (_I32, [_P, C.POINTER(_P)]),
     "nut_result_device_column": (_I32, [_P, _I32, C.POINTER(_P)]),
     "nut_result_free": (None, [_P]),
+    "nut_ctx_memcpy": (_I32, [_P, _P, _P, C.c_size_t]),
+    # multi-GPU (RCCL inside the library)
+    "nut_dist_create": (_I32, [_I32, C.POINTER(_I32), C.POINTER(_P)]),
+    "nut_dist_unique_id": (_I32, [_P]),
+    "nut_dist_create_rank": (_I32, [_I32, _I32, _P, _I32, C.POINTER(_P)]),
+    "nut_dist_create_virtual": (_I32, [_I32, _I32, C.POINTER(_P)]),
+    "nut_dist_info": (_I32, [_P, C.POINTER(_I32), C.POINTER(_I32), C.POINTER(_I32)]),
+    "nut_dist_ctx": (_P, [_P, _I32]),
+    "nut_dist_destroy": (None, [_P]),
+    "nut_dist_groupby": (_I32, [_P, _P, _U64, C.POINTER(_P)]),
+    "nut_dist_sort_i64": (_I32, [_P, C.POINTER(_P), C.POINTER(_U64), C.POINTER(_P), C.POINTER(_U64)]),
+    "nut_dist_filter_i64": (_I32, [_P, C.POINTER(_P), C.POINTER(_U64), _I32, _I64, C.POINTER(_P), C.POINTER(_U64),
+                                   C.POINTER(_U64)]),
+    "nut_dist_join_i64": (_I32, [_P, C.POINTER(_P), C.POINTER(_U64), C.POINTER(_I64), C.POINTER(_P), C.POINTER(_U64),
+                                 C.POINTER(_I64), _I32, C.POINTER(_P), C.POINTER(_P), C.POINTER(_U64)]),
 }
+NUT_DIST_ID_BYTES = 128
 
 
 def _load() -> C.CDLL:

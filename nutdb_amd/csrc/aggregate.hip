@@ -1038,6 +1038,43 @@ nut_status hash_partition16(nut_ctx *c, const int64_t *keys, uint64_t n, uint64_
   for (size_t i = 0; i < 65536; ++i) counts[i] = h2[i];
   return NUT_OK;
 }
+// ------------------------------------------------------------ multi-GPU merge (dist.cpp)
+int groups_width(const nut_groups *g) { return g->nk + g->naggs; }
+
+void groups_merge_spec(const nut_groups *g, const uint64_t *seg, uint64_t c, nut_agg_spec *s, nut_prog_node *nodes) {
+  memset(s, 0, sizeof(*s));
+  s->n = c;
+  s->nkeys = g->nk;
+  for (int j = 0; j < g->nk; ++j) s->keys[j] = (const int64_t *)(seg + (uint64_t)j * c);
+  s->naggs = g->naggs;
+  const bool prog = g->naggs > NUT_MAX_VALS;  // more partial columns than fused value slots
+  if (prog) {
+    s->prog_mode = 1;
+    s->nprog_cols = g->naggs;
+  } else {
+    s->nvals = g->naggs;
+  }
+  for (int a = 0; a < g->naggs; ++a) {
+    const int k = g->kinds[a];
+    const bool f64 = k == AK_SUM_F64 || k == AK_MIN_F64 || k == AK_MAX_F64;
+    const void *col = seg + (uint64_t)(g->nk + a) * c;
+    // a COUNT partial is an int64 word: the merge adds them
+    s->agg_op[a] = (k == AK_MIN_F64 || k == AK_MIN_I64) ? NUT_AGG_MIN
+                   : (k == AK_MAX_F64 || k == AK_MAX_I64) ? NUT_AGG_MAX : NUT_AGG_SUM;
+    if (prog) {
+      s->prog_col[a] = col;
+      s->prog_col_type[a] = f64 ? NUT_T_F64 : NUT_T_I64;
+      nodes[a] = nut_prog_node{NUT_P_COL, a, 0};
+      s->agg_val[a] = nut_prog{1, &nodes[a]};
+    } else {
+      s->val_col[a] = col;
+      s->val_type[a] = f64 ? NUT_T_F64 : NUT_T_I64;
+      s->agg_expr[a] = NUT_EX_COL;
+      s->agg_arg[a][0] = a;
+    }
+  }
+}
+
 }  // namespace nut
 
 extern "C" {

@@ -181,6 +181,15 @@ nut_status nut_ctx_sync(nut_ctx *c) {
   return NUT_OK;
 }
 
+nut_status nut_ctx_memcpy(nut_ctx *c, void *dst, const void *src, size_t bytes) {
+  if (!c || (bytes && (!dst || !src))) return fail(NUT_ERR_INVALID_ARG, "nut_ctx_memcpy: NULL argument");
+  if (bytes == 0) return NUT_OK;
+  DeviceGuard g(c->device);
+  NUT_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, c->stream));
+  NUT_HIP(hipStreamSynchronize(c->stream));
+  return NUT_OK;
+}
+
 nut_status nut_ctx_enable_timing(nut_ctx *c, int enable) {
   if (!c) return fail(NUT_ERR_INVALID_ARG, "nut_ctx_enable_timing: ctx is NULL");
   DeviceGuard g(c->device);

@@ -126,6 +126,13 @@ nut_status hip_fail(hipError_t e, const char *what);
     if (e_ != hipSuccess) return ::nut::hip_fail(e_, #call); \
   } while (0)
 
+// Multi-GPU merge of partial groups (aggregate.hip, used by dist.cpp): words per group,
+// and the spec that folds c partial groups stored column-major at seg (the
+// nut_groups_to_device layout of g) into a result of g's shape (SUM and COUNT partials
+// add, MIN/MAX re-min/max).  nodes: NUT_MAX_AGGS program nodes the spec may point to.
+int groups_width(const nut_groups *g);
+void groups_merge_spec(const nut_groups *g, const uint64_t *seg, uint64_t c, nut_agg_spec *s, nut_prog_node *nodes);
+
 // Device scratch that only grows; reused across calls (no malloc in steady state).
 struct Scratch {
   void *ptr = nullptr;
@@ -179,16 +186,23 @@ struct nut_ctx {
 };
 
 namespace nut {
-// RAII device guard: switch to ctx->device for the call, restore afterwards.
+// RAII device guard: switch to ctx->device for the call, restore afterwards.  It also
+// clears this thread's HIP last-error slot on entry and exit: other libraries in the
+// process (torch, RCCL) leave stale errors there (measured: an ncclAllToAllv left
+// hipErrorInvalidDevice), the launch checks below (NUT_HIP(hipGetLastError())) must see
+// only this call's errors, and a caller's own checks must not see ours (every error this
+// library meets is returned as a status).
 struct DeviceGuard {
   int prev = -1;
   explicit DeviceGuard(int dev) {
+    (void)hipGetLastError();
     if (hipGetDevice(&prev) != hipSuccess) prev = -1;
     if (prev != dev) (void)hipSetDevice(dev);
   }
   ~DeviceGuard() {
     int cur;
     if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    (void)hipGetLastError();  // and leaves none behind for the caller's own checks (torch's)
   }
 };
 }  // namespace nut

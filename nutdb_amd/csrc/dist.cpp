@@ -1,0 +1,678 @@
+// dist.cpp — multi-GPU execution inside the C ABI (nut_dist_*).
+//
+// A nut_dist is P ranks, one GPU each.  Its exchanges are RCCL collectives on each
+// member's stream (ncclAllGather for the small per-rank headers, ncclAllToAllv for the
+// records: xGMI is a full point-to-point mesh, so one all-to-all uses every link at once),
+// or — for nut_dist_create_virtual — device copies between P members sharing one GPU,
+// so that the same partition / exchange / merge code runs with P > 1 on a single device.
+//
+// RCCL is resolved with dlopen on the first nut_dist_create*: the single-GPU entry points
+// never load it.  By soname ("librccl.so.1"), so a process that already holds an RCCL
+// (torch's) reuses that copy and its HIP runtime instead of loading a second one.
+//
+// Every collective call starts with an all-gather of a small header that carries each
+// rank's status, so a rank whose local step failed fails the call on every rank instead
+// of leaving the others blocked in an all-to-all.
+#include <dlfcn.h>
+#include <rccl/rccl.h>
+#include <string.h>
+
+#include <algorithm>
+#include <condition_variable>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "common.hpp"
+
+using namespace nut;
+
+namespace {
+
+// ------------------------------------------------------------------ RCCL entry points
+struct Rccl {
+  decltype(&ncclGetUniqueId) get_unique_id = nullptr;
+  decltype(&ncclCommInitRank) comm_init_rank = nullptr;
+  decltype(&ncclCommInitAll) comm_init_all = nullptr;
+  decltype(&ncclCommDestroy) comm_destroy = nullptr;
+  decltype(&ncclAllGather) all_gather = nullptr;
+  decltype(&ncclAllToAllv) all_to_allv = nullptr;
+  decltype(&ncclGetErrorString) error_string = nullptr;
+  std::string load_error;
+};
+
+Rccl g_rccl;
+std::once_flag g_rccl_once;
+
+template <class F>
+bool bind(void *h, const char *name, F &fn) {
+  fn = reinterpret_cast<F>(dlsym(h, name));
+  return fn != nullptr;
+}
+
+const Rccl *rccl() {
+  std::call_once(g_rccl_once, [] {
+    void *h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) {
+      const char *e = dlerror();
+      g_rccl.load_error = std::string("cannot load librccl.so.1: ") + (e ? e : "?");
+      return;
+    }
+    Rccl r;
+    if (!bind(h, "ncclGetUniqueId", r.get_unique_id) || !bind(h, "ncclCommInitRank", r.comm_init_rank) ||
+        !bind(h, "ncclCommInitAll", r.comm_init_all) || !bind(h, "ncclCommDestroy", r.comm_destroy) ||
+        !bind(h, "ncclAllGather", r.all_gather) || !bind(h, "ncclAllToAllv", r.all_to_allv) ||
+        !bind(h, "ncclGetErrorString", r.error_string)) {
+      g_rccl.load_error = "librccl.so.1 lacks an entry point nut_dist needs";
+      return;
+    }
+    g_rccl = r;
+  });
+  return g_rccl.all_to_allv ? &g_rccl : nullptr;
+}
+
+nut_status rccl_fail(const Rccl *r, ncclResult_t e, const char *what) {
+  return fail(NUT_ERR_HIP, std::string(what) + ": " + (r ? r->error_string(e) : "RCCL") + " (" +
+                               std::to_string((int)e) + ")");
+}
+
+// ------------------------------------------------------------------ virtual ranks
+// P members on one device: a post-and-copy exchange between threads.  A member posts its
+// send buffer once its stream has drained, every member copies its parts out of the
+// others' buffers on its own stream, and nobody leaves before all copies are complete.
+struct Hub {
+  std::mutex mu;
+  std::condition_variable cv;
+  int n = 0, arrived = 0;
+  uint64_t generation = 0;
+  struct Post {
+    const uint64_t *send = nullptr;
+    const size_t *count = nullptr, *displ = nullptr;  // words, per destination
+    size_t words = 0;                                  // all-gather: words per rank
+  };
+  std::vector<Post> post;
+  void barrier() {
+    std::unique_lock<std::mutex> lk(mu);
+    const uint64_t g = generation;
+    if (++arrived == n) {
+      arrived = 0;
+      ++generation;
+      cv.notify_all();
+    } else {
+      cv.wait(lk, [&] { return generation != g; });
+    }
+  }
+};
+
+}  // namespace
+
+struct nut_dist {
+  enum Mode { kRcclAll, kRcclRank, kVirtual } mode = kRcclAll;
+  int nranks = 1, first_rank = 0;
+  const Rccl *r = nullptr;
+  Hub hub;
+  struct Member {
+    int rank = 0;
+    nut_ctx *ctx = nullptr;
+    ncclComm_t comm = nullptr;
+    Scratch hdr_dev;                  // headers: this rank's and the all-gathered ones
+    uint64_t *hdr_host = nullptr;     // pinned, kHdrBytes
+    Scratch buf[10];                  // send / receive / output buffers of the calls
+  };
+  std::vector<Member> m;
+};
+
+namespace {
+
+constexpr int kMaxRanks = 64;  // nut_groups_partition / nut_partition_i64 bound
+constexpr size_t kHdrWords = 2 + 2 * kMaxRanks;
+constexpr size_t kHdrBytes = kHdrWords * kMaxRanks * 8;
+constexpr int kSamples = 4096;  // sample sort: strided samples per rank
+
+using Member = nut_dist::Member;
+
+uint64_t *buf(Member &mb, int i) { return (uint64_t *)mb.buf[i].ptr; }
+nut_status reserve(Member &mb, int i, uint64_t words) { return mb.buf[i].reserve(std::max<uint64_t>(words, 1) * 8); }
+
+// all-gather of `words` words from every rank: recv[q * words + i]
+nut_status allgather(nut_dist *d, int l, const uint64_t *send, uint64_t *recv, size_t words) {
+  Member &mb = d->m[l];
+  hipStream_t s = mb.ctx->stream;
+  if (d->mode != nut_dist::kVirtual) {
+    ncclResult_t e = d->r->all_gather(send, recv, words, ncclUint64, mb.comm, s);
+    (void)hipGetLastError();  // RCCL leaves stale HIP errors in this thread's slot
+    return e == ncclSuccess ? NUT_OK : rccl_fail(d->r, e, "ncclAllGather");
+  }
+  Hub &h = d->hub;
+  NUT_HIP(hipStreamSynchronize(s));
+  h.post[l] = Hub::Post{send, nullptr, nullptr, words};
+  h.barrier();
+  hipError_t e = hipSuccess;
+  for (int q = 0; q < d->nranks && e == hipSuccess; ++q)
+    if (words) e = hipMemcpyAsync(recv + (size_t)q * words, h.post[q].send, words * 8, hipMemcpyDeviceToDevice, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  h.barrier();  // the senders' buffers stay untouched until every copy is done
+  return e == hipSuccess ? NUT_OK : hip_fail(e, "nut_dist (virtual) all-gather");
+}
+
+// all-to-all of variable segments (words): segment q of send goes to rank q
+nut_status alltoallv(nut_dist *d, int l, const uint64_t *send, const size_t *sc, const size_t *sd, uint64_t *recv,
+                     const size_t *rc, const size_t *rd) {
+  Member &mb = d->m[l];
+  hipStream_t s = mb.ctx->stream;
+  if (d->mode != nut_dist::kVirtual) {
+    ncclResult_t e = d->r->all_to_allv(send, sc, sd, recv, rc, rd, ncclUint64, mb.comm, s);
+    (void)hipGetLastError();
+    return e == ncclSuccess ? NUT_OK : rccl_fail(d->r, e, "ncclAllToAllv");
+  }
+  Hub &h = d->hub;
+  const int me = mb.rank;
+  NUT_HIP(hipStreamSynchronize(s));
+  h.post[l] = Hub::Post{send, sc, sd, 0};
+  h.barrier();
+  hipError_t e = hipSuccess;
+  nut_status st = NUT_OK;
+  for (int q = 0; q < d->nranks && e == hipSuccess; ++q) {
+    const Hub::Post &p = h.post[q];
+    if (p.count[me] != rc[q]) {
+      st = fail(NUT_ERR_INVALID_ARG, "nut_dist (virtual) all-to-all: receive count mismatch");
+      break;
+    }
+    if (rc[q]) e = hipMemcpyAsync(recv + rd[q], p.send + p.displ[me], rc[q] * 8, hipMemcpyDeviceToDevice, s);
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  h.barrier();
+  if (st) return st;
+  return e == hipSuccess ? NUT_OK : hip_fail(e, "nut_dist (virtual) all-to-all");
+}
+
+// All-gather of a `w`-word host header whose word 0 is this rank's status.  On return
+// all[q * w + i] holds rank q's header; NUT_OK only if every rank reported NUT_OK.
+nut_status exchange_header(nut_dist *d, int l, nut_status mine, const std::vector<uint64_t> &hdr,
+                           std::vector<uint64_t> &all) {
+  Member &mb = d->m[l];
+  const size_t w = hdr.size();
+  std::string my_error = mine ? nut_last_error() : "";
+  uint64_t *dev = (uint64_t *)mb.hdr_dev.ptr;
+  hipStream_t s = mb.ctx->stream;
+  std::vector<uint64_t> h = hdr;
+  h[0] = (uint64_t)mine;
+  NUT_HIP(hipMemcpyAsync(dev, h.data(), w * 8, hipMemcpyHostToDevice, s));
+  nut_status st = allgather(d, l, dev, dev + w, w);
+  if (st) return st;
+  NUT_HIP(hipMemcpyAsync(mb.hdr_host, dev + w, w * d->nranks * 8, hipMemcpyDeviceToHost, s));
+  NUT_HIP(hipStreamSynchronize(s));
+  all.assign(mb.hdr_host, mb.hdr_host + w * d->nranks);
+  if (mine) return fail(mine, my_error);
+  for (int q = 0; q < d->nranks; ++q)
+    if (all[(size_t)q * w])
+      return fail((nut_status)all[(size_t)q * w], "nut_dist: rank " + std::to_string(q) + " failed (status " +
+                                                      std::to_string(all[(size_t)q * w]) + ")");
+  return NUT_OK;
+}
+
+nut_status agree(nut_dist *d, int l, nut_status mine) {
+  std::vector<uint64_t> all;
+  return exchange_header(d, l, mine, std::vector<uint64_t>(1, 0), all);
+}
+
+// run f(l) for every local member: one host thread per member when there are several
+template <class F>
+nut_status run_members(nut_dist *d, F &&f) {
+  const int L = (int)d->m.size();
+  if (L == 1) {
+    DeviceGuard dg(d->m[0].ctx->device);
+    return f(0);
+  }
+  std::vector<nut_status> st(L, NUT_OK);
+  std::vector<std::string> err(L);
+  std::vector<std::thread> th;
+  th.reserve(L);
+  for (int l = 0; l < L; ++l)
+    th.emplace_back([&, l] {
+      (void)hipSetDevice(d->m[l].ctx->device);
+      (void)hipGetLastError();
+      st[l] = f(l);
+      if (st[l]) err[l] = nut_last_error();
+    });
+  for (auto &t : th) t.join();
+  // report the first member that failed on its own rather than through another's status
+  int pick = -1;
+  for (int l = 0; l < L && pick < 0; ++l)
+    if (st[l] && err[l].rfind("nut_dist: rank", 0) != 0) pick = l;
+  for (int l = 0; l < L && pick < 0; ++l)
+    if (st[l]) pick = l;
+  return pick < 0 ? NUT_OK : fail(st[pick], err[pick]);
+}
+
+nut_status member_init(nut_dist *d, Member &mb, int device) {
+  nut_status st = nut_ctx_create(device, &mb.ctx);
+  if (st) return st;
+  DeviceGuard dg(device);
+  st = mb.hdr_dev.reserve(kHdrBytes * 2);
+  if (st) return st;
+  NUT_HIP(hipHostMalloc((void **)&mb.hdr_host, kHdrBytes, hipHostMallocDefault));
+  (void)d;
+  return NUT_OK;
+}
+
+void member_free(Member &mb) {
+  if (!mb.ctx) return;
+  {
+    DeviceGuard dg(mb.ctx->device);
+    (void)hipStreamSynchronize(mb.ctx->stream);
+    for (auto &b : mb.buf) b.release();
+    mb.hdr_dev.release();
+    if (mb.hdr_host) (void)hipHostFree(mb.hdr_host);
+    mb.hdr_host = nullptr;
+  }
+  nut_ctx_destroy(mb.ctx);
+  mb.ctx = nullptr;
+}
+
+nut_status check_dist(nut_dist *d, const char *what) {
+  if (!d || d->m.empty()) return fail(NUT_ERR_INVALID_ARG, std::string(what) + ": NULL nut_dist");
+  return NUT_OK;
+}
+
+// ------------------------------------------------------------------ group-by
+nut_status groupby_member(nut_dist *d, int l, const nut_agg_spec *spec, uint64_t hint, nut_groups **out) {
+  Member &mb = d->m[l];
+  nut_ctx *c = mb.ctx;
+  const int P = d->nranks, me = mb.rank;
+  *out = nullptr;
+  // 1. local pre-aggregation, partial groups partitioned by owner rank
+  nut_groups *g = nullptr;
+  uint64_t n = 0;
+  int W = 0;
+  std::vector<uint64_t> counts(P, 0);
+  nut_status st = nut_groupby(c, spec, hint, &g);
+  if (!st) st = nut_groups_size(g, &n);
+  if (!st) {
+    W = groups_width(g);
+    st = reserve(mb, 0, (uint64_t)W * n);
+  }
+  if (!st) st = nut_groups_partition(g, P, buf(mb, 0), n, counts.data());
+  std::vector<uint64_t> hdr(2 + P, 0), all;
+  hdr[1] = (uint64_t)W;
+  for (int q = 0; q < P; ++q) hdr[2 + q] = counts[q];
+  st = exchange_header(d, l, st, hdr, all);
+  if (st) {
+    nut_groups_free(g);
+    return st;
+  }
+  // 2. all-to-all of the partial groups (column-major segments of W words per group)
+  std::vector<size_t> sc(P), sd(P), rc(P), rd(P);
+  size_t stot = 0, rtot = 0;
+  for (int q = 0; q < P; ++q) {
+    if (all[(size_t)q * (2 + P) + 1] != (uint64_t)W) {
+      nut_groups_free(g);
+      return fail(NUT_ERR_INVALID_ARG, "nut_dist_groupby: ranks passed specs of different shapes");
+    }
+    sc[q] = (size_t)W * counts[q];
+    sd[q] = stot;
+    stot += sc[q];
+    rc[q] = (size_t)W * all[(size_t)q * (2 + P) + 2 + me];
+    rd[q] = rtot;
+    rtot += rc[q];
+  }
+  st = agree(d, l, reserve(mb, 1, rtot));
+  if (!st) st = alltoallv(d, l, buf(mb, 0), sc.data(), sd.data(), buf(mb, 1), rc.data(), rd.data());
+  // 3. the owner merges what it received
+  nut_groups *own = nullptr;
+  nut_prog_node nodes[NUT_MAX_AGGS];
+  nut_agg_spec ms;
+  for (int q = 0; q < P && !st; ++q) {
+    const uint64_t cq = rc[q] / W;
+    if (!cq && (own || q + 1 < P)) continue;
+    groups_merge_spec(g, buf(mb, 1) + rd[q], cq, &ms, nodes);  // cq = 0: an empty result of g's shape
+    st = own ? nut_groupby_accumulate(c, &ms, own) : nut_groupby(c, &ms, hint, &own);
+  }
+  nut_groups_free(g);
+  // 4. the owners' groups are gathered on rank 0, which folds them into its own
+  uint64_t n_own = 0;
+  if (!st) st = nut_groups_size(own, &n_own);
+  if (!st && me != 0) st = reserve(mb, 0, (uint64_t)W * n_own);
+  if (!st && me != 0) st = nut_groups_to_device(own, buf(mb, 0), n_own);
+  hdr.assign(2, 0);
+  hdr[1] = n_own;
+  st = exchange_header(d, l, st, hdr, all);
+  if (!st) {
+    std::fill(sc.begin(), sc.end(), 0);
+    std::fill(sd.begin(), sd.end(), 0);
+    std::fill(rc.begin(), rc.end(), 0);
+    rtot = 0;
+    for (int q = 0; q < P; ++q) {
+      rd[q] = rtot;
+      if (me == 0 && q != 0) rc[q] = (size_t)W * all[(size_t)q * 2 + 1];
+      rtot += rc[q];
+    }
+    if (me != 0) sc[0] = (size_t)W * n_own;
+    st = agree(d, l, reserve(mb, 1, rtot));
+  }
+  if (!st) st = alltoallv(d, l, buf(mb, 0), sc.data(), sd.data(), buf(mb, 1), rc.data(), rd.data());
+  if (!st && me == 0) {
+    for (int q = 1; q < P && !st; ++q) {
+      const uint64_t cq = rc[q] / W;
+      if (!cq) continue;
+      groups_merge_spec(own, buf(mb, 1) + rd[q], cq, &ms, nodes);
+      st = nut_groupby_accumulate(c, &ms, own);
+    }
+  }
+  if (!st) st = nut_ctx_sync(c);
+  if (st || me != 0) {
+    nut_groups_free(own);
+    return st;
+  }
+  *out = own;
+  return NUT_OK;
+}
+
+// ------------------------------------------------------------------ sample sort
+nut_status sort_member(nut_dist *d, int l, const int64_t *in, uint64_t n, const int64_t **out, uint64_t *out_n) {
+  Member &mb = d->m[l];
+  nut_ctx *c = mb.ctx;
+  const int P = d->nranks, me = mb.rank;
+  hipStream_t s = c->stream;
+  // 1. a strided sample of the local keys, all-gathered; splitters at the pooled quantiles
+  nut_status st = reserve(mb, 3, 2 * (uint64_t)kSamples + (uint64_t)P * kSamples);
+  if (!st && n) {
+    std::vector<int64_t> idx(kSamples);
+    for (int i = 0; i < kSamples; ++i) idx[i] = (int64_t)(((unsigned __int128)i * n) / kSamples);
+    int64_t *didx = (int64_t *)buf(mb, 3);
+    hipError_t e = hipMemcpyAsync(didx, idx.data(), kSamples * 8, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);  // idx is pageable: complete before it goes
+    st = e == hipSuccess ? nut_gather_u64(c, (const uint64_t *)in, didx, kSamples, 0, buf(mb, 3) + kSamples)
+                         : hip_fail(e, "nut_dist_sort_i64 sample indices");
+  }
+  std::vector<uint64_t> hdr(2, 0), all;
+  hdr[1] = n ? 1 : 0;
+  st = exchange_header(d, l, st, hdr, all);
+  if (st) return st;
+  uint64_t *pool_dev = buf(mb, 3) + 2 * kSamples;
+  st = allgather(d, l, buf(mb, 3) + kSamples, pool_dev, kSamples);
+  if (st) return st;
+  std::vector<int64_t> pool((size_t)P * kSamples);
+  NUT_HIP(hipMemcpyAsync(pool.data(), pool_dev, pool.size() * 8, hipMemcpyDeviceToHost, s));
+  NUT_HIP(hipStreamSynchronize(s));
+  std::vector<int64_t> live;
+  live.reserve(pool.size());
+  for (int q = 0; q < P; ++q)
+    if (all[(size_t)q * 2 + 1]) live.insert(live.end(), pool.begin() + (size_t)q * kSamples, pool.begin() + (size_t)(q + 1) * kSamples);
+  std::sort(live.begin(), live.end());
+  std::vector<int64_t> spl(P > 1 ? P - 1 : 1, 0);
+  for (int i = 1; i < P; ++i) spl[i - 1] = live.empty() ? 0 : live[(live.size() * (size_t)i) / P];
+  // 2. stable partition into P key ranges
+  std::vector<uint64_t> counts(P, 0);
+  st = reserve(mb, 0, n);
+  if (!st) st = nut_partition_i64(c, in, n, spl.data(), P - 1, (int64_t *)buf(mb, 0), counts.data());
+  hdr.assign(1 + P, 0);
+  for (int q = 0; q < P; ++q) hdr[1 + q] = counts[q];
+  st = exchange_header(d, l, st, hdr, all);
+  if (st) return st;
+  std::vector<size_t> sc(P), sd(P), rc(P), rd(P);
+  size_t stot = 0, rtot = 0;
+  for (int q = 0; q < P; ++q) {
+    sc[q] = counts[q];
+    sd[q] = stot;
+    stot += sc[q];
+    rc[q] = all[(size_t)q * (1 + P) + 1 + me];
+    rd[q] = rtot;
+    rtot += rc[q];
+  }
+  st = reserve(mb, 1, rtot);
+  if (!st) st = reserve(mb, 2, rtot);
+  st = agree(d, l, st);
+  // 3. one all-to-all of keys, then the local radix sort of the received range
+  if (!st) st = alltoallv(d, l, buf(mb, 0), sc.data(), sd.data(), buf(mb, 1), rc.data(), rd.data());
+  if (!st) st = nut_sort_i64(c, (const int64_t *)buf(mb, 1), (int64_t *)buf(mb, 2), rtot);
+  if (!st) st = nut_ctx_sync(c);
+  if (st) return st;
+  *out = (const int64_t *)buf(mb, 2);
+  *out_n = rtot;
+  return NUT_OK;
+}
+
+// ------------------------------------------------------------------ filter
+nut_status filter_member(nut_dist *d, int l, const int64_t *col, uint64_t n, int cmp, int64_t k, int64_t *out,
+                         uint64_t *out_n, uint64_t *out_offset) {
+  Member &mb = d->m[l];
+  uint64_t cnt = 0;
+  nut_status st = nut_filter_i64(mb.ctx, col, n, cmp, k, out, &cnt);
+  std::vector<uint64_t> hdr(2, 0), all;
+  hdr[1] = cnt;
+  st = exchange_header(d, l, st, hdr, all);
+  if (st) return st;
+  uint64_t off = 0;
+  for (int q = 0; q < mb.rank; ++q) off += all[(size_t)q * 2 + 1];
+  *out_n = cnt;
+  *out_offset = off;
+  return NUT_OK;
+}
+
+// ------------------------------------------------------------------ hash join
+nut_status join_member(nut_dist *d, int l, const int64_t *build, uint64_t nb, int64_t brow0, const int64_t *probe,
+                       uint64_t np, int64_t prow0, int type, const int64_t **pout, const int64_t **bout,
+                       uint64_t *npairs) {
+  Member &mb = d->m[l];
+  nut_ctx *c = mb.ctx;
+  const int P = d->nranks, me = mb.rank;
+  // buffers: 0/1 build keys/rows by part, 2/3 probe keys/rows by part, 4..7 received, 8/9 pairs
+  std::vector<uint64_t> bc(P, 0), pc(P, 0);
+  nut_status st = reserve(mb, 0, nb);
+  if (!st) st = reserve(mb, 1, nb);
+  if (!st) st = reserve(mb, 2, np);
+  if (!st) st = reserve(mb, 3, np);
+  if (!st) st = nut_hash_partition_i64(c, build, nb, P, brow0, (int64_t *)buf(mb, 0), (int64_t *)buf(mb, 1), bc.data());
+  if (!st) st = nut_hash_partition_i64(c, probe, np, P, prow0, (int64_t *)buf(mb, 2), (int64_t *)buf(mb, 3), pc.data());
+  std::vector<uint64_t> hdr(1 + 2 * P, 0), all;
+  for (int q = 0; q < P; ++q) hdr[1 + q] = bc[q], hdr[1 + P + q] = pc[q];
+  st = exchange_header(d, l, st, hdr, all);
+  if (st) return st;
+  const size_t w = 1 + 2 * (size_t)P;
+  std::vector<size_t> bsc(P), bsd(P), brc(P), brd(P), psc(P), psd(P), prc(P), prd(P);
+  size_t bs = 0, br = 0, ps = 0, pr = 0;
+  for (int q = 0; q < P; ++q) {
+    bsc[q] = bc[q], bsd[q] = bs, bs += bc[q];
+    psc[q] = pc[q], psd[q] = ps, ps += pc[q];
+    brc[q] = all[q * w + 1 + me], brd[q] = br, br += brc[q];
+    prc[q] = all[q * w + 1 + P + me], prd[q] = pr, pr += prc[q];
+  }
+  st = reserve(mb, 4, br);
+  if (!st) st = reserve(mb, 5, br);
+  if (!st) st = reserve(mb, 6, pr);
+  if (!st) st = reserve(mb, 7, pr);
+  st = agree(d, l, st);
+  if (!st) st = alltoallv(d, l, buf(mb, 0), bsc.data(), bsd.data(), buf(mb, 4), brc.data(), brd.data());
+  if (!st) st = alltoallv(d, l, buf(mb, 1), bsc.data(), bsd.data(), buf(mb, 5), brc.data(), brd.data());
+  if (!st) st = alltoallv(d, l, buf(mb, 2), psc.data(), psd.data(), buf(mb, 6), prc.data(), prd.data());
+  if (!st) st = alltoallv(d, l, buf(mb, 3), psc.data(), psd.data(), buf(mb, 7), prc.data(), prd.data());
+  if (st) return st;
+  // local join of what this rank owns; local pair indices -> global rows
+  nut_join *j = nullptr;
+  uint64_t np2 = 0;
+  st = nut_join_i64(c, (const int64_t *)buf(mb, 4), br, (const int64_t *)buf(mb, 6), pr, type, &j, &np2);
+  if (!st) st = reserve(mb, 0, np2);  // the send buffers are free again: local pair indices
+  if (!st) st = reserve(mb, 1, np2);
+  if (!st) st = reserve(mb, 8, np2);
+  if (!st) st = reserve(mb, 9, np2);
+  if (!st) st = nut_join_write(j, (int64_t *)buf(mb, 0), (int64_t *)buf(mb, 1));
+  nut_join_free(j);
+  if (!st) st = nut_gather_u64(c, buf(mb, 7), (const int64_t *)buf(mb, 0), np2, ~0ull, buf(mb, 8));
+  if (!st) st = nut_gather_u64(c, buf(mb, 5), (const int64_t *)buf(mb, 1), np2, ~0ull, buf(mb, 9));
+  if (!st) st = nut_ctx_sync(c);
+  if (st) return st;
+  *pout = (const int64_t *)buf(mb, 8);
+  *bout = (const int64_t *)buf(mb, 9);
+  *npairs = np2;
+  return NUT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+nut_status nut_dist_unique_id(void *id) {
+  if (!id) return fail(NUT_ERR_INVALID_ARG, "nut_dist_unique_id: NULL id");
+  const Rccl *r = rccl();
+  if (!r) return fail(NUT_ERR_UNSUPPORTED, g_rccl.load_error);
+  ncclUniqueId u;
+  ncclResult_t e = r->get_unique_id(&u);
+  if (e != ncclSuccess) return rccl_fail(r, e, "ncclGetUniqueId");
+  memcpy(id, &u, NUT_DIST_ID_BYTES);
+  return NUT_OK;
+}
+
+nut_status nut_dist_create(int ndev, const int *devs, nut_dist **out) {
+  if (!out || !devs || ndev < 1 || ndev > kMaxRanks) return fail(NUT_ERR_INVALID_ARG, "nut_dist_create: bad argument");
+  *out = nullptr;
+  const Rccl *r = rccl();
+  if (!r) return fail(NUT_ERR_UNSUPPORTED, g_rccl.load_error);
+  nut_dist *d = new nut_dist();
+  d->mode = nut_dist::kRcclAll;
+  d->nranks = ndev;
+  d->r = r;
+  d->m.resize(ndev);
+  std::vector<ncclComm_t> comms(ndev, nullptr);
+  nut_status st = NUT_OK;
+  for (int i = 0; i < ndev && !st; ++i) {
+    d->m[i].rank = i;
+    st = member_init(d, d->m[i], devs[i]);
+  }
+  if (!st) {
+    ncclResult_t e = r->comm_init_all(comms.data(), ndev, devs);
+    (void)hipGetLastError();
+    if (e != ncclSuccess) st = rccl_fail(r, e, "ncclCommInitAll");
+  }
+  for (int i = 0; i < ndev; ++i) d->m[i].comm = comms[i];
+  if (st) {
+    nut_dist_destroy(d);
+    return st;
+  }
+  *out = d;
+  return NUT_OK;
+}
+
+nut_status nut_dist_create_rank(int nranks, int rank, const void *id, int device, nut_dist **out) {
+  if (!out || !id || nranks < 1 || nranks > kMaxRanks || rank < 0 || rank >= nranks)
+    return fail(NUT_ERR_INVALID_ARG, "nut_dist_create_rank: bad argument");
+  *out = nullptr;
+  const Rccl *r = rccl();
+  if (!r) return fail(NUT_ERR_UNSUPPORTED, g_rccl.load_error);
+  nut_dist *d = new nut_dist();
+  d->mode = nut_dist::kRcclRank;
+  d->nranks = nranks;
+  d->first_rank = rank;
+  d->r = r;
+  d->m.resize(1);
+  d->m[0].rank = rank;
+  nut_status st = member_init(d, d->m[0], device);
+  if (!st) {
+    DeviceGuard dg(device);
+    ncclUniqueId u;
+    memcpy(&u, id, NUT_DIST_ID_BYTES);
+    ncclResult_t e = r->comm_init_rank(&d->m[0].comm, nranks, u, rank);
+    (void)hipGetLastError();
+    if (e != ncclSuccess) {
+      d->m[0].comm = nullptr;
+      st = rccl_fail(r, e, "ncclCommInitRank");
+    }
+  }
+  if (st) {
+    nut_dist_destroy(d);
+    return st;
+  }
+  *out = d;
+  return NUT_OK;
+}
+
+nut_status nut_dist_create_virtual(int nranks, int device, nut_dist **out) {
+  if (!out || nranks < 1 || nranks > kMaxRanks) return fail(NUT_ERR_INVALID_ARG, "nut_dist_create_virtual: bad argument");
+  *out = nullptr;
+  nut_dist *d = new nut_dist();
+  d->mode = nut_dist::kVirtual;
+  d->nranks = nranks;
+  d->hub.n = nranks;
+  d->hub.post.resize(nranks);
+  d->m.resize(nranks);
+  nut_status st = NUT_OK;
+  for (int i = 0; i < nranks && !st; ++i) {
+    d->m[i].rank = i;
+    st = member_init(d, d->m[i], device);
+  }
+  if (st) {
+    nut_dist_destroy(d);
+    return st;
+  }
+  *out = d;
+  return NUT_OK;
+}
+
+nut_status nut_dist_info(const nut_dist *d, int *nranks, int *nlocal, int *first_rank) {
+  if (!d) return fail(NUT_ERR_INVALID_ARG, "nut_dist_info: NULL nut_dist");
+  if (nranks) *nranks = d->nranks;
+  if (nlocal) *nlocal = (int)d->m.size();
+  if (first_rank) *first_rank = d->first_rank;
+  return NUT_OK;
+}
+
+nut_ctx *nut_dist_ctx(nut_dist *d, int local) {
+  if (!d || local < 0 || local >= (int)d->m.size()) return nullptr;
+  return d->m[local].ctx;
+}
+
+void nut_dist_destroy(nut_dist *d) {
+  if (!d) return;
+  for (auto &mb : d->m) {
+    if (mb.comm && d->r) {
+      DeviceGuard dg(mb.ctx ? mb.ctx->device : 0);
+      if (mb.ctx) (void)hipStreamSynchronize(mb.ctx->stream);
+      (void)d->r->comm_destroy(mb.comm);
+    }
+    mb.comm = nullptr;
+    member_free(mb);
+  }
+  delete d;
+}
+
+nut_status nut_dist_groupby(nut_dist *d, const nut_agg_spec *specs, uint64_t group_hint, nut_groups **out) {
+  nut_status st = check_dist(d, "nut_dist_groupby");
+  if (st) return st;
+  if (!specs || !out) return fail(NUT_ERR_INVALID_ARG, "nut_dist_groupby: NULL argument");
+  return run_members(d, [&](int l) { return groupby_member(d, l, &specs[l], group_hint, &out[l]); });
+}
+
+nut_status nut_dist_sort_i64(nut_dist *d, const int64_t *const *in, const uint64_t *n, const int64_t **out,
+                             uint64_t *out_n) {
+  nut_status st = check_dist(d, "nut_dist_sort_i64");
+  if (st) return st;
+  if (!in || !n || !out || !out_n) return fail(NUT_ERR_INVALID_ARG, "nut_dist_sort_i64: NULL argument");
+  return run_members(d, [&](int l) { return sort_member(d, l, in[l], n[l], &out[l], &out_n[l]); });
+}
+
+nut_status nut_dist_filter_i64(nut_dist *d, const int64_t *const *col, const uint64_t *n, int cmp, int64_t k,
+                               int64_t *const *out, uint64_t *out_n, uint64_t *out_offset) {
+  nut_status st = check_dist(d, "nut_dist_filter_i64");
+  if (st) return st;
+  if (!col || !n || !out || !out_n || !out_offset) return fail(NUT_ERR_INVALID_ARG, "nut_dist_filter_i64: NULL argument");
+  return run_members(d, [&](int l) {
+    return filter_member(d, l, col[l], n[l], cmp, k, out[l], &out_n[l], &out_offset[l]);
+  });
+}
+
+nut_status nut_dist_join_i64(nut_dist *d, const int64_t *const *build, const uint64_t *nbuild, const int64_t *build_row0,
+                             const int64_t *const *probe, const uint64_t *nprobe, const int64_t *probe_row0,
+                             int join_type, const int64_t **probe_idx, const int64_t **build_idx, uint64_t *npairs) {
+  nut_status st = check_dist(d, "nut_dist_join_i64");
+  if (st) return st;
+  if (!build || !nbuild || !build_row0 || !probe || !nprobe || !probe_row0 || !probe_idx || !build_idx || !npairs)
+    return fail(NUT_ERR_INVALID_ARG, "nut_dist_join_i64: NULL argument");
+  return run_members(d, [&](int l) {
+    return join_member(d, l, build[l], nbuild[l], build_row0[l], probe[l], nprobe[l], probe_row0[l], join_type,
+                       &probe_idx[l], &build_idx[l], &npairs[l]);
+  });
+}
+
+}  // extern "C"

@@ -14,6 +14,8 @@ counts[p] groups as (nkeys + naggs) consecutive 64-bit columns.
 """
 from __future__ import annotations
 
+import ctypes as C
+import weakref
 from typing import Callable, List, Optional
 
 import numpy as np
@@ -214,3 +216,169 @@ def distributed_sort(local: torch.Tensor, partition: Callable, sort: Callable, g
     part, counts = partition(local, splitters)
     recv = exchange_keys(part, counts, group)
     return sort(recv)
+
+
+# ---------------------------------------------------------------------------- nut_dist
+class _MemberEx:
+    """What Groups needs of an executor: the member's context and device."""
+
+    def __init__(self, ctx, device: torch.device):
+        self.ctx = ctx
+        self.device = device
+
+
+class NutDist:
+    """The library's own multi-GPU path (include/nutexec.h nut_dist_*): RCCL communicators
+    and the partition / all-to-all / merge steps live inside libnutexec.so, so a host
+    without torch.distributed (the Rust / C hosts of INTEGRATION.md) drives every GPU of
+    the exchange through the C ABI alone.  Three constructors:
+      NutDist.create([0, 1, ...])          one process drives several GPUs (ncclCommInitAll)
+      NutDist.create_rank(P, r, uid, dev)  one process per GPU (ncclCommInitRank); rank 0
+                                           makes `uid` with NutDist.unique_id()
+      NutDist.virtual(P, dev)              P ranks on one GPU, exchanges as device copies
+    Every call takes one entry per local member (member l = global rank first_rank + l)."""
+
+    def __init__(self, handle: C.c_void_p, devices):
+        from ._lib import lib
+        self.h = handle
+        P, nl, first = C.c_int(), C.c_int(), C.c_int()
+        _check(lib.nut_dist_info(self.h, C.byref(P), C.byref(nl), C.byref(first)), "nut_dist_info")
+        self.nranks, self.nlocal, self.first_rank = P.value, nl.value, first.value
+        self.devices = [torch.device("cuda", d) for d in devices]
+        self.members = [_MemberEx(C.c_void_p(lib.nut_dist_ctx(self.h, l)), self.devices[l]) for l in range(self.nlocal)]
+        self._results = weakref.WeakSet()  # Groups on member contexts: freed before the members
+
+    @staticmethod
+    def unique_id() -> bytes:
+        from ._lib import NUT_DIST_ID_BYTES, lib
+        buf = C.create_string_buffer(NUT_DIST_ID_BYTES)
+        _check(lib.nut_dist_unique_id(buf), "nut_dist_unique_id")
+        return buf.raw
+
+    @classmethod
+    def create(cls, devices) -> "NutDist":
+        from ._lib import lib
+        devs = (C.c_int * len(devices))(*devices)
+        h = C.c_void_p()
+        _check(lib.nut_dist_create(len(devices), devs, C.byref(h)), "nut_dist_create")
+        return cls(h, list(devices))
+
+    @classmethod
+    def create_rank(cls, nranks: int, rank: int, uid: bytes, device: int) -> "NutDist":
+        from ._lib import lib
+        h = C.c_void_p()
+        _check(lib.nut_dist_create_rank(nranks, rank, C.create_string_buffer(uid, len(uid)), device, C.byref(h)),
+               "nut_dist_create_rank")
+        return cls(h, [device])
+
+    @classmethod
+    def virtual(cls, nranks: int, device: int = 0) -> "NutDist":
+        from ._lib import lib
+        h = C.c_void_p()
+        _check(lib.nut_dist_create_virtual(nranks, device, C.byref(h)), "nut_dist_create_virtual")
+        return cls(h, [device] * nranks)
+
+    def close(self) -> None:
+        from ._lib import lib
+        if self.h:
+            for g in list(self._results):  # a result must not outlive its member's context
+                g.free()
+            lib.nut_dist_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def ctx(self, l: int):
+        return self.members[l].ctx
+
+    def _ready(self):
+        # inputs come from torch's streams; the members run on their own
+        for d in set(self.devices):
+            torch.cuda.synchronize(d)
+
+    def _copy_out(self, l: int, ptr: int, n: int) -> torch.Tensor:
+        from ._lib import lib
+        out = torch.empty(n, dtype=torch.int64, device=self.devices[l])
+        if n:
+            torch.cuda.synchronize(self.devices[l])
+            _check(lib.nut_ctx_memcpy(self.members[l].ctx, C.c_void_p(out.data_ptr()), C.c_void_p(ptr), n * 8),
+                   "nut_ctx_memcpy")
+        return out
+
+    def groupby(self, queries, group_hint: int = 0):
+        """nut_dist_groupby: queries[l] = member l's AggQuery / ProgQuery over its shard.
+        Returns one entry per member: the global Groups on the member holding rank 0, None
+        on the others."""
+        from ._lib import NutAggSpec, lib
+        from .executor import Groups
+        specs = (NutAggSpec * self.nlocal)()
+        keep = []
+        for l, q in enumerate(queries):
+            s = q.to_spec(self.devices[l])
+            keep.append(s)
+            C.memmove(C.byref(specs[l]), C.byref(s), C.sizeof(NutAggSpec))
+        out = (C.c_void_p * self.nlocal)()
+        self._ready()
+        _check(lib.nut_dist_groupby(self.h, specs, group_hint, out), "nut_dist_groupby")
+        res = []
+        for l, q in enumerate(queries):
+            res.append(Groups(self.members[l], out[l], max(specs[l].nkeys, 1), q.result_types()) if out[l] else None)
+            if res[-1] is not None:
+                self._results.add(res[-1])
+        return res
+
+    def sort_i64(self, cols):
+        """nut_dist_sort_i64: member l's sorted key range (the r-th of the global order)."""
+        from ._lib import lib
+        ins = (C.c_void_p * self.nlocal)(*[c.data_ptr() if c.numel() else None for c in cols])
+        ns = (C.c_uint64 * self.nlocal)(*[c.numel() for c in cols])
+        outs = (C.c_void_p * self.nlocal)()
+        on = (C.c_uint64 * self.nlocal)()
+        self._ready()
+        _check(lib.nut_dist_sort_i64(self.h, ins, ns, outs, on), "nut_dist_sort_i64")
+        return [self._copy_out(l, outs[l], on[l]) for l in range(self.nlocal)]
+
+    def filter_i64(self, cols, op, k: int):
+        """nut_dist_filter_i64: [(selected values of member l, global offset)]."""
+        from ._lib import lib
+        from .executor import CMP
+        outs = [torch.empty(max(c.numel(), 1), dtype=torch.int64, device=self.devices[l]) for l, c in enumerate(cols)]
+        ins = (C.c_void_p * self.nlocal)(*[c.data_ptr() if c.numel() else None for c in cols])
+        ns = (C.c_uint64 * self.nlocal)(*[c.numel() for c in cols])
+        op_ = (C.c_void_p * self.nlocal)(*[o.data_ptr() for o in outs])
+        on = (C.c_uint64 * self.nlocal)()
+        off = (C.c_uint64 * self.nlocal)()
+        self._ready()
+        _check(lib.nut_dist_filter_i64(self.h, ins, ns, CMP[op] if isinstance(op, str) else int(op), int(k), op_, on,
+                                       off), "nut_dist_filter_i64")
+        return [(outs[l][:on[l]], int(off[l])) for l in range(self.nlocal)]
+
+    def join_i64(self, builds, probes, how: str = "inner", build_row0=None, probe_row0=None):
+        """nut_dist_join_i64: [(global probe rows, global build rows)] per member."""
+        from ._lib import lib
+        from .executor import Executor
+        L_ = self.nlocal
+        bro = build_row0 if build_row0 is not None else [0] * L_
+        pro = probe_row0 if probe_row0 is not None else [0] * L_
+        bp = (C.c_void_p * L_)(*[t.data_ptr() if t.numel() else None for t in builds])
+        bn = (C.c_uint64 * L_)(*[t.numel() for t in builds])
+        pp = (C.c_void_p * L_)(*[t.data_ptr() if t.numel() else None for t in probes])
+        pn = (C.c_uint64 * L_)(*[t.numel() for t in probes])
+        b0 = (C.c_int64 * L_)(*bro)
+        p0 = (C.c_int64 * L_)(*pro)
+        po = (C.c_void_p * L_)()
+        bo = (C.c_void_p * L_)()
+        npairs = (C.c_uint64 * L_)()
+        self._ready()
+        _check(lib.nut_dist_join_i64(self.h, bp, bn, b0, pp, pn, p0, Executor.JOIN_TYPES[how], po, bo, npairs),
+               "nut_dist_join_i64")
+        return [(self._copy_out(l, po[l], npairs[l]), self._copy_out(l, bo[l], npairs[l])) for l in range(L_)]
+
+
+def _check(status: int, where: str) -> None:
+    from ._lib import check
+    check(status, where)

@@ -19,6 +19,10 @@ def _build_native():
     mod.build()
     from oracle import oracle
     oracle.build()
+    spec = importlib.util.spec_from_file_location("_nut_c_hosts", ROOT / "tests" / "c" / "build.py")
+    hosts = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(hosts)
+    hosts.build()
 
 
 def pytest_configure(config):

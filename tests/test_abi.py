@@ -74,3 +74,21 @@ def test_library_is_gfx950_code_object():
     assert ".hip_fatbin" in out
     blob = LIB_PATH.read_bytes()
     assert b"gfx950" in blob
+
+
+def test_dist_loads_rccl_and_fails_cleanly_without_gpu():
+    """nut_dist_*: RCCL resolves (dlopen by soname) and makes a 128-byte unique id on a
+    host without a GPU; creating ranks fails with a status, not a crash."""
+    import torch
+    from nutdb_amd import NutError
+    from nutdb_amd.dist import NutDist
+    assert len(NutDist.unique_id()) == 128
+    if torch.cuda.is_available():
+        return
+    for make in (lambda: NutDist.virtual(2), lambda: NutDist.create([0])):
+        try:
+            make()
+        except NutError as e:
+            assert e.status != 0
+        else:
+            raise AssertionError("nut_dist created without a GPU")
