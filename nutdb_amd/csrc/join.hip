@@ -231,7 +231,8 @@ __global__ __launch_bounds__(HJ_THREADS) void hj_probe_kernel(HjTable t, const i
 #pragma unroll
   for (int i = 0; i < HJ_ITEMS; ++i) {
     const uint64_t r = base + (uint64_t)i * HJ_THREADS;
-    key[i] = r < n ? __builtin_nontemporal_load(probe + r) : 0;
+    // clamped, unconditional: a conditional load compiles to a branch and a wait per item
+    key[i] = __builtin_nontemporal_load(probe + (r < n ? r : n - 1));
     s[i] = (uint32_t)hj_home(key[i], t);
     m[i] = 0;
     first[i] = 0;
@@ -244,12 +245,13 @@ __global__ __launch_bounds__(HJ_THREADS) void hj_probe_kernel(HjTable t, const i
   // (unconditionally — a finished item re-reads its empty slot from cache — so all of
   // them are in flight together), then consumes them
   while (__any(act)) {
+    // finished items issue no request; their v[i] is never read (occ below tests act), so
+    // it needs no default — a default merged with the loaded value made the compiler wait
+    // for each load before the next (one round trip per item instead of one per round)
     i64x2 v[HJ_ITEMS];
 #pragma unroll
-    for (int i = 0; i < HJ_ITEMS; ++i) {
-      v[i] = i64x2{0, -1};
-      if ((act >> i) & 1u) v[i] = t.slot[s[i]];  // finished items issue no request
-    }
+    for (int i = 0; i < HJ_ITEMS; ++i)
+      if ((act >> i) & 1u) v[i] = t.slot[s[i]];
 #pragma unroll
     for (int i = 0; i < HJ_ITEMS; ++i) {
       const bool occ = ((act >> i) & 1u) && v[i].y != -1;

@@ -32,13 +32,15 @@ namespace nut {
 
 constexpr int MH_THREADS = 256;
 constexpr uint32_t MH_TILE = 1u << 16;  // keys per histogram / copy tile
-constexpr int MS_THREADS = 512;
+constexpr int MS_THREADS = 1024;
 constexpr int MS_ITEMS = 16;
-constexpr uint32_t MS_TILE = MS_THREADS * MS_ITEMS;  // 8192 keys per scatter tile
-constexpr int MS_BINS = 256;
+constexpr uint32_t MS_TILE = MS_THREADS * MS_ITEMS;  // 16384 keys per scatter tile
+constexpr int MS_BITS = 9;                          // digit width of a scatter level
+constexpr int MS_BINS = 1 << MS_BITS;               // 512: 32 keys (256 B) per digit per tile
+static_assert(MS_BINS <= MS_THREADS, "one scan thread per digit");
 // local-sort classes: threads x max items per thread (ms_local_kernel)
 constexpr int LS_S_THREADS = 256, LS_S_ITEMS = 8;    // <= 2048 keys
-constexpr int LS_M_THREADS = 512, LS_M_ITEMS = 16;   // <= 8192 keys
+constexpr int LS_M_THREADS = 512, LS_M_ITEMS = 12;   // <= 6144 keys, 2 workgroups per CU
 constexpr int LS_L_THREADS = 1024, LS_L_ITEMS = 24;  // <= 24576 keys
 constexpr uint64_t LS_S_CAP = LS_S_THREADS * LS_S_ITEMS;
 constexpr uint64_t LS_M_CAP = LS_M_THREADS * LS_M_ITEMS;
@@ -48,15 +50,22 @@ constexpr uint64_t LS_CAP = LS_L_THREADS * LS_L_ITEMS;
 struct MsSeg {
   uint64_t start, count;
   uint32_t buf;  // 0: caller's input (raw int64: flip on load), 1: out, 2: tmp
-  uint32_t aux;  // hist / scatter / copy: first tile of the segment; local sort: digits left
+  uint32_t aux;  // hist / scatter / copy: first tile of the segment; local sort: hi, the
+                 // number of low bits of (key - base) its keys may still differ in
 };
 struct MsBufs {
   const uint64_t *in;
   uint64_t *a;  // out
   uint64_t *b;  // tmp
 };
-struct MsShifts {
-  int s[8];  // bit offsets of the varying digits, least significant first
+// The digit of a level: bits [shift, shift + log2(mask + 1)) of (key - base).  Every key
+// is >= base (the minimum, or 0), so (key - base) orders like key; subtracting the
+// minimum makes the first digit split a narrow key range (a sample-sort rank's) evenly.
+struct MsDigit {
+  uint64_t base;
+  int shift;
+  uint32_t mask;
+  __device__ __forceinline__ uint32_t operator()(uint64_t k) const { return (uint32_t)((k - base) >> shift) & mask; }
 };
 
 __device__ __forceinline__ const uint64_t *ms_src(const MsBufs &bf, uint32_t buf) {
@@ -65,12 +74,12 @@ __device__ __forceinline__ const uint64_t *ms_src(const MsBufs &bf, uint32_t buf
 
 // ---------------------------------------------------------------- level histogram
 __global__ __launch_bounds__(MH_THREADS) void ms_hist_kernel(MsBufs bf, const MsSeg *__restrict__ segs,
-                                                             const uint32_t *__restrict__ tile_seg, int shift,
+                                                             const uint32_t *__restrict__ tile_seg, MsDigit dg,
                                                              uint64_t flip, unsigned long long *__restrict__ hist,
-                                                             unsigned long long *__restrict__ orand) {
+                                                             unsigned long long *__restrict__ minmax) {
   __shared__ uint32_t h[MS_BINS];
   const int tid = threadIdx.x;
-  h[tid] = 0;
+  for (int i = tid; i < MS_BINS; i += MH_THREADS) h[i] = 0;
   __syncthreads();
   const uint32_t s = tile_seg[blockIdx.x];
   const MsSeg sg = segs[s];
@@ -78,51 +87,51 @@ __global__ __launch_bounds__(MH_THREADS) void ms_hist_kernel(MsBufs bf, const Ms
   const uint32_t cnt = (uint32_t)min<uint64_t>(MH_TILE, sg.count - lo);
   const uint64_t *src = ms_src(bf, sg.buf) + sg.start + lo;
   const uint64_t f = sg.buf == 0 ? flip : 0;
-  uint64_t vor = 0, vand = ~0ull;
+  uint64_t vmin = ~0ull, vmax = 0;
   for (uint32_t i = tid; i < cnt; i += MH_THREADS * 8) {
     uint64_t k[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const uint32_t idx = i + j * MH_THREADS;
-      k[j] = idx < cnt ? (__builtin_nontemporal_load(src + idx) ^ f) : 0;
-    }
+    for (int j = 0; j < 8; ++j)  // unconditional (clamped) loads: a conditional one compiles to
+      k[j] = __builtin_nontemporal_load(src + min(i + j * MH_THREADS, cnt - 1)) ^ f;  // a branch + wait per key
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       if (i + j * MH_THREADS < cnt) {
-        atomicAdd(&h[(k[j] >> shift) & 255], 1u);
-        vor |= k[j];
-        vand &= k[j];
+        atomicAdd(&h[dg(k[j])], 1u);
+        vmin = k[j] < vmin ? k[j] : vmin;
+        vmax = k[j] > vmax ? k[j] : vmax;
       }
     }
   }
-  if (orand) {
+  if (minmax) {
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
-      vor |= __shfl_xor(vor, off, 64);
-      vand &= __shfl_xor(vand, off, 64);
+      const uint64_t a = __shfl_xor(vmin, off, 64), b = __shfl_xor(vmax, off, 64);
+      vmin = a < vmin ? a : vmin;
+      vmax = b > vmax ? b : vmax;
     }
     if ((tid & 63) == 0) {
-      atomicOr(&orand[0], (unsigned long long)vor);
-      atomicAnd(&orand[1], (unsigned long long)vand);
+      atomicMin(&minmax[0], (unsigned long long)vmin);
+      atomicMax(&minmax[1], (unsigned long long)vmax);
     }
   }
   __syncthreads();
-  if (h[tid]) atomicAdd(&hist[(uint64_t)s * MS_BINS + tid], (unsigned long long)h[tid]);
+  for (int i = tid; i < MS_BINS; i += MH_THREADS)
+    if (h[i]) atomicAdd(&hist[(uint64_t)s * MS_BINS + i], (unsigned long long)h[i]);
 }
 
 // ---------------------------------------------------------------- scatter level
-// Unstable partition of every listed segment by digit (key >> shift) & 255 into the other
-// buffer (in / tmp -> ... see ms_dst).  cursor[s][d] starts at the absolute position of
+// Unstable partition of every listed segment by its digit into the other buffer (in /
+// tmp -> out ... see ms_dst).  cursor[s][d] starts at the absolute position of
 // sub-segment (s, d) and is advanced by one atomic per (tile, digit).
 __device__ __forceinline__ uint64_t *ms_dst(const MsBufs &bf, uint32_t buf) { return buf == 2 ? bf.a : bf.b; }
 
 // Persistent: workgroup b takes tiles b, b + grid, ...; the next tile's keys are loaded into
 // the key registers as soon as the current tile is staged in LDS, so its HBM latency hides
 // behind the current tile's write-out (and the segment lookup behind the ranking).
-__global__ __launch_bounds__(MS_THREADS, 4) void ms_scatter_kernel(MsBufs bf, const MsSeg *__restrict__ segs,
+__global__ __launch_bounds__(MS_THREADS) void ms_scatter_kernel(MsBufs bf, const MsSeg *__restrict__ segs,
                                                                    const uint32_t *__restrict__ tile_seg, uint32_t ntiles,
-                                                                int shift, uint64_t flip,
-                                                                unsigned long long *__restrict__ cursor) {
+                                                                   MsDigit dg, uint64_t flip,
+                                                                   unsigned long long *__restrict__ cursor) {
   __shared__ uint64_t s_keys[MS_TILE];
   __shared__ uint32_t s_cnt[MS_BINS];
   __shared__ uint32_t s_tex[MS_BINS];
@@ -136,11 +145,10 @@ __global__ __launch_bounds__(MS_THREADS, 4) void ms_scatter_kernel(MsBufs bf, co
     const uint32_t cn = (uint32_t)min<uint64_t>(MS_TILE, g.count - lo);
     const uint64_t *sp = ms_src(bf, g.buf) + g.start + lo;
     const uint64_t ff = g.buf == 0 ? flip : 0;
+    // every load unconditional (clamped to the tile): all MS_ITEMS stay in flight together
 #pragma unroll
-    for (int i = 0; i < MS_ITEMS; ++i) {
-      const uint32_t idx = (uint32_t)i * MS_THREADS + tid;
-      key[i] = idx < cn ? (__builtin_nontemporal_load(sp + idx) ^ ff) : 0;
-    }
+    for (int i = 0; i < MS_ITEMS; ++i)
+      key[i] = __builtin_nontemporal_load(sp + min((uint32_t)i * MS_THREADS + tid, cn - 1)) ^ ff;
   };
   uint32_t s = tile_seg[t];
   MsSeg sg = segs[s];
@@ -153,13 +161,13 @@ __global__ __launch_bounds__(MS_THREADS, 4) void ms_scatter_kernel(MsBufs bf, co
     const uint32_t ns = next < ntiles ? tile_seg[next] : 0;
     if (tid < MS_BINS) s_cnt[tid] = 0;
     __syncthreads();
-    uint32_t rk[MS_ITEMS / 2];  // ranks in the tile's digit run (< 8192), 16-bit pairs
+    uint32_t rk[MS_ITEMS / 2];  // ranks in the tile's digit run (< 16384), 16-bit pairs
 #pragma unroll
     for (int i = 0; i < MS_ITEMS; i += 2) rk[i / 2] = 0;
 #pragma unroll
     for (int i = 0; i < MS_ITEMS; ++i) {
       const uint32_t idx = (uint32_t)i * MS_THREADS + tid;
-      if (idx < cnt) rk[i / 2] |= atomicAdd(&s_cnt[(key[i] >> shift) & 255], 1u) << (16 * (i & 1));
+      if (idx < cnt) rk[i / 2] |= atomicAdd(&s_cnt[dg(key[i])], 1u) << (16 * (i & 1));
     }
     __syncthreads();
     uint32_t c = 0, incl = 0;
@@ -187,7 +195,7 @@ __global__ __launch_bounds__(MS_THREADS, 4) void ms_scatter_kernel(MsBufs bf, co
 #pragma unroll
     for (int i = 0; i < MS_ITEMS; ++i) {
       const uint32_t idx = (uint32_t)i * MS_THREADS + tid;
-      if (idx < cnt) s_keys[s_tex[(key[i] >> shift) & 255] + ((rk[i / 2] >> (16 * (i & 1))) & 0xFFFFu)] = key[i];
+      if (idx < cnt) s_keys[s_tex[dg(key[i])] + ((rk[i / 2] >> (16 * (i & 1))) & 0xFFFFu)] = key[i];
     }
     MsSeg nsg = sg;
     if (next < ntiles) {  // the key registers are free: fetch the next tile now
@@ -200,7 +208,7 @@ __global__ __launch_bounds__(MS_THREADS, 4) void ms_scatter_kernel(MsBufs bf, co
       const uint32_t j = (uint32_t)i * MS_THREADS + tid;
       if (j < cnt) {
         const uint64_t k = s_keys[j];
-        dst[s_gb[(k >> shift) & 255] + j] = k;
+        dst[s_gb[dg(k)] + j] = k;
       }
     }
     if (next >= ntiles) break;
@@ -211,13 +219,56 @@ __global__ __launch_bounds__(MS_THREADS, 4) void ms_scatter_kernel(MsBufs bf, co
   }
 }
 
+// ---------------------------------------------------------------- device-planned level
+// After a level's histogram: one block per segment, one thread per digit.  The digit's
+// exclusive prefix gives the scatter cursor and the sub-segment it will hold; the
+// sub-segment goes straight into the list of its local-sort class (3 = too large for one:
+// the host takes it to another level).  Replaces a host round trip over every
+// (segment, digit) pair — 2^18 of them at the second level of 1.25e9 keys.
+__global__ __launch_bounds__(MS_BINS) void ms_plan_kernel(const MsSeg *__restrict__ segs,
+                                                          const unsigned long long *__restrict__ hist, int hi,
+                                                          unsigned long long *__restrict__ cursor,
+                                                          MsSeg *__restrict__ lists, uint64_t cap,
+                                                          unsigned int *__restrict__ counts) {
+  __shared__ unsigned long long s_wsum[MS_BINS / kWave];
+  const int d = threadIdx.x, lane = d & 63, wave = d >> 6;
+  const MsSeg sg = segs[blockIdx.x];
+  const uint64_t c = hist[(uint64_t)blockIdx.x * MS_BINS + d];
+  uint64_t incl = c;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint64_t y = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += y;
+  }
+  if (lane == 63) s_wsum[wave] = incl;
+  __syncthreads();
+  uint64_t add = 0;
+#pragma unroll
+  for (int w = 0; w < MS_BINS / kWave; ++w) add += (w < wave) ? s_wsum[w] : 0ull;
+  const uint64_t start = sg.start + incl - c + add;
+  cursor[(uint64_t)blockIdx.x * MS_BINS + d] = start;
+  // list slots: one atomic per (wave, class present) — a per-thread atomic on four
+  // addresses serialised 2^18 claims at the memory side (3 ms)
+  const int cls = c == 0 ? -1 : (c <= LS_S_CAP ? 0 : (c <= LS_M_CAP ? 1 : (c <= LS_CAP ? 2 : 3)));
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint64_t m = __ballot(cls == k);
+    if (!m) continue;
+    const int leader = __builtin_ctzll(m);
+    unsigned int b = 0;
+    if (lane == leader) b = atomicAdd(&counts[k], (unsigned int)__popcll(m));
+    b = __shfl(b, leader, 64);
+    if (cls == k) lists[(uint64_t)k * cap + b + lane_rank(m)] = MsSeg{start, c, sg.buf == 2 ? 1u : 2u, (uint32_t)hi};
+  }
+}
+
 // ---------------------------------------------------------------- local sort
-// One workgroup sorts one segment of <= THREADS * MAXK keys by its `aux` remaining varying
-// digits (sh.s[0 .. aux-1], least significant first) and writes it to out at the same range.
+// One workgroup sorts one segment of <= THREADS * MAXK keys, whose keys agree on every bit
+// of (key - base) at or above hi = aux, and writes it to out at the same range.
 //
 // Main path (MSD split + bitonic windows):
 //   1. the keys sit in registers; each takes a rank in its bucket with one LDS atomic, the
-//      bucket being the top log2(THREADS) remaining varying bits (unstable: keys only);
+//      bucket being the top SB bits of (key - base) below hi (unstable: keys only);
 //   2. an exclusive scan gives bucket offsets; buckets are grouped into WINDOWS — the
 //      positions from the first bucket start >= q*WS up to the next such start — so a window
 //      is a run of whole buckets of about WS + (one bucket) keys;
@@ -452,9 +503,9 @@ __device__ __forceinline__ void wave_bitonic32_multi(uint64_t (&v)[NR], int lane
   cx64<1, 1, NR>(v, lane);
 }
 
-template <int THREADS, int MAXK>
-__global__ __launch_bounds__(THREADS) void ms_local_kernel(MsBufs bf, const MsSeg *__restrict__ segs, MsShifts sh,
-                                                           uint64_t flip, uint32_t *__restrict__ fb) {
+template <int THREADS, int MAXK, bool PREFETCH>
+__global__ __launch_bounds__(THREADS, 4) void ms_local_kernel(MsBufs bf, const MsSeg *__restrict__ segs, uint32_t nseg,
+                                                           uint64_t base, uint64_t flip, uint32_t *__restrict__ fb) {
   using C = LocalCfg<THREADS, MAXK>;
   constexpr int WAVES = C::WAVES, NB = C::NB, SB = C::SB;
   __shared__ __attribute__((aligned(16))) char lds[C::BYTES];
@@ -464,27 +515,37 @@ __global__ __launch_bounds__(THREADS) void ms_local_kernel(MsBufs bf, const MsSe
   uint32_t *s_ws = s_win + C::NWIN;                        // 16 scan words
   uint32_t *s_misc = s_ws + 16;                            // [0] max window, [1] round split
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const MsSeg sg = segs[blockIdx.x];
+  uint64_t key[MAXK];
+  // segment g's keys into registers: item i of lane l in wave w = position w*64*K + i*64 + l
+  auto load = [&](const MsSeg &g) {
+    const uint32_t cc = (uint32_t)g.count, kk = (cc + THREADS - 1) / THREADS;
+    const uint32_t pp = (uint32_t)wave * kWave * kk + lane;
+    const uint64_t *sp = ms_src(bf, g.buf) + g.start;
+    const uint64_t ff = g.buf == 0 ? flip : 0;
+    // unconditional (clamped) loads, so that all MAXK are in flight at once
+#pragma unroll
+    for (int i = 0; i < MAXK; ++i) {
+      const uint32_t p = pp + (uint32_t)i * kWave;
+      const uint64_t v = __builtin_nontemporal_load(sp + min(p, cc - 1)) ^ ff;
+      key[i] = ((uint32_t)i < kk && p < cc) ? v : ~0ull;
+    }
+  };
+  // one segment; returns whether the next segment's keys were loaded (PREFETCH: as soon as
+  // this one's are staged, so their latency hides behind the window sorts).  Every early
+  // return is block-uniform.
+  auto process = [&](const uint32_t sidx, const MsSeg &sg, const MsSeg &nsg, const bool has_next) -> bool {
   const uint32_t c = (uint32_t)sg.count;
-  const int ndig = (int)sg.aux;
+  const int hi = (int)sg.aux;
   const uint32_t K = (c + THREADS - 1) / THREADS;
   const uint32_t pw = (uint32_t)wave * kWave * K + lane;
-  const uint64_t *src = ms_src(bf, sg.buf) + sg.start;
   uint64_t *dst = bf.a + sg.start;
-  const uint64_t f = sg.buf == 0 ? flip : 0;
-  uint64_t key[MAXK];
-#pragma unroll
-  for (int i = 0; i < MAXK; ++i) {
-    const uint32_t p = pw + (uint32_t)i * kWave;
-    if ((uint32_t)i < K) key[i] = p < c ? (src[p] ^ f) : ~0ull;
-  }
-  if (ndig == 0) {  // every key equal: copy
+  if (hi == 0) {  // every key equal: copy
 #pragma unroll
     for (int i = 0; i < MAXK; ++i) {
       const uint32_t p = pw + (uint32_t)i * kWave;
       if ((uint32_t)i < K && p < c) dst[p] = key[i] ^ flip;
     }
-    return;
+    return false;
   }
   if (MS_STOP(1)) {
     uint64_t x = 0;
@@ -492,17 +553,11 @@ __global__ __launch_bounds__(THREADS) void ms_local_kernel(MsBufs bf, const MsSe
     for (int i = 0; i < MAXK; ++i)
       if ((uint32_t)i < K) x ^= key[i];
     dst[tid] = x;
-    return;
+    return false;
   }
-  // ---- 1. bucket ranks: top SB remaining varying bits
-  const int top = sh.s[ndig - 1];
-  const int nxt = ndig >= 2 ? sh.s[ndig - 2] : -1;
-  constexpr int EXTRA = SB - 8;
-  auto bucket = [&](uint64_t k) -> uint32_t {
-    uint32_t b = ((uint32_t)(k >> top) & 255u) << EXTRA;
-    if (nxt >= 0) b |= (uint32_t)(k >> (nxt + 8 - EXTRA)) & ((1u << EXTRA) - 1u);
-    return b;
-  };
+  // ---- 1. bucket ranks: the top SB of the hi bits of (key - base) that may differ
+  //         (fewer than SB: zero-padded, so only some buckets are used)
+  auto bucket = [&](uint64_t k) -> uint32_t { return (uint32_t)(((k - base) << (64 - hi)) >> (64 - SB)); };
 #pragma unroll
   for (int j = 0; j < C::BPT; ++j) s_off[C::BPT * tid + j] = 0;
   if (tid == 0) {
@@ -530,29 +585,26 @@ __global__ __launch_bounds__(THREADS) void ms_local_kernel(MsBufs bf, const MsSe
     uint32_t tot;
     uint32_t e = block_excl_scan<THREADS>(sum, s_ws, &tot);
     __syncthreads();  // every count read before the starts overwrite them
+    // Window q starts at the first bucket start >= q * WS: the bucket b whose end
+    // (start + count) is the first >= q * WS > its start owns every q with q * WS in
+    // (start_b, end_b], and window q then starts at end_b (the next bucket's start).  Each
+    // thread assigns the windows its own buckets end — no search; usually none or one.
+    const uint32_t nqq = (c + LS_WS - 1) / LS_WS;
 #pragma unroll
     for (int j = 0; j < C::BPT; ++j) {
       s_off[C::BPT * tid + j] = e;
-      e += cb[j];
+      const uint32_t end = e + cb[j];
+      for (uint32_t q = e / LS_WS + 1; q * LS_WS <= end && q < nqq; ++q) s_win[q] = end;
+      e = end;
     }
-    if (tid == 0) s_off[NB] = c;
+    if (tid == 0) {
+      s_off[NB] = c;
+      s_win[0] = 0;
+      s_win[nqq] = c;
+    }
   }
   __syncthreads();
   const uint32_t nq = (c + LS_WS - 1) / LS_WS;
-#pragma unroll
-  for (int j = 0; j < C::WPT; ++j) {
-    const uint32_t q = (uint32_t)tid + (uint32_t)j * THREADS;
-    if (q < nq) {  // first bucket start >= q * WS
-      const uint32_t target = q * LS_WS;
-      uint32_t lo = 0;
-#pragma unroll
-      for (int step = NB / 2; step >= 1; step >>= 1)
-        if (s_off[lo + step - 1] < target) lo += step;
-      s_win[q] = s_off[lo];  // s_off[NB] = c bounds the search
-    }
-  }
-  if (tid == 0) s_win[nq] = c;
-  __syncthreads();
 #pragma unroll
   for (int j = 0; j < C::WPT; ++j) {
     const uint32_t q = (uint32_t)tid + (uint32_t)j * THREADS;
@@ -567,8 +619,8 @@ __global__ __launch_bounds__(THREADS) void ms_local_kernel(MsBufs bf, const MsSe
   const uint32_t split = c > (uint32_t)C::LDS_KEYS ? s_misc[1] : nq;
   const uint32_t mid = split < nq ? s_win[split] : c;
   if (s_misc[0] > (uint32_t)LS_MAX_WINDOW || c - mid > (uint32_t)C::LDS_KEYS) {
-    if (tid == 0) fb[1 + atomicAdd(&fb[0], 1u)] = blockIdx.x;  // uniform: to ms_lsd_kernel
-    return;
+    if (tid == 0) fb[1 + atomicAdd(&fb[0], 1u)] = sidx;  // uniform: to ms_lsd_kernel
+    return false;
   }
   // ---- 3. keys to their bucket positions: round 0's into LDS, round 1's parked in out at
   //         their final range (L2-resident; safe in place, every key is in registers)
@@ -583,13 +635,18 @@ __global__ __launch_bounds__(THREADS) void ms_local_kernel(MsBufs bf, const MsSe
         dst[pos] = key[i];
     }
   }
+  bool pf = false;
+  if (PREFETCH && has_next) {  // the key registers are free: fetch the next segment now
+    load(nsg);
+    pf = true;
+  }
   if (MS_STOP(3)) {
     __syncthreads();
     dst[tid] = s_keys[tid];
-    return;
+    return pf;
   }
   for (int round = 0; round < 2; ++round) {
-    const uint32_t base = round ? mid : 0;
+    const uint32_t rbase = round ? mid : 0;
     const uint32_t w0 = round ? split : 0, w1 = round ? nq : split;
     if (w0 >= w1) break;
     if (round) {  // round 0's windows are done with LDS: bring the parked keys back
@@ -603,7 +660,7 @@ __global__ __launch_bounds__(THREADS) void ms_local_kernel(MsBufs bf, const MsSe
 #pragma unroll 1
     for (int j = 0; j < C::WPT && !MS_STOP(5); ++j) {
       const uint32_t t = w0 + (uint32_t)tid + (uint32_t)j * THREADS;
-      const uint32_t wa = t < w1 ? s_win[t] - base : 0, wm = t < w1 ? s_win[t + 1] - s_win[t] : 0;
+      const uint32_t wa = t < w1 ? s_win[t] - rbase : 0, wm = t < w1 ? s_win[t + 1] - s_win[t] : 0;
       const bool mine = wm > 1 && wm <= (uint32_t)LS_LANE_N;
       if (__ballot(mine)) {
         uint64_t v[LS_LANE_N];
@@ -646,7 +703,28 @@ __global__ __launch_bounds__(THREADS) void ms_local_kernel(MsBufs bf, const MsSe
     __syncthreads();
     if (MS_STOP(4)) continue;
     const uint32_t rend = round ? c : mid;
-    for (uint32_t j = tid; j < rend - base; j += THREADS) dst[base + j] = s_keys[j] ^ flip;
+    for (uint32_t j = tid; j < rend - rbase; j += THREADS) dst[rbase + j] = s_keys[j] ^ flip;
+  }
+  return pf;
+  };
+  uint32_t sidx = blockIdx.x;
+  if (sidx >= nseg) return;
+  MsSeg sg = segs[sidx];
+  load(sg);
+  if constexpr (!PREFETCH) {  // one segment per workgroup (grid = nseg)
+    (void)process(sidx, sg, sg, false);
+    return;
+  }
+  for (;;) {  // persistent: segments blockIdx.x, + gridDim.x, ...
+    const uint32_t nidx = sidx + gridDim.x;
+    const bool has_next = nidx < nseg;
+    const MsSeg nsg = has_next ? segs[nidx] : sg;
+    const bool pf = process(sidx, sg, nsg, has_next);
+    if (!has_next) break;
+    if (!pf) load(nsg);
+    __syncthreads();  // LDS is reused by the next segment
+    sidx = nidx;
+    sg = nsg;
   }
 }
 
@@ -654,20 +732,22 @@ __global__ __launch_bounds__(THREADS) void ms_local_kernel(MsBufs bf, const MsSe
 // get stable LSD passes in LDS.  Item i of lane l in wave w sits at canonical position
 // w*64*K + i*64 + l; positions >= count hold all-ones padding, which a stable sort keeps
 // behind every real key.
+constexpr int LSD_BINS = 256;  // 8-bit passes
+
 template <int THREADS, int MAXK>
-__global__ __launch_bounds__(THREADS) void ms_lsd_kernel(MsBufs bf, const MsSeg *__restrict__ segs, MsShifts sh,
+__global__ __launch_bounds__(THREADS) void ms_lsd_kernel(MsBufs bf, const MsSeg *__restrict__ segs, uint64_t base,
                                                          uint64_t flip, const uint32_t *__restrict__ fb) {
   using C = LocalCfg<THREADS, MAXK>;
   constexpr int WAVES = C::WAVES;
   if (blockIdx.x >= fb[0]) return;
   __shared__ uint32_t s_x[C::CAP];
-  __shared__ uint32_t s_wcnt[WAVES][MS_BINS];
-  __shared__ uint32_t s_tex[MS_BINS];
-  __shared__ uint32_t s_wsum[MS_BINS / kWave];
+  __shared__ uint32_t s_wcnt[WAVES][LSD_BINS];
+  __shared__ uint32_t s_tex[LSD_BINS];
+  __shared__ uint32_t s_wsum[LSD_BINS / kWave];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const MsSeg sg = segs[fb[1 + blockIdx.x]];
   const uint32_t c = (uint32_t)sg.count;
-  const int ndig = (int)sg.aux;
+  const int nbits = (int)sg.aux;  // passes over bits [0, nbits) of (key - base)
   const uint32_t K = (c + THREADS - 1) / THREADS;
   const uint32_t pw = (uint32_t)wave * kWave * K + lane;
   const uint64_t *src = ms_src(bf, sg.buf) + sg.start;
@@ -676,23 +756,22 @@ __global__ __launch_bounds__(THREADS) void ms_lsd_kernel(MsBufs bf, const MsSeg 
   uint32_t lo[MAXK], hi[MAXK], pos[MAXK];
 #pragma unroll
   for (int i = 0; i < MAXK; ++i) {
-    if ((uint32_t)i < K) {
-      const uint32_t p = pw + (uint32_t)i * kWave;
-      const uint64_t k = p < c ? (src[p] ^ f) : ~0ull;
-      lo[i] = (uint32_t)k;
-      hi[i] = (uint32_t)(k >> 32);
-    }
+    const uint32_t p = pw + (uint32_t)i * kWave;
+    const uint64_t v = src[min(p, c - 1)] ^ f;  // unconditional: the loads overlap
+    const uint64_t k = ((uint32_t)i < K && p < c) ? v : ~0ull;
+    lo[i] = (uint32_t)k;
+    hi[i] = (uint32_t)(k >> 32);
   }
-  for (int pass = 0; pass < ndig; ++pass) {
-    const int shift = sh.s[pass];
-    const bool low = shift < 32;
-    const int sft = low ? shift : shift - 32;
-    for (int i = tid; i < WAVES * MS_BINS; i += THREADS) (&s_wcnt[0][0])[i] = 0;
+  auto digit = [&](int i, int shift) -> uint32_t {
+    return (uint32_t)(((((uint64_t)hi[i] << 32) | lo[i]) - base) >> shift) & 255u;
+  };
+  for (int shift = 0; shift < nbits; shift += 8) {
+    for (int i = tid; i < WAVES * LSD_BINS; i += THREADS) (&s_wcnt[0][0])[i] = 0;
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < MAXK; ++i) {
       if ((uint32_t)i < K) {
-        const uint32_t d = ((low ? lo[i] : hi[i]) >> sft) & 255u;
+        const uint32_t d = digit(i, shift);
         uint64_t peers = ~0ull;
 #pragma unroll
         for (int b = 0; b < 8; ++b) {
@@ -707,7 +786,7 @@ __global__ __launch_bounds__(THREADS) void ms_lsd_kernel(MsBufs bf, const MsSeg 
     }
     __syncthreads();
     uint32_t tot = 0, incl = 0;
-    if (tid < MS_BINS) {
+    if (tid < LSD_BINS) {
 #pragma unroll
       for (int w = 0; w < WAVES; ++w) {
         const uint32_t x = s_wcnt[w][tid];
@@ -723,17 +802,17 @@ __global__ __launch_bounds__(THREADS) void ms_lsd_kernel(MsBufs bf, const MsSeg 
       if (lane == 63) s_wsum[wave] = incl;
     }
     __syncthreads();
-    if (tid < MS_BINS) {
+    if (tid < LSD_BINS) {
       uint32_t add = 0;
 #pragma unroll
-      for (int w = 0; w < MS_BINS / kWave; ++w) add += (w < wave) ? s_wsum[w] : 0u;
+      for (int w = 0; w < LSD_BINS / kWave; ++w) add += (w < wave) ? s_wsum[w] : 0u;
       s_tex[tid] = incl - tot + add;
     }
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < MAXK; ++i) {
       if ((uint32_t)i < K) {
-        const uint32_t d = ((low ? lo[i] : hi[i]) >> sft) & 255u;
+        const uint32_t d = digit(i, shift);
         pos[i] += s_tex[d] + s_wcnt[wave][d];
         s_x[pos[i]] = lo[i];
       }
@@ -821,14 +900,24 @@ uint64_t tile_table(std::vector<MsSeg> &segs, uint32_t tile, std::vector<uint32_
 
 }  // namespace
 
+// Local sorts are persistent (the S and M classes prefetch the next segment's keys): as
+// many workgroups as fit on the device, each walking the list with stride gridDim.x.
 template <int T, int K>
-static void launch_class(hipStream_t st, const MsBufs &bf, const MsSeg *d, unsigned n, const MsShifts &sh,
-                         uint64_t flip, uint32_t *fb) {
-  hipLaunchKernelGGL((ms_local_kernel<T, K>), dim3(n), dim3(T), 0, st, bf, d, sh, flip, fb);
-  hipLaunchKernelGGL((ms_lsd_kernel<T, K>), dim3(n), dim3(T), 0, st, bf, d, sh, flip, (const uint32_t *)fb);
+static void launch_class(nut_ctx *c, const MsBufs &bf, const MsSeg *d, unsigned n, uint64_t base, uint64_t flip,
+                         uint32_t *fb) {
+  constexpr bool PF = K <= 12;  // the L class has no registers to spare for a second key set
+  static int per_cu = 0;        // resident workgroups per CU (occupancy query, once)
+  if (per_cu == 0) {
+    int b = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, ms_local_kernel<T, K, PF>, T, 0) != hipSuccess || b < 1) b = 1;
+    per_cu = b;
+  }
+  const unsigned grid = PF ? (unsigned)std::min<uint64_t>(n, (uint64_t)c->num_cus * per_cu) : n;
+  hipLaunchKernelGGL((ms_local_kernel<T, K, PF>), dim3(grid), dim3(T), 0, c->stream, bf, d, n, base, flip, fb);
+  hipLaunchKernelGGL((ms_lsd_kernel<T, K>), dim3(n), dim3(T), 0, c->stream, bf, d, base, flip, (const uint32_t *)fb);
 }
 
-static nut_status launch_local(nut_ctx *c, MetaArena &ar, const MsBufs &bf, const MsShifts &sh, uint64_t flip,
+static nut_status launch_local(nut_ctx *c, MetaArena &ar, const MsBufs &bf, uint64_t base, uint64_t flip,
                                const std::vector<MsSeg> &segs, int cls) {
   if (segs.empty()) return NUT_OK;
   MsSeg *d;
@@ -838,12 +927,98 @@ static nut_status launch_local(nut_ctx *c, MetaArena &ar, const MsBufs &bf, cons
   NUT_HIP(hipMemsetAsync(fb, 0, 4, c->stream));
   const unsigned n = (unsigned)segs.size();
   if (cls == 0)
-    launch_class<LS_S_THREADS, LS_S_ITEMS>(c->stream, bf, d, n, sh, flip, fb);
+    launch_class<LS_S_THREADS, LS_S_ITEMS>(c, bf, d, n, base, flip, fb);
   else if (cls == 1)
-    launch_class<LS_M_THREADS, LS_M_ITEMS>(c->stream, bf, d, n, sh, flip, fb);
+    launch_class<LS_M_THREADS, LS_M_ITEMS>(c, bf, d, n, base, flip, fb);
   else
-    launch_class<LS_L_THREADS, LS_L_ITEMS>(c->stream, bf, d, n, sh, flip, fb);
+    launch_class<LS_L_THREADS, LS_L_ITEMS>(c, bf, d, n, base, flip, fb);
   NUT_HIP(hipGetLastError());
+  return NUT_OK;
+}
+
+static int local_class(uint64_t count) { return count <= LS_S_CAP ? 0 : (count <= LS_M_CAP ? 1 : 2); }
+
+// local sorts of n segments listed in device memory (a device-planned level's class list)
+static nut_status launch_local_dev(nut_ctx *c, const MsBufs &bf, uint64_t base, uint64_t flip, const MsSeg *d,
+                                   unsigned n, uint32_t *fb, int cls) {
+  if (n == 0) return NUT_OK;
+  NUT_HIP(hipMemsetAsync(fb, 0, 4, c->stream));
+  if (cls == 0)
+    launch_class<LS_S_THREADS, LS_S_ITEMS>(c, bf, d, n, base, flip, fb);
+  else if (cls == 1)
+    launch_class<LS_M_THREADS, LS_M_ITEMS>(c, bf, d, n, base, flip, fb);
+  else
+    launch_class<LS_L_THREADS, LS_L_ITEMS>(c, bf, d, n, base, flip, fb);
+  NUT_HIP(hipGetLastError());
+  return NUT_OK;
+}
+
+// One device-planned level over `big` (segments whose sizes the host knows): histogram,
+// plan (cursors + class lists on the device), scatter, local sorts of the listed classes.
+// Only the four class counts come back to the host (read while the scatter runs); the
+// sub-segments too large for a local sort are returned in `over` for another level.
+static nut_status device_level(nut_ctx *c, MetaArena &ar, const MsBufs &bf, const MsDigit &dg, uint64_t flip,
+                               std::vector<MsSeg> &big, std::vector<MsSeg> &over) {
+  hipStream_t st = c->stream;
+  over.clear();
+  std::vector<uint32_t> tiles;
+  const uint64_t nht = tile_table(big, MH_TILE, tiles);
+  std::vector<uint32_t> stiles;
+  std::vector<MsSeg> sbig = big;
+  const uint64_t nst = tile_table(sbig, MS_TILE, stiles);
+  if (nht > 0x7FFFFFFFull || nst > 0x7FFFFFFFull) return fail(NUT_ERR_UNSUPPORTED, "nut_sort_i64: too many tiles");
+  const uint64_t ns = big.size(), cap = ns * MS_BINS;
+  const size_t hbytes = ns * MS_BINS * 8;
+  nut_status s = ar.begin(2 * MetaArena::align(ns * sizeof(MsSeg)) + MetaArena::align(tiles.size() * 4) +
+                          MetaArena::align(stiles.size() * 4) + 2 * MetaArena::align(hbytes) +
+                          MetaArena::align(4 * cap * sizeof(MsSeg)) + 3 * MetaArena::align((cap + 1) * 4) + 1024);
+  if (s) return s;
+  MsSeg *dseg, *dsseg;
+  uint32_t *dtile, *dstile;
+  if ((s = ar.upload(big, &dseg)) || (s = ar.upload(tiles, &dtile)) || (s = ar.upload(sbig, &dsseg)) ||
+      (s = ar.upload(stiles, &dstile)))
+    return s;
+  unsigned long long *dhist = (unsigned long long *)ar.alloc(hbytes);
+  unsigned long long *dcur = (unsigned long long *)ar.alloc(hbytes);
+  MsSeg *lists = (MsSeg *)ar.alloc(4 * cap * sizeof(MsSeg));
+  unsigned int *counts = (unsigned int *)ar.alloc(16);
+  uint32_t *fb[3];
+  for (auto &f : fb) f = (uint32_t *)ar.alloc((cap + 1) * 4);
+  NUT_HIP(hipMemsetAsync(dhist, 0, hbytes, st));
+  NUT_HIP(hipMemsetAsync(counts, 0, 16, st));
+  uint64_t total = 0;
+  for (const MsSeg &sg : big) total += sg.count;
+  hipLaunchKernelGGL(ms_hist_kernel, dim3((unsigned)nht), dim3(MH_THREADS), 0, st, bf, (const MsSeg *)dseg,
+                     (const uint32_t *)dtile, dg, flip, dhist, (unsigned long long *)nullptr);
+  hipLaunchKernelGGL(ms_plan_kernel, dim3((unsigned)ns), dim3(MS_BINS), 0, st, (const MsSeg *)dseg,
+                     (const unsigned long long *)dhist, dg.shift, dcur, lists, cap, counts);
+  NUT_HIP(hipGetLastError());
+  hipEvent_t ev = nullptr;
+  NUT_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  uint32_t *hc = (uint32_t *)c->host_pinned;
+  hipError_t e = hipMemcpyAsync(hc, counts, 16, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipEventRecord(ev, st);
+  if (e == hipSuccess)
+    hipLaunchKernelGGL(ms_scatter_kernel, dim3((unsigned)std::min<uint64_t>(nst, (uint64_t)c->num_cus)),
+                       dim3(MS_THREADS), 0, st, bf, (const MsSeg *)dsseg, (const uint32_t *)dstile, (uint32_t)nst, dg,
+                       flip, dcur);
+  if (e == hipSuccess) e = hipGetLastError();
+  if (e == hipSuccess) e = hipEventSynchronize(ev);  // the counts, while the scatter runs
+  (void)hipEventDestroy(ev);
+  if (e != hipSuccess) return hip_fail(e, "nut_sort_i64 (device-planned level)");
+  const uint32_t cnt[4] = {hc[0], hc[1], hc[2], hc[3]};
+  c->sort_bytes += 8 * total + 16 * total;
+  ++c->sort_levels;
+  for (int cls = 2; cls >= 0; --cls)
+    if ((s = launch_local_dev(c, bf, dg.base, flip, lists + (uint64_t)cls * cap, cnt[cls], fb[cls], cls))) return s;
+  if (cnt[3]) {  // sub-segments too large for a local sort: to the host, for another level
+    over.resize(cnt[3]);
+    NUT_HIP(hipMemcpyAsync(over.data(), lists + 3 * cap, cnt[3] * sizeof(MsSeg), hipMemcpyDeviceToHost, st));
+    NUT_HIP(hipStreamSynchronize(st));
+  }
+  uint64_t over_keys = 0;
+  for (const MsSeg &sg : over) over_keys += sg.count;
+  c->sort_bytes += 16 * (total - over_keys);
   return NUT_OK;
 }
 
@@ -857,28 +1032,28 @@ nut_status msd_sort_i64(nut_ctx *c, const int64_t *in, int64_t *out, uint64_t n,
   c->sort_levels = 0;
   c->timer.begin(st, NUT_KERNEL_SORT);
 
-  if (n <= LS_CAP) {  // one workgroup, all eight digits
-    MsShifts all;
-    for (int p = 0; p < 8; ++p) all.s[p] = 8 * p;
-    std::vector<MsSeg> one{{0, n, 0, 8}};
+  if (n <= LS_CAP) {  // one workgroup, all 64 bits
+    std::vector<MsSeg> one{{0, n, 0, 64}};
     s = ar.begin(1024);
     if (s) return s;
-    s = launch_local(c, ar, bf, all, flip, one, n <= LS_S_CAP ? 0 : (n <= LS_M_CAP ? 1 : 2));
+    s = launch_local(c, ar, bf, 0, flip, one, local_class(n));
     if (s) return s;
     c->sort_bytes = 16 * n;
     c->timer.end(st);
     return NUT_OK;
   }
 
+  // Levels of MS_BITS-bit digits of (key - base), most significant first.  The first
+  // histogram speculates base 0 and the top 9 key bits while it reduces the keys' min and
+  // max; if the top bits barely vary (a narrow key range, e.g. a sample-sort rank's), the
+  // histogram is redone with base = min and the digit below the top bit of max - min.
   std::vector<MsSeg> big{{0, n, 0, 0}}, scat, next, small[3], done;
   std::vector<uint32_t> tiles;
   std::vector<uint64_t> hist, cursor;
-  std::vector<int> vary;  // varying digits, most significant first
-  MsShifts asc{};         // varying digit shifts, least significant first
-  int digit = 7;          // first histogram: digit 7, speculatively, with the OR/AND reduction
+  MsDigit dg{0, 64 - MS_BITS, (uint32_t)MS_BINS - 1};
   bool first = true;
   while (!big.empty()) {
-    // ---- histograms of `digit` over the big segments
+    // ---- histograms of the level's digit over the big segments
     const uint64_t nht = tile_table(big, MH_TILE, tiles);
     if (nht > 0x7FFFFFFFull) return fail(NUT_ERR_UNSUPPORTED, "nut_sort_i64: too many tiles");
     const size_t hbytes = big.size() * MS_BINS * 8;
@@ -889,52 +1064,48 @@ nut_status msd_sort_i64(nut_ctx *c, const int64_t *in, int64_t *out, uint64_t n,
     uint32_t *dtile;
     if ((s = ar.upload(big, &dseg)) || (s = ar.upload(tiles, &dtile))) return s;
     unsigned long long *dhist = (unsigned long long *)ar.alloc(hbytes);
-    unsigned long long *dor = (unsigned long long *)ar.alloc(16);
+    unsigned long long *dmm = (unsigned long long *)ar.alloc(16);
     NUT_HIP(hipMemsetAsync(dhist, 0, hbytes, st));
     if (first) {
-      const unsigned long long init[2] = {0ull, ~0ull};
+      const unsigned long long init[2] = {~0ull, 0ull};
       ar.keep.emplace_back((const char *)init, (const char *)init + 16);
-      NUT_HIP(hipMemcpyAsync(dor, ar.keep.back().data(), 16, hipMemcpyHostToDevice, st));
+      NUT_HIP(hipMemcpyAsync(dmm, ar.keep.back().data(), 16, hipMemcpyHostToDevice, st));
     }
     for (const MsSeg &sg : big) c->sort_bytes += 8 * sg.count;
     hipLaunchKernelGGL(ms_hist_kernel, dim3((unsigned)nht), dim3(MH_THREADS), 0, st, bf, (const MsSeg *)dseg,
-                       (const uint32_t *)dtile, 8 * digit, flip, dhist, first ? dor : nullptr);
+                       (const uint32_t *)dtile, dg, flip, dhist, first ? dmm : nullptr);
     NUT_HIP(hipGetLastError());
     hist.resize(big.size() * MS_BINS);
     NUT_HIP(hipMemcpyAsync(hist.data(), dhist, hbytes, hipMemcpyDeviceToHost, st));
-    unsigned long long horand[2] = {0, 0};
-    if (first) NUT_HIP(hipMemcpyAsync(horand, dor, 16, hipMemcpyDeviceToHost, st));
+    unsigned long long hmm[2] = {0, 0};
+    if (first) NUT_HIP(hipMemcpyAsync(hmm, dmm, 16, hipMemcpyDeviceToHost, st));
     NUT_HIP(hipStreamSynchronize(st));
     if (first) {
       first = false;
-      const uint64_t diff = horand[0] ^ horand[1];
-      for (int p = 7; p >= 0; --p)
-        if ((diff >> (8 * p)) & 255) vary.push_back(p);
-      for (size_t i = 0; i < vary.size(); ++i) asc.s[i] = 8 * vary[vary.size() - 1 - i];
-      if (vary.empty()) {  // all keys equal
-        MsSeg all{0, n, 0, 0};
-        done.push_back(all);
+      const uint64_t mn = hmm[0], mx = hmm[1];
+      if (mn == mx) {  // all keys equal
+        done.push_back(MsSeg{0, n, 0, 0});
         big.clear();
         break;
       }
-      if (vary[0] != 7) {  // digit 7 constant: histogram the top varying digit instead
-        digit = vary[0];
+      if ((mx >> (64 - MS_BITS)) - (mn >> (64 - MS_BITS)) < (uint64_t)MS_BINS / 4) {
+        const int hb = 64 - __builtin_clzll(mx - mn);  // (key - mn) < 2^hb
+        const int w = std::min(MS_BITS, hb);
+        dg = MsDigit{mn, hb - w, (1u << w) - 1u};
         continue;
       }
     }
-    // varying digits below this level
-    const int below = (int)(std::find(vary.begin(), vary.end(), digit) - vary.begin());
-    const uint32_t left = (uint32_t)(vary.size() - 1 - below);
+    const int hi = dg.shift;  // sub-segments of this level agree on bits >= shift
     // ---- classify: segments whose digit takes one value pass through unmoved
     scat.clear();
     next.clear();
     std::vector<uint64_t> scat_hist;
     auto classify = [&](MsSeg sg) {
-      if (left == 0) {
+      if (hi == 0) {
         done.push_back(sg);
       } else if (sg.count <= LS_CAP) {
-        sg.aux = left;
-        small[sg.count <= LS_S_CAP ? 0 : (sg.count <= LS_M_CAP ? 1 : 2)].push_back(sg);
+        sg.aux = (uint32_t)hi;
+        small[local_class(sg.count)].push_back(sg);
       } else {
         next.push_back(sg);
       }
@@ -974,13 +1145,25 @@ nut_status msd_sort_i64(nut_ctx *c, const int64_t *in, int64_t *out, uint64_t n,
       if ((s = ar.upload(scat, &dsc)) || (s = ar.upload(tiles, &dt)) || (s = ar.upload(cursor, &dcur))) return s;
       for (const MsSeg &sg : scat) c->sort_bytes += 16 * sg.count;
       ++c->sort_levels;
-      const unsigned sgrid = (unsigned)std::min<uint64_t>(nst, (uint64_t)c->num_cus * 2);  // persistent, 2 per CU
+      const unsigned sgrid = (unsigned)std::min<uint64_t>(nst, (uint64_t)c->num_cus);  // persistent, 1 per CU (128 KB LDS)
       hipLaunchKernelGGL(ms_scatter_kernel, dim3(sgrid), dim3(MS_THREADS), 0, st, bf, (const MsSeg *)dsc,
-                         (const uint32_t *)dt, (uint32_t)nst, 8 * digit, flip, (unsigned long long *)dcur);
+                         (const uint32_t *)dt, (uint32_t)nst, dg, flip, (unsigned long long *)dcur);
       NUT_HIP(hipGetLastError());
     }
     big.swap(next);
-    if (below + 1 < (int)vary.size()) digit = vary[below + 1];
+    const int w = std::min(MS_BITS, hi);  // the next level's digit: the bits just below
+    dg = MsDigit{dg.base, hi - w, (1u << w) - 1u};
+    break;  // further levels are planned on the device
+  }
+  // ---- further levels: device-planned (histogram, cursors and class lists on the GPU)
+  for (std::vector<MsSeg> over; !big.empty(); big.swap(over)) {
+    if (dg.mask == 0) {  // the previous level consumed the last bit: each segment is one key value
+      done.insert(done.end(), big.begin(), big.end());
+      break;
+    }
+    if ((s = device_level(c, ar, bf, dg, flip, big, over))) return s;
+    const int hi = dg.shift, w = std::min(MS_BITS, hi);
+    dg = MsDigit{dg.base, hi - w, (1u << w) - 1u};
   }
   // ---- finish: local sorts and equal-key runs
   size_t total = 256;
@@ -992,7 +1175,7 @@ nut_status msd_sort_i64(nut_ctx *c, const int64_t *in, int64_t *out, uint64_t n,
   if (s) return s;
   for (int cls = 2; cls >= 0; --cls) {
     for (const MsSeg &sg : small[cls]) c->sort_bytes += 16 * sg.count;
-    if ((s = launch_local(c, ar, bf, asc, flip, small[cls], cls))) return s;
+    if ((s = launch_local(c, ar, bf, dg.base, flip, small[cls], cls))) return s;
   }
   for (const MsSeg &sg : done) c->sort_bytes += 16 * sg.count;
   if (!done.empty()) {

@@ -139,6 +139,62 @@ static float time_it(hipEvent_t a, hipEvent_t b) {
   return ms;
 }
 
+template <int T, int K, bool PF>
+static void local_sweep(nut::MsBufs bf, uint64_t *a, uint64_t *b, uint64_t n, uint32_t seglen, hipEvent_t e0,
+                        hipEvent_t e1, unsigned long long *bad) {
+  const uint64_t nseg = n / seglen;
+  std::vector<nut::MsSeg> segs(nseg);
+  std::vector<uint32_t> fb(nseg + 1);
+  fb[0] = (uint32_t)nseg;
+  for (uint64_t i = 0; i < nseg; ++i) {
+    segs[i] = nut::MsSeg{i * seglen, seglen, 2, 48};  // keys share their top 16 bits
+    fb[1 + i] = (uint32_t)i;
+  }
+  nut::MsSeg *dseg;
+  uint32_t *dfb, *dfb0;
+  CK(hipMalloc(&dseg, nseg * sizeof(nut::MsSeg)));
+  CK(hipMalloc(&dfb, (nseg + 1) * 4));
+  CK(hipMalloc(&dfb0, (nseg + 1) * 4));
+  CK(hipMemcpy(dseg, segs.data(), nseg * sizeof(nut::MsSeg), hipMemcpyHostToDevice));
+  CK(hipMemcpy(dfb, fb.data(), (nseg + 1) * 4, hipMemcpyHostToDevice));
+  int per_cu = 1, ncu = 256;
+  CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nut::ms_local_kernel<T, K, PF>, T, 0));
+  CK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
+  const unsigned grid = PF ? (unsigned)std::min<uint64_t>(nseg, (uint64_t)ncu * per_cu) : (unsigned)nseg;
+  printf("local<%d,%d,%d>: %d workgroups per CU, grid %u\n", T, K, (int)PF, per_cu, grid);
+  const int stops[] = {0, 1, 3, 4, 5, 0};
+  for (int variant = 0; variant < 6; ++variant) {
+    const int stop = stops[variant];
+    CK(hipMemcpyToSymbol(HIP_SYMBOL(nut::g_ms_stop), &stop, sizeof(int)));
+    float best = 1e9;
+    for (int r = 0; r < 3; ++r) {
+      hipLaunchKernelGGL(gen48, dim3(4096), dim3(256), 0, 0, b, n);
+      CK(hipMemset(dfb0, 0, 4));
+      CK(hipEventRecord(e0));
+      if (variant < 5)
+        hipLaunchKernelGGL((nut::ms_local_kernel<T, K, PF>), dim3(grid), dim3(T), 0, 0, bf,
+                           (const nut::MsSeg *)dseg, (uint32_t)nseg, 0ull, 0ull, dfb0);
+      else
+        hipLaunchKernelGGL((nut::ms_lsd_kernel<T, K>), dim3((unsigned)nseg), dim3(T), 0, 0, bf,
+                           (const nut::MsSeg *)dseg, 0ull, 0ull, (const uint32_t *)dfb);
+      CK(hipEventRecord(e1));
+      best = std::min(best, time_it(e0, e1));
+    }
+    uint32_t nfb = 0;
+    CK(hipMemcpy(&nfb, dfb0, 4, hipMemcpyDeviceToHost));
+    CK(hipMemset(bad, 0, 8));
+    hipLaunchKernelGGL(check_sorted<0>, dim3(4096), dim3(256), 0, 0, a, nseg * seglen, seglen, 64, bad);
+    unsigned long long hb;
+    CK(hipMemcpy(&hb, bad, 8, hipMemcpyDeviceToHost));
+    printf("local<%d,%d> %s stop=%d seglen=%u: %.3f ms  (%.0f GB/s) unsorted pairs %llu fallbacks %u\n", T, K,
+           variant < 5 ? "msd+net" : "lsd-ballot", stop, seglen, best, 16.0 * nseg * seglen / best / 1e6, hb,
+           variant < 5 ? nfb : 0u);
+  }
+  CK(hipFree(dseg));
+  CK(hipFree(dfb));
+  CK(hipFree(dfb0));
+}
+
 int main(int argc, char **argv) {
   const uint64_t n = argc > 1 ? strtoull(argv[1], 0, 10) : 1250000000ull;
   uint64_t *a, *b;
@@ -180,54 +236,9 @@ int main(int argc, char **argv) {
   RUN_SCATTER(1024, 16, 0);
   RUN_SCATTER(512, 8, 0);
 
-  const uint32_t seglen = argc > 2 ? (uint32_t)atoi(argv[2]) : 19073;
-  const uint64_t nseg = n / seglen;
-  {
-    std::vector<nut::MsSeg> segs(nseg);
-    std::vector<uint32_t> fb(nseg + 1);
-    fb[0] = (uint32_t)nseg;
-    for (uint64_t i = 0; i < nseg; ++i) {
-      segs[i] = nut::MsSeg{i * seglen, seglen, 2, 6};
-      fb[1 + i] = (uint32_t)i;
-    }
-    nut::MsSeg *dseg;
-    uint32_t *dfb, *dfb0;
-    CK(hipMalloc(&dseg, nseg * sizeof(nut::MsSeg)));
-    CK(hipMalloc(&dfb, (nseg + 1) * 4));
-    CK(hipMalloc(&dfb0, (nseg + 1) * 4));
-    CK(hipMemcpy(dseg, segs.data(), nseg * sizeof(nut::MsSeg), hipMemcpyHostToDevice));
-    CK(hipMemcpy(dfb, fb.data(), (nseg + 1) * 4, hipMemcpyHostToDevice));
-    nut::MsShifts sh{{0, 8, 16, 24, 32, 40, 48, 56}};
-    // bufs: in unused, a = out, b = tmp (segment source)
-    nut::MsBufs bf{nullptr, a, b};
-    const int stops[] = {0, 1, 3, 4, 5, 0};
-    for (int variant = 0; variant < 6; ++variant) {
-      const int stop = stops[variant];
-      CK(hipMemcpyToSymbol(HIP_SYMBOL(nut::g_ms_stop), &stop, sizeof(int)));
-      float best = 1e9;
-      for (int r = 0; r < 3; ++r) {
-        hipLaunchKernelGGL(gen48, dim3(4096), dim3(256), 0, 0, b, n);
-        CK(hipMemset(dfb0, 0, 4));
-        CK(hipEventRecord(e0));
-        if (variant < 5)
-          hipLaunchKernelGGL((nut::ms_local_kernel<1024, 24>), dim3((unsigned)nseg), dim3(1024), 0, 0, bf,
-                             (const nut::MsSeg *)dseg, sh, 0ull, dfb0);
-        else
-          hipLaunchKernelGGL((nut::ms_lsd_kernel<1024, 24>), dim3((unsigned)nseg), dim3(1024), 0, 0, bf,
-                             (const nut::MsSeg *)dseg, sh, 0ull, (const uint32_t *)dfb);
-        CK(hipEventRecord(e1));
-        best = std::min(best, time_it(e0, e1));
-      }
-      uint32_t nfb = 0;
-      CK(hipMemcpy(&nfb, dfb0, 4, hipMemcpyDeviceToHost));
-      CK(hipMemset(bad, 0, 8));
-      hipLaunchKernelGGL(check_sorted<0>, dim3(4096), dim3(256), 0, 0, a, nseg * seglen, seglen, 64, bad);
-      unsigned long long hb;
-      CK(hipMemcpy(&hb, bad, 8, hipMemcpyDeviceToHost));
-      printf("local %s stop=%d seglen=%u: %.3f ms  (%.0f GB/s) unsorted pairs %llu fallbacks %u\n",
-             variant < 5 ? "msd+net" : "lsd-ballot", stop, seglen, best, 16.0 * nseg * seglen / best / 1e6, hb,
-             variant < 5 ? nfb : 0u);
-    }
-  }
+  nut::MsBufs bf{nullptr, a, b};  // in unused, a = out, b = tmp (segment source)
+  const uint32_t seglen = argc > 2 ? (uint32_t)atoi(argv[2]) : 4768;
+  if (seglen <= 6144) local_sweep<512, 12, true>(bf, a, b, n, seglen, e0, e1, bad);
+  else local_sweep<1024, 24, false>(bf, a, b, n, seglen, e0, e1, bad);
   return 0;
 }

@@ -467,3 +467,29 @@ def test_sort_stats(ex):
     ex.sort_i64(keys)
     nbytes, levels = ex.sort_stats()
     assert levels == 2 and nbytes == 64 * n
+
+
+@pytest.mark.parametrize("kind", ["cluster", "narrow_range", "rank_range", "two_clusters_dups"])
+def test_sort_deep_levels(ex, orc, kind):
+    """MSD levels beyond the second: sub-segments too large for a local
+    sort after a device-planned level go back to the host for another level; a narrow key
+    range rebases the digits on the minimum (a sample-sort rank's range)."""
+    rng = np.random.default_rng(21)
+    n = 60_000_000
+    if kind == "cluster":          # half the keys inside a 2^40-wide range: 4 levels there
+        v = np.concatenate([rng.integers(I64_MIN, I64_MAX, n // 2, dtype=np.int64),
+                            (1 << 50) + rng.integers(0, 1 << 40, n - n // 2, dtype=np.int64)])
+    elif kind == "narrow_range":   # every key in [x, x + 2^35): rebased digits
+        v = (-(1 << 61)) + rng.integers(0, 1 << 35, n, dtype=np.int64)
+    elif kind == "rank_range":     # 1/8 of the key space, not aligned to a digit boundary
+        lo = I64_MIN // 8 * 3 + 12345
+        v = lo + rng.integers(0, 1 << 61, n, dtype=np.int64)
+    else:                          # two tight clusters with many duplicates
+        v = np.concatenate([rng.integers(0, 1000, n // 2, dtype=np.int64) * (1 << 20),
+                            rng.integers(-(1 << 24), -(1 << 24) + 50_000, n - n // 2, dtype=np.int64)])
+    rng.shuffle(v)
+    o = host(ex.sort_i64(dev(v, ex)))
+    assert np.all(o[1:] >= o[:-1])
+    assert orc.multiset_hash(o) == orc.multiset_hash(v)
+    if kind != "cluster":
+        assert np.array_equal(o, np.sort(v))
