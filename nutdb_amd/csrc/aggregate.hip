@@ -149,8 +149,16 @@ nut_status alloc_table(nut_groups *g, uint64_t cap) {
   if (!(g->mem && g->mem_bytes >= off)) {
     if (g->mem) (void)hipFree(g->mem);
     g->mem = nullptr;
-    NUT_HIP(hipMalloc(&g->mem, off));
-    g->mem_bytes = off;
+    nut_ctx *c = g->ctx;
+    if (c->tbl_pool && c->tbl_pool_bytes >= off) {  // a freed table's allocation, reused
+      g->mem = c->tbl_pool;
+      g->mem_bytes = c->tbl_pool_bytes;
+      c->tbl_pool = nullptr;
+      c->tbl_pool_bytes = 0;
+    } else {
+      NUT_HIP(hipMalloc(&g->mem, off));
+      g->mem_bytes = off;
+    }
   }
   char *b = (char *)g->mem;
   GTable &t = g->gt;
@@ -522,7 +530,10 @@ nut_status gp_level(nut_ctx *c, GpMeta &mm, std::vector<GpSeg> &segs, int shift,
       }
     }
   }
-  const uint32_t nst = gp_tiles(segs, GP_TILE, ts);
+  // 1024-thread workgroups of 16K-record tiles (one per CU): 64 records per digit per tile;
+  // measured 9.2 vs 10.1 ms for the 512-thread 8K tiles (G = 1e5, 1e9 rows); NUT_GP_T=512
+  const int big = env_int("NUT_GP_T", 1024) == 1024;
+  const uint32_t nst = gp_tiles(segs, big ? 2 * GP_TILE : GP_TILE, ts);
   s = mm.begin(GpMeta::al(segs.size() * sizeof(GpSeg)) + GpMeta::al(ts.size() * 4 + 1) + GpMeta::al(cur.size() * 8));
   if (s) return s;
   uint64_t *dcur;
@@ -533,10 +544,148 @@ nut_status gp_level(nut_ctx *c, GpMeta &mm, std::vector<GpSeg> &segs, int shift,
     ar.dst[a] = dst[a];
   }
   ar.narr = narr;
-  if (nst) hipLaunchKernelGGL(gp_scatter_kernel, dim3(nst), dim3(GP_THREADS), 0, st, ar, (const GpSeg *)dseg,
-                              (const uint32_t *)dts, shift, gather ? 1 : 0, (unsigned long long *)dcur, kx);
+  if (nst && big) {
+    const unsigned grid = std::min<unsigned>(nst, (unsigned)c->num_cus);
+    if (src[2])
+      hipLaunchKernelGGL((gp_scatter_kernel<2, 1024>), dim3(grid), dim3(1024), 0, st, ar, (const GpSeg *)dseg,
+                         (const uint32_t *)dts, nst, shift, gather ? 1 : 0, (unsigned long long *)dcur, kx);
+    else
+      hipLaunchKernelGGL((gp_scatter_kernel<1, 1024>), dim3(grid), dim3(1024), 0, st, ar, (const GpSeg *)dseg,
+                         (const uint32_t *)dts, nst, shift, gather ? 1 : 0, (unsigned long long *)dcur, kx);
+  } else if (nst) {  // persistent: two 512-thread workgroups per CU walk the tiles
+    const unsigned grid = std::min<unsigned>(nst, (unsigned)c->num_cus * 2);
+    if (src[2])
+      hipLaunchKernelGGL((gp_scatter_kernel<2, GP_THREADS>), dim3(grid), dim3(GP_THREADS), 0, st, ar,
+                         (const GpSeg *)dseg, (const uint32_t *)dts, nst, shift, gather ? 1 : 0,
+                         (unsigned long long *)dcur, kx);
+    else
+      hipLaunchKernelGGL((gp_scatter_kernel<1, GP_THREADS>), dim3(grid), dim3(GP_THREADS), 0, st, ar,
+                         (const GpSeg *)dseg, (const uint32_t *)dts, nst, shift, gather ? 1 : 0,
+                         (unsigned long long *)dcur, kx);
+  }
   NUT_HIP(hipGetLastError());
   return NUT_OK;
+}
+
+// per-partition aggregation of partitioned records (final level's `parts`) into g's table
+nut_status gp_aggregate(nut_groups *g, GpMeta &mm, const std::vector<uint64_t> &parts, const nut_agg_spec &s2,
+                        const int32_t *kinds2, uint64_t group_hint) {
+  nut_ctx *c = g->ctx;
+  hipStream_t st = c->stream;
+  const uint32_t nparts = (uint32_t)(parts.size() / 2);
+  if (nparts == 0) return NUT_OK;
+  // split partitions into chunks (even boundaries) so that the grid fills the chip (chunks
+  // of one partition merge the same keys: a handful of extra merges per group)
+  const uint64_t k = std::max<uint64_t>(1, ((uint64_t)c->num_cus * 4 + nparts - 1) / nparts);
+  std::vector<uint64_t> off;
+  for (uint32_t p = 0; p < nparts; ++p) {
+    const uint64_t a0 = parts[2 * p], a1 = parts[2 * p + 1];
+    uint64_t prev = a0;
+    for (uint64_t j = 1; j <= k; ++j) {
+      const uint64_t cut = j == k ? a1 : std::max<uint64_t>(prev, (a0 + (a1 - a0) * j / k) & ~1ull);
+      if (cut > prev) {
+        off.push_back(prev);
+        off.push_back(cut);
+        prev = cut;
+      }
+    }
+  }
+  nut_status e = mm.begin(GpMeta::al(off.size() * 8));
+  if (e) return e;
+  uint64_t *doff;
+  if ((e = mm.up(off, &doff))) return e;
+  LaunchExtra sg;
+  sg.seg_off = doff;
+  sg.nseg = (uint32_t)(off.size() / 2);
+  const uint64_t per = std::max<uint64_t>(64, 2 * ((group_hint + nparts - 1) / nparts));
+  uint32_t ctl[4];
+  for (int attempt = 0;; ++attempt) {
+    e = launch_agg(g, &s2, per, kinds2, &sg);
+    if (!e) e = read_ctl(g, ctl);
+    if (e) return e;
+    if (!(ctl[1] & 1u)) break;
+    // more groups than the table admits: a larger table, then the same partitions again
+    if (g->gt.cap >= (1ull << 34) || attempt > 12) return fail(NUT_ERR_OOM, "nut_groupby: group table too large");
+    e = alloc_table(g, g->gt.cap * 4);
+    if (e) return e;
+  }
+  NUT_HIP(hipStreamSynchronize(st));  // the host tables in mm.keep outlive their copies
+  return NUT_OK;
+}
+
+// Spill-free partitioned aggregation (no WHERE, plain-column arguments): the key and value
+// columns are partitioned by the key hash straight from the caller's columns.
+nut_status groupby_partitioned_direct(nut_groups *g, const nut_agg_spec *s, uint64_t group_hint) {
+  nut_ctx *c = g->ctx;
+  hipStream_t st = c->stream;
+  const int nk = g->nk, na = g->naggs;
+  const uint64_t n = s->n;
+  // value columns the aggregates read, each partitioned once
+  int vmap[NUT_MAX_VALS];
+  int nv = 0;
+  for (int j = 0; j < NUT_MAX_VALS; ++j) vmap[j] = -1;
+  for (int a = 0; a < na; ++a)
+    if (s->agg_op[a] != NUT_AGG_COUNT && vmap[s->agg_arg[a][0]] < 0) vmap[s->agg_arg[a][0]] = nv++;
+  const int narr = 3 + nv;
+  const uint64_t rows = (n + 2 * 65536 + 64 + 31) & ~31ull;  // + one alignment gap per partition
+  const int nstore = narr - 1 - (nk == 1 ? 1 : 0);
+  nut_status e = c->gp_data.reserve(2 * (size_t)nstore * rows * 8 + 256);
+  if (e) return e;
+  uint64_t *A[GP_MAX_ARR] = {}, *B[GP_MAX_ARR] = {};
+  for (int i = 1, k = 0; i < narr; ++i) {
+    if (i == 2 && nk == 1) continue;
+    A[i] = (uint64_t *)c->gp_data.ptr + (size_t)k * rows;
+    B[i] = (uint64_t *)c->gp_data.ptr + (size_t)(nstore + k) * rows;
+    ++k;
+  }
+  const uint64_t *src[GP_MAX_ARR] = {};
+  src[1] = (const uint64_t *)s->keys[0];
+  src[2] = nk == 2 ? (const uint64_t *)s->keys[1] : nullptr;
+  for (int j = 0; j < NUT_MAX_VALS; ++j)
+    if (vmap[j] >= 0) src[3 + vmap[j]] = (const uint64_t *)s->val_col[j];
+  GpMeta mm{c};
+  int levels = group_hint > 256ull * 1024 ? 2 : 1;
+  levels = env_int("NUT_GP_LEVELS", levels) == 2 ? 2 : 1;
+  c->timer.begin(st, NUT_KERNEL_AGGREGATE);
+  std::vector<GpSeg> segs{GpSeg{0, n, 0, 0}};
+  std::vector<uint64_t> hist, parts;
+  uint64_t **fin = B;
+  if (levels == 1) {
+    e = gp_level(c, mm, segs, 56, src, B, narr, false, false, hist, &parts);
+    if (e) return e;
+  } else {
+    e = gp_level(c, mm, segs, 56, src, A, narr, false, false, hist);
+    if (e) return e;
+    std::vector<GpSeg> s2;
+    uint64_t run = 0;
+    for (int d = 0; d < GP_BINS; ++d) {
+      if (hist[d]) s2.push_back(GpSeg{run, hist[d], 0, 0});
+      run += hist[d];
+    }
+    std::vector<uint64_t> h2;
+    e = gp_level(c, mm, s2, 48, A, B, narr, false, false, h2, &parts);
+    if (e) return e;
+  }
+  c->timer.end(st);
+  nut_agg_spec s2;
+  memset(&s2, 0, sizeof(s2));
+  s2.n = n;  // (segment mode reads only the listed ranges)
+  s2.nkeys = nk;
+  s2.keys[0] = (const int64_t *)fin[1];
+  s2.keys[1] = nk == 2 ? (const int64_t *)fin[2] : nullptr;
+  s2.nvals = nv;
+  s2.naggs = na;
+  for (int j = 0; j < NUT_MAX_VALS; ++j)
+    if (vmap[j] >= 0) {
+      s2.val_col[vmap[j]] = fin[3 + vmap[j]];
+      s2.val_type[vmap[j]] = s->val_type[j];
+    }
+  for (int a = 0; a < na; ++a) {
+    s2.agg_op[a] = s->agg_op[a];
+    s2.agg_expr[a] = NUT_EX_COL;
+    if (s->agg_op[a] != NUT_AGG_COUNT) s2.agg_arg[a][0] = vmap[s->agg_arg[a][0]];
+  }
+  return gp_aggregate(g, mm, parts, s2, g->kinds, group_hint);
 }
 
 // Spill -> partition -> per-partition aggregation into g's table.  *used = false when the
@@ -559,6 +708,12 @@ nut_status groupby_partitioned(nut_groups *g, const nut_agg_spec *s, uint64_t gr
   }
   if (nv > NUT_MAX_VALS) return NUT_OK;
   *used = true;
+  // Direct path: no WHERE and every argument a plain column (BASELINE config 3) — the
+  // spill would only copy the key and value columns, so the first partition level reads
+  // them in place (a key histogram pass of 8 B/row instead of a 32 B/row spill).
+  bool direct = !s->prog_mode && s->npred == 0 && env_int("NUT_GP_DIRECT", 1) != 0;
+  for (int a = 0; a < na && direct; ++a) direct = s->agg_op[a] == NUT_AGG_COUNT || s->agg_expr[a] == NUT_EX_COL;
+  if (direct) return groupby_partitioned_direct(g, s, group_hint);
   const int narr = 3 + nv;  // -, k1, k2 (unused for one key), values
   const uint64_t n = s->n;
   // staging: every block's region (<= n + one region of slack per block) in A, the
@@ -626,24 +781,6 @@ nut_status groupby_partitioned(nut_groups *g, const nut_agg_spec *s, uint64_t gr
     fin = A;
   }
   c->timer.end(st);
-  const uint32_t nparts = (uint32_t)(parts.size() / 2);
-  // split partitions into chunks (even boundaries) so that the grid fills the chip (chunks
-  // of one partition merge the same keys: a handful of extra merges per group)
-  const uint64_t k = std::max<uint64_t>(1, ((uint64_t)c->num_cus * 4 + nparts - 1) / nparts);
-  std::vector<uint64_t> off;
-  for (uint32_t p = 0; p < nparts; ++p) {
-    const uint64_t a0 = parts[2 * p], a1 = parts[2 * p + 1];
-    uint64_t prev = a0;
-    for (uint64_t j = 1; j <= k; ++j) {
-      const uint64_t cut = j == k ? a1 : std::max<uint64_t>(prev, (a0 + (a1 - a0) * j / k) & ~1ull);
-      if (cut > prev) {
-        off.push_back(prev);
-        off.push_back(cut);
-        prev = cut;
-      }
-    }
-  }
-  const uint32_t nblk = (uint32_t)(off.size() / 2);
   // ---- 3. one workgroup per partition, its groups in LDS, merged into g's table once
   nut_agg_spec s2;
   memset(&s2, 0, sizeof(s2));
@@ -664,26 +801,7 @@ nut_status groupby_partitioned(nut_groups *g, const nut_agg_spec *s, uint64_t gr
       s2.val_type[sp.sp_map[a]] = (k == AK_SUM_F64 || k == AK_MIN_F64 || k == AK_MAX_F64) ? NUT_T_F64 : NUT_T_I64;
     }
   }
-  e = mm.begin(GpMeta::al(off.size() * 8));
-  if (e) return e;
-  uint64_t *doff;
-  if ((e = mm.up(off, &doff))) return e;
-  LaunchExtra sg;
-  sg.seg_off = doff;
-  sg.nseg = nblk;
-  const uint64_t per = std::max<uint64_t>(64, 2 * ((group_hint + nparts - 1) / nparts));
-  for (int attempt = 0;; ++attempt) {
-    e = launch_agg(g, &s2, per, kinds2, &sg);
-    if (!e) e = read_ctl(g, ctl);
-    if (e) return e;
-    if (!(ctl[1] & 1u)) break;
-    // more groups than the table admits: a larger table, then the same partitions again
-    if (g->gt.cap >= (1ull << 34) || attempt > 12) return fail(NUT_ERR_OOM, "nut_groupby: group table too large");
-    e = alloc_table(g, g->gt.cap * 4);
-    if (e) return e;
-  }
-  NUT_HIP(hipStreamSynchronize(st));  // the host tables in mm.keep outlive their copies
-  return NUT_OK;
+  return gp_aggregate(g, mm, parts, s2, kinds2, group_hint);
 }
 
 }  // namespace
@@ -794,7 +912,7 @@ nut_status nut_groups_to_device(nut_groups *g, uint64_t *out, uint64_t cap) {
   DeviceGuard dg(c->device);
   NUT_HIP(hipMemsetAsync(g->dev_cursors, 0, 64 * 8, c->stream));
   uint64_t stride = g->gt.cap + 1;
-  uint64_t blocks = std::min<uint64_t>((stride + 255) / 256, (uint64_t)c->num_cus * 8);
+  uint64_t blocks = std::min<uint64_t>((stride + GT_CHUNK - 1) / GT_CHUNK, (uint64_t)c->num_cus * 8);
   hipLaunchKernelGGL(gtable_compact_kernel, dim3((unsigned)blocks), dim3(256), 0, c->stream,
                      (const GTable *)g->dev_gt, g->nk, out, n, g->dev_cursors, 1, (const uint64_t *)nullptr);
   NUT_HIP(hipGetLastError());
@@ -814,7 +932,7 @@ nut_status nut_groups_partition(nut_groups *g, int nparts, uint64_t *out, uint64
     return nut_groups_to_device(g, out, cap);
   }
   uint64_t stride = g->gt.cap + 1;
-  uint64_t blocks = std::min<uint64_t>((stride + 255) / 256, (uint64_t)c->num_cus * 8);
+  uint64_t blocks = std::min<uint64_t>((stride + GT_CHUNK - 1) / GT_CHUNK, (uint64_t)c->num_cus * 8);
   NUT_HIP(hipMemsetAsync(g->dev_cursors, 0, 64 * 8, c->stream));
   hipLaunchKernelGGL(gtable_owner_count_kernel, dim3((unsigned)blocks), dim3(256), 0, c->stream,
                      (const GTable *)g->dev_gt, g->nk, nparts, g->dev_cursors);
@@ -1117,11 +1235,9 @@ nut_status nut_groups_to_host(nut_groups *g, int64_t *keys, uint64_t *aggs, uint
       hipLaunchKernelGGL(groups_place_kernel, dim3((unsigned)blocks), dim3(256), 0, c->stream, (const uint64_t *)dev,
                          (const int64_t *)sorted, n, g->naggs, dk, da);
       hipError_t e = hipGetLastError();
-      if (e == hipSuccess) e = hipMemcpyAsync(keys, dk, nb, hipMemcpyDeviceToHost, c->stream);
-      if (e == hipSuccess && g->naggs)
-        e = hipMemcpyAsync(aggs, da, nb * g->naggs, hipMemcpyDeviceToHost, c->stream);
-      if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
       if (e != hipSuccess) st = hip_fail(e, "nut_groups_to_host (device order)");
+      if (!st) st = copy_to_host(c, keys, dk, nb);
+      if (!st && g->naggs) st = copy_to_host(c, aggs, da, nb * g->naggs);
     }
     (void)hipFreeAsync(buf, c->stream);
     (void)hipFreeAsync(dev, c->stream);
@@ -1155,9 +1271,16 @@ nut_status nut_groups_to_host(nut_groups *g, int64_t *keys, uint64_t *aggs, uint
 void nut_groups_free(nut_groups *g) {
   if (!g) return;
   if (g->mem) {
-    DeviceGuard dg(g->ctx->device);
-    (void)hipStreamSynchronize(g->ctx->stream);
-    (void)hipFree(g->mem);
+    nut_ctx *c = g->ctx;
+    DeviceGuard dg(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    if (g->mem_bytes >= c->tbl_pool_bytes) {  // keep the larger allocation for the next table
+      if (c->tbl_pool) (void)hipFree(c->tbl_pool);
+      c->tbl_pool = g->mem;
+      c->tbl_pool_bytes = g->mem_bytes;
+    } else {
+      (void)hipFree(g->mem);
+    }
   }
   delete g;
 }

@@ -2,6 +2,9 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <algorithm>
+#include <thread>
+
 #include "common.hpp"
 
 namespace nut {
@@ -107,6 +110,48 @@ __global__ void gen_column_kernel(int kind, uint64_t seed, int64_t a, int64_t b,
   }
 }
 
+// ------------------------------------------------------------ large D2H
+constexpr size_t kStageBytes = 32u << 20;  // per pinned chunk
+constexpr int kCopyThreads = 8;
+
+nut_status copy_to_host(nut_ctx *c, void *dst, const void *src, size_t bytes) {
+  if (bytes < (8u << 20)) {  // small: one plain copy
+    NUT_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
+    NUT_HIP(hipStreamSynchronize(c->stream));
+    return NUT_OK;
+  }
+  for (auto &b : c->stage)
+    if (!b) NUT_HIP(hipHostMalloc((void **)&b, kStageBytes, hipHostMallocDefault));
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  for (auto &e : ev) NUT_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  const size_t nch = (bytes + kStageBytes - 1) / kStageBytes;
+  auto chunk = [&](size_t i) { return std::min(kStageBytes, bytes - i * kStageBytes); };
+  hipError_t e = hipMemcpyAsync(c->stage[0], src, chunk(0), hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipEventRecord(ev[0], c->stream);
+  for (size_t i = 0; i < nch && e == hipSuccess; ++i) {
+    if (i + 1 < nch) {  // the next chunk's transfer overlaps this chunk's host copy
+      e = hipMemcpyAsync(c->stage[(i + 1) & 1], (const char *)src + (i + 1) * kStageBytes, chunk(i + 1),
+                         hipMemcpyDeviceToHost, c->stream);
+      if (e == hipSuccess) e = hipEventRecord(ev[(i + 1) & 1], c->stream);
+    }
+    if (e == hipSuccess) e = hipEventSynchronize(ev[i & 1]);
+    if (e != hipSuccess) break;
+    const char *from = c->stage[i & 1];
+    char *to = (char *)dst + i * kStageBytes;
+    const size_t len = chunk(i), per = (len + kCopyThreads - 1) / kCopyThreads;
+    std::thread th[kCopyThreads];
+    for (int t = 0; t < kCopyThreads; ++t) {
+      const size_t a = std::min(len, t * per), b = std::min(len, a + per);
+      th[t] = std::thread([=] { memcpy(to + a, from + a, b - a); });
+    }
+    for (auto &t : th) t.join();
+  }
+  // the staging buffer of the last chunk must not be rewritten before its event
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  for (auto &ev1 : ev) (void)hipEventDestroy(ev1);
+  return e == hipSuccess ? NUT_OK : hip_fail(e, "copy_to_host");
+}
+
 }  // namespace nut
 
 using namespace nut;
@@ -163,6 +208,9 @@ void nut_ctx_destroy(nut_ctx *c) {
   c->gp_meta.release();
   c->misc.release();
   c->timer.release();
+  for (auto &b : c->stage)
+    if (b) (void)hipHostFree(b);
+  if (c->tbl_pool) (void)hipFree(c->tbl_pool);
   if (c->host_pinned) (void)hipHostFree(c->host_pinned);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;

@@ -133,6 +133,12 @@ nut_status hip_fail(hipError_t e, const char *what);
 int groups_width(const nut_groups *g);
 void groups_merge_spec(const nut_groups *g, const uint64_t *seg, uint64_t c, nut_agg_spec *s, nut_prog_node *nodes);
 
+// Device -> pageable host copy of a large result, synchronous (api.hip): chunks go
+// through two pinned staging buffers while host threads move the previous chunk into
+// place — a plain hipMemcpy to pageable (often untouched, freshly allocated) memory ran
+// at ~10 GB/s, its page faults and staging copies serialised on one thread.
+nut_status copy_to_host(nut_ctx *c, void *dst, const void *src, size_t bytes);
+
 // Device scratch that only grows; reused across calls (no malloc in steady state).
 struct Scratch {
   void *ptr = nullptr;
@@ -182,6 +188,9 @@ struct nut_ctx {
   nut::Scratch gp_meta;       //   and their per-level tables
   nut::Scratch misc;
   uint64_t *host_pinned = nullptr;  // small pinned staging for counts/flags
+  char *stage[2] = {nullptr, nullptr};  // copy_to_host's pinned chunks (allocated on first use)
+  void *tbl_pool = nullptr;             // the last freed group table's allocation, for reuse:
+  size_t tbl_pool_bytes = 0;            //   hipMalloc / hipFree of a 10^7-group table cost ms
   nut::KernelTimer timer;
 };
 

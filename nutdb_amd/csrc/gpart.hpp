@@ -17,8 +17,8 @@
 namespace nut {
 
 constexpr int GP_THREADS = 512;
-constexpr int GP_ITEMS = 8;
-constexpr uint32_t GP_TILE = GP_THREADS * GP_ITEMS;  // 4096 records per scatter tile
+constexpr int GP_ITEMS = 16;
+constexpr uint32_t GP_TILE = GP_THREADS * GP_ITEMS;  // 8192 records per scatter tile
 constexpr int GP_HTHREADS = 256;
 constexpr uint32_t GP_HTILE = 1u << 16;              // records per histogram tile
 constexpr int GP_BINS = 256;
@@ -75,86 +75,111 @@ __global__ __launch_bounds__(GP_HTHREADS) void gp_hist_kernel(const uint64_t *__
 
 // Unstable partition of every segment's records by (hash >> shift) & 255: a tile ranks its
 // records with LDS atomics and claims each digit's output run with one global atomic on
-// the segment's digit cursor; then every array is staged in LDS in digit order (coalesced
-// loads in, one LDS write per record) and written out in coalesced runs.
+// the segment's digit cursor; then every array is staged in LDS in digit order (one LDS
+// write per record) and written out in coalesced runs.  Persistent (2 workgroups per CU):
+// the keys stay in registers from the digit to their own staging, and the next tile's
+// keys are fetched while this tile's value arrays go through.
 // Gather mode: all segments share one set of 256 cursors (the spilled blocks' regions ->
 // one compact partitioned array).
-__global__ __launch_bounds__(GP_THREADS) void gp_scatter_kernel(GpArrays ar, const GpSeg *__restrict__ segs,
-                                                                const uint32_t *__restrict__ tile_seg, int shift,
-                                                                int gather, unsigned long long *__restrict__ cursor,
-                                                                uint64_t kx) {
-  __shared__ uint64_t s_stage[GP_TILE];
-  __shared__ uint8_t s_dig[GP_TILE];
+template <int NK, int T>
+__global__ __launch_bounds__(T) void gp_scatter_kernel(GpArrays ar, const GpSeg *__restrict__ segs,
+                                                                const uint32_t *__restrict__ tile_seg, uint32_t ntiles,
+                                                                int shift, int gather,
+                                                                unsigned long long *__restrict__ cursor, uint64_t kx) {
+  __shared__ uint64_t s_stage[(T * GP_ITEMS)];
+  __shared__ uint8_t s_dig[(T * GP_ITEMS)];
   __shared__ uint32_t s_cnt[GP_BINS];
   __shared__ uint32_t s_tex[GP_BINS];
   __shared__ uint64_t s_gb[GP_BINS];
   __shared__ uint32_t s_wsum[GP_BINS / kWave];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (tid < GP_BINS) s_cnt[tid] = 0;
-  const uint32_t s = tile_seg[blockIdx.x];
-  const GpSeg sg = segs[s];
-  const uint64_t lo = sg.start + (uint64_t)(blockIdx.x - sg.tile0) * GP_TILE;
-  const uint32_t n = (uint32_t)min<uint64_t>(GP_TILE, sg.start + sg.count - lo);
-  __syncthreads();
-  uint32_t d[GP_ITEMS], slot[GP_ITEMS];
+  uint64_t k1[GP_ITEMS], k2[NK == 2 ? GP_ITEMS : 1];
+  auto load_keys = [&](uint32_t tt) {
+    const GpSeg g = segs[tile_seg[tt]];
+    const uint64_t lo = g.start + (uint64_t)(tt - g.tile0) * (T * GP_ITEMS);
+    const uint32_t n = (uint32_t)min<uint64_t>((T * GP_ITEMS), g.start + g.count - lo);
 #pragma unroll
-  for (int i = 0; i < GP_ITEMS; ++i) {
-    const uint32_t idx = (uint32_t)i * GP_THREADS + tid;
-    d[i] = idx < n ? gp_digit(ar.src[1], ar.src[2], lo + idx, shift, kx) : 0u;
-    slot[i] = idx < n ? atomicAdd(&s_cnt[d[i]], 1u) : 0u;
-  }
-  __syncthreads();
-  uint32_t c = 0, incl = 0;
-  if (tid < GP_BINS) {
-    c = s_cnt[tid];
-    incl = c;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const uint32_t y = __shfl_up(incl, off, 64);
-      if (lane >= off) incl += y;
+    for (int i = 0; i < GP_ITEMS; ++i) {  // unconditional (clamped): all loads in flight at once
+      const uint64_t r = lo + min((uint32_t)i * T + tid, n - 1);
+      k1[i] = __builtin_nontemporal_load(ar.src[1] + r);
+      if (NK == 2) k2[i] = __builtin_nontemporal_load(ar.src[2] + r);
     }
-    if (lane == 63) s_wsum[wave] = incl;
-  }
-  __syncthreads();
-  if (tid < GP_BINS) {
-    uint32_t add = 0;
-#pragma unroll
-    for (int w = 0; w < GP_BINS / kWave; ++w) add += (w < wave) ? s_wsum[w] : 0u;
-    const uint32_t tex = incl - c + add;
-    s_tex[tid] = tex;
-    const uint64_t cs = gather ? 0 : (uint64_t)s;
-    const uint64_t gb = c ? (uint64_t)atomicAdd(&cursor[cs * GP_BINS + tid], (unsigned long long)c) : 0;
-    s_gb[tid] = gb - tex;  // output position of tile slot j with digit d = s_gb[d] + j
-  }
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < GP_ITEMS; ++i) {
-    const uint32_t idx = (uint32_t)i * GP_THREADS + tid;
-    if (idx < n) {
-      slot[i] += s_tex[d[i]];
-      s_dig[slot[i]] = (uint8_t)d[i];
-    }
-  }
-  for (int a = 1; a < ar.narr; ++a) {
-    if (!ar.src[a]) continue;  // k2 of one-key queries
-    const uint64_t *src = ar.src[a] + lo;
-    uint64_t *dst = ar.dst[a];
-    uint64_t v[GP_ITEMS];
+  };
+  uint32_t t = blockIdx.x;
+  if (t >= ntiles) return;
+  load_keys(t);
+  for (;;) {
+    const uint32_t s = tile_seg[t];
+    const GpSeg sg = segs[s];
+    const uint64_t lo = sg.start + (uint64_t)(t - sg.tile0) * (T * GP_ITEMS);
+    const uint32_t n = (uint32_t)min<uint64_t>((T * GP_ITEMS), sg.start + sg.count - lo);
+    if (tid < GP_BINS) s_cnt[tid] = 0;
+    __syncthreads();
+    uint32_t dg[GP_ITEMS], slot[GP_ITEMS];
 #pragma unroll
     for (int i = 0; i < GP_ITEMS; ++i) {
-      const uint32_t idx = (uint32_t)i * GP_THREADS + tid;
-      v[i] = idx < n ? __builtin_nontemporal_load(src + idx) : 0;
+      const bool v = (uint32_t)i * T + tid < n;
+      dg[i] = (uint32_t)(owner_hash(k1[i] ^ kx, NK == 2 ? k2[i] : 0, NK) >> shift) & 255u;
+      slot[i] = v ? atomicAdd(&s_cnt[dg[i]], 1u) : 0u;
     }
-    __syncthreads();  // the previous array's write-out is done with s_stage
+    __syncthreads();
+    uint32_t c = 0, incl = 0;
+    if (tid < GP_BINS) {
+      c = s_cnt[tid];
+      incl = c;
 #pragma unroll
-    for (int i = 0; i < GP_ITEMS; ++i)
-      if ((uint32_t)i * GP_THREADS + tid < n) s_stage[slot[i]] = v[i];
+      for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += y;
+      }
+      if (lane == 63) s_wsum[wave] = incl;
+    }
+    __syncthreads();
+    if (tid < GP_BINS) {
+      uint32_t add = 0;
+#pragma unroll
+      for (int w = 0; w < GP_BINS / kWave; ++w) add += (w < wave) ? s_wsum[w] : 0u;
+      const uint32_t tex = incl - c + add;
+      s_tex[tid] = tex;
+      const uint64_t cs = gather ? 0 : (uint64_t)s;
+      const uint64_t gb = c ? (uint64_t)atomicAdd(&cursor[cs * GP_BINS + tid], (unsigned long long)c) : 0;
+      s_gb[tid] = gb - tex;  // output position of tile slot j with digit d = s_gb[d] + j
+    }
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < GP_ITEMS; ++i) {
-      const uint32_t j = (uint32_t)i * GP_THREADS + tid;
-      if (j < n) dst[s_gb[s_dig[j]] + j] = s_stage[j];
+      if ((uint32_t)i * T + tid < n) {
+        slot[i] += s_tex[dg[i]];
+        s_dig[slot[i]] = (uint8_t)dg[i];
+      }
     }
+    // one array through LDS: stage in digit order, write out coalesced runs
+    auto pass = [&](const uint64_t (&v)[GP_ITEMS], uint64_t *dst) {
+      __syncthreads();  // the previous array's write-out is done with s_stage
+#pragma unroll
+      for (int i = 0; i < GP_ITEMS; ++i)
+        if ((uint32_t)i * T + tid < n) s_stage[slot[i]] = v[i];
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < GP_ITEMS; ++i) {
+        const uint32_t j = (uint32_t)i * T + tid;
+        if (j < n) dst[s_gb[s_dig[j]] + j] = s_stage[j];
+      }
+    };
+    pass(k1, ar.dst[1]);
+    if constexpr (NK == 2) pass(k2, ar.dst[2]);
+    const uint32_t next = t + gridDim.x;
+    if (next < ntiles) load_keys(next);  // the key registers are free
+    for (int a = 3; a < ar.narr; ++a) {
+      uint64_t v[GP_ITEMS];
+#pragma unroll
+      for (int i = 0; i < GP_ITEMS; ++i)
+        v[i] = __builtin_nontemporal_load(ar.src[a] + lo + min((uint32_t)i * T + tid, n - 1));
+      pass(v, ar.dst[a]);
+    }
+    if (next >= ntiles) break;
+    __syncthreads();  // s_cnt / s_stage / s_dig / s_gb are reused
+    t = next;
   }
 }
 

@@ -201,55 +201,114 @@ __global__ void gtable_sum_kernel(const GTable *__restrict__ gtp) {
   }
 }
 
-// dense column-major copy of the occupied slots; owner partitioning optional (one
-// cursor atomic per wave when not partitioned)
-__global__ void gtable_compact_kernel(const GTable *__restrict__ gtp, int nk, uint64_t *__restrict__ out,
-                                      uint64_t out_cap, unsigned long long *__restrict__ cursors, int nparts,
-                                      const uint64_t *__restrict__ seg_base) {
+// dense column-major copy of the occupied slots; owner partitioning optional.  A block
+// takes GT_CHUNK consecutive slots at a time, counts them per part in LDS (wave-aggregated
+// when unpartitioned) and claims each part's run with ONE global atomic per chunk: a
+// cursor atomic per wave serialised 10^7 groups on one address (6.3 ms).
+constexpr int GT_THREADS = 256;  // the launch's block size
+constexpr int GT_PER = 8;
+constexpr uint32_t GT_CHUNK = GT_THREADS * GT_PER;
+__global__ __launch_bounds__(GT_THREADS) void gtable_compact_kernel(const GTable *__restrict__ gtp, int nk,
+                                                                    uint64_t *__restrict__ out, uint64_t out_cap,
+                                                                    unsigned long long *__restrict__ cursors,
+                                                                    int nparts, const uint64_t *__restrict__ seg_base) {
+  __shared__ uint32_t s_cnt[64];
+  __shared__ unsigned long long s_base[64];
   const GTable t = *gtp;
   const uint64_t stride = t.cap + 1;
-  const int w = nk + t.naggs;
-  for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < stride;
-       s += (uint64_t)gridDim.x * blockDim.x) {
-    uint64_t k1, k2;
-    const bool occ = slot_keys(t, nk, s, k1, k2);
-    int part = 0;
-    uint64_t pos;
-    if (nparts > 1) {
-      if (!occ) continue;
-      part = (int)(owner_hash(k1, k2, nk) % (uint64_t)nparts);
-      pos = atomicAdd(&cursors[part], 1ull);
-    } else {
-      const uint64_t m = __ballot(occ);
-      if (!occ) continue;
-      const int lane = threadIdx.x & 63, leader = __builtin_ctzll(m);
-      unsigned long long b = 0;
-      if (lane == leader) b = atomicAdd(&cursors[0], (unsigned long long)__popcll(m));
-      pos = __shfl(b, leader, 64) + lane_rank(m);
+  const int tid = threadIdx.x, lane = tid & 63;
+  for (uint64_t c0 = (uint64_t)blockIdx.x * GT_CHUNK; c0 < stride; c0 += (uint64_t)gridDim.x * GT_CHUNK) {
+    if (tid < nparts) s_cnt[tid] = 0;
+    __syncthreads();
+    uint64_t k1[GT_PER], k2[GT_PER];
+    uint32_t rank[GT_PER];
+    int part[GT_PER];
+    bool occ[GT_PER];
+    // slot words first, all in flight (clamped, unconditional), then the tuple lookups
+    uint64_t wd[GT_PER];
+#pragma unroll
+    for (int i = 0; i < GT_PER; ++i) {
+      const uint64_t sl = c0 + (uint64_t)i * GT_THREADS + tid;
+      wd[i] = t.slot[sl < stride ? sl : stride - 1];
     }
-    // segment `part` starts at word w*seg_base[part]; each of its columns has seg_n rows
-    uint64_t seg_n = nparts > 1 ? seg_base[nparts + part] : out_cap;
-    uint64_t *seg = out + (nparts > 1 ? (uint64_t)w * seg_base[part] : 0);
-    seg[pos] = k1;
-    if (nk == 2) seg[seg_n + pos] = k2;
-    for (int a = 0; a < t.naggs; ++a) {
-      uint64_t x = t.agg[a * stride + s];
-      int kind = kind_at(t.kinds, a);
-      if (kind == AK_MIN_F64 || kind == AK_MAX_F64) x = ord_to_f64(x);
-      seg[(uint64_t)(nk + a) * seg_n + pos] = x;
+#pragma unroll
+    for (int i = 0; i < GT_PER; ++i) {
+      const uint64_t sl = c0 + (uint64_t)i * GT_THREADS + tid;
+      if (nk == 1) {
+        k1[i] = sl == t.cap ? kEmpty : wd[i];
+        k2[i] = 0;
+        occ[i] = sl < stride && (sl == t.cap ? t.ctl[2] != 0u : wd[i] != kEmpty);
+      } else {
+        occ[i] = sl < t.cap && wd[i] != kEmpty2;
+        const uint32_t ai = occ[i] ? (uint32_t)wd[i] : 0u;  // unconditional: the loads overlap
+        k1[i] = (uint64_t)t.ak1[ai];
+        k2[i] = (uint64_t)t.ak2[ai];
+      }
     }
+#pragma unroll
+    for (int i = 0; i < GT_PER; ++i) {
+      part[i] = 0;
+      rank[i] = 0;
+      if (nparts > 1) {
+        if (occ[i]) {
+          part[i] = (int)(owner_hash(k1[i], k2[i], nk) % (uint64_t)nparts);
+          rank[i] = atomicAdd(&s_cnt[part[i]], 1u);
+        }
+      } else {
+        const uint64_t m = __ballot(occ[i]);
+        if (m) {
+          const int leader = __builtin_ctzll(m);
+          uint32_t b = 0;
+          if (lane == leader) b = atomicAdd(&s_cnt[0], (uint32_t)__popcll(m));
+          rank[i] = __shfl(b, leader, 64) + lane_rank(m);
+        }
+      }
+    }
+    __syncthreads();
+    if (tid < nparts) s_base[tid] = s_cnt[tid] ? atomicAdd(&cursors[tid], (unsigned long long)s_cnt[tid]) : 0ull;
+    __syncthreads();
+    const int w = nk + t.naggs;
+#pragma unroll
+    for (int i = 0; i < GT_PER; ++i) {
+      if (!occ[i]) continue;
+      const uint64_t sl = c0 + (uint64_t)i * GT_THREADS + tid;
+      const int pt = part[i];
+      const uint64_t pos = s_base[pt] + rank[i];
+      // segment `pt` starts at word w*seg_base[pt]; each of its columns has seg_n rows
+      const uint64_t seg_n = nparts > 1 ? seg_base[nparts + pt] : out_cap;
+      uint64_t *seg = out + (nparts > 1 ? (uint64_t)w * seg_base[pt] : 0);
+      seg[pos] = k1[i];
+      if (nk == 2) seg[seg_n + pos] = k2[i];
+      for (int a = 0; a < t.naggs; ++a) {
+        uint64_t x = t.agg[a * stride + sl];
+        const int kind = kind_at(t.kinds, a);
+        if (kind == AK_MIN_F64 || kind == AK_MAX_F64) x = ord_to_f64(x);
+        seg[(uint64_t)(nk + a) * seg_n + pos] = x;
+      }
+    }
+    __syncthreads();  // s_cnt / s_base are reused
   }
 }
 
-__global__ void gtable_owner_count_kernel(const GTable *__restrict__ gtp, int nk, int nparts,
-                                          unsigned long long *counts) {
+// groups per owner part: LDS counts per block chunk, one global atomic per (chunk, part)
+__global__ __launch_bounds__(GT_THREADS) void gtable_owner_count_kernel(const GTable *__restrict__ gtp, int nk,
+                                                                        int nparts, unsigned long long *counts) {
+  __shared__ uint32_t s_cnt[64];
   const GTable t = *gtp;
   const uint64_t stride = t.cap + 1;
-  for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < stride;
-       s += (uint64_t)gridDim.x * blockDim.x) {
-    uint64_t k1, k2;
-    if (!slot_keys(t, nk, s, k1, k2)) continue;
-    atomicAdd(&counts[owner_hash(k1, k2, nk) % (uint64_t)nparts], 1ull);
+  const int tid = threadIdx.x;
+  for (uint64_t c0 = (uint64_t)blockIdx.x * GT_CHUNK; c0 < stride; c0 += (uint64_t)gridDim.x * GT_CHUNK) {
+    if (tid < nparts) s_cnt[tid] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < GT_PER; ++i) {
+      const uint64_t sl = c0 + (uint64_t)i * GT_THREADS + tid;
+      uint64_t k1, k2;
+      if (sl < stride && slot_keys(t, nk, sl, k1, k2)) atomicAdd(&s_cnt[owner_hash(k1, k2, nk) % (uint64_t)nparts], 1u);
+    }
+    __syncthreads();
+    if (tid < nparts && s_cnt[tid]) atomicAdd(&counts[tid], (unsigned long long)s_cnt[tid]);
+    __syncthreads();
   }
 }
 

@@ -233,8 +233,9 @@ class Groups:
     def to_host_words(self):
         """(keys int64 [n, nkeys], aggs uint64 [n, naggs]) sorted by key tuple."""
         n = len(self)
-        keys = np.zeros((n, self.nkeys), dtype=np.int64)
-        aggs = np.zeros((n, max(self.naggs, 1)), dtype=np.uint64)
+        # np.empty: the library writes every word; np.zeros spent ~10 ms zeroing 1e7 groups
+        keys = np.empty((n, self.nkeys), dtype=np.int64)
+        aggs = np.empty((n, max(self.naggs, 1)), dtype=np.uint64)
         check(lib.nut_groups_to_host(self.h, keys.ctypes.data, aggs.ctypes.data, n), "nut_groups_to_host")
         return keys, aggs[:, : self.naggs]
 
