@@ -286,6 +286,15 @@ nut_status nut_q1(nut_ctx *ctx, const int64_t *shipdate, const int64_t *returnfl
 nut_status nut_sort_i64(nut_ctx *ctx, const int64_t *in, int64_t *out, uint64_t n);
 /* ORDER BY k DESC (the same passes with the key order complemented; no extra pass) */
 nut_status nut_sort_i64_desc(nut_ctx *ctx, const int64_t *in, int64_t *out, uint64_t n);
+/* ORDER BY with projected columns (OrderByClause.keys, query.rs:86-90): a STABLE sort of
+ * (key, payload) pairs that returns the payload in key order — vals_out[i] = the payload
+ * of the i-th smallest key (DESC: largest), ties in input order.  keys: n int64
+ * (key_type NUT_T_I64) or float64 (NUT_T_F64, IEEE total order: -NaN < -inf < ... < -0 <
+ * +0 < ... < +inf < NaN) values; vals: n int64 payloads, or NULL for the row ids 0..n-1.
+ * Several ORDER BY keys: sort by the last key first and feed each result as the next
+ * call's payload (LSD order, the sort is stable).  vals and vals_out may not alias. */
+nut_status nut_sort_pairs(nut_ctx *ctx, const void *keys, int key_type, int desc, const int64_t *vals,
+                          int64_t *vals_out, uint64_t n);
 /* Stable partition of int64 keys into nsplit+1 buckets, bucket(k) = #{i : splitters[i] <= k}
  * (splitters_host ascending, 0 <= nsplit < 64).  Bucket b is written to out at offset
  * sum_{c<b} counts_host[c]; counts_host receives nsplit+1 counts.  The local step of the

@@ -185,6 +185,7 @@ SIGNATURES = {
     "nut_result_device_column": (_I32, [_P, _I32, C.POINTER(_P)]),
     "nut_result_free": (None, [_P]),
     "nut_ctx_memcpy": (_I32, [_P, _P, _P, C.c_size_t]),
+    "nut_sort_pairs": (_I32, [_P, _P, _I32, _I32, _P, _P, _U64]),
     # multi-GPU (RCCL inside the library)
     "nut_dist_create": (_I32, [_I32, C.POINTER(_I32), C.POINTER(_P)]),
     "nut_dist_unique_id": (_I32, [_P]),

@@ -160,14 +160,20 @@ __device__ __forceinline__ uint64_t digit_peers(uint32_t d, bool valid) {
 
 // FIRST: input is raw int64 (flip on load); LAST: write int64 (flip back).
 // nbins: digits in use (256 for radix passes, #buckets for a partition).
-template <bool FIRST, bool LAST, class Digit>
+// PAIRS: every key carries a 64-bit payload (vin -> vout, moved with it; vin == NULL on
+// the first pass = the row ids 0..n-1) — the stable key + row id sort of ORDER BY with
+// projected columns (nut_sort_pairs).
+template <bool FIRST, bool LAST, class Digit, bool PAIRS = false>
 __global__ __launch_bounds__(RS_THREADS) void rs_pass_kernel(const uint64_t *__restrict__ in, uint64_t *__restrict__ out,
                                                              uint64_t n, Digit dig, const int64_t *__restrict__ splitters,
                                                              int nbins, uint64_t flip, const uint64_t *__restrict__ dbase,
                                                              uint64_t *__restrict__ status, uint32_t epoch,
                                                              uint32_t *__restrict__ ticket,
-                                                             uint32_t *__restrict__ err) {
+                                                             uint32_t *__restrict__ err,
+                                                             const uint64_t *__restrict__ vin = nullptr,
+                                                             uint64_t *__restrict__ vout = nullptr) {
   __shared__ uint64_t s_keys[RS_TILE];             // tile staged in digit order
+  __shared__ uint64_t s_vals[PAIRS ? RS_TILE : 1];  // and its payload
   __shared__ uint32_t s_wcnt[RS_WAVES][RS_BINS];    // per-wave digit counters -> wave prefixes
   __shared__ uint32_t s_tex[RS_BINS];              // exclusive digit offsets inside the tile
   __shared__ uint64_t s_gbase[RS_BINS];            // global position of the tile's first key of digit d
@@ -187,13 +193,16 @@ __global__ __launch_bounds__(RS_THREADS) void rs_pass_kernel(const uint64_t *__r
   const uint64_t wbase = tbase + (uint64_t)wave * RS_ITEMS * kWave;
 
   uint64_t key[RS_ITEMS];
+  uint64_t val[PAIRS ? RS_ITEMS : 1];
   uint32_t rank[RS_ITEMS];
 #pragma unroll
   for (int i = 0; i < RS_ITEMS; ++i) {
     const uint64_t idx = wbase + (uint64_t)i * kWave + lane;
-    uint64_t k = idx < n ? in[idx] : 0;
+    const uint64_t ci = idx < n ? idx : n - 1;  // clamped, unconditional: the loads overlap
+    uint64_t k = in[ci];
     if (FIRST) k ^= flip;
     key[i] = k;
+    if constexpr (PAIRS) val[i] = (FIRST && !vin) ? idx : vin[ci];
   }
   // stable in-wave ranking, items in order
 #pragma unroll
@@ -271,7 +280,9 @@ __global__ __launch_bounds__(RS_THREADS) void rs_pass_kernel(const uint64_t *__r
     const uint64_t idx = wbase + (uint64_t)i * kWave + lane;
     if (idx < n) {
       const uint32_t dd = dig(key[i], s_spl);
-      s_keys[s_tex[dd] + s_wcnt[wave][dd] + rank[i]] = key[i];
+      const uint32_t pos = s_tex[dd] + s_wcnt[wave][dd] + rank[i];
+      s_keys[pos] = key[i];
+      if constexpr (PAIRS) s_vals[pos] = val[i];
     }
   }
   __syncthreads();
@@ -283,8 +294,21 @@ __global__ __launch_bounds__(RS_THREADS) void rs_pass_kernel(const uint64_t *__r
     if (j < valid_n) {
       const uint64_t k = s_keys[j];
       const uint32_t dd = dig(k, s_spl);
-      out[s_gbase[dd] + (j - s_tex[dd])] = LAST ? (k ^ flip) : k;
+      const uint64_t o = s_gbase[dd] + (j - s_tex[dd]);
+      out[o] = LAST ? (k ^ flip) : k;
+      if constexpr (PAIRS) vout[o] = s_vals[j];
     }
+  }
+}
+
+// sort keys of nut_sort_pairs in unsigned order: int64 with the sign bit flipped, f64 by
+// the IEEE total order (-0 < +0, NaNs at the ends); DESC: the complement
+__global__ void sort_key_kernel(const uint64_t *__restrict__ in, int type, int desc, uint64_t n,
+                                uint64_t *__restrict__ out) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t b = in[i];
+    uint64_t u = type == NUT_T_F64 ? f64_to_ord(b) : (b ^ RS_FLIP);
+    out[i] = desc ? ~u : u;
   }
 }
 
@@ -371,7 +395,8 @@ nut_status nut::lsd_sort_i64(nut_ctx *c, const int64_t *in, int64_t *out, uint64
     auto kern = first ? (last ? rs_pass_kernel<true, true, RadixDigit> : rs_pass_kernel<true, false, RadixDigit>)
                       : (last ? rs_pass_kernel<false, true, RadixDigit> : rs_pass_kernel<false, false, RadixDigit>);
     hipLaunchKernelGGL(kern, dim3((unsigned)ntiles), dim3(RS_THREADS), 0, st, src, dst, n, RadixDigit{8 * p},
-                       (const int64_t *)nullptr, RS_BINS, flip, db, status, epoch, tickets + k, err);
+                       (const int64_t *)nullptr, RS_BINS, flip, db, status, epoch, tickets + k, err,
+                       (const uint64_t *)nullptr, (uint64_t *)nullptr);
     NUT_HIP(hipGetLastError());
     src = dst;
   }
@@ -379,6 +404,80 @@ nut_status nut::lsd_sort_i64(nut_ctx *c, const int64_t *in, int64_t *out, uint64
   NUT_HIP(hipMemcpyAsync(htriv, err, 4, hipMemcpyDeviceToHost, st));
   NUT_HIP(hipStreamSynchronize(st));
   if (htriv[0]) return fail(NUT_ERR_TIMEOUT, "nut_sort_i64: look-back spin limit hit");
+  return NUT_OK;
+}
+
+// Stable sort of (key, payload) pairs: ORDER BY keys with projected columns.  Keys are
+// mapped to unsigned order once (sort_key_kernel), then LSD passes move key and payload
+// together; only the permuted payload is returned (the caller gathers its columns
+// through it).  16 B/key per executed pass + 8 B/key histogram + 16 B/key key mapping.
+extern "C" nut_status nut_sort_pairs(nut_ctx *c, const void *keys, int key_type, int desc, const int64_t *vals,
+                                     int64_t *vals_out, uint64_t n) {
+  if (!c || (n && (!keys || !vals_out))) return fail(NUT_ERR_INVALID_ARG, "nut_sort_pairs: NULL argument");
+  if (key_type != NUT_T_I64 && key_type != NUT_T_F64) return fail(NUT_ERR_INVALID_ARG, "nut_sort_pairs: key type");
+  if (n == 0) return NUT_OK;
+  DeviceGuard g(c->device);
+  const uint64_t ntiles = (n + RS_TILE - 1) / RS_TILE;
+  if (ntiles > 0x7FFFFFF0ull || n > RS_VAL) return fail(NUT_ERR_UNSUPPORTED, "nut_sort_pairs: n too large");
+  hipStream_t st = c->stream;
+  // scratch: [err | tickets | hist 8x256 | base 8x256 | trivial] + keys A, keys B, payload B
+  const size_t o_hist = 256;
+  const size_t o_base = o_hist + 8 * RS_BINS * 8;
+  const size_t o_triv = o_base + 8 * RS_BINS * 8;
+  const size_t o_ka = (o_triv + 64 + 255) & ~size_t(255);
+  const size_t o_kb = o_ka + ((n * 8 + 255) & ~size_t(255));
+  const size_t o_vb = o_kb + ((n * 8 + 255) & ~size_t(255));
+  nut_status s = c->sort_tmp.reserve(o_vb + n * 8);
+  if (s) return s;
+  char *b = (char *)c->sort_tmp.ptr;
+  uint32_t *err = (uint32_t *)b;
+  uint32_t *tickets = (uint32_t *)(b + 16);
+  unsigned long long *hist = (unsigned long long *)(b + o_hist);
+  uint64_t *base = (uint64_t *)(b + o_base);
+  uint32_t *triv = (uint32_t *)(b + o_triv);
+  uint64_t *ka = (uint64_t *)(b + o_ka), *kb = (uint64_t *)(b + o_kb), *vb = (uint64_t *)(b + o_vb);
+  c->timer.begin(st, NUT_KERNEL_SORT);
+  const unsigned gk = (unsigned)std::min<uint64_t>((n + 255) / 256, (uint64_t)c->num_cus * 16);
+  hipLaunchKernelGGL(sort_key_kernel, dim3(gk), dim3(256), 0, st, (const uint64_t *)keys, key_type, desc, n, ka);
+  NUT_HIP(hipMemsetAsync(b, 0, o_base, st));
+  const uint64_t hblocks =
+      std::min<uint64_t>((n + 2 * RS_HIST_THREADS - 1) / (2 * RS_HIST_THREADS), (uint64_t)c->num_cus * 4);
+  hipLaunchKernelGGL(rs_hist_kernel, dim3((unsigned)hblocks), dim3(RS_HIST_THREADS), 0, st, (const int64_t *)ka, n,
+                     (uint64_t)0, hist);
+  hipLaunchKernelGGL(rs_scan_kernel, dim3(8), dim3(RS_BINS), 0, st, (const unsigned long long *)hist, n, base, triv);
+  NUT_HIP(hipGetLastError());
+  uint32_t htriv[8];
+  NUT_HIP(hipMemcpyAsync(htriv, triv, sizeof(htriv), hipMemcpyDeviceToHost, st));
+  NUT_HIP(hipStreamSynchronize(st));
+  int passes[8], np = 0;
+  for (int p = 0; p < 8; ++p)
+    if (!htriv[p]) passes[np++] = p;
+  if (np == 0) passes[np++] = 0;  // all keys equal: one (identity) pass still writes the payload
+  c->sort_bytes = 16 * n + 8 * n + 16 * n * (uint64_t)np;
+  c->sort_levels = (uint32_t)np;
+  // payload ping-pong so that the last pass writes vals_out; keys alternate A / B
+  const uint64_t *kin = ka, *vin = (const uint64_t *)vals;
+  for (int k = 0; k < np; ++k) {
+    uint64_t *kout = (k % 2 == 0) ? kb : ka;
+    uint64_t *vout = ((np - 1 - k) % 2 == 0) ? (uint64_t *)vals_out : vb;
+    uint64_t *status;
+    uint32_t epoch;
+    s = next_status(c, ntiles, &status, &epoch);
+    if (s) return s;
+    const int p = passes[k];
+    auto kern = k == 0 ? rs_pass_kernel<true, false, RadixDigit, true> : rs_pass_kernel<false, false, RadixDigit, true>;
+    hipLaunchKernelGGL(kern, dim3((unsigned)ntiles), dim3(RS_THREADS), 0, st, (const uint64_t *)kin, kout, n,
+                       RadixDigit{8 * p}, (const int64_t *)nullptr, RS_BINS, (uint64_t)0,
+                       (const uint64_t *)(base + p * RS_BINS), status, epoch, tickets + k, err,
+                       k == 0 ? (const uint64_t *)vals : vin, vout);
+    NUT_HIP(hipGetLastError());
+    kin = kout;
+    vin = vout;
+  }
+  c->timer.end(st);
+  NUT_HIP(hipMemcpyAsync(htriv, err, 4, hipMemcpyDeviceToHost, st));
+  NUT_HIP(hipStreamSynchronize(st));
+  if (htriv[0]) return fail(NUT_ERR_TIMEOUT, "nut_sort_pairs: look-back spin limit hit");
   return NUT_OK;
 }
 
@@ -451,7 +550,8 @@ extern "C" nut_status nut_partition_i64(nut_ctx *c, const int64_t *in, uint64_t 
   if (s) return s;
   hipLaunchKernelGGL((rs_pass_kernel<false, false, BucketDigit>), dim3((unsigned)ntiles), dim3(RS_THREADS), 0, st,
                      (const uint64_t *)in, (uint64_t *)out, n, dig, (const int64_t *)spl, nb, (uint64_t)0,
-                     (const uint64_t *)base, status, epoch, ticket, err);
+                     (const uint64_t *)base, status, epoch, ticket, err, (const uint64_t *)nullptr,
+                     (uint64_t *)nullptr);
   NUT_HIP(hipGetLastError());
   c->timer.end(st);
   uint32_t herr = 0;

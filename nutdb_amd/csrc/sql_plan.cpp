@@ -309,6 +309,10 @@ struct nut_plan {
   int proj = -1;                  // FILTER/SORT column (the first projected one)
   std::vector<int> projs;         // every projected column (expression-mode scans: several)
   bool desc = false;              // SORT direction
+  // SORT: the ORDER BY keys as (plan column, desc), most significant first.  One key equal
+  // to the only projected column: a keys-only sort; otherwise row ids are sorted by the
+  // keys (stable pair sorts, last key first) and every projected column gathered.
+  std::vector<std::pair<int, bool>> sort_keys;
   std::vector<int> keys, vals;    // GROUPBY key / value columns (indices into cols)
   std::vector<PlanAgg> aggs;
   std::vector<PlanOut> outs;
@@ -1191,9 +1195,22 @@ bool lower_mode(const Statement &st, nut_plan &p, Lowering &L) {
     p.outs.push_back(o);
   }
   p.proj = p.projs[0];
+  // ORDER BY keys: columns of the table, projected or not (an output alias names its column)
+  std::vector<std::pair<int, bool>> okeys;
+  if (b.order_by) {
+    for (const OrderKey &k : *b.order_by) {
+      sv oname;
+      if (!column_ref(p, k.e.e, oname)) return L.fail("ORDER BY '" + expr_text(k.e.e) + "' is not a column");
+      int ci = -1;
+      for (size_t j = 0; j < p.outs.size() && ci < 0; ++j)
+        if (ieq(oname, p.outs[j].name)) ci = p.projs[j];
+      okeys.push_back({ci >= 0 ? ci : col_index(p, oname), k.desc});
+    }
+  }
+  const bool keys_only = okeys.size() == 1 && p.projs.size() == 1 && okeys[0].first == p.proj;
   if (p.projs.size() > 1 && !p.compiled) return L.fail("a fused scan projects one column");
-  if (p.projs.size() > 1 && b.order_by)
-    return L.fail("ORDER BY with several projected columns is not executed (keys-only sort)");
+  if (!okeys.empty() && !keys_only && !p.compiled)
+    return L.fail("ORDER BY with other columns than the projected one runs in expression mode");
   // fused scans: one comparison of the projected column (nut_filter_i64); anything else
   // is an expression-mode scan (nut_select_rows, WHERE compiled for the query)
   for (const PlanPred &pr : p.preds) {
@@ -1202,13 +1219,9 @@ bool lower_mode(const Statement &st, nut_plan &p, Lowering &L) {
   }
   if (p.preds.size() > 1) return L.fail("a scan takes one comparison");
   if (b.order_by) {
-    if (b.order_by->size() != 1) return L.fail("ORDER BY takes one key");
-    const OrderKey &k = (*b.order_by)[0];
-    sv oname;
-    if (!column_ref(p, k.e.e, oname) || !(ieq(oname, p.cols[p.proj]) || ieq(oname, p.outs[0].name)))
-      return L.fail("ORDER BY must name the projected column");
     p.kind = NUT_PLAN_SORT;
-    p.desc = k.desc;
+    p.desc = okeys[0].second;
+    p.sort_keys = okeys;
   } else {
     p.kind = NUT_PLAN_FILTER;
   }
@@ -1358,7 +1371,17 @@ std::string describe(const nut_plan &p) {
       o += ']';
     }
   }
-  if (p.kind == NUT_PLAN_SORT) o += p.desc ? ",\"desc\":true" : ",\"desc\":false";
+  if (p.kind == NUT_PLAN_SORT) {
+    o += p.desc ? ",\"desc\":true" : ",\"desc\":false";
+    o += ",\"sort\":[";
+    for (size_t i = 0; i < p.sort_keys.size(); ++i) {
+      if (i) o += ',';
+      o += "{\"column\":";
+      json_str(o, p.cols[p.sort_keys[i].first]);
+      o += p.sort_keys[i].second ? ",\"desc\":true}" : ",\"desc\":false}";
+    }
+    o += ']';
+  }
   o += ",\"outputs\":[";
   for (size_t i = 0; i < p.outs.size(); ++i) {
     const PlanOut &u = p.outs[i];
@@ -1485,8 +1508,80 @@ nut_status build_spec(const nut_plan &p, const nut_column *const *bound, const D
 PProg and_all(const std::vector<PProg> &cs);
 PProg pred_prog(const PlanPred &pr);
 
+// ORDER BY with projected columns / several keys (SQL scans): the selected row ids are
+// sorted by the keys — one stable (key, row id) sort per key, the least significant
+// first (nut_sort_pairs) — and every projected column is gathered through them.
+nut_status exec_sort_rows(nut_ctx *c, const nut_plan &p, const nut_column *const *bound, const Dict *const *dicts,
+                          uint64_t n, nut_result *r) {
+  for (const auto &k : p.sort_keys) {
+    if (dicts && dicts[k.first])
+      return fail(NUT_ERR_PLAN, "ORDER BY string column '" + p.cols[k.first] + "' is not executed (dictionary codes "
+                                "are in first-seen order)");
+    if (bound[k.first]->type != NUT_T_I64 && bound[k.first]->type != NUT_T_F64)
+      return fail(NUT_ERR_PLAN, "ORDER BY column '" + p.cols[k.first] + "' must be int64 or float64");
+  }
+  for (size_t j = 0; j < p.projs.size(); ++j) {
+    r->names.push_back(p.outs[j].name);
+    r->types.push_back(dicts && dicts[p.projs[j]] ? NUT_T_STR : bound[p.projs[j]]->type);
+  }
+  uint64_t cnt = 0;
+  DevBuf rows, perm, keys;
+  if (!p.never && n) {
+    nut_agg_spec sp;
+    std::deque<std::vector<nut_prog_node>> store;
+    std::vector<int> agg_f64;
+    nut_status s = build_spec(p, bound, dicts, n, sp, store, agg_f64);
+    if (s) return s;
+    NUT_HIP(hipMalloc(&rows.p, n * 8));
+    s = nut_select_rows(c, &sp, (int64_t *)rows.p, &cnt);
+    if (s) return s;
+  }
+  const uint64_t m = std::max<uint64_t>(cnt, 1);
+  NUT_HIP(hipMalloc(&r->dev, m * 8 * p.projs.size()));
+  r->dev_stride = cnt;
+  if (cnt) {
+    NUT_HIP(hipMalloc(&perm.p, m * 8));
+    NUT_HIP(hipMalloc(&keys.p, m * 8));
+    nut_status s = NUT_OK;
+    for (size_t i = p.sort_keys.size(); i-- > 0 && !s;) {
+      const nut_column *kc = bound[p.sort_keys[i].first];
+      s = nut_gather_u64(c, (const uint64_t *)kc->data, (const int64_t *)rows.p, cnt, 0, (uint64_t *)keys.p);
+      if (!s) s = nut_sort_pairs(c, keys.p, kc->type, p.sort_keys[i].second ? 1 : 0, (const int64_t *)rows.p,
+                                 (int64_t *)perm.p, cnt);
+      std::swap(rows.p, perm.p);  // the sorted row ids feed the next (more significant) key
+    }
+    for (size_t j = 0; j < p.projs.size() && !s; ++j)
+      s = nut_gather_u64(c, (const uint64_t *)bound[p.projs[j]]->data, (const int64_t *)rows.p, cnt, 0,
+                         (uint64_t *)r->dev + j * cnt);
+    if (!s) s = nut_ctx_sync(c);
+    if (s) return s;
+  }
+  const uint64_t off = p.has_limit ? std::min(p.offset, cnt) : 0;
+  uint64_t nrows = cnt - off;
+  if (p.has_limit) nrows = std::min(nrows, p.limit);
+  r->dev_off = off;
+  r->nrows = nrows;
+  for (size_t j = 0; j < p.projs.size(); ++j) {  // decode string columns (codes -> text)
+    if (r->types[j] != NUT_T_STR) continue;
+    r->strs.resize(p.projs.size());
+    std::vector<int64_t> codes(nrows);
+    if (nrows) NUT_HIP(hipMemcpy(codes.data(), (const int64_t *)r->dev + j * r->dev_stride + off, nrows * 8,
+                                 hipMemcpyDeviceToHost));
+    const Dict *d = dicts[p.projs[j]];
+    r->strs[j].reserve(nrows);
+    for (int64_t cde : codes) {
+      const std::string *v = d->decode(cde);
+      r->strs[j].push_back(v ? *v : std::string());
+    }
+  }
+  return NUT_OK;
+}
+
 nut_status exec_scan(nut_ctx *c, const nut_plan &p, const nut_column *const *bound, const Dict *const *dicts,
                      uint64_t n, nut_result *r) {
+  if (p.kind == NUT_PLAN_SORT &&
+      !(p.sort_keys.size() == 1 && p.projs.size() == 1 && p.sort_keys[0].first == p.proj))
+    return exec_sort_rows(c, p, bound, dicts, n, r);
   const nut_column *col = bound[p.proj];
   if (!p.compiled && p.kind == NUT_PLAN_FILTER && dicts && dicts[p.proj]) {
     // a string column: rerun as an expression-mode scan (codes gathered, then decoded)

@@ -284,8 +284,14 @@ def test_plan_scan_several_columns():
     d = Plan("select a, b as bb, c from t where a > 1 or c < 0").describe()
     assert d["kind"] == "filter" and d["mode"] == "compiled" and d["project"] == ["a", "b", "c"]
     assert [o["name"] for o in d["outputs"]] == ["a", "bb", "c"]
-    with pytest.raises(NutError, match="several projected columns"):
-        Plan("select a, b from t where a > 1 order by a")
+    # ORDER BY with projected columns: row ids sorted by the keys, columns gathered
+    d = Plan("select a, b from t where a > 1 order by a").describe()
+    assert d["kind"] == "sort" and d["mode"] == "compiled" and d["sort"] == [{"column": "a", "desc": False}]
+    d = Plan("select a, b as bb from t order by bb desc, z").describe()
+    assert d["sort"] == [{"column": "b", "desc": True}, {"column": "z", "desc": False}]
+    assert d["project"] == ["a", "b"] and "z" in d["columns"]
+    with pytest.raises(NutError, match="is not a column"):
+        Plan("select a from t order by a + 1")
 
 
 def test_plan_select_distinct():
