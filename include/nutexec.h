@@ -163,7 +163,10 @@ typedef enum {
  *   BITAND BITOR BITXOR BITNOT SHL SHR  ints; shift counts outside [0, 63] give 0
  *            (SHR of a negative value: -1); SHR is arithmetic
  *   IF       pops cond, then, else: the chosen branch (only its errors count)
- *   ABS, TO_F64  one operand; bool operands count as int 0/1 in arithmetic */
+ *   ABS, TO_F64  one operand; bool operands count as int 0/1 in arithmetic
+ *   LOOKUP   one int operand x; v = device address of a byte table, arg = its length:
+ *            bool table[x] != 0 for 0 <= x < arg, else false (dictionary predicates such
+ *            as LIKE over dictionary codes; the table must outlive the call) */
 typedef enum {
   NUT_P_COL = 0, NUT_P_I64 = 1, NUT_P_F64 = 2,
   NUT_P_ADD = 3, NUT_P_SUB = 4, NUT_P_MUL = 5, NUT_P_DIV = 6, NUT_P_MOD = 7, NUT_P_INTDIV = 8,
@@ -171,13 +174,13 @@ typedef enum {
   NUT_P_AND = 15, NUT_P_OR = 16, NUT_P_XOR = 17, NUT_P_NOT = 18,
   NUT_P_BITAND = 19, NUT_P_BITOR = 20, NUT_P_BITXOR = 21, NUT_P_BITNOT = 22,
   NUT_P_SHL = 23, NUT_P_SHR = 24,
-  NUT_P_IF = 25, NUT_P_ABS = 26, NUT_P_TO_F64 = 27
+  NUT_P_IF = 25, NUT_P_ABS = 26, NUT_P_TO_F64 = 27, NUT_P_LOOKUP = 28
 } nut_prog_op;
 typedef enum { NUT_PT_I64 = 0, NUT_PT_F64 = 1, NUT_PT_BOOL = 2 } nut_prog_value_type;
 typedef struct {
   int32_t op;   /* nut_prog_op */
-  int32_t arg;  /* NUT_P_COL: column index */
-  int64_t v;    /* NUT_P_I64 / NUT_P_F64 constant */
+  int32_t arg;  /* NUT_P_COL: column index; NUT_P_LOOKUP: table length */
+  int64_t v;    /* NUT_P_I64 / NUT_P_F64 constant; NUT_P_LOOKUP: table address */
 } nut_prog_node;
 typedef struct {
   int32_t n;                  /* 0..NUT_MAX_PROG_NODES */
@@ -347,7 +350,8 @@ nut_status nut_select_jit_compile(const nut_agg_spec *s);
 nut_status nut_hash_partition_i64(nut_ctx *ctx, const int64_t *keys, uint64_t n, int nparts, int64_t row0,
                                   int64_t *out_keys, int64_t *out_rows, uint64_t *counts_host);
 /* out[i] = src[idx[i]] (8-byte words), or `null_bits` where idx[i] < 0: carries any
- * int64 / f64 column through a join index */
+ * int64 / f64 column through a join index.  out may be idx itself (in place); it must
+ * not overlap src. */
 nut_status nut_gather_u64(nut_ctx *ctx, const uint64_t *src, const int64_t *idx, uint64_t n, uint64_t null_bits,
                           uint64_t *out);
 
@@ -563,6 +567,12 @@ nut_status nut_table_execute(nut_ctx *ctx, nut_table *t, const nut_plan *plan, u
  * semantics).  String columns travel through the join as codes of their own table's
  * dictionary and decode on output; JOIN keys must be integer columns. */
 nut_status nut_table_execute2(nut_ctx *ctx, nut_table *left, nut_table *right, const nut_plan *plan,
+                              uint64_t group_hint, nut_result **out);
+/* A chain of INNER joins over typed tables (tables[0] = FROM, tables[k] = the k-th JOIN
+ * source; nut_plan_executen semantics).  Strings as in nut_table_execute2: filters
+ * (= / != / IN / LIKE), GROUP BY keys and projections use each column's own dictionary;
+ * JOIN keys must be integer columns. */
+nut_status nut_table_executen(nut_ctx *ctx, nut_table *const *tables, int ntables, const nut_plan *plan,
                               uint64_t group_hint, nut_result **out);
 void nut_table_free(nut_table *t);
 

@@ -44,7 +44,7 @@ AGG_SUM, AGG_COUNT, AGG_MIN, AGG_MAX = range(4)
 EX_COL, EX_MUL, EX_ADD, EX_SUB, EX_MUL_1M, EX_MUL_1M_1P = range(6)
 # nut_prog_op (expression programs, RPN) and nut_prog_value_type
 PROG_OPS = ["col", "i64", "f64", "add", "sub", "mul", "div", "mod", "intdiv", "lt", "le", "gt", "ge", "eq", "ne",
-            "and", "or", "xor", "not", "bitand", "bitor", "bitxor", "bitnot", "shl", "shr", "if", "abs", "to_f64"]
+            "and", "or", "xor", "not", "bitand", "bitor", "bitxor", "bitnot", "shl", "shr", "if", "abs", "to_f64", "lookup"]
 P = {name: i for i, name in enumerate(PROG_OPS)}
 PT_I64, PT_F64, PT_BOOL = 0, 1, 2
 
@@ -152,6 +152,7 @@ SIGNATURES = {
     "nut_table_append": (_I32, [_P, _P, _I32, _P, _P, _U64]),
     "nut_table_execute": (_I32, [_P, _P, _P, _U64, C.POINTER(_P)]),
     "nut_table_execute2": (_I32, [_P, _P, _P, _P, _U64, C.POINTER(_P)]),
+    "nut_table_executen": (_I32, [_P, C.POINTER(_P), _I32, _P, _U64, C.POINTER(_P)]),
     "nut_table_free": (None, [_P]),
     "nut_groups_size": (_I32, [_P, C.POINTER(_U64)]),
     "nut_groups_to_host": (_I32, [_P, _P, _P, _U64]),

@@ -75,8 +75,9 @@ struct Gen {
       PVal a[3];
       const int op = nd.op;
       const int arity = op <= NUT_P_F64 ? 0 : (op == NUT_P_NOT || op == NUT_P_BITNOT || op == NUT_P_ABS ||
-                                                op == NUT_P_TO_F64) ? 1 : op == NUT_P_IF ? 3 : 2;
-      if (op < 0 || op > NUT_P_TO_F64) return fail("unknown program op " + std::to_string(op));
+                                                op == NUT_P_TO_F64 || op == NUT_P_LOOKUP) ? 1
+                                                                                         : op == NUT_P_IF ? 3 : 2;
+      if (op < 0 || op > NUT_P_LOOKUP) return fail("unknown program op " + std::to_string(op));
       if (!pop(arity, a)) return fail("program stack underflow at node " + std::to_string(i));
       PVal r;
       const bool f = arity == 2 && (a[0].t == NUT_PT_F64 || a[1].t == NUT_PT_F64);
@@ -161,6 +162,13 @@ struct Gen {
                                    : PVal{NUT_PT_I64, "jabs(" + as_i(a[0]) + ")"};
           break;
         case NUT_P_TO_F64: r = {NUT_PT_F64, as_f(a[0])}; break;
+        case NUT_P_LOOKUP:
+          if (a[0].t == NUT_PT_F64) return fail("LOOKUP needs an integer operand");
+          if (nd.arg < 0) return fail("LOOKUP table length is negative");
+          if (nd.arg > 0 && nd.v == 0) return fail("LOOKUP table has no address");
+          r = {NUT_PT_BOOL, "jlookup(" + as_i(a[0]) + ", " + konst((uint64_t)nd.v) + ", " +
+                                konst((uint64_t)(int64_t)nd.arg) + ")"};
+          break;
       }
       if (r.s.size() > (1u << 20)) return fail("expression program too large");
       st.push_back(std::move(r));
@@ -197,6 +205,11 @@ __device__ __forceinline__ int64_t jshr(int64_t a, int64_t b) {
   return (b >= 0 && b < 64) ? (a >> b) : (a < 0 ? -1 : 0);
 }
 __device__ __forceinline__ int64_t jabs(int64_t a) { return a < 0 ? (int64_t)(0 - (uint64_t)a) : a; }
+// byte-table membership; an empty table (n == 0) is never read
+__device__ __forceinline__ bool jlookup(int64_t x, uint64_t t, uint64_t n) {
+  if ((uint64_t)x >= n) return false;
+  return ((const uint8_t *)t)[x] != 0;
+}
 )";
 
 std::string bits_of(const PVal &v) {

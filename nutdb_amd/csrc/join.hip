@@ -355,8 +355,10 @@ nut_status join_matched(nut_ctx *c, const int64_t *bi, uint64_t n, int64_t *out)
   return NUT_OK;
 }
 
-__global__ void gather_u64_kernel(const uint64_t *__restrict__ src, const int64_t *__restrict__ idx, uint64_t n,
-                                  uint64_t null_bits, uint64_t *__restrict__ out) {
+// out may be idx itself (each lane reads idx[i] before writing out[i]), so neither is
+// __restrict__; src must not overlap out
+__global__ void gather_u64_kernel(const uint64_t *__restrict__ src, const int64_t *idx, uint64_t n,
+                                  uint64_t null_bits, uint64_t *out) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     const int64_t j = idx[i];
     out[i] = j < 0 ? null_bits : src[j];

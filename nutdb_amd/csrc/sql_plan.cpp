@@ -352,7 +352,7 @@ struct nut_result {
 namespace {
 
 // internal program leaves (never reach nut_prog): `col [I]LIKE 'pattern'` over a
-// dictionary column, expanded at execution into equalities with the matching strings
+// dictionary column, lowered at execution to COL + LOOKUP in a per-code match table
 constexpr int P_LIKE = 1000, P_ILIKE = 1001;
 
 int pnode_arity(int op) {
@@ -361,8 +361,15 @@ int pnode_arity(int op) {
                                 op == NUT_P_TO_F64) ? 1 : op == NUT_P_IF ? 3 : 2;
 }
 
-// SQL LIKE: % any run, _ any one byte, backslash escapes the next pattern byte;
-// ILIKE folds ASCII case
+// bytes of the UTF-8 sequence starting at s[i] (a stray continuation byte counts alone)
+size_t u8len(const std::string &s, size_t i) {
+  const unsigned char c = (unsigned char)s[i];
+  const size_t n = c < 0x80 ? 1 : (c >> 5) == 6 ? 2 : (c >> 4) == 14 ? 3 : (c >> 3) == 30 ? 4 : 1;
+  return std::min(n, s.size() - i);
+}
+
+// SQL LIKE: % any run, _ any one character (UTF-8 code point), backslash escapes the next
+// pattern character; ILIKE folds ASCII case (other code points compare exactly)
 bool like_match(const std::string &str, const std::string &pat, bool ci) {
   auto eq = [&](char a, char b) {
     if (ci) {
@@ -380,16 +387,24 @@ bool like_match(const std::string &str, const std::string &pat, bool ci) {
     }
     if (p < pat.size()) {
       const bool esc = pat[p] == '\\' && p + 1 < pat.size();
-      const char pc = esc ? pat[p + 1] : pat[p];
-      if ((!esc && pc == '_') || eq(pc, str[s])) {
-        p += esc ? 2 : 1;
-        ++s;
+      if (!esc && pat[p] == '_') {
+        ++p;
+        s += u8len(str, s);
+        continue;
+      }
+      const size_t pp = esc ? p + 1 : p, pl = u8len(pat, pp), sl = u8len(str, s);
+      bool same = pl == sl;
+      for (size_t k = 0; same && k < pl; ++k) same = eq(pat[pp + k], str[s + k]);
+      if (same) {
+        p = pp + pl;
+        s += sl;
         continue;
       }
     }
     if (star_p == std::string::npos) return false;
     p = star_p;
-    s = ++star_s;
+    star_s += u8len(str, star_s);
+    s = star_s;
   }
   while (p < pat.size() && pat[p] == '%') ++p;
   return p == pat.size();
@@ -1498,13 +1513,22 @@ const nut_column *bind(const nut_plan &p, int ci, const nut_column *cols, int nc
 
 struct DevBuf {
   void *p = nullptr;
+  DevBuf() = default;
+  DevBuf(const DevBuf &) = delete;
+  DevBuf &operator=(const DevBuf &) = delete;
   ~DevBuf() {
     if (p) (void)hipFree(p);
   }
 };
 
+// what the programs of one nut_agg_spec point at: node arrays and LOOKUP tables (device)
+struct ProgStore {
+  std::deque<std::vector<nut_prog_node>> nodes;
+  std::deque<DevBuf> tables;
+};
+
 nut_status build_spec(const nut_plan &p, const nut_column *const *bound, const Dict *const *dicts, uint64_t n,
-                      nut_agg_spec &s, std::deque<std::vector<nut_prog_node>> &store, std::vector<int> &agg_f64);
+                      nut_agg_spec &s, ProgStore &store, std::vector<int> &agg_f64);
 PProg and_all(const std::vector<PProg> &cs);
 PProg pred_prog(const PlanPred &pr);
 
@@ -1528,7 +1552,7 @@ nut_status exec_sort_rows(nut_ctx *c, const nut_plan &p, const nut_column *const
   DevBuf rows, perm, keys;
   if (!p.never && n) {
     nut_agg_spec sp;
-    std::deque<std::vector<nut_prog_node>> store;
+    ProgStore store;
     std::vector<int> agg_f64;
     nut_status s = build_spec(p, bound, dicts, n, sp, store, agg_f64);
     if (s) return s;
@@ -1624,7 +1648,7 @@ nut_status exec_scan(nut_ctx *c, const nut_plan &p, const nut_column *const *bou
     // expression-mode scan: row ids where the WHERE program holds, then the projected
     // column gathered through them (ascending ids), then sorted for ORDER BY
     nut_agg_spec sp;
-    std::deque<std::vector<nut_prog_node>> store;
+    ProgStore store;
     std::vector<int> agg_f64;
     nut_status s = build_spec(p, bound, dicts, n, sp, store, agg_f64);
     if (s) return s;
@@ -1770,7 +1794,7 @@ nut_status check_strings(const nut_plan &p, const PProg &pp, const Dict *const *
 }
 
 nut_status build_spec(const nut_plan &p, const nut_column *const *bound, const Dict *const *dicts, uint64_t n,
-                      nut_agg_spec &s, std::deque<std::vector<nut_prog_node>> &store, std::vector<int> &agg_f64) {
+                      nut_agg_spec &s, ProgStore &store, std::vector<int> &agg_f64) {
   memset(&s, 0, sizeof s);
   s.n = p.never ? 0 : n;
   s.nkeys = (int32_t)p.keys.size();
@@ -1784,67 +1808,83 @@ nut_status build_spec(const nut_plan &p, const nut_column *const *bound, const D
     // expression mode: bind the programs' columns (first use order) and constants
     s.prog_mode = 1;
     std::vector<int> pcol(p.cols.size(), -1);
-    std::deque<PProg> expanded;
-    auto resolve = [&](const PProg &pp0, nut_prog &out, const char *what, int32_t *type) -> nut_status {
-      // [I]LIKE over a dictionary column -> OR of equalities with the matching strings
-      expanded.emplace_back();
-      PProg &pp = expanded.back();
-      for (const PNode &n : pp0) {
-        if (n.op != P_LIKE && n.op != P_ILIKE) {
-          pp.push_back(n);
-          continue;
-        }
-        PNode zero;
-        zero.op = NUT_P_I64;
-        zero.c.is_int = true;
-        zero.c.v = 0;
-        std::vector<std::string> hits;
-        if (dicts) {
-          const Dict *d = dicts[n.col];
-          if (!d) return fail(NUT_ERR_PLAN, "LIKE needs a string column ('" + p.cols[n.col] + "')");
-          auto test = [&](const std::string &v) {
-            if (like_match(v, n.c.s, n.op == P_ILIKE)) hits.push_back(v);
-          };
-          if (d->fixed) {
-            for (const auto &kv : d->codes) test(kv.first);
-          } else {
-            for (const std::string &v : d->strs) test(v);
-          }
-          if (hits.size() > 48)
-            return fail(NUT_ERR_PLAN, "LIKE " + cval_str(n.c) + " matches " + std::to_string(hits.size()) +
-                                          " strings of '" + p.cols[n.col] + "' (at most 48)");
-        }
-        if (hits.empty()) {  // false (also the compile-only shape of nut_plan_prepare)
-          pp.push_back(zero);
-          pp.push_back(zero);
-          PNode ne;
-          ne.op = NUT_P_NE;
-          pp.push_back(ne);
-          continue;
-        }
-        for (size_t h = 0; h < hits.size(); ++h) {
-          PNode col, k, eqn;
-          col.op = NUT_P_COL;
-          col.col = n.col;
-          k.op = NUT_P_I64;
-          k.col = n.col;
-          k.c.is_str = true;
-          k.c.s = hits[h];
-          eqn.op = NUT_P_EQ;
-          pp.push_back(col);
-          pp.push_back(k);
-          pp.push_back(eqn);
-          if (h) {
-            PNode orn;
-            orn.op = NUT_P_OR;
-            pp.push_back(orn);
-          }
-        }
+    auto bind_col = [&](int ci, int32_t &arg) -> nut_status {
+      if (pcol[ci] < 0) {
+        if (s.nprog_cols >= NUT_MAX_PROG_COLS) return fail(NUT_ERR_PLAN, "expressions read more than 16 columns");
+        pcol[ci] = s.nprog_cols;
+        s.prog_col[s.nprog_cols] = bound[ci]->data;
+        s.prog_col_type[s.nprog_cols] = bound[ci]->type;
+        s.nprog_cols++;
       }
-      store.emplace_back();
-      std::vector<nut_prog_node> &v = store.back();
+      arg = pcol[ci];
+      return NUT_OK;
+    };
+    // [I]LIKE over a dictionary column: COL, LOOKUP in a per-code byte table of the
+    // dictionary strings the pattern matches (any number of them); an Enum whose codes do
+    // not index a table compactly ORs equalities with the matching codes instead
+    auto lower_like = [&](const PNode &n, std::vector<nut_prog_node> &v) -> nut_status {
+      nut_prog_node col{NUT_P_COL, 0, 0};
+      nut_status bs = bind_col(n.col, col.arg);
+      if (bs) return bs;
+      v.push_back(col);
+      if (!dicts) {  // compile-only shape (nut_plan_prepare): an empty table
+        v.push_back(nut_prog_node{NUT_P_LOOKUP, 0, 0});
+        return NUT_OK;
+      }
+      const Dict *d = dicts[n.col];
+      if (!d) return fail(NUT_ERR_PLAN, "LIKE needs a string column ('" + p.cols[n.col] + "')");
+      const bool ci = n.op == P_ILIKE;
+      std::vector<uint8_t> table;
+      if (d->fixed) {
+        int64_t lo = 0, hi = -1;
+        for (const auto &kv : d->codes) {
+          lo = std::min(lo, kv.second);
+          hi = std::max(hi, kv.second);
+        }
+        if (lo < 0 || hi >= (1 << 24)) {
+          size_t hits = 0;
+          for (const auto &kv : d->codes) {
+            if (!like_match(kv.first, n.c.s, ci)) continue;
+            if (hits) v.push_back(col);
+            v.push_back(nut_prog_node{NUT_P_I64, 0, kv.second});
+            v.push_back(nut_prog_node{NUT_P_EQ, 0, 0});
+            if (hits++) v.push_back(nut_prog_node{NUT_P_OR, 0, 0});
+            if (v.size() > NUT_MAX_PROG_NODES)
+              return fail(NUT_ERR_PLAN, "LIKE " + cval_str(n.c) + " over Enum column '" + p.cols[n.col] +
+                                            "' (codes outside [0, 2^24)) matches too many values for one program");
+          }
+          if (!hits) v.push_back(nut_prog_node{NUT_P_LOOKUP, 0, 0});  // false
+          return NUT_OK;
+        }
+        table.assign((size_t)(hi + 1), 0);
+        for (const auto &kv : d->codes) table[(size_t)kv.second] = like_match(kv.first, n.c.s, ci);
+      } else {
+        if (d->strs.size() > (size_t)INT32_MAX)
+          return fail(NUT_ERR_PLAN, "LIKE over a dictionary of more than 2^31 strings");
+        table.resize(d->strs.size());
+        for (size_t i = 0; i < d->strs.size(); ++i) table[i] = like_match(d->strs[i], n.c.s, ci);
+      }
+      nut_prog_node lk{NUT_P_LOOKUP, (int32_t)table.size(), 0};
+      if (!table.empty()) {
+        store.tables.emplace_back();
+        DevBuf &t = store.tables.back();
+        NUT_HIP(hipMalloc(&t.p, table.size()));
+        NUT_HIP(hipMemcpy(t.p, table.data(), table.size(), hipMemcpyHostToDevice));
+        lk.v = (int64_t)(uintptr_t)t.p;
+      }
+      v.push_back(lk);
+      return NUT_OK;
+    };
+    auto resolve = [&](const PProg &pp, nut_prog &out, const char *what, int32_t *type) -> nut_status {
+      store.nodes.emplace_back();
+      std::vector<nut_prog_node> &v = store.nodes.back();
       for (const PNode &n : pp) {
         nut_prog_node q{n.op, 0, 0};
+        if (n.op == P_LIKE || n.op == P_ILIKE) {
+          nut_status ls = lower_like(n, v);
+          if (ls) return ls;
+          continue;
+        }
         if (n.op == NUT_P_COL) {
           if (pcol[n.col] < 0) {
             if (s.nprog_cols >= NUT_MAX_PROG_COLS) return fail(NUT_ERR_PLAN, "expressions read more than 16 columns");
@@ -2020,7 +2060,7 @@ nut_status build_spec(const nut_plan &p, const nut_column *const *bound, const D
 nut_status exec_groupby(nut_ctx *c, const nut_plan &p, const nut_column *const *bound, const Dict *const *dicts,
                         uint64_t n, uint64_t hint, nut_result *r) {
   nut_agg_spec s;
-  std::deque<std::vector<nut_prog_node>> store;  // program nodes, alive until nut_groupby returns
+  ProgStore store;  // program nodes, alive until nut_groupby returns
   std::vector<int> agg_f64;
   nut_status bs = build_spec(p, bound, dicts, n, s, store, agg_f64);
   if (bs) return bs;
@@ -2341,7 +2381,7 @@ nut_status exec_join(nut_ctx *c, const nut_plan &p, const nut_column *lc, int nl
     q.cols = p.cols;
     q.where = and_all(push[sd]);
     nut_agg_spec spec;
-    std::deque<std::vector<nut_prog_node>> store;
+    ProgStore store;
     std::vector<int> agg_f64;
     nut_status es = build_spec(q, src.data(), sdict.data(), rows_s[sd], spec, store, agg_f64);
     if (es) return es;
@@ -2447,8 +2487,11 @@ namespace {
 // A chain of INNER joins (nut_plan_executen): FROM t0 JOIN t1 ON .. JOIN t2 ON ..  Single-
 // table WHERE conjuncts are pushed down per table; the accumulated join result is kept as
 // one row-id array per joined table (the probe side); each step builds on the next table.
+// tdicts (typed tables, nut_table_executen): per table, the dictionary of each column
+// (NULL = numeric); string columns filter, group and project with their own table's codes.
 nut_status exec_joinn(nut_ctx *c, const nut_plan &p, const nut_column *const *tabs, const int *ncols,
-                      const uint64_t *nrows, int nt, uint64_t hint, nut_result *r) {
+                      const uint64_t *nrows, int nt, uint64_t hint, nut_result *r,
+                      const Dict *const *const *tdicts = nullptr) {
   const size_t nc = p.cols.size();
   if (nt != (int)p.jn.size() + 1)
     return fail(NUT_ERR_INVALID_ARG, "nut_plan_executen: the plan joins " + std::to_string(p.jn.size() + 1) +
@@ -2464,6 +2507,7 @@ nut_status exec_joinn(nut_ctx *c, const nut_plan &p, const nut_column *const *ta
   };
   std::vector<int> side(nc);
   std::vector<const nut_column *> src(nc);
+  std::vector<const Dict *> sdict(nc + 1, nullptr);
   for (size_t i = 0; i < nc; ++i) {
     const std::string &nm = p.cols[i];
     int hit = -1, nh = 0;
@@ -2487,6 +2531,7 @@ nut_status exec_joinn(nut_ctx *c, const nut_plan &p, const nut_column *const *ta
     if (nrows[hit] && !col->data) return fail(NUT_ERR_INVALID_ARG, "nut_plan_executen: column '" + nm + "' is NULL");
     side[i] = hit;
     src[i] = col;
+    if (tdicts && tdicts[hit]) sdict[i] = tdicts[hit][col - tabs[hit]];
   }
   std::vector<int> knew(nt - 1), kold(nt - 1);
   for (int k = 0; k + 1 < nt; ++k) {
@@ -2496,6 +2541,9 @@ nut_status exec_joinn(nut_ctx *c, const nut_plan &p, const nut_column *const *ta
     else return fail(NUT_ERR_PLAN, "JOIN " + std::to_string(t) + ": ON must compare a column of '" + tname[t] +
                                        "' with a column of an earlier table");
     if (src[a]->type != NUT_T_I64 || src[b]->type != NUT_T_I64) return fail(NUT_ERR_PLAN, "JOIN keys must be int64 columns");
+    if (sdict[a] || sdict[b])  // codes of two dictionaries do not compare
+      return fail(NUT_ERR_PLAN, "JOIN " + std::to_string(t) + ": string keys are not executed (each table has its own "
+                                    "dictionary)");
   }
   nut_plan p2 = p;
   std::vector<std::vector<PProg>> push(nt);
@@ -2513,7 +2561,6 @@ nut_status exec_joinn(nut_ctx *c, const nut_plan &p, const nut_column *const *ta
     p2.preds.clear();
     for (const PlanPred &pr : p.preds) push[side[pr.col]].push_back(pred_prog(pr));
   }
-  const std::vector<const Dict *> nodict(nc + 1, nullptr);
   std::vector<DevBuf> ids(nt);
   std::vector<uint64_t> rows(nrows, nrows + nt);
   for (int t = 0; t < nt; ++t) {
@@ -2523,9 +2570,9 @@ nut_status exec_joinn(nut_ctx *c, const nut_plan &p, const nut_column *const *ta
     q.cols = p.cols;
     q.where = and_all(push[t]);
     nut_agg_spec spec;
-    std::deque<std::vector<nut_prog_node>> store;
+    ProgStore store;
     std::vector<int> agg_f64;
-    nut_status es = build_spec(q, src.data(), nodict.data(), rows[t], spec, store, agg_f64);
+    nut_status es = build_spec(q, src.data(), sdict.data(), rows[t], spec, store, agg_f64);
     if (es) return es;
     NUT_HIP(hipMalloc(&ids[t].p, std::max<uint64_t>(rows[t], 1) * 8));
     uint64_t cnt = 0;
@@ -2615,8 +2662,8 @@ nut_status exec_joinn(nut_ctx *c, const nut_plan &p, const nut_column *const *ta
   }
   std::vector<const nut_column *> bound(nc);
   for (size_t i = 0; i < nc; ++i) bound[i] = &jc[i];
-  st = p2.kind == NUT_PLAN_GROUPBY ? exec_groupby(c, p2, bound.data(), nodict.data(), ncur, hint, r)
-                                   : exec_scan(c, p2, bound.data(), nodict.data(), ncur, r);
+  st = p2.kind == NUT_PLAN_GROUPBY ? exec_groupby(c, p2, bound.data(), sdict.data(), ncur, hint, r)
+                                   : exec_scan(c, p2, bound.data(), sdict.data(), ncur, r);
   NUT_HIP(hipStreamSynchronize(c->stream));
   return st;
 }
@@ -2804,7 +2851,7 @@ nut_status nut_plan_prepare(const nut_plan *p, const nut_column *cols, int ncols
       return fail(NUT_ERR_INVALID_ARG, "nut_plan_prepare: column '" + p->cols[i] + "' has an unknown type");
   }
   nut_agg_spec s;
-  std::deque<std::vector<nut_prog_node>> store;
+  ProgStore store;
   std::vector<int> agg_f64;
   nut_status st = build_spec(*p, bound.data(), nullptr, 0, s, store, agg_f64);
   if (st) return st;
@@ -2870,6 +2917,51 @@ nut_status nut_table_execute2(nut_ctx *c, nut_table *left, nut_table *right, con
   DeviceGuard g(c->device);
   nut_status st = exec_join(c, *p, cols[0].data(), (int)cols[0].size(), left->rows(), cols[1].data(),
                             (int)cols[1].size(), right->rows(), group_hint, r, dicts[0].data(), dicts[1].data());
+  if (st) {
+    nut_result_free(r);
+    return st;
+  }
+  *out = r;
+  return NUT_OK;
+}
+
+nut_status nut_table_executen(nut_ctx *c, nut_table *const *tables, int ntables, const nut_plan *p,
+                              uint64_t group_hint, nut_result **out) {
+  if (!c || !tables || ntables < 1 || !p || !out) return fail(NUT_ERR_INVALID_ARG, "nut_table_executen: NULL argument");
+  for (int k = 0; k < ntables; ++k)
+    if (!tables[k]) return fail(NUT_ERR_INVALID_ARG, "nut_table_executen: NULL table");
+  if (p->jn.empty()) {
+    if (ntables == 1) return nut_table_execute(c, tables[0], p, group_hint, out);
+    if (ntables == 2) return nut_table_execute2(c, tables[0], tables[1], p, group_hint, out);
+    return fail(NUT_ERR_INVALID_ARG, "nut_table_executen: the plan joins fewer tables");
+  }
+  *out = nullptr;
+  std::vector<std::vector<nut_column>> cols(ntables);
+  std::vector<std::vector<const Dict *>> dicts(ntables);
+  std::vector<const nut_column *> tabs(ntables);
+  std::vector<const Dict *const *> tdicts(ntables);
+  std::vector<int> ncols(ntables);
+  std::vector<uint64_t> nrows(ntables);
+  for (int k = 0; k < ntables; ++k) {
+    nut_table *t = tables[k];
+    if (t->ragged()) return fail(NUT_ERR_INVALID_ARG, "nut_table_executen: table '" + t->name + "' has ragged columns");
+    if (t->device >= 0 && t->device != c->device)
+      return fail(NUT_ERR_INVALID_ARG, "nut_table_executen: table '" + t->name + "' lives on another device");
+    for (const TCol &x : t->cols) {
+      cols[k].push_back(nut_column{x.name.c_str(), x.dev, x.exec_type});
+      dicts[k].push_back(x.dict);
+    }
+    tabs[k] = cols[k].data();
+    tdicts[k] = dicts[k].data();
+    ncols[k] = (int)cols[k].size();
+    nrows[k] = t->rows();
+  }
+  nut_result *r = new (std::nothrow) nut_result;
+  if (!r) return fail(NUT_ERR_OOM, "nut_table_executen: out of host memory");
+  r->kind = p->kind;
+  r->device = c->device;
+  DeviceGuard g(c->device);
+  nut_status st = exec_joinn(c, *p, tabs.data(), ncols.data(), nrows.data(), ntables, group_hint, r, tdicts.data());
   if (st) {
     nut_result_free(r);
     return st;

@@ -12,7 +12,7 @@ to codes; string group keys come back as str).
 from __future__ import annotations
 
 import ctypes as C
-from typing import Dict
+from typing import Dict, List
 
 import numpy as np
 
@@ -88,7 +88,20 @@ class Table:
               "nut_table_execute2")
         return read_result(res)
 
-    def sql(self, query: str, group_hint: int = 0, right: "Table" = None) -> Dict[str, np.ndarray]:
+    def execute_joins(self, plan: Plan, joined: List["Table"], group_hint: int = 0) -> Dict[str, np.ndarray]:
+        """A chain of JOINs with this table as FROM and `joined[k]` as the k-th JOIN source
+        (nut_table_executen), strings as in execute_join."""
+        res = C.c_void_p()
+        self.ex._bind_stream()
+        hs = (C.c_void_p * (len(joined) + 1))(self._h, *[t._h for t in joined])
+        check(lib.nut_table_executen(self.ex.ctx, hs, len(joined) + 1, plan._handle(), group_hint, C.byref(res)),
+              "nut_table_executen")
+        return read_result(res)
+
+    def sql(self, query: str, group_hint: int = 0, right: "Table" = None,
+            joined: List["Table"] = None) -> Dict[str, np.ndarray]:
+        if joined is not None:
+            return self.execute_joins(Plan(query), joined, group_hint)
         if right is not None:
             return self.execute_join(Plan(query), right, group_hint)
         return self.execute(Plan(query), group_hint)

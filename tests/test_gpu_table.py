@@ -243,8 +243,8 @@ def _like(v, pat, ci=False):
 
 
 def test_like_on_dictionary_columns(ex):
-    """[NOT] [I]LIKE over String / Enum columns: evaluated once per dictionary string (the
-    matching codes become equalities), in scans, aggregates and joins' pushed WHERE."""
+    """[NOT] [I]LIKE over String / Enum columns: evaluated once per dictionary string (a
+    per-code match table), in scans, aggregates and joins' pushed WHERE."""
     rng = np.random.default_rng(43)
     n = 200_003
     types = np.array(["STANDARD POLISHED BRASS", "SMALL BRUSHED TIN", "LARGE PLATED BRASS", "ECONOMY ANODIZED STEEL",
@@ -292,3 +292,84 @@ def test_like_through_a_join(ex):
         got = li.sql(f"select count(*) as c, sum(l_qty) as s from lineitem join part on l_part = p_key where {where}",
                      right=part)
         assert got["c"].tolist() == [int(m.sum())] and got["s"].tolist() == [int(qty[m].sum())], where
+
+
+def test_like_large_dictionaries(ex):
+    """LIKE is a per-code byte table over the dictionary (nut_prog LOOKUP): thousands of
+    matching strings, two LIKEs in one program, `_` as one UTF-8 character, and an Enum
+    whose ids are too sparse for a table (ORed equalities)."""
+    rng = np.random.default_rng(53)
+    n = 300_007
+    words = np.array([f"W{i:05d}-{'é' if i % 3 == 0 else 'e'}nd" for i in range(6000)], dtype=object)
+    w = words[rng.integers(0, len(words), n)]
+    x = rng.integers(0, 100, n)
+    big = np.array(["lo", "hi", "mid"], dtype=object)[rng.integers(0, 3, n)]
+    t = Table(ex, "CREATE TABLE t (w String, x Int64, e Enum('lo' = 7, 'hi' = 100000000, 'mid' = 4000000000))")
+    t.append(w=w, x=x, e=big)
+    cases = [
+        ("w like 'W0%'", np.array([v.startswith("W0") for v in w])),  # ~4000 matching strings
+        ("w like '%_nd' and w not like 'W1%'", np.array([not v.startswith("W1") for v in w])),
+        ("w like 'W____0-_nd'", np.array([_like(v, "W____0-_nd") for v in w])),  # é is one `_`
+        ("w like '%é%' or x < 3", np.array(["é" in v for v in w]) | (x < 3)),
+        ("e like '%i%'", (big == "hi") | (big == "mid")),
+        ("e like 'l_'", big == "lo"),
+        ("e like 'zz%'", np.zeros(n, bool)),
+    ]
+    for where, m in cases:
+        assert m.any() or "zz" in where
+        got = t.sql(f"select count(*) as c, sum(x) as s from t where {where}")
+        assert got["c"].tolist() == [int(m.sum())] and got["s"].tolist() == [int(x[m].sum())], where
+    got = t.sql("select x from t where w like 'W00___-é%' limit 100000")
+    m = np.array([_like(v, "W00___-é%") for v in w])
+    assert m.sum() > 0 and got["x"].tolist() == x[m].tolist()
+
+
+def test_join_chain_typed_tables(ex):
+    """lineitem JOIN orders JOIN customer over typed tables (nut_table_executen): LIKE /
+    IN / = on the strings of every table, string GROUP BY keys and string projections
+    decoded from their own table's dictionary; string JOIN keys are rejected."""
+    rng = np.random.default_rng(61)
+    nc, no, nl = 2000, 20_000, 100_003
+    segs = np.array(["AUTOMOBILE", "BUILDING", "FURNITURE", "HOUSEHOLD", "MACHINERY"], dtype=object)
+    prios = np.array(["1-URGENT", "2-HIGH", "3-MEDIUM", "4-NOT SPECIFIED", "5-LOW"], dtype=object)
+    modes = np.array(["MAIL", "SHIP", "AIR", "RAIL", "TRUCK"], dtype=object)
+    ckey = rng.permutation(nc).astype(np.int64) + 10
+    seg = segs[rng.integers(0, len(segs), nc)]
+    okey = rng.permutation(no).astype(np.int64) * 3
+    ocust = ckey[rng.integers(0, nc, no)]
+    ocust[:50] = -5  # no customer
+    prio = prios[rng.integers(0, len(prios), no)]
+    lkey = okey[rng.integers(0, no, nl)]
+    qty = rng.integers(1, 51, nl).astype(np.int64)
+    mode = modes[rng.integers(0, len(modes), nl)]
+    customer = Table(ex, "CREATE TABLE customer (c_custkey Int64, c_mktsegment String)")
+    customer.append(c_custkey=ckey, c_mktsegment=seg)
+    orders = Table(ex, "CREATE TABLE orders (o_orderkey Int64, o_custkey Int64, o_orderpriority String)")
+    orders.append(o_orderkey=okey, o_custkey=ocust, o_orderpriority=prio)
+    lineitem = Table(ex, "CREATE TABLE lineitem (l_orderkey Int64, l_quantity Int64, l_shipmode Dictionary(String))")
+    lineitem.append(l_orderkey=lkey, l_quantity=qty, l_shipmode=mode)
+    opos = {k: i for i, k in enumerate(okey.tolist())}
+    cpos = {k: i for i, k in enumerate(ckey.tolist())}
+    oi = np.array([opos[k] for k in lkey.tolist()])
+    ci = np.array([cpos.get(k, -1) for k in ocust[oi].tolist()])
+    ok = ci >= 0
+    lseg = np.where(ok, seg[np.maximum(ci, 0)], "")
+    lprio = prio[oi]
+    frm = "from lineitem join orders on l_orderkey = o_orderkey join customer on o_custkey = c_custkey"
+    got = lineitem.sql(f"""select c_mktsegment, count(*) as c, sum(l_quantity) as s {frm}
+        where (o_orderpriority like '1-%' or o_orderpriority = '2-HIGH') and l_shipmode in ('MAIL', 'SHIP')
+        group by c_mktsegment order by c_mktsegment""", group_hint=8, joined=[orders, customer])
+    m = ok & np.isin(lprio, ["1-URGENT", "2-HIGH"]) & np.isin(mode, ["MAIL", "SHIP"])
+    want = sorted(set(lseg[m].tolist()))
+    assert got["c_mktsegment"].tolist() == want
+    assert got["c"].tolist() == [int(np.sum(m & (lseg == s))) for s in want]
+    assert got["s"].tolist() == [int(qty[m & (lseg == s)].sum()) for s in want]
+    got = lineitem.sql(f"""select l_shipmode, c_mktsegment, o_orderpriority, l_quantity {frm}
+        where l_quantity > 47 and c_mktsegment like 'B%'""", joined=[orders, customer])
+    m = ok & (qty > 47) & (lseg == "BUILDING")
+    rows = sorted(zip(got["l_shipmode"].tolist(), got["c_mktsegment"].tolist(), got["o_orderpriority"].tolist(),
+                      got["l_quantity"].tolist()))
+    assert rows == sorted(zip(mode[m].tolist(), lseg[m].tolist(), lprio[m].tolist(), qty[m].tolist()))
+    with pytest.raises(NutError, match="string keys"):
+        lineitem.sql("select count(*) from lineitem join orders on l_orderkey = o_orderkey "
+                     "join customer on o_orderpriority = c_mktsegment", joined=[orders, customer])
