@@ -320,6 +320,9 @@ nut_status nut_partition_i64(nut_ctx *ctx, const int64_t *in, uint64_t n, const 
  * pointers; the index arrays live in HBM, owned by the nut_join.
  * ------------------------------------------------------------------------ */
 typedef enum { NUT_JOIN_INNER = 0, NUT_JOIN_LEFT = 1, NUT_JOIN_SEMI = 2, NUT_JOIN_ANTI = 3 } nut_join_type;
+/* OR-ed into join_type: the pairs may come out in any order (aggregates over a join need
+ * none) — one unordered probe pass with no tile ordering */
+#define NUT_JOIN_ANY_ORDER 0x100
 typedef struct nut_join nut_join;
 /* builds the table and counts the pairs (the key arrays must stay valid until
  * nut_join_write); *npairs receives the result length */

@@ -149,16 +149,8 @@ nut_status alloc_table(nut_groups *g, uint64_t cap) {
   if (!(g->mem && g->mem_bytes >= off)) {
     if (g->mem) (void)hipFree(g->mem);
     g->mem = nullptr;
-    nut_ctx *c = g->ctx;
-    if (c->tbl_pool && c->tbl_pool_bytes >= off) {  // a freed table's allocation, reused
-      g->mem = c->tbl_pool;
-      g->mem_bytes = c->tbl_pool_bytes;
-      c->tbl_pool = nullptr;
-      c->tbl_pool_bytes = 0;
-    } else {
-      NUT_HIP(hipMalloc(&g->mem, off));
-      g->mem_bytes = off;
-    }
+    nut_status ps = pool_take(g->ctx, off, &g->mem, &g->mem_bytes);  // a freed table's allocation, reused
+    if (ps) return ps;
   }
   char *b = (char *)g->mem;
   GTable &t = g->gt;
@@ -1128,14 +1120,18 @@ namespace nut {
 // 16 bits of owner_hash(key ^ kx) — two gp_levels, 8 bits each — into outk / outr; tmpk /
 // tmpr hold the first level.  counts[65536] = records per 16-bit partition, in order.
 nut_status hash_partition16(nut_ctx *c, const int64_t *keys, uint64_t n, uint64_t kx, int64_t *tmpk, int64_t *tmpr,
-                            int64_t *outk, int64_t *outr, std::vector<uint64_t> &counts) {
+                            int64_t *outk, int64_t *outr, std::vector<uint64_t> &counts, const int64_t *rows) {
   hipStream_t st = c->stream;
   counts.assign(65536, 0);
   if (n == 0) return NUT_OK;
-  // row ids: staged in outr, partitioned into tmpr by level 1, into outr by level 2
-  const unsigned g = (unsigned)std::min<uint64_t>((n + 255) / 256, (uint64_t)c->num_cus * 16);
-  hipLaunchKernelGGL(iota_kernel, dim3(g), dim3(256), 0, st, outr, n, (int64_t)0);
-  const uint64_t *s1[GP_MAX_ARR] = {nullptr, (const uint64_t *)keys, nullptr, (const uint64_t *)outr};
+  // row ids (`rows`, or indices staged in outr) partitioned into tmpr by level 1, into
+  // outr by level 2
+  if (!rows) {
+    const unsigned g = (unsigned)std::min<uint64_t>((n + 255) / 256, (uint64_t)c->num_cus * 16);
+    hipLaunchKernelGGL(iota_kernel, dim3(g), dim3(256), 0, st, outr, n, (int64_t)0);
+    rows = outr;
+  }
+  const uint64_t *s1[GP_MAX_ARR] = {nullptr, (const uint64_t *)keys, nullptr, (const uint64_t *)rows};
   uint64_t *d1[GP_MAX_ARR] = {nullptr, (uint64_t *)tmpk, nullptr, (uint64_t *)tmpr};
   std::vector<GpSeg> segs{GpSeg{0, n, 0, 0}};
   std::vector<uint64_t> h1;
@@ -1270,18 +1266,7 @@ nut_status nut_groups_to_host(nut_groups *g, int64_t *keys, uint64_t *aggs, uint
 
 void nut_groups_free(nut_groups *g) {
   if (!g) return;
-  if (g->mem) {
-    nut_ctx *c = g->ctx;
-    DeviceGuard dg(c->device);
-    (void)hipStreamSynchronize(c->stream);
-    if (g->mem_bytes >= c->tbl_pool_bytes) {  // keep the larger allocation for the next table
-      if (c->tbl_pool) (void)hipFree(c->tbl_pool);
-      c->tbl_pool = g->mem;
-      c->tbl_pool_bytes = g->mem_bytes;
-    } else {
-      (void)hipFree(g->mem);
-    }
-  }
+  if (g->mem) pool_give(g->ctx, g->mem, g->mem_bytes);  // kept for the next table
   delete g;
 }
 

@@ -196,6 +196,40 @@ nut_status nut_ctx_create(int device, nut_ctx **out) {
   return NUT_OK;
 }
 
+}  // extern "C"
+
+namespace nut {
+
+nut_status pool_take(nut_ctx *c, size_t bytes, void **p, size_t *got) {
+  if (c->tbl_pool && c->tbl_pool_bytes >= bytes) {
+    *p = c->tbl_pool;
+    *got = c->tbl_pool_bytes;
+    c->tbl_pool = nullptr;
+    c->tbl_pool_bytes = 0;
+    return NUT_OK;
+  }
+  NUT_HIP(hipMalloc(p, bytes));
+  *got = bytes;
+  return NUT_OK;
+}
+
+void pool_give(nut_ctx *c, void *p, size_t bytes) {
+  if (!p) return;
+  DeviceGuard dg(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  if (bytes >= c->tbl_pool_bytes) {
+    if (c->tbl_pool) (void)hipFree(c->tbl_pool);
+    c->tbl_pool = p;
+    c->tbl_pool_bytes = bytes;
+  } else {
+    (void)hipFree(p);
+  }
+}
+
+}  // namespace nut
+
+extern "C" {
+
 void nut_ctx_destroy(nut_ctx *c) {
   if (!c) return;
   DeviceGuard g(c->device);

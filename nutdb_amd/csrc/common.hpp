@@ -138,6 +138,11 @@ void groups_merge_spec(const nut_groups *g, const uint64_t *seg, uint64_t c, nut
 // place — a plain hipMemcpy to pageable (often untouched, freshly allocated) memory ran
 // at ~10 GB/s, its page faults and staging copies serialised on one thread.
 nut_status copy_to_host(nut_ctx *c, void *dst, const void *src, size_t bytes);
+// the context's one cached large allocation (group tables, join tables): pool_take hands it
+// out when it holds >= bytes (*got = its size) or hipMallocs exactly `bytes`; pool_give
+// syncs the stream and keeps the larger of the returned and the cached allocation
+nut_status pool_take(nut_ctx *c, size_t bytes, void **p, size_t *got);
+void pool_give(nut_ctx *c, void *p, size_t bytes);
 
 // Device scratch that only grows; reused across calls (no malloc in steady state).
 struct Scratch {

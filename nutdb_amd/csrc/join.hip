@@ -63,7 +63,9 @@ __device__ __forceinline__ uint64_t hj_next(uint64_t s, const HjTable &t) {
 // loads are issued together each round, like the probe's run walks).
 constexpr int HJ_BITEMS = 4;
 
-__global__ __launch_bounds__(256) void hj_build_kernel(const int64_t *__restrict__ keys, uint64_t n, HjTable t) {
+// rows: the row id stored per build record (NULL = its index)
+__global__ __launch_bounds__(256) void hj_build_kernel(const int64_t *__restrict__ keys, uint64_t n, HjTable t,
+                                                       const int64_t *__restrict__ rows) {
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < n; i0 += stride * HJ_BITEMS) {
     int64_t k[HJ_BITEMS];
@@ -88,7 +90,7 @@ __global__ __launch_bounds__(256) void hj_build_kernel(const int64_t *__restrict
       for (int j = 0; j < HJ_BITEMS; ++j)
         if (((act >> j) & 1u) && old[j] == HJ_EMPTY)
           old[j] = atomicCAS(reinterpret_cast<unsigned long long *>(&t.slot[s[j]]) + 1, HJ_EMPTY,
-                             (unsigned long long)(i0 + j * stride));
+                             (unsigned long long)(rows ? rows[i0 + j * stride] : (int64_t)(i0 + j * stride)));
 #pragma unroll
       for (int j = 0; j < HJ_BITEMS; ++j) {
         if (!((act >> j) & 1u)) continue;
@@ -107,6 +109,7 @@ __global__ __launch_bounds__(256) void hj_build_kernel(const int64_t *__restrict
 // same key before it means the key repeats (of two equal keys, the one placed later in the
 // run meets the other).  Unique build keys let the probe stop at its first match.
 __global__ __launch_bounds__(256) void hj_dupcheck_kernel(const int64_t *__restrict__ keys, uint64_t n, HjTable t,
+                                                          const int64_t *__restrict__ rows,
                                                           uint32_t *__restrict__ dup) {
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   bool found = false;
@@ -131,7 +134,7 @@ __global__ __launch_bounds__(256) void hj_dupcheck_kernel(const int64_t *__restr
 #pragma unroll
       for (int j = 0; j < HJ_BITEMS; ++j) {
         if (!((act >> j) & 1u)) continue;
-        const bool mine = v[j].y == (int64_t)(i0 + j * stride);
+        const bool mine = v[j].y == (rows ? rows[i0 + j * stride] : (int64_t)(i0 + j * stride));
         found = found || (!mine && v[j].x == k[j]);
         if (mine || v[j].x == k[j]) act &= ~(1u << j);
         s[j] = hj_next(s[j], t);
@@ -148,6 +151,9 @@ __global__ __launch_bounds__(256) void hj_dupcheck_kernel(const int64_t *__restr
 constexpr uint32_t HJ_RS = 8192;
 constexpr int HJ_RTHREADS = 1024;
 
+// records per lane: the host sends a region at most 7/8 x HJ_RS records
+constexpr int HJ_RK = (HJ_RS * 7 / 8 + HJ_RTHREADS - 1) / HJ_RTHREADS;
+
 __global__ __launch_bounds__(HJ_RTHREADS) void hj_region_build_kernel(const int64_t *__restrict__ keys,
                                                                       const int64_t *__restrict__ rows,
                                                                       const uint64_t *__restrict__ region_off,
@@ -157,16 +163,29 @@ __global__ __launch_bounds__(HJ_RTHREADS) void hj_region_build_kernel(const int6
   __shared__ unsigned long long s_row[HJ_RS];
   const int tid = threadIdx.x;
   const uint64_t r = blockIdx.x;
+  const uint64_t lo = region_off[r], hi = region_off[r + 1];
+  // the region's records, all loads issued together (clamped: no per-record branch) and
+  // kept in registers for the duplicate check
+  int64_t k[HJ_RK];
+  unsigned long long row[HJ_RK];
+  if (hi > lo) {
+#pragma unroll
+    for (int j = 0; j < HJ_RK; ++j) {
+      const uint64_t i = lo + tid + (uint64_t)j * HJ_RTHREADS;
+      const uint64_t ic = i < hi ? i : hi - 1;
+      k[j] = keys[ic];
+      row[j] = (unsigned long long)(rows[ic] + row_base);
+    }
+  }
   for (uint32_t i = tid; i < HJ_RS; i += HJ_RTHREADS) s_row[i] = HJ_EMPTY;
   __syncthreads();
-  const uint64_t lo = region_off[r], hi = region_off[r + 1];
-  for (uint64_t i = lo + tid; i < hi; i += HJ_RTHREADS) {
-    const int64_t k = keys[i];
-    const unsigned long long row = (unsigned long long)(rows[i] + row_base);
-    uint32_t s = (uint32_t)(hj_home(k, t) & (HJ_RS - 1));
+#pragma unroll
+  for (int j = 0; j < HJ_RK; ++j) {
+    if (lo + tid + (uint64_t)j * HJ_RTHREADS >= hi) break;
+    uint32_t s = (uint32_t)(hj_home(k[j], t) & (HJ_RS - 1));
     for (;;) {  // the host checked that the region has empty slots
-      if (s_row[s] == HJ_EMPTY && atomicCAS(&s_row[s], HJ_EMPTY, row) == HJ_EMPTY) {
-        s_key[s] = k;
+      if (s_row[s] == HJ_EMPTY && atomicCAS(&s_row[s], HJ_EMPTY, row[j]) == HJ_EMPTY) {
+        s_key[s] = k[j];
         break;
       }
       s = (s + 1) & (HJ_RS - 1);
@@ -174,12 +193,12 @@ __global__ __launch_bounds__(HJ_RTHREADS) void hj_region_build_kernel(const int6
   }
   __syncthreads();
   bool found = false;
-  for (uint64_t i = lo + tid; i < hi; i += HJ_RTHREADS) {
-    const int64_t k = keys[i];
-    const unsigned long long row = (unsigned long long)(rows[i] + row_base);
-    for (uint32_t s = (uint32_t)(hj_home(k, t) & (HJ_RS - 1));; s = (s + 1) & (HJ_RS - 1)) {
-      if (s_row[s] == row) break;
-      if (s_key[s] == k) {
+#pragma unroll
+  for (int j = 0; j < HJ_RK; ++j) {
+    if (lo + tid + (uint64_t)j * HJ_RTHREADS >= hi) break;
+    for (uint32_t s = (uint32_t)(hj_home(k[j], t) & (HJ_RS - 1));; s = (s + 1) & (HJ_RS - 1)) {
+      if (s_row[s] == row[j]) break;
+      if (s_key[s] == k[j]) {
         found = true;
         break;
       }
@@ -203,15 +222,19 @@ __device__ __forceinline__ uint32_t hj_out_count(uint32_t m, int type) {
 // WRITE = false: count pass (tile = blockIdx.x, tile totals added to *total).
 // WRITE = true: ticket-ordered tiles, look-back offsets, pairs written below `cap`; the
 // last tile stores the grand total in *total.
-template <bool WRITE, int HJ_THREADS, int HJ_ITEMS>
-__global__ __launch_bounds__(HJ_THREADS) void hj_probe_kernel(HjTable t, const int64_t *__restrict__ probe,
+// ANY (with WRITE; NUT_JOIN_ANY_ORDER, aggregates over a join): tiles in launch order, each
+// claims its output run with one atomic on *total — no ticket, no look-back chain, no
+// status array; pairs come out grouped by tile in completion order.
+template <bool WRITE, int HJ_THREADS, int HJ_ITEMS, bool ANY = false>
+__global__ __launch_bounds__(HJ_THREADS, HJ_ITEMS <= 8 ? 4 : 1) void hj_probe_kernel(HjTable t, const int64_t *__restrict__ probe,
                                                               uint64_t n, int type, uint32_t *__restrict__ ticket,
                                                               uint64_t *__restrict__ status, uint32_t ntiles,
                                                               unsigned long long *__restrict__ total,
                                                               int64_t *__restrict__ out_p,
                                                               int64_t *__restrict__ out_b, uint64_t cap,
                                                               uint32_t *__restrict__ err,
-                                                              const uint32_t *__restrict__ dup) {
+                                                              const uint32_t *__restrict__ dup,
+                                                              const int64_t *__restrict__ prows) {
   constexpr int HJ_WAVES = HJ_THREADS / kWave;
   constexpr uint32_t HJ_TILE = HJ_THREADS * HJ_ITEMS;
   __shared__ uint64_t s_pre[HJ_ITEMS][HJ_WAVES];
@@ -219,7 +242,7 @@ __global__ __launch_bounds__(HJ_THREADS) void hj_probe_kernel(HjTable t, const i
   __shared__ uint32_t s_tile;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   uint32_t tile = blockIdx.x;
-  if (WRITE) {
+  if (WRITE && !ANY) {
     if (tid == 0) s_tile = atomicAdd(ticket, 1u);
     __syncthreads();
     tile = s_tile;
@@ -306,6 +329,8 @@ __global__ __launch_bounds__(HJ_THREADS) void hj_probe_kernel(HjTable t, const i
     }
     if (!WRITE) {
       if (lane == 0 && tot) atomicAdd(total, (unsigned long long)tot);
+    } else if (ANY) {
+      if (lane == 0) s_excl = tot ? atomicAdd(total, (unsigned long long)tot) : 0;
     } else {
       const uint64_t e = lookback(status, tile, tot, err, lane);
       if (lane == 0) {
@@ -324,17 +349,18 @@ __global__ __launch_bounds__(HJ_THREADS) void hj_probe_kernel(HjTable t, const i
     if (!c) continue;
     uint64_t pos = off0 + s_pre[i][wave] + ex[i];
     if (pos + c > cap) continue;  // too small: the caller retries with the total
+    const int64_t pr = prows ? prows[r] : (int64_t)r;
     if (m[i] == 0 || type >= NUT_JOIN_SEMI) {
-      out_p[pos] = (int64_t)r;
+      out_p[pos] = pr;
       out_b[pos] = -1;
     } else if (m[i] == 1) {
-      out_p[pos] = (int64_t)r;
+      out_p[pos] = pr;
       out_b[pos] = (int64_t)first[i];
     } else {
       uint64_t q = hj_home(key[i], t);
       for (i64x2 v = t.slot[q]; v.y != -1; q = hj_next(q, t), v = t.slot[q])
         if (v.x == key[i]) {
-          out_p[pos] = (int64_t)r;
+          out_p[pos] = pr;
           out_b[pos++] = v.y;
         }
     }
@@ -372,15 +398,17 @@ using namespace nut;
 namespace {
 
 using HjProbeFn = void (*)(HjTable, const int64_t *, uint64_t, int, uint32_t *, uint64_t *, uint32_t,
-                           unsigned long long *, int64_t *, int64_t *, uint64_t, uint32_t *, const uint32_t *);
+                           unsigned long long *, int64_t *, int64_t *, uint64_t, uint32_t *, const uint32_t *,
+                           const int64_t *);
 struct HjCfg {
   int threads;
   uint32_t tile;
-  HjProbeFn write, count;
+  HjProbeFn write, count, any;
 };
 template <int T, int I>
 constexpr HjCfg hj_make() {
-  return HjCfg{T, (uint32_t)(T * I), hj_probe_kernel<true, T, I>, hj_probe_kernel<false, T, I>};
+  return HjCfg{T, (uint32_t)(T * I), hj_probe_kernel<true, T, I>, hj_probe_kernel<false, T, I>,
+               hj_probe_kernel<true, T, I, true>};
 }
 // probe tile shapes (threads x rows per lane); NUT_HJ_CFG picks one for tuning runs
 const HjCfg &hj_cfg() {
@@ -393,16 +421,31 @@ const HjCfg &hj_cfg() {
   }();
   return cfgs[pick];
 }
+// the unordered probe's tile shape: no look-back chain to shorten, so the smallest tiles
+// with the fewest registers (most waves, most slot loads in flight) — NUT_HJ_ANYCFG for tuning
+const HjCfg &hj_any_cfg() {
+  static const HjCfg cfgs[] = {hj_make<256, 4>(), hj_make<512, 8>(), hj_make<256, 8>(), hj_make<512, 4>(),
+                               hj_make<128, 4>()};
+  static const int pick = [] {
+    const char *e = getenv("NUT_HJ_ANYCFG");
+    const int v = e ? atoi(e) : 0;
+    return v >= 0 && v < (int)(sizeof cfgs / sizeof cfgs[0]) ? v : 0;
+  }();
+  return cfgs[pick];
+}
 
 }  // namespace
 
 struct nut_join {
   nut_ctx *ctx = nullptr;
   void *mem = nullptr;  // table slots + probe state (status per tile, ticket, error, total)
+  size_t mem_bytes = 0;  // (a pooled allocation: pool_take / pool_give)
   HjTable t{};
   const int64_t *probe = nullptr;
+  const int64_t *brows = nullptr, *prows = nullptr;  // row ids of the build / probe records (NULL: index)
   uint64_t np = 0, ntiles = 0, n = 0;
   int type = 0;
+  bool any_order = false;  // NUT_JOIN_ANY_ORDER: the unordered probe
   uint64_t *status = nullptr;
   uint32_t *ticket = nullptr, *err = nullptr, *dup = nullptr;
   unsigned long long *total = nullptr;
@@ -421,7 +464,8 @@ nut_status join_build(nut_ctx *c, nut_join *j, const int64_t *build, uint64_t nb
   // [slots 16 B x cap | dup u32, pad | ticket u32, err u32, total u64 | status u64 x ntiles]
   const size_t o_dup = cap * 16, o_state = o_dup + 16;
   j->state_bytes = 16 + j->ntiles * 8;
-  NUT_HIP(hipMalloc(&j->mem, o_state + j->state_bytes));
+  nut_status ps = pool_take(c, o_state + j->state_bytes, &j->mem, &j->mem_bytes);
+  if (ps) return ps;
   char *b = (char *)j->mem;
   j->t = HjTable{(i64x2 *)b, cap - 1, 64 - log2c};
   j->ticket = (uint32_t *)(b + o_state);
@@ -442,7 +486,7 @@ nut_status join_build(nut_ctx *c, nut_join *j, const int64_t *build, uint64_t nb
     int64_t *tmp = nullptr;
     NUT_HIP(hipMallocAsync((void **)&tmp, nb * 32, st));
     std::vector<uint64_t> counts;
-    nut_status e = hash_partition16(c, build, nb, HJ_KX, tmp, tmp + nb, tmp + 2 * nb, tmp + 3 * nb, counts);
+    nut_status e = hash_partition16(c, build, nb, HJ_KX, tmp, tmp + nb, tmp + 2 * nb, tmp + 3 * nb, counts, j->brows);
     if (e) {
       (void)hipFreeAsync(tmp, st);
       return e;
@@ -474,9 +518,9 @@ nut_status join_build(nut_ctx *c, nut_join *j, const int64_t *build, uint64_t nb
   NUT_HIP(hipMemsetAsync(b, 0xFF, cap * 16, st));
   if (nb) {
     const unsigned g = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((nb + 255) / 256, c->num_cus * 16ull));
-    hipLaunchKernelGGL(hj_build_kernel, dim3(g), dim3(256), 0, st, build, nb, j->t);
+    hipLaunchKernelGGL(hj_build_kernel, dim3(g), dim3(256), 0, st, build, nb, j->t, j->brows);
     if (j->type <= NUT_JOIN_LEFT)
-      hipLaunchKernelGGL(hj_dupcheck_kernel, dim3(g), dim3(256), 0, st, build, nb, j->t, j->dup);
+      hipLaunchKernelGGL(hj_dupcheck_kernel, dim3(g), dim3(256), 0, st, build, nb, j->t, j->brows, j->dup);
   }
   NUT_HIP(hipGetLastError());
   return NUT_OK;
@@ -488,11 +532,21 @@ nut_status join_probe(nut_join *j, bool write, int64_t *pi, int64_t *bi, uint64_
   hipStream_t st = c->stream;
   *npairs = 0;
   if (!j->ntiles) return NUT_OK;
-  NUT_HIP(hipMemsetAsync(j->ticket, 0, j->state_bytes, st));
-  const HjCfg &cf = hj_cfg();
-  (write ? cf.write : cf.count)<<<dim3((unsigned)j->ntiles), dim3(cf.threads), 0, st>>>(
-      j->t, j->probe, j->np, j->type, j->ticket, j->status, (uint32_t)j->ntiles, j->total, pi, bi, cap, j->err,
-      (const uint32_t *)j->dup);
+  if (j->any_order && write) {
+    NUT_HIP(hipMemsetAsync(j->ticket, 0, 16, st));
+    const HjCfg &cf = hj_any_cfg();
+    const uint64_t nt = (j->np + cf.tile - 1) / cf.tile;
+    if (nt > 0x7FFFFFFFull) return fail(NUT_ERR_UNSUPPORTED, "nut_join: probe side too large");
+    cf.any<<<dim3((unsigned)nt), dim3(cf.threads), 0, st>>>(j->t, j->probe, j->np, j->type, j->ticket, j->status,
+                                                         (uint32_t)nt, j->total, pi, bi, cap, j->err,
+                                                         (const uint32_t *)j->dup, j->prows);
+  } else {
+    NUT_HIP(hipMemsetAsync(j->ticket, 0, j->state_bytes, st));
+    const HjCfg &cf = hj_cfg();
+    (write ? cf.write : cf.count)<<<dim3((unsigned)j->ntiles), dim3(cf.threads), 0, st>>>(
+        j->t, j->probe, j->np, j->type, j->ticket, j->status, (uint32_t)j->ntiles, j->total, pi, bi, cap, j->err,
+        (const uint32_t *)j->dup, j->prows);
+  }
   NUT_HIP(hipGetLastError());
   NUT_HIP(hipMemcpyAsync(c->host_pinned, j->ticket, 16, hipMemcpyDeviceToHost, st));
   NUT_HIP(hipStreamSynchronize(st));
@@ -502,7 +556,10 @@ nut_status join_probe(nut_join *j, bool write, int64_t *pi, int64_t *bi, uint64_
 }
 
 nut_status join_begin(nut_ctx *c, const int64_t *build, uint64_t nb, const int64_t *probe, uint64_t np, int type,
-                      nut_join **out, const char *who) {
+                      nut_join **out, const char *who, const int64_t *brows = nullptr,
+                      const int64_t *prows = nullptr) {
+  const bool any_order = (type & NUT_JOIN_ANY_ORDER) != 0;
+  type &= ~NUT_JOIN_ANY_ORDER;
   if (type < NUT_JOIN_INNER || type > NUT_JOIN_ANTI) return fail(NUT_ERR_INVALID_ARG, std::string(who) + ": bad join type");
   if (nb >= (1ull << 31)) return fail(NUT_ERR_UNSUPPORTED, std::string(who) + ": build side >= 2^31 rows");
   nut_join *j = new (std::nothrow) nut_join();
@@ -511,6 +568,9 @@ nut_status join_begin(nut_ctx *c, const int64_t *build, uint64_t nb, const int64
   j->probe = probe;
   j->np = np;
   j->type = type;
+  j->any_order = any_order;
+  j->brows = brows;
+  j->prows = prows;
   nut_status s = join_build(c, j, build, nb);
   if (s) {
     nut_join_free(j);
@@ -521,6 +581,26 @@ nut_status join_begin(nut_ctx *c, const int64_t *build, uint64_t nb, const int64
 }
 
 }  // namespace
+
+nut_status nut::join_i64_into_rows(nut_ctx *c, const int64_t *build, const int64_t *brows, uint64_t nb,
+                                   const int64_t *probe, const int64_t *prows, uint64_t np, int type,
+                                   int64_t *probe_idx, int64_t *build_idx, uint64_t cap, uint64_t *npairs) {
+  if (!c || !npairs || (nb && !build) || (np && !probe) || (cap && (!probe_idx || !build_idx)))
+    return fail(NUT_ERR_INVALID_ARG, "nut_join_i64_into: NULL argument");
+  DeviceGuard dg(c->device);
+  nut_join *j = nullptr;
+  c->timer.begin(c->stream, NUT_KERNEL_JOIN);
+  nut_status s = join_begin(c, build, nb, probe, np, type, &j, "nut_join_i64_into", brows, prows);
+  uint64_t n = 0;
+  if (!s) s = join_probe(j, true, probe_idx, build_idx, cap, &n);
+  c->timer.end(c->stream);
+  nut_join_free(j);
+  if (s) return s;
+  *npairs = n;
+  if (n > cap) return fail(NUT_ERR_CAPACITY, "nut_join_i64_into: " + std::to_string(n) + " pairs > capacity " +
+                                                std::to_string(cap));
+  return NUT_OK;
+}
 
 extern "C" {
 
@@ -559,30 +639,12 @@ nut_status nut_join_write(nut_join *j, int64_t *probe_idx, int64_t *build_idx) {
 
 nut_status nut_join_i64_into(nut_ctx *c, const int64_t *build, uint64_t nb, const int64_t *probe, uint64_t np,
                              int type, int64_t *probe_idx, int64_t *build_idx, uint64_t cap, uint64_t *npairs) {
-  if (!c || !npairs || (nb && !build) || (np && !probe) || (cap && (!probe_idx || !build_idx)))
-    return fail(NUT_ERR_INVALID_ARG, "nut_join_i64_into: NULL argument");
-  DeviceGuard dg(c->device);
-  nut_join *j = nullptr;
-  c->timer.begin(c->stream, NUT_KERNEL_JOIN);
-  nut_status s = join_begin(c, build, nb, probe, np, type, &j, "nut_join_i64_into");
-  uint64_t n = 0;
-  if (!s) s = join_probe(j, true, probe_idx, build_idx, cap, &n);
-  c->timer.end(c->stream);
-  nut_join_free(j);
-  if (s) return s;
-  *npairs = n;
-  if (n > cap) return fail(NUT_ERR_CAPACITY, "nut_join_i64_into: " + std::to_string(n) + " pairs > capacity " +
-                                                std::to_string(cap));
-  return NUT_OK;
+  return join_i64_into_rows(c, build, nullptr, nb, probe, nullptr, np, type, probe_idx, build_idx, cap, npairs);
 }
 
 void nut_join_free(nut_join *j) {
   if (!j) return;
-  if (j->mem) {
-    DeviceGuard dg(j->ctx->device);
-    (void)hipStreamSynchronize(j->ctx->stream);
-    (void)hipFree(j->mem);
-  }
+  if (j->mem) pool_give(j->ctx, j->mem, j->mem_bytes);
   delete j;
 }
 

@@ -12,5 +12,11 @@ nut_status lsd_sort_i64(nut_ctx *c, const int64_t *in, int64_t *out, uint64_t n,
 nut_status msd_sort_i64(nut_ctx *c, const int64_t *in, int64_t *out, uint64_t n, uint64_t flip);  // msd_sort.hip
 nut_status join_matched(nut_ctx *c, const int64_t *bi, uint64_t n, int64_t *out);                   // join.hip
 nut_status hash_partition16(nut_ctx *c, const int64_t *keys, uint64_t n, uint64_t kx, int64_t *tmpk,  // aggregate.hip
-                            int64_t *tmpr, int64_t *outk, int64_t *outr, std::vector<uint64_t> &counts);
+                            int64_t *tmpr, int64_t *outk, int64_t *outr, std::vector<uint64_t> &counts,
+                            const int64_t *rows = nullptr);
+// nut_join_i64_into whose pairs carry given row ids: brows[i] for build record i, prows[r]
+// for probe record r (NULL: the index) — joins over pushed-down selections (sql_plan.cpp)
+nut_status join_i64_into_rows(nut_ctx *c, const int64_t *build, const int64_t *brows, uint64_t nb,
+                              const int64_t *probe, const int64_t *prows, uint64_t np, int type, int64_t *probe_idx,
+                              int64_t *build_idx, uint64_t cap, uint64_t *npairs);
 }  // namespace nut

@@ -2408,14 +2408,17 @@ nut_status exec_join(nut_ctx *c, const nut_plan &p, const nut_column *lc, int nl
     used[i] = row || agg;
   }
   // one pass into arrays of np pairs (enough unless the build keys repeat), else again
-  // with the exact count
+  // with the exact count; aggregates take the pairs in any order (the unordered probe)
+  const int any_order = p.kind == NUT_PLAN_GROUPBY ? NUT_JOIN_ANY_ORDER : 0;
   DevBuf idx;
   uint64_t cap = std::max<uint64_t>(np, 1), npairs = 0;
   nut_status st;
   for (;;) {
     hipError_t he = hipMalloc(&idx.p, cap * 16);
     if (he != hipSuccess) return hip_fail(he, "hipMalloc (join index)");
-    st = nut_join_i64_into(c, bkd, nb, pkd, np, p.join, (int64_t *)idx.p, (int64_t *)idx.p + cap, cap, &npairs);
+    // the pairs carry table rows: the pushed-down selections' ids ride along as row ids
+    st = join_i64_into_rows(c, bkd, (const int64_t *)ids_s[1 - ps].p, nb, pkd, (const int64_t *)ids_s[ps].p, np,
+                            p.join | any_order, (int64_t *)idx.p, (int64_t *)idx.p + cap, cap, &npairs);
     if (st != NUT_ERR_CAPACITY || npairs <= cap) break;
     NUT_HIP(hipFree(idx.p));
     idx.p = nullptr;
@@ -2423,15 +2426,6 @@ nut_status exec_join(nut_ctx *c, const nut_plan &p, const nut_column *lc, int nl
   }
   if (st) return st;
   int64_t *pi = (int64_t *)idx.p, *bi = pi + cap;
-  // indices into the pushed-down selections -> table rows (-1 stays -1)
-  if (ids_s[ps].p && npairs) {
-    st = nut_gather_u64(c, (const uint64_t *)ids_s[ps].p, pi, npairs, 0, (uint64_t *)pi);
-    if (st) return st;
-  }
-  if (ids_s[1 - ps].p && npairs) {
-    st = nut_gather_u64(c, (const uint64_t *)ids_s[1 - ps].p, bi, npairs, ~0ull, (uint64_t *)bi);
-    if (st) return st;
-  }
   // the joined table: every plan column gathered through its side's index
   const bool mask_col = outer && p.kind == NUT_PLAN_GROUPBY;
   std::vector<DevBuf> bufs(nc + 1);
@@ -2605,8 +2599,9 @@ nut_status exec_joinn(nut_ctx *c, const nut_plan &p, const nut_column *const *ta
     uint64_t cap = std::max<uint64_t>(ncur, 1), m = 0;
     for (;;) {
       if (hipMalloc(&pairs.p, cap * 16) != hipSuccess) return fail(NUT_ERR_OOM, "hipMalloc (join index)");
-      st = nut_join_i64_into(c, bkd, rows[t], pkd, ncur, NUT_JOIN_INNER, (int64_t *)pairs.p,
-                             (int64_t *)pairs.p + cap, cap, &m);
+      st = nut_join_i64_into(c, bkd, rows[t], pkd, ncur,
+                             NUT_JOIN_INNER | (p.kind == NUT_PLAN_GROUPBY ? NUT_JOIN_ANY_ORDER : 0),
+                             (int64_t *)pairs.p, (int64_t *)pairs.p + cap, cap, &m);
       if (st != NUT_ERR_CAPACITY || m <= cap) break;
       NUT_HIP(hipFree(pairs.p));
       pairs.p = nullptr;

@@ -402,9 +402,12 @@ class Executor:
     # ---------------------------------------------------------------- join
     JOIN_TYPES = {"inner": 0, "left": 1, "semi": 2, "anti": 3}
 
-    def join_i64(self, build: torch.Tensor, probe: torch.Tensor, how: str = "inner", passes: int = 1):
+    def join_i64(self, build: torch.Tensor, probe: torch.Tensor, how: str = "inner", passes: int = 1,
+                 any_order: bool = False):
         """Hash equi-join (nut_join_i64): (probe_idx, build_idx) int64 tensors, ordered by
-        probe row; build_idx = -1 for LEFT rows without a match and for SEMI / ANTI rows.
+        probe row (any_order: in unspecified order, NUT_JOIN_ANY_ORDER — the unordered
+        probe); build_idx = -1 for LEFT rows without a match and for SEMI /
+        ANTI rows.
         Lowered from JoinClause (src/parser/ast/query.rs:55-66, 100-117).  passes=1:
         nut_join_i64_into (one probe pass into arrays of len(probe) pairs, again with the
         exact size if the build keys repeat); passes=2: nut_join_i64 (count) +
@@ -421,7 +424,9 @@ class Executor:
         pp = C.c_void_p(_col(probe, self.device) if np_ else None)
         if passes == 2:
             h = C.c_void_p()
-            check(lib.nut_join_i64(self.ctx, bp, nb, pp, np_, self.JOIN_TYPES[how], C.byref(h), C.byref(n)),
+            check(lib.nut_join_i64(self.ctx, bp, nb, pp, np_,
+                                   self.JOIN_TYPES[how] | (L.NUT_JOIN_ANY_ORDER if any_order else 0), C.byref(h),
+                                   C.byref(n)),
                   "nut_join_i64")
             try:
                 pi = torch.empty(n.value, dtype=torch.int64, device=self.device)
@@ -436,7 +441,8 @@ class Executor:
         while True:
             pi = torch.empty(cap, dtype=torch.int64, device=self.device)
             bi = torch.empty(cap, dtype=torch.int64, device=self.device)
-            st = lib.nut_join_i64_into(self.ctx, bp, nb, pp, np_, self.JOIN_TYPES[how],
+            st = lib.nut_join_i64_into(self.ctx, bp, nb, pp, np_,
+                                       self.JOIN_TYPES[how] | (L.NUT_JOIN_ANY_ORDER if any_order else 0),
                                        C.c_void_p(pi.data_ptr() if cap else None),
                                        C.c_void_p(bi.data_ptr() if cap else None), cap, C.byref(n))
             if st == L.NUT_ERR_CAPACITY and n.value > cap:

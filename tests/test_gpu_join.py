@@ -18,11 +18,12 @@ def canon(pi, bi):
     return pi[o], bi[o]
 
 
-def check(ex, orc, b, p, how, passes=1):
-    pi, bi = ex.join_i64(dev(b, ex), dev(p, ex), how, passes=passes)
+def check(ex, orc, b, p, how, passes=1, any_order=False):
+    pi, bi = ex.join_i64(dev(b, ex), dev(p, ex), how, passes=passes, any_order=any_order)
     pi, bi = host(pi), host(bi)
     wp, wb = orc.join_i64(b, p, how)
-    assert np.all(pi[1:] >= pi[:-1]), "pairs not in probe-row order"
+    if not any_order:
+        assert np.all(pi[1:] >= pi[:-1]), "pairs not in probe-row order"
     gp, gb = canon(pi, bi)
     assert np.array_equal(gp, wp) and np.array_equal(gb, wb), how
 
@@ -93,6 +94,28 @@ def test_join_extreme_keys(ex, orc, how):
     check(ex, orc, b, p, how)
 
 
+@pytest.mark.parametrize("passes", [1, 2])
+@pytest.mark.parametrize("how", HOW)
+def test_join_any_order(ex, orc, how, passes):
+    """NUT_JOIN_ANY_ORDER (the unordered probe, used under aggregates): the same pair
+    multiset as the ordered join — unique keys, repeated keys past the first capacity,
+    region-built tables, long runs, extreme keys, empty sides."""
+    rng = np.random.default_rng(77)
+    cases = [
+        (rng.permutation(np.arange(100_000, dtype=np.int64) * 7 - 1000), rng.integers(-2000, 700_000, 1_000_003)),
+        (rng.integers(0, 300, 20_000), rng.integers(-50, 350, 30_001)),
+        (rng.integers(0, 1_500_000, 2_100_000), rng.integers(-100_000, 1_600_000, 3_000_001)),
+        (np.repeat(np.array([7, -7, 2**40], dtype=np.int64), 1000), rng.choice(np.array([7, -7, 2**40, 8, 9]), 5_000)),
+        (np.array([I64_MIN, I64_MAX, 0, -1], dtype=np.int64)[rng.integers(0, 4, 50)],
+         np.array([I64_MIN, I64_MAX, 0, -1, 1, 5], dtype=np.int64)[rng.integers(0, 6, 10_000)]),
+        (np.zeros(0, np.int64), rng.integers(0, 9, 1000)),
+        (rng.integers(0, 9, 1000), np.zeros(0, np.int64)),
+        (np.array([3], np.int64), np.array([3], np.int64)),
+    ]
+    for b, p in cases:
+        check(ex, orc, b.astype(np.int64), p.astype(np.int64), how, passes=passes, any_order=True)
+
+
 def test_join_large_property(ex, orc):
     """1e7 unique build keys, 2e8 probe keys (~90 % matching): count and a checksum of the
     pairs against numpy."""
@@ -108,6 +131,10 @@ def test_join_large_property(ex, orc):
     assert len(pi) == int((~miss).sum())
     assert np.array_equal(host(pi), np.nonzero(~miss)[0])
     assert np.array_equal(bh[host(bi)], hp[~miss])
+    # the unordered probe: the same pairs once sorted by probe row
+    ui, ub = ex.join_i64(b, p, "inner", any_order=True)
+    o = torch.argsort(ui)
+    assert torch.equal(ui[o], pi) and torch.equal(ub[o], bi)
 
 
 def test_gather_null_and_f64(ex):
