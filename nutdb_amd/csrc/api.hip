@@ -115,7 +115,12 @@ constexpr size_t kStageBytes = 32u << 20;  // per pinned chunk
 constexpr int kCopyThreads = 8;
 
 nut_status copy_to_host(nut_ctx *c, void *dst, const void *src, size_t bytes) {
-  if (bytes < (8u << 20)) {  // small: one plain copy
+  // pinned (page-locked) destination: the copy engine writes it directly at the link rate
+  hipPointerAttribute_t pa;
+  bool pinned = false;
+  if (hipPointerGetAttributes(&pa, dst) == hipSuccess) pinned = pa.type == hipMemoryTypeHost;
+  (void)hipGetLastError();  // pageable memory reports an error here
+  if (bytes < (8u << 20) || pinned) {  // small or pinned: one plain copy
     NUT_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
     NUT_HIP(hipStreamSynchronize(c->stream));
     return NUT_OK;

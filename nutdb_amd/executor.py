@@ -230,9 +230,21 @@ class Groups:
         check(lib.nut_groups_size(self.h, C.byref(n)), "nut_groups_size")
         return n.value
 
-    def to_host_words(self):
-        """(keys int64 [n, nkeys], aggs uint64 [n, naggs]) sorted by key tuple."""
+    def to_host_words(self, out=None):
+        """(keys int64 [n, nkeys], aggs uint64 [n, naggs]) sorted by key tuple.  out: a
+        (keys, aggs) pair of C-contiguous host arrays with room for n rows to fill instead
+        (a caller's reused result buffers; page-locked ones are written by the copy engine
+        directly)."""
         n = len(self)
+        if out is not None:
+            ko, ao = out
+            if (ko.dtype != np.int64 or ao.dtype.itemsize != 8 or ko.shape[0] < n or ao.shape[0] < n
+                    or ko.shape[1:] != (self.nkeys,) or ao.shape[1:] != (max(self.naggs, 1),)
+                    or not ko.flags.c_contiguous or not ao.flags.c_contiguous):
+                raise ValueError("to_host_words: out arrays must be C-contiguous int64 [>=n, nkeys] / "
+                                 "8-byte [>=n, max(naggs, 1)]")
+            check(lib.nut_groups_to_host(self.h, ko.ctypes.data, ao.ctypes.data, n), "nut_groups_to_host")
+            return ko[:n], ao[:n, : self.naggs].view(np.uint64)
         # np.empty: the library writes every word; np.zeros spent ~10 ms zeroing 1e7 groups
         keys = np.empty((n, self.nkeys), dtype=np.int64)
         aggs = np.empty((n, max(self.naggs, 1)), dtype=np.uint64)
