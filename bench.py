@@ -488,6 +488,8 @@ def cpu_baseline(args, workload: str, target_s: float):
     probe = min(full, 4_000_000)
     per_row = timed(prepare(probe)) / probe
     sample = int(min(full, max(probe, target_s / max(per_row, 1e-12))))
+    if workload == "join":  # the pair-set parity check sorts every pair on the host: keep it to seconds
+        sample = min(sample, 50_000_000)
     fn = prepare(sample)
     times = [timed(fn)]
     while sum(times) < target_s and len(times) < 10:

@@ -191,6 +191,15 @@ nut_status nut_ctx_create(int device, nut_ctx **out) {
     return hip_fail(e, "hipStreamCreate");
   }
   c->stream = c->own_stream;
+  {  // the device's stream-ordered pool keeps what queries free (hipMallocAsync scratch,
+     // sql_plan.cpp DevBuf) instead of returning it at every synchronisation
+    hipMemPool_t pool;
+    if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
+      uint64_t keep = UINT64_MAX;
+      (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+    }
+    (void)hipGetLastError();
+  }
   e = hipHostMalloc((void **)&c->host_pinned, 4096, hipHostMallocDefault);
   if (e != hipSuccess) {
     (void)hipStreamDestroy(c->own_stream);

@@ -1511,14 +1511,25 @@ const nut_column *bind(const nut_plan &p, int ci, const nut_column *cols, int nc
   return nullptr;
 }
 
+// a query-lifetime device buffer: stream-ordered (hipMallocAsync on the context's stream,
+// whose pool keeps freed memory — nut_ctx_create), so the per-query selections, join
+// indices and gathered columns cost no hipMalloc / hipFree round trip
 struct DevBuf {
   void *p = nullptr;
+  hipStream_t s = nullptr;
   DevBuf() = default;
   DevBuf(const DevBuf &) = delete;
   DevBuf &operator=(const DevBuf &) = delete;
-  ~DevBuf() {
-    if (p) (void)hipFree(p);
+  hipError_t alloc(nut_ctx *c, size_t bytes) {
+    reset();
+    s = c->stream;
+    return hipMallocAsync(&p, bytes, s);
   }
+  void reset() {
+    if (p) (void)(s ? hipFreeAsync(p, s) : hipFree(p));
+    p = nullptr;
+  }
+  ~DevBuf() { reset(); }
 };
 
 // what the programs of one nut_agg_spec point at: node arrays and LOOKUP tables (device)
@@ -1556,7 +1567,7 @@ nut_status exec_sort_rows(nut_ctx *c, const nut_plan &p, const nut_column *const
     std::vector<int> agg_f64;
     nut_status s = build_spec(p, bound, dicts, n, sp, store, agg_f64);
     if (s) return s;
-    NUT_HIP(hipMalloc(&rows.p, n * 8));
+    NUT_HIP(rows.alloc(c, n * 8));
     s = nut_select_rows(c, &sp, (int64_t *)rows.p, &cnt);
     if (s) return s;
   }
@@ -1564,8 +1575,8 @@ nut_status exec_sort_rows(nut_ctx *c, const nut_plan &p, const nut_column *const
   NUT_HIP(hipMalloc(&r->dev, m * 8 * p.projs.size()));
   r->dev_stride = cnt;
   if (cnt) {
-    NUT_HIP(hipMalloc(&perm.p, m * 8));
-    NUT_HIP(hipMalloc(&keys.p, m * 8));
+    NUT_HIP(perm.alloc(c, m * 8));
+    NUT_HIP(keys.alloc(c, m * 8));
     nut_status s = NUT_OK;
     for (size_t i = p.sort_keys.size(); i-- > 0 && !s;) {
       const nut_column *kc = bound[p.sort_keys[i].first];
@@ -1653,7 +1664,7 @@ nut_status exec_scan(nut_ctx *c, const nut_plan &p, const nut_column *const *bou
     nut_status s = build_spec(p, bound, dicts, n, sp, store, agg_f64);
     if (s) return s;
     DevBuf rows;
-    NUT_HIP(hipMalloc(&rows.p, n * 8));
+    NUT_HIP(rows.alloc(c, n * 8));
     s = nut_select_rows(c, &sp, (int64_t *)rows.p, &cnt);
     if (s) return s;
     const size_t k = p.kind == NUT_PLAN_FILTER ? p.projs.size() : 1;
@@ -1665,7 +1676,7 @@ nut_status exec_scan(nut_ctx *c, const nut_plan &p, const nut_column *const *bou
                            (uint64_t *)r->dev + j * cnt);
     } else {
       DevBuf vals;
-      NUT_HIP(hipMalloc(&vals.p, std::max<uint64_t>(cnt, 1) * 8));
+      NUT_HIP(vals.alloc(c, std::max<uint64_t>(cnt, 1) * 8));
       s = nut_gather_u64(c, (const uint64_t *)col->data, (const int64_t *)rows.p, cnt, 0, (uint64_t *)vals.p);
       if (!s) s = p.desc ? nut_sort_i64_desc(c, (const int64_t *)vals.p, (int64_t *)r->dev, cnt)
                          : nut_sort_i64(c, (const int64_t *)vals.p, (int64_t *)r->dev, cnt);
@@ -1682,7 +1693,7 @@ nut_status exec_scan(nut_ctx *c, const nut_plan &p, const nut_column *const *bou
       DevBuf tmp;
       cnt = n;
       if (!p.preds.empty() && !(op == NUT_GE && k == INT64_MIN)) {
-        NUT_HIP(hipMalloc(&tmp.p, n * 8));
+        NUT_HIP(tmp.alloc(c, n * 8));
         nut_status s = nut_filter_i64(c, src, n, op, k, (int64_t *)tmp.p, &cnt);
         if (s) return s;
         src = (const int64_t *)tmp.p;
@@ -2385,11 +2396,11 @@ nut_status exec_join(nut_ctx *c, const nut_plan &p, const nut_column *lc, int nl
     std::vector<int> agg_f64;
     nut_status es = build_spec(q, src.data(), sdict.data(), rows_s[sd], spec, store, agg_f64);
     if (es) return es;
-    NUT_HIP(hipMalloc(&ids_s[sd].p, std::max<uint64_t>(rows_s[sd], 1) * 8));
+    NUT_HIP(ids_s[sd].alloc(c, std::max<uint64_t>(rows_s[sd], 1) * 8));
     uint64_t cnt = 0;
     if (rows_s[sd]) es = nut_select_rows(c, &spec, (int64_t *)ids_s[sd].p, &cnt);
     if (es) return es;
-    NUT_HIP(hipMalloc(&keybuf[sd].p, std::max<uint64_t>(cnt, 1) * 8));
+    NUT_HIP(keybuf[sd].alloc(c, std::max<uint64_t>(cnt, 1) * 8));
     es = nut_gather_u64(c, (const uint64_t *)keycol[sd]->data, (const int64_t *)ids_s[sd].p, cnt, 0,
                         (uint64_t *)keybuf[sd].p);
     if (es) return es;
@@ -2414,14 +2425,13 @@ nut_status exec_join(nut_ctx *c, const nut_plan &p, const nut_column *lc, int nl
   uint64_t cap = std::max<uint64_t>(np, 1), npairs = 0;
   nut_status st;
   for (;;) {
-    hipError_t he = hipMalloc(&idx.p, cap * 16);
+    hipError_t he = idx.alloc(c, cap * 16);
     if (he != hipSuccess) return hip_fail(he, "hipMalloc (join index)");
     // the pairs carry table rows: the pushed-down selections' ids ride along as row ids
     st = join_i64_into_rows(c, bkd, (const int64_t *)ids_s[1 - ps].p, nb, pkd, (const int64_t *)ids_s[ps].p, np,
                             p.join | any_order, (int64_t *)idx.p, (int64_t *)idx.p + cap, cap, &npairs);
     if (st != NUT_ERR_CAPACITY || npairs <= cap) break;
-    NUT_HIP(hipFree(idx.p));
-    idx.p = nullptr;
+    idx.reset();
     cap = npairs;
   }
   if (st) return st;
@@ -2435,7 +2445,7 @@ nut_status exec_join(nut_ctx *c, const nut_plan &p, const nut_column *lc, int nl
       jc[i] = nut_column{p.cols[i].c_str(), src[i]->data, src[i]->type};
       continue;
     }
-    NUT_HIP(hipMalloc(&bufs[i].p, std::max<uint64_t>(npairs, 1) * 8));
+    NUT_HIP(bufs[i].alloc(c, std::max<uint64_t>(npairs, 1) * 8));
     // SEMI / ANTI pairs carry no build row: the other ON column reads the preserved one
     // (outer joins: equal on matched rows; aggregates mask the NULL-extended ones)
     const bool via_probe = side[i] == ps || (p.join != NUT_JOIN_INNER && (int)i == bkey);
@@ -2445,7 +2455,7 @@ nut_status exec_join(nut_ctx *c, const nut_plan &p, const nut_column *lc, int nl
     jc[i] = nut_column{p.cols[i].c_str(), bufs[i].p, src[i]->type};
   }
   if (mask_col) {  // aggregates over the other table skip the NULL-extended rows
-    NUT_HIP(hipMalloc(&bufs[nc].p, std::max<uint64_t>(npairs, 1) * 8));
+    NUT_HIP(bufs[nc].alloc(c, std::max<uint64_t>(npairs, 1) * 8));
     st = join_matched(c, bi, npairs, (int64_t *)bufs[nc].p);
     if (st) return st;
     p2.cols.push_back("__matched");
@@ -2568,14 +2578,14 @@ nut_status exec_joinn(nut_ctx *c, const nut_plan &p, const nut_column *const *ta
     std::vector<int> agg_f64;
     nut_status es = build_spec(q, src.data(), sdict.data(), rows[t], spec, store, agg_f64);
     if (es) return es;
-    NUT_HIP(hipMalloc(&ids[t].p, std::max<uint64_t>(rows[t], 1) * 8));
+    NUT_HIP(ids[t].alloc(c, std::max<uint64_t>(rows[t], 1) * 8));
     uint64_t cnt = 0;
     if (rows[t]) es = nut_select_rows(c, &spec, (int64_t *)ids[t].p, &cnt);
     if (es) return es;
     rows[t] = cnt;
   }
   auto gather_to = [&](const void *col, const int64_t *idx, uint64_t n, DevBuf &out) -> nut_status {
-    if (hipMalloc(&out.p, std::max<uint64_t>(n, 1) * 8) != hipSuccess) return fail(NUT_ERR_OOM, "hipMalloc (join)");
+    if (out.alloc(c, std::max<uint64_t>(n, 1) * 8) != hipSuccess) return fail(NUT_ERR_OOM, "hipMalloc (join)");
     return n ? nut_gather_u64(c, (const uint64_t *)col, idx, n, 0, (uint64_t *)out.p) : NUT_OK;
   };
   std::vector<DevBuf> acc(nt);
@@ -2598,13 +2608,12 @@ nut_status exec_joinn(nut_ctx *c, const nut_plan &p, const nut_column *const *ta
     DevBuf pairs;
     uint64_t cap = std::max<uint64_t>(ncur, 1), m = 0;
     for (;;) {
-      if (hipMalloc(&pairs.p, cap * 16) != hipSuccess) return fail(NUT_ERR_OOM, "hipMalloc (join index)");
+      if (pairs.alloc(c, cap * 16) != hipSuccess) return fail(NUT_ERR_OOM, "hipMalloc (join index)");
       st = nut_join_i64_into(c, bkd, rows[t], pkd, ncur,
                              NUT_JOIN_INNER | (p.kind == NUT_PLAN_GROUPBY ? NUT_JOIN_ANY_ORDER : 0),
                              (int64_t *)pairs.p, (int64_t *)pairs.p + cap, cap, &m);
       if (st != NUT_ERR_CAPACITY || m <= cap) break;
-      NUT_HIP(hipFree(pairs.p));
-      pairs.p = nullptr;
+      pairs.reset();
       cap = m;
     }
     if (st) break;
@@ -2616,7 +2625,7 @@ nut_status exec_joinn(nut_ctx *c, const nut_plan &p, const nut_column *const *ta
       if (base) {
         st = gather_to(base, through, m, next[v]);
       } else {
-        if (hipMalloc(&next[v].p, std::max<uint64_t>(m, 1) * 8) != hipSuccess) return fail(NUT_ERR_OOM, "hipMalloc");
+        if (next[v].alloc(c, std::max<uint64_t>(m, 1) * 8) != hipSuccess) return fail(NUT_ERR_OOM, "hipMalloc");
         if (m) NUT_HIP(hipMemcpyAsync(next[v].p, through, m * 8, hipMemcpyDeviceToDevice, c->stream));
       }
     }
@@ -2624,6 +2633,7 @@ nut_status exec_joinn(nut_ctx *c, const nut_plan &p, const nut_column *const *ta
     NUT_HIP(hipStreamSynchronize(c->stream));
     for (int v = 0; v <= t; ++v) {
       std::swap(acc[v].p, next[v].p);
+      std::swap(acc[v].s, next[v].s);
       accp[v] = (const int64_t *)acc[v].p;
     }
     ncur = m;

@@ -20,7 +20,8 @@ WORKLOAD_KERNEL = {"q1": ("tpch_q1_shape_filter_groupby", "agg_kernel"),
                    "sort": ("sort_i64_radix", "nut::ms_"),
                    "q12expr": ("q12_shape_expression_groupby", "agg_kernel"),
                    "join": ("join_i64_hash", "hj_"),
-                   "scanexpr": ("scan_expr_i64_compaction", "select_kernel")}
+                   "scanexpr": ("scan_expr_i64_compaction", "select_kernel"),
+                   "q12join": ("tpch_q12_join", "select_kernel")}
 # sort: one step = every kernel of one MSD sort (2 histograms, 2 scatter levels, the
 # local sort and its fallback); traffic is summed per step (one local-sort launch per step)
 STEP_KERNEL = {"sort": "ms_local_kernel", "join": "hj_probe_kernel"}
@@ -32,7 +33,8 @@ def main():
     wl = args[args.index("--workload") + 1] if "--workload" in args else "q1"
     rows = float(args[args.index("--rows") + 1]) if "--rows" in args else {"q1": 1e9, "groupby": 1e9, "filter": 1e8,
                                                                            "sort": 1.25e9, "q12expr": 1e9,
-                                                                           "join": 1e9, "scanexpr": 1e8}[wl]
+                                                                           "join": 1e9, "scanexpr": 1e8,
+                                                                           "q12join": 1e9}[wl]
     name, match = WORKLOAD_KERNEL[wl]
     s = summarize(d, match, STEP_KERNEL.get(wl, ""))
     c = s["counters"]
