@@ -8,18 +8,23 @@
 //     8 (histogram) + 16 (level 0) + 8 (histogram) + 16 (level 1) + 16 (local) = 64 B/key
 // instead of 8 + 8 x 16 = 136 B/key.
 //
-//   * level histograms (ms_hist_kernel): one 256-bin LDS histogram per 64 Ki-key tile of a
-//     segment, flushed with 256 global atomics; the first also reduces OR / AND of all keys,
-//     whose XOR names the digits that vary (the others are skipped everywhere).
-//   * scatter levels (ms_scatter_kernel): keys only, so a level needs no stability — the
-//     local sort re-sorts every segment completely.  A tile (8192 keys) ranks its keys with
-//     LDS atomics (one per key, no ballots), stages them in LDS in digit order and claims
-//     each digit's output run with ONE global atomic on the segment's digit cursor: no
-//     look-back chain, no spin, progress independent of dispatch order.
-//   * local sort (ms_local_kernel): a segment of <= 32768 keys is loaded into registers
-//     (lo / hi 32-bit halves), sorted by its remaining varying digits with stable LSD passes
-//     entirely in LDS (ballot peer ranking, per-wave digit counters, exchange by halves so
-//     the exchange buffer is 4 B/key = 128 KiB), and written once, coalesced.
+//   * level histograms (ms_hist_kernel): one 512-bin LDS histogram per 64 Ki-key tile of a
+//     segment, flushed with global atomics; the first also reduces min / max, so the levels
+//     sort (key - base) by its varying bits (a narrow key range is rebased onto 0 and its
+//     first digit starts at the top bit of max - min).
+//   * plans (ms_plan_kernel): a level's per-segment digit counts become the next level's
+//     work lists (scatter again / local-sort size class) on the device.
+//   * scatter levels (ms_scatter_kernel): 9-bit digits, 16 Ki-key tiles, persistent; keys
+//     only, so a level needs no stability — the local sort re-sorts every segment.  A tile
+//     ranks its keys with LDS atomics (one per key), stages them in LDS in digit order and
+//     claims each digit's output run with ONE global atomic on the segment's digit cursor:
+//     no look-back chain, no spin, progress independent of dispatch order.
+//   * local sort (ms_local_kernel, three size classes): a segment's keys in registers are
+//     placed at their bucket positions (next varying bits) in LDS, every lane sorts one
+//     window of whole buckets with an in-register network (wider windows: half-wave /
+//     wave bitonic networks), and the segment is written once, coalesced.  Segments the
+//     windows cannot split (heavy duplicates) fall back to ms_lsd_kernel (stable LSD passes
+//     in LDS).
 // Keys map to u64 with the sign bit flipped (DESC: its complement) on the first load and
 // back on the final store.
 #include <algorithm>
