@@ -334,6 +334,8 @@ struct nut_plan {
   std::string jtable, talias, jalias;  // JOIN source; FROM / JOIN aliases (qualifiers)
   int jkey[2] = {-1, -1};  // plan columns of the ON equality
   std::deque<std::string> qnames;  // storage of qualified column names (column_ref)
+  // JOIN ... USING (u): the plain name u, and the qualified column it stands for
+  std::vector<std::pair<std::string, std::string>> using_cols;
 };
 
 struct nut_result {
@@ -1055,6 +1057,21 @@ bool lower_having(nut_plan &p, const Expr &e, HNode &h, Lowering &L) {
   return L.fail("unsupported HAVING term '" + expr_text(e) + "'");
 }
 
+PProg and_all(const std::vector<PProg> &cs);
+
+// ON a = b [AND c = d ...]: every equality of two columns, in order (the first is the hash
+// key, the rest residual equalities); false if the condition has any other shape
+bool on_equalities(nut_plan &p, const Expr &e, std::vector<std::pair<int, int>> &eqs) {
+  if (e.k == EK::BinaryOp && e.bop() == BinOp::And)
+    return on_equalities(p, e.kids[0], eqs) && on_equalities(p, e.kids[1], eqs);
+  sv ka, kb;
+  if (!(e.k == EK::BinaryOp && e.bop() == BinOp::Eq && column_ref(p, e.kids[0], ka) && column_ref(p, e.kids[1], kb)))
+    return false;
+  const int a = col_index(p, ka);
+  eqs.emplace_back(a, col_index(p, kb));
+  return true;
+}
+
 bool lower_mode(const Statement &st, nut_plan &p, Lowering &L) {
   if (st.k != StmtKind::Select) return L.fail("only SELECT statements execute");
   if (st.query.is_union) return L.fail("UNION/INTERSECT/EXCEPT are not executed (one query body per plan)");
@@ -1062,24 +1079,24 @@ bool lower_mode(const Statement &st, nut_plan &p, Lowering &L) {
   if (b.with) return L.fail("WITH is not executed");
   if (b.distinct && b.group_by) return L.fail("DISTINCT with GROUP BY is not executed");
   if (!b.from || b.from->k != SourceKind::Table) return L.fail("FROM must name one table");
+  std::vector<std::pair<int, int>> join_extra;  // residual ON equalities (INNER), applied as WHERE terms
   if (b.joins.size() > 1) {  // a chain of INNER joins: FROM t0 JOIN t1 ON .. JOIN t2 ON ..
     p.join = NUT_JOIN_INNER;
     if (b.from->alias) p.talias = std::string(*b.from->alias);
     for (const JoinClause &jc : b.joins) {
       if (jc.src.k != SourceKind::Table) return L.fail("JOIN source must be a table");
-      if (!jc.on) return L.fail("JOIN ... USING is not executed (ON a = b)");
+      if (!jc.on) return L.fail("JOIN ... USING in a chain of joins is not executed (ON a = b)");
       if (jc.t != JoinType::Inner) return L.fail("several JOINs: INNER only");
-      const Expr &cnd = jc.cond;
-      sv ka, kb;
-      if (!(cnd.k == EK::BinaryOp && cnd.bop() == BinOp::Eq && column_ref(p, cnd.kids[0], ka) &&
-            column_ref(p, cnd.kids[1], kb)))
-        return L.fail("JOIN ON must be one equality of two columns");
+      std::vector<std::pair<int, int>> eqs;
+      if (!on_equalities(p, jc.cond, eqs))
+        return L.fail("JOIN ON must be equalities of two columns (ANDed)");
       nut_plan::JoinStep js;
       js.table = std::string(jc.src.table);
       if (jc.src.alias) js.alias = std::string(*jc.src.alias);
-      js.key[0] = col_index(p, ka);
-      js.key[1] = col_index(p, kb);
+      js.key[0] = eqs[0].first;
+      js.key[1] = eqs[0].second;
       p.jn.push_back(js);
+      join_extra.insert(join_extra.end(), eqs.begin() + 1, eqs.end());
     }
     if (p.jn.size() > 7) return L.fail("at most 8 joined tables");
     p.jtable = p.jn[0].table;
@@ -1089,8 +1106,6 @@ bool lower_mode(const Statement &st, nut_plan &p, Lowering &L) {
   } else if (!b.joins.empty()) {
     const JoinClause &jc = b.joins[0];
     if (jc.src.k != SourceKind::Table) return L.fail("JOIN source must be a table");
-    if (!jc.on) return L.fail("JOIN ... USING is not executed (ON a = b)");
-    const Expr &cnd = jc.cond;
     switch (jc.t) {
       case JoinType::Inner: p.join = NUT_JOIN_INNER; break;
       case JoinType::LeftOuter: p.join = NUT_JOIN_LEFT; break;
@@ -1101,15 +1116,30 @@ bool lower_mode(const Statement &st, nut_plan &p, Lowering &L) {
       case JoinType::RightAnti: p.join = NUT_JOIN_ANTI, p.jright = true; break;
       default: return L.fail("FULL OUTER and ASOF JOIN are not executed");
     }
-    sv ka, kb;  // (p.join is set: qualified ON columns keep their qualifier)
-    if (!(cnd.k == EK::BinaryOp && cnd.bop() == BinOp::Eq && column_ref(p, cnd.kids[0], ka) &&
-          column_ref(p, cnd.kids[1], kb)))
-      return L.fail("JOIN ON must be one equality of two columns");
     p.jtable = std::string(jc.src.table);
     if (jc.src.alias) p.jalias = std::string(*jc.src.alias);
     if (b.from && b.from->alias) p.talias = std::string(*b.from->alias);
-    p.jkey[0] = col_index(p, ka);
-    p.jkey[1] = col_index(p, kb);
+    std::vector<std::pair<int, int>> eqs;  // (p.join is set: qualified ON columns keep their qualifier)
+    if (jc.on) {
+      if (!on_equalities(p, jc.cond, eqs)) return L.fail("JOIN ON must be equalities of two columns (ANDed)");
+    } else {
+      // USING (u, ...): u of the FROM table = u of the JOIN source; an unqualified u
+      // elsewhere in the query is the preserved table's (INNER: the FROM table's)
+      const std::string lq = p.talias.empty() ? std::string(b.from->table) : p.talias;
+      const std::string rq = p.jalias.empty() ? p.jtable : p.jalias;
+      for (const Identifier &u : jc.using_) {
+        const std::string un(u.name);
+        eqs.emplace_back(col_index(p, p.qnames.emplace_back(lq + "." + un)),
+                         col_index(p, p.qnames.emplace_back(rq + "." + un)));
+        p.using_cols.push_back({un, p.jright ? rq + "." + un : lq + "." + un});
+      }
+      if (eqs.empty()) return L.fail("JOIN ... USING () names no column");
+    }
+    if (eqs.size() > 1 && p.join != NUT_JOIN_INNER)
+      return L.fail("JOIN with several key columns: INNER only (outer / semi / anti joins take one ON equality)");
+    p.jkey[0] = eqs[0].first;
+    p.jkey[1] = eqs[0].second;
+    join_extra.insert(join_extra.end(), eqs.begin() + 1, eqs.end());
   }
   if (b.having && !b.group_by) return L.fail("HAVING needs GROUP BY");
   p.table = std::string(b.from->table);
@@ -1122,6 +1152,21 @@ bool lower_mode(const Statement &st, nut_plan &p, Lowering &L) {
     }
   } else if (b.where && !lower_where(p, *b.where, L)) {
     return false;
+  }
+  if (!join_extra.empty()) {  // the further key columns of the join: equalities above it
+    if (!p.compiled) return L.fail("JOIN with several key columns runs in expression mode");
+    std::vector<PProg> cs;
+    if (!p.where.empty()) cs.push_back(p.where);
+    for (const auto &e : join_extra) {
+      PNode a, c, eq;
+      a.op = NUT_P_COL;
+      a.col = e.first;
+      c.op = NUT_P_COL;
+      c.col = e.second;
+      eq.op = NUT_P_EQ;
+      cs.push_back(PProg{a, c, eq});
+    }
+    p.where = and_all(cs);
   }
   if (p.preds.size() > NUT_MAX_PRED) return L.fail("more than " + std::to_string(NUT_MAX_PRED) + " WHERE terms");
   if (b.limit) {
@@ -1247,9 +1292,19 @@ bool lower_mode(const Statement &st, nut_plan &p, Lowering &L) {
 // comparisons ANDed, the fused expression shapes); anything else — arbitrary
 // expressions, OR / NOT / CASE, column-to-column comparisons, more than 6 terms — to
 // expression programs compiled for the query (jit.cpp).  Scans stay on the filter kernel.
+// USING columns: an unqualified reference binds to the preserved table's column
+void resolve_using(nut_plan &p) {
+  for (const auto &u : p.using_cols)
+    for (std::string &c : p.cols)
+      if (ieq(c, u.first)) c = u.second;
+}
+
 bool lower(const Statement &st, nut_plan &p, Lowering &L) {
   Lowering L1;
-  if (lower_mode(st, p, L1)) return true;
+  if (lower_mode(st, p, L1)) {
+    resolve_using(p);
+    return true;
+  }
   bool agg = false;
   if (st.k == StmtKind::Select && !st.query.is_union && st.query.body) {
     const QueryBody &b = *st.query.body;
@@ -1262,6 +1317,7 @@ bool lower(const Statement &st, nut_plan &p, Lowering &L) {
   p2.compiled = true;
   Lowering L2;
   if (!lower_mode(st, p2, L2)) return L.fail(L2.err);
+  resolve_using(p2);
   p = std::move(p2);
   return true;
 }

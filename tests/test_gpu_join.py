@@ -376,3 +376,35 @@ def test_sql_three_table_join(ex, orc):
                  "group by c_nation order by c_nation", on_dev(ex, lines), right=[on_dev(ex, orders), on_dev(ex, cust)])
     assert got["c_nation"].tolist() == g.index.tolist()
     assert got["n"].tolist() == g.n.tolist() and got["q"].tolist() == g.q.tolist()
+
+
+def test_sql_join_using_and_multi_key(ex, orc):
+    """JOIN ... USING (k) (the shared name binds to the preserved table) and joins on two
+    key columns (USING (a, b) / ON a = b AND c = d: hash join on the first, the rest
+    filtered above the join) against pandas merges."""
+    rng = np.random.default_rng(71)
+    n1, n2 = 3000, 40_000
+    t1 = {"k": rng.permutation(n1).astype(np.int64), "s": rng.integers(0, 4, n1).astype(np.int64),
+          "v1": rng.integers(0, 100, n1).astype(np.int64)}
+    t2 = {"k": rng.integers(-100, n1 + 100, n2).astype(np.int64), "s": rng.integers(0, 4, n2).astype(np.int64),
+          "v2": rng.integers(0, 100, n2).astype(np.int64)}
+    d1, d2 = pd.DataFrame(t1), pd.DataFrame(t2)
+    got = ex.sql("select k, count(*) as c, sum(v2) as s2 from t1 join t2 using (k) where k < 1000 "
+                 "group by k order by k", on_dev(ex, t1), right=on_dev(ex, t2))
+    m = d1.merge(d2, on="k")
+    g = m[m.k < 1000].groupby("k").agg(c=("v2", "size"), s2=("v2", "sum"))
+    assert got["k"].tolist() == g.index.tolist() and got["c"].tolist() == g.c.tolist()
+    assert got["s2"].tolist() == g.s2.tolist()
+    m2 = d1.merge(d2, on=["k", "s"])
+    for sql in ("select s, count(*) as c, sum(v1) as a, sum(v2) as b from t1 join t2 using (k, s) group by s order by s",
+                "select t1.s, count(*) as c, sum(v1) as a, sum(v2) as b from t1 join t2 on t1.k = t2.k and t1.s = t2.s "
+                "group by t1.s order by t1.s"):
+        got = ex.sql(sql, on_dev(ex, t1), right=on_dev(ex, t2))
+        g = m2.groupby("s").agg(c=("v1", "size"), a=("v1", "sum"), b=("v2", "sum"))
+        vals = list(got.values())
+        assert vals[0].tolist() == g.index.tolist(), sql
+        assert vals[1].tolist() == g.c.tolist() and vals[2].tolist() == g.a.tolist() and vals[3].tolist() == g.b.tolist()
+    # LEFT JOIN USING: the unmatched FROM rows count, their k is the FROM table's
+    got = ex.sql("select count(*) as c, sum(k) as sk from t2 left join t1 using (k)", on_dev(ex, t2),
+                 right=on_dev(ex, t1))
+    assert got["c"].tolist() == [n2] and got["sk"].tolist() == [int(t2["k"].sum())]

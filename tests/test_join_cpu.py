@@ -71,9 +71,11 @@ def test_sql_no_join_has_no_join_key():
 
 @pytest.mark.parametrize("sql,msg", [
     ("select count(*) from a full join b on x = y", "FULL OUTER"),
-    ("select count(*) from a join b using (x)", "USING"),
-    ("select count(*) from a join b on x < y", "one equality"),
-    ("select count(*) from a join b on x = y and u = v", "one equality"),
+    ("select count(*) from a join b on x < y", "equalities of two columns"),
+    ("select count(*) from a join b on x = y and u < v", "equalities of two columns"),
+    ("select count(*) from a left join b on x = y and u = v", "INNER only"),
+    ("select count(*) from a left semi join b using (x, y)", "INNER only"),
+    ("select count(*) from a join b using (x) join c using (x)", "USING in a chain"),
     ("select count(*) from a join b on x = y full join c on y = z", "INNER only"),
     ("select count(*) from a join (select x from b) on x = y", "must be a table")])
 def test_sql_join_rejections(sql, msg):
@@ -125,3 +127,21 @@ def test_sql_join_chain_lowering():
     from nutdb_amd import NutError
     with pytest.raises(NutError, match="INNER only"):
         Plan("select count(*) from a join b on x = y left join c on y = z")
+
+
+def test_sql_join_using_and_multi_key_lowering():
+    """USING (u): the FROM table's u = the source's u, an unqualified u elsewhere is the
+    preserved table's; further key columns (USING (a, b), ON a = b AND c = d) join on the
+    first and filter the pairs by the rest above the join (INNER)."""
+    from nutdb_amd.sql import Plan
+    d = Plan("select k, count(*) from orders join lineitem using (k) group by k").describe()
+    assert d["join"]["on"] == ["orders.k", "lineitem.k"] and d["keys"] == ["orders.k"]
+    d = Plan("select sum(v) from orders as o right join lineitem as l using (k) where k > 3").describe()
+    assert d["join"]["on"] == ["o.k", "l.k"] and d["join"]["right"] is True
+    assert "l.k" in d["columns"] and "k" not in d["columns"]
+    d = Plan("select count(*) from a join b using (x, y)").describe()
+    assert d["join"]["on"] == ["a.x", "b.x"] and d["mode"] == "compiled" and d["where_expr"] == "(a.y = b.y)"
+    d = Plan("select count(*) from a join b on a.x = b.x and a.y = b.y where a.z > 1").describe()
+    assert d["join"]["on"] == ["a.x", "b.x"] and d["where_expr"] == "((a.z > 1) and (a.y = b.y))"
+    d = Plan("select count(*) from l join o on lk = ok join c on oc = ck and on_ = cn").describe()
+    assert d["joins"][1] == {"table": "c", "on": ["oc", "ck"]} and d["where_expr"] == "(on_ = cn)"
