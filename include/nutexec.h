@@ -479,9 +479,14 @@ typedef enum { NUT_PLAN_FILTER = 0, NUT_PLAN_GROUPBY = 1, NUT_PLAN_SORT = 2 } nu
 
 typedef struct {
   const char *name;   /* column name as written in the SQL (ASCII case-insensitive match) */
-  const void *data;   /* device pointer, nrows elements */
-  int32_t type;       /* nut_type */
+  const void *data;   /* device pointer, nrows elements (host pointer with NUT_COL_HOST) */
+  int32_t type;       /* nut_type, optionally | NUT_COL_HOST */
 } nut_column;
+/* OR-ed into nut_column.type: `data` is host memory (pageable or page-locked).  The
+ * nut_plan_execute* calls copy such a column into HBM on the context's stream (8 B x nrows
+ * over PCIe) before running the plan and free the copy before they return; the caller
+ * keeps ownership.  Device-resident columns are read in place. */
+#define NUT_COL_HOST 0x100
 
 nut_status nut_sql_plan(const char *sql, size_t len, nut_plan **out);
 int nut_plan_kind_of(const nut_plan *plan);

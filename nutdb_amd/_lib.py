@@ -29,6 +29,7 @@ NUT_MAX_PROG_NODES = 256
 NUT_OK = 0
 NUT_ERR_CAPACITY = 5
 NUT_JOIN_ANY_ORDER = 0x100
+NUT_COL_HOST = 0x100
 STATUS_NAMES = {
     0: "NUT_OK", 1: "NUT_ERR_INVALID_ARG", 2: "NUT_ERR_HIP", 3: "NUT_ERR_OOM",
     4: "NUT_ERR_UNSUPPORTED", 5: "NUT_ERR_CAPACITY", 6: "NUT_ERR_PARSE", 7: "NUT_ERR_PLAN",

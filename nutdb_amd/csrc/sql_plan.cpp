@@ -2729,6 +2729,31 @@ nut_status exec_joinn(nut_ctx *c, const nut_plan &p, const nut_column *const *ta
   return st;
 }
 
+// NUT_COL_HOST columns: copied into stream-ordered HBM for one execute call
+struct HostStage {
+  std::vector<nut_column> cols;
+  std::deque<DevBuf> bufs;
+};
+
+nut_status stage_host(nut_ctx *c, const nut_column *cols, int n, uint64_t rows, HostStage &hs, const nut_column **out) {
+  *out = cols;
+  bool any = false;
+  for (int i = 0; i < n; ++i) any = any || (cols[i].type & NUT_COL_HOST);
+  if (!any) return NUT_OK;
+  hs.cols.assign(cols, cols + n);
+  for (nut_column &col : hs.cols) {
+    if (!(col.type & NUT_COL_HOST)) continue;
+    col.type &= ~NUT_COL_HOST;
+    if (!rows || !col.data) continue;
+    hs.bufs.emplace_back();
+    NUT_HIP(hs.bufs.back().alloc(c, rows * 8));
+    NUT_HIP(hipMemcpyAsync(hs.bufs.back().p, col.data, rows * 8, hipMemcpyHostToDevice, c->stream));
+    col.data = hs.bufs.back().p;
+  }
+  *out = hs.cols.data();
+  return NUT_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -2830,6 +2855,10 @@ nut_status nut_plan_execute(nut_ctx *c, const nut_plan *p, const nut_column *col
   if (!c || !p || !out || (ncols && !cols) || ncols < 0) return fail(NUT_ERR_INVALID_ARG, "nut_plan_execute: NULL argument");
   *out = nullptr;
   if (p->join >= 0) return fail(NUT_ERR_INVALID_ARG, "nut_plan_execute: the plan has a JOIN (nut_plan_execute2)");
+  DeviceGuard g0(c->device);
+  HostStage hs;
+  nut_status hst = stage_host(c, cols, ncols, nrows, hs, &cols);
+  if (hst) return hst;
   std::vector<const nut_column *> bound(p->cols.size());
   for (size_t i = 0; i < p->cols.size(); ++i) {
     bound[i] = bind(*p, (int)i, cols, ncols);
@@ -2862,12 +2891,16 @@ nut_status nut_plan_execute2(nut_ctx *c, const nut_plan *p, const nut_column *le
   if (p->join < 0) return nut_plan_execute(c, p, left, nleft, lrows, group_hint, out);
   if (!p->jn.empty()) return fail(NUT_ERR_INVALID_ARG, "nut_plan_execute2: the plan joins several tables (nut_plan_executen)");
   *out = nullptr;
+  DeviceGuard g(c->device);
+  HostStage hl, hr;
+  nut_status st = stage_host(c, left, nleft, lrows, hl, &left);
+  if (!st) st = stage_host(c, right, nright, rrows, hr, &right);
+  if (st) return st;
   nut_result *r = new (std::nothrow) nut_result;
   if (!r) return fail(NUT_ERR_OOM, "nut_plan_execute2: out of host memory");
   r->kind = p->kind;
   r->device = c->device;
-  DeviceGuard g(c->device);
-  nut_status st = exec_join(c, *p, left, nleft, lrows, right, nright, rrows, group_hint, r);
+  st = exec_join(c, *p, left, nleft, lrows, right, nright, rrows, group_hint, r);
   if (st) {
     nut_result_free(r);
     return st;
@@ -2887,12 +2920,19 @@ nut_status nut_plan_executen(nut_ctx *c, const nut_plan *p, const nut_column *co
     return fail(NUT_ERR_INVALID_ARG, "nut_plan_executen: the plan joins fewer tables");
   }
   *out = nullptr;
+  DeviceGuard g(c->device);
+  std::deque<HostStage> hs(ntables);
+  std::vector<const nut_column *> tabs(tables, tables + ntables);
+  for (int k = 0; k < ntables; ++k) {
+    if (ncols[k] && !tables[k]) return fail(NUT_ERR_INVALID_ARG, "nut_plan_executen: NULL table");
+    nut_status hst = stage_host(c, tables[k], ncols[k], nrows[k], hs[k], &tabs[k]);
+    if (hst) return hst;
+  }
   nut_result *r = new (std::nothrow) nut_result;
   if (!r) return fail(NUT_ERR_OOM, "nut_plan_executen: out of host memory");
   r->kind = p->kind;
   r->device = c->device;
-  DeviceGuard g(c->device);
-  nut_status st = exec_joinn(c, *p, tables, ncols, nrows, ntables, group_hint, r);
+  nut_status st = exec_joinn(c, *p, tabs.data(), ncols, nrows, ntables, group_hint, r);
   if (st) {
     nut_result_free(r);
     return st;
@@ -2905,9 +2945,13 @@ nut_status nut_plan_prepare(const nut_plan *p, const nut_column *cols, int ncols
   if (!p || (ncols && !cols) || ncols < 0) return fail(NUT_ERR_INVALID_ARG, "nut_plan_prepare: NULL argument");
   if (!p->compiled) return NUT_OK;  // precompiled kernels only
   std::vector<const nut_column *> bound(p->cols.size());
+  std::vector<nut_column> typed(p->cols.size());
   for (size_t i = 0; i < p->cols.size(); ++i) {
     bound[i] = bind(*p, (int)i, cols, ncols);
     if (!bound[i]) return fail(NUT_ERR_INVALID_ARG, "nut_plan_prepare: column '" + p->cols[i] + "' is not bound");
+    typed[i] = *bound[i];
+    typed[i].type &= ~NUT_COL_HOST;  // only the type matters here
+    bound[i] = &typed[i];
     if (bound[i]->type != NUT_T_I64 && bound[i]->type != NUT_T_F64)
       return fail(NUT_ERR_INVALID_ARG, "nut_plan_prepare: column '" + p->cols[i] + "' has an unknown type");
   }

@@ -23,7 +23,7 @@ from typing import Dict, List, Optional, Tuple
 
 import numpy as np
 
-from ._lib import (NUT_OK, STMT_KINDS, TOKEN_TYPES, NutColumn, NutError, T_F64, T_I64, T_STR, check, lib)
+from ._lib import (NUT_COL_HOST, NUT_OK, STMT_KINDS, TOKEN_TYPES, NutColumn, NutError, T_F64, T_I64, T_STR, check, lib)
 
 NUT_ERR_PARSE = 6
 NUT_ERR_CAPACITY = 5
@@ -233,8 +233,12 @@ class Plan:
         keep = []
         n = None
         for i, (name, t) in enumerate(columns.items()):
-            if not isinstance(t, torch.Tensor) or not t.is_cuda or t.dim() != 1 or not t.is_contiguous():
-                raise ValueError(f"column {name!r} must be a contiguous 1-D CUDA tensor")
+            host = isinstance(t, np.ndarray) or (isinstance(t, torch.Tensor) and not t.is_cuda)
+            if host:  # host memory: the library copies it into HBM for the call (NUT_COL_HOST)
+                t = torch.from_numpy(np.ascontiguousarray(t)) if isinstance(t, np.ndarray) else t.contiguous()
+                keep.append(t)
+            if not isinstance(t, torch.Tensor) or t.dim() != 1 or not t.is_contiguous():
+                raise ValueError(f"column {name!r} must be a contiguous 1-D CUDA tensor or host array")
             if t.dtype == torch.int64:
                 typ = T_I64
             elif t.dtype == torch.float64:
@@ -243,7 +247,7 @@ class Plan:
                 raise ValueError(f"column {name!r}: dtype {t.dtype} is not int64/float64")
             nb = name.encode()
             keep.append(nb)
-            arr[i] = NutColumn(nb, t.data_ptr(), typ)
+            arr[i] = NutColumn(nb, t.data_ptr(), typ | (NUT_COL_HOST if host else 0))
             low = name.lower()
             if any(low == c.lower() or c.lower().endswith("." + low) for c in names):  # JOIN plans qualify
                 n = t.numel() if n is None else n

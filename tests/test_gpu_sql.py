@@ -215,3 +215,28 @@ def test_sql_in_lists(ex):
     g = ex.groupby(AggQuery(keys=[t["k"]], aggs=[Agg("count")], preds=[(t["k"], "in", [1, 2, 3])]))
     keys, words = g.to_host_words()
     assert keys[:, 0].tolist() == [1, 2, 3] and words[:, 0].tolist() == [int((k == x).sum()) for x in (1, 2, 3)]
+
+
+def test_sql_host_resident_columns(ex):
+    """nut_column tagged NUT_COL_HOST (numpy arrays here): the library copies them into HBM
+    for the call; results equal the device-resident run, for a group-by, an ORDER BY scan
+    and a JOIN with one host and one device table."""
+    rng = np.random.default_rng(81)
+    n = 1_000_003
+    k = rng.integers(0, 100, n).astype(np.int64)
+    v = rng.integers(-1000, 1000, n).astype(np.float64) / 8.0
+    w = rng.integers(0, 1 << 40, n).astype(np.int64)
+    host = {"k": k, "v": v, "w": w}
+    devc = {name: torch.from_numpy(a).to(ex.device) for name, a in host.items()}
+    for sql in ("select k, sum(v) as s, count(*) as c, max(w) as m from t where w > 1000 group by k order by k",
+                "select w, v from t where k < 3 order by v desc, w limit 1000",
+                "select sum(v * 2) as s from t where k % 7 = 1 or w < 12345"):
+        a, b = ex.sql(sql, host), ex.sql(sql, devc)
+        for c in b:
+            assert a[c].tolist() == b[c].tolist(), (sql, c)
+    dim = {"dk": np.arange(100, dtype=np.int64), "dv": np.arange(100, dtype=np.int64) * 3}
+    sql = "select dv, count(*) as c from t join dim on k = dk where w > 5000 group by dv order by dv"
+    a = ex.sql(sql, host, right={n_: torch.from_numpy(x).to(ex.device) for n_, x in dim.items()})
+    b = ex.sql(sql, devc, right=dim)
+    m = w > 5000
+    assert a["c"].tolist() == b["c"].tolist() == np.bincount(k[m], minlength=100).tolist()
