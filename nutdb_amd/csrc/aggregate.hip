@@ -1059,7 +1059,9 @@ nut_status nut_select_rows(nut_ctx *c, const nut_agg_spec *s, int64_t *out_rows,
   size_t asz = sizeof sa;
   void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &sa, HIP_LAUNCH_PARAM_BUFFER_SIZE, &asz, HIP_LAUNCH_PARAM_END};
   c->timer.begin(c->stream, NUT_KERNEL_FILTER);
-  hipError_t e = hipModuleLaunchKernel(fn, (unsigned)ntiles, 1, 1, SEL_THREADS, 1, 1, 0, c->stream, nullptr, cfg);
+  // persistent workgroups (tiles by ticket): enough for full occupancy, never more than tiles
+  const unsigned grid = (unsigned)std::min<uint64_t>(ntiles, (uint64_t)c->num_cus * 8);
+  hipError_t e = hipModuleLaunchKernel(fn, grid, 1, 1, SEL_THREADS, 1, 1, 0, c->stream, nullptr, cfg);
   c->timer.end(c->stream);
   if (e != hipSuccess) return hip_fail(e, "hipModuleLaunchKernel (select kernel)");
   NUT_HIP(hipMemcpyAsync(c->host_pinned, base, 16, hipMemcpyDeviceToHost, c->stream));

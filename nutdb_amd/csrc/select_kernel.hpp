@@ -2,12 +2,15 @@
 //   SELECT ... FROM t WHERE <any expression program>
 // The WHERE program is the same generated kProg shape the expression-mode group-by uses
 // (jit.cpp: where(p, v, r, err)), compiled into this kernel with hipRTC.  The kernel writes
-// the row ids of the selected rows in row order (order-preserving stream compaction, the
-// filter's scheme, csrc/filter.hip): a 512-thread workgroup takes a tile of 16384 rows by
-// atomic ticket, evaluates the program on 32 striped rows per lane (the generated code
-// reads only the columns the program names), ranks the selected rows with ballots, and
-// takes its global offset by decoupled look-back (lookback.hpp).  Callers gather any
-// column through the row ids (nut_gather_u64: ascending ids, near-sequential reads).
+// the row ids of the selected rows in row order (order-preserving stream compaction): a
+// 512-thread workgroup takes tiles of 16384 rows by atomic ticket, evaluates the program on
+// 32 striped rows per lane (the generated code reads only the columns the program names)
+// and ranks the selected rows with ballots.  A tile's state after evaluation is one
+// selection word per lane, so the workgroup is persistent and one tile ahead: it publishes
+// tile t's count, evaluates tile t+1 (its HBM reads), and only then resolves t's global
+// offset by decoupled look-back (lookback.hpp) and writes t's row ids — the look-back
+// round trips overlap the next tile's reads instead of idling the workgroup.  Callers
+// gather any column through the row ids (nut_gather_u64: ascending ids, near-sequential).
 #pragma once
 
 #include "agg_ops.hpp"
@@ -31,58 +34,80 @@ struct SelArgs {
 
 template <class S>
 __global__ __launch_bounds__(SEL_THREADS) void select_kernel(SelArgs sa) {
-  __shared__ uint32_t s_cnt[SEL_ITEMS][SEL_WAVES];
+  __shared__ uint32_t s_cnt[2][SEL_ITEMS][SEL_WAVES];
+  __shared__ uint32_t s_tile[2];
   __shared__ uint64_t s_excl;
-  __shared__ uint32_t s_tile;
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
-  if (tid == 0) s_tile = atomicAdd(sa.ticket, 1u);
-  __syncthreads();
-  const uint32_t tile = s_tile;
   const uint64_t n = sa.a.n;
-  const uint64_t base = (uint64_t)tile * SEL_TILE + tid;
-  uint32_t sel = 0;
-  bool err = false;
+  // evaluate tile t into a selection word; per-(item, wave) counts into s_cnt[b]
+  auto eval = [&](uint32_t t, int b) -> uint32_t {
+    const uint64_t base = (uint64_t)t * SEL_TILE + tid;
+    uint32_t sel = 0;
+    bool err = false;
 #pragma unroll
-  for (int i = 0; i < SEL_ITEMS; ++i) {
-    const uint64_t r = base + (uint64_t)i * SEL_THREADS;
-    const bool ok = r < n;
-    uint64_t vv[S::MV > 0 ? S::MV : 1][1];
+    for (int i = 0; i < SEL_ITEMS; ++i) {
+      const uint64_t r = base + (uint64_t)i * SEL_THREADS;
+      const bool ok = r < n;
+      uint64_t vv[S::MV > 0 ? S::MV : 1][1];
 #pragma unroll
-    for (int c = 0; c < S::MV; ++c) vv[c][0] = ok ? __builtin_nontemporal_load(sa.a.val_col[c] + r) : 0;
-    bool e = false;
-    const bool w = S::where(sa.a, vv, 0, e) && ok;
-    err = err || (e && ok);
-    sel |= (w ? 1u : 0u) << i;
-    const uint64_t b = __ballot(w);
-    if (lane == 0) s_cnt[i][wave] = (uint32_t)__popcll(b);
-  }
-  if (__any(err) && lane == 0) atomicOr(sa.ticket + 1, 2u);
-  __syncthreads();
-  if (wave == 0) {
-    uint32_t c = 0;
-#pragma unroll
-    for (int k = lane; k < SEL_ITEMS * SEL_WAVES; k += kWave) c += (&s_cnt[0][0])[k];
-    const uint64_t total = wave_sum_u64(c);
-    const uint64_t excl = lookback(sa.status, tile, total, sa.ticket + 1, lane);
-    if (lane == 0) {
-      s_excl = excl;
-      if (tile == sa.ntiles - 1) *sa.out_n = excl + total;
+      for (int c = 0; c < S::MV; ++c) vv[c][0] = ok ? __builtin_nontemporal_load(sa.a.val_col[c] + r) : 0;
+      bool e = false;
+      const bool w = S::where(sa.a, vv, 0, e) && ok;
+      err = err || (e && ok);
+      sel |= (w ? 1u : 0u) << i;
+      const uint64_t bb = __ballot(w);
+      if (lane == 0) s_cnt[b][i][wave] = (uint32_t)__popcll(bb);
     }
-  }
+    if (__any(err) && lane == 0) atomicOr(sa.ticket + 1, 2u);
+    return sel;
+  };
+  if (tid == 0) s_tile[0] = atomicAdd(sa.ticket, 1u);
   __syncthreads();
-  uint64_t off = s_excl;
+  uint32_t tile = s_tile[0];
+  if (tile >= sa.ntiles) return;
+  int b = 0;
+  uint32_t sel = eval(tile, b);
+  for (;;) {
+    __syncthreads();  // s_cnt[b] complete
+    uint64_t total = 0;
+    if (wave == 0) {
+      uint32_t c = 0;
 #pragma unroll
-  for (int i = 0; i < SEL_ITEMS; ++i) {
-    uint32_t before = 0, all = 0;
-#pragma unroll
-    for (int w = 0; w < SEL_WAVES; ++w) {
-      before += w < wave ? s_cnt[i][w] : 0u;
-      all += s_cnt[i][w];
+      for (int k = lane; k < SEL_ITEMS * SEL_WAVES; k += kWave) c += (&s_cnt[b][0][0])[k];
+      total = wave_sum_u64(c);
+      if (lane == 0) lookback_publish(sa.status, tile, total);
     }
-    const bool w = (sel >> i) & 1u;
-    const uint64_t b = __ballot(w);
-    if (w) sa.out[off + before + lane_rank(b)] = (int64_t)(base + (uint64_t)i * SEL_THREADS);
-    off += all;
+    if (tid == kWave) s_tile[b ^ 1] = atomicAdd(sa.ticket, 1u);
+    __syncthreads();
+    const uint32_t next = s_tile[b ^ 1];
+    const uint32_t sel_next = next < sa.ntiles ? eval(next, b ^ 1) : 0u;
+    if (wave == 0) {
+      const uint64_t excl = lookback_resolve(sa.status, tile, total, sa.ticket + 1, lane);
+      if (lane == 0) {
+        s_excl = excl;
+        if (tile == sa.ntiles - 1) *sa.out_n = excl + total;
+      }
+    }
+    __syncthreads();
+    const uint64_t base = (uint64_t)tile * SEL_TILE + tid;
+    uint64_t off = s_excl;
+#pragma unroll
+    for (int i = 0; i < SEL_ITEMS; ++i) {
+      uint32_t before = 0, all = 0;
+#pragma unroll
+      for (int w = 0; w < SEL_WAVES; ++w) {
+        before += w < wave ? s_cnt[b][i][w] : 0u;
+        all += s_cnt[b][i][w];
+      }
+      const bool w = (sel >> i) & 1u;
+      const uint64_t bb = __ballot(w);
+      if (w) sa.out[off + before + lane_rank(bb)] = (int64_t)(base + (uint64_t)i * SEL_THREADS);
+      off += all;
+    }
+    if (next >= sa.ntiles) break;
+    tile = next;
+    sel = sel_next;
+    b ^= 1;
   }
 }
 

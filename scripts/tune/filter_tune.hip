@@ -62,7 +62,7 @@ __device__ uint64_t lookback(uint64_t *__restrict__ status, uint32_t tile, uint6
 
 // THREADS x (STRIPES x 2 rows) per tile.  LDS: stage the tile's selected values and
 // write them out contiguously.  NT: non-temporal loads.
-template <int THREADS, int STRIPES, bool LDS, bool NT, int SLEEP, bool TICKET = true, int LB = 1, int MODE = 0>
+template <int THREADS, int STRIPES, bool LDS, bool NT, int SLEEP, bool TICKET = true, int LB = 1, int MODE = 0, bool NTS = false>
 __global__ __launch_bounds__(THREADS) void filt(const int64_t *__restrict__ col, uint64_t n, int64_t k,
                                                 int64_t *__restrict__ out, uint64_t *__restrict__ out_n,
                                                 uint32_t *__restrict__ ticket, uint64_t *__restrict__ status,
@@ -118,7 +118,7 @@ __global__ __launch_bounds__(THREADS) void filt(const int64_t *__restrict__ col,
     uint32_t c = 0;
     for (int i = lane; i < STRIPES * WAVES; i += 64) c += (&s_cnt[0][0])[i];
     uint64_t total = wave_sum_u64(c);
-    uint64_t excl = MODE == 1 ? base : lookback<LB>(status, tile, total, lane, SLEEP);
+    uint64_t excl = (MODE == 1 || MODE == 3) ? base : lookback<LB>(status, tile, total, lane, SLEEP);
     if (lane == 0) {
       s_excl = excl;
       s_total = total;
@@ -154,9 +154,14 @@ __global__ __launch_bounds__(THREADS) void filt(const int64_t *__restrict__ col,
       for (int w = 0; w < WAVES; ++w) before += (w < wave) ? s_cnt[j][w] : 0u;
       uint64_t pos = off + before + r0[j];
       bool p0 = (sel >> (2 * j)) & 1u, p1 = (sel >> (2 * j + 1)) & 1u;
-      if (MODE != 2) {
-        if (p0) out[pos] = v0[j];
-        if (p1) out[pos + (p0 ? 1 : 0)] = v1[j];
+      if (MODE != 2 && MODE != 3) {
+        if (NTS) {
+          if (p0) __builtin_nontemporal_store(v0[j], &out[pos]);
+          if (p1) __builtin_nontemporal_store(v1[j], &out[pos + (p0 ? 1 : 0)]);
+        } else {
+          if (p0) out[pos] = v0[j];
+          if (p1) out[pos + (p0 ? 1 : 0)] = v1[j];
+        }
       }
 #pragma unroll
       for (int w = 0; w < WAVES; ++w) off += s_cnt[j][w];
@@ -179,7 +184,7 @@ __global__ void copyk(const int64_t *__restrict__ a, int64_t *__restrict__ b, ui
 // better copy: 4 x 16 B loads in flight per thread, grid-stride
 __global__ __launch_bounds__(256) void copy4(const int64_t *__restrict__ a, int64_t *__restrict__ b, uint64_t n) {
   const uint64_t stride = (uint64_t)gridDim.x * 256 * 8;
-  for (uint64_t i = (blockIdx.x * 256ull + threadIdx.x) * 2; i < n; i += stride) {
+  for (uint64_t i = blockIdx.x * 2048ull + threadIdx.x * 2; i < n; i += stride) {
     i64x2 v[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -190,6 +195,35 @@ __global__ __launch_bounds__(256) void copy4(const int64_t *__restrict__ a, int6
     for (int j = 0; j < 4; ++j) {
       uint64_t q = i + (uint64_t)j * 512;
       if (q + 1 < n && (j & 1) == 0) *reinterpret_cast<i64x2 *>(b + q / 2) = v[j] + v[j + 1];
+    }
+  }
+}
+
+// read 8n, write 4n (every other 16-B vector): the HBM ceiling for a 2:1 read:write stream
+template <int LOADS, bool NTL, bool NTS>
+__global__ __launch_bounds__(256) void copyN(const int64_t *__restrict__ a, int64_t *__restrict__ b, uint64_t n) {
+  const uint64_t stride = (uint64_t)gridDim.x * 512 * LOADS;
+  for (uint64_t i = blockIdx.x * 512ull * LOADS + threadIdx.x * 2; i < n; i += stride) {
+    i64x2 v[LOADS];
+#pragma unroll
+    for (int j = 0; j < LOADS; ++j) {
+      uint64_t q = i + (uint64_t)j * 512;
+      if (NTL)
+        v[j] = q + 1 < n ? __builtin_nontemporal_load(reinterpret_cast<const i64x2 *>(a + q)) : i64x2{0, 0};
+      else
+        v[j] = q + 1 < n ? *reinterpret_cast<const i64x2 *>(a + q) : i64x2{0, 0};
+    }
+#pragma unroll
+    for (int j = 0; j < LOADS; j += 2) {
+      uint64_t q = i + (uint64_t)j * 512;
+      i64x2 w = v[j] + v[j + 1];
+      i64x2 *d = reinterpret_cast<i64x2 *>(b + (q - threadIdx.x * 2) / 2 + threadIdx.x * 2);
+      if (q + 1 < n) {
+        if (NTS)
+          __builtin_nontemporal_store(w, d);
+        else
+          *d = w;
+      }
     }
   }
 }
@@ -210,7 +244,7 @@ __global__ void checksum(const int64_t *o, uint64_t n, unsigned long long *h) {
     }                                                                          \
   } while (0)
 
-template <int THREADS, int STRIPES, bool LDS, bool NT, int SLEEP, bool TICKET = true, int LB = 1, int MODE = 0>
+template <int THREADS, int STRIPES, bool LDS, bool NT, int SLEEP, bool TICKET = true, int LB = 1, int MODE = 0, bool NTS = false>
 void run(const char *name, const int64_t *col, uint64_t n, int64_t k, int64_t *out, uint64_t *dn, void *state,
          int R, unsigned long long *dh) {
   constexpr int TILE = THREADS * 2 * STRIPES;
@@ -223,7 +257,7 @@ void run(const char *name, const int64_t *col, uint64_t n, int64_t k, int64_t *o
   for (int r = 0; r < R + 2; ++r) {
     CK(hipMemsetAsync(state, 0, sb, 0));
     CK(hipEventRecord(a, 0));
-    hipLaunchKernelGGL((filt<THREADS, STRIPES, LDS, NT, SLEEP, TICKET, LB, MODE>), dim3(ntiles), dim3(THREADS), 0, 0, col, n, k, out, dn,
+    hipLaunchKernelGGL((filt<THREADS, STRIPES, LDS, NT, SLEEP, TICKET, LB, MODE, NTS>), dim3(ntiles), dim3(THREADS), 0, 0, col, n, k, out, dn,
                        (uint32_t *)state, (uint64_t *)((char *)state + 16), ntiles);
     CK(hipEventRecord(b, 0));
     CK(hipEventSynchronize(b));
@@ -518,6 +552,294 @@ void run_w(const char *name, const int64_t *col, uint64_t n, int64_t k, int64_t 
          (unsigned long long)cnt, h);
 }
 
+// persistent + ticketed + software-pipelined: a workgroup publishes tile t's aggregate,
+// takes its next ticket and issues that tile's loads BEFORE resolving t's look-back, so the
+// look-back round trips overlap the next tile's HBM reads.  Wave 0 resolves first and loads
+// its share of the next tile afterwards (its vmcnt holds no data loads while it spins).
+template <int THREADS, int STRIPES, int OCC>
+__global__ __launch_bounds__(THREADS, OCC) void filt_q(const int64_t *__restrict__ col, uint64_t n, int64_t k,
+                                                     int64_t *__restrict__ out, uint64_t *__restrict__ out_n,
+                                                     uint32_t *__restrict__ ticket, uint64_t *__restrict__ status,
+                                                     uint32_t ntiles) {
+  constexpr int WAVES = THREADS / kWave;
+  constexpr int SROWS = THREADS * 2;
+  constexpr int TILE = SROWS * STRIPES;
+  __shared__ uint32_t s_cnt[STRIPES][WAVES];
+  __shared__ uint32_t s_next;
+  __shared__ uint64_t s_excl;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  i64x2 cur[STRIPES], nxt[STRIPES];
+  auto load = [&](i64x2(&v)[STRIPES], uint32_t t) {
+    const uint64_t base = (uint64_t)t * TILE;
+    if (base + TILE <= n) {
+#pragma unroll
+      for (int j = 0; j < STRIPES; ++j)
+        v[j] = __builtin_nontemporal_load(reinterpret_cast<const i64x2 *>(col + base + j * SROWS + 2 * tid));
+    } else {
+#pragma unroll
+      for (int j = 0; j < STRIPES; ++j) {
+        const uint64_t idx = base + j * SROWS + 2 * tid;
+        v[j].x = idx < n ? col[idx] : 0;
+        v[j].y = idx + 1 < n ? col[idx + 1] : 0;
+      }
+    }
+  };
+  if (tid == 0) s_next = atomicAdd(ticket, 1u);
+  __syncthreads();
+  uint32_t tile = s_next;
+  if (tile >= ntiles) return;
+  load(cur, tile);
+  for (;;) {
+    const uint64_t base = (uint64_t)tile * TILE;
+    const bool full = base + TILE <= n;
+    uint32_t r0[STRIPES];
+    uint32_t sel = 0;
+#pragma unroll
+    for (int j = 0; j < STRIPES; ++j) {
+      const uint64_t idx = base + j * SROWS + 2 * tid;
+      bool p0 = cur[j].x < k && (full || idx < n);
+      bool p1 = cur[j].y < k && (full || idx + 1 < n);
+      uint64_t b0 = __ballot(p0), b1 = __ballot(p1);
+      r0[j] = lane_rank(b0) + lane_rank(b1);
+      sel |= (p0 ? 1u : 0u) << (2 * j);
+      sel |= (p1 ? 1u : 0u) << (2 * j + 1);
+      if (lane == 0) s_cnt[j][wave] = (uint32_t)(__popcll(b0) + __popcll(b1));
+    }
+    if (tid == 64) s_next = atomicAdd(ticket, 1u);
+    __syncthreads();
+    const uint32_t tn = s_next;
+    if (wave == 0) {
+      uint32_t c = 0;
+      for (int i = lane; i < STRIPES * WAVES; i += 64) c += (&s_cnt[0][0])[i];
+      uint64_t total = wave_sum_u64(c);
+      uint64_t excl = lookback<1>(status, tile, total, lane, 1);
+      if (lane == 0) {
+        s_excl = excl;
+        if (tile == ntiles - 1) *out_n = excl + total;
+      }
+    }
+    if (tn < ntiles) load(nxt, tn);
+    __syncthreads();
+    uint64_t off = s_excl;
+#pragma unroll
+    for (int j = 0; j < STRIPES; ++j) {
+      uint64_t before = 0;
+#pragma unroll
+      for (int w = 0; w < WAVES; ++w) before += (w < wave) ? s_cnt[j][w] : 0u;
+      uint64_t pos = off + before + r0[j];
+      bool p0 = (sel >> (2 * j)) & 1u, p1 = (sel >> (2 * j + 1)) & 1u;
+      if (p0) out[pos] = cur[j].x;
+      if (p1) out[pos + (p0 ? 1 : 0)] = cur[j].y;
+#pragma unroll
+      for (int w = 0; w < WAVES; ++w) off += s_cnt[j][w];
+    }
+    if (tn >= ntiles) break;
+    tile = tn;
+#pragma unroll
+    for (int j = 0; j < STRIPES; ++j) cur[j] = nxt[j];
+    __syncthreads();
+  }
+}
+
+// persistent + ticketed, selected values staged in LDS: once a tile is ranked its rows move
+// from registers into an LDS buffer (tile-local order), the registers take the NEXT tile's
+// loads, and only then is the look-back resolved and the buffer written out with aligned
+// 16-B (non-temporal) stores.  The look-back wait overlaps the next tile's HBM reads.
+template <int THREADS, int STRIPES, int CAP, bool NTS, int OCC = 1>
+__global__ __launch_bounds__(THREADS, OCC) void filt_L(const int64_t *__restrict__ col, uint64_t n, int64_t k,
+                                                   int64_t *__restrict__ out, uint64_t *__restrict__ out_n,
+                                                   uint32_t *__restrict__ ticket, uint64_t *__restrict__ status,
+                                                   uint32_t ntiles) {
+  constexpr int WAVES = THREADS / kWave;
+  constexpr int SROWS = THREADS * 2;
+  constexpr int TILE = SROWS * STRIPES;
+  static_assert(STRIPES <= 16, "stripe bases live in lanes 0..15");
+  __shared__ int64_t s_buf[CAP];
+  __shared__ uint32_t s_cnt[STRIPES][WAVES];
+  __shared__ uint32_t s_next;
+  __shared__ uint64_t s_excl;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  i64x2 v[STRIPES];
+  // one code path: 16-B loads at clamped (even) row indices; rows >= n are masked in the rank
+  const uint64_t last2 = (n - 2) & ~1ull;  // n >= 2, col 16-B aligned
+  auto load = [&](uint32_t t) {
+    const uint64_t base = (uint64_t)t * TILE;
+#pragma unroll
+    for (int j = 0; j < STRIPES; ++j) {
+      const uint64_t idx = min(base + j * SROWS + 2 * tid, last2);
+      v[j] = __builtin_nontemporal_load(reinterpret_cast<const i64x2 *>(col + idx));
+    }
+  };
+if (tid == 0) s_next = atomicAdd(ticket, 1u);
+  __syncthreads();
+  uint32_t tile = s_next;
+  if (tile >= ntiles) return;
+  load(tile);
+  for (;;) {
+    const uint64_t base = (uint64_t)tile * TILE;
+    const bool full = base + TILE <= n;
+    uint32_t rk[(STRIPES + 3) / 4] = {};  // 7-bit in-wave ranks, 4 per word
+    uint32_t sel = 0;
+#pragma unroll
+    for (int j = 0; j < STRIPES; ++j) {
+      const uint64_t idx = base + j * SROWS + 2 * tid;
+      bool p0 = v[j].x < k && (full || idx < n);
+      bool p1 = v[j].y < k && (full || idx + 1 < n);
+      uint64_t b0 = __ballot(p0), b1 = __ballot(p1);
+      rk[j / 4] |= (lane_rank(b0) + lane_rank(b1)) << (8 * (j % 4));
+      sel |= (p0 ? 1u : 0u) << (2 * j);
+      sel |= (p1 ? 1u : 0u) << (2 * j + 1);
+      if (lane == 0) s_cnt[j][wave] = (uint32_t)(__popcll(b0) + __popcll(b1));
+    }
+    if (tid == 64) s_next = atomicAdd(ticket, 1u);
+    __syncthreads();
+    const uint32_t tn = s_next;
+    // lane j < STRIPES: stripe j's total (T) and the part before this wave (P); scan T
+    uint32_t T = 0, P = 0;
+    if (lane < STRIPES) {
+#pragma unroll
+      for (int w = 0; w < WAVES; ++w) {
+        const uint32_t c = s_cnt[lane][w];
+        T += c;
+        P += w < wave ? c : 0u;
+      }
+    }
+    uint32_t incl = T;
+#pragma unroll
+    for (int d = 1; d < 16; d <<= 1) {
+      const uint32_t o = __shfl_up(incl, d, 64);
+      incl += lane >= d ? o : 0u;
+    }
+    const uint32_t pre = incl - T + P;  // tile-local start of this wave's rows of stripe `lane`
+    const uint32_t total = __builtin_amdgcn_readlane(incl, STRIPES - 1);
+    const bool staged = total <= CAP;  // uniform
+    auto resolve = [&]() {
+      if (wave == 0) {
+        uint64_t excl = lookback<1>(status, tile, total, lane, 1);
+        if (lane == 0) {
+          s_excl = excl;
+          if (tile == ntiles - 1) *out_n = excl + total;
+        }
+      }
+    };
+    if (staged) {
+#pragma unroll
+      for (int j = 0; j < STRIPES; ++j) {
+        const uint32_t pos = __builtin_amdgcn_readlane(pre, j) + ((rk[j / 4] >> (8 * (j % 4))) & 0xFFu);
+        const bool p0 = (sel >> (2 * j)) & 1u, p1 = (sel >> (2 * j + 1)) & 1u;
+        if (p0) s_buf[pos] = v[j].x;
+        if (p1) s_buf[pos + (p0 ? 1 : 0)] = v[j].y;
+      }
+    } else {  // more selected rows than the buffer: resolve first, write from registers
+      resolve();
+      __syncthreads();
+      const uint64_t off = s_excl;
+#pragma unroll
+      for (int j = 0; j < STRIPES; ++j) {
+        const uint64_t pos = off + __builtin_amdgcn_readlane(pre, j) + ((rk[j / 4] >> (8 * (j % 4))) & 0xFFu);
+        const bool p0 = (sel >> (2 * j)) & 1u, p1 = (sel >> (2 * j + 1)) & 1u;
+        if (p0) out[pos] = v[j].x;
+        if (p1) out[pos + (p0 ? 1 : 0)] = v[j].y;
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);  // the registers are free from here on
+    if (staged) resolve();              // wave 0 walks before it has data loads in flight
+    if (tn < ntiles) load(tn);
+    if (staged) {
+      __syncthreads();
+      const uint64_t excl = s_excl;
+      const uint32_t head = (uint32_t)(excl & 1);  // out + excl + head is 16-B aligned
+      if (head && tid == 0 && total) out[excl] = s_buf[0];
+      for (uint32_t i = head + 2 * tid; i + 1 < total; i += 2 * THREADS) {
+        i64x2 w = {s_buf[i], s_buf[i + 1]};
+        if (NTS)
+          __builtin_nontemporal_store(w, reinterpret_cast<i64x2 *>(out + excl + i));
+        else
+          *reinterpret_cast<i64x2 *>(out + excl + i) = w;
+      }
+      if (total > head && ((total - head) & 1) && tid == THREADS - 1) out[excl + total - 1] = s_buf[total - 1];
+    }
+    if (tn >= ntiles) break;
+    tile = tn;
+  }
+}
+
+template <int THREADS, int STRIPES, int CAP, bool NTS, int OCC = 1>
+void run_L(const char *name, const int64_t *col, uint64_t n, int64_t k, int64_t *out, uint64_t *dn, void *state,
+           int R, unsigned long long *dh) {
+  constexpr int TILE = THREADS * 2 * STRIPES;
+  uint32_t ntiles = (uint32_t)((n + TILE - 1) / TILE);
+  size_t sb = 16 + (size_t)ntiles * 8;
+  hipDeviceProp_t prop;
+  CK(hipGetDeviceProperties(&prop, 0));
+  int per_cu = 0;
+  CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, filt_L<THREADS, STRIPES, CAP, NTS, OCC>, THREADS, 0));
+  uint32_t grid = (uint32_t)std::min<uint64_t>(ntiles, (uint64_t)prop.multiProcessorCount * per_cu);
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  float tot = 0;
+  for (int r = 0; r < R + 2; ++r) {
+    CK(hipMemsetAsync(state, 0, sb, 0));
+    CK(hipEventRecord(a, 0));
+    hipLaunchKernelGGL((filt_L<THREADS, STRIPES, CAP, NTS, OCC>), dim3(grid), dim3(THREADS), 0, 0, col, n, k, out, dn,
+                       (uint32_t *)state, (uint64_t *)((char *)state + 16), ntiles);
+    CK(hipEventRecord(b, 0));
+    CK(hipEventSynchronize(b));
+    float ms;
+    CK(hipEventElapsedTime(&ms, a, b));
+    if (r >= 2) tot += ms;
+  }
+  uint64_t cnt;
+  CK(hipMemcpy(&cnt, dn, 8, hipMemcpyDeviceToHost));
+  CK(hipMemset(dh, 0, 8));
+  hipLaunchKernelGGL(checksum, dim3(1024), dim3(256), 0, 0, out, cnt, dh);
+  unsigned long long h;
+  CK(hipMemcpy(&h, dh, 8, hipMemcpyDeviceToHost));
+  double ms = tot / R;
+  double gb = (8.0 * n + 8.0 * cnt) / 1e9;
+  printf("%-28s g%-5u %8.4f ms  %7.1f GB/s  count=%llu hash=%016llx\n", name, grid, ms, gb / (ms * 1e-3),
+         (unsigned long long)cnt, h);
+}
+
+template <int THREADS, int STRIPES, int OCC>
+void run_q(const char *name, const int64_t *col, uint64_t n, int64_t k, int64_t *out, uint64_t *dn, void *state,
+           int R, unsigned long long *dh, int gridmul) {
+  constexpr int TILE = THREADS * 2 * STRIPES;
+  uint32_t ntiles = (uint32_t)((n + TILE - 1) / TILE);
+  size_t sb = 16 + (size_t)ntiles * 8;
+  int per_cu = 0;
+  CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, filt_q<THREADS, STRIPES, OCC>, THREADS, 0));
+  hipDeviceProp_t prop;
+  CK(hipGetDeviceProperties(&prop, 0));
+  uint32_t grid = (uint32_t)std::min<uint64_t>(ntiles, (uint64_t)per_cu * prop.multiProcessorCount * gridmul / 4);
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  float tot = 0;
+  for (int r = 0; r < R + 2; ++r) {
+    CK(hipMemsetAsync(state, 0, sb, 0));
+    CK(hipEventRecord(a, 0));
+    hipLaunchKernelGGL((filt_q<THREADS, STRIPES, OCC>), dim3(grid), dim3(THREADS), 0, 0, col, n, k, out, dn,
+                       (uint32_t *)state, (uint64_t *)((char *)state + 16), ntiles);
+    CK(hipEventRecord(b, 0));
+    CK(hipEventSynchronize(b));
+    float ms;
+    CK(hipEventElapsedTime(&ms, a, b));
+    if (r >= 2) tot += ms;
+  }
+  uint64_t cnt;
+  CK(hipMemcpy(&cnt, dn, 8, hipMemcpyDeviceToHost));
+  CK(hipMemset(dh, 0, 8));
+  hipLaunchKernelGGL(checksum, dim3(1024), dim3(256), 0, 0, out, cnt, dh);
+  unsigned long long h;
+  CK(hipMemcpy(&h, dh, 8, hipMemcpyDeviceToHost));
+  double ms = tot / R;
+  double gb = (8.0 * n + 8.0 * cnt) / 1e9;
+  printf("%-28s occ%d g%-5u %8.4f ms  %7.1f GB/s  count=%llu hash=%016llx\n", name, per_cu, grid, ms,
+         gb / (ms * 1e-3), (unsigned long long)cnt, h);
+}
+
 int main(int argc, char **argv) {
   setvbuf(stdout, NULL, _IONBF, 0);
   uint64_t n = argc > 1 ? strtoull(argv[1], 0, 10) : 100000000ull;
@@ -535,7 +857,8 @@ int main(int argc, char **argv) {
   CK(hipMalloc(&state, 16 + (n / 256 + 16) * 8));
   hipLaunchKernelGGL(gen, dim3(4096), dim3(256), 0, 0, col, n);
   CK(hipDeviceSynchronize());
-  if (argc > 3 && atoi(argv[3]) != 99) goto variants;
+  if (argc > 3 && atoi(argv[3]) != 99 && atoi(argv[3]) != 98) goto variants;
+  if (argc > 3 && atoi(argv[3]) == 98) goto copies;
   {  // reference copy bandwidth: read n*8, write n*4 (half)
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
@@ -572,6 +895,36 @@ int main(int argc, char **argv) {
       printf("copy4 grid %-5d                   %8.4f ms  %7.1f GB/s\n", grid, ms, 12.0 * n / 1e9 / (ms * 1e-3));
     }
   }
+copies:
+  if (argc > 3 && atoi(argv[3]) == 98) {
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    auto T = [&](const char *nm, void (*kf)(const int64_t *, int64_t *, uint64_t), int grid) {
+      float tot = 0;
+      for (int r = 0; r < R + 2; ++r) {
+        CK(hipEventRecord(a, 0));
+        hipLaunchKernelGGL(kf, dim3(grid), dim3(256), 0, 0, col, out, n);
+        CK(hipEventRecord(b, 0));
+        CK(hipEventSynchronize(b));
+        float ms;
+        CK(hipEventElapsedTime(&ms, a, b));
+        if (r >= 2) tot += ms;
+      }
+      double ms = tot / R;
+      printf("%-22s grid %-5d %8.4f ms  %7.1f GB/s\n", nm, grid, ms, 12.0 * n / 1e9 / (ms * 1e-3));
+    };
+    for (int grid : {1024, 2048, 4096}) {
+      T("copyN 4", copyN<4, false, false>, grid);
+      T("copyN 4 NTL", copyN<4, true, false>, grid);
+      T("copyN 4 NTL NTS", copyN<4, true, true>, grid);
+      T("copyN 8 NTL", copyN<8, true, false>, grid);
+      T("copyN 8 NTL NTS", copyN<8, true, true>, grid);
+      T("copyN 16 NTL", copyN<16, true, false>, grid);
+      T("copyN 16 NTL NTS", copyN<16, true, true>, grid);
+    }
+    return 0;
+  }
 variants:
   int v = argc > 3 ? atoi(argv[3]) : -1;
   int idx = 0;
@@ -592,6 +945,63 @@ variants:
   if (v < 0 || v == idx) run<512, 16, false, false, 0, false>("512x16 noticket nosleep", col, n, k, out, dn, state, R, dh);
   ++idx;
   if (v < 0 || v == idx) run<512, 16, true, false, 1, false>("512x16 LDS noticket", col, n, k, out, dn, state, R, dh);
+  ++idx;
+  // 9: the product kernel's scheme (ticket + NT)
+  if (v < 0 || v == idx) run<512, 16, false, true, 1, true>("512x16 ticket NT (product)", col, n, k, out, dn, state, R, dh);
+  ++idx;
+  if (v < 0 || v == idx) run<512, 16, false, true, 1, false, 1, 1>("NT nolookback", col, n, k, out, dn, state, R, dh);
+  ++idx;
+  if (v < 0 || v == idx) run<512, 16, false, true, 1, false, 1, 2>("NT nowrite", col, n, k, out, dn, state, R, dh);
+  ++idx;
+  if (v < 0 || v == idx) run<512, 16, false, true, 1, false, 1, 3>("NT read+rank only", col, n, k, out, dn, state, R, dh);
+  ++idx;
+  if (v < 0 || v == idx) run<256, 16, false, true, 1, false, 1, 3>("256x16 NT read+rank only", col, n, k, out, dn, state, R, dh);
+  ++idx;
+  if (v < 0 || v == idx) run<256, 8, false, true, 1, false, 1, 3>("256x8 NT read+rank only", col, n, k, out, dn, state, R, dh);
+  ++idx;
+  if (v < 0 || v == idx) run<256, 8, false, true, 1, false, 1, 1>("256x8 NT nolookback", col, n, k, out, dn, state, R, dh);
+  ++idx;
+  if (v < 0 || v == idx) run<512, 16, false, true, 1, true, 1, 0, true>("product + NTS", col, n, k, out, dn, state, R, dh);
+  ++idx;
+  if (v < 0 || v == idx) run<512, 16, false, true, 1, false, 1, 1, true>("nolookback NTS", col, n, k, out, dn, state, R, dh);
+  ++idx;
+  if (v < 0 || v == idx) run<256, 8, false, true, 1, false>("256x8 noticket NT", col, n, k, out, dn, state, R, dh);
+  ++idx;
+  if (v < 0 || v == idx) run<256, 16, false, true, 1, false>("256x16 noticket NT", col, n, k, out, dn, state, R, dh);
+  ++idx;
+  if (v < 0 || v == idx) run<512, 8, false, true, 1, false>("512x8 noticket NT", col, n, k, out, dn, state, R, dh);
+  ++idx;
+  if (v < 0 || v == idx) run<256, 16, false, true, 1, false, 1, 0, true>("256x16 noticket NT NTS", col, n, k, out, dn, state, R, dh);
+  ++idx;
+  if (v < 0 || v == idx) run_L<1024, 16, 18944, true>("L 1024x16 NTS", col, n, k, out, dn, state, R, dh);
+  ++idx;
+  if (v < 0 || v == idx) run_L<1024, 16, 18944, false>("L 1024x16", col, n, k, out, dn, state, R, dh);
+  ++idx;
+  if (v < 0 || v == idx) run_L<1024, 8, 18944, true>("L 1024x8 NTS", col, n, k, out, dn, state, R, dh);
+  ++idx;
+  if (v < 0 || v == idx) run_L<512, 16, 18944, true>("L 512x16 NTS", col, n, k, out, dn, state, R, dh);
+  ++idx;
+  if (v < 0 || v == idx) run_L<512, 16, 9984, true, 2>("L 512x16 cap9984 occ2 NTS", col, n, k, out, dn, state, R, dh);
+  ++idx;
+  if (v < 0 || v == idx) run_L<256, 16, 4992, true, 4>("L 256x16 cap4992 occ4 NTS", col, n, k, out, dn, state, R, dh);
+  ++idx;
+  if (v < 0 || v == idx) run_L<1024, 16, 20224, true>("L 1024x16 cap20224 NTS", col, n, k, out, dn, state, R, dh);
+  ++idx;
+  if (v < 0 || v == idx) run_q<512, 16, 1>("q 512x16 occ1", col, n, k, out, dn, state, R, dh, 4);
+  ++idx;
+  if (v < 0 || v == idx) run_q<512, 8, 2>("q 512x8 occ2", col, n, k, out, dn, state, R, dh, 4);
+  ++idx;
+  if (v < 0 || v == idx) run_q<1024, 8, 1>("q 1024x8 occ1", col, n, k, out, dn, state, R, dh, 4);
+  ++idx;
+  if (v < 0 || v == idx) run_q<256, 16, 2>("q 256x16 occ2", col, n, k, out, dn, state, R, dh, 4);
+  ++idx;
+  if (v < 0 || v == idx) run_q<512, 12, 1>("q 512x12 occ1", col, n, k, out, dn, state, R, dh, 4);
+  ++idx;
+  if (v < 0 || v == idx) run_q<512, 16, 1>("q 512x16 occ1 grid x2", col, n, k, out, dn, state, R, dh, 8);
+  ++idx;
+  if (v < 0 || v == idx) run_p<512, 16, true, 1>("p 512x16 NT", col, n, k, out, dn, state, R, dh, 4);
+  ++idx;
+  if (v < 0 || v == idx) run_w<512, 16, true>("w 512x16 ticket", col, n, k, out, dn, state, R, dh);
   ++idx;
   return 0;
 }

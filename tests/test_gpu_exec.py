@@ -57,6 +57,23 @@ def test_filter_sizes_vs_oracle(ex, orc, n):
             assert np.array_equal(got, want), (n, s, op)
 
 
+@pytest.mark.parametrize("n", [32767, 32768, 32769, 3 * 32768 - 1, 257 * 32768 + 5])
+def test_filter_staged_tiles_vs_oracle(ex, orc, n):
+    """The persistent LDS-staged kernel (32768-row tiles, 20224-row buffer): tile-multiple
+    and ragged sizes, tiles denser than the buffer (s = 0.62 .. 1, staged in two halves),
+    and an output pointer 8 bytes off 16-B alignment (scalar head / tail stores)."""
+    col = orc.gen_column(0, 0x2A, n)
+    d = dev(col, ex)
+    for s in (0.05, 0.5, 0.62, 0.7, 0.95, 1.0):
+        k = int(s * 2**62)
+        got = host(ex.filter_i64(d, "<", k))
+        assert np.array_equal(got, orc.filter_i64(col, OPCODE["<"], k)), (n, s)
+    buf = torch.empty(n + 1, dtype=torch.int64, device=ex.device)
+    k = int(0.7 * 2**62)
+    got = host(ex.filter_i64(d, "<", k, out=buf[1:]))
+    assert np.array_equal(got, orc.filter_i64(col, OPCODE["<"], k))
+
+
 def test_filter_extremes_and_unaligned(ex, orc):
     rng = np.random.default_rng(7)
     v = rng.integers(I64_MIN, I64_MAX, size=50_001, dtype=np.int64)
