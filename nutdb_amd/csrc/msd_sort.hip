@@ -8,7 +8,7 @@
 //     8 (histogram) + 16 (level 0) + 8 (histogram) + 16 (level 1) + 16 (local) = 64 B/key
 // instead of 8 + 8 x 16 = 136 B/key.
 //
-//   * level histograms (ms_hist_kernel): one 512-bin LDS histogram per 64 Ki-key tile of a
+//   * level histograms (ms_hist_kernel): one 512-bin LDS histogram per 256 Ki-key tile of a
 //     segment, flushed with global atomics; the first also reduces min / max, so the levels
 //     sort (key - base) by its varying bits (a narrow key range is rebased onto 0 and its
 //     first digit starts at the top bit of max - min).
@@ -36,7 +36,9 @@
 namespace nut {
 
 constexpr int MH_THREADS = 256;
-constexpr uint32_t MH_TILE = 1u << 16;  // keys per histogram / copy tile
+constexpr uint32_t MH_TILE = 1u << 16;  // keys per copy tile
+constexpr uint32_t MH_HTILE = 1u << 18; // keys per histogram tile (one LDS histogram flush each)
+constexpr int MH_LOADS = 16;            // keys in flight per lane in the histogram loop
 constexpr int MS_THREADS = 1024;
 constexpr int MS_ITEMS = 16;
 constexpr uint32_t MS_TILE = MS_THREADS * MS_ITEMS;  // 16384 keys per scatter tile
@@ -88,18 +90,18 @@ __global__ __launch_bounds__(MH_THREADS) void ms_hist_kernel(MsBufs bf, const Ms
   __syncthreads();
   const uint32_t s = tile_seg[blockIdx.x];
   const MsSeg sg = segs[s];
-  const uint64_t lo = (uint64_t)(blockIdx.x - sg.aux) * MH_TILE;
-  const uint32_t cnt = (uint32_t)min<uint64_t>(MH_TILE, sg.count - lo);
+  const uint64_t lo = (uint64_t)(blockIdx.x - sg.aux) * MH_HTILE;
+  const uint32_t cnt = (uint32_t)min<uint64_t>(MH_HTILE, sg.count - lo);
   const uint64_t *src = ms_src(bf, sg.buf) + sg.start + lo;
   const uint64_t f = sg.buf == 0 ? flip : 0;
   uint64_t vmin = ~0ull, vmax = 0;
-  for (uint32_t i = tid; i < cnt; i += MH_THREADS * 8) {
-    uint64_t k[8];
+  for (uint32_t i = tid; i < cnt; i += MH_THREADS * MH_LOADS) {
+    uint64_t k[MH_LOADS];
 #pragma unroll
-    for (int j = 0; j < 8; ++j)  // unconditional (clamped) loads: a conditional one compiles to
-      k[j] = __builtin_nontemporal_load(src + min(i + j * MH_THREADS, cnt - 1)) ^ f;  // a branch + wait per key
+    for (int j = 0; j < MH_LOADS; ++j)  // unconditional (clamped) loads: a conditional one compiles
+      k[j] = __builtin_nontemporal_load(src + min(i + j * MH_THREADS, cnt - 1)) ^ f;  // to a branch + wait per key
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
+    for (int j = 0; j < MH_LOADS; ++j) {
       if (i + j * MH_THREADS < cnt) {
         atomicAdd(&h[dg(k[j])], 1u);
         vmin = k[j] < vmin ? k[j] : vmin;
@@ -213,7 +215,7 @@ __global__ __launch_bounds__(MS_THREADS) void ms_scatter_kernel(MsBufs bf, const
       const uint32_t j = (uint32_t)i * MS_THREADS + tid;
       if (j < cnt) {
         const uint64_t k = s_keys[j];
-        dst[s_gb[dg(k)] + j] = k;
+        dst[s_gb[dg(k)] + j] = k;  // (non-temporal stores measured 2.4 ms slower per sort)
       }
     }
     if (next >= ntiles) break;
@@ -708,7 +710,7 @@ __global__ __launch_bounds__(THREADS, 4) void ms_local_kernel(MsBufs bf, const M
     __syncthreads();
     if (MS_STOP(4)) continue;
     const uint32_t rend = round ? c : mid;
-    for (uint32_t j = tid; j < rend - rbase; j += THREADS) dst[rbase + j] = s_keys[j] ^ flip;
+    for (uint32_t j = tid; j < rend - rbase; j += THREADS) __builtin_nontemporal_store(s_keys[j] ^ flip, &dst[rbase + j]);
   }
   return pf;
   };
@@ -967,7 +969,7 @@ static nut_status device_level(nut_ctx *c, MetaArena &ar, const MsBufs &bf, cons
   hipStream_t st = c->stream;
   over.clear();
   std::vector<uint32_t> tiles;
-  const uint64_t nht = tile_table(big, MH_TILE, tiles);
+  const uint64_t nht = tile_table(big, MH_HTILE, tiles);
   std::vector<uint32_t> stiles;
   std::vector<MsSeg> sbig = big;
   const uint64_t nst = tile_table(sbig, MS_TILE, stiles);
@@ -1059,7 +1061,7 @@ nut_status msd_sort_i64(nut_ctx *c, const int64_t *in, int64_t *out, uint64_t n,
   bool first = true;
   while (!big.empty()) {
     // ---- histograms of the level's digit over the big segments
-    const uint64_t nht = tile_table(big, MH_TILE, tiles);
+    const uint64_t nht = tile_table(big, MH_HTILE, tiles);
     if (nht > 0x7FFFFFFFull) return fail(NUT_ERR_UNSUPPORTED, "nut_sort_i64: too many tiles");
     const size_t hbytes = big.size() * MS_BINS * 8;
     s = ar.begin(MetaArena::align(big.size() * sizeof(MsSeg)) + MetaArena::align(tiles.size() * 4) +
