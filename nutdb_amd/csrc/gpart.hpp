@@ -20,7 +20,8 @@ constexpr int GP_THREADS = 512;
 constexpr int GP_ITEMS = 16;
 constexpr uint32_t GP_TILE = GP_THREADS * GP_ITEMS;  // 8192 records per scatter tile
 constexpr int GP_HTHREADS = 256;
-constexpr uint32_t GP_HTILE = 1u << 16;              // records per histogram tile
+constexpr uint32_t GP_HTILE = 1u << 18;              // records per histogram tile (one flush each)
+constexpr int GP_HLOADS = 16;                        // keys in flight per lane in the histogram
 constexpr int GP_BINS = 256;
 constexpr int GP_MAX_ARR = 3 + NUT_MAX_VALS;         // hash, k1, k2, value arrays
 
@@ -58,16 +59,19 @@ __global__ __launch_bounds__(GP_HTHREADS) void gp_hist_kernel(const uint64_t *__
   const GpSeg sg = segs[s];
   const uint64_t lo = sg.start + (uint64_t)(blockIdx.x - sg.tile0) * GP_HTILE;
   const uint32_t n = (uint32_t)min<uint64_t>(GP_HTILE, sg.start + sg.count - lo);
-  for (uint32_t i = tid; i < n; i += GP_HTHREADS * 4) {
-    uint32_t d[4];
+  for (uint32_t i = tid; i < n; i += GP_HTHREADS * GP_HLOADS) {
+    // unconditional (clamped) non-temporal loads: all GP_HLOADS keys in flight at once
+    uint64_t a[GP_HLOADS], b[GP_HLOADS];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint32_t k = i + j * GP_HTHREADS;
-      d[j] = k < n ? gp_digit(k1, k2, lo + k, shift, kx) : 0;
+    for (int j = 0; j < GP_HLOADS; ++j) {
+      const uint64_t r = lo + min(i + j * GP_HTHREADS, n - 1);
+      a[j] = __builtin_nontemporal_load(k1 + r);
+      b[j] = k2 ? __builtin_nontemporal_load(k2 + r) : 0;
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      if (i + j * GP_HTHREADS < n) atomicAdd(&cnt[d[j]], 1u);
+    for (int j = 0; j < GP_HLOADS; ++j)
+      if (i + j * GP_HTHREADS < n)
+        atomicAdd(&cnt[(uint32_t)(owner_hash(a[j] ^ kx, b[j], k2 ? 2 : 1) >> shift) & 255u], 1u);
   }
   __syncthreads();
   if (cnt[tid]) atomicAdd(&hist[(gather ? 0 : (uint64_t)s) * GP_BINS + tid], (unsigned long long)cnt[tid]);
@@ -86,41 +90,53 @@ __global__ __launch_bounds__(T) void gp_scatter_kernel(GpArrays ar, const GpSeg 
                                                                 const uint32_t *__restrict__ tile_seg, uint32_t ntiles,
                                                                 int shift, int gather,
                                                                 unsigned long long *__restrict__ cursor, uint64_t kx) {
-  __shared__ uint64_t s_stage[(T * GP_ITEMS)];
-  __shared__ uint8_t s_dig[(T * GP_ITEMS)];
+  constexpr uint32_t TILE = T * GP_ITEMS;
+  static_assert(TILE <= (1u << 24), "slot bits");
+  __shared__ uint64_t s_stage[TILE];
+  __shared__ uint8_t s_dig[TILE];
   __shared__ uint32_t s_cnt[GP_BINS];
   __shared__ uint32_t s_tex[GP_BINS];
   __shared__ uint64_t s_gb[GP_BINS];
   __shared__ uint32_t s_wsum[GP_BINS / kWave];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   uint64_t k1[GP_ITEMS], k2[NK == 2 ? GP_ITEMS : 1];
-  auto load_keys = [&](uint32_t tt) {
+  // records of tile tt: [lo, lo + n); item i of this lane is record i * T + tid
+  auto tile_range = [&](uint32_t tt, uint64_t &lo, uint32_t &n) {
     const GpSeg g = segs[tile_seg[tt]];
-    const uint64_t lo = g.start + (uint64_t)(tt - g.tile0) * (T * GP_ITEMS);
-    const uint32_t n = (uint32_t)min<uint64_t>((T * GP_ITEMS), g.start + g.count - lo);
+    lo = g.start + (uint64_t)(tt - g.tile0) * TILE;
+    n = (uint32_t)min<uint64_t>(TILE, g.start + g.count - lo);
+  };
+  // unconditional (clamped) loads from one per-tile base: all in flight at once, one
+  // 32-bit offset per item
+  auto load_arr = [&](const uint64_t *src, uint64_t lo, uint32_t n, uint64_t (&v)[GP_ITEMS]) {
+    const uint64_t *b = src + lo;
 #pragma unroll
-    for (int i = 0; i < GP_ITEMS; ++i) {  // unconditional (clamped): all loads in flight at once
-      const uint64_t r = lo + min((uint32_t)i * T + tid, n - 1);
-      k1[i] = __builtin_nontemporal_load(ar.src[1] + r);
-      if (NK == 2) k2[i] = __builtin_nontemporal_load(ar.src[2] + r);
-    }
+    for (int i = 0; i < GP_ITEMS; ++i) v[i] = __builtin_nontemporal_load(b + min((uint32_t)i * T + tid, n - 1));
   };
   uint32_t t = blockIdx.x;
   if (t >= ntiles) return;
-  load_keys(t);
+  uint64_t lo;
+  uint32_t n;
+  tile_range(t, lo, n);
+  load_arr(ar.src[1], lo, n, k1);
+  if constexpr (NK == 2) load_arr(ar.src[2], lo, n, k2);
   for (;;) {
+    // per-item offsets (i * T + tid) are loop-invariant; hoisted out of the tile loop they
+    // pinned 16+ registers and pushed the keys into scratch (serialising their loads), so
+    // the loop works from an opaque copy of tid
+    int tid_ = tid;
+    asm volatile("" : "+v"(tid_));
+    const int tid = tid_;
     const uint32_t s = tile_seg[t];
-    const GpSeg sg = segs[s];
-    const uint64_t lo = sg.start + (uint64_t)(t - sg.tile0) * (T * GP_ITEMS);
-    const uint32_t n = (uint32_t)min<uint64_t>((T * GP_ITEMS), sg.start + sg.count - lo);
     if (tid < GP_BINS) s_cnt[tid] = 0;
     __syncthreads();
-    uint32_t dg[GP_ITEMS], slot[GP_ITEMS];
+    // rank: sd[i] = digit | in-digit rank << 8, then the tile slot once the digit starts are known
+    uint32_t sd[GP_ITEMS];
 #pragma unroll
     for (int i = 0; i < GP_ITEMS; ++i) {
-      const bool v = (uint32_t)i * T + tid < n;
-      dg[i] = (uint32_t)(owner_hash(k1[i] ^ kx, NK == 2 ? k2[i] : 0, NK) >> shift) & 255u;
-      slot[i] = v ? atomicAdd(&s_cnt[dg[i]], 1u) : 0u;
+      const uint32_t d = (uint32_t)(owner_hash(k1[i] ^ kx, NK == 2 ? k2[i] : 0, NK) >> shift) & 255u;
+      const uint32_t r = (uint32_t)i * T + tid < n ? atomicAdd(&s_cnt[d], 1u) : 0u;
+      sd[i] = d | (r << 8);
     }
     __syncthreads();
     uint32_t c = 0, incl = 0;
@@ -148,38 +164,55 @@ __global__ __launch_bounds__(T) void gp_scatter_kernel(GpArrays ar, const GpSeg 
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < GP_ITEMS; ++i) {
-      if ((uint32_t)i * T + tid < n) {
-        slot[i] += s_tex[dg[i]];
-        s_dig[slot[i]] = (uint8_t)dg[i];
-      }
+      const uint32_t d = sd[i] & 255u;
+      sd[i] = (sd[i] >> 8) + s_tex[d];  // the tile slot
+      if ((uint32_t)i * T + tid < n) s_dig[sd[i]] = (uint8_t)d;
     }
-    // one array through LDS: stage in digit order, write out coalesced runs
-    auto pass = [&](const uint64_t (&v)[GP_ITEMS], uint64_t *dst) {
+    // one array through LDS: stage in digit order (its registers are then free), write
+    // out coalesced runs.  The first value array loads while the keys are written out,
+    // the next tile's keys while the values are.
+    auto stage = [&](const uint64_t (&v)[GP_ITEMS]) {
       __syncthreads();  // the previous array's write-out is done with s_stage
 #pragma unroll
       for (int i = 0; i < GP_ITEMS; ++i)
-        if ((uint32_t)i * T + tid < n) s_stage[slot[i]] = v[i];
+        if ((uint32_t)i * T + tid < n) s_stage[sd[i]] = v[i];
       __syncthreads();
-#pragma unroll
+    };
+    auto flush = [&](uint64_t *dst) {
+      // not fully unrolled: the scheduler would hoist every item's LDS reads (and their
+      // registers) above the first store
+#pragma unroll 2
       for (int i = 0; i < GP_ITEMS; ++i) {
         const uint32_t j = (uint32_t)i * T + tid;
         if (j < n) dst[s_gb[s_dig[j]] + j] = s_stage[j];
       }
     };
-    pass(k1, ar.dst[1]);
-    if constexpr (NK == 2) pass(k2, ar.dst[2]);
+    uint64_t v[GP_ITEMS];
+    stage(k1);
+    if constexpr (NK == 2) {
+      flush(ar.dst[1]);
+      stage(k2);
+    }
+    if (ar.narr > 3) load_arr(ar.src[3], lo, n, v);
+    flush(ar.dst[NK == 2 ? 2 : 1]);
     const uint32_t next = t + gridDim.x;
-    if (next < ntiles) load_keys(next);  // the key registers are free
+    uint64_t nlo = 0;
+    uint32_t nn = 0;
+    if (next < ntiles) {  // the key registers are free
+      tile_range(next, nlo, nn);
+      load_arr(ar.src[1], nlo, nn, k1);
+      if constexpr (NK == 2) load_arr(ar.src[2], nlo, nn, k2);
+    }
     for (int a = 3; a < ar.narr; ++a) {
-      uint64_t v[GP_ITEMS];
-#pragma unroll
-      for (int i = 0; i < GP_ITEMS; ++i)
-        v[i] = __builtin_nontemporal_load(ar.src[a] + lo + min((uint32_t)i * T + tid, n - 1));
-      pass(v, ar.dst[a]);
+      stage(v);
+      if (a + 1 < ar.narr) load_arr(ar.src[a + 1], lo, n, v);
+      flush(ar.dst[a]);
     }
     if (next >= ntiles) break;
     __syncthreads();  // s_cnt / s_stage / s_dig / s_gb are reused
     t = next;
+    lo = nlo;
+    n = nn;
   }
 }
 
