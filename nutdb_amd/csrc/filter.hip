@@ -172,6 +172,11 @@ __global__ __launch_bounds__(FS_THREADS, 1) void filter_i64_staged_kernel(
   if (tile >= ntiles) return;
   load(tile);
   for (;;) {
+    // an opaque copy of tid per tile: hoisted out of the loop, the per-stripe row offsets
+    // pinned registers the stripes need (spills)
+    int tid_ = tid;
+    asm volatile("" : "+v"(tid_));
+    const int tid = tid_;
     const uint64_t base = (uint64_t)tile * FS_TILE;
     const bool full = base + FS_TILE <= n;
     uint32_t rk[FS_STRIPES / 4] = {};  // in-wave ranks (<= 126), 4 per word

@@ -16,7 +16,7 @@ from prof_summary import summarize  # noqa: E402
 
 WORKLOAD_KERNEL = {"q1": ("tpch_q1_shape_filter_groupby", "agg_kernel"),
                    "groupby": ("groupby_i64_sum_f64", "agg_kernel"),
-                   "filter": ("filter_i64_compaction", "filter_i64_kernel"),
+                   "filter": ("filter_i64_compaction", "filter_i64_staged_kernel"),
                    "sort": ("sort_i64_radix", "nut::ms_"),
                    "q12expr": ("q12_shape_expression_groupby", "agg_kernel"),
                    "join": ("join_i64_hash", "hj_"),
