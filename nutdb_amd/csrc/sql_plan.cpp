@@ -298,6 +298,10 @@ struct HNode {
 
 }  // namespace
 
+// FULL OUTER JOIN (plans only): executed as a LEFT join plus the JOIN source's unmatched
+// rows (an ANTI join with the roles swapped); the kernels know types 0..3
+constexpr int PJ_FULL = 4;
+
 struct nut_plan {
   int kind = NUT_PLAN_FILTER;
   bool compiled = false;          // expression mode: WHERE / aggregate arguments are programs
@@ -323,7 +327,7 @@ struct nut_plan {
   uint64_t limit = 0, offset = 0;
   // JOIN (one JoinClause with ON a = b), executed by nut_plan_execute2: a hash join
   // (nut_join_i64) then gathers into the joined table the rest of the plan runs on
-  int join = -1;           // nut_join_type; -1: no JOIN
+  int join = -1;           // nut_join_type, or PJ_FULL; -1: no JOIN
   // several INNER JoinClauses (nut_plan_executen): table k+1 joins on jn[k].key
   struct JoinStep {
     std::string table, alias;
@@ -1114,7 +1118,8 @@ bool lower_mode(const Statement &st, nut_plan &p, Lowering &L) {
       case JoinType::RightSemi: p.join = NUT_JOIN_SEMI, p.jright = true; break;
       case JoinType::LeftAnti: p.join = NUT_JOIN_ANTI; break;
       case JoinType::RightAnti: p.join = NUT_JOIN_ANTI, p.jright = true; break;
-      default: return L.fail("FULL OUTER and ASOF JOIN are not executed");
+      case JoinType::FullOuter: p.join = PJ_FULL; break;
+      default: return L.fail("ASOF JOIN is not executed");
     }
     p.jtable = std::string(jc.src.table);
     if (jc.src.alias) p.jalias = std::string(*jc.src.alias);
@@ -1235,7 +1240,7 @@ bool lower_mode(const Statement &st, nut_plan &p, Lowering &L) {
     }
     if (p.aggs.size() > NUT_MAX_AGGS) return L.fail("more than 8 aggregates (HAVING / ORDER BY included)");
     if (p.vals.size() > NUT_MAX_VALS) return L.fail("aggregates reference more than 4 value columns");
-    if (!p.compiled && p.join == NUT_JOIN_LEFT)  // NULL-extended rows need aggregate masks
+    if (!p.compiled && (p.join == NUT_JOIN_LEFT || p.join == PJ_FULL))  // NULL-extended rows need aggregate masks
       return L.fail("outer-join aggregates lower to expression mode");
     return true;
   }
@@ -1475,7 +1480,7 @@ std::string describe(const nut_plan &p) {
   o += "],\"limit\":";
   o += p.has_limit ? std::to_string(p.limit) : "null";
   if (p.join >= 0) {
-    static const char *jn[] = {"inner", "left", "semi", "anti"};
+    static const char *jn[] = {"inner", "left", "semi", "anti", "full"};
     o += ",\"join\":{\"type\":\"";
     o += jn[p.join];
     o += p.jright ? "\",\"right\":true" : "\",\"right\":false";
@@ -2379,7 +2384,8 @@ nut_status exec_join(nut_ctx *c, const nut_plan &p, const nut_column *lc, int nl
   // INNER builds the smaller table (decided after the pushdown below); the outer / semi /
   // anti joins preserve their side
   int ps = p.join == NUT_JOIN_INNER ? (lrows >= rrows ? 0 : 1) : (p.jright ? 1 : 0);
-  const bool outer = p.join == NUT_JOIN_LEFT;
+  const bool full = p.join == PJ_FULL;  // both tables NULL-extended; probe = the FROM table
+  const bool outer = p.join == NUT_JOIN_LEFT || full;
   // what the other (build) table may feed
   int bkey = side[k0] == ps ? k1 : k0, pkey = side[k0] == ps ? k0 : k1;
   auto in_prog = [](const PProg &pp, int i) {  // (LIKE leaves read their column too)
@@ -2404,6 +2410,8 @@ nut_status exec_join(nut_ctx *c, const nut_plan &p, const nut_column *lc, int nl
     const int ci = (int)i;
     bool row, agg;
     reads(p, ci, row, agg);
+    if (full && row && side[i] >= 0)
+      return fail(NUT_ERR_PLAN, "FULL OUTER JOIN: column '" + p.cols[i] + "' may only appear inside aggregates");
     if (side[i] == ps) continue;
     if (p.join == NUT_JOIN_SEMI || p.join == NUT_JOIN_ANTI) {
       // SEMI: the other table's ON column equals the preserved one; nothing else exists
@@ -2420,7 +2428,7 @@ nut_status exec_join(nut_ctx *c, const nut_plan &p, const nut_column *lc, int nl
   // preserved one (WHERE may not read the other table there).
   nut_plan p2 = p;
   std::vector<PProg> push[2];
-  auto pushable = [&](int sd) { return sd >= 0 && (p.join == NUT_JOIN_INNER || sd == ps); };
+  auto pushable = [&](int sd) { return sd >= 0 && !full && (p.join == NUT_JOIN_INNER || sd == ps); };
   if (p.compiled) {
     std::vector<PProg> conj, keep;
     split_and(p.where, conj);
@@ -2485,13 +2493,44 @@ nut_status exec_join(nut_ctx *c, const nut_plan &p, const nut_column *lc, int nl
     if (he != hipSuccess) return hip_fail(he, "hipMalloc (join index)");
     // the pairs carry table rows: the pushed-down selections' ids ride along as row ids
     st = join_i64_into_rows(c, bkd, (const int64_t *)ids_s[1 - ps].p, nb, pkd, (const int64_t *)ids_s[ps].p, np,
-                            p.join | any_order, (int64_t *)idx.p, (int64_t *)idx.p + cap, cap, &npairs);
+                            (full ? NUT_JOIN_LEFT : p.join) | any_order, (int64_t *)idx.p, (int64_t *)idx.p + cap, cap,
+                            &npairs);
     if (st != NUT_ERR_CAPACITY || npairs <= cap) break;
     idx.reset();
     cap = npairs;
   }
   if (st) return st;
   int64_t *pi = (int64_t *)idx.p, *bi = pi + cap;
+  DevBuf fidx;
+  if (full) {
+    // the JOIN source's rows without a match: ANTI with the roles swapped (build = the
+    // FROM table's keys), appended as pairs (-1, source row)
+    const uint64_t nsrc = rows_s[1 - ps];
+    DevBuf anti;
+    uint64_t nanti = 0;
+    if (nsrc) {
+      NUT_HIP(anti.alloc(c, nsrc * 16));
+      st = join_i64_into_rows(c, keys_s[ps], (const int64_t *)ids_s[ps].p, rows_s[ps], keys_s[1 - ps],
+                              (const int64_t *)ids_s[1 - ps].p, nsrc, NUT_JOIN_ANTI | any_order, (int64_t *)anti.p,
+                              (int64_t *)anti.p + nsrc, nsrc, &nanti);
+      if (st) return st;
+    }
+    const uint64_t tot = npairs + nanti, fcap = std::max<uint64_t>(tot, 1);
+    NUT_HIP(fidx.alloc(c, fcap * 16));
+    int64_t *fp = (int64_t *)fidx.p, *fb = fp + fcap;
+    if (npairs) {
+      NUT_HIP(hipMemcpyAsync(fp, pi, npairs * 8, hipMemcpyDeviceToDevice, c->stream));
+      NUT_HIP(hipMemcpyAsync(fb, bi, npairs * 8, hipMemcpyDeviceToDevice, c->stream));
+    }
+    if (nanti) {
+      NUT_HIP(hipMemsetAsync(fp + npairs, 0xFF, nanti * 8, c->stream));  // -1: no FROM row
+      NUT_HIP(hipMemcpyAsync(fb + npairs, anti.p, nanti * 8, hipMemcpyDeviceToDevice, c->stream));
+    }
+    NUT_HIP(hipStreamSynchronize(c->stream));  // `anti` is freed on scope exit
+    pi = fp;
+    bi = fb;
+    npairs = tot;
+  }
   // the joined table: every plan column gathered through its side's index
   const bool mask_col = outer && p.kind == NUT_PLAN_GROUPBY;
   std::vector<DevBuf> bufs(nc + 1);
@@ -2504,31 +2543,45 @@ nut_status exec_join(nut_ctx *c, const nut_plan &p, const nut_column *lc, int nl
     NUT_HIP(bufs[i].alloc(c, std::max<uint64_t>(npairs, 1) * 8));
     // SEMI / ANTI pairs carry no build row: the other ON column reads the preserved one
     // (outer joins: equal on matched rows; aggregates mask the NULL-extended ones)
-    const bool via_probe = side[i] == ps || (p.join != NUT_JOIN_INNER && (int)i == bkey);
+    const bool via_probe = side[i] == ps || (p.join != NUT_JOIN_INNER && !full && (int)i == bkey);
     st = nut_gather_u64(c, (const uint64_t *)src[via_probe && (int)i == bkey ? pkey : i]->data, via_probe ? pi : bi,
                         npairs, 0, (uint64_t *)bufs[i].p);
     if (st) return st;
     jc[i] = nut_column{p.cols[i].c_str(), bufs[i].p, src[i]->type};
   }
-  if (mask_col) {  // aggregates over the other table skip the NULL-extended rows
+  DevBuf lmask;
+  if (mask_col) {  // aggregates over a NULL-extended table skip its NULL rows
+    p2.cols.reserve(nc + 2);  // jc keeps c_str() pointers into p2.cols
     NUT_HIP(bufs[nc].alloc(c, std::max<uint64_t>(npairs, 1) * 8));
     st = join_matched(c, bi, npairs, (int64_t *)bufs[nc].p);
     if (st) return st;
     p2.cols.push_back("__matched");
     jc[nc] = nut_column{p2.cols[nc].c_str(), bufs[nc].p, NUT_T_I64};
-    const int m = (int)nc;
-    for (PlanAgg &a : p2.aggs) {
-      bool other = false;
-      for (int ref : a.refs) other = other || side[ref] != ps;
-      if (!other) continue;
+    if (full) {  // FULL: the FROM table's columns are NULL on the source's unmatched rows
+      NUT_HIP(lmask.alloc(c, std::max<uint64_t>(npairs, 1) * 8));
+      st = join_matched(c, pi, npairs, (int64_t *)lmask.p);
+      if (st) return st;
+      p2.cols.push_back("__lmatched");
+      jc.push_back(nut_column{p2.cols[nc + 1].c_str(), lmask.p, NUT_T_I64});
+    }
+    auto add_mask = [](PlanAgg &a, int m) {  // (m != 0) [AND the argument's own mask]
       const bool had = !a.mask.empty();
       PNode col;
       col.op = NUT_P_COL;
       col.col = m;
-      a.mask.push_back(col);  // (__matched != 0) [AND the argument's own mask]
+      a.mask.push_back(col);
       emit_int(a.mask, 0);
       emit(a.mask, NUT_P_NE);
       if (had) emit(a.mask, NUT_P_AND);
+    };
+    for (PlanAgg &a : p2.aggs) {
+      bool other = false, mine = false;
+      for (int ref : a.refs) {
+        other = other || side[ref] != ps;
+        mine = mine || side[ref] == ps;
+      }
+      if (other) add_mask(a, (int)nc);
+      if (full && mine) add_mask(a, (int)nc + 1);
     }
   }
   std::vector<const nut_column *> bound(p2.cols.size());

@@ -250,6 +250,34 @@ def test_sql_semi_anti_join(ex, orc, how):
             ex.sql(sql, on_dev(ex, lines), right=on_dev(ex, orders))
 
 
+@pytest.mark.parametrize("sizes", [(30_000, 60_000), (0, 1000), (1000, 0)])
+def test_sql_full_outer_join(ex, orc, sizes):
+    """FULL OUTER JOIN = the LEFT join's pairs + the JOIN source's unmatched rows; each
+    side's aggregates skip the rows where that side is NULL (pandas outer merge)."""
+    orders, lines = tables(6, *sizes, miss=0.3)
+    if len(orders["o_okey"]):
+        orders["o_cust"][:40] += 7
+        lines["l_okey"][np.isin(lines["l_okey"], orders["o_okey"][:40])] = -5  # orders with no line
+    sql = """select count(*) as c, count(l_qty) as cl, sum(l_qty) as s, count(o_cust) as co,
+                    sum(o_cust) as so, sum(l_price) as p, min(o_okey) as mn, max(l_okey) as mx
+             from orders full outer join lineitem on o_okey = l_okey"""
+    got = ex.sql(sql, on_dev(ex, orders), right=on_dev(ex, lines))
+    m = pd.DataFrame(orders).merge(pd.DataFrame(lines), left_on="o_okey", right_on="l_okey", how="outer")
+    assert got["c"].tolist() == [len(m)]
+    assert got["cl"].tolist() == [int(m.l_qty.notna().sum())]
+    assert got["co"].tolist() == [int(m.o_cust.notna().sum())]
+    assert got["s"].tolist() == [int(m.l_qty.sum())]
+    assert got["so"].tolist() == [int(m.o_cust.sum())]
+    assert got["p"].tolist() == [float(m.l_price.sum())]  # dyadic values: exact in any order
+    if m.o_okey.notna().any():
+        assert got["mn"].tolist() == [int(m.o_okey.min())]
+    if m.l_okey.notna().any():
+        assert got["mx"].tolist() == [int(m.l_okey.max())]
+    with pytest.raises(NutError, match="FULL OUTER JOIN: column 'o_cust'"):
+        ex.sql("select o_cust, count(*) from orders full join lineitem on o_okey = l_okey group by o_cust",
+               on_dev(ex, orders), right=on_dev(ex, lines))
+
+
 def test_sql_join_scan_and_sort(ex, orc):
     orders, lines = tables(4, 10_000, 40_000)
     got = ex.sql("select l_qty from lineitem join orders on l_okey = o_okey where l_qty >= 30",
