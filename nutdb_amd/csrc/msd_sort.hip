@@ -28,6 +28,7 @@
 // Keys map to u64 with the sign bit flipped (DESC: its complement) on the first load and
 // back on the final store.
 #include <algorithm>
+#include <cstdlib>
 #include <vector>
 
 #include "common.hpp"
@@ -135,10 +136,17 @@ __device__ __forceinline__ uint64_t *ms_dst(const MsBufs &bf, uint32_t buf) { re
 // Persistent: workgroup b takes tiles b, b + grid, ...; the next tile's keys are loaded into
 // the key registers as soon as the current tile is staged in LDS, so its HBM latency hides
 // behind the current tile's write-out (and the segment lookup behind the ranking).
+// H = 2: 32 Ki-key tiles (32 keys per lane in registers), staged and written out in two
+// halves of the tile's digit order through the same 16 Ki-key LDS buffer, so each digit's
+// output run per tile is twice as long (512 B instead of 256 B: fewer partial 128-B lines).
+template <int H>
 __global__ __launch_bounds__(MS_THREADS) void ms_scatter_kernel(MsBufs bf, const MsSeg *__restrict__ segs,
                                                                    const uint32_t *__restrict__ tile_seg, uint32_t ntiles,
                                                                    MsDigit dg, uint64_t flip,
                                                                    unsigned long long *__restrict__ cursor) {
+  constexpr int ITEMS = MS_ITEMS * H;
+  constexpr uint32_t TILE = MS_TILE * H;
+  static_assert(TILE <= 65536, "16-bit ranks");
   __shared__ uint64_t s_keys[MS_TILE];
   __shared__ uint32_t s_cnt[MS_BINS];
   __shared__ uint32_t s_tex[MS_BINS];
@@ -146,33 +154,33 @@ __global__ __launch_bounds__(MS_THREADS) void ms_scatter_kernel(MsBufs bf, const
   __shared__ uint32_t s_wsum[MS_BINS / kWave];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   uint32_t t = blockIdx.x;
-  uint64_t key[MS_ITEMS];
+  uint64_t key[ITEMS];
   auto load = [&](uint32_t tt, const MsSeg &g) {
-    const uint64_t lo = (uint64_t)(tt - g.aux) * MS_TILE;
-    const uint32_t cn = (uint32_t)min<uint64_t>(MS_TILE, g.count - lo);
+    const uint64_t lo = (uint64_t)(tt - g.aux) * TILE;
+    const uint32_t cn = (uint32_t)min<uint64_t>(TILE, g.count - lo);
     const uint64_t *sp = ms_src(bf, g.buf) + g.start + lo;
     const uint64_t ff = g.buf == 0 ? flip : 0;
-    // every load unconditional (clamped to the tile): all MS_ITEMS stay in flight together
+    // every load unconditional (clamped to the tile): all ITEMS stay in flight together
 #pragma unroll
-    for (int i = 0; i < MS_ITEMS; ++i)
+    for (int i = 0; i < ITEMS; ++i)
       key[i] = __builtin_nontemporal_load(sp + min((uint32_t)i * MS_THREADS + tid, cn - 1)) ^ ff;
   };
   uint32_t s = tile_seg[t];
   MsSeg sg = segs[s];
   load(t, sg);
   for (;;) {
-    const uint64_t lo = (uint64_t)(t - sg.aux) * MS_TILE;
-    const uint32_t cnt = (uint32_t)min<uint64_t>(MS_TILE, sg.count - lo);
+    const uint64_t lo = (uint64_t)(t - sg.aux) * TILE;
+    const uint32_t cnt = (uint32_t)min<uint64_t>(TILE, sg.count - lo);
     uint64_t *dst = ms_dst(bf, sg.buf);
     const uint32_t next = t + gridDim.x;
     const uint32_t ns = next < ntiles ? tile_seg[next] : 0;
     if (tid < MS_BINS) s_cnt[tid] = 0;
     __syncthreads();
-    uint32_t rk[MS_ITEMS / 2];  // ranks in the tile's digit run (< 16384), 16-bit pairs
+    uint32_t rk[ITEMS / 2];  // ranks in the tile's digit run (< TILE), 16-bit pairs
 #pragma unroll
-    for (int i = 0; i < MS_ITEMS; i += 2) rk[i / 2] = 0;
+    for (int i = 0; i < ITEMS; i += 2) rk[i / 2] = 0;
 #pragma unroll
-    for (int i = 0; i < MS_ITEMS; ++i) {
+    for (int i = 0; i < ITEMS; ++i) {
       const uint32_t idx = (uint32_t)i * MS_THREADS + tid;
       if (idx < cnt) rk[i / 2] |= atomicAdd(&s_cnt[dg(key[i])], 1u) << (16 * (i & 1));
     }
@@ -196,26 +204,40 @@ __global__ __launch_bounds__(MS_THREADS) void ms_scatter_kernel(MsBufs bf, const
       const uint32_t tex = incl - c + add;
       s_tex[tid] = tex;
       const uint64_t gb = c ? (uint64_t)atomicAdd(&cursor[(uint64_t)s * MS_BINS + tid], (unsigned long long)c) : 0;
-      s_gb[tid] = gb - tex;  // out position of LDS slot j of this digit = s_gb[d] + j
+      s_gb[tid] = gb - tex;  // out position of tile slot j of this digit = s_gb[d] + j
     }
     __syncthreads();
+    // rank -> tile slot, in place (16-bit pairs)
 #pragma unroll
-    for (int i = 0; i < MS_ITEMS; ++i) {
-      const uint32_t idx = (uint32_t)i * MS_THREADS + tid;
-      if (idx < cnt) s_keys[s_tex[dg(key[i])] + ((rk[i / 2] >> (16 * (i & 1))) & 0xFFFFu)] = key[i];
+    for (int i = 0; i < ITEMS; i += 2) {
+      const uint32_t s0 = s_tex[dg(key[i])] + (rk[i / 2] & 0xFFFFu);
+      const uint32_t s1 = s_tex[dg(key[i + 1])] + (rk[i / 2] >> 16);
+      rk[i / 2] = (s0 & 0xFFFFu) | (s1 << 16);
     }
     MsSeg nsg = sg;
-    if (next < ntiles) {  // the key registers are free: fetch the next tile now
-      nsg = segs[ns];
-      load(next, nsg);
-    }
-    __syncthreads();
 #pragma unroll
-    for (int i = 0; i < MS_ITEMS; ++i) {
-      const uint32_t j = (uint32_t)i * MS_THREADS + tid;
-      if (j < cnt) {
-        const uint64_t k = s_keys[j];
-        dst[s_gb[dg(k)] + j] = k;  // (non-temporal stores measured 2.4 ms slower per sort)
+    for (int h = 0; h < H; ++h) {
+      if (h) __syncthreads();  // the previous half's write-out is done with s_keys
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i) {
+        const uint32_t idx = (uint32_t)i * MS_THREADS + tid;
+        const uint32_t slot = (rk[i / 2] >> (16 * (i & 1))) & 0xFFFFu;
+        if (idx < cnt && (H == 1 || slot / MS_TILE == (uint32_t)h)) s_keys[slot % MS_TILE] = key[i];
+      }
+      if (h == H - 1 && next < ntiles) {  // the key registers are free: fetch the next tile now
+        nsg = segs[ns];
+        load(next, nsg);
+      }
+      __syncthreads();
+      // H = 2: not fully unrolled, or the scheduler hoists every item's LDS read (and its
+      // registers) above the first store while the next tile's 32 keys are in flight
+#pragma unroll(H == 1 ? MS_ITEMS : 2)
+      for (int i = 0; i < MS_ITEMS; ++i) {
+        const uint32_t j = (uint32_t)i * MS_THREADS + tid, jj = j + (uint32_t)h * MS_TILE;
+        if (jj < cnt) {
+          const uint64_t k = s_keys[j];
+          dst[s_gb[dg(k)] + jj] = k;  // (non-temporal stores measured 2.4 ms slower per sort)
+        }
       }
     }
     if (next >= ntiles) break;
@@ -960,6 +982,23 @@ static nut_status launch_local_dev(nut_ctx *c, const MsBufs &bf, uint64_t base, 
   return NUT_OK;
 }
 
+// Scatter tile halves (ms_scatter_kernel<H>): NUT_MS_HALVES=1 keeps 16 Ki-key tiles
+static int ms_halves() {
+  static const int h = [] {
+    const char *e = getenv("NUT_MS_HALVES");
+    return e && atoi(e) == 1 ? 1 : 2;
+  }();
+  return h;
+}
+
+static void launch_scatter(hipStream_t st, unsigned grid, const MsBufs &bf, const MsSeg *segs, const uint32_t *tiles,
+                           uint32_t ntiles, const MsDigit &dg, uint64_t flip, unsigned long long *cur) {
+  if (ms_halves() == 2)
+    hipLaunchKernelGGL(ms_scatter_kernel<2>, dim3(grid), dim3(MS_THREADS), 0, st, bf, segs, tiles, ntiles, dg, flip, cur);
+  else
+    hipLaunchKernelGGL(ms_scatter_kernel<1>, dim3(grid), dim3(MS_THREADS), 0, st, bf, segs, tiles, ntiles, dg, flip, cur);
+}
+
 // One device-planned level over `big` (segments whose sizes the host knows): histogram,
 // plan (cursors + class lists on the device), scatter, local sorts of the listed classes.
 // Only the four class counts come back to the host (read while the scatter runs); the
@@ -972,7 +1011,7 @@ static nut_status device_level(nut_ctx *c, MetaArena &ar, const MsBufs &bf, cons
   const uint64_t nht = tile_table(big, MH_HTILE, tiles);
   std::vector<uint32_t> stiles;
   std::vector<MsSeg> sbig = big;
-  const uint64_t nst = tile_table(sbig, MS_TILE, stiles);
+  const uint64_t nst = tile_table(sbig, MS_TILE * ms_halves(), stiles);
   if (nht > 0x7FFFFFFFull || nst > 0x7FFFFFFFull) return fail(NUT_ERR_UNSUPPORTED, "nut_sort_i64: too many tiles");
   const uint64_t ns = big.size(), cap = ns * MS_BINS;
   const size_t hbytes = ns * MS_BINS * 8;
@@ -1006,9 +1045,8 @@ static nut_status device_level(nut_ctx *c, MetaArena &ar, const MsBufs &bf, cons
   hipError_t e = hipMemcpyAsync(hc, counts, 16, hipMemcpyDeviceToHost, st);
   if (e == hipSuccess) e = hipEventRecord(ev, st);
   if (e == hipSuccess)
-    hipLaunchKernelGGL(ms_scatter_kernel, dim3((unsigned)std::min<uint64_t>(nst, (uint64_t)c->num_cus)),
-                       dim3(MS_THREADS), 0, st, bf, (const MsSeg *)dsseg, (const uint32_t *)dstile, (uint32_t)nst, dg,
-                       flip, dcur);
+    launch_scatter(st, (unsigned)std::min<uint64_t>(nst, (uint64_t)c->num_cus), bf, (const MsSeg *)dsseg,
+                   (const uint32_t *)dstile, (uint32_t)nst, dg, flip, dcur);
   if (e == hipSuccess) e = hipGetLastError();
   if (e == hipSuccess) e = hipEventSynchronize(ev);  // the counts, while the scatter runs
   (void)hipEventDestroy(ev);
@@ -1141,7 +1179,7 @@ nut_status msd_sort_i64(nut_ctx *c, const int64_t *in, int64_t *out, uint64_t n,
           run += cnt;
         }
       }
-      const uint64_t nst = tile_table(scat, MS_TILE, tiles);
+      const uint64_t nst = tile_table(scat, MS_TILE * ms_halves(), tiles);
       if (nst > 0x7FFFFFFFull) return fail(NUT_ERR_UNSUPPORTED, "nut_sort_i64: too many tiles");
       s = ar.begin(MetaArena::align(scat.size() * sizeof(MsSeg)) + MetaArena::align(tiles.size() * 4) +
                    MetaArena::align(cursor.size() * 8));
@@ -1153,8 +1191,8 @@ nut_status msd_sort_i64(nut_ctx *c, const int64_t *in, int64_t *out, uint64_t n,
       for (const MsSeg &sg : scat) c->sort_bytes += 16 * sg.count;
       ++c->sort_levels;
       const unsigned sgrid = (unsigned)std::min<uint64_t>(nst, (uint64_t)c->num_cus);  // persistent, 1 per CU (128 KB LDS)
-      hipLaunchKernelGGL(ms_scatter_kernel, dim3(sgrid), dim3(MS_THREADS), 0, st, bf, (const MsSeg *)dsc,
-                         (const uint32_t *)dt, (uint32_t)nst, dg, flip, (unsigned long long *)dcur);
+      launch_scatter(st, sgrid, bf, (const MsSeg *)dsc, (const uint32_t *)dt, (uint32_t)nst, dg, flip,
+                     (unsigned long long *)dcur);
       NUT_HIP(hipGetLastError());
     }
     big.swap(next);

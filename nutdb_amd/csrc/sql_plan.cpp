@@ -332,6 +332,7 @@ struct nut_plan {
   struct JoinStep {
     std::string table, alias;
     int key[2];
+    int type = NUT_JOIN_INNER;  // NUT_JOIN_INNER or NUT_JOIN_LEFT
   };
   std::vector<JoinStep> jn;
   bool jright = false;     // RIGHT OUTER / SEMI / ANTI: the JOIN source is the preserved side
@@ -1084,17 +1085,21 @@ bool lower_mode(const Statement &st, nut_plan &p, Lowering &L) {
   if (b.distinct && b.group_by) return L.fail("DISTINCT with GROUP BY is not executed");
   if (!b.from || b.from->k != SourceKind::Table) return L.fail("FROM must name one table");
   std::vector<std::pair<int, int>> join_extra;  // residual ON equalities (INNER), applied as WHERE terms
-  if (b.joins.size() > 1) {  // a chain of INNER joins: FROM t0 JOIN t1 ON .. JOIN t2 ON ..
+  if (b.joins.size() > 1) {  // a chain of INNER / LEFT joins: FROM t0 JOIN t1 ON .. LEFT JOIN t2 ON ..
     p.join = NUT_JOIN_INNER;
     if (b.from->alias) p.talias = std::string(*b.from->alias);
     for (const JoinClause &jc : b.joins) {
       if (jc.src.k != SourceKind::Table) return L.fail("JOIN source must be a table");
       if (!jc.on) return L.fail("JOIN ... USING in a chain of joins is not executed (ON a = b)");
-      if (jc.t != JoinType::Inner) return L.fail("several JOINs: INNER only");
+      if (jc.t != JoinType::Inner && jc.t != JoinType::LeftOuter)
+        return L.fail("several JOINs: INNER and LEFT OUTER only");
       std::vector<std::pair<int, int>> eqs;
       if (!on_equalities(p, jc.cond, eqs))
         return L.fail("JOIN ON must be equalities of two columns (ANDed)");
+      if (eqs.size() > 1 && jc.t != JoinType::Inner)
+        return L.fail("JOIN with several key columns: INNER only (outer / semi / anti joins take one ON equality)");
       nut_plan::JoinStep js;
+      js.type = jc.t == JoinType::Inner ? NUT_JOIN_INNER : NUT_JOIN_LEFT;
       js.table = std::string(jc.src.table);
       if (jc.src.alias) js.alias = std::string(*jc.src.alias);
       js.key[0] = eqs[0].first;
@@ -1240,7 +1245,9 @@ bool lower_mode(const Statement &st, nut_plan &p, Lowering &L) {
     }
     if (p.aggs.size() > NUT_MAX_AGGS) return L.fail("more than 8 aggregates (HAVING / ORDER BY included)");
     if (p.vals.size() > NUT_MAX_VALS) return L.fail("aggregates reference more than 4 value columns");
-    if (!p.compiled && (p.join == NUT_JOIN_LEFT || p.join == PJ_FULL))  // NULL-extended rows need aggregate masks
+    bool outer = p.join == NUT_JOIN_LEFT || p.join == PJ_FULL;
+    for (const nut_plan::JoinStep &js : p.jn) outer = outer || js.type == NUT_JOIN_LEFT;
+    if (!p.compiled && outer)  // NULL-extended rows need aggregate masks
       return L.fail("outer-join aggregates lower to expression mode");
     return true;
   }
@@ -1502,6 +1509,7 @@ std::string describe(const nut_plan &p) {
         if (k) o += ',';
         o += "{\"table\":";
         json_str(o, p.jn[k].table);
+        o += p.jn[k].type == NUT_JOIN_LEFT ? ",\"type\":\"left\"" : ",\"type\":\"inner\"";
         o += ",\"on\":[";
         json_str(o, p.cols[p.jn[k].key[0]]);
         o += ',';
@@ -2337,6 +2345,18 @@ PProg pred_prog(const PlanPred &pr) {
   return r;
 }
 
+// an aggregate's row mask gains (column m != 0) [AND its own mask]: outer joins' NULL rows
+void add_null_mask(PlanAgg &a, int m) {
+  const bool had = !a.mask.empty();
+  PNode col;
+  col.op = NUT_P_COL;
+  col.col = m;
+  a.mask.push_back(col);
+  emit_int(a.mask, 0);
+  emit(a.mask, NUT_P_NE);
+  if (had) emit(a.mask, NUT_P_AND);
+}
+
 // ldict / rdict (may be null): the dictionary of each column of lc / rc (typed tables)
 nut_status exec_join(nut_ctx *c, const nut_plan &p, const nut_column *lc, int nl, uint64_t lrows,
                      const nut_column *rc, int nr, uint64_t rrows, uint64_t hint, nut_result *r,
@@ -2564,24 +2584,14 @@ nut_status exec_join(nut_ctx *c, const nut_plan &p, const nut_column *lc, int nl
       p2.cols.push_back("__lmatched");
       jc.push_back(nut_column{p2.cols[nc + 1].c_str(), lmask.p, NUT_T_I64});
     }
-    auto add_mask = [](PlanAgg &a, int m) {  // (m != 0) [AND the argument's own mask]
-      const bool had = !a.mask.empty();
-      PNode col;
-      col.op = NUT_P_COL;
-      col.col = m;
-      a.mask.push_back(col);
-      emit_int(a.mask, 0);
-      emit(a.mask, NUT_P_NE);
-      if (had) emit(a.mask, NUT_P_AND);
-    };
     for (PlanAgg &a : p2.aggs) {
       bool other = false, mine = false;
       for (int ref : a.refs) {
         other = other || side[ref] != ps;
         mine = mine || side[ref] == ps;
       }
-      if (other) add_mask(a, (int)nc);
-      if (full && mine) add_mask(a, (int)nc + 1);
+      if (other) add_null_mask(a, (int)nc);
+      if (full && mine) add_null_mask(a, (int)nc + 1);
     }
   }
   std::vector<const nut_column *> bound(p2.cols.size());
@@ -2658,6 +2668,37 @@ nut_status exec_joinn(nut_ctx *c, const nut_plan &p, const nut_column *const *ta
       return fail(NUT_ERR_PLAN, "JOIN " + std::to_string(t) + ": string keys are not executed (each table has its own "
                                     "dictionary)");
   }
+  auto in_prog = [](const PProg &pp, int i) {
+    for (const PNode &nd : pp)
+      if ((nd.op == NUT_P_COL || nd.op == P_LIKE || nd.op == P_ILIKE) && nd.col == i) return true;
+    return false;
+  };
+  // read by plan q after the joins: as a row decider / projection / key, or inside an aggregate
+  auto reads = [&](const nut_plan &q, int ci, bool &row, bool &agg) {
+    row = ci == q.proj || in_prog(q.where, ci);
+    for (int pj : q.projs) row = row || pj == ci;
+    for (int k2 : q.keys) row = row || k2 == ci;
+    for (const PlanPred &pr : q.preds) row = row || pr.col == ci;
+    agg = false;
+    for (int v : q.vals) agg = agg || v == ci;
+    for (const PlanAgg &a : q.aggs) {
+      for (int ref : a.refs) agg = agg || ref == ci;
+      agg = agg || in_prog(a.val, ci) || in_prog(a.mask, ci);
+    }
+  };
+  // NULL-extended tables: the ones joined by LEFT (their accumulated row ids hold -1 on the
+  // NULL rows; an INNER step on such a table's key drops them, a LEFT step keeps them, its
+  // own table NULL there).  As for one LEFT join, their columns may only feed aggregates,
+  // which skip the NULL rows.
+  std::vector<char> nullable(nt, 0);
+  for (int k = 0; k + 1 < nt; ++k) nullable[k + 1] = p.jn[k].type == NUT_JOIN_LEFT;
+  for (size_t i = 0; i < nc; ++i) {
+    bool row, agg;
+    reads(p, (int)i, row, agg);
+    if (row && nullable[side[i]])
+      return fail(NUT_ERR_PLAN, "outer JOIN: the NULL-extended table's column '" + p.cols[i] +
+                                    "' may only appear inside aggregates");
+  }
   nut_plan p2 = p;
   std::vector<std::vector<PProg>> push(nt);
   if (p.compiled) {
@@ -2697,6 +2738,29 @@ nut_status exec_joinn(nut_ctx *c, const nut_plan &p, const nut_column *const *ta
     if (out.alloc(c, std::max<uint64_t>(n, 1) * 8) != hipSuccess) return fail(NUT_ERR_OOM, "hipMalloc (join)");
     return n ? nut_gather_u64(c, (const uint64_t *)col, idx, n, 0, (uint64_t *)out.p) : NUT_OK;
   };
+  // positions i < n with (rowids[i] cmp 0), ascending (a one-column WHERE program)
+  auto select_pos = [&](const int64_t *rowids, uint64_t n, int cmp, DevBuf &out, uint64_t *cnt) -> nut_status {
+    nut_plan q;
+    q.compiled = true;
+    q.cols = {"__row"};
+    PNode col;
+    col.op = NUT_P_COL;
+    col.col = 0;
+    q.where.push_back(col);
+    emit_int(q.where, 0);
+    emit(q.where, cmp);
+    const nut_column rc{q.cols[0].c_str(), rowids, NUT_T_I64};
+    const nut_column *rs[1] = {&rc};
+    const Dict *rd[1] = {nullptr};
+    nut_agg_spec spec;
+    ProgStore store;
+    std::vector<int> agg_f64;
+    nut_status es = build_spec(q, rs, rd, n, spec, store, agg_f64);
+    if (es) return es;
+    if (out.alloc(c, std::max<uint64_t>(n, 1) * 8) != hipSuccess) return fail(NUT_ERR_OOM, "hipMalloc (join)");
+    *cnt = 0;
+    return n ? nut_select_rows(c, &spec, (int64_t *)out.p, cnt) : NUT_OK;
+  };
   std::vector<DevBuf> acc(nt);
   std::vector<const int64_t *> accp(nt, nullptr);
   accp[0] = (const int64_t *)ids[0].p;
@@ -2704,9 +2768,21 @@ nut_status exec_joinn(nut_ctx *c, const nut_plan &p, const nut_column *const *ta
   nut_status st = NUT_OK;
   for (int k = 0; k + 1 < nt && !st; ++k) {
     const int t = k + 1, u = side[kold[k]];
-    DevBuf pk, bk;
+    const bool left = p.jn[k].type == NUT_JOIN_LEFT;
+    DevBuf pk, bk, vpos, vrow, npos;
     const int64_t *pkd = (const int64_t *)src[kold[k]]->data, *bkd = (const int64_t *)src[knew[k]]->data;
-    if (accp[u]) {
+    const int64_t *prow = nullptr;  // probe row of each probe key (nullptr: its position)
+    uint64_t np = ncur, nnull = 0;
+    if (nullable[u]) {
+      // a NULL ON key matches nothing: probe only the positions whose table-u row exists;
+      // LEFT appends the others as (position, -1)
+      if ((st = select_pos(accp[u], ncur, NUT_P_GE, vpos, &np))) break;
+      if (left && (st = select_pos(accp[u], ncur, NUT_P_LT, npos, &nnull))) break;
+      if ((st = gather_to(accp[u], (const int64_t *)vpos.p, np, vrow))) break;
+      if ((st = gather_to(pkd, (const int64_t *)vrow.p, np, pk))) break;
+      pkd = (const int64_t *)pk.p;
+      prow = (const int64_t *)vpos.p;
+    } else if (accp[u]) {
       if ((st = gather_to(pkd, accp[u], ncur, pk))) break;
       pkd = (const int64_t *)pk.p;
     }
@@ -2714,28 +2790,34 @@ nut_status exec_joinn(nut_ctx *c, const nut_plan &p, const nut_column *const *ta
       if ((st = gather_to(bkd, (const int64_t *)ids[t].p, rows[t], bk))) break;
       bkd = (const int64_t *)bk.p;
     }
+    // pairs (accumulated position, table-t row): the pushed-down ids ride along as rows
     DevBuf pairs;
-    uint64_t cap = std::max<uint64_t>(ncur, 1), m = 0;
+    uint64_t cap = std::max<uint64_t>(np, 1), m = 0, half = 0;
     for (;;) {
-      if (pairs.alloc(c, cap * 16) != hipSuccess) return fail(NUT_ERR_OOM, "hipMalloc (join index)");
-      st = nut_join_i64_into(c, bkd, rows[t], pkd, ncur,
-                             NUT_JOIN_INNER | (p.kind == NUT_PLAN_GROUPBY ? NUT_JOIN_ANY_ORDER : 0),
-                             (int64_t *)pairs.p, (int64_t *)pairs.p + cap, cap, &m);
+      half = cap + nnull;
+      if (pairs.alloc(c, half * 16) != hipSuccess) return fail(NUT_ERR_OOM, "hipMalloc (join index)");
+      st = join_i64_into_rows(c, bkd, (const int64_t *)ids[t].p, rows[t], pkd, prow, np,
+                              (left ? NUT_JOIN_LEFT : NUT_JOIN_INNER) |
+                                  (p.kind == NUT_PLAN_GROUPBY ? NUT_JOIN_ANY_ORDER : 0),
+                              (int64_t *)pairs.p, (int64_t *)pairs.p + half, cap, &m);
       if (st != NUT_ERR_CAPACITY || m <= cap) break;
       pairs.reset();
       cap = m;
     }
     if (st) break;
-    const int64_t *pi = (const int64_t *)pairs.p, *bi = pi + cap;
+    int64_t *pi = (int64_t *)pairs.p, *bi = pi + half;
+    if (nnull) {
+      NUT_HIP(hipMemcpyAsync(pi + m, npos.p, nnull * 8, hipMemcpyDeviceToDevice, c->stream));
+      NUT_HIP(hipMemsetAsync(bi + m, 0xFF, nnull * 8, c->stream));  // -1: no table-t row
+      m += nnull;
+    }
     std::vector<DevBuf> next(nt);
     for (int v = 0; v <= t && !st; ++v) {
-      const int64_t *base = v == t ? (const int64_t *)ids[t].p : accp[v];
-      const int64_t *through = v == t ? bi : pi;
-      if (base) {
-        st = gather_to(base, through, m, next[v]);
+      if (v < t && accp[v]) {
+        st = gather_to(accp[v], pi, m, next[v]);
       } else {
         if (next[v].alloc(c, std::max<uint64_t>(m, 1) * 8) != hipSuccess) return fail(NUT_ERR_OOM, "hipMalloc");
-        if (m) NUT_HIP(hipMemcpyAsync(next[v].p, through, m * 8, hipMemcpyDeviceToDevice, c->stream));
+        if (m) NUT_HIP(hipMemcpyAsync(next[v].p, v == t ? bi : pi, m * 8, hipMemcpyDeviceToDevice, c->stream));
       }
     }
     if (st) break;
@@ -2748,11 +2830,6 @@ nut_status exec_joinn(nut_ctx *c, const nut_plan &p, const nut_column *const *ta
     ncur = m;
   }
   if (st) return st;
-  auto in_prog = [](const PProg &pp, int i) {
-    for (const PNode &nd : pp)
-      if ((nd.op == NUT_P_COL || nd.op == P_LIKE || nd.op == P_ILIKE) && nd.col == i) return true;
-    return false;
-  };
   std::vector<DevBuf> bufs(nc);
   std::vector<nut_column> jc(nc);
   for (size_t i = 0; i < nc; ++i) {
@@ -2774,8 +2851,28 @@ nut_status exec_joinn(nut_ctx *c, const nut_plan &p, const nut_column *const *ta
     if (st) return st;
     jc[i] = nut_column{p.cols[i].c_str(), bufs[i].p, src[i]->type};
   }
-  std::vector<const nut_column *> bound(nc);
-  for (size_t i = 0; i < nc; ++i) bound[i] = &jc[i];
+  // aggregates over a NULL-extended table skip its NULL rows: (__matched<t> != 0) per table read
+  std::vector<DevBuf> mbuf(nt);
+  p2.cols.reserve(nc + nt);  // jc keeps c_str() pointers into p2.cols
+  for (int v = 1; v < nt && p2.kind == NUT_PLAN_GROUPBY; ++v) {
+    if (!nullable[v]) continue;
+    std::vector<PlanAgg *> reading;
+    for (PlanAgg &a : p2.aggs) {
+      bool rd = false;
+      for (int ref : a.refs) rd = rd || side[ref] == v;
+      if (rd) reading.push_back(&a);
+    }
+    if (reading.empty()) continue;
+    if (mbuf[v].alloc(c, std::max<uint64_t>(ncur, 1) * 8) != hipSuccess) return fail(NUT_ERR_OOM, "hipMalloc");
+    if ((st = join_matched(c, accp[v], ncur, (int64_t *)mbuf[v].p))) return st;
+    const int mc = (int)p2.cols.size();
+    p2.cols.push_back("__matched" + std::to_string(v));
+    jc.push_back(nut_column{p2.cols[mc].c_str(), mbuf[v].p, NUT_T_I64});
+    for (PlanAgg *a : reading) add_null_mask(*a, mc);
+  }
+  sdict.resize(p2.cols.size());
+  std::vector<const nut_column *> bound(jc.size());
+  for (size_t i = 0; i < jc.size(); ++i) bound[i] = &jc[i];
   st = p2.kind == NUT_PLAN_GROUPBY ? exec_groupby(c, p2, bound.data(), sdict.data(), ncur, hint, r)
                                    : exec_scan(c, p2, bound.data(), sdict.data(), ncur, r);
   NUT_HIP(hipStreamSynchronize(c->stream));

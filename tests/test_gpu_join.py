@@ -436,3 +436,61 @@ def test_sql_join_using_and_multi_key(ex, orc):
     got = ex.sql("select count(*) as c, sum(k) as sk from t2 left join t1 using (k)", on_dev(ex, t2),
                  right=on_dev(ex, t1))
     assert got["c"].tolist() == [n2] and got["sk"].tolist() == [int(t2["k"].sum())]
+
+
+def test_sql_left_join_chain(ex, orc):
+    """Chains with LEFT OUTER steps (the shape of the reference's fixture tests/sql/10.sql):
+    INNER, then LEFT, then LEFT through a NULL-extended table's ON key (a NULL key matches
+    nothing), or INNER through it (its NULL rows drop).  Aggregates over NULL-extended
+    tables skip their NULL rows; pandas merges are the reference."""
+    rng = np.random.default_rng(123)
+    no, nl = 20_000, 60_000
+    orders = {"o_okey": rng.permutation(no).astype(np.int64), "o_cust": rng.integers(0, 3000, no).astype(np.int64)}
+    lines = {"l_okey": rng.integers(-500, no, nl).astype(np.int64), "l_qty": rng.integers(1, 50, nl).astype(np.int64)}
+    cust = {"c_key": rng.permutation(3000)[:2000].astype(np.int64),  # a third of the customers missing
+            "c_nation": rng.integers(0, 40, 2000).astype(np.int64)}
+    nk = np.concatenate([np.arange(30), np.arange(10)])  # nations 30..39 missing, 0..9 twice
+    nation = {"n_key": nk.astype(np.int64), "n_region": rng.integers(0, 5, len(nk)).astype(np.int64)}
+    dl, do, dc, dn = (pd.DataFrame(t) for t in (lines, orders, cust, nation))
+    right = [on_dev(ex, orders), on_dev(ex, cust), on_dev(ex, nation)]
+    base = dl.merge(do, left_on="l_okey", right_on="o_okey").merge(dc, left_on="o_cust", right_on="c_key", how="left")
+    for how in ("left", "inner"):
+        m = base.merge(dn, left_on="c_nation", right_on="n_key", how=how)
+        m = m[m.l_qty < 40]
+        kw = "left join" if how == "left" else "join"
+        got = ex.sql(f"""select l_qty, count(*) as c, count(c_nation) as cc, sum(c_nation) as sc,
+                           count(n_region) as cr, sum(n_region) as sr, max(n_region) as mr
+                         from lineitem join orders on l_okey = o_okey left join customer on o_cust = c_key
+                         {kw} nation on c_nation = n_key where l_qty < 40 group by l_qty order by l_qty""",
+                     on_dev(ex, lines), right=right)
+        g = m.groupby("l_qty").agg(c=("l_qty", "size"), cc=("c_nation", "count"), sc=("c_nation", "sum"),
+                                   cr=("n_region", "count"), sr=("n_region", "sum"), mr=("n_region", "max"))
+        assert got["l_qty"].tolist() == g.index.tolist(), how
+        for col in ("c", "cc", "sc", "cr", "sr"):
+            assert got[col].tolist() == g[col].astype(np.int64).tolist(), (how, col)
+        ok = g.mr.notna().to_numpy()
+        assert got["mr"][ok].tolist() == g.mr[ok].astype(np.int64).tolist(), how
+        if how == "inner":
+            assert m.c_nation.notna().all()
+    # global aggregates over a chain preserved from the FROM table; a scan keeps every row
+    m = do.merge(dc, left_on="o_cust", right_on="c_key", how="left").merge(dn, left_on="c_nation", right_on="n_key",
+                                                                          how="left")
+    got = ex.sql("select count(*) as c, sum(n_region) as s, count(c_key) as k from orders "
+                 "left join customer on o_cust = c_key left join nation on c_nation = n_key",
+                 on_dev(ex, orders), right=right[1:])
+    assert got["c"].tolist() == [len(m)] and got["s"].tolist() == [int(m.n_region.sum())]
+    assert got["k"].tolist() == [int(m.c_key.notna().sum())]
+    got = ex.sql("select o_okey from orders left join customer on o_cust = c_key left join nation on c_nation = n_key "
+                 "where o_cust < 100 order by o_okey", on_dev(ex, orders), right=right[1:])
+    assert got["o_okey"].tolist() == sorted(m.o_okey[m.o_cust < 100].tolist())
+    # an INNER step on a NULL-extended key: its own table is never NULL (may be a group key)
+    m = do.merge(dc, left_on="o_cust", right_on="c_key", how="left").merge(dn, left_on="c_nation", right_on="n_key")
+    got = ex.sql("select n_region, count(*) as c, count(c_key) as k from orders left join customer on o_cust = c_key "
+                 "join nation on c_nation = n_key group by n_region order by n_region", on_dev(ex, orders),
+                 right=right[1:])
+    g = m.groupby("n_region").agg(c=("o_okey", "size"), k=("c_key", "count"))
+    assert got["n_region"].tolist() == g.index.tolist() and got["c"].tolist() == g.c.tolist()
+    assert got["k"].tolist() == g.k.tolist()
+    with pytest.raises(NutError, match="may only appear inside aggregates"):
+        ex.sql("select n_region, count(*) from orders join customer on o_cust = c_key left join nation "
+               "on c_nation = n_key group by n_region", on_dev(ex, orders), right=right[1:])

@@ -84,7 +84,7 @@ def test_sql_no_join_has_no_join_key():
     ("select count(*) from a left join b on x = y and u = v", "INNER only"),
     ("select count(*) from a left semi join b using (x, y)", "INNER only"),
     ("select count(*) from a join b using (x) join c using (x)", "USING in a chain"),
-    ("select count(*) from a join b on x = y full join c on y = z", "INNER only"),
+    ("select count(*) from a join b on x = y full join c on y = z", "INNER and LEFT OUTER only"),
     ("select count(*) from a join (select x from b) on x = y", "must be a table")])
 def test_sql_join_rejections(sql, msg):
     from nutdb_amd import NutError
@@ -130,11 +130,18 @@ def test_sql_join_chain_lowering():
     from nutdb_amd.sql import Plan
     d = Plan("select c_nation, count(*) from lineitem join orders on l_okey = o_okey join customer on "
              "o_cust = c_key group by c_nation").describe()
-    assert d["joins"] == [{"table": "orders", "on": ["l_okey", "o_okey"]},
-                          {"table": "customer", "on": ["o_cust", "c_key"]}]
+    assert d["joins"] == [{"table": "orders", "type": "inner", "on": ["l_okey", "o_okey"]},
+                          {"table": "customer", "type": "inner", "on": ["o_cust", "c_key"]}]
+    # LEFT OUTER steps (fixture 10's chain shape); other types and several LEFT keys are not
+    d = Plan("select count(*) from a join b on x = y left join c on y = z left join d on z = w").describe()
+    assert [j["type"] for j in d["joins"]] == ["inner", "left", "left"]
+    # aggregates over a chain with a LEFT step take expression mode (NULL-row masks)
+    assert Plan("select x, sum(z) from a join b on x = y left join c on y = z group by x").describe()["mode"] == "compiled"
     from nutdb_amd import NutError
-    with pytest.raises(NutError, match="INNER only"):
-        Plan("select count(*) from a join b on x = y left join c on y = z")
+    with pytest.raises(NutError, match="INNER and LEFT OUTER only"):
+        Plan("select count(*) from a join b on x = y right join c on y = z")
+    with pytest.raises(NutError, match="several key columns: INNER only"):
+        Plan("select count(*) from a join b on x = y left join c on y = z and x = w")
 
 
 def test_sql_join_using_and_multi_key_lowering():
@@ -152,4 +159,4 @@ def test_sql_join_using_and_multi_key_lowering():
     d = Plan("select count(*) from a join b on a.x = b.x and a.y = b.y where a.z > 1").describe()
     assert d["join"]["on"] == ["a.x", "b.x"] and d["where_expr"] == "((a.z > 1) and (a.y = b.y))"
     d = Plan("select count(*) from l join o on lk = ok join c on oc = ck and on_ = cn").describe()
-    assert d["joins"][1] == {"table": "c", "on": ["oc", "ck"]} and d["where_expr"] == "(on_ = cn)"
+    assert d["joins"][1] == {"table": "c", "type": "inner", "on": ["oc", "ck"]} and d["where_expr"] == "(on_ = cn)"
