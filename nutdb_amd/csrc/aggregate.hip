@@ -480,13 +480,58 @@ uint32_t gp_tiles(std::vector<GpSeg> &segs, uint32_t tile, std::vector<uint32_t>
 // [start, end) pairs are appended to *parts
 nut_status gp_level(nut_ctx *c, GpMeta &mm, std::vector<GpSeg> &segs, int shift, const uint64_t *const *src,
                     uint64_t *const *dst, int narr, bool gather, bool have_hist, std::vector<uint64_t> &hist,
-                    std::vector<uint64_t> *parts = nullptr, uint64_t kx = 0) {
+                    std::vector<uint64_t> *parts = nullptr, uint64_t kx = 0, uint64_t opt_cap = 0) {
   hipStream_t st = c->stream;
   std::vector<uint32_t> ts;
   nut_status s;
   GpSeg *dseg;
   uint32_t *dts;
   const size_t nh = gather ? 1 : segs.size();  // gather: every segment into one compact range
+  if (opt_cap) {
+    // optimistic layout (one segment, no histogram pass): digit d owns rows [d * opt_cap,
+    // (d + 1) * opt_cap) of dst (opt_cap even: 16-B aligned partitions); the counts are the
+    // cursors read back after the scatter; rows [256 * opt_cap, + 16 Ki) of every dst array
+    // must exist (overflowing runs land there).  NUT_ERR_CAPACITY (no message) if a digit
+    // outgrew its rows: nothing is usable, partition again with a histogram.
+    if (segs.size() != 1 || gather || have_hist || !parts || (opt_cap & 1))
+      return fail(NUT_ERR_INVALID_ARG, "gp_level: optimistic layout needs one segment");
+    std::vector<uint64_t> cur(GP_BINS + 1, 0);
+    for (int d = 0; d < GP_BINS; ++d) cur[d] = (uint64_t)d * opt_cap;
+    const uint32_t nst = gp_tiles(segs, 2 * GP_TILE, ts);
+    s = mm.begin(GpMeta::al(sizeof(GpSeg)) + GpMeta::al(ts.size() * 4 + 1) + GpMeta::al(cur.size() * 8));
+    if (s) return s;
+    uint64_t *dcur;
+    if ((s = mm.up(segs, &dseg)) || (s = mm.up(ts, &dts)) || (s = mm.up(cur, &dcur))) return s;
+    GpArrays ar;
+    for (int a = 0; a < GP_MAX_ARR; ++a) {
+      ar.src[a] = src[a];
+      ar.dst[a] = dst[a];
+    }
+    ar.narr = narr;
+    if (nst) {
+      const unsigned grid = std::min<unsigned>(nst, (unsigned)c->num_cus);
+      if (src[2])
+        hipLaunchKernelGGL((gp_scatter_kernel<2, 1024>), dim3(grid), dim3(1024), 0, st, ar, (const GpSeg *)dseg,
+                           (const uint32_t *)dts, nst, shift, 0, (unsigned long long *)dcur, kx, opt_cap);
+      else
+        hipLaunchKernelGGL((gp_scatter_kernel<1, 1024>), dim3(grid), dim3(1024), 0, st, ar, (const GpSeg *)dseg,
+                           (const uint32_t *)dts, nst, shift, 0, (unsigned long long *)dcur, kx, opt_cap);
+      NUT_HIP(hipGetLastError());
+    }
+    std::vector<uint64_t> back(GP_BINS + 1);
+    NUT_HIP(hipMemcpyAsync(back.data(), dcur, back.size() * 8, hipMemcpyDeviceToHost, st));
+    NUT_HIP(hipStreamSynchronize(st));
+    if (back[GP_BINS]) return NUT_ERR_CAPACITY;
+    hist.assign(GP_BINS, 0);
+    for (int d = 0; d < GP_BINS; ++d) {
+      hist[d] = back[d] - cur[d];
+      if (hist[d]) {
+        parts->push_back(cur[d]);
+        parts->push_back(back[d]);
+      }
+    }
+    return NUT_OK;
+  }
   if (!have_hist) {
     const uint32_t nht = gp_tiles(segs, GP_HTILE, ts);
     const size_t hb = nh * GP_BINS * 8;
@@ -540,20 +585,20 @@ nut_status gp_level(nut_ctx *c, GpMeta &mm, std::vector<GpSeg> &segs, int shift,
     const unsigned grid = std::min<unsigned>(nst, (unsigned)c->num_cus);
     if (src[2])
       hipLaunchKernelGGL((gp_scatter_kernel<2, 1024>), dim3(grid), dim3(1024), 0, st, ar, (const GpSeg *)dseg,
-                         (const uint32_t *)dts, nst, shift, gather ? 1 : 0, (unsigned long long *)dcur, kx);
+                         (const uint32_t *)dts, nst, shift, gather ? 1 : 0, (unsigned long long *)dcur, kx, 0);
     else
       hipLaunchKernelGGL((gp_scatter_kernel<1, 1024>), dim3(grid), dim3(1024), 0, st, ar, (const GpSeg *)dseg,
-                         (const uint32_t *)dts, nst, shift, gather ? 1 : 0, (unsigned long long *)dcur, kx);
+                         (const uint32_t *)dts, nst, shift, gather ? 1 : 0, (unsigned long long *)dcur, kx, 0);
   } else if (nst) {  // persistent: two 512-thread workgroups per CU walk the tiles
     const unsigned grid = std::min<unsigned>(nst, (unsigned)c->num_cus * 2);
     if (src[2])
       hipLaunchKernelGGL((gp_scatter_kernel<2, GP_THREADS>), dim3(grid), dim3(GP_THREADS), 0, st, ar,
                          (const GpSeg *)dseg, (const uint32_t *)dts, nst, shift, gather ? 1 : 0,
-                         (unsigned long long *)dcur, kx);
+                         (unsigned long long *)dcur, kx, 0);
     else
       hipLaunchKernelGGL((gp_scatter_kernel<1, GP_THREADS>), dim3(grid), dim3(GP_THREADS), 0, st, ar,
                          (const GpSeg *)dseg, (const uint32_t *)dts, nst, shift, gather ? 1 : 0,
-                         (unsigned long long *)dcur, kx);
+                         (unsigned long long *)dcur, kx, 0);
   }
   NUT_HIP(hipGetLastError());
   return NUT_OK;
@@ -621,41 +666,68 @@ nut_status groupby_partitioned_direct(nut_groups *g, const nut_agg_spec *s, uint
   const int narr = 3 + nv;
   const uint64_t rows = (n + 2 * 65536 + 64 + 31) & ~31ull;  // + one alignment gap per partition
   const int nstore = narr - 1 - (nk == 1 ? 1 : 0);
-  nut_status e = c->gp_data.reserve(2 * (size_t)nstore * rows * 8 + 256);
+  int levels = group_hint > 256ull * 1024 ? 2 : 1;
+  levels = env_int("NUT_GP_LEVELS", levels) == 2 ? 2 : 1;
+  const bool opt = env_int("NUT_GP_OPT", 1) != 0;
+  // A, B: the histogram layout (level 0 -> A -> level 1 -> B, or level 0 -> B); O: the
+  // optimistic level 0 (2 x rows per array over A + B); B2: two levels' final arrays after O
+  nut_status e = c->gp_data.reserve((levels == 2 && opt ? 3 : 2) * (size_t)nstore * rows * 8 + 256);
   if (e) return e;
-  uint64_t *A[GP_MAX_ARR] = {}, *B[GP_MAX_ARR] = {};
+  uint64_t *A[GP_MAX_ARR] = {}, *B[GP_MAX_ARR] = {}, *O[GP_MAX_ARR] = {}, *B2[GP_MAX_ARR] = {};
   for (int i = 1, k = 0; i < narr; ++i) {
     if (i == 2 && nk == 1) continue;
     A[i] = (uint64_t *)c->gp_data.ptr + (size_t)k * rows;
     B[i] = (uint64_t *)c->gp_data.ptr + (size_t)(nstore + k) * rows;
+    O[i] = (uint64_t *)c->gp_data.ptr + (size_t)k * 2 * rows;
+    B2[i] = (uint64_t *)c->gp_data.ptr + (size_t)(2 * nstore + k) * rows;
     ++k;
   }
+  // optimistic level 0: no histogram pass; a digit owns twice its even share of rows (the
+  // rows after the 256 partitions take overflowing runs: at least one tile), so only a key
+  // hash skewed that far falls back to the histogram layout
+  const uint64_t ocap = ((2 * rows - 2 * GP_TILE) / GP_BINS) & ~1ull;
   const uint64_t *src[GP_MAX_ARR] = {};
   src[1] = (const uint64_t *)s->keys[0];
   src[2] = nk == 2 ? (const uint64_t *)s->keys[1] : nullptr;
   for (int j = 0; j < NUT_MAX_VALS; ++j)
     if (vmap[j] >= 0) src[3 + vmap[j]] = (const uint64_t *)s->val_col[j];
   GpMeta mm{c};
-  int levels = group_hint > 256ull * 1024 ? 2 : 1;
-  levels = env_int("NUT_GP_LEVELS", levels) == 2 ? 2 : 1;
   c->timer.begin(st, NUT_KERNEL_AGGREGATE);
   std::vector<GpSeg> segs{GpSeg{0, n, 0, 0}};
   std::vector<uint64_t> hist, parts;
   uint64_t **fin = B;
   if (levels == 1) {
-    e = gp_level(c, mm, segs, 56, src, B, narr, false, false, hist, &parts);
+    e = opt ? gp_level(c, mm, segs, 56, src, O, narr, false, false, hist, &parts, 0, ocap) : NUT_ERR_CAPACITY;
+    if (!e) fin = O;
+    if (e == NUT_ERR_CAPACITY) {
+      hist.clear();
+      parts.clear();
+      e = gp_level(c, mm, segs, 56, src, B, narr, false, false, hist, &parts);
+    }
     if (e) return e;
   } else {
-    e = gp_level(c, mm, segs, 56, src, A, narr, false, false, hist);
-    if (e) return e;
     std::vector<GpSeg> s2;
-    uint64_t run = 0;
-    for (int d = 0; d < GP_BINS; ++d) {
-      if (hist[d]) s2.push_back(GpSeg{run, hist[d], 0, 0});
-      run += hist[d];
+    std::vector<uint64_t> p0;
+    uint64_t **mid = A;
+    e = opt ? gp_level(c, mm, segs, 56, src, O, narr, false, false, hist, &p0, 0, ocap) : NUT_ERR_CAPACITY;
+    if (!e) {
+      for (size_t i = 0; i < p0.size(); i += 2) s2.push_back(GpSeg{p0[i], p0[i + 1] - p0[i], 0, 0});
+      mid = O;
+      fin = B2;
+    } else if (e == NUT_ERR_CAPACITY) {
+      hist.clear();
+      e = gp_level(c, mm, segs, 56, src, A, narr, false, false, hist);
+      if (e) return e;
+      uint64_t run = 0;
+      for (int d = 0; d < GP_BINS; ++d) {
+        if (hist[d]) s2.push_back(GpSeg{run, hist[d], 0, 0});
+        run += hist[d];
+      }
+    } else {
+      return e;
     }
     std::vector<uint64_t> h2;
-    e = gp_level(c, mm, s2, 48, A, B, narr, false, false, h2, &parts);
+    e = gp_level(c, mm, s2, 48, mid, fin, narr, false, false, h2, &parts);
     if (e) return e;
   }
   c->timer.end(st);

@@ -89,7 +89,8 @@ template <int NK, int T>
 __global__ __launch_bounds__(T) void gp_scatter_kernel(GpArrays ar, const GpSeg *__restrict__ segs,
                                                                 const uint32_t *__restrict__ tile_seg, uint32_t ntiles,
                                                                 int shift, int gather,
-                                                                unsigned long long *__restrict__ cursor, uint64_t kx) {
+                                                                unsigned long long *__restrict__ cursor, uint64_t kx,
+                                                                uint64_t cap) {
   constexpr uint32_t TILE = T * GP_ITEMS;
   static_assert(TILE <= (1u << 24), "slot bits");
   __shared__ uint64_t s_stage[TILE];
@@ -159,7 +160,13 @@ __global__ __launch_bounds__(T) void gp_scatter_kernel(GpArrays ar, const GpSeg 
       s_tex[tid] = tex;
       const uint64_t cs = gather ? 0 : (uint64_t)s;
       const uint64_t gb = c ? (uint64_t)atomicAdd(&cursor[cs * GP_BINS + tid], (unsigned long long)c) : 0;
-      s_gb[tid] = gb - tex;  // output position of tile slot j with digit d = s_gb[d] + j
+      // cap (optimistic layout, no histogram; one segment): digit d owns rows
+      // [d * cap, (d + 1) * cap); a run past it goes to the scratch rows after the 256
+      // partitions (>= one tile of them), and the flag after the 256 cursors tells the host
+      // to partition again with a histogram
+      const bool over = cap && c && gb + c > (uint64_t)(tid + 1) * cap;
+      if (over) atomicOr(&cursor[GP_BINS], 1ull);
+      s_gb[tid] = (over ? (uint64_t)GP_BINS * cap : gb) - tex;  // out position of tile slot j with digit d = s_gb[d] + j
     }
     __syncthreads();
 #pragma unroll

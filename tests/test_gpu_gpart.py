@@ -128,3 +128,25 @@ def test_gp_table_growth(ex, orc, monkeypatch):
     g = ex.groupby(gb_query(dev(key, ex), dev(val, ex)), group_hint=1000)
     ok, ow = orc.groupby([key], AGGS4, values=[val])
     check_vs_oracle(g, ok, ow, ["sum_f64", "i", "i", "i"])
+
+
+@pytest.mark.parametrize("levels", ["1", "2"])
+@pytest.mark.parametrize("opt", ["0", "1"])
+def test_gp_optimistic_layout_and_fallback(ex, orc, monkeypatch, opt, levels):
+    """Direct partitioning whose first level has no histogram pass (NUT_GP_OPT=1, the
+    default): each of the 256 level-0 partitions owns twice its even share of rows.  Uniform keys fit; a heavy
+    key (half the rows) overflows its partition, whose runs go to the scratch rows, and the
+    level runs again with a histogram.  Both layouts equal the oracle bit for bit."""
+    monkeypatch.setenv("NUT_GP", "1")
+    monkeypatch.setenv("NUT_GP_LEVELS", levels)
+    monkeypatch.setenv("NUT_GP_OPT", opt)
+    n = 3_000_017
+    for heavy in (False, True):
+        key = orc.gen_column(2, 0x61, n, a=100_000)
+        if heavy:
+            key[::2] = 12345
+        val = orc.gen_column(3, 0x62, n)  # dyadic: every sum exact
+        g = ex.groupby(gb_query(dev(key, ex), dev(val, ex)), group_hint=100_000)
+        ok, ow = orc.groupby([key], AGGS4, values=[val])
+        keys, words = g.to_host_words()
+        assert np.array_equal(keys, ok) and np.array_equal(words, ow), heavy
