@@ -514,10 +514,12 @@ nut_status nut_plan_execute(nut_ctx *ctx, const nut_plan *plan, const nut_column
 nut_status nut_plan_execute2(nut_ctx *ctx, const nut_plan *plan, const nut_column *left, int nleft, uint64_t lrows,
                              const nut_column *right, int nright, uint64_t rrows, uint64_t group_hint,
                              nut_result **out);
-/* Several INNER JOINs (FROM t0 JOIN t1 ON .. JOIN t2 ON ..): tables[k] / ncols[k] /
- * nrows[k] = table k in FROM / JOIN order.  Each ON compares a column of its table with a
- * column of an earlier one; single-table WHERE conjuncts are pushed down.  Plans with at
- * most one JOIN are forwarded to nut_plan_execute / nut_plan_execute2. */
+/* Several INNER / LEFT OUTER JOINs (FROM t0 JOIN t1 ON .. LEFT JOIN t2 ON ..): tables[k] /
+ * ncols[k] / nrows[k] = table k in FROM / JOIN order.  Each ON compares a column of its
+ * table with a column of an earlier one; single-table WHERE conjuncts are pushed down.  A
+ * LEFT-joined table is NULL on the rows without a match (a later ON reading it matches
+ * nothing there); its columns may only appear inside aggregates, which skip those rows.
+ * Plans with at most one JOIN are forwarded to nut_plan_execute / nut_plan_execute2. */
 nut_status nut_plan_executen(nut_ctx *ctx, const nut_plan *plan, const nut_column *const *tables, const int *ncols,
                              const uint64_t *nrows, int ntables, uint64_t group_hint, nut_result **out);
 /* Result = ncols output columns (the SELECT list, in order) x nrows rows. */
