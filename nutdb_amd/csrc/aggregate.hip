@@ -1058,12 +1058,41 @@ nut_status nut_groupby_jit_compile(const nut_agg_spec *s) {
 namespace nut {
 // Row i of the compacted columns goes to its key's rank among the (unique, sorted) keys:
 // keys_out[rank] = key, aggs_out[rank * naggs + a] = aggregate a.
+// Bucket index over the sorted unique keys (n >= 2): bucket(k) = (k - sorted[0]) >> shift,
+// at most 2^PL_BITS + 1 buckets; start[b] = the first i with bucket(sorted[i]) >= b, for
+// b in [0, nb].  A group then binary-searches only its bucket's run (a few keys, one or two
+// cache lines) instead of the whole array (~12 random HBM lines per key at 1e7 groups).
+constexpr int PL_BITS = 20;
+struct PlaceBuckets {
+  uint64_t mn;
+  int shift;
+  uint64_t nb;  // buckets 0 .. nb - 1
+};
+__device__ __forceinline__ PlaceBuckets place_buckets(const int64_t *sorted, uint64_t n) {
+  const uint64_t mn = (uint64_t)sorted[0], range = (uint64_t)sorted[n - 1] - mn;
+  const int hb = range ? 64 - __builtin_clzll(range) : 0;
+  const int shift = hb > PL_BITS ? hb - PL_BITS : 0;
+  return PlaceBuckets{mn, shift, (range >> shift) + 1};
+}
+
+__global__ void place_index_kernel(const int64_t *__restrict__ sorted, uint64_t n, uint64_t *__restrict__ start) {
+  const PlaceBuckets pb = place_buckets(sorted, n);
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t b0 = i == 0 ? 0 : (((uint64_t)sorted[i - 1] - pb.mn) >> pb.shift) + 1;
+    const uint64_t b1 = i == n ? pb.nb : (((uint64_t)sorted[i] - pb.mn) >> pb.shift);
+    for (uint64_t b = b0; b <= b1; ++b) start[b] = i;
+  }
+}
+
 __global__ void groups_place_kernel(const uint64_t *__restrict__ cols, const int64_t *__restrict__ sorted, uint64_t n,
-                                    int naggs, int64_t *__restrict__ keys_out, uint64_t *__restrict__ aggs_out) {
+                                    int naggs, int64_t *__restrict__ keys_out, uint64_t *__restrict__ aggs_out,
+                                    const uint64_t *__restrict__ start) {
+  const PlaceBuckets pb = place_buckets(sorted, n);
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     const int64_t k = (int64_t)cols[i];
-    uint64_t lo = 0, len = n;
-    while (len > 0) {  // lower bound
+    const uint64_t b = ((uint64_t)k - pb.mn) >> pb.shift;
+    uint64_t lo = start[b], len = start[b + 1] - lo;
+    while (len > 0) {  // lower bound within the bucket
       const uint64_t half = len >> 1;
       if (sorted[lo + half] < k) {
         lo += half + 1;
@@ -1300,15 +1329,23 @@ nut_status nut_groups_to_host(nut_groups *g, int64_t *keys, uint64_t *aggs, uint
     st = msd_sort_i64(c, (const int64_t *)dev, sorted, n, 0x8000000000000000ull);
     c->sort_bytes = saved_bytes;
     c->sort_levels = saved_levels;
+    uint64_t *bstart = nullptr;
+    if (!st) {
+      const hipError_t he = hipMallocAsync((void **)&bstart, ((1ull << PL_BITS) + 2) * 8, c->stream);
+      if (he != hipSuccess) st = hip_fail(he, "nut_groups_to_host (bucket index)");
+    }
     if (!st) {
       const uint64_t blocks = std::min<uint64_t>((n + 255) / 256, (uint64_t)c->num_cus * 16);
+      hipLaunchKernelGGL(place_index_kernel, dim3((unsigned)blocks), dim3(256), 0, c->stream, (const int64_t *)sorted, n,
+                         bstart);
       hipLaunchKernelGGL(groups_place_kernel, dim3((unsigned)blocks), dim3(256), 0, c->stream, (const uint64_t *)dev,
-                         (const int64_t *)sorted, n, g->naggs, dk, da);
+                         (const int64_t *)sorted, n, g->naggs, dk, da, (const uint64_t *)bstart);
       hipError_t e = hipGetLastError();
       if (e != hipSuccess) st = hip_fail(e, "nut_groups_to_host (device order)");
       if (!st) st = copy_to_host(c, keys, dk, nb);
       if (!st && g->naggs) st = copy_to_host(c, aggs, da, nb * g->naggs);
     }
+    if (bstart) (void)hipFreeAsync(bstart, c->stream);
     (void)hipFreeAsync(buf, c->stream);
     (void)hipFreeAsync(dev, c->stream);
     return st;
