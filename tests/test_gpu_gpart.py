@@ -150,3 +150,23 @@ def test_gp_optimistic_layout_and_fallback(ex, orc, monkeypatch, opt, levels):
         ok, ow = orc.groupby([key], AGGS4, values=[val])
         keys, words = g.to_host_words()
         assert np.array_equal(keys, ok) and np.array_equal(words, ow), heavy
+
+
+def test_ordered_result_bucket_index(ex, orc):
+    """Large one-key results are ordered on the device: sort of the unique keys, then each
+    group binary-searches its bucket of a 2^20-bucket index over (k - min) >> shift.  Key
+    sets with a small range (shift 0, consecutive ids), two clusters 2^62 apart (most
+    buckets empty) and negative keys all come back in key order with their sums."""
+    rng = np.random.default_rng(11)
+    cases = {"consecutive": np.arange(-50_000, 150_000, dtype=np.int64),
+             "two_clusters": np.concatenate([np.arange(100_000, dtype=np.int64) - 2**62,
+                                             np.arange(100_000, dtype=np.int64) + 2**62]),
+             "full_range": rng.integers(I64_MIN, I64_MAX, 300_000, dtype=np.int64)}
+    for name, uniq in cases.items():
+        key = np.repeat(uniq, 3)
+        rng.shuffle(key)
+        val = (np.abs(key) % 1000).astype(np.float64)
+        g = ex.groupby(gb_query(dev(key, ex), dev(val, ex)), group_hint=len(uniq))
+        ok, ow = orc.groupby([key], AGGS4, values=[val])
+        keys, words = g.to_host_words()
+        assert np.array_equal(keys, ok) and np.array_equal(words, ow), name
