@@ -7,9 +7,12 @@ Default workload (N=1): BASELINE config 4, the TPC-H Q1-shape filter -> group-by
          sum(l_extendedprice*(1-l_discount)), count(*)
   FROM lineitem WHERE l_shipdate <= 10471 GROUP BY l_returnflag, l_linestatus
 on 1e9 rows per GPU (6 x 8 B columns = 48 GB resident in HBM).  With --gpus N
-(torchrun, one rank per GPU) every rank scans its own 1e9-row shard (weak scaling),
-pre-aggregates locally, exchanges partial groups by key hash with one RCCL
-all-to-all and merges the groups it owns; rank 0 gathers the final result.
+(torchrun, one rank per GPU) every rank scans its own 1e9-row shard (weak scaling)
+through the library's own multi-GPU path, nut_dist_* in libnutexec.so (what a Rust
+host binds): ncclCommInitRank per process, local pre-aggregation,
+partial groups exchanged by key hash with one RCCL all-to-all, owner merge, gather to
+rank 0.  torch.distributed (gloo, CPU) is only the control plane: it broadcasts the
+RCCL unique id and provides the barriers and the max-over-ranks time.
 
 A "step" = one complete query over the resident columns (kernels + exchange + result
 to host).  Other configs: --workload groupby (config 3), filter (config 2), sort
@@ -53,6 +56,10 @@ def parse():
     p.add_argument("--selectivity", type=float, default=0.5, help="filter: fraction selected")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline work")
+    p.add_argument("--dist", action="store_true",
+                   help="run N=1 through nut_dist_* too (one RCCL rank), as the N>1 runs do")
+    p.add_argument("--option", action="append", default=[], metavar="NAME=VALUE",
+                   help="nut_ctx_set_option for A/B runs (Executor.OPTIONS names); recorded in config")
     return p.parse_args()
 
 
@@ -82,14 +89,18 @@ class Q1:
         (gk, gw), (ck, cw) = gpu, cpu
         return _cmp_groups(gk, gw, ck, cw, f64_cols=(0, 1, 2), rtol=1e-12)
 
-    def merge_query(self, seg):
+    def run_dist(self, nd):  # N > 1: nut_dist_groupby of the same query (nut_q1's spec)
         from nutdb_amd import Agg, AggQuery
-        # partial record: rf, ls, sum_qty, sum_price, sum_disc_price, count
-        return AggQuery(keys=[seg[0].contiguous(), seg[1].contiguous()],
-                        values=[seg[2].contiguous().view(torch.float64), seg[3].contiguous().view(torch.float64),
-                                seg[4].contiguous().view(torch.float64), seg[5].contiguous()],
-                        aggs=[Agg("sum", "col", (0,)), Agg("sum", "col", (1,)), Agg("sum", "col", (2,)),
-                              Agg("sum", "col", (3,))])
+        sd, rf, ls, qty, price, disc = self.cols
+        q = AggQuery(keys=[rf, ls], values=[qty, price, disc], preds=[(sd, "<=", self.k)],
+                     aggs=[Agg("sum", "col", (0,)), Agg("sum", "col", (1,)), Agg("sum", "mul_1m", (1, 2)),
+                           Agg("count")])
+        g = nd.groupby([q], group_hint=8)[0]
+        if g is None:
+            return None
+        r = g.to_host_words()
+        g.free()
+        return r
 
     kernel_kind = 1
     groups_hint = 8
@@ -136,10 +147,15 @@ class GroupBy:
         (gk, gw), (ck, cw) = gpu, cpu
         return _cmp_groups(gk, gw, ck, cw, f64_cols=(), rtol=0.0)
 
-    def merge_query(self, seg):
+    def run_dist(self, nd):  # N > 1: nut_dist_groupby; rank 0 receives the global groups
         from nutdb_amd import Agg, AggQuery
-        return AggQuery(keys=[seg[0].contiguous()], values=[seg[1].contiguous().view(torch.float64)],
-                        aggs=[Agg("sum", "col", (0,))])
+        g = nd.groupby([AggQuery(keys=[self.key], values=[self.val], aggs=[Agg("sum", "col", (0,))])],
+                       group_hint=self.G)[0]
+        if g is None:
+            return None
+        r = g.to_host_words()
+        g.free()
+        return r
 
     def config(self):
         return {"workload": self.name, "query": "SELECT key, SUM(val) FROM t GROUP BY key", "groups": self.G,
@@ -164,6 +180,9 @@ class Filter:
     def run(self):
         self.ex.filter_i64_async(self.col, "<", self.k, self.out, self.out_n)
         return self.out, self.out_n
+
+    def run_dist(self, nd):  # N > 1: shards are independent; one all-gather of counts
+        return nd.filter_i64([self.col], "<", self.k)[0]
 
     @staticmethod
     def parity(gpu, cpu):
@@ -209,21 +228,20 @@ class Sort:
     """config 5: ORDER BY a full-range i64 key.  N=1: local hybrid MSD radix sort
     (msd_sort.hip: two segmented scatter levels + on-chip local sorts for 1.25e9 random
     keys).  N>1: sample sort — splitters from an all_gather'd sample, local stable
-    partition into P buckets (nut_partition_i64), ONE RCCL all-to-all of keys, local sort
-    of the received range (nutdb_amd/dist.py distributed_sort).  Rank r ends with the r-th
-    key range.  Algorithmic bytes come from the library (nut_ctx_sort_stats): 8 B/key per
+    partition into skew-safe key ranges (nut_partition_i64), ONE RCCL all-to-all of keys,
+    local sort of the received range (nut_dist_sort_i64).  Rank r ends with the r-th key
+    range.  Algorithmic bytes come from the library (nut_ctx_sort_stats): 8 B/key per
     histogram read, 16 B/key per scatter level, local sort and copy."""
     name = "sort_i64_radix"
     kernel_kind = 2
 
-    def __init__(self, ex, rows, row0, world=1, group=None):
+    def __init__(self, ex, rows, row0, world=1):
         from nutdb_amd.workloads import SORT_COL, gen
         self.ex = ex
         self.col = gen(ex, SORT_COL, rows, row0=row0)
-        self.out = torch.empty_like(self.col)
+        self.out = torch.empty_like(self.col) if world == 1 else None
         self.rows = rows
         self.world = world
-        self.group = group
         self.sort_bytes, self.levels = 0, 0
 
     # roofline numerator: SURVEY.md §8(d)'s HBM lower bound, one read + one write of every
@@ -236,13 +254,14 @@ class Sort:
         return self.sort_bytes / self.rows + (24 if self.world > 1 else 0)
 
     def run(self):
-        if self.world == 1:
-            self.ex.sort_i64(self.col, out=self.out)
-        else:
-            from nutdb_amd.dist import distributed_sort
-            self.out = distributed_sort(self.col, self.ex.partition_i64, self.ex.sort_i64, self.group)
+        self.ex.sort_i64(self.col, out=self.out)
         self.sort_bytes, self.levels = self.ex.sort_stats()
         return self.out
+
+    def run_dist(self, nd):  # the received range stays in the member's buffer (no copy)
+        r = nd.sort_i64([self.col], copy=False)[0]
+        self.sort_bytes, self.levels = nd.sort_stats()
+        return r
 
     @staticmethod
     def parity(gpu, cpu):
@@ -302,11 +321,11 @@ class Join:
     name = "join_i64_hash"
     kernel_kind = 3
 
-    def __init__(self, ex, rows, row0, world=1, group=None, rank=0):
+    def __init__(self, ex, rows, row0, world=1, rank=0):
         self.ex = ex
         self.rows = rows
         self.nb = rows // 4
-        self.world, self.group, self.rank = world, group, rank
+        self.world, self.rank = world, rank
         self.build = ex.gen_column(0, 0x71 + row0, self.nb)  # 62-bit: unique w.h.p.
         sel = ex.gen_column(0, 0x72 + row0, rows)
         self.probe = torch.where(sel % 10 == 0, sel | (1 << 62), self.build[sel % self.nb])
@@ -318,14 +337,15 @@ class Join:
         return (24.0 * self.nb + 8.0 * self.rows + 16.0 * self.npairs) / self.rows
 
     def run(self):
-        if self.world == 1:
-            pi, bi = self.ex.join_i64(self.build, self.probe, "inner")
-        else:
-            from nutdb_amd.dist import distributed_join
-            pi, bi = distributed_join(self.build, self.probe, self.ex.hash_partition_i64, self.ex.join_i64, "inner",
-                                      self.rank * self.nb, self.rank * self.rows, self.group)
+        pi, bi = self.ex.join_i64(self.build, self.probe, "inner")
         self.npairs = pi.numel()
         return pi, bi
+
+    def run_dist(self, nd):  # global row ids; pairs stay in the member's buffers
+        r = nd.join_i64([self.build], [self.probe], "inner", [self.rank * self.nb], [self.rank * self.rows],
+                        copy=False)[0]
+        self.npairs = int(r[2])
+        return r
 
     @staticmethod
     def parity(gpu, cpu):
@@ -405,21 +425,6 @@ class Q12Join:
                 "lineitem_rows": self.rows, "orders_rows": self.rows // 4, "bytes_per_row": self.cols_bytes,
                 "plan": "WHERE pushed below the join (select kernel) -> hash join (selected lines x orders) -> "
                         "gathers -> expression-mode group-by"}
-
-
-# ------------------------------------------------------------------ one step
-def groupby_step(w, rank, world, group):
-    """Local scan -> (N>1) all-to-all of partial groups by owner -> owner merge ->
-    gather to rank 0 (nutdb_amd/dist.py).  Returns the number of result groups on rank 0."""
-    g = w.local()
-    if world == 1:
-        keys, _ = g.to_host_words()
-        g.free()
-        return len(keys)
-    from nutdb_amd.dist import distributed_groupby
-    res = distributed_groupby(w.ex, g, w.merge_query, w.groups_hint, group)
-    g.free()
-    return res.shape[1] if res is not None else 0
 
 
 # ------------------------------------------------------------------ CPU baseline
@@ -599,12 +604,27 @@ def main():
             print("bench.py: --gpus N>1 must be launched with torch.distributed.run", file=sys.stderr)
             sys.exit(2)
     torch.cuda.set_device(local_rank)
-    group = None
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-        group = dist.group.WORLD
     from nutdb_amd import Executor
     ex = Executor(local_rank)
+    nd = None
+    if world > 1 or args.dist:
+        # control plane only (CPU): the RCCL unique id, barriers, the max-over-ranks time;
+        # every data exchange runs inside libnutexec.so (nut_dist_*, ncclCommInitRank)
+        if world == 1:  # --dist without torchrun
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29517")
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
+        dist.init_process_group("gloo")
+        from nutdb_amd.dist import NutDist
+        uid = [NutDist.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        nd = NutDist.create_rank(world, rank, uid[0], local_rank)
+    options = {}
+    for o in args.option:
+        name, val = o.split("=", 1)
+        ex.set_option(name, int(val))
+        options[name] = int(val)
     default_rows = {"q1": 1e9, "groupby": 1e9, "filter": 1e8, "sort": 1.25e9, "q12expr": 1e9,
                     "join": 1e9, "scanexpr": 1e8, "q12join": 1e9}[args.workload]
     rows = int(args.rows or default_rows)
@@ -612,20 +632,22 @@ def main():
     if args.workload in ("q12expr", "q12join") and world > 1:
         print(f"bench.py: {args.workload} is a single-GPU workload", file=sys.stderr)
         sys.exit(2)
-    w = make_workload(args, ex, rows, row0, world, group, rank)
+    w = make_workload(args, ex, rows, row0, world, rank)
     torch.cuda.synchronize()
     last = [None]
+    if nd is not None:
+        for o in args.option:
+            name, val = o.split("=", 1)
+            from nutdb_amd._lib import lib
+            lib.nut_ctx_set_option(nd.ctx(0), ex.OPTIONS[name], int(val))
 
     def step():
         last[0] = None  # the previous step's result is dropped before the next one runs
-        if world == 1 or args.workload not in ("q1", "groupby"):
-            last[0] = w.run()
-        else:
-            groupby_step(w, rank, world, group)
+        last[0] = w.run() if nd is None else w.run_dist(nd)
 
     for _ in range(args.warmup):
         step()
-    ex.enable_timing(True)
+    (ex if nd is None else nd).enable_timing(True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -636,10 +658,11 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kern_ms, launches = ex.kernel_time(w.kernel_kind)
-    ex.enable_timing(False)
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=ex.device)
+    kern_ms, launches = (ex if nd is None else nd).kernel_time(w.kernel_kind)
+    (ex if nd is None else nd).enable_timing(False)
+    gb_stats = ex.groupby_stats() if nd is None and args.workload in ("q1", "groupby", "q12expr", "q12join") else None
+    if nd is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms_step = elapsed * 1e3 / args.steps
@@ -669,22 +692,50 @@ def main():
             traffic = None
     parity = None
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and nd is None and not args.no_cpu_baseline:
         cpu, cpu_res, sample = cpu_baseline(args, args.workload, args.cpu_seconds)
-        if sample == rows:
+        if args.workload == "groupby" and sample != rows:
+            # full size: the pool keys are a bijection of an index, so the indexed dense-array
+            # oracle checks the last timed step itself (exact, seconds at 1e9 rows x 1e7 groups)
+            from oracle import oracle as orc
+            from nutdb_amd.workloads import GB_KEY_SEED, GB_VAL_SEED
+            del cpu_res
+            t0 = time.perf_counter()
+            ok, ow = orc.groupby_pool_dyadic(args.groups, rows, row0=0, key_seed=GB_KEY_SEED, val_seed=GB_VAL_SEED)
+            cpu_res = (ok, np.ascontiguousarray(ow[:, :1]))
+            sample = rows
+            how = ("last timed step vs the indexed dense-array oracle (oracle.h orc_groupby_pool_dyadic, "
+                   f"{time.perf_counter() - t0:.1f} s) on the same full-size input")
+            gpu_res = last[0]
+        elif sample == rows:
             how = "last timed step vs the CPU baseline's result on the same full-size input"
             gpu_res = last[0]
         else:  # the GPU rerun (untimed) on the CPU sample's input: the first `sample` rows
             how = f"GPU rerun (untimed) on the CPU sample's {sample} rows vs the CPU baseline's result"
             last[0] = None
-            gpu_res = make_workload(args, ex, sample, 0, 1, None, 0).run()
+            gpu_res = make_workload(args, ex, sample, 0, 1, 0).run()
         parity = {"rows": sample, "full_size": sample == rows, "method": how}
+        if gb_stats is not None:
+            parity["timed_path"] = gb_stats
+            if sample != rows:
+                parity["checked_path"] = ex.groupby_stats()
         parity.update(type(w).parity(gpu_res, cpu_res))
         del cpu_res, gpu_res
     if rank == 0:
         cfg = w.config()
-        cfg.update({"rows_per_gpu": rows, "parallelism": f"dp{world} (row shards; key-hash all-to-all of "
-                    "partial groups over RCCL)" if world > 1 else "single GPU", "gpu": ex.info()["name"],
+        if gb_stats is not None:
+            cfg["groupby_path"] = gb_stats
+        if options:
+            cfg["options"] = options
+        if nd is not None:
+            cfg["dist"] = {"api": "nut_dist_create_rank + nut_dist_* (libnutexec.so, RCCL)", "nranks": nd.nranks,
+                           "control_plane": "torch.distributed gloo (unique id, barriers, max time)"}
+        cfg.update({"rows_per_gpu": rows, "parallelism": f"dp{world} (row shards; " + {
+                        "q1": "key-hash all-to-all of partial groups", "groupby": "key-hash all-to-all of partial groups",
+                        "sort": "sample sort: skew-safe key ranges + one all-to-all of keys",
+                        "filter": "independent shards + all-gather of counts",
+                        "join": "key-owner all-to-all of both sides"}.get(args.workload, "") + " over RCCL)"
+                    if world > 1 else "single GPU", "gpu": ex.info()["name"],
                     "kernel_launches": launches, "kernel_ms_per_step": avg_kernel_ms})
         line = {
             "metric": METRIC, "value": value, "unit": "rows/s", "n_gpus": world, "steps": args.steps,
@@ -692,32 +743,39 @@ def main():
             "vs_baseline": None, "dtype": "i64+f64", "data": "synthetic (counter-based splitmix64 columns "
             "generated in HBM)", "config": cfg,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
+                         "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
+                         # the same bytes over the whole step's wall time (host overheads and any
+                         # result copy included): reproducible from ms_per_step alone
+                         "achieved_wall": bytes_per_step / (ms_step * 1e-3) / 1e9,
+                         "frac_wall": bytes_per_step / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                         "traffic": traffic,
                          "traffic_source": traffic_src},
         }
         if cpu is not None:
             line["cpu_baseline"] = cpu
             line["parity"] = parity
         print(json.dumps(line), flush=True)
+    if nd is not None:
+        nd.close()
     ex.close()
-    if world > 1:
+    if nd is not None or world > 1:
         dist.destroy_process_group()
     if parity is not None and not parity["ok"]:
         print(f"bench.py: PARITY FAILURE vs the CPU oracle: {parity}", file=sys.stderr)
         sys.exit(1)
 
 
-def make_workload(args, ex, rows, row0, world, group, rank):
+def make_workload(args, ex, rows, row0, world, rank):
     if args.workload == "q1":
         return Q1(ex, rows, row0)
     if args.workload == "groupby":
         return GroupBy(ex, rows, row0, args.groups)
     if args.workload == "sort":
-        return Sort(ex, rows, row0, world, group)
+        return Sort(ex, rows, row0, world)
     if args.workload == "q12expr":
         return Q12Expr(ex, rows, row0)
     if args.workload == "join":
-        return Join(ex, rows, row0, world, group, rank)
+        return Join(ex, rows, row0, world, rank)
     if args.workload == "scanexpr":
         return ScanExpr(ex, rows, row0)
     if args.workload == "q12join":

@@ -88,6 +88,33 @@ nut_status nut_ctx_kernel_time(nut_ctx *ctx, int kind, double *total_ms, uint64_
  * depend on the data: 8 B/key per histogram read, 16 B/key per scatter level, local sort
  * and copy) and the number of scatter levels it ran — the roofline numerator for sorts. */
 nut_status nut_ctx_sort_stats(nut_ctx *ctx, uint64_t *bytes, uint32_t *levels);
+/* The algorithm the last nut_groupby on this context took (parity tests and bench lines
+ * name the path they checked): path = nut_groupby_path, levels = partition levels of a
+ * partitioned path (0 otherwise), optimistic = 1 when its first level ran without a
+ * histogram pass. */
+typedef enum {
+  NUT_GB_ONCHIP = 0,           /* streaming kernel, per-workgroup LDS tables (+ global table) */
+  NUT_GB_PARTITIONED_DIRECT = 1, /* key-hash partition of the caller's columns, then LDS tables */
+  NUT_GB_PARTITIONED_SPILL = 2   /* WHERE / expressions staged first, then partitioned */
+} nut_groupby_path;
+nut_status nut_ctx_groupby_stats(nut_ctx *ctx, uint32_t *path, uint32_t *levels, uint32_t *optimistic);
+
+/* Algorithm options of one context, for tuning A/B runs and tests that drive a path at
+ * a size where the planner would not pick it.  The defaults are the product choice;
+ * the library reads no environment variables.  Results never depend on them. */
+typedef enum {
+  NUT_OPT_GB_PARTITION = 0,    /* -1 auto (default), 0 never, 1 always (keyed group-bys) */
+  NUT_OPT_GB_LEVELS = 1,       /* 0 auto (default), 1 or 2 partition levels */
+  NUT_OPT_GB_OPTIMISTIC = 2,   /* 1 (default): first direct level without a histogram pass */
+  NUT_OPT_GB_DIRECT = 3,       /* 1 (default): partition plain columns in place (no spill) */
+  NUT_OPT_GB_CHUNKS = 4,       /* aggregation workgroups per CU over the partitions (8) */
+  NUT_OPT_JOIN_REGION = 5,     /* 1 (default): LDS region build of large join tables */
+  NUT_OPT_JOIN_PROBE_CFG = 6,  /* ordered probe tile shape 0..4 (0) */
+  NUT_OPT_JOIN_ANY_CFG = 7,    /* unordered probe tile shape 0..4 (0) */
+  NUT_OPT_COUNT = 8
+} nut_option;
+nut_status nut_ctx_set_option(nut_ctx *ctx, int option, int64_t value);
+nut_status nut_ctx_get_option(nut_ctx *ctx, int option, int64_t *value);
 
 /* ------------------------------------------------------------------------
  * Synthetic columns (bench / tests): counter-based splitmix64 generator,

@@ -129,6 +129,9 @@ SIGNATURES = {
     "nut_ctx_enable_timing": (_I32, [_P, _I32]),
     "nut_ctx_kernel_time": (_I32, [_P, _I32, C.POINTER(C.c_double), C.POINTER(_U64)]),
     "nut_ctx_sort_stats": (_I32, [_P, C.POINTER(_U64), C.POINTER(C.c_uint32)]),
+    "nut_ctx_groupby_stats": (_I32, [_P, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
+    "nut_ctx_set_option": (_I32, [_P, _I32, _I64]),
+    "nut_ctx_get_option": (_I32, [_P, _I32, C.POINTER(_I64)]),
     "nut_join_i64": (_I32, [_P, _P, _U64, _P, _U64, _I32, C.POINTER(_P), C.POINTER(_U64)]),
     "nut_join_write": (_I32, [_P, _P, _P]),
     "nut_join_i64_into": (_I32, [_P, _P, _U64, _P, _U64, _I32, _P, _P, _U64, C.POINTER(_U64)]),

@@ -425,13 +425,9 @@ nut_status ensure_room(nut_groups *g, uint64_t extra) {
 
 // ---------------------------------------------------------------- partitioned aggregation
 // (gpart.hpp).  Used when the expected groups exceed what the on-chip tables hold.
-// NUT_GP=0 / 1 forces the path off / on, NUT_GP_LEVELS=1|2 the partition levels (tests).
+// nut_ctx_set_option NUT_OPT_GB_PARTITION / NUT_OPT_GB_LEVELS force the path and its
+// levels (tests drive them at small sizes).
 constexpr uint64_t kGpMinGroups = 1ull << 16;
-
-int env_int(const char *name, int dflt) {
-  const char *e = getenv(name);
-  return e && *e ? atoi(e) : dflt;
-}
 
 // upload host vectors into a fresh region of ctx->gp_meta (grown after a sync)
 struct GpMeta {
@@ -568,9 +564,8 @@ nut_status gp_level(nut_ctx *c, GpMeta &mm, std::vector<GpSeg> &segs, int shift,
     }
   }
   // 1024-thread workgroups of 16K-record tiles (one per CU): 64 records per digit per tile;
-  // measured 9.2 vs 10.1 ms for the 512-thread 8K tiles (G = 1e5, 1e9 rows); NUT_GP_T=512
-  const int big = env_int("NUT_GP_T", 1024) == 1024;
-  const uint32_t nst = gp_tiles(segs, big ? 2 * GP_TILE : GP_TILE, ts);
+  // measured 9.2 vs 10.1 ms for 512-thread 8K tiles at two per CU (G = 1e5, 1e9 rows)
+  const uint32_t nst = gp_tiles(segs, 2 * GP_TILE, ts);
   s = mm.begin(GpMeta::al(segs.size() * sizeof(GpSeg)) + GpMeta::al(ts.size() * 4 + 1) + GpMeta::al(cur.size() * 8));
   if (s) return s;
   uint64_t *dcur;
@@ -581,7 +576,7 @@ nut_status gp_level(nut_ctx *c, GpMeta &mm, std::vector<GpSeg> &segs, int shift,
     ar.dst[a] = dst[a];
   }
   ar.narr = narr;
-  if (nst && big) {
+  if (nst) {
     const unsigned grid = std::min<unsigned>(nst, (unsigned)c->num_cus);
     if (src[2])
       hipLaunchKernelGGL((gp_scatter_kernel<2, 1024>), dim3(grid), dim3(1024), 0, st, ar, (const GpSeg *)dseg,
@@ -589,16 +584,6 @@ nut_status gp_level(nut_ctx *c, GpMeta &mm, std::vector<GpSeg> &segs, int shift,
     else
       hipLaunchKernelGGL((gp_scatter_kernel<1, 1024>), dim3(grid), dim3(1024), 0, st, ar, (const GpSeg *)dseg,
                          (const uint32_t *)dts, nst, shift, gather ? 1 : 0, (unsigned long long *)dcur, kx, 0);
-  } else if (nst) {  // persistent: two 512-thread workgroups per CU walk the tiles
-    const unsigned grid = std::min<unsigned>(nst, (unsigned)c->num_cus * 2);
-    if (src[2])
-      hipLaunchKernelGGL((gp_scatter_kernel<2, GP_THREADS>), dim3(grid), dim3(GP_THREADS), 0, st, ar,
-                         (const GpSeg *)dseg, (const uint32_t *)dts, nst, shift, gather ? 1 : 0,
-                         (unsigned long long *)dcur, kx, 0);
-    else
-      hipLaunchKernelGGL((gp_scatter_kernel<1, GP_THREADS>), dim3(grid), dim3(GP_THREADS), 0, st, ar,
-                         (const GpSeg *)dseg, (const uint32_t *)dts, nst, shift, gather ? 1 : 0,
-                         (unsigned long long *)dcur, kx, 0);
   }
   NUT_HIP(hipGetLastError());
   return NUT_OK;
@@ -613,7 +598,7 @@ nut_status gp_aggregate(nut_groups *g, GpMeta &mm, const std::vector<uint64_t> &
   if (nparts == 0) return NUT_OK;
   // split partitions into chunks (even boundaries) so that the grid fills the chip (chunks
   // of one partition merge the same keys: a handful of extra merges per group)
-  const uint64_t wpc = (uint64_t)std::max(1, env_int("NUT_GP_CHUNKS", 8));  // workgroups per CU (4: +0.12 ms at G = 1e5)
+  const uint64_t wpc = (uint64_t)std::max<int64_t>(1, c->opt[NUT_OPT_GB_CHUNKS]);  // workgroups per CU (4: +0.12 ms at G = 1e5)
   const uint64_t k = std::max<uint64_t>(1, ((uint64_t)c->num_cus * wpc + nparts - 1) / nparts);
   std::vector<uint64_t> off;
   for (uint32_t p = 0; p < nparts; ++p) {
@@ -667,9 +652,11 @@ nut_status groupby_partitioned_direct(nut_groups *g, const nut_agg_spec *s, uint
   const int narr = 3 + nv;
   const uint64_t rows = (n + 2 * 65536 + 64 + 31) & ~31ull;  // + one alignment gap per partition
   const int nstore = narr - 1 - (nk == 1 ? 1 : 0);
-  int levels = group_hint > 256ull * 1024 ? 2 : 1;
-  levels = env_int("NUT_GP_LEVELS", levels) == 2 ? 2 : 1;
-  const bool opt = env_int("NUT_GP_OPT", 1) != 0;
+  const int levels = c->opt[NUT_OPT_GB_LEVELS] ? (int)c->opt[NUT_OPT_GB_LEVELS] : group_hint > 256ull * 1024 ? 2 : 1;
+  const bool opt = c->opt[NUT_OPT_GB_OPTIMISTIC] != 0;
+  c->gb_path = NUT_GB_PARTITIONED_DIRECT;
+  c->gb_levels = (uint32_t)levels;
+  c->gb_optimistic = 0;
   // A, B: the histogram layout (level 0 -> A -> level 1 -> B, or level 0 -> B); O: the
   // optimistic level 0 (2 x rows per array over A + B); B2: two levels' final arrays after O
   nut_status e = c->gp_data.reserve((levels == 2 && opt ? 3 : 2) * (size_t)nstore * rows * 8 + 256);
@@ -699,7 +686,10 @@ nut_status groupby_partitioned_direct(nut_groups *g, const nut_agg_spec *s, uint
   uint64_t **fin = B;
   if (levels == 1) {
     e = opt ? gp_level(c, mm, segs, 56, src, O, narr, false, false, hist, &parts, 0, ocap) : NUT_ERR_CAPACITY;
-    if (!e) fin = O;
+    if (!e) {
+      fin = O;
+      c->gb_optimistic = 1;
+    }
     if (e == NUT_ERR_CAPACITY) {
       hist.clear();
       parts.clear();
@@ -715,6 +705,7 @@ nut_status groupby_partitioned_direct(nut_groups *g, const nut_agg_spec *s, uint
       for (size_t i = 0; i < p0.size(); i += 2) s2.push_back(GpSeg{p0[i], p0[i + 1] - p0[i], 0, 0});
       mid = O;
       fin = B2;
+      c->gb_optimistic = 1;
     } else if (e == NUT_ERR_CAPACITY) {
       hist.clear();
       e = gp_level(c, mm, segs, 56, src, A, narr, false, false, hist);
@@ -776,7 +767,7 @@ nut_status groupby_partitioned(nut_groups *g, const nut_agg_spec *s, uint64_t gr
   // Direct path: no WHERE and every argument a plain column (BASELINE config 3) — the
   // spill would only copy the key and value columns, so the first partition level reads
   // them in place (a key histogram pass of 8 B/row instead of a 32 B/row spill).
-  bool direct = !s->prog_mode && s->npred == 0 && env_int("NUT_GP_DIRECT", 1) != 0;
+  bool direct = !s->prog_mode && s->npred == 0 && c->opt[NUT_OPT_GB_DIRECT] != 0;
   for (int a = 0; a < na && direct; ++a) direct = s->agg_op[a] == NUT_AGG_COUNT || s->agg_expr[a] == NUT_EX_COL;
   if (direct) return groupby_partitioned_direct(g, s, group_hint);
   const int narr = 3 + nv;  // -, k1, k2 (unused for one key), values
@@ -823,8 +814,10 @@ nut_status groupby_partitioned(nut_groups *g, const nut_agg_spec *s, uint64_t gr
   }
   if (nsp == 0) return NUT_OK;
   // ---- 2. partition by the key hash: 256 or 65536 partitions of ~<= 1K groups
-  int levels = group_hint > 256ull * 1024 ? 2 : 1;
-  levels = env_int("NUT_GP_LEVELS", levels) == 2 ? 2 : 1;
+  const int levels = c->opt[NUT_OPT_GB_LEVELS] ? (int)c->opt[NUT_OPT_GB_LEVELS] : group_hint > 256ull * 1024 ? 2 : 1;
+  c->gb_path = NUT_GB_PARTITIONED_SPILL;
+  c->gb_levels = (uint32_t)levels;
+  c->gb_optimistic = 0;
   c->timer.begin(st, NUT_KERNEL_AGGREGATE);
   std::vector<uint64_t> parts;  // [start, end) pairs of the final partitions
   uint64_t **fin = B;
@@ -886,7 +879,9 @@ nut_status nut_groupby(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hint, n
   for (int a = 0; a < s->naggs; ++a) g->kinds[a] = kind_of(s, a);
   if (s->nkeys == 0) group_hint = 1;
   uint64_t cap = table_cap_for(group_hint ? group_hint : 8192);
-  const int gp = env_int("NUT_GP", -1);
+  const int64_t gp = c->opt[NUT_OPT_GB_PARTITION];
+  c->gb_path = NUT_GB_ONCHIP;
+  c->gb_levels = c->gb_optimistic = 0;
   if (s->nkeys >= 1 && s->n && gp != 0 && (gp == 1 || (group_hint >= kGpMinGroups && s->n >= 4 * group_hint))) {
     bool used = false;
     st = alloc_table(g, cap);

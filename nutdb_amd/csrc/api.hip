@@ -302,6 +302,31 @@ nut_status nut_ctx_sort_stats(nut_ctx *c, uint64_t *bytes, uint32_t *levels) {
   return NUT_OK;
 }
 
+nut_status nut_ctx_groupby_stats(nut_ctx *c, uint32_t *path, uint32_t *levels, uint32_t *optimistic) {
+  if (!c) return fail(NUT_ERR_INVALID_ARG, "nut_ctx_groupby_stats: NULL context");
+  if (path) *path = c->gb_path;
+  if (levels) *levels = c->gb_levels;
+  if (optimistic) *optimistic = c->gb_optimistic;
+  return NUT_OK;
+}
+
+nut_status nut_ctx_set_option(nut_ctx *c, int option, int64_t value) {
+  if (!c || option < 0 || option >= NUT_OPT_COUNT) return fail(NUT_ERR_INVALID_ARG, "nut_ctx_set_option: bad option");
+  static const int64_t lo[NUT_OPT_COUNT] = {-1, 0, 0, 0, 1, 0, 0, 0}, hi[NUT_OPT_COUNT] = {1, 2, 1, 1, 64, 1, 4, 4};
+  if (value < lo[option] || value > hi[option])
+    return fail(NUT_ERR_INVALID_ARG, "nut_ctx_set_option: value " + std::to_string(value) + " out of range [" +
+                                         std::to_string(lo[option]) + ", " + std::to_string(hi[option]) + "]");
+  c->opt[option] = value;
+  return NUT_OK;
+}
+
+nut_status nut_ctx_get_option(nut_ctx *c, int option, int64_t *value) {
+  if (!c || !value || option < 0 || option >= NUT_OPT_COUNT)
+    return fail(NUT_ERR_INVALID_ARG, "nut_ctx_get_option: bad argument");
+  *value = c->opt[option];
+  return NUT_OK;
+}
+
 nut_status nut_ctx_kernel_time(nut_ctx *c, int kind, double *total_ms, uint64_t *launches) {
   if (!c || kind < 0 || kind > 3) return fail(NUT_ERR_INVALID_ARG, "nut_ctx_kernel_time: bad argument");
   DeviceGuard g(c->device);

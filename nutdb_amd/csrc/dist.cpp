@@ -371,6 +371,94 @@ nut_status groupby_member(nut_dist *d, int l, const nut_agg_spec *spec, uint64_t
 }
 
 // ------------------------------------------------------------------ sample sort
+// Skew-safe key ranges.  s = the P-1 splitters at the pooled sample's quantiles (ascending,
+// repeating when one key fills several quantiles).  A key k goes to rank #{i : s[i] <= k}
+// — except a key equal to a splitter value v at positions a..b of s: it may sit on any of
+// the ranks a .. b+1 (the ranks between hold only v, so the ranks' outputs still
+// concatenate in order).  Such keys get a bucket of their own in the partition (splitters
+// v and v+1: [v, v+1) = {v}); every bucket maps to a rank range, and the all-to-all splits
+// an equal-key bucket's count over that range in proportion to how much of v's run in the
+// sorted pooled sample falls in each rank's quantile range (so a key holding half the rows
+// fills the ranks around it instead of doubling one).  All distinct splitter values get
+// such a bucket when <= 63 splitters result, otherwise the repeated ones (a key holding
+// >= 1/P of the sample) — always <= P - 1 splitters.
+struct SortRanges {
+  std::vector<int64_t> e;  // partition splitters, strictly ascending (nut_partition_i64)
+  std::vector<int> lo, hi; // bucket j (keys in [e[j-1], e[j])) -> ranks lo[j] .. hi[j]
+  std::vector<std::vector<uint64_t>> w;  // bucket j's weights over lo[j] .. hi[j] (sum > 0)
+};
+
+// pool: the sorted pooled sample (s[i] = pool[(i + 1) * m / P])
+SortRanges sort_ranges(const std::vector<int64_t> &s, const std::vector<int64_t> &pool, int P) {
+  struct V {
+    int64_t v;
+    int a, b;
+  };
+  std::vector<V> vs;
+  for (int i = 0; i < (int)s.size(); ++i)
+    if (vs.empty() || vs.back().v != s[i]) vs.push_back(V{s[i], i, i});
+    else vs.back().b = i;
+  auto count_e = [&](bool all) {
+    int m = 0;
+    for (size_t i = 0; i < vs.size(); ++i) {
+      ++m;
+      const bool eq = all || vs[i].b > vs[i].a;
+      if (eq && vs[i].v != INT64_MAX && !(i + 1 < vs.size() && vs[i + 1].v == vs[i].v + 1)) ++m;
+    }
+    return m;
+  };
+  const bool all = count_e(true) <= 63;
+  const uint64_t m = pool.size();
+  SortRanges r;
+  auto one = [&](int rank) {
+    r.lo.push_back(rank);
+    r.hi.push_back(rank);
+    r.w.push_back(std::vector<uint64_t>(1, 1));
+  };
+  one(0);  // bucket 0: keys below every splitter
+  for (size_t i = 0; i < vs.size(); ++i) {
+    const V &x = vs[i];
+    const bool eq = all || x.b > x.a;
+    r.e.push_back(x.v);
+    if (eq) {  // bucket {v}: ranks a .. b+1, weighted by v's run [f, l) in the pool
+      const uint64_t f = (uint64_t)(std::lower_bound(pool.begin(), pool.end(), x.v) - pool.begin());
+      const uint64_t l = (uint64_t)(std::upper_bound(pool.begin(), pool.end(), x.v) - pool.begin());
+      std::vector<uint64_t> w;
+      uint64_t tot = 0;
+      for (int t = x.a; t <= x.b + 1; ++t) {
+        const uint64_t q0 = (uint64_t)t * m / P, q1 = (uint64_t)(t + 1) * m / P;
+        const uint64_t o = std::min(l, q1) > std::max(f, q0) ? std::min(l, q1) - std::max(f, q0) : 0;
+        w.push_back(o);
+        tot += o;
+      }
+      if (!tot) std::fill(w.begin(), w.end(), 1);
+      r.lo.push_back(x.a);
+      r.hi.push_back(x.b + 1);
+      r.w.push_back(std::move(w));
+      if (x.v != INT64_MAX && !(i + 1 < vs.size() && vs[i + 1].v == x.v + 1)) {
+        r.e.push_back(x.v + 1);  // keys in (v, next splitter value): rank b+1
+        one(x.b + 1);
+      }
+    } else {  // keys in [v, next): rank b+1, as without the tie split
+      one(x.b + 1);
+    }
+  }
+  return r;
+}
+
+// count c of bucket j split over its ranks by weight (cumulative rounding: sums to c)
+void split_bucket(const SortRanges &r, size_t j, uint64_t c, std::vector<uint64_t> &counts) {
+  const std::vector<uint64_t> &w = r.w[j];
+  uint64_t W = 0, acc = 0, prev = 0;
+  for (uint64_t x : w) W += x;
+  for (size_t t = 0; t < w.size(); ++t) {
+    acc += w[t];
+    const uint64_t upto = (uint64_t)((unsigned __int128)c * acc / W);
+    counts[r.lo[j] + t] += upto - prev;
+    prev = upto;
+  }
+}
+
 nut_status sort_member(nut_dist *d, int l, const int64_t *in, uint64_t n, const int64_t **out, uint64_t *out_n) {
   Member &mb = d->m[l];
   nut_ctx *c = mb.ctx;
@@ -392,22 +480,28 @@ nut_status sort_member(nut_dist *d, int l, const int64_t *in, uint64_t n, const 
   st = exchange_header(d, l, st, hdr, all);
   if (st) return st;
   uint64_t *pool_dev = buf(mb, 3) + 2 * kSamples;
+  // a local failure from here on travels in the next header (every rank returns together)
   st = allgather(d, l, buf(mb, 3) + kSamples, pool_dev, kSamples);
-  if (st) return st;
   std::vector<int64_t> pool((size_t)P * kSamples);
-  NUT_HIP(hipMemcpyAsync(pool.data(), pool_dev, pool.size() * 8, hipMemcpyDeviceToHost, s));
-  NUT_HIP(hipStreamSynchronize(s));
+  if (!st) {
+    hipError_t e = hipMemcpyAsync(pool.data(), pool_dev, pool.size() * 8, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) st = hip_fail(e, "nut_dist_sort_i64 sample copy");
+  }
   std::vector<int64_t> live;
   live.reserve(pool.size());
   for (int q = 0; q < P; ++q)
     if (all[(size_t)q * 2 + 1]) live.insert(live.end(), pool.begin() + (size_t)q * kSamples, pool.begin() + (size_t)(q + 1) * kSamples);
   std::sort(live.begin(), live.end());
-  std::vector<int64_t> spl(P > 1 ? P - 1 : 1, 0);
+  std::vector<int64_t> spl(P - 1, 0);
   for (int i = 1; i < P; ++i) spl[i - 1] = live.empty() ? 0 : live[(live.size() * (size_t)i) / P];
-  // 2. stable partition into P key ranges
-  std::vector<uint64_t> counts(P, 0);
-  st = reserve(mb, 0, n);
-  if (!st) st = nut_partition_i64(c, in, n, spl.data(), P - 1, (int64_t *)buf(mb, 0), counts.data());
+  const SortRanges rg = sort_ranges(spl, live, P);
+  // 2. stable partition into the ranges' buckets (bucket order = destination order)
+  const int nb = (int)rg.e.size() + 1;
+  std::vector<uint64_t> bcount(nb, 0), counts(P, 0);
+  if (!st) st = reserve(mb, 0, n);
+  if (!st) st = nut_partition_i64(c, in, n, rg.e.data(), nb - 1, (int64_t *)buf(mb, 0), bcount.data());
+  for (int j = 0; j < nb; ++j) split_bucket(rg, (size_t)j, bcount[j], counts);
   hdr.assign(1 + P, 0);
   for (int q = 0; q < P; ++q) hdr[1 + q] = counts[q];
   st = exchange_header(d, l, st, hdr, all);

@@ -410,28 +410,18 @@ constexpr HjCfg hj_make() {
   return HjCfg{T, (uint32_t)(T * I), hj_probe_kernel<true, T, I>, hj_probe_kernel<false, T, I>,
                hj_probe_kernel<true, T, I, true>};
 }
-// probe tile shapes (threads x rows per lane); NUT_HJ_CFG picks one for tuning runs
-const HjCfg &hj_cfg() {
+// probe tile shapes (threads x rows per lane); NUT_OPT_JOIN_PROBE_CFG picks one for tuning runs
+const HjCfg &hj_cfg(const nut_ctx *c) {
   static const HjCfg cfgs[] = {hj_make<512, 8>(), hj_make<256, 8>(), hj_make<256, 16>(), hj_make<512, 16>(),
                                hj_make<256, 4>()};
-  static const int pick = [] {
-    const char *e = getenv("NUT_HJ_CFG");
-    const int v = e ? atoi(e) : 0;
-    return v >= 0 && v < (int)(sizeof cfgs / sizeof cfgs[0]) ? v : 0;
-  }();
-  return cfgs[pick];
+  return cfgs[c->opt[NUT_OPT_JOIN_PROBE_CFG]];
 }
 // the unordered probe's tile shape: no look-back chain to shorten, so the smallest tiles
-// with the fewest registers (most waves, most slot loads in flight) — NUT_HJ_ANYCFG for tuning
-const HjCfg &hj_any_cfg() {
+// with the fewest registers (most waves, most slot loads in flight) — NUT_OPT_JOIN_ANY_CFG
+const HjCfg &hj_any_cfg(const nut_ctx *c) {
   static const HjCfg cfgs[] = {hj_make<256, 4>(), hj_make<512, 8>(), hj_make<256, 8>(), hj_make<512, 4>(),
                                hj_make<128, 4>()};
-  static const int pick = [] {
-    const char *e = getenv("NUT_HJ_ANYCFG");
-    const int v = e ? atoi(e) : 0;
-    return v >= 0 && v < (int)(sizeof cfgs / sizeof cfgs[0]) ? v : 0;
-  }();
-  return cfgs[pick];
+  return cfgs[c->opt[NUT_OPT_JOIN_ANY_CFG]];
 }
 
 }  // namespace
@@ -459,7 +449,7 @@ nut_status join_build(nut_ctx *c, nut_join *j, const int64_t *build, uint64_t nb
   int log2c = 6;  // >= 2 slots per build row, >= 64 slots
   while ((1ull << log2c) < 2 * nb) ++log2c;
   const uint64_t cap = 1ull << log2c;
-  j->ntiles = (j->np + hj_cfg().tile - 1) / hj_cfg().tile;
+  j->ntiles = (j->np + hj_cfg(c).tile - 1) / hj_cfg(c).tile;
   if (j->ntiles > 0xFFFFFFF0ull) return fail(NUT_ERR_UNSUPPORTED, "nut_join_i64: probe side too large");
   // [slots 16 B x cap | dup u32, pad | ticket u32, err u32, total u64 | status u64 x ntiles]
   const size_t o_dup = cap * 16, o_state = o_dup + 16;
@@ -476,10 +466,7 @@ nut_status join_build(nut_ctx *c, nut_join *j, const int64_t *build, uint64_t nb
   NUT_HIP(hipMemsetAsync(j->dup, 0, 16, st));
   // region build for tables of 2^22 .. 2^29 slots (regions of 8192 slots, one 16-bit
   // partition), unless a region would be too full (many equal keys): then global CAS
-  static const bool region_on = [] {
-    const char *e = getenv("NUT_HJ_REGION");
-    return !(e && *e == '0');
-  }();
+  const bool region_on = c->opt[NUT_OPT_JOIN_REGION] != 0;
   if (nb && region_on && log2c >= 22 && log2c <= 29) {
     const int rb = log2c - 13;
     const uint64_t nreg = 1ull << rb;
@@ -534,7 +521,7 @@ nut_status join_probe(nut_join *j, bool write, int64_t *pi, int64_t *bi, uint64_
   if (!j->ntiles) return NUT_OK;
   if (j->any_order && write) {
     NUT_HIP(hipMemsetAsync(j->ticket, 0, 16, st));
-    const HjCfg &cf = hj_any_cfg();
+    const HjCfg &cf = hj_any_cfg(c);
     const uint64_t nt = (j->np + cf.tile - 1) / cf.tile;
     if (nt > 0x7FFFFFFFull) return fail(NUT_ERR_UNSUPPORTED, "nut_join: probe side too large");
     cf.any<<<dim3((unsigned)nt), dim3(cf.threads), 0, st>>>(j->t, j->probe, j->np, j->type, j->ticket, j->status,
@@ -542,7 +529,7 @@ nut_status join_probe(nut_join *j, bool write, int64_t *pi, int64_t *bi, uint64_
                                                          (const uint32_t *)j->dup, j->prows);
   } else {
     NUT_HIP(hipMemsetAsync(j->ticket, 0, j->state_bytes, st));
-    const HjCfg &cf = hj_cfg();
+    const HjCfg &cf = hj_cfg(c);
     (write ? cf.write : cf.count)<<<dim3((unsigned)j->ntiles), dim3(cf.threads), 0, st>>>(
         j->t, j->probe, j->np, j->type, j->ticket, j->status, (uint32_t)j->ntiles, j->total, pi, bi, cap, j->err,
         (const uint32_t *)j->dup, j->prows);

@@ -982,21 +982,14 @@ static nut_status launch_local_dev(nut_ctx *c, const MsBufs &bf, uint64_t base, 
   return NUT_OK;
 }
 
-// Scatter tile halves (ms_scatter_kernel<H>): NUT_MS_HALVES=1 keeps 16 Ki-key tiles
-static int ms_halves() {
-  static const int h = [] {
-    const char *e = getenv("NUT_MS_HALVES");
-    return e && atoi(e) == 1 ? 1 : 2;
-  }();
-  return h;
-}
+// Scatter tiles are staged and written in two halves (ms_scatter_kernel<2>): ~512-B digit
+// runs instead of 256 (29.24 -> 28.72 ms per 1.25e9-key sort, round-2 same-box A/B)
+static constexpr int ms_halves() { return 2; }
 
 static void launch_scatter(hipStream_t st, unsigned grid, const MsBufs &bf, const MsSeg *segs, const uint32_t *tiles,
                            uint32_t ntiles, const MsDigit &dg, uint64_t flip, unsigned long long *cur) {
-  if (ms_halves() == 2)
-    hipLaunchKernelGGL(ms_scatter_kernel<2>, dim3(grid), dim3(MS_THREADS), 0, st, bf, segs, tiles, ntiles, dg, flip, cur);
-  else
-    hipLaunchKernelGGL(ms_scatter_kernel<1>, dim3(grid), dim3(MS_THREADS), 0, st, bf, segs, tiles, ntiles, dg, flip, cur);
+  hipLaunchKernelGGL(ms_scatter_kernel<ms_halves()>, dim3(grid), dim3(MS_THREADS), 0, st, bf, segs, tiles, ntiles, dg,
+                     flip, cur);
 }
 
 // One device-planned level over `big` (segments whose sizes the host knows): histogram,

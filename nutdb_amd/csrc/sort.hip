@@ -312,11 +312,6 @@ __global__ void sort_key_kernel(const uint64_t *__restrict__ in, int type, int d
   }
 }
 
-__global__ void rs_copy_kernel(const uint64_t *__restrict__ in, uint64_t *__restrict__ out, uint64_t n) {
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
-    out[i] = in[i];
-}
-
 // Status granules for `ntiles` tiles, tagged with a fresh pass epoch.  The array is
 // cleared only when it is (re)allocated or the 8-bit epoch wraps.
 nut_status next_status(nut_ctx *c, uint64_t ntiles, uint64_t **status, uint32_t *epoch) {
@@ -337,75 +332,6 @@ nut_status next_status(nut_ctx *c, uint64_t ntiles, uint64_t **status, uint32_t 
 }  // namespace nut
 
 using namespace nut;
-
-nut_status nut::lsd_sort_i64(nut_ctx *c, const int64_t *in, int64_t *out, uint64_t n, uint64_t flip) {
-  if (!c || (n && (!in || !out))) return fail(NUT_ERR_INVALID_ARG, "nut_sort_i64: NULL argument");
-  const uint64_t ntiles = (n + RS_TILE - 1) / RS_TILE;
-  if (ntiles > 0x7FFFFFF0ull || n > RS_VAL) return fail(NUT_ERR_UNSUPPORTED, "nut_sort_i64: n too large");
-  // scratch: [err 4 B, pad | tickets 8 x 4 B at +16 | hist 8*256*8 at +256 | base 8*256*8 |
-  //           trivial 8*4 | ping-pong buffer n*8]
-  const size_t o_hist = 256;
-  const size_t o_base = o_hist + 8 * RS_BINS * 8;
-  const size_t o_triv = o_base + 8 * RS_BINS * 8;
-  const size_t o_tmp = (o_triv + 64 + 255) & ~size_t(255);
-  nut_status s = c->sort_tmp.reserve(o_tmp + n * 8);
-  if (s) return s;
-  char *b = (char *)c->sort_tmp.ptr;
-  uint32_t *err = (uint32_t *)b;
-  uint32_t *tickets = (uint32_t *)(b + 16);
-  unsigned long long *hist = (unsigned long long *)(b + o_hist);
-  uint64_t *base = (uint64_t *)(b + o_base);
-  uint32_t *triv = (uint32_t *)(b + o_triv);
-  uint64_t *tmp = (uint64_t *)(b + o_tmp);
-  hipStream_t st = c->stream;
-
-  c->timer.begin(st, NUT_KERNEL_SORT);
-  NUT_HIP(hipMemsetAsync(b, 0, o_base, st));  // err + tickets + histograms
-  uint64_t hblocks = std::min<uint64_t>((n + 2 * RS_HIST_THREADS - 1) / (2 * RS_HIST_THREADS), (uint64_t)c->num_cus * 4);
-  hipLaunchKernelGGL(rs_hist_kernel, dim3((unsigned)hblocks), dim3(RS_HIST_THREADS), 0, st, in, n, flip, hist);
-  hipLaunchKernelGGL(rs_scan_kernel, dim3(8), dim3(RS_BINS), 0, st, (const unsigned long long *)hist, n, base, triv);
-  NUT_HIP(hipGetLastError());
-  // which passes run is decided on the host (8 flags)
-  uint32_t htriv[8];
-  NUT_HIP(hipMemcpyAsync(htriv, triv, sizeof(htriv), hipMemcpyDeviceToHost, st));
-  NUT_HIP(hipStreamSynchronize(st));
-  int passes[8], np = 0;
-  for (int p = 0; p < 8; ++p)
-    if (!htriv[p]) passes[np++] = p;
-  c->sort_bytes = 8 * n + 16 * n * (uint64_t)(np ? np : 1);
-  c->sort_levels = (uint32_t)np;
-  if (np == 0) {  // all keys equal
-    hipLaunchKernelGGL(rs_copy_kernel, dim3((unsigned)std::min<uint64_t>((n + 255) / 256, 4096)), dim3(256), 0, st,
-                       (const uint64_t *)in, (uint64_t *)out, n);
-    c->timer.end(st);
-    NUT_HIP(hipGetLastError());
-    return NUT_OK;
-  }
-  // ping-pong so that the last executed pass writes `out`
-  const uint64_t *src = (const uint64_t *)in;
-  for (int k = 0; k < np; ++k) {
-    const bool first = k == 0, last = k == np - 1;
-    uint64_t *dst = ((np - 1 - k) % 2 == 0) ? (uint64_t *)out : tmp;
-    uint64_t *status;
-    uint32_t epoch;
-    s = next_status(c, ntiles, &status, &epoch);
-    if (s) return s;
-    const int p = passes[k];
-    const uint64_t *db = base + p * RS_BINS;
-    auto kern = first ? (last ? rs_pass_kernel<true, true, RadixDigit> : rs_pass_kernel<true, false, RadixDigit>)
-                      : (last ? rs_pass_kernel<false, true, RadixDigit> : rs_pass_kernel<false, false, RadixDigit>);
-    hipLaunchKernelGGL(kern, dim3((unsigned)ntiles), dim3(RS_THREADS), 0, st, src, dst, n, RadixDigit{8 * p},
-                       (const int64_t *)nullptr, RS_BINS, flip, db, status, epoch, tickets + k, err,
-                       (const uint64_t *)nullptr, (uint64_t *)nullptr);
-    NUT_HIP(hipGetLastError());
-    src = dst;
-  }
-  c->timer.end(st);
-  NUT_HIP(hipMemcpyAsync(htriv, err, 4, hipMemcpyDeviceToHost, st));
-  NUT_HIP(hipStreamSynchronize(st));
-  if (htriv[0]) return fail(NUT_ERR_TIMEOUT, "nut_sort_i64: look-back spin limit hit");
-  return NUT_OK;
-}
 
 // Stable sort of (key, payload) pairs: ORDER BY keys with projected columns.  Keys are
 // mapped to unsigned order once (sort_key_kernel), then LSD passes move key and payload
@@ -481,17 +407,14 @@ extern "C" nut_status nut_sort_pairs(nut_ctx *c, const void *keys, int key_type,
   return NUT_OK;
 }
 
-// NUT_SORT=lsd selects the 8-pass LSD sort above (A/B measurements); default: msd_sort.hip
+// keys-only sorts run the hybrid MSD radix sort (msd_sort.hip); the LSD passes above
+// serve the stable (key, payload) sorts and the sample sort's partition
 static nut_status sort_i64(nut_ctx *c, const int64_t *in, int64_t *out, uint64_t n, uint64_t flip) {
   if (!c || (n && (!in || !out))) return fail(NUT_ERR_INVALID_ARG, "nut_sort_i64: NULL argument");
   if (n && (uintptr_t)in == (uintptr_t)out) return fail(NUT_ERR_INVALID_ARG, "nut_sort_i64: in and out alias");
   if (n == 0) return NUT_OK;
   DeviceGuard g(c->device);
-  static const bool lsd = [] {
-    const char *e = getenv("NUT_SORT");
-    return e && strcmp(e, "lsd") == 0;
-  }();
-  return lsd ? lsd_sort_i64(c, in, out, n, flip) : msd_sort_i64(c, in, out, n, flip);
+  return msd_sort_i64(c, in, out, n, flip);
 }
 
 extern "C" nut_status nut_sort_i64(nut_ctx *c, const int64_t *in, int64_t *out, uint64_t n) {

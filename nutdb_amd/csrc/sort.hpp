@@ -8,7 +8,6 @@
 #include "common.hpp"
 
 namespace nut {
-nut_status lsd_sort_i64(nut_ctx *c, const int64_t *in, int64_t *out, uint64_t n, uint64_t flip);  // sort.hip
 nut_status msd_sort_i64(nut_ctx *c, const int64_t *in, int64_t *out, uint64_t n, uint64_t flip);  // msd_sort.hip
 nut_status join_matched(nut_ctx *c, const int64_t *bi, uint64_t n, int64_t *out);                   // join.hip
 nut_status hash_partition16(nut_ctx *c, const int64_t *keys, uint64_t n, uint64_t kx, int64_t *tmpk,  // aggregate.hip

@@ -1304,19 +1304,24 @@ bool lower_mode(const Statement &st, nut_plan &p, Lowering &L) {
 // comparisons ANDed, the fused expression shapes); anything else — arbitrary
 // expressions, OR / NOT / CASE, column-to-column comparisons, more than 6 terms — to
 // expression programs compiled for the query (jit.cpp).  Scans stay on the filter kernel.
-// USING columns: an unqualified reference binds to the preserved table's column
-void resolve_using(nut_plan &p) {
+// USING columns: an unqualified reference binds to the preserved table's column.  FULL
+// OUTER preserves both: there an unqualified u means COALESCE(l.u, r.u), which is not
+// executed, so it is rejected (qualified l.u / r.u inside aggregates run).
+bool resolve_using(nut_plan &p, Lowering &L) {
   for (const auto &u : p.using_cols)
     for (std::string &c : p.cols)
-      if (ieq(c, u.first)) c = u.second;
+      if (ieq(c, u.first)) {
+        if (p.join == PJ_FULL)
+          return L.fail("FULL OUTER JOIN ... USING: unqualified '" + u.first +
+                        "' (COALESCE of both tables' columns) is not executed; qualify it");
+        c = u.second;
+      }
+  return true;
 }
 
 bool lower(const Statement &st, nut_plan &p, Lowering &L) {
   Lowering L1;
-  if (lower_mode(st, p, L1)) {
-    resolve_using(p);
-    return true;
-  }
+  if (lower_mode(st, p, L1)) return resolve_using(p, L);
   bool agg = false;
   if (st.k == StmtKind::Select && !st.query.is_union && st.query.body) {
     const QueryBody &b = *st.query.body;
@@ -1329,7 +1334,7 @@ bool lower(const Statement &st, nut_plan &p, Lowering &L) {
   p2.compiled = true;
   Lowering L2;
   if (!lower_mode(st, p2, L2)) return L.fail(L2.err);
-  resolve_using(p2);
+  if (!resolve_using(p2, L)) return false;
   p = std::move(p2);
   return true;
 }
@@ -1844,30 +1849,36 @@ bool having_true(const HNode &h, const std::vector<std::vector<uint64_t>> &cols,
 // the nut_agg_spec of an aggregate plan over bound columns (program nodes live in store)
 // String programs: a dictionary column or string constant may only meet another string
 // in = / != (IN and CASE x WHEN lower to those), or be a GROUP BY key.
+// Each table has its own dictionary: two columns compare only when their codes come from
+// the same one (columns of one table; a join's two tables do not).
 nut_status check_strings(const nut_plan &p, const PProg &pp, const Dict *const *dicts, const char *what) {
-  std::vector<char> st;
+  static const Dict *const kConst = reinterpret_cast<const Dict *>(uintptr_t(1));  // a string constant
+  std::vector<const Dict *> st;
   for (const PNode &n : pp) {
     const int op = n.op;
     const int k = pnode_arity(op);
-    char a[3] = {0, 0, 0};
+    const Dict *a[3] = {nullptr, nullptr, nullptr};
     for (int i = k - 1; i >= 0; --i) {
       if (st.empty()) return NUT_OK;  // malformed: nut_prog_type reports it
       a[i] = st.back();
       st.pop_back();
     }
     if (op == NUT_P_COL) {
-      st.push_back(dicts[n.col] != nullptr);
+      st.push_back(dicts[n.col]);
       continue;
     }
     if (op == NUT_P_I64 || op == NUT_P_F64) {
-      st.push_back(n.c.is_str);
+      st.push_back(n.c.is_str ? kConst : nullptr);
       continue;
     }
-    if ((op == NUT_P_EQ || op == NUT_P_NE) && a[0] != a[1])
+    if ((op == NUT_P_EQ || op == NUT_P_NE) && (a[0] != nullptr) != (a[1] != nullptr))
       return fail(NUT_ERR_PLAN, std::string(what) + ": a string compared with a number");
+    if ((op == NUT_P_EQ || op == NUT_P_NE) && a[0] && a[1] && a[0] != kConst && a[1] != kConst && a[0] != a[1])
+      return fail(NUT_ERR_PLAN, std::string(what) + ": string columns of two tables compared (their dictionaries "
+                                                    "differ; only columns of one table compare)");
     if (!(op == NUT_P_EQ || op == NUT_P_NE) && (a[0] || a[1] || a[2]))
       return fail(NUT_ERR_PLAN, std::string(what) + ": strings are executed in = / != / IN and as GROUP BY keys only");
-    st.push_back(0);
+    st.push_back(nullptr);
   }
   if (!st.empty() && st.back()) return fail(NUT_ERR_PLAN, std::string(what) + ": a string value (only count() takes strings)");
   return NUT_OK;
@@ -2418,6 +2429,7 @@ nut_status exec_join(nut_ctx *c, const nut_plan &p, const nut_column *lc, int nl
     row = ci == q.proj || in_prog(q.where, ci);
     for (int pj : q.projs) row = row || pj == ci;
     for (int k : q.keys) row = row || k == ci;
+    for (const auto &sk : q.sort_keys) row = row || sk.first == ci;  // ORDER BY, projected or not
     for (const PlanPred &pr : q.preds) row = row || pr.col == ci;
     agg = false;
     for (int v : q.vals) agg = agg || v == ci;
@@ -2678,6 +2690,7 @@ nut_status exec_joinn(nut_ctx *c, const nut_plan &p, const nut_column *const *ta
     row = ci == q.proj || in_prog(q.where, ci);
     for (int pj : q.projs) row = row || pj == ci;
     for (int k2 : q.keys) row = row || k2 == ci;
+    for (const auto &sk : q.sort_keys) row = row || sk.first == ci;  // ORDER BY, projected or not
     for (const PlanPred &pr : q.preds) row = row || pr.col == ci;
     agg = false;
     for (int v : q.vals) agg = agg || v == ci;
@@ -2837,6 +2850,7 @@ nut_status exec_joinn(nut_ctx *c, const nut_plan &p, const nut_column *const *ta
     bool used = ci == p2.proj || in_prog(p2.where, ci);
     for (int pj : p2.projs) used = used || pj == ci;
     for (int k2 : p2.keys) used = used || k2 == ci;
+    for (const auto &sk : p2.sort_keys) used = used || sk.first == ci;
     for (const PlanPred &pr : p2.preds) used = used || pr.col == ci;
     for (int v : p2.vals) used = used || v == ci;
     for (const PlanAgg &a : p2.aggs) {

@@ -111,7 +111,7 @@ def distributed_groupby(ex, local, merge_query: Callable[[torch.Tensor], "object
 
 
 # ---------------------------------------------------------------------------- sample sort
-def choose_splitters(local: torch.Tensor, group=None, samples_per_rank: int = 4096) -> np.ndarray:
+def choose_splitters(local: torch.Tensor, group=None, samples_per_rank: int = 4096, with_pool: bool = False):
     """Regular sample of the local keys -> all_gather -> P-1 splitters at the global
     sample's quantiles (host array, ascending).  The sample is a strided read of
     `samples_per_rank` keys (with repetition when the shard is smaller); a rank with no
@@ -132,11 +132,75 @@ def choose_splitters(local: torch.Tensor, group=None, samples_per_rank: int = 40
     dist.all_gather(haves, have, group=group)
     pool = np.concatenate([s.cpu().numpy() for s, h in zip(samples, haves) if int(h.item())] or
                           [np.zeros(0, np.int64)])
-    if len(pool) == 0:
-        return np.zeros(world - 1, dtype=np.int64)
     pool.sort()
     m = len(pool)
-    return np.array([pool[(i * m) // world] for i in range(1, world)], dtype=np.int64)
+    spl = np.array([pool[(i * m) // world] if m else 0 for i in range(1, world)], dtype=np.int64)
+    return (spl, pool) if with_pool else spl
+
+
+INT64_MAX = (1 << 63) - 1
+
+
+def sort_ranges(splitters, pool, world):
+    """Skew-safe key ranges of the sample sort (restatement of csrc/dist.cpp sort_ranges).
+    A key k goes to rank #{i : s[i] <= k}, except a key equal to a splitter value v at
+    positions a..b: it may sit on ranks a .. b+1 (the ranks in between hold only v), split
+    in proportion to how much of v's run in the sorted pooled sample `pool` falls in each
+    rank's quantile range.  Returns (e, lo, hi, w): the strictly ascending partition
+    splitters (an equal-key bucket is [v, v+1)), each bucket's rank range and weights."""
+    pool = np.asarray(pool, dtype=np.int64)
+    m = len(pool)
+    s = [int(x) for x in splitters]
+    vs = []  # [v, a, b]
+    for i, v in enumerate(s):
+        if vs and vs[-1][0] == v:
+            vs[-1][2] = i
+        else:
+            vs.append([v, i, i])
+
+    def n_e(all_):
+        m = 0
+        for i, (v, a, b) in enumerate(vs):
+            m += 1
+            if (all_ or b > a) and v != INT64_MAX and not (i + 1 < len(vs) and vs[i + 1][0] == v + 1):
+                m += 1
+        return m
+    all_ = n_e(True) <= 63
+    e, lo, hi, w = [], [0], [0], [[1]]
+    for i, (v, a, b) in enumerate(vs):
+        e.append(v)
+        if all_ or b > a:
+            f = int(np.searchsorted(pool, v, "left"))
+            l_ = int(np.searchsorted(pool, v, "right"))
+            ws = [max(0, min(l_, (t + 1) * m // world) - max(f, t * m // world)) for t in range(a, b + 2)]
+            lo.append(a)
+            hi.append(b + 1)
+            w.append(ws if sum(ws) else [1] * len(ws))
+            if v != INT64_MAX and not (i + 1 < len(vs) and vs[i + 1][0] == v + 1):
+                e.append(v + 1)
+                lo.append(b + 1)
+                hi.append(b + 1)
+                w.append([1])
+        else:
+            lo.append(b + 1)
+            hi.append(b + 1)
+            w.append([1])
+    return np.array(e, dtype=np.int64), lo, hi, w
+
+
+def split_counts(bucket_counts, lo, w, world):
+    """Per-destination key counts: bucket j's keys over ranks lo[j] .. by weight w[j]
+    (cumulative rounding; bucket order = destination order, so each rank's keys stay
+    contiguous in the partitioned array)."""
+    out = [0] * world
+    for c, a, ws in zip(bucket_counts, lo, w):
+        W, acc, prev = sum(ws), 0, 0
+        for t, x in enumerate(ws):
+            acc += x
+            upto = c * acc // W
+            out[a + t] += upto - prev
+            prev = upto
+    return out
 
 
 def exchange_keys(part: torch.Tensor, counts: List[int], group=None) -> torch.Tensor:
@@ -207,13 +271,17 @@ def distributed_join(build: torch.Tensor, probe: torch.Tensor, partition: Callab
 def distributed_sort(local: torch.Tensor, partition: Callable, sort: Callable, group=None,
                      samples_per_rank: int = 4096) -> torch.Tensor:
     """Multi-GPU ORDER BY k (BASELINE config 5): sample -> splitters ->
-    local stable partition into P buckets (`partition(keys, splitters) -> (keys, counts)`,
-    nut_partition_i64 on a GPU) -> ONE all-to-all of keys over RCCL -> local radix sort
-    (`sort(keys) -> keys`, nut_sort_i64).  Rank r returns the r-th range of the global
-    order: every key on rank r is <= every key on rank r+1 (keys equal to a splitter all
-    land on the higher rank)."""
-    splitters = choose_splitters(local, group, samples_per_rank)
-    part, counts = partition(local, splitters)
+    skew-safe ranges (sort_ranges) -> local stable partition into their buckets
+    (`partition(keys, splitters) -> (keys, counts)`, nut_partition_i64 on a GPU) -> ONE
+    all-to-all of keys -> local radix sort (`sort(keys) -> keys`, nut_sort_i64).  Rank r
+    returns the r-th range of the global order: every key on rank r is <= every key on
+    rank r+1; a key filling several quantiles of the sample is spread over their ranks.
+    (Restatement for the gloo tests; the product path is nut_dist_sort_i64.)"""
+    world = dist.get_world_size(group)
+    splitters, pool = choose_splitters(local, group, samples_per_rank, with_pool=True)
+    e, lo, hi, w = sort_ranges(splitters, pool, world)
+    part, bcounts = partition(local, e)
+    counts = split_counts(bcounts, lo, w, world)
     recv = exchange_keys(part, counts, group)
     return sort(recv)
 
@@ -331,8 +399,10 @@ class NutDist:
                 self._results.add(res[-1])
         return res
 
-    def sort_i64(self, cols):
-        """nut_dist_sort_i64: member l's sorted key range (the r-th of the global order)."""
+    def sort_i64(self, cols, copy: bool = True):
+        """nut_dist_sort_i64: member l's sorted key range (the r-th of the global order) —
+        copied into a tensor, or (copy=False) the member-owned (device address, count),
+        valid until the member's next nut_dist call."""
         from ._lib import lib
         ins = (C.c_void_p * self.nlocal)(*[c.data_ptr() if c.numel() else None for c in cols])
         ns = (C.c_uint64 * self.nlocal)(*[c.numel() for c in cols])
@@ -340,7 +410,29 @@ class NutDist:
         on = (C.c_uint64 * self.nlocal)()
         self._ready()
         _check(lib.nut_dist_sort_i64(self.h, ins, ns, outs, on), "nut_dist_sort_i64")
+        if not copy:
+            return [(outs[l], on[l]) for l in range(self.nlocal)]
         return [self._copy_out(l, outs[l], on[l]) for l in range(self.nlocal)]
+
+    def enable_timing(self, on: bool = True) -> None:
+        """hipEvent timing of the hot kernels on every member context (nut_ctx_enable_timing)."""
+        from ._lib import lib
+        for m in self.members:
+            _check(lib.nut_ctx_enable_timing(m.ctx, int(on)), "nut_ctx_enable_timing")
+
+    def kernel_time(self, kind: int, l: int = 0):
+        """(total ms, launches) of one kernel kind on member l since the last call."""
+        from ._lib import lib
+        ms, cnt = C.c_double(), C.c_uint64()
+        _check(lib.nut_ctx_kernel_time(self.members[l].ctx, kind, C.byref(ms), C.byref(cnt)), "nut_ctx_kernel_time")
+        return ms.value, cnt.value
+
+    def sort_stats(self, l: int = 0):
+        """(algorithmic bytes, scatter levels) of member l's last local sort."""
+        from ._lib import lib
+        b, lv = C.c_uint64(), C.c_uint32()
+        _check(lib.nut_ctx_sort_stats(self.members[l].ctx, C.byref(b), C.byref(lv)), "nut_ctx_sort_stats")
+        return b.value, lv.value
 
     def filter_i64(self, cols, op, k: int):
         """nut_dist_filter_i64: [(selected values of member l, global offset)]."""
@@ -357,8 +449,9 @@ class NutDist:
                                        off), "nut_dist_filter_i64")
         return [(outs[l][:on[l]], int(off[l])) for l in range(self.nlocal)]
 
-    def join_i64(self, builds, probes, how: str = "inner", build_row0=None, probe_row0=None):
-        """nut_dist_join_i64: [(global probe rows, global build rows)] per member."""
+    def join_i64(self, builds, probes, how: str = "inner", build_row0=None, probe_row0=None, copy: bool = True):
+        """nut_dist_join_i64: [(global probe rows, global build rows)] per member (copy=False:
+        the member-owned (probe address, build address, pairs))."""
         from ._lib import lib
         from .executor import Executor
         L_ = self.nlocal
@@ -376,6 +469,8 @@ class NutDist:
         self._ready()
         _check(lib.nut_dist_join_i64(self.h, bp, bn, b0, pp, pn, p0, Executor.JOIN_TYPES[how], po, bo, npairs),
                "nut_dist_join_i64")
+        if not copy:
+            return [(po[l], bo[l], npairs[l]) for l in range(L_)]
         return [(self._copy_out(l, po[l], npairs[l]), self._copy_out(l, bo[l], npairs[l])) for l in range(L_)]
 
 

@@ -339,6 +339,24 @@ class Executor:
         check(lib.nut_ctx_sort_stats(self.ctx, C.byref(b), C.byref(lv)), "nut_ctx_sort_stats")
         return b.value, lv.value
 
+    GROUPBY_PATHS = ("onchip", "partitioned_direct", "partitioned_spill")
+    OPTIONS = {"gb_partition": 0, "gb_levels": 1, "gb_optimistic": 2, "gb_direct": 3, "gb_chunks": 4,
+               "join_region": 5, "join_probe_cfg": 6, "join_any_cfg": 7}
+
+    def groupby_stats(self) -> dict:
+        """The algorithm the last group-by on this context took (nut_ctx_groupby_stats)."""
+        p, lv, opt = C.c_uint32(), C.c_uint32(), C.c_uint32()
+        check(lib.nut_ctx_groupby_stats(self.ctx, C.byref(p), C.byref(lv), C.byref(opt)), "nut_ctx_groupby_stats")
+        return {"path": self.GROUPBY_PATHS[p.value], "levels": lv.value, "optimistic": bool(opt.value)}
+
+    def set_option(self, name: str, value: int) -> int:
+        """nut_ctx_set_option (tuning / tests); returns the previous value."""
+        key = self.OPTIONS[name]
+        old = C.c_int64()
+        check(lib.nut_ctx_get_option(self.ctx, key, C.byref(old)), "nut_ctx_get_option")
+        check(lib.nut_ctx_set_option(self.ctx, key, int(value)), "nut_ctx_set_option")
+        return old.value
+
     def sync(self):
         check(lib.nut_ctx_sync(self.ctx), "nut_ctx_sync")
 

@@ -428,6 +428,89 @@ uint64_t orc_multiset_hash_i64(const int64_t *v, uint64_t n) {
   return h;
 }
 
+/* ------------------------------------------------- indexed pool-key group-by */
+/* The synthetic config-3 key of row r is mix64((u_k(r) % G) ^ POOL_SALT): mix64 is a
+ * bijection, so the pool index g = u_k(r) % G names the group.  The rows are accumulated
+ * into dense per-thread [G] arrays indexed by g — no hashing, and for dyadic values
+ * ((u_v >> 44) / 64) the sums are kept as integer 1/64 units, exact in any order (1e9 rows
+ * x 2^20 units < 2^53).  Keys are regenerated from g and the groups ordered by key. */
+typedef struct {
+  int64_t key;
+  uint64_t g;
+} orc_kg;
+
+static int kg_cmp(const void *a, const void *b) {
+  const int64_t x = ((const orc_kg *)a)->key, y = ((const orc_kg *)b)->key;
+  return x < y ? -1 : x > y;
+}
+
+uint64_t orc_groupby_pool_dyadic(uint64_t key_seed, uint64_t groups, uint64_t val_seed, uint64_t row0, uint64_t n,
+                                 int64_t *out_keys, uint64_t *out_words, int nthreads) {
+  if (groups == 0) return 0;
+  int nt = nthreads > 0 ? nthreads : orc_max_threads();
+  const uint64_t G = groups;
+  uint64_t *sum = (uint64_t *)calloc((size_t)nt * G, 8);
+  uint64_t *cnt = (uint64_t *)calloc((size_t)nt * G, 8);
+  uint32_t *mn = (uint32_t *)malloc((size_t)nt * G * 4);
+  uint32_t *mx = (uint32_t *)calloc((size_t)nt * G, 4);
+  if (!sum || !cnt || !mn || !mx) {
+    free(sum); free(cnt); free(mn); free(mx);
+    return UINT64_MAX;
+  }
+  memset(mn, 0xFF, (size_t)nt * G * 4);
+  const uint64_t chunk = (n + (uint64_t)nt - 1) / (uint64_t)nt;
+#pragma omp parallel num_threads(nt)
+  {
+#ifdef _OPENMP
+    const int t = omp_get_thread_num();
+#else
+    const int t = 0;
+#endif
+    uint64_t *s = sum + (size_t)t * G, *c = cnt + (size_t)t * G;
+    uint32_t *lo = mn + (size_t)t * G, *hi = mx + (size_t)t * G;
+    const uint64_t a = (uint64_t)t * chunk, b = a + chunk > n ? n : a + chunk;
+    for (uint64_t i = a; i < b; ++i) {
+      const uint64_t g = orc_gen_u64(key_seed, row0 + i) % G;
+      const uint32_t v = (uint32_t)(orc_gen_u64(val_seed, row0 + i) >> 44);
+      s[g] += v;
+      c[g] += 1;
+      if (v < lo[g]) lo[g] = v;
+      if (v > hi[g]) hi[g] = v;
+    }
+  }
+  /* merge into thread 0's arrays */
+#pragma omp parallel for num_threads(nt) schedule(static)
+  for (int64_t g = 0; g < (int64_t)G; ++g)
+    for (int t = 1; t < nt; ++t) {
+      const size_t j = (size_t)t * G + (size_t)g;
+      sum[g] += sum[j];
+      cnt[g] += cnt[j];
+      if (mn[j] < mn[g]) mn[g] = mn[j];
+      if (mx[j] > mx[g]) mx[g] = mx[j];
+    }
+  orc_kg *kg = (orc_kg *)malloc((size_t)G * sizeof(orc_kg));
+  uint64_t m = 0;
+  for (uint64_t g = 0; g < G; ++g)
+    if (cnt[g]) {
+      kg[m].key = (int64_t)orc_mix64(g ^ ORC_POOL_SALT);
+      kg[m].g = g;
+      ++m;
+    }
+  qsort(kg, (size_t)m, sizeof(orc_kg), kg_cmp);
+#pragma omp parallel for num_threads(nt) schedule(static)
+  for (int64_t i = 0; i < (int64_t)m; ++i) {
+    const uint64_t g = kg[i].g;
+    const double fs = (double)sum[g] / 64.0, fmn = (double)mn[g] / 64.0, fmx = (double)mx[g] / 64.0;
+    out_keys[i] = kg[i].key;
+    memcpy(&out_words[4 * i + 0], &fs, 8);
+    out_words[4 * i + 1] = cnt[g];
+    memcpy(&out_words[4 * i + 2], &fmn, 8);
+    memcpy(&out_words[4 * i + 3], &fmx, 8);
+  }
+  free(kg); free(sum); free(cnt); free(mn); free(mx);
+  return m;
+}
+
 /* Hash equi-join (include/nutexec.h nut_join_i64 semantics; join types 0 INNER, 1 LEFT,
  * 2 SEMI, 3 ANTI): a CSR bucket table over the build keys (OpenMP count / scan / fill),
  * then an OpenMP probe in two passes per thread chunk (count pairs, write them), so the

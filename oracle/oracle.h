@@ -88,6 +88,17 @@ typedef struct {
 uint64_t orc_groupby(const orc_agg_spec *spec, uint64_t cap, int64_t *out_keys,
                      uint64_t *out_aggs, int nthreads);
 
+/* ---- indexed group-by of the synthetic pool-key workload (config 3 at full size) ----
+ * SELECT key, SUM(val), COUNT(*), MIN(val), MAX(val) GROUP BY key over rows
+ * [row0, row0+n) of key = ORC_GEN_POOL_KEY(key_seed, a = groups), val =
+ * ORC_GEN_DYADIC(val_seed): accumulated by pool index in dense arrays (exact, no hash
+ * table), so 1e9 rows x 1e7 groups take seconds.  out_keys[m], out_words[m][4] (f64 bits
+ * of SUM, COUNT, f64 bits of MIN, MAX), groups ordered by key; returns m (groups with at
+ * least one row), UINT64_MAX on allocation failure.  Pinned against orc_groupby on the
+ * same generated columns (tests/test_oracle_golden.py). */
+uint64_t orc_groupby_pool_dyadic(uint64_t key_seed, uint64_t groups, uint64_t val_seed, uint64_t row0, uint64_t n,
+                                 int64_t *out_keys, uint64_t *out_words, int nthreads);
+
 /* ---- sort: ascending int64 ---- */
 void orc_sort_i64(const int64_t *in, int64_t *out, uint64_t n, int nthreads);
 /* Hash equi-join, nut_join_i64 semantics (type 0 INNER, 1 LEFT, 2 SEMI, 3 ANTI): pairs in

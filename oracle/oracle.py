@@ -73,6 +73,9 @@ def lib():
         L.orc_multiset_hash_i64.restype = C.c_uint64
         L.orc_multiset_hash_i64.argtypes = [C.c_void_p, C.c_uint64]
         L.orc_max_threads.restype = C.c_int
+        L.orc_groupby_pool_dyadic.restype = C.c_uint64
+        L.orc_groupby_pool_dyadic.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64,
+                                              C.c_void_p, C.c_void_p, C.c_int]
         _lib = L
     return _lib
 
@@ -152,6 +155,20 @@ def groupby(keys, aggs, values=(), preds=(), nthreads=0, cap=None, row_mask=None
     if g == 2**64 - 1:
         raise ValueError("oracle group capacity too small")
     return ok[:g], ow[:g, : s.naggs]
+
+
+def groupby_pool_dyadic(groups: int, n: int, row0: int = 0, key_seed: int = 0x51, val_seed: int = 0x52,
+                        nthreads: int = 0):
+    """Indexed oracle of the synthetic config-3 workload (oracle.h orc_groupby_pool_dyadic):
+    SUM, COUNT, MIN, MAX of the dyadic value per pool key over rows [row0, row0 + n), without
+    materialising the columns.  Returns (keys [m, 1] int64, words [m, 4] uint64) ordered by
+    key — the layout of groupby() with aggs SUM, COUNT, MIN, MAX."""
+    ok = np.empty((groups, 1), dtype=np.int64)
+    ow = np.empty((groups, 4), dtype=np.uint64)
+    m = lib().orc_groupby_pool_dyadic(key_seed, groups, val_seed, row0, n, ok.ctypes.data, ow.ctypes.data, nthreads)
+    if m == 2**64 - 1:
+        raise MemoryError("orc_groupby_pool_dyadic: allocation failed")
+    return ok[:m], ow[:m]
 
 
 def sort_i64(col: np.ndarray, nthreads=0) -> np.ndarray:

@@ -53,3 +53,18 @@ def ex():
     e = Executor(0)
     yield e
     e.close()
+
+
+@pytest.fixture
+def opts(ex):
+    """Set nut_ctx options on the session executor for one test (the library reads no
+    environment variables); every option is restored afterwards."""
+    saved = {}
+
+    def set_(**kw):
+        for k, v in kw.items():
+            old = ex.set_option(k, v)
+            saved.setdefault(k, old)
+    yield set_
+    for k, v in saved.items():
+        ex.set_option(k, v)

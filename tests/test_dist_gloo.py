@@ -106,6 +106,15 @@ def _np_partition(keys, splitters):
     return torch.from_numpy(np.ascontiguousarray(k[order])), [int(c) for c in counts]
 
 
+def _sort_keys(orc, kind, rows, row0):
+    if kind == "heavy":  # half the rows hold one key (skew-safe splitters)
+        k = orc.gen_column(1, 0x50, rows, row0=row0)
+        k[(np.arange(rows) + row0) % 2 == 0] = 12345
+        return k
+    a, b = (0, 0) if kind == 1 else (-3, 7)  # kind 5 (RANGE_I64): heavy duplicates, splitter ties
+    return orc.gen_column(kind, 0x50, rows, row0=row0, a=a, b=b)
+
+
 def _sort_worker(rank, world, port, n, kind, q):
     sys.path.insert(0, str(ROOT))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -115,10 +124,10 @@ def _sort_worker(rank, world, port, n, kind, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         rows = n // world
-        a, b = (0, 0) if kind == 1 else (-3, 7)  # kind 5 (RANGE_I64): heavy duplicates, splitter ties
-        local = torch.from_numpy(orc.gen_column(kind, 0x50, rows, row0=rank * rows, a=a, b=b))
+        local = torch.from_numpy(_sort_keys(orc, kind, rows, rank * rows))
         out = distributed_sort(local, _np_partition, lambda t: torch.from_numpy(np.sort(t.numpy())),
                                samples_per_rank=256)
+        q.put((rank, len(out)))
         allg = gather_groups(out.view(1, -1))
         if rank == 0:
             q.put(allg.numpy()[0])
@@ -193,7 +202,7 @@ def test_distributed_join(world, how, orc):
     assert np.array_equal(got[0][o], wp) and np.array_equal(got[1][o], wb)
 
 
-@pytest.mark.parametrize("world,kind", [(2, 1), (3, 1), (2, 5)])
+@pytest.mark.parametrize("world,kind", [(2, 1), (3, 1), (2, 5), (2, "heavy"), (3, "heavy")])
 def test_sample_sort(world, kind, orc):
     n = 300_000 - (300_000 % world)
     ctx = mp.get_context("spawn")
@@ -202,10 +211,34 @@ def test_sample_sort(world, kind, orc):
     procs = [ctx.Process(target=_sort_worker, args=(r, world, port, n, kind, q)) for r in range(world)]
     for p in procs:
         p.start()
-    got = q.get(timeout=240)
+    msgs = [q.get(timeout=240) for _ in range(world + 1)]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    a, b = (0, 0) if kind == 1 else (-3, 7)
-    want = np.sort(orc.gen_column(kind, 0x50, n, a=a, b=b))
+    got = [m for m in msgs if not isinstance(m, tuple)][0]
+    sizes = dict(m for m in msgs if isinstance(m, tuple))
+    want = np.sort(_sort_keys(orc, kind, n, 0))
     assert np.array_equal(got, want)
+    if kind != 5:  # (kind 5 has only 7 distinct keys: ranges cannot balance finer than a key)
+        assert max(sizes.values()) <= 1.25 * n / world, sizes
+
+
+def test_sort_ranges_split_heavy_keys():
+    """sort_ranges (the restatement of csrc/dist.cpp's): a key filling several sample
+    quantiles is spread over their ranks; concatenating the ranks stays sorted."""
+    from nutdb_amd.dist import sort_ranges, split_counts
+    pool = [1] * 25 + [5] * 70 + [9] * 5  # P = 4: key 5 fills [25, 95) of the pool
+    spl = [pool[i * 100 // 4] for i in range(1, 4)]
+    assert spl == [5, 5, 5]
+    e, lo, hi, w = sort_ranges(spl, pool, 4)
+    assert e.tolist() == [5, 6] and lo == [0, 0, 3] and hi == [0, 3, 3]
+    assert w[1] == [0, 25, 25, 20]  # v's share of each rank's quantile range
+    assert split_counts([250, 700, 50], lo, w, 4) == [250, 250, 250, 250]
+    e, lo, hi, w = sort_ranges([1, 2, 9], [0, 1, 2, 9], 4)  # light keys get their own bucket too
+    assert e.tolist() == [1, 2, 3, 9, 10] and lo == [0, 0, 1, 2, 2, 3] and hi == [0, 1, 2, 2, 3, 3]
+    e, lo, hi, w = sort_ranges([2**63 - 1], [0, 2**63 - 1], 2)
+    assert e.tolist() == [2**63 - 1] and lo == [0, 0] and hi == [0, 1]
+    s = sorted(np.random.default_rng(1).integers(0, 40, 63).tolist())  # 64 ranks, many repeats
+    e, lo, hi, w = sort_ranges(s, s, 64)
+    assert len(e) <= 63 and all(np.diff(e) > 0)
+    assert all(a <= b for a, b in zip(lo, hi)) and all(h <= l2 for h, l2 in zip(hi, lo[1:]))

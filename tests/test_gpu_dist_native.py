@@ -145,6 +145,26 @@ def test_virtual_sample_sort(ND, orc, P):
             assert a[-1] <= b[0]
 
 
+@pytest.mark.parametrize("P,heavy", [(2, 0.5), (3, 0.5), (5, 0.5), (8, 0.9), (4, 1.0)])
+def test_virtual_sample_sort_heavy_key(ND, orc, P, heavy):
+    """Skew-safe ranges: a key holding half (or 90 %, or all) of the rows is
+    spread over the ranks whose quantile ranges it fills — the output stays globally
+    sorted and every rank stays near n / P keys."""
+    n = 2_000_003
+    k = orc.gen_column(1, 0x50, n)
+    rng = np.random.default_rng(P)
+    k[rng.random(n) < heavy] = -77
+    d = ND.virtual(P)
+    try:
+        outs = d.sort_i64([dev(k[a:b]) for a, b in shards(n, P)])
+        got = [o.cpu().numpy() for o in outs]
+    finally:
+        d.close()
+    assert np.array_equal(np.concatenate(got), np.sort(k))
+    sizes = [len(g) for g in got]
+    assert max(sizes) <= 1.15 * n / P, sizes
+
+
 def test_virtual_filter_offsets(ND, orc):
     n = 1_000_003
     col = orc.gen_column(0, 0x2A, n)

@@ -9,6 +9,10 @@ shapes themselves, not scaled-down stand-ins, checked against the C oracle.
 - config 3: GROUP BY key SUM(val) over 1e9 rows, G = 1000, dyadic values -> the f64 sums
   are exact, so the comparison is bit-exact.
 - config 4: the TPC-H Q1 shape over 1e9 rows (keys / counts exact, f64 sums <= 1e-12).
+- config 3 at large G (1e5 and 1e7 groups over 1e9 rows): the partitioned path the bench
+  times (direct key-hash partitioning, one level at 1e5 and two at 1e7, optimistic level
+  0), checked bit-exact against the indexed dense-array oracle (oracle.h
+  orc_groupby_pool_dyadic), which takes seconds at this size.
 
 Host memory: at most ~50 GB at a time (the Q1 columns), freed between tests.
 """
@@ -79,3 +83,26 @@ def test_q1_full_config4(ex, orc):
     assert np.array_equal(gw[:, 3], ow[:, 3])
     for j in range(3):
         assert rel_err(gw[:, j].view(np.float64), ow[:, j].view(np.float64)) <= F64_SUM_RTOL
+
+
+@pytest.mark.parametrize("G,levels", [(100_000, 1), (10_000_000, 2)])
+def test_groupby_full_config3_large_groups(ex, orc, G, levels):
+    from nutdb_amd import Agg, AggQuery
+    from nutdb_amd.workloads import gen, groupby_cols
+    n = 1_000_000_000
+    ks, vs = groupby_cols(G, dyadic=True)
+    key, val = gen(ex, ks, n), gen(ex, vs, n)
+    g = ex.groupby(AggQuery(keys=[key], values=[val], aggs=[Agg("sum", "col", (0,)), Agg("count"),
+                                                             Agg("min", "col", (0,)), Agg("max", "col", (0,))]),
+                   group_hint=G)
+    st = ex.groupby_stats()
+    gk, gw = g.to_host_words()
+    g.free()
+    del key, val
+    assert st == {"path": "partitioned_direct", "levels": levels, "optimistic": True}, st
+    ok, ow = orc.groupby_pool_dyadic(G, n, key_seed=ks[2], val_seed=vs[2])
+    gc.collect()
+    assert len(ok) == G
+    assert np.array_equal(gk, ok)
+    assert np.array_equal(gw, ow), "dyadic sums / counts / min / max must be bit-exact"
+    assert int(gw[:, 1].sum()) == n

@@ -1,6 +1,7 @@
 """GPU parity of the partitioned aggregation path (csrc/gpart.hpp): spill
--> hash partitions (one or two 8-bit levels) -> one workgroup per partition.  NUT_GP=1
-forces the path at test sizes, NUT_GP_LEVELS the partition levels; results must equal the
+-> hash partitions (one or two 8-bit levels) -> one workgroup per partition.  The context
+options gb_partition=1 / gb_levels force the path and its levels at test sizes (and every
+test checks nut_ctx_groupby_stats names that path); results must equal the
 oracle exactly as the on-chip path's do (f64 sums within F64_SUM_RTOL, exact for dyadic)."""
 import numpy as np
 import pytest
@@ -15,9 +16,8 @@ I64_MAX = np.iinfo(np.int64).max
 
 
 @pytest.fixture(params=[1, 2], ids=["levels1", "levels2"])
-def gp(request, monkeypatch):
-    monkeypatch.setenv("NUT_GP", "1")
-    monkeypatch.setenv("NUT_GP_LEVELS", str(request.param))
+def gp(request, opts):
+    opts(gb_partition=1, gb_levels=request.param)
     return request.param
 
 
@@ -28,6 +28,9 @@ def test_gp_cardinalities(ex, orc, gp, G, hint):
     key = orc.gen_column(2, 0x51, n, a=G)
     val = orc.gen_column(4, 0x52, n)
     g = ex.groupby(gb_query(dev(key, ex), dev(val, ex)), group_hint=hint)
+    st = ex.groupby_stats()
+    assert (st["path"], st["levels"]) == ("partitioned_direct", gp)
+    assert st["optimistic"] == (G >= 1000)  # one key holding every row overflows its partition
     ok, ow = orc.groupby([key], AGGS4, values=[val])
     assert len(g) == len(ok)
     check_vs_oracle(g, ok, ow, ["sum_f64", "i", "i", "i"])
@@ -39,6 +42,7 @@ def test_gp_dyadic_exact_and_predicate(ex, orc, gp):
     val = orc.gen_column(3, 0x52, n)  # dyadic: every sum exact
     preds = [(dev(val, ex), "<", 6000.0)]
     g = ex.groupby(gb_query(dev(key, ex), dev(val, ex), preds), group_hint=300_000)
+    assert ex.groupby_stats()["path"] == "partitioned_spill"
     ok, ow = orc.groupby([key], AGGS4, values=[val], preds=[(val, OPCODE["<"], 6000.0)])
     keys, words = g.to_host_words()
     assert np.array_equal(keys, ok) and np.array_equal(words, ow)
@@ -118,10 +122,10 @@ def test_gp_empty_and_all_rejected(ex, orc, gp):
     assert len(g) == 0
 
 
-def test_gp_table_growth(ex, orc, monkeypatch):
+def test_gp_table_growth(ex, orc, opts):
     """A hint far below the real group count: the partitioned pass grows the table and
     re-runs only the per-partition aggregation."""
-    monkeypatch.setenv("NUT_GP", "1")
+    opts(gb_partition=1)
     n = 2_000_000
     key = orc.gen_column(2, 0x51, n, a=500_000)
     val = orc.gen_column(4, 0x52, n)
@@ -132,14 +136,12 @@ def test_gp_table_growth(ex, orc, monkeypatch):
 
 @pytest.mark.parametrize("levels", ["1", "2"])
 @pytest.mark.parametrize("opt", ["0", "1"])
-def test_gp_optimistic_layout_and_fallback(ex, orc, monkeypatch, opt, levels):
-    """Direct partitioning whose first level has no histogram pass (NUT_GP_OPT=1, the
+def test_gp_optimistic_layout_and_fallback(ex, orc, opts, opt, levels):
+    """Direct partitioning whose first level has no histogram pass (gb_optimistic=1, the
     default): each of the 256 level-0 partitions owns twice its even share of rows.  Uniform keys fit; a heavy
     key (half the rows) overflows its partition, whose runs go to the scratch rows, and the
     level runs again with a histogram.  Both layouts equal the oracle bit for bit."""
-    monkeypatch.setenv("NUT_GP", "1")
-    monkeypatch.setenv("NUT_GP_LEVELS", levels)
-    monkeypatch.setenv("NUT_GP_OPT", opt)
+    opts(gb_partition=1, gb_levels=int(levels), gb_optimistic=int(opt))
     n = 3_000_017
     for heavy in (False, True):
         key = orc.gen_column(2, 0x61, n, a=100_000)
@@ -147,6 +149,9 @@ def test_gp_optimistic_layout_and_fallback(ex, orc, monkeypatch, opt, levels):
             key[::2] = 12345
         val = orc.gen_column(3, 0x62, n)  # dyadic: every sum exact
         g = ex.groupby(gb_query(dev(key, ex), dev(val, ex)), group_hint=100_000)
+        st = ex.groupby_stats()
+        assert st["path"] == "partitioned_direct" and st["levels"] == int(levels)
+        assert st["optimistic"] == (opt == "1" and not heavy)
         ok, ow = orc.groupby([key], AGGS4, values=[val])
         keys, words = g.to_host_words()
         assert np.array_equal(keys, ok) and np.array_equal(words, ow), heavy

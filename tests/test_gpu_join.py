@@ -494,3 +494,33 @@ def test_sql_left_join_chain(ex, orc):
     with pytest.raises(NutError, match="may only appear inside aggregates"):
         ex.sql("select n_region, count(*) from orders join customer on o_cust = c_key left join nation "
                "on c_nation = n_key group by n_region", on_dev(ex, orders), right=right[1:])
+
+
+def test_sql_join_order_by_unprojected_column(ex, orc):
+    """ORDER BY a column the SELECT list does not project, over an INNER join and over an
+    INNER chain: the key column is gathered through the join index like a projection
+    (it stayed bound to its source table and was read with joined-row ids).
+    The joined rows outnumber the source table, so a wrong binding would also read out of
+    range.  Ties keep the joined order (the sort is stable)."""
+    orders, lines = tables(21, 5_000, 40_000, miss=0.1)
+    j = joined(orc, lines, "l_okey", orders, "o_okey", "inner")
+    got = ex.sql("select l_qty, l_price from lineitem join orders on l_okey = o_okey order by o_cust, l_price",
+                 on_dev(ex, lines), right=on_dev(ex, orders))
+    o = np.lexsort((j.l_price.to_numpy(), j.o_cust.to_numpy()))
+    assert got["l_qty"].tolist() == j.l_qty.to_numpy()[o].tolist()
+    assert got["l_price"].tolist() == j.l_price.to_numpy()[o].tolist()
+    rng = np.random.default_rng(22)
+    cust = {"c_key": np.arange(50, dtype=np.int64), "c_nation": rng.integers(0, 8, 50).astype(np.int64)}
+    j["c_nation"] = cust["c_nation"][j.o_cust.to_numpy()]
+    got = ex.sql("select l_qty from lineitem join orders on l_okey = o_okey join customer on o_cust = c_key "
+                 "order by c_nation desc, l_qty limit 3000", on_dev(ex, lines),
+                 right=[on_dev(ex, orders), on_dev(ex, cust)])
+    o = np.lexsort((j.l_qty.to_numpy(), -j.c_nation.to_numpy()))
+    assert got["l_qty"].tolist() == j.l_qty.to_numpy()[o][:3000].tolist()
+    # a NULL-extended table's column may not order the rows (it would sort NULLs as 0)
+    with pytest.raises(NutError, match="may only appear inside aggregates"):
+        ex.sql("select o_okey from orders left join lineitem on o_okey = l_okey order by l_qty",
+               on_dev(ex, orders), right=on_dev(ex, lines))
+    with pytest.raises(NutError, match="may only appear inside aggregates"):
+        ex.sql("select o_okey from orders join customer on o_cust = c_key left join lineitem on o_okey = l_okey "
+               "order by l_qty", on_dev(ex, orders), right=[on_dev(ex, cust), on_dev(ex, lines)])

@@ -373,3 +373,26 @@ def test_join_chain_typed_tables(ex):
     with pytest.raises(NutError, match="string keys"):
         lineitem.sql("select count(*) from lineitem join orders on l_orderkey = o_orderkey "
                      "join customer on o_orderpriority = c_mktsegment", joined=[orders, customer])
+
+
+def test_join_string_columns_of_two_tables_rejected(ex):
+    """Each typed table has its own dictionary, so a String column of one table never
+    compares with one of another (USING (k, s) compared codes of two
+    dictionaries and returned wrong rows).  USING / ON / WHERE forms are rejected with a
+    message naming the cause; an integer USING key and strings against constants run."""
+    rng = np.random.default_rng(48)
+    n1, n2 = 500, 4000
+    t1 = Table(ex, "CREATE TABLE t1 (k Int64, s String, v Int64)")
+    t1.append(k=np.arange(n1, dtype=np.int64), s=np.array(["a", "b"], dtype=object)[rng.integers(0, 2, n1)],
+              v=rng.integers(0, 9, n1).astype(np.int64))
+    t2 = Table(ex, "CREATE TABLE t2 (k Int64, s String, w Int64)")
+    s2 = np.array(["b", "a", "c"], dtype=object)[rng.integers(0, 3, n2)]  # first-seen order differs
+    k2 = rng.integers(0, n1, n2).astype(np.int64)
+    t2.append(k=k2, s=s2, w=rng.integers(0, 9, n2).astype(np.int64))
+    for sql in ("select count(*) from t1 join t2 using (k, s)",
+                "select count(*) from t1 join t2 on t1.k = t2.k and t1.s = t2.s",
+                "select count(*) from t1 join t2 on t1.k = t2.k where t1.s = t2.s"):
+        with pytest.raises(NutError, match="dictionaries differ"):
+            t1.sql(sql, right=t2)
+    got = t1.sql("select count(*) as c from t1 join t2 using (k) where t2.s = 'c'", right=t2)
+    assert got["c"].tolist() == [int((s2 == "c").sum())]

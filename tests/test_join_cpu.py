@@ -85,7 +85,10 @@ def test_sql_no_join_has_no_join_key():
     ("select count(*) from a left semi join b using (x, y)", "INNER only"),
     ("select count(*) from a join b using (x) join c using (x)", "USING in a chain"),
     ("select count(*) from a join b on x = y full join c on y = z", "INNER and LEFT OUTER only"),
-    ("select count(*) from a join (select x from b) on x = y", "must be a table")])
+    ("select count(*) from a join (select x from b) on x = y", "must be a table"),
+    # FULL OUTER ... USING (u): an unqualified u would be COALESCE(a.u, b.u)
+    ("select count(u), sum(u) from a full outer join b using (u)", "FULL OUTER JOIN ... USING"),
+    ("select u, count(*) from a full join b using (u) group by u", "FULL OUTER JOIN ... USING")])
 def test_sql_join_rejections(sql, msg):
     from nutdb_amd import NutError
     from nutdb_amd.sql import Plan

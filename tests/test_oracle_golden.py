@@ -101,3 +101,20 @@ def test_groupby_i64_sum_wraps_and_minmax(orc):
     assert list(w[:, 1].view(np.int64)) == [5, np.iinfo(np.int64).min]
     assert list(w[:, 2].view(np.int64)) == [big, 9]
     assert list(w[:, 3].view(np.int64)) == [2, 3]
+
+
+@pytest.mark.parametrize("groups,n,row0", [(1, 1000, 0), (1000, 200_000, 0), (100_000, 2_000_000, 12345),
+                                           (3_000_000, 1_000_000, 7)])
+def test_groupby_pool_indexed_matches_hash_oracle(orc, groups, n, row0):
+    """The indexed dense-array oracle (the full-size config-3 checker, 1e9 rows x G up to
+    1e7) equals the hash-table oracle on the same generated columns — including G > n,
+    where some pool keys take no row and must be absent."""
+    from nutdb_amd.workloads import groupby_cols
+    ks, vs = groupby_cols(groups, dyadic=True)
+    key, val = orc.gen(ks, n, row0=row0), orc.gen(vs, n, row0=row0)
+    hk, hw = orc.groupby([key], [(0, 0, (0,)), (1, 0, ()), (2, 0, (0,)), (3, 0, (0,))], values=[val],
+                         cap=min(groups, n))
+    ik, iw = orc.groupby_pool_dyadic(groups, n, row0=row0, key_seed=ks[2], val_seed=vs[2])
+    assert np.array_equal(ik, hk)
+    assert np.array_equal(iw, hw)
+    assert int(iw[:, 1].sum()) == n
