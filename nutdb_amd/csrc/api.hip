@@ -250,6 +250,7 @@ void nut_ctx_destroy(nut_ctx *c) {
   (void)hipStreamSynchronize(c->stream);
   c->filter_state.release();
   c->sort_tmp.release();
+  c->sort_tmp2.release();
   c->sort_status.release();
   c->sort_meta.release();
   c->gp_data.release();

@@ -182,6 +182,7 @@ struct nut_ctx {
   hipStream_t stream = nullptr;
   nut::Scratch filter_state;  // tile counter + look-back status words
   nut::Scratch sort_tmp;      // sort ping-pong + histograms
+  nut::Scratch sort_tmp2;     // MSD sort, capped layout: the second level's regions
   nut::Scratch sort_status;   // radix-pass look-back granules, epoch-tagged (sort.hip)
   void *sort_status_seen = nullptr;
   size_t sort_status_clean = 0;

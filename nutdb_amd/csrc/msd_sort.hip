@@ -54,18 +54,23 @@ constexpr uint64_t LS_S_CAP = LS_S_THREADS * LS_S_ITEMS;
 constexpr uint64_t LS_M_CAP = LS_M_THREADS * LS_M_ITEMS;
 constexpr uint64_t LS_CAP = LS_L_THREADS * LS_L_ITEMS;
 
-// A contiguous run [start, start + count) of one of the three buffers.
+// A contiguous run [start, start + count) of one of the buffers.
+constexpr uint64_t kSameDst = ~0ull;
 struct MsSeg {
   uint64_t start, count;
-  uint32_t buf;  // 0: caller's input (raw int64: flip on load), 1: out, 2: tmp
+  uint32_t buf;  // 0: caller's input (raw int64: flip on load), 1: out, 2: tmp, 3: tmp2
   uint32_t aux;  // hist / scatter / copy: first tile of the segment; local sort: hi, the
                  // number of low bits of (key - base) its keys may still differ in
+  uint64_t dst = kSameDst;  // local sort / copy: where the sorted run goes in out
+                            // (kSameDst: at start — the exact layout)
 };
 struct MsBufs {
   const uint64_t *in;
   uint64_t *a;  // out
   uint64_t *b;  // tmp
+  uint64_t *c;  // tmp2 (the capped layout's second level)
 };
+__device__ __forceinline__ uint64_t ms_dst_off(const MsSeg &g) { return g.dst == kSameDst ? g.start : g.dst; }
 // The digit of a level: bits [shift, shift + log2(mask + 1)) of (key - base).  Every key
 // is >= base (the minimum, or 0), so (key - base) orders like key; subtracting the
 // minimum makes the first digit split a narrow key range (a sample-sort rank's) evenly.
@@ -77,7 +82,7 @@ struct MsDigit {
 };
 
 __device__ __forceinline__ const uint64_t *ms_src(const MsBufs &bf, uint32_t buf) {
-  return buf == 0 ? bf.in : (buf == 1 ? bf.a : bf.b);
+  return buf == 0 ? bf.in : (buf == 1 ? bf.a : (buf == 2 ? bf.b : bf.c));
 }
 
 // ---------------------------------------------------------------- level histogram
@@ -129,9 +134,15 @@ __global__ __launch_bounds__(MH_THREADS) void ms_hist_kernel(MsBufs bf, const Ms
 
 // ---------------------------------------------------------------- scatter level
 // Unstable partition of every listed segment by its digit into the other buffer (in /
-// tmp -> out ... see ms_dst).  cursor[s][d] starts at the absolute position of
-// sub-segment (s, d) and is advanced by one atomic per (tile, digit).
-__device__ __forceinline__ uint64_t *ms_dst(const MsBufs &bf, uint32_t buf) { return buf == 2 ? bf.a : bf.b; }
+// tmp -> out ... see ms_dst; dst_buf >= 0 overrides).  cursor[s][d] starts at the absolute
+// position of sub-segment (s, d) and is advanced by one atomic per (tile, digit).
+// Capped layout (ocap > 0, no histogram pass): sub-segment (s, d) owns the positions
+// [(s * MS_BINS + d) * ocap, + ocap); a run that would pass its end is not written and
+// sets *oflag (the host then sorts again with the exact layout).
+__device__ __forceinline__ uint64_t *ms_dst(const MsBufs &bf, uint32_t buf, int dst_buf) {
+  return dst_buf == 1 ? bf.a : dst_buf == 2 ? bf.b : dst_buf == 3 ? bf.c : (buf == 2 ? bf.a : bf.b);
+}
+constexpr uint64_t kSkipRun = ~0ull;
 
 // Persistent: workgroup b takes tiles b, b + grid, ...; the next tile's keys are loaded into
 // the key registers as soon as the current tile is staged in LDS, so its HBM latency hides
@@ -143,7 +154,9 @@ template <int H>
 __global__ __launch_bounds__(MS_THREADS) void ms_scatter_kernel(MsBufs bf, const MsSeg *__restrict__ segs,
                                                                    const uint32_t *__restrict__ tile_seg, uint32_t ntiles,
                                                                    MsDigit dg, uint64_t flip,
-                                                                   unsigned long long *__restrict__ cursor) {
+                                                                   unsigned long long *__restrict__ cursor,
+                                                                   int dst_buf = -1, uint64_t ocap = 0,
+                                                                   unsigned long long *__restrict__ oflag = nullptr) {
   constexpr int ITEMS = MS_ITEMS * H;
   constexpr uint32_t TILE = MS_TILE * H;
   static_assert(TILE <= 65536, "16-bit ranks");
@@ -171,7 +184,7 @@ __global__ __launch_bounds__(MS_THREADS) void ms_scatter_kernel(MsBufs bf, const
   for (;;) {
     const uint64_t lo = (uint64_t)(t - sg.aux) * TILE;
     const uint32_t cnt = (uint32_t)min<uint64_t>(TILE, sg.count - lo);
-    uint64_t *dst = ms_dst(bf, sg.buf);
+    uint64_t *dst = ms_dst(bf, sg.buf, dst_buf);
     const uint32_t next = t + gridDim.x;
     const uint32_t ns = next < ntiles ? tile_seg[next] : 0;
     if (tid < MS_BINS) s_cnt[tid] = 0;
@@ -204,7 +217,9 @@ __global__ __launch_bounds__(MS_THREADS) void ms_scatter_kernel(MsBufs bf, const
       const uint32_t tex = incl - c + add;
       s_tex[tid] = tex;
       const uint64_t gb = c ? (uint64_t)atomicAdd(&cursor[(uint64_t)s * MS_BINS + tid], (unsigned long long)c) : 0;
-      s_gb[tid] = gb - tex;  // out position of tile slot j of this digit = s_gb[d] + j
+      const bool over = ocap && c && gb + c > ((uint64_t)s * MS_BINS + tid + 1) * ocap;
+      if (over) atomicOr(oflag, 1ull);
+      s_gb[tid] = over ? kSkipRun : gb - tex;  // out position of tile slot j of this digit = s_gb[d] + j
     }
     __syncthreads();
     // rank -> tile slot, in place (16-bit pairs)
@@ -236,7 +251,8 @@ __global__ __launch_bounds__(MS_THREADS) void ms_scatter_kernel(MsBufs bf, const
         const uint32_t j = (uint32_t)i * MS_THREADS + tid, jj = j + (uint32_t)h * MS_TILE;
         if (jj < cnt) {
           const uint64_t k = s_keys[j];
-          dst[s_gb[dg(k)] + jj] = k;  // (non-temporal stores measured 2.4 ms slower per sort)
+          const uint64_t g = s_gb[dg(k)];
+          if (g != kSkipRun) dst[g + jj] = k;  // (non-temporal stores measured 2.4 ms slower per sort)
         }
       }
     }
@@ -289,6 +305,54 @@ __global__ __launch_bounds__(MS_BINS) void ms_plan_kernel(const MsSeg *__restric
     b = __shfl(b, leader, 64);
     if (cls == k) lists[(uint64_t)k * cap + b + lane_rank(m)] = MsSeg{start, c, sg.buf == 2 ? 1u : 2u, (uint32_t)hi};
   }
+}
+
+// Capped layout's plan (no histogram pass): after the second capped level, one block per
+// first-level segment s, one thread per digit d: the sub-segment's count is its cursor's
+// advance over its region start; the exclusive scan over d plus the first-level segment's
+// place in out (dbase[s], exact: its count is the first level's cursor advance) gives
+// where the sorted run goes.  Lists by local-sort class as ms_plan_kernel; a sub-segment
+// too large for every class sets *oflag (the host sorts again with the exact layout).
+__global__ __launch_bounds__(MS_BINS) void ms_plan_capped_kernel(const unsigned long long *__restrict__ cursor,
+                                                                 const uint64_t *__restrict__ dbase, uint64_t ocap,
+                                                                 int hi, MsSeg *__restrict__ lists, uint64_t cap,
+                                                                 unsigned int *__restrict__ counts,
+                                                                 unsigned long long *__restrict__ oflag) {
+  __shared__ unsigned long long s_wsum[MS_BINS / kWave];
+  const int d = threadIdx.x, lane = d & 63, wave = d >> 6;
+  const uint64_t r = (uint64_t)blockIdx.x * MS_BINS + d, start = r * ocap;
+  const uint64_t c = cursor[r] - start;
+  uint64_t incl = c;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint64_t y = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += y;
+  }
+  if (lane == 63) s_wsum[wave] = incl;
+  __syncthreads();
+  uint64_t add = 0;
+#pragma unroll
+  for (int w = 0; w < MS_BINS / kWave; ++w) add += (w < wave) ? s_wsum[w] : 0ull;
+  const uint64_t dst = dbase[blockIdx.x] + incl - c + add;
+  const int cls = c == 0 ? -1 : (c <= LS_S_CAP ? 0 : (c <= LS_M_CAP ? 1 : (c <= LS_CAP ? 2 : 3)));
+  if (cls == 3) atomicOr(oflag, 1ull);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const uint64_t m = __ballot(cls == k);
+    if (!m) continue;
+    const int leader = __builtin_ctzll(m);
+    unsigned int b = 0;
+    if (lane == leader) b = atomicAdd(&counts[k], (unsigned int)__popcll(m));
+    b = __shfl(b, leader, 64);
+    if (cls == k) lists[(uint64_t)k * cap + b + lane_rank(m)] = MsSeg{start, c, 3u, (uint32_t)hi, dst};
+  }
+}
+
+// strided sample of the (flipped) input for the capped layout's admission check
+__global__ void ms_sample_kernel(const uint64_t *__restrict__ in, uint64_t n, uint64_t flip, uint32_t m,
+                                 uint64_t *__restrict__ out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < m) out[i] = in[(uint64_t)(((unsigned __int128)i * n) / m)] ^ flip;
 }
 
 // ---------------------------------------------------------------- local sort
@@ -567,7 +631,7 @@ __global__ __launch_bounds__(THREADS, 4) void ms_local_kernel(MsBufs bf, const M
   const int hi = (int)sg.aux;
   const uint32_t K = (c + THREADS - 1) / THREADS;
   const uint32_t pw = (uint32_t)wave * kWave * K + lane;
-  uint64_t *dst = bf.a + sg.start;
+  uint64_t *dst = bf.a + ms_dst_off(sg);
   if (hi == 0) {  // every key equal: copy
 #pragma unroll
     for (int i = 0; i < MAXK; ++i) {
@@ -780,7 +844,7 @@ __global__ __launch_bounds__(THREADS) void ms_lsd_kernel(MsBufs bf, const MsSeg 
   const uint32_t K = (c + THREADS - 1) / THREADS;
   const uint32_t pw = (uint32_t)wave * kWave * K + lane;
   const uint64_t *src = ms_src(bf, sg.buf) + sg.start;
-  uint64_t *dst = bf.a + sg.start;
+  uint64_t *dst = bf.a + ms_dst_off(sg);
   const uint64_t f = sg.buf == 0 ? flip : 0;
   uint32_t lo[MAXK], hi[MAXK], pos[MAXK];
 #pragma unroll
@@ -874,7 +938,7 @@ __global__ __launch_bounds__(MH_THREADS) void ms_copy_kernel(MsBufs bf, const Ms
   const uint64_t lo = (uint64_t)(blockIdx.x - sg.aux) * MH_TILE;
   const uint32_t cnt = (uint32_t)min<uint64_t>(MH_TILE, sg.count - lo);
   const uint64_t *src = ms_src(bf, sg.buf) + sg.start + lo;
-  uint64_t *dst = bf.a + sg.start + lo;
+  uint64_t *dst = bf.a + ms_dst_off(sg) + lo;
   const uint64_t f = sg.buf == 0 ? 0 : flip;  // the caller's input is not flipped
   for (uint32_t i = threadIdx.x; i < cnt; i += MH_THREADS) dst[i] = src[i] ^ f;
 }
@@ -1060,15 +1124,143 @@ static nut_status device_level(nut_ctx *c, MetaArena &ar, const MsBufs &bf, cons
   return NUT_OK;
 }
 
+constexpr uint64_t kCappedMin = 1ull << 25;  // smaller inputs: the exact layout (its passes are short)
+
+// Capped two-level layout: large inputs whose two top 9-bit digits look
+// uniform in a strided sample skip both histogram passes.  Level 0 scatters `in` by the top
+// digit into 512 regions of ocap0 rows of tmp (about 1.1 x an even share each); level 1
+// scatters every region by the next digit into 512 regions of ocap1 rows of tmp2; the local
+// sorts read those regions and write each sorted run to its exact place in out, found by a
+// scan of the level-1 cursors (ms_plan_capped_kernel).  48 B/key instead of 64.  A region
+// overflow (a key distribution the sample did not show) or a sub-segment too large for a
+// local sort returns NUT_ERR_CAPACITY without a message: the caller sorts again with the
+// exact layout (`in` is never written).
+static nut_status msd_sort_capped(nut_ctx *c, const int64_t *in, int64_t *out, uint64_t n, uint64_t flip) {
+  hipStream_t st = c->stream;
+  constexpr uint32_t kSample = 16384;
+  MetaArena ar{c};
+  nut_status s = ar.begin(MetaArena::align(kSample * 8) + 1024);
+  if (s) return s;
+  uint64_t *dsamp = (uint64_t *)ar.alloc(kSample * 8);
+  hipLaunchKernelGGL(ms_sample_kernel, dim3(kSample / 256), dim3(256), 0, st, (const uint64_t *)in, n, flip, kSample,
+                     dsamp);
+  NUT_HIP(hipGetLastError());
+  std::vector<uint64_t> samp(kSample);
+  NUT_HIP(hipMemcpyAsync(samp.data(), dsamp, kSample * 8, hipMemcpyDeviceToHost, st));
+  NUT_HIP(hipStreamSynchronize(st));
+  {  // admission: no digit value holds more than twice its share of the sample
+    std::vector<uint32_t> h0(MS_BINS, 0), h1(MS_BINS, 0);
+    for (uint64_t k : samp) {
+      ++h0[k >> (64 - MS_BITS)];
+      ++h1[(k >> (64 - 2 * MS_BITS)) & (MS_BINS - 1)];
+    }
+    const uint32_t lim = 2 * kSample / MS_BINS;
+    for (int d = 0; d < MS_BINS; ++d)
+      if (h0[d] > lim || h1[d] > lim) return NUT_ERR_CAPACITY;
+  }
+  // ---- level 0: in -> tmp, 512 capped regions
+  const uint64_t ocap0 = ((n / MS_BINS) * 11 / 10 + 2 * MS_TILE + 31) & ~31ull;
+  s = c->sort_tmp.reserve((size_t)MS_BINS * ocap0 * 8);
+  if (s) return s;
+  const MsBufs bf0{(const uint64_t *)in, (uint64_t *)out, (uint64_t *)c->sort_tmp.ptr, nullptr};
+  std::vector<MsSeg> one{MsSeg{0, n, 0, 0}};
+  std::vector<uint32_t> tiles;
+  const uint64_t nt0 = tile_table(one, MS_TILE * ms_halves(), tiles);
+  if (nt0 > 0x7FFFFFFFull) return fail(NUT_ERR_UNSUPPORTED, "nut_sort_i64: too many tiles");
+  std::vector<uint64_t> cur0(MS_BINS + 1, 0);
+  for (int d = 0; d < MS_BINS; ++d) cur0[d] = (uint64_t)d * ocap0;
+  s = ar.begin(MetaArena::align(sizeof(MsSeg)) + MetaArena::align(tiles.size() * 4) +
+               MetaArena::align(cur0.size() * 8));
+  if (s) return s;
+  MsSeg *dseg;
+  uint32_t *dtile;
+  uint64_t *dcur0;
+  if ((s = ar.upload(one, &dseg)) || (s = ar.upload(tiles, &dtile)) || (s = ar.upload(cur0, &dcur0))) return s;
+  const MsDigit dg0{0, 64 - MS_BITS, (uint32_t)MS_BINS - 1};
+  hipLaunchKernelGGL(ms_scatter_kernel<ms_halves()>, dim3((unsigned)std::min<uint64_t>(nt0, (uint64_t)c->num_cus)),
+                     dim3(MS_THREADS), 0, st, bf0, (const MsSeg *)dseg, (const uint32_t *)dtile, (uint32_t)nt0, dg0,
+                     flip, (unsigned long long *)dcur0, 2, ocap0, (unsigned long long *)(dcur0 + MS_BINS));
+  NUT_HIP(hipGetLastError());
+  std::vector<uint64_t> end0(MS_BINS + 1);
+  NUT_HIP(hipMemcpyAsync(end0.data(), dcur0, end0.size() * 8, hipMemcpyDeviceToHost, st));
+  NUT_HIP(hipStreamSynchronize(st));
+  if (end0[MS_BINS]) return NUT_ERR_CAPACITY;
+  // ---- level 1: each region -> 512 capped regions of tmp2
+  std::vector<MsSeg> segs(MS_BINS);
+  std::vector<uint64_t> dbase(MS_BINS);
+  uint64_t cmax = 0, run = 0;
+  for (int d = 0; d < MS_BINS; ++d) {
+    const uint64_t cnt = end0[d] - cur0[d];
+    segs[d] = MsSeg{cur0[d], cnt, 2, 0};
+    dbase[d] = run;
+    run += cnt;
+    cmax = std::max(cmax, cnt);
+  }
+  const uint64_t ocap1 = ((cmax / MS_BINS) * 23 / 20 + 64 + 1) & ~1ull;
+  s = c->sort_tmp2.reserve((size_t)MS_BINS * MS_BINS * ocap1 * 8);
+  if (s) return s;
+  const MsBufs bf{(const uint64_t *)in, (uint64_t *)out, (uint64_t *)c->sort_tmp.ptr, (uint64_t *)c->sort_tmp2.ptr};
+  const uint64_t nt1 = tile_table(segs, MS_TILE * ms_halves(), tiles);
+  if (nt1 > 0x7FFFFFFFull) return fail(NUT_ERR_UNSUPPORTED, "nut_sort_i64: too many tiles");
+  const uint64_t nr = (uint64_t)MS_BINS * MS_BINS, lcap = nr;
+  std::vector<uint64_t> cur1(nr + 1, 0);
+  for (uint64_t r = 0; r < nr; ++r) cur1[r] = r * ocap1;
+  s = ar.begin(MetaArena::align(segs.size() * sizeof(MsSeg)) + MetaArena::align(tiles.size() * 4) +
+               MetaArena::align(cur1.size() * 8) + MetaArena::align(dbase.size() * 8) +
+               MetaArena::align(3 * lcap * sizeof(MsSeg)) + 3 * MetaArena::align((lcap + 1) * 4) + 1024);
+  if (s) return s;
+  MsSeg *dsegs;
+  uint32_t *dt1;
+  uint64_t *dcur1, *ddb;
+  if ((s = ar.upload(segs, &dsegs)) || (s = ar.upload(tiles, &dt1)) || (s = ar.upload(cur1, &dcur1)) ||
+      (s = ar.upload(dbase, &ddb)))
+    return s;
+  MsSeg *lists = (MsSeg *)ar.alloc(3 * lcap * sizeof(MsSeg));
+  unsigned int *counts = (unsigned int *)ar.alloc(16);
+  uint32_t *fb[3];
+  for (auto &f : fb) f = (uint32_t *)ar.alloc((lcap + 1) * 4);
+  NUT_HIP(hipMemsetAsync(counts, 0, 16, st));
+  const MsDigit dg1{0, 64 - 2 * MS_BITS, (uint32_t)MS_BINS - 1};
+  hipLaunchKernelGGL(ms_scatter_kernel<ms_halves()>, dim3((unsigned)std::min<uint64_t>(nt1, (uint64_t)c->num_cus)),
+                     dim3(MS_THREADS), 0, st, bf, (const MsSeg *)dsegs, (const uint32_t *)dt1, (uint32_t)nt1, dg1, flip,
+                     (unsigned long long *)dcur1, 3, ocap1, (unsigned long long *)(dcur1 + nr));
+  hipLaunchKernelGGL(ms_plan_capped_kernel, dim3(MS_BINS), dim3(MS_BINS), 0, st, (const unsigned long long *)dcur1,
+                     (const uint64_t *)ddb, ocap1, 64 - 2 * MS_BITS, lists, lcap, counts,
+                     (unsigned long long *)(dcur1 + nr));
+  NUT_HIP(hipGetLastError());
+  uint64_t *hc = c->host_pinned;
+  NUT_HIP(hipMemcpyAsync(hc, counts, 16, hipMemcpyDeviceToHost, st));
+  NUT_HIP(hipMemcpyAsync(hc + 2, dcur1 + nr, 8, hipMemcpyDeviceToHost, st));
+  NUT_HIP(hipStreamSynchronize(st));
+  if (hc[2]) return NUT_ERR_CAPACITY;
+  const uint32_t *cnt = (const uint32_t *)hc;
+  const uint32_t ncls[3] = {cnt[0], cnt[1], cnt[2]};
+  for (int cls = 2; cls >= 0; --cls)
+    if ((s = launch_local_dev(c, bf, 0, flip, lists + (uint64_t)cls * lcap, ncls[cls], fb[cls], cls))) return s;
+  c->sort_bytes = 48 * n;
+  c->sort_levels = 2;
+  return NUT_OK;
+}
+
 nut_status msd_sort_i64(nut_ctx *c, const int64_t *in, int64_t *out, uint64_t n, uint64_t flip) {
   hipStream_t st = c->stream;
-  nut_status s = c->sort_tmp.reserve(n * 8);
-  if (s) return s;
-  const MsBufs bf{(const uint64_t *)in, (uint64_t *)out, (uint64_t *)c->sort_tmp.ptr};
-  MetaArena ar{c};
   c->sort_bytes = 0;
   c->sort_levels = 0;
   c->timer.begin(st, NUT_KERNEL_SORT);
+  if (n >= kCappedMin) {
+    nut_status s = msd_sort_capped(c, in, out, n, flip);
+    if (s != NUT_ERR_CAPACITY) {
+      c->timer.end(st);
+      if (!s) NUT_HIP(hipStreamSynchronize(st));
+      return s;
+    }
+    c->sort_bytes = 0;  // a skewed distribution: the exact layout below
+    c->sort_levels = 0;
+  }
+  nut_status s = c->sort_tmp.reserve(n * 8);
+  if (s) return s;
+  const MsBufs bf{(const uint64_t *)in, (uint64_t *)out, (uint64_t *)c->sort_tmp.ptr, nullptr};
+  MetaArena ar{c};
 
   if (n <= LS_CAP) {  // one workgroup, all 64 bits
     std::vector<MsSeg> one{{0, n, 0, 64}};

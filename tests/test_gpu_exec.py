@@ -510,3 +510,39 @@ def test_sort_deep_levels(ex, orc, kind):
     assert orc.multiset_hash(o) == orc.multiset_hash(v)
     if kind != "cluster":
         assert np.array_equal(o, np.sort(v))
+
+
+@pytest.mark.parametrize("n,desc", [(1 << 25, False), (40_000_003, False), (40_000_003, True)])
+def test_sort_capped_layout(ex, orc, n, desc):
+    """Large full-range inputs take the capped two-level layout (no histogram pass: both
+    scatter levels write into regions of ~1.1x their even share, the local sorts place each
+    run by a scan of the level-1 cursors): 48 B/key, bit-exact."""
+    col = orc.gen_column(1, 0x57, n)
+    got = host(ex.sort_i64(dev(col, ex), descending=desc))
+    nbytes, levels = ex.sort_stats()
+    assert (nbytes, levels) == (48 * n, 2)
+    want = orc.sort_i64(col)
+    assert np.array_equal(got, want[::-1] if desc else want)
+
+
+@pytest.mark.parametrize("kind", ["unsampled_skew", "second_digit_skew", "narrow"])
+def test_sort_capped_fallback(ex, orc, kind):
+    """Inputs the capped layout cannot hold fall back to the exact layout and still sort
+    bit-exact: a skew the admission sample does not see (every sampled key random, every
+    other key one value) overflows a level-0 region at run time; a second digit that takes
+    few values, and a narrow range, are refused by the sample."""
+    n = 1 << 25
+    rng = np.random.default_rng(5)
+    v = rng.integers(I64_MIN, I64_MAX, n, dtype=np.int64)
+    if kind == "unsampled_skew":
+        keep = np.zeros(n, dtype=bool)
+        keep[(np.arange(16384, dtype=np.int64) * n) // 16384] = True
+        v[~keep] = 77
+    elif kind == "second_digit_skew":
+        v = (v & ~np.int64(0x7FC00000000000)) | (np.int64(3) << 46)
+    else:
+        v = rng.integers(0, 1 << 40, n, dtype=np.int64)
+    got = host(ex.sort_i64(dev(v, ex)))
+    nbytes, _ = ex.sort_stats()
+    assert nbytes != 48 * n
+    assert np.array_equal(got, np.sort(v))
