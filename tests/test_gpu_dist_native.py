@@ -257,3 +257,27 @@ def test_c_host_without_torch():
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "host_q1 OK" in r.stdout
+
+
+@pytest.mark.parametrize("mode", ["rank", "virtual"])
+def test_rccl_single_rank_large_sort_filter_join(ND, orc, mode):
+    """One rank through the library's exchange at bench-like sizes (1e8 keys, 0.8 GB through
+    the all-to-all): the sort's received range, the sort statistics (full-range keys take the
+    capped two-level layout: 48 B/key) and the join's global pairs."""
+    n = 100_000_003
+    ks = orc.gen_column(1, 0x50, n)
+    d = ND.create_rank(1, 0, ND.unique_id(), 0) if mode == "rank" else ND.virtual(1)
+    try:
+        s = d.sort_i64([dev(ks)])[0].cpu().numpy()
+        nbytes, levels = d.sort_stats()
+        assert np.array_equal(s, np.sort(ks))
+        assert (nbytes, levels) == (48 * n, 2)
+        b = orc.gen_column(0, 0x71, 2_000_000)
+        p = np.where(ks[:8_000_000] % 10 == 0, ks[:8_000_000] | (1 << 62), b[ks[:8_000_000] % 2_000_000])
+        pi, bi = d.join_i64([dev(b)], [dev(p)], "inner")[0]
+        pi, bi = pi.cpu().numpy(), bi.cpu().numpy()
+        o = np.lexsort((bi, pi))
+        wp, wb = orc.join_i64(b, p, "inner")
+        assert np.array_equal(pi[o], wp) and np.array_equal(bi[o], wb)
+    finally:
+        d.close()
