@@ -157,15 +157,45 @@ nut_status allgather(nut_dist *d, int l, const uint64_t *send, uint64_t *recv, s
   return e == hipSuccess ? NUT_OK : hip_fail(e, "nut_dist (virtual) all-gather");
 }
 
-// all-to-all of variable segments (words): segment q of send goes to rank q
+// RCCL all-to-all rounds move at most this many words per (sender, receiver) pair: a
+// single-rank ncclAllToAllv of 2e8 words (1.6 GB) returned wrong data on this image while
+// 1e8 words were exact (scripts/diag/dist_sort_pieces.py), so large exchanges go in rounds
+constexpr size_t kA2AChunk = size_t(1) << 26;
+
+// the largest (sender, receiver) cell of an all-gathered count matrix: rank q's count for
+// receiver r at all[q * w + off + r], times `mul` words per count
+size_t max_cell(const std::vector<uint64_t> &all, size_t w, size_t off, int P, size_t mul) {
+  uint64_t m = 0;
+  for (int q = 0; q < P; ++q)
+    for (int r = 0; r < P; ++r) m = std::max<uint64_t>(m, all[(size_t)q * w + off + r]);
+  return (size_t)m * mul;
+}
+
+// all-to-all of variable segments (words): segment q of send goes to rank q.  gmax = the
+// largest segment any rank sends to any rank (every rank passes the same value).
 nut_status alltoallv(nut_dist *d, int l, const uint64_t *send, const size_t *sc, const size_t *sd, uint64_t *recv,
-                     const size_t *rc, const size_t *rd) {
+                     const size_t *rc, const size_t *rd, size_t gmax) {
   Member &mb = d->m[l];
   hipStream_t s = mb.ctx->stream;
   if (d->mode != nut_dist::kVirtual) {
-    ncclResult_t e = d->r->all_to_allv(send, sc, sd, recv, rc, rd, ncclUint64, mb.comm, s);
-    (void)hipGetLastError();
-    return e == ncclSuccess ? NUT_OK : rccl_fail(d->r, e, "ncclAllToAllv");
+    const int P = d->nranks;
+    const size_t rounds = std::max<size_t>(1, (gmax + kA2AChunk - 1) / kA2AChunk);
+    std::vector<size_t> c1(P), d1(P), c2(P), d2(P);
+    for (size_t k = 0; k < rounds; ++k) {
+      const size_t o = k * kA2AChunk;
+      for (int q = 0; q < P; ++q) {
+        c1[q] = sc[q] > o ? std::min(kA2AChunk, sc[q] - o) : 0;
+        d1[q] = sd[q] + o;
+        c2[q] = rc[q] > o ? std::min(kA2AChunk, rc[q] - o) : 0;
+        d2[q] = rd[q] + o;
+      }
+      ncclResult_t e = rounds == 1 ? d->r->all_to_allv(send, sc, sd, recv, rc, rd, ncclUint64, mb.comm, s)
+                                   : d->r->all_to_allv(send, c1.data(), d1.data(), recv, c2.data(), d2.data(), ncclUint64,
+                                                       mb.comm, s);
+      (void)hipGetLastError();
+      if (e != ncclSuccess) return rccl_fail(d->r, e, "ncclAllToAllv");
+    }
+    return NUT_OK;
   }
   Hub &h = d->hub;
   const int me = mb.rank;
@@ -319,7 +349,9 @@ nut_status groupby_member(nut_dist *d, int l, const nut_agg_spec *spec, uint64_t
     rtot += rc[q];
   }
   st = agree(d, l, reserve(mb, 1, rtot));
-  if (!st) st = alltoallv(d, l, buf(mb, 0), sc.data(), sd.data(), buf(mb, 1), rc.data(), rd.data());
+  if (!st)
+    st = alltoallv(d, l, buf(mb, 0), sc.data(), sd.data(), buf(mb, 1), rc.data(), rd.data(),
+                   max_cell(all, 2 + (size_t)P, 2, P, (size_t)W));
   // 3. the owner merges what it received
   nut_groups *own = nullptr;
   nut_prog_node nodes[NUT_MAX_AGGS];
@@ -352,7 +384,9 @@ nut_status groupby_member(nut_dist *d, int l, const nut_agg_spec *spec, uint64_t
     if (me != 0) sc[0] = (size_t)W * n_own;
     st = agree(d, l, reserve(mb, 1, rtot));
   }
-  if (!st) st = alltoallv(d, l, buf(mb, 0), sc.data(), sd.data(), buf(mb, 1), rc.data(), rd.data());
+  size_t gmax = 0;
+  for (int q = 0; q < P && !st; ++q) gmax = std::max<size_t>(gmax, (size_t)W * all[(size_t)q * 2 + 1]);
+  if (!st) st = alltoallv(d, l, buf(mb, 0), sc.data(), sd.data(), buf(mb, 1), rc.data(), rd.data(), gmax);
   if (!st && me == 0) {
     for (int q = 1; q < P && !st; ++q) {
       const uint64_t cq = rc[q] / W;
@@ -520,7 +554,9 @@ nut_status sort_member(nut_dist *d, int l, const int64_t *in, uint64_t n, const 
   if (!st) st = reserve(mb, 2, rtot);
   st = agree(d, l, st);
   // 3. one all-to-all of keys, then the local radix sort of the received range
-  if (!st) st = alltoallv(d, l, buf(mb, 0), sc.data(), sd.data(), buf(mb, 1), rc.data(), rd.data());
+  if (!st)
+    st = alltoallv(d, l, buf(mb, 0), sc.data(), sd.data(), buf(mb, 1), rc.data(), rd.data(),
+                   max_cell(all, 1 + (size_t)P, 1, P, 1));
   if (!st) st = nut_sort_i64(c, (const int64_t *)buf(mb, 1), (int64_t *)buf(mb, 2), rtot);
   if (!st) st = nut_ctx_sync(c);
   if (st) return st;
@@ -579,10 +615,11 @@ nut_status join_member(nut_dist *d, int l, const int64_t *build, uint64_t nb, in
   if (!st) st = reserve(mb, 6, pr);
   if (!st) st = reserve(mb, 7, pr);
   st = agree(d, l, st);
-  if (!st) st = alltoallv(d, l, buf(mb, 0), bsc.data(), bsd.data(), buf(mb, 4), brc.data(), brd.data());
-  if (!st) st = alltoallv(d, l, buf(mb, 1), bsc.data(), bsd.data(), buf(mb, 5), brc.data(), brd.data());
-  if (!st) st = alltoallv(d, l, buf(mb, 2), psc.data(), psd.data(), buf(mb, 6), prc.data(), prd.data());
-  if (!st) st = alltoallv(d, l, buf(mb, 3), psc.data(), psd.data(), buf(mb, 7), prc.data(), prd.data());
+  const size_t bmax = max_cell(all, w, 1, P, 1), pmax = max_cell(all, w, 1 + (size_t)P, P, 1);
+  if (!st) st = alltoallv(d, l, buf(mb, 0), bsc.data(), bsd.data(), buf(mb, 4), brc.data(), brd.data(), bmax);
+  if (!st) st = alltoallv(d, l, buf(mb, 1), bsc.data(), bsd.data(), buf(mb, 5), brc.data(), brd.data(), bmax);
+  if (!st) st = alltoallv(d, l, buf(mb, 2), psc.data(), psd.data(), buf(mb, 6), prc.data(), prd.data(), pmax);
+  if (!st) st = alltoallv(d, l, buf(mb, 3), psc.data(), psd.data(), buf(mb, 7), prc.data(), prd.data(), pmax);
   if (st) return st;
   // local join of what this rank owns; local pair indices -> global rows
   nut_join *j = nullptr;

@@ -485,20 +485,22 @@ __device__ int g_ms_stop;  // msd_tune only: 1 load, 3 + ranks/scans/LDS, 4 + wi
 #define MS_STOP(k) false
 #endif
 
-template <int THREADS, int MAXK>
+// SB_ / WS_ = 0: the product defaults (bucket bits by capacity, window stride LS_WS)
+template <int THREADS, int MAXK, int SB_ = 0, int WS_ = 0>
 struct LocalCfg {
   static constexpr int WAVES = THREADS / kWave;
   static constexpr int CAP = THREADS * MAXK;
   static constexpr int LDS_KEYS = CAP < 16384 ? CAP : 16384;  // 8-B keys per round
-  static constexpr int SB = CAP > 8192 ? 12 : (CAP > 2048 ? 11 : 9);  // bucket bits: ~4-6 keys each
+  static constexpr int SB = SB_ ? SB_ : (CAP > 8192 ? 12 : (CAP > 2048 ? 11 : 9));  // bucket bits: ~4-6 keys each
+  static constexpr int WS = WS_ ? WS_ : LS_WS;
   static constexpr int NB = 1 << SB;
   static constexpr int BPT = NB / THREADS;  // buckets per thread in the scan
-  static_assert(BPT * THREADS == NB && BPT <= 4, "whole buckets per thread");
+  static_assert(BPT * THREADS == NB && BPT <= 8, "whole buckets per thread");
   static_assert(CAP <= 2 * LDS_KEYS, "at most two rounds");
-  static constexpr int WPT = (CAP / LS_WS + THREADS - 1) / THREADS;  // windows per thread
+  static constexpr int WPT = (CAP / WS + THREADS - 1) / THREADS;  // windows per thread
   static_assert(WPT <= 2, "at most two windows per thread");
   // LDS: one round of 8-B keys, bucket counts -> starts, window starts, scan words
-  static constexpr int NWIN = CAP / LS_WS + 2;  // window table entries (+ end)
+  static constexpr int NWIN = CAP / WS + 2;  // window table entries (+ end)
   static constexpr int BYTES = LDS_KEYS * 8 + ((NB + 1) + NWIN + 16 + 2) * 4;
 };
 
@@ -596,11 +598,11 @@ __device__ __forceinline__ void wave_bitonic32_multi(uint64_t (&v)[NR], int lane
   cx64<1, 1, NR>(v, lane);
 }
 
-template <int THREADS, int MAXK, bool PREFETCH>
+template <int THREADS, int MAXK, bool PREFETCH, int SB_ = 0, int WS_ = 0>
 __global__ __launch_bounds__(THREADS, 4) void ms_local_kernel(MsBufs bf, const MsSeg *__restrict__ segs, uint32_t nseg,
                                                            uint64_t base, uint64_t flip, uint32_t *__restrict__ fb) {
-  using C = LocalCfg<THREADS, MAXK>;
-  constexpr int WAVES = C::WAVES, NB = C::NB, SB = C::SB;
+  using C = LocalCfg<THREADS, MAXK, SB_, WS_>;
+  constexpr int WAVES = C::WAVES, NB = C::NB, SB = C::SB, LS_WS = C::WS;
   __shared__ __attribute__((aligned(16))) char lds[C::BYTES];
   uint64_t *s_keys = (uint64_t *)lds;
   uint32_t *s_off = (uint32_t *)(lds + C::LDS_KEYS * 8);  // [NB + 1] bucket counts -> starts, then c

@@ -261,10 +261,12 @@ def test_c_host_without_torch():
 
 @pytest.mark.parametrize("mode", ["rank", "virtual"])
 def test_rccl_single_rank_large_sort_filter_join(ND, orc, mode):
-    """One rank through the library's exchange at bench-like sizes (1e8 keys, 0.8 GB through
-    the all-to-all): the sort's received range, the sort statistics (full-range keys take the
-    capped two-level layout: 48 B/key) and the join's global pairs."""
-    n = 100_000_003
+    """One rank through the library's exchange at bench-like sizes (2e8 keys, 1.6 GB through
+    the all-to-all — one ncclAllToAllv of that size returned wrong data on this image, so the
+    library moves large exchanges in rounds of <= 2^26 words per pair): the sort's received
+    range, the sort statistics (full-range keys take the capped two-level layout: 48 B/key)
+    and the join's global pairs."""
+    n = 200_000_003
     ks = orc.gen_column(1, 0x50, n)
     d = ND.create_rank(1, 0, ND.unique_id(), 0) if mode == "rank" else ND.virtual(1)
     try:
