@@ -29,6 +29,7 @@
 // back on the final store.
 #include <algorithm>
 #include <cstdlib>
+#include <utility>
 #include <vector>
 
 #include "common.hpp"
@@ -168,7 +169,7 @@ __global__ __launch_bounds__(MS_THREADS) void ms_scatter_kernel(MsBufs bf, const
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   uint32_t t = blockIdx.x;
   uint64_t key[ITEMS];
-  auto load = [&](uint32_t tt, const MsSeg &g) {
+  auto load = [&](uint32_t tt, const MsSeg g) {
     const uint64_t lo = (uint64_t)(tt - g.aux) * TILE;
     const uint32_t cn = (uint32_t)min<uint64_t>(TILE, g.count - lo);
     const uint64_t *sp = ms_src(bf, g.buf) + g.start + lo;
@@ -484,6 +485,21 @@ __device__ int g_ms_stop;  // msd_tune only: 1 load, 3 + ranks/scans/LDS, 4 + wi
 #else
 #define MS_STOP(k) false
 #endif
+#ifdef NUT_MSD_STAMPS  // local_tune only: per-phase shader cycles of the local sort (thread 0 of each workgroup)
+__device__ unsigned long long g_ms_stamp[8];
+#define MS_STAMP(k)                                        \
+  do {                                                     \
+    if (tid == 0) {                                        \
+      const uint64_t t_ = __builtin_amdgcn_s_memtime();    \
+      if ((k) > 0) st_acc[(k) - 1] += t_ - st_last;        \
+      st_last = t_;                                        \
+    }                                                      \
+  } while (0)
+#else
+#define MS_STAMP(k) \
+  do {              \
+  } while (0)
+#endif
 
 // SB_ / WS_ = 0: the product defaults (bucket bits by capacity, window stride LS_WS)
 template <int THREADS, int MAXK, int SB_ = 0, int WS_ = 0>
@@ -564,17 +580,24 @@ struct OemTable {
 };
 
 // every lane sorts its own N registers ascending: no cross-lane traffic, each compare-
-// exchange is v_cmp_lt_u64 + 4 v_cndmask (N = 16: 63 of them)
+// exchange is v_cmp_lt_u64 + 4 v_cndmask (N = 16: 63 of them).  The pairs are template
+// arguments: indexing v[] with values read from the table at run time (a `#pragma unroll`
+// loop over net.a[i]) compiled to VGPR-indexed moves — s_set_gpr_idx_on / v_readlane of
+// the indices, ~20 instructions per compare-exchange (378 per local-sort kernel in the ISA)
+template <int A, int B, int N>
+__device__ __forceinline__ void lane_cx(uint64_t (&v)[N]) {
+  const uint64_t x = v[A], y = v[B];
+  const bool lt = x < y;
+  v[A] = lt ? x : y;
+  v[B] = lt ? y : x;
+}
+template <int N, int... I>
+__device__ __forceinline__ void lane_sort_net(uint64_t (&v)[N], std::integer_sequence<int, I...>) {
+  (lane_cx<OemTable<N>::net.a[I], OemTable<N>::net.b[I], N>(v), ...);
+}
 template <int N>
 __device__ __forceinline__ void lane_sort(uint64_t (&v)[N]) {
-  constexpr auto &net = OemTable<N>::net;
-#pragma unroll
-  for (int i = 0; i < net.n; ++i) {
-    const uint64_t x = v[net.a[i]], y = v[net.b[i]];
-    const bool lt = x < y;
-    v[net.a[i]] = lt ? x : y;
-    v[net.b[i]] = lt ? y : x;
-  }
+  lane_sort_net<N>(v, std::make_integer_sequence<int, OemTable<N>::net.n>{});
 }
 
 // Half-wave batches: register r holds window 2r in lanes 0-31 and window 2r+1 in lanes
@@ -611,24 +634,36 @@ __global__ __launch_bounds__(THREADS, 4) void ms_local_kernel(MsBufs bf, const M
   uint32_t *s_misc = s_ws + 16;                            // [0] max window, [1] round split
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   uint64_t key[MAXK];
-  // segment g's keys into registers: item i of lane l in wave w = position w*64*K + i*64 + l
-  auto load = [&](const MsSeg &g) {
+#ifdef NUT_MSD_STAMPS
+  uint64_t st_last = 0, st_acc[7] = {0, 0, 0, 0, 0, 0, 0};
+#endif
+  // segment g's keys into registers: item i of lane l in wave w = position w*64*K + i*64 + l.
+  // Raw loads only: the flip and the padding of positions past the count are applied when
+  // the segment is processed (finish_load), so a prefetch does not wait for its data here
+  auto load = [&](const MsSeg g) {
     const uint32_t cc = (uint32_t)g.count, kk = (cc + THREADS - 1) / THREADS;
     const uint32_t pp = (uint32_t)wave * kWave * kk + lane;
     const uint64_t *sp = ms_src(bf, g.buf) + g.start;
-    const uint64_t ff = g.buf == 0 ? flip : 0;
     // unconditional (clamped) loads, so that all MAXK are in flight at once
+#pragma unroll
+    for (int i = 0; i < MAXK; ++i) key[i] = __builtin_nontemporal_load(sp + min(pp + (uint32_t)i * kWave, cc - 1));
+  };
+  auto finish_load = [&](const MsSeg g) {
+    const uint32_t cc = (uint32_t)g.count, kk = (cc + THREADS - 1) / THREADS;
+    const uint32_t pp = (uint32_t)wave * kWave * kk + lane;
+    const uint64_t ff = g.buf == 0 ? flip : 0;
 #pragma unroll
     for (int i = 0; i < MAXK; ++i) {
       const uint32_t p = pp + (uint32_t)i * kWave;
-      const uint64_t v = __builtin_nontemporal_load(sp + min(p, cc - 1)) ^ ff;
-      key[i] = ((uint32_t)i < kk && p < cc) ? v : ~0ull;
+      key[i] = ((uint32_t)i < kk && p < cc) ? (key[i] ^ ff) : ~0ull;
     }
   };
   // one segment; returns whether the next segment's keys were loaded (PREFETCH: as soon as
   // this one's are staged, so their latency hides behind the window sorts).  Every early
   // return is block-uniform.
-  auto process = [&](const uint32_t sidx, const MsSeg &sg, const MsSeg &nsg, const bool has_next) -> bool {
+  auto process = [&](const uint32_t sidx, const MsSeg sg, const MsSeg nsg, const bool has_next) -> bool {
+  MS_STAMP(0);
+  finish_load(sg);
   const uint32_t c = (uint32_t)sg.count;
   const int hi = (int)sg.aux;
   const uint32_t K = (c + THREADS - 1) / THREADS;
@@ -669,6 +704,7 @@ __global__ __launch_bounds__(THREADS, 4) void ms_local_kernel(MsBufs bf, const M
     if ((uint32_t)i < K && p < c) rk[i / 2] |= atomicAdd(&s_off[bucket(key[i])], 1u) << (16 * (i & 1));
   }
   __syncthreads();
+  MS_STAMP(1);
   // ---- 2. bucket starts (BPT consecutive buckets per thread) and windows
   {
     uint32_t cb[C::BPT], sum = 0;
@@ -700,16 +736,30 @@ __global__ __launch_bounds__(THREADS, 4) void ms_local_kernel(MsBufs bf, const M
   }
   __syncthreads();
   const uint32_t nq = (c + LS_WS - 1) / LS_WS;
+  {  // the largest window and the last window that starts inside the first round: a wave
+     // maximum, then one LDS atomic per wave (512 atomics on one word serialised)
+    uint32_t mw = 0, ms = 0;
 #pragma unroll
-  for (int j = 0; j < C::WPT; ++j) {
-    const uint32_t q = (uint32_t)tid + (uint32_t)j * THREADS;
-    if (q < nq) {
-      const uint32_t wa = s_win[q], wb = s_win[q + 1];
-      atomicMax(&s_misc[0], wb - wa);
-      if (wa <= (uint32_t)C::LDS_KEYS) atomicMax(&s_misc[1], q);
+    for (int j = 0; j < C::WPT; ++j) {
+      const uint32_t q = (uint32_t)tid + (uint32_t)j * THREADS;
+      if (q < nq) {
+        const uint32_t wa = s_win[q], wb = s_win[q + 1];
+        mw = max(mw, wb - wa);
+        if (wa <= (uint32_t)C::LDS_KEYS) ms = max(ms, q);
+      }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      mw = max(mw, (uint32_t)__shfl_xor((int)mw, off, 64));
+      ms = max(ms, (uint32_t)__shfl_xor((int)ms, off, 64));
+    }
+    if (lane == 0) {
+      atomicMax(&s_misc[0], mw);
+      atomicMax(&s_misc[1], ms);
     }
   }
   __syncthreads();
+  MS_STAMP(2);
   // rounds: windows [0, split) then [split, nq) with at most LDS_KEYS keys each
   const uint32_t split = c > (uint32_t)C::LDS_KEYS ? s_misc[1] : nq;
   const uint32_t mid = split < nq ? s_win[split] : c;
@@ -735,6 +785,7 @@ __global__ __launch_bounds__(THREADS, 4) void ms_local_kernel(MsBufs bf, const M
     load(nsg);
     pf = true;
   }
+  MS_STAMP(3);
   if (MS_STOP(3)) {
     __syncthreads();
     dst[tid] = s_keys[tid];
@@ -768,27 +819,30 @@ __global__ __launch_bounds__(THREADS, 4) void ms_local_kernel(MsBufs bf, const M
       }
       // windows of LANE_N+1 .. 32 keys: eight at a time, two per register (half-waves)
       for (uint64_t mid32 = __ballot(wm > (uint32_t)LS_LANE_N && wm <= 32); mid32;) {
-        uint32_t ga[8], gm[8];
+        // register r: window 2r in lanes 0-31, window 2r+1 in lanes 32-63; the window's
+        // start / length are wave-uniform (readlane into SGPRs), one VGPR pair per register
+        uint32_t mg[4], ag[4];
 #pragma unroll
-        for (int g = 0; g < 8; ++g) {
-          const int l = mid32 ? __builtin_ctzll(mid32) : 0;
-          gm[g] = mid32 ? __shfl(wm, l, 64) : 0;
-          ga[g] = mid32 ? __shfl(wa, l, 64) : 0;
-          mid32 &= mid32 - 1;
+        for (int r = 0; r < 4; ++r) {
+          uint32_t m2[2], a2[2];
+#pragma unroll
+          for (int hh = 0; hh < 2; ++hh) {
+            const int l = mid32 ? __builtin_ctzll(mid32) : 0;
+            m2[hh] = mid32 ? (uint32_t)__builtin_amdgcn_readlane((int)wm, l) : 0u;
+            a2[hh] = mid32 ? (uint32_t)__builtin_amdgcn_readlane((int)wa, l) : 0u;
+            mid32 &= mid32 - 1;
+          }
+          mg[r] = lane < 32 ? m2[0] : m2[1];
+          ag[r] = lane < 32 ? a2[0] : a2[1];
         }
         const uint32_t h = (uint32_t)lane & 31;
         uint64_t v[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const uint32_t mg = lane < 32 ? gm[2 * r] : gm[2 * r + 1], ag = lane < 32 ? ga[2 * r] : ga[2 * r + 1];
-          v[r] = h < mg ? s_keys[ag + h] : ~0ull;
-        }
+        for (int r = 0; r < 4; ++r) v[r] = h < mg[r] ? s_keys[ag[r] + h] : ~0ull;
         wave_bitonic32_multi<4>(v, lane);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const uint32_t mg = lane < 32 ? gm[2 * r] : gm[2 * r + 1], ag = lane < 32 ? ga[2 * r] : ga[2 * r + 1];
-          if (h < mg) s_keys[ag + h] = v[r];
-        }
+        for (int r = 0; r < 4; ++r)
+          if (h < mg[r]) s_keys[ag[r] + h] = v[r];
       }
       for (uint64_t big = __ballot(wm > 32); big; big &= big - 1) {  // rare: one by one
         const int l = __builtin_ctzll(big);
@@ -796,10 +850,12 @@ __global__ __launch_bounds__(THREADS, 4) void ms_local_kernel(MsBufs bf, const M
       }
     }
     __syncthreads();
+    MS_STAMP(4);
     if (MS_STOP(4)) continue;
     const uint32_t rend = round ? c : mid;
     for (uint32_t j = tid; j < rend - rbase; j += THREADS) __builtin_nontemporal_store(s_keys[j] ^ flip, &dst[rbase + j]);
   }
+  MS_STAMP(5);
   return pf;
   };
   uint32_t sidx = blockIdx.x;
@@ -818,9 +874,14 @@ __global__ __launch_bounds__(THREADS, 4) void ms_local_kernel(MsBufs bf, const M
     if (!has_next) break;
     if (!pf) load(nsg);
     __syncthreads();  // LDS is reused by the next segment
+    MS_STAMP(6);
     sidx = nidx;
     sg = nsg;
   }
+#ifdef NUT_MSD_STAMPS
+  if (tid == 0)
+    for (int k = 0; k < 7; ++k) atomicAdd(&g_ms_stamp[k], (unsigned long long)st_acc[k]);
+#endif
 }
 
 // Fallback local sort: the segments ms_local_kernel listed in fb[1 ..] (fb[0] = count)

@@ -12,6 +12,7 @@
 
 #define NUT_MSD_KERNELS_ONLY
 #define NUT_MSD_PROFILE_STOP
+#define NUT_MSD_STAMPS
 #include "../../nutdb_amd/csrc/msd_sort.hip"
 
 #define CK(x)                                                       \
@@ -74,12 +75,21 @@ static void run(Ctx &c, const char *name, int stop = 0) {
   CK(hipMemcpyToSymbol(HIP_SYMBOL(nut::g_ms_stop), &stop, sizeof(int)));
   nut::MsBufs bf{nullptr, c.dst, c.src, nullptr};
   float best = 1e9;
+  unsigned long long st[8] = {0};
   for (int r = 0; r < 3; ++r) {
     CK(hipMemset(c.fb, 0, 4));
+    CK(hipMemcpyToSymbol(HIP_SYMBOL(nut::g_ms_stamp), st, sizeof(st)));
     CK(hipEventRecord(c.e0));
     hipLaunchKernelGGL(kern, dim3(grid), dim3(T), 0, 0, bf, (const nut::MsSeg *)c.dseg, c.nseg, 0ull, 0ull, c.fb);
     CK(hipEventRecord(c.e1));
     best = std::min(best, elapsed(c.e0, c.e1));
+  }
+  CK(hipMemcpyFromSymbol(st, HIP_SYMBOL(nut::g_ms_stamp), sizeof(st)));
+  if (!stop) {
+    printf("   cycles per segment (thread 0 of each workgroup):");
+    const char *ph[7] = {"ranks", "scan+windows", "place", "sort", "copy", "next", "-"};
+    for (int k = 0; k < 6; ++k) printf(" %s %.0f", ph[k], (double)st[k] / c.nseg);
+    printf("\n");
   }
   uint32_t nfb = 0;
   CK(hipMemcpy(&nfb, c.fb, 4, hipMemcpyDeviceToHost));
@@ -126,6 +136,7 @@ int main(int argc, char **argv) {
   }
   printf("segments %u x %u keys\n", c.nseg, c.seglen);
   run<512, 12, 0, 0>(c, "default <512,12> SB11 WS12");
+  if (argc > 3) return 0;  // profiling runs: the product variant only
   run<512, 12, 12, 12>(c, "<512,12> SB12 WS12");
   run<512, 12, 12, 10>(c, "<512,12> SB12 WS10");
   run<512, 12, 12, 8>(c, "<512,12> SB12 WS8");
