@@ -193,7 +193,11 @@ typedef enum {
  *   ABS, TO_F64  one operand; bool operands count as int 0/1 in arithmetic
  *   LOOKUP   one int operand x; v = device address of a byte table, arg = its length:
  *            bool table[x] != 0 for 0 <= x < arg, else false (dictionary predicates such
- *            as LIKE over dictionary codes; the table must outlive the call) */
+ *            as LIKE over dictionary codes; the table must outlive the call)
+ *   DATEPART one int operand d = days since 1970-01-01 (proleptic Gregorian), int result
+ *            by arg (nut_date_part): year, month 1-12, day of month, quarter 1-4, day of
+ *            week (Monday = 1 .. Sunday = 7), day of year 1-366; d is first clamped to
+ *            [-2^40, 2^40] (beyond any real date), so every d has one defined result. */
 typedef enum {
   NUT_P_COL = 0, NUT_P_I64 = 1, NUT_P_F64 = 2,
   NUT_P_ADD = 3, NUT_P_SUB = 4, NUT_P_MUL = 5, NUT_P_DIV = 6, NUT_P_MOD = 7, NUT_P_INTDIV = 8,
@@ -201,12 +205,15 @@ typedef enum {
   NUT_P_AND = 15, NUT_P_OR = 16, NUT_P_XOR = 17, NUT_P_NOT = 18,
   NUT_P_BITAND = 19, NUT_P_BITOR = 20, NUT_P_BITXOR = 21, NUT_P_BITNOT = 22,
   NUT_P_SHL = 23, NUT_P_SHR = 24,
-  NUT_P_IF = 25, NUT_P_ABS = 26, NUT_P_TO_F64 = 27, NUT_P_LOOKUP = 28
+  NUT_P_IF = 25, NUT_P_ABS = 26, NUT_P_TO_F64 = 27, NUT_P_LOOKUP = 28, NUT_P_DATEPART = 29
 } nut_prog_op;
+typedef enum {
+  NUT_DP_YEAR = 0, NUT_DP_MONTH = 1, NUT_DP_DAY = 2, NUT_DP_QUARTER = 3, NUT_DP_WEEKDAY = 4, NUT_DP_YEARDAY = 5
+} nut_date_part;
 typedef enum { NUT_PT_I64 = 0, NUT_PT_F64 = 1, NUT_PT_BOOL = 2 } nut_prog_value_type;
 typedef struct {
   int32_t op;   /* nut_prog_op */
-  int32_t arg;  /* NUT_P_COL: column index; NUT_P_LOOKUP: table length */
+  int32_t arg;  /* NUT_P_COL: column index; NUT_P_LOOKUP: table length; NUT_P_DATEPART: part */
   int64_t v;    /* NUT_P_I64 / NUT_P_F64 constant; NUT_P_LOOKUP: table address */
 } nut_prog_node;
 typedef struct {
@@ -252,6 +259,11 @@ typedef struct {
   nut_prog agg_mask[NUT_MAX_AGGS];          /* n = 0: every row; else the aggregate takes
                                                only rows where it is true (SQL NULL
                                                arguments of CASE without ELSE) */
+  /* Expression mode: key j (j < nkeys) is the value of key_prog[j] when its n > 0 (an
+   * int64 or bool program; keys[j] is then unused and may be NULL), else keys[j].
+   * Computed keys (getYear(d), a % 10) and packed key tuples: SQL plans pack up to 8
+   * GROUP BY keys into two words this way. */
+  nut_prog key_prog[NUT_MAX_KEYS];
 } nut_agg_spec;
 
 /* Result word per aggregate: f64 bits for SUM/MIN/MAX of an f64 expression,

@@ -46,7 +46,10 @@ AGG_SUM, AGG_COUNT, AGG_MIN, AGG_MAX = range(4)
 EX_COL, EX_MUL, EX_ADD, EX_SUB, EX_MUL_1M, EX_MUL_1M_1P = range(6)
 # nut_prog_op (expression programs, RPN) and nut_prog_value_type
 PROG_OPS = ["col", "i64", "f64", "add", "sub", "mul", "div", "mod", "intdiv", "lt", "le", "gt", "ge", "eq", "ne",
-            "and", "or", "xor", "not", "bitand", "bitor", "bitxor", "bitnot", "shl", "shr", "if", "abs", "to_f64", "lookup"]
+            "and", "or", "xor", "not", "bitand", "bitor", "bitxor", "bitnot", "shl", "shr", "if", "abs", "to_f64", "lookup",
+            "datepart"]
+# nut_date_part (the arg of a "datepart" node)
+DP_YEAR, DP_MONTH, DP_DAY, DP_QUARTER, DP_WEEKDAY, DP_YEARDAY = range(6)
 P = {name: i for i, name in enumerate(PROG_OPS)}
 PT_I64, PT_F64, PT_BOOL = 0, 1, 2
 
@@ -86,6 +89,7 @@ class NutAggSpec(C.Structure):
         ("where", NutProg),
         ("agg_val", NutProg * NUT_MAX_AGGS),
         ("agg_mask", NutProg * NUT_MAX_AGGS),
+        ("key_prog", NutProg * NUT_MAX_KEYS),
     ]
 
 

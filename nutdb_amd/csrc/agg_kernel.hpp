@@ -179,6 +179,13 @@ struct Rows {
   uint64_t vv[S::MV > 0 ? S::MV : 1][4];
 };
 
+// computed keys of a generated shape (bit j: key j is S::key(), nut_agg_spec.key_prog)
+template <class S>
+__device__ constexpr int key_prog_mask() {
+  if constexpr (S::kProg) return S::kKeyProg;
+  else return 0;
+}
+
 // VEC: 1 = all columns 16-B aligned (vector loads), 0 = decided at run time (p.vec)
 template <int VEC>
 __device__ __forceinline__ void load2(const AggArgs &p, const uint64_t *col, uint64_t i, uint64_t &x, uint64_t &y) {
@@ -211,13 +218,14 @@ __device__ __forceinline__ void load_rows(const AggArgs &p, uint64_t i0, uint64_
 #pragma unroll
   for (int t = 0; t < S::MP; ++t)
     if (t < S::np(p)) ld(p.pred_col[t], x.pv[t]);
+  constexpr int KP = key_prog_mask<S>();
   if (NK == 1 && p.nokey) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) x.k1[r] = 0;
-  } else {
+  } else if (!(KP & 1)) {
     ld(p.keys[0], x.k1);
   }
-  if (NK == 2) ld(p.keys[1], x.k2);
+  if (NK == 2 && !(KP & 2)) ld(p.keys[1], x.k2);
 #pragma unroll
   for (int c = 0; c < S::MV; ++c)
     if (c < S::nv(p)) ld(p.val_col[c], x.vv[c]);
@@ -229,8 +237,9 @@ __device__ __forceinline__ void load_rows(const AggArgs &p, uint64_t i0, uint64_
 // aggregate's identity (f64 SUM: -0.0, which leaves every sum bit-identical), a COUNT as
 // 1 / 0 (the partition pass then sums it).
 template <int NK, class S>
-__device__ __forceinline__ void spill_rows(const AggArgs &p, const LTable &lt, const Rows<S> &x,
-                                           const int32_t (&sl)[4], const uint64_t (&av)[S::MA][4],
+__device__ __forceinline__ void spill_rows(const AggArgs &p, const LTable &lt, const uint64_t (&kk1)[4],
+                                           const uint64_t (&kk2)[4], const int32_t (&sl)[4],
+                                           const uint64_t (&av)[S::MA][4],
                                            const bool (&vm)[S::MA][4]) {
   const int lane = threadIdx.x & 63;
   const uint64_t region = (uint64_t)blockIdx.x * p.sp_region;
@@ -245,7 +254,7 @@ __device__ __forceinline__ void spill_rows(const AggArgs &p, const LTable &lt, c
     b = __shfl(b, leader, 64);
     if (mine) {
       const uint64_t pos = region + b + lane_rank(m);
-      const uint64_t k1 = x.k1[r], k2 = NK == 2 ? x.k2[r] : 0;
+      const uint64_t k1 = kk1[r], k2 = NK == 2 ? kk2[r] : 0;
       atomicAdd(&lt.shist[owner_hash(k1, k2, NK) >> 56], 1u);
       p.sp_cols[1][pos] = k1;
       if (NK == 2) p.sp_cols[2][pos] = k2;
@@ -274,6 +283,9 @@ __device__ __forceinline__ void consume_rows(const AggArgs &p, const LTable &lt,
   bool ok[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) ok[r] = !TAIL || ((r < 2 ? i0 : i1) + (r & 1)) < nend;
+  uint64_t kk1[R], kk2[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) kk1[r] = x.k1[r], kk2[r] = NK == 2 ? x.k2[r] : 0;
   if constexpr (S::kProg) {
     // generated WHERE program (padding rows of the tail never raise)
 #pragma unroll
@@ -282,6 +294,15 @@ __device__ __forceinline__ void consume_rows(const AggArgs &p, const LTable &lt,
       const bool w = S::where(p, x.vv, r, e);
       err = err || (e && ok[r]);
       ok[r] = ok[r] && w;
+    }
+    // computed keys: their errors count for rows passing WHERE
+    constexpr int KP = key_prog_mask<S>();
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      bool e = false;
+      if (KP & 1) kk1[r] = S::key(p, 0, x.vv, r, e);
+      if (NK == 2 && (KP & 2)) kk2[r] = S::key(p, 1, x.vv, r, e);
+      err = err || (e && ok[r]);
     }
   }
   // WHERE: one decision per term per four rows
@@ -319,7 +340,7 @@ __device__ __forceinline__ void consume_rows(const AggArgs &p, const LTable &lt,
   uint64_t w[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
-    w[r] = lkey<NK>(x.k1[r], x.k2[r]);
+    w[r] = lkey<NK>(kk1[r], kk2[r]);
     sl[r] = -2;
   }
   if (cap) {
@@ -342,7 +363,7 @@ __device__ __forceinline__ void consume_rows(const AggArgs &p, const LTable &lt,
 #pragma unroll
         for (int j = 3; j >= 0; --j) s = c[j] == w[r] ? (int32_t)hb[r] + j : s;
         bool end = (c[0] == kEmpty) | (c[1] == kEmpty) | (c[2] == kEmpty) | (c[3] == kEmpty);
-        if (NK == 2 && s >= 0 && !keys_match<NK>(lt, (uint32_t)s, x.k1[r], x.k2[r])) s = -1, end = false;
+        if (NK == 2 && s >= 0 && !keys_match<NK>(lt, (uint32_t)s, kk1[r], kk2[r])) s = -1, end = false;
         if (NK == 1 && w[r] == kEmpty) s = -1, end = true;
         if (s < 0 && !end) {
           // continue the probe chain past the bucket (inline: a few slots at most)
@@ -350,7 +371,7 @@ __device__ __forceinline__ void consume_rows(const AggArgs &p, const LTable &lt,
           for (uint32_t probe = kBucket; probe < cap; ++probe) {
             const uint64_t cur =
                 LOCKED ? __hip_atomic_load(&lt.slot[e], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) : lt.slot[e];
-            if (cur == w[r] && keys_match<NK>(lt, e, x.k1[r], x.k2[r])) {
+            if (cur == w[r] && keys_match<NK>(lt, e, kk1[r], kk2[r])) {
               s = (int32_t)e;
               break;
             }
@@ -359,7 +380,7 @@ __device__ __forceinline__ void consume_rows(const AggArgs &p, const LTable &lt,
           }
         }
         // not present: insert (or find a concurrent insert) out of line
-        if (s < 0) s = l_find_slow<NK, LOCKED>(lt, cap, p.lds_limit, p.lds_log2, p.priv, w[r], x.k1[r], x.k2[r]);
+        if (s < 0) s = l_find_slow<NK, LOCKED>(lt, cap, p.lds_limit, p.lds_log2, p.priv, w[r], kk1[r], kk2[r]);
         sl[r] = s;
       }
     }
@@ -427,7 +448,7 @@ __device__ __forceinline__ void consume_rows(const AggArgs &p, const LTable &lt,
   }
   // rows the block table did not admit
   if (p.sp_counts) {
-    spill_rows<NK, S>(p, lt, x, sl, av, vm);
+    spill_rows<NK, S>(p, lt, kk1, kk2, sl, av, vm);
     return;
   }
 #pragma unroll
@@ -437,7 +458,7 @@ __device__ __forceinline__ void consume_rows(const AggArgs &p, const LTable &lt,
       uint32_t m = 0;
 #pragma unroll
       for (int a = 0; a < S::MA && a < 8; ++a) g[a] = av[a][r], m |= vm[a][r] ? 1u << a : 0u;
-      g_row<NK>(p.gt, (int64_t)x.k1[r], (int64_t)x.k2[r], m, g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7]);
+      g_row<NK>(p.gt, (int64_t)kk1[r], (int64_t)kk2[r], m, g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7]);
     }
   }
 }

@@ -49,9 +49,14 @@ nut_status validate(const nut_agg_spec *s) {
   if (s->npred < 0 || s->npred > NUT_MAX_PRED) return fail(NUT_ERR_UNSUPPORTED, "nut_groupby: too many predicate terms");
   if (s->nvals < 0 || s->nvals > NUT_MAX_VALS) return fail(NUT_ERR_UNSUPPORTED, "nut_groupby: too many value columns");
   if (s->naggs < 0 || s->naggs > NUT_MAX_AGGS) return fail(NUT_ERR_UNSUPPORTED, "nut_groupby: too many aggregates");
+  for (int k = 0; k < NUT_MAX_KEYS; ++k) {
+    if (!s->key_prog[k].n) continue;
+    if (!s->prog_mode) return fail(NUT_ERR_INVALID_ARG, "nut_groupby: key programs need expression mode (prog_mode = 1)");
+    if (k >= s->nkeys) return fail(NUT_ERR_INVALID_ARG, "nut_groupby: key program past nkeys");
+  }
   if (s->n) {
     for (int k = 0; k < s->nkeys; ++k)
-      if (!s->keys[k]) return fail(NUT_ERR_INVALID_ARG, "nut_groupby: NULL key column");
+      if (!s->keys[k] && !s->key_prog[k].n) return fail(NUT_ERR_INVALID_ARG, "nut_groupby: NULL key column");
     for (int t = 0; t < s->npred; ++t) {
       if (!s->pred_col[t]) return fail(NUT_ERR_INVALID_ARG, "nut_groupby: NULL predicate column");
       if (s->pred_op[t] < NUT_LT || s->pred_op[t] > NUT_NOT_IN) return fail(NUT_ERR_INVALID_ARG, "nut_groupby: bad cmp op");
@@ -73,6 +78,12 @@ nut_status validate(const nut_agg_spec *s) {
         return fail(NUT_ERR_INVALID_ARG, "nut_groupby: bad program column type");
     }
     int32_t t;
+    for (int k = 0; k < s->nkeys; ++k) {
+      if (!s->key_prog[k].n) continue;
+      nut_status st = prog_check(&s->key_prog[k], s->prog_col_type, s->nprog_cols, &t);
+      if (st) return st;
+      if (t == NUT_PT_F64) return fail(NUT_ERR_INVALID_ARG, "nut_groupby: a key program is float64 (keys are int64)");
+    }
     for (int a = 0; a < s->naggs; ++a) {
       int op = s->agg_op[a];
       if (op < NUT_AGG_SUM || op > NUT_AGG_MAX) return fail(NUT_ERR_INVALID_ARG, "nut_groupby: bad aggregate op");
@@ -276,8 +287,9 @@ nut_status launch_agg(nut_groups *g, const nut_agg_spec *s, uint64_t group_hint,
   a.n = s->n;
   // nkeys == 0 (global aggregate) runs the one-key kernels with every key = 0
   a.nokey = s->nkeys == 0 ? 1 : 0;
-  a.keys[0] = (const uint64_t *)(s->nkeys ? s->keys[0] : nullptr);
-  a.keys[1] = s->nkeys == 2 ? (const uint64_t *)s->keys[1] : a.keys[0];
+  // (a computed key — key_prog — is evaluated in the kernel; its column pointer is unused)
+  a.keys[0] = (const uint64_t *)(s->nkeys && !s->key_prog[0].n ? s->keys[0] : nullptr);
+  a.keys[1] = s->nkeys == 2 && !s->key_prog[1].n ? (const uint64_t *)s->keys[1] : a.keys[0];
   a.npred = s->npred;
   for (int t = 0; t < s->npred; ++t) {
     a.pred_col[t] = (const uint64_t *)s->pred_col[t];

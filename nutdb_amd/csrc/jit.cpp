@@ -75,9 +75,9 @@ struct Gen {
       PVal a[3];
       const int op = nd.op;
       const int arity = op <= NUT_P_F64 ? 0 : (op == NUT_P_NOT || op == NUT_P_BITNOT || op == NUT_P_ABS ||
-                                                op == NUT_P_TO_F64 || op == NUT_P_LOOKUP) ? 1
+                                                op == NUT_P_TO_F64 || op == NUT_P_LOOKUP || op == NUT_P_DATEPART) ? 1
                                                                                          : op == NUT_P_IF ? 3 : 2;
-      if (op < 0 || op > NUT_P_LOOKUP) return fail("unknown program op " + std::to_string(op));
+      if (op < 0 || op > NUT_P_DATEPART) return fail("unknown program op " + std::to_string(op));
       if (!pop(arity, a)) return fail("program stack underflow at node " + std::to_string(i));
       PVal r;
       const bool f = arity == 2 && (a[0].t == NUT_PT_F64 || a[1].t == NUT_PT_F64);
@@ -169,6 +169,11 @@ struct Gen {
           r = {NUT_PT_BOOL, "jlookup(" + as_i(a[0]) + ", " + konst((uint64_t)nd.v) + ", " +
                                 konst((uint64_t)(int64_t)nd.arg) + ")"};
           break;
+        case NUT_P_DATEPART:
+          if (a[0].t == NUT_PT_F64) return fail("DATEPART needs an integer operand (days)");
+          if (nd.arg < NUT_DP_YEAR || nd.arg > NUT_DP_YEARDAY) return fail("DATEPART: unknown part " + std::to_string(nd.arg));
+          r = {NUT_PT_I64, "jdatepart(" + as_i(a[0]) + ", " + std::to_string(nd.arg) + ")"};
+          break;
       }
       if (r.s.size() > (1u << 20)) return fail("expression program too large");
       st.push_back(std::move(r));
@@ -209,6 +214,30 @@ __device__ __forceinline__ int64_t jabs(int64_t a) { return a < 0 ? (int64_t)(0 
 __device__ __forceinline__ bool jlookup(int64_t x, uint64_t t, uint64_t n) {
   if ((uint64_t)x >= n) return false;
   return ((const uint8_t *)t)[x] != 0;
+}
+// civil-from-days (proleptic Gregorian); P = nut_date_part.  d is clamped to +-2^40 days
+// first, so no intermediate overflows.
+__device__ __forceinline__ int64_t jdatepart(int64_t d, const int P) {
+  d = d < -(1ll << 40) ? -(1ll << 40) : d > (1ll << 40) ? (1ll << 40) : d;
+  const int64_t z = d + 719468;
+  const int64_t era = (z >= 0 ? z : z - 146096) / 146097;
+  const int64_t doe = z - era * 146097;
+  const int64_t yoe = (doe - doe / 1460 + doe / 36524 - doe / 146096) / 365;
+  const int64_t doy = doe - (365 * yoe + yoe / 4 - yoe / 100);  // from March 1
+  const int64_t mp = (5 * doy + 2) / 153;
+  const int64_t m = mp < 10 ? mp + 3 : mp - 9;
+  const int64_t y = yoe + era * 400 + (m <= 2 ? 1 : 0);
+  if (P == 0) return y;
+  if (P == 1) return m;
+  if (P == 2) return doy - (153 * mp + 2) / 5 + 1;
+  if (P == 3) return (m - 1) / 3 + 1;
+  if (P == 4) {  // 1970-01-01 was a Thursday (4)
+    int64_t w = d % 7;
+    w = w < 0 ? w + 7 : w;
+    return (w + 3) % 7 + 1;
+  }
+  // day of year: January / February are days 306.. of the March-based year
+  return doy >= 306 ? doy - 305 : doy + 60 + (((y % 4 == 0 && y % 100 != 0) || y % 400 == 0) ? 1 : 0);
 }
 )";
 
@@ -301,6 +330,16 @@ nut_status jit_shape(const nut_agg_spec *s, const int32_t *kinds, JitShape &out)
       valid += ca + b + ";\n";
     }
   }
+  // computed keys (nut_agg_spec.key_prog): int64 / bool programs
+  std::string keys;
+  int kmask = 0;
+  for (int j = 0; j < s->nkeys && j < NUT_MAX_KEYS; ++j) {
+    if (!s->key_prog[j].n) continue;
+    if (!g.run(&s->key_prog[j], r)) return fail(NUT_ERR_INVALID_ARG, "nut_groupby key " + std::to_string(j) + " program: " + g.err);
+    if (r.t == NUT_PT_F64) return fail(NUT_ERR_INVALID_ARG, "nut_groupby key " + std::to_string(j) + " program: float64 keys are not grouped");
+    keys += "      case " + std::to_string(j) + ": return " + bits_of(r) + ";\n";
+    kmask |= 1 << j;
+  }
   uint32_t kp = 0;
   for (int a = 0; a < s->naggs; ++a) kp |= (uint32_t)(kinds[a] & 15) << (4 * a);
   const int ma = s->naggs > 0 ? s->naggs : 1;
@@ -309,6 +348,7 @@ nut_status jit_shape(const nut_agg_spec *s, const int32_t *kinds, JitShape &out)
   src += "  static constexpr bool kProg = true;\n";
   src += "  static constexpr int MP = 0, MV = " + std::to_string(s->nprog_cols) + ", MA = " + std::to_string(ma) + ";\n";
   src += "  static constexpr uint32_t kKinds = " + std::to_string(kp) + "u;\n";
+  src += "  static constexpr int kKeyProg = " + std::to_string(kmask) + ";\n";
   src += "  __device__ static constexpr int np(const AggArgs &) { return 0; }\n";
   src += "  __device__ static constexpr int nv(const AggArgs &) { return MV; }\n";
   src += "  __device__ static constexpr int na(const AggArgs &) { return " + std::to_string(s->naggs) + "; }\n";
@@ -323,6 +363,8 @@ nut_status jit_shape(const nut_agg_spec *s, const int32_t *kinds, JitShape &out)
   src += "    switch (a) {\n" + value + "      default: return 0;\n    }\n  }\n";
   src += "  template <class V>\n  __device__ __forceinline__ static bool valid(const AggArgs &p, int a, const V &v, int r, bool &err) {\n";
   src += "    switch (a) {\n" + valid + "      default: return true;\n    }\n  }\n";
+  src += "  template <class V>\n  __device__ __forceinline__ static uint64_t key(const AggArgs &p, int j, const V &v, int r, bool &err) {\n";
+  src += "    switch (j) {\n" + keys + "      default: return 0;\n    }\n  }\n";
   src += "};\n";
   out.src = std::move(src);
   return NUT_OK;

@@ -124,6 +124,31 @@ void civil_from_days(int64_t z, int64_t &y, unsigned &m, unsigned &d) {
   y += m <= 2;
 }
 bool leap(int64_t y) { return (y % 4 == 0 && y % 100 != 0) || y % 400 == 0; }
+// nut_date_part of a day number (the DATEPART program op's host twin, for constants)
+int64_t date_part(int64_t d, int part) {
+  d = std::max<int64_t>(-(1ll << 40), std::min<int64_t>(1ll << 40, d));
+  int64_t y;
+  unsigned m, dd;
+  civil_from_days(d, y, m, dd);
+  switch (part) {
+    case NUT_DP_YEAR: return y;
+    case NUT_DP_MONTH: return m;
+    case NUT_DP_DAY: return dd;
+    case NUT_DP_QUARTER: return (m - 1) / 3 + 1;
+    case NUT_DP_WEEKDAY: return ((d % 7 + 7) % 7 + 3) % 7 + 1;
+    default: return d - days_from_civil(y, 1, 1) + 1;
+  }
+}
+// SQL date functions (ClickHouse names; getX spellings as in the reference's fixtures):
+// the nut_date_part they compute, or -1
+int date_fn(sv n) {
+  static const char *const names[][2] = {{"toyear", "getyear"},         {"tomonth", "getmonth"},
+                                          {"todayofmonth", "getdayofmonth"}, {"toquarter", "getquarter"},
+                                          {"todayofweek", "getdayofweek"}, {"todayofyear", "getdayofyear"}};
+  for (int i = 0; i < 6; ++i)
+    if (ieq(n, names[i][0]) || ieq(n, names[i][1])) return i;
+  return -1;
+}
 unsigned month_days(int64_t y, unsigned m) {
   static const unsigned md[] = {31, 28, 31, 30, 31, 30, 31, 31, 30, 31, 30, 31};
   return m == 2 && leap(y) ? 29 : md[m - 1];
@@ -193,6 +218,13 @@ bool const_eval(const Expr &e, CVal &out, Lowering &L) {
     if (!parse_date(e.kids[0].lit->str, days)) return L.fail("toDate: '" + e.kids[0].lit->str + "' is not YYYY-MM-DD");
     out.is_int = true;
     out.v = days;
+    return true;
+  }
+  if (e.k == EK::FnCall && e.fn() == FnKind::Others && date_fn(e.id.name) >= 0 && e.kids.size() == 1) {
+    CVal x;
+    if (!const_eval(e.kids[0], x, L) || !x.is_int || x.is_str) return false;
+    out.is_int = true;
+    out.v = date_part((int64_t)std::max<i128>(-(i128(1) << 41), std::min<i128>(i128(1) << 41, x.v)), date_fn(e.id.name));
     return true;
   }
   if (e.k == EK::BinaryOp && (e.bop() == BinOp::Plus || e.bop() == BinOp::Minus)) {
@@ -268,6 +300,7 @@ struct PNode {
   int op = NUT_P_I64;
   int col = -1;  // NUT_P_COL: plan column
   CVal c;        // NUT_P_I64 / NUT_P_F64 constant
+  int arg = 0;   // NUT_P_DATEPART: nut_date_part
 };
 using PProg = std::vector<PNode>;
 
@@ -276,8 +309,21 @@ struct PlanAgg {
   int arg[3];
   PProg val, mask;        // compiled mode: argument program and row mask (empty = every row)
   std::vector<int> refs;  // compiled mode: columns the argument reads (COUNT(x) included)
+  bool distinct = false;  // countUnique(val): distinct values per group (op COUNT; two passes)
 };
-enum OutKind { OUT_KEY, OUT_AGG, OUT_AVG };
+// Arithmetic over a group's outputs (SELECT sum(a) / count(), 100 * sum(x) / sum(y), ...),
+// evaluated on the host per result group with nut_prog semantics: int + - * wrap, an f64
+// operand makes the op f64, / is always f64, % and intDiv truncate (a zero divisor fails).
+enum XKind { X_CONST, X_OUT, X_ADD, X_SUB, X_MUL, X_DIV, X_MOD, X_INTDIV, X_ABS, X_TOF };
+struct XNode {
+  int k = X_CONST;
+  int out = -1;  // X_OUT: output index (a key, an aggregate or avg)
+  bool is_int = true;
+  int64_t i = 0;
+  double f = 0;
+  std::vector<XNode> kids;
+};
+enum OutKind { OUT_KEY, OUT_AGG, OUT_AVG, OUT_EXPR };
 struct PlanOut {
   int kind, a, b;
   std::string name, text;
@@ -301,6 +347,8 @@ struct HNode {
 // FULL OUTER JOIN (plans only): executed as a LEFT join plus the JOIN source's unmatched
 // rows (an ANTI join with the roles swapped); the kernels know types 0..3
 constexpr int PJ_FULL = 4;
+// GROUP BY keys of one plan (packed into the kernels' two key words)
+constexpr int kMaxGroupKeys = 8;
 
 struct nut_plan {
   int kind = NUT_PLAN_FILTER;
@@ -317,7 +365,12 @@ struct nut_plan {
   // to the only projected column: a keys-only sort; otherwise row ids are sorted by the
   // keys (stable pair sorts, last key first) and every projected column gathered.
   std::vector<std::pair<int, bool>> sort_keys;
-  std::vector<int> keys, vals;    // GROUPBY key / value columns (indices into cols)
+  std::vector<int> keys, vals;    // GROUPBY key / value columns (indices into cols; a computed key: -1)
+  // GROUPBY keys (compiled mode): each key's program (a plain key: COL) and expression text
+  // (to match SELECT items); up to kMaxGroupKeys, packed into two words at execution
+  std::vector<PProg> key_progs;
+  std::vector<std::string> key_text;
+  std::vector<XNode> xprs;        // OUT_EXPR outputs' expressions
   std::vector<PlanAgg> aggs;
   std::vector<PlanOut> outs;
   std::vector<std::pair<int, bool>> order;  // GROUPBY: (output, desc)
@@ -365,7 +418,7 @@ constexpr int P_LIKE = 1000, P_ILIKE = 1001;
 int pnode_arity(int op) {
   if (op == P_LIKE || op == P_ILIKE) return 0;
   return op <= NUT_P_F64 ? 0 : (op == NUT_P_NOT || op == NUT_P_BITNOT || op == NUT_P_ABS ||
-                                op == NUT_P_TO_F64) ? 1 : op == NUT_P_IF ? 3 : 2;
+                                op == NUT_P_TO_F64 || op == NUT_P_DATEPART) ? 1 : op == NUT_P_IF ? 3 : 2;
 }
 
 // bytes of the UTF-8 sequence starting at s[i] (a stray continuation byte counts alone)
@@ -541,7 +594,7 @@ bool same_prog(const PProg &x, const PProg &y) {
   if (x.size() != y.size()) return false;
   for (size_t i = 0; i < x.size(); ++i) {
     const PNode &a = x[i], &b = y[i];
-    if (a.op != b.op || a.col != b.col) return false;
+    if (a.op != b.op || a.col != b.col || a.arg != b.arg) return false;
     if (a.op == NUT_P_I64 && !(a.c.is_int == b.c.is_int && a.c.v == b.c.v && a.c.is_str == b.c.is_str &&
                                a.c.s == b.c.s))
       return false;
@@ -794,8 +847,17 @@ bool lower_prog(nut_plan &p, const Expr &e, PProg &o, Lowering &L) {
         emit(o, ieq(n, "intdiv") ? NUT_P_INTDIV : NUT_P_MOD);
         return true;
       }
+      if (date_fn(n) >= 0 && na == 1) {
+        if (!lower_prog(p, e.kids[0], o, L)) return false;
+        PNode dp;
+        dp.op = NUT_P_DATEPART;
+        dp.arg = date_fn(n);
+        o.push_back(dp);
+        return true;
+      }
       if (ieq(n, "todate")) return L.fail("toDate takes one 'YYYY-MM-DD' constant");
-      return L.fail("function '" + std::string(n) + "' is not executed (executed: if, multiIf, abs, toFloat64, intDiv, modulo)");
+      return L.fail("function '" + std::string(n) + "' is not executed (executed: if, multiIf, abs, toFloat64, intDiv, "
+                    "modulo, toYear/getYear, toMonth, toDayOfMonth, toQuarter, toDayOfWeek, toDayOfYear)");
     }
     default: return L.fail("'" + expr_text(e) + "' is not executed (parameters, collections, subqueries)");
   }
@@ -837,7 +899,8 @@ int add_agg(nut_plan &p, const PlanAgg &a) {
   for (size_t i = 0; i < p.aggs.size(); ++i) {
     const PlanAgg &b = p.aggs[i];
     if (p.compiled) {
-      if (b.op == a.op && same_prog(b.mask, a.mask) && (a.op == NUT_AGG_COUNT || same_prog(b.val, a.val)) &&
+      if (b.op == a.op && b.distinct == a.distinct && same_prog(b.mask, a.mask) &&
+          (a.op == NUT_AGG_COUNT || same_prog(b.val, a.val)) && (!a.distinct || same_prog(b.val, a.val)) &&
           b.refs == a.refs)  // count(x) and count(*) differ once outer joins mask x's table
         return (int)i;
       continue;
@@ -907,23 +970,115 @@ bool lower_where(nut_plan &p, const Expr &e, Lowering &L) {
   return lower_pred_term(p, e, L);
 }
 
-// one SELECT-list item of an aggregate plan: a GROUP BY key or sum/count/min/max/avg
-bool lower_output(nut_plan &p, const Expr &e, PlanOut &o, Lowering &L) {
+// the GROUP BY key an expression names (its column, or a computed key's text), or -1
+int key_of(nut_plan &p, const Expr &e) {
   sv name;
   if (column_ref(p, e, name)) {
-    int c = col_index(p, name), j = -1;
+    const int c = col_index(p, name);
     for (size_t i = 0; i < p.keys.size(); ++i)
-      if (p.keys[i] == c) j = (int)i;
-    if (j < 0)
-      return L.fail("column '" + std::string(name) + "' is neither a GROUP BY key nor aggregated" +
-                    (p.keys.empty() ? " (no GROUP BY)" : ""));
-    o.kind = OUT_KEY;
-    o.a = j;
+      if (p.keys[i] == c) return (int)i;
+    return -1;
+  }
+  const std::string t = expr_text(e);
+  for (size_t i = 0; i < p.key_text.size(); ++i)
+    if (p.keys[i] < 0 && ieq(p.key_text[i], t)) return (int)i;
+  return -1;
+}
+bool is_distinct_name(sv n) { return ieq(n, "countunique") || ieq(n, "uniqexact") || ieq(n, "uniq"); }
+bool is_output_leaf(nut_plan &p, const Expr &e) {
+  return key_of(p, e) >= 0 ||
+         (e.k == EK::FnCall && e.fn() == FnKind::Others && (is_agg_name(e.id.name) || is_distinct_name(e.id.name)));
+}
+bool having_output(nut_plan &p, const Expr &e, int &out, Lowering &L);
+
+// arithmetic over keys / aggregates / constants (an OUT_EXPR output)
+bool lower_xpr(nut_plan &p, const Expr &e, XNode &x, Lowering &L) {
+  CVal c;
+  Lowering quiet;
+  if (const_eval(e, c, quiet)) {
+    if (c.is_str) return L.fail("string constants in arithmetic over aggregates are not executed");
+    x.k = X_CONST;
+    if (c.is_int && c.v <= INT64_MAX && c.v >= INT64_MIN) {
+      x.is_int = true;
+      x.i = (int64_t)c.v;
+    } else {
+      x.is_int = false;
+      x.f = c.is_int ? (double)c.v : c.dec.to_f64();
+    }
     return true;
   }
-  if (!(e.k == EK::FnCall && e.fn() == FnKind::Others))
-    return L.fail("SELECT item '" + o.text + "' is not a key column or an aggregate");
+  if (is_output_leaf(p, e)) {
+    x.k = X_OUT;
+    return having_output(p, e, x.out, L);
+  }
+  if (e.k == EK::BinaryOp) {
+    const BinOp b = e.bop();
+    const int k = b == BinOp::Plus ? X_ADD : b == BinOp::Minus ? X_SUB : b == BinOp::Multi ? X_MUL
+                  : b == BinOp::Div ? X_DIV : b == BinOp::Mod ? X_MOD : -1;
+    if (k < 0) return L.fail("operator in '" + expr_text(e) + "' is not executed over aggregates (+ - * / %)");
+    x.k = k;
+    x.kids.resize(2);
+    return lower_xpr(p, e.kids[0], x.kids[0], L) && lower_xpr(p, e.kids[1], x.kids[1], L);
+  }
+  if (e.k == EK::FnCall && e.fn() == FnKind::Others) {
+    const sv n = e.id.name;
+    const size_t na = e.kids.size();
+    int k = -1;
+    if ((ieq(n, "intdiv") || ieq(n, "modulo")) && na == 2) k = ieq(n, "intdiv") ? X_INTDIV : X_MOD;
+    if ((ieq(n, "abs") || ieq(n, "tofloat64")) && na == 1) k = ieq(n, "abs") ? X_ABS : X_TOF;
+    if (k >= 0) {
+      x.k = k;
+      x.kids.resize(na);
+      for (size_t i = 0; i < na; ++i)
+        if (!lower_xpr(p, e.kids[i], x.kids[i], L)) return false;
+      return true;
+    }
+  }
+  return L.fail("SELECT item '" + expr_text(e) + "' is not a GROUP BY key, an aggregate or arithmetic over them");
+}
+
+// one SELECT-list item of an aggregate plan: a GROUP BY key, sum/count/min/max/avg,
+// countUnique, or arithmetic over those
+bool lower_output(nut_plan &p, const Expr &e, PlanOut &o, Lowering &L) {
+  sv name;
+  const int kj = key_of(p, e);
+  if (kj >= 0) {
+    o.kind = OUT_KEY;
+    o.a = kj;
+    return true;
+  }
+  if (column_ref(p, e, name))
+    return L.fail("column '" + std::string(name) + "' is neither a GROUP BY key nor aggregated" +
+                  (p.keys.empty() ? " (no GROUP BY)" : ""));
+  if (!(e.k == EK::FnCall && e.fn() == FnKind::Others && (is_agg_name(e.id.name) || is_distinct_name(e.id.name)))) {
+    XNode x;
+    if (!lower_xpr(p, e, x, L)) return false;
+    p.xprs.push_back(std::move(x));
+    o.kind = OUT_EXPR;
+    o.a = (int)p.xprs.size() - 1;
+    return true;
+  }
   sv fn = e.id.name;
+  if (is_distinct_name(fn)) {
+    // countUnique(x): distinct x per group — GROUP BY (keys, x), then a count per key
+    // tuple (exec_groupby); expression mode only
+    if (!p.compiled) return L.fail("countUnique runs in expression mode");
+    if (e.kids.size() != 1) return L.fail(std::string(fn) + " takes one argument");
+    PlanAgg a{};
+    bool nullable = false;
+    if (!lower_nullable(p, e.kids[0], a.val, a.mask, nullable, L)) return false;
+    for (const PProg *pp : {&a.val, &a.mask})
+      for (const PNode &nd : *pp)
+        if (nd.op == NUT_P_COL || nd.op == P_LIKE || nd.op == P_ILIKE) a.refs.push_back(nd.col);
+    std::sort(a.refs.begin(), a.refs.end());
+    a.refs.erase(std::unique(a.refs.begin(), a.refs.end()), a.refs.end());
+    a.op = NUT_AGG_COUNT;
+    a.expr = NUT_EX_COL;
+    a.distinct = true;
+    o.kind = OUT_AGG;
+    o.a = add_agg(p, a);
+    return true;
+  }
   int op = ieq(fn, "sum") ? NUT_AGG_SUM : ieq(fn, "count") ? NUT_AGG_COUNT : ieq(fn, "min") ? NUT_AGG_MIN
            : ieq(fn, "max") ? NUT_AGG_MAX : ieq(fn, "avg") ? 100 : -1;
   if (op < 0) return L.fail("function '" + std::string(fn) + "' is not an executed aggregate (sum/count/min/max/avg)");
@@ -1077,6 +1232,30 @@ bool on_equalities(nut_plan &p, const Expr &e, std::vector<std::pair<int, int>> 
   return true;
 }
 
+// one GROUP BY key: a column (fused and expression mode) or, in expression mode, any
+// integer expression (getYear(d), a % 10, ...) evaluated by the group-by kernel
+bool add_key(nut_plan &p, const Expr &e, Lowering &L) {
+  sv name;
+  PProg kp;
+  if (column_ref(p, e, name)) {
+    const int c = col_index(p, name);
+    for (int k : p.keys)
+      if (k == c) return true;  // GROUP BY a, a: one key
+    p.keys.push_back(c);
+    PNode n;
+    n.op = NUT_P_COL;
+    n.col = c;
+    kp.push_back(n);
+  } else {
+    if (!p.compiled) return L.fail("computed GROUP BY keys run in expression mode");
+    if (!lower_prog(p, e, kp, L)) return false;
+    p.keys.push_back(-1);
+  }
+  p.key_progs.push_back(std::move(kp));
+  p.key_text.push_back(expr_text(e));
+  return true;
+}
+
 bool lower_mode(const Statement &st, nut_plan &p, Lowering &L) {
   if (st.k != StmtKind::Select) return L.fail("only SELECT statements execute");
   if (st.query.is_union) return L.fail("UNION/INTERSECT/EXCEPT are not executed (one query body per plan)");
@@ -1195,12 +1374,10 @@ bool lower_mode(const Statement &st, nut_plan &p, Lowering &L) {
     p.kind = NUT_PLAN_GROUPBY;
     if (b.distinct) {
       if (has_agg) return L.fail("DISTINCT over aggregates is not executed");
-      for (const QueryExpr &q : b.columns) {
-        sv name;
-        if (!column_ref(p, q.e, name)) return L.fail("SELECT DISTINCT takes columns");
-        p.keys.push_back(col_index(p, name));
-      }
-      if (p.keys.empty() || p.keys.size() > NUT_MAX_KEYS) return L.fail("SELECT DISTINCT takes 1 or 2 columns");
+      for (const QueryExpr &q : b.columns)
+        if (!add_key(p, q.e, L)) return false;
+      if (p.keys.empty() || p.keys.size() > (size_t)kMaxGroupKeys) return L.fail("SELECT DISTINCT takes 1 to 8 columns");
+      if (!p.compiled && p.keys.size() > NUT_MAX_KEYS) return L.fail("DISTINCT over more than 2 columns runs in expression mode");
       PlanAgg cnt{};
       cnt.op = NUT_AGG_COUNT;
       cnt.expr = NUT_EX_COL;
@@ -1208,11 +1385,21 @@ bool lower_mode(const Statement &st, nut_plan &p, Lowering &L) {
     }
     if (b.group_by) {
       for (const QueryExpr &k : *b.group_by) {
+        // a SELECT alias names its expression (GROUP BY l_year of getYear(d) AS l_year)
+        const Expr *ke = &k.e;
         sv name;
-        if (!column_ref(p, k.e, name)) return L.fail("GROUP BY keys must be columns");
-        p.keys.push_back(col_index(p, name));
+        if (column_ref(p, k.e, name) && !k.e.id.qualified)
+          for (const QueryExpr &q : b.columns) {
+            sv qn;
+            if (q.alias && ieq(*q.alias, name) && !(column_ref(p, q.e, qn) && ieq(qn, name))) {
+              ke = &q.e;
+              break;
+            }
+          }
+        if (!add_key(p, *ke, L)) return false;
       }
-      if (p.keys.empty() || p.keys.size() > NUT_MAX_KEYS) return L.fail("GROUP BY takes 1 or 2 key columns");
+      if (p.keys.empty() || p.keys.size() > (size_t)kMaxGroupKeys) return L.fail("GROUP BY takes 1 to 8 keys");
+      if (!p.compiled && p.keys.size() > NUT_MAX_KEYS) return L.fail("more than 2 GROUP BY keys run in expression mode");
     }
     for (const QueryExpr &q : b.columns) {
       PlanOut o;
@@ -1235,7 +1422,8 @@ bool lower_mode(const Statement &st, nut_plan &p, Lowering &L) {
         for (size_t i = 0; i < p.outs.size() && idx < 0; ++i) {
           const PlanOut &o = p.outs[i];
           if (!o.hidden && (ieq(o.name, text) || ieq(o.text, text))) idx = (int)i;
-          if (idx < 0 && !o.hidden && column_ref(p, k.e.e, name) && o.kind == OUT_KEY && ieq(p.cols[p.keys[o.a]], name))
+          if (idx < 0 && !o.hidden && column_ref(p, k.e.e, name) && o.kind == OUT_KEY && p.keys[o.a] >= 0 &&
+              ieq(p.cols[p.keys[o.a]], name))
             idx = (int)i;
         }
         if (idx < 0 && !having_output(p, k.e.e, idx, L))
@@ -1354,7 +1542,10 @@ std::string prog_text(const nut_plan &p, const PProg &pp) {
       st.push_back("(" + p.cols[n.col] + (n.op == P_LIKE ? " like " : " ilike ") + cval_str(n.c) + ")");
     else if (n.op == NUT_P_COL) st.push_back(p.cols[n.col]);
     else if (n.op == NUT_P_I64 || n.op == NUT_P_F64) st.push_back(cval_str(n.c));
-    else if (n.op == NUT_P_NOT || n.op == NUT_P_BITNOT || n.op == NUT_P_ABS || n.op == NUT_P_TO_F64) {
+    else if (n.op == NUT_P_DATEPART) {
+      static const char *dp[] = {"toYear", "toMonth", "toDayOfMonth", "toQuarter", "toDayOfWeek", "toDayOfYear"};
+      st.push_back(std::string(n.arg >= 0 && n.arg < 6 ? dp[n.arg] : "datepart") + "(" + pop() + ")");
+    } else if (n.op == NUT_P_NOT || n.op == NUT_P_BITNOT || n.op == NUT_P_ABS || n.op == NUT_P_TO_F64) {
       const char *f = n.op == NUT_P_NOT ? "not" : n.op == NUT_P_BITNOT ? "~" : n.op == NUT_P_ABS ? "abs" : "toFloat64";
       st.push_back(std::string(f) + "(" + pop() + ")");
     } else if (n.op == NUT_P_IF) {
@@ -1411,7 +1602,7 @@ std::string describe(const nut_plan &p) {
     o += ",\"keys\":[";
     for (size_t i = 0; i < p.keys.size(); ++i) {
       if (i) o += ',';
-      json_str(o, p.cols[p.keys[i]]);
+      json_str(o, p.keys[i] >= 0 ? p.cols[p.keys[i]] : p.key_text[i]);
     }
     o += "],\"values\":[";
     for (size_t i = 0; i < p.vals.size(); ++i) {
@@ -1423,8 +1614,12 @@ std::string describe(const nut_plan &p) {
       const PlanAgg &a = p.aggs[i];
       if (i) o += ',';
       o += "{\"op\":\"";
-      o += aggs[a.op];
+      o += a.distinct ? "count_distinct" : aggs[a.op];
       o += "\"";
+      if (a.distinct) {
+        o += ",\"expr\":";
+        json_str(o, prog_text(p, a.val));
+      }
       if (p.compiled) {
         if (a.op != NUT_AGG_COUNT) {
           o += ",\"expr\":";
@@ -1479,7 +1674,8 @@ std::string describe(const nut_plan &p) {
     if (u.hidden) o += ",\"hidden\":true";
     o += u.kind == OUT_KEY ? ",\"from\":\"key\",\"index\":" + std::to_string(u.a)
          : u.kind == OUT_AGG ? ",\"from\":\"agg\",\"index\":" + std::to_string(u.a)
-                             : ",\"from\":\"avg\",\"sum\":" + std::to_string(u.a) + ",\"count\":" + std::to_string(u.b);
+         : u.kind == OUT_EXPR ? ",\"from\":\"expr\",\"expr\":" + std::to_string(u.a)
+                              : ",\"from\":\"avg\",\"sum\":" + std::to_string(u.a) + ",\"count\":" + std::to_string(u.b);
     o += "}";
   }
   o += "],\"having\":";
@@ -1612,8 +1808,25 @@ struct ProgStore {
   std::deque<DevBuf> tables;
 };
 
+// Key programs and countUnique arguments of a compiled aggregate plan, resolved against
+// the spec's program columns (exec_groupby packs them into key words)
+struct GbExtra {
+  bool active = false;            // keys are programs: computed keys, > 2 keys or countUnique
+  std::vector<int> slot;          // plan aggregate -> spec aggregate (-1: countUnique)
+  std::vector<nut_prog> key;      // per GROUP BY key
+  std::vector<nut_prog> cu_val, cu_mask;  // per plan aggregate (countUnique only)
+};
+bool needs_key_progs(const nut_plan &p) {
+  if (!p.compiled || p.kind != NUT_PLAN_GROUPBY) return false;
+  if (p.keys.size() > NUT_MAX_KEYS) return true;
+  for (int k : p.keys)
+    if (k < 0) return true;
+  for (const PlanAgg &a : p.aggs)
+    if (a.distinct) return true;
+  return false;
+}
 nut_status build_spec(const nut_plan &p, const nut_column *const *bound, const Dict *const *dicts, uint64_t n,
-                      nut_agg_spec &s, ProgStore &store, std::vector<int> &agg_f64);
+                      nut_agg_spec &s, ProgStore &store, std::vector<int> &agg_f64, GbExtra *gx = nullptr);
 PProg and_all(const std::vector<PProg> &cs);
 PProg pred_prog(const PlanPred &pr);
 
@@ -1885,11 +2098,20 @@ nut_status check_strings(const nut_plan &p, const PProg &pp, const Dict *const *
 }
 
 nut_status build_spec(const nut_plan &p, const nut_column *const *bound, const Dict *const *dicts, uint64_t n,
-                      nut_agg_spec &s, ProgStore &store, std::vector<int> &agg_f64) {
+                      nut_agg_spec &s, ProgStore &store, std::vector<int> &agg_f64, GbExtra *gx) {
   memset(&s, 0, sizeof s);
   s.n = p.never ? 0 : n;
-  s.nkeys = (int32_t)p.keys.size();
-  for (size_t j = 0; j < p.keys.size(); ++j) {
+  // keys that are programs are resolved below (and packed into key words by exec_groupby)
+  const bool keyprog = needs_key_progs(p);
+  if (gx) {
+    gx->active = keyprog;
+    gx->slot.assign(p.aggs.size(), -1);
+    gx->key.clear();
+    gx->cu_val.assign(p.aggs.size(), nut_prog{0, nullptr});
+    gx->cu_mask.assign(p.aggs.size(), nut_prog{0, nullptr});
+  }
+  s.nkeys = keyprog ? 0 : (int32_t)p.keys.size();
+  for (size_t j = 0; j < p.keys.size() && !keyprog; ++j) {
     const nut_column *k = bound[p.keys[j]];
     if (k->type != NUT_T_I64) return fail(NUT_ERR_PLAN, "GROUP BY column '" + p.cols[p.keys[j]] + "' must be int64");
     s.keys[j] = (const int64_t *)k->data;
@@ -1966,11 +2188,12 @@ nut_status build_spec(const nut_plan &p, const nut_column *const *bound, const D
       v.push_back(lk);
       return NUT_OK;
     };
-    auto resolve = [&](const PProg &pp, nut_prog &out, const char *what, int32_t *type) -> nut_status {
+    auto resolve = [&](const PProg &pp, nut_prog &out, const char *what, int32_t *type,
+                       bool str_ok = false) -> nut_status {
       store.nodes.emplace_back();
       std::vector<nut_prog_node> &v = store.nodes.back();
       for (const PNode &n : pp) {
-        nut_prog_node q{n.op, 0, 0};
+        nut_prog_node q{n.op, n.op == NUT_P_DATEPART ? n.arg : 0, 0};
         if (n.op == P_LIKE || n.op == P_ILIKE) {
           nut_status ls = lower_like(n, v);
           if (ls) return ls;
@@ -2008,7 +2231,7 @@ nut_status build_spec(const nut_plan &p, const nut_column *const *bound, const D
       }
       out.n = (int32_t)v.size();
       out.node = v.data();
-      if (dicts) {
+      if (dicts && !str_ok) {
         nut_status cs = check_strings(p, pp, dicts, what);
         if (cs) return cs;
       }
@@ -2023,15 +2246,32 @@ nut_status build_spec(const nut_plan &p, const nut_column *const *bound, const D
       st = resolve(p.where, s.where, "WHERE", &t);
       if (!st && t == NUT_PT_F64) st = fail(NUT_ERR_PLAN, "WHERE: a float64 expression is not a condition");
     }
-    s.naggs = (int32_t)p.aggs.size();
+    s.naggs = 0;
     for (size_t a = 0; a < p.aggs.size() && !st; ++a) {
       const PlanAgg &g = p.aggs[a];
-      s.agg_op[a] = g.op;
+      if (g.distinct) {  // countUnique: its own passes (exec_groupby)
+        if (!gx) continue;
+        st = resolve(g.val, gx->cu_val[a], "countUnique argument", &t, true);
+        if (!st && t == NUT_PT_F64) st = fail(NUT_ERR_PLAN, "countUnique of a float64 expression is not executed");
+        if (!st && g.val.size() != 1 && dicts) st = check_strings(p, g.val, dicts, "countUnique argument");
+        if (!st && !g.mask.empty()) st = resolve(g.mask, gx->cu_mask[a], "countUnique argument", &t);
+        continue;
+      }
+      const int k = s.naggs++;
+      if (gx) gx->slot[a] = k;
+      s.agg_op[k] = g.op;
       if (g.op != NUT_AGG_COUNT) {
-        st = resolve(g.val, s.agg_val[a], "aggregate argument", &t);
+        st = resolve(g.val, s.agg_val[k], "aggregate argument", &t);
         agg_f64[a] = t == NUT_PT_F64;
       }
-      if (!st && !g.mask.empty()) st = resolve(g.mask, s.agg_mask[a], "aggregate argument", &t);
+      if (!st && !g.mask.empty()) st = resolve(g.mask, s.agg_mask[k], "aggregate argument", &t);
+    }
+    for (size_t j = 0; j < p.key_progs.size() && !st && keyprog && gx; ++j) {
+      // a plain string column is a key of dictionary codes; computed keys are numbers
+      gx->key.emplace_back();
+      st = resolve(p.key_progs[j], gx->key.back(), "GROUP BY key", &t, p.keys[j] >= 0);
+      if (!st && t == NUT_PT_F64)
+        st = fail(NUT_ERR_PLAN, "GROUP BY key '" + p.key_text[j] + "' is float64 (keys are integers)");
     }
     if (st) return st;
   } else {
@@ -2148,22 +2388,343 @@ nut_status build_spec(const nut_plan &p, const nut_column *const *bound, const D
   return NUT_OK;
 }
 
+// ---- GROUP BY over key programs: computed keys, up to kMaxGroupKeys
+// keys, countUnique.  The group-by kernels take two 64-bit key words, so the key tuple is
+// packed: one range pass (MIN / MAX of every key program under WHERE) sizes each key's
+// field, keys are laid out in order from the top bit of word 0 (63 bits per word; a key
+// whose range needs 64 bits takes a word of its own, raw), and each word is a program
+// OR-ing (key - min) << shift — evaluated inside the same streaming kernel.  The packing is
+// order-preserving, so groups still arrive sorted by key tuple.  countUnique(x) adds x as a
+// last field: GROUP BY (keys, x), then a count per key-word tuple over those groups.
+struct KeyField {
+  nut_prog prog{0, nullptr};
+  int64_t mn = 0;
+  int bits = 64;  // 64: raw, a word of its own
+  int word = 0, shift = 0;
+};
+
+// place fields [0, f.size()) greedily; false if they need more than two words
+bool layout_fields(std::vector<KeyField> &f, int *nwords) {
+  int w = 0, used = 0;
+  for (KeyField &k : f) {
+    if (k.bits >= 64) {
+      if (used) ++w;
+      k.word = w;
+      k.shift = 0;
+      used = 64;
+    } else {
+      if (used + k.bits > 63) ++w, used = 0;
+      k.word = w;
+      k.shift = 63 - used - k.bits;
+      used += k.bits;
+    }
+    if (w >= NUT_MAX_KEYS) return false;
+  }
+  *nwords = f.empty() ? 0 : w + 1;
+  return true;
+}
+
+// the program of key word w: OR over its fields of (prog - mn) << shift (raw: prog);
+// `drop` >= 0: leave field `drop` out
+nut_status word_prog(const std::vector<KeyField> &f, int w, int drop, ProgStore &store, nut_prog &out) {
+  store.nodes.emplace_back();
+  std::vector<nut_prog_node> &v = store.nodes.back();
+  int terms = 0;
+  for (size_t j = 0; j < f.size(); ++j) {
+    const KeyField &k = f[j];
+    if (k.word != w || (int)j == drop) continue;
+    v.insert(v.end(), k.prog.node, k.prog.node + k.prog.n);
+    if (k.bits < 64) {
+      if (k.mn) {
+        v.push_back(nut_prog_node{NUT_P_I64, 0, k.mn});
+        v.push_back(nut_prog_node{NUT_P_SUB, 0, 0});
+      }
+      if (k.shift) {
+        v.push_back(nut_prog_node{NUT_P_I64, 0, k.shift});
+        v.push_back(nut_prog_node{NUT_P_SHL, 0, 0});
+      }
+    }
+    if (terms++) v.push_back(nut_prog_node{NUT_P_BITOR, 0, 0});
+  }
+  if (!terms) v.push_back(nut_prog_node{NUT_P_I64, 0, 0});
+  if (v.size() > NUT_MAX_PROG_NODES)
+    return fail(NUT_ERR_PLAN, "GROUP BY keys: the packed key word program exceeds 256 nodes");
+  out.n = (int32_t)v.size();
+  out.node = v.data();
+  return NUT_OK;
+}
+
+// AND of two programs (either may be empty)
+nut_prog and_prog(const nut_prog &a, const nut_prog &b, ProgStore &store) {
+  if (!a.n) return b;
+  if (!b.n) return a;
+  store.nodes.emplace_back(a.node, a.node + a.n);
+  std::vector<nut_prog_node> &v = store.nodes.back();
+  v.insert(v.end(), b.node, b.node + b.n);
+  v.push_back(nut_prog_node{NUT_P_AND, 0, 0});
+  return nut_prog{(int32_t)v.size(), v.data()};
+}
+
+// run a group-by and copy its groups to the host (keys [ng x nk], words [ng x na])
+nut_status run_groupby(nut_ctx *c, const nut_agg_spec &s, uint64_t hint, std::vector<int64_t> &keys,
+                       std::vector<uint64_t> &words, uint64_t &ng) {
+  nut_groups *g = nullptr;
+  nut_status st = nut_groupby(c, &s, hint, &g);
+  if (st) return st;
+  st = nut_groups_size(g, &ng);
+  if (!st) {
+    keys.assign(ng * std::max(s.nkeys, 1) + 1, 0);
+    words.assign(ng * std::max(s.naggs, 1) + 1, 0);
+    st = nut_groups_to_host(g, keys.data(), words.data(), ng);
+  }
+  nut_groups_free(g);
+  return st;
+}
+
+nut_status groupby_packed(nut_ctx *c, const nut_plan &p, const nut_agg_spec &s, const GbExtra &gx, ProgStore &store,
+                          uint64_t hint, std::vector<int64_t> &keys, std::vector<uint64_t> &words, uint64_t &ng) {
+  const size_t nkey = gx.key.size(), na = p.aggs.size();
+  ng = 0;
+  keys.assign(1, 0);
+  words.assign(1, 0);
+  if (!s.n) return NUT_OK;  // no rows: no groups
+  std::vector<int> cus;  // countUnique aggregates
+  for (size_t a = 0; a < na; ++a)
+    if (p.aggs[a].distinct) cus.push_back((int)a);
+  // fields: the keys, then each countUnique argument
+  std::vector<KeyField> fk(nkey);
+  for (size_t j = 0; j < nkey; ++j) fk[j].prog = gx.key[j];
+  std::vector<KeyField> fx(cus.size());
+  for (size_t i = 0; i < cus.size(); ++i) fx[i].prog = gx.cu_val[cus[i]];
+  ng = 0;
+  const bool ranges = nkey > NUT_MAX_KEYS || !cus.empty();
+  if (ranges && s.n) {
+    // MIN / MAX of every field under WHERE (a countUnique argument under its mask too)
+    std::vector<std::pair<KeyField *, nut_prog>> all;
+    for (KeyField &k : fk) all.push_back({&k, nut_prog{0, nullptr}});
+    for (size_t i = 0; i < cus.size(); ++i) all.push_back({&fx[i], gx.cu_mask[cus[i]]});
+    for (size_t b = 0; b < all.size(); b += NUT_MAX_AGGS / 2) {
+      nut_agg_spec r = s;
+      r.nkeys = 0;
+      r.naggs = 0;
+      for (size_t j = b; j < all.size() && j < b + NUT_MAX_AGGS / 2; ++j)
+        for (int op : {NUT_AGG_MIN, NUT_AGG_MAX}) {
+          r.agg_op[r.naggs] = op;
+          r.agg_val[r.naggs] = all[j].first->prog;
+          r.agg_mask[r.naggs] = all[j].second;
+          r.naggs++;
+        }
+      std::vector<int64_t> rk;
+      std::vector<uint64_t> rw;
+      uint64_t rg = 0;
+      nut_status st = run_groupby(c, r, 1, rk, rw, rg);
+      if (st) return st;
+      if (rg == 0) return NUT_OK;  // no row passes WHERE: no groups
+      for (size_t j = b; j < all.size() && j < b + NUT_MAX_AGGS / 2; ++j) {
+        const int64_t mn = (int64_t)rw[2 * (j - b)], mx = (int64_t)rw[2 * (j - b) + 1];
+        KeyField &k = *all[j].first;
+        if (mx < mn) {  // a masked argument that took no row
+          k.mn = 0;
+          k.bits = 0;
+          continue;
+        }
+        const uint64_t range = (uint64_t)mx - (uint64_t)mn;
+        k.mn = mn;
+        k.bits = range ? 64 - __builtin_clzll(range) : 0;
+      }
+    }
+  }
+  int nwk = 0;
+  if (!layout_fields(fk, &nwk))
+    return fail(NUT_ERR_UNSUPPORTED, "GROUP BY keys: their value ranges need more than 2 x 63 bits packed (" +
+                                         std::to_string(nkey) + " keys)");
+  // main pass: the keys as packed words, the plan's other aggregates
+  nut_agg_spec m = s;
+  m.nkeys = nwk;
+  for (int w = 0; w < nwk; ++w) {
+    nut_status st = word_prog(fk, w, -1, store, m.key_prog[w]);
+    if (st) return st;
+  }
+  const bool dummy = m.naggs == 0;  // (only countUnique aggregates: a COUNT enumerates groups)
+  if (dummy) {
+    m.naggs = 1;
+    m.agg_op[0] = NUT_AGG_COUNT;
+  }
+  std::vector<int64_t> kw;
+  std::vector<uint64_t> sw;
+  nut_status st = run_groupby(c, m, hint, kw, sw, ng);
+  if (st) return st;
+  const int nkw = std::max(nwk, 1);
+  // unpack the key tuples
+  const size_t nk = std::max<size_t>(nkey, 1);
+  keys.assign(ng * nk + 1, 0);
+  for (uint64_t i = 0; i < ng; ++i)
+    for (size_t j = 0; j < nkey; ++j) {
+      const KeyField &k = fk[j];
+      const uint64_t word = (uint64_t)kw[i * nkw + k.word];
+      keys[i * nk + j] = k.bits >= 64 ? (int64_t)word
+                                      : (int64_t)(((word >> k.shift) & ((1ull << k.bits) - 1)) + (uint64_t)k.mn);
+    }
+  words.assign(ng * na + 1, 0);
+  for (size_t a = 0; a < na; ++a)
+    if (gx.slot[a] >= 0)
+      for (uint64_t i = 0; i < ng; ++i) words[i * na + a] = sw[i * m.naggs + gx.slot[a]];
+  // countUnique: GROUP BY (key words, x) -> its groups on the device -> COUNT per key words
+  for (size_t ci = 0; ci < cus.size() && ng; ++ci) {
+    const int a = cus[ci];
+    std::vector<KeyField> f1 = fk;
+    f1.push_back(fx[ci]);
+    int nw1 = 0;
+    if (!layout_fields(f1, &nw1))
+      return fail(NUT_ERR_UNSUPPORTED, "countUnique: the keys and its argument need more than 2 x 63 bits packed");
+    nut_agg_spec q1 = s;
+    q1.where = and_prog(s.where, gx.cu_mask[a], store);
+    q1.nkeys = nw1;
+    for (int w = 0; w < nw1; ++w) {
+      st = word_prog(f1, w, -1, store, q1.key_prog[w]);
+      if (st) return st;
+    }
+    q1.naggs = 1;
+    memset(q1.agg_mask, 0, sizeof q1.agg_mask);
+    memset(q1.agg_val, 0, sizeof q1.agg_val);
+    q1.agg_op[0] = NUT_AGG_COUNT;
+    nut_groups *g1 = nullptr;
+    st = nut_groupby(c, &q1, 0, &g1);
+    if (st) return st;
+    uint64_t n1 = 0;
+    st = nut_groups_size(g1, &n1);
+    DevBuf d1;
+    if (!st && n1) {
+      if (d1.alloc(c, (size_t)(nw1 + 1) * n1 * 8) != hipSuccess) st = fail(NUT_ERR_OOM, "hipMalloc (countUnique)");
+      if (!st) st = nut_groups_to_device(g1, (uint64_t *)d1.p, n1);
+    }
+    nut_groups_free(g1);
+    if (st) return st;
+    std::vector<int64_t> k2;
+    std::vector<uint64_t> w2;
+    uint64_t n2 = 0;
+    if (n1) {
+      // the pass-1 groups' key words with x's bits cleared are the main pass's key words
+      nut_agg_spec q2;
+      memset(&q2, 0, sizeof q2);
+      q2.n = n1;
+      q2.prog_mode = 1;
+      q2.nprog_cols = nw1;
+      for (int w = 0; w < nw1; ++w) {
+        q2.prog_col[w] = (const uint64_t *)d1.p + (size_t)w * n1;
+        q2.prog_col_type[w] = NUT_T_I64;
+      }
+      const KeyField &x = f1.back();
+      q2.nkeys = nwk;
+      for (int w = 0; w < nwk; ++w) {
+        store.nodes.emplace_back();
+        std::vector<nut_prog_node> &v = store.nodes.back();
+        v.push_back(nut_prog_node{NUT_P_COL, w, 0});
+        if (x.word == w && x.bits < 64 && x.bits > 0) {
+          v.push_back(nut_prog_node{NUT_P_I64, 0, (int64_t)~(((1ull << x.bits) - 1) << x.shift)});
+          v.push_back(nut_prog_node{NUT_P_BITAND, 0, 0});
+        }
+        q2.key_prog[w] = nut_prog{(int32_t)v.size(), v.data()};
+      }
+      q2.naggs = 1;
+      q2.agg_op[0] = NUT_AGG_COUNT;
+      st = run_groupby(c, q2, ng, k2, w2, n2);
+      if (st) return st;
+    }
+    // both group lists are sorted by key words: merge
+    uint64_t j = 0;
+    for (uint64_t i = 0; i < ng; ++i) {
+      auto cmp = [&](uint64_t jj) {
+        for (int w = 0; w < nwk; ++w) {
+          const int64_t x0 = kw[i * nkw + w], y0 = k2[jj * nwk + w];
+          if (x0 != y0) return x0 < y0 ? -1 : 1;
+        }
+        return 0;
+      };
+      while (j < n2 && nwk && cmp(j) > 0) ++j;
+      words[i * na + a] = (j < n2 && (nwk == 0 || cmp(j) == 0)) ? w2[nwk ? j : 0] : 0;
+    }
+  }
+  return NUT_OK;
+}
+
+// evaluation of an OUT_EXPR output for group i (nut_prog arithmetic semantics)
+struct XVal {
+  bool is_int;
+  int64_t i;
+  double f;
+  double as_f() const { return is_int ? (double)i : f; }
+};
+XVal xpr_eval(const XNode &x, const std::vector<std::vector<uint64_t>> &cols, const std::vector<int> &types,
+              uint64_t g, bool &div0) {
+  if (x.k == X_CONST) return XVal{x.is_int, x.i, x.f};
+  if (x.k == X_OUT) {
+    const uint64_t w = cols[x.out][g];
+    if (types[x.out] != NUT_T_F64) return XVal{true, (int64_t)w, 0.0};
+    double f;
+    memcpy(&f, &w, 8);
+    return XVal{false, 0, f};
+  }
+  const XVal a = xpr_eval(x.kids[0], cols, types, g, div0);
+  if (x.k == X_ABS) return a.is_int ? XVal{true, a.i < 0 ? (int64_t)(0 - (uint64_t)a.i) : a.i, 0.0} : XVal{false, 0, fabs(a.f)};
+  if (x.k == X_TOF) return XVal{false, 0, a.as_f()};
+  const XVal b = xpr_eval(x.kids[1], cols, types, g, div0);
+  const bool ii = a.is_int && b.is_int;
+  switch (x.k) {
+    case X_ADD: return ii ? XVal{true, (int64_t)((uint64_t)a.i + (uint64_t)b.i), 0.0} : XVal{false, 0, a.as_f() + b.as_f()};
+    case X_SUB: return ii ? XVal{true, (int64_t)((uint64_t)a.i - (uint64_t)b.i), 0.0} : XVal{false, 0, a.as_f() - b.as_f()};
+    case X_MUL: return ii ? XVal{true, (int64_t)((uint64_t)a.i * (uint64_t)b.i), 0.0} : XVal{false, 0, a.as_f() * b.as_f()};
+    case X_DIV: return XVal{false, 0, a.as_f() / b.as_f()};
+    case X_MOD:
+    case X_INTDIV:
+      if (!ii) {
+        if (x.k == X_INTDIV) {
+          div0 = true;  // (reported as a plan error by the caller's type check)
+          return XVal{false, 0, 0.0};
+        }
+        return XVal{false, 0, fmod(a.as_f(), b.as_f())};
+      }
+      if (b.i == 0) {
+        div0 = true;
+        return XVal{true, 0, 0.0};
+      }
+      if (b.i == -1) return XVal{true, x.k == X_MOD ? 0 : (int64_t)(0 - (uint64_t)a.i), 0.0};
+      return XVal{true, x.k == X_MOD ? a.i % b.i : a.i / b.i, 0.0};
+    default: return XVal{true, 0, 0.0};
+  }
+}
+// static type of an OUT_EXPR (NUT_T_I64 / NUT_T_F64); -1: intDiv of a float64
+int xpr_type(const XNode &x, const std::vector<int> &types) {
+  if (x.k == X_CONST) return x.is_int ? NUT_T_I64 : NUT_T_F64;
+  if (x.k == X_OUT) return types[x.out] == NUT_T_F64 ? NUT_T_F64 : NUT_T_I64;
+  if (x.k == X_TOF || x.k == X_DIV) {
+    for (const XNode &k : x.kids)
+      if (xpr_type(k, types) < 0) return -1;
+    return NUT_T_F64;
+  }
+  int t = NUT_T_I64;
+  for (const XNode &k : x.kids) {
+    const int tk = xpr_type(k, types);
+    if (tk < 0) return -1;
+    if (tk == NUT_T_F64) t = NUT_T_F64;
+  }
+  if (x.k == X_INTDIV && t == NUT_T_F64) return -1;
+  return t;
+}
+
 nut_status exec_groupby(nut_ctx *c, const nut_plan &p, const nut_column *const *bound, const Dict *const *dicts,
                         uint64_t n, uint64_t hint, nut_result *r) {
   nut_agg_spec s;
   ProgStore store;  // program nodes, alive until nut_groupby returns
   std::vector<int> agg_f64;
-  nut_status bs = build_spec(p, bound, dicts, n, s, store, agg_f64);
+  GbExtra gx;
+  nut_status bs = build_spec(p, bound, dicts, n, s, store, agg_f64, &gx);
   if (bs) return bs;
-  nut_groups *g = nullptr;
-  nut_status st = nut_groupby(c, &s, hint, &g);
-  if (st) return st;
   uint64_t ng = 0;
-  st = nut_groups_size(g, &ng);
-  std::vector<int64_t> keys(ng * std::max<size_t>(p.keys.size(), 1) + 1);
-  std::vector<uint64_t> words(ng * p.aggs.size() + 1);
-  if (!st) st = nut_groups_to_host(g, keys.data(), words.data(), ng);
-  nut_groups_free(g);
+  std::vector<int64_t> keys;
+  std::vector<uint64_t> words;
+  nut_status st = gx.active ? groupby_packed(c, p, s, gx, store, hint, keys, words, ng)
+                            : run_groupby(c, s, hint, keys, words, ng);
   if (st) return st;
   const size_t nk = std::max<size_t>(p.keys.size(), 1), na = p.aggs.size();
   if (p.keys.empty() && ng == 0) {
@@ -2181,8 +2742,10 @@ nut_status exec_groupby(nut_ctx *c, const nut_plan &p, const nut_column *const *
     std::vector<uint64_t> &col = r->host[j];
     col.resize(ng);
     int type = NUT_T_I64;
-    if (o.kind == OUT_KEY) {
-      if (dicts && dicts[p.keys[o.a]]) {
+    if (o.kind == OUT_EXPR) {
+      type = -1;  // below, once every other output is known
+    } else if (o.kind == OUT_KEY) {
+      if (dicts && p.keys[o.a] >= 0 && dicts[p.keys[o.a]]) {
         type = NUT_T_STR;
         out_dict[j] = dicts[p.keys[o.a]];
       }
@@ -2205,6 +2768,34 @@ nut_status exec_groupby(nut_ctx *c, const nut_plan &p, const nut_column *const *
     }
     r->names.push_back(o.name);
     r->types.push_back(type);
+  }
+  // arithmetic over the outputs (its operands are keys / aggregates / avg, never OUT_EXPR)
+  for (size_t j = 0; j < p.outs.size(); ++j) {
+    const PlanOut &o = p.outs[j];
+    if (o.kind != OUT_EXPR) continue;
+    const XNode &x = p.xprs[o.a];
+    std::vector<const XNode *> todo{&x};
+    while (!todo.empty()) {
+      const XNode *y = todo.back();
+      todo.pop_back();
+      if (y->k == X_OUT && r->types[y->out] == NUT_T_STR)
+        return fail(NUT_ERR_PLAN, "'" + o.text + "': arithmetic on the string key '" + p.outs[y->out].name + "'");
+      for (const XNode &k : y->kids) todo.push_back(&k);
+    }
+    const int t = xpr_type(x, r->types);
+    if (t < 0) return fail(NUT_ERR_PLAN, "'" + o.text + "': intDiv needs integer operands");
+    bool div0 = false;
+    for (uint64_t i = 0; i < ng; ++i) {
+      const XVal v = xpr_eval(x, r->host, r->types, i, div0);
+      if (t == NUT_T_I64) {
+        r->host[j][i] = (uint64_t)v.i;
+      } else {
+        const double f = v.as_f();
+        memcpy(&r->host[j][i], &f, 8);
+      }
+    }
+    if (div0) return fail(NUT_ERR_INVALID_ARG, "'" + o.text + "': division by zero");
+    r->types[j] = t;
   }
   // HAVING, then ORDER BY over outputs (groups arrive sorted by key tuple), then LIMIT
   if (p.has_having) {
@@ -2429,6 +3020,7 @@ nut_status exec_join(nut_ctx *c, const nut_plan &p, const nut_column *lc, int nl
     row = ci == q.proj || in_prog(q.where, ci);
     for (int pj : q.projs) row = row || pj == ci;
     for (int k : q.keys) row = row || k == ci;
+    for (const PProg &kp : q.key_progs) row = row || in_prog(kp, ci);  // computed keys
     for (const auto &sk : q.sort_keys) row = row || sk.first == ci;  // ORDER BY, projected or not
     for (const PlanPred &pr : q.preds) row = row || pr.col == ci;
     agg = false;
@@ -2690,6 +3282,7 @@ nut_status exec_joinn(nut_ctx *c, const nut_plan &p, const nut_column *const *ta
     row = ci == q.proj || in_prog(q.where, ci);
     for (int pj : q.projs) row = row || pj == ci;
     for (int k2 : q.keys) row = row || k2 == ci;
+    for (const PProg &kp : q.key_progs) row = row || in_prog(kp, ci);  // computed keys
     for (const auto &sk : q.sort_keys) row = row || sk.first == ci;  // ORDER BY, projected or not
     for (const PlanPred &pr : q.preds) row = row || pr.col == ci;
     agg = false;

@@ -158,7 +158,8 @@ class ProgQuery:
     """Expression mode of nut_groupby (include/nutexec.h nut_prog): WHERE and every
     aggregate argument are RPN programs over `cols`, compiled for the query at run time
     (csrc/jit.cpp).  aggs = [(op, value program or None, mask program or None)]: the
-    mask keeps only rows where it is true (CASE without ELSE)."""
+    mask keeps only rows where it is true (CASE without ELSE).  A key is an int64 column
+    or an int64 / bool program over `cols` (a computed key: nut_agg_spec.key_prog)."""
     keys: list
     cols: list
     aggs: list
@@ -169,13 +170,16 @@ class ProgQuery:
         s = L.NutAggSpec()
         keep = []
         s._keep = keep  # node arrays live as long as the spec
-        cols = list(self.keys) + list(self.cols)
+        cols = [k for k in self.keys if isinstance(k, torch.Tensor)] + list(self.cols)
         n = int(cols[0].numel()) if cols else int(self.rows or 0)
         s.n = n
         if not 0 <= len(self.keys) <= L.NUT_MAX_KEYS:
             raise ValueError("0, 1 or 2 group keys")
         s.nkeys = len(self.keys)
         for i, k in enumerate(self.keys):
+            if not isinstance(k, torch.Tensor):
+                s.key_prog[i] = _prog(k, keep)
+                continue
             if k.dtype != torch.int64 or k.numel() != n:
                 raise ValueError("group keys are int64 columns of equal length")
             s.keys[i] = _col(k, dev)

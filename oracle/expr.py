@@ -12,7 +12,9 @@ column-at-a-time with numpy, independently of the generated HIP code:
   * AND / OR / XOR / NOT over bools (ints: non-zero = true), both operands evaluated;
   * bit ops and shifts on ints; shift counts outside [0, 63] give 0 (SHR of a
     negative value: -1); SHR is arithmetic;
-  * IF takes the chosen branch's value and only the chosen branch's errors.
+  * IF takes the chosen branch's value and only the chosen branch's errors;
+  * DATEPART (arg = nut_date_part) of a day number (days since 1970-01-01, clamped to
+    +-2^40): proleptic Gregorian civil-from-days with truncating division.
 
 Errors are tracked per row (a bool array); the group-by rule is the kernel's
 (agg_kernel.hpp consume_rows): a WHERE error counts for every row, an aggregate's mask
@@ -28,10 +30,46 @@ from __future__ import annotations
 import numpy as np
 
 OPS = ["col", "i64", "f64", "add", "sub", "mul", "div", "mod", "intdiv", "lt", "le", "gt", "ge", "eq", "ne",
-       "and", "or", "xor", "not", "bitand", "bitor", "bitxor", "bitnot", "shl", "shr", "if", "abs", "to_f64"]
+       "and", "or", "xor", "not", "bitand", "bitor", "bitxor", "bitnot", "shl", "shr", "if", "abs", "to_f64",
+       "lookup", "datepart"]
 OP = {name: i for i, name in enumerate(OPS)}
 I64, F64, BOOL = 0, 1, 2
-_ARITY = {OP["not"]: 1, OP["bitnot"]: 1, OP["abs"]: 1, OP["to_f64"]: 1, OP["if"]: 3}
+_ARITY = {OP["not"]: 1, OP["bitnot"]: 1, OP["abs"]: 1, OP["to_f64"]: 1, OP["if"]: 3, OP["lookup"]: 1,
+          OP["datepart"]: 1}
+DP_YEAR, DP_MONTH, DP_DAY, DP_QUARTER, DP_WEEKDAY, DP_YEARDAY = range(6)
+
+
+def _tdiv(a, b: int):
+    """int64 division truncating toward zero by a positive constant b."""
+    q = np.floor_divide(a, b)
+    return q + ((a - q * b != 0) & (a < 0))
+
+
+def date_part(days, part: int):
+    """nut_date_part `part` of day numbers (int64 array), as nut_prog DATEPART computes it."""
+    d = np.clip(np.asarray(days, dtype=np.int64), -(1 << 40), 1 << 40)
+    z = d + 719468
+    era = _tdiv(np.where(z >= 0, z, z - 146096), 146097)
+    doe = z - era * 146097
+    yoe = _tdiv(doe - _tdiv(doe, 1460) + _tdiv(doe, 36524) - _tdiv(doe, 146096), 365)
+    doy = doe - (365 * yoe + _tdiv(yoe, 4) - _tdiv(yoe, 100))
+    mp = _tdiv(5 * doy + 2, 153)
+    m = np.where(mp < 10, mp + 3, mp - 9)
+    y = yoe + era * 400 + (m <= 2)
+    if part == DP_YEAR:
+        return y
+    if part == DP_MONTH:
+        return m
+    if part == DP_DAY:
+        return doy - _tdiv(153 * mp + 2, 5) + 1
+    if part == DP_QUARTER:
+        return _tdiv(m - 1, 3) + 1
+    if part == DP_WEEKDAY:
+        return (d + 3) % 7 + 1  # numpy % is floor-mod: 1970-01-01 (day 0) is a Thursday (4)
+    if part == DP_YEARDAY:
+        leap = ((y % 4 == 0) & (y % 100 != 0)) | (y % 400 == 0)
+        return np.where(doy >= 306, doy - 305, doy + 60 + leap)
+    raise ProgramError(f"unknown date part {part}")
 
 
 class ProgramError(ValueError):
@@ -156,6 +194,8 @@ def eval_prog(nodes, cols, n=None):
                 r = (np.abs(_f(a[0])), F64) if a[0][1] == F64 else (np.abs(_i(a[0])), I64)
             elif op == OP["to_f64"]:
                 r = (_f(a[0]), F64)
+            elif op == OP["datepart"]:
+                r = (date_part(_i(a[0]), int(arg)).astype(np.int64), I64)
             else:
                 raise ProgramError(f"unknown op {op}")
             st.append((r[0], r[1], err))
@@ -168,15 +208,17 @@ def eval_prog(nodes, cols, n=None):
 
 
 def groupby_prog(keys, cols, where, aggs, n=None):
-    """Expression-mode group-by: keys = list of int64 arrays (empty = global aggregate),
-    where = nodes or None, aggs = [(op, val_nodes or None, mask_nodes or None)] with op
-    0 SUM / 1 COUNT / 2 MIN / 3 MAX.  Returns (keys, words, types) like
-    oracle.groupby (words = result bits) plus each aggregate's value type; raises
-    DivisionByZero under the kernel's error rule."""
+    """Expression-mode group-by: keys = list of int64 arrays or key programs (node lists,
+    int64 / bool; any number of keys; empty = global aggregate), where = nodes or None,
+    aggs = [(op, val_nodes or None, mask_nodes or None)] with op 0 SUM / 1 COUNT / 2 MIN /
+    3 MAX.  Returns (keys, words, types) like oracle.groupby (words = result bits, groups
+    ordered by key tuple) plus each aggregate's value type; raises DivisionByZero under the
+    kernel's error rule (a key program's error counts for rows passing WHERE)."""
     from . import oracle as orc
 
     if n is None:
-        n = len(keys[0]) if keys else len(cols[0])
+        arrs = [k for k in keys if isinstance(k, np.ndarray)]
+        n = len(arrs[0]) if arrs else len(cols[0])
     ok = np.ones(n, dtype=bool)
     bad = np.zeros(n, dtype=bool)
     if where:
@@ -185,6 +227,17 @@ def groupby_prog(keys, cols, where, aggs, n=None):
             raise ProgramError("WHERE is float64")
         ok = w != 0
         bad |= e
+    kv = []
+    for k in keys:
+        if isinstance(k, np.ndarray):
+            kv.append(k.astype(np.int64))
+            continue
+        x, t, e = eval_prog(k, cols, n)
+        if t == F64:
+            raise ProgramError("float64 key program")
+        bad |= ok & e
+        kv.append(x.astype(np.int64))
+    keys = kv
     values, masks, spec, types = [], [], [], []
     for a, (op, val, mask) in enumerate(aggs):
         m = None
@@ -206,5 +259,13 @@ def groupby_prog(keys, cols, where, aggs, n=None):
     if bad.any():
         raise DivisionByZero("division by zero in an expression")
     kk = list(keys) if keys else [np.zeros(n, dtype=np.int64)]
-    ok_keys, words = orc.groupby(kk, spec, values=values, row_mask=ok, agg_masks=masks)
-    return ok_keys, words, types
+    if len(kk) <= 2:
+        ok_keys, words = orc.groupby(kk, spec, values=values, row_mask=ok, agg_masks=masks)
+        return ok_keys, words, types
+    # more keys than the C oracle takes: the tuple's rank among the distinct tuples (numpy
+    # sorts them lexicographically) is one key with the same grouping and order
+    tup = np.stack(kk, axis=1)
+    uniq, rank = np.unique(tup, axis=0, return_inverse=True)
+    ok_rank, words = orc.groupby([rank.reshape(-1).astype(np.int64)], spec, values=values, row_mask=ok,
+                                 agg_masks=masks)
+    return uniq[ok_rank[:, 0]], words, types

@@ -298,9 +298,11 @@ def test_plan_select_distinct():
     d = Plan("select distinct k, j from t where x > 3 order by k desc limit 5").describe()
     assert d["kind"] == "groupby" and d["keys"] == ["k", "j"] and d["aggs"] == [{"op": "count"}]
     assert [o["name"] for o in d["outputs"]] == ["k", "j"]
+    d = Plan("select distinct a, b, c from t").describe()
+    assert d["mode"] == "compiled" and d["keys"] == ["a", "b", "c"]
     for sql, msg in [("select distinct count(*) from t", "over aggregates"),
                      ("select distinct k from t group by k", "with GROUP BY"),
-                     ("select distinct a, b, c from t", "1 or 2 columns")]:
+                     ("select distinct a, b, c, d, e, f, g, h, i from t", "1 to 8 columns")]:
         with pytest.raises(NutError, match=msg):
             Plan(sql)
 
@@ -311,3 +313,79 @@ def test_plan_like():
     assert Plan("select s from t where s not like '%Z'").describe()["where_expr"] == "not((s like '%Z'))"
     with pytest.raises(NutError, match="string pattern"):
         Plan("select count(*) from t where s like 3")
+
+
+# ------------------------------------------------------------------ GROUP BY keys (§3.6)
+def test_plan_many_and_computed_keys():
+    d = Plan("select a, b, c, count(*) from t group by a, b, c").describe()
+    assert d["mode"] == "compiled" and d["keys"] == ["a", "b", "c"]
+    assert [o["from"] for o in d["outputs"]] == ["key", "key", "key", "agg"]
+    # a SELECT alias names its expression; getYear is ClickHouse's toYear
+    d = Plan("select getYear(d) as y, sum(v) from t group by y order by y").describe()
+    assert d["keys"] == ["getYear(d)"] and d["outputs"][0] == {"name": "y", "from": "key", "index": 0}
+    d = Plan("select toMonth(d), a % 10 as r, count() from t group by toMonth(d), r").describe()
+    assert d["keys"] == ["toMonth(d)", "a % 10"] and [o["from"] for o in d["outputs"]] == ["key", "key", "agg"]
+    # date functions of constants fold
+    d = Plan("select count() from t where getYear(d) = getYear(toDate('1996-03-01')) "
+             "and toDayOfWeek(d) < toDayOfWeek(toDate('2024-06-09'))").describe()
+    assert d["where_expr"] == "((toYear(d) = 1996) and (toDayOfWeek(d) < 7))"
+    with pytest.raises(NutError, match="1 to 8 keys"):
+        Plan("select count() from t group by a, b, c, d, e, f, g, h, i")
+    with pytest.raises(NutError, match="neither a GROUP BY key"):
+        Plan("select a, b, count() from t group by a, c, d")
+
+
+def test_plan_count_unique_and_output_arithmetic():
+    d = Plan("select k, countUnique(x) as u, uniqExact(x), sum(v) / count() as m, 100.0 * sum(v) / sum(w) "
+             "from t group by k having sum(v) - sum(w) > 3 order by m desc").describe()
+    assert d["aggs"][0] == {"op": "count_distinct", "expr": "x"}
+    assert [o["from"] for o in d["outputs"] if not o.get("hidden")] == ["key", "agg", "agg", "expr", "expr"]
+    assert d["outputs"][2]["index"] == d["outputs"][1]["index"]  # uniqExact(x) = countUnique(x)
+    d = Plan("select countUnique(case when v > 0 then x end) from t").describe()
+    assert d["keys"] == [] and d["aggs"][0]["op"] == "count_distinct" and "mask" in d["aggs"][0]
+    for sql, msg in [("select k, sum(v) > 3 from t group by k", "not executed over aggregates"),
+                     ("select k, v + sum(v) from t group by k", "not a GROUP BY key, an aggregate"),
+                     ("select k, countUnique(x, y) from t group by k", "takes one argument")]:
+        with pytest.raises(NutError, match=msg):
+            Plan(sql)
+
+
+def test_jit_compiles_key_programs():
+    """computed keys (nut_agg_spec.key_prog) compile into the streaming kernel (hipRTC)"""
+    import torch
+    cols = [_FakeCol(torch.int64), _FakeCol(torch.float64)]
+    yr = [("col", 0), ("datepart", L.DP_YEAR), ("i64", 0, 1970), ("sub",), ("i64", 0, 40), ("shl",),
+          ("col", 0), ("datepart", L.DP_MONTH), ("bitor",)]
+    q = ProgQuery(keys=[yr, [("col", 0), ("i64", 0, 7), ("mod",)]], cols=cols,
+                  aggs=[("sum", [("col", 1)], None), ("count", None, None)])
+    src = jit_source(q)
+    assert "kKeyProg = 3" in src and "jdatepart(" in src
+    assert L.lib.nut_groupby_jit_compile(C.byref(q.to_spec(None))) == 0, L.lib.nut_last_error()
+    bad = ProgQuery(keys=[[("col", 1)]], cols=cols, aggs=[("count", None, None)])
+    assert L.lib.nut_groupby_jit_compile(C.byref(bad.to_spec(None))) != 0
+    assert b"float64" in L.lib.nut_last_error()
+
+
+def test_date_part_oracle_matches_calendar():
+    """oracle.expr.date_part (the DATEPART restatement) against Python's proleptic
+    Gregorian calendar, years 1 .. 9999"""
+    import datetime
+    from oracle.expr import date_part
+    rng = np.random.default_rng(3)
+    lo, hi = datetime.date(1, 1, 1).toordinal(), datetime.date(9999, 12, 31).toordinal()
+    epoch = datetime.date(1970, 1, 1).toordinal()
+    ords = np.concatenate([rng.integers(lo, hi + 1, 20000), np.arange(epoch - 800, epoch + 800),
+                           [lo, hi, datetime.date(2000, 2, 29).toordinal(), datetime.date(1900, 3, 1).toordinal()]])
+    days = (ords - epoch).astype(np.int64)
+    dates = [datetime.date.fromordinal(int(o)) for o in ords]
+    want = {
+        0: [x.year for x in dates], 1: [x.month for x in dates], 2: [x.day for x in dates],
+        3: [(x.month - 1) // 3 + 1 for x in dates], 4: [x.isoweekday() for x in dates],
+        5: [x.timetuple().tm_yday for x in dates],
+    }
+    for part, w in want.items():
+        assert date_part(days, part).tolist() == w, part
+    # beyond any date the input is clamped to +-2^40 days
+    big = np.array([2**62, -2**62, 2**40, -2**40], dtype=np.int64)
+    assert date_part(big, 0).tolist() == [date_part(np.array([2**40]), 0)[0]] * 1 + \
+        [date_part(np.array([-2**40]), 0)[0]] + date_part(big[2:], 0).tolist()
