@@ -90,8 +90,8 @@ nut_status nut_ctx_kernel_time(nut_ctx *ctx, int kind, double *total_ms, uint64_
 nut_status nut_ctx_sort_stats(nut_ctx *ctx, uint64_t *bytes, uint32_t *levels);
 /* The algorithm the last nut_groupby on this context took (parity tests and bench lines
  * name the path they checked): path = nut_groupby_path, levels = partition levels of a
- * partitioned path (0 otherwise), optimistic = 1 when its first level ran without a
- * histogram pass. */
+ * partitioned path (0 otherwise), optimistic = how many of its leading levels ran without
+ * a histogram pass (capped layout: 0, 1 or 2). */
 typedef enum {
   NUT_GB_ONCHIP = 0,           /* streaming kernel, per-workgroup LDS tables (+ global table) */
   NUT_GB_PARTITIONED_DIRECT = 1, /* key-hash partition of the caller's columns, then LDS tables */
@@ -111,7 +111,9 @@ typedef enum {
   NUT_OPT_JOIN_REGION = 5,     /* 1 (default): LDS region build of large join tables */
   NUT_OPT_JOIN_PROBE_CFG = 6,  /* ordered probe tile shape 0..4 (0) */
   NUT_OPT_JOIN_ANY_CFG = 7,    /* unordered probe tile shape 0..4 (0) */
-  NUT_OPT_COUNT = 8
+  NUT_OPT_GB_SEG_SLOTS = 8,    /* partition aggregation: LDS slots per hinted group, 1..8 (2) */
+  NUT_OPT_GB_DENSE = 9,        /* 1 (default): whole partitions append their groups unhashed */
+  NUT_OPT_COUNT = 10
 } nut_option;
 nut_status nut_ctx_set_option(nut_ctx *ctx, int option, int64_t value);
 nut_status nut_ctx_get_option(nut_ctx *ctx, int option, int64_t *value);

@@ -453,7 +453,9 @@ __device__ __forceinline__ void consume_rows(const AggArgs &p, const LTable &lt,
   }
 #pragma unroll
   for (int r = 0; r < R; ++r) {
-    if (sl[r] == -1) {
+    if (sl[r] == -1 && NK == 1 && p.dense) {
+      atomicOr(&p.gt->ctl[1], 4u);  // dense mode needs every group on chip: the host reruns hashed
+    } else if (sl[r] == -1) {
       uint64_t g[8] = {0, 0, 0, 0, 0, 0, 0, 0};
       uint32_t m = 0;
 #pragma unroll
@@ -586,6 +588,55 @@ __global__ __launch_bounds__(BD) void agg_kernel(AggArgs p) {
   // merge the block's table into the global table
   const GTable t = *p.gt;
   const uint64_t gstr = t.cap + 1;
+  if (NK == 1 && p.dense) {
+    // the partition's groups are complete and no other block holds them: append them at
+    // slots claimed with one global atomic per block (no probing, no atomic merges); the
+    // table is a plain array afterwards (nut_groups.dense)
+    __shared__ uint32_t s_n;
+    __shared__ uint64_t s_base;
+    if (threadIdx.x == 0) s_n = 0;
+    __syncthreads();
+    for (uint32_t s = threadIdx.x; s < cap; s += BD) {
+      const uint64_t m = __ballot(lt.slot[s] != kEmpty);
+      if (m && (threadIdx.x & 63) == (uint32_t)__builtin_ctzll(m)) atomicAdd(&s_n, (uint32_t)__popcll(m));
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const uint64_t b = s_n ? atomicAdd(&t.shard[0], s_n) : 0;
+      if (b + s_n > t.limit) atomicOr(&t.ctl[1], 1u);  // more groups than the table holds: retried larger
+      s_base = b + s_n > t.limit ? ~0ull : b;
+      s_n = 0;
+    }
+    __syncthreads();
+    const uint64_t base = s_base;
+    for (uint32_t s = threadIdx.x; s < stride; s += BD) {
+      const uint64_t wd = lt.slot[s];
+      const bool occ = s < cap ? wd != kEmpty : lt.ctl[CTL_SPECIAL] != 0u;
+      const uint64_t m = __ballot(occ && s < cap);
+      uint32_t r = 0;
+      if (m) {
+        const int leader = __builtin_ctzll(m);
+        uint32_t b = 0;
+        if ((threadIdx.x & 63) == (uint32_t)leader) b = atomicAdd(&s_n, (uint32_t)__popcll(m));
+        r = __shfl(b, leader, 64) + lane_rank(m);
+      }
+      if (!occ) continue;
+      if (s == cap) {  // the empty-marker key: its dedicated slot, merged as usual
+        const int64_t gs = g_find<1>(t, key_hash<1>((int64_t)kEmpty, 0), (int64_t)kEmpty, 0);
+#pragma unroll
+        for (int a = 0; a < S::MA; ++a)
+          if (a < na) agg_merge_word(&t.agg[a * gstr + gs], S::kind(p, a), lt.agg[a * stride + s]);
+        continue;
+      }
+      if (base == ~0ull) continue;
+      const uint64_t pos = base + r;
+      t.slot[pos] = wd;
+#pragma unroll
+      for (int a = 0; a < S::MA; ++a)
+        if (a < na) t.agg[a * gstr + pos] = lt.agg[a * stride + s];
+    }
+    return;
+  }
   for (uint32_t s = threadIdx.x; s < stride; s += BD) {
     const uint64_t wd = lt.slot[s];
     const bool occ = s < cap ? wd != kEmpty : lt.ctl[CTL_SPECIAL] != 0u;

@@ -60,6 +60,9 @@ struct AggArgs {
   int32_t sp_map[NUT_MAX_AGGS];
   // Segment mode (seg_off != 0): block b folds rows [seg_off[2b], seg_off[2b+1]) only.
   const uint64_t *seg_off;
+  // dense (segment mode, one key, every segment a whole partition): a block's groups are
+  // final, so they are appended to the table's first slots instead of hashed into it
+  int32_t dense, pad_;
 };
 
 // ------------------------------------------------------------------ query shapes

@@ -27,6 +27,7 @@ struct nut_groups {
   size_t mem_bytes = 0;
   unsigned long long *dev_cursors = nullptr;  // [64] inside mem
   uint64_t *dev_segbase = nullptr;            // [2*64] inside mem
+  bool dense = false;  // groups appended at slots 0.. (not at their hash): rehash before inserting
 };
 
 namespace {
@@ -274,6 +275,7 @@ struct LaunchExtra {
   uint64_t blocks = 0, region = 0;         // out (spill): grid and per-block staging region
   const uint64_t *seg_off = nullptr;       // one block per segment: [start, end) pairs, even starts
   uint32_t nseg = 0;
+  bool dense = false;                      // every segment a whole partition (AggArgs::dense)
 };
 
 // launch the streaming aggregation of spec's rows into g's table.  `kinds` are the
@@ -326,7 +328,10 @@ nut_status launch_agg(nut_groups *g, const nut_agg_spec *s, uint64_t group_hint,
   const int na = s->naggs;
   // (32 slots = 8 buckets x 32 B = one pass over the 64 LDS banks: for <= 8 groups two
   // home buckets never conflict — distinct buckets hit distinct banks, equal ones broadcast)
-  uint64_t want = group_hint ? 4 * group_hint : 4096;
+  // (segment mode: group_hint is already twice a partition's expected groups; the table
+  // size trades LDS occupancy against probe length — NUT_OPT_GB_SEG_SLOTS)
+  uint64_t want = group_hint ? (ex && ex->seg_off ? (uint64_t)c->opt[NUT_OPT_GB_SEG_SLOTS] * group_hint : 4 * group_hint)
+                             : 4096;
   uint32_t lcap = 32;
   while (lcap < want && lds_bytes(lcap * 2, g->nk, na, false, 0, kBdShared) <= lds_max) lcap *= 2;
   if (group_hint > 8ull * lcap) lcap = 0;  // hot keys cannot fit on chip: straight to HBM
@@ -357,6 +362,7 @@ nut_status launch_agg(nut_groups *g, const nut_agg_spec *s, uint64_t group_hint,
   if (blocks == 0) blocks = 1;
   if (ex && ex->seg_off) {  // one block per segment (segments start at even rows)
     a.seg_off = ex->seg_off;
+    a.dense = ex->dense && g->nk == 1 ? 1 : 0;
     blocks = ex->nseg;
   }
   if (ex && ex->spill) {  // block b stages at most the rows it visits: 2 per pair of its lanes
@@ -408,7 +414,7 @@ nut_status ensure_room(nut_groups *g, uint64_t extra) {
   uint64_t need = (uint64_t)ctl[0] + extra + 1;
   // sharded counters (large tables) overflow per shard: keep 1/8 of headroom for variance
   const uint64_t slack = g->gt.nsh_log2 ? need / 8 : 0;
-  if (need + slack <= g->gt.limit && (g->nk == 1 || (uint64_t)ctl[3] + extra + slack <= g->gt.arena_cap))
+  if (!g->dense && need + slack <= g->gt.limit && (g->nk == 1 || (uint64_t)ctl[3] + extra + slack <= g->gt.arena_cap))
     return NUT_OK;
   nut_groups fresh;
   fresh.ctx = g->ctx;
@@ -431,6 +437,7 @@ nut_status ensure_room(nut_groups *g, uint64_t extra) {
   g->dev_gt = fresh.dev_gt;
   g->dev_cursors = fresh.dev_cursors;
   g->dev_segbase = fresh.dev_segbase;
+  g->dense = false;
   fresh.mem = nullptr;
   return NUT_OK;
 }
@@ -488,25 +495,29 @@ uint32_t gp_tiles(std::vector<GpSeg> &segs, uint32_t tile, std::vector<uint32_t>
 // [start, end) pairs are appended to *parts
 nut_status gp_level(nut_ctx *c, GpMeta &mm, std::vector<GpSeg> &segs, int shift, const uint64_t *const *src,
                     uint64_t *const *dst, int narr, bool gather, bool have_hist, std::vector<uint64_t> &hist,
-                    std::vector<uint64_t> *parts = nullptr, uint64_t kx = 0, uint64_t opt_cap = 0) {
+                    std::vector<uint64_t> *parts = nullptr, uint64_t kx = 0, uint64_t ovf = 0) {
   hipStream_t st = c->stream;
   std::vector<uint32_t> ts;
   nut_status s;
   GpSeg *dseg;
   uint32_t *dts;
   const size_t nh = gather ? 1 : segs.size();  // gather: every segment into one compact range
-  if (opt_cap) {
-    // optimistic layout (one segment, no histogram pass): digit d owns rows [d * opt_cap,
-    // (d + 1) * opt_cap) of dst (opt_cap even: 16-B aligned partitions); the counts are the
-    // cursors read back after the scatter; rows [256 * opt_cap, + 16 Ki) of every dst array
-    // must exist (overflowing runs land there).  NUT_ERR_CAPACITY (no message) if a digit
-    // outgrew its rows: nothing is usable, partition again with a histogram.
-    if (segs.size() != 1 || gather || have_hist || !parts || (opt_cap & 1))
-      return fail(NUT_ERR_INVALID_ARG, "gp_level: optimistic layout needs one segment");
-    std::vector<uint64_t> cur(GP_BINS + 1, 0);
-    for (int d = 0; d < GP_BINS; ++d) cur[d] = (uint64_t)d * opt_cap;
+  if (ovf) {
+    // capped layout (no histogram pass): digit d of segment i owns rows [obase + d * ocap,
+    // obase + (d + 1) * ocap) of dst (both even: 16-B aligned partitions), set by the
+    // caller; the counts are the cursors read back after the scatter; rows [ovf, ovf +
+    // 16 Ki) of every dst array must exist (overflowing runs land there).  NUT_ERR_CAPACITY
+    // (no message) if a digit outgrew its rows: nothing is usable, partition again with a
+    // histogram.
+    if (gather || have_hist || !parts) return fail(NUT_ERR_INVALID_ARG, "gp_level: capped layout needs parts");
+    const size_t nc = segs.size() * GP_BINS;
+    std::vector<uint64_t> cur(nc + 1, 0);  // + the overflow flag
+    for (size_t i = 0; i < segs.size(); ++i) {
+      if ((segs[i].obase | segs[i].ocap) & 1) return fail(NUT_ERR_INVALID_ARG, "gp_level: odd capped region");
+      for (int d = 0; d < GP_BINS; ++d) cur[i * GP_BINS + d] = segs[i].obase + (uint64_t)d * segs[i].ocap;
+    }
     const uint32_t nst = gp_tiles(segs, 2 * GP_TILE, ts);
-    s = mm.begin(GpMeta::al(sizeof(GpSeg)) + GpMeta::al(ts.size() * 4 + 1) + GpMeta::al(cur.size() * 8));
+    s = mm.begin(GpMeta::al(segs.size() * sizeof(GpSeg)) + GpMeta::al(ts.size() * 4 + 1) + GpMeta::al(cur.size() * 8));
     if (s) return s;
     uint64_t *dcur;
     if ((s = mm.up(segs, &dseg)) || (s = mm.up(ts, &dts)) || (s = mm.up(cur, &dcur))) return s;
@@ -516,26 +527,27 @@ nut_status gp_level(nut_ctx *c, GpMeta &mm, std::vector<GpSeg> &segs, int shift,
       ar.dst[a] = dst[a];
     }
     ar.narr = narr;
+    unsigned long long *dflag = (unsigned long long *)dcur + nc;
     if (nst) {
       const unsigned grid = std::min<unsigned>(nst, (unsigned)c->num_cus);
       if (src[2])
         hipLaunchKernelGGL((gp_scatter_kernel<2, 1024>), dim3(grid), dim3(1024), 0, st, ar, (const GpSeg *)dseg,
-                           (const uint32_t *)dts, nst, shift, 0, (unsigned long long *)dcur, kx, opt_cap);
+                           (const uint32_t *)dts, nst, shift, 0, (unsigned long long *)dcur, kx, ovf, dflag);
       else
         hipLaunchKernelGGL((gp_scatter_kernel<1, 1024>), dim3(grid), dim3(1024), 0, st, ar, (const GpSeg *)dseg,
-                           (const uint32_t *)dts, nst, shift, 0, (unsigned long long *)dcur, kx, opt_cap);
+                           (const uint32_t *)dts, nst, shift, 0, (unsigned long long *)dcur, kx, ovf, dflag);
       NUT_HIP(hipGetLastError());
     }
-    std::vector<uint64_t> back(GP_BINS + 1);
+    std::vector<uint64_t> back(cur.size());
     NUT_HIP(hipMemcpyAsync(back.data(), dcur, back.size() * 8, hipMemcpyDeviceToHost, st));
     NUT_HIP(hipStreamSynchronize(st));
-    if (back[GP_BINS]) return NUT_ERR_CAPACITY;
-    hist.assign(GP_BINS, 0);
-    for (int d = 0; d < GP_BINS; ++d) {
-      hist[d] = back[d] - cur[d];
-      if (hist[d]) {
-        parts->push_back(cur[d]);
-        parts->push_back(back[d]);
+    if (back[nc]) return NUT_ERR_CAPACITY;
+    hist.assign(nc, 0);
+    for (size_t i = 0; i < nc; ++i) {
+      hist[i] = back[i] - cur[i];
+      if (hist[i]) {
+        parts->push_back(cur[i]);
+        parts->push_back(back[i]);
       }
     }
     return NUT_OK;
@@ -592,10 +604,12 @@ nut_status gp_level(nut_ctx *c, GpMeta &mm, std::vector<GpSeg> &segs, int shift,
     const unsigned grid = std::min<unsigned>(nst, (unsigned)c->num_cus);
     if (src[2])
       hipLaunchKernelGGL((gp_scatter_kernel<2, 1024>), dim3(grid), dim3(1024), 0, st, ar, (const GpSeg *)dseg,
-                         (const uint32_t *)dts, nst, shift, gather ? 1 : 0, (unsigned long long *)dcur, kx, 0);
+                         (const uint32_t *)dts, nst, shift, gather ? 1 : 0, (unsigned long long *)dcur, kx, 0,
+                         (unsigned long long *)nullptr);
     else
       hipLaunchKernelGGL((gp_scatter_kernel<1, 1024>), dim3(grid), dim3(1024), 0, st, ar, (const GpSeg *)dseg,
-                         (const uint32_t *)dts, nst, shift, gather ? 1 : 0, (unsigned long long *)dcur, kx, 0);
+                         (const uint32_t *)dts, nst, shift, gather ? 1 : 0, (unsigned long long *)dcur, kx, 0,
+                         (unsigned long long *)nullptr);
   }
   NUT_HIP(hipGetLastError());
   return NUT_OK;
@@ -632,12 +646,22 @@ nut_status gp_aggregate(nut_groups *g, GpMeta &mm, const std::vector<uint64_t> &
   LaunchExtra sg;
   sg.seg_off = doff;
   sg.nseg = (uint32_t)(off.size() / 2);
+  // one chunk per partition: its groups are final in its block, appended without hashing
+  // (a partition with more groups than its block's table admits reruns hashed)
+  sg.dense = k == 1 && g->nk == 1 && c->opt[NUT_OPT_GB_DENSE] != 0;
   const uint64_t per = std::max<uint64_t>(64, 2 * ((group_hint + nparts - 1) / nparts));
   uint32_t ctl[4];
   for (int attempt = 0;; ++attempt) {
     e = launch_agg(g, &s2, per, kinds2, &sg);
     if (!e) e = read_ctl(g, ctl);
     if (e) return e;
+    if (ctl[1] & 4u) {  // dense: a block could not hold its partition — the hashed merge
+      sg.dense = false;
+      e = alloc_table(g, g->gt.cap);
+      if (e) return e;
+      continue;
+    }
+    g->dense = sg.dense;
     if (!(ctl[1] & 1u)) break;
     // more groups than the table admits: a larger table, then the same partitions again
     if (g->gt.cap >= (1ull << 34) || attempt > 12) return fail(NUT_ERR_OOM, "nut_groupby: group table too large");
@@ -669,9 +693,19 @@ nut_status groupby_partitioned_direct(nut_groups *g, const nut_agg_spec *s, uint
   c->gb_path = NUT_GB_PARTITIONED_DIRECT;
   c->gb_levels = (uint32_t)levels;
   c->gb_optimistic = 0;
+  // Capped level 1: a level-1 partition's rows are about (rows per key) x Poisson(lambda)
+  // with lambda = G / 65536 keys per partition, so a sub-digit owns its even share times
+  // 1 + 6 / sqrt(lambda) (six standard deviations), + 64 rows — offered from lambda >= 100
+  // (G >= 6.5M, slack <= 1.6x); below, level 1 takes the histogram layout.
+  const double lam = (double)group_hint / (GP_BINS * GP_BINS);
+  const double slack1 = levels == 2 && opt && lam >= 100 ? 1.0 + 6.0 / sqrt(lam) : 0.0;
   // A, B: the histogram layout (level 0 -> A -> level 1 -> B, or level 0 -> B); O: the
-  // optimistic level 0 (2 x rows per array over A + B); B2: two levels' final arrays after O
-  nut_status e = c->gp_data.reserve((levels == 2 && opt ? 3 : 2) * (size_t)nstore * rows * 8 + 256);
+  // optimistic level 0 (2 x rows per array over A + B); B2: two levels' final arrays after O,
+  // b2rows each
+  const uint64_t b2rows = slack1 > 0 ? ((uint64_t)ceil(n * slack1) + 66ull * GP_BINS * GP_BINS + 2 * GP_TILE + 64 + 31) & ~31ull
+                                     : rows;
+  const bool two_opt = levels == 2 && opt;
+  nut_status e = c->gp_data.reserve((2 * (size_t)nstore * rows + (two_opt ? (size_t)nstore * b2rows : 0)) * 8 + 256);
   if (e) return e;
   uint64_t *A[GP_MAX_ARR] = {}, *B[GP_MAX_ARR] = {}, *O[GP_MAX_ARR] = {}, *B2[GP_MAX_ARR] = {};
   for (int i = 1, k = 0; i < narr; ++i) {
@@ -679,7 +713,7 @@ nut_status groupby_partitioned_direct(nut_groups *g, const nut_agg_spec *s, uint
     A[i] = (uint64_t *)c->gp_data.ptr + (size_t)k * rows;
     B[i] = (uint64_t *)c->gp_data.ptr + (size_t)(nstore + k) * rows;
     O[i] = (uint64_t *)c->gp_data.ptr + (size_t)k * 2 * rows;
-    B2[i] = (uint64_t *)c->gp_data.ptr + (size_t)(2 * nstore + k) * rows;
+    B2[i] = (uint64_t *)c->gp_data.ptr + 2 * (size_t)nstore * rows + (size_t)k * b2rows;
     ++k;
   }
   // optimistic level 0: no histogram pass; a digit owns twice its even share of rows (the
@@ -694,10 +728,11 @@ nut_status groupby_partitioned_direct(nut_groups *g, const nut_agg_spec *s, uint
   GpMeta mm{c};
   c->timer.begin(st, NUT_KERNEL_AGGREGATE);
   std::vector<GpSeg> segs{GpSeg{0, n, 0, 0}};
+  segs[0].ocap = ocap;
   std::vector<uint64_t> hist, parts;
   uint64_t **fin = B;
   if (levels == 1) {
-    e = opt ? gp_level(c, mm, segs, 56, src, O, narr, false, false, hist, &parts, 0, ocap) : NUT_ERR_CAPACITY;
+    e = opt ? gp_level(c, mm, segs, 56, src, O, narr, false, false, hist, &parts, 0, GP_BINS * ocap) : NUT_ERR_CAPACITY;
     if (!e) {
       fin = O;
       c->gb_optimistic = 1;
@@ -712,9 +747,19 @@ nut_status groupby_partitioned_direct(nut_groups *g, const nut_agg_spec *s, uint
     std::vector<GpSeg> s2;
     std::vector<uint64_t> p0;
     uint64_t **mid = A;
-    e = opt ? gp_level(c, mm, segs, 56, src, O, narr, false, false, hist, &p0, 0, ocap) : NUT_ERR_CAPACITY;
+    uint64_t ovf1 = 0;  // capped level 1: its overflow rows (0: histogram layout)
+    e = opt ? gp_level(c, mm, segs, 56, src, O, narr, false, false, hist, &p0, 0, GP_BINS * ocap) : NUT_ERR_CAPACITY;
     if (!e) {
-      for (size_t i = 0; i < p0.size(); i += 2) s2.push_back(GpSeg{p0[i], p0[i + 1] - p0[i], 0, 0});
+      // level 1 without a histogram pass either (slack1 above; a skewed next hash byte
+      // overflows and takes the histogram layout)
+      for (size_t i = 0; i < p0.size(); i += 2) {
+        GpSeg sg{p0[i], p0[i + 1] - p0[i], 0, 0};
+        sg.obase = ovf1;
+        sg.ocap = ((uint64_t)ceil((double)sg.count / GP_BINS * slack1) + 64 + 1) & ~1ull;
+        ovf1 += GP_BINS * sg.ocap;
+        s2.push_back(sg);
+      }
+      if (slack1 <= 0 || ovf1 + 2 * GP_TILE > b2rows) ovf1 = 0;
       mid = O;
       fin = B2;
       c->gb_optimistic = 1;
@@ -731,7 +776,13 @@ nut_status groupby_partitioned_direct(nut_groups *g, const nut_agg_spec *s, uint
       return e;
     }
     std::vector<uint64_t> h2;
-    e = gp_level(c, mm, s2, 48, mid, fin, narr, false, false, h2, &parts);
+    e = ovf1 ? gp_level(c, mm, s2, 48, mid, fin, narr, false, false, h2, &parts, 0, ovf1) : NUT_ERR_CAPACITY;
+    if (!e) c->gb_optimistic = 2;
+    if (e == NUT_ERR_CAPACITY) {
+      h2.clear();
+      parts.clear();
+      e = gp_level(c, mm, s2, 48, mid, fin, narr, false, false, h2, &parts);
+    }
     if (e) return e;
   }
   c->timer.end(st);

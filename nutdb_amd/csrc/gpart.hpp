@@ -28,6 +28,9 @@ constexpr int GP_MAX_ARR = 3 + NUT_MAX_VALS;         // hash, k1, k2, value arra
 struct GpSeg {  // records [start, start + count) of the current buffer
   uint64_t start, count;
   uint32_t tile0, pad;  // first tile of the segment in the launch's tile table
+  // capped layout (no histogram pass): digit d of this segment owns output rows
+  // [obase + d * ocap, obase + (d + 1) * ocap)
+  uint64_t obase = 0, ocap = 0;
 };
 
 struct GpArrays {
@@ -85,20 +88,24 @@ __global__ __launch_bounds__(GP_HTHREADS) void gp_hist_kernel(const uint64_t *__
 // keys are fetched while this tile's value arrays go through.
 // Gather mode: all segments share one set of 256 cursors (the spilled blocks' regions ->
 // one compact partitioned array).
-template <int NK, int T>
+// (VAR: tuning variants for scripts/tune/gp_tune.hip — bit 0 non-temporal stores, bit 1 no
+// stores, bit 2 tile-sequential output, bit 3 sequential output after the scattered address
+// is computed; the product runs VAR = 0)
+template <int NK, int T, int VAR = 0, int BITS = 8>
 __global__ __launch_bounds__(T) void gp_scatter_kernel(GpArrays ar, const GpSeg *__restrict__ segs,
                                                                 const uint32_t *__restrict__ tile_seg, uint32_t ntiles,
                                                                 int shift, int gather,
                                                                 unsigned long long *__restrict__ cursor, uint64_t kx,
-                                                                uint64_t cap) {
+                                                                uint64_t ovf, unsigned long long *__restrict__ oflag) {
   constexpr uint32_t TILE = T * GP_ITEMS;
+  constexpr int BINS = 1 << BITS;  // (the product: GP_BINS = 256)
   static_assert(TILE <= (1u << 24), "slot bits");
   __shared__ uint64_t s_stage[TILE];
   __shared__ uint8_t s_dig[TILE];
-  __shared__ uint32_t s_cnt[GP_BINS];
-  __shared__ uint32_t s_tex[GP_BINS];
-  __shared__ uint64_t s_gb[GP_BINS];
-  __shared__ uint32_t s_wsum[GP_BINS / kWave];
+  __shared__ uint32_t s_cnt[BINS];
+  __shared__ uint32_t s_tex[BINS];
+  __shared__ uint64_t s_gb[BINS];
+  __shared__ uint32_t s_wsum[BINS / kWave];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   uint64_t k1[GP_ITEMS], k2[NK == 2 ? GP_ITEMS : 1];
   // records of tile tt: [lo, lo + n); item i of this lane is record i * T + tid
@@ -129,19 +136,19 @@ __global__ __launch_bounds__(T) void gp_scatter_kernel(GpArrays ar, const GpSeg 
     asm volatile("" : "+v"(tid_));
     const int tid = tid_;
     const uint32_t s = tile_seg[t];
-    if (tid < GP_BINS) s_cnt[tid] = 0;
+    if (tid < BINS) s_cnt[tid] = 0;
     __syncthreads();
     // rank: sd[i] = digit | in-digit rank << 8, then the tile slot once the digit starts are known
     uint32_t sd[GP_ITEMS];
 #pragma unroll
     for (int i = 0; i < GP_ITEMS; ++i) {
-      const uint32_t d = (uint32_t)(owner_hash(k1[i] ^ kx, NK == 2 ? k2[i] : 0, NK) >> shift) & 255u;
+      const uint32_t d = (uint32_t)(owner_hash(k1[i] ^ kx, NK == 2 ? k2[i] : 0, NK) >> shift) & (BINS - 1);
       const uint32_t r = (uint32_t)i * T + tid < n ? atomicAdd(&s_cnt[d], 1u) : 0u;
-      sd[i] = d | (r << 8);
+      sd[i] = d | (r << BITS);
     }
     __syncthreads();
     uint32_t c = 0, incl = 0;
-    if (tid < GP_BINS) {
+    if (tid < BINS) {
       c = s_cnt[tid];
       incl = c;
 #pragma unroll
@@ -152,27 +159,27 @@ __global__ __launch_bounds__(T) void gp_scatter_kernel(GpArrays ar, const GpSeg 
       if (lane == 63) s_wsum[wave] = incl;
     }
     __syncthreads();
-    if (tid < GP_BINS) {
+    if (tid < BINS) {
       uint32_t add = 0;
 #pragma unroll
-      for (int w = 0; w < GP_BINS / kWave; ++w) add += (w < wave) ? s_wsum[w] : 0u;
+      for (int w = 0; w < BINS / kWave; ++w) add += (w < wave) ? s_wsum[w] : 0u;
       const uint32_t tex = incl - c + add;
       s_tex[tid] = tex;
       const uint64_t cs = gather ? 0 : (uint64_t)s;
-      const uint64_t gb = c ? (uint64_t)atomicAdd(&cursor[cs * GP_BINS + tid], (unsigned long long)c) : 0;
-      // cap (optimistic layout, no histogram; one segment): digit d owns rows
-      // [d * cap, (d + 1) * cap); a run past it goes to the scratch rows after the 256
-      // partitions (>= one tile of them), and the flag after the 256 cursors tells the host
-      // to partition again with a histogram
-      const bool over = cap && c && gb + c > (uint64_t)(tid + 1) * cap;
-      if (over) atomicOr(&cursor[GP_BINS], 1ull);
-      s_gb[tid] = (over ? (uint64_t)GP_BINS * cap : gb) - tex;  // out position of tile slot j with digit d = s_gb[d] + j
+      const uint64_t gb = c ? (uint64_t)atomicAdd(&cursor[cs * BINS + tid], (unsigned long long)c) : 0;
+      // ovf != 0: the capped layout (no histogram pass; GpSeg obase / ocap).  A run past its
+      // digit's rows goes to the scratch rows at ovf (>= one tile of them), and the flag
+      // after the cursors tells the host to partition again with a histogram
+      const GpSeg &g = segs[s];
+      const bool over = ovf && c && gb + c > g.obase + (uint64_t)(tid + 1) * g.ocap;
+      if (over) atomicOr(oflag, 1ull);
+      s_gb[tid] = (over ? ovf : gb) - tex;  // out position of tile slot j with digit d = s_gb[d] + j
     }
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < GP_ITEMS; ++i) {
-      const uint32_t d = sd[i] & 255u;
-      sd[i] = (sd[i] >> 8) + s_tex[d];  // the tile slot
+      const uint32_t d = sd[i] & (BINS - 1);
+      sd[i] = (sd[i] >> BITS) + s_tex[d];  // the tile slot
       if ((uint32_t)i * T + tid < n) s_dig[sd[i]] = (uint8_t)d;
     }
     // one array through LDS: stage in digit order (its registers are then free), write
@@ -191,7 +198,18 @@ __global__ __launch_bounds__(T) void gp_scatter_kernel(GpArrays ar, const GpSeg 
 #pragma unroll 2
       for (int i = 0; i < GP_ITEMS; ++i) {
         const uint32_t j = (uint32_t)i * T + tid;
-        if (j < n) dst[s_gb[s_dig[j]] + j] = s_stage[j];
+        if (j < n) {
+          const uint64_t x = s_stage[j];
+          uint64_t o = (VAR & 4) ? lo + j : s_gb[s_dig[j]] + j;
+          if (VAR & 8) o = o == ~0ull ? o : lo + j;
+          if (VAR & 2) {
+            if (x == 0x0123456789ABCDEFull) dst[o] = x;  // (keeps the LDS reads)
+          } else if (VAR & 1) {
+            __builtin_nontemporal_store(x, &dst[o]);
+          } else {
+            dst[o] = x;
+          }
+        }
       }
     };
     uint64_t v[GP_ITEMS];

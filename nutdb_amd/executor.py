@@ -345,13 +345,15 @@ class Executor:
 
     GROUPBY_PATHS = ("onchip", "partitioned_direct", "partitioned_spill")
     OPTIONS = {"gb_partition": 0, "gb_levels": 1, "gb_optimistic": 2, "gb_direct": 3, "gb_chunks": 4,
-               "join_region": 5, "join_probe_cfg": 6, "join_any_cfg": 7}
+               "join_region": 5, "join_probe_cfg": 6, "join_any_cfg": 7, "gb_seg_slots": 8,
+               "gb_dense": 9}
 
     def groupby_stats(self) -> dict:
         """The algorithm the last group-by on this context took (nut_ctx_groupby_stats)."""
         p, lv, opt = C.c_uint32(), C.c_uint32(), C.c_uint32()
         check(lib.nut_ctx_groupby_stats(self.ctx, C.byref(p), C.byref(lv), C.byref(opt)), "nut_ctx_groupby_stats")
-        return {"path": self.GROUPBY_PATHS[p.value], "levels": lv.value, "optimistic": bool(opt.value)}
+        return {"path": self.GROUPBY_PATHS[p.value], "levels": lv.value, "optimistic": bool(opt.value),
+                "capped_levels": opt.value}
 
     def set_option(self, name: str, value: int) -> int:
         """nut_ctx_set_option (tuning / tests); returns the previous value."""

@@ -152,9 +152,45 @@ def test_gp_optimistic_layout_and_fallback(ex, orc, opts, opt, levels):
         st = ex.groupby_stats()
         assert st["path"] == "partitioned_direct" and st["levels"] == int(levels)
         assert st["optimistic"] == (opt == "1" and not heavy)
+        assert st["capped_levels"] == (1 if opt == "1" and not heavy else 0)  # (G = 1e5: level 1 histogram)
         ok, ow = orc.groupby([key], AGGS4, values=[val])
         keys, words = g.to_host_words()
         assert np.array_equal(keys, ok) and np.array_equal(words, ow), heavy
+
+
+def _owner_hash(k):
+    """common.hpp owner_hash(k, 0, 1) = mix64(k ^ 0x6A09E667F3BCC908), numpy uint64"""
+    z = k.astype(np.uint64) ^ np.uint64(0x6A09E667F3BCC908)
+    z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return z ^ (z >> np.uint64(31))
+
+
+def test_gp_capped_level1_fallback(ex, orc, opts):
+    """Two capped levels (offered from 6.5M expected groups: hint 1e7 over ~3M distinct
+    keys): a key hash whose SECOND byte is skewed (30% of the rows on keys whose level-1
+    digit is 7, spread over every level-0 digit) keeps level 0 capped and overflows level
+    1, which runs again with a histogram; uniform keys keep both capped.  Both equal the
+    oracle bit for bit."""
+    opts(gb_partition=1, gb_levels=2, gb_optimistic=1)
+    n = 3_000_017
+    rng = np.random.default_rng(17)
+    cand = rng.integers(-2**62, 2**62, 4_000_000).astype(np.int64)
+    sub7 = cand[((_owner_hash(cand) >> np.uint64(48)) & np.uint64(255)) == 7][:2000]
+    assert len(sub7) == 2000 and len(np.unique(_owner_hash(sub7) >> np.uint64(56))) > 200
+    for skew in (False, True):
+        key = orc.gen_column(1, 0x63, n)  # distinct keys
+        if skew:
+            m = rng.random(n) < 0.3
+            key[m] = rng.choice(sub7, int(m.sum()))
+        val = orc.gen_column(3, 0x64, n)
+        g = ex.groupby(gb_query(dev(key, ex), dev(val, ex)), group_hint=10_000_000)
+        st = ex.groupby_stats()
+        assert (st["path"], st["levels"], st["optimistic"]) == ("partitioned_direct", 2, True)
+        assert st["capped_levels"] == (1 if skew else 2), st
+        ok, ow = orc.groupby([key], AGGS4, values=[val])
+        keys, words = g.to_host_words()
+        assert np.array_equal(keys, ok) and np.array_equal(words, ow), skew
 
 
 def test_ordered_result_bucket_index(ex, orc):
@@ -175,3 +211,35 @@ def test_ordered_result_bucket_index(ex, orc):
         ok, ow = orc.groupby([key], AGGS4, values=[val])
         keys, words = g.to_host_words()
         assert np.array_equal(keys, ok) and np.array_equal(words, ow), name
+
+
+def test_gp_dense_partitions_and_fallback(ex, orc, opts):
+    """Two levels leave one workgroup per partition, whose groups are final: they are
+    appended to the table unhashed (gb_dense, the default).  A partition with more groups
+    than its workgroup's table admits (a hint far too small) reruns with the hashed merge;
+    accumulating into a dense result rehashes it first.  All equal the oracle."""
+    opts(gb_partition=1, gb_levels=2)
+    n = 4_000_037
+    key = orc.gen_column(1, 0x65, n)  # distinct keys
+    key[::3] = key[1::3][: len(key[::3])]  # and some repeats
+    val = orc.gen_column(3, 0x66, n)
+    ok, ow = orc.groupby([key], AGGS4, values=[val])
+    for hint in (n, 10):
+        for dense in (1, 0):
+            opts(gb_dense=dense)
+            g = ex.groupby(gb_query(dev(key, ex), dev(val, ex)), group_hint=hint)
+            keys, words = g.to_host_words()
+            assert np.array_equal(keys, ok) and np.array_equal(words, ow), (hint, dense)
+    # accumulate more rows into a dense result
+    opts(gb_dense=1)
+    g = ex.groupby(gb_query(dev(key, ex), dev(val, ex)), group_hint=n)
+    from nutdb_amd import Agg, AggQuery
+    key2 = np.concatenate([orc.gen_column(2, 0x67, 500_000, a=1000), key[:1000]])
+    val2 = orc.gen_column(3, 0x68, len(key2))
+    ones = np.ones(len(key2), dtype=np.int64)  # COUNT partials merge as sums
+    ex.accumulate(AggQuery(keys=[dev(key2, ex)], values=[dev(val2, ex), dev(ones, ex)],
+                           aggs=[Agg("sum", "col", (0,)), Agg("sum", "col", (1,)), Agg("min", "col", (0,)),
+                                 Agg("max", "col", (0,))]), g)
+    ok2, ow2 = orc.groupby([np.concatenate([key, key2])], AGGS4, values=[np.concatenate([val, val2])])
+    keys, words = g.to_host_words()
+    assert np.array_equal(keys, ok2) and np.array_equal(words, ow2)
