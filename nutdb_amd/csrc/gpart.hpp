@@ -90,8 +90,9 @@ __global__ __launch_bounds__(GP_HTHREADS) void gp_hist_kernel(const uint64_t *__
 // one compact partitioned array).
 // (VAR: tuning variants for scripts/tune/gp_tune.hip — bit 0 non-temporal stores, bit 1 no
 // stores, bit 2 tile-sequential output, bit 3 sequential output after the scattered address
-// is computed; the product runs VAR = 0)
-template <int NK, int T, int VAR = 0, int BITS = 8>
+// is computed.  The product runs VAR = 1: non-temporal stores measured 7.16-7.24 vs
+// 7.34-7.37 ms per 1e9-record level on two boxes, profiles/r03/gp_tune_*.log)
+template <int NK, int T, int VAR = 1, int BITS = 8>
 __global__ __launch_bounds__(T) void gp_scatter_kernel(GpArrays ar, const GpSeg *__restrict__ segs,
                                                                 const uint32_t *__restrict__ tile_seg, uint32_t ntiles,
                                                                 int shift, int gather,
