@@ -264,7 +264,7 @@ typedef struct {
   /* Expression mode: key j (j < nkeys) is the value of key_prog[j] when its n > 0 (an
    * int64 or bool program; keys[j] is then unused and may be NULL), else keys[j].
    * Computed keys (getYear(d), a % 10) and packed key tuples: SQL plans pack up to 8
-   * GROUP BY keys into two words this way (DESIGN.md §3.6). */
+   * GROUP BY keys into two words this way (DESIGN.md §3.7). */
   nut_prog key_prog[NUT_MAX_KEYS];
 } nut_agg_spec;
 
