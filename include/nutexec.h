@@ -113,7 +113,9 @@ typedef enum {
   NUT_OPT_JOIN_ANY_CFG = 7,    /* unordered probe tile shape 0..4 (0) */
   NUT_OPT_GB_SEG_SLOTS = 8,    /* partition aggregation: LDS slots per hinted group, 1..8 (2) */
   NUT_OPT_GB_DENSE = 9,        /* 1 (default): whole partitions append their groups unhashed */
-  NUT_OPT_COUNT = 10
+  NUT_OPT_GB_L1_BITS = 10,     /* digit bits of a capped second partition level, 6..8 (6) */
+  NUT_OPT_TOPK = 11,           /* 1 (default): plans with ORDER BY ... LIMIT sort only nut_topk_positions' rows */
+  NUT_OPT_COUNT = 12
 } nut_option;
 nut_status nut_ctx_set_option(nut_ctx *ctx, int option, int64_t value);
 nut_status nut_ctx_get_option(nut_ctx *ctx, int option, int64_t *value);
@@ -339,6 +341,15 @@ nut_status nut_sort_i64_desc(nut_ctx *ctx, const int64_t *in, int64_t *out, uint
  * call's payload (LSD order, the sort is stable).  vals and vals_out may not alias. */
 nut_status nut_sort_pairs(nut_ctx *ctx, const void *keys, int key_type, int desc, const int64_t *vals,
                           int64_t *vals_out, uint64_t n);
+/* ORDER BY ... LIMIT k (LimitClause, query.rs:92-98) without sorting every row: the
+ * positions, ascending, of every key ordered at or before the k-th smallest (desc:
+ * largest) of n keys (key_type / order as nut_sort_pairs) — at least k of them, every tie
+ * of the k-th key and a few more included, so a stable sort of just these rows yields the
+ * first k rows of the full sort.  *count_host = their number; NUT_ERR_CAPACITY (no
+ * message) if it exceeds cap (positions untouched).  Radix select: 12-bit digit
+ * histograms, 8 B/key per level (usually one), + 8 B/key to collect. */
+nut_status nut_topk_positions(nut_ctx *ctx, const void *keys, int key_type, int desc, uint64_t n, uint64_t k,
+                              int64_t *positions, uint64_t cap, uint64_t *count_host);
 /* Stable partition of int64 keys into nsplit+1 buckets, bucket(k) = #{i : splitters[i] <= k}
  * (splitters_host ascending, 0 <= nsplit < 64).  Bucket b is written to out at offset
  * sum_{c<b} counts_host[c]; counts_host receives nsplit+1 counts.  The local step of the

@@ -196,6 +196,7 @@ SIGNATURES = {
     "nut_result_free": (None, [_P]),
     "nut_ctx_memcpy": (_I32, [_P, _P, _P, C.c_size_t]),
     "nut_sort_pairs": (_I32, [_P, _P, _I32, _I32, _P, _P, _U64]),
+    "nut_topk_positions": (_I32, [_P, _P, _I32, _I32, _U64, _U64, _P, _U64, C.POINTER(C.c_uint64)]),
     # multi-GPU (RCCL inside the library)
     "nut_dist_create": (_I32, [_I32, C.POINTER(_I32), C.POINTER(_P)]),
     "nut_dist_unique_id": (_I32, [_P]),

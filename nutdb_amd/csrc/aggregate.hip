@@ -495,7 +495,7 @@ uint32_t gp_tiles(std::vector<GpSeg> &segs, uint32_t tile, std::vector<uint32_t>
 // [start, end) pairs are appended to *parts
 nut_status gp_level(nut_ctx *c, GpMeta &mm, std::vector<GpSeg> &segs, int shift, const uint64_t *const *src,
                     uint64_t *const *dst, int narr, bool gather, bool have_hist, std::vector<uint64_t> &hist,
-                    std::vector<uint64_t> *parts = nullptr, uint64_t kx = 0, uint64_t ovf = 0) {
+                    std::vector<uint64_t> *parts = nullptr, uint64_t kx = 0, uint64_t ovf = 0, int bits = 8) {
   hipStream_t st = c->stream;
   std::vector<uint32_t> ts;
   nut_status s;
@@ -509,12 +509,15 @@ nut_status gp_level(nut_ctx *c, GpMeta &mm, std::vector<GpSeg> &segs, int shift,
     // 16 Ki) of every dst array must exist (overflowing runs land there).  NUT_ERR_CAPACITY
     // (no message) if a digit outgrew its rows: nothing is usable, partition again with a
     // histogram.
-    if (gather || have_hist || !parts) return fail(NUT_ERR_INVALID_ARG, "gp_level: capped layout needs parts");
-    const size_t nc = segs.size() * GP_BINS;
+    // (bits: the digit width of this level, 6..8)
+    if (gather || have_hist || !parts || bits < 6 || bits > 8)
+      return fail(NUT_ERR_INVALID_ARG, "gp_level: capped layout needs parts");
+    const int nb = 1 << bits;
+    const size_t nc = segs.size() * nb;
     std::vector<uint64_t> cur(nc + 1, 0);  // + the overflow flag
     for (size_t i = 0; i < segs.size(); ++i) {
       if ((segs[i].obase | segs[i].ocap) & 1) return fail(NUT_ERR_INVALID_ARG, "gp_level: odd capped region");
-      for (int d = 0; d < GP_BINS; ++d) cur[i * GP_BINS + d] = segs[i].obase + (uint64_t)d * segs[i].ocap;
+      for (int d = 0; d < nb; ++d) cur[i * nb + d] = segs[i].obase + (uint64_t)d * segs[i].ocap;
     }
     const uint32_t nst = gp_tiles(segs, 2 * GP_TILE, ts);
     s = mm.begin(GpMeta::al(segs.size() * sizeof(GpSeg)) + GpMeta::al(ts.size() * 4 + 1) + GpMeta::al(cur.size() * 8));
@@ -530,12 +533,14 @@ nut_status gp_level(nut_ctx *c, GpMeta &mm, std::vector<GpSeg> &segs, int shift,
     unsigned long long *dflag = (unsigned long long *)dcur + nc;
     if (nst) {
       const unsigned grid = std::min<unsigned>(nst, (unsigned)c->num_cus);
-      if (src[2])
-        hipLaunchKernelGGL((gp_scatter_kernel<2, 1024>), dim3(grid), dim3(1024), 0, st, ar, (const GpSeg *)dseg,
-                           (const uint32_t *)dts, nst, shift, 0, (unsigned long long *)dcur, kx, ovf, dflag);
-      else
-        hipLaunchKernelGGL((gp_scatter_kernel<1, 1024>), dim3(grid), dim3(1024), 0, st, ar, (const GpSeg *)dseg,
-                           (const uint32_t *)dts, nst, shift, 0, (unsigned long long *)dcur, kx, ovf, dflag);
+      using SK = void (*)(GpArrays, const GpSeg *, const uint32_t *, uint32_t, int, int, unsigned long long *, uint64_t,
+                          uint64_t, unsigned long long *);
+      static const SK kern[2][3] = {{gp_scatter_kernel<1, 1024, 1, 6>, gp_scatter_kernel<1, 1024, 1, 7>,
+                                     gp_scatter_kernel<1, 1024, 1, 8>},
+                                    {gp_scatter_kernel<2, 1024, 1, 6>, gp_scatter_kernel<2, 1024, 1, 7>,
+                                     gp_scatter_kernel<2, 1024, 1, 8>}};
+      hipLaunchKernelGGL(kern[src[2] ? 1 : 0][bits - 6], dim3(grid), dim3(1024), 0, st, ar, (const GpSeg *)dseg,
+                         (const uint32_t *)dts, nst, shift, 0, (unsigned long long *)dcur, kx, ovf, dflag);
       NUT_HIP(hipGetLastError());
     }
     std::vector<uint64_t> back(cur.size());
@@ -693,16 +698,19 @@ nut_status groupby_partitioned_direct(nut_groups *g, const nut_agg_spec *s, uint
   c->gb_path = NUT_GB_PARTITIONED_DIRECT;
   c->gb_levels = (uint32_t)levels;
   c->gb_optimistic = 0;
-  // Capped level 1: a level-1 partition's rows are about (rows per key) x Poisson(lambda)
-  // with lambda = G / 65536 keys per partition, so a sub-digit owns its even share times
-  // 1 + 6 / sqrt(lambda) (six standard deviations), + 64 rows — offered from lambda >= 100
-  // (G >= 6.5M, slack <= 1.6x); below, level 1 takes the histogram layout.
-  const double lam = (double)group_hint / (GP_BINS * GP_BINS);
+  // Capped level 1 (bits1-bit digits; 6 by default — 64-bin runs are 4x longer than 256-bin
+  // ones and 16384 partitions of ~610 groups aggregate faster than 65536 of ~150: same-box
+  // A/B at G = 1e7, 1e9 rows, 19.9 vs 22.7 ms kernels): a level-1 partition's rows are about (rows per key) x
+  // Poisson(lambda) with lambda = G / (256 << bits1) keys per partition, so a sub-digit owns
+  // its even share times 1 + 6 / sqrt(lambda) (six standard deviations), + 64 rows —
+  // offered from lambda >= 100 (slack <= 1.6x); below, level 1 takes the histogram layout.
+  const int bits1 = (int)c->opt[NUT_OPT_GB_L1_BITS];
+  const double lam = (double)group_hint / ((double)GP_BINS * (1 << bits1));
   const double slack1 = levels == 2 && opt && lam >= 100 ? 1.0 + 6.0 / sqrt(lam) : 0.0;
   // A, B: the histogram layout (level 0 -> A -> level 1 -> B, or level 0 -> B); O: the
   // optimistic level 0 (2 x rows per array over A + B); B2: two levels' final arrays after O,
   // b2rows each
-  const uint64_t b2rows = slack1 > 0 ? ((uint64_t)ceil(n * slack1) + 66ull * GP_BINS * GP_BINS + 2 * GP_TILE + 64 + 31) & ~31ull
+  const uint64_t b2rows = slack1 > 0 ? ((uint64_t)ceil(n * slack1) + 66ull * GP_BINS * (1 << bits1) + 2 * GP_TILE + 64 + 31) & ~31ull
                                      : rows;
   const bool two_opt = levels == 2 && opt;
   nut_status e = c->gp_data.reserve((2 * (size_t)nstore * rows + (two_opt ? (size_t)nstore * b2rows : 0)) * 8 + 256);
@@ -755,8 +763,8 @@ nut_status groupby_partitioned_direct(nut_groups *g, const nut_agg_spec *s, uint
       for (size_t i = 0; i < p0.size(); i += 2) {
         GpSeg sg{p0[i], p0[i + 1] - p0[i], 0, 0};
         sg.obase = ovf1;
-        sg.ocap = ((uint64_t)ceil((double)sg.count / GP_BINS * slack1) + 64 + 1) & ~1ull;
-        ovf1 += GP_BINS * sg.ocap;
+        sg.ocap = ((uint64_t)ceil((double)sg.count / (1 << bits1) * slack1) + 64 + 1) & ~1ull;
+        ovf1 += (uint64_t)sg.ocap << bits1;
         s2.push_back(sg);
       }
       if (slack1 <= 0 || ovf1 + 2 * GP_TILE > b2rows) ovf1 = 0;
@@ -776,7 +784,8 @@ nut_status groupby_partitioned_direct(nut_groups *g, const nut_agg_spec *s, uint
       return e;
     }
     std::vector<uint64_t> h2;
-    e = ovf1 ? gp_level(c, mm, s2, 48, mid, fin, narr, false, false, h2, &parts, 0, ovf1) : NUT_ERR_CAPACITY;
+    e = ovf1 ? gp_level(c, mm, s2, 56 - bits1, mid, fin, narr, false, false, h2, &parts, 0, ovf1, bits1)
+             : NUT_ERR_CAPACITY;
     if (!e) c->gb_optimistic = 2;
     if (e == NUT_ERR_CAPACITY) {
       h2.clear();

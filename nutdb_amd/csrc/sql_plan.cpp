@@ -1830,9 +1830,33 @@ nut_status build_spec(const nut_plan &p, const nut_column *const *bound, const D
 PProg and_all(const std::vector<PProg> &cs);
 PProg pred_prog(const PlanPred &pr);
 
+// ORDER BY ... LIMIT: the positions (ascending) of the n keys that can reach the first
+// `need` places (nut_topk_positions) in *pos, *m of them; *m = n (pos untouched) when a
+// full sort is as cheap (few keys, a limit close to n, or the option off)
+nut_status topk_reduce(nut_ctx *c, const nut_plan &p, const void *keys, int type, bool desc, uint64_t n, DevBuf &pos,
+                       uint64_t *m) {
+  *m = n;
+  if (!p.has_limit || !c->opt[NUT_OPT_TOPK] || n < (1u << 16)) return NUT_OK;
+  const uint64_t need = p.offset > n ? n : std::min<uint64_t>(n, p.offset + std::min<uint64_t>(p.limit, n));
+  if (need == 0) {
+    *m = 0;
+    return NUT_OK;
+  }
+  if (need > n / 4) return NUT_OK;
+  const uint64_t cap = n / 2;
+  if (pos.alloc(c, cap * 8) != hipSuccess) return fail(NUT_ERR_OOM, "hipMalloc (top-k)");
+  uint64_t cnt = 0;
+  nut_status s = nut_topk_positions(c, keys, type, desc ? 1 : 0, n, need, (int64_t *)pos.p, cap, &cnt);
+  if (s == NUT_ERR_CAPACITY) return NUT_OK;  // heavy ties at the boundary: the full sort
+  if (s) return s;
+  *m = cnt;
+  return NUT_OK;
+}
+
 // ORDER BY with projected columns / several keys (SQL scans): the selected row ids are
 // sorted by the keys — one stable (key, row id) sort per key, the least significant
-// first (nut_sort_pairs) — and every projected column is gathered through them.
+// first (nut_sort_pairs) — and every projected column is gathered through them.  With a
+// LIMIT, only the rows top-k selection keeps on the most significant key are sorted.
 nut_status exec_sort_rows(nut_ctx *c, const nut_plan &p, const nut_column *const *bound, const Dict *const *dicts,
                           uint64_t n, nut_result *r) {
   for (const auto &k : p.sort_keys) {
@@ -1857,6 +1881,25 @@ nut_status exec_sort_rows(nut_ctx *c, const nut_plan &p, const nut_column *const
     NUT_HIP(rows.alloc(c, n * 8));
     s = nut_select_rows(c, &sp, (int64_t *)rows.p, &cnt);
     if (s) return s;
+  }
+  if (cnt && p.has_limit) {
+    // top-k on the most significant key: keep the candidate rows (ascending ids)
+    const nut_column *kc = bound[p.sort_keys[0].first];
+    NUT_HIP(keys.alloc(c, cnt * 8));
+    nut_status s = nut_gather_u64(c, (const uint64_t *)kc->data, (const int64_t *)rows.p, cnt, 0, (uint64_t *)keys.p);
+    DevBuf pos;
+    uint64_t m2 = cnt;
+    if (!s) s = topk_reduce(c, p, keys.p, kc->type, p.sort_keys[0].second, cnt, pos, &m2);
+    if (s) return s;
+    if (m2 < cnt) {
+      NUT_HIP(perm.alloc(c, std::max<uint64_t>(m2, 1) * 8));
+      s = nut_gather_u64(c, (const uint64_t *)rows.p, (const int64_t *)pos.p, m2, 0, (uint64_t *)perm.p);
+      if (s) return s;
+      std::swap(rows.p, perm.p);
+      cnt = m2;
+      perm.reset();  // (stream-ordered free of the full id list)
+    }
+    keys.reset();
   }
   const uint64_t m = std::max<uint64_t>(cnt, 1);
   NUT_HIP(hipMalloc(&r->dev, m * 8 * p.projs.size()));
@@ -1962,9 +2005,17 @@ nut_status exec_scan(nut_ctx *c, const nut_plan &p, const nut_column *const *bou
         s = nut_gather_u64(c, (const uint64_t *)bound[p.projs[j]]->data, (const int64_t *)rows.p, cnt, 0,
                            (uint64_t *)r->dev + j * cnt);
     } else {
-      DevBuf vals;
+      DevBuf vals, pos, cv;
       NUT_HIP(vals.alloc(c, std::max<uint64_t>(cnt, 1) * 8));
       s = nut_gather_u64(c, (const uint64_t *)col->data, (const int64_t *)rows.p, cnt, 0, (uint64_t *)vals.p);
+      uint64_t m2 = cnt;  // ORDER BY ... LIMIT: only the top-k candidates are sorted
+      if (!s) s = topk_reduce(c, p, vals.p, NUT_T_I64, p.desc, cnt, pos, &m2);
+      if (!s && m2 < cnt) {
+        if (cv.alloc(c, std::max<uint64_t>(m2, 1) * 8) != hipSuccess) return fail(NUT_ERR_OOM, "hipMalloc (top-k)");
+        s = nut_gather_u64(c, (const uint64_t *)vals.p, (const int64_t *)pos.p, m2, 0, (uint64_t *)cv.p);
+        std::swap(vals.p, cv.p);
+        cnt = m2;
+      }
       if (!s) s = p.desc ? nut_sort_i64_desc(c, (const int64_t *)vals.p, (int64_t *)r->dev, cnt)
                          : nut_sort_i64(c, (const int64_t *)vals.p, (int64_t *)r->dev, cnt);
     }
@@ -1985,8 +2036,18 @@ nut_status exec_scan(nut_ctx *c, const nut_plan &p, const nut_column *const *bou
         if (s) return s;
         src = (const int64_t *)tmp.p;
       }
-      nut_status s = p.desc ? nut_sort_i64_desc(c, src, (int64_t *)r->dev, cnt)
-                            : nut_sort_i64(c, src, (int64_t *)r->dev, cnt);
+      DevBuf pos, cv;
+      uint64_t m2 = cnt;  // ORDER BY ... LIMIT: only the top-k candidates are sorted
+      nut_status s = topk_reduce(c, p, src, NUT_T_I64, p.desc, cnt, pos, &m2);
+      if (s) return s;
+      if (m2 < cnt) {
+        if (cv.alloc(c, std::max<uint64_t>(m2, 1) * 8) != hipSuccess) return fail(NUT_ERR_OOM, "hipMalloc (top-k)");
+        s = nut_gather_u64(c, (const uint64_t *)src, (const int64_t *)pos.p, m2, 0, (uint64_t *)cv.p);
+        if (s) return s;
+        src = (const int64_t *)cv.p;
+        cnt = m2;
+      }
+      s = p.desc ? nut_sort_i64_desc(c, src, (int64_t *)r->dev, cnt) : nut_sort_i64(c, src, (int64_t *)r->dev, cnt);
       if (s) return s;
       s = nut_ctx_sync(c);
       if (s) return s;

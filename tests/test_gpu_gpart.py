@@ -166,13 +166,14 @@ def _owner_hash(k):
     return z ^ (z >> np.uint64(31))
 
 
-def test_gp_capped_level1_fallback(ex, orc, opts):
+@pytest.mark.parametrize("bits1", [8, 6])
+def test_gp_capped_level1_fallback(ex, orc, opts, bits1):
     """Two capped levels (offered from 6.5M expected groups: hint 1e7 over ~3M distinct
     keys): a key hash whose SECOND byte is skewed (30% of the rows on keys whose level-1
     digit is 7, spread over every level-0 digit) keeps level 0 capped and overflows level
     1, which runs again with a histogram; uniform keys keep both capped.  Both equal the
     oracle bit for bit."""
-    opts(gb_partition=1, gb_levels=2, gb_optimistic=1)
+    opts(gb_partition=1, gb_levels=2, gb_optimistic=1, gb_l1_bits=bits1)
     n = 3_000_017
     rng = np.random.default_rng(17)
     cand = rng.integers(-2**62, 2**62, 4_000_000).astype(np.int64)

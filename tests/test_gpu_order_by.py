@@ -148,3 +148,82 @@ def test_sql_order_by_string_key_rejected(ex):
     t.append(id=np.arange(10, dtype=np.int64), name=[str(i) for i in range(10)])
     with pytest.raises(NutError, match="string column"):
         t.execute(Plan("SELECT id FROM e ORDER BY name"))
+
+
+# ------------------------------------------------------------------ ORDER BY ... LIMIT (top-k)
+def topk_positions(ex, keys, k, desc=False, cap=None):
+    from nutdb_amd._lib import T_F64, T_I64, lib
+    n = len(keys)
+    d = dev(keys, ex)
+    cap = n if cap is None else cap
+    out = torch.empty(max(cap, 1), dtype=torch.int64, device=ex.device)
+    cnt = C.c_uint64()
+    ex._bind_stream()
+    st = lib.nut_topk_positions(ex.ctx, C.c_void_p(d.data_ptr()), T_F64 if keys.dtype == np.float64 else T_I64,
+                                1 if desc else 0, n, k, C.c_void_p(out.data_ptr()), cap, C.byref(cnt))
+    ex.sync()
+    return st, cnt.value, out[: cnt.value].cpu().numpy()
+
+
+@pytest.mark.parametrize("desc", [False, True])
+@pytest.mark.parametrize("kind", ["uniform", "narrow", "ties", "f64"])
+def test_topk_positions(ex, kind, desc):
+    """nut_topk_positions: ascending positions of every key ordered at or before the k-th
+    (ties included), at least k of them — exactly the keys u <= the k-th key's u plus the
+    rest of its final radix bucket; checked against numpy on the order-mapped keys."""
+    rng = np.random.default_rng(91)
+    n = 3_000_017
+    keys = {"uniform": lambda: rng.integers(I64_MIN, I64_MAX, n, dtype=np.int64),
+            "narrow": lambda: rng.integers(-5000, 5000, n).astype(np.int64),
+            "ties": lambda: np.repeat(rng.integers(0, 40, n // 100 + 1), 100)[:n].astype(np.int64),
+            "f64": lambda: np.where(rng.random(n) < 0.01, -0.0, rng.standard_normal(n))}[kind]()
+    u = ukey(keys, desc)
+    su = np.sort(u)
+    for k in (1, 10, 1000, 250_000, n - 1, n, n + 5):
+        st, cnt, pos = topk_positions(ex, keys, k, desc)
+        assert st == 0, (k, st)
+        kth = su[min(k, n) - 1]
+        assert cnt >= min(k, n) and np.all(np.diff(pos) > 0)
+        assert np.array_equal(np.sort(pos), pos)
+        inside = u[pos]
+        assert np.all(inside <= inside.max()) and int((u <= kth).sum()) <= cnt  # every tie of the k-th key
+        assert np.array_equal(pos, np.flatnonzero(u <= inside.max())), k  # a prefix of the order
+    # capacity: reported, nothing written
+    st, cnt, _ = topk_positions(ex, keys, 1000, desc, cap=10)
+    assert st == 5 and cnt >= 1000
+
+
+@pytest.mark.parametrize("topk", [1, 0])
+def test_sql_order_by_limit_topk(ex, opts, topk):
+    """ORDER BY ... LIMIT runs a stable sort of only the top-k candidate rows; results are
+    identical to the full sort (option topk=0) and to numpy's stable order, ties in row
+    order — keys-only scans (fused and expression mode), projected columns with several
+    keys, DESC, float64 keys, OFFSET, heavy ties at the boundary, and LIMIT 0."""
+    opts(topk=topk)
+    rng = np.random.default_rng(13)
+    n = 2_000_003
+    a = rng.integers(-10**6, 10**6, n).astype(np.int64)
+    b = rng.integers(0, 50, n).astype(np.int64)  # heavy ties
+    f = rng.standard_normal(n)
+    cols = {"a": dev(a, ex), "b": dev(b, ex), "f": dev(f, ex)}
+    # keys-only, fused (no WHERE / one comparison of the column) and expression mode
+    got = ex.sql("select a from t order by a limit 100", cols)["a"]
+    assert np.array_equal(got, np.sort(a)[:100])
+    got = ex.sql("select a from t where a > 5 order by a desc limit 37 offset 11", cols)["a"]
+    assert np.array_equal(got, np.sort(a[a > 5])[::-1][11:48])
+    got = ex.sql("select a from t where a % 3 = 0 order by a limit 1000", cols)["a"]
+    assert np.array_equal(got, np.sort(a[a % 3 == 0])[:1000])
+    # projected columns, several keys, ties broken by the next key then by row order
+    got = ex.sql("select a, b, f from t where b < 45 order by b, a desc limit 500 offset 3", cols)
+    idx = np.flatnonzero(b < 45)
+    o = idx[np.lexsort((-a[idx], b[idx]))][3:503]
+    assert np.array_equal(got["b"], b[o]) and np.array_equal(got["a"], a[o]) and np.array_equal(got["f"], f[o])
+    # a float64 key (IEEE total order), DESC
+    got = ex.sql("select f, a from t order by f desc limit 64", cols)
+    o = np.argsort(ukey(f, desc=True), kind="stable")[:64]
+    assert np.array_equal(got["f"], f[o]) and np.array_equal(got["a"], a[o])
+    # the boundary key repeats ~40000 times: every tie is a candidate
+    got = ex.sql("select b, a from t order by b limit 70000", cols)
+    o = np.argsort(b, kind="stable")[:70000]
+    assert np.array_equal(got["b"], b[o]) and np.array_equal(got["a"], a[o])
+    assert len(ex.sql("select a from t order by a limit 0", cols)["a"]) == 0
