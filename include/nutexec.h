@@ -115,7 +115,8 @@ typedef enum {
   NUT_OPT_GB_DENSE = 9,        /* 1 (default): whole partitions append their groups unhashed */
   NUT_OPT_GB_L1_BITS = 10,     /* digit bits of a capped second partition level, 6..8 (6) */
   NUT_OPT_TOPK = 11,           /* 1 (default): plans with ORDER BY ... LIMIT sort only nut_topk_positions' rows */
-  NUT_OPT_COUNT = 12
+  NUT_OPT_GB_L0_BITS = 12,     /* digit bits of a capped first partition level, 6..8; 0 (default): 7 for one level up to 150 K groups, else 8 */
+  NUT_OPT_COUNT = 13
 } nut_option;
 nut_status nut_ctx_set_option(nut_ctx *ctx, int option, int64_t value);
 nut_status nut_ctx_get_option(nut_ctx *ctx, int option, int64_t *value);

@@ -704,13 +704,18 @@ nut_status groupby_partitioned_direct(nut_groups *g, const nut_agg_spec *s, uint
   // Poisson(lambda) with lambda = G / (256 << bits1) keys per partition, so a sub-digit owns
   // its even share times 1 + 6 / sqrt(lambda) (six standard deviations), + 64 rows —
   // offered from lambda >= 100 (slack <= 1.6x); below, level 1 takes the histogram layout.
+  // level 0's digit: 7 bits for one level up to 150 K groups (128 partitions of <= ~1200
+  // groups still fit a workgroup's 2048-slot table; the runs are twice as long: G = 1e5
+  // 9.98 vs 10.56 ms kernels, same box), else 8 (two levels: G = 1e7 18.4 vs 18.6 ms)
+  const int bits0 = c->opt[NUT_OPT_GB_L0_BITS] >= 6 ? (int)c->opt[NUT_OPT_GB_L0_BITS]
+                    : levels == 1 && group_hint <= 150000 ? 7 : 8;
   const int bits1 = (int)c->opt[NUT_OPT_GB_L1_BITS];
-  const double lam = (double)group_hint / ((double)GP_BINS * (1 << bits1));
+  const double lam = (double)group_hint / ((double)(1 << bits0) * (1 << bits1));
   const double slack1 = levels == 2 && opt && lam >= 100 ? 1.0 + 6.0 / sqrt(lam) : 0.0;
   // A, B: the histogram layout (level 0 -> A -> level 1 -> B, or level 0 -> B); O: the
   // optimistic level 0 (2 x rows per array over A + B); B2: two levels' final arrays after O,
   // b2rows each
-  const uint64_t b2rows = slack1 > 0 ? ((uint64_t)ceil(n * slack1) + 66ull * GP_BINS * (1 << bits1) + 2 * GP_TILE + 64 + 31) & ~31ull
+  const uint64_t b2rows = slack1 > 0 ? ((uint64_t)ceil(n * slack1) + (66ull << (bits0 + bits1)) + 2 * GP_TILE + 64 + 31) & ~31ull
                                      : rows;
   const bool two_opt = levels == 2 && opt;
   nut_status e = c->gp_data.reserve((2 * (size_t)nstore * rows + (two_opt ? (size_t)nstore * b2rows : 0)) * 8 + 256);
@@ -724,10 +729,10 @@ nut_status groupby_partitioned_direct(nut_groups *g, const nut_agg_spec *s, uint
     B2[i] = (uint64_t *)c->gp_data.ptr + 2 * (size_t)nstore * rows + (size_t)k * b2rows;
     ++k;
   }
-  // optimistic level 0: no histogram pass; a digit owns twice its even share of rows (the
-  // rows after the 256 partitions take overflowing runs: at least one tile), so only a key
-  // hash skewed that far falls back to the histogram layout
-  const uint64_t ocap = ((2 * rows - 2 * GP_TILE) / GP_BINS) & ~1ull;
+  // optimistic level 0 (bits0-bit digits): no histogram pass; a digit owns twice its even
+  // share of rows (the rows after the partitions take overflowing runs: at least one tile),
+  // so only a key hash skewed that far falls back to the histogram layout (8-bit digits)
+  const uint64_t ocap = ((2 * rows - 2 * GP_TILE) >> bits0) & ~1ull;
   const uint64_t *src[GP_MAX_ARR] = {};
   src[1] = (const uint64_t *)s->keys[0];
   src[2] = nk == 2 ? (const uint64_t *)s->keys[1] : nullptr;
@@ -739,8 +744,10 @@ nut_status groupby_partitioned_direct(nut_groups *g, const nut_agg_spec *s, uint
   segs[0].ocap = ocap;
   std::vector<uint64_t> hist, parts;
   uint64_t **fin = B;
+  int shift1 = 48;  // level 1's digit: below level 0's
   if (levels == 1) {
-    e = opt ? gp_level(c, mm, segs, 56, src, O, narr, false, false, hist, &parts, 0, GP_BINS * ocap) : NUT_ERR_CAPACITY;
+    e = opt ? gp_level(c, mm, segs, 64 - bits0, src, O, narr, false, false, hist, &parts, 0, ocap << bits0, bits0)
+            : NUT_ERR_CAPACITY;
     if (!e) {
       fin = O;
       c->gb_optimistic = 1;
@@ -756,8 +763,10 @@ nut_status groupby_partitioned_direct(nut_groups *g, const nut_agg_spec *s, uint
     std::vector<uint64_t> p0;
     uint64_t **mid = A;
     uint64_t ovf1 = 0;  // capped level 1: its overflow rows (0: histogram layout)
-    e = opt ? gp_level(c, mm, segs, 56, src, O, narr, false, false, hist, &p0, 0, GP_BINS * ocap) : NUT_ERR_CAPACITY;
+    e = opt ? gp_level(c, mm, segs, 64 - bits0, src, O, narr, false, false, hist, &p0, 0, ocap << bits0, bits0)
+            : NUT_ERR_CAPACITY;
     if (!e) {
+      shift1 = 64 - bits0 - bits1;
       // level 1 without a histogram pass either (slack1 above; a skewed next hash byte
       // overflows and takes the histogram layout)
       for (size_t i = 0; i < p0.size(); i += 2) {
@@ -784,7 +793,7 @@ nut_status groupby_partitioned_direct(nut_groups *g, const nut_agg_spec *s, uint
       return e;
     }
     std::vector<uint64_t> h2;
-    e = ovf1 ? gp_level(c, mm, s2, 56 - bits1, mid, fin, narr, false, false, h2, &parts, 0, ovf1, bits1)
+    e = ovf1 ? gp_level(c, mm, s2, shift1, mid, fin, narr, false, false, h2, &parts, 0, ovf1, bits1)
              : NUT_ERR_CAPACITY;
     if (!e) c->gb_optimistic = 2;
     if (e == NUT_ERR_CAPACITY) {
