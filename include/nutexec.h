@@ -201,7 +201,8 @@ typedef enum {
  *            as LIKE over dictionary codes; the table must outlive the call)
  *   DATEPART one int operand d = days since 1970-01-01 (proleptic Gregorian), int result
  *            by arg (nut_date_part): year, month 1-12, day of month, quarter 1-4, day of
- *            week (Monday = 1 .. Sunday = 7), day of year 1-366; d is first clamped to
+ *            week (Monday = 1 .. Sunday = 7), day of year 1-366, year * 100 + month,
+ *            year * 10000 + month * 100 + day (toYYYYMM / toYYYYMMDD); d is first clamped to
  *            [-2^40, 2^40] (beyond any real date), so every d has one defined result. */
 typedef enum {
   NUT_P_COL = 0, NUT_P_I64 = 1, NUT_P_F64 = 2,
@@ -213,7 +214,8 @@ typedef enum {
   NUT_P_IF = 25, NUT_P_ABS = 26, NUT_P_TO_F64 = 27, NUT_P_LOOKUP = 28, NUT_P_DATEPART = 29
 } nut_prog_op;
 typedef enum {
-  NUT_DP_YEAR = 0, NUT_DP_MONTH = 1, NUT_DP_DAY = 2, NUT_DP_QUARTER = 3, NUT_DP_WEEKDAY = 4, NUT_DP_YEARDAY = 5
+  NUT_DP_YEAR = 0, NUT_DP_MONTH = 1, NUT_DP_DAY = 2, NUT_DP_QUARTER = 3, NUT_DP_WEEKDAY = 4, NUT_DP_YEARDAY = 5,
+  NUT_DP_YYYYMM = 6, NUT_DP_YYYYMMDD = 7
 } nut_date_part;
 typedef enum { NUT_PT_I64 = 0, NUT_PT_F64 = 1, NUT_PT_BOOL = 2 } nut_prog_value_type;
 typedef struct {
@@ -399,6 +401,16 @@ nut_status nut_join_i64_into(nut_ctx *ctx, const int64_t *build, uint64_t nbuild
 nut_status nut_select_rows(nut_ctx *ctx, const nut_agg_spec *s, int64_t *out_rows, uint64_t *count_host);
 /* compile the scan kernel of nut_select_rows for this spec (hipRTC; no GPU needed) */
 nut_status nut_select_jit_compile(const nut_agg_spec *s);
+/* Computed projections (SELECT a * b, CASE ..., toYYYYMMDD(d) FROM t):
+ * for i < m, out[a][i] = program s->agg_val[a] (a < s->naggs, agg_op ignored) evaluated
+ * at row rows[i] of the program columns (rows NULL: row i, m <= s->n), as 8-byte words
+ * (int64, or float64 bits when nut_prog_type says F64); valid[a][i] = 1 where the mask
+ * program s->agg_mask[a] holds (always without one), else 0 with out[a][i] = 0 — a SQL
+ * NULL.  valid NULL or valid[a] NULL: not written.  Row ids must index the program
+ * columns (nut_select_rows output does).  Division by zero: NUT_ERR_INVALID_ARG. */
+nut_status nut_eval_rows(nut_ctx *ctx, const nut_agg_spec *s, const int64_t *rows, uint64_t m, uint64_t *const *out,
+                         uint8_t *const *valid);
+nut_status nut_eval_jit_compile(const nut_agg_spec *s);
 /* The multi-GPU join's exchange step: rows go to part (owner_hash(key) >> 56) * nparts / 256
  * (owner_hash = the group-by's; host restatement nutdb_amd/dist.py join_owner); out_keys /
  * out_rows (row0 + row index) hold the parts one after another in part order, rows
@@ -586,6 +598,13 @@ nut_status nut_result_to_host(const nut_result *res, int j, void *dst, uint64_t 
 nut_status nut_result_device(const nut_result *res, const void **dev);
 /* column j of a FILTER / SORT result in HBM (expression-mode scans may project several) */
 nut_status nut_result_device_column(const nut_result *r, int j, const void **dev);
+/* SQL NULLs of output column j: *dev = nrows 1-byte flags in HBM (1: a value, 0: NULL —
+ * a LEFT-joined table's column on a row without a match, or a CASE branch without ELSE),
+ * or NULL when the column holds no NULLs (GROUPBY results never do).  A NULL row's value
+ * word is 0 (strings: empty). */
+nut_status nut_result_validity(const nut_result *r, int j, const uint8_t **dev);
+/* the same flags copied to host (all 1 for a column without NULLs; cap in rows) */
+nut_status nut_result_validity_to_host(const nut_result *r, int j, uint8_t *dst, uint64_t cap);
 /* row of a NUT_T_STR output column (a string group key of a typed table); the bytes
  * are owned by res and not NUL-terminated */
 nut_status nut_result_string(const nut_result *res, int j, uint64_t row, const char **s, size_t *len);

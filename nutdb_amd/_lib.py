@@ -49,7 +49,7 @@ PROG_OPS = ["col", "i64", "f64", "add", "sub", "mul", "div", "mod", "intdiv", "l
             "and", "or", "xor", "not", "bitand", "bitor", "bitxor", "bitnot", "shl", "shr", "if", "abs", "to_f64", "lookup",
             "datepart"]
 # nut_date_part (the arg of a "datepart" node)
-DP_YEAR, DP_MONTH, DP_DAY, DP_QUARTER, DP_WEEKDAY, DP_YEARDAY = range(6)
+DP_YEAR, DP_MONTH, DP_DAY, DP_QUARTER, DP_WEEKDAY, DP_YEARDAY, DP_YYYYMM, DP_YYYYMMDD = range(8)
 P = {name: i for i, name in enumerate(PROG_OPS)}
 PT_I64, PT_F64, PT_BOOL = 0, 1, 2
 
@@ -144,6 +144,8 @@ SIGNATURES = {
     "nut_gather_u64": (_I32, [_P, _P, _P, _U64, _U64, _P]),
     "nut_select_rows": (_I32, [_P, C.POINTER(NutAggSpec), _P, C.POINTER(_U64)]),
     "nut_select_jit_compile": (_I32, [C.POINTER(NutAggSpec)]),
+    "nut_eval_rows": (_I32, [_P, C.POINTER(NutAggSpec), _P, _U64, _P, _P]),
+    "nut_eval_jit_compile": (_I32, [C.POINTER(NutAggSpec)]),
     "nut_gen_column": (_I32, [_P, _I32, _U64, _I64, _I64, C.c_double, _U64, _U64, _P]),
     "nut_filter_i64": (_I32, [_P, _P, _U64, _I32, _I64, _P, C.POINTER(_U64)]),
     "nut_filter_i64_async": (_I32, [_P, _P, _U64, _I32, _I64, _P, _P]),
@@ -193,6 +195,8 @@ SIGNATURES = {
     "nut_result_to_host": (_I32, [_P, _I32, _P, _U64]),
     "nut_result_device": (_I32, [_P, C.POINTER(_P)]),
     "nut_result_device_column": (_I32, [_P, _I32, C.POINTER(_P)]),
+    "nut_result_validity": (_I32, [_P, _I32, C.POINTER(_P)]),
+    "nut_result_validity_to_host": (_I32, [_P, _I32, _P, _U64]),
     "nut_result_free": (None, [_P]),
     "nut_ctx_memcpy": (_I32, [_P, _P, _P, C.c_size_t]),
     "nut_sort_pairs": (_I32, [_P, _P, _I32, _I32, _P, _P, _U64]),

@@ -1251,6 +1251,82 @@ nut_status nut_select_rows(nut_ctx *c, const nut_agg_spec *s, int64_t *out_rows,
   return NUT_OK;
 }
 
+// Computed projections (select_kernel.hpp eval_kernel): out[a][i] = program s->agg_val[a]
+// at row rows[i] (rows NULL: i), valid[a][i] = its mask s->agg_mask[a] (1 without one).
+static nut_status eval_prepare(const nut_agg_spec *s, JitShape &js) {
+  if (!s->prog_mode) return fail(NUT_ERR_INVALID_ARG, "nut_eval_rows: needs an expression-mode spec (prog_mode = 1)");
+  if (s->naggs < 1 || s->naggs > NUT_MAX_AGGS) return fail(NUT_ERR_INVALID_ARG, "nut_eval_rows: naggs not in [1, 8]");
+  if (s->nprog_cols < 0 || s->nprog_cols > NUT_MAX_PROG_COLS)
+    return fail(NUT_ERR_INVALID_ARG, "nut_eval_rows: bad program column count");
+  nut_agg_spec q = *s;  // the value / mask programs alone
+  q.where.n = 0;
+  q.nkeys = 0;
+  for (int a = 0; a < q.naggs; ++a) {
+    if (!q.agg_val[a].n) return fail(NUT_ERR_INVALID_ARG, "nut_eval_rows: empty value program");
+    q.agg_op[a] = NUT_AGG_SUM;
+  }
+  int32_t kinds[NUT_MAX_AGGS] = {};
+  nut_status st = jit_shape(&q, kinds, js);
+  if (st) return st;
+  if (js.consts.size() > (size_t)kMaxConst)
+    return fail(NUT_ERR_UNSUPPORTED, "nut_eval_rows: more than 64 distinct expression constants");
+  return NUT_OK;
+}
+
+nut_status nut_eval_rows(nut_ctx *c, const nut_agg_spec *s, const int64_t *rows, uint64_t m, uint64_t *const *out,
+                         uint8_t *const *valid) {
+  if (!c || !s || (m && !out)) return fail(NUT_ERR_INVALID_ARG, "nut_eval_rows: NULL argument");
+  JitShape js;
+  nut_status st = eval_prepare(s, js);
+  if (st || m == 0) return st;
+  if (!rows && m > s->n) return fail(NUT_ERR_INVALID_ARG, "nut_eval_rows: m > s->n without row ids");
+  for (int i = 0; i < s->nprog_cols; ++i)
+    if (!s->prog_col[i]) return fail(NUT_ERR_INVALID_ARG, "nut_eval_rows: NULL program column");
+  for (int a = 0; a < s->naggs; ++a)
+    if (!out[a]) return fail(NUT_ERR_INVALID_ARG, "nut_eval_rows: NULL output column");
+  DeviceGuard dg(c->device);
+  hipFunction_t fn;
+  st = jit_kernel(jit_eval_unit(js.src, sizeof(EvalArgs)), true, &fn);
+  if (st) return st;
+  st = c->misc.reserve(64);
+  if (st) return st;
+  uint32_t *derr = (uint32_t *)c->misc.ptr;
+  EvalArgs ea;
+  memset(&ea, 0, sizeof ea);
+  ea.a.n = s->n;
+  ea.a.nvals = s->nprog_cols;
+  for (int i = 0; i < s->nprog_cols; ++i) ea.a.val_col[i] = (const uint64_t *)s->prog_col[i];
+  for (size_t i = 0; i < js.consts.size(); ++i) ea.a.kc[i] = js.consts[i];
+  ea.rows = rows;
+  ea.m = m;
+  for (int a = 0; a < s->naggs; ++a) {
+    ea.out[a] = out[a];
+    ea.valid[a] = valid ? valid[a] : nullptr;
+  }
+  ea.err = derr;
+  ea.nout = s->naggs;
+  NUT_HIP(hipMemsetAsync(derr, 0, 4, c->stream));
+  size_t asz = sizeof ea;
+  void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &ea, HIP_LAUNCH_PARAM_BUFFER_SIZE, &asz, HIP_LAUNCH_PARAM_END};
+  const unsigned grid = (unsigned)std::min<uint64_t>((m + EV_THREADS - 1) / EV_THREADS, (uint64_t)c->num_cus * 16);
+  c->timer.begin(c->stream, NUT_KERNEL_FILTER);
+  hipError_t e = hipModuleLaunchKernel(fn, grid, 1, 1, EV_THREADS, 1, 1, 0, c->stream, nullptr, cfg);
+  c->timer.end(c->stream);
+  if (e != hipSuccess) return hip_fail(e, "hipModuleLaunchKernel (eval kernel)");
+  NUT_HIP(hipMemcpyAsync(c->host_pinned, derr, 4, hipMemcpyDeviceToHost, c->stream));
+  NUT_HIP(hipStreamSynchronize(c->stream));
+  if ((uint32_t)c->host_pinned[0] & 2u) return fail(NUT_ERR_INVALID_ARG, "nut_eval_rows: division by zero in an expression");
+  return NUT_OK;
+}
+
+nut_status nut_eval_jit_compile(const nut_agg_spec *s) {
+  if (!s) return fail(NUT_ERR_INVALID_ARG, "nut_eval_jit_compile: NULL argument");
+  JitShape js;
+  nut_status st = eval_prepare(s, js);
+  if (st) return st;
+  return jit_kernel(jit_eval_unit(js.src, sizeof(EvalArgs)), false, nullptr);
+}
+
 // compile (no GPU needed) the scan kernel nut_select_rows would run for this spec
 nut_status nut_select_jit_compile(const nut_agg_spec *s) {
   if (!s || !s->prog_mode) return fail(NUT_ERR_INVALID_ARG, "nut_select_jit_compile: needs an expression-mode spec");

@@ -171,7 +171,7 @@ struct Gen {
           break;
         case NUT_P_DATEPART:
           if (a[0].t == NUT_PT_F64) return fail("DATEPART needs an integer operand (days)");
-          if (nd.arg < NUT_DP_YEAR || nd.arg > NUT_DP_YEARDAY) return fail("DATEPART: unknown part " + std::to_string(nd.arg));
+          if (nd.arg < NUT_DP_YEAR || nd.arg > NUT_DP_YYYYMMDD) return fail("DATEPART: unknown part " + std::to_string(nd.arg));
           r = {NUT_PT_I64, "jdatepart(" + as_i(a[0]) + ", " + std::to_string(nd.arg) + ")"};
           break;
       }
@@ -230,6 +230,8 @@ __device__ __forceinline__ int64_t jdatepart(int64_t d, const int P) {
   if (P == 0) return y;
   if (P == 1) return m;
   if (P == 2) return doy - (153 * mp + 2) / 5 + 1;
+  if (P == 6) return y * 100 + m;
+  if (P == 7) return y * 10000 + m * 100 + (doy - (153 * mp + 2) / 5 + 1);
   if (P == 3) return (m - 1) / 3 + 1;
   if (P == 4) {  // 1970-01-01 was a Thursday (4)
     int64_t w = d % 7;
@@ -387,6 +389,15 @@ std::string jit_select_unit(const std::string &shape_src, size_t args_size) {
   u += shape_src;
   u += "template __global__ void select_kernel<nut::QShape>(SelArgs);\n}  // namespace nut\n";
   u += "// kernel &nut::select_kernel<nut::QShape>\n";
+  return u;
+}
+
+std::string jit_eval_unit(const std::string &shape_src, size_t args_size) {
+  std::string u = kPrelude;
+  u += "static_assert(sizeof(EvalArgs) == " + std::to_string(args_size) + ", \"EvalArgs layout\");\n";
+  u += shape_src;
+  u += "template __global__ void eval_kernel<nut::QShape>(EvalArgs);\n}  // namespace nut\n";
+  u += "// kernel &nut::eval_kernel<nut::QShape>\n";
   return u;
 }
 

@@ -24,6 +24,7 @@ nut_status jit_shape(const nut_agg_spec *s, const int32_t *kinds, JitShape &out)
 std::string jit_unit(const std::string &shape_src, int nk, bool priv, int bd, size_t args_size);
 // the translation unit of the expression-mode scan (select_kernel.hpp) for a shape
 std::string jit_select_unit(const std::string &shape_src, size_t args_size);
+std::string jit_eval_unit(const std::string &shape_src, size_t args_size);
 // compile (cached per unit) and, when load is set, load on the current device
 nut_status jit_kernel(const std::string &unit, bool load, hipFunction_t *fn);
 

@@ -111,4 +111,44 @@ __global__ __launch_bounds__(SEL_THREADS) void select_kernel(SelArgs sa) {
   }
 }
 
+// Computed projections (nut_eval_rows; SELECT a * b, CASE ..., toYYYYMMDD(d) FROM t ...):
+// out[a][i] = the value program a of the same generated shape at row rows[i] (rows NULL:
+// row i), valid[a][i] = its mask program (a CASE branch that yields NULL; 1 without one,
+// and the value word 0 where it is 0).  One row per lane, grid-stride: the selected row ids
+// ascend, so the column reads are near-sequential; each output is one coalesced store.
+constexpr int EV_THREADS = 256;
+
+struct EvalArgs {
+  AggArgs a;                    // val_col[] (program columns), kc[] (constants)
+  const int64_t *rows;          // row ids (NULL: row i)
+  uint64_t m;                   // rows to evaluate
+  uint64_t *out[NUT_MAX_AGGS];  // one 8-byte word per row and program
+  uint8_t *valid[NUT_MAX_AGGS]; // NULL: not written
+  uint32_t *err;                // bit 2: division by zero
+  int32_t nout, pad_;
+};
+
+template <class S>
+__global__ __launch_bounds__(EV_THREADS) void eval_kernel(EvalArgs ea) {
+  bool err = false;
+  const uint64_t stride = (uint64_t)gridDim.x * EV_THREADS;
+  for (uint64_t i = (uint64_t)blockIdx.x * EV_THREADS + threadIdx.x; i < ea.m; i += stride) {
+    const uint64_t r = ea.rows ? (uint64_t)ea.rows[i] : i;
+    uint64_t vv[S::MV > 0 ? S::MV : 1][1];
+#pragma unroll
+    for (int c = 0; c < S::MV; ++c) vv[c][0] = ea.a.val_col[c][r];
+#pragma unroll
+    for (int a = 0; a < S::MA; ++a) {
+      if (a >= ea.nout) break;
+      bool e = false;
+      const bool ok = S::valid(ea.a, a, vv, 0, e);
+      const uint64_t w = ok ? S::value(ea.a, a, vv, 0, e) : 0ull;
+      err = err || e;
+      ea.out[a][i] = w;
+      if (ea.valid[a]) ea.valid[a][i] = ok ? 1 : 0;
+    }
+  }
+  if (__any(err) && (threadIdx.x & (kWave - 1)) == 0) atomicOr(ea.err, 2u);
+}
+
 }  // namespace nut

@@ -24,6 +24,7 @@
 
 #include <algorithm>
 #include <deque>
+#include <functional>
 
 #include "common.hpp"
 #include "sql_ast.hpp"
@@ -136,6 +137,8 @@ int64_t date_part(int64_t d, int part) {
     case NUT_DP_DAY: return dd;
     case NUT_DP_QUARTER: return (m - 1) / 3 + 1;
     case NUT_DP_WEEKDAY: return ((d % 7 + 7) % 7 + 3) % 7 + 1;
+    case NUT_DP_YYYYMM: return y * 100 + m;
+    case NUT_DP_YYYYMMDD: return y * 10000 + m * 100 + dd;
     default: return d - days_from_civil(y, 1, 1) + 1;
   }
 }
@@ -144,8 +147,9 @@ int64_t date_part(int64_t d, int part) {
 int date_fn(sv n) {
   static const char *const names[][2] = {{"toyear", "getyear"},         {"tomonth", "getmonth"},
                                           {"todayofmonth", "getdayofmonth"}, {"toquarter", "getquarter"},
-                                          {"todayofweek", "getdayofweek"}, {"todayofyear", "getdayofyear"}};
-  for (int i = 0; i < 6; ++i)
+                                          {"todayofweek", "getdayofweek"}, {"todayofyear", "getdayofyear"},
+                                          {"toyyyymm", "toyyyymm"},         {"toyyyymmdd", "toyyyymmdd"}};
+  for (int i = 0; i < 8; ++i)
     if (ieq(n, names[i][0]) || ieq(n, names[i][1])) return i;
   return -1;
 }
@@ -359,7 +363,9 @@ struct nut_plan {
   bool never = false;             // WHERE folded to false
   std::vector<PlanPred> preds;
   int proj = -1;                  // FILTER/SORT column (the first projected one)
-  std::vector<int> projs;         // every projected column (expression-mode scans: several)
+  std::vector<int> projs;         // every projected column (expression-mode scans: several; computed: -1)
+  std::vector<PProg> proj_val, proj_mask;  // per projection: its program and NULL mask (plain columns: empty)
+  std::vector<int> isnull_cols;   // columns under an IS [NOT] NULL (folded to a constant)
   bool desc = false;              // SORT direction
   // SORT: the ORDER BY keys as (plan column, desc), most significant first.  One key equal
   // to the only projected column: a keys-only sort; otherwise row ids are sorted by the
@@ -407,6 +413,10 @@ struct nut_result {
   uint64_t dev_stride = 0;  // FILTER with several columns: column j at dev + j * dev_stride
   std::vector<std::vector<uint64_t>> host;  // GROUPBY: output columns (int64 / f64 bits)
   std::vector<std::vector<std::string>> strs;  // NUT_T_STR columns, decoded (others empty)
+  // SQL NULLs (FILTER/SORT): column j's 1-byte flags at valid + valid_of[j] * dev_stride +
+  // dev_off (valid_of[j] < 0 or empty: no NULLs)
+  uint8_t *valid = nullptr;
+  std::vector<int> valid_of;
 };
 
 namespace {
@@ -803,6 +813,8 @@ bool lower_prog(nut_plan &p, const Expr &e, PProg &o, Lowering &L) {
       if (u == UnOp::IsNull || u == UnOp::IsNotNull) {  // executed columns hold no NULLs
         PProg tmp;
         if (!lower_prog(p, e.kids[0], tmp, L)) return false;
+        for (const PNode &nd : tmp)  // (a NULL-extended table's column would: joins reject it)
+          if (nd.op == NUT_P_COL) p.isnull_cols.push_back(nd.col);
         emit_bool(o, u == UnOp::IsNotNull);
         return true;
       }
@@ -857,7 +869,8 @@ bool lower_prog(nut_plan &p, const Expr &e, PProg &o, Lowering &L) {
       }
       if (ieq(n, "todate")) return L.fail("toDate takes one 'YYYY-MM-DD' constant");
       return L.fail("function '" + std::string(n) + "' is not executed (executed: if, multiIf, abs, toFloat64, intDiv, "
-                    "modulo, toYear/getYear, toMonth, toDayOfMonth, toQuarter, toDayOfWeek, toDayOfYear)");
+                    "modulo, toYear/getYear, toMonth, toDayOfMonth, toQuarter, toDayOfWeek, toDayOfYear, toYYYYMM, "
+                    "toYYYYMMDD)");
     }
     default: return L.fail("'" + expr_text(e) + "' is not executed (parameters, collections, subqueries)");
   }
@@ -1365,9 +1378,19 @@ bool lower_mode(const Statement &st, nut_plan &p, Lowering &L) {
     if (b.limit->with_ties) return L.fail("LIMIT ... WITH TIES is not executed");
   }
 
+  // an aggregate anywhere in a SELECT item (sum(a) / sum(b) too); other functions
+  // (abs, toYYYYMMDD, ...) are computed projections of a scan
+  std::function<bool(const Expr &)> contains_agg = [&](const Expr &e) {
+    if (e.k == EK::FnCall && e.fn() == FnKind::Others && (is_agg_name(e.id.name) || is_distinct_name(e.id.name)))
+      return true;
+    if (e.k == EK::Subquery) return false;
+    for (const Expr &k : e.kids)
+      if (contains_agg(k)) return true;
+    return false;
+  };
   bool has_agg = false;
   for (const QueryExpr &q : b.columns)
-    if (q.e.k == EK::FnCall && q.e.fn() == FnKind::Others) has_agg = true;
+    if (contains_agg(q.e)) has_agg = true;
   if (b.group_by || has_agg || b.distinct) {
     // GROUP BY, or aggregates over the whole table (a global aggregate: no keys), or
     // SELECT DISTINCT of 1-2 columns (= GROUP BY those columns, with a hidden COUNT)
@@ -1440,17 +1463,30 @@ bool lower_mode(const Statement &st, nut_plan &p, Lowering &L) {
     return true;
   }
 
-  // no GROUP BY, no aggregate: projected columns (several: expression-mode scans only)
+  // no GROUP BY, no aggregate: projected columns (several: expression-mode scans only) and
+  // computed projections (expression mode: programs evaluated on the selected rows,
+  // nut_eval_rows; a CASE branch without ELSE yields NULL)
   sv name;
   if (b.columns.empty()) return L.fail("a plan without GROUP BY projects columns");
   for (size_t j = 0; j < b.columns.size(); ++j) {
-    if (!column_ref(p, b.columns[j].e, name))
-      return L.fail("a plan without GROUP BY projects plain columns ('" + expr_text(b.columns[j].e) + "')");
-    p.projs.push_back(col_index(p, name));
     PlanOut o;
     o.kind = OUT_KEY;
     o.a = (int)j;
-    o.text = std::string(name);
+    if (column_ref(p, b.columns[j].e, name)) {
+      p.projs.push_back(col_index(p, name));
+      p.proj_val.emplace_back();
+      p.proj_mask.emplace_back();
+      o.text = std::string(name);
+    } else {
+      if (!p.compiled) return L.fail("computed projections run in expression mode");
+      PProg v, m;
+      bool nullable = false;
+      if (!lower_nullable(p, b.columns[j].e, v, m, nullable, L)) return false;
+      p.projs.push_back(-1);
+      p.proj_val.push_back(std::move(v));
+      p.proj_mask.push_back(std::move(m));
+      o.text = expr_text(b.columns[j].e);
+    }
     o.name = b.columns[j].alias ? std::string(*b.columns[j].alias) : o.text;
     p.outs.push_back(o);
   }
@@ -1463,7 +1499,10 @@ bool lower_mode(const Statement &st, nut_plan &p, Lowering &L) {
       if (!column_ref(p, k.e.e, oname)) return L.fail("ORDER BY '" + expr_text(k.e.e) + "' is not a column");
       int ci = -1;
       for (size_t j = 0; j < p.outs.size() && ci < 0; ++j)
-        if (ieq(oname, p.outs[j].name)) ci = p.projs[j];
+        if (ieq(oname, p.outs[j].name)) {
+          if (p.projs[j] < 0) return L.fail("ORDER BY a computed projection ('" + p.outs[j].name + "') is not executed");
+          ci = p.projs[j];
+        }
       okeys.push_back({ci >= 0 ? ci : col_index(p, oname), k.desc});
     }
   }
@@ -1543,8 +1582,9 @@ std::string prog_text(const nut_plan &p, const PProg &pp) {
     else if (n.op == NUT_P_COL) st.push_back(p.cols[n.col]);
     else if (n.op == NUT_P_I64 || n.op == NUT_P_F64) st.push_back(cval_str(n.c));
     else if (n.op == NUT_P_DATEPART) {
-      static const char *dp[] = {"toYear", "toMonth", "toDayOfMonth", "toQuarter", "toDayOfWeek", "toDayOfYear"};
-      st.push_back(std::string(n.arg >= 0 && n.arg < 6 ? dp[n.arg] : "datepart") + "(" + pop() + ")");
+      static const char *dp[] = {"toYear",      "toMonth",     "toDayOfMonth", "toQuarter",
+                                 "toDayOfWeek", "toDayOfYear", "toYYYYMM",     "toYYYYMMDD"};
+      st.push_back(std::string(n.arg >= 0 && n.arg < 8 ? dp[n.arg] : "datepart") + "(" + pop() + ")");
     } else if (n.op == NUT_P_NOT || n.op == NUT_P_BITNOT || n.op == NUT_P_ABS || n.op == NUT_P_TO_F64) {
       const char *f = n.op == NUT_P_NOT ? "not" : n.op == NUT_P_BITNOT ? "~" : n.op == NUT_P_ABS ? "abs" : "toFloat64";
       st.push_back(std::string(f) + "(" + pop() + ")");
@@ -1643,13 +1683,17 @@ std::string describe(const nut_plan &p) {
     }
     o += "]";
   } else {
+    // a computed projection shows as its program (infix)
+    auto proj_text = [&](size_t j) {
+      return p.projs[j] >= 0 ? p.cols[p.projs[j]] : prog_text(p, p.proj_val[j]);
+    };
     o += ",\"column\":";
-    json_str(o, p.cols[p.proj]);
-    if (p.projs.size() > 1) {
+    json_str(o, proj_text(0));
+    if (p.projs.size() > 1 || p.projs[0] < 0) {
       o += ",\"project\":[";
       for (size_t j = 0; j < p.projs.size(); ++j) {
         if (j) o += ',';
-        json_str(o, p.cols[p.projs[j]]);
+        json_str(o, proj_text(j));
       }
       o += ']';
     }
@@ -1853,10 +1897,16 @@ nut_status topk_reduce(nut_ctx *c, const nut_plan &p, const void *keys, int type
   return NUT_OK;
 }
 
-// ORDER BY with projected columns / several keys (SQL scans): the selected row ids are
-// sorted by the keys — one stable (key, row id) sort per key, the least significant
-// first (nut_sort_pairs) — and every projected column is gathered through them.  With a
-// LIMIT, only the rows top-k selection keeps on the most significant key are sorted.
+bool computed_proj(const nut_plan &p, size_t j) { return j < p.proj_val.size() && !p.proj_val[j].empty(); }
+
+// Row-id scans (expression mode): ORDER BY with projected columns / several keys, several
+// projections, computed projections.  The selected row ids (nut_select_rows, ascending)
+// are sorted by the ORDER BY keys — one stable (key, row id) sort per key, the least
+// significant first (nut_sort_pairs); with a LIMIT only the rows top-k selection keeps on
+// the most significant key are sorted, and without ORDER BY only the first offset + limit
+// ids are kept.  Every plain projection is then gathered through the ids and every
+// computed one evaluated at them (nut_eval_rows, up to 8 programs per launch); a computed
+// projection's NULL mask fills the result's validity flags.
 nut_status exec_sort_rows(nut_ctx *c, const nut_plan &p, const nut_column *const *bound, const Dict *const *dicts,
                           uint64_t n, nut_result *r) {
   for (const auto &k : p.sort_keys) {
@@ -1866,9 +1916,44 @@ nut_status exec_sort_rows(nut_ctx *c, const nut_plan &p, const nut_column *const
     if (bound[k.first]->type != NUT_T_I64 && bound[k.first]->type != NUT_T_F64)
       return fail(NUT_ERR_PLAN, "ORDER BY column '" + p.cols[k.first] + "' must be int64 or float64");
   }
-  for (size_t j = 0; j < p.projs.size(); ++j) {
+  const size_t np = p.projs.size();
+  // computed projections: groups of <= NUT_MAX_AGGS programs, one eval spec each
+  std::vector<size_t> comp;
+  for (size_t j = 0; j < np; ++j)
+    if (computed_proj(p, j)) comp.push_back(j);
+  std::deque<ProgStore> stores;
+  std::vector<nut_agg_spec> specs;
+  std::vector<std::vector<size_t>> members;
+  std::vector<int> ctype(np, NUT_T_I64);
+  for (size_t g0 = 0; g0 < comp.size(); g0 += NUT_MAX_AGGS) {
+    nut_plan q;
+    q.compiled = true;
+    q.cols = p.cols;
+    members.emplace_back();
+    for (size_t t = g0; t < comp.size() && t < g0 + NUT_MAX_AGGS; ++t) {
+      PlanAgg a{};
+      a.op = NUT_AGG_SUM;
+      a.val = p.proj_val[comp[t]];
+      a.mask = p.proj_mask[comp[t]];
+      q.aggs.push_back(std::move(a));
+      members.back().push_back(comp[t]);
+    }
+    specs.emplace_back();
+    stores.emplace_back();
+    std::vector<int> f64;
+    nut_status s = build_spec(q, bound, dicts, n, specs.back(), stores.back(), f64);
+    if (s) return s;
+    for (size_t t = 0; t < members.back().size(); ++t) ctype[members.back()[t]] = f64[t] ? NUT_T_F64 : NUT_T_I64;
+  }
+  // a string output: a plain dictionary column, or a computed projection that is one (the
+  // NULL-masked column of a LEFT-joined table)
+  std::vector<int> sdict(np, -1);
+  for (size_t j = 0; j < np; ++j) {
+    int dc = p.projs[j];
+    if (computed_proj(p, j)) dc = p.proj_val[j].size() == 1 && p.proj_val[j][0].op == NUT_P_COL ? p.proj_val[j][0].col : -1;
+    if (dc >= 0 && dicts && dicts[dc]) sdict[j] = dc;
     r->names.push_back(p.outs[j].name);
-    r->types.push_back(dicts && dicts[p.projs[j]] ? NUT_T_STR : bound[p.projs[j]]->type);
+    r->types.push_back(sdict[j] >= 0 ? NUT_T_STR : p.projs[j] >= 0 ? bound[p.projs[j]]->type : ctype[j]);
   }
   uint64_t cnt = 0;
   DevBuf rows, perm, keys;
@@ -1876,13 +1961,19 @@ nut_status exec_sort_rows(nut_ctx *c, const nut_plan &p, const nut_column *const
     nut_agg_spec sp;
     ProgStore store;
     std::vector<int> agg_f64;
-    nut_status s = build_spec(p, bound, dicts, n, sp, store, agg_f64);
+    nut_plan q = p;  // the WHERE program alone
+    q.aggs.clear();
+    nut_status s = build_spec(q, bound, dicts, n, sp, store, agg_f64);
     if (s) return s;
     NUT_HIP(rows.alloc(c, n * 8));
     s = nut_select_rows(c, &sp, (int64_t *)rows.p, &cnt);
     if (s) return s;
   }
-  if (cnt && p.has_limit) {
+  if (cnt && p.has_limit && p.sort_keys.empty()) {
+    // no ORDER BY: the first offset + limit selected rows (table order)
+    const uint64_t need = p.offset >= cnt ? 0 : p.offset + std::min<uint64_t>(p.limit, cnt - p.offset);
+    cnt = std::min(cnt, need);
+  } else if (cnt && p.has_limit) {
     // top-k on the most significant key: keep the candidate rows (ascending ids)
     const nut_column *kc = bound[p.sort_keys[0].first];
     NUT_HIP(keys.alloc(c, cnt * 8));
@@ -1902,8 +1993,13 @@ nut_status exec_sort_rows(nut_ctx *c, const nut_plan &p, const nut_column *const
     keys.reset();
   }
   const uint64_t m = std::max<uint64_t>(cnt, 1);
-  NUT_HIP(hipMalloc(&r->dev, m * 8 * p.projs.size()));
+  NUT_HIP(hipMalloc(&r->dev, m * 8 * np));
   r->dev_stride = cnt;
+  int nvalid = 0;
+  r->valid_of.assign(np, -1);
+  for (size_t j : comp)
+    if (!p.proj_mask[j].empty()) r->valid_of[j] = nvalid++;
+  if (nvalid) NUT_HIP(hipMalloc(&r->valid, m * nvalid));
   if (cnt) {
     NUT_HIP(perm.alloc(c, m * 8));
     NUT_HIP(keys.alloc(c, m * 8));
@@ -1915,9 +2011,20 @@ nut_status exec_sort_rows(nut_ctx *c, const nut_plan &p, const nut_column *const
                                  (int64_t *)perm.p, cnt);
       std::swap(rows.p, perm.p);  // the sorted row ids feed the next (more significant) key
     }
-    for (size_t j = 0; j < p.projs.size() && !s; ++j)
-      s = nut_gather_u64(c, (const uint64_t *)bound[p.projs[j]]->data, (const int64_t *)rows.p, cnt, 0,
-                         (uint64_t *)r->dev + j * cnt);
+    for (size_t j = 0; j < np && !s; ++j)
+      if (!computed_proj(p, j))
+        s = nut_gather_u64(c, (const uint64_t *)bound[p.projs[j]]->data, (const int64_t *)rows.p, cnt, 0,
+                           (uint64_t *)r->dev + j * cnt);
+    for (size_t g = 0; g < specs.size() && !s; ++g) {
+      uint64_t *outs[NUT_MAX_AGGS] = {};
+      uint8_t *vals[NUT_MAX_AGGS] = {};
+      for (size_t t = 0; t < members[g].size(); ++t) {
+        const size_t j = members[g][t];
+        outs[t] = (uint64_t *)r->dev + j * cnt;
+        vals[t] = r->valid_of[j] >= 0 ? r->valid + (uint64_t)r->valid_of[j] * cnt : nullptr;
+      }
+      s = nut_eval_rows(c, &specs[g], (const int64_t *)rows.p, cnt, outs, vals);
+    }
     if (!s) s = nut_ctx_sync(c);
     if (s) return s;
   }
@@ -1926,16 +2033,20 @@ nut_status exec_sort_rows(nut_ctx *c, const nut_plan &p, const nut_column *const
   if (p.has_limit) nrows = std::min(nrows, p.limit);
   r->dev_off = off;
   r->nrows = nrows;
-  for (size_t j = 0; j < p.projs.size(); ++j) {  // decode string columns (codes -> text)
+  for (size_t j = 0; j < np; ++j) {  // decode string columns (codes -> text; NULL rows: empty)
     if (r->types[j] != NUT_T_STR) continue;
-    r->strs.resize(p.projs.size());
+    r->strs.resize(np);
     std::vector<int64_t> codes(nrows);
+    std::vector<uint8_t> ok(nrows, 1);
     if (nrows) NUT_HIP(hipMemcpy(codes.data(), (const int64_t *)r->dev + j * r->dev_stride + off, nrows * 8,
                                  hipMemcpyDeviceToHost));
-    const Dict *d = dicts[p.projs[j]];
+    if (nrows && r->valid_of[j] >= 0)
+      NUT_HIP(hipMemcpy(ok.data(), r->valid + (uint64_t)r->valid_of[j] * r->dev_stride + off, nrows,
+                        hipMemcpyDeviceToHost));
+    const Dict *d = dicts[sdict[j]];
     r->strs[j].reserve(nrows);
-    for (int64_t cde : codes) {
-      const std::string *v = d->decode(cde);
+    for (uint64_t i = 0; i < nrows; ++i) {
+      const std::string *v = ok[i] ? d->decode(codes[i]) : nullptr;
       r->strs[j].push_back(v ? *v : std::string());
     }
   }
@@ -1944,8 +2055,10 @@ nut_status exec_sort_rows(nut_ctx *c, const nut_plan &p, const nut_column *const
 
 nut_status exec_scan(nut_ctx *c, const nut_plan &p, const nut_column *const *bound, const Dict *const *dicts,
                      uint64_t n, nut_result *r) {
-  if (p.kind == NUT_PLAN_SORT &&
-      !(p.sort_keys.size() == 1 && p.projs.size() == 1 && p.sort_keys[0].first == p.proj))
+  bool computed = false;
+  for (size_t j = 0; j < p.projs.size(); ++j) computed = computed || computed_proj(p, j);
+  if (computed || (p.kind == NUT_PLAN_SORT &&
+                   !(p.sort_keys.size() == 1 && p.projs.size() == 1 && p.sort_keys[0].first == p.proj)))
     return exec_sort_rows(c, p, bound, dicts, n, r);
   const nut_column *col = bound[p.proj];
   if (!p.compiled && p.kind == NUT_PLAN_FILTER && dicts && dicts[p.proj]) {
@@ -3020,6 +3133,55 @@ void add_null_mask(PlanAgg &a, int m) {
   if (had) emit(a.mask, NUT_P_AND);
 }
 
+// A scan's projections that read NULL-extended tables (outer joins): each becomes a
+// computed projection masked by those tables' matched flags — SQL NULL on the rows where a
+// table has no row (an expression over a NULL is NULL).  nullable(ci): the column's table
+// is NULL-extended; mflag(ci): the plan column of that table's matched flag.  A fused scan
+// turns into an expression-mode one (its comparisons into the WHERE program).
+bool mask_null_projections(nut_plan &q, const std::function<bool(int)> &nullable, const std::function<int(int)> &mflag) {
+  bool any = false;
+  for (size_t j = 0; j < q.projs.size(); ++j) {
+    std::vector<int> read;
+    if (q.projs[j] >= 0) read.push_back(q.projs[j]);
+    for (const PProg *pp : {&q.proj_val[j], &q.proj_mask[j]})
+      for (const PNode &nd : *pp)
+        if (nd.op == NUT_P_COL || nd.op == P_LIKE || nd.op == P_ILIKE) read.push_back(nd.col);
+    std::vector<int> flags;
+    for (int ci : read)
+      if (nullable(ci)) {
+        const int f = mflag(ci);
+        if (std::find(flags.begin(), flags.end(), f) == flags.end()) flags.push_back(f);
+      }
+    if (flags.empty()) continue;
+    any = true;
+    if (q.projs[j] >= 0) {
+      PNode col;
+      col.op = NUT_P_COL;
+      col.col = q.projs[j];
+      q.proj_val[j] = PProg{col};
+      q.projs[j] = -1;
+    }
+    for (int f : flags) {
+      const bool had = !q.proj_mask[j].empty();
+      PNode col;
+      col.op = NUT_P_COL;
+      col.col = f;
+      q.proj_mask[j].push_back(col);
+      emit_int(q.proj_mask[j], 0);
+      emit(q.proj_mask[j], NUT_P_NE);
+      if (had) emit(q.proj_mask[j], NUT_P_AND);
+    }
+  }
+  if (any && !q.compiled) {
+    std::vector<PProg> cs;
+    for (const PlanPred &pr : q.preds) cs.push_back(pred_prog(pr));
+    q.preds.clear();
+    q.where = and_all(cs);
+    q.compiled = true;
+  }
+  return any;
+}
+
 // ldict / rdict (may be null): the dictionary of each column of lc / rc (typed tables)
 nut_status exec_join(nut_ctx *c, const nut_plan &p, const nut_column *lc, int nl, uint64_t lrows,
                      const nut_column *rc, int nr, uint64_t rrows, uint64_t hint, nut_result *r,
@@ -3076,10 +3238,16 @@ nut_status exec_join(nut_ctx *c, const nut_plan &p, const nut_column *lc, int nl
       if ((nd.op == NUT_P_COL || nd.op == P_LIKE || nd.op == P_ILIKE) && nd.col == i) return true;
     return false;
   };
-  // read by plan q after the join: as a row decider / projection, or inside an aggregate
-  auto reads = [&](const nut_plan &q, int ci, bool &row, bool &agg) {
-    row = ci == q.proj || in_prog(q.where, ci);
-    for (int pj : q.projs) row = row || pj == ci;
+  // read by plan q after the join: as a row decider, a projection (proj NULL: counted as a
+  // row decider), or inside an aggregate
+  auto reads = [&](const nut_plan &q, int ci, bool &row, bool &agg, bool *proj = nullptr) {
+    bool pr = ci == q.proj;
+    for (int pj : q.projs) pr = pr || pj == ci;
+    for (const PProg &pp : q.proj_val) pr = pr || in_prog(pp, ci);
+    for (const PProg &pp : q.proj_mask) pr = pr || in_prog(pp, ci);
+    row = in_prog(q.where, ci);
+    if (proj) *proj = pr;
+    else row = row || pr;
     for (int k : q.keys) row = row || k == ci;
     for (const PProg &kp : q.key_progs) row = row || in_prog(kp, ci);  // computed keys
     for (const auto &sk : q.sort_keys) row = row || sk.first == ci;  // ORDER BY, projected or not
@@ -3091,20 +3259,26 @@ nut_status exec_join(nut_ctx *c, const nut_plan &p, const nut_column *lc, int nl
       agg = agg || in_prog(a.val, ci) || in_prog(a.mask, ci);
     }
   };
+  // a NULL-extended table's column may feed aggregates (they skip its NULL rows) and scan
+  // projections (NULL there), not WHERE / GROUP BY / ORDER BY or IS [NOT] NULL
+  auto null_side = [&](int ci) { return full || (outer && side[ci] != ps); };
   for (size_t i = 0; i < nc; ++i) {
     const int ci = (int)i;
-    bool row, agg;
-    reads(p, ci, row, agg);
-    if (full && row && side[i] >= 0)
-      return fail(NUT_ERR_PLAN, "FULL OUTER JOIN: column '" + p.cols[i] + "' may only appear inside aggregates");
+    bool row, agg, proj;
+    reads(p, ci, row, agg, &proj);
+    const bool isnull = std::find(p.isnull_cols.begin(), p.isnull_cols.end(), ci) != p.isnull_cols.end();
+    if (full && (row || isnull))
+      return fail(NUT_ERR_PLAN, "FULL OUTER JOIN: column '" + p.cols[i] + "' may only appear inside aggregates and "
+                                "projections");
     if (side[i] == ps) continue;
     if (p.join == NUT_JOIN_SEMI || p.join == NUT_JOIN_ANTI) {
       // SEMI: the other table's ON column equals the preserved one; nothing else exists
-      if ((row || agg) && !(p.join == NUT_JOIN_SEMI && ci == bkey))
+      if ((row || agg || proj) && !(p.join == NUT_JOIN_SEMI && ci == bkey))
         return fail(NUT_ERR_PLAN, "SEMI / ANTI JOIN output only the preserved table's columns ('" + p.cols[i] + "')");
-    } else if (outer && row) {
+    } else if (outer && (row || isnull)) {
       return fail(NUT_ERR_PLAN, "outer JOIN: the NULL-extended table's column '" + p.cols[i] +
-                                    "' may only appear inside aggregates");
+                                    "' may only appear inside aggregates and projections" +
+                                    (isnull ? " (IS [NOT] NULL over it is not executed)" : ""));
     }
   }
   // ---- predicate pushdown: WHERE conjuncts that read one table filter that table before
@@ -3217,7 +3391,13 @@ nut_status exec_join(nut_ctx *c, const nut_plan &p, const nut_column *lc, int nl
     npairs = tot;
   }
   // the joined table: every plan column gathered through its side's index
-  const bool mask_col = outer && p.kind == NUT_PLAN_GROUPBY;
+  bool proj_null = false;  // a scan projecting a NULL-extended table's column
+  for (size_t i = 0; i < nc && outer && p.kind != NUT_PLAN_GROUPBY; ++i) {
+    bool row, agg, proj;
+    reads(p2, (int)i, row, agg, &proj);
+    proj_null = proj_null || (proj && null_side((int)i));
+  }
+  const bool mask_col = outer && (p.kind == NUT_PLAN_GROUPBY || proj_null);
   std::vector<DevBuf> bufs(nc + 1);
   std::vector<nut_column> jc(nc + 1);
   for (size_t i = 0; i < nc; ++i) {
@@ -3258,6 +3438,8 @@ nut_status exec_join(nut_ctx *c, const nut_plan &p, const nut_column *lc, int nl
       if (other) add_null_mask(a, (int)nc);
       if (full && mine) add_null_mask(a, (int)nc + 1);
     }
+    if (proj_null)
+      mask_null_projections(p2, null_side, [&](int ci) { return side[ci] == ps ? (int)nc + 1 : (int)nc; });
   }
   std::vector<const nut_column *> bound(p2.cols.size());
   for (size_t i = 0; i < p2.cols.size(); ++i) bound[i] = &jc[i];
@@ -3338,10 +3520,13 @@ nut_status exec_joinn(nut_ctx *c, const nut_plan &p, const nut_column *const *ta
       if ((nd.op == NUT_P_COL || nd.op == P_LIKE || nd.op == P_ILIKE) && nd.col == i) return true;
     return false;
   };
-  // read by plan q after the joins: as a row decider / projection / key, or inside an aggregate
-  auto reads = [&](const nut_plan &q, int ci, bool &row, bool &agg) {
-    row = ci == q.proj || in_prog(q.where, ci);
-    for (int pj : q.projs) row = row || pj == ci;
+  // read by plan q after the joins: as a row decider / key, a projection, or inside an aggregate
+  auto reads = [&](const nut_plan &q, int ci, bool &row, bool &agg, bool &proj) {
+    proj = ci == q.proj;
+    for (int pj : q.projs) proj = proj || pj == ci;
+    for (const PProg &pp : q.proj_val) proj = proj || in_prog(pp, ci);
+    for (const PProg &pp : q.proj_mask) proj = proj || in_prog(pp, ci);
+    row = in_prog(q.where, ci);
     for (int k2 : q.keys) row = row || k2 == ci;
     for (const PProg &kp : q.key_progs) row = row || in_prog(kp, ci);  // computed keys
     for (const auto &sk : q.sort_keys) row = row || sk.first == ci;  // ORDER BY, projected or not
@@ -3359,12 +3544,16 @@ nut_status exec_joinn(nut_ctx *c, const nut_plan &p, const nut_column *const *ta
   // which skip the NULL rows.
   std::vector<char> nullable(nt, 0);
   for (int k = 0; k + 1 < nt; ++k) nullable[k + 1] = p.jn[k].type == NUT_JOIN_LEFT;
+  bool proj_null = false;  // a scan projecting a NULL-extended table's column (NULL there)
   for (size_t i = 0; i < nc; ++i) {
-    bool row, agg;
-    reads(p, (int)i, row, agg);
-    if (row && nullable[side[i]])
+    bool row, agg, proj;
+    reads(p, (int)i, row, agg, proj);
+    const bool isnull = std::find(p.isnull_cols.begin(), p.isnull_cols.end(), (int)i) != p.isnull_cols.end();
+    if ((row || isnull) && nullable[side[i]])
       return fail(NUT_ERR_PLAN, "outer JOIN: the NULL-extended table's column '" + p.cols[i] +
-                                    "' may only appear inside aggregates");
+                                    "' may only appear inside aggregates and projections" +
+                                    (isnull ? " (IS [NOT] NULL over it is not executed)" : ""));
+    proj_null = proj_null || (proj && nullable[side[i]] && p.kind != NUT_PLAN_GROUPBY);
   }
   nut_plan p2 = p;
   std::vector<std::vector<PProg>> push(nt);
@@ -3503,6 +3692,8 @@ nut_status exec_joinn(nut_ctx *c, const nut_plan &p, const nut_column *const *ta
     const int ci = (int)i;
     bool used = ci == p2.proj || in_prog(p2.where, ci);
     for (int pj : p2.projs) used = used || pj == ci;
+    for (const PProg &pp : p2.proj_val) used = used || in_prog(pp, ci);
+    for (const PProg &pp : p2.proj_mask) used = used || in_prog(pp, ci);
     for (int k2 : p2.keys) used = used || k2 == ci;
     for (const auto &sk : p2.sort_keys) used = used || sk.first == ci;
     for (const PlanPred &pr : p2.preds) used = used || pr.col == ci;
@@ -3522,7 +3713,8 @@ nut_status exec_joinn(nut_ctx *c, const nut_plan &p, const nut_column *const *ta
   // aggregates over a NULL-extended table skip its NULL rows: (__matched<t> != 0) per table read
   std::vector<DevBuf> mbuf(nt);
   p2.cols.reserve(nc + nt);  // jc keeps c_str() pointers into p2.cols
-  for (int v = 1; v < nt && p2.kind == NUT_PLAN_GROUPBY; ++v) {
+  std::vector<int> mflag(nt, -1);
+  for (int v = 1; v < nt && (p2.kind == NUT_PLAN_GROUPBY || proj_null); ++v) {
     if (!nullable[v]) continue;
     std::vector<PlanAgg *> reading;
     for (PlanAgg &a : p2.aggs) {
@@ -3530,14 +3722,24 @@ nut_status exec_joinn(nut_ctx *c, const nut_plan &p, const nut_column *const *ta
       for (int ref : a.refs) rd = rd || side[ref] == v;
       if (rd) reading.push_back(&a);
     }
-    if (reading.empty()) continue;
+    bool projected = false;
+    for (size_t i = 0; i < nc && proj_null; ++i) {
+      bool row, agg, proj;
+      reads(p2, (int)i, row, agg, proj);
+      projected = projected || (proj && side[i] == v);
+    }
+    if (reading.empty() && !projected) continue;
     if (mbuf[v].alloc(c, std::max<uint64_t>(ncur, 1) * 8) != hipSuccess) return fail(NUT_ERR_OOM, "hipMalloc");
     if ((st = join_matched(c, accp[v], ncur, (int64_t *)mbuf[v].p))) return st;
     const int mc = (int)p2.cols.size();
     p2.cols.push_back("__matched" + std::to_string(v));
     jc.push_back(nut_column{p2.cols[mc].c_str(), mbuf[v].p, NUT_T_I64});
     for (PlanAgg *a : reading) add_null_mask(*a, mc);
+    mflag[v] = mc;
   }
+  if (proj_null)
+    mask_null_projections(p2, [&](int ci) { return ci < (int)nc && nullable[side[ci]] != 0; },
+                          [&](int ci) { return mflag[side[ci]]; });
   sdict.resize(p2.cols.size());
   std::vector<const nut_column *> bound(jc.size());
   for (size_t i = 0; i < jc.size(); ++i) bound[i] = &jc[i];
@@ -3778,7 +3980,29 @@ nut_status nut_plan_prepare(const nut_plan *p, const nut_column *cols, int ncols
   std::vector<int> agg_f64;
   nut_status st = build_spec(*p, bound.data(), nullptr, 0, s, store, agg_f64);
   if (st) return st;
-  return p->kind == NUT_PLAN_GROUPBY ? nut_groupby_jit_compile(&s) : nut_select_jit_compile(&s);
+  st = p->kind == NUT_PLAN_GROUPBY ? nut_groupby_jit_compile(&s) : nut_select_jit_compile(&s);
+  // computed projections: their evaluation kernels (groups of NUT_MAX_AGGS, as executed)
+  std::vector<size_t> comp;
+  for (size_t j = 0; j < p->projs.size(); ++j)
+    if (computed_proj(*p, j)) comp.push_back(j);
+  for (size_t g0 = 0; g0 < comp.size() && !st; g0 += NUT_MAX_AGGS) {
+    nut_plan q;
+    q.compiled = true;
+    q.cols = p->cols;
+    for (size_t t = g0; t < comp.size() && t < g0 + NUT_MAX_AGGS; ++t) {
+      PlanAgg a{};
+      a.op = NUT_AGG_SUM;
+      a.val = p->proj_val[comp[t]];
+      a.mask = p->proj_mask[comp[t]];
+      q.aggs.push_back(std::move(a));
+    }
+    nut_agg_spec es;
+    ProgStore estore;
+    std::vector<int> f64;
+    st = build_spec(q, bound.data(), nullptr, 0, es, estore, f64);
+    if (!st) st = nut_eval_jit_compile(&es);
+  }
+  return st;
 }
 
 nut_status nut_table_execute(nut_ctx *c, nut_table *t, const nut_plan *p, uint64_t group_hint, nut_result **out) {
@@ -3959,7 +4183,34 @@ void nut_result_free(nut_result *r) {
     DeviceGuard g(r->device);
     (void)hipFree(r->dev);
   }
+  if (r->valid) {
+    DeviceGuard g(r->device);
+    (void)hipFree(r->valid);
+  }
   delete r;
+}
+
+nut_status nut_result_validity(const nut_result *r, int j, const uint8_t **dev) {
+  if (!r || !dev || j < 0 || j >= (int)r->names.size()) return fail(NUT_ERR_INVALID_ARG, "nut_result_validity: bad argument");
+  const int v = j < (int)r->valid_of.size() ? r->valid_of[j] : -1;
+  *dev = v >= 0 && r->valid ? r->valid + (uint64_t)v * r->dev_stride + r->dev_off : nullptr;
+  return NUT_OK;
+}
+
+nut_status nut_result_validity_to_host(const nut_result *r, int j, uint8_t *dst, uint64_t cap) {
+  const uint8_t *dev = nullptr;
+  nut_status s = nut_result_validity(r, j, &dev);
+  if (s) return s;
+  if (r->nrows > cap) return fail(NUT_ERR_CAPACITY, "nut_result_validity_to_host: capacity < " + std::to_string(r->nrows));
+  if (r->nrows == 0) return NUT_OK;
+  if (!dst) return fail(NUT_ERR_INVALID_ARG, "nut_result_validity_to_host: NULL dst");
+  if (!dev) {
+    memset(dst, 1, r->nrows);
+    return NUT_OK;
+  }
+  DeviceGuard g(r->device);
+  NUT_HIP(hipMemcpy(dst, dev, r->nrows, hipMemcpyDeviceToHost));
+  return NUT_OK;
 }
 
 }  // extern "C"

@@ -127,7 +127,8 @@ def unescape_double_quoted_string(s: str) -> str:
 
 def read_result(res) -> Dict[str, np.ndarray]:
     """nut_result -> {output name: numpy array} (NUT_T_STR columns: object arrays of str);
-    frees the result."""
+    a column holding SQL NULLs (nut_result_validity: a LEFT-joined table's column, a CASE
+    without ELSE) is a numpy masked array, masked where NULL.  Frees the result."""
     try:
         nr = C.c_uint64(0)
         nc = C.c_int(0)
@@ -146,6 +147,13 @@ def read_result(res) -> Dict[str, np.ndarray]:
             else:
                 a = np.empty(nr.value, dtype=np.float64 if typ.value == T_F64 else np.int64)
                 check(lib.nut_result_to_host(res, j, a.ctypes.data_as(C.c_void_p), nr.value), "nut_result_to_host")
+            vd = C.c_void_p()  # (any type: string columns hold NULLs too)
+            check(lib.nut_result_validity(res, j, C.byref(vd)), "nut_result_validity")
+            if vd.value:
+                ok = np.empty(nr.value, dtype=np.uint8)
+                check(lib.nut_result_validity_to_host(res, j, ok.ctypes.data_as(C.c_void_p), nr.value),
+                      "nut_result_validity_to_host")
+                a = np.ma.masked_array(a, mask=ok == 0)
             out[nm.value.decode()] = a
         return out
     finally:

@@ -36,7 +36,7 @@ OP = {name: i for i, name in enumerate(OPS)}
 I64, F64, BOOL = 0, 1, 2
 _ARITY = {OP["not"]: 1, OP["bitnot"]: 1, OP["abs"]: 1, OP["to_f64"]: 1, OP["if"]: 3, OP["lookup"]: 1,
           OP["datepart"]: 1}
-DP_YEAR, DP_MONTH, DP_DAY, DP_QUARTER, DP_WEEKDAY, DP_YEARDAY = range(6)
+DP_YEAR, DP_MONTH, DP_DAY, DP_QUARTER, DP_WEEKDAY, DP_YEARDAY, DP_YYYYMM, DP_YYYYMMDD = range(8)
 
 
 def _tdiv(a, b: int):
@@ -69,6 +69,10 @@ def date_part(days, part: int):
     if part == DP_YEARDAY:
         leap = ((y % 4 == 0) & (y % 100 != 0)) | (y % 400 == 0)
         return np.where(doy >= 306, doy - 305, doy + 60 + leap)
+    if part == DP_YYYYMM:
+        return y * 100 + m
+    if part == DP_YYYYMMDD:
+        return y * 10000 + m * 100 + (doy - _tdiv(153 * mp + 2, 5) + 1)
     raise ProgramError(f"unknown date part {part}")
 
 

@@ -382,6 +382,7 @@ def test_date_part_oracle_matches_calendar():
         0: [x.year for x in dates], 1: [x.month for x in dates], 2: [x.day for x in dates],
         3: [(x.month - 1) // 3 + 1 for x in dates], 4: [x.isoweekday() for x in dates],
         5: [x.timetuple().tm_yday for x in dates],
+        6: [x.year * 100 + x.month for x in dates], 7: [int(x.strftime("%Y%m%d")) for x in dates],
     }
     for part, w in want.items():
         assert date_part(days, part).tolist() == w, part
@@ -389,3 +390,29 @@ def test_date_part_oracle_matches_calendar():
     big = np.array([2**62, -2**62, 2**40, -2**40], dtype=np.int64)
     assert date_part(big, 0).tolist() == [date_part(np.array([2**40]), 0)[0]] * 1 + \
         [date_part(np.array([-2**40]), 0)[0]] + date_part(big[2:], 0).tolist()
+
+
+def test_plan_computed_projections():
+    """SELECT items that are expressions (no aggregate anywhere) are computed projections of
+    an expression-mode scan (nut_eval_rows on the selected rows); a CASE without ELSE is a
+    NULL mask; an aggregate inside arithmetic makes a global aggregate instead."""
+    d = Plan("select a * 2 + b as s, toYYYYMMDD(d), a from t where a > 1 order by a limit 3").describe()
+    assert d["kind"] == "sort" and d["mode"] == "compiled"
+    assert d["project"] == ["((a * 2) + b)", "toYYYYMMDD(d)", "a"]
+    assert [o["name"] for o in d["outputs"]] == ["s", "toYYYYMMDD(d)", "a"]
+    d = Plan("select abs(x), case when x > 0 then x end from t").describe()
+    assert d["kind"] == "filter" and d["mode"] == "compiled" and len(d["project"]) == 2
+    assert Plan("select sum(a) / sum(b) from t").kind == "groupby"
+    with pytest.raises(NutError, match="ORDER BY a computed projection"):
+        Plan("select a + 1 as c from t order by c")
+
+
+@pytest.mark.parametrize("sql,types", [
+    ("select a * 2 + b, toYYYYMM(d), case when b > 0.5 then b end from t where a > 1",
+     {"a": "int64", "b": "float64", "d": "int64"}),
+    ("select " + ", ".join(f"a + {i}" for i in range(10)) + " from t order by a",
+     {"a": "int64"})])
+def test_eval_jit_compiles(sql, types):
+    """the evaluation kernels (select_kernel.hpp eval_kernel, <= 8 programs each) of computed
+    projections compile with hipRTC next to the scan kernel"""
+    Plan(sql).prepare(types)
