@@ -366,6 +366,7 @@ struct nut_plan {
   std::vector<int> projs;         // every projected column (expression-mode scans: several; computed: -1)
   std::vector<PProg> proj_val, proj_mask;  // per projection: its program and NULL mask (plain columns: empty)
   std::vector<int> isnull_cols;   // columns under an IS [NOT] NULL (folded to a constant)
+  bool star = false;              // SELECT *: every bound column, expanded at execution (expand_star)
   bool desc = false;              // SORT direction
   // SORT: the ORDER BY keys as (plan column, desc), most significant first.  One key equal
   // to the only projected column: a keys-only sort; otherwise row ids are sorted by the
@@ -1299,7 +1300,7 @@ bool lower_mode(const Statement &st, nut_plan &p, Lowering &L) {
       p.jn.push_back(js);
       join_extra.insert(join_extra.end(), eqs.begin() + 1, eqs.end());
     }
-    if (p.jn.size() > 7) return L.fail("at most 8 joined tables");
+    if (p.jn.size() > 15) return L.fail("at most 16 joined tables");
     p.jtable = p.jn[0].table;
     p.jalias = p.jn[0].alias;
     p.jkey[0] = p.jn[0].key[0];
@@ -1468,6 +1469,29 @@ bool lower_mode(const Statement &st, nut_plan &p, Lowering &L) {
   // nut_eval_rows; a CASE branch without ELSE yields NULL)
   sv name;
   if (b.columns.empty()) return L.fail("a plan without GROUP BY projects columns");
+  for (const QueryExpr &q : b.columns)
+    if (q.e.k == EK::Identifier && q.e.id.wildcard) {
+      // SELECT * (the reference's criterion statement `SELECT * FROM table WHERE 1 = 1`):
+      // every column the execution binds, in binding order
+      if (b.columns.size() != 1 || q.e.id.qualified || q.alias)
+        return L.fail("SELECT * is executed alone and unqualified");
+      if (!p.compiled) return L.fail("SELECT * runs in expression mode");
+      if (p.join >= 0 || !p.jn.empty()) return L.fail("SELECT * over a JOIN is not executed (name the columns)");
+      p.star = true;
+      std::vector<std::pair<int, bool>> okeys;
+      if (b.order_by)
+        for (const OrderKey &k : *b.order_by) {
+          sv oname;
+          if (!column_ref(p, k.e.e, oname)) return L.fail("ORDER BY '" + expr_text(k.e.e) + "' is not a column");
+          okeys.push_back({col_index(p, oname), k.desc});
+        }
+      p.kind = b.order_by ? NUT_PLAN_SORT : NUT_PLAN_FILTER;
+      if (b.order_by) {
+        p.desc = okeys[0].second;
+        p.sort_keys = okeys;
+      }
+      return true;
+    }
   for (size_t j = 0; j < b.columns.size(); ++j) {
     PlanOut o;
     o.kind = OUT_KEY;
@@ -1688,8 +1712,8 @@ std::string describe(const nut_plan &p) {
       return p.projs[j] >= 0 ? p.cols[p.projs[j]] : prog_text(p, p.proj_val[j]);
     };
     o += ",\"column\":";
-    json_str(o, proj_text(0));
-    if (p.projs.size() > 1 || p.projs[0] < 0) {
+    json_str(o, p.star ? std::string("*") : proj_text(0));
+    if (!p.star && (p.projs.size() > 1 || p.projs[0] < 0)) {
       o += ",\"project\":[";
       for (size_t j = 0; j < p.projs.size(); ++j) {
         if (j) o += ',';
@@ -3182,6 +3206,33 @@ bool mask_null_projections(nut_plan &q, const std::function<bool(int)> &nullable
   return any;
 }
 
+// SELECT *: the plan with every bound column projected, in binding order (names: the
+// execution's columns); other plans are returned as they are
+const nut_plan *expand_star(const nut_plan &p, const std::vector<std::string> &names, nut_plan &q) {
+  if (!p.star) return &p;
+  q = p;
+  q.star = false;
+  for (const std::string &nm : names) {
+    int idx = -1;
+    for (size_t i = 0; i < q.cols.size() && idx < 0; ++i)
+      if (ieq(q.cols[i], nm)) idx = (int)i;
+    if (idx < 0) {
+      idx = (int)q.cols.size();
+      q.cols.push_back(nm);
+    }
+    q.projs.push_back(idx);
+    q.proj_val.emplace_back();
+    q.proj_mask.emplace_back();
+    PlanOut o;
+    o.kind = OUT_KEY;
+    o.a = (int)q.outs.size();
+    o.text = o.name = nm;
+    q.outs.push_back(o);
+  }
+  q.proj = q.projs.empty() ? -1 : q.projs[0];
+  return &q;
+}
+
 // ldict / rdict (may be null): the dictionary of each column of lc / rc (typed tables)
 nut_status exec_join(nut_ctx *c, const nut_plan &p, const nut_column *lc, int nl, uint64_t lrows,
                      const nut_column *rc, int nr, uint64_t rrows, uint64_t hint, nut_result *r,
@@ -3875,6 +3926,14 @@ nut_status nut_plan_execute(nut_ctx *c, const nut_plan *p, const nut_column *col
   if (!c || !p || !out || (ncols && !cols) || ncols < 0) return fail(NUT_ERR_INVALID_ARG, "nut_plan_execute: NULL argument");
   *out = nullptr;
   if (p->join >= 0) return fail(NUT_ERR_INVALID_ARG, "nut_plan_execute: the plan has a JOIN (nut_plan_execute2)");
+  nut_plan sq;
+  if (p->star) {
+    std::vector<std::string> names;
+    for (int i = 0; i < ncols; ++i)
+      if (cols[i].name) names.push_back(cols[i].name);
+    if (names.empty()) return fail(NUT_ERR_INVALID_ARG, "nut_plan_execute: SELECT * over no columns");
+    p = expand_star(*p, names, sq);
+  }
   DeviceGuard g0(c->device);
   HostStage hs;
   nut_status hst = stage_host(c, cols, ncols, nrows, hs, &cols);
@@ -3964,6 +4023,13 @@ nut_status nut_plan_executen(nut_ctx *c, const nut_plan *p, const nut_column *co
 nut_status nut_plan_prepare(const nut_plan *p, const nut_column *cols, int ncols) {
   if (!p || (ncols && !cols) || ncols < 0) return fail(NUT_ERR_INVALID_ARG, "nut_plan_prepare: NULL argument");
   if (!p->compiled) return NUT_OK;  // precompiled kernels only
+  nut_plan sq;
+  if (p->star) {
+    std::vector<std::string> names;
+    for (int i = 0; i < ncols; ++i)
+      if (cols[i].name) names.push_back(cols[i].name);
+    p = expand_star(*p, names, sq);
+  }
   std::vector<const nut_column *> bound(p->cols.size());
   std::vector<nut_column> typed(p->cols.size());
   for (size_t i = 0; i < p->cols.size(); ++i) {
@@ -4012,6 +4078,13 @@ nut_status nut_table_execute(nut_ctx *c, nut_table *t, const nut_plan *p, uint64
   if (t->device >= 0 && t->device != c->device)
     return fail(NUT_ERR_INVALID_ARG, "nut_table_execute: the table lives on another device");
   const uint64_t nrows = t->rows();
+  nut_plan sq;
+  if (p->star) {
+    std::vector<std::string> names;
+    for (const TCol &x : t->cols) names.push_back(x.name);
+    if (names.empty()) return fail(NUT_ERR_INVALID_ARG, "nut_table_execute: SELECT * over no columns");
+    p = expand_star(*p, names, sq);
+  }
   std::vector<nut_column> cols(p->cols.size());
   std::vector<const nut_column *> bound(p->cols.size());
   std::vector<const Dict *> dicts(p->cols.size(), nullptr);

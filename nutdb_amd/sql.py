@@ -236,7 +236,9 @@ class Plan:
 
     def _bind(self, columns):
         import torch
-        names = self.columns
+        d = self.describe()
+        names = d["columns"]
+        star = d.get("column") == "*"  # SELECT *: every column given is projected
         arr = (NutColumn * max(len(columns), 1))()
         keep = []
         n = None
@@ -257,7 +259,7 @@ class Plan:
             keep.append(nb)
             arr[i] = NutColumn(nb, t.data_ptr(), typ | (NUT_COL_HOST if host else 0))
             low = name.lower()
-            if any(low == c.lower() or c.lower().endswith("." + low) for c in names):  # JOIN plans qualify
+            if star or any(low == c.lower() or c.lower().endswith("." + low) for c in names):  # JOIN plans qualify
                 n = t.numel() if n is None else n
                 if t.numel() != n:
                     raise ValueError("bound columns differ in length")

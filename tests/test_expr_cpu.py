@@ -416,3 +416,17 @@ def test_eval_jit_compiles(sql, types):
     """the evaluation kernels (select_kernel.hpp eval_kernel, <= 8 programs each) of computed
     projections compile with hipRTC next to the scan kernel"""
     Plan(sql).prepare(types)
+
+
+def test_plan_select_star():
+    """SELECT * (the reference's criterion statement `SELECT * FROM table WHERE 1 = 1`,
+    benches/parser.rs): every column bound at execution, in binding order"""
+    d = Plan("SELECT * FROM table WHERE 1 = 1").describe()
+    assert d["kind"] == "filter" and d["column"] == "*" and d["mode"] == "compiled" and d["where_expr"] == ""
+    d = Plan("select * from t where a > 3 order by b desc limit 2").describe()
+    assert d["kind"] == "sort" and d["sort"] == [{"column": "b", "desc": True}] and d["limit"] == 2
+    for sql, frag in [("select *, a from t", "alone"), ("select t.* from t", "unqualified"),
+                      ("select * from a join b on x = y", "over a JOIN")]:
+        with pytest.raises(NutError, match=frag):
+            Plan(sql)
+    Plan("select * from t where a > 1.5 and b < 3").prepare({"a": "int64", "b": "float64", "c": "int64"})

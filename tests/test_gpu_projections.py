@@ -171,3 +171,119 @@ def test_null_projection_rejections(ex):
                "on o_okey = l_okey", o, right=l_)
     with pytest.raises(NutError, match="may only appear inside aggregates and projections"):
         ex.sql("select o_okey from orders left join lineitem on o_okey = l_okey where l_qty > 3", o, right=l_)
+
+
+def test_select_star(ex, table):
+    """SELECT * projects every bound column in binding order: the reference's criterion
+    statement (tests/golden/sql/bench_short.sql) over a table, WHERE / ORDER BY / LIMIT."""
+    from pathlib import Path
+    sql = (Path(__file__).parent / "golden" / "sql" / "bench_short.sql").read_text()
+    got = ex.sql(sql, on_dev(ex, table))
+    assert list(got) == list(table)
+    for c in table:
+        assert np.array_equal(got[c], table[c]), c
+    got = ex.sql("select * from t where k = 5 order by a desc limit 20", on_dev(ex, table))
+    sel = np.flatnonzero(table["k"] == 5)
+    o = sel[np.argsort(-table["a"][sel], kind="stable")][:20]
+    for c in table:
+        assert np.array_equal(got[c], table[c][o]), c
+
+
+def test_select_star_typed_table(ex):
+    from nutdb_amd.table import Table
+    rng = np.random.default_rng(8)
+    n = 10_007
+    s = np.array(["lo", "mid", "hi"], dtype=object)[rng.integers(0, 3, n)]
+    v = rng.integers(-50, 50, n)
+    t = Table(ex, "CREATE TABLE t (s String, v Int32, f Float64)")
+    f = rng.random(n)
+    t.append(s=s, v=v.astype(np.int32), f=f)
+    got = t.sql("select * from t where v > 10")
+    m = v > 10
+    assert list(got) == ["s", "v", "f"]
+    assert got["s"].tolist() == s[m].tolist() and got["v"].tolist() == v[m].tolist()
+    assert np.array_equal(got["f"], f[m])
+
+
+FIXTURE10_NUMERIC = """SELECT
+    e.employee_id AS `Employee #`,
+    toYYYYMMDD(e.hire_date) AS `Hire Date`,
+    e.commission_pct AS `Comission %`,
+    jh.job_id AS `History Job ID`,
+    case jh.level >> jh.offset
+        when 0x1 then 1
+        when 0x2 then 2
+        when 0x3 then 3
+        else jh.n * (jh.k + 1 * 3 % 4)
+    end AS level,
+    r.region_id AS region,
+    dd.location_id AS hist_location
+FROM employees AS e
+JOIN jobs AS j
+  ON e.job_id = j.job_id
+LEFT JOIN employees AS m
+  ON e.manager_id = m.employee_id
+LEFT JOIN departments AS d
+  ON d.department_id = e.department_id
+LEFT JOIN employees AS dm
+  ON d.manager_id = dm.employee_id
+LEFT JOIN locations AS l
+  ON d.location_id = l.location_id
+LEFT JOIN countries AS c
+  ON l.country_id = c.country_id
+LEFT JOIN regions AS r
+  ON c.region_id = r.region_id
+LEFT JOIN job_history AS jh
+  ON e.employee_id = jh.employee_id
+LEFT JOIN jobs AS jj
+  ON jj.job_id = jh.job_id
+LEFT JOIN departments AS dd
+  ON dd.department_id = jh.department_id
+ORDER BY
+  e.employee_id"""
+
+
+def test_fixture10_join_chain(ex):
+    """The reference fixture tests/sql/10.sql's FROM / JOIN chain verbatim (11 tables, three
+    of them twice under other aliases, 9 LEFT steps, ON keys read from NULL-extended tables),
+    its toYYYYMMDD and its CASE over jh columns, with the string items (`first_name + ' ' +
+    last_name`, the 'A'..'F' branches) replaced by numeric ones.  Reference: pandas merges."""
+    rng = np.random.default_rng(10)
+    ne, nj, nd, nl, nc, nr, nh = 2000, 30, 60, 40, 20, 5, 3000
+    i64 = lambda lo, hi, n: rng.integers(lo, hi, n).astype(np.int64)
+    emp = {"employee_id": rng.permutation(ne).astype(np.int64), "job_id": i64(0, nj + 5, ne),
+           "manager_id": i64(-5, ne, ne), "department_id": i64(0, nd + 10, ne), "hire_date": i64(5000, 20000, ne),
+           "commission_pct": rng.random(ne)}
+    jobs = {"job_id": np.arange(nj, dtype=np.int64)}
+    dept = {"department_id": np.arange(nd, dtype=np.int64), "manager_id": i64(0, ne + 100, nd),
+            "location_id": i64(0, nl + 5, nd)}
+    loc = {"location_id": np.arange(nl, dtype=np.int64), "country_id": i64(0, nc + 3, nl)}
+    ctry = {"country_id": np.arange(nc, dtype=np.int64), "region_id": i64(0, nr + 1, nc)}
+    reg = {"region_id": np.arange(nr, dtype=np.int64)}
+    hist = {"employee_id": i64(0, ne + 500, nh), "job_id": i64(0, nj + 10, nh), "department_id": i64(0, nd + 5, nh),
+            "level": i64(0, 16, nh), "offset": i64(0, 3, nh), "n": i64(-9, 9, nh), "k": i64(0, 5, nh)}
+    chain = [("j", jobs), ("m", emp), ("d", dept), ("dm", emp), ("l", loc), ("c", ctry), ("r", reg), ("jh", hist),
+             ("jj", jobs), ("dd", dept)]
+    got = ex.sql(FIXTURE10_NUMERIC, on_dev(ex, emp), right=[on_dev(ex, t) for _, t in chain])
+    # pandas: every table's columns prefixed by its alias
+    pre = lambda a, t: pd.DataFrame({f"{a}.{k}": v for k, v in t.items()})
+    m = pre("e", emp).merge(pre("j", jobs), left_on="e.job_id", right_on="j.job_id")
+    for a, t, lk, rk in [("m", emp, "e.manager_id", "m.employee_id"), ("d", dept, "e.department_id", "d.department_id"),
+                         ("dm", emp, "d.manager_id", "dm.employee_id"), ("l", loc, "d.location_id", "l.location_id"),
+                         ("c", ctry, "l.country_id", "c.country_id"), ("r", reg, "c.region_id", "r.region_id"),
+                         ("jh", hist, "e.employee_id", "jh.employee_id"), ("jj", jobs, "jh.job_id", "jj.job_id"),
+                         ("dd", dept, "jh.department_id", "dd.department_id")]:
+        m = m.merge(pre(a, t), left_on=lk, right_on=rk, how="left")
+    assert got["Employee #"].tolist() == sorted(m["e.employee_id"].tolist())
+    nn = lambda s: np.where(s.isna(), NULL, s.fillna(0)).astype(np.int64)
+    lv, off = nn(m["jh.level"]), nn(m["jh.offset"])
+    sh = lv >> np.clip(off, 0, 63)
+    level = np.where(sh == 1, 1, np.where(sh == 2, 2, np.where(sh == 3, 3, nn(m["jh.n"]) * (nn(m["jh.k"]) + 3))))
+    level = np.where(m["jh.level"].isna(), NULL, level)
+    want = rows_of([m["e.employee_id"].to_numpy(), date_part(m["e.hire_date"].to_numpy(), 7),
+                    m["e.commission_pct"].to_numpy(), nn(m["jh.job_id"]), level, nn(m["r.region_id"]),
+                    nn(m["dd.location_id"])])
+    cols = ["Employee #", "Hire Date", "Comission %", "History Job ID", "level", "region", "hist_location"]
+    assert rows_of([filled(got[c]) for c in cols]) == want
+    for c, src in (("History Job ID", "jh.job_id"), ("region", "r.region_id"), ("hist_location", "dd.location_id")):
+        assert int(np.ma.getmaskarray(got[c]).sum()) == int(m[src].isna().sum()) > 0, c
