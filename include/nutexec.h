@@ -579,11 +579,14 @@ nut_status nut_plan_execute(nut_ctx *ctx, const nut_plan *plan, const nut_column
 nut_status nut_plan_execute2(nut_ctx *ctx, const nut_plan *plan, const nut_column *left, int nleft, uint64_t lrows,
                              const nut_column *right, int nright, uint64_t rrows, uint64_t group_hint,
                              nut_result **out);
-/* Several INNER / LEFT OUTER JOINs (FROM t0 JOIN t1 ON .. LEFT JOIN t2 ON ..): tables[k] /
- * ncols[k] / nrows[k] = table k in FROM / JOIN order.  Each ON compares a column of its
- * table with a column of an earlier one; single-table WHERE conjuncts are pushed down.  A
- * LEFT-joined table is NULL on the rows without a match (a later ON reading it matches
- * nothing there); its columns may only appear inside aggregates, which skip those rows.
+/* Several JOINs (FROM t0 JOIN t1 ON .. LEFT JOIN t2 ON ..; INNER, LEFT / RIGHT / FULL OUTER,
+ * LEFT SEMI / ANTI steps): tables[k] / ncols[k] / nrows[k] = table k in FROM / JOIN order.
+ * Each ON compares a column of its table with a column of an earlier one; single-table
+ * WHERE conjuncts are pushed down.  A NULL-extended table (LEFT-joined; every earlier one
+ * after a RIGHT step; both sides of FULL) is NULL on the rows without a match (a later ON
+ * reading it matches nothing there); its columns may only appear inside aggregates, which
+ * skip those rows, and in scan projections (NULL there, nut_result_validity).  A SEMI /
+ * ANTI step's table only filters (its columns are not output).
  * Plans with at most one JOIN are forwarded to nut_plan_execute / nut_plan_execute2. */
 nut_status nut_plan_executen(nut_ctx *ctx, const nut_plan *plan, const nut_column *const *tables, const int *ncols,
                              const uint64_t *nrows, int ntables, uint64_t group_hint, nut_result **out);

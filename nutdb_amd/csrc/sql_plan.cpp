@@ -351,6 +351,9 @@ struct HNode {
 // FULL OUTER JOIN (plans only): executed as a LEFT join plus the JOIN source's unmatched
 // rows (an ANTI join with the roles swapped); the kernels know types 0..3
 constexpr int PJ_FULL = 4;
+// RIGHT OUTER as a step of a chain (the JOIN source preserved, every earlier table
+// NULL-extended); a single RIGHT JOIN is a LEFT join with jright
+constexpr int PJ_RIGHT = 5;
 // GROUP BY keys of one plan (packed into the kernels' two key words)
 constexpr int kMaxGroupKeys = 8;
 
@@ -392,7 +395,7 @@ struct nut_plan {
   struct JoinStep {
     std::string table, alias;
     int key[2];
-    int type = NUT_JOIN_INNER;  // NUT_JOIN_INNER or NUT_JOIN_LEFT
+    int type = NUT_JOIN_INNER;  // NUT_JOIN_INNER / LEFT / SEMI / ANTI, PJ_RIGHT, PJ_FULL
   };
   std::vector<JoinStep> jn;
   bool jright = false;     // RIGHT OUTER / SEMI / ANTI: the JOIN source is the preserved side
@@ -1284,15 +1287,23 @@ bool lower_mode(const Statement &st, nut_plan &p, Lowering &L) {
     for (const JoinClause &jc : b.joins) {
       if (jc.src.k != SourceKind::Table) return L.fail("JOIN source must be a table");
       if (!jc.on) return L.fail("JOIN ... USING in a chain of joins is not executed (ON a = b)");
-      if (jc.t != JoinType::Inner && jc.t != JoinType::LeftOuter)
-        return L.fail("several JOINs: INNER and LEFT OUTER only");
+      int type;
+      switch (jc.t) {
+        case JoinType::Inner: type = NUT_JOIN_INNER; break;
+        case JoinType::LeftOuter: type = NUT_JOIN_LEFT; break;
+        case JoinType::RightOuter: type = PJ_RIGHT; break;
+        case JoinType::FullOuter: type = PJ_FULL; break;
+        case JoinType::LeftSemi: type = NUT_JOIN_SEMI; break;
+        case JoinType::LeftAnti: type = NUT_JOIN_ANTI; break;
+        default: return L.fail("several JOINs: INNER, LEFT / RIGHT / FULL OUTER, LEFT SEMI / ANTI steps only");
+      }
       std::vector<std::pair<int, int>> eqs;
       if (!on_equalities(p, jc.cond, eqs))
         return L.fail("JOIN ON must be equalities of two columns (ANDed)");
       if (eqs.size() > 1 && jc.t != JoinType::Inner)
         return L.fail("JOIN with several key columns: INNER only (outer / semi / anti joins take one ON equality)");
       nut_plan::JoinStep js;
-      js.type = jc.t == JoinType::Inner ? NUT_JOIN_INNER : NUT_JOIN_LEFT;
+      js.type = type;
       js.table = std::string(jc.src.table);
       if (jc.src.alias) js.alias = std::string(*jc.src.alias);
       js.key[0] = eqs[0].first;
@@ -1458,7 +1469,8 @@ bool lower_mode(const Statement &st, nut_plan &p, Lowering &L) {
     if (p.aggs.size() > NUT_MAX_AGGS) return L.fail("more than 8 aggregates (HAVING / ORDER BY included)");
     if (p.vals.size() > NUT_MAX_VALS) return L.fail("aggregates reference more than 4 value columns");
     bool outer = p.join == NUT_JOIN_LEFT || p.join == PJ_FULL;
-    for (const nut_plan::JoinStep &js : p.jn) outer = outer || js.type == NUT_JOIN_LEFT;
+    for (const nut_plan::JoinStep &js : p.jn)
+      outer = outer || js.type == NUT_JOIN_LEFT || js.type == PJ_RIGHT || js.type == PJ_FULL;
     if (!p.compiled && outer)  // NULL-extended rows need aggregate masks
       return L.fail("outer-join aggregates lower to expression mode");
     return true;
@@ -1778,7 +1790,10 @@ std::string describe(const nut_plan &p) {
         if (k) o += ',';
         o += "{\"table\":";
         json_str(o, p.jn[k].table);
-        o += p.jn[k].type == NUT_JOIN_LEFT ? ",\"type\":\"left\"" : ",\"type\":\"inner\"";
+        static const char *st[] = {"inner", "left", "semi", "anti", "full", "right"};
+        o += ",\"type\":\"";
+        o += st[p.jn[k].type];
+        o += '"';
         o += ",\"on\":[";
         json_str(o, p.cols[p.jn[k].key[0]]);
         o += ',';
@@ -3589,17 +3604,30 @@ nut_status exec_joinn(nut_ctx *c, const nut_plan &p, const nut_column *const *ta
       agg = agg || in_prog(a.val, ci) || in_prog(a.mask, ci);
     }
   };
-  // NULL-extended tables: the ones joined by LEFT (their accumulated row ids hold -1 on the
-  // NULL rows; an INNER step on such a table's key drops them, a LEFT step keeps them, its
-  // own table NULL there).  As for one LEFT join, their columns may only feed aggregates,
-  // which skip the NULL rows.
-  std::vector<char> nullable(nt, 0);
-  for (int k = 0; k + 1 < nt; ++k) nullable[k + 1] = p.jn[k].type == NUT_JOIN_LEFT;
+  // NULL-extended tables: the one a LEFT step joins, every earlier one after a RIGHT step,
+  // both sides of a FULL step (their accumulated row ids hold -1 on the NULL rows; a later
+  // step's ON key from such a table matches nothing there).  Their columns may only feed
+  // aggregates, which skip the NULL rows, and projections (NULL there).  A LEFT SEMI / ANTI
+  // step's table only filters: its columns are not output.
+  std::vector<char> nullable(nt, 0), absent(nt, 0);
+  for (int k = 0; k + 1 < nt; ++k) {
+    const int t = k + 1, type = p.jn[k].type;
+    if (type == NUT_JOIN_LEFT || type == PJ_FULL) nullable[t] = 1;
+    if (type == PJ_RIGHT || type == PJ_FULL)
+      for (int v = 0; v < t; ++v) nullable[v] = 1;
+    if (type == NUT_JOIN_SEMI || type == NUT_JOIN_ANTI) absent[t] = 1;
+    if (absent[side[kold[k]]])
+      return fail(NUT_ERR_PLAN, "JOIN " + std::to_string(t) + ": ON reads a SEMI / ANTI-joined table ('" +
+                                    tname[side[kold[k]]] + "'), whose columns are not output");
+  }
   bool proj_null = false;  // a scan projecting a NULL-extended table's column (NULL there)
   for (size_t i = 0; i < nc; ++i) {
     bool row, agg, proj;
     reads(p, (int)i, row, agg, proj);
     const bool isnull = std::find(p.isnull_cols.begin(), p.isnull_cols.end(), (int)i) != p.isnull_cols.end();
+    if ((row || agg || proj) && absent[side[i]])
+      return fail(NUT_ERR_PLAN, "SEMI / ANTI JOIN: the columns of '" + tname[side[i]] + "' are not output ('" +
+                                    p.cols[i] + "')");
     if ((row || isnull) && nullable[side[i]])
       return fail(NUT_ERR_PLAN, "outer JOIN: the NULL-extended table's column '" + p.cols[i] +
                                     "' may only appear inside aggregates and projections" +
@@ -3645,6 +3673,11 @@ nut_status exec_joinn(nut_ctx *c, const nut_plan &p, const nut_column *const *ta
     if (out.alloc(c, std::max<uint64_t>(n, 1) * 8) != hipSuccess) return fail(NUT_ERR_OOM, "hipMalloc (join)");
     return n ? nut_gather_u64(c, (const uint64_t *)col, idx, n, 0, (uint64_t *)out.p) : NUT_OK;
   };
+  // accumulated row ids through positions (a -1 position, RIGHT / FULL: row id -1)
+  auto gather_rows = [&](const int64_t *ids_, const int64_t *idx, uint64_t n, DevBuf &out) -> nut_status {
+    if (out.alloc(c, std::max<uint64_t>(n, 1) * 8) != hipSuccess) return fail(NUT_ERR_OOM, "hipMalloc (join)");
+    return n ? nut_gather_u64(c, (const uint64_t *)ids_, idx, n, ~0ull, (uint64_t *)out.p) : NUT_OK;
+  };
   // positions i < n with (rowids[i] cmp 0), ascending (a one-column WHERE program)
   auto select_pos = [&](const int64_t *rowids, uint64_t n, int cmp, DevBuf &out, uint64_t *cnt) -> nut_status {
     nut_plan q;
@@ -3673,18 +3706,21 @@ nut_status exec_joinn(nut_ctx *c, const nut_plan &p, const nut_column *const *ta
   accp[0] = (const int64_t *)ids[0].p;
   uint64_t ncur = rows[0];
   nut_status st = NUT_OK;
+  std::vector<char> cur_null(nt, 0);  // table v's accumulated row ids may hold -1 (so far)
+  const int any = p.kind == NUT_PLAN_GROUPBY ? NUT_JOIN_ANY_ORDER : 0;
   for (int k = 0; k + 1 < nt && !st; ++k) {
-    const int t = k + 1, u = side[kold[k]];
-    const bool left = p.jn[k].type == NUT_JOIN_LEFT;
+    const int t = k + 1, u = side[kold[k]], type = p.jn[k].type;
+    // accumulated positions without a match stay (their table-t row -1)
+    const bool keep = type == NUT_JOIN_LEFT || type == PJ_FULL || type == NUT_JOIN_ANTI;
     DevBuf pk, bk, vpos, vrow, npos;
     const int64_t *pkd = (const int64_t *)src[kold[k]]->data, *bkd = (const int64_t *)src[knew[k]]->data;
-    const int64_t *prow = nullptr;  // probe row of each probe key (nullptr: its position)
+    const int64_t *prow = nullptr;  // position of each accumulated key (nullptr: its index)
     uint64_t np = ncur, nnull = 0;
-    if (nullable[u]) {
-      // a NULL ON key matches nothing: probe only the positions whose table-u row exists;
-      // LEFT appends the others as (position, -1)
+    if (cur_null[u]) {
+      // a NULL ON key matches nothing: only the positions whose table-u row exists take
+      // part; LEFT / FULL / ANTI append the others as (position, -1)
       if ((st = select_pos(accp[u], ncur, NUT_P_GE, vpos, &np))) break;
-      if (left && (st = select_pos(accp[u], ncur, NUT_P_LT, npos, &nnull))) break;
+      if (keep && (st = select_pos(accp[u], ncur, NUT_P_LT, npos, &nnull))) break;
       if ((st = gather_to(accp[u], (const int64_t *)vpos.p, np, vrow))) break;
       if ((st = gather_to(pkd, (const int64_t *)vrow.p, np, pk))) break;
       pkd = (const int64_t *)pk.p;
@@ -3697,16 +3733,22 @@ nut_status exec_joinn(nut_ctx *c, const nut_plan &p, const nut_column *const *ta
       if ((st = gather_to(bkd, (const int64_t *)ids[t].p, rows[t], bk))) break;
       bkd = (const int64_t *)bk.p;
     }
-    // pairs (accumulated position, table-t row): the pushed-down ids ride along as rows
+    // pairs (accumulated position, table-t row), -1 = none; the pushed-down ids ride along
+    // as rows.  RIGHT probes with table t (its rows all stay) against the accumulated keys.
+    const bool right = type == PJ_RIGHT;
     DevBuf pairs;
-    uint64_t cap = std::max<uint64_t>(np, 1), m = 0, half = 0;
+    uint64_t cap = std::max<uint64_t>(right ? rows[t] : np, 1), m = 0, half = 0;
+    const uint64_t extra = nnull + (type == PJ_FULL ? rows[t] : 0);  // appended below
     for (;;) {
-      half = cap + nnull;
+      half = cap + extra;
       if (pairs.alloc(c, half * 16) != hipSuccess) return fail(NUT_ERR_OOM, "hipMalloc (join index)");
-      st = join_i64_into_rows(c, bkd, (const int64_t *)ids[t].p, rows[t], pkd, prow, np,
-                              (left ? NUT_JOIN_LEFT : NUT_JOIN_INNER) |
-                                  (p.kind == NUT_PLAN_GROUPBY ? NUT_JOIN_ANY_ORDER : 0),
-                              (int64_t *)pairs.p, (int64_t *)pairs.p + half, cap, &m);
+      int64_t *o0 = (int64_t *)pairs.p, *o1 = o0 + half;
+      if (right)  // probe = table t: (t row, position)
+        st = join_i64_into_rows(c, pkd, prow, np, bkd, (const int64_t *)ids[t].p, rows[t], NUT_JOIN_LEFT | any, o1, o0,
+                                cap, &m);
+      else
+        st = join_i64_into_rows(c, bkd, (const int64_t *)ids[t].p, rows[t], pkd, prow, np,
+                                (type == PJ_FULL ? NUT_JOIN_LEFT : type) | any, o0, o1, cap, &m);
       if (st != NUT_ERR_CAPACITY || m <= cap) break;
       pairs.reset();
       cap = m;
@@ -3718,10 +3760,21 @@ nut_status exec_joinn(nut_ctx *c, const nut_plan &p, const nut_column *const *ta
       NUT_HIP(hipMemsetAsync(bi + m, 0xFF, nnull * 8, c->stream));  // -1: no table-t row
       m += nnull;
     }
+    if (type == PJ_FULL && rows[t]) {
+      // table t's rows without a match: ANTI with the roles swapped, appended as (-1, row)
+      uint64_t na = 0;
+      st = join_i64_into_rows(c, pkd, prow, np, bkd, (const int64_t *)ids[t].p, rows[t], NUT_JOIN_ANTI | any,
+                              bi + m, pi + m, rows[t], &na);
+      if (st) break;
+      NUT_HIP(hipMemsetAsync(pi + m, 0xFF, na * 8, c->stream));  // -1: no accumulated row
+      m += na;
+    }
+    const bool semi = type == NUT_JOIN_SEMI || type == NUT_JOIN_ANTI;  // table t contributes no rows
     std::vector<DevBuf> next(nt);
     for (int v = 0; v <= t && !st; ++v) {
+      if (v == t && semi) continue;
       if (v < t && accp[v]) {
-        st = gather_to(accp[v], pi, m, next[v]);
+        st = gather_rows(accp[v], pi, m, next[v]);
       } else {
         if (next[v].alloc(c, std::max<uint64_t>(m, 1) * 8) != hipSuccess) return fail(NUT_ERR_OOM, "hipMalloc");
         if (m) NUT_HIP(hipMemcpyAsync(next[v].p, v == t ? bi : pi, m * 8, hipMemcpyDeviceToDevice, c->stream));
@@ -3730,11 +3783,15 @@ nut_status exec_joinn(nut_ctx *c, const nut_plan &p, const nut_column *const *ta
     if (st) break;
     NUT_HIP(hipStreamSynchronize(c->stream));
     for (int v = 0; v <= t; ++v) {
+      if (v == t && semi) continue;
       std::swap(acc[v].p, next[v].p);
       std::swap(acc[v].s, next[v].s);
       accp[v] = (const int64_t *)acc[v].p;
     }
     ncur = m;
+    if (type == NUT_JOIN_LEFT || type == PJ_FULL) cur_null[t] = 1;
+    if (type == PJ_RIGHT || type == PJ_FULL)
+      for (int v = 0; v < t; ++v) cur_null[v] = 1;
   }
   if (st) return st;
   std::vector<DevBuf> bufs(nc);
@@ -3765,8 +3822,8 @@ nut_status exec_joinn(nut_ctx *c, const nut_plan &p, const nut_column *const *ta
   std::vector<DevBuf> mbuf(nt);
   p2.cols.reserve(nc + nt);  // jc keeps c_str() pointers into p2.cols
   std::vector<int> mflag(nt, -1);
-  for (int v = 1; v < nt && (p2.kind == NUT_PLAN_GROUPBY || proj_null); ++v) {
-    if (!nullable[v]) continue;
+  for (int v = 0; v < nt && (p2.kind == NUT_PLAN_GROUPBY || proj_null); ++v) {
+    if (!nullable[v]) continue;  // (table 0 too, after a RIGHT / FULL step)
     std::vector<PlanAgg *> reading;
     for (PlanAgg &a : p2.aggs) {
       bool rd = false;

@@ -287,3 +287,48 @@ def test_fixture10_join_chain(ex):
     assert rows_of([filled(got[c]) for c in cols]) == want
     for c, src in (("History Job ID", "jh.job_id"), ("region", "r.region_id"), ("hist_location", "dd.location_id")):
         assert int(np.ma.getmaskarray(got[c]).sum()) == int(m[src].isna().sum()) > 0, c
+
+
+def test_chain_step_types(ex):
+    """RIGHT / FULL OUTER and LEFT SEMI / ANTI steps inside join chains (nut_plan_executen):
+    RIGHT keeps every row of its table and NULL-extends every earlier one, FULL both; SEMI /
+    ANTI filter the accumulated rows by a match (a NULL key has none).  pandas merges."""
+    rng = np.random.default_rng(55)
+    na, nb, nc = 3000, 2500, 800
+    A = {"a_k": rng.integers(0, 2000, na).astype(np.int64), "a_v": rng.integers(-100, 100, na).astype(np.int64)}
+    B = {"b_k": rng.permutation(2500).astype(np.int64), "b_x": rng.integers(0, 1200, nb).astype(np.int64)}
+    C = {"c_k": rng.permutation(1000)[:nc].astype(np.int64), "c_v": rng.integers(0, 10**6, nc).astype(np.int64)}
+    dA, dB, dC = pd.DataFrame(A), pd.DataFrame(B), pd.DataFrame(C)
+    ab = dA.merge(dB, left_on="a_k", right_on="b_k")
+    tabs = [on_dev(ex, B), on_dev(ex, C)]
+    cols = ("a_k", "a_v", "b_x", "c_k", "c_v")
+    nn = lambda s: np.where(s.isna(), NULL, s.fillna(0)).astype(np.int64)
+    for kw, how in (("right join", "right"), ("full outer join", "outer")):
+        m = ab.merge(dC, left_on="b_x", right_on="c_k", how=how)
+        got = ex.sql(f"select a_k, a_v, b_x, c_k, c_v from a join b on a_k = b_k {kw} c on b_x = c_k",
+                     on_dev(ex, A), right=tabs)
+        assert rows_of([filled(got[c]) for c in cols]) == rows_of([nn(m[c]) for c in cols]), how
+        got = ex.sql(f"select count(*) as n, count(a_v) as ca, sum(a_v) as sa, count(c_v) as cc, sum(c_v) as sc "
+                     f"from a join b on a_k = b_k {kw} c on b_x = c_k", on_dev(ex, A), right=tabs)
+        assert [got[k][0] for k in ("n", "ca", "sa", "cc", "sc")] == [
+            len(m), int(m.a_v.notna().sum()), int(m.a_v.sum()), int(m.c_v.notna().sum()), int(m.c_v.sum())], how
+    for kw, keep in (("left semi join", True), ("left anti join", False)):
+        m = ab[ab.b_x.isin(dC.c_k) == keep]
+        got = ex.sql(f"select a_k, a_v, b_x from a join b on a_k = b_k {kw} c on b_x = c_k", on_dev(ex, A), right=tabs)
+        assert rows_of([got[c] for c in ("a_k", "a_v", "b_x")]) == rows_of([m[c].to_numpy() for c in ("a_k", "a_v", "b_x")])
+    # after LEFT, a NULL-extended ON key: ANTI keeps those rows, SEMI drops them
+    ab_l = dA.merge(dB, left_on="a_k", right_on="b_k", how="left")
+    for kw, keep in (("left semi join", True), ("left anti join", False)):
+        m = ab_l[ab_l.b_x.isin(dC.c_k) == keep]
+        got = ex.sql(f"select a_k, a_v, count(*) as n from a left join b on a_k = b_k {kw} c on b_x = c_k "
+                     "group by a_k, a_v", on_dev(ex, A), right=tabs)
+        g = m.groupby(["a_k", "a_v"]).size()
+        assert rows_of([got["a_k"], got["a_v"], got["n"]]) == sorted((k[0], k[1], int(v)) for k, v in g.items()), kw
+    # RIGHT then LEFT through a key of the NULL-extended table
+    m = dA.merge(dB, left_on="a_k", right_on="b_k", how="right").merge(dC, left_on="a_v", right_on="c_k", how="left")
+    got = ex.sql("select b_k, a_v, c_v from a right join b on a_k = b_k left join c on a_v = c_k", on_dev(ex, A),
+                 right=tabs)
+    assert rows_of([filled(got[c]) for c in ("b_k", "a_v", "c_v")]) == rows_of([nn(m[c]) for c in ("b_k", "a_v", "c_v")])
+    from nutdb_amd import NutError
+    with pytest.raises(NutError, match="are not output"):
+        ex.sql("select c_v from a join b on a_k = b_k left semi join c on b_x = c_k", on_dev(ex, A), right=tabs)

@@ -84,7 +84,7 @@ def test_sql_no_join_has_no_join_key():
     ("select count(*) from a left join b on x = y and u = v", "INNER only"),
     ("select count(*) from a left semi join b using (x, y)", "INNER only"),
     ("select count(*) from a join b using (x) join c using (x)", "USING in a chain"),
-    ("select count(*) from a join b on x = y full join c on y = z", "INNER and LEFT OUTER only"),
+    ("select count(*) from a join b on x = y right anti join c on y = z", "steps only"),
     ("select count(*) from a join (select x from b) on x = y", "must be a table"),
     # FULL OUTER ... USING (u): an unqualified u would be COALESCE(a.u, b.u)
     ("select count(u), sum(u) from a full outer join b using (u)", "FULL OUTER JOIN ... USING"),
@@ -141,8 +141,12 @@ def test_sql_join_chain_lowering():
     # aggregates over a chain with a LEFT step take expression mode (NULL-row masks)
     assert Plan("select x, sum(z) from a join b on x = y left join c on y = z group by x").describe()["mode"] == "compiled"
     from nutdb_amd import NutError
-    with pytest.raises(NutError, match="INNER and LEFT OUTER only"):
-        Plan("select count(*) from a join b on x = y right join c on y = z")
+    # RIGHT / FULL OUTER and LEFT SEMI / ANTI steps too; not RIGHT SEMI / ANTI or ASOF
+    d = Plan("select count(*) from a join b on x = y right join c on y = z full join d on z = w "
+             "left semi join e on w = v left anti join f on w = u").describe()
+    assert [j["type"] for j in d["joins"]] == ["inner", "right", "full", "semi", "anti"]
+    with pytest.raises(NutError, match="steps only"):
+        Plan("select count(*) from a join b on x = y right semi join c on y = z")
     with pytest.raises(NutError, match="several key columns: INNER only"):
         Plan("select count(*) from a join b on x = y left join c on y = z and x = w")
 
