@@ -913,12 +913,16 @@ bool lower_nullable(nut_plan &p, const Expr &e, PProg &val, PProg &mask, bool &n
 }
 
 int add_agg(nut_plan &p, const PlanAgg &a) {
+  // count(x) and count(*) differ only once an outer join masks x's table
+  bool outer = p.join == NUT_JOIN_LEFT || p.join == PJ_FULL;
+  for (const nut_plan::JoinStep &js : p.jn)
+    outer = outer || js.type == NUT_JOIN_LEFT || js.type == PJ_RIGHT || js.type == PJ_FULL;
   for (size_t i = 0; i < p.aggs.size(); ++i) {
     const PlanAgg &b = p.aggs[i];
     if (p.compiled) {
       if (b.op == a.op && b.distinct == a.distinct && same_prog(b.mask, a.mask) &&
           (a.op == NUT_AGG_COUNT || same_prog(b.val, a.val)) && (!a.distinct || same_prog(b.val, a.val)) &&
-          b.refs == a.refs)  // count(x) and count(*) differ once outer joins mask x's table
+          (b.refs == a.refs || (a.op == NUT_AGG_COUNT && !a.distinct && !outer)))
         return (int)i;
       continue;
     }

@@ -396,3 +396,49 @@ def test_join_string_columns_of_two_tables_rejected(ex):
             t1.sql(sql, right=t2)
     got = t1.sql("select count(*) as c from t1 join t2 using (k) where t2.s = 'c'", right=t2)
     assert got["c"].tolist() == [int((s2 == "c").sum())]
+
+
+def test_fixture1_tpch_q1_with_joins_flattened(ex):
+    """The reference fixture tests/sql/1.sql (TPC-H Q1 with the Q2-style join predicates
+    flattened into one table's WHERE: p_partkey = ps_partkey, p_type LIKE '%BRASS',
+    r_name = 'EUROPE', ...) over one denormalised typed table.  Its ORDER BY's first key
+    s_acctbal is neither grouped nor aggregated — an error in SQL — and is dropped; the rest
+    runs verbatim: 10 SELECT items, three AVGs sharing count(*) (6 aggregates)."""
+    from helpers import F64_SUM_RTOL, rel_err
+    sql = (GOLDEN / "1.sql").read_text().replace("s_acctbal desc,", "")
+    rng = np.random.default_rng(101)
+    n = 400_009
+    types = np.array(["SMALL BRASS", "LARGE BRASS", "PLATED STEEL", "BRASS TIN"], dtype=object)
+    regions = np.array(["EUROPE", "ASIA", "AMERICA"], dtype=object)
+    pk = rng.integers(0, 50, n)
+    sk = rng.integers(0, 50, n)
+    nk = rng.integers(0, 25, n)
+    c = dict(l_returnflag=rng.integers(0, 3, n), l_linestatus=rng.integers(0, 2, n),
+             l_quantity=rng.integers(1, 51, n).astype(np.float64), l_extendedprice=rng.integers(90000, 10494900, n) / 100,
+             l_discount=rng.integers(0, 11, n) / 100, l_tax=rng.integers(0, 9, n) / 100,
+             l_shipdate=rng.integers(8036, 10562, n), p_partkey=pk,
+             ps_partkey=np.where(rng.random(n) < 0.7, pk, pk + 1), s_suppkey=sk,
+             ps_suppkey=np.where(rng.random(n) < 0.8, sk, sk + 3), p_size=rng.integers(10, 20, n),
+             p_type=types[rng.integers(0, 4, n)], s_nationkey=nk,
+             n_nationkey=np.where(rng.random(n) < 0.9, nk, nk + 1), r_name=regions[rng.integers(0, 3, n)])
+    t = Table(ex, """CREATE TABLE lineitem (l_returnflag Int64, l_linestatus Int64, l_quantity Float64,
+        l_extendedprice Float64, l_discount Float64, l_tax Float64, l_shipdate Date, p_partkey Int64,
+        ps_partkey Int64, s_suppkey Int64, ps_suppkey Int64, p_size Int64, p_type String, s_nationkey Int64,
+        n_nationkey Int64, r_name String)""")
+    t.append(**c)
+    got = t.sql(sql, group_hint=6)
+    m = ((c["l_shipdate"] <= 10561 - 10) & (c["p_partkey"] == c["ps_partkey"]) & (c["s_suppkey"] == c["ps_suppkey"])
+         & (c["p_size"] == 15) & np.array([s.endswith("BRASS") for s in c["p_type"]])
+         & (c["s_nationkey"] == c["n_nationkey"]) & (c["l_shipdate"] > 9204) & (c["r_name"] == "EUROPE"))
+    keys = sorted({(a, b) for a, b in zip(c["l_returnflag"][m], c["l_linestatus"][m])})
+    assert list(zip(got["l_returnflag"], got["l_linestatus"])) == keys and len(keys) == 6
+    price, disc, tax, qty = c["l_extendedprice"], c["l_discount"], c["l_tax"], c["l_quantity"]
+    for i, (a, b) in enumerate(keys):
+        s = m & (c["l_returnflag"] == a) & (c["l_linestatus"] == b)
+        want = {"sum_qty": qty[s].sum(), "sum_base_price": price[s].sum(),
+                "sum_disc_price": (price[s] * (1 - disc[s])).sum(),
+                "sum_charge": (price[s] * (1 - disc[s]) * (1 + tax[s])).sum(),
+                "avg_qty": qty[s].mean(), "avg_price": price[s].mean(), "avg_disc": disc[s].mean()}
+        for k, w in want.items():
+            assert rel_err(np.array([got[k][i]]), np.array([w])) <= F64_SUM_RTOL, (k, a, b)
+        assert got["count_order"][i] == int(s.sum())
