@@ -55,6 +55,7 @@ def parse():
     p.add_argument("--groups", type=int, default=1000, help="groupby: distinct keys")
     p.add_argument("--selectivity", type=float, default=0.5, help="filter: fraction selected")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-copy-floor", action="store_true", help="skip the in-run device-copy floor probe")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline work")
     p.add_argument("--dist", action="store_true",
                    help="run N=1 through nut_dist_* too (one RCCL rank), as the N>1 runs do")
@@ -176,6 +177,7 @@ class Filter:
         self.out_n = torch.zeros(1, dtype=torch.int64, device=ex.device)
         self.rows = rows
         self.cols_bytes = 8 + 8 * sel
+        self.write_bytes = 8 * sel  # per row, of cols_bytes (the copy floor's write share)
 
     def run(self):
         self.ex.filter_i64_async(self.col, "<", self.k, self.out, self.out_n)
@@ -209,6 +211,7 @@ class ScanExpr:
         self.where = [("col", 0), ("col", 1), ("lt",)]
         self.rows = rows
         self.cols_bytes = 16 + 8 * 0.5
+        self.write_bytes = 8 * 0.5
 
     def run(self):  # results stay in HBM (as nut_plan_execute's scan results do)
         ids = self.ex.select_rows([self.a, self.b], self.where)
@@ -247,6 +250,7 @@ class Sort:
     # roofline numerator: SURVEY.md §8(d)'s HBM lower bound, one read + one write of every
     # key (16 B/key); the bytes the passes actually stream are reported beside it
     cols_bytes = 16
+    write_bytes = 8  # copy floor: one read and one write of every key
 
     @property
     def pass_bytes(self):
@@ -320,6 +324,7 @@ class Join:
     algorithmic bytes: they show up in the PMC traffic."""
     name = "join_i64_hash"
     kernel_kind = 3
+    write_bytes = None  # random-read bound (§4.4): a streaming copy floor does not apply
 
     def __init__(self, ex, rows, row0, world=1, rank=0):
         self.ex = ex
@@ -408,6 +413,7 @@ class Q12Join:
             lambda k, seed, n, a, b: ex.gen_column(k, seed, n, a=a, b=b), rows)
         self.plan = Plan(Q12J_SQL)
         self.cols_bytes = 32 + 8 * (2 / 7) / 6
+        self.write_bytes = self.cols_bytes - 32
 
     def run(self):
         return self.plan.execute_join(self.ex, self.orders, self.lineitem, group_hint=8)
@@ -690,6 +696,18 @@ def main():
                                f"{m.get('commit', 'unknown')} (separate rocprofv3 --pmc passes of the same command)")
         except Exception:
             traffic = None
+    # copy floor: the in-build streaming probe moving the same read / write
+    # bytes as the timed kernels, on this board, right after the timed loop
+    copy_floor = None
+    wb = getattr(w, "write_bytes", 0)
+    if rank == 0 and not args.no_copy_floor and wb is not None and launches:
+        rb = int((w.cols_bytes - wb) * rows)
+        probe_ms = ex.stream_probe(rb, int(wb * rows), reps=5)
+        copy_floor = {"kernel": "nut_stream_probe (16-B non-temporal loads / stores, same read:write ratio)",
+                      "read_bytes": rb, "write_bytes": int(wb * rows), "ms": probe_ms,
+                      "achieved": bytes_per_step / (probe_ms * 1e-3) / 1e9,
+                      "frac_of_peak": bytes_per_step / (probe_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                      "kernel_frac_of_copy": probe_ms / avg_kernel_ms}
     parity = None
     cpu = None
     if rank == 0 and world == 1 and nd is None and not args.no_cpu_baseline:
@@ -749,7 +767,8 @@ def main():
                          "achieved_wall": bytes_per_step / (ms_step * 1e-3) / 1e9,
                          "frac_wall": bytes_per_step / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
                          "traffic": traffic,
-                         "traffic_source": traffic_src},
+                         "traffic_source": traffic_src,
+                         "copy_floor": copy_floor},
         }
         if cpu is not None:
             line["cpu_baseline"] = cpu

@@ -139,6 +139,15 @@ typedef enum {
 nut_status nut_gen_column(nut_ctx *ctx, int kind, uint64_t seed, int64_t a, int64_t b,
                           double c, uint64_t row0, uint64_t n, void *out);
 
+/* Copy-floor probe ("the fraction of a measured in-build device-copy
+ * kernel's bandwidth"): streams read_bytes from src with 16-B non-temporal loads and writes
+ * write_bytes (<= read_bytes) of them to dst with non-temporal stores, interleaved at the
+ * same read:write ratio as a scan that keeps that fraction of its input.  Both sizes are
+ * multiples of 16 and the buffers 16-B aligned.  Runs `reps` launches on the context's
+ * stream and returns the fastest one's device time (hipEvents) in *best_ms. */
+nut_status nut_stream_probe(nut_ctx *ctx, const void *src, uint64_t read_bytes, void *dst,
+                            uint64_t write_bytes, int reps, double *best_ms);
+
 /* ------------------------------------------------------------------------
  * Filter scan + selection-vector compaction (BASELINE config 2)
  *   SELECT col FROM t WHERE col <cmp> k

@@ -147,6 +147,7 @@ SIGNATURES = {
     "nut_eval_rows": (_I32, [_P, C.POINTER(NutAggSpec), _P, _U64, _P, _P]),
     "nut_eval_jit_compile": (_I32, [C.POINTER(NutAggSpec)]),
     "nut_gen_column": (_I32, [_P, _I32, _U64, _I64, _I64, C.c_double, _U64, _U64, _P]),
+    "nut_stream_probe": (_I32, [_P, _P, _U64, _P, _U64, _I32, C.POINTER(C.c_double)]),
     "nut_filter_i64": (_I32, [_P, _P, _U64, _I32, _I64, _P, C.POINTER(_U64)]),
     "nut_filter_i64_async": (_I32, [_P, _P, _U64, _I32, _I64, _P, _P]),
     "nut_groupby": (_I32, [_P, C.POINTER(NutAggSpec), _U64, C.POINTER(_P)]),

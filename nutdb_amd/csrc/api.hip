@@ -110,6 +110,41 @@ __global__ void gen_column_kernel(int kind, uint64_t seed, int64_t a, int64_t b,
   }
 }
 
+// ------------------------------------------------------------ copy-floor probe
+// 16-B chunk i of the read stream is stored when its lane (i mod 64) is below q64: every
+// wave-instruction of loads is one contiguous KiB and its stores one contiguous run of
+// q64 x 16 B, so reads and writes interleave at the q64 / 64 ratio through the whole pass.
+// Four loads in flight per lane; what is not stored folds into a word that is written only
+// on an impossible value (keeps the loads live).
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(256) void stream_probe_kernel(const u32x4 *__restrict__ src, uint64_t nchunks,
+                                                           u32x4 *__restrict__ dst, uint32_t q64,
+                                                           u32x4 *__restrict__ sink) {
+  constexpr int U = 4;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  uint32_t acc = 0;
+  for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; base < nchunks; base += stride * U) {
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t i = base + u * stride;
+      if (i < nchunks) v[u] = __builtin_nontemporal_load(src + i);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t i = base + u * stride;
+      if (i >= nchunks) break;
+      const uint32_t lane = (uint32_t)(i & 63);
+      if (lane < q64)
+        __builtin_nontemporal_store(v[u], dst + (i >> 6) * q64 + lane);
+      else
+        acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+    }
+  }
+  if (acc == 0x9E3779B9u) sink[blockIdx.x] = u32x4{acc, 0u, 0u, 0u};
+}
+
 // ------------------------------------------------------------ large D2H
 constexpr size_t kStageBytes = 32u << 20;  // per pinned chunk
 constexpr int kCopyThreads = 8;
@@ -345,6 +380,37 @@ nut_status nut_ctx_info(nut_ctx *c, int *num_cus, char *name, size_t name_len) {
   if (!c) return fail(NUT_ERR_INVALID_ARG, "nut_ctx_info: ctx is NULL");
   if (num_cus) *num_cus = c->num_cus;
   if (name && name_len) snprintf(name, name_len, "%s", c->name);
+  return NUT_OK;
+}
+
+nut_status nut_stream_probe(nut_ctx *c, const void *src, uint64_t read_bytes, void *dst, uint64_t write_bytes,
+                            int reps, double *best_ms) {
+  if (!c || !best_ms || reps < 1 || !src || read_bytes == 0 || (write_bytes && !dst) || write_bytes > read_bytes ||
+      (read_bytes | write_bytes | (uintptr_t)src | (uintptr_t)dst) % 16)
+    return fail(NUT_ERR_INVALID_ARG, "nut_stream_probe: bad argument (16-B multiples, write_bytes <= read_bytes)");
+  DeviceGuard g(c->device);
+  const uint64_t nchunks = read_bytes / 16;
+  const uint32_t q64 = (uint32_t)((unsigned __int128)write_bytes * 64 / read_bytes);
+  const unsigned blocks = (unsigned)c->num_cus * 8;  // 2048 lanes x 4 loads in flight per CU
+  if (nut_status st = c->misc.reserve((size_t)blocks * 16)) return st;
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  for (auto &e : ev) NUT_HIP(hipEventCreate(&e));
+  float best = 0.f;
+  hipError_t e = hipSuccess;
+  for (int r = 0; r < reps && e == hipSuccess; ++r) {
+    e = hipEventRecord(ev[0], c->stream);
+    hipLaunchKernelGGL(stream_probe_kernel, dim3(blocks), dim3(256), 0, c->stream, (const u32x4 *)src, nchunks,
+                       (u32x4 *)dst, q64, (u32x4 *)c->misc.ptr);
+    if (e == hipSuccess) e = hipGetLastError();
+    if (e == hipSuccess) e = hipEventRecord(ev[1], c->stream);
+    if (e == hipSuccess) e = hipEventSynchronize(ev[1]);
+    float ms = 0.f;
+    if (e == hipSuccess) e = hipEventElapsedTime(&ms, ev[0], ev[1]);
+    if (e == hipSuccess && (r == 0 || ms < best)) best = ms;
+  }
+  for (auto &x : ev) (void)hipEventDestroy(x);
+  if (e != hipSuccess) return hip_fail(e, "nut_stream_probe");
+  *best_ms = best;
   return NUT_OK;
 }
 

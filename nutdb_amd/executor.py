@@ -367,6 +367,20 @@ class Executor:
     def sync(self):
         check(lib.nut_ctx_sync(self.ctx), "nut_ctx_sync")
 
+    def stream_probe(self, read_bytes: int, write_bytes: int, reps: int = 5) -> float:
+        """Device ms of the fastest of `reps` copy-floor launches (nut_stream_probe) that read
+        read_bytes and write write_bytes of them; the buffers are allocated here and freed."""
+        read_bytes -= read_bytes % 16
+        write_bytes -= write_bytes % 16
+        src = torch.empty(read_bytes, dtype=torch.uint8, device=self.device)
+        dst = torch.empty(write_bytes + 1024 if write_bytes else 16, dtype=torch.uint8, device=self.device)
+        self._bind_stream()
+        ms = C.c_double()
+        check(lib.nut_stream_probe(self.ctx, C.c_void_p(src.data_ptr()), read_bytes, C.c_void_p(dst.data_ptr()),
+                                   write_bytes, reps, C.byref(ms)), "nut_stream_probe")
+        del src, dst
+        return ms.value
+
     # ---------------------------------------------------------------- data
     def gen_column(self, kind: int, seed: int, n: int, row0: int = 0, a: int = 0, b: int = 0,
                    c: float = 1.0, out: torch.Tensor | None = None) -> torch.Tensor:
