@@ -703,7 +703,8 @@ def main():
     if rank == 0 and not args.no_copy_floor and wb is not None and launches:
         rb = int((w.cols_bytes - wb) * rows)
         probe_ms = ex.stream_probe(rb, int(wb * rows), reps=5)
-        copy_floor = {"kernel": "nut_stream_probe (16-B non-temporal loads / stores, same read:write ratio)",
+        copy_floor = {"kernel": "nut_stream_probe (16-B non-temporal loads / stores, same read:write ratio, "
+                                "best of 2 / 4 / 8 workgroups per CU x 5 launches)",
                       "read_bytes": rb, "write_bytes": int(wb * rows), "ms": probe_ms,
                       "achieved": bytes_per_step / (probe_ms * 1e-3) / 1e9,
                       "frac_of_peak": bytes_per_step / (probe_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,

@@ -116,7 +116,10 @@ typedef enum {
   NUT_OPT_GB_L1_BITS = 10,     /* digit bits of a capped second partition level, 6..8 (6) */
   NUT_OPT_TOPK = 11,           /* 1 (default): plans with ORDER BY ... LIMIT sort only nut_topk_positions' rows */
   NUT_OPT_GB_L0_BITS = 12,     /* digit bits of a capped first partition level, 6..8; 0 (default): 7 for one level up to 150 K groups, else 8 */
-  NUT_OPT_COUNT = 13
+  NUT_OPT_STREAM_BLOCKS = 13,  /* nut_stream_probe: workgroups per CU, 0 (default) = 8 */
+  NUT_OPT_PRIV_BD = 14,        /* compiled Q1 kernel: threads per workgroup 128 / 192 / 256; 0 (default) = 192 */
+  NUT_OPT_PRIV_BLOCKS = 15,    /* compiled Q1 kernel: at most this many workgroups per CU; 0 (default) = 2 */
+  NUT_OPT_COUNT = 16
 } nut_option;
 nut_status nut_ctx_set_option(nut_ctx *ctx, int option, int64_t value);
 nut_status nut_ctx_get_option(nut_ctx *ctx, int option, int64_t *value);
@@ -143,8 +146,9 @@ nut_status nut_gen_column(nut_ctx *ctx, int kind, uint64_t seed, int64_t a, int6
  * kernel's bandwidth"): streams read_bytes from src with 16-B non-temporal loads and writes
  * write_bytes (<= read_bytes) of them to dst with non-temporal stores, interleaved at the
  * same read:write ratio as a scan that keeps that fraction of its input.  Both sizes are
- * multiples of 16 and the buffers 16-B aligned.  Runs `reps` launches on the context's
- * stream and returns the fastest one's device time (hipEvents) in *best_ms. */
+ * multiples of 16, the buffers 16-B aligned, dst holds write_bytes + 1 KiB.  Runs `reps`
+ * launches at 2, 4 and 8 workgroups of 256 threads per CU (or NUT_OPT_STREAM_BLOCKS) on
+ * the context's stream and returns the fastest one's device time (hipEvents) in *best_ms. */
 nut_status nut_stream_probe(nut_ctx *ctx, const void *src, uint64_t read_bytes, void *dst,
                             uint64_t write_bytes, int reps, double *best_ms);
 

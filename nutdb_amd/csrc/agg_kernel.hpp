@@ -11,7 +11,9 @@
 //     is half-published and nothing is wasted; single-key shared tables claim by CAS;
 //   * PRIV: the first P groups of a block fold into per-thread private accumulators
 //     laid out [group][agg][thread] (plain read-modify-write, conflict-free), reduced
-//     once per block;
+//     once per block; keys in a small range (one key < 256, or two keys < 16 each:
+//     dictionary codes such as Q1's flags) find their private id in a direct map (one LDS
+//     word per key value, filled from the hash table on first sight) without hashing;
 //   * rows of keys the block table does not admit fold into the global table (g_row);
 //     at block end the LDS table is merged into the global (HBM) table.
 #pragma once
@@ -23,14 +25,16 @@ namespace nut {
 // ------------------------------------------------------------------ LDS table
 // Layout (dynamic LDS, this order, 16-B aligned):
 //   slot[cap+1] u64 | agg[na][cap+1] u64 | k12[cap+1] {i64,i64} (NK=2) | did[cap+1] u32
-//   (PRIV) | dslot[kPrivMax] u32 (PRIV) | ctl[4] u32 | priv[P][na][BD] u64 (PRIV)
+//   (PRIV) | dslot[kPrivMax] u32 + dmap[kDirect] u32 (PRIV) | ctl[4] u32 | priv[P][na][BD] u64 (PRIV)
 enum { CTL_CLAIMED = 0, CTL_SPECIAL = 1, CTL_LOCK = 2, CTL_NDENSE = 3 };
 constexpr uint32_t kNoDense = 0xFFFFFFFFu;
+constexpr uint32_t kDirect = 256;  // direct-map entries (PRIV): key < 256, or 16 x 16 key pairs
 
 struct LTable {
   uint64_t *slot, *agg;
   i64x2 *k12;
   uint32_t *did, *dslot, *ctl;
+  uint32_t *dmap;  // PRIV: private id of a small key (tuple), kNoDense until first seen
   uint64_t *priv;
   uint32_t *spill;  // spill mode: the block's append cursor (LDS)
   uint32_t *shist;  //   and its histogram of the key hash's top byte (LDS, 256)
@@ -47,7 +51,7 @@ __host__ __device__ inline size_t lds_layout(uint32_t cap, int nk, int na, bool 
   *o_did = o;
   if (privm) o += stride * 4;
   *o_dslot = o;
-  if (privm) o += kPrivMax * 4;
+  if (privm) o += (kPrivMax + kDirect) * 4;
   *o_ctl = o;
   o += 16;
   o = (o + 15) & ~size_t(15);
@@ -72,6 +76,13 @@ constexpr uint32_t kBucket = 4;
 __device__ __forceinline__ uint32_t lhome(uint64_t w, int log2cap) {
   const uint32_t f = (uint32_t)w ^ (uint32_t)(w >> 32);
   return ((f * 0x9E3779B1u) >> (32 - log2cap)) & ~(kBucket - 1);
+}
+
+// direct-map index of a key (tuple), or kDirect when it is out of the map's range
+template <int NK>
+__device__ __forceinline__ uint32_t direct_idx(uint64_t k1, uint64_t k2) {
+  if (NK == 1) return k1 < kDirect ? (uint32_t)k1 : kDirect;
+  return (k1 | k2) < 16 ? (uint32_t)(k1 << 4 | k2) : kDirect;
 }
 
 template <int NK>
@@ -333,55 +344,78 @@ __device__ __forceinline__ void consume_rows(const AggArgs &p, const LTable &lt,
       }
     }
   }
-  // GROUP BY: home-bucket lookup of all four rows (four ds_read_b128 in flight), then
-  // the probe loop only for rows that missed
+  // GROUP BY.  PRIV: keys in the direct map's range take their private id from it (one
+  // LDS word, no hashing); the rest — and every row of a shared table — do a home-bucket
+  // lookup of all four rows (four ds_read_b128 in flight), then the probe loop only for
+  // rows that missed.  A wave none of whose rows needs the table skips it.
   const uint32_t cap = p.lds_cap;
   int32_t sl[R];
-  uint64_t w[R];
+  bool need[R];
+  uint32_t di[R], dm[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
-    w[r] = lkey<NK>(kk1[r], kk2[r]);
     sl[r] = -2;
+    need[r] = ok[r];
+    di[r] = kDirect;
+    dm[r] = kNoDense;
+  }
+  if (PRIV && cap) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      di[r] = direct_idx<NK>(kk1[r], kk2[r]);
+      dm[r] = di[r] < kDirect ? lt.dmap[di[r]] : kNoDense;
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if (ok[r] && dm[r] != kNoDense) sl[r] = 0, need[r] = false;  // any slot >= 0: the fold goes private
+    }
   }
   if (cap) {
-    u64x2 b0[R], b1[R];
-    uint32_t hb[R];
+    bool any = false;
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      hb[r] = lhome(w[r], p.lds_log2);
-      b0[r] = *reinterpret_cast<const u64x2 *>(&lt.slot[hb[r]]);
-      b1[r] = *reinterpret_cast<const u64x2 *>(&lt.slot[hb[r] + 2]);
-    }
-    if (LOCKED) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    for (int r = 0; r < R; ++r) any = any || need[r];
+    if (!PRIV || __any(any)) {
+      uint64_t w[R];
+      u64x2 b0[R], b1[R];
+      uint32_t hb[R];
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      if (ok[r]) {
-        // home bucket: the first slot holding w; no match and an empty slot in the
-        // bucket ends the chain (no deletes: a key never sits behind an empty slot)
-        int32_t s = -1;
-        const uint64_t c[4] = {b0[r].x, b0[r].y, b1[r].x, b1[r].y};
+      for (int r = 0; r < R; ++r) {
+        w[r] = lkey<NK>(kk1[r], kk2[r]);
+        hb[r] = lhome(w[r], p.lds_log2);
+        b0[r] = *reinterpret_cast<const u64x2 *>(&lt.slot[hb[r]]);
+        b1[r] = *reinterpret_cast<const u64x2 *>(&lt.slot[hb[r] + 2]);
+      }
+      if (LOCKED) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 #pragma unroll
-        for (int j = 3; j >= 0; --j) s = c[j] == w[r] ? (int32_t)hb[r] + j : s;
-        bool end = (c[0] == kEmpty) | (c[1] == kEmpty) | (c[2] == kEmpty) | (c[3] == kEmpty);
-        if (NK == 2 && s >= 0 && !keys_match<NK>(lt, (uint32_t)s, kk1[r], kk2[r])) s = -1, end = false;
-        if (NK == 1 && w[r] == kEmpty) s = -1, end = true;
-        if (s < 0 && !end) {
-          // continue the probe chain past the bucket (inline: a few slots at most)
-          uint32_t e = (hb[r] + kBucket) & (cap - 1);
-          for (uint32_t probe = kBucket; probe < cap; ++probe) {
-            const uint64_t cur =
-                LOCKED ? __hip_atomic_load(&lt.slot[e], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) : lt.slot[e];
-            if (cur == w[r] && keys_match<NK>(lt, e, kk1[r], kk2[r])) {
-              s = (int32_t)e;
-              break;
+      for (int r = 0; r < R; ++r) {
+        if (need[r]) {
+          // home bucket: the first slot holding w; no match and an empty slot in the
+          // bucket ends the chain (no deletes: a key never sits behind an empty slot)
+          int32_t s = -1;
+          const uint64_t c[4] = {b0[r].x, b0[r].y, b1[r].x, b1[r].y};
+#pragma unroll
+          for (int j = 3; j >= 0; --j) s = c[j] == w[r] ? (int32_t)hb[r] + j : s;
+          bool end = (c[0] == kEmpty) | (c[1] == kEmpty) | (c[2] == kEmpty) | (c[3] == kEmpty);
+          if (NK == 2 && s >= 0 && !keys_match<NK>(lt, (uint32_t)s, kk1[r], kk2[r])) s = -1, end = false;
+          if (NK == 1 && w[r] == kEmpty) s = -1, end = true;
+          if (s < 0 && !end) {
+            // continue the probe chain past the bucket (inline: a few slots at most)
+            uint32_t e = (hb[r] + kBucket) & (cap - 1);
+            for (uint32_t probe = kBucket; probe < cap; ++probe) {
+              const uint64_t cur =
+                  LOCKED ? __hip_atomic_load(&lt.slot[e], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) : lt.slot[e];
+              if (cur == w[r] && keys_match<NK>(lt, e, kk1[r], kk2[r])) {
+                s = (int32_t)e;
+                break;
+              }
+              if (cur == kEmpty) break;
+              e = (e + 1) & (cap - 1);
             }
-            if (cur == kEmpty) break;
-            e = (e + 1) & (cap - 1);
           }
+          // not present: insert (or find a concurrent insert) out of line
+          if (s < 0) s = l_find_slow<NK, LOCKED>(lt, cap, p.lds_limit, p.lds_log2, p.priv, w[r], kk1[r], kk2[r]);
+          sl[r] = s;
         }
-        // not present: insert (or find a concurrent insert) out of line
-        if (s < 0) s = l_find_slow<NK, LOCKED>(lt, cap, p.lds_limit, p.lds_log2, p.priv, w[r], kk1[r], kk2[r]);
-        sl[r] = s;
       }
     }
   } else {
@@ -390,7 +424,17 @@ __device__ __forceinline__ void consume_rows(const AggArgs &p, const LTable &lt,
   }
   uint32_t dd[R];
 #pragma unroll
-  for (int r = 0; r < R; ++r) dd[r] = (PRIV && sl[r] >= 0 && sl[r] < (int32_t)cap) ? lt.did[sl[r]] : kNoDense;
+  for (int r = 0; r < R; ++r) {
+    if (!PRIV) {
+      dd[r] = kNoDense;
+    } else if (!need[r]) {
+      dd[r] = dm[r];  // a direct-map hit (or a row WHERE dropped: sl = -2, never folded)
+    } else {
+      dd[r] = (sl[r] >= 0 && sl[r] < (int32_t)cap) ? lt.did[sl[r]] : kNoDense;
+      // the private id of a slot never changes once published: cache it for the key
+      if (dd[r] != kNoDense && di[r] < kDirect) lt.dmap[di[r]] = dd[r];
+    }
+  }
 
   // aggregate inputs
   uint64_t av[S::MA][R];
@@ -482,6 +526,7 @@ __global__ __launch_bounds__(BD) void agg_kernel(AggArgs p) {
     lt.k12 = (i64x2 *)(b + o_k12);
     lt.did = PRIV ? (uint32_t *)(b + o_did) : nullptr;
     lt.dslot = (uint32_t *)(b + o_dslot);
+    lt.dmap = PRIV ? lt.dslot + kPrivMax : nullptr;
     lt.ctl = (uint32_t *)(b + o_ctl);
     lt.priv = (uint64_t *)(b + o_priv);
   }
@@ -503,6 +548,8 @@ __global__ __launch_bounds__(BD) void agg_kernel(AggArgs p) {
       if (PRIV) lt.did[s] = kNoDense;
     }
     if (threadIdx.x < 4) lt.ctl[threadIdx.x] = 0;
+    if (PRIV)
+      for (uint32_t i = threadIdx.x; i < kDirect; i += BD) lt.dmap[i] = kNoDense;
     if (PRIV) {
 #pragma unroll
       for (int a = 0; a < S::MA; ++a)

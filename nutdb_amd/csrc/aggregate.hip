@@ -244,10 +244,12 @@ constexpr int kBdPriv = 256;
 
 // Compiled shapes assume 16-B aligned columns (vector loads); anything else runs the
 // generic kernel, which decides the load width at run time.
-KernelFn pick_kernel(int nk, bool priv, int shape, bool vec) {
+KernelFn pick_kernel(int nk, bool priv, int shape, bool vec, int bd) {
   if (!vec) shape = SHAPE_GENERIC;
   if (priv) {
-    if (shape == SHAPE_Q1) return agg_kernel<2, true, kBdPriv, ShapeQ1, 1>;
+    if (shape == SHAPE_Q1)
+      return bd == 128 ? agg_kernel<2, true, 128, ShapeQ1, 1>
+           : bd == 192 ? agg_kernel<2, true, 192, ShapeQ1, 1> : agg_kernel<2, true, kBdPriv, ShapeQ1, 1>;
     if (shape == SHAPE_SUM) return agg_kernel<1, true, kBdPriv, ShapeSum, 1>;
     if (shape == SHAPE_ALL4) return agg_kernel<1, true, kBdPriv, ShapeAll4, 1>;
     return nk == 1 ? agg_kernel<1, true, kBdPriv, Generic, 0> : agg_kernel<2, true, kBdPriv, Generic, 0>;
@@ -349,7 +351,12 @@ nut_status launch_agg(nut_groups *g, const nut_agg_spec *s, uint64_t group_hint,
     if (lds_bytes(lcap, g->nk, na, true, P, kBdPriv) > lds_max / 2) P = 0;
   }
   const bool priv = P > 0;
-  const int bd = priv ? kBdPriv : kBdShared;
+  const int shape = detect_shape(s, kinds, a);
+  const bool q1_tuned = priv && shape == SHAPE_Q1 && !s->prog_mode && a.vec;
+  // the compiled Q1 kernel runs 6 waves per CU (2 x 192 threads): 8 waves issue too many
+  // concurrent six-column streams (7.85 vs 7.27 ms at 1e9 rows, same box), 4 leave its
+  // fold's latency exposed (8.7 ms) — NUT_OPT_PRIV_BD / _BLOCKS override for sweeps
+  const int bd = !priv ? kBdShared : !q1_tuned ? kBdPriv : c->opt[NUT_OPT_PRIV_BD] ? (int)c->opt[NUT_OPT_PRIV_BD] : 192;
   a.lds_cap = lcap;
   a.lds_limit = lcap - lcap / 4;
   a.lds_log2 = lcap ? ilog2(lcap) : 0;
@@ -357,6 +364,7 @@ nut_status launch_agg(nut_groups *g, const nut_agg_spec *s, uint64_t group_hint,
   a.gt = g->dev_gt;
   const size_t lb = lds_bytes(lcap, g->nk, na, priv, P, bd);
   int blocks_per_cu = lb ? (int)std::max<size_t>(1, std::min<size_t>(bd == 512 ? 4 : 8, lds_max / lb)) : 4;
+  if (q1_tuned) blocks_per_cu = std::min<int>(blocks_per_cu, c->opt[NUT_OPT_PRIV_BLOCKS] ? (int)c->opt[NUT_OPT_PRIV_BLOCKS] : 2);
   uint64_t pairs = (s->n + 1) / 2;
   uint64_t blocks = std::min<uint64_t>((uint64_t)c->num_cus * blocks_per_cu, (pairs + bd - 1) / bd);
   if (blocks == 0) blocks = 1;
@@ -390,8 +398,7 @@ nut_status launch_agg(nut_groups *g, const nut_agg_spec *s, uint64_t group_hint,
     if (e != hipSuccess) return hip_fail(e, "hipModuleLaunchKernel (expression kernel)");
     return NUT_OK;
   }
-  const int shape = detect_shape(s, kinds, a);
-  KernelFn fn = pick_kernel(g->nk, priv, shape, a.vec != 0);
+  KernelFn fn = pick_kernel(g->nk, priv, shape, a.vec != 0, bd);
   NUT_HIP(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_max));
   c->timer.begin(c->stream, NUT_KERNEL_AGGREGATE);
   hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(bd), lb, c->stream, a);

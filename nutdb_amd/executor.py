@@ -347,7 +347,8 @@ class Executor:
     OPTIONS = {"gb_partition": 0, "gb_levels": 1, "gb_optimistic": 2, "gb_direct": 3, "gb_chunks": 4,
                "join_region": 5, "join_probe_cfg": 6, "join_any_cfg": 7, "gb_seg_slots": 8,
                "gb_dense": 9, "gb_l1_bits": 10,
-               "topk": 11, "gb_l0_bits": 12}
+               "topk": 11, "gb_l0_bits": 12, "stream_blocks": 13,
+               "priv_bd": 14, "priv_blocks": 15}
 
     def groupby_stats(self) -> dict:
         """The algorithm the last group-by on this context took (nut_ctx_groupby_stats)."""

@@ -198,6 +198,25 @@ def test_groupby_two_keys_preds_exprs(ex, orc):
     check_vs_oracle(g, ok, ow, ["sum_f64", "sum_f64", "i", "i", "i", "sum_f64"])
 
 
+@pytest.mark.parametrize("nk,lo,hi,hint", [(1, 0, 6, 6), (1, -3, 300, 8), (1, 250, 262, 8), (2, 0, 3, 6),
+                                           (2, -2, 20, 8), (2, 0, 16, 4), (2, 14, 18, 8)])
+def test_groupby_private_direct_map(ex, orc, nk, lo, hi, hint):
+    """Private-accumulator kernels (group_hint <= 8): keys inside the direct map's range
+    (one key < 256, two keys < 16 each) take their private id from it, keys outside it,
+    negative keys and groups beyond the hint go through the hash table — all mixed in
+    one launch; bit-exact integer aggregates, f64 sums to 1e-12."""
+    from nutdb_amd import Agg, AggQuery
+    rng = np.random.default_rng(nk * 1000 + lo + hi)
+    n = 1_500_007
+    keys = [rng.integers(lo, hi, n).astype(np.int64) for _ in range(nk)]
+    v = rng.random(n)
+    q = AggQuery(keys=[dev(k, ex) for k in keys], values=[dev(v, ex)],
+                 aggs=[Agg("sum", "col", (0,)), Agg("count"), Agg("min", "col", (0,)), Agg("max", "col", (0,))])
+    g = ex.groupby(q, group_hint=hint)
+    ok, ow = orc.groupby(keys, AGGS4, values=[v])
+    check_vs_oracle(g, ok, ow, ["sum_f64", "i", "i", "i"])
+
+
 def test_groupby_empty_and_tiny(ex, orc):
     for n in (0, 1, 2, 3):
         key = np.arange(n, dtype=np.int64) % 2
