@@ -365,6 +365,7 @@ nut_status launch_agg(nut_groups *g, const nut_agg_spec *s, uint64_t group_hint,
   const size_t lb = lds_bytes(lcap, g->nk, na, priv, P, bd);
   int blocks_per_cu = lb ? (int)std::max<size_t>(1, std::min<size_t>(bd == 512 ? 4 : 8, lds_max / lb)) : 4;
   if (q1_tuned) blocks_per_cu = std::min<int>(blocks_per_cu, c->opt[NUT_OPT_PRIV_BLOCKS] ? (int)c->opt[NUT_OPT_PRIV_BLOCKS] : 2);
+  if (!priv && c->opt[NUT_OPT_AGG_BLOCKS]) blocks_per_cu = std::min<int>(blocks_per_cu, (int)c->opt[NUT_OPT_AGG_BLOCKS]);
   uint64_t pairs = (s->n + 1) / 2;
   uint64_t blocks = std::min<uint64_t>((uint64_t)c->num_cus * blocks_per_cu, (pairs + bd - 1) / bd);
   if (blocks == 0) blocks = 1;
