@@ -1246,7 +1246,8 @@ nut_status nut_select_rows(nut_ctx *c, const nut_agg_spec *s, int64_t *out_rows,
   void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &sa, HIP_LAUNCH_PARAM_BUFFER_SIZE, &asz, HIP_LAUNCH_PARAM_END};
   c->timer.begin(c->stream, NUT_KERNEL_FILTER);
   // persistent workgroups (tiles by ticket): enough for full occupancy, never more than tiles
-  const unsigned grid = (unsigned)std::min<uint64_t>(ntiles, (uint64_t)c->num_cus * 8);
+  const uint64_t per_cu = c->opt[NUT_OPT_SEL_BLOCKS] ? (uint64_t)c->opt[NUT_OPT_SEL_BLOCKS] : 8;
+  const unsigned grid = (unsigned)std::min<uint64_t>(ntiles, (uint64_t)c->num_cus * per_cu);
   hipError_t e = hipModuleLaunchKernel(fn, grid, 1, 1, SEL_THREADS, 1, 1, 0, c->stream, nullptr, cfg);
   c->timer.end(c->stream);
   if (e != hipSuccess) return hip_fail(e, "hipModuleLaunchKernel (select kernel)");

@@ -25,6 +25,7 @@
 #include <algorithm>
 #include <deque>
 #include <functional>
+#include <memory>
 
 #include "common.hpp"
 #include "sql_ast.hpp"
@@ -96,6 +97,7 @@ struct CVal {
   Decimal dec;       // float value
   bool is_str = false;  // string constant (binds to a dictionary code at execution)
   std::string s;
+  int param = -1;       // >= 0: the value of scalar subquery nut_plan.subs[param], known at execution
 };
 
 i128 sat_from_u128(u128 m, bool neg) {
@@ -259,7 +261,10 @@ bool const_eval(const Expr &e, CVal &out, Lowering &L) {
   return false;
 }
 
-std::string cval_str(const CVal &c) { return c.is_str ? "'" + c.s + "'" : c.is_int ? i128_str(c.v) : c.dec.str(); }
+std::string cval_str(const CVal &c) {
+  if (c.param >= 0) return "$subquery" + std::to_string(c.param);
+  return c.is_str ? "'" + c.s + "'" : c.is_int ? i128_str(c.v) : c.dec.str();
+}
 
 // floor of an exact decimal, saturated; frac = true if it had a fractional part
 i128 dec_floor(const Decimal &d, bool &frac) {
@@ -343,6 +348,7 @@ struct HNode {
   bool is_int = false, b = true;
   int64_t i = 0;
   double f = 0;
+  int param = -1;    // H_CONST: >= 0, the value of scalar subquery nut_plan.subs[param]
   std::vector<HNode> kids;
 };
 
@@ -404,6 +410,10 @@ struct nut_plan {
   std::deque<std::string> qnames;  // storage of qualified column names (column_ref)
   // JOIN ... USING (u): the plain name u, and the qualified column it stands for
   std::vector<std::pair<std::string, std::string>> using_cols;
+  // uncorrelated scalar subqueries `(SELECT agg(..) FROM t WHERE ..)` compared in WHERE /
+  // HAVING or used as a value: global-aggregate plans over the same table, executed first;
+  // their one value replaces every constant whose param names them (resolve_subqueries)
+  std::vector<std::shared_ptr<nut_plan>> subs;
 };
 
 struct nut_result {
@@ -676,6 +686,7 @@ bool is_agg_name(sv n) {
 // A conditional: conds[i] -> vals[i], else vals.back().  CASE WHEN / IF / multiIf and
 // CASE x WHEN v (cond x = v).  Returns false if e is not a conditional.
 bool lower_prog(nut_plan &p, const Expr &e, PProg &o, Lowering &L);
+bool scalar_subquery(nut_plan &p, const Expr &e, CVal &c, Lowering &L);
 bool conditional(nut_plan &p, const Expr &e, std::vector<PProg> &conds, std::vector<const Expr *> &vals,
                  Lowering &L, bool &ok) {
   ok = true;
@@ -738,6 +749,13 @@ bool lower_prog(nut_plan &p, const Expr &e, PProg &o, Lowering &L) {
     return true;
   }
   if (!L.err.empty()) return false;
+  if (e.k == EK::Subquery) {
+    PNode n;
+    n.op = NUT_P_F64;  // the type is the subquery's, set when its value is put in
+    if (!scalar_subquery(p, e, n.c, L)) return L.fail(L.err.empty() ? "subquery is not a value here" : L.err);
+    o.push_back(n);
+    return true;
+  }
   switch (e.k) {
     case EK::Identifier: {
       if (e.id.wildcard) return L.fail("'*' is not a value");
@@ -945,14 +963,15 @@ bool lower_pred_term(nut_plan &p, const Expr &e, Lowering &L) {
   if (e.k == EK::BinaryOp && cmp_of(e.bop()) >= 0) {
     int op = cmp_of(e.bop());
     const Expr &l = e.kids[0], &r = e.kids[1];
-    if (column_ref(p, l, name) && const_eval(r, c, L)) {
+    if (column_ref(p, l, name) && (const_eval(r, c, L) || scalar_subquery(p, r, c, L))) {
       p.preds.push_back({col_index(p, name), op, c});
       return true;
     }
-    if (column_ref(p, r, name) && const_eval(l, c, L)) {
+    if (column_ref(p, r, name) && (const_eval(l, c, L) || scalar_subquery(p, l, c, L))) {
       p.preds.push_back({col_index(p, name), mirror(op), c});
       return true;
     }
+    if (!L.err.empty()) return false;
   }
   if (e.k == EK::BinaryOp && (e.bop() == BinOp::In || e.bop() == BinOp::NotIn) && column_ref(p, e.kids[0], name)) {
     // col [NOT] IN (c1, c2, ...): a tuple of constants, or one constant
@@ -1195,6 +1214,12 @@ bool lower_having(nut_plan &p, const Expr &e, HNode &h, Lowering &L) {
   auto operand = [&](const Expr &x, HNode &o) {
     CVal c;
     Lowering quiet;
+    if (x.k == EK::Subquery) {
+      if (!scalar_subquery(p, x, c, L)) return false;
+      o.k = H_CONST;
+      o.param = c.param;
+      return true;
+    }
     if (const_eval(x, c, quiet)) {
       if (c.is_str) return L.fail("string constants in HAVING are not executed");
       o.k = H_CONST;
@@ -1277,10 +1302,9 @@ bool add_key(nut_plan &p, const Expr &e, Lowering &L) {
   return true;
 }
 
-bool lower_mode(const Statement &st, nut_plan &p, Lowering &L) {
-  if (st.k != StmtKind::Select) return L.fail("only SELECT statements execute");
-  if (st.query.is_union) return L.fail("UNION/INTERSECT/EXCEPT are not executed (one query body per plan)");
-  const QueryBody &b = *st.query.body;
+bool lower_mode(const Query &qry, nut_plan &p, Lowering &L) {
+  if (qry.is_union) return L.fail("UNION/INTERSECT/EXCEPT are not executed (one query body per plan)");
+  const QueryBody &b = *qry.body;
   if (b.with) return L.fail("WITH is not executed");
   if (b.distinct && b.group_by) return L.fail("DISTINCT with GROUP BY is not executed");
   if (!b.from || b.from->k != SourceKind::Table) return L.fail("FROM must name one table");
@@ -1586,23 +1610,46 @@ bool resolve_using(nut_plan &p, Lowering &L) {
   return true;
 }
 
-bool lower(const Statement &st, nut_plan &p, Lowering &L) {
+bool lower_query(const Query &q, nut_plan &p, Lowering &L) {
   Lowering L1;
-  if (lower_mode(st, p, L1)) return resolve_using(p, L);
-  bool agg = false;
-  if (st.k == StmtKind::Select && !st.query.is_union && st.query.body) {
-    const QueryBody &b = *st.query.body;
-    agg = b.group_by.has_value();
-    for (const QueryExpr &q : b.columns)
-      if (q.e.k == EK::FnCall && q.e.fn() == FnKind::Others) agg = true;
-  }
-  (void)agg;  // aggregate plans and scans both retry in expression mode
+  if (lower_mode(q, p, L1)) return resolve_using(p, L);
+  // aggregate plans and scans both retry in expression mode
   nut_plan p2;
   p2.compiled = true;
   Lowering L2;
-  if (!lower_mode(st, p2, L2)) return L.fail(L2.err);
+  if (!lower_mode(q, p2, L2)) return L.fail(L2.err);
   if (!resolve_using(p2, L)) return false;
   p = std::move(p2);
+  return true;
+}
+
+bool lower(const Statement &st, nut_plan &p, Lowering &L) {
+  if (st.k != StmtKind::Select) return L.fail("only SELECT statements execute");
+  return lower_query(st.query, p, L);
+}
+
+// An uncorrelated scalar subquery in a value position: planned on its own (a global
+// aggregate with one output over the same table, no JOIN), executed before the plan; `c`
+// becomes a placeholder naming it (resolve_subqueries puts the value in at execution).
+bool scalar_subquery(nut_plan &p, const Expr &e, CVal &c, Lowering &L) {
+  if (e.k != EK::Subquery || !e.q) return false;
+  auto sub = std::make_shared<nut_plan>();
+  Lowering Ls;
+  if (!lower_query(*e.q, *sub, Ls)) return L.fail("scalar subquery: " + Ls.err);
+  int visible = 0;
+  for (const PlanOut &o : sub->outs) visible += o.hidden ? 0 : 1;
+  if (sub->kind != NUT_PLAN_GROUPBY || !sub->keys.empty() || !sub->key_progs.empty() || visible != 1)
+    return L.fail("a scalar subquery executes as a global aggregate with one output (SELECT agg(..) FROM t ..)");
+  if (sub->join >= 0 || !sub->subs.empty() || sub->star)
+    return L.fail("a scalar subquery executes over one table, without JOIN or nested subqueries");
+  if (p.join >= 0) return L.fail("scalar subqueries execute in single-table plans (the query has a JOIN)");
+  if (!p.table.empty() && !sub->table.empty() && !ieq(p.table, sub->table))
+    return L.fail("scalar subquery over table '" + sub->table + "' (the query reads '" + p.table +
+                  "'): subqueries execute over the same table");
+  c = CVal{};
+  c.is_int = false;
+  c.param = (int)p.subs.size();
+  p.subs.push_back(std::move(sub));
   return true;
 }
 
@@ -1807,7 +1854,13 @@ std::string describe(const nut_plan &p) {
       o += ']';
     }
   }
-  o += ",\"offset\":" + std::to_string(p.offset) + "}";
+  o += ",\"offset\":" + std::to_string(p.offset);
+  if (!p.subs.empty()) {  // scalar subqueries, by placeholder index ($subqueryN)
+    o += ",\"subqueries\":[";
+    for (size_t i = 0; i < p.subs.size(); ++i) o += (i ? "," : "") + describe(*p.subs[i]);
+    o += "]";
+  }
+  o += "}";
   return o;
 }
 
@@ -3890,6 +3943,114 @@ nut_status stage_host(nut_ctx *c, const nut_column *cols, int n, uint64_t rows, 
 
 extern "C" {
 
+namespace {
+
+// exact decimal of a finite double (17 significant digits: strtod gives the double back)
+Decimal decimal_of(double d) {
+  Decimal x;
+  if (d == 0.0) return x;
+  char buf[64];
+  snprintf(buf, sizeof buf, "%.16e", d);  // [-]d.dddddddddddddddde[+-]XX
+  const char *q = buf;
+  if (*q == '-') x.neg = true, ++q;
+  std::string digs;
+  for (; *q && *q != 'e'; ++q)
+    if (*q != '.') digs += *q;
+  const int64_t ex = strtoll(q + 1, nullptr, 10);
+  size_t z = 0;
+  while (z < digs.size() && digs[z] == '0') ++z;
+  x.digits = digs.substr(z);
+  x.scale = 16 - ex;
+  return x;
+}
+
+// Scalar subqueries (nut_plan.subs): run each (run(sub) executes it over the caller's
+// binding), check it returned one value, and copy the plan with every placeholder constant
+// replaced by that value.  A global aggregate over no rows is one row of defaults
+// (ClickHouse: count / sum / min / max 0, avg NaN); a NaN (or no row) is treated as SQL
+// NULL: a WHERE term comparing with it is never true; anywhere else it is rejected.
+nut_status resolve_subqueries(const nut_plan &p, nut_plan &q,
+                              const std::function<nut_status(const nut_plan *, nut_result **)> &run) {
+  std::vector<CVal> vals(p.subs.size());
+  std::vector<bool> null(p.subs.size(), false);
+  for (size_t i = 0; i < p.subs.size(); ++i) {
+    nut_result *r = nullptr;
+    nut_status st = run(p.subs[i].get(), &r);
+    if (st) return st;
+    std::unique_ptr<nut_result, void (*)(nut_result *)> hold(r, nut_result_free);
+    if (r->nrows > 1)
+      return fail(NUT_ERR_PLAN, "scalar subquery returned " + std::to_string(r->nrows) + " rows (one expected)");
+    if (r->nrows == 0 || r->host.empty() || r->host[0].empty()) {
+      null[i] = true;
+      continue;
+    }
+    const uint64_t w = r->host[0][0];
+    if (r->types[0] == NUT_T_F64) {
+      double d;
+      memcpy(&d, &w, 8);
+      if (std::isnan(d)) {  // avg over no rows: comparisons with NaN are never true, as with NULL
+        null[i] = true;
+        continue;
+      }
+      if (!std::isfinite(d)) return fail(NUT_ERR_UNSUPPORTED, "scalar subquery returned an infinite value");
+      vals[i].is_int = false;
+      vals[i].dec = decimal_of(d);
+    } else {
+      vals[i].is_int = true;
+      vals[i].v = (int64_t)w;
+    }
+  }
+  q = p;
+  q.subs.clear();
+  bool bad_null = false;
+  auto put = [&](CVal &c) {
+    if (c.param < 0) return;
+    if (null[c.param]) bad_null = true;
+    c = vals[c.param];
+  };
+  for (PlanPred &pr : q.preds) {
+    if ((pr.c.param >= 0 && null[pr.c.param])) {
+      q.never = true;  // col <cmp> NULL: never true (the terms are ANDed)
+      pr.c = CVal{};
+      continue;
+    }
+    put(pr.c);
+    for (CVal &v : pr.set) put(v);
+  }
+  auto prog = [&](PProg &pp) {
+    for (PNode &n : pp)
+      if (n.c.param >= 0) {
+        put(n.c);
+        n.op = n.c.is_int ? NUT_P_I64 : NUT_P_F64;
+      }
+  };
+  prog(q.where);
+  for (PProg &pp : q.proj_val) prog(pp);
+  for (PProg &pp : q.proj_mask) prog(pp);
+  for (PProg &pp : q.key_progs) prog(pp);
+  for (PlanAgg &a : q.aggs) prog(a.val), prog(a.mask);
+  std::function<void(HNode &)> hv = [&](HNode &h) {
+    if (h.k == H_CONST && h.param >= 0) {
+      if (null[h.param]) bad_null = true;
+      const CVal &v = vals[h.param];
+      h.param = -1;
+      if (v.is_int && v.v <= INT64_MAX && v.v >= INT64_MIN) {
+        h.is_int = true;
+        h.i = (int64_t)v.v;
+      } else {
+        h.is_int = false;
+        h.f = v.is_int ? (double)v.v : v.dec.to_f64();
+      }
+    }
+    for (HNode &k : h.kids) hv(k);
+  };
+  hv(q.having);
+  if (bad_null) return fail(NUT_ERR_UNSUPPORTED, "a scalar subquery returned no row (NULL) where only a WHERE comparison can take it");
+  return NUT_OK;
+}
+
+}  // namespace
+
 nut_status nut_sql_parse(const char *sql, size_t len, nut_stmt **out) {
   if (!out || (!sql && len)) return fail(NUT_ERR_INVALID_ARG, "nut_sql_parse: NULL argument");
   *out = nullptr;
@@ -3987,6 +4148,13 @@ nut_status nut_plan_execute(nut_ctx *c, const nut_plan *p, const nut_column *col
   if (!c || !p || !out || (ncols && !cols) || ncols < 0) return fail(NUT_ERR_INVALID_ARG, "nut_plan_execute: NULL argument");
   *out = nullptr;
   if (p->join >= 0) return fail(NUT_ERR_INVALID_ARG, "nut_plan_execute: the plan has a JOIN (nut_plan_execute2)");
+  if (!p->subs.empty()) {  // scalar subqueries first, over the same columns
+    nut_plan q;
+    nut_status st = resolve_subqueries(*p, q, [&](const nut_plan *sp, nut_result **r) {
+      return nut_plan_execute(c, sp, cols, ncols, nrows, 1, r);
+    });
+    return st ? st : nut_plan_execute(c, &q, cols, ncols, nrows, group_hint, out);
+  }
   nut_plan sq;
   if (p->star) {
     std::vector<std::string> names;
@@ -4029,6 +4197,7 @@ nut_status nut_plan_execute2(nut_ctx *c, const nut_plan *p, const nut_column *le
   if (!c || !p || !out || (nleft && !left) || (nright && !right) || nleft < 0 || nright < 0)
     return fail(NUT_ERR_INVALID_ARG, "nut_plan_execute2: NULL argument");
   if (p->join < 0) return nut_plan_execute(c, p, left, nleft, lrows, group_hint, out);
+  if (!p->subs.empty()) return fail(NUT_ERR_UNSUPPORTED, "scalar subqueries execute in single-table plans");
   if (!p->jn.empty()) return fail(NUT_ERR_INVALID_ARG, "nut_plan_execute2: the plan joins several tables (nut_plan_executen)");
   *out = nullptr;
   DeviceGuard g(c->device);
@@ -4059,6 +4228,7 @@ nut_status nut_plan_executen(nut_ctx *c, const nut_plan *p, const nut_column *co
       return nut_plan_execute2(c, p, tables[0], ncols[0], nrows[0], tables[1], ncols[1], nrows[1], group_hint, out);
     return fail(NUT_ERR_INVALID_ARG, "nut_plan_executen: the plan joins fewer tables");
   }
+  if (!p->subs.empty()) return fail(NUT_ERR_UNSUPPORTED, "scalar subqueries execute in single-table plans");
   *out = nullptr;
   DeviceGuard g(c->device);
   std::deque<HostStage> hs(ntables);
@@ -4139,6 +4309,13 @@ nut_status nut_table_execute(nut_ctx *c, nut_table *t, const nut_plan *p, uint64
   if (t->device >= 0 && t->device != c->device)
     return fail(NUT_ERR_INVALID_ARG, "nut_table_execute: the table lives on another device");
   const uint64_t nrows = t->rows();
+  if (!p->subs.empty()) {  // scalar subqueries first, over the same table
+    nut_plan q;
+    nut_status st = resolve_subqueries(*p, q, [&](const nut_plan *sp, nut_result **r) {
+      return nut_table_execute(c, t, sp, 1, r);
+    });
+    return st ? st : nut_table_execute(c, t, &q, group_hint, out);
+  }
   nut_plan sq;
   if (p->star) {
     std::vector<std::string> names;
@@ -4177,6 +4354,7 @@ nut_status nut_table_execute2(nut_ctx *c, nut_table *left, nut_table *right, con
                               nut_result **out) {
   if (!c || !left || !right || !p || !out) return fail(NUT_ERR_INVALID_ARG, "nut_table_execute2: NULL argument");
   if (p->join < 0) return nut_table_execute(c, left, p, group_hint, out);
+  if (!p->subs.empty()) return fail(NUT_ERR_UNSUPPORTED, "scalar subqueries execute in single-table plans");
   *out = nullptr;
   std::vector<nut_column> cols[2];
   std::vector<const Dict *> dicts[2];
@@ -4216,6 +4394,7 @@ nut_status nut_table_executen(nut_ctx *c, nut_table *const *tables, int ntables,
     if (ntables == 2) return nut_table_execute2(c, tables[0], tables[1], p, group_hint, out);
     return fail(NUT_ERR_INVALID_ARG, "nut_table_executen: the plan joins fewer tables");
   }
+  if (!p->subs.empty()) return fail(NUT_ERR_UNSUPPORTED, "scalar subqueries execute in single-table plans");
   *out = nullptr;
   std::vector<std::vector<nut_column>> cols(ntables);
   std::vector<std::vector<const Dict *>> dicts(ntables);

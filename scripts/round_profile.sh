@@ -11,6 +11,6 @@ mkdir -p "$out"
 args=("$@" --no-cpu-baseline)
 set -o pipefail
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$out/trace" -o trace --output-format csv -- python3 bench.py "${args[@]}" > "$out/trace.log" 2>&1 || exit $?
-timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -d "$out/fetch" -o fetch --output-format csv -- python3 bench.py "${args[@]}" > "$out/fetch.log" 2>&1 || exit $?
-timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE -d "$out/write" -o write --output-format csv -- python3 bench.py "${args[@]}" > "$out/write.log" 2>&1 || exit $?
+timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -d "$out/fetch" -o fetch --output-format csv -- python3 bench.py "${args[@]}" --no-copy-floor > "$out/fetch.log" 2>&1 || exit $?
+timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE -d "$out/write" -o write --output-format csv -- python3 bench.py "${args[@]}" --no-copy-floor > "$out/write.log" 2>&1 || exit $?
 python3 scripts/pmc_traffic.py "$out" "${args[@]}"

@@ -240,3 +240,48 @@ def test_sql_host_resident_columns(ex):
     b = ex.sql(sql, devc, right=dim)
     m = w > 5000
     assert a["c"].tolist() == b["c"].tolist() == np.bincount(k[m], minlength=100).tolist()
+
+
+def test_sql_scalar_subqueries(ex):
+    """Uncorrelated scalar subqueries, executed first over the same columns (fixture 9's
+    `c_acctbal > (select avg(c_acctbal) ...)`, fixture 4's HAVING > (select sum(..) * k),
+    fixture 6's `= (select max(..))`), vs numpy on the same data.  Dyadic values: every
+    sum and the avg division are exact / identically rounded, so comparisons are exact."""
+    rng = np.random.default_rng(91)
+    n = 1_000_003
+    bal = (rng.integers(-2**20, 2**20, n) / 64.0).astype(np.float64)
+    key = rng.integers(0, 100, n).astype(np.int64)
+    qty = rng.integers(1, 50, n).astype(np.int64)
+    cols = {"c_custkey": dev(np.arange(n, dtype=np.int64), ex), "c_acctbal": dev(bal, ex), "k": dev(key, ex),
+            "qty": dev(qty, ex)}
+    # WHERE col > (avg over a filtered set): a float placeholder
+    pos = bal[bal > 0.0]
+    avg = pos.sum() / len(pos)
+    got = ex.sql("select c_custkey, c_acctbal from customer where c_acctbal > "
+                 "(select avg(c_acctbal) from customer where c_acctbal > 0.00) and k < 50", cols)
+    m = (bal > avg) & (key < 50)
+    assert np.array_equal(got["c_custkey"], np.nonzero(m)[0]) and np.array_equal(got["c_acctbal"], bal[m])
+    # = (select max(..)) over an int column, a count over the rows that equal it
+    got = ex.sql("select count(*) as c from customer where qty = (select max(qty) from customer)", cols)
+    assert int(got["c"][0]) == int((qty == qty.max()).sum())
+    # two subqueries, one inside an expression (expression mode)
+    got = ex.sql("select count(*) as c from customer where qty + 1 > (select max(qty) from customer) - 3 "
+                 "and k >= (select min(k) from customer where qty > 40)", cols)
+    kmin = key[qty > 40].min()
+    assert int(got["c"][0]) == int(((qty + 1 > qty.max() - 3) & (key >= kmin)).sum())
+    # HAVING sum(..) > (select sum(..) * 0.011 ...) over groups
+    got = ex.sql("select k, sum(qty) as s from customer where qty > 2 group by k "
+                 "having sum(qty) > (select sum(qty) * 0.011 from customer where qty > 2) order by k", cols,
+                 group_hint=100)
+    sel = qty > 2
+    sums = np.bincount(key[sel], weights=qty[sel], minlength=100).astype(np.int64)
+    bound = float(qty[sel].sum()) * 0.011
+    want_k = np.nonzero(sums > bound)[0]
+    assert np.array_equal(got["k"], want_k) and np.array_equal(got["s"], sums[want_k])
+    # a global aggregate over no rows is one row of defaults (max 0), avg NaN acts as NULL
+    got = ex.sql("select count(*) as c from customer where qty > (select max(qty) from customer where qty > 1000)",
+                 cols)
+    assert int(got["c"][0]) == n
+    got = ex.sql("select count(*) as c from customer where c_acctbal > "
+                 "(select avg(c_acctbal) from customer where qty > 1000)", cols)
+    assert int(got["c"][0]) == 0

@@ -478,6 +478,37 @@ def test_plan_tpch_q6_global_aggregate():
     assert d["outputs"] == [{"name": "revenue", "from": "agg", "index": 0}]
 
 
+def test_plan_scalar_subqueries():
+    """Uncorrelated scalar subqueries (fixtures 4, 6, 9): a child plan per subquery (a
+    global aggregate over the same table), a $subqueryN placeholder where its value goes."""
+    d = Plan("select x from t where x > (select avg(x) from t where x > 0.00)").describe()
+    assert d["kind"] == "filter" and d["where"] == [
+        {"col": "x", "op": ">", "value": "$subquery0", "value_kind": "decimal"}]
+    (sub,) = d["subqueries"]
+    assert sub["kind"] == "groupby" and sub["keys"] == [] and sub["where"][0]["value"] == "0.00"
+    d = Plan("select k, sum(v * w) as s from t where k > 2 group by k "
+             "having sum(v * w) > (select sum(v * w) * 0.0001000000 from t where k > 2) order by s desc").describe()
+    assert d["having"] is True and len(d["subqueries"]) == 1
+    assert len([o for o in d["subqueries"][0]["outputs"] if not o.get("hidden")]) == 1
+    d = Plan("select count(*) from t where a = (select max(a) from t) and b < (select min(b) from t)").describe()
+    assert [w["value"] for w in d["where"]] == ["$subquery0", "$subquery1"]
+    # a value inside an expression: expression mode, the placeholder in the program text
+    d = Plan("select count(*) from t where a + 1 > (select max(a) from t) - 5").describe()
+    assert d["mode"] == "compiled" and "$subquery0" in d["where_expr"]
+
+
+@pytest.mark.parametrize("sql,frag", [
+    ("select x from t where x > (select avg(x) from u)", "over the same table"),
+    ("select x from t where x > (select x from t)", "global aggregate with one output"),
+    ("select x from t where x > (select k, max(x) from t group by k)", "global aggregate with one output"),
+    ("select x from t where x in (select x from t)", "IN (subquery)"),
+])
+def test_plan_scalar_subquery_errors(sql, frag):
+    with pytest.raises(NutError) as e:
+        Plan(sql)
+    assert e.value.status == 7 and frag in str(e.value)
+
+
 @pytest.mark.parametrize("sql,frag", [
     ("insert into t values (1)", "only SELECT"),
     ("select a + 1 as c from t order by c", "ORDER BY a computed projection"),
