@@ -352,8 +352,10 @@ nut_status launch_agg(nut_groups *g, const nut_agg_spec *s, uint64_t group_hint,
   }
   const bool priv = P > 0;
   const int shape = detect_shape(s, kinds, a);
-  const bool q1_tuned = priv && shape == SHAPE_Q1 && !s->prog_mode && a.vec;
-  // the compiled Q1 kernel runs 6 waves per CU (2 x 192 threads): 8 waves issue too many
+  // private-accumulator kernels built for 128 / 192 / 256 threads: the compiled Q1 shape
+  // and every run-time-compiled (expression-mode) kernel
+  const bool q1_tuned = priv && ((shape == SHAPE_Q1 && !s->prog_mode && a.vec) || s->prog_mode);
+  // the Q1 kernel runs 6 waves per CU (2 x 192 threads): 8 waves issue too many
   // concurrent six-column streams (7.85 vs 7.27 ms at 1e9 rows, same box), 4 leave its
   // fold's latency exposed (8.7 ms) — NUT_OPT_PRIV_BD / _BLOCKS override for sweeps
   const int bd = !priv ? kBdShared : !q1_tuned ? kBdPriv : c->opt[NUT_OPT_PRIV_BD] ? (int)c->opt[NUT_OPT_PRIV_BD] : 192;
