@@ -580,7 +580,10 @@ void nut_plan_free(nut_plan *plan);
  * types matter (data may be NULL).  A no-op for plans on the precompiled kernels. */
 nut_status nut_plan_prepare(const nut_plan *plan, const nut_column *cols, int ncols);
 /* Execute on nrows rows of the bound columns (every column the plan names must be
- * bound).  group_hint as for nut_groupby.  Synchronous. */
+ * bound).  group_hint as for nut_groupby.  Synchronous.  A plan with uncorrelated scalar
+ * subqueries (`x > (SELECT avg(x) FROM t ...)`, describe: "subqueries") runs each of them
+ * first over the same columns (nut_plan_execute / nut_table_execute only; the multi-table
+ * entry points reject such plans with NUT_ERR_UNSUPPORTED). */
 nut_status nut_plan_execute(nut_ctx *ctx, const nut_plan *plan, const nut_column *cols, int ncols,
                             uint64_t nrows, uint64_t group_hint, nut_result **out);
 /* A plan with a JOIN: `left` = the FROM table (lrows rows), `right` = the JOIN source.
