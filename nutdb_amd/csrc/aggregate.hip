@@ -28,6 +28,10 @@ struct nut_groups {
   unsigned long long *dev_cursors = nullptr;  // [64] inside mem
   uint64_t *dev_segbase = nullptr;            // [2*64] inside mem
   bool dense = false;  // groups appended at slots 0.. (not at their hash): rehash before inserting
+  // the table's control words as last read (read_ctl) while no launch has written the table
+  // since: a result's size / to_host calls reuse them instead of one more round trip each
+  uint32_t ctl_cache[4] = {0, 0, 0, 0};
+  bool ctl_valid = false;
 };
 
 namespace {
@@ -137,6 +141,7 @@ int32_t kind_of(const nut_agg_spec *s, int a) {
 // of `cap` tuples (3/4 of it holds admitted keys, the rest absorbs lost claim races)
 // (re)allocate the global table for `cap` slots and initialise it on the stream
 nut_status alloc_table(nut_groups *g, uint64_t cap) {
+  g->ctl_valid = false;
   const uint64_t stride = cap + 1;
   // two-key arena: one entry per claimable slot plus slack for claim races lost by
   // concurrent inserters of the same key (each loser leaks at most one entry)
@@ -196,12 +201,18 @@ nut_status alloc_table(nut_groups *g, uint64_t cap) {
 }
 
 nut_status read_ctl(nut_groups *g, uint32_t *ctl4) {
+  if (g->ctl_valid) {
+    memcpy(ctl4, g->ctl_cache, 16);
+    return NUT_OK;
+  }
   nut_ctx *c = g->ctx;
   hipLaunchKernelGGL(gtable_sum_kernel, dim3(1), dim3(256), 0, c->stream, (const GTable *)g->dev_gt);
   NUT_HIP(hipGetLastError());
   NUT_HIP(hipMemcpyAsync(c->host_pinned, g->gt.ctl, 16, hipMemcpyDeviceToHost, c->stream));
   NUT_HIP(hipStreamSynchronize(c->stream));
   memcpy(ctl4, c->host_pinned, 16);
+  memcpy(g->ctl_cache, ctl4, 16);
+  g->ctl_valid = true;
   return NUT_OK;
 }
 
@@ -284,6 +295,7 @@ struct LaunchExtra {
 // per-row update kinds (COUNT partials are merged as integer sums).
 nut_status launch_agg(nut_groups *g, const nut_agg_spec *s, uint64_t group_hint, const int32_t *kinds,
                       LaunchExtra *ex = nullptr) {
+  g->ctl_valid = false;  // this launch writes the table
   nut_ctx *c = g->ctx;
   if (s->n == 0) return NUT_OK;
   AggArgs a;
@@ -445,6 +457,7 @@ nut_status ensure_room(nut_groups *g, uint64_t extra) {
   g->mem_bytes = fresh.mem_bytes;
   g->gt = fresh.gt;
   g->dev_gt = fresh.dev_gt;
+  g->ctl_valid = false;
   g->dev_cursors = fresh.dev_cursors;
   g->dev_segbase = fresh.dev_segbase;
   g->dense = false;
