@@ -54,6 +54,8 @@ def parse():
     p.add_argument("--rows", type=float, default=None, help="rows per GPU (default: config size)")
     p.add_argument("--groups", type=int, default=1000, help="groupby: distinct keys")
     p.add_argument("--selectivity", type=float, default=0.5, help="filter: fraction selected")
+    p.add_argument("--key-range", type=float, default=None, metavar="FRACTION",
+                   help="sort: keys uniform over this fraction of the int64 range (a sample-sort rank's share)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-copy-floor", action="store_true", help="skip the in-run device-copy floor probe")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline work")
@@ -238,10 +240,11 @@ class Sort:
     name = "sort_i64_radix"
     kernel_kind = 2
 
-    def __init__(self, ex, rows, row0, world=1):
-        from nutdb_amd.workloads import SORT_COL, gen
+    def __init__(self, ex, rows, row0, world=1, key_range=None):
+        from nutdb_amd.workloads import gen, sort_col
         self.ex = ex
-        self.col = gen(ex, SORT_COL, rows, row0=row0)
+        self.key_range = key_range
+        self.col = gen(ex, sort_col(key_range), rows, row0=row0)
         self.out = torch.empty_like(self.col) if world == 1 else None
         self.rows = rows
         self.world = world
@@ -272,7 +275,8 @@ class Sort:
         return _cmp_arrays(gpu.cpu().numpy(), cpu)
 
     def config(self):
-        return {"workload": self.name, "query": "SELECT k FROM t ORDER BY k (full-range i64)",
+        kr = "full-range i64" if self.key_range is None else f"i64 keys over {self.key_range:g} of the int64 range"
+        return {"workload": self.name, "query": f"SELECT k FROM t ORDER BY k ({kr})",
                 "algorithm": f"hybrid MSD radix: {self.levels} segmented scatter levels + on-chip local sorts"
                 + ("; sample sort across ranks: partition by P-1 splitters + RCCL all-to-all" if self.world > 1
                    else ""),
@@ -439,7 +443,7 @@ def cpu_baseline(args, workload: str, target_s: float):
     once (not timed); the scan is timed repeatedly up to ~target_s and the best run is
     reported."""
     from oracle import oracle as orc
-    from nutdb_amd.workloads import FILTER_COL, Q1_COLS, Q1_DATE_K, SORT_COL, filter_k, groupby_cols
+    from nutdb_amd.workloads import FILTER_COL, Q1_COLS, Q1_DATE_K, filter_k, groupby_cols, sort_col
     threads = orc.max_threads()
 
     def prepare(n):
@@ -451,7 +455,7 @@ def cpu_baseline(args, workload: str, target_s: float):
             key, val = [orc.gen(s, n) for s in groupby_cols(args.groups, dyadic=True)]
             return lambda: orc.groupby([key], [(0, 0, (0,))], values=[val], cap=max(args.groups, 1))
         if workload == "sort":
-            col = orc.gen(SORT_COL, n)
+            col = orc.gen(sort_col(args.key_range), n)
             return lambda: orc.sort_i64(col)
         if workload == "q12join":
             o, li = q12j_tables(lambda k, seed, m, a, b: orc.gen_column(k, seed, m, a=a, b=b), n)
@@ -791,7 +795,7 @@ def make_workload(args, ex, rows, row0, world, rank):
     if args.workload == "groupby":
         return GroupBy(ex, rows, row0, args.groups)
     if args.workload == "sort":
-        return Sort(ex, rows, row0, world)
+        return Sort(ex, rows, row0, world, args.key_range)
     if args.workload == "q12expr":
         return Q12Expr(ex, rows, row0)
     if args.workload == "join":

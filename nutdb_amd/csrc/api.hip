@@ -23,12 +23,12 @@ nut_status hip_fail(hipError_t e, const char *what) {
   return e == hipErrorOutOfMemory ? NUT_ERR_OOM : NUT_ERR_HIP;
 }
 
-nut_status Scratch::reserve(size_t need) {
+nut_status Scratch::reserve(size_t need, bool grow) {
   if (need <= bytes) return NUT_OK;
   if (ptr) (void)hipFree(ptr);
   ptr = nullptr;
   bytes = 0;
-  size_t want = need + need / 4;
+  size_t want = grow ? need + need / 4 : need;
   hipError_t e = hipMalloc(&ptr, want);
   if (e != hipSuccess) {
     ptr = nullptr;

@@ -148,7 +148,8 @@ void pool_give(nut_ctx *c, void *p, size_t bytes);
 struct Scratch {
   void *ptr = nullptr;
   size_t bytes = 0;
-  nut_status reserve(size_t need);
+  // grow: allocate 25 % more than asked, for buffers whose size creeps up call by call
+  nut_status reserve(size_t need, bool grow = true);
   void release();
 };
 

@@ -25,6 +25,7 @@
 #include <vector>
 
 #include "common.hpp"
+#include "sort.hpp"
 
 using namespace nut;
 
@@ -130,6 +131,7 @@ constexpr int kMaxRanks = 64;  // nut_groups_partition / nut_partition_i64 bound
 constexpr size_t kHdrWords = 2 + 2 * kMaxRanks;
 constexpr size_t kHdrBytes = kHdrWords * kMaxRanks * 8;
 constexpr int kSamples = 4096;  // sample sort: strided samples per rank
+constexpr uint64_t kSortFlip = 1ull << 63;  // int64 order -> unsigned order
 
 using Member = nut_dist::Member;
 
@@ -557,7 +559,21 @@ nut_status sort_member(nut_dist *d, int l, const int64_t *in, uint64_t n, const 
   if (!st)
     st = alltoallv(d, l, buf(mb, 0), sc.data(), sd.data(), buf(mb, 1), rc.data(), rd.data(),
                    max_cell(all, 1 + (size_t)P, 1, P, 1));
-  if (!st) st = nut_sort_i64(c, (const int64_t *)buf(mb, 1), (int64_t *)buf(mb, 2), rtot);
+  // this rank's key range from its buckets' splitters: the local sort's capped layout
+  // spreads exactly that range, not the full 64-bit one
+  uint64_t bnd[2] = {~0ull, 0};
+  for (int j = 0; j < nb; ++j) {
+    if (rg.lo[j] > me || rg.hi[j] < me) continue;
+    const uint64_t a = j == 0 ? 0 : (uint64_t)rg.e[j - 1] ^ kSortFlip;
+    const uint64_t b = j == nb - 1 ? ~0ull : ((uint64_t)rg.e[j] ^ kSortFlip) - 1;
+    bnd[0] = std::min(bnd[0], a);
+    bnd[1] = std::max(bnd[1], b);
+  }
+  if (!st && rtot) {
+    DeviceGuard dg(c->device);
+    st = nut::msd_sort_i64(c, (const int64_t *)buf(mb, 1), (int64_t *)buf(mb, 2), rtot, kSortFlip,
+                           bnd[0] <= bnd[1] ? bnd : nullptr);
+  }
   if (!st) st = nut_ctx_sync(c);
   if (st) return st;
   *out = (const int64_t *)buf(mb, 2);

@@ -410,18 +410,19 @@ constexpr HjCfg hj_make() {
   return HjCfg{T, (uint32_t)(T * I), hj_probe_kernel<true, T, I>, hj_probe_kernel<false, T, I>,
                hj_probe_kernel<true, T, I, true>};
 }
-// probe tile shapes (threads x rows per lane); NUT_OPT_JOIN_PROBE_CFG picks one for tuning runs
-const HjCfg &hj_cfg(const nut_ctx *c) {
+// probe tile shapes (threads x rows per lane); NUT_OPT_JOIN_PROBE_CFG picks one for tuning
+// runs.  A join keeps the index it was built with (its status array is sized by the tile).
+const HjCfg &hj_cfg(int i) {
   static const HjCfg cfgs[] = {hj_make<512, 8>(), hj_make<256, 8>(), hj_make<256, 16>(), hj_make<512, 16>(),
                                hj_make<256, 4>()};
-  return cfgs[c->opt[NUT_OPT_JOIN_PROBE_CFG]];
+  return cfgs[i];
 }
 // the unordered probe's tile shape: no look-back chain to shorten, so the smallest tiles
 // with the fewest registers (most waves, most slot loads in flight) — NUT_OPT_JOIN_ANY_CFG
-const HjCfg &hj_any_cfg(const nut_ctx *c) {
+const HjCfg &hj_any_cfg(int i) {
   static const HjCfg cfgs[] = {hj_make<256, 4>(), hj_make<512, 8>(), hj_make<256, 8>(), hj_make<512, 4>(),
                                hj_make<128, 4>()};
-  return cfgs[c->opt[NUT_OPT_JOIN_ANY_CFG]];
+  return cfgs[i];
 }
 
 }  // namespace
@@ -436,6 +437,7 @@ struct nut_join {
   uint64_t np = 0, ntiles = 0, n = 0;
   int type = 0;
   bool any_order = false;  // NUT_JOIN_ANY_ORDER: the unordered probe
+  int cfg = 0, any_cfg = 0;  // probe tile shapes chosen at build (context options then)
   uint64_t *status = nullptr;
   uint32_t *ticket = nullptr, *err = nullptr, *dup = nullptr;
   unsigned long long *total = nullptr;
@@ -449,7 +451,9 @@ nut_status join_build(nut_ctx *c, nut_join *j, const int64_t *build, uint64_t nb
   int log2c = 6;  // >= 2 slots per build row, >= 64 slots
   while ((1ull << log2c) < 2 * nb) ++log2c;
   const uint64_t cap = 1ull << log2c;
-  j->ntiles = (j->np + hj_cfg(c).tile - 1) / hj_cfg(c).tile;
+  j->cfg = (int)c->opt[NUT_OPT_JOIN_PROBE_CFG];
+  j->any_cfg = (int)c->opt[NUT_OPT_JOIN_ANY_CFG];
+  j->ntiles = (j->np + hj_cfg(j->cfg).tile - 1) / hj_cfg(j->cfg).tile;
   if (j->ntiles > 0xFFFFFFF0ull) return fail(NUT_ERR_UNSUPPORTED, "nut_join_i64: probe side too large");
   // [slots 16 B x cap | dup u32, pad | ticket u32, err u32, total u64 | status u64 x ntiles]
   const size_t o_dup = cap * 16, o_state = o_dup + 16;
@@ -521,7 +525,7 @@ nut_status join_probe(nut_join *j, bool write, int64_t *pi, int64_t *bi, uint64_
   if (!j->ntiles) return NUT_OK;
   if (j->any_order && write) {
     NUT_HIP(hipMemsetAsync(j->ticket, 0, 16, st));
-    const HjCfg &cf = hj_any_cfg(c);
+    const HjCfg &cf = hj_any_cfg(j->any_cfg);
     const uint64_t nt = (j->np + cf.tile - 1) / cf.tile;
     if (nt > 0x7FFFFFFFull) return fail(NUT_ERR_UNSUPPORTED, "nut_join: probe side too large");
     cf.any<<<dim3((unsigned)nt), dim3(cf.threads), 0, st>>>(j->t, j->probe, j->np, j->type, j->ticket, j->status,
@@ -529,7 +533,7 @@ nut_status join_probe(nut_join *j, bool write, int64_t *pi, int64_t *bi, uint64_
                                                          (const uint32_t *)j->dup, j->prows);
   } else {
     NUT_HIP(hipMemsetAsync(j->ticket, 0, j->state_bytes, st));
-    const HjCfg &cf = hj_cfg(c);
+    const HjCfg &cf = hj_cfg(j->cfg);
     (write ? cf.write : cf.count)<<<dim3((unsigned)j->ntiles), dim3(cf.threads), 0, st>>>(
         j->t, j->probe, j->np, j->type, j->ticket, j->status, (uint32_t)j->ntiles, j->total, pi, bi, cap, j->err,
         (const uint32_t *)j->dup, j->prows);

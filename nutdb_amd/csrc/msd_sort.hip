@@ -80,6 +80,29 @@ struct MsDigit {
   int shift;
   uint32_t mask;
   __device__ __forceinline__ uint32_t operator()(uint64_t k) const { return (uint32_t)((k - base) >> shift) & mask; }
+  static constexpr bool kMayFlag = false;
+  __device__ __forceinline__ bool out(uint64_t) const { return false; }
+};
+// The capped layout's digits: keys known (or sampled) to lie in [base,
+// base + span] are mapped monotonically onto 2^18 cells, so that the two capped levels use
+// all 512 x 512 regions whatever the span — a sample-sort rank's range, or a column's
+// narrow one, as evenly as the full 64-bit range.  x = (k - base) >> t < 2^32 (t = the
+// span's bit width - 32, or 0), p = x * mul < 2^50 (mul = floor(2^50 / ((span >> t) + 1))),
+// level 0's digit = p >> 41, level 1's = (p >> 32) & 511.  For the full range (base 0,
+// t = 32, mul = 2^18) these are the top two 9-bit digits of k.  A key above the span (lim =
+// span >> t; below base wraps above it) is out of range: level 0 flags it and the caller
+// sorts again with the exact layout.
+struct MsMap {
+  uint64_t base;
+  uint32_t mul, lim;
+  int t, pshift;
+  bool check;  // level 0: flag keys out of range
+  static constexpr bool kMayFlag = true;
+  __device__ __forceinline__ uint32_t operator()(uint64_t k) const {
+    const uint64_t p = (uint64_t)(uint32_t)((k - base) >> t) * mul;
+    return (uint32_t)(p >> pshift) & (MS_BINS - 1);
+  }
+  __device__ __forceinline__ bool out(uint64_t k) const { return check && ((k - base) >> t) > lim; }
 };
 
 __device__ __forceinline__ const uint64_t *ms_src(const MsBufs &bf, uint32_t buf) {
@@ -151,10 +174,10 @@ constexpr uint64_t kSkipRun = ~0ull;
 // H = 2: 32 Ki-key tiles (32 keys per lane in registers), staged and written out in two
 // halves of the tile's digit order through the same 16 Ki-key LDS buffer, so each digit's
 // output run per tile is twice as long (512 B instead of 256 B: fewer partial 128-B lines).
-template <int H>
+template <int H, class DG>
 __global__ __launch_bounds__(MS_THREADS) void ms_scatter_kernel(MsBufs bf, const MsSeg *__restrict__ segs,
                                                                    const uint32_t *__restrict__ tile_seg, uint32_t ntiles,
-                                                                   MsDigit dg, uint64_t flip,
+                                                                   DG dg, uint64_t flip,
                                                                    unsigned long long *__restrict__ cursor,
                                                                    int dst_buf = -1, uint64_t ocap = 0,
                                                                    unsigned long long *__restrict__ oflag = nullptr) {
@@ -193,11 +216,17 @@ __global__ __launch_bounds__(MS_THREADS) void ms_scatter_kernel(MsBufs bf, const
     uint32_t rk[ITEMS / 2];  // ranks in the tile's digit run (< TILE), 16-bit pairs
 #pragma unroll
     for (int i = 0; i < ITEMS; i += 2) rk[i / 2] = 0;
+    bool bad = false;  // a key outside the capped layout's span (MsMap, level 0)
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i) {
       const uint32_t idx = (uint32_t)i * MS_THREADS + tid;
-      if (idx < cnt) rk[i / 2] |= atomicAdd(&s_cnt[dg(key[i])], 1u) << (16 * (i & 1));
+      if (idx < cnt) {
+        rk[i / 2] |= atomicAdd(&s_cnt[dg(key[i])], 1u) << (16 * (i & 1));
+        bad |= dg.out(key[i]);
+      }
     }
+    if constexpr (DG::kMayFlag)
+      if (__ballot(bad) && lane == 0) atomicOr(oflag, 1ull);
     __syncthreads();
     uint32_t c = 0, incl = 0;
     if (tid < MS_BINS) {
@@ -517,7 +546,8 @@ struct LocalCfg {
   static_assert(WPT <= 2, "at most two windows per thread");
   // LDS: one round of 8-B keys, bucket counts -> starts, window starts, scan words
   static constexpr int NWIN = CAP / WS + 2;  // window table entries (+ end)
-  static constexpr int BYTES = LDS_KEYS * 8 + ((NB + 1) + NWIN + 16 + 2) * 4;
+  static constexpr int MM_OFF = (LDS_KEYS * 8 + ((NB + 1) + NWIN + 16 + 2) * 4 + 7) & ~7;
+  static constexpr int BYTES = MM_OFF + WAVES * 16;
 };
 
 // block-wide exclusive scan of one value per thread (THREADS <= 1024); returns the prefix
@@ -623,7 +653,7 @@ __device__ __forceinline__ void wave_bitonic32_multi(uint64_t (&v)[NR], int lane
 
 template <int THREADS, int MAXK, bool PREFETCH, int SB_ = 0, int WS_ = 0>
 __global__ __launch_bounds__(THREADS, 4) void ms_local_kernel(MsBufs bf, const MsSeg *__restrict__ segs, uint32_t nseg,
-                                                           uint64_t base, uint64_t flip, uint32_t *__restrict__ fb) {
+                                                           uint64_t flip, uint32_t *__restrict__ fb) {
   using C = LocalCfg<THREADS, MAXK, SB_, WS_>;
   constexpr int WAVES = C::WAVES, NB = C::NB, SB = C::SB, LS_WS = C::WS;
   __shared__ __attribute__((aligned(16))) char lds[C::BYTES];
@@ -632,6 +662,7 @@ __global__ __launch_bounds__(THREADS, 4) void ms_local_kernel(MsBufs bf, const M
   uint32_t *s_win = s_off + NB + 1;                        // [NWIN] window starts
   uint32_t *s_ws = s_win + C::NWIN;                        // 16 scan words
   uint32_t *s_misc = s_ws + 16;                            // [0] max window, [1] round split
+  uint64_t *s_wmm = (uint64_t *)(lds + C::MM_OFF);          // [WAVES][2] per-wave key min / max
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   uint64_t key[MAXK];
 #ifdef NUT_MSD_STAMPS
@@ -665,11 +696,47 @@ __global__ __launch_bounds__(THREADS, 4) void ms_local_kernel(MsBufs bf, const M
   MS_STAMP(0);
   finish_load(sg);
   const uint32_t c = (uint32_t)sg.count;
-  const int hi = (int)sg.aux;
   const uint32_t K = (c + THREADS - 1) / THREADS;
   const uint32_t pw = (uint32_t)wave * kWave * K + lane;
   uint64_t *dst = bf.a + ms_dst_off(sg);
-  if (hi == 0) {  // every key equal: copy
+  // ---- 0. the segment's own key range (a wave reduction, one LDS word pair per wave):
+  //         buckets split [min, max] whatever layout or key mapping produced the segment
+#pragma unroll
+  for (int j = 0; j < C::BPT; ++j) s_off[C::BPT * tid + j] = 0;
+  {
+    uint64_t mn = ~0ull, mx = 0;
+#pragma unroll
+    for (int i = 0; i < MAXK; ++i) {
+      const uint32_t p = pw + (uint32_t)i * kWave;
+      if ((uint32_t)i < K && p < c) {
+        mn = key[i] < mn ? key[i] : mn;
+        mx = key[i] > mx ? key[i] : mx;
+      }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      const uint64_t a = __shfl_xor(mn, off, 64), b = __shfl_xor(mx, off, 64);
+      mn = a < mn ? a : mn;
+      mx = b > mx ? b : mx;
+    }
+    if (lane == 0) {
+      s_wmm[2 * wave] = mn;
+      s_wmm[2 * wave + 1] = mx;
+    }
+  }
+  if (tid == 0) {
+    s_misc[0] = 0;
+    s_misc[1] = 0;
+  }
+  __syncthreads();
+  uint64_t kmin = s_wmm[0], kmax = s_wmm[1];
+#pragma unroll
+  for (int w = 1; w < WAVES; ++w) {
+    const uint64_t a = s_wmm[2 * w], b = s_wmm[2 * w + 1];
+    kmin = a < kmin ? a : kmin;
+    kmax = b > kmax ? b : kmax;
+  }
+  if (kmin == kmax) {  // every key equal: copy
 #pragma unroll
     for (int i = 0; i < MAXK; ++i) {
       const uint32_t p = pw + (uint32_t)i * kWave;
@@ -685,16 +752,10 @@ __global__ __launch_bounds__(THREADS, 4) void ms_local_kernel(MsBufs bf, const M
     dst[tid] = x;
     return false;
   }
-  // ---- 1. bucket ranks: the top SB of the hi bits of (key - base) that may differ
+  // ---- 1. bucket ranks: the top SB of the hi bits of (key - min) that may differ
   //         (fewer than SB: zero-padded, so only some buckets are used)
-  auto bucket = [&](uint64_t k) -> uint32_t { return (uint32_t)(((k - base) << (64 - hi)) >> (64 - SB)); };
-#pragma unroll
-  for (int j = 0; j < C::BPT; ++j) s_off[C::BPT * tid + j] = 0;
-  if (tid == 0) {
-    s_misc[0] = 0;
-    s_misc[1] = 0;
-  }
-  __syncthreads();
+  const int hi = 64 - __builtin_clzll(kmax - kmin);
+  auto bucket = [&](uint64_t k) -> uint32_t { return (uint32_t)(((k - kmin) << (64 - hi)) >> (64 - SB)); };
   uint32_t rk[(MAXK + 1) / 2];  // ranks in the bucket, 16-bit pairs
 #pragma unroll
   for (int i = 0; i < MAXK; i += 2) rk[i / 2] = 0;
@@ -891,8 +952,8 @@ __global__ __launch_bounds__(THREADS, 4) void ms_local_kernel(MsBufs bf, const M
 constexpr int LSD_BINS = 256;  // 8-bit passes
 
 template <int THREADS, int MAXK>
-__global__ __launch_bounds__(THREADS) void ms_lsd_kernel(MsBufs bf, const MsSeg *__restrict__ segs, uint64_t base,
-                                                         uint64_t flip, const uint32_t *__restrict__ fb) {
+__global__ __launch_bounds__(THREADS) void ms_lsd_kernel(MsBufs bf, const MsSeg *__restrict__ segs, uint64_t flip,
+                                                         const uint32_t *__restrict__ fb) {
   using C = LocalCfg<THREADS, MAXK>;
   constexpr int WAVES = C::WAVES;
   if (blockIdx.x >= fb[0]) return;
@@ -900,26 +961,57 @@ __global__ __launch_bounds__(THREADS) void ms_lsd_kernel(MsBufs bf, const MsSeg 
   __shared__ uint32_t s_wcnt[WAVES][LSD_BINS];
   __shared__ uint32_t s_tex[LSD_BINS];
   __shared__ uint32_t s_wsum[LSD_BINS / kWave];
+  __shared__ uint64_t s_wmm[WAVES][2];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const MsSeg sg = segs[fb[1 + blockIdx.x]];
   const uint32_t c = (uint32_t)sg.count;
-  const int nbits = (int)sg.aux;  // passes over bits [0, nbits) of (key - base)
   const uint32_t K = (c + THREADS - 1) / THREADS;
   const uint32_t pw = (uint32_t)wave * kWave * K + lane;
   const uint64_t *src = ms_src(bf, sg.buf) + sg.start;
   uint64_t *dst = bf.a + ms_dst_off(sg);
   const uint64_t f = sg.buf == 0 ? flip : 0;
   uint32_t lo[MAXK], hi[MAXK], pos[MAXK];
+  uint64_t mn = ~0ull, mx = 0;
 #pragma unroll
   for (int i = 0; i < MAXK; ++i) {
     const uint32_t p = pw + (uint32_t)i * kWave;
     const uint64_t v = src[min(p, c - 1)] ^ f;  // unconditional: the loads overlap
-    const uint64_t k = ((uint32_t)i < K && p < c) ? v : ~0ull;
-    lo[i] = (uint32_t)k;
-    hi[i] = (uint32_t)(k >> 32);
+    if ((uint32_t)i < K && p < c) {
+      mn = v < mn ? v : mn;
+      mx = v > mx ? v : mx;
+    }
+    lo[i] = (uint32_t)v;
+    hi[i] = (uint32_t)(v >> 32);
+  }
+  // the segment's key range: passes over bits [0, nbits) of x = key - min; padding
+  // (positions >= count) is x = all ones, behind every real key in every pass
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const uint64_t a = __shfl_xor(mn, off, 64), b = __shfl_xor(mx, off, 64);
+    mn = a < mn ? a : mn;
+    mx = b > mx ? b : mx;
+  }
+  if (lane == 0) {
+    s_wmm[wave][0] = mn;
+    s_wmm[wave][1] = mx;
+  }
+  __syncthreads();
+  uint64_t kmin = s_wmm[0][0], kmax = s_wmm[0][1];
+#pragma unroll
+  for (int w = 1; w < WAVES; ++w) {
+    kmin = s_wmm[w][0] < kmin ? s_wmm[w][0] : kmin;
+    kmax = s_wmm[w][1] > kmax ? s_wmm[w][1] : kmax;
+  }
+  const int nbits = kmax == kmin ? 0 : 64 - __builtin_clzll(kmax - kmin);
+#pragma unroll
+  for (int i = 0; i < MAXK; ++i) {
+    const uint32_t p = pw + (uint32_t)i * kWave;
+    const uint64_t x = ((uint32_t)i < K && p < c) ? ((((uint64_t)hi[i] << 32) | lo[i]) - kmin) : ~0ull;
+    lo[i] = (uint32_t)x;
+    hi[i] = (uint32_t)(x >> 32);
   }
   auto digit = [&](int i, int shift) -> uint32_t {
-    return (uint32_t)(((((uint64_t)hi[i] << 32) | lo[i]) - base) >> shift) & 255u;
+    return (uint32_t)((((uint64_t)hi[i] << 32) | lo[i]) >> shift) & 255u;
   };
   for (int shift = 0; shift < nbits; shift += 8) {
     for (int i = tid; i < WAVES * LSD_BINS; i += THREADS) (&s_wcnt[0][0])[i] = 0;
@@ -990,7 +1082,7 @@ __global__ __launch_bounds__(THREADS) void ms_lsd_kernel(MsBufs bf, const MsSeg 
 #pragma unroll
   for (int i = 0; i < MAXK; ++i) {
     const uint32_t p = pw + (uint32_t)i * kWave;
-    if ((uint32_t)i < K && p < c) dst[p] = (((uint64_t)hi[i] << 32) | lo[i]) ^ flip;
+    if ((uint32_t)i < K && p < c) dst[p] = ((((uint64_t)hi[i] << 32) | lo[i]) + kmin) ^ flip;
   }
 }
 
@@ -1059,8 +1151,7 @@ uint64_t tile_table(std::vector<MsSeg> &segs, uint32_t tile, std::vector<uint32_
 // Local sorts are persistent (the S and M classes prefetch the next segment's keys): as
 // many workgroups as fit on the device, each walking the list with stride gridDim.x.
 template <int T, int K>
-static void launch_class(nut_ctx *c, const MsBufs &bf, const MsSeg *d, unsigned n, uint64_t base, uint64_t flip,
-                         uint32_t *fb) {
+static void launch_class(nut_ctx *c, const MsBufs &bf, const MsSeg *d, unsigned n, uint64_t flip, uint32_t *fb) {
   constexpr bool PF = K <= 12;  // the L class has no registers to spare for a second key set
   static int per_cu = 0;        // resident workgroups per CU (occupancy query, once)
   if (per_cu == 0) {
@@ -1069,11 +1160,11 @@ static void launch_class(nut_ctx *c, const MsBufs &bf, const MsSeg *d, unsigned 
     per_cu = b;
   }
   const unsigned grid = PF ? (unsigned)std::min<uint64_t>(n, (uint64_t)c->num_cus * per_cu) : n;
-  hipLaunchKernelGGL((ms_local_kernel<T, K, PF>), dim3(grid), dim3(T), 0, c->stream, bf, d, n, base, flip, fb);
-  hipLaunchKernelGGL((ms_lsd_kernel<T, K>), dim3(n), dim3(T), 0, c->stream, bf, d, base, flip, (const uint32_t *)fb);
+  hipLaunchKernelGGL((ms_local_kernel<T, K, PF>), dim3(grid), dim3(T), 0, c->stream, bf, d, n, flip, fb);
+  hipLaunchKernelGGL((ms_lsd_kernel<T, K>), dim3(n), dim3(T), 0, c->stream, bf, d, flip, (const uint32_t *)fb);
 }
 
-static nut_status launch_local(nut_ctx *c, MetaArena &ar, const MsBufs &bf, uint64_t base, uint64_t flip,
+static nut_status launch_local(nut_ctx *c, MetaArena &ar, const MsBufs &bf, uint64_t flip,
                                const std::vector<MsSeg> &segs, int cls) {
   if (segs.empty()) return NUT_OK;
   MsSeg *d;
@@ -1083,11 +1174,11 @@ static nut_status launch_local(nut_ctx *c, MetaArena &ar, const MsBufs &bf, uint
   NUT_HIP(hipMemsetAsync(fb, 0, 4, c->stream));
   const unsigned n = (unsigned)segs.size();
   if (cls == 0)
-    launch_class<LS_S_THREADS, LS_S_ITEMS>(c, bf, d, n, base, flip, fb);
+    launch_class<LS_S_THREADS, LS_S_ITEMS>(c, bf, d, n, flip, fb);
   else if (cls == 1)
-    launch_class<LS_M_THREADS, LS_M_ITEMS>(c, bf, d, n, base, flip, fb);
+    launch_class<LS_M_THREADS, LS_M_ITEMS>(c, bf, d, n, flip, fb);
   else
-    launch_class<LS_L_THREADS, LS_L_ITEMS>(c, bf, d, n, base, flip, fb);
+    launch_class<LS_L_THREADS, LS_L_ITEMS>(c, bf, d, n, flip, fb);
   NUT_HIP(hipGetLastError());
   return NUT_OK;
 }
@@ -1095,16 +1186,16 @@ static nut_status launch_local(nut_ctx *c, MetaArena &ar, const MsBufs &bf, uint
 static int local_class(uint64_t count) { return count <= LS_S_CAP ? 0 : (count <= LS_M_CAP ? 1 : 2); }
 
 // local sorts of n segments listed in device memory (a device-planned level's class list)
-static nut_status launch_local_dev(nut_ctx *c, const MsBufs &bf, uint64_t base, uint64_t flip, const MsSeg *d,
-                                   unsigned n, uint32_t *fb, int cls) {
+static nut_status launch_local_dev(nut_ctx *c, const MsBufs &bf, uint64_t flip, const MsSeg *d, unsigned n,
+                                   uint32_t *fb, int cls) {
   if (n == 0) return NUT_OK;
   NUT_HIP(hipMemsetAsync(fb, 0, 4, c->stream));
   if (cls == 0)
-    launch_class<LS_S_THREADS, LS_S_ITEMS>(c, bf, d, n, base, flip, fb);
+    launch_class<LS_S_THREADS, LS_S_ITEMS>(c, bf, d, n, flip, fb);
   else if (cls == 1)
-    launch_class<LS_M_THREADS, LS_M_ITEMS>(c, bf, d, n, base, flip, fb);
+    launch_class<LS_M_THREADS, LS_M_ITEMS>(c, bf, d, n, flip, fb);
   else
-    launch_class<LS_L_THREADS, LS_L_ITEMS>(c, bf, d, n, base, flip, fb);
+    launch_class<LS_L_THREADS, LS_L_ITEMS>(c, bf, d, n, flip, fb);
   NUT_HIP(hipGetLastError());
   return NUT_OK;
 }
@@ -1115,7 +1206,7 @@ static constexpr int ms_halves() { return 2; }
 
 static void launch_scatter(hipStream_t st, unsigned grid, const MsBufs &bf, const MsSeg *segs, const uint32_t *tiles,
                            uint32_t ntiles, const MsDigit &dg, uint64_t flip, unsigned long long *cur) {
-  hipLaunchKernelGGL(ms_scatter_kernel<ms_halves()>, dim3(grid), dim3(MS_THREADS), 0, st, bf, segs, tiles, ntiles, dg,
+  hipLaunchKernelGGL((ms_scatter_kernel<ms_halves(), MsDigit>), dim3(grid), dim3(MS_THREADS), 0, st, bf, segs, tiles, ntiles, dg,
                      flip, cur);
 }
 
@@ -1175,7 +1266,7 @@ static nut_status device_level(nut_ctx *c, MetaArena &ar, const MsBufs &bf, cons
   c->sort_bytes += 8 * total + 16 * total;
   ++c->sort_levels;
   for (int cls = 2; cls >= 0; --cls)
-    if ((s = launch_local_dev(c, bf, dg.base, flip, lists + (uint64_t)cls * cap, cnt[cls], fb[cls], cls))) return s;
+    if ((s = launch_local_dev(c, bf, flip, lists + (uint64_t)cls * cap, cnt[cls], fb[cls], cls))) return s;
   if (cnt[3]) {  // sub-segments too large for a local sort: to the host, for another level
     over.resize(cnt[3]);
     NUT_HIP(hipMemcpyAsync(over.data(), lists + 3 * cap, cnt[3] * sizeof(MsSeg), hipMemcpyDeviceToHost, st));
@@ -1189,16 +1280,37 @@ static nut_status device_level(nut_ctx *c, MetaArena &ar, const MsBufs &bf, cons
 
 constexpr uint64_t kCappedMin = 1ull << 25;  // smaller inputs: the exact layout (its passes are short)
 
-// Capped two-level layout: large inputs whose two top 9-bit digits look
-// uniform in a strided sample skip both histogram passes.  Level 0 scatters `in` by the top
-// digit into 512 regions of ocap0 rows of tmp (about 1.1 x an even share each); level 1
-// scatters every region by the next digit into 512 regions of ocap1 rows of tmp2; the local
-// sorts read those regions and write each sorted run to its exact place in out, found by a
-// scan of the level-1 cursors (ms_plan_capped_kernel).  48 B/key instead of 64.  A region
-// overflow (a key distribution the sample did not show) or a sub-segment too large for a
-// local sort returns NUT_ERR_CAPACITY without a message: the caller sorts again with the
-// exact layout (`in` is never written).
-static nut_status msd_sort_capped(nut_ctx *c, const int64_t *in, int64_t *out, uint64_t n, uint64_t flip) {
+// The capped layout's key map (MsMap) for keys in [lo, hi] of the flipped key space; false
+// when the span is too narrow for 2^18 cells (the exact layout then runs).
+static bool capped_map(uint64_t lo, uint64_t hi, MsMap &m) {
+  if (hi < lo || hi - lo < (1ull << 18)) return false;
+  const uint64_t span = hi - lo;
+  const int bw = 64 - __builtin_clzll(span);
+  const int t = bw > 32 ? bw - 32 : 0;
+  const uint64_t lim = span >> t;  // < 2^32
+  const uint64_t mul = (1ull << 50) / (lim + 1);  // (2^18, 2^32): lim >= 2^18
+  m = MsMap{lo, (uint32_t)mul, (uint32_t)lim, t, 41, true};
+  return true;
+}
+// host copy of MsMap's cell (level-0 digit * 512 + level-1 digit)
+static uint32_t capped_cell(const MsMap &m, uint64_t k) {
+  return (uint32_t)(((uint64_t)(uint32_t)((k - m.base) >> m.t) * m.mul) >> 32);
+}
+
+// Capped two-level layout: large inputs whose keys spread evenly over their
+// range (in a strided sample) skip both histogram passes.  The keys' range is the sample's
+// [min, max] widened by 1/1024 of its span on each side, intersected with the caller's
+// bounds when it knows them (a sample-sort rank's splitters); MsMap spreads it over 2^18
+// cells.  Level 0 scatters `in` by the cell's top 9 bits into 512 regions of ocap0 rows of
+// tmp (about 1.1 x an even share each); level 1 scatters every region by the low 9 bits
+// into 512 regions of ocap1 rows of tmp2; the local sorts read those regions and write each
+// sorted run to its exact place in out, found by a scan of the level-1 cursors
+// (ms_plan_capped_kernel).  48 B/key instead of 64.  A key outside the range, a region
+// overflow (a key distribution the sample did not show), a sub-segment too large for a
+// local sort or scratch that does not fit returns NUT_ERR_CAPACITY without a message: the
+// caller sorts again with the exact layout (`in` is never written).
+static nut_status msd_sort_capped(nut_ctx *c, const int64_t *in, int64_t *out, uint64_t n, uint64_t flip,
+                                  const uint64_t *bounds) {
   hipStream_t st = c->stream;
   constexpr uint32_t kSample = 16384;
   MetaArena ar{c};
@@ -1211,20 +1323,41 @@ static nut_status msd_sort_capped(nut_ctx *c, const int64_t *in, int64_t *out, u
   std::vector<uint64_t> samp(kSample);
   NUT_HIP(hipMemcpyAsync(samp.data(), dsamp, kSample * 8, hipMemcpyDeviceToHost, st));
   NUT_HIP(hipStreamSynchronize(st));
-  {  // admission: no digit value holds more than twice its share of the sample
+  MsMap m0;
+  {  // the key range, then admission: no digit value holds more than twice its share
+    uint64_t smin = ~0ull, smax = 0;
+    for (uint64_t k : samp) {
+      smin = std::min(smin, k);
+      smax = std::max(smax, k);
+    }
+    const uint64_t d = (smax - smin) >> 10;
+    uint64_t lo = smin >= d ? smin - d : 0, hi = smax <= ~0ull - d ? smax + d : ~0ull;
+    if (bounds) {
+      lo = std::max(lo, bounds[0]);
+      hi = std::min(hi, bounds[1]);
+    }
+    if (!capped_map(lo, hi, m0)) return NUT_ERR_CAPACITY;
     std::vector<uint32_t> h0(MS_BINS, 0), h1(MS_BINS, 0);
     for (uint64_t k : samp) {
-      ++h0[k >> (64 - MS_BITS)];
-      ++h1[(k >> (64 - 2 * MS_BITS)) & (MS_BINS - 1)];
+      if (k < lo || k > hi) return NUT_ERR_CAPACITY;  // outside the caller's bounds: not a capped input
+      const uint32_t cell = capped_cell(m0, k);
+      ++h0[cell >> MS_BITS];
+      ++h1[cell & (MS_BINS - 1)];
     }
     const uint32_t lim = 2 * kSample / MS_BINS;
     for (int d = 0; d < MS_BINS; ++d)
       if (h0[d] > lim || h1[d] > lim) return NUT_ERR_CAPACITY;
   }
+  // scratch that does not fit is a reason for the exact layout (1.25 x n), not a failure
+  auto reserve = [&](Scratch &sc, size_t bytes) -> nut_status {
+    if (sc.reserve(bytes, false) == NUT_OK) return NUT_OK;
+    (void)hipGetLastError();
+    c->sort_tmp2.release();
+    return NUT_ERR_CAPACITY;
+  };
   // ---- level 0: in -> tmp, 512 capped regions
   const uint64_t ocap0 = ((n / MS_BINS) * 11 / 10 + 2 * MS_TILE + 31) & ~31ull;
-  s = c->sort_tmp.reserve((size_t)MS_BINS * ocap0 * 8);
-  if (s) return s;
+  if ((s = reserve(c->sort_tmp, (size_t)MS_BINS * ocap0 * 8))) return s;
   const MsBufs bf0{(const uint64_t *)in, (uint64_t *)out, (uint64_t *)c->sort_tmp.ptr, nullptr};
   std::vector<MsSeg> one{MsSeg{0, n, 0, 0}};
   std::vector<uint32_t> tiles;
@@ -1239,10 +1372,10 @@ static nut_status msd_sort_capped(nut_ctx *c, const int64_t *in, int64_t *out, u
   uint32_t *dtile;
   uint64_t *dcur0;
   if ((s = ar.upload(one, &dseg)) || (s = ar.upload(tiles, &dtile)) || (s = ar.upload(cur0, &dcur0))) return s;
-  const MsDigit dg0{0, 64 - MS_BITS, (uint32_t)MS_BINS - 1};
-  hipLaunchKernelGGL(ms_scatter_kernel<ms_halves()>, dim3((unsigned)std::min<uint64_t>(nt0, (uint64_t)c->num_cus)),
-                     dim3(MS_THREADS), 0, st, bf0, (const MsSeg *)dseg, (const uint32_t *)dtile, (uint32_t)nt0, dg0,
-                     flip, (unsigned long long *)dcur0, 2, ocap0, (unsigned long long *)(dcur0 + MS_BINS));
+  hipLaunchKernelGGL((ms_scatter_kernel<ms_halves(), MsMap>),
+                     dim3((unsigned)std::min<uint64_t>(nt0, (uint64_t)c->num_cus)), dim3(MS_THREADS), 0, st, bf0,
+                     (const MsSeg *)dseg, (const uint32_t *)dtile, (uint32_t)nt0, m0, flip,
+                     (unsigned long long *)dcur0, 2, ocap0, (unsigned long long *)(dcur0 + MS_BINS));
   NUT_HIP(hipGetLastError());
   std::vector<uint64_t> end0(MS_BINS + 1);
   NUT_HIP(hipMemcpyAsync(end0.data(), dcur0, end0.size() * 8, hipMemcpyDeviceToHost, st));
@@ -1260,8 +1393,7 @@ static nut_status msd_sort_capped(nut_ctx *c, const int64_t *in, int64_t *out, u
     cmax = std::max(cmax, cnt);
   }
   const uint64_t ocap1 = ((cmax / MS_BINS) * 23 / 20 + 64 + 1) & ~1ull;
-  s = c->sort_tmp2.reserve((size_t)MS_BINS * MS_BINS * ocap1 * 8);
-  if (s) return s;
+  if ((s = reserve(c->sort_tmp2, (size_t)MS_BINS * MS_BINS * ocap1 * 8))) return s;
   const MsBufs bf{(const uint64_t *)in, (uint64_t *)out, (uint64_t *)c->sort_tmp.ptr, (uint64_t *)c->sort_tmp2.ptr};
   const uint64_t nt1 = tile_table(segs, MS_TILE * ms_halves(), tiles);
   if (nt1 > 0x7FFFFFFFull) return fail(NUT_ERR_UNSUPPORTED, "nut_sort_i64: too many tiles");
@@ -1283,13 +1415,15 @@ static nut_status msd_sort_capped(nut_ctx *c, const int64_t *in, int64_t *out, u
   uint32_t *fb[3];
   for (auto &f : fb) f = (uint32_t *)ar.alloc((lcap + 1) * 4);
   NUT_HIP(hipMemsetAsync(counts, 0, 16, st));
-  const MsDigit dg1{0, 64 - 2 * MS_BITS, (uint32_t)MS_BINS - 1};
-  hipLaunchKernelGGL(ms_scatter_kernel<ms_halves()>, dim3((unsigned)std::min<uint64_t>(nt1, (uint64_t)c->num_cus)),
-                     dim3(MS_THREADS), 0, st, bf, (const MsSeg *)dsegs, (const uint32_t *)dt1, (uint32_t)nt1, dg1, flip,
-                     (unsigned long long *)dcur1, 3, ocap1, (unsigned long long *)(dcur1 + nr));
+  MsMap m1 = m0;
+  m1.pshift = 32;
+  m1.check = false;
+  hipLaunchKernelGGL((ms_scatter_kernel<ms_halves(), MsMap>),
+                     dim3((unsigned)std::min<uint64_t>(nt1, (uint64_t)c->num_cus)), dim3(MS_THREADS), 0, st, bf,
+                     (const MsSeg *)dsegs, (const uint32_t *)dt1, (uint32_t)nt1, m1, flip, (unsigned long long *)dcur1,
+                     3, ocap1, (unsigned long long *)(dcur1 + nr));
   hipLaunchKernelGGL(ms_plan_capped_kernel, dim3(MS_BINS), dim3(MS_BINS), 0, st, (const unsigned long long *)dcur1,
-                     (const uint64_t *)ddb, ocap1, 64 - 2 * MS_BITS, lists, lcap, counts,
-                     (unsigned long long *)(dcur1 + nr));
+                     (const uint64_t *)ddb, ocap1, 64, lists, lcap, counts, (unsigned long long *)(dcur1 + nr));
   NUT_HIP(hipGetLastError());
   uint64_t *hc = c->host_pinned;
   NUT_HIP(hipMemcpyAsync(hc, counts, 16, hipMemcpyDeviceToHost, st));
@@ -1299,19 +1433,20 @@ static nut_status msd_sort_capped(nut_ctx *c, const int64_t *in, int64_t *out, u
   const uint32_t *cnt = (const uint32_t *)hc;
   const uint32_t ncls[3] = {cnt[0], cnt[1], cnt[2]};
   for (int cls = 2; cls >= 0; --cls)
-    if ((s = launch_local_dev(c, bf, 0, flip, lists + (uint64_t)cls * lcap, ncls[cls], fb[cls], cls))) return s;
+    if ((s = launch_local_dev(c, bf, flip, lists + (uint64_t)cls * lcap, ncls[cls], fb[cls], cls))) return s;
   c->sort_bytes = 48 * n;
   c->sort_levels = 2;
   return NUT_OK;
 }
 
-nut_status msd_sort_i64(nut_ctx *c, const int64_t *in, int64_t *out, uint64_t n, uint64_t flip) {
+nut_status msd_sort_i64(nut_ctx *c, const int64_t *in, int64_t *out, uint64_t n, uint64_t flip,
+                        const uint64_t *bounds) {
   hipStream_t st = c->stream;
   c->sort_bytes = 0;
   c->sort_levels = 0;
   c->timer.begin(st, NUT_KERNEL_SORT);
   if (n >= kCappedMin) {
-    nut_status s = msd_sort_capped(c, in, out, n, flip);
+    nut_status s = msd_sort_capped(c, in, out, n, flip, bounds);
     if (s != NUT_ERR_CAPACITY) {
       c->timer.end(st);
       if (!s) NUT_HIP(hipStreamSynchronize(st));
@@ -1321,7 +1456,10 @@ nut_status msd_sort_i64(nut_ctx *c, const int64_t *in, int64_t *out, uint64_t n,
     c->sort_levels = 0;
   }
   nut_status s = c->sort_tmp.reserve(n * 8);
-  if (s) return s;
+  if (s) {
+    c->timer.end(st);
+    return s;
+  }
   const MsBufs bf{(const uint64_t *)in, (uint64_t *)out, (uint64_t *)c->sort_tmp.ptr, nullptr};
   MetaArena ar{c};
 
@@ -1329,7 +1467,7 @@ nut_status msd_sort_i64(nut_ctx *c, const int64_t *in, int64_t *out, uint64_t n,
     std::vector<MsSeg> one{{0, n, 0, 64}};
     s = ar.begin(1024);
     if (s) return s;
-    s = launch_local(c, ar, bf, 0, flip, one, local_class(n));
+    s = launch_local(c, ar, bf, flip, one, local_class(n));
     if (s) return s;
     c->sort_bytes = 16 * n;
     c->timer.end(st);
@@ -1468,7 +1606,7 @@ nut_status msd_sort_i64(nut_ctx *c, const int64_t *in, int64_t *out, uint64_t n,
   if (s) return s;
   for (int cls = 2; cls >= 0; --cls) {
     for (const MsSeg &sg : small[cls]) c->sort_bytes += 16 * sg.count;
-    if ((s = launch_local(c, ar, bf, dg.base, flip, small[cls], cls))) return s;
+    if ((s = launch_local(c, ar, bf, flip, small[cls], cls))) return s;
   }
   for (const MsSeg &sg : done) c->sort_bytes += 16 * sg.count;
   if (!done.empty()) {

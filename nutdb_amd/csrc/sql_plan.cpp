@@ -2858,8 +2858,16 @@ nut_status groupby_packed(nut_ctx *c, const nut_plan &p, const nut_agg_spec &s, 
     memset(q1.agg_mask, 0, sizeof q1.agg_mask);
     memset(q1.agg_val, 0, sizeof q1.agg_val);
     q1.agg_op[0] = NUT_AGG_COUNT;
+    // group hint: the main pass's groups times the argument's value range, capped at a
+    // quarter of the rows and 2^26 (the result table is sized from it) — a high-cardinality
+    // countUnique takes the partitioned path in one pass instead of regrowing an on-chip
+    // table with a rescan per growth step
+    const int xb = fx[ci].bits;
+    const uint64_t xr = xb >= 40 ? (1ull << 40) : (1ull << xb);
+    const uint64_t hcap = std::min<uint64_t>(s.n / 4, 1ull << 26);
+    const uint64_t hint1 = std::max<uint64_t>(1, ng > hcap / xr ? hcap : std::min(hcap, ng * xr));
     nut_groups *g1 = nullptr;
-    st = nut_groupby(c, &q1, 0, &g1);
+    st = nut_groupby(c, &q1, hint1, &g1);
     if (st) return st;
     uint64_t n1 = 0;
     st = nut_groups_size(g1, &n1);
@@ -3985,6 +3993,9 @@ nut_status resolve_subqueries(const nut_plan &p, nut_plan &q,
       continue;
     }
     const uint64_t w = r->host[0][0];
+    if (r->types[0] != NUT_T_F64 && r->types[0] != NUT_T_I64)  // a dictionary code is no number
+      return fail(NUT_ERR_PLAN, "scalar subquery returned a non-numeric value (type " +
+                                    std::to_string(r->types[0]) + "); only int64 / float64 results compare");
     if (r->types[0] == NUT_T_F64) {
       double d;
       memcpy(&d, &w, 8);
@@ -4254,6 +4265,9 @@ nut_status nut_plan_executen(nut_ctx *c, const nut_plan *p, const nut_column *co
 nut_status nut_plan_prepare(const nut_plan *p, const nut_column *cols, int ncols) {
   if (!p || (ncols && !cols) || ncols < 0) return fail(NUT_ERR_INVALID_ARG, "nut_plan_prepare: NULL argument");
   if (!p->compiled) return NUT_OK;  // precompiled kernels only
+  // scalar subqueries: their values (int64 or f64 constants) decide the program types, so
+  // the shape is compiled when the plan executes with the values in place
+  if (!p->subs.empty()) return NUT_OK;
   nut_plan sq;
   if (p->star) {
     std::vector<std::string> names;

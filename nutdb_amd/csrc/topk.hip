@@ -87,7 +87,10 @@ extern "C" nut_status nut_topk_positions(nut_ctx *c, const void *keys, int key_t
   if (k >= n) {  // every key
     *count_host = n;
     if (n > cap) return NUT_ERR_CAPACITY;
-    if (!positions) return fail(NUT_ERR_INVALID_ARG, "nut_topk_positions: NULL output");
+    if (!positions) {
+    c->timer.end(st);
+    return fail(NUT_ERR_INVALID_ARG, "nut_topk_positions: NULL output");
+  }
     hipLaunchKernelGGL(topk_iota_kernel, dim3((unsigned)std::min<uint64_t>((n + 255) / 256, 4096)), dim3(256), 0, st,
                        positions, n);
     NUT_HIP(hipGetLastError());
@@ -129,7 +132,10 @@ extern "C" nut_status nut_topk_positions(nut_ctx *c, const void *keys, int key_t
     c->timer.end(st);
     return NUT_ERR_CAPACITY;
   }
-  if (!positions) return fail(NUT_ERR_INVALID_ARG, "nut_topk_positions: NULL output");
+  if (!positions) {
+    c->timer.end(st);
+    return fail(NUT_ERR_INVALID_ARG, "nut_topk_positions: NULL output");
+  }
   // collect (unordered) into scratch, then sort the positions ascending into `positions`
   int64_t *tmp = nullptr;
   NUT_HIP(hipMallocAsync((void **)&tmp, cand * 8, st));

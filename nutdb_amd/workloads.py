@@ -43,6 +43,18 @@ Q1_COLS = [
 # config 5: SELECT k FROM t ORDER BY k     full-range random i64
 SORT_COL = ("k", L.GEN_FULL_I64, 0x50, 0, 0, 1.0)
 
+
+def sort_col(key_range=None):
+    """The sort column: full-range keys, or (key_range = f < 1/2) keys uniform over a
+    fraction f of the int64 range — from 3 * 2^60 while it fits, else from -2^63 — the
+    share one rank of an 8-GPU sample sort holds at f = 1/8."""
+    if key_range is None:
+        return SORT_COL
+    width = int(float(key_range) * 2.0**64)
+    assert 1 <= width <= 2**63 - 1, key_range
+    start = 3 << 60 if width <= 5 << 60 else -(2**63)
+    return ("k", L.GEN_RANGE_I64, 0x50, start, width, 1.0)
+
 # Expression-mode workload: the reference fixture tests/sql/5.sql (TPC-H Q12 shape) with
 # integer codes for its strings; 7 int64 columns = 56 B/row.
 Q12_COLS = [

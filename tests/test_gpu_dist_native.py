@@ -58,8 +58,8 @@ def _cmp(got, want, f64_sum_cols=()):
             assert np.array_equal(gw[:, j], ww[:, j]), j
 
 
-@pytest.mark.parametrize("P", [1, 2, 3, 5])
-@pytest.mark.parametrize("G", [7, 1000, 200_000])
+@pytest.mark.parametrize("P", [1, 2, 3, 5, 8])
+@pytest.mark.parametrize("G", [7, 1000, 100_000, 200_000])
 def test_virtual_groupby_vs_oracle(ND, orc, P, G):
     from nutdb_amd import Agg
     n = 1_000_003
@@ -82,9 +82,10 @@ def test_virtual_groupby_vs_oracle(ND, orc, P, G):
     _cmp(got, want)
 
 
-@pytest.mark.parametrize("P", [2, 4])
+@pytest.mark.parametrize("P", [2, 4, 8])
 def test_virtual_q1_two_keys(ND, orc, P):
-    """config 4 across P ranks: 2 keys, predicate, the fused disc_price expression."""
+    """config 4 across P ranks (P = 8: the driver's 8-GPU split): 2 keys, predicate, the
+    fused disc_price expression."""
     from nutdb_amd import Agg, AggQuery
     from nutdb_amd.workloads import Q1_COLS, Q1_DATE_K
     n = 2_000_001
