@@ -64,6 +64,7 @@ struct MsSeg {
                  // number of low bits of (key - base) its keys may still differ in
   uint64_t dst = kSameDst;  // local sort / copy: where the sorted run goes in out
                             // (kSameDst: at start — the exact layout)
+  uint64_t base = 0;        // local sort: the segment's keys k satisfy 0 <= k - base < 2^aux
 };
 struct MsBufs {
   const uint64_t *in;
@@ -80,29 +81,29 @@ struct MsDigit {
   int shift;
   uint32_t mask;
   __device__ __forceinline__ uint32_t operator()(uint64_t k) const { return (uint32_t)((k - base) >> shift) & mask; }
-  static constexpr bool kMayFlag = false;
-  __device__ __forceinline__ bool out(uint64_t) const { return false; }
+  static constexpr bool kCheck = false;
+  uint64_t maxx = ~0ull;
 };
 // The capped layout's digits: keys known (or sampled) to lie in [base,
 // base + span] are mapped monotonically onto 2^18 cells, so that the two capped levels use
 // all 512 x 512 regions whatever the span — a sample-sort rank's range, or a column's
 // narrow one, as evenly as the full 64-bit range.  x = (k - base) >> t < 2^32 (t = the
-// span's bit width - 32, or 0), p = x * mul < 2^50 (mul = floor(2^50 / ((span >> t) + 1))),
-// level 0's digit = p >> 41, level 1's = (p >> 32) & 511.  For the full range (base 0,
-// t = 32, mul = 2^18) these are the top two 9-bit digits of k.  A key above the span (lim =
-// span >> t; below base wraps above it) is out of range: level 0 flags it and the caller
-// sorts again with the exact layout.
+// span's bit width - 32, or 0), cell = (x * mul) >> 32 < 2^18 (mul = floor(2^50 / ((span >>
+// t) + 1))): one v_mul_hi_u32; level 0's digit = cell >> 9, level 1's = cell & 511.  For the
+// full range (base 0, t = 32, mul = 2^18) these are the top two 9-bit digits of k.  Level 0
+// flags a key outside the span (k - base > maxx; a key below base wraps above it), whose
+// digit is garbage but whose write stays inside its region: the caller sorts again with the
+// exact layout.  Cell v holds the keys with (k - base) >> t in [ceil(v 2^32 / mul),
+// ceil((v + 1) 2^32 / mul)): ms_plan_capped_kernel gives each cell's segment that base.
 struct MsMap {
   uint64_t base;
   uint32_t mul, lim;
-  int t, pshift;
-  bool check;  // level 0: flag keys out of range
-  static constexpr bool kMayFlag = true;
+  int t, dshift;  // dshift: 9 (level 0) or 0 (level 1)
+  uint64_t maxx;  // level 0: ((lim + 1) << t) - 1, the largest k - base in range; level 1: ~0
+  static constexpr bool kCheck = true;
   __device__ __forceinline__ uint32_t operator()(uint64_t k) const {
-    const uint64_t p = (uint64_t)(uint32_t)((k - base) >> t) * mul;
-    return (uint32_t)(p >> pshift) & (MS_BINS - 1);
+    return (__umulhi((uint32_t)((k - base) >> t), mul) >> dshift) & (MS_BINS - 1);
   }
-  __device__ __forceinline__ bool out(uint64_t k) const { return check && ((k - base) >> t) > lim; }
 };
 
 __device__ __forceinline__ const uint64_t *ms_src(const MsBufs &bf, uint32_t buf) {
@@ -216,16 +217,16 @@ __global__ __launch_bounds__(MS_THREADS) void ms_scatter_kernel(MsBufs bf, const
     uint32_t rk[ITEMS / 2];  // ranks in the tile's digit run (< TILE), 16-bit pairs
 #pragma unroll
     for (int i = 0; i < ITEMS; i += 2) rk[i / 2] = 0;
-    bool bad = false;  // a key outside the capped layout's span (MsMap, level 0)
+    bool bad = false;  // MsMap level 0: a key outside the mapped span
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i) {
       const uint32_t idx = (uint32_t)i * MS_THREADS + tid;
       if (idx < cnt) {
         rk[i / 2] |= atomicAdd(&s_cnt[dg(key[i])], 1u) << (16 * (i & 1));
-        bad |= dg.out(key[i]);
+        if constexpr (DG::kCheck) bad |= key[i] - dg.base > dg.maxx;
       }
     }
-    if constexpr (DG::kMayFlag)
+    if constexpr (DG::kCheck)
       if (__ballot(bad) && lane == 0) atomicOr(oflag, 1ull);
     __syncthreads();
     uint32_t c = 0, incl = 0;
@@ -302,6 +303,7 @@ __global__ __launch_bounds__(MS_THREADS) void ms_scatter_kernel(MsBufs bf, const
 // (segment, digit) pair — 2^18 of them at the second level of 1.25e9 keys.
 __global__ __launch_bounds__(MS_BINS) void ms_plan_kernel(const MsSeg *__restrict__ segs,
                                                           const unsigned long long *__restrict__ hist, int hi,
+                                                          uint64_t base,
                                                           unsigned long long *__restrict__ cursor,
                                                           MsSeg *__restrict__ lists, uint64_t cap,
                                                           unsigned int *__restrict__ counts) {
@@ -333,7 +335,8 @@ __global__ __launch_bounds__(MS_BINS) void ms_plan_kernel(const MsSeg *__restric
     unsigned int b = 0;
     if (lane == leader) b = atomicAdd(&counts[k], (unsigned int)__popcll(m));
     b = __shfl(b, leader, 64);
-    if (cls == k) lists[(uint64_t)k * cap + b + lane_rank(m)] = MsSeg{start, c, sg.buf == 2 ? 1u : 2u, (uint32_t)hi};
+    if (cls == k)
+      lists[(uint64_t)k * cap + b + lane_rank(m)] = MsSeg{start, c, sg.buf == 2 ? 1u : 2u, (uint32_t)hi, kSameDst, base};
   }
 }
 
@@ -345,7 +348,7 @@ __global__ __launch_bounds__(MS_BINS) void ms_plan_kernel(const MsSeg *__restric
 // too large for every class sets *oflag (the host sorts again with the exact layout).
 __global__ __launch_bounds__(MS_BINS) void ms_plan_capped_kernel(const unsigned long long *__restrict__ cursor,
                                                                  const uint64_t *__restrict__ dbase, uint64_t ocap,
-                                                                 int hi, MsSeg *__restrict__ lists, uint64_t cap,
+                                                                 MsMap m, MsSeg *__restrict__ lists, uint64_t cap,
                                                                  unsigned int *__restrict__ counts,
                                                                  unsigned long long *__restrict__ oflag) {
   __shared__ unsigned long long s_wsum[MS_BINS / kWave];
@@ -366,15 +369,22 @@ __global__ __launch_bounds__(MS_BINS) void ms_plan_capped_kernel(const unsigned 
   const uint64_t dst = dbase[blockIdx.x] + incl - c + add;
   const int cls = c == 0 ? -1 : (c <= LS_S_CAP ? 0 : (c <= LS_M_CAP ? 1 : (c <= LS_CAP ? 2 : 3)));
   if (cls == 3) atomicOr(oflag, 1ull);
+  // cell r's keys: (k - m.base) >> m.t in [x0, x1), x_v = ceil(v 2^32 / mul) (the first x with
+  // umulhi(x, mul) >= v), x1 capped at lim + 1: the segment's base and the bits that vary
+  const uint64_t x0 = ((r << 32) + m.mul - 1) / m.mul;
+  const uint64_t x1 = min<uint64_t>((((r + 1) << 32) + m.mul - 1) / m.mul, (uint64_t)m.lim + 1);
+  const uint64_t width = x1 > x0 ? (x1 - x0) << m.t : 1;  // < 2^64: at most 2^14 x-steps of 2^t
+  const uint64_t sbase = m.base + (x0 << m.t);
+  const uint32_t hi = width <= 1 ? 0u : (uint32_t)(64 - __builtin_clzll(width - 1));
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
-    const uint64_t m = __ballot(cls == k);
-    if (!m) continue;
-    const int leader = __builtin_ctzll(m);
+    const uint64_t mk = __ballot(cls == k);
+    if (!mk) continue;
+    const int leader = __builtin_ctzll(mk);
     unsigned int b = 0;
-    if (lane == leader) b = atomicAdd(&counts[k], (unsigned int)__popcll(m));
+    if (lane == leader) b = atomicAdd(&counts[k], (unsigned int)__popcll(mk));
     b = __shfl(b, leader, 64);
-    if (cls == k) lists[(uint64_t)k * cap + b + lane_rank(m)] = MsSeg{start, c, 3u, (uint32_t)hi, dst};
+    if (cls == k) lists[(uint64_t)k * cap + b + lane_rank(mk)] = MsSeg{start, c, 3u, hi, dst, sbase};
   }
 }
 
@@ -546,8 +556,7 @@ struct LocalCfg {
   static_assert(WPT <= 2, "at most two windows per thread");
   // LDS: one round of 8-B keys, bucket counts -> starts, window starts, scan words
   static constexpr int NWIN = CAP / WS + 2;  // window table entries (+ end)
-  static constexpr int MM_OFF = (LDS_KEYS * 8 + ((NB + 1) + NWIN + 16 + 2) * 4 + 7) & ~7;
-  static constexpr int BYTES = MM_OFF + WAVES * 16;
+  static constexpr int BYTES = LDS_KEYS * 8 + ((NB + 1) + NWIN + 16 + 2) * 4;
 };
 
 // block-wide exclusive scan of one value per thread (THREADS <= 1024); returns the prefix
@@ -662,7 +671,6 @@ __global__ __launch_bounds__(THREADS, 4) void ms_local_kernel(MsBufs bf, const M
   uint32_t *s_win = s_off + NB + 1;                        // [NWIN] window starts
   uint32_t *s_ws = s_win + C::NWIN;                        // 16 scan words
   uint32_t *s_misc = s_ws + 16;                            // [0] max window, [1] round split
-  uint64_t *s_wmm = (uint64_t *)(lds + C::MM_OFF);          // [WAVES][2] per-wave key min / max
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   uint64_t key[MAXK];
 #ifdef NUT_MSD_STAMPS
@@ -699,44 +707,9 @@ __global__ __launch_bounds__(THREADS, 4) void ms_local_kernel(MsBufs bf, const M
   const uint32_t K = (c + THREADS - 1) / THREADS;
   const uint32_t pw = (uint32_t)wave * kWave * K + lane;
   uint64_t *dst = bf.a + ms_dst_off(sg);
-  // ---- 0. the segment's own key range (a wave reduction, one LDS word pair per wave):
-  //         buckets split [min, max] whatever layout or key mapping produced the segment
-#pragma unroll
-  for (int j = 0; j < C::BPT; ++j) s_off[C::BPT * tid + j] = 0;
-  {
-    uint64_t mn = ~0ull, mx = 0;
-#pragma unroll
-    for (int i = 0; i < MAXK; ++i) {
-      const uint32_t p = pw + (uint32_t)i * kWave;
-      if ((uint32_t)i < K && p < c) {
-        mn = key[i] < mn ? key[i] : mn;
-        mx = key[i] > mx ? key[i] : mx;
-      }
-    }
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-      const uint64_t a = __shfl_xor(mn, off, 64), b = __shfl_xor(mx, off, 64);
-      mn = a < mn ? a : mn;
-      mx = b > mx ? b : mx;
-    }
-    if (lane == 0) {
-      s_wmm[2 * wave] = mn;
-      s_wmm[2 * wave + 1] = mx;
-    }
-  }
-  if (tid == 0) {
-    s_misc[0] = 0;
-    s_misc[1] = 0;
-  }
-  __syncthreads();
-  uint64_t kmin = s_wmm[0], kmax = s_wmm[1];
-#pragma unroll
-  for (int w = 1; w < WAVES; ++w) {
-    const uint64_t a = s_wmm[2 * w], b = s_wmm[2 * w + 1];
-    kmin = a < kmin ? a : kmin;
-    kmax = b > kmax ? b : kmax;
-  }
-  if (kmin == kmax) {  // every key equal: copy
+  const int hi = (int)sg.aux;   // the keys agree on every bit of (key - base) at or above hi
+  const uint64_t base = sg.base;
+  if (hi == 0) {  // every key equal: copy
 #pragma unroll
     for (int i = 0; i < MAXK; ++i) {
       const uint32_t p = pw + (uint32_t)i * kWave;
@@ -752,10 +725,16 @@ __global__ __launch_bounds__(THREADS, 4) void ms_local_kernel(MsBufs bf, const M
     dst[tid] = x;
     return false;
   }
-  // ---- 1. bucket ranks: the top SB of the hi bits of (key - min) that may differ
+  // ---- 1. bucket ranks: the top SB of the hi bits of (key - base) that may differ
   //         (fewer than SB: zero-padded, so only some buckets are used)
-  const int hi = 64 - __builtin_clzll(kmax - kmin);
-  auto bucket = [&](uint64_t k) -> uint32_t { return (uint32_t)(((k - kmin) << (64 - hi)) >> (64 - SB)); };
+  auto bucket = [&](uint64_t k) -> uint32_t { return (uint32_t)(((k - base) << (64 - hi)) >> (64 - SB)); };
+#pragma unroll
+  for (int j = 0; j < C::BPT; ++j) s_off[C::BPT * tid + j] = 0;
+  if (tid == 0) {
+    s_misc[0] = 0;
+    s_misc[1] = 0;
+  }
+  __syncthreads();
   uint32_t rk[(MAXK + 1) / 2];  // ranks in the bucket, 16-bit pairs
 #pragma unroll
   for (int i = 0; i < MAXK; i += 2) rk[i / 2] = 0;
@@ -1111,10 +1090,14 @@ struct MetaArena {
   std::vector<std::vector<char>> keep;  // host copies live until the sort returns
 
   static size_t align(size_t x) { return (x + 255) & ~size_t(255); }
+  // A phase reuses the region from offset 0 while the previous phase's kernels may still
+  // read their tables from it (the exact layout's first scatter runs while the next level
+  // is planned): wait for them first.  The uploads are stream-ordered anyway, but
+  // hipMemcpyAsync from pageable memory makes no such promise for every size.
   nut_status begin(size_t total) {
     off = 0;
+    NUT_HIP(hipStreamSynchronize(c->stream));
     if (total > c->sort_meta.bytes) {
-      NUT_HIP(hipStreamSynchronize(c->stream));
       nut_status s = c->sort_meta.reserve(total);
       if (s) return s;
     }
@@ -1248,7 +1231,7 @@ static nut_status device_level(nut_ctx *c, MetaArena &ar, const MsBufs &bf, cons
   hipLaunchKernelGGL(ms_hist_kernel, dim3((unsigned)nht), dim3(MH_THREADS), 0, st, bf, (const MsSeg *)dseg,
                      (const uint32_t *)dtile, dg, flip, dhist, (unsigned long long *)nullptr);
   hipLaunchKernelGGL(ms_plan_kernel, dim3((unsigned)ns), dim3(MS_BINS), 0, st, (const MsSeg *)dseg,
-                     (const unsigned long long *)dhist, dg.shift, dcur, lists, cap, counts);
+                     (const unsigned long long *)dhist, dg.shift, dg.base, dcur, lists, cap, counts);
   NUT_HIP(hipGetLastError());
   hipEvent_t ev = nullptr;
   NUT_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
@@ -1282,14 +1265,14 @@ constexpr uint64_t kCappedMin = 1ull << 25;  // smaller inputs: the exact layout
 
 // The capped layout's key map (MsMap) for keys in [lo, hi] of the flipped key space; false
 // when the span is too narrow for 2^18 cells (the exact layout then runs).
-static bool capped_map(uint64_t lo, uint64_t hi, MsMap &m) {
+static bool capped_map(uint64_t lo, uint64_t hi, MsMap &m) {  // (m.dshift = 9: level 0)
   if (hi < lo || hi - lo < (1ull << 18)) return false;
   const uint64_t span = hi - lo;
   const int bw = 64 - __builtin_clzll(span);
   const int t = bw > 32 ? bw - 32 : 0;
   const uint64_t lim = span >> t;  // < 2^32
   const uint64_t mul = (1ull << 50) / (lim + 1);  // (2^18, 2^32): lim >= 2^18
-  m = MsMap{lo, (uint32_t)mul, (uint32_t)lim, t, 41, true};
+  m = MsMap{lo, (uint32_t)mul, (uint32_t)lim, t, 9, ((lim + 1) << t) - 1};  // (2^64 wraps to ~0)
   return true;
 }
 // host copy of MsMap's cell (level-0 digit * 512 + level-1 digit)
@@ -1372,10 +1355,18 @@ static nut_status msd_sort_capped(nut_ctx *c, const int64_t *in, int64_t *out, u
   uint32_t *dtile;
   uint64_t *dcur0;
   if ((s = ar.upload(one, &dseg)) || (s = ar.upload(tiles, &dtile)) || (s = ar.upload(cur0, &dcur0))) return s;
-  hipLaunchKernelGGL((ms_scatter_kernel<ms_halves(), MsMap>),
-                     dim3((unsigned)std::min<uint64_t>(nt0, (uint64_t)c->num_cus)), dim3(MS_THREADS), 0, st, bf0,
-                     (const MsSeg *)dseg, (const uint32_t *)dtile, (uint32_t)nt0, m0, flip,
-                     (unsigned long long *)dcur0, 2, ocap0, (unsigned long long *)(dcur0 + MS_BINS));
+  // the full 64-bit range maps to the keys' top digits: the shift digits (no range check,
+  // fewer registers) do the same partition
+  const bool ident = m0.base == 0 && m0.t == 32 && m0.mul == (1u << 18);
+  const unsigned g0 = (unsigned)std::min<uint64_t>(nt0, (uint64_t)c->num_cus);
+  if (ident)
+    hipLaunchKernelGGL((ms_scatter_kernel<ms_halves(), MsDigit>), dim3(g0), dim3(MS_THREADS), 0, st, bf0,
+                       (const MsSeg *)dseg, (const uint32_t *)dtile, (uint32_t)nt0, MsDigit{0, 64 - MS_BITS, MS_BINS - 1},
+                       flip, (unsigned long long *)dcur0, 2, ocap0, (unsigned long long *)(dcur0 + MS_BINS));
+  else
+    hipLaunchKernelGGL((ms_scatter_kernel<ms_halves(), MsMap>), dim3(g0), dim3(MS_THREADS), 0, st, bf0,
+                       (const MsSeg *)dseg, (const uint32_t *)dtile, (uint32_t)nt0, m0, flip,
+                       (unsigned long long *)dcur0, 2, ocap0, (unsigned long long *)(dcur0 + MS_BINS));
   NUT_HIP(hipGetLastError());
   std::vector<uint64_t> end0(MS_BINS + 1);
   NUT_HIP(hipMemcpyAsync(end0.data(), dcur0, end0.size() * 8, hipMemcpyDeviceToHost, st));
@@ -1416,14 +1407,20 @@ static nut_status msd_sort_capped(nut_ctx *c, const int64_t *in, int64_t *out, u
   for (auto &f : fb) f = (uint32_t *)ar.alloc((lcap + 1) * 4);
   NUT_HIP(hipMemsetAsync(counts, 0, 16, st));
   MsMap m1 = m0;
-  m1.pshift = 32;
-  m1.check = false;
-  hipLaunchKernelGGL((ms_scatter_kernel<ms_halves(), MsMap>),
-                     dim3((unsigned)std::min<uint64_t>(nt1, (uint64_t)c->num_cus)), dim3(MS_THREADS), 0, st, bf,
-                     (const MsSeg *)dsegs, (const uint32_t *)dt1, (uint32_t)nt1, m1, flip, (unsigned long long *)dcur1,
-                     3, ocap1, (unsigned long long *)(dcur1 + nr));
+  m1.dshift = 0;
+  m1.maxx = ~0ull;  // level 0 checked every key
+  const unsigned g1 = (unsigned)std::min<uint64_t>(nt1, (uint64_t)c->num_cus);
+  if (ident)
+    hipLaunchKernelGGL((ms_scatter_kernel<ms_halves(), MsDigit>), dim3(g1), dim3(MS_THREADS), 0, st, bf,
+                       (const MsSeg *)dsegs, (const uint32_t *)dt1, (uint32_t)nt1,
+                       MsDigit{0, 64 - 2 * MS_BITS, MS_BINS - 1}, flip, (unsigned long long *)dcur1, 3, ocap1,
+                       (unsigned long long *)(dcur1 + nr));
+  else
+    hipLaunchKernelGGL((ms_scatter_kernel<ms_halves(), MsMap>), dim3(g1), dim3(MS_THREADS), 0, st, bf,
+                       (const MsSeg *)dsegs, (const uint32_t *)dt1, (uint32_t)nt1, m1, flip,
+                       (unsigned long long *)dcur1, 3, ocap1, (unsigned long long *)(dcur1 + nr));
   hipLaunchKernelGGL(ms_plan_capped_kernel, dim3(MS_BINS), dim3(MS_BINS), 0, st, (const unsigned long long *)dcur1,
-                     (const uint64_t *)ddb, ocap1, 64, lists, lcap, counts, (unsigned long long *)(dcur1 + nr));
+                     (const uint64_t *)ddb, ocap1, m0, lists, lcap, counts, (unsigned long long *)(dcur1 + nr));
   NUT_HIP(hipGetLastError());
   uint64_t *hc = c->host_pinned;
   NUT_HIP(hipMemcpyAsync(hc, counts, 16, hipMemcpyDeviceToHost, st));
@@ -1536,6 +1533,7 @@ nut_status msd_sort_i64(nut_ctx *c, const int64_t *in, int64_t *out, uint64_t n,
         done.push_back(sg);
       } else if (sg.count <= LS_CAP) {
         sg.aux = (uint32_t)hi;
+        sg.base = dg.base;
         small[local_class(sg.count)].push_back(sg);
       } else {
         next.push_back(sg);

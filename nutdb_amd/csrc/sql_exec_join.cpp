@@ -1,5 +1,7 @@
 // sql_exec_join.cpp — executing JOIN plans: one clause of any type (nut_plan_execute2) and
 // chains (nut_plan_executen), predicate pushdown, gathers into the joined table.
+#include <array>
+
 #include "sql_plan.hpp"
 
 namespace nut {
@@ -441,6 +443,122 @@ nut_status exec_join(nut_ctx *c, const nut_plan &p, const nut_column *lc, int nl
 
 
 
+// The residual step of a correlated EXISTS / NOT EXISTS: the subquery's
+// rows (inner keys bk and the residual's inner column, pushed-down ids applied) are grouped
+// by key with MIN and MAX of that column; each accumulated row looks its key up (a LEFT
+// join on unique keys) and has a qualifying inner row iff the key is present and
+//   inner <> x: min != x or max != x;  < x: min < x;  <= x: min <= x;  > x: max > x;  >= x: max >= x
+// with x its outer column.  Writes the accumulated positions that pass EXISTS (or, anti,
+// NOT EXISTS) to pos[0 .. *m), ascending.
+nut_status residual_semi(nut_ctx *c, const nut_plan &p, int k, int op, const nut_column *icol, const nut_column *ocol,
+                         const int64_t *iids, const int64_t *bk, uint64_t nb, const int64_t *pk, const int64_t *prow,
+                         uint64_t np, int otab, const int64_t *oacc, bool onull, bool anti, int64_t *pos, uint64_t *m) {
+  *m = 0;
+  const std::string who = "subquery " + std::to_string(p.jn[k].scope);
+  if (onull) return fail(NUT_ERR_PLAN, who + ": its outer column comes from a NULL-extended table");
+  (void)otab;
+  auto gather = [&](const void *col, const int64_t *idx, uint64_t n, uint64_t fill, DevBuf &out) -> nut_status {
+    if (out.alloc(c, std::max<uint64_t>(n, 1) * 8) != hipSuccess) return fail(NUT_ERR_OOM, "hipMalloc (EXISTS)");
+    return n ? nut_gather_u64(c, (const uint64_t *)col, idx, n, fill, (uint64_t *)out.p) : NUT_OK;
+  };
+  // 1. MIN / MAX of the inner column per key of the subquery's rows
+  DevBuf icb, gw;
+  const void *ic = icol->data;
+  nut_status st = NUT_OK;
+  if (iids && (st = gather(ic, iids, nb, 0, icb))) return st;
+  if (iids) ic = icb.p;
+  uint64_t G = 0;
+  if (nb) {
+    nut_agg_spec gs;
+    memset(&gs, 0, sizeof gs);
+    gs.n = nb;
+    gs.nkeys = 1;
+    gs.keys[0] = bk;
+    gs.nvals = 1;
+    gs.val_col[0] = ic;
+    gs.val_type[0] = icol->type;
+    gs.naggs = 2;
+    gs.agg_op[0] = NUT_AGG_MIN;
+    gs.agg_op[1] = NUT_AGG_MAX;
+    gs.agg_expr[0] = gs.agg_expr[1] = NUT_EX_COL;
+    nut_groups *g = nullptr;
+    st = nut_groupby(c, &gs, std::max<uint64_t>(1, std::min<uint64_t>(nb / 4, 1ull << 26)), &g);
+    if (!st) st = nut_groups_size(g, &G);
+    if (!st && gw.alloc(c, std::max<uint64_t>(G, 1) * 24) != hipSuccess) st = fail(NUT_ERR_OOM, "hipMalloc (EXISTS)");
+    if (!st && G) st = nut_groups_to_device(g, (uint64_t *)gw.p, G);
+    nut_groups_free(g);
+    if (st) return st;
+  }
+  // 2. each accumulated row's key among the groups' (unique): (probe row, group or -1)
+  DevBuf pr;
+  if (pr.alloc(c, std::max<uint64_t>(np, 1) * 16) != hipSuccess) return fail(NUT_ERR_OOM, "hipMalloc (EXISTS)");
+  int64_t *o0 = (int64_t *)pr.p, *o1 = o0 + std::max<uint64_t>(np, 1);
+  uint64_t m2 = 0;
+  if (np) {
+    if (G) {
+      st = join_i64_into_rows(c, (const int64_t *)gw.p, nullptr, G, pk, prow, np, NUT_JOIN_LEFT, o0, o1, np, &m2);
+    } else {  // no inner row at all: every probe row unmatched
+      st = join_i64_into_rows(c, pk, nullptr, 0, pk, prow, np, NUT_JOIN_LEFT, o0, o1, np, &m2);
+    }
+    if (st) return st;
+    if (m2 != np) return fail(NUT_ERR_UNSUPPORTED, who + ": key lookup returned " + std::to_string(m2) + " rows");
+  }
+  // 3. per row: min, max (0 where unmatched) and the outer value
+  DevBuf mn, mx, orow, ov;
+  if (G && ((st = gather((const uint64_t *)gw.p + G, o1, np, 0, mn)) || (st = gather((const uint64_t *)gw.p + 2 * G, o1, np, 0, mx))))
+    return st;
+  if (!G && (mn.alloc(c, std::max<uint64_t>(np, 1) * 8) != hipSuccess || mx.alloc(c, std::max<uint64_t>(np, 1) * 8) != hipSuccess))
+    return fail(NUT_ERR_OOM, "hipMalloc (EXISTS)");
+  const int64_t *orows = o0;  // accumulated position -> the outer table's row
+  if (oacc) {
+    if ((st = gather(oacc, o0, np, ~0ull, orow))) return st;
+    orows = (const int64_t *)orow.p;
+  }
+  if ((st = gather(ocol->data, orows, np, 0, ov))) return st;
+  // 4. the rows that pass: SEMI (g >= 0) and cond; ANTI its negation
+  nut_plan q;
+  q.compiled = true;
+  q.cols = {"__g", "__mn", "__mx", "__x"};
+  auto col = [](PProg &pp, int ci) {
+    PNode n;
+    n.op = NUT_P_COL;
+    n.col = ci;
+    pp.push_back(n);
+  };
+  PProg &w = q.where;
+  col(w, 0);
+  emit_int(w, 0);
+  emit(w, NUT_P_GE);
+  if (op == NUT_P_NE) {
+    col(w, 1), col(w, 3), emit(w, NUT_P_NE);
+    col(w, 2), col(w, 3), emit(w, NUT_P_NE);
+    emit(w, NUT_P_OR);
+  } else {
+    col(w, op == NUT_P_LT || op == NUT_P_LE ? 1 : 2), col(w, 3), emit(w, op);
+  }
+  emit(w, NUT_P_AND);
+  if (anti) emit(w, NUT_P_NOT);
+  const nut_column qc[4] = {{q.cols[0].c_str(), o1, NUT_T_I64},
+                            {q.cols[1].c_str(), mn.p, icol->type},
+                            {q.cols[2].c_str(), mx.p, icol->type},
+                            {q.cols[3].c_str(), ov.p, ocol->type}};
+  const nut_column *qb[4] = {&qc[0], &qc[1], &qc[2], &qc[3]};
+  const Dict *qd[4] = {nullptr, nullptr, nullptr, nullptr};
+  nut_agg_spec spec;
+  ProgStore store;
+  std::vector<int> agg_f64;
+  if ((st = build_spec(q, qb, qd, np, spec, store, agg_f64))) return st;
+  DevBuf sel;
+  if (sel.alloc(c, std::max<uint64_t>(np, 1) * 8) != hipSuccess) return fail(NUT_ERR_OOM, "hipMalloc (EXISTS)");
+  uint64_t ns = 0;
+  if (np && (st = nut_select_rows(c, &spec, (int64_t *)sel.p, &ns))) return st;
+  // 5. their accumulated positions (the probe rows of step 2, in probe order)
+  if (ns && (st = nut_gather_u64(c, (const uint64_t *)o0, (const int64_t *)sel.p, ns, 0, (uint64_t *)pos))) return st;
+  NUT_HIP(hipStreamSynchronize(c->stream));
+  *m = ns;
+  return NUT_OK;
+}
+
 // A chain of INNER joins (nut_plan_executen): FROM t0 JOIN t1 ON .. JOIN t2 ON ..  Single-
 // table WHERE conjuncts are pushed down per table; the accumulated join result is kept as
 // one row-id array per joined table (the probe side); each step builds on the next table.
@@ -462,14 +580,25 @@ nut_status exec_joinn(nut_ctx *c, const nut_plan &p, const nut_column *const *ta
       if (tabs[t][i].name && ieq(tabs[t][i].name, name)) return &tabs[t][i];
     return nullptr;
   };
+  // scopes: the FROM table and JOIN sources are the outer query's (0); an EXISTS / IN
+  // step's table is its subquery's.  An unqualified name of scope s >= 1 binds to scope s's
+  // table if it has the column, else to the outer tables (a correlation); a scope-0 name
+  // to the outer tables only.  Qualified names bind by qualifier whatever their scope.
+  std::vector<int> tscope(nt, 0);
+  for (int k = 1; k < nt; ++k) tscope[k] = p.jn[k - 1].scope;
   std::vector<int> side(nc);
   std::vector<const nut_column *> src(nc);
   std::vector<const Dict *> sdict(nc + 1, nullptr);
   for (size_t i = 0; i < nc; ++i) {
-    const std::string &nm = p.cols[i];
+    std::string nm;
+    const int sc = name_scope(p.cols[i], &nm);
     int hit = -1, nh = 0;
-    for (int t = 0; t < nt; ++t)
-      if (find(nm, t)) hit = t, ++nh;
+    for (int t = 0; t < nt && sc > 0 && !nh; ++t)
+      if (tscope[t] == sc && find(nm, t)) hit = t, ++nh;
+    for (int t = 0; t < nt && !nh; ++t)
+      if (tscope[t] == 0 && find(nm, t)) hit = t, ++nh;
+    for (int t = hit + 1; t < nt && nh; ++t)
+      if (tscope[t] == 0 && tscope[hit] == 0 && find(nm, t)) ++nh;
     const nut_column *col = hit >= 0 ? find(nm, hit) : nullptr;
     const size_t dot = nm.find('.');
     if (!nh && dot != std::string::npos) {
@@ -483,6 +612,8 @@ nut_status exec_joinn(nut_ctx *c, const nut_plan &p, const nut_column *const *ta
     }
     if (nh > 1) return fail(NUT_ERR_INVALID_ARG, "nut_plan_executen: column '" + nm + "' is in several tables");
     if (!col) return fail(NUT_ERR_INVALID_ARG, "nut_plan_executen: column '" + nm + "' is not bound");
+    if (sc > 0 && tscope[hit] != 0 && tscope[hit] != sc)
+      return fail(NUT_ERR_PLAN, "a subquery reads column '" + nm + "' of another subquery's table");
     if (col->type != NUT_T_I64 && col->type != NUT_T_F64)
       return fail(NUT_ERR_INVALID_ARG, "nut_plan_executen: column '" + nm + "' has an unknown type");
     if (nrows[hit] && !col->data) return fail(NUT_ERR_INVALID_ARG, "nut_plan_executen: column '" + nm + "' is NULL");
@@ -490,9 +621,65 @@ nut_status exec_joinn(nut_ctx *c, const nut_plan &p, const nut_column *const *ta
     src[i] = col;
     if (tdicts && tdicts[hit]) sdict[i] = tdicts[hit][col - tabs[hit]];
   }
+  // EXISTS / IN steps: each conjunct of the subquery's WHERE is a filter of its own table
+  // (pushed down), the correlation equality (EXISTS: the first equality of a column of
+  // its table with an earlier table's int64 column is the key) or the residual: one
+  // comparison `inner <op> outer` (executed through MIN / MAX per key, below)
+  std::vector<std::array<int, 2>> jkey(nt - 1);
+  std::vector<std::vector<PProg>> sub_push(nt);
+  struct Residual {
+    int op = -1, in = -1, out = -1;  // inner <op> outer
+  };
+  std::vector<Residual> res(nt - 1);
+  for (int k = 0; k + 1 < nt; ++k) {
+    const nut_plan::JoinStep &js = p.jn[k];
+    const int t = k + 1;
+    jkey[k] = {js.key[0], js.key[1]};
+    if (!js.scope) continue;
+    std::vector<PProg> conj;
+    split_and(js.cond, conj);
+    for (PProg &cj : conj) {
+      bool inner = false, outer = false, later = false;
+      for (const PNode &nd : cj)
+        if (nd.op == NUT_P_COL || nd.op == P_LIKE || nd.op == P_ILIKE) {
+          inner = inner || side[nd.col] == t;
+          outer = outer || side[nd.col] < t;
+          later = later || side[nd.col] > t;
+        }
+      if (later) return fail(NUT_ERR_PLAN, "subquery " + std::to_string(js.scope) + ": reads a later table");
+      if (!outer) {  // a filter of the subquery's own table (or a constant)
+        sub_push[t].push_back(std::move(cj));
+        continue;
+      }
+      if (!inner)
+        return fail(NUT_ERR_PLAN, "subquery " + std::to_string(js.scope) +
+                                      ": a condition on the outer query's tables alone is not executed inside EXISTS / IN");
+      const bool cmp2 = cj.size() == 3 && cj[0].op == NUT_P_COL && cj[1].op == NUT_P_COL && cj[2].op >= NUT_P_LT &&
+                        cj[2].op <= NUT_P_NE;
+      if (!cmp2)
+        return fail(NUT_ERR_PLAN, "subquery " + std::to_string(js.scope) +
+                                      ": a correlated condition must compare a column of its table with an outer column");
+      int a = cj[0].col, b = cj[1].col, op = cj[2].op;
+      if (side[a] != t) {  // inner on the left: a <op> b
+        std::swap(a, b);
+        op = op == NUT_P_LT ? NUT_P_GT : op == NUT_P_GT ? NUT_P_LT : op == NUT_P_LE ? NUT_P_GE : op == NUT_P_GE ? NUT_P_LE : op;
+      }
+      if (op == NUT_P_EQ && jkey[k][0] < 0 && src[a]->type == NUT_T_I64 && src[b]->type == NUT_T_I64) {
+        jkey[k] = {b, a};
+      } else if (res[k].op < 0 && op != NUT_P_EQ) {
+        res[k] = Residual{op, a, b};
+      } else {
+        return fail(NUT_ERR_PLAN, "subquery " + std::to_string(js.scope) +
+                                      ": one equality with the outer query and at most one other comparison are executed");
+      }
+    }
+    if (jkey[k][0] < 0)
+      return fail(NUT_ERR_PLAN, "EXISTS: the subquery needs an equality between an int64 column of its table and one of "
+                                "the outer query's (an uncorrelated EXISTS is not executed)");
+  }
   std::vector<int> knew(nt - 1), kold(nt - 1);
   for (int k = 0; k + 1 < nt; ++k) {
-    const int a = p.jn[k].key[0], b = p.jn[k].key[1], t = k + 1;
+    const int a = jkey[k][0], b = jkey[k][1], t = k + 1;
     if (side[a] == t && side[b] < t) knew[k] = a, kold[k] = b;
     else if (side[b] == t && side[a] < t) knew[k] = b, kold[k] = a;
     else return fail(NUT_ERR_PLAN, "JOIN " + std::to_string(t) + ": ON must compare a column of '" + tname[t] +
@@ -571,6 +758,8 @@ nut_status exec_joinn(nut_ctx *c, const nut_plan &p, const nut_column *const *ta
     p2.preds.clear();
     for (const PlanPred &pr : p.preds) push[side[pr.col]].push_back(pred_prog(pr));
   }
+  for (int t = 0; t < nt; ++t)
+    for (PProg &cj : sub_push[t]) push[t].push_back(std::move(cj));
   std::vector<DevBuf> ids(nt);
   std::vector<uint64_t> rows(nrows, nrows + nt);
   for (int t = 0; t < nt; ++t) {
@@ -660,7 +849,15 @@ nut_status exec_joinn(nut_ctx *c, const nut_plan &p, const nut_column *const *ta
     DevBuf pairs;
     uint64_t cap = std::max<uint64_t>(right ? rows[t] : np, 1), m = 0, half = 0;
     const uint64_t extra = nnull + (type == PJ_FULL ? rows[t] : 0);  // appended below
-    for (;;) {
+    if (res[k].op >= 0) {  // EXISTS / NOT EXISTS with a residual comparison: positions kept
+      half = cap + extra;
+      if (pairs.alloc(c, half * 16) != hipSuccess) return fail(NUT_ERR_OOM, "hipMalloc (join index)");
+      st = residual_semi(c, p, k, res[k].op, src[res[k].in], src[res[k].out], ids[t].p ? (const int64_t *)ids[t].p : nullptr,
+                         bkd, rows[t], pkd, prow, np, side[res[k].out], accp[side[res[k].out]], cur_null[side[res[k].out]],
+                         type == NUT_JOIN_ANTI, (int64_t *)pairs.p, &m);
+      if (st) break;
+    }
+    for (; res[k].op < 0;) {
       half = cap + extra;
       if (pairs.alloc(c, half * 16) != hipSuccess) return fail(NUT_ERR_OOM, "hipMalloc (join index)");
       int64_t *o0 = (int64_t *)pairs.p, *o1 = o0 + half;

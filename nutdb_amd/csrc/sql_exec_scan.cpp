@@ -35,6 +35,11 @@ double resolve_f64(const CVal &c) { return c.is_int ? (double)c.v : c.dec.to_f64
 const nut_column *bind(const nut_plan &p, int ci, const nut_column *cols, int ncols) {
   for (int i = 0; i < ncols; ++i)
     if (cols[i].name && ieq(cols[i].name, p.cols[ci])) return &cols[i];
+  // a qualified name (a single-table plan's n1.n_name) binds to its bare column otherwise
+  const size_t dot = p.cols[ci].find('.');
+  if (dot != std::string::npos)
+    for (int i = 0; i < ncols; ++i)
+      if (cols[i].name && ieq(cols[i].name, sv(p.cols[ci]).substr(dot + 1))) return &cols[i];
   return nullptr;
 }
 

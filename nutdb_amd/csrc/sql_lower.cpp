@@ -328,15 +328,40 @@ int col_index(nut_plan &p, sv name) {
 // A column reference.  In a JOIN plan a qualified name keeps its qualifier ("o.custkey"):
 // exec_join binds it to the table named or aliased so (and `a.k = b.k` can join two
 // columns of the same name); elsewhere the qualifier is dropped.
+// Inside an EXISTS / IN subquery (p.scope >= 1) an unqualified name is scoped: it binds to
+// the subquery's table first, then to the outer query's (a correlation).
 bool column_ref(nut_plan &p, const Expr &e, sv &name) {
   if (e.k != EK::Identifier || e.id.wildcard) return false;
-  if (p.join >= 0 && e.id.qualified) {
+  if (e.id.qualified && (p.join >= 0 || !(ieq(e.id.qualifier, p.table) || (!p.talias.empty() && ieq(e.id.qualifier, p.talias))))) {
+    // a JOIN plan's qualified name, or a single-table plan's with another qualifier
+    // (n1.n_name of a flat table: bound to a column of that name, else to n_name)
     p.qnames.push_back(std::string(e.id.qualifier) + "." + std::string(e.id.name));
+    name = p.qnames.back();
+  } else if (p.scope > 0) {
+    p.qnames.push_back(scoped_name(p.scope, e.id.name));
     name = p.qnames.back();
   } else {
     name = e.id.name;
   }
   return true;
+}
+
+std::string scoped_name(int scope, sv name) {
+  return "\x1f" + std::to_string(scope) + "\x1f" + std::string(name);
+}
+
+int name_scope(const std::string &name, std::string *bare) {
+  if (name.size() < 3 || name[0] != '\x1f') {
+    if (bare) *bare = name;
+    return 0;
+  }
+  const size_t e = name.find('\x1f', 1);
+  if (e == std::string::npos) {
+    if (bare) *bare = name;
+    return 0;
+  }
+  if (bare) *bare = name.substr(e + 1);
+  return atoi(name.c_str() + 1);
 }
 
 std::string expr_text(const Expr &e) {
@@ -1126,12 +1151,127 @@ bool add_key(nut_plan &p, const Expr &e, Lowering &L) {
   return true;
 }
 
+// ---- EXISTS / NOT EXISTS (subquery), x [NOT] IN (subquery) as SEMI / ANTI join steps
+// (DESIGN.md §3.8).  The reference parses them (TPC-H Q4 / Q16 / Q21 = its fixtures
+// tests/sql/2.sql:9-17, 7.sql:13-20, 8.sql:11-27); this executes the correlated shapes: the
+// subquery reads one table, its WHERE is an AND chain holding one equality with the outer
+// query (EXISTS; for IN, the projected column = x is the key), filters of its own table,
+// and at most one other comparison between its table and the outer query.
+
+// the AND chain's conjuncts, in order
+void and_conjuncts(const Expr &e, std::vector<const Expr *> &out) {
+  if (e.k == EK::BinaryOp && e.bop() == BinOp::And) {
+    and_conjuncts(e.kids[0], out);
+    and_conjuncts(e.kids[1], out);
+  } else {
+    out.push_back(&e);
+  }
+}
+
+// e is `[NOT] EXISTS (subquery)` or `x [NOT] IN (subquery)`: *sq = the subquery expression,
+// *x = the IN operand (NULL for EXISTS), *neg = NOT EXISTS / NOT IN
+bool semi_conjunct(const Expr &e, const Expr **sq, const Expr **x, bool *neg) {
+  bool n = false;
+  const Expr *f = &e;
+  if (f->k == EK::UnaryOp && f->uop() == UnOp::Not) {  // prefix NOT binds to exists(...)
+    n = true;
+    f = &f->kids[0];
+  }
+  if (f->k == EK::FnCall && f->kids.size() == 1 && f->kids[0].k == EK::Subquery &&
+      (f->fn() == FnKind::Exists || f->fn() == FnKind::NotExists || (f->fn() == FnKind::Others && ieq(f->id.name, "exists")))) {
+    *sq = &f->kids[0];
+    *x = nullptr;
+    *neg = n != (f->fn() == FnKind::NotExists);
+    return true;
+  }
+  if (!n && f->k == EK::BinaryOp && (f->bop() == BinOp::In || f->bop() == BinOp::NotIn) && f->kids[1].k == EK::Subquery) {
+    *sq = &f->kids[1];
+    *x = &f->kids[0];
+    *neg = f->bop() == BinOp::NotIn;
+    return true;
+  }
+  return false;
+}
+
+bool lower_semi(nut_plan &p, const Expr &sq, const Expr *x, bool neg, Lowering &L) {
+  const char *what = x ? (neg ? "NOT IN (subquery)" : "IN (subquery)") : (neg ? "NOT EXISTS" : "EXISTS");
+  auto bad = [&](const std::string &m) { return L.fail(std::string(what) + ": " + m); };
+  if (!sq.q || sq.q->is_union) return bad("UNION subqueries are not executed");
+  const QueryBody &b = *sq.q->body;
+  if (b.with || b.distinct || b.group_by || b.having || b.order_by || b.limit)
+    return bad("the subquery may have WHERE only (no WITH / DISTINCT / GROUP BY / HAVING / ORDER BY / LIMIT)");
+  if (!b.from || b.from->k != SourceKind::Table) return bad("the subquery must read one table");
+  if (!b.joins.empty()) return bad("a subquery with JOIN is not executed");
+  for (const QueryExpr &c : b.columns)
+    if (c.e.k == EK::FnCall && c.e.fn() == FnKind::Others && is_agg_name(c.e.id.name))
+      return bad("an aggregate subquery is not a row set");
+  nut_plan::JoinStep js;
+  js.type = neg ? NUT_JOIN_ANTI : NUT_JOIN_SEMI;
+  js.table = std::string(b.from->table);
+  if (b.from->alias) js.alias = std::string(*b.from->alias);
+  int nscope = 1;
+  for (const nut_plan::JoinStep &o : p.jn) nscope = std::max(nscope, o.scope + 1);
+  js.scope = nscope;
+  sv name;
+  if (x) {  // x [NOT] IN (SELECT y FROM t ...): the key pair (x, y)
+    if (b.columns.size() != 1) return bad("the subquery must select one column");
+    if (!column_ref(p, *x, name)) return bad("the IN operand must be a column");
+    js.key[0] = col_index(p, name);
+    p.scope = js.scope;
+    const bool ok = column_ref(p, b.columns[0].e, name);
+    p.scope = 0;
+    if (!ok) return bad("the subquery must select a column");
+    js.key[1] = col_index(p, name);
+  }
+  if (b.where) {
+    bool wb;
+    p.scope = js.scope;
+    const size_t nsubs = p.subs.size();
+    bool ok = true;
+    if (b.where->is_bool_lit(&wb)) {
+      if (!wb) {
+        PNode f;
+        f.op = NUT_P_I64;
+        f.c.v = 0;
+        js.cond.push_back(f);
+      }
+    } else {
+      ok = lower_prog(p, *b.where, js.cond, L);
+    }
+    p.scope = 0;
+    if (!ok) return false;
+    if (p.subs.size() != nsubs) return bad("a scalar subquery inside it is not executed");
+  } else if (!x) {
+    return bad("an uncorrelated EXISTS (no WHERE) is not executed");
+  }
+  p.jn.push_back(std::move(js));
+  return true;
+}
+
 bool lower_mode(const Query &qry, nut_plan &p, Lowering &L) {
   if (qry.is_union) return L.fail("UNION/INTERSECT/EXCEPT are not executed (one query body per plan)");
   const QueryBody &b = *qry.body;
   if (b.with) return L.fail("WITH is not executed");
   if (b.distinct && b.group_by) return L.fail("DISTINCT with GROUP BY is not executed");
   if (!b.from || b.from->k != SourceKind::Table) return L.fail("FROM must name one table");
+  p.table = std::string(b.from->table);
+  if (b.from->alias) p.talias = std::string(*b.from->alias);
+  // EXISTS / IN subqueries among the WHERE conjuncts: SEMI / ANTI steps of a join chain
+  std::vector<const Expr *> wconj;
+  bool has_semi = false;
+  if (b.where) {
+    and_conjuncts(*b.where, wconj);
+    for (const Expr *e : wconj) {
+      const Expr *sq, *x;
+      bool neg;
+      has_semi = has_semi || semi_conjunct(*e, &sq, &x, &neg);
+    }
+  }
+  if (has_semi) {
+    if (!p.compiled) return L.fail("EXISTS / IN (subquery) run in expression mode");
+    if (b.from->alias) p.talias = std::string(*b.from->alias);
+    p.join = NUT_JOIN_INNER;  // a chain (qualified names keep their qualifier from here on)
+  }
   std::vector<std::pair<int, int>> join_extra;  // residual ON equalities (INNER), applied as WHERE terms
   if (b.joins.size() > 1) {  // a chain of INNER / LEFT joins: FROM t0 JOIN t1 ON .. LEFT JOIN t2 ON ..
     p.join = NUT_JOIN_INNER;
@@ -1206,11 +1346,47 @@ bool lower_mode(const Query &qry, nut_plan &p, Lowering &L) {
     p.jkey[0] = eqs[0].first;
     p.jkey[1] = eqs[0].second;
     join_extra.insert(join_extra.end(), eqs.begin() + 1, eqs.end());
+    if (has_semi) {  // the one JOIN becomes the first step of a chain the subqueries extend
+      if (p.jright && p.join != NUT_JOIN_LEFT) return L.fail("RIGHT SEMI / ANTI JOIN with EXISTS / IN subqueries is not executed");
+      if (!p.using_cols.empty()) return L.fail("JOIN ... USING with EXISTS / IN subqueries is not executed (ON a = b)");
+      nut_plan::JoinStep js;
+      js.table = p.jtable;
+      js.alias = p.jalias;
+      js.key[0] = p.jkey[0];
+      js.key[1] = p.jkey[1];
+      js.type = p.jright ? PJ_RIGHT : p.join;
+      p.jn.push_back(js);
+      p.join = NUT_JOIN_INNER;
+      p.jright = false;
+    }
   }
   if (b.having && !b.group_by) return L.fail("HAVING needs GROUP BY");
   p.table = std::string(b.from->table);
   bool wb;
-  if (p.compiled && b.where) {
+  if (has_semi) {  // the other conjuncts form the WHERE (expression mode)
+    std::vector<PProg> cs;
+    for (const Expr *e : wconj) {
+      const Expr *sq, *x;
+      bool neg;
+      if (semi_conjunct(*e, &sq, &x, &neg)) {
+        if (!lower_semi(p, *sq, x, neg, L)) return false;
+        continue;
+      }
+      if (e->is_bool_lit(&wb)) {
+        if (!wb) p.never = true;
+        continue;
+      }
+      PProg c;
+      if (!lower_prog(p, *e, c, L)) return false;
+      cs.push_back(std::move(c));
+    }
+    p.where = and_all(cs);
+    if (p.jn.size() > 15) return L.fail("at most 16 joined tables (JOINs and EXISTS / IN subqueries)");
+    p.jtable = p.jn[0].table;
+    p.jalias = p.jn[0].alias;
+    p.jkey[0] = p.jn[0].key[0];
+    p.jkey[1] = p.jn[0].key[1];
+  } else if (p.compiled && b.where) {
     if (b.where->is_bool_lit(&wb)) {
       if (!wb) p.never = true;
     } else if (!lower_prog(p, *b.where, p.where, L)) {
@@ -1434,7 +1610,210 @@ bool resolve_using(nut_plan &p, Lowering &L) {
   return true;
 }
 
+// ---- derived tables: FROM (SELECT e1 AS a1, ... FROM t [JOIN ..] WHERE w) AS d
+// with a projection-only body (no aggregate, GROUP BY, DISTINCT, ORDER BY or LIMIT) is
+// flattened into the outer query — the shape of the reference's fixture tests/sql/3.sql
+// (TPC-H Q7's `shipping`): every outer reference to a_i (or d.a_i) becomes e_i, the body's
+// FROM / JOINs become the outer FROM / JOINs and its WHERE is ANDed to the outer WHERE.
+Expr clone_expr(const Expr &e);
+std::unique_ptr<Query> clone_query(const Query &q);
+
+QuerySource clone_source(const QuerySource &s) {
+  QuerySource o;
+  o.k = s.k;
+  o.table = s.table;
+  o.e = clone_expr(s.e);
+  o.alias = s.alias;
+  return o;
+}
+
+QueryExpr clone_qexpr(const QueryExpr &q) {
+  QueryExpr o;
+  o.e = clone_expr(q.e);
+  o.alias = q.alias;
+  return o;
+}
+
+std::unique_ptr<Query> clone_query(const Query &q) {
+  auto o = std::make_unique<Query>();
+  o->is_union = q.is_union;
+  o->ut = q.ut;
+  if (q.l) o->l = clone_query(*q.l);
+  if (q.r) o->r = clone_query(*q.r);
+  if (!q.body) return o;
+  const QueryBody &b = *q.body;
+  o->body = std::make_unique<QueryBody>();
+  QueryBody &n = *o->body;
+  if (b.with) {
+    n.with.emplace();
+    for (const CTE &c : *b.with) {
+      CTE x;
+      x.q = c.q ? clone_query(*c.q) : nullptr;
+      x.alias = c.alias;
+      n.with->push_back(std::move(x));
+    }
+  }
+  n.distinct = b.distinct;
+  if (b.distinct_on) {
+    n.distinct_on.emplace();
+    for (const QueryExpr &x : *b.distinct_on) n.distinct_on->push_back(clone_qexpr(x));
+  }
+  for (const QueryExpr &x : b.columns) n.columns.push_back(clone_qexpr(x));
+  if (b.from) n.from = clone_source(*b.from);
+  for (const JoinClause &j : b.joins) {
+    JoinClause x;
+    x.t = j.t;
+    x.src = clone_source(j.src);
+    x.on = j.on;
+    x.cond = clone_expr(j.cond);
+    x.using_ = j.using_;
+    n.joins.push_back(std::move(x));
+  }
+  if (b.where) n.where = clone_expr(*b.where);
+  if (b.group_by) {
+    n.group_by.emplace();
+    for (const QueryExpr &x : *b.group_by) n.group_by->push_back(clone_qexpr(x));
+  }
+  if (b.having) n.having = clone_expr(*b.having);
+  if (b.order_by) {
+    n.order_by.emplace();
+    for (const OrderKey &k : *b.order_by) {
+      OrderKey x;
+      x.e = clone_qexpr(k.e);
+      x.desc = k.desc;
+      n.order_by->push_back(std::move(x));
+    }
+  }
+  n.limit = b.limit;
+  return o;
+}
+
+Expr clone_expr(const Expr &e) {
+  Expr o;
+  o.k = e.k;
+  o.op = e.op;
+  o.id = e.id;
+  o.param = e.param;
+  if (e.lit) o.lit = std::make_unique<Literal>(*e.lit);
+  for (const Expr &k : e.kids) o.kids.push_back(clone_expr(k));
+  if (e.q) o.q = clone_query(*e.q);
+  return o;
+}
+
+// e with every reference to a derived table's output (unqualified, or qualified by its
+// alias d) replaced by the output's expression; subqueries are copied unchanged
+Expr subst_derived(const Expr &e, const std::vector<std::pair<sv, const Expr *>> &outs, std::optional<sv> d) {
+  if (e.k == EK::Identifier && !e.id.wildcard && (!e.id.qualified || (d && ieq(e.id.qualifier, *d))))
+    for (const auto &o : outs)
+      if (ieq(o.first, e.id.name)) return clone_expr(*o.second);
+  if (e.k == EK::Subquery) return clone_expr(e);
+  Expr o;
+  o.k = e.k;
+  o.op = e.op;
+  o.id = e.id;
+  o.param = e.param;
+  if (e.lit) o.lit = std::make_unique<Literal>(*e.lit);
+  for (const Expr &k : e.kids) o.kids.push_back(subst_derived(k, outs, d));
+  return o;
+}
+
+bool flatten_derived(const Query &q, std::unique_ptr<Query> &flat, Lowering &L) {
+  const QueryBody &b = *q.body;
+  const QuerySource &src = *b.from;
+  if (!src.e.q || src.e.q->is_union || !src.e.q->body) return L.fail("derived table: UNION bodies are not executed");
+  const QueryBody &in = *src.e.q->body;
+  if (in.with || in.distinct || in.distinct_on || in.group_by || in.having || in.order_by || in.limit)
+    return L.fail("derived table: only projection bodies (SELECT exprs FROM .. WHERE ..) are flattened");
+  if (!in.from) return L.fail("derived table: its body needs FROM");
+  if (!b.joins.empty() && !in.joins.empty()) return L.fail("derived table with JOINs inside a query with JOINs is not executed");
+  // the body's outputs by name: its alias, or a column's own name
+  std::vector<std::pair<sv, const Expr *>> outs;
+  std::function<bool(const Expr &)> has_agg = [&](const Expr &e) {
+    if (e.k == EK::FnCall && e.fn() == FnKind::Others && is_agg_name(e.id.name)) return true;
+    for (const Expr &k : e.kids)
+      if (has_agg(k)) return true;
+    return false;
+  };
+  for (const QueryExpr &c : in.columns) {
+    if (c.e.k == EK::Identifier && c.e.id.wildcard) return L.fail("derived table: SELECT * inside it is not executed");
+    if (has_agg(c.e)) return L.fail("derived table: aggregates inside it are not executed");
+    if (c.alias)
+      outs.push_back({*c.alias, &c.e});
+    else if (c.e.k == EK::Identifier)
+      outs.push_back({c.e.id.name, &c.e});
+    else
+      return L.fail("derived table: output '" + expr_text(c.e) + "' needs an alias");
+  }
+  flat = std::make_unique<Query>();
+  flat->body = std::make_unique<QueryBody>();
+  QueryBody &n = *flat->body;
+  const std::optional<sv> d = src.alias;
+  n.distinct = b.distinct;
+  for (const QueryExpr &c : b.columns) {
+    if (c.e.k == EK::Identifier && c.e.id.wildcard) return L.fail("derived table: SELECT * over it is not executed");
+    QueryExpr x;
+    x.e = subst_derived(c.e, outs, d);
+    // a bare reference keeps its name as the output's (ORDER BY / result columns use it)
+    x.alias = c.alias ? c.alias : (c.e.k == EK::Identifier ? std::optional<sv>(c.e.id.name) : std::nullopt);
+    n.columns.push_back(std::move(x));
+  }
+  n.from = clone_source(*in.from);
+  for (const JoinClause &j : in.joins.empty() ? b.joins : in.joins) {
+    JoinClause x;
+    x.t = j.t;
+    x.src = clone_source(j.src);
+    x.on = j.on;
+    x.cond = in.joins.empty() ? subst_derived(j.cond, outs, d) : clone_expr(j.cond);
+    x.using_ = j.using_;
+    n.joins.push_back(std::move(x));
+  }
+  if (in.where && b.where) {
+    Expr a;
+    a.k = EK::BinaryOp;
+    a.op = (uint8_t)BinOp::And;
+    a.kids.push_back(clone_expr(*in.where));
+    a.kids.push_back(subst_derived(*b.where, outs, d));
+    n.where = std::move(a);
+  } else if (in.where) {
+    n.where = clone_expr(*in.where);
+  } else if (b.where) {
+    n.where = subst_derived(*b.where, outs, d);
+  }
+  if (b.group_by) {
+    n.group_by.emplace();
+    for (const QueryExpr &k : *b.group_by) {
+      QueryExpr x;
+      x.e = subst_derived(k.e, outs, d);
+      x.alias = k.alias;
+      n.group_by->push_back(std::move(x));
+    }
+  }
+  if (b.having) n.having = subst_derived(*b.having, outs, d);
+  if (b.order_by) {
+    n.order_by.emplace();
+    for (const OrderKey &k : *b.order_by) {
+      OrderKey x;
+      // an output alias of the outer SELECT stays a name (it is matched to an output)
+      bool outer_alias = false;
+      if (k.e.e.k == EK::Identifier && !k.e.e.id.qualified)
+        for (const QueryExpr &c : b.columns)
+          outer_alias = outer_alias || (c.alias && ieq(*c.alias, k.e.e.id.name));
+      x.e.e = outer_alias ? clone_expr(k.e.e) : subst_derived(k.e.e, outs, d);
+      x.e.alias = k.e.alias;
+      x.desc = k.desc;
+      n.order_by->push_back(std::move(x));
+    }
+  }
+  n.limit = b.limit;
+  return true;
+}
+
 bool lower_query(const Query &q, nut_plan &p, Lowering &L) {
+  if (!q.is_union && q.body && q.body->from && q.body->from->k == SourceKind::Subquery) {
+    std::unique_ptr<Query> flat;
+    if (!flatten_derived(q, flat, L)) return false;
+    return lower_query(*flat, p, L);
+  }
   Lowering L1;
   if (lower_mode(q, p, L1)) return resolve_using(p, L);
   // aggregate plans and scans both retry in expression mode
@@ -1477,6 +1856,13 @@ bool scalar_subquery(nut_plan &p, const Expr &e, CVal &c, Lowering &L) {
   return true;
 }
 
+// a plan column's name as describe() shows it (subquery scope n: "sub<n>:name")
+std::string shown(const std::string &name) {
+  std::string bare;
+  const int sc = name_scope(name, &bare);
+  return sc ? "sub" + std::to_string(sc) + ":" + bare : name;
+}
+
 // RPN -> infix text, for describe()
 std::string prog_text(const nut_plan &p, const PProg &pp) {
   static const char *bin[] = {"", "", "", "+", "-", "*", "/", "%", "div", "<", "<=", ">", ">=", "=", "!=",
@@ -1489,8 +1875,8 @@ std::string prog_text(const nut_plan &p, const PProg &pp) {
       return t;
     };
     if (n.op == P_LIKE || n.op == P_ILIKE)
-      st.push_back("(" + p.cols[n.col] + (n.op == P_LIKE ? " like " : " ilike ") + cval_str(n.c) + ")");
-    else if (n.op == NUT_P_COL) st.push_back(p.cols[n.col]);
+      st.push_back("(" + shown(p.cols[n.col]) + (n.op == P_LIKE ? " like " : " ilike ") + cval_str(n.c) + ")");
+    else if (n.op == NUT_P_COL) st.push_back(shown(p.cols[n.col]));
     else if (n.op == NUT_P_I64 || n.op == NUT_P_F64) st.push_back(cval_str(n.c));
     else if (n.op == NUT_P_DATEPART) {
       static const char *dp[] = {"toYear",      "toMonth",     "toDayOfMonth", "toQuarter",
@@ -1523,7 +1909,7 @@ std::string describe(const nut_plan &p) {
   o += ",\"columns\":[";
   for (size_t i = 0; i < p.cols.size(); ++i) {
     if (i) o += ',';
-    json_str(o, p.cols[i]);
+    json_str(o, shown(p.cols[i]));
   }
   o += "],\"never\":";
   o += p.never ? "true" : "false";
@@ -1654,11 +2040,17 @@ std::string describe(const nut_plan &p) {
     o += ',';
     json_str(o, p.jalias);
     o += ']';
-    o += ",\"on\":[";
-    json_str(o, p.cols[p.jkey[0]]);
-    o += ',';
-    json_str(o, p.cols[p.jkey[1]]);
-    o += "]}";
+    o += ",\"on\":";
+    if (p.jkey[0] >= 0) {
+      o += '[';
+      json_str(o, shown(p.cols[p.jkey[0]]));
+      o += ',';
+      json_str(o, shown(p.cols[p.jkey[1]]));
+      o += ']';
+    } else {
+      o += "null";
+    }
+    o += '}';
     if (!p.jn.empty()) {
       o += ",\"joins\":[";
       for (size_t k = 0; k < p.jn.size(); ++k) {
@@ -1669,11 +2061,23 @@ std::string describe(const nut_plan &p) {
         o += ",\"type\":\"";
         o += st[p.jn[k].type];
         o += '"';
-        o += ",\"on\":[";
-        json_str(o, p.cols[p.jn[k].key[0]]);
-        o += ',';
-        json_str(o, p.cols[p.jn[k].key[1]]);
-        o += "]}";
+        o += ",\"on\":";
+        if (p.jn[k].key[0] >= 0) {
+          o += '[';
+          json_str(o, shown(p.cols[p.jn[k].key[0]]));
+          o += ',';
+          json_str(o, shown(p.cols[p.jn[k].key[1]]));
+          o += ']';
+        } else {
+          o += "null";
+        }
+        if (p.jn[k].scope) {
+          o += ",\"subquery\":" + std::to_string(p.jn[k].scope) + ",\"alias\":";
+          json_str(o, p.jn[k].alias);
+          o += ",\"where\":";
+          json_str(o, prog_text(p, p.jn[k].cond));
+        }
+        o += '}';
       }
       o += ']';
     }

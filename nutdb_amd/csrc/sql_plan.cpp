@@ -398,6 +398,9 @@ nut_status nut_table_execute(nut_ctx *c, nut_table *t, const nut_plan *p, uint64
     const TCol *tc = nullptr;
     for (const TCol &x : t->cols)
       if (ieq(x.name, p->cols[i])) tc = &x;
+    const size_t dot = p->cols[i].find('.');  // a qualified name: its bare column otherwise
+    for (const TCol &x : t->cols)
+      if (!tc && dot != std::string::npos && ieq(x.name, sv(p->cols[i]).substr(dot + 1))) tc = &x;
     if (!tc) return fail(NUT_ERR_PLAN, "table '" + t->name + "' has no column '" + p->cols[i] + "'");
     cols[i] = nut_column{tc->name.c_str(), tc->dev, tc->exec_type};
     bound[i] = &cols[i];

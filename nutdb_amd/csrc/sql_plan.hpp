@@ -4,6 +4,7 @@
 #pragma once
 #include <math.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -152,8 +153,16 @@ struct nut_plan {
   // several INNER JoinClauses (nut_plan_executen): table k+1 joins on jn[k].key
   struct JoinStep {
     std::string table, alias;
-    int key[2];
+    int key[2] = {-1, -1};      // plan columns of the ON equality (EXISTS: found at execution)
     int type = NUT_JOIN_INNER;  // NUT_JOIN_INNER / LEFT / SEMI / ANTI, PJ_RIGHT, PJ_FULL
+    // A correlated EXISTS / NOT EXISTS or [NOT] IN (subquery): a SEMI /
+    // ANTI step over the subquery's table.  scope >= 1 names the subquery: its unqualified
+    // names are plan columns of that scope (scoped_name) and bind to its table first.
+    // cond = its WHERE conjuncts, split at execution (when each column's table is known)
+    // into pushed-down filters of the subquery's table, the correlation equality (the
+    // key, EXISTS) and at most one other comparison with the outer query (the residual).
+    int scope = 0;
+    PProg cond;
   };
   std::vector<JoinStep> jn;
   bool jright = false;     // RIGHT OUTER / SEMI / ANTI: the JOIN source is the preserved side
@@ -166,6 +175,7 @@ struct nut_plan {
   // HAVING or used as a value: global-aggregate plans over the same table, executed first;
   // their one value replaces every constant whose param names them (resolve_subqueries)
   std::vector<std::shared_ptr<nut_plan>> subs;
+  int scope = 0;  // lowering state: the EXISTS / IN subquery whose names are being lowered
 };
 
 struct nut_result {
@@ -242,6 +252,12 @@ struct HostStage {
 
 nut_status build_spec(const nut_plan &p, const nut_column *const *bound, const Dict *const *dicts, uint64_t n,
                       nut_agg_spec &s, ProgStore &store, std::vector<int> &agg_f64, GbExtra *gx = nullptr);
+
+// A plan column name inside EXISTS / IN subquery `scope` (>= 1): "\x1f<scope>\x1f<name>",
+// so the same name in the outer query and in a subquery are two plan columns.
+std::string scoped_name(int scope, sv name);
+// the scope and bare name of a plan column name (scope 0: the outer query's)
+int name_scope(const std::string &name, std::string *bare);
 
 // ---- lower
 bool ieq(sv a, sv b);

@@ -18,6 +18,7 @@ this module except ``execute`` runs on the CPU.
 from __future__ import annotations
 
 import ctypes as C
+import re
 import json
 from typing import Dict, List, Optional, Tuple
 
@@ -237,7 +238,8 @@ class Plan:
     def _bind(self, columns):
         import torch
         d = self.describe()
-        names = d["columns"]
+        # a subquery's columns are shown "subN:name" 
+        names = [re.sub(r"^sub\d+:", "", c) for c in d["columns"]]
         star = d.get("column") == "*"  # SELECT *: every column given is projected
         arr = (NutColumn * max(len(columns), 1))()
         keep = []

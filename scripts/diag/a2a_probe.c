@@ -61,7 +61,9 @@ int main(int argc, char **argv) {
   NCCLOK(ncclGetUniqueId(&id));
   ncclComm_t comm;
   NCCLOK(ncclCommInitRank(&comm, 1, id, 0));
-  const double sizes[] = {1e8, 1.5e8, 2e8, 2.5e8, 2.68e8, 2.7e8, 3e8};
+  /* 2^27 words = 2^30 bytes: 1.3e8 (1.040 GB) and 1.342e8 (1.0736 GB) sit just below it,
+   * 1.3422e8 (1.07376 GB) and 1.35e8 just above */
+  const double sizes[] = {1e8, 1.3e8, 1.342e8, 1.3422e8, 1.35e8, 1.5e8, 2e8, 2.7e8};
   const int nsizes = argc > 1 ? atoi(argv[1]) : (int)(sizeof sizes / sizeof sizes[0]);
   const size_t nmax = (size_t)sizes[nsizes - 1];
   uint64_t *send, *recv;
@@ -85,7 +87,7 @@ int main(int argc, char **argv) {
         NCCLOK(ncclRecv(recv, n, ncclUint64, 0, comm, st));
         NCCLOK(ncclGroupEnd());
       } else {
-        const size_t ch = (size_t)1 << 26;
+        const size_t ch = (size_t)1 << 27;  /* 2^30-byte rounds: the largest that stays exact? */
         for (size_t o = 0; o < n; o += ch) {
           size_t cc = n - o < ch ? n - o : ch, d = o;
           NCCLOK(ncclAllToAllv(send, &cc, &d, recv, &cc, &d, ncclUint64, comm, st));
@@ -93,7 +95,7 @@ int main(int argc, char **argv) {
       }
       HIPOK(hipStreamSynchronize(st));
       HIPOK(hipMemcpy(hg, recv, n * 8, hipMemcpyDeviceToHost));
-      report(mode == 0 ? "alltoallv" : mode == 1 ? "send/recv" : "rounds", n, hw, hg);
+      report(mode == 0 ? "alltoallv" : mode == 1 ? "send/recv" : "rounds2^27", n, hw, hg);
     }
   }
   NCCLOK(ncclCommDestroy(comm));

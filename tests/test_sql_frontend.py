@@ -501,7 +501,10 @@ def test_plan_scalar_subqueries():
     ("select x from t where x > (select avg(x) from u)", "over the same table"),
     ("select x from t where x > (select x from t)", "global aggregate with one output"),
     ("select x from t where x > (select k, max(x) from t group by k)", "global aggregate with one output"),
-    ("select x from t where x in (select x from t)", "IN (subquery)"),
+    ("select x from t where x in (select k, x from t)", "must select one column"),
+    ("select x from t where exists (select * from u)", "uncorrelated EXISTS"),
+    ("select x from t where exists (select max(y) from u where y = x)", "aggregate subquery"),
+    ("select x from t where x in (select y from u group by y)", "WHERE only"),
 ])
 def test_plan_scalar_subquery_errors(sql, frag):
     with pytest.raises(NutError) as e:
@@ -533,3 +536,49 @@ def test_plan_lowering_errors(sql, frag):
     with pytest.raises(NutError) as e:
         Plan(sql)
     assert e.value.status == 7 and frag in str(e.value)
+
+
+def _golden(name):
+    from pathlib import Path
+    return (Path(__file__).parent / "golden" / "sql" / name).read_text()
+
+
+def test_plan_exists_in_subqueries():
+    """EXISTS / NOT EXISTS / [NOT] IN (subquery) lower to SEMI / ANTI steps of a join chain
+    (DESIGN.md §3.8): the reference's fixtures 2 (TPC-H Q4), 7 (Q16) and 8 (Q21) as
+    written.  Unqualified names inside a subquery are scoped to it (shown "subN:name");
+    the correlation key is found at execution, when each name's table is known."""
+    d = Plan(_golden("2.sql")).describe()
+    assert d["kind"] == "groupby" and d["mode"] == "compiled"
+    (step,) = d["join"] and d["joins"]
+    assert step["type"] == "semi" and step["table"] == "lineitem" and step["subquery"] == 1 and step["on"] is None
+    assert "sub1:l_orderkey = sub1:o_orderkey" in step["where"] and "sub1:l_commitdate" in step["where"]
+    assert "o_orderdate" in d["columns"] and "o_orderpriority" in d["columns"]
+    d = Plan(_golden("7.sql")).describe()
+    (step,) = d["joins"]
+    assert step["type"] == "anti" and step["on"] == ["ps_suppkey", "sub1:s_suppkey"]
+    assert step["where"] == "(sub1:s_comment like '%Customer%Complaints%')"
+    d = Plan(_golden("8.sql")).describe()
+    assert [(j["type"], j["alias"], j["subquery"]) for j in d["joins"]] == [("semi", "l2", 1), ("anti", "l3", 2)]
+    assert "l2.l_suppkey != l1.l_suppkey" in d["joins"][0]["where"]
+    # IN keeps x as the key's outer side; a JOIN before the subqueries stays the first step
+    d = Plan("select a, count(*) from t join u on t.k = u.k where t.a in (select b from v where c > 1) "
+             "group by a").describe()
+    assert [j["type"] for j in d["joins"]] == ["inner", "semi"]
+    assert d["joins"][1]["on"] == ["t.a", "sub1:b"]
+
+
+def test_plan_derived_table_flattened():
+    """FROM (SELECT e AS a, ... FROM t WHERE w) AS d (fixture 3, TPC-H Q7): every outer
+    reference to a (or d.a) becomes e; qualified names of other tables in a single-table
+    plan keep their qualifier (n1.n_name and n2.n_name stay two columns)."""
+    d = Plan(_golden("3.sql")).describe()
+    assert d["kind"] == "groupby" and d["table"] == "supplier"
+    assert d["keys"] == ["n1.n_name", "n2.n_name", "getYear(l_shipdate)"]
+    assert [o["name"] for o in d["outputs"]] == ["supp_nation", "cust_nation", "l_year", "revenue"]
+    assert d["aggs"] == [{"op": "sum", "expr": "(l_extendedprice * (1 - l_discount))"}]
+    assert "(s_suppkey = l_suppkey)" in d["where_expr"] and "l_shipdate <= 9861" in d["where_expr"]
+    d = Plan("select v, count(*) from (select a + 1 as v, b from t where b > 0) as s where s.v < 10 group by v").describe()
+    assert d["keys"] == ["a + 1"] and "(b > 0)" in d["where_expr"] and "((a + 1) < 10)" in d["where_expr"]
+    with pytest.raises(NutError, match="projection bodies"):
+        Plan("select x from (select k, count(*) as x from t group by k) as s")
