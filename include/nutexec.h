@@ -121,7 +121,8 @@ typedef enum {
   NUT_OPT_PRIV_BLOCKS = 15,    /* compiled Q1 kernel: at most this many workgroups per CU; 0 (default) = 2 */
   NUT_OPT_AGG_BLOCKS = 16,     /* shared-table streaming group-by: at most this many workgroups per CU; 0 (default) = as LDS allows */
   NUT_OPT_SEL_BLOCKS = 17,     /* expression scans (nut_select_rows): persistent workgroups per CU; 0 (default) = 8 */
-  NUT_OPT_COUNT = 18
+  NUT_OPT_SORT_BD = 18,        /* sort, capped scatter levels: threads per workgroup 1024 (0, default) or 512 (two per CU) */
+  NUT_OPT_COUNT = 19
 } nut_option;
 nut_status nut_ctx_set_option(nut_ctx *ctx, int option, int64_t value);
 nut_status nut_ctx_get_option(nut_ctx *ctx, int option, int64_t *value);

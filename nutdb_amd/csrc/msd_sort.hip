@@ -175,17 +175,19 @@ constexpr uint64_t kSkipRun = ~0ull;
 // H = 2: 32 Ki-key tiles (32 keys per lane in registers), staged and written out in two
 // halves of the tile's digit order through the same 16 Ki-key LDS buffer, so each digit's
 // output run per tile is twice as long (512 B instead of 256 B: fewer partial 128-B lines).
-template <int H, class DG>
-__global__ __launch_bounds__(MS_THREADS) void ms_scatter_kernel(MsBufs bf, const MsSeg *__restrict__ segs,
+template <int H, class DG, int T = MS_THREADS>
+__global__ __launch_bounds__(T, 2048 / T) void ms_scatter_kernel(MsBufs bf, const MsSeg *__restrict__ segs,
                                                                    const uint32_t *__restrict__ tile_seg, uint32_t ntiles,
                                                                    DG dg, uint64_t flip,
                                                                    unsigned long long *__restrict__ cursor,
                                                                    int dst_buf = -1, uint64_t ocap = 0,
                                                                    unsigned long long *__restrict__ oflag = nullptr) {
   constexpr int ITEMS = MS_ITEMS * H;
-  constexpr uint32_t TILE = MS_TILE * H;
+  constexpr uint32_t STAGE = (uint32_t)T * MS_ITEMS;  // keys staged in LDS at a time
+  constexpr uint32_t TILE = STAGE * H;
+  static_assert(MS_BINS <= T, "one scan thread per digit");
   static_assert(TILE <= 65536, "16-bit ranks");
-  __shared__ uint64_t s_keys[MS_TILE];
+  __shared__ uint64_t s_keys[STAGE];
   __shared__ uint32_t s_cnt[MS_BINS];
   __shared__ uint32_t s_tex[MS_BINS];
   __shared__ uint64_t s_gb[MS_BINS];
@@ -201,7 +203,7 @@ __global__ __launch_bounds__(MS_THREADS) void ms_scatter_kernel(MsBufs bf, const
     // every load unconditional (clamped to the tile): all ITEMS stay in flight together
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i)
-      key[i] = __builtin_nontemporal_load(sp + min((uint32_t)i * MS_THREADS + tid, cn - 1)) ^ ff;
+      key[i] = __builtin_nontemporal_load(sp + min((uint32_t)i * T + tid, cn - 1)) ^ ff;
   };
   uint32_t s = tile_seg[t];
   MsSeg sg = segs[s];
@@ -220,7 +222,7 @@ __global__ __launch_bounds__(MS_THREADS) void ms_scatter_kernel(MsBufs bf, const
     bool bad = false;  // MsMap level 0: a key outside the mapped span
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i) {
-      const uint32_t idx = (uint32_t)i * MS_THREADS + tid;
+      const uint32_t idx = (uint32_t)i * T + tid;
       if (idx < cnt) {
         rk[i / 2] |= atomicAdd(&s_cnt[dg(key[i])], 1u) << (16 * (i & 1));
         if constexpr (DG::kCheck) bad |= key[i] - dg.base > dg.maxx;
@@ -266,9 +268,9 @@ __global__ __launch_bounds__(MS_THREADS) void ms_scatter_kernel(MsBufs bf, const
       if (h) __syncthreads();  // the previous half's write-out is done with s_keys
 #pragma unroll
       for (int i = 0; i < ITEMS; ++i) {
-        const uint32_t idx = (uint32_t)i * MS_THREADS + tid;
+        const uint32_t idx = (uint32_t)i * T + tid;
         const uint32_t slot = (rk[i / 2] >> (16 * (i & 1))) & 0xFFFFu;
-        if (idx < cnt && (H == 1 || slot / MS_TILE == (uint32_t)h)) s_keys[slot % MS_TILE] = key[i];
+        if (idx < cnt && (H == 1 || slot / STAGE == (uint32_t)h)) s_keys[slot % STAGE] = key[i];
       }
       if (h == H - 1 && next < ntiles) {  // the key registers are free: fetch the next tile now
         nsg = segs[ns];
@@ -279,7 +281,7 @@ __global__ __launch_bounds__(MS_THREADS) void ms_scatter_kernel(MsBufs bf, const
       // registers) above the first store while the next tile's 32 keys are in flight
 #pragma unroll(H == 1 ? MS_ITEMS : 2)
       for (int i = 0; i < MS_ITEMS; ++i) {
-        const uint32_t j = (uint32_t)i * MS_THREADS + tid, jj = j + (uint32_t)h * MS_TILE;
+        const uint32_t j = (uint32_t)i * T + tid, jj = j + (uint32_t)h * STAGE;
         if (jj < cnt) {
           const uint64_t k = s_keys[j];
           const uint64_t g = s_gb[dg(k)];
@@ -1263,6 +1265,26 @@ static nut_status device_level(nut_ctx *c, MetaArena &ar, const MsBufs &bf, cons
 
 constexpr uint64_t kCappedMin = 1ull << 25;  // smaller inputs: the exact layout (its passes are short)
 
+// a capped scatter level at T threads per workgroup (NUT_OPT_SORT_BD: 512 = two per CU)
+template <class DG, int T>
+static void capped_scatter_t(hipStream_t st, unsigned grid, const MsBufs &bf, const MsSeg *segs, const uint32_t *tiles,
+                             uint32_t nt, const DG &dg, uint64_t flip, unsigned long long *cur, int dst_buf,
+                             uint64_t ocap, unsigned long long *oflag) {
+  hipLaunchKernelGGL((ms_scatter_kernel<ms_halves(), DG, T>), dim3(grid), dim3(T), 0, st, bf, segs, tiles, nt, dg, flip,
+                     cur, dst_buf, ocap, oflag);
+}
+template <class DG>
+static void capped_scatter(nut_ctx *c, uint64_t nt, const MsBufs &bf, const MsSeg *segs, const uint32_t *tiles,
+                           const DG &dg, uint64_t flip, unsigned long long *cur, int dst_buf, uint64_t ocap,
+                           unsigned long long *oflag) {
+  const bool half = c->opt[NUT_OPT_SORT_BD] == 512;
+  const unsigned grid = (unsigned)std::min<uint64_t>(nt, (uint64_t)c->num_cus * (half ? 2 : 1));
+  if (half)
+    capped_scatter_t<DG, 512>(c->stream, grid, bf, segs, tiles, (uint32_t)nt, dg, flip, cur, dst_buf, ocap, oflag);
+  else
+    capped_scatter_t<DG, MS_THREADS>(c->stream, grid, bf, segs, tiles, (uint32_t)nt, dg, flip, cur, dst_buf, ocap, oflag);
+}
+
 // The capped layout's key map (MsMap) for keys in [lo, hi] of the flipped key space; false
 // when the span is too narrow for 2^18 cells (the exact layout then runs).
 static bool capped_map(uint64_t lo, uint64_t hi, MsMap &m) {  // (m.dshift = 9: level 0)
@@ -1344,7 +1366,8 @@ static nut_status msd_sort_capped(nut_ctx *c, const int64_t *in, int64_t *out, u
   const MsBufs bf0{(const uint64_t *)in, (uint64_t *)out, (uint64_t *)c->sort_tmp.ptr, nullptr};
   std::vector<MsSeg> one{MsSeg{0, n, 0, 0}};
   std::vector<uint32_t> tiles;
-  const uint64_t nt0 = tile_table(one, MS_TILE * ms_halves(), tiles);
+  const uint32_t stile = (c->opt[NUT_OPT_SORT_BD] == 512 ? 512u : (uint32_t)MS_THREADS) * MS_ITEMS * ms_halves();
+  const uint64_t nt0 = tile_table(one, stile, tiles);
   if (nt0 > 0x7FFFFFFFull) return fail(NUT_ERR_UNSUPPORTED, "nut_sort_i64: too many tiles");
   std::vector<uint64_t> cur0(MS_BINS + 1, 0);
   for (int d = 0; d < MS_BINS; ++d) cur0[d] = (uint64_t)d * ocap0;
@@ -1358,15 +1381,11 @@ static nut_status msd_sort_capped(nut_ctx *c, const int64_t *in, int64_t *out, u
   // the full 64-bit range maps to the keys' top digits: the shift digits (no range check,
   // fewer registers) do the same partition
   const bool ident = m0.base == 0 && m0.t == 32 && m0.mul == (1u << 18);
-  const unsigned g0 = (unsigned)std::min<uint64_t>(nt0, (uint64_t)c->num_cus);
+  unsigned long long *dc0 = (unsigned long long *)dcur0, *of0 = (unsigned long long *)(dcur0 + MS_BINS);
   if (ident)
-    hipLaunchKernelGGL((ms_scatter_kernel<ms_halves(), MsDigit>), dim3(g0), dim3(MS_THREADS), 0, st, bf0,
-                       (const MsSeg *)dseg, (const uint32_t *)dtile, (uint32_t)nt0, MsDigit{0, 64 - MS_BITS, MS_BINS - 1},
-                       flip, (unsigned long long *)dcur0, 2, ocap0, (unsigned long long *)(dcur0 + MS_BINS));
+    capped_scatter(c, nt0, bf0, dseg, dtile, MsDigit{0, 64 - MS_BITS, MS_BINS - 1}, flip, dc0, 2, ocap0, of0);
   else
-    hipLaunchKernelGGL((ms_scatter_kernel<ms_halves(), MsMap>), dim3(g0), dim3(MS_THREADS), 0, st, bf0,
-                       (const MsSeg *)dseg, (const uint32_t *)dtile, (uint32_t)nt0, m0, flip,
-                       (unsigned long long *)dcur0, 2, ocap0, (unsigned long long *)(dcur0 + MS_BINS));
+    capped_scatter(c, nt0, bf0, dseg, dtile, m0, flip, dc0, 2, ocap0, of0);
   NUT_HIP(hipGetLastError());
   std::vector<uint64_t> end0(MS_BINS + 1);
   NUT_HIP(hipMemcpyAsync(end0.data(), dcur0, end0.size() * 8, hipMemcpyDeviceToHost, st));
@@ -1386,7 +1405,7 @@ static nut_status msd_sort_capped(nut_ctx *c, const int64_t *in, int64_t *out, u
   const uint64_t ocap1 = ((cmax / MS_BINS) * 23 / 20 + 64 + 1) & ~1ull;
   if ((s = reserve(c->sort_tmp2, (size_t)MS_BINS * MS_BINS * ocap1 * 8))) return s;
   const MsBufs bf{(const uint64_t *)in, (uint64_t *)out, (uint64_t *)c->sort_tmp.ptr, (uint64_t *)c->sort_tmp2.ptr};
-  const uint64_t nt1 = tile_table(segs, MS_TILE * ms_halves(), tiles);
+  const uint64_t nt1 = tile_table(segs, stile, tiles);
   if (nt1 > 0x7FFFFFFFull) return fail(NUT_ERR_UNSUPPORTED, "nut_sort_i64: too many tiles");
   const uint64_t nr = (uint64_t)MS_BINS * MS_BINS, lcap = nr;
   std::vector<uint64_t> cur1(nr + 1, 0);
@@ -1409,16 +1428,11 @@ static nut_status msd_sort_capped(nut_ctx *c, const int64_t *in, int64_t *out, u
   MsMap m1 = m0;
   m1.dshift = 0;
   m1.maxx = ~0ull;  // level 0 checked every key
-  const unsigned g1 = (unsigned)std::min<uint64_t>(nt1, (uint64_t)c->num_cus);
+  unsigned long long *dc1 = (unsigned long long *)dcur1, *of1 = (unsigned long long *)(dcur1 + nr);
   if (ident)
-    hipLaunchKernelGGL((ms_scatter_kernel<ms_halves(), MsDigit>), dim3(g1), dim3(MS_THREADS), 0, st, bf,
-                       (const MsSeg *)dsegs, (const uint32_t *)dt1, (uint32_t)nt1,
-                       MsDigit{0, 64 - 2 * MS_BITS, MS_BINS - 1}, flip, (unsigned long long *)dcur1, 3, ocap1,
-                       (unsigned long long *)(dcur1 + nr));
+    capped_scatter(c, nt1, bf, dsegs, dt1, MsDigit{0, 64 - 2 * MS_BITS, MS_BINS - 1}, flip, dc1, 3, ocap1, of1);
   else
-    hipLaunchKernelGGL((ms_scatter_kernel<ms_halves(), MsMap>), dim3(g1), dim3(MS_THREADS), 0, st, bf,
-                       (const MsSeg *)dsegs, (const uint32_t *)dt1, (uint32_t)nt1, m1, flip,
-                       (unsigned long long *)dcur1, 3, ocap1, (unsigned long long *)(dcur1 + nr));
+    capped_scatter(c, nt1, bf, dsegs, dt1, m1, flip, dc1, 3, ocap1, of1);
   hipLaunchKernelGGL(ms_plan_capped_kernel, dim3(MS_BINS), dim3(MS_BINS), 0, st, (const unsigned long long *)dcur1,
                      (const uint64_t *)ddb, ocap1, m0, lists, lcap, counts, (unsigned long long *)(dcur1 + nr));
   NUT_HIP(hipGetLastError());

@@ -348,7 +348,7 @@ class Executor:
                "join_region": 5, "join_probe_cfg": 6, "join_any_cfg": 7, "gb_seg_slots": 8,
                "gb_dense": 9, "gb_l1_bits": 10,
                "topk": 11, "gb_l0_bits": 12, "stream_blocks": 13,
-               "priv_bd": 14, "priv_blocks": 15, "agg_blocks": 16, "sel_blocks": 17}
+               "priv_bd": 14, "priv_blocks": 15, "agg_blocks": 16, "sel_blocks": 17, "sort_bd": 18}
 
     def groupby_stats(self) -> dict:
         """The algorithm the last group-by on this context took (nut_ctx_groupby_stats)."""

@@ -80,7 +80,7 @@ static void run(Ctx &c, const char *name, int stop = 0) {
     CK(hipMemset(c.fb, 0, 4));
     CK(hipMemcpyToSymbol(HIP_SYMBOL(nut::g_ms_stamp), st, sizeof(st)));
     CK(hipEventRecord(c.e0));
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(T), 0, 0, bf, (const nut::MsSeg *)c.dseg, c.nseg, 0ull, 0ull, c.fb);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(T), 0, 0, bf, (const nut::MsSeg *)c.dseg, c.nseg, 0ull, c.fb);
     CK(hipEventRecord(c.e1));
     best = std::min(best, elapsed(c.e0, c.e1));
   }
