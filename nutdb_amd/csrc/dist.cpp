@@ -532,11 +532,19 @@ nut_status sort_member(nut_dist *d, int l, const int64_t *in, uint64_t n, const 
   std::vector<int64_t> spl(P - 1, 0);
   for (int i = 1; i < P; ++i) spl[i - 1] = live.empty() ? 0 : live[(live.size() * (size_t)i) / P];
   const SortRanges rg = sort_ranges(spl, live, P);
-  // 2. stable partition into the ranges' buckets (bucket order = destination order)
+  // 2. partition into the ranges' buckets (bucket order = destination order; unstable:
+  //    the receiver sorts, and equal keys split by position are still equal keys)
   const int nb = (int)rg.e.size() + 1;
   std::vector<uint64_t> bcount(nb, 0), counts(P, 0);
-  if (!st) st = reserve(mb, 0, n);
-  if (!st) st = nut_partition_i64(c, in, n, rg.e.data(), nb - 1, (int64_t *)buf(mb, 0), bcount.data());
+  const uint64_t *send = buf(mb, 0);
+  if (nb == 1) {  // one rank: every key stays, in place
+    bcount[0] = n;
+    send = (const uint64_t *)in;
+  } else {
+    if (!st) st = reserve(mb, 0, n);
+    send = buf(mb, 0);
+    if (!st) st = nut::partition_i64_ranges(c, in, n, rg.e.data(), nb - 1, (int64_t *)buf(mb, 0), bcount.data());
+  }
   for (int j = 0; j < nb; ++j) split_bucket(rg, (size_t)j, bcount[j], counts);
   hdr.assign(1 + P, 0);
   for (int q = 0; q < P; ++q) hdr[1 + q] = counts[q];
@@ -552,12 +560,15 @@ nut_status sort_member(nut_dist *d, int l, const int64_t *in, uint64_t n, const 
     rd[q] = rtot;
     rtot += rc[q];
   }
-  st = reserve(mb, 1, rtot);
+  st = P == 1 ? NUT_OK : reserve(mb, 1, rtot);  // (one rank sorts its input in place of a copy)
   if (!st) st = reserve(mb, 2, rtot);
   st = agree(d, l, st);
   // 3. one all-to-all of keys, then the local radix sort of the received range
-  if (!st)
-    st = alltoallv(d, l, buf(mb, 0), sc.data(), sd.data(), buf(mb, 1), rc.data(), rd.data(),
+  const int64_t *sort_in = (const int64_t *)buf(mb, 1);
+  if (P == 1)  // one rank: nothing to exchange, the local sort reads the input
+    sort_in = in;
+  else if (!st)
+    st = alltoallv(d, l, send, sc.data(), sd.data(), buf(mb, 1), rc.data(), rd.data(),
                    max_cell(all, 1 + (size_t)P, 1, P, 1));
   // this rank's key range from its buckets' splitters: the local sort's capped layout
   // spreads exactly that range, not the full 64-bit one
@@ -571,8 +582,7 @@ nut_status sort_member(nut_dist *d, int l, const int64_t *in, uint64_t n, const 
   }
   if (!st && rtot) {
     DeviceGuard dg(c->device);
-    st = nut::msd_sort_i64(c, (const int64_t *)buf(mb, 1), (int64_t *)buf(mb, 2), rtot, kSortFlip,
-                           bnd[0] <= bnd[1] ? bnd : nullptr);
+    st = nut::msd_sort_i64(c, sort_in, (int64_t *)buf(mb, 2), rtot, kSortFlip, bnd[0] <= bnd[1] ? bnd : nullptr);
   }
   if (!st) st = nut_ctx_sync(c);
   if (st) return st;

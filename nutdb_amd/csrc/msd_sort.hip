@@ -82,6 +82,9 @@ struct MsDigit {
   uint32_t mask;
   __device__ __forceinline__ uint32_t operator()(uint64_t k) const { return (uint32_t)((k - base) >> shift) & mask; }
   static constexpr bool kCheck = false;
+  static constexpr int kAux = 0;
+  __device__ __forceinline__ void setup(uint8_t *) const {}
+  __device__ __forceinline__ uint32_t operator()(uint64_t k, const uint8_t *) const { return (*this)(k); }
   uint64_t maxx = ~0ull;
 };
 // The capped layout's digits: keys known (or sampled) to lie in [base,
@@ -95,15 +98,44 @@ struct MsDigit {
 // digit is garbage but whose write stays inside its region: the caller sorts again with the
 // exact layout.  Cell v holds the keys with (k - base) >> t in [ceil(v 2^32 / mul),
 // ceil((v + 1) 2^32 / mul)): ms_plan_capped_kernel gives each cell's segment that base.
+// The sample sort's range partition (dist.cpp): bucket = #{splitters <= key} (signed keys,
+// flip 0), at most 63 splitters in the kernel arguments (a uniform loop of scalar loads).
+// Few buckets would put every key's LDS rank atomic on a handful of counters, so each
+// bucket is split into 2^sbits sub-bins by hashed key bits (bin = bucket << sbits | h):
+// the bins of one bucket stay adjacent, so a bucket is still one contiguous run.
+// The bucket comes from a 4096-entry table over the top 12 bits of the (sign-flipped)
+// key, copied to LDS by the kernel (kAux): a cell no splitter falls in holds one bucket;
+// a cell with splitters inside (flag 0x80) counts the splitters <= key from its first one.
+struct MsSplit {
+  int ns, sbits;
+  int64_t e[63];
+  const uint8_t *tab;  // 4096 cells (device), copied to LDS by setup()
+  static constexpr bool kCheck = false;
+  static constexpr int kAux = 4096;
+  __device__ __forceinline__ void setup(uint8_t *s) const {
+    for (int i = threadIdx.x; i < kAux; i += blockDim.x) s[i] = tab[i];
+  }
+  __device__ __forceinline__ uint32_t operator()(uint64_t k, const uint8_t *lds) const {
+    const uint32_t t = lds[(k ^ 0x8000000000000000ull) >> 52];
+    uint32_t d = t & 63u;
+    if (t & 0x80u)
+      while (d < (uint32_t)ns && (int64_t)k >= e[d]) ++d;
+    const uint32_t h = (uint32_t)(k ^ (k >> 29) ^ (k >> 43));
+    return (d << sbits) | (h & ((1u << sbits) - 1u));
+  }
+};
 struct MsMap {
   uint64_t base;
   uint32_t mul, lim;
   int t, dshift;  // dshift: 9 (level 0) or 0 (level 1)
   uint64_t maxx;  // level 0: ((lim + 1) << t) - 1, the largest k - base in range; level 1: ~0
   static constexpr bool kCheck = true;
+  static constexpr int kAux = 0;
+  __device__ __forceinline__ void setup(uint8_t *) const {}
   __device__ __forceinline__ uint32_t operator()(uint64_t k) const {
     return (__umulhi((uint32_t)((k - base) >> t), mul) >> dshift) & (MS_BINS - 1);
   }
+  __device__ __forceinline__ uint32_t operator()(uint64_t k, const uint8_t *) const { return (*this)(k); }
 };
 
 __device__ __forceinline__ const uint64_t *ms_src(const MsBufs &bf, uint32_t buf) {
@@ -111,12 +143,16 @@ __device__ __forceinline__ const uint64_t *ms_src(const MsBufs &bf, uint32_t buf
 }
 
 // ---------------------------------------------------------------- level histogram
+template <class DG>
 __global__ __launch_bounds__(MH_THREADS) void ms_hist_kernel(MsBufs bf, const MsSeg *__restrict__ segs,
-                                                             const uint32_t *__restrict__ tile_seg, MsDigit dg,
+                                                             const uint32_t *__restrict__ tile_seg, DG dg0,
                                                              uint64_t flip, unsigned long long *__restrict__ hist,
                                                              unsigned long long *__restrict__ minmax) {
   __shared__ uint32_t h[MS_BINS];
+  __shared__ uint8_t s_aux[DG::kAux > 0 ? DG::kAux : 4];
   const int tid = threadIdx.x;
+  dg0.setup(s_aux);
+  auto dg = [&](uint64_t k) { return dg0(k, s_aux); };
   for (int i = tid; i < MS_BINS; i += MH_THREADS) h[i] = 0;
   __syncthreads();
   const uint32_t s = tile_seg[blockIdx.x];
@@ -178,7 +214,7 @@ constexpr uint64_t kSkipRun = ~0ull;
 template <int H, class DG, int T = MS_THREADS>
 __global__ __launch_bounds__(T, 2048 / T) void ms_scatter_kernel(MsBufs bf, const MsSeg *__restrict__ segs,
                                                                    const uint32_t *__restrict__ tile_seg, uint32_t ntiles,
-                                                                   DG dg, uint64_t flip,
+                                                                   DG dg0, uint64_t flip,
                                                                    unsigned long long *__restrict__ cursor,
                                                                    int dst_buf = -1, uint64_t ocap = 0,
                                                                    unsigned long long *__restrict__ oflag = nullptr) {
@@ -192,7 +228,10 @@ __global__ __launch_bounds__(T, 2048 / T) void ms_scatter_kernel(MsBufs bf, cons
   __shared__ uint32_t s_tex[MS_BINS];
   __shared__ uint64_t s_gb[MS_BINS];
   __shared__ uint32_t s_wsum[MS_BINS / kWave];
+  __shared__ uint8_t s_aux[DG::kAux > 0 ? DG::kAux : 4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  dg0.setup(s_aux);  // (visible after the loop's first barrier)
+  auto dg = [&](uint64_t k) { return dg0(k, s_aux); };
   uint32_t t = blockIdx.x;
   uint64_t key[ITEMS];
   auto load = [&](uint32_t tt, const MsSeg g) {
@@ -225,7 +264,7 @@ __global__ __launch_bounds__(T, 2048 / T) void ms_scatter_kernel(MsBufs bf, cons
       const uint32_t idx = (uint32_t)i * T + tid;
       if (idx < cnt) {
         rk[i / 2] |= atomicAdd(&s_cnt[dg(key[i])], 1u) << (16 * (i & 1));
-        if constexpr (DG::kCheck) bad |= key[i] - dg.base > dg.maxx;
+        if constexpr (DG::kCheck) bad |= key[i] - dg0.base > dg0.maxx;
       }
     }
     if constexpr (DG::kCheck)
@@ -1112,6 +1151,8 @@ struct MetaArena {
   }
   template <class T>
   nut_status upload(const std::vector<T> &v, T **dev) {
+    if (off + align(v.size() * sizeof(T)) > c->sort_meta.bytes)  // begin() was sized too small
+      return fail(NUT_ERR_UNSUPPORTED, "nut_sort_i64: device table arena overflow");
     *dev = (T *)alloc(v.size() * sizeof(T));
     if (v.empty()) return NUT_OK;
     keep.emplace_back((const char *)v.data(), (const char *)(v.data() + v.size()));
@@ -1230,7 +1271,7 @@ static nut_status device_level(nut_ctx *c, MetaArena &ar, const MsBufs &bf, cons
   NUT_HIP(hipMemsetAsync(counts, 0, 16, st));
   uint64_t total = 0;
   for (const MsSeg &sg : big) total += sg.count;
-  hipLaunchKernelGGL(ms_hist_kernel, dim3((unsigned)nht), dim3(MH_THREADS), 0, st, bf, (const MsSeg *)dseg,
+  hipLaunchKernelGGL(ms_hist_kernel<MsDigit>, dim3((unsigned)nht), dim3(MH_THREADS), 0, st, bf, (const MsSeg *)dseg,
                      (const uint32_t *)dtile, dg, flip, dhist, (unsigned long long *)nullptr);
   hipLaunchKernelGGL(ms_plan_kernel, dim3((unsigned)ns), dim3(MS_BINS), 0, st, (const MsSeg *)dseg,
                      (const unsigned long long *)dhist, dg.shift, dg.base, dcur, lists, cap, counts);
@@ -1514,7 +1555,7 @@ nut_status msd_sort_i64(nut_ctx *c, const int64_t *in, int64_t *out, uint64_t n,
       NUT_HIP(hipMemcpyAsync(dmm, ar.keep.back().data(), 16, hipMemcpyHostToDevice, st));
     }
     for (const MsSeg &sg : big) c->sort_bytes += 8 * sg.count;
-    hipLaunchKernelGGL(ms_hist_kernel, dim3((unsigned)nht), dim3(MH_THREADS), 0, st, bf, (const MsSeg *)dseg,
+    hipLaunchKernelGGL(ms_hist_kernel<MsDigit>, dim3((unsigned)nht), dim3(MH_THREADS), 0, st, bf, (const MsSeg *)dseg,
                        (const uint32_t *)dtile, dg, flip, dhist, first ? dmm : nullptr);
     NUT_HIP(hipGetLastError());
     hist.resize(big.size() * MS_BINS);
@@ -1631,6 +1672,85 @@ nut_status msd_sort_i64(nut_ctx *c, const int64_t *in, int64_t *out, uint64_t n,
   }
   c->timer.end(st);
   NUT_HIP(hipStreamSynchronize(st));  // host tables in `ar.keep` must outlive the copies
+  return NUT_OK;
+}
+
+// Unstable range partition for the sample sort (dist.cpp sort_member): out holds bucket 0's
+// keys, then bucket 1's, ...; counts_host[b] = bucket b's count.  A 512-bin histogram pass
+// and one scatter level of the MSD sort's kernels (24 B/key; the stable LSD-pass partition,
+// nut_partition_i64, took a look-back chain per tile) — the keys of one bucket may come out
+// in any order: the receiver sorts them, and an equal-key bucket split over ranks by
+// position is split among equal keys.
+nut_status partition_i64_ranges(nut_ctx *c, const int64_t *in, uint64_t n, const int64_t *spl, int ns, int64_t *out,
+                                uint64_t *counts_host) {
+  if (ns < 0 || ns > 63) return fail(NUT_ERR_INVALID_ARG, "partition_i64_ranges: 0..63 splitters");
+  for (int b = 0; b <= ns; ++b) counts_host[b] = 0;
+  if (n == 0) return NUT_OK;
+  DeviceGuard g(c->device);
+  hipStream_t st = c->stream;
+  MsSplit dg;
+  dg.ns = ns;
+  dg.sbits = 0;
+  while ((ns + 1) << (dg.sbits + 1) <= MS_BINS) ++dg.sbits;
+  for (int j = 0; j < 63; ++j) dg.e[j] = j < ns ? spl[j] : INT64_MAX;
+  // cell c holds the flipped keys [c << 52, (c + 1) << 52): its first bucket, and whether
+  // a splitter lies inside it
+  std::vector<uint8_t> tab(MsSplit::kAux);
+  for (int cc = 0, j = 0; cc < MsSplit::kAux; ++cc) {
+    const uint64_t lo = (uint64_t)cc << 52, hi = lo + ((1ull << 52) - 1);
+    while (j < ns && ((uint64_t)spl[j] ^ 0x8000000000000000ull) <= lo) ++j;
+    int j2 = j;
+    while (j2 < ns && ((uint64_t)spl[j2] ^ 0x8000000000000000ull) <= hi) ++j2;
+    tab[cc] = (uint8_t)(j | (j2 > j ? 0x80 : 0));
+  }
+  const MsBufs bf{(const uint64_t *)in, (uint64_t *)out, nullptr, nullptr};
+  std::vector<MsSeg> one{MsSeg{0, n, 0, 0}};
+  std::vector<uint32_t> htiles, stiles;
+  std::vector<MsSeg> sone = one;
+  const uint64_t nht = tile_table(one, MH_HTILE, htiles);
+  const uint64_t nst = tile_table(sone, MS_TILE * ms_halves(), stiles);
+  if (nht > 0x7FFFFFFFull || nst > 0x7FFFFFFFull) return fail(NUT_ERR_UNSUPPORTED, "partition_i64_ranges: too many tiles");
+  MetaArena ar{c};
+  nut_status s = ar.begin(2 * MetaArena::align(sizeof(MsSeg)) + MetaArena::align(htiles.size() * 4) +
+                          MetaArena::align(stiles.size() * 4) + 2 * MetaArena::align(MS_BINS * 8) +
+                          MetaArena::align(MsSplit::kAux));
+  if (s) return s;
+  MsSeg *dseg, *dsseg;
+  uint32_t *dht, *dst;
+  uint8_t *dtab;
+  if ((s = ar.upload(one, &dseg)) || (s = ar.upload(htiles, &dht)) || (s = ar.upload(sone, &dsseg)) ||
+      (s = ar.upload(stiles, &dst)) || (s = ar.upload(tab, &dtab)))
+    return s;
+  dg.tab = dtab;
+  unsigned long long *dhist = (unsigned long long *)ar.alloc(MS_BINS * 8);
+  unsigned long long *dcur = (unsigned long long *)ar.alloc(MS_BINS * 8);
+  c->timer.begin(st, NUT_KERNEL_SORT);
+  NUT_HIP(hipMemsetAsync(dhist, 0, MS_BINS * 8, st));
+  hipLaunchKernelGGL(ms_hist_kernel<MsSplit>, dim3((unsigned)nht), dim3(MH_THREADS), 0, st, bf, (const MsSeg *)dseg,
+                     (const uint32_t *)dht, dg, (uint64_t)0, dhist, (unsigned long long *)nullptr);
+  NUT_HIP(hipGetLastError());
+  uint64_t *hc = c->host_pinned;  // 512 words = the whole 4 KB staging buffer
+  NUT_HIP(hipMemcpyAsync(hc, dhist, MS_BINS * 8, hipMemcpyDeviceToHost, st));
+  NUT_HIP(hipStreamSynchronize(st));
+  std::vector<uint64_t> cur(MS_BINS, 0);
+  uint64_t run = 0;
+  for (int d = 0; d < ((ns + 1) << dg.sbits); ++d) {
+    counts_host[d >> dg.sbits] += hc[d];
+    cur[d] = run;
+    run += hc[d];
+  }
+  if (run != n) {
+    c->timer.end(st);
+    return fail(NUT_ERR_UNSUPPORTED, "partition_i64_ranges: histogram lost keys");
+  }
+  ar.keep.emplace_back((const char *)cur.data(), (const char *)(cur.data() + MS_BINS));
+  NUT_HIP(hipMemcpyAsync(dcur, ar.keep.back().data(), MS_BINS * 8, hipMemcpyHostToDevice, st));
+  hipLaunchKernelGGL((ms_scatter_kernel<ms_halves(), MsSplit>), dim3((unsigned)std::min<uint64_t>(nst, (uint64_t)c->num_cus)),
+                     dim3(MS_THREADS), 0, st, bf, (const MsSeg *)dsseg, (const uint32_t *)dst, (uint32_t)nst, dg,
+                     (uint64_t)0, dcur, 1, (uint64_t)0, (unsigned long long *)nullptr);
+  NUT_HIP(hipGetLastError());
+  c->timer.end(st);
+  NUT_HIP(hipStreamSynchronize(st));  // the host tables of `ar` live until here
   return NUT_OK;
 }
 
