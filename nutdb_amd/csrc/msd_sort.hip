@@ -42,7 +42,7 @@ constexpr uint32_t MH_TILE = 1u << 16;  // keys per copy tile
 constexpr uint32_t MH_HTILE = 1u << 18; // keys per histogram tile (one LDS histogram flush each)
 constexpr int MH_LOADS = 16;            // keys in flight per lane in the histogram loop
 constexpr int MS_THREADS = 1024;
-constexpr int MS_ITEMS = 16;
+constexpr int MS_ITEMS = 14;
 constexpr uint32_t MS_TILE = MS_THREADS * MS_ITEMS;  // 16384 keys per scatter tile
 constexpr int MS_BITS = 9;                          // digit width of a scatter level
 constexpr int MS_BINS = 1 << MS_BITS;               // 512: 32 keys (256 B) per digit per tile
@@ -234,20 +234,33 @@ __global__ __launch_bounds__(T, 2048 / T) void ms_scatter_kernel(MsBufs bf, cons
   auto dg = [&](uint64_t k) { return dg0(k, s_aux); };
   uint32_t t = blockIdx.x;
   uint64_t key[ITEMS];
+  // raw loads: the flip is applied when the tile is ranked, so that a prefetch issued
+  // before the current tile's write-out does not wait for its data there
   auto load = [&](uint32_t tt, const MsSeg g) {
     const uint64_t lo = (uint64_t)(tt - g.aux) * TILE;
     const uint32_t cn = (uint32_t)min<uint64_t>(TILE, g.count - lo);
     const uint64_t *sp = ms_src(bf, g.buf) + g.start + lo;
-    const uint64_t ff = g.buf == 0 ? flip : 0;
+    // an opaque copy of tid: hoisted out of the tile loop, the ITEMS per-item offsets
+    // would pin registers the next tile's keys need (spills that wait for the prefetch)
+    int tq = tid;
+    asm volatile("" : "+v"(tq));
     // every load unconditional (clamped to the tile): all ITEMS stay in flight together
 #pragma unroll
-    for (int i = 0; i < ITEMS; ++i)
-      key[i] = __builtin_nontemporal_load(sp + min((uint32_t)i * T + tid, cn - 1)) ^ ff;
+    for (int i = 0; i < ITEMS; ++i) key[i] = __builtin_nontemporal_load(sp + min((uint32_t)(i * T + tq), cn - 1));
   };
   uint32_t s = tile_seg[t];
   MsSeg sg = segs[s];
   load(t, sg);
   for (;;) {
+    // an opaque copy of tid per tile: tid-derived addresses are recomputed, not pinned in
+    // registers (or spilled) across the loop
+    int tid_ = tid;
+    asm volatile("" : "+v"(tid_));
+    const int tid = tid_;
+    if (sg.buf == 0 && flip) {  // (uniform)
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i) key[i] ^= flip;
+    }
     const uint64_t lo = (uint64_t)(t - sg.aux) * TILE;
     const uint32_t cnt = (uint32_t)min<uint64_t>(TILE, sg.count - lo);
     uint64_t *dst = ms_dst(bf, sg.buf, dst_buf);
@@ -266,6 +279,7 @@ __global__ __launch_bounds__(T, 2048 / T) void ms_scatter_kernel(MsBufs bf, cons
         rk[i / 2] |= atomicAdd(&s_cnt[dg(key[i])], 1u) << (16 * (i & 1));
         if constexpr (DG::kCheck) bad |= key[i] - dg0.base > dg0.maxx;
       }
+      if (i % 8 == 7) __builtin_amdgcn_sched_barrier(0);  // (as in the slot loop below)
     }
     if constexpr (DG::kCheck)
       if (__ballot(bad) && lane == 0) atomicOr(oflag, 1ull);
@@ -300,6 +314,9 @@ __global__ __launch_bounds__(T, 2048 / T) void ms_scatter_kernel(MsBufs bf, cons
       const uint32_t s0 = s_tex[dg(key[i])] + (rk[i / 2] & 0xFFFFu);
       const uint32_t s1 = s_tex[dg(key[i + 1])] + (rk[i / 2] >> 16);
       rk[i / 2] = (s0 & 0xFFFFu) | (s1 << 16);
+      // groups of 8: with all ITEMS LDS reads hoisted together their results, the keys
+      // and the ranks exceed 128 VGPRs, and the spills wait for the next tile's prefetch
+      if (i % 8 == 6) __builtin_amdgcn_sched_barrier(0);
     }
     MsSeg nsg = sg;
 #pragma unroll
@@ -312,6 +329,7 @@ __global__ __launch_bounds__(T, 2048 / T) void ms_scatter_kernel(MsBufs bf, cons
         if (idx < cnt && (H == 1 || slot / STAGE == (uint32_t)h)) s_keys[slot % STAGE] = key[i];
       }
       if (h == H - 1 && next < ntiles) {  // the key registers are free: fetch the next tile now
+        __builtin_amdgcn_sched_barrier(0);  // (not interleaved with the staging: spills)
         nsg = segs[ns];
         load(next, nsg);
       }
@@ -721,8 +739,10 @@ __global__ __launch_bounds__(THREADS, 4) void ms_local_kernel(MsBufs bf, const M
   // Raw loads only: the flip and the padding of positions past the count are applied when
   // the segment is processed (finish_load), so a prefetch does not wait for its data here
   auto load = [&](const MsSeg g) {
+    int tq = tid;  // opaque: the item offsets are recomputed, not kept (or spilled) in registers
+    asm volatile("" : "+v"(tq));
     const uint32_t cc = (uint32_t)g.count, kk = (cc + THREADS - 1) / THREADS;
-    const uint32_t pp = (uint32_t)wave * kWave * kk + lane;
+    const uint32_t pp = (uint32_t)(tq >> 6) * kWave * kk + (tq & 63);
     const uint64_t *sp = ms_src(bf, g.buf) + g.start;
     // unconditional (clamped) loads, so that all MAXK are in flight at once
 #pragma unroll
@@ -742,6 +762,12 @@ __global__ __launch_bounds__(THREADS, 4) void ms_local_kernel(MsBufs bf, const M
   // this one's are staged, so their latency hides behind the window sorts).  Every early
   // return is block-uniform.
   auto process = [&](const uint32_t sidx, const MsSeg sg, const MsSeg nsg, const bool has_next) -> bool {
+  // an opaque copy of tid per segment: tid-derived addresses kept across the loop were
+  // spilled, and a spill reloaded after the prefetch waited for the prefetch (vmcnt is in
+  // order), which made it synchronous
+  int tq = threadIdx.x;
+  asm volatile("" : "+v"(tq));
+  const int tid = tq, lane = tid & 63, wave = tid >> 6;
   MS_STAMP(0);
   finish_load(sg);
   const uint32_t c = (uint32_t)sg.count;
