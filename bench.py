@@ -134,16 +134,17 @@ class GroupBy:
                                group_hint=self.G)
 
     def run(self):
-        g = self.local()
-        n = len(g)
-        if self.out is None or self.out[0].shape[0] < n:
+        # one call, query -> ordered host result (nut_groupby_to_host: at large G the
+        # key-range partitioned path, its transfer overlapped with the work)
+        from nutdb_amd import Agg, AggQuery
+        if self.out is None:
             # the result's host buffers: page-locked, allocated once and refilled every step
             # (fresh pageable arrays cost ~10 ms of first-touch page faults at 1e7 groups)
-            self.out = tuple(torch.empty((max(n, 1), 1), dtype=torch.int64, pin_memory=True).numpy()
-                             for _ in range(2))
-        r = g.to_host_words(out=self.out)  # views of the reused buffers: the last step's result stays
-        g.free()
-        return r
+            rows = max(2 * self.G, 1024)
+            self.out = tuple(torch.empty((rows, 1), dtype=torch.int64, pin_memory=True).numpy() for _ in range(2))
+        q = AggQuery(keys=[self.key], values=[self.val], aggs=[Agg("sum", "col", (0,))])
+        # views of the reused buffers: the last step's result stays
+        return self.ex.groupby_to_host(q, group_hint=self.G, out=self.out)
 
     @staticmethod
     def parity(gpu, cpu):  # dyadic values: the f64 sums are exact, so compare bits

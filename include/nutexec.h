@@ -95,7 +95,8 @@ nut_status nut_ctx_sort_stats(nut_ctx *ctx, uint64_t *bytes, uint32_t *levels);
 typedef enum {
   NUT_GB_ONCHIP = 0,           /* streaming kernel, per-workgroup LDS tables (+ global table) */
   NUT_GB_PARTITIONED_DIRECT = 1, /* key-hash partition of the caller's columns, then LDS tables */
-  NUT_GB_PARTITIONED_SPILL = 2   /* WHERE / expressions staged first, then partitioned */
+  NUT_GB_PARTITIONED_SPILL = 2,  /* WHERE / expressions staged first, then partitioned */
+  NUT_GB_PARTITIONED_ORDERED = 3 /* nut_groupby_to_host: key-range partitions, ordered per partition, streamed to the host */
 } nut_groupby_path;
 nut_status nut_ctx_groupby_stats(nut_ctx *ctx, uint32_t *path, uint32_t *levels, uint32_t *optimistic);
 
@@ -122,7 +123,8 @@ typedef enum {
   NUT_OPT_AGG_BLOCKS = 16,     /* shared-table streaming group-by: at most this many workgroups per CU; 0 (default) = as LDS allows */
   NUT_OPT_SEL_BLOCKS = 17,     /* expression scans (nut_select_rows): persistent workgroups per CU; 0 (default) = 8 */
   NUT_OPT_SORT_BD = 18,        /* sort, capped scatter levels: threads per workgroup 1024 (0, default) or 512 (two per CU) */
-  NUT_OPT_COUNT = 19
+  NUT_OPT_GB_ORDERED = 19,     /* nut_groupby_to_host: the range-partitioned ordered path where it applies (1, default) or the hashed path + ordering (0) */
+  NUT_OPT_COUNT = 20
 } nut_option;
 nut_status nut_ctx_set_option(nut_ctx *ctx, int option, int64_t value);
 nut_status nut_ctx_get_option(nut_ctx *ctx, int option, int64_t *value);
@@ -326,6 +328,16 @@ nut_status nut_groups_to_device(nut_groups *g, uint64_t *out_dev, uint64_t cap);
 nut_status nut_groups_partition(nut_groups *g, int nparts, uint64_t *out_dev, uint64_t cap,
                                 uint64_t *counts_host);
 void nut_groups_free(nut_groups *g);
+/* nut_groupby + nut_groups_to_host + nut_groups_free in one call: the groups sorted
+ * ascending by key into keys[g*nkeys+j] / aggs[g*naggs+a] (cap groups of room), their
+ * number in *n_out (also on NUT_ERR_CAPACITY: the room needed).  For one plain key column
+ * and plain-column aggregates over >= 2^24 rows with group_hint >= ~1.6e6 and page-locked
+ * outputs, the groups are partitioned by key range so that they come out ordered without
+ * a sort, and the result crosses to the host in chunks while the rest is computed
+ * (nut_ctx_groupby_stats: NUT_GB_PARTITIONED_ORDERED); every other case runs the three
+ * calls.  The results are the same either way. */
+nut_status nut_groupby_to_host(nut_ctx *ctx, const nut_agg_spec *spec, uint64_t group_hint, int64_t *keys,
+                               uint64_t *aggs, uint64_t cap, uint64_t *n_out);
 
 /* Convenience forms named in SURVEY.md §8(b). */
 #define NUT_AGGMASK_SUM 1u

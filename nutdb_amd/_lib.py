@@ -171,6 +171,7 @@ SIGNATURES = {
     "nut_groups_to_device": (_I32, [_P, _P, _U64]),
     "nut_groups_partition": (_I32, [_P, _I32, _P, _U64, C.POINTER(_U64)]),
     "nut_groups_free": (None, [_P]),
+    "nut_groupby_to_host": (_I32, [_P, C.POINTER(NutAggSpec), _U64, _P, _P, _U64, C.POINTER(_U64)]),
     "nut_groupby_i64_f64": (_I32, [_P, _P, _P, _U64, C.c_uint32, _U64, C.POINTER(_P)]),
     "nut_q1": (_I32, [_P, _P, _P, _P, _P, _P, _P, _U64, _I64, C.POINTER(_P)]),
     "nut_sort_i64": (_I32, [_P, _P, _P, _U64]),

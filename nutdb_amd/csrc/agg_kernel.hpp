@@ -566,8 +566,8 @@ __global__ __launch_bounds__(BD) void agg_kernel(AggArgs p) {
   // block's rows [seg_off[2b], seg_off[2b+1]), block-stride (row base `rb`).
   uint64_t rb = 0, nrows = p.n, gstride = (uint64_t)gridDim.x * BD, q = (uint64_t)blockIdx.x * BD + threadIdx.x;
   if (p.seg_off) {
-    rb = p.seg_off[2 * blockIdx.x];
-    nrows = p.seg_off[2 * blockIdx.x + 1] - rb;
+    rb = p.seg_end ? p.seg_off[blockIdx.x] : p.seg_off[2 * blockIdx.x];
+    nrows = (p.seg_end ? p.seg_end[blockIdx.x] : p.seg_off[2 * blockIdx.x + 1]) - rb;
     gstride = BD;
     q = threadIdx.x;
   }
@@ -635,6 +635,33 @@ __global__ __launch_bounds__(BD) void agg_kernel(AggArgs p) {
   // merge the block's table into the global table
   const GTable t = *p.gt;
   const uint64_t gstr = t.cap + 1;
+  if (NK == 1 && p.dense && p.dcount) {
+    // dense staging: the block's region of the table, its count for the ordering pass
+    __shared__ uint32_t s_m;
+    if (threadIdx.x == 0) s_m = 0;
+    __syncthreads();
+    const uint64_t base = (p.dbase + blockIdx.x) * p.dregion;
+    for (uint32_t s = threadIdx.x; s < stride; s += BD) {
+      const uint64_t wd = lt.slot[s];
+      const bool occ = s < cap ? wd != kEmpty : lt.ctl[CTL_SPECIAL] != 0u;
+      const uint64_t m = __ballot(occ);
+      uint32_t r = 0;
+      if (m) {
+        const int leader = __builtin_ctzll(m);
+        uint32_t b = 0;
+        if ((threadIdx.x & 63) == (uint32_t)leader) b = atomicAdd(&s_m, (uint32_t)__popcll(m));
+        r = __shfl(b, leader, 64) + lane_rank(m);
+      }
+      if (!occ) continue;
+      t.slot[base + r] = s < cap ? wd : kEmpty;
+#pragma unroll
+      for (int a = 0; a < S::MA; ++a)
+        if (a < na) t.agg[a * gstr + base + r] = lt.agg[a * stride + s];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) p.dcount[blockIdx.x] = s_m;
+    return;
+  }
   if (NK == 1 && p.dense) {
     // the partition's groups are complete and no other block holds them: append them at
     // slots claimed with one global atomic per block (no probing, no atomic merges); the

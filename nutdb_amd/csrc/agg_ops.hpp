@@ -60,9 +60,14 @@ struct AggArgs {
   int32_t sp_map[NUT_MAX_AGGS];
   // Segment mode (seg_off != 0): block b folds rows [seg_off[2b], seg_off[2b+1]) only.
   const uint64_t *seg_off;
+  const uint64_t *seg_end;  // non-null: block b's rows are [seg_off[b], seg_end[b]) instead
   // dense (segment mode, one key, every segment a whole partition): a block's groups are
   // final, so they are appended to the table's first slots instead of hashed into it
   int32_t dense, pad_;
+  // dense staging (the ordered group-by): block b's groups (the empty-marker key's included)
+  // go to table slots [(dbase + b) * dregion, + count) in any order, count to dcount[b]
+  unsigned long long *dcount;
+  uint64_t dregion, dbase;
 };
 
 // ------------------------------------------------------------------ query shapes

@@ -287,9 +287,25 @@ struct LaunchExtra {
   int32_t sp_map[NUT_MAX_AGGS] = {};
   uint64_t blocks = 0, region = 0;         // out (spill): grid and per-block staging region
   const uint64_t *seg_off = nullptr;       // one block per segment: [start, end) pairs, even starts
+  const uint64_t *seg_end = nullptr;       //   or starts in seg_off, ends here (AggArgs::seg_end)
   uint32_t nseg = 0;
   bool dense = false;                      // every segment a whole partition (AggArgs::dense)
+  unsigned long long *dcount = nullptr;    // dense staging (AggArgs::dcount / dregion / dbase)
+  uint64_t dregion = 0, dbase = 0;
 };
+
+// the on-chip table of a launch: 4x the expected groups (load <= 1/4: a key almost always
+// sits in its 4-slot home bucket) within the LDS budget; segment mode: NUT_OPT_GB_SEG_SLOTS x
+// group_hint (already twice a partition's expected groups).  0: hot keys cannot fit on chip
+constexpr size_t kAggLdsMax = 160 * 1024 - 2048;  // the kernel also holds static LDS (spill cursor, histogram)
+uint32_t agg_lcap(nut_ctx *c, int nk, int na, uint64_t group_hint, bool seg) {
+  // (32 slots = 8 buckets x 32 B = one pass over the 64 LDS banks: for <= 8 groups two
+  // home buckets never conflict — distinct buckets hit distinct banks, equal ones broadcast)
+  const uint64_t want = group_hint ? (seg ? (uint64_t)c->opt[NUT_OPT_GB_SEG_SLOTS] * group_hint : 4 * group_hint) : 4096;
+  uint32_t lcap = 32;
+  while (lcap < want && lds_bytes(lcap * 2, nk, na, false, 0, kBdShared) <= kAggLdsMax) lcap *= 2;
+  return group_hint > 8ull * lcap ? 0 : lcap;
+}
 
 // launch the streaming aggregation of spec's rows into g's table.  `kinds` are the
 // per-row update kinds (COUNT partials are merged as integer sums).
@@ -336,19 +352,9 @@ nut_status launch_agg(nut_groups *g, const nut_agg_spec *s, uint64_t group_hint,
   for (int v = 0; v < a.nvals; ++v) bad |= misaligned(a.val_col[v]);
   a.vec = bad ? 0 : 1;  // 8-B aligned columns (e.g. slices) take two 8-B loads per pair
 
-  // on-chip table: 4x the expected groups (load <= 1/4: a key almost always sits in
-  // its 4-slot home bucket) within the LDS budget
-  const size_t lds_max = 160 * 1024 - 2048;  // the kernel also holds static LDS (spill cursor, histogram)
+  const size_t lds_max = kAggLdsMax;
   const int na = s->naggs;
-  // (32 slots = 8 buckets x 32 B = one pass over the 64 LDS banks: for <= 8 groups two
-  // home buckets never conflict — distinct buckets hit distinct banks, equal ones broadcast)
-  // (segment mode: group_hint is already twice a partition's expected groups; the table
-  // size trades LDS occupancy against probe length — NUT_OPT_GB_SEG_SLOTS)
-  uint64_t want = group_hint ? (ex && ex->seg_off ? (uint64_t)c->opt[NUT_OPT_GB_SEG_SLOTS] * group_hint : 4 * group_hint)
-                             : 4096;
-  uint32_t lcap = 32;
-  while (lcap < want && lds_bytes(lcap * 2, g->nk, na, false, 0, kBdShared) <= lds_max) lcap *= 2;
-  if (group_hint > 8ull * lcap) lcap = 0;  // hot keys cannot fit on chip: straight to HBM
+  uint32_t lcap = agg_lcap(c, g->nk, na, group_hint, ex && ex->seg_off);
   if (ex && ex->spill) {
     lcap = 0;
     a.sp_counts = ex->sp_counts;
@@ -385,8 +391,16 @@ nut_status launch_agg(nut_groups *g, const nut_agg_spec *s, uint64_t group_hint,
   if (blocks == 0) blocks = 1;
   if (ex && ex->seg_off) {  // one block per segment (segments start at even rows)
     a.seg_off = ex->seg_off;
+    a.seg_end = ex->seg_end;
     a.dense = ex->dense && g->nk == 1 ? 1 : 0;
     blocks = ex->nseg;
+    if (ex->dcount) {  // dense staging: every region must hold a full block table
+      if (!a.dense || !lcap || ex->dregion < (uint64_t)lcap + 1)
+        return fail(NUT_ERR_INVALID_ARG, "launch_agg: dense staging region smaller than the block table");
+      a.dcount = ex->dcount;
+      a.dregion = ex->dregion;
+      a.dbase = ex->dbase;
+    }
   }
   if (ex && ex->spill) {  // block b stages at most the rows it visits: 2 per pair of its lanes
     a.sp_region = 2ull * bd * ((pairs + blocks * bd - 1) / (blocks * bd));
@@ -510,6 +524,25 @@ uint32_t gp_tiles(std::vector<GpSeg> &segs, uint32_t tile, std::vector<uint32_t>
   return (uint32_t)ts.size();
 }
 
+// the capped scatter launch (no histogram; see gp_level): hash digits, or range digits of
+// one key (rg: GpRange, t >= 0 ... the ordered group-by)
+void gp_capped_launch(nut_ctx *c, const GpArrays &ar, const GpSeg *dseg, const uint32_t *dts, uint32_t nst, int shift,
+                      unsigned long long *dcur, uint64_t kx, uint64_t ovf, unsigned long long *dflag, int bits,
+                      bool two_keys, const GpRange *rg) {
+  if (!nst) return;
+  const unsigned grid = std::min<unsigned>(nst, (unsigned)c->num_cus);
+  using SK = void (*)(GpArrays, const GpSeg *, const uint32_t *, uint32_t, int, int, unsigned long long *, uint64_t,
+                      uint64_t, unsigned long long *, GpRange);
+  static const SK kern[3][3] = {
+      {gp_scatter_kernel<1, 1024, 1, 6>, gp_scatter_kernel<1, 1024, 1, 7>, gp_scatter_kernel<1, 1024, 1, 8>},
+      {gp_scatter_kernel<2, 1024, 1, 6>, gp_scatter_kernel<2, 1024, 1, 7>, gp_scatter_kernel<2, 1024, 1, 8>},
+      {gp_scatter_kernel<1, 1024, 1, 6, true>, gp_scatter_kernel<1, 1024, 1, 7, true>,
+       gp_scatter_kernel<1, 1024, 1, 8, true>}};
+  const int kv = rg ? 2 : two_keys ? 1 : 0;
+  hipLaunchKernelGGL(kern[kv][bits - 6], dim3(grid), dim3(1024), 0, c->stream, ar, dseg, dts, nst, shift, 0, dcur, kx,
+                     ovf, dflag, rg ? *rg : GpRange{});
+}
+
 // one partition level: histogram + scatter of every segment; returns the 256 counts per
 // segment in `hist` (gather mode: one histogram for all segments; `have_hist`: the caller
 // already holds it — the spill pass counts level 0)
@@ -518,7 +551,8 @@ uint32_t gp_tiles(std::vector<GpSeg> &segs, uint32_t tile, std::vector<uint32_t>
 // [start, end) pairs are appended to *parts
 nut_status gp_level(nut_ctx *c, GpMeta &mm, std::vector<GpSeg> &segs, int shift, const uint64_t *const *src,
                     uint64_t *const *dst, int narr, bool gather, bool have_hist, std::vector<uint64_t> &hist,
-                    std::vector<uint64_t> *parts = nullptr, uint64_t kx = 0, uint64_t ovf = 0, int bits = 8) {
+                    std::vector<uint64_t> *parts = nullptr, uint64_t kx = 0, uint64_t ovf = 0, int bits = 8,
+                    const GpRange *rg = nullptr) {
   hipStream_t st = c->stream;
   std::vector<uint32_t> ts;
   nut_status s;
@@ -554,18 +588,9 @@ nut_status gp_level(nut_ctx *c, GpMeta &mm, std::vector<GpSeg> &segs, int shift,
     }
     ar.narr = narr;
     unsigned long long *dflag = (unsigned long long *)dcur + nc;
-    if (nst) {
-      const unsigned grid = std::min<unsigned>(nst, (unsigned)c->num_cus);
-      using SK = void (*)(GpArrays, const GpSeg *, const uint32_t *, uint32_t, int, int, unsigned long long *, uint64_t,
-                          uint64_t, unsigned long long *);
-      static const SK kern[2][3] = {{gp_scatter_kernel<1, 1024, 1, 6>, gp_scatter_kernel<1, 1024, 1, 7>,
-                                     gp_scatter_kernel<1, 1024, 1, 8>},
-                                    {gp_scatter_kernel<2, 1024, 1, 6>, gp_scatter_kernel<2, 1024, 1, 7>,
-                                     gp_scatter_kernel<2, 1024, 1, 8>}};
-      hipLaunchKernelGGL(kern[src[2] ? 1 : 0][bits - 6], dim3(grid), dim3(1024), 0, st, ar, (const GpSeg *)dseg,
-                         (const uint32_t *)dts, nst, shift, 0, (unsigned long long *)dcur, kx, ovf, dflag);
-      NUT_HIP(hipGetLastError());
-    }
+    gp_capped_launch(c, ar, dseg, dts, nst, shift, (unsigned long long *)dcur, kx, ovf, dflag, bits, src[2] != nullptr,
+                     rg);
+    NUT_HIP(hipGetLastError());
     std::vector<uint64_t> back(cur.size());
     NUT_HIP(hipMemcpyAsync(back.data(), dcur, back.size() * 8, hipMemcpyDeviceToHost, st));
     NUT_HIP(hipStreamSynchronize(st));
@@ -633,11 +658,11 @@ nut_status gp_level(nut_ctx *c, GpMeta &mm, std::vector<GpSeg> &segs, int shift,
     if (src[2])
       hipLaunchKernelGGL((gp_scatter_kernel<2, 1024>), dim3(grid), dim3(1024), 0, st, ar, (const GpSeg *)dseg,
                          (const uint32_t *)dts, nst, shift, gather ? 1 : 0, (unsigned long long *)dcur, kx, 0,
-                         (unsigned long long *)nullptr);
+                         (unsigned long long *)nullptr, GpRange{});
     else
       hipLaunchKernelGGL((gp_scatter_kernel<1, 1024>), dim3(grid), dim3(1024), 0, st, ar, (const GpSeg *)dseg,
                          (const uint32_t *)dts, nst, shift, gather ? 1 : 0, (unsigned long long *)dcur, kx, 0,
-                         (unsigned long long *)nullptr);
+                         (unsigned long long *)nullptr, GpRange{});
   }
   NUT_HIP(hipGetLastError());
   return NUT_OK;
@@ -846,6 +871,312 @@ nut_status groupby_partitioned_direct(nut_groups *g, const nut_agg_spec *s, uint
     if (s->agg_op[a] != NUT_AGG_COUNT) s2.agg_arg[a][0] = vmap[s->agg_arg[a][0]];
   }
   return gp_aggregate(g, mm, parts, s2, g->kinds, group_hint);
+}
+
+// ------------------------------------------------------------ ordered group-by (to host)
+// A table for dense staging (AggArgs::dcount): `slots` slots and their aggregate words, no
+// hashing, nothing initialised but the control words.
+nut_status alloc_stage(nut_groups *g, uint64_t slots) {
+  g->ctl_valid = false;
+  size_t off = 0;
+  auto carve = [&](size_t bytes) {
+    size_t o = off;
+    off += (bytes + 255) & ~size_t(255);
+    return o;
+  };
+  const size_t o_slot = carve(slots * 8), o_agg = carve(slots * 8 * (size_t)std::max(g->naggs, 1));
+  const size_t o_ctl = carve(64), o_sh = carve(16 * 4), o_gt = carve(sizeof(GTable)), o_cur = carve(64 * 8),
+               o_seg = carve(128 * 8);
+  if (!(g->mem && g->mem_bytes >= off)) {
+    if (g->mem) (void)hipFree(g->mem);
+    g->mem = nullptr;
+    nut_status ps = pool_take(g->ctx, off, &g->mem, &g->mem_bytes);
+    if (ps) return ps;
+  }
+  char *b = (char *)g->mem;
+  GTable &t = g->gt;
+  memset(&t, 0, sizeof(t));
+  t.slot = (uint64_t *)(b + o_slot);
+  t.agg = (uint64_t *)(b + o_agg);
+  t.ctl = (uint32_t *)(b + o_ctl);
+  t.shard = (uint32_t *)(b + o_sh);
+  t.cap = slots - 1;  // (stride = slots)
+  t.log2cap = ilog2(slots);
+  t.naggs = g->naggs;
+  t.kinds = pack_kinds(g->kinds, g->naggs);
+  g->dev_gt = (GTable *)(b + o_gt);
+  g->dev_cursors = (unsigned long long *)(b + o_cur);
+  g->dev_segbase = (uint64_t *)(b + o_seg);
+  NUT_HIP(hipMemsetAsync(t.ctl, 0, 64, g->ctx->stream));
+  NUT_HIP(hipMemcpyAsync(g->dev_gt, &g->gt, sizeof(GTable), hipMemcpyHostToDevice, g->ctx->stream));
+  return NUT_OK;
+}
+
+bool host_pinned_ptr(const void *p) {
+  hipPointerAttribute_t pa;
+  const bool ok = p && hipPointerGetAttributes(&pa, p) == hipSuccess && pa.type == hipMemoryTypeHost;
+  (void)hipGetLastError();  // pageable memory reports an error here
+  return ok;
+}
+
+// The ordered group-by of config 3's shape at large G (one key, plain columns, no WHERE),
+// straight into page-locked host arrays: the two capped partition levels take RANGE digits
+// (GpRange over a sampled key range, 2^14 cells), so the 16384 final partitions are in key
+// order and every one is final in its workgroup; each workgroup stages its groups, a
+// per-partition pass ranks them by key and writes them to the ordered result at a prefix
+// offset.  Level 1, the aggregation and the ordering run in chunks of level-0 partitions,
+// and each finished chunk crosses to the host on a second stream while the next one is
+// computed (the 16 B/group result at 1e7 groups is ~4.7 ms of PCIe): no device sort, no
+// placement, and most of the transfer hidden.  NUT_ERR_UNSUPPORTED: not this shape, or the
+// keys' spread or a partition overflowed the capped layout — the caller takes the hashed
+// path (the host arrays may hold partial output then; it rewrites them).
+nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hint, int64_t *keys_h, uint64_t *aggs_h,
+                           uint64_t cap, uint64_t *n_out) {
+  const uint64_t n = s->n;
+  const int na = s->naggs;
+  bool shape = s->nkeys == 1 && !s->prog_mode && s->npred == 0 && !s->key_prog[0].n && c->opt[NUT_OPT_GB_ORDERED] != 0 &&
+               c->opt[NUT_OPT_GB_DIRECT] != 0 && c->opt[NUT_OPT_GB_OPTIMISTIC] != 0 && c->opt[NUT_OPT_GB_PARTITION] != 0 &&
+               c->opt[NUT_OPT_GB_LEVELS] != 1 && c->opt[NUT_OPT_GB_DENSE] != 0 && na >= 1 && n >= (1ull << 24) &&
+               n >= 4 * group_hint && host_pinned_ptr(keys_h) && host_pinned_ptr(aggs_h) && cap > 0;
+  for (int a = 0; a < na && shape; ++a) shape = s->agg_op[a] == NUT_AGG_COUNT || s->agg_expr[a] == NUT_EX_COL;
+  constexpr int bits0 = 8, bits1 = 6;
+  const double lam = (double)group_hint / (double)(1 << (bits0 + bits1));
+  if (!shape || lam < 100 || ((uintptr_t)s->keys[0] & 15)) return NUT_ERR_UNSUPPORTED;
+  hipStream_t st = c->stream;
+  // ---- the key range from a strided sample (+ 1/1024 of the span on either side)
+  constexpr uint32_t kSample = 65536;
+  nut_status e = c->misc.reserve(kSample * 8);
+  if (e) return e;
+  hipLaunchKernelGGL(go_sample_kernel, dim3(64), dim3(256), 0, st, s->keys[0], n, kSample, (int64_t *)c->misc.ptr);
+  NUT_HIP(hipGetLastError());
+  std::vector<int64_t> smp(kSample);
+  NUT_HIP(hipMemcpyAsync(smp.data(), c->misc.ptr, kSample * 8, hipMemcpyDeviceToHost, st));
+  NUT_HIP(hipStreamSynchronize(st));
+  const auto mm2 = std::minmax_element(smp.begin(), smp.end());
+  uint64_t lo = (uint64_t)*mm2.first ^ 0x8000000000000000ull, hi = (uint64_t)*mm2.second ^ 0x8000000000000000ull;
+  const uint64_t margin = (hi - lo) >> 10;
+  lo = lo > margin ? lo - margin : 0;
+  hi = hi < ~0ull - margin ? hi + margin : ~0ull;
+  GpRange rg{};
+  rg.lo = lo;
+  rg.span = hi - lo;
+  if (rg.span < (1ull << 16)) return NUT_ERR_UNSUPPORTED;  // (mul must fit 32 bits; tiny spans hash fine)
+  rg.t = rg.span >> 32 ? 32 - __builtin_clzll(rg.span) : 0;
+  rg.mul = (uint32_t)((1ull << 46) / ((rg.span >> rg.t) + 1));
+  // ---- partition buffers: level 0 capped over O (2 x rows per array), level 1 into B2
+  nut_groups *g = new nut_groups();
+  struct Free {
+    nut_groups *g;
+    ~Free() { nut_groups_free(g); }
+  } free_g{g};
+  g->ctx = c;
+  g->nk = 1;
+  g->naggs = na;
+  for (int a = 0; a < na; ++a) g->kinds[a] = kind_of(s, a);
+  int vmap[NUT_MAX_VALS];
+  int nv = 0;
+  for (int j = 0; j < NUT_MAX_VALS; ++j) vmap[j] = -1;
+  for (int a = 0; a < na; ++a)
+    if (s->agg_op[a] != NUT_AGG_COUNT && vmap[s->agg_arg[a][0]] < 0) vmap[s->agg_arg[a][0]] = nv++;
+  const int narr = 3 + nv, nstore = narr - 2;
+  const uint64_t rows = (n + 2 * 65536 + 64 + 31) & ~31ull;
+  const double slack1 = 1.0 + 6.0 / sqrt(lam);
+  const uint64_t b2rows = ((uint64_t)ceil(n * slack1) + (66ull << (bits0 + bits1)) + 2 * GP_TILE + 64 + 31) & ~31ull;
+  e = c->gp_data.reserve((2 * (size_t)nstore * rows + (size_t)nstore * b2rows) * 8 + 256);
+  if (e) return e;
+  uint64_t *O[GP_MAX_ARR] = {}, *B2[GP_MAX_ARR] = {};
+  for (int i = 1, k = 0; i < narr; ++i) {
+    if (i == 2) continue;
+    O[i] = (uint64_t *)c->gp_data.ptr + (size_t)k * 2 * rows;
+    B2[i] = (uint64_t *)c->gp_data.ptr + 2 * (size_t)nstore * rows + (size_t)k * b2rows;
+    ++k;
+  }
+  const uint64_t *src[GP_MAX_ARR] = {};
+  src[1] = (const uint64_t *)s->keys[0];
+  for (int j = 0; j < NUT_MAX_VALS; ++j)
+    if (vmap[j] >= 0) src[3 + vmap[j]] = (const uint64_t *)s->val_col[j];
+  GpMeta mm{c};
+  c->gb_path = NUT_GB_PARTITIONED_ORDERED;
+  c->gb_levels = 2;
+  c->gb_optimistic = 2;
+  // ---- level 0 (range digit = cell >> 6)
+  const uint64_t ocap = ((2 * rows - 2 * GP_TILE) >> bits0) & ~1ull;
+  std::vector<GpSeg> segs{GpSeg{0, n, 0, 0}};
+  segs[0].ocap = ocap;
+  std::vector<uint64_t> hist, p0;
+  c->timer.begin(st, NUT_KERNEL_AGGREGATE);
+  e = gp_level(c, mm, segs, bits1, src, O, narr, false, false, hist, &p0, 0, ocap << bits0, bits0, &rg);
+  c->timer.end(st);
+  if (e) return e == NUT_ERR_CAPACITY ? NUT_ERR_UNSUPPORTED : e;
+  // ---- level-1 regions, as the hashed path sizes them
+  const uint32_t np0 = (uint32_t)(p0.size() / 2), nb1 = 1u << bits1;
+  std::vector<GpSeg> s2;
+  uint64_t ovf1 = 0;
+  for (uint32_t i = 0; i < np0; ++i) {
+    GpSeg sg{p0[2 * i], p0[2 * i + 1] - p0[2 * i], 0, 0};
+    sg.obase = ovf1;
+    sg.ocap = ((uint64_t)ceil((double)sg.count / nb1 * slack1) + 64 + 1) & ~1ull;
+    ovf1 += sg.ocap << bits1;
+    s2.push_back(sg);
+  }
+  if (ovf1 + 2 * GP_TILE > b2rows) return NUT_ERR_UNSUPPORTED;
+  const uint64_t nparts = (uint64_t)np0 * nb1;
+  // chunks of level-0 partitions (in key order) halving in size — 1/2, 1/4, 1/8, 1/16,
+  // 1/16: a chunk's transfer (~0.4x its compute) hides behind the next, smaller chunk, and
+  // only the last 1/16 crosses after the work; each launch costs a tail, so few chunks
+  std::vector<uint32_t> cb{0};
+  for (uint32_t f : {8u, 12u, 14u, 15u, 16u}) {
+    const uint32_t e1 = (uint32_t)((uint64_t)np0 * f / 16);
+    if (e1 > cb.back()) cb.push_back(e1);
+  }
+  const uint32_t nch = (uint32_t)cb.size() - 1;
+  std::vector<uint32_t> tiles, tile0(nch + 1, 0), ntile(nch, 0);
+  for (uint32_t j = 0; j < nch; ++j) {
+    std::vector<GpSeg> sub(s2.begin() + cb[j], s2.begin() + cb[j + 1]);
+    std::vector<uint32_t> ts;
+    ntile[j] = gp_tiles(sub, 2 * GP_TILE, ts);
+    for (uint32_t i = 0; i < sub.size(); ++i) s2[cb[j] + i].tile0 = sub[i].tile0;
+    tile0[j] = (uint32_t)tiles.size();
+    tiles.insert(tiles.end(), ts.begin(), ts.end());
+  }
+  std::vector<uint64_t> init(nparts + nch, 0);  // + one overflow flag per chunk
+  for (uint32_t i = 0; i < np0; ++i)
+    for (uint32_t d = 0; d < nb1; ++d) init[(uint64_t)i * nb1 + d] = s2[i].obase + (uint64_t)d * s2[i].ocap;
+  // the aggregation's table regions: every one holds a full block table (+ the special key)
+  nut_agg_spec s3;
+  memset(&s3, 0, sizeof(s3));
+  s3.n = n;
+  s3.nkeys = 1;
+  s3.keys[0] = (const int64_t *)B2[1];
+  s3.nvals = nv;
+  s3.naggs = na;
+  for (int j = 0; j < NUT_MAX_VALS; ++j)
+    if (vmap[j] >= 0) {
+      s3.val_col[vmap[j]] = B2[3 + vmap[j]];
+      s3.val_type[vmap[j]] = s->val_type[j];
+    }
+  for (int a = 0; a < na; ++a) {
+    s3.agg_op[a] = s->agg_op[a];
+    s3.agg_expr[a] = NUT_EX_COL;
+    if (s->agg_op[a] != NUT_AGG_COUNT) s3.agg_arg[a][0] = vmap[s->agg_arg[a][0]];
+  }
+  const uint64_t per = std::max<uint64_t>(64, 2 * ((group_hint + nparts - 1) / nparts));
+  const uint32_t lcap = agg_lcap(c, 1, na, per, true);
+  if (!lcap) return NUT_ERR_UNSUPPORTED;
+  const uint64_t dregion = (uint64_t)lcap + 1;
+  if (dregion > 4097) return NUT_ERR_UNSUPPORTED;  // (the ordering pass holds a region in LDS, <= 17 keys per thread)
+  e = alloc_stage(g, nparts * dregion);
+  if (e) return e;
+  // device tables, uploaded once
+  GpSeg *dseg;
+  uint32_t *dts;
+  uint64_t *dinit;
+  e = mm.begin(GpMeta::al(s2.size() * sizeof(GpSeg)) + GpMeta::al(tiles.size() * 4 + 1) + GpMeta::al(init.size() * 8) +
+               GpMeta::al(init.size() * 8) + 2 * GpMeta::al(nparts * 8) + GpMeta::al(64));
+  if (e) return e;
+  if ((e = mm.up(s2, &dseg)) || (e = mm.up(tiles, &dts)) || (e = mm.up(init, &dinit))) return e;
+  unsigned long long *dcur = (unsigned long long *)mm.alloc(init.size() * 8);
+  unsigned long long *dcount = (unsigned long long *)mm.alloc(nparts * 8);
+  uint64_t *doffs = (uint64_t *)mm.alloc(nparts * 8);
+  unsigned long long *drun = (unsigned long long *)mm.alloc(64);
+  NUT_HIP(hipMemcpyAsync(dcur, dinit, init.size() * 8, hipMemcpyDeviceToDevice, st));
+  NUT_HIP(hipMemsetAsync(drun, 0, 64, st));
+  // the ordered result on the device (at most one group per row, at most cap)
+  const uint64_t rcap = std::min<uint64_t>(cap, n);
+  if (!c->copy_stream) NUT_HIP(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+  // released on every return, after the copy stream has drained (it reads `res` and
+  // waits on the events)
+  struct Cleanup {
+    hipStream_t st, cs;
+    uint64_t *res = nullptr;
+    std::vector<hipEvent_t> ev;
+    ~Cleanup() {
+      (void)hipStreamSynchronize(cs);
+      for (auto x : ev)
+        if (x) (void)hipEventDestroy(x);
+      if (res) (void)hipFreeAsync(res, st);
+    }
+  } cl{st, c->copy_stream};
+  NUT_HIP(hipMallocAsync((void **)&cl.res, rcap * 8 * (1 + (size_t)na), st));
+  int64_t *rk = (int64_t *)cl.res;
+  uint64_t *ra = cl.res + rcap;
+  std::vector<hipEvent_t> &ev = cl.ev;
+  ev.assign(nch, nullptr);
+  for (auto &x : ev) NUT_HIP(hipEventCreateWithFlags(&x, hipEventDisableTiming));
+  volatile uint64_t *runs = (volatile uint64_t *)c->host_pinned + 64;  // [nch] (pinned: 512 words)
+  NUT_HIP(hipFuncSetAttribute((const void *)go_order_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)go_order_lds(dregion)));
+  GpArrays ar;
+  for (int a = 0; a < GP_MAX_ARR; ++a) {
+    ar.src[a] = O[a];
+    ar.dst[a] = B2[a];
+  }
+  ar.narr = narr;
+  auto enqueue = [&](uint32_t j) -> nut_status {
+    const uint32_t a0 = cb[j], a1 = cb[j + 1];
+    const uint64_t q0 = (uint64_t)a0 * nb1, nq = (uint64_t)(a1 - a0) * nb1;
+    c->timer.begin(st, NUT_KERNEL_AGGREGATE);
+    gp_capped_launch(c, ar, dseg + a0, dts + tile0[j], ntile[j], 0, dcur + q0, 0, ovf1, dcur + nparts + j, bits1, false,
+                     &rg);
+    c->timer.end(st);
+    LaunchExtra sg;  // partition rows [first row, cursor after the scatter)
+    sg.seg_off = dinit + q0;
+    sg.seg_end = (const uint64_t *)dcur + q0;
+    sg.nseg = (uint32_t)nq;
+    sg.dense = true;
+    sg.dcount = dcount + q0;
+    sg.dregion = dregion;
+    sg.dbase = q0;
+    nut_status e2 = launch_agg(g, &s3, per, g->kinds, &sg);
+    if (e2) return e2;
+    c->timer.begin(st, NUT_KERNEL_AGGREGATE);
+    hipLaunchKernelGGL(go_scan_kernel, dim3(1), dim3(1024), 0, st, (const unsigned long long *)dcount + q0, (uint32_t)nq,
+                       doffs + q0, drun);
+    hipLaunchKernelGGL(go_order_kernel, dim3((unsigned)nq), dim3(GO_ORDER_THREADS), (unsigned)go_order_lds(dregion), st,
+                       (const uint64_t *)g->gt.slot, (const uint64_t *)g->gt.agg, g->gt.cap + 1, dregion, q0,
+                       (const unsigned long long *)dcount + q0, (const uint64_t *)doffs + q0, na, g->gt.kinds, rk, ra,
+                       rcap);
+    c->timer.end(st);
+    NUT_HIP(hipGetLastError());
+    NUT_HIP(hipMemcpyAsync((void *)(runs + j), drun, 8, hipMemcpyDeviceToHost, st));
+    NUT_HIP(hipEventRecord(ev[j], st));
+    return NUT_OK;
+  };
+  // two chunks in flight ahead of the host; chunk j crosses on the copy stream once its
+  // count is known
+  constexpr uint32_t kAhead = 2;
+  uint64_t done = 0;  // groups already sent to the host
+  bool over = false;
+  for (uint32_t j = 0; j < std::min(nch, kAhead); ++j)
+    if ((e = enqueue(j))) return e;
+  for (uint32_t j = 0; j < nch; ++j) {
+    NUT_HIP(hipEventSynchronize(ev[j]));
+    const uint64_t total = runs[j];
+    if (j + kAhead < nch && (e = enqueue(j + kAhead))) return e;
+    if (total > rcap) over = true;
+    if (!over && total > done) {
+      NUT_HIP(hipStreamWaitEvent(c->copy_stream, ev[j], 0));
+      NUT_HIP(hipMemcpyAsync(keys_h + done, rk + done, (total - done) * 8, hipMemcpyDeviceToHost, c->copy_stream));
+      NUT_HIP(hipMemcpyAsync(aggs_h + done * na, ra + done * na, (total - done) * 8 * na, hipMemcpyDeviceToHost,
+                             c->copy_stream));
+    }
+    done = total;
+  }
+  // the capped level-1 flags and the aggregation's control words
+  std::vector<uint64_t> flags(nch);
+  NUT_HIP(hipMemcpyAsync(flags.data(), dcur + nparts, nch * 8, hipMemcpyDeviceToHost, st));
+  uint32_t ctl[4];
+  NUT_HIP(hipMemcpyAsync(c->host_pinned, g->gt.ctl, 16, hipMemcpyDeviceToHost, st));
+  NUT_HIP(hipStreamSynchronize(st));
+  memcpy(ctl, c->host_pinned, 16);
+  NUT_HIP(hipStreamSynchronize(c->copy_stream));
+  for (uint64_t f : flags)
+    if (f) return NUT_ERR_UNSUPPORTED;  // a level-1 run outgrew its region
+  if (ctl[1] & 4u) return NUT_ERR_UNSUPPORTED;  // a partition outgrew its block's table
+  *n_out = done;
+  if (over) return fail(NUT_ERR_CAPACITY, "nut_groupby_to_host: capacity " + std::to_string(cap) + " < " +
+                                              std::to_string(done) + " groups");
+  return NUT_OK;
 }
 
 // Spill -> partition -> per-partition aggregation into g's table.  *used = false when the
@@ -1550,6 +1881,29 @@ nut_status nut_groups_to_host(nut_groups *g, int64_t *keys, uint64_t *aggs, uint
     for (int a = 0; a < g->naggs; ++a) aggs[i * g->naggs + a] = h[(size_t)(nk + a) * n + src];
   }
   return NUT_OK;
+}
+
+nut_status nut_groupby_to_host(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hint, int64_t *keys, uint64_t *aggs,
+                               uint64_t cap, uint64_t *n_out) {
+  if (!c || !n_out) return fail(NUT_ERR_INVALID_ARG, "nut_groupby_to_host: NULL argument");
+  *n_out = 0;
+  nut_status st = validate(s);
+  if (st) return st;
+  DeviceGuard dg(c->device);
+  st = groupby_ordered(c, s, group_hint, keys, aggs, cap, n_out);
+  if (st != NUT_ERR_UNSUPPORTED) return st;
+  *n_out = 0;
+  nut_groups *g = nullptr;
+  st = nut_groupby(c, s, group_hint, &g);
+  if (st) return st;
+  uint64_t n = 0;
+  st = nut_groups_size(g, &n);
+  if (!st) {
+    *n_out = n;
+    st = nut_groups_to_host(g, keys, aggs, cap);
+  }
+  nut_groups_free(g);
+  return st;
 }
 
 void nut_groups_free(nut_groups *g) {

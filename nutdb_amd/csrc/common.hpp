@@ -181,6 +181,7 @@ struct nut_ctx {
   char name[64] = {0};
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
+  hipStream_t copy_stream = nullptr;  // device -> host transfers beside the work (nut_groupby_to_host)
   nut::Scratch filter_state;  // tile counter + look-back status words
   nut::Scratch sort_tmp;      // sort ping-pong + histograms
   nut::Scratch sort_tmp2;     // MSD sort, capped layout: the second level's regions
@@ -200,7 +201,7 @@ struct nut_ctx {
   size_t tbl_pool_bytes = 0;            //   hipMalloc / hipFree of a 10^7-group table cost ms
   nut::KernelTimer timer;
   // nut_ctx_set_option (tuning / tests; defaults = the product choice, nut_option order)
-  int64_t opt[NUT_OPT_COUNT] = {-1, 0, 1, 1, 8, 1, 0, 0, 2, 1, 6, 1, 0, 0, 0, 0, 0, 0, 0};
+  int64_t opt[NUT_OPT_COUNT] = {-1, 0, 1, 1, 8, 1, 0, 0, 2, 1, 6, 1, 0, 0, 0, 0, 0, 0, 0, 1};
   uint32_t gb_path = 0, gb_levels = 0, gb_optimistic = 0;  // nut_ctx_groupby_stats
 };
 

@@ -13,6 +13,7 @@
 #pragma once
 
 #include "common.hpp"
+#include "gtable.hpp"
 
 namespace nut {
 
@@ -37,6 +38,23 @@ struct GpArrays {
   const uint64_t *src[GP_MAX_ARR];  // [0] unused, [1] k1, [2] k2 (two keys), values
   uint64_t *dst[GP_MAX_ARR];
   int narr;
+};
+
+// Range digits (the ordered group-by, aggregate.hip groupby_ordered): keys mapped
+// monotonically onto 2^14 cells over a sampled range [lo, lo + span] (signed order; keys
+// outside are clamped to the end cells, so the order holds and only the balance suffers):
+// x = (k ^ 2^63) - lo, clamped to [0, span]; cell = mulhi((x >> t), mul) with mul =
+// floor(2^46 / ((span >> t) + 1)).  Level 0's digit is cell >> 6, level 1's cell & 63, so
+// the partitions are in key order.
+struct GpRange {
+  uint64_t lo, span;
+  uint32_t mul;
+  int t;  // 0 = hash digits (owner_hash)
+  __host__ __device__ __forceinline__ uint32_t cell(uint64_t k) const {
+    uint64_t x = (k ^ 0x8000000000000000ull) - lo;
+    x = (k ^ 0x8000000000000000ull) < lo ? 0 : (x > span ? span : x);
+    return (uint32_t)(((uint64_t)(uint32_t)(x >> t) * mul) >> 32);  // (v_mul_hi_u32)
+  }
 };
 
 // the partition digit: a byte of the key tuple's owner hash (recomputed, never stored);
@@ -92,12 +110,15 @@ __global__ __launch_bounds__(GP_HTHREADS) void gp_hist_kernel(const uint64_t *__
 // stores, bit 2 tile-sequential output, bit 3 sequential output after the scattered address
 // is computed.  The product runs VAR = 1: non-temporal stores measured 7.16-7.24 vs
 // 7.34-7.37 ms per 1e9-record level on two boxes, profiles/r03/gp_tune_*.log)
-template <int NK, int T, int VAR = 1, int BITS = 8>
+// RANGE: digits (rg.cell(k) >> shift) & (BINS - 1) of one key (GpRange) instead of the hash.
+template <int NK, int T, int VAR = 1, int BITS = 8, bool RANGE = false>
 __global__ __launch_bounds__(T) void gp_scatter_kernel(GpArrays ar, const GpSeg *__restrict__ segs,
                                                                 const uint32_t *__restrict__ tile_seg, uint32_t ntiles,
                                                                 int shift, int gather,
                                                                 unsigned long long *__restrict__ cursor, uint64_t kx,
-                                                                uint64_t ovf, unsigned long long *__restrict__ oflag) {
+                                                                uint64_t ovf, unsigned long long *__restrict__ oflag,
+                                                                GpRange rg = GpRange{}) {
+  static_assert(!RANGE || NK == 1, "range digits: one key");
   constexpr uint32_t TILE = T * GP_ITEMS;
   constexpr int BINS = 1 << BITS;  // (the product: GP_BINS = 256)
   static_assert(TILE <= (1u << 24), "slot bits");
@@ -143,7 +164,8 @@ __global__ __launch_bounds__(T) void gp_scatter_kernel(GpArrays ar, const GpSeg 
     uint32_t sd[GP_ITEMS];
 #pragma unroll
     for (int i = 0; i < GP_ITEMS; ++i) {
-      const uint32_t d = (uint32_t)(owner_hash(k1[i] ^ kx, NK == 2 ? k2[i] : 0, NK) >> shift) & (BINS - 1);
+      const uint32_t d = RANGE ? (rg.cell(k1[i]) >> shift) & (BINS - 1)
+                               : (uint32_t)(owner_hash(k1[i] ^ kx, NK == 2 ? k2[i] : 0, NK) >> shift) & (BINS - 1);
       const uint32_t r = (uint32_t)i * T + tid < n ? atomicAdd(&s_cnt[d], 1u) : 0u;
       sd[i] = d | (r << BITS);
     }
@@ -239,6 +261,171 @@ __global__ __launch_bounds__(T) void gp_scatter_kernel(GpArrays ar, const GpSeg 
     t = next;
     lo = nlo;
     n = nn;
+  }
+}
+
+// ---------------------------------------------------------------- ordered group-by
+// (aggregate.hip groupby_ordered: range-partitioned levels, per-partition ordering, the
+// result streamed to the host chunk by chunk)
+
+// m keys at even strides of the column: the sample the range digits are cut from
+__global__ void go_sample_kernel(const int64_t *__restrict__ k, uint64_t n, uint32_t m, int64_t *__restrict__ out) {
+  const uint64_t step = n / m;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) out[i] = k[i * step];
+}
+
+// one workgroup: offs[p] = *run + the groups of the partitions before p (np <= 4096), then
+// *run += all of them
+constexpr int GO_SCAN_PER = 4;
+__global__ __launch_bounds__(1024) void go_scan_kernel(const unsigned long long *__restrict__ cnt, uint32_t np,
+                                                       uint64_t *__restrict__ offs, unsigned long long *__restrict__ run) {
+  __shared__ uint64_t ws[16];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  uint64_t v[GO_SCAN_PER], sum = 0;
+#pragma unroll
+  for (int j = 0; j < GO_SCAN_PER; ++j) {
+    const uint32_t i = (uint32_t)tid * GO_SCAN_PER + j;
+    v[j] = i < np ? cnt[i] : 0;
+    sum += v[j];
+  }
+  uint64_t incl = sum;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint64_t y = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += y;
+  }
+  if (lane == 63) ws[wave] = incl;
+  __syncthreads();
+  uint64_t add = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < 16; ++w) {
+    add += w < wave ? ws[w] : 0;
+    tot += ws[w];
+  }
+  const uint64_t base = *run;
+  uint64_t e = base + add + incl - sum;
+#pragma unroll
+  for (int j = 0; j < GO_SCAN_PER; ++j) {
+    const uint32_t i = (uint32_t)tid * GO_SCAN_PER + j;
+    if (i < np) offs[i] = e;
+    e += v[j];
+  }
+  __syncthreads();  // every thread has read *run
+  if (tid == 0) *run = base + tot;
+}
+
+// one workgroup per partition: its staged groups (unique keys, any order) ordered by key
+// and written to the ordered result at offs[p] + rank: keys rk[pos], aggregate words
+// ra[pos * na + a] (MIN / MAX of f64 back from their ordered encoding).  A counting sort in
+// LDS: each key's bucket is its place in the partition's own [min, max] cut into nb >= n
+// buckets (a monotone map, as the sort's MsMap), ranks in the bucket by LDS atomics, a
+// scan, then a key's rank = its bucket's start + the keys of its bucket that are smaller
+// (~0.6 per bucket: a short loop).  Positions >= cap are not written (the host reports the
+// count).  Dynamic LDS: go_order_lds(dregion).
+constexpr int GO_ORDER_THREADS = 256;
+__host__ __device__ inline uint32_t go_order_nb(uint64_t dregion) {
+  uint32_t nb = GO_ORDER_THREADS;
+  while (nb < dregion) nb *= 2;
+  return nb;
+}
+inline size_t go_order_lds(uint64_t dregion) { return dregion * 12 + (size_t)go_order_nb(dregion) * 4 + 64; }
+__global__ __launch_bounds__(GO_ORDER_THREADS) void go_order_kernel(
+    const uint64_t *__restrict__ slot, const uint64_t *__restrict__ agg, uint64_t gstr, uint64_t dregion,
+    uint64_t dbase, const unsigned long long *__restrict__ cnt, const uint64_t *__restrict__ offs, int na,
+    uint32_t kinds, int64_t *__restrict__ rk, uint64_t *__restrict__ ra, uint64_t cap) {
+  extern __shared__ uint64_t s_u[];  // [dregion] keys (sign-flipped), then [nb] bucket counts, [dregion] members
+  uint32_t *s_b = (uint32_t *)(s_u + dregion);
+  uint32_t *s_m = s_b + go_order_nb(dregion);
+  __shared__ uint64_t s_mn[GO_ORDER_THREADS / 64], s_mx[GO_ORDER_THREADS / 64];
+  __shared__ uint32_t s_ws[GO_ORDER_THREADS / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t p = blockIdx.x, n = (uint32_t)cnt[p];
+  if (n == 0) return;
+  const uint32_t nb = go_order_nb(n);  // buckets: a power of two >= n
+  const uint64_t base = (dbase + p) * dregion;
+  uint64_t mn = ~0ull, mx = 0;
+  for (uint32_t i = tid; i < n; i += GO_ORDER_THREADS) {
+    const uint64_t u = slot[base + i] ^ 0x8000000000000000ull;
+    s_u[i] = u;
+    mn = u < mn ? u : mn;
+    mx = u > mx ? u : mx;
+  }
+  for (uint32_t b = tid; b < nb; b += GO_ORDER_THREADS) s_b[b] = 0;
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const uint64_t a = __shfl_xor(mn, off, 64), b = __shfl_xor(mx, off, 64);
+    mn = a < mn ? a : mn;
+    mx = b > mx ? b : mx;
+  }
+  if (lane == 0) {
+    s_mn[wave] = mn;
+    s_mx[wave] = mx;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int w = 0; w < GO_ORDER_THREADS / 64; ++w) {
+    mn = s_mn[w] < mn ? s_mn[w] : mn;
+    mx = s_mx[w] > mx ? s_mx[w] : mx;
+  }
+  const uint64_t span = mx - mn;
+  const int sh = span >> 32 ? 64 - __clzll((long long)span) - 32 : 0;
+  const uint64_t mulb = ((uint64_t)nb << 32) / ((span >> sh) + 1);  // bucket = ((u - mn) >> sh) * mulb >> 32 < nb
+  auto bucket = [&](uint64_t u) { return (uint32_t)((((u - mn) >> sh) * mulb) >> 32); };
+  // the keys' ranks in their buckets (kept in registers: <= dregion / 256 keys per thread)
+  constexpr int KPT = 17;  // dregion <= 4097 (the host checks)
+  uint32_t r[KPT];
+#pragma unroll
+  for (int j = 0; j < KPT; ++j) {
+    const uint32_t i = tid + j * GO_ORDER_THREADS;
+    r[j] = i < n ? atomicAdd(&s_b[bucket(s_u[i])], 1u) : 0u;
+  }
+  __syncthreads();
+  // bucket counts -> starts (nb / 256 consecutive buckets per thread)
+  const uint32_t per = nb / GO_ORDER_THREADS;
+  uint32_t sum = 0;
+  for (uint32_t b = 0; b < per; ++b) sum += s_b[tid * per + b];
+  uint32_t incl = sum;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t y = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += y;
+  }
+  if (lane == 63) s_ws[wave] = incl;
+  __syncthreads();
+  uint32_t e = incl - sum;
+#pragma unroll
+  for (int w = 0; w < GO_ORDER_THREADS / 64; ++w) e += w < wave ? s_ws[w] : 0u;
+  for (uint32_t b = 0; b < per; ++b) {
+    const uint32_t c = s_b[tid * per + b];
+    s_b[tid * per + b] = e;
+    e += c;
+  }
+  __syncthreads();
+  // members of every bucket, contiguous from its start
+#pragma unroll
+  for (int j = 0; j < KPT; ++j) {
+    const uint32_t i = tid + j * GO_ORDER_THREADS;
+    if (i < n) s_m[s_b[bucket(s_u[i])] + r[j]] = i;
+  }
+  __syncthreads();
+  const uint64_t o = offs[p];
+#pragma unroll
+  for (int j = 0; j < KPT; ++j) {
+    const uint32_t i = tid + j * GO_ORDER_THREADS;
+    if (i >= n) continue;
+    const uint64_t u = s_u[i];
+    const uint32_t b = bucket(u), b0 = s_b[b], b1 = b + 1 < nb ? s_b[b + 1] : n;
+    uint32_t rank = b0;
+    for (uint32_t q = b0; q < b1; ++q) rank += s_u[s_m[q]] < u;
+    const uint64_t pos = o + rank;
+    if (pos >= cap) continue;
+    rk[pos] = (int64_t)(u ^ 0x8000000000000000ull);
+    for (int a = 0; a < na; ++a) {
+      uint64_t x = agg[(uint64_t)a * gstr + base + i];
+      const int kd = kind_at(kinds, a);
+      if (kd == AK_MIN_F64 || kd == AK_MAX_F64) x = ord_to_f64(x);
+      ra[pos * na + a] = x;
+    }
   }
 }
 

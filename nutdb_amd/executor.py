@@ -343,12 +343,13 @@ class Executor:
         check(lib.nut_ctx_sort_stats(self.ctx, C.byref(b), C.byref(lv)), "nut_ctx_sort_stats")
         return b.value, lv.value
 
-    GROUPBY_PATHS = ("onchip", "partitioned_direct", "partitioned_spill")
+    GROUPBY_PATHS = ("onchip", "partitioned_direct", "partitioned_spill", "partitioned_ordered")
     OPTIONS = {"gb_partition": 0, "gb_levels": 1, "gb_optimistic": 2, "gb_direct": 3, "gb_chunks": 4,
                "join_region": 5, "join_probe_cfg": 6, "join_any_cfg": 7, "gb_seg_slots": 8,
                "gb_dense": 9, "gb_l1_bits": 10,
                "topk": 11, "gb_l0_bits": 12, "stream_blocks": 13,
-               "priv_bd": 14, "priv_blocks": 15, "agg_blocks": 16, "sel_blocks": 17, "sort_bd": 18}
+               "priv_bd": 14, "priv_blocks": 15, "agg_blocks": 16, "sel_blocks": 17, "sort_bd": 18,
+               "gb_ordered": 19}
 
     def groupby_stats(self) -> dict:
         """The algorithm the last group-by on this context took (nut_ctx_groupby_stats)."""
@@ -421,6 +422,38 @@ class Executor:
         h = C.c_void_p()
         check(lib.nut_groupby(self.ctx, C.byref(spec), group_hint, C.byref(h)), "nut_groupby")
         return Groups(self, h.value, max(spec.nkeys, 1), q.result_types())
+
+    def groupby_to_host(self, q: "AggQuery | ProgQuery", group_hint: int = 0, out=None):
+        """nut_groupby_to_host: (keys int64 [n, nkeys], aggs uint64 [n, naggs]) sorted by key
+        tuple, as groupby(q).to_host_words() — for one plain key column at large G the
+        range-partitioned path that needs no sort and overlaps the transfer (page-locked
+        `out` arrays: a (keys, aggs) pair with room for the groups; without `out` page-locked
+        arrays of max(2 * group_hint, 1024) rows are made, and again at the size the library
+        reports if that was too small)."""
+        spec = q.to_spec(self.device)
+        nk, na = max(spec.nkeys, 1), len(q.result_types())
+        self._bind_stream()
+        n = C.c_uint64()
+        rows = max(2 * int(group_hint), 1024)
+        for _ in range(2):
+            if out is None:
+                ko = torch.empty((rows, nk), dtype=torch.int64, pin_memory=True).numpy()
+                ao = torch.empty((rows, max(na, 1)), dtype=torch.int64, pin_memory=True).numpy().view(np.uint64)
+            else:
+                ko, ao = out
+                if (ko.dtype != np.int64 or ao.dtype.itemsize != 8 or ko.shape[1:] != (nk,) or ko.shape[0] != ao.shape[0]
+                        or ao.shape[1:] != (max(na, 1),) or not ko.flags.c_contiguous or not ao.flags.c_contiguous):
+                    raise ValueError("groupby_to_host: out arrays must be C-contiguous int64 [cap, nkeys] / "
+                                     "8-byte [cap, max(naggs, 1)]")
+            st = lib.nut_groupby_to_host(self.ctx, C.byref(spec), group_hint, ko.ctypes.data, ao.ctypes.data,
+                                         ko.shape[0], C.byref(n))
+            if st == L.NUT_ERR_CAPACITY and out is None:
+                rows = n.value
+                continue
+            check(st, "nut_groupby_to_host")
+            m = n.value
+            return ko[:m], ao[:m, :na].view(np.uint64)
+        raise RuntimeError("nut_groupby_to_host: result size changed between two runs")
 
     def accumulate(self, q: AggQuery, acc: Groups) -> None:
         spec = q.to_spec(self.device)

@@ -1,0 +1,138 @@
+"""GPU parity of nut_groupby_to_host: at large G the ordered path —
+key-range partitions (GpRange), per-partition ordering, the result streamed to page-locked
+host arrays chunk by chunk — must return exactly what nut_groupby + nut_groups_to_host
+return (the hashed path + device ordering), and the oracle's groups: keys, counts, MIN /
+MAX bit-exact, f64 sums within F64_SUM_RTOL (exact for dyadic values).  Shapes it does not
+take (skewed keys, pageable outputs, the option off) fall back and give the same result."""
+import numpy as np
+import pytest
+import torch
+
+from helpers import F64_SUM_RTOL, rel_err
+from test_gpu_exec import AGGS4, dev, gb_query
+
+pytestmark = pytest.mark.gpu
+
+I64_MIN = np.iinfo(np.int64).min
+I64_MAX = np.iinfo(np.int64).max
+N = (1 << 24) + 4099  # the ordered path starts at 2^24 rows
+
+
+def pinned(rows, cols):
+    return torch.empty((rows, cols), dtype=torch.int64, pin_memory=True).numpy()
+
+
+def run_to_host(ex, q, hint, rows=None, pin=True):
+    rows = rows or 2 * hint
+    if pin:
+        out = (pinned(rows, 1), pinned(rows, 4))
+    else:
+        out = (np.empty((rows, 1), np.int64), np.empty((rows, 4), np.int64))
+    k, w = ex.groupby_to_host(q, group_hint=hint, out=out)
+    return k.copy(), w.copy(), ex.groupby_stats()["path"]
+
+
+def check(keys, words, ok, ow, sums_exact=False):
+    assert np.array_equal(keys, ok)
+    if sums_exact:
+        assert np.array_equal(words[:, 0], ow[:, 0])
+    else:
+        assert rel_err(words[:, 0].view(np.float64), ow[:, 0].view(np.float64)) <= F64_SUM_RTOL
+    assert np.array_equal(words[:, 1:], ow[:, 1:])
+
+
+@pytest.mark.parametrize("G,dyadic", [(2_000_000, False), (3_000_000, True)])
+def test_ordered_vs_oracle_and_hashed(ex, orc, G, dyadic):
+    key = orc.gen_column(2, 0x61, N, a=G)
+    val = orc.gen_column(3 if dyadic else 4, 0x62, N)
+    q = gb_query(dev(key, ex), dev(val, ex))
+    k, w, path = run_to_host(ex, q, G)
+    assert path == "partitioned_ordered"
+    ok, ow = orc.groupby([key], AGGS4, values=[val])
+    assert len(k) == len(ok) > 0.99 * G
+    check(k, w, ok, ow, sums_exact=dyadic)
+    # the hashed path + device ordering: the same groups, counts, MIN / MAX
+    g = ex.groupby(q, group_hint=G)
+    hk, hw = g.to_host_words()
+    g.free()
+    assert np.array_equal(hk, k)
+    assert np.array_equal(hw[:, 1:], w[:, 1:])
+    if dyadic:
+        assert np.array_equal(hw, w)
+
+
+def test_ordered_extreme_keys(ex, orc):
+    """INT64_MIN (the tables' empty marker), INT64_MAX and -0.0 / NaN-free extremes at both
+    ends of the range: the edge cells clamp, the order holds."""
+    rng = np.random.default_rng(7)
+    pool = rng.integers(I64_MIN, I64_MAX, 2_000_000, dtype=np.int64)
+    pool[:4] = [I64_MIN, I64_MAX, I64_MIN + 1, I64_MAX - 1]
+    key = pool[rng.integers(0, len(pool), N)]
+    key[::100_000] = I64_MIN  # (light enough to stay inside the capped regions)
+    key[1::100_000] = I64_MAX
+    val = rng.standard_normal(N)
+    val[::97] = -0.0
+    G = len(np.unique(key))
+    q = gb_query(dev(key, ex), dev(val, ex))
+    k, w, path = run_to_host(ex, q, G)
+    assert path == "partitioned_ordered"
+    ok, ow = orc.groupby([key], AGGS4, values=[val])
+    check(k, w, ok, ow)
+    assert k[0, 0] == I64_MIN and k[-1, 0] == I64_MAX
+
+
+def test_ordered_i64_values(ex, orc):
+    from nutdb_amd import Agg, AggQuery
+    rng = np.random.default_rng(8)
+    G = 2_000_000
+    key = orc.gen_column(2, 0x63, N, a=G)
+    val = rng.integers(-(1 << 40), 1 << 40, N, dtype=np.int64)
+    q = AggQuery(keys=[dev(key, ex)], values=[dev(val, ex)],
+                 aggs=[Agg("sum", "col", (0,)), Agg("count"), Agg("min", "col", (0,)), Agg("max", "col", (0,))])
+    k, w, path = run_to_host(ex, q, G)
+    assert path == "partitioned_ordered"
+    ok, ow = orc.groupby([key], AGGS4, values=[val])
+    assert np.array_equal(k, ok) and np.array_equal(w, ow)
+
+
+def test_skewed_keys_fall_back(ex, orc):
+    """Half the rows on one key overflow its range cell's capped region: the hashed path
+    runs instead (same result)."""
+    G = 2_000_000
+    key = orc.gen_column(2, 0x64, N, a=G)
+    key[::2] = key[1]
+    val = orc.gen_column(3, 0x65, N)
+    q = gb_query(dev(key, ex), dev(val, ex))
+    k, w, path = run_to_host(ex, q, G)
+    assert path != "partitioned_ordered"
+    ok, ow = orc.groupby([key], AGGS4, values=[val])
+    check(k, w, ok, ow, sums_exact=True)
+
+
+def test_pageable_and_option_off_fall_back(ex, orc, opts):
+    G = 2_000_000
+    key = orc.gen_column(2, 0x66, N, a=G)
+    val = orc.gen_column(3, 0x67, N)
+    q = gb_query(dev(key, ex), dev(val, ex))
+    ok, ow = orc.groupby([key], AGGS4, values=[val])
+    k, w, path = run_to_host(ex, q, G, pin=False)
+    assert path == "partitioned_direct"
+    check(k, w, ok, ow, sums_exact=True)
+    opts(gb_ordered=0)
+    k, w, path = run_to_host(ex, q, G)
+    assert path == "partitioned_direct"
+    check(k, w, ok, ow, sums_exact=True)
+
+
+def test_capacity_and_auto_size(ex, orc):
+    from nutdb_amd._lib import NUT_ERR_CAPACITY, NutError
+    G = 2_000_000
+    key = orc.gen_column(2, 0x68, N, a=G)
+    val = orc.gen_column(3, 0x69, N)
+    q = gb_query(dev(key, ex), dev(val, ex))
+    with pytest.raises(NutError) as ei:
+        ex.groupby_to_host(q, group_hint=G, out=(pinned(G - 1, 1), pinned(G - 1, 4)))
+    assert ei.value.status == NUT_ERR_CAPACITY
+    k, w = ex.groupby_to_host(q, group_hint=G // 4)  # library-made arrays, resized once
+    ok, ow = orc.groupby([key], AGGS4, values=[val])
+    check(k, w, ok, ow, sums_exact=True)
