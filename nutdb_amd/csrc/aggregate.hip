@@ -1087,16 +1087,21 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
   // released on every return, after the copy stream has drained (it reads `res` and
   // waits on the events)
   struct Cleanup {
-    hipStream_t st, cs;
+    nut_ctx *c;
+    hipStream_t st;
     uint64_t *res = nullptr;
-    std::vector<hipEvent_t> ev;
+    std::vector<hipEvent_t> ev, ev1;
     ~Cleanup() {
-      (void)hipStreamSynchronize(cs);
+      if (c->aux_stream) (void)hipStreamSynchronize(c->aux_stream);
+      (void)hipStreamSynchronize(c->copy_stream);
       for (auto x : ev)
         if (x) (void)hipEventDestroy(x);
+      for (auto x : ev1)
+        if (x) (void)hipEventDestroy(x);
+      c->stream = st;
       if (res) (void)hipFreeAsync(res, st);
     }
-  } cl{st, c->copy_stream};
+  } cl{c, st};
   NUT_HIP(hipMallocAsync((void **)&cl.res, rcap * 8 * (1 + (size_t)na), st));
   int64_t *rk = (int64_t *)cl.res;
   uint64_t *ra = cl.res + rcap;
@@ -1112,6 +1117,15 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
     ar.dst[a] = B2[a];
   }
   ar.narr = narr;
+  // Three streams: level 1 of every chunk back to back on the context's stream; each
+  // chunk's aggregation and ordering on a second one as soon as its level 1 is done
+  // (they overlap the next chunk's level 1, so neither launch's tail idles the chip); its
+  // transfer on the third once the host has read the chunk's running total
+  if (!c->aux_stream) NUT_HIP(hipStreamCreateWithFlags(&c->aux_stream, hipStreamNonBlocking));
+  hipStream_t ax = c->aux_stream;
+  std::vector<hipEvent_t> &ev1 = cl.ev1;
+  ev1.assign(nch, nullptr);
+  for (auto &x : ev1) NUT_HIP(hipEventCreateWithFlags(&x, hipEventDisableTiming));
   auto enqueue = [&](uint32_t j) -> nut_status {
     const uint32_t a0 = cb[j], a1 = cb[j + 1];
     const uint64_t q0 = (uint64_t)a0 * nb1, nq = (uint64_t)(a1 - a0) * nb1;
@@ -1119,6 +1133,9 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
     gp_capped_launch(c, ar, dseg + a0, dts + tile0[j], ntile[j], 0, dcur + q0, 0, ovf1, dcur + nparts + j, bits1, false,
                      &rg);
     c->timer.end(st);
+    NUT_HIP(hipGetLastError());
+    NUT_HIP(hipEventRecord(ev1[j], st));
+    NUT_HIP(hipStreamWaitEvent(ax, ev1[j], 0));
     LaunchExtra sg;  // partition rows [first row, cursor after the scatter)
     sg.seg_off = dinit + q0;
     sg.seg_end = (const uint64_t *)dcur + q0;
@@ -1127,32 +1144,32 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
     sg.dcount = dcount + q0;
     sg.dregion = dregion;
     sg.dbase = q0;
+    c->stream = ax;  // (launch_agg launches on the context's stream)
     nut_status e2 = launch_agg(g, &s3, per, g->kinds, &sg);
+    c->stream = st;
     if (e2) return e2;
-    c->timer.begin(st, NUT_KERNEL_AGGREGATE);
-    hipLaunchKernelGGL(go_scan_kernel, dim3(1), dim3(1024), 0, st, (const unsigned long long *)dcount + q0, (uint32_t)nq,
+    c->timer.begin(ax, NUT_KERNEL_AGGREGATE);
+    hipLaunchKernelGGL(go_scan_kernel, dim3(1), dim3(1024), 0, ax, (const unsigned long long *)dcount + q0, (uint32_t)nq,
                        doffs + q0, drun);
-    hipLaunchKernelGGL(go_order_kernel, dim3((unsigned)nq), dim3(GO_ORDER_THREADS), (unsigned)go_order_lds(dregion), st,
+    hipLaunchKernelGGL(go_order_kernel, dim3((unsigned)nq), dim3(GO_ORDER_THREADS), (unsigned)go_order_lds(dregion), ax,
                        (const uint64_t *)g->gt.slot, (const uint64_t *)g->gt.agg, g->gt.cap + 1, dregion, q0,
                        (const unsigned long long *)dcount + q0, (const uint64_t *)doffs + q0, na, g->gt.kinds, rk, ra,
                        rcap);
-    c->timer.end(st);
+    c->timer.end(ax);
     NUT_HIP(hipGetLastError());
-    NUT_HIP(hipMemcpyAsync((void *)(runs + j), drun, 8, hipMemcpyDeviceToHost, st));
-    NUT_HIP(hipEventRecord(ev[j], st));
+    NUT_HIP(hipMemcpyAsync((void *)(runs + j), drun, 8, hipMemcpyDeviceToHost, ax));
+    NUT_HIP(hipEventRecord(ev[j], ax));
     return NUT_OK;
   };
-  // two chunks in flight ahead of the host; chunk j crosses on the copy stream once its
-  // count is known
-  constexpr uint32_t kAhead = 2;
+  // every chunk queued (nothing waits for the host); chunk j crosses on the copy stream
+  // once its count is known
   uint64_t done = 0;  // groups already sent to the host
   bool over = false;
-  for (uint32_t j = 0; j < std::min(nch, kAhead); ++j)
+  for (uint32_t j = 0; j < nch; ++j)
     if ((e = enqueue(j))) return e;
   for (uint32_t j = 0; j < nch; ++j) {
     NUT_HIP(hipEventSynchronize(ev[j]));
     const uint64_t total = runs[j];
-    if (j + kAhead < nch && (e = enqueue(j + kAhead))) return e;
     if (total > rcap) over = true;
     if (!over && total > done) {
       NUT_HIP(hipStreamWaitEvent(c->copy_stream, ev[j], 0));
@@ -1163,6 +1180,7 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
     done = total;
   }
   // the capped level-1 flags and the aggregation's control words
+  NUT_HIP(hipStreamSynchronize(ax));
   std::vector<uint64_t> flags(nch);
   NUT_HIP(hipMemcpyAsync(flags.data(), dcur + nparts, nch * 8, hipMemcpyDeviceToHost, st));
   uint32_t ctl[4];

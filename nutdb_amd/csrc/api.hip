@@ -298,6 +298,7 @@ void nut_ctx_destroy(nut_ctx *c) {
   if (c->host_pinned) (void)hipHostFree(c->host_pinned);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
+  if (c->aux_stream) (void)hipStreamDestroy(c->aux_stream);
   delete c;
 }
 

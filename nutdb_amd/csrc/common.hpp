@@ -182,6 +182,7 @@ struct nut_ctx {
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
   hipStream_t copy_stream = nullptr;  // device -> host transfers beside the work (nut_groupby_to_host)
+  hipStream_t aux_stream = nullptr;   // a second compute stream (nut_groupby_to_host's per-chunk aggregation)
   nut::Scratch filter_state;  // tile counter + look-back status words
   nut::Scratch sort_tmp;      // sort ping-pong + histograms
   nut::Scratch sort_tmp2;     // MSD sort, capped layout: the second level's regions

@@ -155,17 +155,19 @@ __global__ __launch_bounds__(FS_THREADS, 1) void filter_i64_staged_kernel(
   i64x2 v[FS_STRIPES];
   // one code path: 16-B loads at row indices clamped to n - 2 (n >= 2); rows >= n are
   // masked in the rank.  Only the pair (n - 1, n) of an odd n is clamped while holding a
-  // valid row: it loads (n - 2, n - 1) and takes its row from the upper half.
+  // valid row: it loads (n - 2, n - 1) and takes its row from the upper half — when the
+  // tile is ranked, not at the load: a select on a loaded value waits for it,
+  // and the next tile's loads, issued before this tile's write-out, would all be waited
+  // for before that write-out could start (vmcnt is in order)
   auto load = [&](uint32_t t) {
     const uint64_t base = (uint64_t)t * FS_TILE;
 #pragma unroll
     for (int j = 0; j < FS_STRIPES; ++j) {
-      const uint64_t raw = base + j * FS_STRIPE_ROWS + 2 * tid;
-      const uint64_t idx = min(raw, n - 2);
+      const uint64_t idx = min(base + j * FS_STRIPE_ROWS + 2 * tid, n - 2);
       v[j] = __builtin_nontemporal_load(reinterpret_cast<const i64x2 *>(col + idx));
-      if (raw == n - 1) v[j].x = v[j].y;
     }
   };
+
   if (tid == 0) s_next = atomicAdd(ticket, 1u);
   __syncthreads();
   uint32_t tile = s_next;
@@ -179,6 +181,13 @@ __global__ __launch_bounds__(FS_THREADS, 1) void filter_i64_staged_kernel(
     const int tid = tid_;
     const uint64_t base = (uint64_t)tile * FS_TILE;
     const bool full = base + FS_TILE <= n;
+    if (!full) {  // (the last tile only) the pair holding row n - 1 alone takes its upper half
+      const uint64_t r = n - 1 - base;
+      const bool mine = (r & 1) == 0 && (uint32_t)((r % FS_STRIPE_ROWS) / 2) == (uint32_t)tid;
+      const uint32_t js = (uint32_t)(r / FS_STRIPE_ROWS);
+#pragma unroll
+      for (int j = 0; j < FS_STRIPES; ++j) v[j].x = mine && js == (uint32_t)j ? v[j].y : v[j].x;
+    }
     uint32_t rk[FS_STRIPES / 4] = {};  // in-wave ranks (<= 126), 4 per word
     uint32_t sel = 0;                  // bit 2j: row0 of stripe j selected, bit 2j+1: row1
 #pragma unroll

@@ -274,20 +274,15 @@ __global__ void go_sample_kernel(const int64_t *__restrict__ k, uint64_t n, uint
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) out[i] = k[i * step];
 }
 
-// one workgroup: offs[p] = *run + the groups of the partitions before p (np <= 4096), then
-// *run += all of them
-constexpr int GO_SCAN_PER = 4;
+// one workgroup: offs[p] = *run + the groups of the partitions before p, then *run += all
+// of them (each thread a run of ceil(np / 1024) consecutive partitions)
 __global__ __launch_bounds__(1024) void go_scan_kernel(const unsigned long long *__restrict__ cnt, uint32_t np,
                                                        uint64_t *__restrict__ offs, unsigned long long *__restrict__ run) {
   __shared__ uint64_t ws[16];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  uint64_t v[GO_SCAN_PER], sum = 0;
-#pragma unroll
-  for (int j = 0; j < GO_SCAN_PER; ++j) {
-    const uint32_t i = (uint32_t)tid * GO_SCAN_PER + j;
-    v[j] = i < np ? cnt[i] : 0;
-    sum += v[j];
-  }
+  const uint32_t per = (np + 1023) / 1024, i0 = (uint32_t)tid * per, i1 = min(np, i0 + per);
+  uint64_t sum = 0;
+  for (uint32_t i = i0; i < i1; ++i) sum += cnt[i];
   uint64_t incl = sum;
 #pragma unroll
   for (int off = 1; off < 64; off <<= 1) {
@@ -304,11 +299,9 @@ __global__ __launch_bounds__(1024) void go_scan_kernel(const unsigned long long 
   }
   const uint64_t base = *run;
   uint64_t e = base + add + incl - sum;
-#pragma unroll
-  for (int j = 0; j < GO_SCAN_PER; ++j) {
-    const uint32_t i = (uint32_t)tid * GO_SCAN_PER + j;
-    if (i < np) offs[i] = e;
-    e += v[j];
+  for (uint32_t i = i0; i < i1; ++i) {
+    offs[i] = e;
+    e += cnt[i];
   }
   __syncthreads();  // every thread has read *run
   if (tid == 0) *run = base + tot;

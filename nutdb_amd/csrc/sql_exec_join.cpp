@@ -635,9 +635,18 @@ nut_status exec_joinn(nut_ctx *c, const nut_plan &p, const nut_column *const *ta
     const nut_plan::JoinStep &js = p.jn[k];
     const int t = k + 1;
     jkey[k] = {js.key[0], js.key[1]};
-    if (!js.scope) continue;
     std::vector<PProg> conj;
     split_and(js.cond, conj);
+    if (!js.scope) {  // ON filters: conditions on the step's own table, applied before it joins
+      for (PProg &cj : conj) {
+        for (const PNode &nd : cj)
+          if ((nd.op == NUT_P_COL || nd.op == P_LIKE || nd.op == P_ILIKE) && side[nd.col] != t)
+            return fail(NUT_ERR_PLAN, "JOIN " + std::to_string(t) + ": an ON condition beyond the key equality must read '" +
+                                          tname[t] + "' alone (column '" + p.cols[nd.col] + "')");
+        sub_push[t].push_back(std::move(cj));
+      }
+      continue;
+    }
     for (PProg &cj : conj) {
       bool inner = false, outer = false, later = false;
       for (const PNode &nd : cj)

@@ -1116,6 +1116,37 @@ PProg and_all(const std::vector<PProg> &cs);
 
 // ON a = b [AND c = d ...]: every equality of two columns, in order (the first is the hash
 // key, the rest residual equalities); false if the condition has any other shape
+// ON split into its column = column equalities (the keys) and its other conjuncts (`rest`:
+// filters of the JOIN source's table)
+void on_split(nut_plan &p, const Expr &e, std::vector<std::pair<int, int>> &eqs, std::vector<const Expr *> &rest) {
+  if (e.k == EK::BinaryOp && e.bop() == BinOp::And) {
+    on_split(p, e.kids[0], eqs, rest);
+    on_split(p, e.kids[1], eqs, rest);
+    return;
+  }
+  sv ka, kb;
+  if (e.k == EK::BinaryOp && e.bop() == BinOp::Eq && column_ref(p, e.kids[0], ka) && column_ref(p, e.kids[1], kb)) {
+    const int a = col_index(p, ka);
+    eqs.emplace_back(a, col_index(p, kb));
+  } else {
+    rest.push_back(&e);
+  }
+}
+
+// the ON filters as one program (expression mode): and_all of each conjunct's
+bool on_filters(nut_plan &p, const std::vector<const Expr *> &rest, PProg &cond, Lowering &L) {
+  if (rest.empty()) return true;
+  if (!p.compiled) return L.fail("JOIN ON conditions beyond key equalities run in expression mode");
+  std::vector<PProg> cs;
+  for (const Expr *e : rest) {
+    PProg c;
+    if (!lower_prog(p, *e, c, L)) return false;
+    cs.push_back(std::move(c));
+  }
+  cond = and_all(cs);
+  return true;
+}
+
 bool on_equalities(nut_plan &p, const Expr &e, std::vector<std::pair<int, int>> &eqs) {
   if (e.k == EK::BinaryOp && e.bop() == BinOp::And)
     return on_equalities(p, e.kids[0], eqs) && on_equalities(p, e.kids[1], eqs);
@@ -1290,12 +1321,16 @@ bool lower_mode(const Query &qry, nut_plan &p, Lowering &L) {
         default: return L.fail("several JOINs: INNER, LEFT / RIGHT / FULL OUTER, LEFT SEMI / ANTI steps only");
       }
       std::vector<std::pair<int, int>> eqs;
-      if (!on_equalities(p, jc.cond, eqs))
-        return L.fail("JOIN ON must be equalities of two columns (ANDed)");
+      std::vector<const Expr *> rest;
+      on_split(p, jc.cond, eqs, rest);
+      if (eqs.empty()) return L.fail("JOIN ON needs an equality of two columns (the key)");
       if (eqs.size() > 1 && jc.t != JoinType::Inner)
         return L.fail("JOIN with several key columns: INNER only (outer / semi / anti joins take one ON equality)");
+      if (!rest.empty() && (type == PJ_RIGHT || type == PJ_FULL))
+        return L.fail("JOIN ON conditions beyond key equalities: INNER, LEFT, SEMI and ANTI joins (they filter the JOIN source)");
       nut_plan::JoinStep js;
       js.type = type;
+      if (!on_filters(p, rest, js.cond, L)) return false;
       js.table = std::string(jc.src.table);
       if (jc.src.alias) js.alias = std::string(*jc.src.alias);
       js.key[0] = eqs[0].first;
@@ -1326,8 +1361,14 @@ bool lower_mode(const Query &qry, nut_plan &p, Lowering &L) {
     if (jc.src.alias) p.jalias = std::string(*jc.src.alias);
     if (b.from && b.from->alias) p.talias = std::string(*b.from->alias);
     std::vector<std::pair<int, int>> eqs;  // (p.join is set: qualified ON columns keep their qualifier)
+    PProg on_cond;                         // ON filters of the JOIN source: the join runs as a one-step chain
     if (jc.on) {
-      if (!on_equalities(p, jc.cond, eqs)) return L.fail("JOIN ON must be equalities of two columns (ANDed)");
+      std::vector<const Expr *> rest;
+      on_split(p, jc.cond, eqs, rest);
+      if (eqs.empty()) return L.fail("JOIN ON needs an equality of two columns (the key)");
+      if (!rest.empty() && (p.jright || p.join == PJ_FULL))
+        return L.fail("JOIN ON conditions beyond key equalities: INNER, LEFT, SEMI and ANTI joins (they filter the JOIN source)");
+      if (!on_filters(p, rest, on_cond, L)) return false;
     } else {
       // USING (u, ...): u of the FROM table = u of the JOIN source; an unqualified u
       // elsewhere in the query is the preserved table's (INNER: the FROM table's)
@@ -1346,7 +1387,7 @@ bool lower_mode(const Query &qry, nut_plan &p, Lowering &L) {
     p.jkey[0] = eqs[0].first;
     p.jkey[1] = eqs[0].second;
     join_extra.insert(join_extra.end(), eqs.begin() + 1, eqs.end());
-    if (has_semi) {  // the one JOIN becomes the first step of a chain the subqueries extend
+    if (has_semi || !on_cond.empty()) {  // the one JOIN becomes the first step of a chain (the subqueries extend it)
       if (p.jright && p.join != NUT_JOIN_LEFT) return L.fail("RIGHT SEMI / ANTI JOIN with EXISTS / IN subqueries is not executed");
       if (!p.using_cols.empty()) return L.fail("JOIN ... USING with EXISTS / IN subqueries is not executed (ON a = b)");
       nut_plan::JoinStep js;
@@ -1355,6 +1396,7 @@ bool lower_mode(const Query &qry, nut_plan &p, Lowering &L) {
       js.key[0] = p.jkey[0];
       js.key[1] = p.jkey[1];
       js.type = p.jright ? PJ_RIGHT : p.join;
+      js.cond = std::move(on_cond);
       p.jn.push_back(js);
       p.join = NUT_JOIN_INNER;
       p.jright = false;
@@ -1808,8 +1850,62 @@ bool flatten_derived(const Query &q, std::unique_ptr<Query> &flat, Lowering &L) 
   return true;
 }
 
+// a derived table whose body groups or aggregates: materialized (nut_plan::inner) when the
+// outer query reads it alone (no JOIN), by name, as its own table
+bool grouped_body(const QueryBody &in) {
+  std::function<bool(const Expr &)> has_agg = [&](const Expr &e) {
+    if (e.k == EK::FnCall && e.fn() == FnKind::Others && is_agg_name(e.id.name)) return true;
+    for (const Expr &k : e.kids)
+      if (has_agg(k)) return true;
+    return false;
+  };
+  if (in.group_by) return true;
+  for (const QueryExpr &c : in.columns)
+    if (has_agg(c.e)) return true;
+  return false;
+}
+
 bool lower_query(const Query &q, nut_plan &p, Lowering &L) {
+  // WITH name AS (query) ... FROM name [alias]: the CTE as a derived table
+  if (!q.is_union && q.body && q.body->with && q.body->from && q.body->from->k == SourceKind::Table) {
+    const QuerySource &f = *q.body->from;
+    for (const CTE &c : *q.body->with) {
+      if (!c.q || !ieq(c.alias, f.table)) continue;
+      auto n = clone_query(q);
+      n->body->with.reset();
+      QuerySource d;
+      d.k = SourceKind::Subquery;
+      d.e.k = EK::Subquery;
+      d.e.q = clone_query(*c.q);
+      d.alias = f.alias ? f.alias : std::optional<sv>(c.alias);
+      n->body->from = std::move(d);
+      return lower_query(*n, p, L);
+    }
+    return L.fail("WITH: the query reads no CTE from FROM (CTEs in JOINs or subqueries are not executed)");
+  }
+  if (!q.is_union && q.body && q.body->with) return L.fail("WITH: a CTE is executed when FROM names it");
   if (!q.is_union && q.body && q.body->from && q.body->from->k == SourceKind::Subquery) {
+    const QuerySource &src = *q.body->from;
+    const bool grouped = src.e.q && !src.e.q->is_union && src.e.q->body && grouped_body(*src.e.q->body);
+    if (grouped) {
+      if (!q.body->joins.empty()) return L.fail("derived table: a grouped derived table is not joined");
+      auto inner = std::make_shared<nut_plan>();
+      Lowering Li;
+      if (!lower_query(*src.e.q, *inner, Li)) return L.fail("derived table: " + Li.err);
+      if (inner->kind != NUT_PLAN_GROUPBY) return L.fail("derived table: its grouped body must lower to a group-by");
+      for (const PlanOut &o : inner->outs)
+        if (o.name.empty() && !o.hidden) return L.fail("derived table: every output of its body needs a name");
+      // the outer query over a table named by the derived table's alias
+      auto n = clone_query(q);
+      QuerySource t;
+      t.k = SourceKind::Table;
+      t.table = src.alias ? *src.alias : sv("derived");
+      n->body->from = std::move(t);
+      if (!lower_query(*n, p, L)) return false;
+      if (p.join >= 0 || !p.jn.empty()) return L.fail("derived table: a grouped derived table is not joined");
+      p.inner = std::move(inner);
+      return true;
+    }
     std::unique_ptr<Query> flat;
     if (!flatten_derived(q, flat, L)) return false;
     return lower_query(*flat, p, L);
@@ -1906,10 +2002,20 @@ std::string describe(const nut_plan &p) {
   o += kinds[p.kind];
   o += "\",\"table\":";
   json_str(o, p.table);
+  // (a materialized derived table: the columns the caller binds are its body's; this
+  // plan's own, over the body's outputs, are "derived_columns")
+  const std::vector<std::string> &bcols = p.inner ? p.inner->cols : p.cols;
   o += ",\"columns\":[";
-  for (size_t i = 0; i < p.cols.size(); ++i) {
+  for (size_t i = 0; i < bcols.size(); ++i) {
     if (i) o += ',';
-    json_str(o, shown(p.cols[i]));
+    json_str(o, shown(bcols[i]));
+  }
+  if (p.inner) {
+    o += "],\"derived_columns\":[";
+    for (size_t i = 0; i < p.cols.size(); ++i) {
+      if (i) o += ',';
+      json_str(o, shown(p.cols[i]));
+    }
   }
   o += "],\"never\":";
   o += p.never ? "true" : "false";
@@ -2076,6 +2182,9 @@ std::string describe(const nut_plan &p) {
           json_str(o, p.jn[k].alias);
           o += ",\"where\":";
           json_str(o, prog_text(p, p.jn[k].cond));
+        } else if (!p.jn[k].cond.empty()) {  // ON filters of the step's table
+          o += ",\"on_filter\":";
+          json_str(o, prog_text(p, p.jn[k].cond));
         }
         o += '}';
       }
@@ -2083,6 +2192,7 @@ std::string describe(const nut_plan &p) {
     }
   }
   o += ",\"offset\":" + std::to_string(p.offset);
+  if (p.inner) o += ",\"derived\":" + describe(*p.inner);
   if (!p.subs.empty()) {  // scalar subqueries, by placeholder index ($subqueryN)
     o += ",\"subqueries\":[";
     for (size_t i = 0; i < p.subs.size(); ++i) o += (i ? "," : "") + describe(*p.subs[i]);

@@ -112,6 +112,26 @@ nut_status resolve_subqueries(const nut_plan &p, nut_plan &q,
   return NUT_OK;
 }
 
+// The rest of a plan over its materialized derived table: the body's result (a group-by:
+// host columns) bound by output name as the outer plan's table (copied into HBM by the
+// call, NUT_COL_HOST).  Takes r1.
+nut_status run_over_derived(nut_ctx *c, const nut_plan &p, nut_result *r1, nut_result **out) {
+  struct Free {
+    nut_result *r;
+    ~Free() { nut_result_free(r); }
+  } f{r1};
+  if (r1->kind != NUT_PLAN_GROUPBY || r1->host.size() != r1->names.size())
+    return fail(NUT_ERR_UNSUPPORTED, "derived table: its body did not produce a group-by result");
+  std::vector<nut_column> cols;
+  for (size_t j = 0; j < r1->names.size(); ++j) {
+    if (r1->types[j] != NUT_T_I64 && r1->types[j] != NUT_T_F64) continue;  // (string outputs are not read back)
+    cols.push_back(nut_column{r1->names[j].c_str(), r1->host[j].data(), r1->types[j] | NUT_COL_HOST});
+  }
+  nut_plan o = p;
+  o.inner.reset();
+  return nut_plan_execute(c, &o, cols.data(), (int)cols.size(), r1->nrows, 0, out);
+}
+
 }  // namespace
 
 extern "C" {
@@ -212,6 +232,12 @@ nut_status nut_plan_execute(nut_ctx *c, const nut_plan *p, const nut_column *col
                             uint64_t group_hint, nut_result **out) {
   if (!c || !p || !out || (ncols && !cols) || ncols < 0) return fail(NUT_ERR_INVALID_ARG, "nut_plan_execute: NULL argument");
   *out = nullptr;
+  if (p->inner) {  // a materialized derived table: its body first, over the caller's columns
+    if (p->inner->join >= 0) return fail(NUT_ERR_INVALID_ARG, "nut_plan_execute: the derived table has a JOIN (nut_plan_execute2)");
+    nut_result *r1 = nullptr;
+    nut_status st = nut_plan_execute(c, p->inner.get(), cols, ncols, nrows, group_hint, &r1);
+    return st ? st : run_over_derived(c, *p, r1, out);
+  }
   if (p->join >= 0) return fail(NUT_ERR_INVALID_ARG, "nut_plan_execute: the plan has a JOIN (nut_plan_execute2)");
   if (!p->subs.empty()) {  // scalar subqueries first, over the same columns
     nut_plan q;
@@ -261,8 +287,20 @@ nut_status nut_plan_execute2(nut_ctx *c, const nut_plan *p, const nut_column *le
                              nut_result **out) {
   if (!c || !p || !out || (nleft && !left) || (nright && !right) || nleft < 0 || nright < 0)
     return fail(NUT_ERR_INVALID_ARG, "nut_plan_execute2: NULL argument");
+  if (p->inner) {  // a materialized derived table over the two tables, then the rest over it
+    *out = nullptr;
+    nut_result *r1 = nullptr;
+    nut_status st = nut_plan_execute2(c, p->inner.get(), left, nleft, lrows, right, nright, rrows, group_hint, &r1);
+    return st ? st : run_over_derived(c, *p, r1, out);
+  }
   if (p->join < 0) return nut_plan_execute(c, p, left, nleft, lrows, group_hint, out);
   if (!p->subs.empty()) return fail(NUT_ERR_UNSUPPORTED, "scalar subqueries execute in single-table plans");
+  if (p->jn.size() == 1) {  // one JOIN run as a chain step (ON filters, EXISTS / IN)
+    const nut_column *tabs[2] = {left, right};
+    const int nc[2] = {nleft, nright};
+    const uint64_t nr[2] = {lrows, rrows};
+    return nut_plan_executen(c, p, tabs, nc, nr, 2, group_hint, out);
+  }
   if (!p->jn.empty()) return fail(NUT_ERR_INVALID_ARG, "nut_plan_execute2: the plan joins several tables (nut_plan_executen)");
   *out = nullptr;
   DeviceGuard g(c->device);
@@ -287,6 +325,12 @@ nut_status nut_plan_executen(nut_ctx *c, const nut_plan *p, const nut_column *co
                              const uint64_t *nrows, int ntables, uint64_t group_hint, nut_result **out) {
   if (!c || !p || !out || !tables || !ncols || !nrows || ntables < 1)
     return fail(NUT_ERR_INVALID_ARG, "nut_plan_executen: NULL argument");
+  if (p->inner) {  // a materialized derived table over the tables, then the rest over it
+    *out = nullptr;
+    nut_result *r1 = nullptr;
+    nut_status st = nut_plan_executen(c, p->inner.get(), tables, ncols, nrows, ntables, group_hint, &r1);
+    return st ? st : run_over_derived(c, *p, r1, out);
+  }
   if (p->jn.empty()) {
     if (ntables == 1) return nut_plan_execute(c, p, tables[0], ncols[0], nrows[0], group_hint, out);
     if (ntables == 2)
@@ -318,6 +362,7 @@ nut_status nut_plan_executen(nut_ctx *c, const nut_plan *p, const nut_column *co
 
 nut_status nut_plan_prepare(const nut_plan *p, const nut_column *cols, int ncols) {
   if (!p || (ncols && !cols) || ncols < 0) return fail(NUT_ERR_INVALID_ARG, "nut_plan_prepare: NULL argument");
+  if (p->inner) return nut_plan_prepare(p->inner.get(), cols, ncols);  // (the rest compiles when it runs)
   if (!p->compiled) return NUT_OK;  // precompiled kernels only
   // scalar subqueries: their values (int64 or f64 constants) decide the program types, so
   // the shape is compiled when the plan executes with the values in place
@@ -373,6 +418,12 @@ nut_status nut_plan_prepare(const nut_plan *p, const nut_column *cols, int ncols
 nut_status nut_table_execute(nut_ctx *c, nut_table *t, const nut_plan *p, uint64_t group_hint, nut_result **out) {
   if (!c || !t || !p || !out) return fail(NUT_ERR_INVALID_ARG, "nut_table_execute: NULL argument");
   *out = nullptr;
+  if (p->inner) {  // a materialized derived table (string outputs of its body stay unread)
+    if (p->inner->join >= 0) return fail(NUT_ERR_INVALID_ARG, "nut_table_execute: the derived table has a JOIN (nut_table_execute2)");
+    nut_result *r1 = nullptr;
+    nut_status st = nut_table_execute(c, t, p->inner.get(), group_hint, &r1);
+    return st ? st : run_over_derived(c, *p, r1, out);
+  }
   if (t->ragged()) return fail(NUT_ERR_INVALID_ARG, "nut_table_execute: table '" + t->name + "' has ragged columns");
   if (t->device >= 0 && t->device != c->device)
     return fail(NUT_ERR_INVALID_ARG, "nut_table_execute: the table lives on another device");
@@ -424,7 +475,17 @@ nut_status nut_table_execute(nut_ctx *c, nut_table *t, const nut_plan *p, uint64
 nut_status nut_table_execute2(nut_ctx *c, nut_table *left, nut_table *right, const nut_plan *p, uint64_t group_hint,
                               nut_result **out) {
   if (!c || !left || !right || !p || !out) return fail(NUT_ERR_INVALID_ARG, "nut_table_execute2: NULL argument");
+  if (p->inner) {
+    *out = nullptr;
+    nut_result *r1 = nullptr;
+    nut_status st = nut_table_execute2(c, left, right, p->inner.get(), group_hint, &r1);
+    return st ? st : run_over_derived(c, *p, r1, out);
+  }
   if (p->join < 0) return nut_table_execute(c, left, p, group_hint, out);
+  if (!p->jn.empty()) {  // one JOIN run as a chain step (ON filters, EXISTS / IN)
+    nut_table *const tabs[2] = {left, right};
+    return nut_table_executen(c, tabs, 2, p, group_hint, out);
+  }
   if (!p->subs.empty()) return fail(NUT_ERR_UNSUPPORTED, "scalar subqueries execute in single-table plans");
   *out = nullptr;
   std::vector<nut_column> cols[2];
@@ -460,6 +521,12 @@ nut_status nut_table_executen(nut_ctx *c, nut_table *const *tables, int ntables,
   if (!c || !tables || ntables < 1 || !p || !out) return fail(NUT_ERR_INVALID_ARG, "nut_table_executen: NULL argument");
   for (int k = 0; k < ntables; ++k)
     if (!tables[k]) return fail(NUT_ERR_INVALID_ARG, "nut_table_executen: NULL table");
+  if (p->inner) {
+    *out = nullptr;
+    nut_result *r1 = nullptr;
+    nut_status st = nut_table_executen(c, tables, ntables, p->inner.get(), group_hint, &r1);
+    return st ? st : run_over_derived(c, *p, r1, out);
+  }
   if (p->jn.empty()) {
     if (ntables == 1) return nut_table_execute(c, tables[0], p, group_hint, out);
     if (ntables == 2) return nut_table_execute2(c, tables[0], tables[1], p, group_hint, out);

@@ -176,6 +176,10 @@ struct nut_plan {
   // their one value replaces every constant whose param names them (resolve_subqueries)
   std::vector<std::shared_ptr<nut_plan>> subs;
   int scope = 0;  // lowering state: the EXISTS / IN subquery whose names are being lowered
+  // FROM (SELECT .. GROUP BY ..) d, or a CTE of that shape: the derived
+  // table is materialized — `inner` executes over the caller's columns first and this plan
+  // runs over its result columns (bound by output name)
+  std::shared_ptr<nut_plan> inner;
 };
 
 struct nut_result {

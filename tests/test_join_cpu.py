@@ -79,8 +79,8 @@ def test_sql_no_join_has_no_join_key():
 
 @pytest.mark.parametrize("sql,msg", [
     ("select count(*) from a full join b on x = y and u = v", "INNER only"),
-    ("select count(*) from a join b on x < y", "equalities of two columns"),
-    ("select count(*) from a join b on x = y and u < v", "equalities of two columns"),
+    ("select count(*) from a join b on x < y", "needs an equality of two columns"),
+    ("select count(*) from a right join b on x = y and u < v", "INNER, LEFT, SEMI and ANTI"),
     ("select count(*) from a left join b on x = y and u = v", "INNER only"),
     ("select count(*) from a left semi join b using (x, y)", "INNER only"),
     ("select count(*) from a join b using (x) join c using (x)", "USING in a chain"),
@@ -167,3 +167,44 @@ def test_sql_join_using_and_multi_key_lowering():
     assert d["join"]["on"] == ["a.x", "b.x"] and d["where_expr"] == "((a.z > 1) and (a.y = b.y))"
     d = Plan("select count(*) from l join o on lk = ok join c on oc = ck and on_ = cn").describe()
     assert d["joins"][1] == {"table": "c", "type": "inner", "on": ["oc", "ck"]} and d["where_expr"] == "(on_ = cn)"
+
+
+# ---- grouped derived tables, CTEs, JOIN ON filters
+from nutdb_amd._lib import NutError  # noqa: E402
+from nutdb_amd.sql import Plan  # noqa: E402
+
+Q13_CTE = ("with c_orders as (select c_custkey, count(o_orderkey) as c_count from customer left outer join orders "
+           "on c_custkey = o_custkey and o_comment not like '%special%requests%' group by c_custkey) "
+           "select c_count, count(*) as custdist from c_orders group by c_count order by custdist desc, c_count desc")
+
+
+def test_plan_cte_materialized_with_on_filter():
+    d = Plan(Q13_CTE).describe()
+    assert d["kind"] == "groupby" and d["table"] == "c_orders" and d["keys"] == ["c_count"]
+    assert d["derived_columns"] == ["c_count"]
+    inner = d["derived"]
+    assert inner["kind"] == "groupby" and inner["table"] == "customer" and inner["keys"] == ["c_custkey"]
+    assert d["columns"] == inner["columns"]  # the caller binds the body's tables
+    step = inner["joins"][0]
+    assert step["type"] == "left" and step["on"] == ["c_custkey", "o_custkey"]
+    assert "o_comment" in step["on_filter"] and "special" in step["on_filter"]
+
+
+def test_plan_grouped_derived_table():
+    d = Plan("select m, count(*) as n from (select k, max(v) as m from t group by k) as d "
+             "where m > 3 group by m").describe()
+    assert d["table"] == "d" and d["derived"]["table"] == "t" and d["columns"] == ["k", "v"]
+    assert d["where"] == [{"col": "m", "op": ">", "value": "3", "value_kind": "int"}]
+
+
+def test_plan_on_filter_and_cte_errors():
+    d = Plan("select count(*) from a join b on k = bk and w < 5").describe()
+    assert d["joins"][0]["type"] == "inner" and "w" in d["joins"][0]["on_filter"]
+    with pytest.raises(NutError, match="INNER, LEFT, SEMI and ANTI"):
+        Plan("select count(*) from a right join b on k = bk and w < 5")
+    with pytest.raises(NutError, match="needs an equality"):
+        Plan("select count(*) from a join b on w < 5")
+    with pytest.raises(NutError, match="WITH"):
+        Plan("with c as (select k from t) select count(*) from u")
+    with pytest.raises(NutError, match="not joined"):
+        Plan("select count(*) from (select k, count(*) as c from t group by k) as d join u on d.k = u.k")

@@ -580,5 +580,8 @@ def test_plan_derived_table_flattened():
     assert "(s_suppkey = l_suppkey)" in d["where_expr"] and "l_shipdate <= 9861" in d["where_expr"]
     d = Plan("select v, count(*) from (select a + 1 as v, b from t where b > 0) as s where s.v < 10 group by v").describe()
     assert d["keys"] == ["a + 1"] and "(b > 0)" in d["where_expr"] and "((a + 1) < 10)" in d["where_expr"]
+    # a grouped body is not flattened: it is materialized (nut_plan::inner)
+    d = Plan("select x from (select k, count(*) as x from t group by k) as s").describe()
+    assert d["derived"]["kind"] == "groupby" and d["table"] == "s" and d["column"] == "x"
     with pytest.raises(NutError, match="projection bodies"):
-        Plan("select x from (select k, count(*) as x from t group by k) as s")
+        Plan("select x from (select distinct k as x from t) as s")
