@@ -581,8 +581,18 @@ __global__ __launch_bounds__(BD) void agg_kernel(AggArgs p) {
     for (;;) {
       const uint64_t qn = q + 2 * gstride;
       const bool more = qn + gstride < full_pairs;
+      // shared-table kernels: unconditional (the last step reloads this one, unused) — a
+      // load under `if (more)` was issued where its data is consumed, a step late, no
+      // prefetch at all (same-box A/B: G = 1000 2.81 -> 2.73 ms).  The private-accumulator
+      // kernels (Q1, expression shapes) keep the late load: their 6 waves per CU hide it,
+      // and the prefetch's registers cost them (Q1 7.74 -> 7.80, Q12 8.72 -> 8.90 ms)
       Rows<S> nxt;
-      if (more) load_rows<NK, S, VEC, false>(p, rb + 2 * qn, rb + 2 * (qn + gstride), nend, nxt);
+      if (!PRIV) {
+        const uint64_t ql = more ? qn : q;
+        load_rows<NK, S, VEC, false>(p, rb + 2 * ql, rb + 2 * (ql + gstride), nend, nxt);
+      } else if (more) {
+        load_rows<NK, S, VEC, false>(p, rb + 2 * qn, rb + 2 * (qn + gstride), nend, nxt);
+      }
       consume_rows<NK, PRIV, BD, S, false>(p, lt, rb + 2 * q, rb + 2 * (q + gstride), nend, cur, err);
       q = qn;
       if (!more) break;

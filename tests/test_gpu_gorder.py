@@ -70,7 +70,7 @@ def test_ordered_extreme_keys(ex, orc):
     key = pool[rng.integers(0, len(pool), N)]
     key[::100_000] = I64_MIN  # (light enough to stay inside the capped regions)
     key[1::100_000] = I64_MAX
-    val = rng.standard_normal(N)
+    val = rng.random(N)  # (positive: sums of ~8 values without cancellation, so 1e-12 relative holds per group)
     val[::97] = -0.0
     G = len(np.unique(key))
     q = gb_query(dev(key, ex), dev(val, ex))
@@ -131,7 +131,7 @@ def test_capacity_and_auto_size(ex, orc):
     val = orc.gen_column(3, 0x69, N)
     q = gb_query(dev(key, ex), dev(val, ex))
     with pytest.raises(NutError) as ei:
-        ex.groupby_to_host(q, group_hint=G, out=(pinned(G - 1, 1), pinned(G - 1, 4)))
+        ex.groupby_to_host(q, group_hint=G, out=(pinned(G // 2, 1), pinned(G // 2, 4)))
     assert ei.value.status == NUT_ERR_CAPACITY
     k, w = ex.groupby_to_host(q, group_hint=G // 4)  # library-made arrays, resized once
     ok, ow = orc.groupby([key], AGGS4, values=[val])
