@@ -113,7 +113,7 @@ static void run(Ctx &c, const char *name, bool check) {
     CK(hipMemcpy(c.cur, cur0.data(), cur0.size() * 8, hipMemcpyHostToDevice));
     CK(hipEventRecord(c.e0));
     hipLaunchKernelGGL(kern, dim3(grid), dim3(T), 0, 0, ar, (const nut::GpSeg *)c.dseg, (const uint32_t *)dts, ntiles,
-                       64 - BITS, 0, c.cur, 0ull, (uint64_t)BINS * cap, c.cur + BINS);
+                       64 - BITS, 0, c.cur, 0ull, (uint64_t)BINS * cap, c.cur + BINS, nut::GpRange{});
     CK(hipEventRecord(c.e1));
     best = std::min(best, elapsed(c.e0, c.e1));
   }
@@ -165,6 +165,11 @@ int main(int argc, char **argv) {
   printf("records %llu, groups %llu\n", (unsigned long long)c.n, (unsigned long long)groups);
   run<1024, 1>(c, "product <1,1024> (nt stores)", true);
   if (argc > 3) return 0;  // profiling runs: the product variant only
+  run<1024, 1, 7>(c, "<1,1024> nt, 128 bins (G = 1e5)", true);
+  run<512, 1, 7>(c, "<1,512> nt, 128 bins, 2 WG/CU", true);
+  run<512, 1, 6>(c, "<1,512> nt, 64 bins, 2 WG/CU", true);
+  run<1024, 3, 7>(c, "<1,1024> 128 bins no stores", false);
+  run<512, 3, 7>(c, "<1,512> 128 bins no stores", false);
   run<1024, 0>(c, "<1,1024> plain stores", true);
   run<1024, 4>(c, "<1,1024> tile-sequential out", false);
   run<1024, 2>(c, "<1,1024> no stores", false);
