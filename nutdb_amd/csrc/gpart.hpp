@@ -128,7 +128,9 @@ __global__ __launch_bounds__(T) void gp_scatter_kernel(GpArrays ar, const GpSeg 
   __shared__ uint32_t s_tex[BINS];
   __shared__ uint64_t s_gb[BINS];
   __shared__ uint32_t s_wsum[BINS / kWave];
+  __shared__ uint32_t s_run[(VAR & 16) ? BINS : 1];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if ((VAR & 16) && tid < BINS) s_run[tid] = 0;
   uint64_t k1[GP_ITEMS], k2[NK == 2 ? GP_ITEMS : 1];
   // records of tile tt: [lo, lo + n); item i of this lane is record i * T + tid
   auto tile_range = [&](uint32_t tt, uint64_t &lo, uint32_t &n) {
@@ -189,12 +191,16 @@ __global__ __launch_bounds__(T) void gp_scatter_kernel(GpArrays ar, const GpSeg 
       const uint32_t tex = incl - c + add;
       s_tex[tid] = tex;
       const uint64_t cs = gather ? 0 : (uint64_t)s;
-      const uint64_t gb = c ? (uint64_t)atomicAdd(&cursor[cs * BINS + tid], (unsigned long long)c) : 0;
+      // (VAR & 16, timing only: per-workgroup sub-regions instead of the global cursor)
+      const GpSeg &g0 = segs[s];
+      const uint64_t gb = (VAR & 16) ? g0.obase + (uint64_t)tid * g0.ocap + (uint64_t)blockIdx.x * (g0.ocap / gridDim.x) + s_run[tid]
+                          : c ? (uint64_t)atomicAdd(&cursor[cs * BINS + tid], (unsigned long long)c) : 0;
+      if (VAR & 16) s_run[tid] += c;
       // ovf != 0: the capped layout (no histogram pass; GpSeg obase / ocap).  A run past its
       // digit's rows goes to the scratch rows at ovf (>= one tile of them), and the flag
       // after the cursors tells the host to partition again with a histogram
       const GpSeg &g = segs[s];
-      const bool over = ovf && c && gb + c > g.obase + (uint64_t)(tid + 1) * g.ocap;
+      const bool over = !(VAR & 16) && ovf && c && gb + c > g.obase + (uint64_t)(tid + 1) * g.ocap;
       if (over) atomicOr(oflag, 1ull);
       s_gb[tid] = (over ? ovf : gb) - tex;  // out position of tile slot j with digit d = s_gb[d] + j
     }

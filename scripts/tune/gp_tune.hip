@@ -168,6 +168,7 @@ int main(int argc, char **argv) {
   run<1024, 1, 7>(c, "<1,1024> nt, 128 bins (G = 1e5)", true);
   run<512, 1, 7>(c, "<1,512> nt, 128 bins, 2 WG/CU", true);
   run<512, 1, 6>(c, "<1,512> nt, 64 bins, 2 WG/CU", true);
+  run<1024, 17, 7>(c, "<1,1024> 128 bins private cursors", false);
   run<1024, 3, 7>(c, "<1,1024> 128 bins no stores", false);
   run<512, 3, 7>(c, "<1,512> 128 bins no stores", false);
   run<1024, 0>(c, "<1,1024> plain stores", true);
