@@ -605,8 +605,12 @@ struct LocalCfg {
   static constexpr int WAVES = THREADS / kWave;
   static constexpr int CAP = THREADS * MAXK;
   static constexpr int LDS_KEYS = CAP < 16384 ? CAP : 16384;  // 8-B keys per round
-  static constexpr int SB = SB_ ? SB_ : (CAP > 8192 ? 12 : (CAP > 2048 ? 11 : 9));  // bucket bits: ~4-6 keys each
-  static constexpr int WS = WS_ ? WS_ : LS_WS;
+  // bucket bits (~1-6 keys each) and window stride.  The M class (6144 keys) takes 4096
+  // buckets and windows of ~10 keys: scripts/tune/local_tune.hip -DLT_PLAIN on 262144
+  // segments of 4768 keys, two runs: 6.53-6.57 ms vs 6.81-6.85 for 2048 buckets / stride 12
+  // (profiles/r04/sort/local_tune_plain.log)
+  static constexpr int SB = SB_ ? SB_ : (CAP > 4096 ? 12 : (CAP > 2048 ? 11 : 9));
+  static constexpr int WS = WS_ ? WS_ : (CAP > 4096 && CAP <= 8192 ? 10 : LS_WS);
   static constexpr int NB = 1 << SB;
   static constexpr int BPT = NB / THREADS;  // buckets per thread in the scan
   static_assert(BPT * THREADS == NB && BPT <= 8, "whole buckets per thread");

@@ -11,8 +11,10 @@
 #include <vector>
 
 #define NUT_MSD_KERNELS_ONLY
+#ifndef LT_PLAIN  // -DLT_PLAIN: the product kernel as built (no stop checks, no cycle stamps)
 #define NUT_MSD_PROFILE_STOP
 #define NUT_MSD_STAMPS
+#endif
 #include "../../nutdb_amd/csrc/msd_sort.hip"
 
 #define CK(x)                                                       \
@@ -72,18 +74,25 @@ static void run(Ctx &c, const char *name, int stop = 0) {
   CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, T, 0));
   CK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
   const unsigned grid = (unsigned)std::min<uint64_t>(c.nseg, (uint64_t)ncu * per_cu);
+#ifndef LT_PLAIN
   CK(hipMemcpyToSymbol(HIP_SYMBOL(nut::g_ms_stop), &stop, sizeof(int)));
+#else
+  if (stop) return;
+#endif
   nut::MsBufs bf{nullptr, c.dst, c.src, nullptr};
   float best = 1e9;
   unsigned long long st[8] = {0};
   for (int r = 0; r < 3; ++r) {
     CK(hipMemset(c.fb, 0, 4));
+#ifndef LT_PLAIN
     CK(hipMemcpyToSymbol(HIP_SYMBOL(nut::g_ms_stamp), st, sizeof(st)));
+#endif
     CK(hipEventRecord(c.e0));
     hipLaunchKernelGGL(kern, dim3(grid), dim3(T), 0, 0, bf, (const nut::MsSeg *)c.dseg, c.nseg, 0ull, c.fb);
     CK(hipEventRecord(c.e1));
     best = std::min(best, elapsed(c.e0, c.e1));
   }
+#ifndef LT_PLAIN
   CK(hipMemcpyFromSymbol(st, HIP_SYMBOL(nut::g_ms_stamp), sizeof(st)));
   if (!stop) {
     printf("   cycles per segment (thread 0 of each workgroup):");
@@ -91,6 +100,7 @@ static void run(Ctx &c, const char *name, int stop = 0) {
     for (int k = 0; k < 6; ++k) printf(" %s %.0f", ph[k], (double)st[k] / c.nseg);
     printf("\n");
   }
+#endif
   uint32_t nfb = 0;
   CK(hipMemcpy(&nfb, c.fb, 4, hipMemcpyDeviceToHost));
   unsigned long long h[2] = {0, 0};
@@ -135,12 +145,23 @@ int main(int argc, char **argv) {
     printf("%-28s                 %7.3f ms  %6.0f GB/s\n", "copy (HBM floor)", best, 16.0 * c.n / best / 1e6);
   }
   printf("segments %u x %u keys\n", c.nseg, c.seglen);
-  run<512, 12, 0, 0>(c, "default <512,12> SB11 WS12");
+  run<512, 12, 0, 0>(c, "default <512,12> (SB12 WS10)");
+  run<512, 12, 11, 12>(c, "<512,12> SB11 WS12 (round-4 product)");
   if (argc > 3) return 0;  // profiling runs: the product variant only
   run<512, 12, 12, 12>(c, "<512,12> SB12 WS12");
   run<512, 12, 12, 10>(c, "<512,12> SB12 WS10");
   run<512, 12, 12, 8>(c, "<512,12> SB12 WS8");
   run<512, 12, 11, 8>(c, "<512,12> SB11 WS8");
+  // odd window strides: window starts ~WS keys apart land on 2-bank pairs WS * lane mod 32,
+  // a full cycle for odd WS (WS = 12: a cycle of 8, i.e. 4 lanes per bank pair before noise)
+  run<512, 12, 11, 11>(c, "<512,12> SB11 WS11");
+  run<512, 12, 11, 13>(c, "<512,12> SB11 WS13");
+  run<512, 12, 11, 9>(c, "<512,12> SB11 WS9");
+  run<512, 12, 12, 11>(c, "<512,12> SB12 WS11");
+  run<512, 12, 12, 9>(c, "<512,12> SB12 WS9");
+  run<512, 12, 0, 0>(c, "default again (order check)");
+  run<512, 12, 12, 10>(c, "<512,12> SB12 WS10 again");
+  run<512, 12, 11, 11>(c, "<512,12> SB11 WS11 again");
   run<512, 12, 0, 0>(c, "default: load only", 1);
   run<512, 12, 0, 0>(c, "default: + ranks/stage", 3);
   run<512, 12, 0, 0>(c, "default: + windows", 4);
