@@ -116,7 +116,7 @@ typedef enum {
   NUT_OPT_GB_DENSE = 9,        /* 1 (default): whole partitions append their groups unhashed */
   NUT_OPT_GB_L1_BITS = 10,     /* digit bits of a capped second partition level, 6..8 (6) */
   NUT_OPT_TOPK = 11,           /* 1 (default): plans with ORDER BY ... LIMIT sort only nut_topk_positions' rows */
-  NUT_OPT_GB_L0_BITS = 12,     /* digit bits of a capped first partition level, 6..8; 0 (default): 7 for one level up to 150 K groups, else 8 */
+  NUT_OPT_GB_L0_BITS = 12,     /* digit bits of a capped first partition level, 6..8; 0 (default): 7 for one level up to 150 K groups, else 8; nut_groupby_to_host's ordered path: 7, with 14 - bits at level 1 */
   NUT_OPT_STREAM_BLOCKS = 13,  /* nut_stream_probe: workgroups per CU, 0 (default) = 8 */
   NUT_OPT_PRIV_BD = 14,        /* compiled Q1 kernel: threads per workgroup 128 / 192 / 256; 0 (default) = 192 */
   NUT_OPT_PRIV_BLOCKS = 15,    /* compiled Q1 kernel: at most this many workgroups per CU; 0 (default) = 2 */

@@ -939,7 +939,12 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
                c->opt[NUT_OPT_GB_LEVELS] != 1 && c->opt[NUT_OPT_GB_DENSE] != 0 && na >= 1 && n >= (1ull << 24) &&
                n >= 4 * group_hint && host_pinned_ptr(keys_h) && host_pinned_ptr(aggs_h) && cap > 0;
   for (int a = 0; a < na && shape; ++a) shape = s->agg_op[a] == NUT_AGG_COUNT || s->agg_expr[a] == NUT_EX_COL;
-  constexpr int bits0 = 8, bits1 = 6;
+  // the 2^14 range cells split into a level-0 and a level-1 digit (NUT_OPT_GB_L0_BITS 6..8;
+  // default 7 + 7: level 0's runs twice as long as at 8 + 6 for level 1's half as long —
+  // same-box A/B at G = 1e7, 1e9 rows, three rounds: step 21.63-21.81 ms vs 22.44-22.56
+  // (8 + 6) and 22.48-22.56 (6 + 8), profiles/r04/groupby1e7/ab_l0bits.txt)
+  const int bits0 = c->opt[NUT_OPT_GB_L0_BITS] >= 6 && c->opt[NUT_OPT_GB_L0_BITS] <= 8 ? (int)c->opt[NUT_OPT_GB_L0_BITS] : 7;
+  const int bits1 = 14 - bits0;
   const double lam = (double)group_hint / (double)(1 << (bits0 + bits1));
   if (!shape || lam < 100 || ((uintptr_t)s->keys[0] & 15)) return NUT_ERR_UNSUPPORTED;
   hipStream_t st = c->stream;
@@ -999,7 +1004,7 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
   c->gb_path = NUT_GB_PARTITIONED_ORDERED;
   c->gb_levels = 2;
   c->gb_optimistic = 2;
-  // ---- level 0 (range digit = cell >> 6)
+  // ---- level 0 (range digit = cell >> bits1)
   const uint64_t ocap = ((2 * rows - 2 * GP_TILE) >> bits0) & ~1ull;
   std::vector<GpSeg> segs{GpSeg{0, n, 0, 0}};
   segs[0].ocap = ocap;
