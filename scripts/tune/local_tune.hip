@@ -159,6 +159,8 @@ int main(int argc, char **argv) {
   run<512, 12, 11, 9>(c, "<512,12> SB11 WS9");
   run<512, 12, 12, 11>(c, "<512,12> SB12 WS11");
   run<512, 12, 12, 9>(c, "<512,12> SB12 WS9");
+  run<1024, 6, 0, 0>(c, "<1024,6> SB12 WS10");
+  run<1024, 6, 12, 12>(c, "<1024,6> SB12 WS12");
   run<512, 12, 0, 0>(c, "default again (order check)");
   run<512, 12, 12, 10>(c, "<512,12> SB12 WS10 again");
   run<512, 12, 11, 11>(c, "<512,12> SB11 WS11 again");
