@@ -53,6 +53,8 @@ def parse():
                                                    "parse"])
     p.add_argument("--rows", type=float, default=None, help="rows per GPU (default: config size)")
     p.add_argument("--groups", type=int, default=1000, help="groupby: distinct keys")
+    p.add_argument("--skew", action="store_true",
+                   help="groupby: Zipf-like keys from the same pool (pool index i on ~1/i of the rows)")
     p.add_argument("--selectivity", type=float, default=0.5, help="filter: fraction selected")
     p.add_argument("--key-range", type=float, default=None, metavar="FRACTION",
                    help="sort: keys uniform over this fraction of the int64 range (a sample-sort rank's share)")
@@ -119,12 +121,13 @@ class GroupBy:
     cols_bytes = 16
     kernel_kind = 1
 
-    def __init__(self, ex, rows, row0, groups):
+    def __init__(self, ex, rows, row0, groups, skew=False):
         from nutdb_amd.workloads import groupby_cols, gen
         self.ex = ex
         self.G = groups
+        self.skew = skew
         self.groups_hint = groups
-        self.key, self.val = [gen(ex, spec, rows, row0=row0) for spec in groupby_cols(groups, dyadic=True)]
+        self.key, self.val = [gen(ex, spec, rows, row0=row0) for spec in groupby_cols(groups, dyadic=True, skew=skew)]
         self.rows = rows
         self.out = None
 
@@ -163,7 +166,8 @@ class GroupBy:
 
     def config(self):
         return {"workload": self.name, "query": "SELECT key, SUM(val) FROM t GROUP BY key", "groups": self.G,
-                "columns": "i64 key + f64 val (dyadic)", "bytes_per_row": 16}
+                "keys": "Zipf-like (GEN_SKEW_KEY, pool index i on ~1/i of the rows)" if self.skew
+                else "uniform over the pool", "columns": "i64 key + f64 val (dyadic)", "bytes_per_row": 16}
 
 
 class Filter:
@@ -453,7 +457,7 @@ def cpu_baseline(args, workload: str, target_s: float):
             return lambda: orc.groupby([rf, ls], [(0, 0, (0,)), (0, 0, (1,)), (0, 4, (1, 2)), (1, 0, ())],
                                        values=[qty, price, disc], preds=[(sd, 1, Q1_DATE_K)], cap=64)
         if workload == "groupby":
-            key, val = [orc.gen(s, n) for s in groupby_cols(args.groups, dyadic=True)]
+            key, val = [orc.gen(s, n) for s in groupby_cols(args.groups, dyadic=True, skew=args.skew)]
             return lambda: orc.groupby([key], [(0, 0, (0,))], values=[val], cap=max(args.groups, 1))
         if workload == "sort":
             col = orc.gen(sort_col(args.key_range), n)
@@ -461,19 +465,20 @@ def cpu_baseline(args, workload: str, target_s: float):
         if workload == "q12join":
             o, li = q12j_tables(lambda k, seed, m, a, b: orc.gen_column(k, seed, m, a=a, b=b), n)
 
-            def q12():
-                m = (np.isin(li["l_shipmode"], [3, 5]) & (li["l_commitdate"] < li["l_receiptdate"])
-                     & (li["l_shipdate"] < li["l_commitdate"]))
-                ids = np.nonzero(m)[0]
+            lcols = [li["l_shipmode"], li["l_commitdate"], li["l_receiptdate"], li["l_shipdate"]]
+            where = [("col", 0), ("i64", 0, 3), ("eq",), ("col", 0), ("i64", 0, 5), ("eq",), ("or",), ("col", 1),
+                     ("col", 2), ("lt",), ("and",), ("col", 3), ("col", 1), ("lt",), ("and",)]
+
+            def q12():  # the pushed-down WHERE in C on every core (orc_eval_int), then the join
+                ids = np.flatnonzero(orc.eval_int(where, lcols, n))
                 pi, bi = orc.join_i64_c(o["o_orderkey"], li["l_orderkey"][ids], "inner")
                 pr, mode = o["o_orderpriority"][bi], li["l_shipmode"][ids[pi]]
                 hi = (pr == 1) | (pr == 2)
                 return [(s_, int(np.sum(hi & (mode == s_))), int(np.sum(~hi & (mode == s_)))) for s_ in (3, 5)]
             return q12
-        if workload == "scanexpr":
-            from oracle.expr import eval_prog
+        if workload == "scanexpr":  # the WHERE program in C on every core, numpy compaction
             a, b = orc.gen_column(1, 0x81, n), orc.gen_column(1, 0x82, n)
-            return lambda: a[eval_prog([("col", 0), ("col", 1), ("lt",)], [a, b], n)[0] != 0]
+            return lambda: a[orc.eval_int([("col", 0), ("col", 1), ("lt",)], [a, b], n) != 0]
         if workload == "join":  # the columns of bench's Join (same generator, rank 0)
             nb = n // 4
             b = orc.gen_column(0, 0x71, nb)
@@ -485,7 +490,7 @@ def cpu_baseline(args, workload: str, target_s: float):
             from nutdb_amd.workloads import Q12_AGGS, Q12_COLS, Q12_WHERE
             from oracle.expr import groupby_prog
             cols = [orc.gen(s, n) for s in Q12_COLS]
-            return lambda: groupby_prog([cols[2]], cols, Q12_WHERE, Q12_AGGS)
+            return lambda: groupby_prog([cols[2]], cols, Q12_WHERE, Q12_AGGS, threads=threads, engine="c")
         col = orc.gen(FILTER_COL, n)
         k = filter_k(args.selectivity)
         return lambda: orc.filter_i64(col, 0, k)
@@ -515,13 +520,17 @@ def cpu_baseline(args, workload: str, target_s: float):
         how, cores = (f"C hash join (oracle/oracle.c orc_join_i64: CSR bucket table + two-pass probe), OpenMP "
                       f"over {threads} host threads; probe rows, build = probe/4"), threads
     elif workload == "scanexpr":
-        how, cores = "numpy expression oracle (oracle/expr.py) + boolean compaction, 1 host thread", 1
+        how, cores = (f"C expression evaluator (oracle/oracle.c orc_eval_int, OpenMP over {threads} host threads) + "
+                      f"numpy boolean compaction (1 thread)"), threads
     elif workload == "q12join":
-        how, cores = (f"numpy filter (pushed down, 1 thread) + C hash join (oracle/oracle.c, OpenMP over {threads} "
-                      f"threads) + numpy CASE sums"), threads
+        how, cores = (f"C expression evaluator for the pushed-down WHERE + C hash join (oracle/oracle.c, OpenMP over "
+                      f"{threads} threads) + numpy CASE sums"), threads
     elif workload == "q12expr":
-        how, cores = (f"numpy expression oracle (oracle/expr.py, 1 thread) + C oracle group-by (oracle/oracle.c, "
-                      f"OpenMP over {threads} host threads)"), threads
+        how, cores = (f"C expression evaluator (oracle/oracle.c orc_eval_int) + C oracle group-by, OpenMP over "
+                      f"{threads} host threads"), threads
+    elif workload == "groupby":
+        how, cores = (f"C oracle (oracle/oracle.c orc_groupby: per-thread tables for few groups, key-range "
+                      f"partitioned per-partition merge for many), OpenMP over {threads} host threads"), threads
     else:
         how, cores = f"C oracle (oracle/oracle.c), OpenMP over {threads} host threads", threads
     del fn
@@ -672,6 +681,8 @@ def main():
     kern_ms, launches = (ex if nd is None else nd).kernel_time(w.kernel_kind)
     (ex if nd is None else nd).enable_timing(False)
     gb_stats = ex.groupby_stats() if nd is None and args.workload in ("q1", "groupby", "q12expr", "q12join") else None
+    if gb_stats is not None and gb_stats["path"] == "partitioned_ordered":
+        gb_stats["overflow_rows"] = ex.groupby_overflow_rows()
     if nd is not None:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -714,6 +725,26 @@ def main():
                       "achieved": bytes_per_step / (probe_ms * 1e-3) / 1e9,
                       "frac_of_peak": bytes_per_step / (probe_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                       "kernel_frac_of_copy": probe_ms / avg_kernel_ms}
+    # the compiled Q1 kernel's launch shapes on this board (untimed, after the timed loop):
+    # the shape the library's probe chose, and each candidate's kernel time over the same
+    # full-size step (3 runs each, best), next to the copy floor above
+    shapes = None
+    if args.workload == "q1" and nd is None and rank == 0 and not args.no_copy_floor:
+        shapes = {"chosen": ex.priv_shape(), "kernel_ms_full_size": {}}
+        for bd, bl in ((192, 2), (128, 3), (128, 4)):
+            old = ex.set_option("priv_bd", bd), ex.set_option("priv_blocks", bl)
+            best = None
+            for _ in range(3):
+                ex.enable_timing(True)
+                w.run()
+                ms, n = ex.kernel_time(w.kernel_kind)
+                ex.enable_timing(False)
+                best = ms / max(n, 1) if best is None else min(best, ms / max(n, 1))
+            ex.set_option("priv_bd", old[0])
+            ex.set_option("priv_blocks", old[1])
+            shapes["kernel_ms_full_size"][f"{bd}x{bl}"] = round(best, 4)
+        if copy_floor:
+            shapes["copy_floor_ms"] = copy_floor["ms"]
     parity = None
     cpu = None
     if rank == 0 and world == 1 and nd is None and not args.no_cpu_baseline:
@@ -725,7 +756,8 @@ def main():
             from nutdb_amd.workloads import GB_KEY_SEED, GB_VAL_SEED
             del cpu_res
             t0 = time.perf_counter()
-            ok, ow = orc.groupby_pool_dyadic(args.groups, rows, row0=0, key_seed=GB_KEY_SEED, val_seed=GB_VAL_SEED)
+            ok, ow = orc.groupby_pool_dyadic(args.groups, rows, row0=0, key_seed=GB_KEY_SEED, val_seed=GB_VAL_SEED,
+                                             kind=7 if args.skew else 2)
             cpu_res = (ok, np.ascontiguousarray(ow[:, :1]))
             sample = rows
             how = ("last timed step vs the indexed dense-array oracle (oracle.h orc_groupby_pool_dyadic, "
@@ -751,6 +783,8 @@ def main():
             cfg["groupby_path"] = gb_stats
         if options:
             cfg["options"] = options
+        if shapes is not None:
+            cfg["launch_shape"] = shapes
         if nd is not None:
             cfg["dist"] = {"api": "nut_dist_create_rank + nut_dist_* (libnutexec.so, RCCL)", "nranks": nd.nranks,
                            "control_plane": "torch.distributed gloo (unique id, barriers, max time)"}
@@ -794,7 +828,7 @@ def make_workload(args, ex, rows, row0, world, rank):
     if args.workload == "q1":
         return Q1(ex, rows, row0)
     if args.workload == "groupby":
-        return GroupBy(ex, rows, row0, args.groups)
+        return GroupBy(ex, rows, row0, args.groups, args.skew)
     if args.workload == "sort":
         return Sort(ex, rows, row0, world, args.key_range)
     if args.workload == "q12expr":

@@ -99,6 +99,15 @@ typedef enum {
   NUT_GB_PARTITIONED_ORDERED = 3 /* nut_groupby_to_host: key-range partitions, ordered per partition, streamed to the host */
 } nut_groupby_path;
 nut_status nut_ctx_groupby_stats(nut_ctx *ctx, uint32_t *path, uint32_t *levels, uint32_t *optimistic);
+/* Rows of the last nut_groupby_to_host on the ordered path (NUT_GB_PARTITIONED_ORDERED)
+ * that did not fit their capped partition regions — a heavy key's excess, mostly — and
+ * were aggregated from its overflow arenas and folded into the result (0: none). */
+nut_status nut_ctx_groupby_overflow(nut_ctx *ctx, uint64_t *rows);
+/* The compiled Q1 kernel's launch shape on this context's device (NUT_OPT_PRIV_PROBE):
+ * threads per workgroup and workgroups per CU the next launch takes, and the probe's best
+ * kernel time per candidate shape {192 x 2, 128 x 3, 128 x 4} in ms (-1: not probed in
+ * this process). */
+nut_status nut_ctx_priv_shape(nut_ctx *ctx, int *threads, int *blocks_per_cu, double probe_ms[3]);
 
 /* Algorithm options of one context, for tuning A/B runs and tests that drive a path at
  * a size where the planner would not pick it.  The defaults are the product choice;
@@ -118,13 +127,14 @@ typedef enum {
   NUT_OPT_TOPK = 11,           /* 1 (default): plans with ORDER BY ... LIMIT sort only nut_topk_positions' rows */
   NUT_OPT_GB_L0_BITS = 12,     /* digit bits of a capped first partition level, 6..8; 0 (default): 7 for one level up to 150 K groups, else 8; nut_groupby_to_host's ordered path: 7, with 14 - bits at level 1 */
   NUT_OPT_STREAM_BLOCKS = 13,  /* nut_stream_probe: workgroups per CU, 0 (default) = 8 */
-  NUT_OPT_PRIV_BD = 14,        /* compiled Q1 kernel: threads per workgroup 128 / 192 / 256; 0 (default) = 192 */
-  NUT_OPT_PRIV_BLOCKS = 15,    /* compiled Q1 kernel: at most this many workgroups per CU; 0 (default) = 2 */
+  NUT_OPT_PRIV_BD = 14,        /* compiled Q1 kernel: threads per workgroup 128 / 192 / 256; 0 (default) = the probed shape (NUT_OPT_PRIV_PROBE), else 192 */
+  NUT_OPT_PRIV_BLOCKS = 15,    /* compiled Q1 kernel: at most this many workgroups per CU; 0 (default) = the probed shape, else 2 */
   NUT_OPT_AGG_BLOCKS = 16,     /* shared-table streaming group-by: at most this many workgroups per CU; 0 (default) = as LDS allows */
   NUT_OPT_SEL_BLOCKS = 17,     /* expression scans (nut_select_rows): persistent workgroups per CU; 0 (default) = 8 */
   NUT_OPT_SORT_BD = 18,        /* sort, capped scatter levels: threads per workgroup 1024 (0, default) or 512 (two per CU) */
   NUT_OPT_GB_ORDERED = 19,     /* nut_groupby_to_host: the range-partitioned ordered path where it applies (1, default) or the hashed path + ordering (0) */
-  NUT_OPT_COUNT = 20
+  NUT_OPT_PRIV_PROBE = 20,     /* 1 (default): the first compiled-Q1-shape group-by of >= 2^27 rows on a device times the kernel at 192 x 2, 128 x 3 and 128 x 4 threads x workgroups per CU on its first 2^28 rows (discarded) and keeps the fastest for that device (nut_ctx_priv_shape); 0: 192 x 2 */
+  NUT_OPT_COUNT = 21
 } nut_option;
 nut_status nut_ctx_set_option(nut_ctx *ctx, int option, int64_t value);
 nut_status nut_ctx_get_option(nut_ctx *ctx, int option, int64_t *value);
@@ -141,7 +151,10 @@ typedef enum {
   NUT_GEN_DYADIC = 3,    /* f64: (u >> 44) / 64                   */
   NUT_GEN_UNIT_F64 = 4,  /* f64: (u >> 11) * 2^-53                */
   NUT_GEN_RANGE_I64 = 5, /* int64: a + u % b                      */
-  NUT_GEN_RANGE_F64 = 6  /* f64: (double)(a + u % b) / c          */
+  NUT_GEN_RANGE_F64 = 6, /* f64: (double)(a + u % b) / c          */
+  NUT_GEN_SKEW_KEY = 7   /* int64: mix64(((u % a) >> ((mix64(u) >> 59) * 3 >> 2)) ^ 0x5DEECE66D2545F49) —
+                            a log-uniform (Zipf-like, exponent ~1) draw of a distinct keys: pool index 0
+                            takes ~3 %, index i ~ 1 / i of the rows */
 } nut_gen_kind;
 
 nut_status nut_gen_column(nut_ctx *ctx, int kind, uint64_t seed, int64_t a, int64_t b,

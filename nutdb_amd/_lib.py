@@ -37,7 +37,7 @@ STATUS_NAMES = {
 }
 
 # enums (include/nutexec.h)
-GEN_U62, GEN_FULL_I64, GEN_POOL_KEY, GEN_DYADIC, GEN_UNIT_F64, GEN_RANGE_I64, GEN_RANGE_F64 = range(7)
+GEN_U62, GEN_FULL_I64, GEN_POOL_KEY, GEN_DYADIC, GEN_UNIT_F64, GEN_RANGE_I64, GEN_RANGE_F64, GEN_SKEW_KEY = range(8)
 LT, LE, GT, GE, EQ, NE, IN, NOT_IN = range(8)
 T_I64, T_F64, T_STR = 0, 1, 2
 COL_KINDS = ["int", "uint", "float", "bool", "date", "datetime", "string", "enum"]
@@ -134,6 +134,8 @@ SIGNATURES = {
     "nut_ctx_kernel_time": (_I32, [_P, _I32, C.POINTER(C.c_double), C.POINTER(_U64)]),
     "nut_ctx_sort_stats": (_I32, [_P, C.POINTER(_U64), C.POINTER(C.c_uint32)]),
     "nut_ctx_groupby_stats": (_I32, [_P, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
+    "nut_ctx_groupby_overflow": (_I32, [_P, C.POINTER(_U64)]),
+    "nut_ctx_priv_shape": (_I32, [_P, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_double)]),
     "nut_ctx_set_option": (_I32, [_P, _I32, _I64]),
     "nut_ctx_get_option": (_I32, [_P, _I32, C.POINTER(_I64)]),
     "nut_join_i64": (_I32, [_P, _P, _U64, _P, _U64, _I32, C.POINTER(_P), C.POINTER(_U64)]),

@@ -6,6 +6,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <mutex>
 #include <vector>
 
 #include "agg_kernel.hpp"
@@ -292,7 +293,26 @@ struct LaunchExtra {
   bool dense = false;                      // every segment a whole partition (AggArgs::dense)
   unsigned long long *dcount = nullptr;    // dense staging (AggArgs::dcount / dregion / dbase)
   uint64_t dregion = 0, dbase = 0;
+  bool dry = false;       // compute the launch configuration only (nothing is launched)
+  bool q1_fused = false;  // out (dry): the launch takes the compiled Q1 kernel
 };
+
+// The compiled Q1 kernel's launch shapes, threads x workgroups per CU.  All run 6-8 waves
+// per CU; which one streams the six columns best differs between boards (the driver's box
+// reached 0.929 of its copy floor at 192 x 2 where builder boxes reached 0.97-1.0), so the
+// first large launch on a device times each (probe_priv_shape) and the device keeps the
+// fastest for the process.
+constexpr int kPrivShapes[3][2] = {{192, 2}, {128, 3}, {128, 4}};
+struct PrivShape {
+  int shape = -1;  // index into kPrivShapes; -1: not probed (192 x 2)
+  double ms[3] = {-1, -1, -1};
+};
+static PrivShape g_priv_shape[64];
+static std::mutex g_priv_mu;
+static PrivShape priv_shape_of(int dev) {
+  std::lock_guard<std::mutex> lk(g_priv_mu);
+  return dev >= 0 && dev < 64 ? g_priv_shape[dev] : PrivShape{};
+}
 
 // the on-chip table of a launch: 4x the expected groups (load <= 1/4: a key almost always
 // sits in its 4-slot home bucket) within the LDS budget; segment mode: NUT_OPT_GB_SEG_SLOTS x
@@ -375,8 +395,19 @@ nut_status launch_agg(nut_groups *g, const nut_agg_spec *s, uint64_t group_hint,
   const bool q1_tuned = priv && ((shape == SHAPE_Q1 && !s->prog_mode && a.vec) || s->prog_mode);
   // the Q1 kernel runs 6 waves per CU (2 x 192 threads): 8 waves issue too many
   // concurrent six-column streams (7.85 vs 7.27 ms at 1e9 rows, same box), 4 leave its
-  // fold's latency exposed (8.7 ms) — NUT_OPT_PRIV_BD / _BLOCKS override for sweeps
-  const int bd = !priv ? kBdShared : !q1_tuned ? kBdPriv : c->opt[NUT_OPT_PRIV_BD] ? (int)c->opt[NUT_OPT_PRIV_BD] : 192;
+  // fold's latency exposed (8.7 ms) — NUT_OPT_PRIV_BD / _BLOCKS override for sweeps.  The
+  // compiled (fused) Q1 kernel takes the shape its device's probe chose (kPrivShapes).
+  const bool q1_fused = q1_tuned && !s->prog_mode;
+  int pbd = 192, pblocks = 2;
+  if (q1_fused) {
+    const int k = c->priv_probe >= 0 ? c->priv_probe : priv_shape_of(c->device).shape;
+    if (k >= 0) pbd = kPrivShapes[k][0], pblocks = kPrivShapes[k][1];
+  }
+  if (ex && ex->dry) {
+    ex->q1_fused = q1_fused;
+    return NUT_OK;
+  }
+  const int bd = !priv ? kBdShared : !q1_tuned ? kBdPriv : c->opt[NUT_OPT_PRIV_BD] ? (int)c->opt[NUT_OPT_PRIV_BD] : pbd;
   a.lds_cap = lcap;
   a.lds_limit = lcap - lcap / 4;
   a.lds_log2 = lcap ? ilog2(lcap) : 0;
@@ -384,7 +415,9 @@ nut_status launch_agg(nut_groups *g, const nut_agg_spec *s, uint64_t group_hint,
   a.gt = g->dev_gt;
   const size_t lb = lds_bytes(lcap, g->nk, na, priv, P, bd);
   int blocks_per_cu = lb ? (int)std::max<size_t>(1, std::min<size_t>(bd == 512 ? 4 : 8, lds_max / lb)) : 4;
-  if (q1_tuned) blocks_per_cu = std::min<int>(blocks_per_cu, c->opt[NUT_OPT_PRIV_BLOCKS] ? (int)c->opt[NUT_OPT_PRIV_BLOCKS] : 2);
+  if (q1_tuned)
+    blocks_per_cu = std::min<int>(blocks_per_cu, c->opt[NUT_OPT_PRIV_BLOCKS] ? (int)c->opt[NUT_OPT_PRIV_BLOCKS]
+                                                 : q1_fused ? pblocks : 2);
   if (!priv && c->opt[NUT_OPT_AGG_BLOCKS]) blocks_per_cu = std::min<int>(blocks_per_cu, (int)c->opt[NUT_OPT_AGG_BLOCKS]);
   uint64_t pairs = (s->n + 1) / 2;
   uint64_t blocks = std::min<uint64_t>((uint64_t)c->num_cus * blocks_per_cu, (pairs + bd - 1) / bd);
@@ -528,11 +561,11 @@ uint32_t gp_tiles(std::vector<GpSeg> &segs, uint32_t tile, std::vector<uint32_t>
 // one key (rg: GpRange, t >= 0 ... the ordered group-by)
 void gp_capped_launch(nut_ctx *c, const GpArrays &ar, const GpSeg *dseg, const uint32_t *dts, uint32_t nst, int shift,
                       unsigned long long *dcur, uint64_t kx, uint64_t ovf, unsigned long long *dflag, int bits,
-                      bool two_keys, const GpRange *rg) {
+                      bool two_keys, const GpRange *rg, unsigned long long *acur = nullptr, uint64_t acap = 0) {
   if (!nst) return;
   const unsigned grid = std::min<unsigned>(nst, (unsigned)c->num_cus);
   using SK = void (*)(GpArrays, const GpSeg *, const uint32_t *, uint32_t, int, int, unsigned long long *, uint64_t,
-                      uint64_t, unsigned long long *, GpRange);
+                      uint64_t, unsigned long long *, GpRange, unsigned long long *, uint64_t);
   static const SK kern[3][3] = {
       {gp_scatter_kernel<1, 1024, 1, 6>, gp_scatter_kernel<1, 1024, 1, 7>, gp_scatter_kernel<1, 1024, 1, 8>},
       {gp_scatter_kernel<2, 1024, 1, 6>, gp_scatter_kernel<2, 1024, 1, 7>, gp_scatter_kernel<2, 1024, 1, 8>},
@@ -540,7 +573,7 @@ void gp_capped_launch(nut_ctx *c, const GpArrays &ar, const GpSeg *dseg, const u
        gp_scatter_kernel<1, 1024, 1, 8, true>}};
   const int kv = rg ? 2 : two_keys ? 1 : 0;
   hipLaunchKernelGGL(kern[kv][bits - 6], dim3(grid), dim3(1024), 0, c->stream, ar, dseg, dts, nst, shift, 0, dcur, kx,
-                     ovf, dflag, rg ? *rg : GpRange{});
+                     ovf, dflag, rg ? *rg : GpRange{}, acur, acap);
 }
 
 // one partition level: histogram + scatter of every segment; returns the 256 counts per
@@ -552,7 +585,7 @@ void gp_capped_launch(nut_ctx *c, const GpArrays &ar, const GpSeg *dseg, const u
 nut_status gp_level(nut_ctx *c, GpMeta &mm, std::vector<GpSeg> &segs, int shift, const uint64_t *const *src,
                     uint64_t *const *dst, int narr, bool gather, bool have_hist, std::vector<uint64_t> &hist,
                     std::vector<uint64_t> *parts = nullptr, uint64_t kx = 0, uint64_t ovf = 0, int bits = 8,
-                    const GpRange *rg = nullptr) {
+                    const GpRange *rg = nullptr, unsigned long long *acur = nullptr, uint64_t acap = 0) {
   hipStream_t st = c->stream;
   std::vector<uint32_t> ts;
   nut_status s;
@@ -589,7 +622,7 @@ nut_status gp_level(nut_ctx *c, GpMeta &mm, std::vector<GpSeg> &segs, int shift,
     ar.narr = narr;
     unsigned long long *dflag = (unsigned long long *)dcur + nc;
     gp_capped_launch(c, ar, dseg, dts, nst, shift, (unsigned long long *)dcur, kx, ovf, dflag, bits, src[2] != nullptr,
-                     rg);
+                     rg, acur, acap);
     NUT_HIP(hipGetLastError());
     std::vector<uint64_t> back(cur.size());
     NUT_HIP(hipMemcpyAsync(back.data(), dcur, back.size() * 8, hipMemcpyDeviceToHost, st));
@@ -930,6 +963,72 @@ bool host_pinned_ptr(const void *p) {
 // placement, and most of the transfer hidden.  NUT_ERR_UNSUPPORTED: not this shape, or the
 // keys' spread or a partition overflowed the capped layout — the caller takes the hashed
 // path (the host arrays may hold partial output then; it rewrites them).
+
+// Fold groups sorted by key (hk, hw: result words, SELECT order) into a sorted host result
+// of n groups with room for cap: equal keys combine by kind (SUM f64 adds, SUM i64 / COUNT
+// wrap-add, MIN / MAX of f64 in the tables' total order: -0 < +0, NaN above +inf), the rest
+// are merged in by one backward pass.  Returns the new count; *over when it exceeds cap
+// (the result is then left as it was).
+static uint64_t fold_sorted_groups(int64_t *keys, uint64_t *aggs, uint64_t n, uint64_t cap,
+                                   const std::vector<int64_t> &hk, const std::vector<uint64_t> &hw,
+                                   const int32_t *kinds, int na, bool *over) {
+  const uint64_t m = hk.size();
+  auto ord = [](uint64_t b) { return (b >> 63) ? ~b : (b | 0x8000000000000000ull); };
+  auto combine = [&](uint64_t *dst, const uint64_t *src) {
+    for (int a = 0; a < na; ++a) {
+      uint64_t &x = dst[a];
+      const uint64_t y = src[a];
+      switch (kinds[a]) {
+        case AK_SUM_F64: {
+          double dx, dy;
+          memcpy(&dx, &x, 8);
+          memcpy(&dy, &y, 8);
+          dx += dy;
+          memcpy(&x, &dx, 8);
+          break;
+        }
+        case AK_MIN_F64: x = ord(y) < ord(x) ? y : x; break;
+        case AK_MAX_F64: x = ord(y) > ord(x) ? y : x; break;
+        case AK_MIN_I64: x = (int64_t)y < (int64_t)x ? y : x; break;
+        case AK_MAX_I64: x = (int64_t)y > (int64_t)x ? y : x; break;
+        default: x += y; break;  // SUM i64, COUNT
+      }
+    }
+  };
+  uint64_t fresh = 0;  // keys not in the result yet
+  for (uint64_t i = 0, j = 0; j < m;) {
+    if (i < n && keys[i] < hk[j]) {
+      ++i;
+    } else if (i < n && keys[i] == hk[j]) {
+      ++i, ++j;
+    } else {
+      ++fresh, ++j;
+    }
+  }
+  if (n + fresh > cap) {
+    *over = true;
+    return n + fresh;
+  }
+  uint64_t i = n, j = m, w = n + fresh;  // backward merge: the write position never passes i
+  while (j > 0) {
+    if (i > 0 && keys[i - 1] > hk[j - 1]) {
+      --i, --w;
+      keys[w] = keys[i];
+      memmove(aggs + w * na, aggs + i * na, (size_t)na * 8);
+    } else if (i > 0 && keys[i - 1] == hk[j - 1]) {
+      --i, --j, --w;
+      keys[w] = keys[i];
+      memmove(aggs + w * na, aggs + i * na, (size_t)na * 8);
+      combine(aggs + w * na, &hw[j * na]);
+    } else {
+      --j, --w;
+      keys[w] = hk[j];
+      memcpy(aggs + w * na, &hw[j * na], (size_t)na * 8);
+    }
+  }
+  return n + fresh;
+}
+
 nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hint, int64_t *keys_h, uint64_t *aggs_h,
                            uint64_t cap, uint64_t *n_out) {
   const uint64_t n = s->n;
@@ -946,6 +1045,7 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
   const int bits0 = c->opt[NUT_OPT_GB_L0_BITS] >= 6 && c->opt[NUT_OPT_GB_L0_BITS] <= 8 ? (int)c->opt[NUT_OPT_GB_L0_BITS] : 7;
   const int bits1 = 14 - bits0;
   const double lam = (double)group_hint / (double)(1 << (bits0 + bits1));
+  c->gb_overflow_rows = 0;
   if (!shape || lam < 100 || ((uintptr_t)s->keys[0] & 15)) return NUT_ERR_UNSUPPORTED;
   hipStream_t st = c->stream;
   // ---- the key range from a strided sample (+ 1/1024 of the span on either side)
@@ -968,6 +1068,25 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
   if (rg.span < (1ull << 16)) return NUT_ERR_UNSUPPORTED;  // (mul must fit 32 bits; tiny spans hash fine)
   rg.t = rg.span >> 32 ? 32 - __builtin_clzll(rg.span) : 0;
   rg.mul = (uint32_t)((1ull << 46) / ((rg.span >> rg.t) + 1));
+  {  // admission: the sample's distinct keys spread over the level-0 partitions.  Keys
+     // clustered inside the sampled range would overfill some partitions' tables (each
+     // holds ~2x its share of groups) and send the call to the hashed path after all the
+     // work; decline up front instead.  Repeated keys count once: a heavy key is rows,
+     // not groups, and its excess rows go to the overflow arenas below.
+    // (raw counts first — one pass; only a partition above the bound has its samples
+    // deduplicated, so uniform keys pay no sort)
+    const uint32_t np0 = 1u << bits0, bound = 2 * kSample / np0 + 16;
+    std::vector<uint32_t> raw(np0, 0);
+    for (int64_t k : smp) ++raw[rg.cell((uint64_t)k) >> bits1];
+    for (uint32_t p = 0; p < np0; ++p) {
+      if (raw[p] <= bound) continue;
+      std::vector<int64_t> ks;
+      for (int64_t k : smp)
+        if (rg.cell((uint64_t)k) >> bits1 == p) ks.push_back(k);
+      std::sort(ks.begin(), ks.end());
+      if ((uint64_t)(std::unique(ks.begin(), ks.end()) - ks.begin()) > bound) return NUT_ERR_UNSUPPORTED;
+    }
+  }
   // ---- partition buffers: level 0 capped over O (2 x rows per array), level 1 into B2
   nut_groups *g = new nut_groups();
   struct Free {
@@ -986,7 +1105,11 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
   const int narr = 3 + nv, nstore = narr - 2;
   const uint64_t rows = (n + 2 * 65536 + 64 + 31) & ~31ull;
   const double slack1 = 1.0 + 6.0 / sqrt(lam);
-  const uint64_t b2rows = ((uint64_t)ceil(n * slack1) + (66ull << (bits0 + bits1)) + 2 * GP_TILE + 64 + 31) & ~31ull;
+  // B2: the level-1 regions (n x slack1 + per-region slack), then level 1's overflow arena
+  // (n / 4 rows), then one tile of scratch for runs an exhausted arena cannot take
+  const uint64_t arena1 = (n / 4 + 31) & ~31ull;
+  const uint64_t b2rows =
+      ((uint64_t)ceil(n * slack1) + (66ull << (bits0 + bits1)) + arena1 + 2 * GP_TILE + 64 + 31) & ~31ull;
   e = c->gp_data.reserve((2 * (size_t)nstore * rows + (size_t)nstore * b2rows) * 8 + 256);
   if (e) return e;
   uint64_t *O[GP_MAX_ARR] = {}, *B2[GP_MAX_ARR] = {};
@@ -1004,13 +1127,25 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
   c->gb_path = NUT_GB_PARTITIONED_ORDERED;
   c->gb_levels = 2;
   c->gb_optimistic = 2;
-  // ---- level 0 (range digit = cell >> bits1)
-  const uint64_t ocap = ((2 * rows - 2 * GP_TILE) >> bits0) & ~1ull;
+  // overflow arenas (a run past its capped region keeps its rows there, gpart.hpp), one
+  // cursor per level: [0] level 0's (in O), [1] level 1's (in B2)
+  unsigned long long *darena = nullptr;
+  NUT_HIP(hipMallocAsync((void **)&darena, 16, st));
+  struct FreeArena {
+    unsigned long long *p;
+    hipStream_t s;
+    ~FreeArena() { (void)hipFreeAsync(p, s); }
+  } free_arena{darena, st};
+  NUT_HIP(hipMemsetAsync(darena, 0, 16, st));
+  // ---- level 0 (range digit = cell >> bits1): 1.5 x the even share per partition, the rest
+  // of O (~n / 2 rows) its arena
+  const uint64_t ocap = ((3 * rows / 2) >> bits0) & ~1ull;
+  const uint64_t abase0 = ocap << bits0, acap0 = 2 * rows - abase0 - 2 * GP_TILE;
   std::vector<GpSeg> segs{GpSeg{0, n, 0, 0}};
   segs[0].ocap = ocap;
   std::vector<uint64_t> hist, p0;
   c->timer.begin(st, NUT_KERNEL_AGGREGATE);
-  e = gp_level(c, mm, segs, bits1, src, O, narr, false, false, hist, &p0, 0, ocap << bits0, bits0, &rg);
+  e = gp_level(c, mm, segs, bits1, src, O, narr, false, false, hist, &p0, 0, abase0, bits0, &rg, darena, acap0);
   c->timer.end(st);
   if (e) return e == NUT_ERR_CAPACITY ? NUT_ERR_UNSUPPORTED : e;
   // ---- level-1 regions, as the hashed path sizes them
@@ -1025,6 +1160,7 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
     s2.push_back(sg);
   }
   if (ovf1 + 2 * GP_TILE > b2rows) return NUT_ERR_UNSUPPORTED;
+  const uint64_t acap1 = b2rows - ovf1 - 2 * GP_TILE;  // level 1's arena: rows [ovf1, ovf1 + acap1) of B2
   const uint64_t nparts = (uint64_t)np0 * nb1;
   // chunks of level-0 partitions (in key order) halving in size — 1/2, 1/4, 1/8, 1/16,
   // 1/16: a chunk's transfer (~0.4x its compute) hides behind the next, smaller chunk, and
@@ -1044,9 +1180,12 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
     tile0[j] = (uint32_t)tiles.size();
     tiles.insert(tiles.end(), ts.begin(), ts.end());
   }
-  std::vector<uint64_t> init(nparts + nch, 0);  // + one overflow flag per chunk
+  std::vector<uint64_t> init(nparts + nch, 0), rend(nparts);  // + one overflow flag per chunk
   for (uint32_t i = 0; i < np0; ++i)
-    for (uint32_t d = 0; d < nb1; ++d) init[(uint64_t)i * nb1 + d] = s2[i].obase + (uint64_t)d * s2[i].ocap;
+    for (uint32_t d = 0; d < nb1; ++d) {
+      init[(uint64_t)i * nb1 + d] = s2[i].obase + (uint64_t)d * s2[i].ocap;
+      rend[(uint64_t)i * nb1 + d] = s2[i].obase + (uint64_t)(d + 1) * s2[i].ocap;
+    }
   // the aggregation's table regions: every one holds a full block table (+ the special key)
   nut_agg_spec s3;
   memset(&s3, 0, sizeof(s3));
@@ -1075,11 +1214,13 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
   // device tables, uploaded once
   GpSeg *dseg;
   uint32_t *dts;
-  uint64_t *dinit;
+  uint64_t *dinit, *drend;
   e = mm.begin(GpMeta::al(s2.size() * sizeof(GpSeg)) + GpMeta::al(tiles.size() * 4 + 1) + GpMeta::al(init.size() * 8) +
-               GpMeta::al(init.size() * 8) + 2 * GpMeta::al(nparts * 8) + GpMeta::al(64));
+               GpMeta::al(init.size() * 8) + 4 * GpMeta::al(nparts * 8) + GpMeta::al(64));
   if (e) return e;
-  if ((e = mm.up(s2, &dseg)) || (e = mm.up(tiles, &dts)) || (e = mm.up(init, &dinit))) return e;
+  if ((e = mm.up(s2, &dseg)) || (e = mm.up(tiles, &dts)) || (e = mm.up(init, &dinit)) || (e = mm.up(rend, &drend)))
+    return e;
+  uint64_t *dend = (uint64_t *)mm.alloc(nparts * 8);  // partition ends, cut at their regions' ends
   unsigned long long *dcur = (unsigned long long *)mm.alloc(init.size() * 8);
   unsigned long long *dcount = (unsigned long long *)mm.alloc(nparts * 8);
   uint64_t *doffs = (uint64_t *)mm.alloc(nparts * 8);
@@ -1136,14 +1277,18 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
     const uint64_t q0 = (uint64_t)a0 * nb1, nq = (uint64_t)(a1 - a0) * nb1;
     c->timer.begin(st, NUT_KERNEL_AGGREGATE);
     gp_capped_launch(c, ar, dseg + a0, dts + tile0[j], ntile[j], 0, dcur + q0, 0, ovf1, dcur + nparts + j, bits1, false,
-                     &rg);
+                     &rg, darena + 1, acap1);
     c->timer.end(st);
     NUT_HIP(hipGetLastError());
     NUT_HIP(hipEventRecord(ev1[j], st));
     NUT_HIP(hipStreamWaitEvent(ax, ev1[j], 0));
-    LaunchExtra sg;  // partition rows [first row, cursor after the scatter)
+    // partition rows [first row, cursor after the scatter), cut at the region's end: an
+    // overflowed run (flag read by the host afterwards) must not send the reads past it
+    hipLaunchKernelGGL(go_clamp_kernel, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, ax,
+                       (const unsigned long long *)dcur + q0, (const uint64_t *)drend + q0, (uint32_t)nq, dend + q0);
+    LaunchExtra sg;
     sg.seg_off = dinit + q0;
-    sg.seg_end = (const uint64_t *)dcur + q0;
+    sg.seg_end = (const uint64_t *)dend + q0;
     sg.nseg = (uint32_t)nq;
     sg.dense = true;
     sg.dcount = dcount + q0;
@@ -1184,18 +1329,51 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
     }
     done = total;
   }
-  // the capped level-1 flags and the aggregation's control words
+  // the capped level-1 flags (an exhausted arena), the arenas' fill and the aggregation's
+  // control words
   NUT_HIP(hipStreamSynchronize(ax));
   std::vector<uint64_t> flags(nch);
   NUT_HIP(hipMemcpyAsync(flags.data(), dcur + nparts, nch * 8, hipMemcpyDeviceToHost, st));
   uint32_t ctl[4];
   NUT_HIP(hipMemcpyAsync(c->host_pinned, g->gt.ctl, 16, hipMemcpyDeviceToHost, st));
+  NUT_HIP(hipMemcpyAsync(c->host_pinned + 2, darena, 16, hipMemcpyDeviceToHost, st));
   NUT_HIP(hipStreamSynchronize(st));
   memcpy(ctl, c->host_pinned, 16);
+  const uint64_t used0 = c->host_pinned[2], used1 = c->host_pinned[3];
   NUT_HIP(hipStreamSynchronize(c->copy_stream));
   for (uint64_t f : flags)
-    if (f) return NUT_ERR_UNSUPPORTED;  // a level-1 run outgrew its region
+    if (f) return NUT_ERR_UNSUPPORTED;  // a level-1 run found the arena full
   if (ctl[1] & 4u) return NUT_ERR_UNSUPPORTED;  // a partition outgrew its block's table
+  c->gb_overflow_rows = used0 + used1;
+  if (used0 + used1 && !over) {
+    // the arenas' rows (heavy keys' excess, mostly) aggregated on their own and folded
+    // into the ordered host result
+    nut_agg_spec sa = s3;
+    const uint32_t path = c->gb_path, lv = c->gb_levels, opt = c->gb_optimistic;
+    const int64_t part = c->opt[NUT_OPT_GB_PARTITION];
+    c->opt[NUT_OPT_GB_PARTITION] = 0;  // (the partitioned path would reuse gp_data, which holds the arenas)
+    nut_groups *ga = nullptr;
+    uint64_t na_groups = 0;
+    for (int lvl = 0; lvl < 2 && !e; ++lvl) {
+      const uint64_t rows_l = lvl ? used1 : used0, base = lvl ? ovf1 : abase0;
+      uint64_t *const *arr = lvl ? B2 : O;
+      if (!rows_l) continue;
+      sa.n = rows_l;
+      sa.keys[0] = (const int64_t *)(arr[1] + base);
+      for (int j = 0; j < NUT_MAX_VALS; ++j)
+        if (vmap[j] >= 0) sa.val_col[vmap[j]] = arr[3 + vmap[j]] + base;
+      e = ga ? nut_groupby_accumulate(c, &sa, ga) : nut_groupby(c, &sa, std::min<uint64_t>(rows_l, group_hint), &ga);
+    }
+    c->opt[NUT_OPT_GB_PARTITION] = part;
+    c->gb_path = path, c->gb_levels = lv, c->gb_optimistic = opt;
+    if (!e) e = nut_groups_size(ga, &na_groups);
+    std::vector<int64_t> hk(na_groups);
+    std::vector<uint64_t> hw(na_groups * (size_t)na);
+    if (!e && na_groups) e = nut_groups_to_host(ga, hk.data(), hw.data(), na_groups);
+    nut_groups_free(ga);
+    if (e) return e;
+    done = fold_sorted_groups(keys_h, aggs_h, done, cap, hk, hw, g->kinds, na, &over);
+  }
   *n_out = done;
   if (over) return fail(NUT_ERR_CAPACITY, "nut_groupby_to_host: capacity " + std::to_string(cap) + " < " +
                                               std::to_string(done) + " groups");
@@ -1324,6 +1502,78 @@ nut_status groupby_partitioned(nut_groups *g, const nut_agg_spec *s, uint64_t gr
 
 extern "C" {
 
+// NUT_OPT_PRIV_PROBE: before the first compiled-Q1-shape launch of >= 2^27 rows on a
+// device, time the kernel at each of kPrivShapes on the first 2^28 rows of the caller's
+// columns (two interleaved rounds, best of each; the kernel timer is paused, so no probe
+// launch is counted as the caller's work) and keep the fastest for the device.  The probe
+// launches fold into g's table, which is initialised again afterwards: the result is the
+// real launch's alone.
+static nut_status probe_priv_shape(nut_groups *g, const nut_agg_spec *s, uint64_t group_hint, uint64_t cap) {
+  nut_ctx *c = g->ctx;
+  if (!c->opt[NUT_OPT_PRIV_PROBE] || c->opt[NUT_OPT_PRIV_BD] || c->opt[NUT_OPT_PRIV_BLOCKS] || s->n < (1ull << 27) ||
+      c->device < 0 || c->device >= 64 || priv_shape_of(c->device).shape >= 0)
+    return NUT_OK;
+  LaunchExtra dry;
+  dry.dry = true;
+  nut_status st = launch_agg(g, s, group_hint, g->kinds, &dry);
+  if (st || !dry.q1_fused) return st;
+  nut_agg_spec s2 = *s;
+  s2.n = std::min<uint64_t>(s->n, 1ull << 28);
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  NUT_HIP(hipEventCreate(&e0));
+  hipError_t he = hipEventCreate(&e1);
+  if (he != hipSuccess) {
+    (void)hipEventDestroy(e0);
+    return hip_fail(he, "hipEventCreate");
+  }
+  const bool timing = c->timer.enabled;
+  c->timer.enabled = false;
+  double best[3] = {1e30, 1e30, 1e30};
+  for (int rep = 0; rep < 2 && !st; ++rep)
+    for (int k = 0; k < 3 && !st; ++k) {
+      c->priv_probe = k;
+      he = hipEventRecord(e0, c->stream);
+      if (he == hipSuccess) st = launch_agg(g, &s2, group_hint, g->kinds);
+      if (he == hipSuccess && !st) he = hipEventRecord(e1, c->stream);
+      if (he == hipSuccess && !st) he = hipEventSynchronize(e1);
+      float ms = 0;
+      if (he == hipSuccess && !st) he = hipEventElapsedTime(&ms, e0, e1);
+      if (he != hipSuccess && !st) st = hip_fail(he, "nut_groupby (launch-shape probe)");
+      best[k] = std::min(best[k], (double)ms);
+    }
+  c->priv_probe = -1;
+  c->timer.enabled = timing;
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  if (st) return st;
+  int k = 0;
+  for (int j = 1; j < 3; ++j)
+    if (best[j] < best[k]) k = j;
+  {
+    std::lock_guard<std::mutex> lk(g_priv_mu);
+    g_priv_shape[c->device].shape = k;
+    for (int j = 0; j < 3; ++j) g_priv_shape[c->device].ms[j] = best[j];
+  }
+  return alloc_table(g, cap);  // the probe's partial groups are discarded
+}
+
+nut_status nut_ctx_groupby_overflow(nut_ctx *c, uint64_t *rows) {
+  if (!c || !rows) return fail(NUT_ERR_INVALID_ARG, "nut_ctx_groupby_overflow: NULL argument");
+  *rows = c->gb_overflow_rows;
+  return NUT_OK;
+}
+
+nut_status nut_ctx_priv_shape(nut_ctx *c, int *threads, int *blocks_per_cu, double probe_ms[3]) {
+  if (!c) return fail(NUT_ERR_INVALID_ARG, "nut_ctx_priv_shape: NULL context");
+  const PrivShape p = priv_shape_of(c->device);
+  const int k = p.shape >= 0 ? p.shape : 0;
+  if (threads) *threads = c->opt[NUT_OPT_PRIV_BD] ? (int)c->opt[NUT_OPT_PRIV_BD] : kPrivShapes[k][0];
+  if (blocks_per_cu) *blocks_per_cu = c->opt[NUT_OPT_PRIV_BLOCKS] ? (int)c->opt[NUT_OPT_PRIV_BLOCKS] : kPrivShapes[k][1];
+  if (probe_ms)
+    for (int j = 0; j < 3; ++j) probe_ms[j] = p.ms[j];
+  return NUT_OK;
+}
+
 nut_status nut_groupby(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hint, nut_groups **out) {
   if (!c || !out) return fail(NUT_ERR_INVALID_ARG, "nut_groupby: NULL argument");
   *out = nullptr;
@@ -1355,6 +1605,7 @@ nut_status nut_groupby(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hint, n
   }
   for (int attempt = 0;; ++attempt) {
     st = alloc_table(g, cap);
+    if (!st && attempt == 0) st = probe_priv_shape(g, s, group_hint, cap);
     if (!st) st = launch_agg(g, s, group_hint, g->kinds);
     uint32_t ctl[4] = {0, 0, 0, 0};
     if (!st) st = read_ctl(g, ctl);

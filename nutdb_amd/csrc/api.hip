@@ -105,6 +105,7 @@ __global__ void gen_column_kernel(int kind, uint64_t seed, int64_t a, int64_t b,
       case NUT_GEN_DYADIC: od[i] = (double)(u >> 44) / 64.0; break;
       case NUT_GEN_UNIT_F64: od[i] = (double)(u >> 11) * 0x1p-53; break;
       case NUT_GEN_RANGE_I64: oi[i] = a + (int64_t)(u % (uint64_t)b); break;
+      case NUT_GEN_SKEW_KEY: oi[i] = (int64_t)mix64(((u % (uint64_t)a) >> (((mix64(u) >> 59) * 3) >> 2)) ^ kPoolSalt); break;
       default: od[i] = (double)(a + (int64_t)(u % (uint64_t)b)) / c; break;
     }
   }
@@ -350,8 +351,8 @@ nut_status nut_ctx_groupby_stats(nut_ctx *c, uint32_t *path, uint32_t *levels, u
 
 nut_status nut_ctx_set_option(nut_ctx *c, int option, int64_t value) {
   if (!c || option < 0 || option >= NUT_OPT_COUNT) return fail(NUT_ERR_INVALID_ARG, "nut_ctx_set_option: bad option");
-  static const int64_t lo[NUT_OPT_COUNT] = {-1, 0, 0, 0, 1, 0, 0, 0, 1, 0, 6, 0, 0, 0, 0, 0, 0, 0, 0, 0},
-                       hi[NUT_OPT_COUNT] = {1, 2, 1, 1, 64, 1, 4, 4, 8, 1, 8, 1, 8, 32, 256, 16, 16, 16, 1024, 1};
+  static const int64_t lo[NUT_OPT_COUNT] = {-1, 0, 0, 0, 1, 0, 0, 0, 1, 0, 6, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0},
+                       hi[NUT_OPT_COUNT] = {1, 2, 1, 1, 64, 1, 4, 4, 8, 1, 8, 1, 8, 32, 256, 16, 16, 16, 1024, 1, 1};
   if (value < lo[option] || value > hi[option])
     return fail(NUT_ERR_INVALID_ARG, "nut_ctx_set_option: value " + std::to_string(value) + " out of range [" +
                                          std::to_string(lo[option]) + ", " + std::to_string(hi[option]) + "]");
@@ -430,9 +431,9 @@ nut_status nut_stream_probe(nut_ctx *c, const void *src, uint64_t read_bytes, vo
 nut_status nut_gen_column(nut_ctx *c, int kind, uint64_t seed, int64_t a, int64_t b, double cc,
                           uint64_t row0, uint64_t n, void *out) {
   if (!c || (!out && n)) return fail(NUT_ERR_INVALID_ARG, "nut_gen_column: NULL argument");
-  if (kind < NUT_GEN_U62 || kind > NUT_GEN_RANGE_F64)
+  if (kind < NUT_GEN_U62 || kind > NUT_GEN_SKEW_KEY)
     return fail(NUT_ERR_INVALID_ARG, "nut_gen_column: unknown kind " + std::to_string(kind));
-  if ((kind == NUT_GEN_POOL_KEY && a <= 0) ||
+  if (((kind == NUT_GEN_POOL_KEY || kind == NUT_GEN_SKEW_KEY) && a <= 0) ||
       ((kind == NUT_GEN_RANGE_I64 || kind == NUT_GEN_RANGE_F64) && b <= 0))
     return fail(NUT_ERR_INVALID_ARG, "nut_gen_column: empty range");
   if (n == 0) return NUT_OK;

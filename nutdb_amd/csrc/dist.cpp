@@ -159,10 +159,14 @@ nut_status allgather(nut_dist *d, int l, const uint64_t *send, uint64_t *recv, s
   return e == hipSuccess ? NUT_OK : hip_fail(e, "nut_dist (virtual) all-gather");
 }
 
-// RCCL all-to-all rounds move at most this many words per (sender, receiver) pair: a
-// single-rank ncclAllToAllv of 2e8 words (1.6 GB) returned wrong data on this image while
-// 1e8 words were exact (scripts/diag/dist_sort_pieces.py), so large exchanges go in rounds
-constexpr size_t kA2AChunk = size_t(1) << 26;
+// RCCL all-to-all rounds move at most this many words per (sender, receiver) pair.  On
+// RCCL 2.27.7 / ROCm 7.2 one P2P transfer of more than 2^30 bytes leaves everything after
+// its first half unwritten (ncclAllToAllv and grouped ncclSend / ncclRecv alike; 134,200,000
+// words exact, 134,220,000 wrong — the torch-free probe scripts/diag/a2a_probe.c,
+// profiles/r04/dist/), so no pair moves more than half that limit per round
+constexpr size_t kRcclP2PMaxBytes = size_t(1) << 30;
+constexpr size_t kA2AChunk = kRcclP2PMaxBytes / 2 / sizeof(uint64_t);  // 2^26 words = 2^29 bytes
+static_assert(kA2AChunk * sizeof(uint64_t) < kRcclP2PMaxBytes, "a round's transfer stays under RCCL's limit");
 
 // the largest (sender, receiver) cell of an all-gathered count matrix: rank q's count for
 // receiver r at all[q * w + off + r], times `mul` words per count

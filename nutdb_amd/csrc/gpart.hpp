@@ -44,12 +44,14 @@ struct GpArrays {
 // monotonically onto 2^14 cells over a sampled range [lo, lo + span] (signed order; keys
 // outside are clamped to the end cells, so the order holds and only the balance suffers):
 // x = (k ^ 2^63) - lo, clamped to [0, span]; cell = mulhi((x >> t), mul) with mul =
-// floor(2^46 / ((span >> t) + 1)).  Level 0's digit is cell >> 6, level 1's cell & 63, so
-// the partitions are in key order.
+// floor(2^46 / ((span >> t) + 1)).  With the cells split into bits0 + bits1 digits
+// (NUT_OPT_GB_L0_BITS, default 7 + 7), level 0's digit is cell >> bits1 and level 1's
+// cell & (2^bits1 - 1), so the partitions are in key order.  (The scatter kernel's RANGE
+// template flag chooses these digits over the hash's; t is the range shift, 0 included.)
 struct GpRange {
   uint64_t lo, span;
   uint32_t mul;
-  int t;  // 0 = hash digits (owner_hash)
+  int t;  // x's shift: (span >> t) < 2^32
   __host__ __device__ __forceinline__ uint32_t cell(uint64_t k) const {
     uint64_t x = (k ^ 0x8000000000000000ull) - lo;
     x = (k ^ 0x8000000000000000ull) < lo ? 0 : (x > span ? span : x);
@@ -117,7 +119,9 @@ __global__ __launch_bounds__(T) void gp_scatter_kernel(GpArrays ar, const GpSeg 
                                                                 int shift, int gather,
                                                                 unsigned long long *__restrict__ cursor, uint64_t kx,
                                                                 uint64_t ovf, unsigned long long *__restrict__ oflag,
-                                                                GpRange rg = GpRange{}) {
+                                                                GpRange rg = GpRange{},
+                                                                unsigned long long *__restrict__ acur = nullptr,
+                                                                uint64_t acap = 0) {
   static_assert(!RANGE || NK == 1, "range digits: one key");
   constexpr uint32_t TILE = T * GP_ITEMS;
   constexpr int BINS = 1 << BITS;  // (the product: GP_BINS = 256)
@@ -198,11 +202,21 @@ __global__ __launch_bounds__(T) void gp_scatter_kernel(GpArrays ar, const GpSeg 
       if (VAR & 16) s_run[tid] += c;
       // ovf != 0: the capped layout (no histogram pass; GpSeg obase / ocap).  A run past its
       // digit's rows goes to the scratch rows at ovf (>= one tile of them), and the flag
-      // after the cursors tells the host to partition again with a histogram
+      // after the cursors tells the host to partition again with a histogram.  With an
+      // overflow arena (acur: the ordered group-by) the run is kept instead: it claims rows
+      // [ovf + *acur, + c) of the arena (acap rows, scratch after them), which the host
+      // aggregates on its own and folds into the result — a heavy key costs its excess
+      // rows, not a rerun; only an exhausted arena sets the flag.
       const GpSeg &g = segs[s];
       const bool over = !(VAR & 16) && ovf && c && gb + c > g.obase + (uint64_t)(tid + 1) * g.ocap;
-      if (over) atomicOr(oflag, 1ull);
-      s_gb[tid] = (over ? ovf : gb) - tex;  // out position of tile slot j with digit d = s_gb[d] + j
+      uint64_t o = gb;
+      if (over) {
+        const uint64_t ga = acur ? (uint64_t)atomicAdd(acur, (unsigned long long)c) : acap;
+        const bool kept = acur && ga + c <= acap;
+        if (!kept) atomicOr(oflag, 1ull);
+        o = ovf + (kept ? ga : acap);
+      }
+      s_gb[tid] = o - tex;  // out position of tile slot j with digit d = s_gb[d] + j
     }
     __syncthreads();
 #pragma unroll
@@ -278,6 +292,16 @@ __global__ __launch_bounds__(T) void gp_scatter_kernel(GpArrays ar, const GpSeg 
 __global__ void go_sample_kernel(const int64_t *__restrict__ k, uint64_t n, uint32_t m, int64_t *__restrict__ out) {
   const uint64_t step = n / m;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) out[i] = k[i * step];
+}
+
+// end[q] = min(cursor[q], rend[q]): a capped level's partition ends cut at their regions'
+// ends.  When a run overflows its region the cursor still advances by the whole run (the
+// run itself goes to the scratch rows), so the raw cursor would send the aggregation past
+// the region — past the buffer for the last partitions — before the host sees the flag.
+__global__ void go_clamp_kernel(const unsigned long long *__restrict__ cursor, const uint64_t *__restrict__ rend,
+                                uint32_t n, uint64_t *__restrict__ end) {
+  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q < n) end[q] = min((uint64_t)cursor[q], rend[q]);
 }
 
 // one workgroup: offs[p] = *run + the groups of the partitions before p, then *run += all

@@ -43,9 +43,9 @@ constexpr uint32_t MH_HTILE = 1u << 18; // keys per histogram tile (one LDS hist
 constexpr int MH_LOADS = 16;            // keys in flight per lane in the histogram loop
 constexpr int MS_THREADS = 1024;
 constexpr int MS_ITEMS = 14;
-constexpr uint32_t MS_TILE = MS_THREADS * MS_ITEMS;  // 16384 keys per scatter tile
+constexpr uint32_t MS_TILE = MS_THREADS * MS_ITEMS;  // keys staged in LDS at a time (14336)
 constexpr int MS_BITS = 9;                          // digit width of a scatter level
-constexpr int MS_BINS = 1 << MS_BITS;               // 512: 32 keys (256 B) per digit per tile
+constexpr int MS_BINS = 1 << MS_BITS;               // 512: MS_TILE / 512 = 28 keys (224 B) per digit per stage
 static_assert(MS_BINS <= MS_THREADS, "one scan thread per digit");
 // local-sort classes: threads x max items per thread (ms_local_kernel)
 constexpr int LS_S_THREADS = 256, LS_S_ITEMS = 8;    // <= 2048 keys
@@ -208,9 +208,10 @@ constexpr uint64_t kSkipRun = ~0ull;
 // Persistent: workgroup b takes tiles b, b + grid, ...; the next tile's keys are loaded into
 // the key registers as soon as the current tile is staged in LDS, so its HBM latency hides
 // behind the current tile's write-out (and the segment lookup behind the ranking).
-// H = 2: 32 Ki-key tiles (32 keys per lane in registers), staged and written out in two
-// halves of the tile's digit order through the same 16 Ki-key LDS buffer, so each digit's
-// output run per tile is twice as long (512 B instead of 256 B: fewer partial 128-B lines).
+// H = 2: tiles of 2 x MS_TILE keys (2 x MS_ITEMS = 28 keys per lane in registers), staged
+// and written out in two halves of the tile's digit order through the same MS_TILE-key LDS
+// buffer, so each digit's output run per tile is twice as long (~448 B instead of ~224 B:
+// fewer partial 128-B lines).
 template <int H, class DG, int T = MS_THREADS>
 __global__ __launch_bounds__(T, 2048 / T) void ms_scatter_kernel(MsBufs bf, const MsSeg *__restrict__ segs,
                                                                    const uint32_t *__restrict__ tile_seg, uint32_t ntiles,

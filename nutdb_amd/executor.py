@@ -336,6 +336,17 @@ class Executor:
         check(lib.nut_ctx_kernel_time(self.ctx, kind, C.byref(ms), C.byref(cnt)), "nut_ctx_kernel_time")
         return ms.value, cnt.value
 
+    def priv_shape(self) -> dict:
+        """The compiled Q1 kernel's launch shape on this device (nut_ctx_priv_shape): threads
+        per workgroup, workgroups per CU, and the shape probe's kernel ms per candidate
+        (None where the probe has not run in this process)."""
+        t, b = C.c_int(), C.c_int()
+        ms = (C.c_double * 3)()
+        check(lib.nut_ctx_priv_shape(self.ctx, C.byref(t), C.byref(b), ms), "nut_ctx_priv_shape")
+        return {"threads": t.value, "blocks_per_cu": b.value,
+                "probe_ms": {f"{a}x{c}": (round(m, 4) if m >= 0 else None)
+                             for (a, c), m in zip(((192, 2), (128, 3), (128, 4)), ms)}}
+
     def sort_stats(self):
         """(algorithmic HBM bytes, scatter levels) of the last sort on this context."""
         b = C.c_uint64()
@@ -349,7 +360,7 @@ class Executor:
                "gb_dense": 9, "gb_l1_bits": 10,
                "topk": 11, "gb_l0_bits": 12, "stream_blocks": 13,
                "priv_bd": 14, "priv_blocks": 15, "agg_blocks": 16, "sel_blocks": 17, "sort_bd": 18,
-               "gb_ordered": 19}
+               "gb_ordered": 19, "priv_probe": 20}
 
     def groupby_stats(self) -> dict:
         """The algorithm the last group-by on this context took (nut_ctx_groupby_stats)."""
@@ -357,6 +368,13 @@ class Executor:
         check(lib.nut_ctx_groupby_stats(self.ctx, C.byref(p), C.byref(lv), C.byref(opt)), "nut_ctx_groupby_stats")
         return {"path": self.GROUPBY_PATHS[p.value], "levels": lv.value, "optimistic": bool(opt.value),
                 "capped_levels": opt.value}
+
+    def groupby_overflow_rows(self) -> int:
+        """Rows of the last ordered group-by (groupby_to_host) aggregated from its overflow
+        arenas — a heavy key's excess past its capped partition (nut_ctx_groupby_overflow)."""
+        r = C.c_uint64()
+        check(lib.nut_ctx_groupby_overflow(self.ctx, C.byref(r)), "nut_ctx_groupby_overflow")
+        return r.value
 
     def set_option(self, name: str, value: int) -> int:
         """nut_ctx_set_option (tuning / tests); returns the previous value."""

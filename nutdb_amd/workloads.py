@@ -22,9 +22,10 @@ GB_KEY_SEED = 0x51
 GB_VAL_SEED = 0x52
 
 
-def groupby_cols(groups: int, dyadic: bool = True):
+def groupby_cols(groups: int, dyadic: bool = True, skew: bool = False):
+    """skew: Zipf-like keys from the same pool (GEN_SKEW_KEY: pool index i on ~1/i of the rows)."""
     return [
-        ("key", L.GEN_POOL_KEY, GB_KEY_SEED, groups, 0, 1.0),
+        ("key", L.GEN_SKEW_KEY if skew else L.GEN_POOL_KEY, GB_KEY_SEED, groups, 0, 1.0),
         ("val", L.GEN_DYADIC if dyadic else L.GEN_UNIT_F64, GB_VAL_SEED, 0, 0, 1.0),
     ]
 

@@ -211,14 +211,41 @@ def eval_prog(nodes, cols, n=None):
     return x, t, err
 
 
-def groupby_prog(keys, cols, where, aggs, n=None):
+def eval_prog_par(nodes, cols, n=None, threads=1):
+    """eval_prog over row chunks on `threads` host threads (numpy releases the GIL in its
+    array loops).  Programs are row-wise, so the result is eval_prog's, bit for bit; the
+    CPU baseline (bench.py) uses it to run the expression oracle on every host core."""
+    if n is None:
+        n = len(cols[0]) if cols else 0
+    if threads <= 1 or n < (1 << 20):
+        return eval_prog(nodes, cols, n)
+    from concurrent.futures import ThreadPoolExecutor
+    bounds = [n * i // threads for i in range(threads + 1)]
+    with ThreadPoolExecutor(threads) as pool:
+        parts = list(pool.map(lambda lh: eval_prog(nodes, [c[lh[0]:lh[1]] for c in cols], lh[1] - lh[0]),
+                              zip(bounds[:-1], bounds[1:])))
+    return np.concatenate([p[0] for p in parts]), parts[0][1], np.concatenate([p[2] for p in parts])
+
+
+def groupby_prog(keys, cols, where, aggs, n=None, threads=1, engine="numpy"):
     """Expression-mode group-by: keys = list of int64 arrays or key programs (node lists,
     int64 / bool; any number of keys; empty = global aggregate), where = nodes or None,
     aggs = [(op, val_nodes or None, mask_nodes or None)] with op 0 SUM / 1 COUNT / 2 MIN /
     3 MAX.  Returns (keys, words, types) like oracle.groupby (words = result bits, groups
     ordered by key tuple) plus each aggregate's value type; raises DivisionByZero under the
-    kernel's error rule (a key program's error counts for rows passing WHERE)."""
+    kernel's error rule (a key program's error counts for rows passing WHERE).  threads > 1:
+    the programs run on that many host threads (eval_prog_par; same result).  engine "c":
+    integer / bool programs run in C on every core (oracle.eval_int, no row errors possible
+    in that subset; pinned to eval_prog by tests/test_expr_cpu.py), the rest as above —
+    the CPU baseline's form."""
     from . import oracle as orc
+
+    def eval_prog(nodes, cols, n):  # noqa: F811  (the row-chunked / C forms)
+        if engine == "c" and n and cols:
+            x = orc.eval_int(nodes, cols, n)
+            if x is not None:  # the type from one row of the numpy form
+                return x, _eval_numpy(nodes, [c[:1] for c in cols], 1)[1], np.zeros(n, dtype=bool)
+        return eval_prog_par(nodes, cols, n, threads)
 
     if n is None:
         arrs = [k for k in keys if isinstance(k, np.ndarray)]
@@ -273,3 +300,6 @@ def groupby_prog(keys, cols, where, aggs, n=None):
     ok_rank, words = orc.groupby([rank.reshape(-1).astype(np.int64)], spec, values=values, row_mask=ok,
                                  agg_masks=masks)
     return uniq[ok_rank[:, 0]], words, types
+
+
+_eval_numpy = eval_prog

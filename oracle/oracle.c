@@ -57,6 +57,7 @@ void orc_gen_column(int kind, uint64_t seed, int64_t a, int64_t b, double c,
       case ORC_GEN_UNIT_F64: od[i] = (double)(u >> 11) * 0x1p-53; break;
       case ORC_GEN_RANGE_I64: oi[i] = a + (int64_t)(u % (uint64_t)b); break;
       case ORC_GEN_RANGE_F64: od[i] = (double)(a + (int64_t)(u % (uint64_t)b)) / c; break;
+      case ORC_GEN_SKEW_KEY: oi[i] = (int64_t)orc_mix64(ORC_SKEW_INDEX(u, a) ^ ORC_POOL_SALT); break;
       default: oi[i] = 0;
     }
   }
@@ -309,8 +310,203 @@ static int cmp_grp(const void *pa, const void *pb, void *nkp) {
 static int g_sort_nk;
 static int cmp_grp_q(const void *a, const void *b) { return cmp_grp(a, b, &g_sort_nk); }
 
+/* the group's result words (f64 sums folded with their compensation, MIN / MAX of f64
+ * back from the ordered encoding) */
+static void grp_out(const grp_t *g, const orc_agg_spec *s, int64_t *ok, uint64_t *ow) {
+  ok[0] = g->k[0];
+  if (s->nkeys == 2) ok[1] = g->k[1];
+  for (int a = 0; a < s->naggs; ++a) {
+    uint64_t w = g->w[a];
+    int op = s->agg_op[a];
+    if (op != ORC_AGG_COUNT && !agg_is_i64(s, a)) {
+      double d;
+      if (op == ORC_AGG_SUM) {
+        d = g->sumf[a] + g->comp[a];
+      } else {
+        uint64_t b = (w >> 63) ? (w & 0x7FFFFFFFFFFFFFFFull) : ~w;
+        memcpy(&d, &b, 8);
+      }
+      memcpy(&w, &d, 8);
+    }
+    ow[a] = w;
+  }
+}
+
+/* key tuple order (signed, lexicographic) */
+static int tuple_lt(const int64_t *a, const int64_t *b, int nk) {
+  if (a[0] != b[0]) return a[0] < b[0];
+  return nk == 2 && a[1] < b[1];
+}
+static int cmp_tuple(const void *pa, const void *pb) {
+  const int64_t *a = (const int64_t *)pa, *b = (const int64_t *)pb;
+  if (a[0] != b[0]) return a[0] < b[0] ? -1 : 1;
+  if (g_sort_nk == 2 && a[1] != b[1]) return a[1] < b[1] ? -1 : 1;
+  return 0;
+}
+
+/* Large group counts: the same result as the per-thread tables below, computed without
+ * their serial merge.  Rows are range-partitioned by key tuple (P - 1 splitters from a
+ * sorted row sample); each partition then runs on one thread with tables that fit its
+ * cache: per partition, the rows of thread chunk t (the chunks orc_groupby uses) fold in
+ * row order into a fresh table, which merges into the partition's result in chunk order —
+ * exactly the per-group order of the per-thread tables and their merge into table 0 (a
+ * group merged into a fresh group is that group, bit for bit), so the two paths agree
+ * bitwise.  Partitions are key ranges, so each one's groups sorted and laid out in
+ * partition order are the global order.  Returns UINT64_MAX - 1 when the sample shows few
+ * groups (the per-thread tables are faster there). */
+static uint64_t groupby_ranges(const orc_agg_spec *s, uint64_t cap, int64_t *out_keys, uint64_t *out_aggs, int nt) {
+  const uint64_t n = s->n, chunk = (n + (uint64_t)nt - 1) / (uint64_t)nt;
+  const int nk = s->nkeys;
+  if (nk < 1 || n < ((uint64_t)1 << 22)) return UINT64_MAX - 1;
+  /* ---- distinct-group estimate from a strided sample (Chao1: d + f1^2 / (2 f2)) */
+  const uint64_t m = 65536;
+  int64_t *smp = (int64_t *)malloc(m * 2 * sizeof(int64_t));
+  for (uint64_t j = 0; j < m; ++j) {
+    const uint64_t i = (uint64_t)(((unsigned __int128)j * n) / m);
+    smp[2 * j] = s->keys[0][i];
+    smp[2 * j + 1] = nk == 2 ? s->keys[1][i] : 0;
+  }
+  g_sort_nk = nk;
+  qsort(smp, m, 2 * sizeof(int64_t), cmp_tuple);
+  double d = 0, f1 = 0, f2 = 0;
+  for (uint64_t j = 0; j < m;) {
+    uint64_t e = j + 1;
+    while (e < m && cmp_tuple(&smp[2 * j], &smp[2 * e]) == 0) ++e;
+    d += 1;
+    f1 += e - j == 1;
+    f2 += e - j == 2;
+    j = e;
+  }
+  const double gest = d + f1 * f1 / (2.0 * (f2 > 0 ? f2 : 1.0));
+  if (gest < 16384) {
+    free(smp);
+    return UINT64_MAX - 1;
+  }
+  int P = 2;
+  while (P < 4096 && (double)P * 4096 < gest) P *= 2;
+  int64_t *spl = (int64_t *)malloc((size_t)P * 2 * sizeof(int64_t));  /* P - 1 splitters */
+  for (int p = 1; p < P; ++p) {
+    const uint64_t j = (uint64_t)p * m / (uint64_t)P;
+    spl[2 * (p - 1)] = smp[2 * j];
+    spl[2 * (p - 1) + 1] = smp[2 * j + 1];
+  }
+  free(smp);
+  /* ---- pass 1: each passing row's partition (#splitters <= its tuple), counts per (t, p) */
+  uint16_t *pid = (uint16_t *)malloc(n * sizeof(uint16_t));
+  uint64_t *cnt = (uint64_t *)calloc((size_t)nt * (size_t)P + 1, sizeof(uint64_t));
+#pragma omp parallel num_threads(nt)
+  {
+#ifdef _OPENMP
+    int t = omp_get_thread_num();
+#else
+    int t = 0;
+#endif
+    const uint64_t lo = (uint64_t)t * chunk, hi = lo + chunk > n ? n : lo + chunk;
+    uint64_t *c = cnt + (size_t)t * (size_t)P;
+    for (uint64_t i = lo; i < hi; ++i) {
+      if (!row_passes(s, i)) {
+        pid[i] = 0xFFFF;
+        continue;
+      }
+      const int64_t k[2] = {s->keys[0][i], nk == 2 ? s->keys[1][i] : 0};
+      int a = 0, b = P - 1; /* first splitter > k, in [0, P - 1] */
+      while (a < b) {
+        const int mid = (a + b) >> 1;
+        if (tuple_lt(k, &spl[2 * mid], nk)) b = mid;
+        else a = mid + 1;
+      }
+      pid[i] = (uint16_t)a;
+      ++c[a];
+    }
+  }
+  free(spl);
+  /* partition-major layout: partition p's rows, thread chunk by thread chunk, row order */
+  uint64_t *base = (uint64_t *)malloc(((size_t)P * (size_t)nt + 1) * sizeof(uint64_t));
+  uint64_t run = 0;
+  for (int p = 0; p < P; ++p)
+    for (int t = 0; t < nt; ++t) {
+      base[(size_t)p * nt + t] = run;
+      run += cnt[(size_t)t * P + p];
+    }
+  base[(size_t)P * nt] = run;
+  uint64_t *idx = (uint64_t *)malloc((run ? run : 1) * sizeof(uint64_t));
+#pragma omp parallel num_threads(nt)
+  {
+#ifdef _OPENMP
+    int t = omp_get_thread_num();
+#else
+    int t = 0;
+#endif
+    const uint64_t lo = (uint64_t)t * chunk, hi = lo + chunk > n ? n : lo + chunk;
+    uint64_t *w = cnt + (size_t)t * (size_t)P; /* reused as this thread's write cursors */
+    for (int p = 0; p < P; ++p) w[p] = base[(size_t)p * nt + t];
+    for (uint64_t i = lo; i < hi; ++i)
+      if (pid[i] != 0xFFFF) idx[w[pid[i]]++] = i;
+  }
+  free(pid);
+  /* ---- pass 2: one partition per thread at a time */
+  grp_t **pg = (grp_t **)calloc((size_t)P, sizeof(grp_t *));
+  uint64_t *pn = (uint64_t *)calloc((size_t)P + 1, sizeof(uint64_t));
+  g_sort_nk = nk;
+#pragma omp parallel num_threads(nt)
+  {
+    table_t A, B;
+    tbl_init(&A, 1024);
+    tbl_init(&B, 1024);
+#pragma omp for schedule(dynamic, 1)
+    for (int p = 0; p < P; ++p) {
+      A.n = 0;
+      memset(A.slot, 0xff, A.cap * sizeof(int64_t));
+      for (int t = 0; t < nt; ++t) {
+        const uint64_t r0 = base[(size_t)p * nt + t], r1 = base[(size_t)p * nt + t + 1];
+        if (r0 == r1) continue;
+        B.n = 0;
+        memset(B.slot, 0xff, B.cap * sizeof(int64_t));
+        for (uint64_t r = r0; r < r1; ++r) {
+          const uint64_t i = idx[r];
+          const int64_t k[2] = {s->keys[0][i], nk == 2 ? s->keys[1][i] : 0};
+          grp_update(tbl_find(&B, s, k), s, i);
+        }
+        for (uint64_t j = 0; j < B.n; ++j) grp_merge(tbl_find(&A, s, B.g[j].k), &B.g[j], s);
+      }
+      qsort(A.g, A.n, sizeof(grp_t), cmp_grp_q);
+      pg[p] = (grp_t *)malloc((A.n ? A.n : 1) * sizeof(grp_t));
+      memcpy(pg[p], A.g, A.n * sizeof(grp_t));
+      pn[p] = A.n;
+    }
+    tbl_free(&A);
+    tbl_free(&B);
+  }
+  free(idx);
+  free(base);
+  free(cnt);
+  uint64_t ng = 0;
+  for (int p = 0; p < P; ++p) ng += pn[p];
+  if (ng <= cap) {
+    uint64_t *off = (uint64_t *)malloc((size_t)P * sizeof(uint64_t));
+    for (int p = 0; p < P; ++p) off[p] = p ? off[p - 1] + pn[p - 1] : 0;
+#pragma omp parallel for schedule(dynamic, 4) num_threads(nt)
+    for (int p = 0; p < P; ++p)
+      for (uint64_t j = 0; j < pn[p]; ++j)
+        grp_out(&pg[p][j], s, out_keys + (off[p] + j) * (uint64_t)nk, out_aggs + (off[p] + j) * (uint64_t)s->naggs);
+    free(off);
+  }
+  for (int p = 0; p < P; ++p) free(pg[p]);
+  free(pg);
+  free(pn);
+  return ng <= cap ? ng : UINT64_MAX;
+}
+
 uint64_t orc_groupby(const orc_agg_spec *s, uint64_t cap, int64_t *out_keys,
                      uint64_t *out_aggs, int nthreads) {
+  int nt = nthreads > 0 ? nthreads : orc_max_threads();
+  const uint64_t r = groupby_ranges(s, cap, out_keys, out_aggs, nt);
+  return r != UINT64_MAX - 1 ? r : orc_groupby_tables(s, cap, out_keys, out_aggs, nt);
+}
+
+/* per-thread tables over row chunks, merged into thread 0's in thread order, then sorted */
+uint64_t orc_groupby_tables(const orc_agg_spec *s, uint64_t cap, int64_t *out_keys,
+                            uint64_t *out_aggs, int nthreads) {
   int nt = nthreads > 0 ? nthreads : orc_max_threads();
   table_t *tl = (table_t *)calloc((size_t)nt, sizeof(table_t));
   uint64_t n = s->n, chunk = (n + (uint64_t)nt - 1) / (uint64_t)nt;
@@ -352,26 +548,8 @@ uint64_t orc_groupby(const orc_agg_spec *s, uint64_t cap, int64_t *out_keys,
   }
   g_sort_nk = s->nkeys;
   qsort(G->g, ng, sizeof(grp_t), cmp_grp_q);
-  for (uint64_t i = 0; i < ng; ++i) {
-    grp_t *g = &G->g[i];
-    out_keys[i * (uint64_t)s->nkeys] = g->k[0];
-    if (s->nkeys == 2) out_keys[i * 2 + 1] = g->k[1];
-    for (int a = 0; a < s->naggs; ++a) {
-      uint64_t w = g->w[a];
-      int op = s->agg_op[a];
-      if (op != ORC_AGG_COUNT && !agg_is_i64(s, a)) {
-        double d;
-        if (op == ORC_AGG_SUM) {
-          d = g->sumf[a] + g->comp[a];
-        } else {
-          uint64_t b = (w >> 63) ? (w & 0x7FFFFFFFFFFFFFFFull) : ~w;
-          memcpy(&d, &b, 8);
-        }
-        memcpy(&w, &d, 8);
-      }
-      out_aggs[i * (uint64_t)s->naggs + a] = w;
-    }
-  }
+  for (uint64_t i = 0; i < ng; ++i)
+    grp_out(&G->g[i], s, out_keys + i * (uint64_t)s->nkeys, out_aggs + i * (uint64_t)s->naggs);
   tbl_free(G);
   free(tl);
   return ng;
@@ -421,6 +599,86 @@ void orc_sort_i64(const int64_t *in, int64_t *out, uint64_t n, int nthreads) {
   free(b);
 }
 
+/* ------------------------------------------------------- expression programs */
+enum { EO_COL = 0, EO_I64 = 1, EO_ADD = 3, EO_SUB = 4, EO_MUL = 5, EO_LT = 9, EO_LE, EO_GT, EO_GE, EO_EQ, EO_NE,
+       EO_AND = 15, EO_OR, EO_XOR, EO_NOT, EO_BAND, EO_BOR, EO_BXOR, EO_BNOT, EO_IF = 25 };
+#define EO_BLOCK 2048
+#define EO_STACK 32
+
+int orc_eval_int(const int32_t *op, const int32_t *arg, const int64_t *v, int nnodes, const int64_t *const *cols,
+                 int ncols, uint64_t n, int64_t *out) {
+  int depth = 0, maxd = 0;
+  for (int j = 0; j < nnodes; ++j) {  /* validate: the subset, the stack, the columns */
+    const int o = op[j];
+    int k;
+    if (o == EO_COL || o == EO_I64) k = 0;
+    else if (o == EO_NOT || o == EO_BNOT) k = 1;
+    else if (o == EO_IF) k = 3;
+    else if (o == EO_ADD || o == EO_SUB || o == EO_MUL || (o >= EO_LT && o <= EO_NE) || o == EO_AND || o == EO_OR ||
+             o == EO_XOR || o == EO_BAND || o == EO_BOR || o == EO_BXOR) k = 2;
+    else return -1;
+    if (o == EO_COL && (arg[j] < 0 || arg[j] >= ncols)) return -1;
+    if (depth < k) return -1;
+    depth = depth - k + 1;
+    if (depth > maxd) maxd = depth;
+  }
+  if (depth != 1 || maxd > EO_STACK) return -1;
+  const uint64_t nb = (n + EO_BLOCK - 1) / EO_BLOCK;
+#pragma omp parallel
+  {
+    int64_t *st = (int64_t *)malloc((size_t)EO_STACK * EO_BLOCK * sizeof(int64_t));
+#pragma omp for schedule(static)
+    for (int64_t b = 0; b < (int64_t)nb; ++b) {
+      const uint64_t lo = (uint64_t)b * EO_BLOCK, m = n - lo < EO_BLOCK ? n - lo : EO_BLOCK;
+      int sp = 0;
+      for (int j = 0; j < nnodes; ++j) {
+        const int o = op[j];
+        int64_t *r;
+        if (o == EO_COL || o == EO_I64) {
+          r = st + (size_t)sp++ * EO_BLOCK;
+          if (o == EO_COL) memcpy(r, cols[arg[j]] + lo, m * sizeof(int64_t));
+          else for (uint64_t i = 0; i < m; ++i) r[i] = v[j];
+          continue;
+        }
+        if (o == EO_NOT || o == EO_BNOT) {
+          r = st + (size_t)(sp - 1) * EO_BLOCK;
+          if (o == EO_NOT) for (uint64_t i = 0; i < m; ++i) r[i] = r[i] == 0;
+          else for (uint64_t i = 0; i < m; ++i) r[i] = ~r[i];
+          continue;
+        }
+        if (o == EO_IF) {
+          sp -= 2;
+          int64_t *c = st + (size_t)(sp - 1) * EO_BLOCK, *x = c + EO_BLOCK, *y = x + EO_BLOCK;
+          for (uint64_t i = 0; i < m; ++i) c[i] = c[i] ? x[i] : y[i];
+          continue;
+        }
+        --sp;
+        int64_t *a = st + (size_t)(sp - 1) * EO_BLOCK, *y = a + EO_BLOCK;
+        switch (o) {
+          case EO_ADD: for (uint64_t i = 0; i < m; ++i) a[i] = (int64_t)((uint64_t)a[i] + (uint64_t)y[i]); break;
+          case EO_SUB: for (uint64_t i = 0; i < m; ++i) a[i] = (int64_t)((uint64_t)a[i] - (uint64_t)y[i]); break;
+          case EO_MUL: for (uint64_t i = 0; i < m; ++i) a[i] = (int64_t)((uint64_t)a[i] * (uint64_t)y[i]); break;
+          case EO_LT: for (uint64_t i = 0; i < m; ++i) a[i] = a[i] < y[i]; break;
+          case EO_LE: for (uint64_t i = 0; i < m; ++i) a[i] = a[i] <= y[i]; break;
+          case EO_GT: for (uint64_t i = 0; i < m; ++i) a[i] = a[i] > y[i]; break;
+          case EO_GE: for (uint64_t i = 0; i < m; ++i) a[i] = a[i] >= y[i]; break;
+          case EO_EQ: for (uint64_t i = 0; i < m; ++i) a[i] = a[i] == y[i]; break;
+          case EO_NE: for (uint64_t i = 0; i < m; ++i) a[i] = a[i] != y[i]; break;
+          case EO_AND: for (uint64_t i = 0; i < m; ++i) a[i] = (a[i] != 0) & (y[i] != 0); break;
+          case EO_OR: for (uint64_t i = 0; i < m; ++i) a[i] = (a[i] != 0) | (y[i] != 0); break;
+          case EO_XOR: for (uint64_t i = 0; i < m; ++i) a[i] = (a[i] != 0) != (y[i] != 0); break;
+          case EO_BAND: for (uint64_t i = 0; i < m; ++i) a[i] &= y[i]; break;
+          case EO_BOR: for (uint64_t i = 0; i < m; ++i) a[i] |= y[i]; break;
+          default: for (uint64_t i = 0; i < m; ++i) a[i] ^= y[i]; break;
+        }
+      }
+      memcpy(out + lo, st, m * sizeof(int64_t));
+    }
+    free(st);
+  }
+  return 0;
+}
+
 uint64_t orc_multiset_hash_i64(const int64_t *v, uint64_t n) {
   uint64_t h = 0;
 #pragma omp parallel for reduction(+ : h)
@@ -446,6 +704,12 @@ static int kg_cmp(const void *a, const void *b) {
 
 uint64_t orc_groupby_pool_dyadic(uint64_t key_seed, uint64_t groups, uint64_t val_seed, uint64_t row0, uint64_t n,
                                  int64_t *out_keys, uint64_t *out_words, int nthreads) {
+  return orc_groupby_pool_dyadic_kind(ORC_GEN_POOL_KEY, key_seed, groups, val_seed, row0, n, out_keys, out_words,
+                                      nthreads);
+}
+
+uint64_t orc_groupby_pool_dyadic_kind(int kind, uint64_t key_seed, uint64_t groups, uint64_t val_seed, uint64_t row0,
+                                      uint64_t n, int64_t *out_keys, uint64_t *out_words, int nthreads) {
   if (groups == 0) return 0;
   int nt = nthreads > 0 ? nthreads : orc_max_threads();
   const uint64_t G = groups;
@@ -470,7 +734,8 @@ uint64_t orc_groupby_pool_dyadic(uint64_t key_seed, uint64_t groups, uint64_t va
     uint32_t *lo = mn + (size_t)t * G, *hi = mx + (size_t)t * G;
     const uint64_t a = (uint64_t)t * chunk, b = a + chunk > n ? n : a + chunk;
     for (uint64_t i = a; i < b; ++i) {
-      const uint64_t g = orc_gen_u64(key_seed, row0 + i) % G;
+      const uint64_t u = orc_gen_u64(key_seed, row0 + i);
+      const uint64_t g = kind == ORC_GEN_SKEW_KEY ? ORC_SKEW_INDEX(u, G) : u % G;
       const uint32_t v = (uint32_t)(orc_gen_u64(val_seed, row0 + i) >> 44);
       s[g] += v;
       c[g] += 1;

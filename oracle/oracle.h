@@ -39,7 +39,10 @@ enum {
   ORC_GEN_UNIT_F64 = 4,  /* (double)(u >> 11) * 2^-53              uniform [0,1) f64     */
   ORC_GEN_RANGE_I64 = 5, /* a + (int64)(u % b)                     uniform [a, a+b)      */
   ORC_GEN_RANGE_F64 = 6, /* (double)(a + (int64)(u % b)) / c       decimal-like f64      */
+  ORC_GEN_SKEW_KEY = 7,  /* pool[(u % a) >> ((mix64(u) >> 59) * 3 >> 2)]: log-uniform    */
 };
+/* the pool index of a skewed key (ORC_GEN_SKEW_KEY): index i takes ~1/i of the rows */
+#define ORC_SKEW_INDEX(u, a) (((u) % (uint64_t)(a)) >> (((orc_mix64(u) >> 59) * 3) >> 2))
 #define ORC_POOL_SALT 0x5DEECE66D2545F49ull
 void orc_gen_column(int kind, uint64_t seed, int64_t a, int64_t b, double c,
                     uint64_t row0, uint64_t n, void *out);
@@ -87,6 +90,13 @@ typedef struct {
  * f64 sums are Neumaier-compensated (≈ correctly rounded). nthreads<=0: all cores. */
 uint64_t orc_groupby(const orc_agg_spec *spec, uint64_t cap, int64_t *out_keys,
                      uint64_t *out_aggs, int nthreads);
+/* The same result by one fixed method: per-thread tables over the row chunks, merged into
+ * thread 0's in thread order.  orc_groupby runs this for few groups; for many (a sample
+ * estimate >= 16384, >= 2^22 rows) it range-partitions the rows and merges per partition
+ * on every thread with the same per-group order — bitwise the same result
+ * (tests/test_oracle_golden.py checks the two against each other). */
+uint64_t orc_groupby_tables(const orc_agg_spec *spec, uint64_t cap, int64_t *out_keys,
+                            uint64_t *out_aggs, int nthreads);
 
 /* ---- indexed group-by of the synthetic pool-key workload (config 3 at full size) ----
  * SELECT key, SUM(val), COUNT(*), MIN(val), MAX(val) GROUP BY key over rows
@@ -98,6 +108,10 @@ uint64_t orc_groupby(const orc_agg_spec *spec, uint64_t cap, int64_t *out_keys,
  * same generated columns (tests/test_oracle_golden.py). */
 uint64_t orc_groupby_pool_dyadic(uint64_t key_seed, uint64_t groups, uint64_t val_seed, uint64_t row0, uint64_t n,
                                  int64_t *out_keys, uint64_t *out_words, int nthreads);
+/* the same for kind ORC_GEN_POOL_KEY or ORC_GEN_SKEW_KEY keys (the skewed workload's
+ * full-size checker) */
+uint64_t orc_groupby_pool_dyadic_kind(int kind, uint64_t key_seed, uint64_t groups, uint64_t val_seed, uint64_t row0,
+                                      uint64_t n, int64_t *out_keys, uint64_t *out_words, int nthreads);
 
 /* ---- sort: ascending int64 ---- */
 void orc_sort_i64(const int64_t *in, int64_t *out, uint64_t n, int nthreads);
@@ -106,6 +120,15 @@ void orc_sort_i64(const int64_t *in, int64_t *out, uint64_t n, int nthreads);
  * Writes at most cap pairs and returns the pair count. */
 uint64_t orc_join_i64(const int64_t *build, uint64_t nb, const int64_t *probe, uint64_t np, int type,
                       int64_t *out_p, int64_t *out_b, uint64_t cap);
+
+/* ---- expression programs, integer subset, on every host core (bench CPU baseline) ----
+ * RPN nodes (op, arg, v) with oracle/expr.py's op numbering: col (int64 columns), i64,
+ * add / sub / mul (wrapping), lt le gt ge eq ne, and / or / xor / not (non-zero = true),
+ * bitand / bitor / bitxor / bitnot, if.  None of these can fail a row, so the values are
+ * those of expr.py's eval_prog (bools as 0/1).  Row blocks of 2048 on OpenMP threads.
+ * Returns 0, or -1 for a program outside the subset (nothing written). */
+int orc_eval_int(const int32_t *op, const int32_t *arg, const int64_t *v, int nnodes, const int64_t *const *cols,
+                 int ncols, uint64_t n, int64_t *out);
 
 /* order-independent multiset hash (sum of mix64 of each element), for sort parity */
 uint64_t orc_multiset_hash_i64(const int64_t *v, uint64_t n);

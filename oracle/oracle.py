@@ -65,6 +65,8 @@ def lib():
         L.orc_filter_i64.argtypes = [C.c_void_p, C.c_uint64, C.c_int, C.c_int64, C.c_void_p]
         L.orc_groupby.restype = C.c_uint64
         L.orc_groupby.argtypes = [C.POINTER(OrcAggSpec), C.c_uint64, C.c_void_p, C.c_void_p, C.c_int]
+        L.orc_groupby_tables.restype = C.c_uint64
+        L.orc_groupby_tables.argtypes = [C.POINTER(OrcAggSpec), C.c_uint64, C.c_void_p, C.c_void_p, C.c_int]
         L.orc_join_i64.restype = C.c_uint64
         L.orc_join_i64.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_int, C.c_void_p,
                                    C.c_void_p, C.c_uint64]
@@ -73,6 +75,12 @@ def lib():
         L.orc_multiset_hash_i64.restype = C.c_uint64
         L.orc_multiset_hash_i64.argtypes = [C.c_void_p, C.c_uint64]
         L.orc_max_threads.restype = C.c_int
+        L.orc_eval_int.restype = C.c_int
+        L.orc_eval_int.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_uint64,
+                                   C.c_void_p]
+        L.orc_groupby_pool_dyadic_kind.restype = C.c_uint64
+        L.orc_groupby_pool_dyadic_kind.argtypes = [C.c_int, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64,
+                                                   C.c_uint64, C.c_void_p, C.c_void_p, C.c_int]
         L.orc_groupby_pool_dyadic.restype = C.c_uint64
         L.orc_groupby_pool_dyadic.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64,
                                               C.c_void_p, C.c_void_p, C.c_int]
@@ -101,11 +109,14 @@ def filter_i64(col: np.ndarray, op: int, k: int) -> np.ndarray:
     return out[:cnt]
 
 
-def groupby(keys, aggs, values=(), preds=(), nthreads=0, cap=None, row_mask=None, agg_masks=None):
+def groupby(keys, aggs, values=(), preds=(), nthreads=0, cap=None, row_mask=None, agg_masks=None,
+            method="auto"):
     """keys: list of int64 arrays; values: list of arrays; preds: (array, op_int, literal);
     aggs: (op_int, expr_int, args).  row_mask / agg_masks[a]: optional bool arrays (the
     expression-mode WHERE and per-aggregate row masks, oracle/expr.py).  Returns
-    (keys [n, nk] int64, words [n, na] uint64) sorted by key tuple."""
+    (keys [n, nk] int64, words [n, na] uint64) sorted by key tuple.  method "tables" pins
+    orc_groupby_tables (the per-thread-table merge; "auto" range-partitions large G with a
+    bitwise-identical result)."""
     keep = []
     s = OrcAggSpec()
     if row_mask is not None:
@@ -151,21 +162,24 @@ def groupby(keys, aggs, values=(), preds=(), nthreads=0, cap=None, row_mask=None
     cap = cap if cap is not None else max(n, 1)
     ok = np.empty((cap, s.nkeys), dtype=np.int64)
     ow = np.empty((cap, max(s.naggs, 1)), dtype=np.uint64)
-    g = lib().orc_groupby(C.byref(s), cap, ok.ctypes.data, ow.ctypes.data, nthreads)
+    fn = lib().orc_groupby_tables if method == "tables" else lib().orc_groupby
+    g = fn(C.byref(s), cap, ok.ctypes.data, ow.ctypes.data, nthreads)
     if g == 2**64 - 1:
         raise ValueError("oracle group capacity too small")
     return ok[:g], ow[:g, : s.naggs]
 
 
 def groupby_pool_dyadic(groups: int, n: int, row0: int = 0, key_seed: int = 0x51, val_seed: int = 0x52,
-                        nthreads: int = 0):
+                        nthreads: int = 0, kind: int = 2):
     """Indexed oracle of the synthetic config-3 workload (oracle.h orc_groupby_pool_dyadic):
     SUM, COUNT, MIN, MAX of the dyadic value per pool key over rows [row0, row0 + n), without
     materialising the columns.  Returns (keys [m, 1] int64, words [m, 4] uint64) ordered by
-    key — the layout of groupby() with aggs SUM, COUNT, MIN, MAX."""
+    key — the layout of groupby() with aggs SUM, COUNT, MIN, MAX.  kind 7: the skewed keys
+    (GEN_SKEW_KEY) of the same pool."""
     ok = np.empty((groups, 1), dtype=np.int64)
     ow = np.empty((groups, 4), dtype=np.uint64)
-    m = lib().orc_groupby_pool_dyadic(key_seed, groups, val_seed, row0, n, ok.ctypes.data, ow.ctypes.data, nthreads)
+    m = lib().orc_groupby_pool_dyadic_kind(kind, key_seed, groups, val_seed, row0, n, ok.ctypes.data, ow.ctypes.data,
+                                           nthreads)
     if m == 2**64 - 1:
         raise MemoryError("orc_groupby_pool_dyadic: allocation failed")
     return ok[:m], ow[:m]
@@ -229,3 +243,23 @@ def join_i64_c(build: np.ndarray, probe: np.ndarray, how: str = "inner"):
         if n <= cap:
             return pi[:n], bi[:n]
         cap = n
+
+
+def eval_int(nodes, cols, n):
+    """orc_eval_int: an integer / bool RPN program (oracle/expr.py node form) over int64
+    columns on every host core; None when the program is outside the C subset."""
+    from .expr import OP
+    ops, args, vs = [], [], []
+    for node in nodes:
+        op, arg, v = (tuple(node) + (0, 0))[:3]
+        ops.append(OP[op] if isinstance(op, str) else int(op))
+        args.append(int(arg))
+        vs.append(int(v) if not isinstance(v, float) else 0)
+    if any(np.asarray(c).dtype != np.int64 for c in cols):
+        return None
+    cols = [np.ascontiguousarray(c) for c in cols]
+    ptrs = (C.c_void_p * max(len(cols), 1))(*[c.ctypes.data for c in cols])
+    o, a, v = (np.asarray(x, dtype=t) for x, t in ((ops, np.int32), (args, np.int32), (vs, np.int64)))
+    out = np.empty(max(n, 1), dtype=np.int64)
+    r = lib().orc_eval_int(o.ctypes.data, a.ctypes.data, v.ctypes.data, len(ops), ptrs, len(cols), n, out.ctypes.data)
+    return None if r else out[:n]

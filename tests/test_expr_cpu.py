@@ -430,3 +430,46 @@ def test_plan_select_star():
         with pytest.raises(NutError, match=frag):
             Plan(sql)
     Plan("select * from t where a > 1.5 and b < 3").prepare({"a": "int64", "b": "float64", "c": "int64"})
+
+
+def test_c_integer_evaluator_matches_numpy_oracle():
+    """oracle.eval_int (the CPU baseline's C evaluator of integer / bool programs) equals
+    eval_prog on random programs of its subset over columns with extremes, and declines
+    programs outside it (f64, MOD, shifts)."""
+    from oracle import oracle as orc
+    rng = np.random.default_rng(7)
+    n = (1 << 20) + 77
+    cols = [rng.integers(-5, 6, n), rng.integers(I64MIN, I64MAX, n, endpoint=True), rng.integers(0, 3, n)]
+    cols[1][:4] = [I64MIN, I64MAX, 0, -1]
+    bin_ops = ["add", "sub", "mul", "lt", "le", "gt", "ge", "eq", "ne", "and", "or", "xor", "bitand", "bitor",
+               "bitxor"]
+    for trial in range(40):
+        prog, depth = [], 0
+        for _ in range(int(rng.integers(1, 14))):
+            r = rng.random()
+            if depth >= 3 and r < 0.2:
+                prog.append(("if",))
+                depth -= 2
+            elif depth >= 2 and r < 0.7:
+                prog.append((bin_ops[int(rng.integers(len(bin_ops)))],))
+                depth -= 1
+            elif depth >= 1 and r < 0.78:
+                prog.append((["not", "bitnot"][int(rng.integers(2))],))
+            elif r < 0.9:
+                prog.append(("col", int(rng.integers(3))))
+                depth += 1
+            else:
+                prog.append(("i64", 0, int(rng.integers(-9, 10))))
+                depth += 1
+        while depth > 1:
+            prog.append(("add",))
+            depth -= 1
+        if depth == 0:
+            prog = [("col", 1)]
+        want, _, err = eval_prog(prog, cols)
+        got = orc.eval_int(prog, cols, n)
+        assert got is not None, prog
+        assert not err.any() and np.array_equal(got, want), (trial, prog)
+    assert orc.eval_int([("col", 0), ("col", 1), ("mod",)], cols, n) is None
+    assert orc.eval_int([("col", 0), ("i64", 0, 3), ("shl",)], cols, n) is None
+    assert orc.eval_int([("col", 0)], [np.zeros(n)], n) is None

@@ -107,3 +107,33 @@ def test_groupby_full_config3_large_groups(ex, orc, G, levels):
     assert np.array_equal(gk, ok)
     assert np.array_equal(gw, ow), "dyadic sums / counts / min / max must be bit-exact"
     assert int(gw[:, 1].sum()) == n
+
+
+@pytest.mark.parametrize("skew", [False, True])
+def test_groupby_full_config3_ordered_to_host(ex, orc, skew):
+    """Config 3 at G = 1e7 as the bench runs it (nut_groupby_to_host, the key-range ordered
+    path) on 1e9 rows: uniform pool keys, and Zipf-like keys (GEN_SKEW_KEY: pool index i on
+    ~1/i of the rows, the top key ~6 %) whose heavy keys overflow their capped partitions
+    into the arenas — both bit-exact against the indexed oracle, both on the ordered path."""
+    import torch
+    from nutdb_amd import Agg, AggQuery
+    from nutdb_amd import _lib as L
+    from nutdb_amd.workloads import GB_KEY_SEED, GB_VAL_SEED, gen, groupby_cols
+    n, G = 1_000_000_000, 10_000_000
+    ks, vs = groupby_cols(G, dyadic=True, skew=skew)
+    key, val = gen(ex, ks, n), gen(ex, vs, n)
+    out = tuple(torch.empty((G, w), dtype=torch.int64, pin_memory=True).numpy() for w in (1, 4))
+    q = AggQuery(keys=[key], values=[val], aggs=[Agg("sum", "col", (0,)), Agg("count"), Agg("min", "col", (0,)),
+                                                   Agg("max", "col", (0,))])
+    gk, gw = ex.groupby_to_host(q, group_hint=G, out=out)
+    st, ovf = ex.groupby_stats(), ex.groupby_overflow_rows()
+    gk, gw = gk.copy(), gw.copy()
+    del key, val, out
+    assert st["path"] == "partitioned_ordered", st
+    assert (ovf > 0) == skew, ovf
+    ok, ow = orc.groupby_pool_dyadic(G, n, key_seed=GB_KEY_SEED, val_seed=GB_VAL_SEED,
+                                     kind=L.GEN_SKEW_KEY if skew else L.GEN_POOL_KEY)
+    gc.collect()
+    assert np.array_equal(gk, ok)
+    assert np.array_equal(gw.view(np.uint64), ow), "dyadic sums / counts / min / max must be bit-exact"
+    assert int(gw[:, 1].sum()) == n

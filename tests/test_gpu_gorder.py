@@ -3,7 +3,8 @@ key-range partitions (GpRange), per-partition ordering, the result streamed to p
 host arrays chunk by chunk — must return exactly what nut_groupby + nut_groups_to_host
 return (the hashed path + device ordering), and the oracle's groups: keys, counts, MIN /
 MAX bit-exact, f64 sums within F64_SUM_RTOL (exact for dyadic values).  Shapes it does not
-take (skewed keys, pageable outputs, the option off) fall back and give the same result."""
+take (clustered keys, pageable outputs, the option off) fall back and give the same result;
+heavy keys stay on it through the overflow arenas."""
 import numpy as np
 import pytest
 import torch
@@ -61,24 +62,72 @@ def test_ordered_vs_oracle_and_hashed(ex, orc, G, dyadic):
         assert np.array_equal(hw, w)
 
 
+def check_signed(keys, words, ok, ow, absum):
+    """f64 sums of signed values: within F64_SUM_RTOL of the group's sum of |value| (the sums
+    may cancel, so a relative bound on the sum itself does not apply); the rest exact."""
+    assert np.array_equal(keys, ok)
+    a, b = words[:, 0].view(np.float64), ow[:, 0].view(np.float64)
+    assert np.all(np.abs(a - b) <= F64_SUM_RTOL * absum[:, 0].view(np.float64) + 1e-300)
+    assert np.array_equal(words[:, 1:], ow[:, 1:])
+
+
 def test_ordered_extreme_keys(ex, orc):
-    """INT64_MIN (the tables' empty marker), INT64_MAX and -0.0 / NaN-free extremes at both
-    ends of the range: the edge cells clamp, the order holds."""
+    """INT64_MIN (the tables' empty marker) and INT64_MAX each on 1/1000 of the rows, signed
+    values and -0.0: the edge cells clamp, the order holds, and both heavy keys' excess
+    rows go through the overflow arenas (the call stays on the ordered path)."""
     rng = np.random.default_rng(7)
     pool = rng.integers(I64_MIN, I64_MAX, 2_000_000, dtype=np.int64)
     pool[:4] = [I64_MIN, I64_MAX, I64_MIN + 1, I64_MAX - 1]
     key = pool[rng.integers(0, len(pool), N)]
-    key[::100_000] = I64_MIN  # (light enough to stay inside the capped regions)
-    key[1::100_000] = I64_MAX
-    val = rng.random(N)  # (positive: sums of ~8 values without cancellation, so 1e-12 relative holds per group)
+    key[::1000] = I64_MIN
+    key[1::1000] = I64_MAX
+    val = rng.standard_normal(N)
     val[::97] = -0.0
     G = len(np.unique(key))
     q = gb_query(dev(key, ex), dev(val, ex))
     k, w, path = run_to_host(ex, q, G)
     assert path == "partitioned_ordered"
+    assert ex.groupby_overflow_rows() > 0
     ok, ow = orc.groupby([key], AGGS4, values=[val])
-    check(k, w, ok, ow)
+    _, absum = orc.groupby([key], [(0, 0, (0,))], values=[np.abs(val)])
+    check_signed(k, w, ok, ow, absum)
     assert k[0, 0] == I64_MIN and k[-1, 0] == I64_MAX
+
+
+@pytest.mark.parametrize("share", [0.003, 0.02, 0.1])
+def test_ordered_heavy_key(ex, orc, share):
+    """One key on `share` of the rows: 0.3 % passes level 0 and overflows its level-1 region
+    (ADVICE r4: the aggregation must not read past the region, and the result must hold);
+    2 % and 10 % overflow level 0 too.  The excess is aggregated from the arenas and folded
+    into the ordered result — same groups as the oracle, ordered path kept."""
+    G = 2_000_000
+    key = orc.gen_column(2, 0x6A, N, a=G)
+    rng = np.random.default_rng(11)
+    heavy = rng.random(N) < share
+    key[heavy] = key[12345]
+    val = orc.gen_column(3, 0x6B, N)
+    q = gb_query(dev(key, ex), dev(val, ex))
+    k, w, path = run_to_host(ex, q, G)
+    assert path == "partitioned_ordered"
+    assert ex.groupby_overflow_rows() > 0
+    ok, ow = orc.groupby([key], AGGS4, values=[val])
+    check(k, w, ok, ow, sums_exact=True)
+
+
+def test_ordered_skew_generator(ex, orc):
+    """Zipf-like keys (GEN_SKEW_KEY: pool index i on ~1/i of the rows, the top key ~6 %)
+    on the ordered path vs the indexed oracle of the same generator."""
+    from nutdb_amd import _lib as L
+    G = 4_000_000
+    key = ex.gen_column(L.GEN_SKEW_KEY, 0x51, N, a=G)
+    val = ex.gen_column(L.GEN_DYADIC, 0x52, N)
+    q = gb_query(key, val)
+    hint = int(orc.groupby_pool_dyadic(G, N, key_seed=0x51, val_seed=0x52, kind=7)[0].shape[0])
+    k, w, path = run_to_host(ex, q, hint)
+    ok, ow = orc.groupby_pool_dyadic(G, N, key_seed=0x51, val_seed=0x52, kind=7)
+    assert path == "partitioned_ordered"
+    assert ex.groupby_overflow_rows() > 0
+    assert np.array_equal(k, ok) and np.array_equal(w.view(np.uint64), ow)
 
 
 def test_ordered_i64_values(ex, orc):
@@ -95,16 +144,31 @@ def test_ordered_i64_values(ex, orc):
     assert np.array_equal(k, ok) and np.array_equal(w, ow)
 
 
-def test_skewed_keys_fall_back(ex, orc):
-    """Half the rows on one key overflow its range cell's capped region: the hashed path
-    runs instead (same result)."""
+def test_half_rows_on_one_key(ex, orc):
+    """Half the rows on one key: the level-0 arena takes most of them (or, exhausted,
+    the call falls back to the hashed path); either way the same result."""
     G = 2_000_000
     key = orc.gen_column(2, 0x64, N, a=G)
     key[::2] = key[1]
     val = orc.gen_column(3, 0x65, N)
     q = gb_query(dev(key, ex), dev(val, ex))
     k, w, path = run_to_host(ex, q, G)
-    assert path != "partitioned_ordered"
+    ok, ow = orc.groupby([key], AGGS4, values=[val])
+    check(k, w, ok, ow, sums_exact=True)
+
+
+def test_clustered_keys_declined_up_front(ex, orc):
+    """Half the distinct keys inside 1/2^20 of the sampled range would overfill one
+    partition's table: the sample admission declines before any work (hashed path)."""
+    G = 2_000_000
+    rng = np.random.default_rng(13)
+    pool = np.concatenate([rng.integers(I64_MIN, I64_MAX, G // 2, dtype=np.int64),
+                           rng.integers(0, 1 << 43, G // 2, dtype=np.int64)])
+    key = pool[rng.integers(0, G, N)]
+    val = orc.gen_column(3, 0x6C, N)
+    q = gb_query(dev(key, ex), dev(val, ex))
+    k, w, path = run_to_host(ex, q, len(np.unique(key)))
+    assert path == "partitioned_direct"
     ok, ow = orc.groupby([key], AGGS4, values=[val])
     check(k, w, ok, ow, sums_exact=True)
 

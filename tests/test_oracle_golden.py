@@ -118,3 +118,27 @@ def test_groupby_pool_indexed_matches_hash_oracle(orc, groups, n, row0):
     assert np.array_equal(ik, hk)
     assert np.array_equal(iw, hw)
     assert int(iw[:, 1].sum()) == n
+
+
+@pytest.mark.parametrize("groups,nk,masked", [(100_000, 1, False), (1_000_000, 1, True), (300_000, 2, True),
+                                              (20_000, 1, False)])
+def test_groupby_partitioned_merge_is_bitwise_the_table_merge(orc, groups, nk, masked):
+    """orc_groupby's key-range partitioned merge (large G: the CPU baseline's path) gives
+    the per-thread-table merge's result bit for bit — keys, counts, i64 / f64 MIN / MAX and
+    Neumaier f64 sums of non-dyadic values (the same per-group fold and merge order) —
+    with a WHERE, a row mask and two keys."""
+    n = (1 << 22) + 12345
+    from nutdb_amd.workloads import groupby_cols
+    ks, _ = groupby_cols(groups, dyadic=True)
+    key = orc.gen(ks, n)
+    keys = [key] if nk == 1 else [key, orc.gen_column(5, 0x3A, n, a=-3, b=7)]
+    v = orc.gen_column(4, 0x55, n)              # unit f64: sums round
+    iv = orc.gen_column(0, 0x56, n) - (1 << 61)  # signed i64
+    aggs = [(0, 0, (0,)), (1, 0, ()), (2, 0, (0,)), (3, 0, (0,)), (0, 0, (1,)), (2, 0, (1,))]
+    kw = {}
+    if masked:
+        kw = {"preds": [(iv, 0, 1 << 60)], "row_mask": (key & 7) != 3}
+    a = orc.groupby(keys, aggs, values=[v, iv], **kw)
+    b = orc.groupby(keys, aggs, values=[v, iv], method="tables", **kw)
+    assert len(a[0]) > 1000
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
