@@ -101,8 +101,17 @@ typedef enum {
 nut_status nut_ctx_groupby_stats(nut_ctx *ctx, uint32_t *path, uint32_t *levels, uint32_t *optimistic);
 /* Rows of the last nut_groupby_to_host on the ordered path (NUT_GB_PARTITIONED_ORDERED)
  * that did not fit their capped partition regions — a heavy key's excess, mostly — and
- * were aggregated from its overflow arenas and folded into the result (0: none). */
-nut_status nut_ctx_groupby_overflow(nut_ctx *ctx, uint64_t *rows);
+ * were aggregated from its overflow arenas and folded into the result (0: none); and, when
+ * that call took the hashed path instead, why the ordered path declined. */
+typedef enum {
+  NUT_GB_DECLINE_NONE = 0,
+  NUT_GB_DECLINE_SHAPE = 1,      /* not its shape: keys / aggregates / size / hint / alignment / key span */
+  NUT_GB_DECLINE_CLUSTERED = 2,  /* the sample's distinct keys crowd some partitions (admission, before any work) */
+  NUT_GB_DECLINE_ARENA = 3,      /* an overflow arena filled up */
+  NUT_GB_DECLINE_CAPACITY = 4,   /* partition regions or tables do not fit their buffers */
+  NUT_GB_DECLINE_TABLE = 5       /* a partition held more groups than its table */
+} nut_gb_decline;
+nut_status nut_ctx_groupby_overflow(nut_ctx *ctx, uint64_t *rows, uint32_t *declined);
 /* The compiled Q1 kernel's launch shape on this context's device (NUT_OPT_PRIV_PROBE):
  * threads per workgroup and workgroups per CU the next launch takes, and the probe's best
  * kernel time per candidate shape {192 x 2, 128 x 3, 128 x 4} in ms (-1: not probed in

@@ -1046,7 +1046,14 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
   const int bits1 = 14 - bits0;
   const double lam = (double)group_hint / (double)(1 << (bits0 + bits1));
   c->gb_overflow_rows = 0;
-  if (!shape || lam < 100 || ((uintptr_t)s->keys[0] & 15)) return NUT_ERR_UNSUPPORTED;
+  c->gb_decline = 0;
+  // every NUT_ERR_UNSUPPORTED names its reason (nut_ctx_groupby_overflow): the caller then
+  // runs the hashed path, with the same result
+  auto decline = [c](uint32_t why) {
+    c->gb_decline = why;
+    return NUT_ERR_UNSUPPORTED;
+  };
+  if (!shape || lam < 100 || ((uintptr_t)s->keys[0] & 15)) return decline(NUT_GB_DECLINE_SHAPE);
   hipStream_t st = c->stream;
   // ---- the key range from a strided sample (+ 1/1024 of the span on either side)
   constexpr uint32_t kSample = 65536;
@@ -1065,7 +1072,7 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
   GpRange rg{};
   rg.lo = lo;
   rg.span = hi - lo;
-  if (rg.span < (1ull << 16)) return NUT_ERR_UNSUPPORTED;  // (mul must fit 32 bits; tiny spans hash fine)
+  if (rg.span < (1ull << 16)) return decline(NUT_GB_DECLINE_SHAPE);  // (mul must fit 32 bits; tiny spans hash fine)
   rg.t = rg.span >> 32 ? 32 - __builtin_clzll(rg.span) : 0;
   rg.mul = (uint32_t)((1ull << 46) / ((rg.span >> rg.t) + 1));
   {  // admission: the sample's distinct keys spread over the level-0 partitions.  Keys
@@ -1084,7 +1091,7 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
       for (int64_t k : smp)
         if (rg.cell((uint64_t)k) >> bits1 == p) ks.push_back(k);
       std::sort(ks.begin(), ks.end());
-      if ((uint64_t)(std::unique(ks.begin(), ks.end()) - ks.begin()) > bound) return NUT_ERR_UNSUPPORTED;
+      if ((uint64_t)(std::unique(ks.begin(), ks.end()) - ks.begin()) > bound) return decline(NUT_GB_DECLINE_CLUSTERED);
     }
   }
   // ---- partition buffers: level 0 capped over O (2 x rows per array), level 1 into B2
@@ -1147,7 +1154,7 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
   c->timer.begin(st, NUT_KERNEL_AGGREGATE);
   e = gp_level(c, mm, segs, bits1, src, O, narr, false, false, hist, &p0, 0, abase0, bits0, &rg, darena, acap0);
   c->timer.end(st);
-  if (e) return e == NUT_ERR_CAPACITY ? NUT_ERR_UNSUPPORTED : e;
+  if (e) return e == NUT_ERR_CAPACITY ? decline(NUT_GB_DECLINE_ARENA) : e;
   // ---- level-1 regions, as the hashed path sizes them
   const uint32_t np0 = (uint32_t)(p0.size() / 2), nb1 = 1u << bits1;
   std::vector<GpSeg> s2;
@@ -1159,7 +1166,7 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
     ovf1 += sg.ocap << bits1;
     s2.push_back(sg);
   }
-  if (ovf1 + 2 * GP_TILE > b2rows) return NUT_ERR_UNSUPPORTED;
+  if (ovf1 + 2 * GP_TILE > b2rows) return decline(NUT_GB_DECLINE_CAPACITY);
   const uint64_t acap1 = b2rows - ovf1 - 2 * GP_TILE;  // level 1's arena: rows [ovf1, ovf1 + acap1) of B2
   const uint64_t nparts = (uint64_t)np0 * nb1;
   // chunks of level-0 partitions (in key order) halving in size — 1/2, 1/4, 1/8, 1/16,
@@ -1206,9 +1213,9 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
   }
   const uint64_t per = std::max<uint64_t>(64, 2 * ((group_hint + nparts - 1) / nparts));
   const uint32_t lcap = agg_lcap(c, 1, na, per, true);
-  if (!lcap) return NUT_ERR_UNSUPPORTED;
+  if (!lcap) return decline(NUT_GB_DECLINE_CAPACITY);
   const uint64_t dregion = (uint64_t)lcap + 1;
-  if (dregion > 4097) return NUT_ERR_UNSUPPORTED;  // (the ordering pass holds a region in LDS, <= 17 keys per thread)
+  if (dregion > 4097) return decline(NUT_GB_DECLINE_CAPACITY);  // (the ordering pass holds a region in LDS, <= 17 keys per thread)
   e = alloc_stage(g, nparts * dregion);
   if (e) return e;
   // device tables, uploaded once
@@ -1342,8 +1349,8 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
   const uint64_t used0 = c->host_pinned[2], used1 = c->host_pinned[3];
   NUT_HIP(hipStreamSynchronize(c->copy_stream));
   for (uint64_t f : flags)
-    if (f) return NUT_ERR_UNSUPPORTED;  // a level-1 run found the arena full
-  if (ctl[1] & 4u) return NUT_ERR_UNSUPPORTED;  // a partition outgrew its block's table
+    if (f) return decline(NUT_GB_DECLINE_ARENA);  // a level-1 run found the arena full
+  if (ctl[1] & 4u) return decline(NUT_GB_DECLINE_TABLE);  // a partition outgrew its block's table
   c->gb_overflow_rows = used0 + used1;
   if (used0 + used1 && !over) {
     // the arenas' rows (heavy keys' excess, mostly) aggregated on their own and folded
@@ -1557,9 +1564,10 @@ static nut_status probe_priv_shape(nut_groups *g, const nut_agg_spec *s, uint64_
   return alloc_table(g, cap);  // the probe's partial groups are discarded
 }
 
-nut_status nut_ctx_groupby_overflow(nut_ctx *c, uint64_t *rows) {
-  if (!c || !rows) return fail(NUT_ERR_INVALID_ARG, "nut_ctx_groupby_overflow: NULL argument");
-  *rows = c->gb_overflow_rows;
+nut_status nut_ctx_groupby_overflow(nut_ctx *c, uint64_t *rows, uint32_t *declined) {
+  if (!c) return fail(NUT_ERR_INVALID_ARG, "nut_ctx_groupby_overflow: NULL context");
+  if (rows) *rows = c->gb_overflow_rows;
+  if (declined) *declined = c->gb_decline;
   return NUT_OK;
 }
 

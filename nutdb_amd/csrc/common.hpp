@@ -206,6 +206,7 @@ struct nut_ctx {
   int priv_probe = -1;  // the compiled Q1 kernel's shape during the shape probe (aggregate.hip)
   uint32_t gb_path = 0, gb_levels = 0, gb_optimistic = 0;  // nut_ctx_groupby_stats
   uint64_t gb_overflow_rows = 0;  // nut_ctx_groupby_overflow (the ordered path's arenas)
+  uint32_t gb_decline = 0;        //   and why the ordered path last declined (nut_gb_decline)
 };
 
 namespace nut {

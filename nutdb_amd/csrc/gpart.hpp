@@ -110,7 +110,10 @@ __global__ __launch_bounds__(GP_HTHREADS) void gp_hist_kernel(const uint64_t *__
 // one compact partitioned array).
 // (VAR: tuning variants for scripts/tune/gp_tune.hip — bit 0 non-temporal stores, bit 1 no
 // stores, bit 2 tile-sequential output, bit 3 sequential output after the scattered address
-// is computed.  The product runs VAR = 1: non-temporal stores measured 7.16-7.24 vs
+// is computed, bit 5 early loads (one key array: the first value array's loads at the top
+// of the tile, in flight while the tile ranks; the next tile's keys right after this
+// tile's keys are staged, before their write-out; every write-out a fixed number of
+// stores).  The product runs VAR = 1: non-temporal stores measured 7.16-7.24 vs
 // 7.34-7.37 ms per 1e9-record level on two boxes, profiles/r03/gp_tune_*.log)
 // RANGE: digits (rg.cell(k) >> shift) & (BINS - 1) of one key (GpRange) instead of the hash.
 template <int NK, int T, int VAR = 1, int BITS = 8, bool RANGE = false>
@@ -164,6 +167,10 @@ __global__ __launch_bounds__(T) void gp_scatter_kernel(GpArrays ar, const GpSeg 
     asm volatile("" : "+v"(tid_));
     const int tid = tid_;
     const uint32_t s = tile_seg[t];
+    constexpr bool EARLY = (VAR & 32) && NK == 1;
+    uint64_t v[GP_ITEMS];
+    if constexpr (EARLY)
+      if (ar.narr > 3) load_arr(ar.src[3], lo, n, v);  // in flight while the tile ranks
     if (tid < BINS) s_cnt[tid] = 0;
     __syncthreads();
     // rank: sd[i] = digit | in-digit rank << 8, then the tile slot once the digit starts are known
@@ -240,8 +247,10 @@ __global__ __launch_bounds__(T) void gp_scatter_kernel(GpArrays ar, const GpSeg 
       // registers) above the first store
 #pragma unroll 2
       for (int i = 0; i < GP_ITEMS; ++i) {
-        const uint32_t j = (uint32_t)i * T + tid;
-        if (j < n) {
+        // (EARLY: unconditional, clamped to the tile's last record — a repeat stores the
+        // same word — so that the stores behind a load are a known count)
+        const uint32_t j = EARLY ? min((uint32_t)i * T + tid, n - 1) : (uint32_t)i * T + tid;
+        if (EARLY || j < n) {
           const uint64_t x = s_stage[j];
           uint64_t o = (VAR & 4) ? lo + j : s_gb[s_dig[j]] + j;
           if (VAR & 8) o = o == ~0ull ? o : lo + j;
@@ -255,21 +264,28 @@ __global__ __launch_bounds__(T) void gp_scatter_kernel(GpArrays ar, const GpSeg 
         }
       }
     };
-    uint64_t v[GP_ITEMS];
     stage(k1);
-    if constexpr (NK == 2) {
-      flush(ar.dst[1]);
-      stage(k2);
-    }
-    if (ar.narr > 3) load_arr(ar.src[3], lo, n, v);
-    flush(ar.dst[NK == 2 ? 2 : 1]);
     const uint32_t next = t + gridDim.x;
     uint64_t nlo = 0;
     uint32_t nn = 0;
-    if (next < ntiles) {  // the key registers are free
-      tile_range(next, nlo, nn);
-      load_arr(ar.src[1], nlo, nn, k1);
-      if constexpr (NK == 2) load_arr(ar.src[2], nlo, nn, k2);
+    if constexpr (EARLY) {  // the key registers are free: the next tile's keys now
+      if (next < ntiles) {
+        tile_range(next, nlo, nn);
+        load_arr(ar.src[1], nlo, nn, k1);
+      }
+      flush(ar.dst[1]);
+    } else {
+      if constexpr (NK == 2) {
+        flush(ar.dst[1]);
+        stage(k2);
+      }
+      if (ar.narr > 3) load_arr(ar.src[3], lo, n, v);
+      flush(ar.dst[NK == 2 ? 2 : 1]);
+      if (next < ntiles) {  // the key registers are free
+        tile_range(next, nlo, nn);
+        load_arr(ar.src[1], nlo, nn, k1);
+        if constexpr (NK == 2) load_arr(ar.src[2], nlo, nn, k2);
+      }
     }
     for (int a = 3; a < ar.narr; ++a) {
       stage(v);

@@ -47,13 +47,23 @@ constexpr uint32_t MS_TILE = MS_THREADS * MS_ITEMS;  // keys staged in LDS at a 
 constexpr int MS_BITS = 9;                          // digit width of a scatter level
 constexpr int MS_BINS = 1 << MS_BITS;               // 512: MS_TILE / 512 = 28 keys (224 B) per digit per stage
 static_assert(MS_BINS <= MS_THREADS, "one scan thread per digit");
-// local-sort classes: threads x max items per thread (ms_local_kernel)
-constexpr int LS_S_THREADS = 256, LS_S_ITEMS = 8;    // <= 2048 keys
-constexpr int LS_M_THREADS = 512, LS_M_ITEMS = 12;   // <= 6144 keys, 2 workgroups per CU
-constexpr int LS_L_THREADS = 1024, LS_L_ITEMS = 24;  // <= 24576 keys
+// local-sort classes: threads x max items per thread (ms_local_kernel), by segment size.
+// The segments of a 1.25e9-key sort (~4768 keys) take class 1: 256 threads x 20 keys, three
+// workgroups per CU (51 KB of LDS each) — scripts/tune/local_tune.hip, 262144 segments of
+// 4768 keys: 5.70 ms vs 6.65 for 512 x 12 at two per CU (profiles/r05/sort/)
+constexpr int LS_NCLS = 4;
+constexpr int LS_S_THREADS = 256, LS_S_ITEMS = 8;     // class 0: <= 2048 keys
+constexpr int LS_M_THREADS = 256, LS_M_ITEMS = 20;    // class 1: <= 5120 keys, 3 workgroups per CU
+constexpr int LS_M2_THREADS = 512, LS_M2_ITEMS = 12;  // class 2: <= 6144 keys, 2 workgroups per CU
+constexpr int LS_L_THREADS = 1024, LS_L_ITEMS = 24;   // class 3: <= 24576 keys
 constexpr uint64_t LS_S_CAP = LS_S_THREADS * LS_S_ITEMS;
 constexpr uint64_t LS_M_CAP = LS_M_THREADS * LS_M_ITEMS;
+constexpr uint64_t LS_M2_CAP = LS_M2_THREADS * LS_M2_ITEMS;
 constexpr uint64_t LS_CAP = LS_L_THREADS * LS_L_ITEMS;
+// the class of a segment of c keys: 0 .. LS_NCLS - 1, or LS_NCLS when no class holds it
+__host__ __device__ constexpr int ls_class(uint64_t c) {
+  return c <= LS_S_CAP ? 0 : c <= LS_M_CAP ? 1 : c <= LS_M2_CAP ? 2 : c <= LS_CAP ? 3 : LS_NCLS;
+}
 
 // A contiguous run [start, start + count) of one of the buffers.
 constexpr uint64_t kSameDst = ~0ull;
@@ -358,7 +368,7 @@ __global__ __launch_bounds__(T, 2048 / T) void ms_scatter_kernel(MsBufs bf, cons
 // ---------------------------------------------------------------- device-planned level
 // After a level's histogram: one block per segment, one thread per digit.  The digit's
 // exclusive prefix gives the scatter cursor and the sub-segment it will hold; the
-// sub-segment goes straight into the list of its local-sort class (3 = too large for one:
+// sub-segment goes straight into the list of its local-sort class (LS_NCLS = too large for one:
 // the host takes it to another level).  Replaces a host round trip over every
 // (segment, digit) pair — 2^18 of them at the second level of 1.25e9 keys.
 __global__ __launch_bounds__(MS_BINS) void ms_plan_kernel(const MsSeg *__restrict__ segs,
@@ -386,9 +396,9 @@ __global__ __launch_bounds__(MS_BINS) void ms_plan_kernel(const MsSeg *__restric
   cursor[(uint64_t)blockIdx.x * MS_BINS + d] = start;
   // list slots: one atomic per (wave, class present) — a per-thread atomic on four
   // addresses serialised 2^18 claims at the memory side (3 ms)
-  const int cls = c == 0 ? -1 : (c <= LS_S_CAP ? 0 : (c <= LS_M_CAP ? 1 : (c <= LS_CAP ? 2 : 3)));
+  const int cls = c == 0 ? -1 : ls_class(c);
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
+  for (int k = 0; k <= LS_NCLS; ++k) {
     const uint64_t m = __ballot(cls == k);
     if (!m) continue;
     const int leader = __builtin_ctzll(m);
@@ -427,8 +437,8 @@ __global__ __launch_bounds__(MS_BINS) void ms_plan_capped_kernel(const unsigned 
 #pragma unroll
   for (int w = 0; w < MS_BINS / kWave; ++w) add += (w < wave) ? s_wsum[w] : 0ull;
   const uint64_t dst = dbase[blockIdx.x] + incl - c + add;
-  const int cls = c == 0 ? -1 : (c <= LS_S_CAP ? 0 : (c <= LS_M_CAP ? 1 : (c <= LS_CAP ? 2 : 3)));
-  if (cls == 3) atomicOr(oflag, 1ull);
+  const int cls = c == 0 ? -1 : ls_class(c);
+  if (cls == LS_NCLS) atomicOr(oflag, 1ull);
   // cell r's keys: (k - m.base) >> m.t in [x0, x1), x_v = ceil(v 2^32 / mul) (the first x with
   // umulhi(x, mul) >= v), x1 capped at lim + 1: the segment's base and the bits that vary
   const uint64_t x0 = ((r << 32) + m.mul - 1) / m.mul;
@@ -437,7 +447,7 @@ __global__ __launch_bounds__(MS_BINS) void ms_plan_capped_kernel(const unsigned 
   const uint64_t sbase = m.base + (x0 << m.t);
   const uint32_t hi = width <= 1 ? 0u : (uint32_t)(64 - __builtin_clzll(width - 1));
 #pragma unroll
-  for (int k = 0; k < 3; ++k) {
+  for (int k = 0; k < LS_NCLS; ++k) {
     const uint64_t mk = __ballot(cls == k);
     if (!mk) continue;
     const int leader = __builtin_ctzll(mk);
@@ -610,14 +620,15 @@ struct LocalCfg {
   // buckets and windows of ~10 keys: scripts/tune/local_tune.hip -DLT_PLAIN on 262144
   // segments of 4768 keys, two runs: 6.53-6.57 ms vs 6.81-6.85 for 2048 buckets / stride 12
   // (profiles/r04/sort/local_tune_plain.log)
-  static constexpr int SB = SB_ ? SB_ : (CAP > 4096 ? 12 : (CAP > 2048 ? 11 : 9));
+  // (256 x 20: 2048 buckets keep its LDS at 51 KB, three workgroups per CU)
+  static constexpr int SB = SB_ ? SB_ : (CAP > 4096 ? (THREADS >= 512 ? 12 : 11) : (CAP > 2048 ? 11 : 9));
   static constexpr int WS = WS_ ? WS_ : (CAP > 4096 && CAP <= 8192 ? 10 : LS_WS);
   static constexpr int NB = 1 << SB;
   static constexpr int BPT = NB / THREADS;  // buckets per thread in the scan
-  static_assert(BPT * THREADS == NB && BPT <= 8, "whole buckets per thread");
+  static_assert(BPT * THREADS == NB && BPT <= 16, "whole buckets per thread");
   static_assert(CAP <= 2 * LDS_KEYS, "at most two rounds");
   static constexpr int WPT = (CAP / WS + THREADS - 1) / THREADS;  // windows per thread
-  static_assert(WPT <= 2, "at most two windows per thread");
+  static_assert(WPT <= 3, "at most three windows per thread");
   // LDS: one round of 8-B keys, bucket counts -> starts, window starts, scan words
   static constexpr int NWIN = CAP / WS + 2;  // window table entries (+ end)
   static constexpr int BYTES = LDS_KEYS * 8 + ((NB + 1) + NWIN + 16 + 2) * 4;
@@ -626,8 +637,8 @@ struct LocalCfg {
 // block-wide exclusive scan of one value per thread (THREADS <= 1024); returns the prefix
 // and writes the total to *total.  `ws` = 16 words of LDS.
 template <int THREADS>
-__device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t *ws, uint32_t *total) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t *ws, uint32_t *total, int tid) {
+  const int lane = tid & 63, wave = tid >> 6;
   uint32_t incl = x;
 #pragma unroll
   for (int off = 1; off < 64; off <<= 1) {
@@ -735,7 +746,18 @@ __global__ __launch_bounds__(THREADS, 4) void ms_local_kernel(MsBufs bf, const M
   uint32_t *s_win = s_off + NB + 1;                        // [NWIN] window starts
   uint32_t *s_ws = s_win + C::NWIN;                        // 16 scan words
   uint32_t *s_misc = s_ws + 16;                            // [0] max window, [1] round split
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // The thread id without a long-lived VGPR: the wave index in an SGPR and the lane from
+  // v_mbcnt, recomputed where needed.  Kept in a VGPR across the segment loop, threadIdx.x
+  // was spilled and reloaded before the back edge, and that scratch load — issued after
+  // the next segment's loads — made the loop head wait for vmcnt(0): for the prefetch
+  // and for this segment's write-out stores (in-order counter)
+  const int wv_s = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+  auto cur_tid = [&]() -> int {  // (volatile: recomputed where used, never hoisted and spilled)
+    int l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return (wv_s << 6) | l;
+  };
+  const int tid = cur_tid(), lane = tid & 63, wave = wv_s;
   uint64_t key[MAXK];
 #ifdef NUT_MSD_STAMPS
   uint64_t st_last = 0, st_acc[7] = {0, 0, 0, 0, 0, 0, 0};
@@ -744,7 +766,7 @@ __global__ __launch_bounds__(THREADS, 4) void ms_local_kernel(MsBufs bf, const M
   // Raw loads only: the flip and the padding of positions past the count are applied when
   // the segment is processed (finish_load), so a prefetch does not wait for its data here
   auto load = [&](const MsSeg g) {
-    int tq = tid;  // opaque: the item offsets are recomputed, not kept (or spilled) in registers
+    int tq = cur_tid();  // opaque: the item offsets are recomputed, not kept (or spilled) in registers
     asm volatile("" : "+v"(tq));
     const uint32_t cc = (uint32_t)g.count, kk = (cc + THREADS - 1) / THREADS;
     const uint32_t pp = (uint32_t)(tq >> 6) * kWave * kk + (tq & 63);
@@ -753,9 +775,9 @@ __global__ __launch_bounds__(THREADS, 4) void ms_local_kernel(MsBufs bf, const M
 #pragma unroll
     for (int i = 0; i < MAXK; ++i) key[i] = __builtin_nontemporal_load(sp + min(pp + (uint32_t)i * kWave, cc - 1));
   };
-  auto finish_load = [&](const MsSeg g) {
+  auto finish_load = [&](const MsSeg g, const int ftid) {
     const uint32_t cc = (uint32_t)g.count, kk = (cc + THREADS - 1) / THREADS;
-    const uint32_t pp = (uint32_t)wave * kWave * kk + lane;
+    const uint32_t pp = (uint32_t)wv_s * kWave * kk + (uint32_t)(ftid & 63);
     const uint64_t ff = g.buf == 0 ? flip : 0;
 #pragma unroll
     for (int i = 0; i < MAXK; ++i) {
@@ -763,146 +785,159 @@ __global__ __launch_bounds__(THREADS, 4) void ms_local_kernel(MsBufs bf, const M
       key[i] = ((uint32_t)i < kk && p < cc) ? (key[i] ^ ff) : ~0ull;
     }
   };
-  // one segment; returns whether the next segment's keys were loaded (PREFETCH: as soon as
-  // this one's are staged, so their latency hides behind the window sorts).  Every early
-  // return is block-uniform.
-  auto process = [&](const uint32_t sidx, const MsSeg sg, const MsSeg nsg, const bool has_next) -> bool {
+  // One step of the persistent loop: sort segment sg (when `active`), and fetch the next
+  // segment's keys (PREFETCH, has_next) as soon as this one's are staged in LDS, so their
+  // latency hides behind the window sorts and the write-out.  Every path — a segment of
+  // equal keys, one for ms_lsd_kernel, the loop's first step that only fetches — passes
+  // the ONE load site below, and the write-out issues a fixed number of stores: the
+  // compiler then knows how many memory operations follow the loads, so the next step
+  // waits for its keys but not for this step's stores (vmcnt counts both, in order).
+  // Every condition is block-uniform.
+  auto process = [&](const bool active, const uint32_t sidx, const MsSeg sg, const MsSeg nsg, const bool has_next) {
   // an opaque copy of tid per segment: tid-derived addresses kept across the loop were
   // spilled, and a spill reloaded after the prefetch waited for the prefetch (vmcnt is in
   // order), which made it synchronous
-  int tq = threadIdx.x;
+  int tq = cur_tid();
   asm volatile("" : "+v"(tq));
-  const int tid = tq, lane = tid & 63, wave = tid >> 6;
+  const int tid = tq, lane = tid & 63, wave = wv_s;
+  bool work = active;
   MS_STAMP(0);
-  finish_load(sg);
   const uint32_t c = (uint32_t)sg.count;
   const uint32_t K = (c + THREADS - 1) / THREADS;
   const uint32_t pw = (uint32_t)wave * kWave * K + lane;
   uint64_t *dst = bf.a + ms_dst_off(sg);
   const int hi = (int)sg.aux;   // the keys agree on every bit of (key - base) at or above hi
   const uint64_t base = sg.base;
-  if (hi == 0) {  // every key equal: copy
+  auto bucket = [&](uint64_t k) -> uint32_t { return (uint32_t)(((k - base) << (64 - hi)) >> (64 - SB)); };
+  uint32_t rk[(MAXK + 1) / 2];  // ranks in the bucket, 16-bit pairs
+  uint32_t nq = 0, split = 0, mid = 0;
+  if (work) {
+    finish_load(sg, tid);
+    if (hi == 0) {  // every key equal: copy
 #pragma unroll
-    for (int i = 0; i < MAXK; ++i) {
-      const uint32_t p = pw + (uint32_t)i * kWave;
-      if ((uint32_t)i < K && p < c) dst[p] = key[i] ^ flip;
+      for (int i = 0; i < MAXK; ++i) {
+        const uint32_t p = pw + (uint32_t)i * kWave;
+        if ((uint32_t)i < K && p < c) dst[p] = key[i] ^ flip;
+      }
+      work = false;
     }
-    return false;
   }
-  if (MS_STOP(1)) {
+  if (work && MS_STOP(1)) {
     uint64_t x = 0;
 #pragma unroll
     for (int i = 0; i < MAXK; ++i)
       if ((uint32_t)i < K) x ^= key[i];
     dst[tid] = x;
-    return false;
+    work = false;
   }
-  // ---- 1. bucket ranks: the top SB of the hi bits of (key - base) that may differ
-  //         (fewer than SB: zero-padded, so only some buckets are used)
-  auto bucket = [&](uint64_t k) -> uint32_t { return (uint32_t)(((k - base) << (64 - hi)) >> (64 - SB)); };
+  if (work) {
+    // ---- 1. bucket ranks: the top SB of the hi bits of (key - base) that may differ
+    //         (fewer than SB: zero-padded, so only some buckets are used)
 #pragma unroll
-  for (int j = 0; j < C::BPT; ++j) s_off[C::BPT * tid + j] = 0;
-  if (tid == 0) {
-    s_misc[0] = 0;
-    s_misc[1] = 0;
-  }
-  __syncthreads();
-  uint32_t rk[(MAXK + 1) / 2];  // ranks in the bucket, 16-bit pairs
-#pragma unroll
-  for (int i = 0; i < MAXK; i += 2) rk[i / 2] = 0;
-#pragma unroll
-  for (int i = 0; i < MAXK; ++i) {
-    const uint32_t p = pw + (uint32_t)i * kWave;
-    if ((uint32_t)i < K && p < c) rk[i / 2] |= atomicAdd(&s_off[bucket(key[i])], 1u) << (16 * (i & 1));
-  }
-  __syncthreads();
-  MS_STAMP(1);
-  // ---- 2. bucket starts (BPT consecutive buckets per thread) and windows
-  {
-    uint32_t cb[C::BPT], sum = 0;
-#pragma unroll
-    for (int j = 0; j < C::BPT; ++j) {
-      cb[j] = s_off[C::BPT * tid + j];
-      sum += cb[j];
-    }
-    uint32_t tot;
-    uint32_t e = block_excl_scan<THREADS>(sum, s_ws, &tot);
-    __syncthreads();  // every count read before the starts overwrite them
-    // Window q starts at the first bucket start >= q * WS: the bucket b whose end
-    // (start + count) is the first >= q * WS > its start owns every q with q * WS in
-    // (start_b, end_b], and window q then starts at end_b (the next bucket's start).  Each
-    // thread assigns the windows its own buckets end — no search; usually none or one.
-    const uint32_t nqq = (c + LS_WS - 1) / LS_WS;
-#pragma unroll
-    for (int j = 0; j < C::BPT; ++j) {
-      s_off[C::BPT * tid + j] = e;
-      const uint32_t end = e + cb[j];
-      for (uint32_t q = e / LS_WS + 1; q * LS_WS <= end && q < nqq; ++q) s_win[q] = end;
-      e = end;
-    }
+    for (int j = 0; j < C::BPT; ++j) s_off[C::BPT * tid + j] = 0;
     if (tid == 0) {
-      s_off[NB] = c;
-      s_win[0] = 0;
-      s_win[nqq] = c;
+      s_misc[0] = 0;
+      s_misc[1] = 0;
     }
-  }
-  __syncthreads();
-  const uint32_t nq = (c + LS_WS - 1) / LS_WS;
-  {  // the largest window and the last window that starts inside the first round: a wave
-     // maximum, then one LDS atomic per wave (512 atomics on one word serialised)
-    uint32_t mw = 0, ms = 0;
+    __syncthreads();
 #pragma unroll
-    for (int j = 0; j < C::WPT; ++j) {
-      const uint32_t q = (uint32_t)tid + (uint32_t)j * THREADS;
-      if (q < nq) {
-        const uint32_t wa = s_win[q], wb = s_win[q + 1];
-        mw = max(mw, wb - wa);
-        if (wa <= (uint32_t)C::LDS_KEYS) ms = max(ms, q);
+    for (int i = 0; i < MAXK; i += 2) rk[i / 2] = 0;
+#pragma unroll
+    for (int i = 0; i < MAXK; ++i) {
+      const uint32_t p = pw + (uint32_t)i * kWave;
+      if ((uint32_t)i < K && p < c) rk[i / 2] |= atomicAdd(&s_off[bucket(key[i])], 1u) << (16 * (i & 1));
+    }
+    __syncthreads();
+    MS_STAMP(1);
+    // ---- 2. bucket starts (BPT consecutive buckets per thread) and windows
+    {
+      uint32_t cb[C::BPT], sum = 0;
+#pragma unroll
+      for (int j = 0; j < C::BPT; ++j) {
+        cb[j] = s_off[C::BPT * tid + j];
+        sum += cb[j];
+      }
+      uint32_t tot;
+      uint32_t e = block_excl_scan<THREADS>(sum, s_ws, &tot, tid);
+      __syncthreads();  // every count read before the starts overwrite them
+      // Window q starts at the first bucket start >= q * WS: the bucket b whose end
+      // (start + count) is the first >= q * WS > its start owns every q with q * WS in
+      // (start_b, end_b], and window q then starts at end_b (the next bucket's start).  Each
+      // thread assigns the windows its own buckets end — no search; usually none or one.
+      const uint32_t nqq = (c + LS_WS - 1) / LS_WS;
+#pragma unroll
+      for (int j = 0; j < C::BPT; ++j) {
+        s_off[C::BPT * tid + j] = e;
+        const uint32_t end = e + cb[j];
+        for (uint32_t q = e / LS_WS + 1; q * LS_WS <= end && q < nqq; ++q) s_win[q] = end;
+        e = end;
+      }
+      if (tid == 0) {
+        s_off[NB] = c;
+        s_win[0] = 0;
+        s_win[nqq] = c;
       }
     }
+    __syncthreads();
+    nq = (c + LS_WS - 1) / LS_WS;
+    {  // the largest window and the last window that starts inside the first round: a wave
+       // maximum, then one LDS atomic per wave (512 atomics on one word serialised)
+      uint32_t mw = 0, ms = 0;
 #pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-      mw = max(mw, (uint32_t)__shfl_xor((int)mw, off, 64));
-      ms = max(ms, (uint32_t)__shfl_xor((int)ms, off, 64));
-    }
-    if (lane == 0) {
-      atomicMax(&s_misc[0], mw);
-      atomicMax(&s_misc[1], ms);
-    }
-  }
-  __syncthreads();
-  MS_STAMP(2);
-  // rounds: windows [0, split) then [split, nq) with at most LDS_KEYS keys each
-  const uint32_t split = c > (uint32_t)C::LDS_KEYS ? s_misc[1] : nq;
-  const uint32_t mid = split < nq ? s_win[split] : c;
-  if (s_misc[0] > (uint32_t)LS_MAX_WINDOW || c - mid > (uint32_t)C::LDS_KEYS) {
-    if (tid == 0) fb[1 + atomicAdd(&fb[0], 1u)] = sidx;  // uniform: to ms_lsd_kernel
-    return false;
-  }
-  // ---- 3. keys to their bucket positions: round 0's into LDS, round 1's parked in out at
-  //         their final range (L2-resident; safe in place, every key is in registers)
+      for (int j = 0; j < C::WPT; ++j) {
+        const uint32_t q = (uint32_t)tid + (uint32_t)j * THREADS;
+        if (q < nq) {
+          const uint32_t wa = s_win[q], wb = s_win[q + 1];
+          mw = max(mw, wb - wa);
+          if (wa <= (uint32_t)C::LDS_KEYS) ms = max(ms, q);
+        }
+      }
 #pragma unroll
-  for (int i = 0; i < MAXK; ++i) {
-    const uint32_t p = pw + (uint32_t)i * kWave;
-    if ((uint32_t)i < K && p < c) {
-      const uint32_t pos = s_off[bucket(key[i])] + ((rk[i / 2] >> (16 * (i & 1))) & 0xFFFFu);
-      if (pos < mid)
-        s_keys[pos] = key[i];
-      else
-        dst[pos] = key[i];
+      for (int off = 32; off >= 1; off >>= 1) {
+        mw = max(mw, (uint32_t)__shfl_xor((int)mw, off, 64));
+        ms = max(ms, (uint32_t)__shfl_xor((int)ms, off, 64));
+      }
+      if (lane == 0) {
+        atomicMax(&s_misc[0], mw);
+        atomicMax(&s_misc[1], ms);
+      }
+    }
+    __syncthreads();
+    MS_STAMP(2);
+    // rounds: windows [0, split) then [split, nq) with at most LDS_KEYS keys each
+    split = c > (uint32_t)C::LDS_KEYS ? s_misc[1] : nq;
+    mid = split < nq ? s_win[split] : c;
+    if (s_misc[0] > (uint32_t)LS_MAX_WINDOW || c - mid > (uint32_t)C::LDS_KEYS) {
+      if (tid == 0) fb[1 + atomicAdd(&fb[0], 1u)] = sidx;  // to ms_lsd_kernel
+      work = false;
     }
   }
-  bool pf = false;
-  if (PREFETCH && has_next) {  // the key registers are free: fetch the next segment now
-    load(nsg);
-    pf = true;
+  if (work) {
+    // ---- 3. keys to their bucket positions: round 0's into LDS, round 1's parked in out at
+    //         their final range (L2-resident; safe in place, every key is in registers)
+#pragma unroll
+    for (int i = 0; i < MAXK; ++i) {
+      const uint32_t p = pw + (uint32_t)i * kWave;
+      if ((uint32_t)i < K && p < c) {
+        const uint32_t pos = s_off[bucket(key[i])] + ((rk[i / 2] >> (16 * (i & 1))) & 0xFFFFu);
+        if (pos < mid)
+          s_keys[pos] = key[i];
+        else
+          dst[pos] = key[i];
+      }
+    }
   }
+  // the key registers are free: the one load site, unconditional (the last step reloads
+  // its own segment) — under a branch, the registers' merge with the unloaded path
+  // compiled to copies that waited for the loads right here
+  if (PREFETCH) load(nsg);
   MS_STAMP(3);
-  if (MS_STOP(3)) {
+  if (work && MS_STOP(3)) {
     __syncthreads();
     dst[tid] = s_keys[tid];
-    return pf;
+    work = false;
   }
+  if (!work) return;
   for (int round = 0; round < 2; ++round) {
     const uint32_t rbase = round ? mid : 0;
     const uint32_t w0 = round ? split : 0, w1 = round ? nq : split;
@@ -965,30 +1000,51 @@ __global__ __launch_bounds__(THREADS, 4) void ms_local_kernel(MsBufs bf, const M
     MS_STAMP(4);
     if (MS_STOP(4)) continue;
     const uint32_t rend = round ? c : mid;
-    for (uint32_t j = tid; j < rend - rbase; j += THREADS) __builtin_nontemporal_store(s_keys[j] ^ flip, &dst[rbase + j]);
+#ifndef NUT_MSD_DYNAMIC_WRITEOUT  // (scripts/tune/local_tune.hip A/B: the round-4 loop)
+    if constexpr (PREFETCH && C::LDS_KEYS == C::CAP) {
+#else
+    if constexpr (false) {
+#endif
+      // one round of <= CAP keys: exactly MAXK stores per lane, clamped to the last key
+      // (repeats store the same value): a store loop of data-dependent length would leave
+      // the compiler no count of the operations behind the next segment's loads
+      const uint32_t last = rend - rbase - 1;
+      const int tw = cur_tid();
+#pragma unroll
+      for (int i = 0; i < MAXK; ++i) {
+        const uint32_t j = min((uint32_t)(i * THREADS + tw), last);
+        __builtin_nontemporal_store(s_keys[j] ^ flip, &dst[rbase + j]);
+      }
+    } else {
+      for (uint32_t j = tid; j < rend - rbase; j += THREADS) __builtin_nontemporal_store(s_keys[j] ^ flip, &dst[rbase + j]);
+    }
   }
   MS_STAMP(5);
-  return pf;
   };
-  uint32_t sidx = blockIdx.x;
-  if (sidx >= nseg) return;
-  MsSeg sg = segs[sidx];
-  load(sg);
   if constexpr (!PREFETCH) {  // one segment per workgroup (grid = nseg)
-    (void)process(sidx, sg, sg, false);
+    if (blockIdx.x >= nseg) return;
+    const MsSeg sg = segs[blockIdx.x];
+    load(sg);
+    process(true, blockIdx.x, sg, sg, false);
     return;
   }
-  for (;;) {  // persistent: segments blockIdx.x, + gridDim.x, ...
-    const uint32_t nidx = sidx + gridDim.x;
+  // persistent: segments blockIdx.x, + gridDim.x, ...; the first step only fetches
+  uint32_t nidx = blockIdx.x;
+  if (nidx >= nseg) return;
+  MsSeg sg{}, nsg = segs[nidx];
+  uint32_t sidx = 0;
+  bool active = false;
+  for (;;) {
     const bool has_next = nidx < nseg;
-    const MsSeg nsg = has_next ? segs[nidx] : sg;
-    const bool pf = process(sidx, sg, nsg, has_next);
+    process(active, sidx, sg, has_next ? nsg : sg, has_next);
     if (!has_next) break;
-    if (!pf) load(nsg);
     __syncthreads();  // LDS is reused by the next segment
     MS_STAMP(6);
     sidx = nidx;
     sg = nsg;
+    active = true;
+    nidx += gridDim.x;
+    if (nidx < nseg) nsg = segs[nidx];
   }
 #ifdef NUT_MSD_STAMPS
   if (tid == 0)
@@ -1007,133 +1063,137 @@ __global__ __launch_bounds__(THREADS) void ms_lsd_kernel(MsBufs bf, const MsSeg 
                                                          const uint32_t *__restrict__ fb) {
   using C = LocalCfg<THREADS, MAXK>;
   constexpr int WAVES = C::WAVES;
-  if (blockIdx.x >= fb[0]) return;
   __shared__ uint32_t s_x[C::CAP];
   __shared__ uint32_t s_wcnt[WAVES][LSD_BINS];
   __shared__ uint32_t s_tex[LSD_BINS];
   __shared__ uint32_t s_wsum[LSD_BINS / kWave];
   __shared__ uint64_t s_wmm[WAVES][2];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const MsSeg sg = segs[fb[1 + blockIdx.x]];
-  const uint32_t c = (uint32_t)sg.count;
-  const uint32_t K = (c + THREADS - 1) / THREADS;
-  const uint32_t pw = (uint32_t)wave * kWave * K + lane;
-  const uint64_t *src = ms_src(bf, sg.buf) + sg.start;
-  uint64_t *dst = bf.a + ms_dst_off(sg);
-  const uint64_t f = sg.buf == 0 ? flip : 0;
-  uint32_t lo[MAXK], hi[MAXK], pos[MAXK];
-  uint64_t mn = ~0ull, mx = 0;
-#pragma unroll
-  for (int i = 0; i < MAXK; ++i) {
-    const uint32_t p = pw + (uint32_t)i * kWave;
-    const uint64_t v = src[min(p, c - 1)] ^ f;  // unconditional: the loads overlap
-    if ((uint32_t)i < K && p < c) {
-      mn = v < mn ? v : mn;
-      mx = v > mx ? v : mx;
-    }
-    lo[i] = (uint32_t)v;
-    hi[i] = (uint32_t)(v >> 32);
-  }
-  // the segment's key range: passes over bits [0, nbits) of x = key - min; padding
-  // (positions >= count) is x = all ones, behind every real key in every pass
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) {
-    const uint64_t a = __shfl_xor(mn, off, 64), b = __shfl_xor(mx, off, 64);
-    mn = a < mn ? a : mn;
-    mx = b > mx ? b : mx;
-  }
-  if (lane == 0) {
-    s_wmm[wave][0] = mn;
-    s_wmm[wave][1] = mx;
-  }
-  __syncthreads();
-  uint64_t kmin = s_wmm[0][0], kmax = s_wmm[0][1];
-#pragma unroll
-  for (int w = 1; w < WAVES; ++w) {
-    kmin = s_wmm[w][0] < kmin ? s_wmm[w][0] : kmin;
-    kmax = s_wmm[w][1] > kmax ? s_wmm[w][1] : kmax;
-  }
-  const int nbits = kmax == kmin ? 0 : 64 - __builtin_clzll(kmax - kmin);
-#pragma unroll
-  for (int i = 0; i < MAXK; ++i) {
-    const uint32_t p = pw + (uint32_t)i * kWave;
-    const uint64_t x = ((uint32_t)i < K && p < c) ? ((((uint64_t)hi[i] << 32) | lo[i]) - kmin) : ~0ull;
-    lo[i] = (uint32_t)x;
-    hi[i] = (uint32_t)(x >> 32);
-  }
-  auto digit = [&](int i, int shift) -> uint32_t {
-    return (uint32_t)((((uint64_t)hi[i] << 32) | lo[i]) >> shift) & 255u;
-  };
-  for (int shift = 0; shift < nbits; shift += 8) {
-    for (int i = tid; i < WAVES * LSD_BINS; i += THREADS) (&s_wcnt[0][0])[i] = 0;
-    __syncthreads();
+  // persistent over the listed segments (grid = min(count, a few per CU)): most launches
+  // find none, and a grid of one workgroup per possible segment cost ~0.1 ms per sort
+  for (uint32_t blk = blockIdx.x; blk < fb[0]; blk += gridDim.x) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const MsSeg sg = segs[fb[1 + blk]];
+    const uint32_t c = (uint32_t)sg.count;
+    const uint32_t K = (c + THREADS - 1) / THREADS;
+    const uint32_t pw = (uint32_t)wave * kWave * K + lane;
+    const uint64_t *src = ms_src(bf, sg.buf) + sg.start;
+    uint64_t *dst = bf.a + ms_dst_off(sg);
+    const uint64_t f = sg.buf == 0 ? flip : 0;
+    uint32_t lo[MAXK], hi[MAXK], pos[MAXK];
+    uint64_t mn = ~0ull, mx = 0;
 #pragma unroll
     for (int i = 0; i < MAXK; ++i) {
-      if ((uint32_t)i < K) {
-        const uint32_t d = digit(i, shift);
-        uint64_t peers = ~0ull;
+      const uint32_t p = pw + (uint32_t)i * kWave;
+      const uint64_t v = src[min(p, c - 1)] ^ f;  // unconditional: the loads overlap
+      if ((uint32_t)i < K && p < c) {
+        mn = v < mn ? v : mn;
+        mx = v > mx ? v : mx;
+      }
+      lo[i] = (uint32_t)v;
+      hi[i] = (uint32_t)(v >> 32);
+    }
+    // the segment's key range: passes over bits [0, nbits) of x = key - min; padding
+    // (positions >= count) is x = all ones, behind every real key in every pass
 #pragma unroll
-        for (int b = 0; b < 8; ++b) {
-          const uint64_t bb = __ballot((d >> b) & 1u);
-          peers &= ((d >> b) & 1u) ? bb : ~bb;
+    for (int off = 32; off >= 1; off >>= 1) {
+      const uint64_t a = __shfl_xor(mn, off, 64), b = __shfl_xor(mx, off, 64);
+      mn = a < mn ? a : mn;
+      mx = b > mx ? b : mx;
+    }
+    if (lane == 0) {
+      s_wmm[wave][0] = mn;
+      s_wmm[wave][1] = mx;
+    }
+    __syncthreads();
+    uint64_t kmin = s_wmm[0][0], kmax = s_wmm[0][1];
+#pragma unroll
+    for (int w = 1; w < WAVES; ++w) {
+      kmin = s_wmm[w][0] < kmin ? s_wmm[w][0] : kmin;
+      kmax = s_wmm[w][1] > kmax ? s_wmm[w][1] : kmax;
+    }
+    const int nbits = kmax == kmin ? 0 : 64 - __builtin_clzll(kmax - kmin);
+#pragma unroll
+    for (int i = 0; i < MAXK; ++i) {
+      const uint32_t p = pw + (uint32_t)i * kWave;
+      const uint64_t x = ((uint32_t)i < K && p < c) ? ((((uint64_t)hi[i] << 32) | lo[i]) - kmin) : ~0ull;
+      lo[i] = (uint32_t)x;
+      hi[i] = (uint32_t)(x >> 32);
+    }
+    auto digit = [&](int i, int shift) -> uint32_t {
+      return (uint32_t)((((uint64_t)hi[i] << 32) | lo[i]) >> shift) & 255u;
+    };
+    for (int shift = 0; shift < nbits; shift += 8) {
+      for (int i = tid; i < WAVES * LSD_BINS; i += THREADS) (&s_wcnt[0][0])[i] = 0;
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < MAXK; ++i) {
+        if ((uint32_t)i < K) {
+          const uint32_t d = digit(i, shift);
+          uint64_t peers = ~0ull;
+#pragma unroll
+          for (int b = 0; b < 8; ++b) {
+            const uint64_t bb = __ballot((d >> b) & 1u);
+            peers &= ((d >> b) & 1u) ? bb : ~bb;
+          }
+          const uint32_t before = lane_rank(peers);
+          const uint32_t prior = s_wcnt[wave][d];  // all peers read before the leader writes
+          pos[i] = prior + before;
+          if (before == 0) s_wcnt[wave][d] = prior + (uint32_t)__popcll(peers);
         }
-        const uint32_t before = lane_rank(peers);
-        const uint32_t prior = s_wcnt[wave][d];  // all peers read before the leader writes
-        pos[i] = prior + before;
-        if (before == 0) s_wcnt[wave][d] = prior + (uint32_t)__popcll(peers);
       }
-    }
-    __syncthreads();
-    uint32_t tot = 0, incl = 0;
-    if (tid < LSD_BINS) {
+      __syncthreads();
+      uint32_t tot = 0, incl = 0;
+      if (tid < LSD_BINS) {
 #pragma unroll
-      for (int w = 0; w < WAVES; ++w) {
-        const uint32_t x = s_wcnt[w][tid];
-        s_wcnt[w][tid] = tot;  // exclusive prefix over waves
-        tot += x;
+        for (int w = 0; w < WAVES; ++w) {
+          const uint32_t x = s_wcnt[w][tid];
+          s_wcnt[w][tid] = tot;  // exclusive prefix over waves
+          tot += x;
+        }
+        incl = tot;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+          const uint32_t y = __shfl_up(incl, off, 64);
+          if (lane >= off) incl += y;
+        }
+        if (lane == 63) s_wsum[wave] = incl;
       }
-      incl = tot;
+      __syncthreads();
+      if (tid < LSD_BINS) {
+        uint32_t add = 0;
 #pragma unroll
-      for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t y = __shfl_up(incl, off, 64);
-        if (lane >= off) incl += y;
+        for (int w = 0; w < LSD_BINS / kWave; ++w) add += (w < wave) ? s_wsum[w] : 0u;
+        s_tex[tid] = incl - tot + add;
       }
-      if (lane == 63) s_wsum[wave] = incl;
-    }
-    __syncthreads();
-    if (tid < LSD_BINS) {
-      uint32_t add = 0;
+      __syncthreads();
 #pragma unroll
-      for (int w = 0; w < LSD_BINS / kWave; ++w) add += (w < wave) ? s_wsum[w] : 0u;
-      s_tex[tid] = incl - tot + add;
+      for (int i = 0; i < MAXK; ++i) {
+        if ((uint32_t)i < K) {
+          const uint32_t d = digit(i, shift);
+          pos[i] += s_tex[d] + s_wcnt[wave][d];
+          s_x[pos[i]] = lo[i];
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < MAXK; ++i)
+        if ((uint32_t)i < K) lo[i] = s_x[pw + (uint32_t)i * kWave];
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < MAXK; ++i)
+        if ((uint32_t)i < K) s_x[pos[i]] = hi[i];
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < MAXK; ++i)
+        if ((uint32_t)i < K) hi[i] = s_x[pw + (uint32_t)i * kWave];
+      __syncthreads();
     }
-    __syncthreads();
 #pragma unroll
     for (int i = 0; i < MAXK; ++i) {
-      if ((uint32_t)i < K) {
-        const uint32_t d = digit(i, shift);
-        pos[i] += s_tex[d] + s_wcnt[wave][d];
-        s_x[pos[i]] = lo[i];
-      }
+      const uint32_t p = pw + (uint32_t)i * kWave;
+      if ((uint32_t)i < K && p < c) dst[p] = ((((uint64_t)hi[i] << 32) | lo[i]) + kmin) ^ flip;
     }
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < MAXK; ++i)
-      if ((uint32_t)i < K) lo[i] = s_x[pw + (uint32_t)i * kWave];
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < MAXK; ++i)
-      if ((uint32_t)i < K) s_x[pos[i]] = hi[i];
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < MAXK; ++i)
-      if ((uint32_t)i < K) hi[i] = s_x[pw + (uint32_t)i * kWave];
-    __syncthreads();
-  }
-#pragma unroll
-  for (int i = 0; i < MAXK; ++i) {
-    const uint32_t p = pw + (uint32_t)i * kWave;
-    if ((uint32_t)i < K && p < c) dst[p] = ((((uint64_t)hi[i] << 32) | lo[i]) + kmin) ^ flip;
+    __syncthreads();  // LDS is reused by the next segment
   }
 }
 
@@ -1207,9 +1267,8 @@ uint64_t tile_table(std::vector<MsSeg> &segs, uint32_t tile, std::vector<uint32_
 
 // Local sorts are persistent (the S and M classes prefetch the next segment's keys): as
 // many workgroups as fit on the device, each walking the list with stride gridDim.x.
-template <int T, int K>
+template <int T, int K, bool PF>
 static void launch_class(nut_ctx *c, const MsBufs &bf, const MsSeg *d, unsigned n, uint64_t flip, uint32_t *fb) {
-  constexpr bool PF = K <= 12;  // the L class has no registers to spare for a second key set
   static int per_cu = 0;        // resident workgroups per CU (occupancy query, once)
   if (per_cu == 0) {
     int b = 0;
@@ -1218,7 +1277,27 @@ static void launch_class(nut_ctx *c, const MsBufs &bf, const MsSeg *d, unsigned 
   }
   const unsigned grid = PF ? (unsigned)std::min<uint64_t>(n, (uint64_t)c->num_cus * per_cu) : n;
   hipLaunchKernelGGL((ms_local_kernel<T, K, PF>), dim3(grid), dim3(T), 0, c->stream, bf, d, n, flip, fb);
-  hipLaunchKernelGGL((ms_lsd_kernel<T, K>), dim3(n), dim3(T), 0, c->stream, bf, d, flip, (const uint32_t *)fb);
+  hipLaunchKernelGGL((ms_lsd_kernel<T, K>), dim3((unsigned)std::min<uint64_t>(n, (uint64_t)c->num_cus * 2)), dim3(T), 0,
+                     c->stream, bf, d, flip, (const uint32_t *)fb);
+}
+
+// local sorts of n segments listed in device memory (a device-planned level's class list)
+// (the persistent classes prefetch the next segment's keys; the L class has no registers
+// to spare for a second key set)
+static nut_status launch_local_dev(nut_ctx *c, const MsBufs &bf, uint64_t flip, const MsSeg *d, unsigned n,
+                                   uint32_t *fb, int cls) {
+  if (n == 0) return NUT_OK;
+  NUT_HIP(hipMemsetAsync(fb, 0, 4, c->stream));
+  if (cls == 0)
+    launch_class<LS_S_THREADS, LS_S_ITEMS, true>(c, bf, d, n, flip, fb);
+  else if (cls == 1)
+    launch_class<LS_M_THREADS, LS_M_ITEMS, true>(c, bf, d, n, flip, fb);
+  else if (cls == 2)
+    launch_class<LS_M2_THREADS, LS_M2_ITEMS, true>(c, bf, d, n, flip, fb);
+  else
+    launch_class<LS_L_THREADS, LS_L_ITEMS, false>(c, bf, d, n, flip, fb);
+  NUT_HIP(hipGetLastError());
+  return NUT_OK;
 }
 
 static nut_status launch_local(nut_ctx *c, MetaArena &ar, const MsBufs &bf, uint64_t flip,
@@ -1229,33 +1308,9 @@ static nut_status launch_local(nut_ctx *c, MetaArena &ar, const MsBufs &bf, uint
   if (s) return s;
   uint32_t *fb = (uint32_t *)ar.alloc((segs.size() + 1) * 4);
   NUT_HIP(hipMemsetAsync(fb, 0, 4, c->stream));
-  const unsigned n = (unsigned)segs.size();
-  if (cls == 0)
-    launch_class<LS_S_THREADS, LS_S_ITEMS>(c, bf, d, n, flip, fb);
-  else if (cls == 1)
-    launch_class<LS_M_THREADS, LS_M_ITEMS>(c, bf, d, n, flip, fb);
-  else
-    launch_class<LS_L_THREADS, LS_L_ITEMS>(c, bf, d, n, flip, fb);
-  NUT_HIP(hipGetLastError());
-  return NUT_OK;
+  return launch_local_dev(c, bf, flip, d, (unsigned)segs.size(), fb, cls);
 }
 
-static int local_class(uint64_t count) { return count <= LS_S_CAP ? 0 : (count <= LS_M_CAP ? 1 : 2); }
-
-// local sorts of n segments listed in device memory (a device-planned level's class list)
-static nut_status launch_local_dev(nut_ctx *c, const MsBufs &bf, uint64_t flip, const MsSeg *d, unsigned n,
-                                   uint32_t *fb, int cls) {
-  if (n == 0) return NUT_OK;
-  NUT_HIP(hipMemsetAsync(fb, 0, 4, c->stream));
-  if (cls == 0)
-    launch_class<LS_S_THREADS, LS_S_ITEMS>(c, bf, d, n, flip, fb);
-  else if (cls == 1)
-    launch_class<LS_M_THREADS, LS_M_ITEMS>(c, bf, d, n, flip, fb);
-  else
-    launch_class<LS_L_THREADS, LS_L_ITEMS>(c, bf, d, n, flip, fb);
-  NUT_HIP(hipGetLastError());
-  return NUT_OK;
-}
 
 // Scatter tiles are staged and written in two halves (ms_scatter_kernel<2>): ~512-B digit
 // runs instead of 256 (29.24 -> 28.72 ms per 1.25e9-key sort, round-2 same-box A/B)
@@ -1285,7 +1340,8 @@ static nut_status device_level(nut_ctx *c, MetaArena &ar, const MsBufs &bf, cons
   const size_t hbytes = ns * MS_BINS * 8;
   nut_status s = ar.begin(2 * MetaArena::align(ns * sizeof(MsSeg)) + MetaArena::align(tiles.size() * 4) +
                           MetaArena::align(stiles.size() * 4) + 2 * MetaArena::align(hbytes) +
-                          MetaArena::align(4 * cap * sizeof(MsSeg)) + 3 * MetaArena::align((cap + 1) * 4) + 1024);
+                          MetaArena::align((LS_NCLS + 1) * cap * sizeof(MsSeg)) +
+                          LS_NCLS * MetaArena::align((cap + 1) * 4) + 1024);
   if (s) return s;
   MsSeg *dseg, *dsseg;
   uint32_t *dtile, *dstile;
@@ -1294,12 +1350,12 @@ static nut_status device_level(nut_ctx *c, MetaArena &ar, const MsBufs &bf, cons
     return s;
   unsigned long long *dhist = (unsigned long long *)ar.alloc(hbytes);
   unsigned long long *dcur = (unsigned long long *)ar.alloc(hbytes);
-  MsSeg *lists = (MsSeg *)ar.alloc(4 * cap * sizeof(MsSeg));
-  unsigned int *counts = (unsigned int *)ar.alloc(16);
-  uint32_t *fb[3];
+  MsSeg *lists = (MsSeg *)ar.alloc((LS_NCLS + 1) * cap * sizeof(MsSeg));
+  unsigned int *counts = (unsigned int *)ar.alloc(4 * (LS_NCLS + 1));
+  uint32_t *fb[LS_NCLS];
   for (auto &f : fb) f = (uint32_t *)ar.alloc((cap + 1) * 4);
   NUT_HIP(hipMemsetAsync(dhist, 0, hbytes, st));
-  NUT_HIP(hipMemsetAsync(counts, 0, 16, st));
+  NUT_HIP(hipMemsetAsync(counts, 0, 4 * (LS_NCLS + 1), st));
   uint64_t total = 0;
   for (const MsSeg &sg : big) total += sg.count;
   hipLaunchKernelGGL(ms_hist_kernel<MsDigit>, dim3((unsigned)nht), dim3(MH_THREADS), 0, st, bf, (const MsSeg *)dseg,
@@ -1310,7 +1366,7 @@ static nut_status device_level(nut_ctx *c, MetaArena &ar, const MsBufs &bf, cons
   hipEvent_t ev = nullptr;
   NUT_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
   uint32_t *hc = (uint32_t *)c->host_pinned;
-  hipError_t e = hipMemcpyAsync(hc, counts, 16, hipMemcpyDeviceToHost, st);
+  hipError_t e = hipMemcpyAsync(hc, counts, 4 * (LS_NCLS + 1), hipMemcpyDeviceToHost, st);
   if (e == hipSuccess) e = hipEventRecord(ev, st);
   if (e == hipSuccess)
     launch_scatter(st, (unsigned)std::min<uint64_t>(nst, (uint64_t)c->num_cus), bf, (const MsSeg *)dsseg,
@@ -1319,14 +1375,16 @@ static nut_status device_level(nut_ctx *c, MetaArena &ar, const MsBufs &bf, cons
   if (e == hipSuccess) e = hipEventSynchronize(ev);  // the counts, while the scatter runs
   (void)hipEventDestroy(ev);
   if (e != hipSuccess) return hip_fail(e, "nut_sort_i64 (device-planned level)");
-  const uint32_t cnt[4] = {hc[0], hc[1], hc[2], hc[3]};
+  uint32_t cnt[LS_NCLS + 1];
+  for (int k = 0; k <= LS_NCLS; ++k) cnt[k] = hc[k];
   c->sort_bytes += 8 * total + 16 * total;
   ++c->sort_levels;
-  for (int cls = 2; cls >= 0; --cls)
+  for (int cls = LS_NCLS - 1; cls >= 0; --cls)
     if ((s = launch_local_dev(c, bf, flip, lists + (uint64_t)cls * cap, cnt[cls], fb[cls], cls))) return s;
-  if (cnt[3]) {  // sub-segments too large for a local sort: to the host, for another level
-    over.resize(cnt[3]);
-    NUT_HIP(hipMemcpyAsync(over.data(), lists + 3 * cap, cnt[3] * sizeof(MsSeg), hipMemcpyDeviceToHost, st));
+  if (cnt[LS_NCLS]) {  // sub-segments too large for a local sort: to the host, for another level
+    over.resize(cnt[LS_NCLS]);
+    NUT_HIP(hipMemcpyAsync(over.data(), lists + (uint64_t)LS_NCLS * cap, cnt[LS_NCLS] * sizeof(MsSeg),
+                           hipMemcpyDeviceToHost, st));
     NUT_HIP(hipStreamSynchronize(st));
   }
   uint64_t over_keys = 0;
@@ -1484,7 +1542,7 @@ static nut_status msd_sort_capped(nut_ctx *c, const int64_t *in, int64_t *out, u
   for (uint64_t r = 0; r < nr; ++r) cur1[r] = r * ocap1;
   s = ar.begin(MetaArena::align(segs.size() * sizeof(MsSeg)) + MetaArena::align(tiles.size() * 4) +
                MetaArena::align(cur1.size() * 8) + MetaArena::align(dbase.size() * 8) +
-               MetaArena::align(3 * lcap * sizeof(MsSeg)) + 3 * MetaArena::align((lcap + 1) * 4) + 1024);
+               MetaArena::align(LS_NCLS * lcap * sizeof(MsSeg)) + LS_NCLS * MetaArena::align((lcap + 1) * 4) + 1024);
   if (s) return s;
   MsSeg *dsegs;
   uint32_t *dt1;
@@ -1492,11 +1550,11 @@ static nut_status msd_sort_capped(nut_ctx *c, const int64_t *in, int64_t *out, u
   if ((s = ar.upload(segs, &dsegs)) || (s = ar.upload(tiles, &dt1)) || (s = ar.upload(cur1, &dcur1)) ||
       (s = ar.upload(dbase, &ddb)))
     return s;
-  MsSeg *lists = (MsSeg *)ar.alloc(3 * lcap * sizeof(MsSeg));
-  unsigned int *counts = (unsigned int *)ar.alloc(16);
-  uint32_t *fb[3];
+  MsSeg *lists = (MsSeg *)ar.alloc(LS_NCLS * lcap * sizeof(MsSeg));
+  unsigned int *counts = (unsigned int *)ar.alloc(4 * LS_NCLS);
+  uint32_t *fb[LS_NCLS];
   for (auto &f : fb) f = (uint32_t *)ar.alloc((lcap + 1) * 4);
-  NUT_HIP(hipMemsetAsync(counts, 0, 16, st));
+  NUT_HIP(hipMemsetAsync(counts, 0, 4 * LS_NCLS, st));
   MsMap m1 = m0;
   m1.dshift = 0;
   m1.maxx = ~0ull;  // level 0 checked every key
@@ -1509,13 +1567,15 @@ static nut_status msd_sort_capped(nut_ctx *c, const int64_t *in, int64_t *out, u
                      (const uint64_t *)ddb, ocap1, m0, lists, lcap, counts, (unsigned long long *)(dcur1 + nr));
   NUT_HIP(hipGetLastError());
   uint64_t *hc = c->host_pinned;
-  NUT_HIP(hipMemcpyAsync(hc, counts, 16, hipMemcpyDeviceToHost, st));
+  static_assert(4 * LS_NCLS <= 16, "class counts in the first two pinned words");
+  NUT_HIP(hipMemcpyAsync(hc, counts, 4 * LS_NCLS, hipMemcpyDeviceToHost, st));
   NUT_HIP(hipMemcpyAsync(hc + 2, dcur1 + nr, 8, hipMemcpyDeviceToHost, st));
   NUT_HIP(hipStreamSynchronize(st));
   if (hc[2]) return NUT_ERR_CAPACITY;
   const uint32_t *cnt = (const uint32_t *)hc;
-  const uint32_t ncls[3] = {cnt[0], cnt[1], cnt[2]};
-  for (int cls = 2; cls >= 0; --cls)
+  uint32_t ncls[LS_NCLS];
+  for (int k = 0; k < LS_NCLS; ++k) ncls[k] = cnt[k];
+  for (int cls = LS_NCLS - 1; cls >= 0; --cls)
     if ((s = launch_local_dev(c, bf, flip, lists + (uint64_t)cls * lcap, ncls[cls], fb[cls], cls))) return s;
   c->sort_bytes = 48 * n;
   c->sort_levels = 2;
@@ -1550,7 +1610,7 @@ nut_status msd_sort_i64(nut_ctx *c, const int64_t *in, int64_t *out, uint64_t n,
     std::vector<MsSeg> one{{0, n, 0, 64}};
     s = ar.begin(1024);
     if (s) return s;
-    s = launch_local(c, ar, bf, flip, one, local_class(n));
+    s = launch_local(c, ar, bf, flip, one, ls_class(n));
     if (s) return s;
     c->sort_bytes = 16 * n;
     c->timer.end(st);
@@ -1561,7 +1621,7 @@ nut_status msd_sort_i64(nut_ctx *c, const int64_t *in, int64_t *out, uint64_t n,
   // histogram speculates base 0 and the top 9 key bits while it reduces the keys' min and
   // max; if the top bits barely vary (a narrow key range, e.g. a sample-sort rank's), the
   // histogram is redone with base = min and the digit below the top bit of max - min.
-  std::vector<MsSeg> big{{0, n, 0, 0}}, scat, next, small[3], done;
+  std::vector<MsSeg> big{{0, n, 0, 0}}, scat, next, small[LS_NCLS], done;
   std::vector<uint32_t> tiles;
   std::vector<uint64_t> hist, cursor;
   MsDigit dg{0, 64 - MS_BITS, (uint32_t)MS_BINS - 1};
@@ -1620,7 +1680,7 @@ nut_status msd_sort_i64(nut_ctx *c, const int64_t *in, int64_t *out, uint64_t n,
       } else if (sg.count <= LS_CAP) {
         sg.aux = (uint32_t)hi;
         sg.base = dg.base;
-        small[local_class(sg.count)].push_back(sg);
+        small[ls_class(sg.count)].push_back(sg);
       } else {
         next.push_back(sg);
       }
@@ -1688,7 +1748,7 @@ nut_status msd_sort_i64(nut_ctx *c, const int64_t *in, int64_t *out, uint64_t n,
   total += MetaArena::align(done.size() * sizeof(MsSeg)) + MetaArena::align(ctiles.size() * 4);
   s = ar.begin(total);
   if (s) return s;
-  for (int cls = 2; cls >= 0; --cls) {
+  for (int cls = LS_NCLS - 1; cls >= 0; --cls) {
     for (const MsSeg &sg : small[cls]) c->sort_bytes += 16 * sg.count;
     if ((s = launch_local(c, ar, bf, flip, small[cls], cls))) return s;
   }

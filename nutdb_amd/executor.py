@@ -369,12 +369,20 @@ class Executor:
         return {"path": self.GROUPBY_PATHS[p.value], "levels": lv.value, "optimistic": bool(opt.value),
                 "capped_levels": opt.value}
 
+    GB_DECLINES = ("none", "shape", "clustered", "arena", "capacity", "table")
+
     def groupby_overflow_rows(self) -> int:
         """Rows of the last ordered group-by (groupby_to_host) aggregated from its overflow
         arenas — a heavy key's excess past its capped partition (nut_ctx_groupby_overflow)."""
-        r = C.c_uint64()
-        check(lib.nut_ctx_groupby_overflow(self.ctx, C.byref(r)), "nut_ctx_groupby_overflow")
+        r, d = C.c_uint64(), C.c_uint32()
+        check(lib.nut_ctx_groupby_overflow(self.ctx, C.byref(r), C.byref(d)), "nut_ctx_groupby_overflow")
         return r.value
+
+    def groupby_declined(self) -> str:
+        """Why the last groupby_to_host left the ordered path ("none" if it did not)."""
+        r, d = C.c_uint64(), C.c_uint32()
+        check(lib.nut_ctx_groupby_overflow(self.ctx, C.byref(r), C.byref(d)), "nut_ctx_groupby_overflow")
+        return self.GB_DECLINES[d.value] if d.value < len(self.GB_DECLINES) else str(d.value)
 
     def set_option(self, name: str, value: int) -> int:
         """nut_ctx_set_option (tuning / tests); returns the previous value."""

@@ -113,7 +113,8 @@ static void run(Ctx &c, const char *name, bool check) {
     CK(hipMemcpy(c.cur, cur0.data(), cur0.size() * 8, hipMemcpyHostToDevice));
     CK(hipEventRecord(c.e0));
     hipLaunchKernelGGL(kern, dim3(grid), dim3(T), 0, 0, ar, (const nut::GpSeg *)c.dseg, (const uint32_t *)dts, ntiles,
-                       64 - BITS, 0, c.cur, 0ull, (uint64_t)BINS * cap, c.cur + BINS, nut::GpRange{});
+                       64 - BITS, 0, c.cur, 0ull, (uint64_t)BINS * cap, c.cur + BINS, nut::GpRange{},
+                       (unsigned long long *)nullptr, (uint64_t)0);
     CK(hipEventRecord(c.e1));
     best = std::min(best, elapsed(c.e0, c.e1));
   }
@@ -166,6 +167,9 @@ int main(int argc, char **argv) {
   run<1024, 1>(c, "product <1,1024> (nt stores)", true);
   if (argc > 3) return 0;  // profiling runs: the product variant only
   run<1024, 1, 7>(c, "<1,1024> nt, 128 bins (G = 1e5)", true);
+  run<1024, 33, 7>(c, "<1,1024> nt early loads, 128 bins", true);
+  run<1024, 1, 7>(c, "<1,1024> nt, 128 bins again", true);
+  run<1024, 33, 7>(c, "<1,1024> nt early loads again", true);
   run<512, 1, 7>(c, "<1,512> nt, 128 bins, 2 WG/CU", true);
   run<512, 1, 6>(c, "<1,512> nt, 64 bins, 2 WG/CU", true);
   run<1024, 17, 7>(c, "<1,1024> 128 bins private cursors", false);

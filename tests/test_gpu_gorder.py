@@ -30,7 +30,10 @@ def run_to_host(ex, q, hint, rows=None, pin=True):
     else:
         out = (np.empty((rows, 1), np.int64), np.empty((rows, 4), np.int64))
     k, w = ex.groupby_to_host(q, group_hint=hint, out=out)
-    return k.copy(), w.copy(), ex.groupby_stats()["path"]
+    path = ex.groupby_stats()["path"]
+    if path != "partitioned_ordered":
+        path += ":" + ex.groupby_declined()
+    return k.copy(), w.copy(), path
 
 
 def check(keys, words, ok, ow, sums_exact=False):
@@ -168,7 +171,7 @@ def test_clustered_keys_declined_up_front(ex, orc):
     val = orc.gen_column(3, 0x6C, N)
     q = gb_query(dev(key, ex), dev(val, ex))
     k, w, path = run_to_host(ex, q, len(np.unique(key)))
-    assert path == "partitioned_direct"
+    assert path == "partitioned_direct:clustered"
     ok, ow = orc.groupby([key], AGGS4, values=[val])
     check(k, w, ok, ow, sums_exact=True)
 
@@ -180,11 +183,11 @@ def test_pageable_and_option_off_fall_back(ex, orc, opts):
     q = gb_query(dev(key, ex), dev(val, ex))
     ok, ow = orc.groupby([key], AGGS4, values=[val])
     k, w, path = run_to_host(ex, q, G, pin=False)
-    assert path == "partitioned_direct"
+    assert path == "partitioned_direct:shape"
     check(k, w, ok, ow, sums_exact=True)
     opts(gb_ordered=0)
     k, w, path = run_to_host(ex, q, G)
-    assert path == "partitioned_direct"
+    assert path == "partitioned_direct:shape"
     check(k, w, ok, ow, sums_exact=True)
 
 
