@@ -526,6 +526,7 @@ struct GpMeta {
   static size_t al(size_t x) { return (x + 255) & ~size_t(255); }
   nut_status begin(size_t total) {
     off = 0;
+    total += 16 * 256;  // (up() adds a byte to every upload: one extra 256-B unit each, <= 16 per call)
     if (total > c->gp_meta.bytes) {
       NUT_HIP(hipStreamSynchronize(c->stream));
       nut_status s = c->gp_meta.reserve(total);
@@ -561,11 +562,12 @@ uint32_t gp_tiles(std::vector<GpSeg> &segs, uint32_t tile, std::vector<uint32_t>
 // one key (rg: GpRange, t >= 0 ... the ordered group-by)
 void gp_capped_launch(nut_ctx *c, const GpArrays &ar, const GpSeg *dseg, const uint32_t *dts, uint32_t nst, int shift,
                       unsigned long long *dcur, uint64_t kx, uint64_t ovf, unsigned long long *dflag, int bits,
-                      bool two_keys, const GpRange *rg, unsigned long long *acur = nullptr, uint64_t acap = 0) {
+                      bool two_keys, const GpRange *rg, unsigned long long *acur = nullptr, uint64_t acap = 0,
+                      unsigned long long *acut = nullptr) {
   if (!nst) return;
   const unsigned grid = std::min<unsigned>(nst, (unsigned)c->num_cus);
   using SK = void (*)(GpArrays, const GpSeg *, const uint32_t *, uint32_t, int, int, unsigned long long *, uint64_t,
-                      uint64_t, unsigned long long *, GpRange, unsigned long long *, uint64_t);
+                      uint64_t, unsigned long long *, GpRange, unsigned long long *, uint64_t, unsigned long long *);
   static const SK kern[3][3] = {
       {gp_scatter_kernel<1, 1024, 1, 6>, gp_scatter_kernel<1, 1024, 1, 7>, gp_scatter_kernel<1, 1024, 1, 8>},
       {gp_scatter_kernel<2, 1024, 1, 6>, gp_scatter_kernel<2, 1024, 1, 7>, gp_scatter_kernel<2, 1024, 1, 8>},
@@ -573,7 +575,7 @@ void gp_capped_launch(nut_ctx *c, const GpArrays &ar, const GpSeg *dseg, const u
        gp_scatter_kernel<1, 1024, 1, 8, true>}};
   const int kv = rg ? 2 : two_keys ? 1 : 0;
   hipLaunchKernelGGL(kern[kv][bits - 6], dim3(grid), dim3(1024), 0, c->stream, ar, dseg, dts, nst, shift, 0, dcur, kx,
-                     ovf, dflag, rg ? *rg : GpRange{}, acur, acap);
+                     ovf, dflag, rg ? *rg : GpRange{}, acur, acap, acut);
 }
 
 // one partition level: histogram + scatter of every segment; returns the 256 counts per
@@ -598,7 +600,8 @@ nut_status gp_level(nut_ctx *c, GpMeta &mm, std::vector<GpSeg> &segs, int shift,
     // caller; the counts are the cursors read back after the scatter; rows [ovf, ovf +
     // 16 Ki) of every dst array must exist (overflowing runs land there).  NUT_ERR_CAPACITY
     // (no message) if a digit outgrew its rows: nothing is usable, partition again with a
-    // histogram.
+    // histogram.  With an overflow arena (acur) an overflowing run goes there instead and
+    // its digit's rows end at the first such run (see gp_scatter_kernel).
     // (bits: the digit width of this level, 6..8)
     if (gather || have_hist || !parts || bits < 6 || bits > 8)
       return fail(NUT_ERR_INVALID_ARG, "gp_level: capped layout needs parts");
@@ -610,10 +613,16 @@ nut_status gp_level(nut_ctx *c, GpMeta &mm, std::vector<GpSeg> &segs, int shift,
       for (int d = 0; d < nb; ++d) cur[i * nb + d] = segs[i].obase + (uint64_t)d * segs[i].ocap;
     }
     const uint32_t nst = gp_tiles(segs, 2 * GP_TILE, ts);
-    s = mm.begin(GpMeta::al(segs.size() * sizeof(GpSeg)) + GpMeta::al(ts.size() * 4 + 1) + GpMeta::al(cur.size() * 8));
+    s = mm.begin(GpMeta::al(segs.size() * sizeof(GpSeg)) + GpMeta::al(ts.size() * 4 + 1) + GpMeta::al(cur.size() * 8) +
+                 (acur ? GpMeta::al(nc * 8) : 0));
     if (s) return s;
     uint64_t *dcur;
     if ((s = mm.up(segs, &dseg)) || (s = mm.up(ts, &dts)) || (s = mm.up(cur, &dcur))) return s;
+    unsigned long long *dcut = nullptr;  // first overflowing run per digit (none: ~0)
+    if (acur) {
+      dcut = (unsigned long long *)mm.alloc(nc * 8);
+      NUT_HIP(hipMemsetAsync(dcut, 0xff, nc * 8, st));
+    }
     GpArrays ar;
     for (int a = 0; a < GP_MAX_ARR; ++a) {
       ar.src[a] = src[a];
@@ -622,12 +631,14 @@ nut_status gp_level(nut_ctx *c, GpMeta &mm, std::vector<GpSeg> &segs, int shift,
     ar.narr = narr;
     unsigned long long *dflag = (unsigned long long *)dcur + nc;
     gp_capped_launch(c, ar, dseg, dts, nst, shift, (unsigned long long *)dcur, kx, ovf, dflag, bits, src[2] != nullptr,
-                     rg, acur, acap);
+                     rg, acur, acap, dcut);
     NUT_HIP(hipGetLastError());
-    std::vector<uint64_t> back(cur.size());
+    std::vector<uint64_t> back(cur.size()), cut(dcut ? nc : 0);
     NUT_HIP(hipMemcpyAsync(back.data(), dcur, back.size() * 8, hipMemcpyDeviceToHost, st));
+    if (dcut) NUT_HIP(hipMemcpyAsync(cut.data(), dcut, nc * 8, hipMemcpyDeviceToHost, st));
     NUT_HIP(hipStreamSynchronize(st));
     if (back[nc]) return NUT_ERR_CAPACITY;
+    for (size_t i = 0; i < cut.size(); ++i) back[i] = std::min(back[i], cut[i]);
     hist.assign(nc, 0);
     for (size_t i = 0; i < nc; ++i) {
       hist[i] = back[i] - cur[i];
@@ -1113,8 +1124,9 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
   const uint64_t rows = (n + 2 * 65536 + 64 + 31) & ~31ull;
   const double slack1 = 1.0 + 6.0 / sqrt(lam);
   // B2: the level-1 regions (n x slack1 + per-region slack), then level 1's overflow arena
-  // (n / 4 rows), then one tile of scratch for runs an exhausted arena cannot take
-  const uint64_t arena1 = (n / 4 + 31) & ~31ull;
+  // (n / 2 rows: Zipf-like keys over 1e7 groups put ~1/3 of the rows there), then one tile
+  // of scratch for runs an exhausted arena cannot take
+  const uint64_t arena1 = (n / 2 + 31) & ~31ull;
   const uint64_t b2rows =
       ((uint64_t)ceil(n * slack1) + (66ull << (bits0 + bits1)) + arena1 + 2 * GP_TILE + 64 + 31) & ~31ull;
   e = c->gp_data.reserve((2 * (size_t)nstore * rows + (size_t)nstore * b2rows) * 8 + 256);
@@ -1223,7 +1235,7 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
   uint32_t *dts;
   uint64_t *dinit, *drend;
   e = mm.begin(GpMeta::al(s2.size() * sizeof(GpSeg)) + GpMeta::al(tiles.size() * 4 + 1) + GpMeta::al(init.size() * 8) +
-               GpMeta::al(init.size() * 8) + 4 * GpMeta::al(nparts * 8) + GpMeta::al(64));
+               2 * GpMeta::al(init.size() * 8) + 4 * GpMeta::al(nparts * 8) + GpMeta::al(64));
   if (e) return e;
   if ((e = mm.up(s2, &dseg)) || (e = mm.up(tiles, &dts)) || (e = mm.up(init, &dinit)) || (e = mm.up(rend, &drend)))
     return e;
@@ -1232,6 +1244,9 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
   unsigned long long *dcount = (unsigned long long *)mm.alloc(nparts * 8);
   uint64_t *doffs = (uint64_t *)mm.alloc(nparts * 8);
   unsigned long long *drun = (unsigned long long *)mm.alloc(64);
+  // the first overflowing run's start per partition (go_clamp_kernel), from the region ends
+  unsigned long long *dcut = (unsigned long long *)mm.alloc(nparts * 8);
+  NUT_HIP(hipMemcpyAsync(dcut, drend, nparts * 8, hipMemcpyDeviceToDevice, st));
   NUT_HIP(hipMemcpyAsync(dcur, dinit, init.size() * 8, hipMemcpyDeviceToDevice, st));
   NUT_HIP(hipMemsetAsync(drun, 0, 64, st));
   // the ordered result on the device (at most one group per row, at most cap)
@@ -1284,15 +1299,16 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
     const uint64_t q0 = (uint64_t)a0 * nb1, nq = (uint64_t)(a1 - a0) * nb1;
     c->timer.begin(st, NUT_KERNEL_AGGREGATE);
     gp_capped_launch(c, ar, dseg + a0, dts + tile0[j], ntile[j], 0, dcur + q0, 0, ovf1, dcur + nparts + j, bits1, false,
-                     &rg, darena + 1, acap1);
+                     &rg, darena + 1, acap1, dcut + q0);
     c->timer.end(st);
     NUT_HIP(hipGetLastError());
     NUT_HIP(hipEventRecord(ev1[j], st));
     NUT_HIP(hipStreamWaitEvent(ax, ev1[j], 0));
-    // partition rows [first row, cursor after the scatter), cut at the region's end: an
-    // overflowed run (flag read by the host afterwards) must not send the reads past it
+    // partition rows [first row, cursor after the scatter), cut at the first run that went
+    // to the arena (the rows after it are not the partition's)
     hipLaunchKernelGGL(go_clamp_kernel, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, ax,
-                       (const unsigned long long *)dcur + q0, (const uint64_t *)drend + q0, (uint32_t)nq, dend + q0);
+                       (const unsigned long long *)dcur + q0, (const unsigned long long *)dcut + q0, (uint32_t)nq,
+                       dend + q0);
     LaunchExtra sg;
     sg.seg_off = dinit + q0;
     sg.seg_end = (const uint64_t *)dend + q0;

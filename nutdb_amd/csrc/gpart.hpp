@@ -124,7 +124,8 @@ __global__ __launch_bounds__(T) void gp_scatter_kernel(GpArrays ar, const GpSeg 
                                                                 uint64_t ovf, unsigned long long *__restrict__ oflag,
                                                                 GpRange rg = GpRange{},
                                                                 unsigned long long *__restrict__ acur = nullptr,
-                                                                uint64_t acap = 0) {
+                                                                uint64_t acap = 0,
+                                                                unsigned long long *__restrict__ acut = nullptr) {
   static_assert(!RANGE || NK == 1, "range digits: one key");
   constexpr uint32_t TILE = T * GP_ITEMS;
   constexpr int BINS = 1 << BITS;  // (the product: GP_BINS = 256)
@@ -213,7 +214,10 @@ __global__ __launch_bounds__(T) void gp_scatter_kernel(GpArrays ar, const GpSeg 
       // overflow arena (acur: the ordered group-by) the run is kept instead: it claims rows
       // [ovf + *acur, + c) of the arena (acap rows, scratch after them), which the host
       // aggregates on its own and folds into the result — a heavy key costs its excess
-      // rows, not a rerun; only an exhausted arena sets the flag.
+      // rows, not a rerun; only an exhausted arena sets the flag.  The digit's valid rows
+      // then end where the first overflowing run would have started (acut[digit] = the
+      // least such start: every run claimed after it overflows too), so the rows between
+      // there and the region's end, never written, are never read.
       const GpSeg &g = segs[s];
       const bool over = !(VAR & 16) && ovf && c && gb + c > g.obase + (uint64_t)(tid + 1) * g.ocap;
       uint64_t o = gb;
@@ -221,6 +225,7 @@ __global__ __launch_bounds__(T) void gp_scatter_kernel(GpArrays ar, const GpSeg 
         const uint64_t ga = acur ? (uint64_t)atomicAdd(acur, (unsigned long long)c) : acap;
         const bool kept = acur && ga + c <= acap;
         if (!kept) atomicOr(oflag, 1ull);
+        if (acut) atomicMin(&acut[cs * BINS + tid], (unsigned long long)gb);
         o = ovf + (kept ? ga : acap);
       }
       s_gb[tid] = o - tex;  // out position of tile slot j with digit d = s_gb[d] + j
@@ -310,14 +315,15 @@ __global__ void go_sample_kernel(const int64_t *__restrict__ k, uint64_t n, uint
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) out[i] = k[i * step];
 }
 
-// end[q] = min(cursor[q], rend[q]): a capped level's partition ends cut at their regions'
-// ends.  When a run overflows its region the cursor still advances by the whole run (the
-// run itself goes to the scratch rows), so the raw cursor would send the aggregation past
-// the region — past the buffer for the last partitions — before the host sees the flag.
-__global__ void go_clamp_kernel(const unsigned long long *__restrict__ cursor, const uint64_t *__restrict__ rend,
+// end[q] = min(cursor[q], cut[q]): a capped level's partition ends.  When a run overflows
+// its region the cursor still advances by the whole run (the run itself goes to the
+// arena), so the raw cursor would send the aggregation past the region; cut[q] starts at
+// the region's end and the scatter lowers it to the first overflowing run's start
+// (gp_scatter_kernel's acut), below which every row was written.
+__global__ void go_clamp_kernel(const unsigned long long *__restrict__ cursor, const unsigned long long *__restrict__ cut,
                                 uint32_t n, uint64_t *__restrict__ end) {
   const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
-  if (q < n) end[q] = min((uint64_t)cursor[q], rend[q]);
+  if (q < n) end[q] = min((uint64_t)cursor[q], (uint64_t)cut[q]);
 }
 
 // one workgroup: offs[p] = *run + the groups of the partitions before p, then *run += all

@@ -1265,8 +1265,9 @@ uint64_t tile_table(std::vector<MsSeg> &segs, uint32_t tile, std::vector<uint32_
 
 }  // namespace
 
-// Local sorts are persistent (the S and M classes prefetch the next segment's keys): as
-// many workgroups as fit on the device, each walking the list with stride gridDim.x.
+// Local sorts: PF = persistent (as many workgroups as fit on the device, each walking the
+// list with stride gridDim.x, the next segment's keys prefetched), else one workgroup per
+// segment.
 template <int T, int K, bool PF>
 static void launch_class(nut_ctx *c, const MsBufs &bf, const MsSeg *d, unsigned n, uint64_t flip, uint32_t *fb) {
   static int per_cu = 0;        // resident workgroups per CU (occupancy query, once)
@@ -1282,8 +1283,11 @@ static void launch_class(nut_ctx *c, const MsBufs &bf, const MsSeg *d, unsigned 
 }
 
 // local sorts of n segments listed in device memory (a device-planned level's class list)
-// (the persistent classes prefetch the next segment's keys; the L class has no registers
-// to spare for a second key set)
+// (only the S class is persistent: for the M classes one workgroup per segment measured
+// 5.14 vs 5.73 ms (256x20) and 6.21-6.29 vs 6.56-6.65 ms (512x12) over 262144 segments of
+// 4768 keys, profiles/r05/sort/local_tune_sweep.log — the prefetch's extra registers and its
+// loop-carried loads cost more than the launch slots they save; the L class has no
+// registers to spare for a second key set)
 static nut_status launch_local_dev(nut_ctx *c, const MsBufs &bf, uint64_t flip, const MsSeg *d, unsigned n,
                                    uint32_t *fb, int cls) {
   if (n == 0) return NUT_OK;
@@ -1291,9 +1295,9 @@ static nut_status launch_local_dev(nut_ctx *c, const MsBufs &bf, uint64_t flip, 
   if (cls == 0)
     launch_class<LS_S_THREADS, LS_S_ITEMS, true>(c, bf, d, n, flip, fb);
   else if (cls == 1)
-    launch_class<LS_M_THREADS, LS_M_ITEMS, true>(c, bf, d, n, flip, fb);
+    launch_class<LS_M_THREADS, LS_M_ITEMS, false>(c, bf, d, n, flip, fb);
   else if (cls == 2)
-    launch_class<LS_M2_THREADS, LS_M2_ITEMS, true>(c, bf, d, n, flip, fb);
+    launch_class<LS_M2_THREADS, LS_M2_ITEMS, false>(c, bf, d, n, flip, fb);
   else
     launch_class<LS_L_THREADS, LS_L_ITEMS, false>(c, bf, d, n, flip, fb);
   NUT_HIP(hipGetLastError());

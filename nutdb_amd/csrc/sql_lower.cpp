@@ -17,6 +17,8 @@
 //     fused expression shapes of nut_expr (a*b, a+b, a-b, a*(1-b), a*(1-b)*(1+c)).
 //   * GROUP BY: 1-2 column identifiers; ORDER BY/LIMIT over the (small) group result
 //     run on the host after the device aggregation.
+#include <functional>
+
 #include "sql_plan.hpp"
 
 namespace nut {
@@ -1865,7 +1867,46 @@ bool grouped_body(const QueryBody &in) {
   return false;
 }
 
+// the number of columns a plan outputs (-1: SELECT *, known at execution)
+int visible_columns(const nut_plan &p) {
+  if (p.kind != NUT_PLAN_GROUPBY) return p.star ? -1 : (int)p.projs.size();
+  int n = 0;
+  for (const PlanOut &o : p.outs) n += o.hidden ? 0 : 1;
+  return n;
+}
+
 bool lower_query(const Query &q, nut_plan &p, Lowering &L) {
+  if (q.is_union) {  // UNION ALL: every branch its own plan, the results concatenated (§3.9)
+    std::vector<const Query *> br;
+    std::function<bool(const Query &)> collect = [&](const Query &x) -> bool {
+      if (!x.is_union) {
+        br.push_back(&x);
+        return true;
+      }
+      return x.ut == UnionType::UnionAll && x.l && x.r && collect(*x.l) && collect(*x.r);
+    };
+    if (!collect(q)) return L.fail("UNION [DISTINCT], INTERSECT and EXCEPT are not executed (UNION ALL is)");
+    for (size_t k = 0; k < br.size(); ++k) {
+      auto bp = std::make_shared<nut_plan>();
+      Lowering Lb;
+      const std::string which = "UNION ALL branch " + std::to_string(k + 1) + ": ";
+      if (!lower_query(*br[k], *bp, Lb)) return L.fail(which + Lb.err);
+      if (bp->join >= 0 || !bp->jn.empty() || bp->inner || !bp->uni.empty())
+        return L.fail(which + "a branch executes over one table (no JOIN or derived table)");
+      if (k && (bp->kind == NUT_PLAN_GROUPBY) != (p.uni[0]->kind == NUT_PLAN_GROUPBY))
+        return L.fail("UNION ALL: every branch a scan, or every branch an aggregate");
+      if (k && visible_columns(*bp) >= 0 && visible_columns(*p.uni[0]) >= 0 &&
+          visible_columns(*bp) != visible_columns(*p.uni[0]))
+        return L.fail("UNION ALL: the branches output different numbers of columns");
+      p.uni.push_back(bp);
+    }
+    p.kind = p.uni[0]->kind;
+    p.table = p.uni[0]->table;
+    for (const auto &b : p.uni)
+      for (const std::string &c : b->cols)
+        if (std::find(p.cols.begin(), p.cols.end(), c) == p.cols.end()) p.cols.push_back(c);
+    return true;
+  }
   // WITH name AS (query) ... FROM name [alias]: the CTE as a derived table
   if (!q.is_union && q.body && q.body->with && q.body->from && q.body->from->k == SourceKind::Table) {
     const QuerySource &f = *q.body->from;
@@ -1923,7 +1964,10 @@ bool lower_query(const Query &q, nut_plan &p, Lowering &L) {
 }
 
 bool lower(const Statement &st, nut_plan &p, Lowering &L) {
-  if (st.k != StmtKind::Select) return L.fail("only SELECT statements execute");
+  // CREATE VIEW v AS query: the rows the view holds — its query (the reference's fixture
+  // tests/sql/12.sql, a UNION ALL of four tables); nothing is stored
+  if (st.k == StmtKind::Create && st.is_view && st.view) return lower_query(st.view->query, p, L);
+  if (st.k != StmtKind::Select) return L.fail("only SELECT statements (and CREATE VIEW bodies) execute");
   return lower_query(st.query, p, L);
 }
 
@@ -2091,8 +2135,8 @@ std::string describe(const nut_plan &p) {
       return p.projs[j] >= 0 ? p.cols[p.projs[j]] : prog_text(p, p.proj_val[j]);
     };
     o += ",\"column\":";
-    json_str(o, p.star ? std::string("*") : proj_text(0));
-    if (!p.star && (p.projs.size() > 1 || p.projs[0] < 0)) {
+    json_str(o, p.star ? std::string("*") : p.projs.empty() ? std::string() : proj_text(0));  // (UNION ALL: its branches)
+    if (!p.star && (p.projs.size() > 1 || (!p.projs.empty() && p.projs[0] < 0))) {
       o += ",\"project\":[";
       for (size_t j = 0; j < p.projs.size(); ++j) {
         if (j) o += ',';
@@ -2193,6 +2237,11 @@ std::string describe(const nut_plan &p) {
   }
   o += ",\"offset\":" + std::to_string(p.offset);
   if (p.inner) o += ",\"derived\":" + describe(*p.inner);
+  if (!p.uni.empty()) {  // UNION ALL: the branches, in order
+    o += ",\"union_all\":[";
+    for (size_t i = 0; i < p.uni.size(); ++i) o += (i ? "," : "") + describe(*p.uni[i]);
+    o += "]";
+  }
   if (!p.subs.empty()) {  // scalar subqueries, by placeholder index ($subqueryN)
     o += ",\"subqueries\":[";
     for (size_t i = 0; i < p.subs.size(); ++i) o += (i ? "," : "") + describe(*p.subs[i]);

@@ -132,6 +132,89 @@ nut_status run_over_derived(nut_ctx *c, const nut_plan &p, nut_result *r1, nut_r
   return nut_plan_execute(c, &o, cols.data(), (int)cols.size(), r1->nrows, 0, out);
 }
 
+// UNION ALL: the branches' results in branch order as one result — device
+// columns copied after each other (scans), host columns appended (aggregates), decoded
+// strings appended, NULL flags kept per column.  Column names are branch 0's; each
+// column's type must agree across the branches.  Frees the parts.
+nut_status concat_results(nut_ctx *c, std::vector<nut_result *> &parts, nut_result **out) {
+  struct Free {
+    std::vector<nut_result *> &v;
+    ~Free() {
+      for (nut_result *r : v) nut_result_free(r);
+    }
+  } f{parts};
+  const nut_result &r0 = *parts[0];
+  const size_t nc = r0.names.size();
+  uint64_t total = 0;
+  for (size_t k = 0; k < parts.size(); ++k) {
+    const nut_result &r = *parts[k];
+    if (r.names.size() != nc)
+      return fail(NUT_ERR_PLAN, "UNION ALL: branch " + std::to_string(k + 1) + " outputs " + std::to_string(r.names.size()) +
+                                    " columns, branch 1 " + std::to_string(nc));
+    for (size_t j = 0; j < nc; ++j)
+      if (r.types[j] != r0.types[j])
+        return fail(NUT_ERR_PLAN, "UNION ALL: column " + std::to_string(j + 1) + " ('" + r0.names[j] +
+                                      "') has another type in branch " + std::to_string(k + 1));
+    total += r.nrows;
+  }
+  nut_result *u = new (std::nothrow) nut_result;
+  if (!u) return fail(NUT_ERR_OOM, "UNION ALL: out of host memory");
+  std::unique_ptr<nut_result, void (*)(nut_result *)> keep(u, nut_result_free);
+  u->kind = r0.kind;
+  u->device = c->device;
+  u->nrows = total;
+  u->names = r0.names;
+  u->types = r0.types;
+  bool any_str = false;
+  for (int t : r0.types) any_str |= t == NUT_T_STR;
+  if (any_str) {
+    u->strs.assign(nc, {});
+    for (size_t j = 0; j < nc; ++j)
+      if (r0.types[j] == NUT_T_STR)
+        for (const nut_result *r : parts)
+          if (j < r->strs.size()) u->strs[j].insert(u->strs[j].end(), r->strs[j].begin(), r->strs[j].end());
+  }
+  if (r0.kind == NUT_PLAN_GROUPBY) {
+    u->host.assign(nc, {});
+    for (size_t j = 0; j < nc; ++j)
+      for (const nut_result *r : parts)
+        if (j < r->host.size()) u->host[j].insert(u->host[j].end(), r->host[j].begin(), r->host[j].end());
+    *out = keep.release();
+    return NUT_OK;
+  }
+  DeviceGuard g(c->device);
+  u->dev_stride = total;
+  if (total) NUT_HIP(hipMalloc(&u->dev, total * nc * 8));
+  std::vector<int> vcols;  // columns with NULL flags in any branch
+  for (size_t j = 0; j < nc; ++j) {
+    bool v = false;
+    for (const nut_result *r : parts) v |= j < r->valid_of.size() && r->valid_of[j] >= 0 && r->valid;
+    u->valid_of.push_back(v ? (int)vcols.size() : -1);
+    if (v) vcols.push_back((int)j);
+  }
+  if (!vcols.empty() && total) NUT_HIP(hipMalloc((void **)&u->valid, total * vcols.size()));
+  uint64_t row = 0;
+  for (const nut_result *r : parts) {
+    if (r->nrows) {
+      for (size_t j = 0; j < nc; ++j) {
+        NUT_HIP(hipMemcpyAsync((int64_t *)u->dev + j * total + row, (const int64_t *)r->dev + j * r->dev_stride + r->dev_off,
+                               r->nrows * 8, hipMemcpyDeviceToDevice, c->stream));
+        if (u->valid_of[j] < 0) continue;
+        uint8_t *dv = u->valid + (size_t)u->valid_of[j] * total + row;
+        if (j < r->valid_of.size() && r->valid_of[j] >= 0 && r->valid)
+          NUT_HIP(hipMemcpyAsync(dv, r->valid + (size_t)r->valid_of[j] * r->dev_stride + r->dev_off, r->nrows,
+                                 hipMemcpyDeviceToDevice, c->stream));
+        else
+          NUT_HIP(hipMemsetAsync(dv, 1, r->nrows, c->stream));
+      }
+    }
+    row += r->nrows;
+  }
+  NUT_HIP(hipStreamSynchronize(c->stream));  // the parts' buffers are freed on return
+  *out = keep.release();
+  return NUT_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -230,6 +313,20 @@ void nut_plan_free(nut_plan *p) { delete p; }
 
 nut_status nut_plan_execute(nut_ctx *c, const nut_plan *p, const nut_column *cols, int ncols, uint64_t nrows,
                             uint64_t group_hint, nut_result **out) {
+  if (p && out && !p->uni.empty()) {  // UNION ALL: every branch over the same columns
+    *out = nullptr;
+    std::vector<nut_result *> parts;
+    for (const auto &b : p->uni) {
+      nut_result *r = nullptr;
+      nut_status st = nut_plan_execute(c, b.get(), cols, ncols, nrows, group_hint, &r);
+      if (st) {
+        for (nut_result *x : parts) nut_result_free(x);
+        return st;
+      }
+      parts.push_back(r);
+    }
+    return concat_results(c, parts, out);
+  }
   if (!c || !p || !out || (ncols && !cols) || ncols < 0) return fail(NUT_ERR_INVALID_ARG, "nut_plan_execute: NULL argument");
   *out = nullptr;
   if (p->inner) {  // a materialized derived table: its body first, over the caller's columns
@@ -287,6 +384,12 @@ nut_status nut_plan_execute2(nut_ctx *c, const nut_plan *p, const nut_column *le
                              nut_result **out) {
   if (!c || !p || !out || (nleft && !left) || (nright && !right) || nleft < 0 || nright < 0)
     return fail(NUT_ERR_INVALID_ARG, "nut_plan_execute2: NULL argument");
+  if (!p->uni.empty()) {  // UNION ALL of two branches: branch k over table k
+    const nut_column *tabs[2] = {left, right};
+    const int nc[2] = {nleft, nright};
+    const uint64_t nr[2] = {lrows, rrows};
+    return nut_plan_executen(c, p, tabs, nc, nr, 2, group_hint, out);
+  }
   if (p->inner) {  // a materialized derived table over the two tables, then the rest over it
     *out = nullptr;
     nut_result *r1 = nullptr;
@@ -325,6 +428,24 @@ nut_status nut_plan_executen(nut_ctx *c, const nut_plan *p, const nut_column *co
                              const uint64_t *nrows, int ntables, uint64_t group_hint, nut_result **out) {
   if (!c || !p || !out || !tables || !ncols || !nrows || ntables < 1)
     return fail(NUT_ERR_INVALID_ARG, "nut_plan_executen: NULL argument");
+  if (!p->uni.empty()) {  // UNION ALL: branch k over table k (or every branch over table 0)
+    if (ntables != 1 && (size_t)ntables != p->uni.size())
+      return fail(NUT_ERR_INVALID_ARG, "nut_plan_executen: a UNION ALL of " + std::to_string(p->uni.size()) +
+                                           " branches takes one table per branch (or one for all)");
+    *out = nullptr;
+    std::vector<nut_result *> parts;
+    for (size_t k = 0; k < p->uni.size(); ++k) {
+      const int t = ntables == 1 ? 0 : (int)k;
+      nut_result *r = nullptr;
+      nut_status st = nut_plan_execute(c, p->uni[k].get(), tables[t], ncols[t], nrows[t], group_hint, &r);
+      if (st) {
+        for (nut_result *x : parts) nut_result_free(x);
+        return st;
+      }
+      parts.push_back(r);
+    }
+    return concat_results(c, parts, out);
+  }
   if (p->inner) {  // a materialized derived table over the tables, then the rest over it
     *out = nullptr;
     nut_result *r1 = nullptr;
@@ -363,6 +484,19 @@ nut_status nut_plan_executen(nut_ctx *c, const nut_plan *p, const nut_column *co
 nut_status nut_plan_prepare(const nut_plan *p, const nut_column *cols, int ncols) {
   if (!p || (ncols && !cols) || ncols < 0) return fail(NUT_ERR_INVALID_ARG, "nut_plan_prepare: NULL argument");
   if (p->inner) return nut_plan_prepare(p->inner.get(), cols, ncols);  // (the rest compiles when it runs)
+  for (const auto &b : p->uni) {  // UNION ALL: every branch whose columns are all given
+    bool all = true;
+    for (const std::string &n : b->cols) {
+      bool found = false;
+      for (int i = 0; i < ncols && !found; ++i) found = cols[i].name && n == cols[i].name;
+      all = all && found;
+    }
+    if (all) {
+      nut_status st = nut_plan_prepare(b.get(), cols, ncols);
+      if (st) return st;
+    }
+  }
+  if (!p->uni.empty()) return NUT_OK;
   if (!p->compiled) return NUT_OK;  // precompiled kernels only
   // scalar subqueries: their values (int64 or f64 constants) decide the program types, so
   // the shape is compiled when the plan executes with the values in place
@@ -418,6 +552,10 @@ nut_status nut_plan_prepare(const nut_plan *p, const nut_column *cols, int ncols
 nut_status nut_table_execute(nut_ctx *c, nut_table *t, const nut_plan *p, uint64_t group_hint, nut_result **out) {
   if (!c || !t || !p || !out) return fail(NUT_ERR_INVALID_ARG, "nut_table_execute: NULL argument");
   *out = nullptr;
+  if (!p->uni.empty()) {  // UNION ALL: every branch over the one table
+    std::vector<nut_table *> ts(p->uni.size(), t);
+    return nut_table_executen(c, ts.data(), (int)ts.size(), p, group_hint, out);
+  }
   if (p->inner) {  // a materialized derived table (string outputs of its body stay unread)
     if (p->inner->join >= 0) return fail(NUT_ERR_INVALID_ARG, "nut_table_execute: the derived table has a JOIN (nut_table_execute2)");
     nut_result *r1 = nullptr;
@@ -475,6 +613,10 @@ nut_status nut_table_execute(nut_ctx *c, nut_table *t, const nut_plan *p, uint64
 nut_status nut_table_execute2(nut_ctx *c, nut_table *left, nut_table *right, const nut_plan *p, uint64_t group_hint,
                               nut_result **out) {
   if (!c || !left || !right || !p || !out) return fail(NUT_ERR_INVALID_ARG, "nut_table_execute2: NULL argument");
+  if (!p->uni.empty()) {  // UNION ALL of two branches: branch k over table k
+    nut_table *ts[2] = {left, right};
+    return nut_table_executen(c, ts, 2, p, group_hint, out);
+  }
   if (p->inner) {
     *out = nullptr;
     nut_result *r1 = nullptr;
@@ -521,6 +663,23 @@ nut_status nut_table_executen(nut_ctx *c, nut_table *const *tables, int ntables,
   if (!c || !tables || ntables < 1 || !p || !out) return fail(NUT_ERR_INVALID_ARG, "nut_table_executen: NULL argument");
   for (int k = 0; k < ntables; ++k)
     if (!tables[k]) return fail(NUT_ERR_INVALID_ARG, "nut_table_executen: NULL table");
+  if (!p->uni.empty()) {  // UNION ALL: branch k over table k (or every branch over table 0)
+    if (ntables != 1 && (size_t)ntables != p->uni.size())
+      return fail(NUT_ERR_INVALID_ARG, "nut_table_executen: a UNION ALL of " + std::to_string(p->uni.size()) +
+                                           " branches takes one table per branch (or one for all)");
+    *out = nullptr;
+    std::vector<nut_result *> parts;
+    for (size_t k = 0; k < p->uni.size(); ++k) {
+      nut_result *r = nullptr;
+      nut_status st = nut_table_execute(c, tables[ntables == 1 ? 0 : k], p->uni[k].get(), group_hint, &r);
+      if (st) {
+        for (nut_result *x : parts) nut_result_free(x);
+        return st;
+      }
+      parts.push_back(r);
+    }
+    return concat_results(c, parts, out);
+  }
   if (p->inner) {
     *out = nullptr;
     nut_result *r1 = nullptr;

@@ -180,6 +180,11 @@ struct nut_plan {
   // table is materialized — `inner` executes over the caller's columns first and this plan
   // runs over its result columns (bound by output name)
   std::shared_ptr<nut_plan> inner;
+  // UNION ALL: the branches, each its own single-table plan, run in order
+  // and their results concatenated; this plan mirrors branch 0's kind, and `cols` lists
+  // every branch's columns once (what nut_plan_execute binds; nut_plan_executen gives
+  // branch k the k-th table)
+  std::vector<std::shared_ptr<nut_plan>> uni;
 };
 
 struct nut_result {

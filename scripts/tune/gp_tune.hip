@@ -114,7 +114,7 @@ static void run(Ctx &c, const char *name, bool check) {
     CK(hipEventRecord(c.e0));
     hipLaunchKernelGGL(kern, dim3(grid), dim3(T), 0, 0, ar, (const nut::GpSeg *)c.dseg, (const uint32_t *)dts, ntiles,
                        64 - BITS, 0, c.cur, 0ull, (uint64_t)BINS * cap, c.cur + BINS, nut::GpRange{},
-                       (unsigned long long *)nullptr, (uint64_t)0);
+                       (unsigned long long *)nullptr, (uint64_t)0, (unsigned long long *)nullptr);
     CK(hipEventRecord(c.e1));
     best = std::min(best, elapsed(c.e0, c.e1));
   }

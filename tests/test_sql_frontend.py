@@ -529,7 +529,7 @@ def test_plan_scalar_subquery_errors(sql, frag):
     ("select k, sum(median(v)) from t group by k", "median"),
     ("select count(*), v from t", "no GROUP BY"),
     ("select x, y from t where x > 1 order by x + y", "is not a column"),
-    ("select x from t where x < 1 union all select x from t", "UNION"),
+    ("select x from t where x < 1 union distinct select x from t", "UNION ALL is"),
     ("select x from t where x >= toDate('1998-13-01')", "toDate"),
 ])
 def test_plan_lowering_errors(sql, frag):
@@ -585,3 +585,21 @@ def test_plan_derived_table_flattened():
     assert d["derived"]["kind"] == "groupby" and d["table"] == "s" and d["column"] == "x"
     with pytest.raises(NutError, match="projection bodies"):
         Plan("select x from (select distinct k as x from t) as s")
+
+
+def test_plan_union_all_and_view_body():
+    """UNION ALL lowers to one plan per branch; CREATE VIEW .. AS query
+    plans the view's query (the reference's fixture 12, a UNION ALL of four tables)."""
+    from pathlib import Path
+    d = Plan((Path(__file__).parent / "golden" / "sql" / "12.sql").read_text()).describe()
+    assert d["kind"] == "filter" and [b["table"] for b in d["union_all"]] == ["SUPPLY1", "SUPPLY2", "SUPPLY3", "SUPPLY4"]
+    assert set(d["columns"]) == {"sth", "supplyID", "supplier"}
+    assert "sth" in d["union_all"][0].get("where_expr", "") and "sth" not in d["union_all"][1]["columns"]
+    g = Plan("select k, sum(v) from a group by k union all select k, sum(v) from b group by k").describe()
+    assert g["kind"] == "groupby" and len(g["union_all"]) == 2
+    for sql, frag in [("select a from t union all select a, b from u", "different numbers of columns"),
+                      ("select a from t union all select count() from u", "every branch a scan"),
+                      ("select a from t union distinct select a from u", "UNION ALL is"),
+                      ("select a from t join u on t.x = u.x union all select a from v", "over one table")]:
+        with pytest.raises(NutError, match=frag):
+            Plan(sql)
