@@ -239,6 +239,9 @@ typedef enum {
  *   LOOKUP   one int operand x; v = device address of a byte table, arg = its length:
  *            bool table[x] != 0 for 0 <= x < arg, else false (dictionary predicates such
  *            as LIKE over dictionary codes; the table must outlive the call)
+ *   MAP      one int operand x; v = device address of an int64 table, arg = its length:
+ *            int table[x] for 0 <= x < arg, else -1 (dictionary functions such as
+ *            substring over dictionary codes: code -> the result string's code)
  *   DATEPART one int operand d = days since 1970-01-01 (proleptic Gregorian), int result
  *            by arg (nut_date_part): year, month 1-12, day of month, quarter 1-4, day of
  *            week (Monday = 1 .. Sunday = 7), day of year 1-366, year * 100 + month,
@@ -251,7 +254,8 @@ typedef enum {
   NUT_P_AND = 15, NUT_P_OR = 16, NUT_P_XOR = 17, NUT_P_NOT = 18,
   NUT_P_BITAND = 19, NUT_P_BITOR = 20, NUT_P_BITXOR = 21, NUT_P_BITNOT = 22,
   NUT_P_SHL = 23, NUT_P_SHR = 24,
-  NUT_P_IF = 25, NUT_P_ABS = 26, NUT_P_TO_F64 = 27, NUT_P_LOOKUP = 28, NUT_P_DATEPART = 29
+  NUT_P_IF = 25, NUT_P_ABS = 26, NUT_P_TO_F64 = 27, NUT_P_LOOKUP = 28, NUT_P_DATEPART = 29,
+  NUT_P_MAP = 30
 } nut_prog_op;
 typedef enum {
   NUT_DP_YEAR = 0, NUT_DP_MONTH = 1, NUT_DP_DAY = 2, NUT_DP_QUARTER = 3, NUT_DP_WEEKDAY = 4, NUT_DP_YEARDAY = 5,
@@ -260,8 +264,8 @@ typedef enum {
 typedef enum { NUT_PT_I64 = 0, NUT_PT_F64 = 1, NUT_PT_BOOL = 2 } nut_prog_value_type;
 typedef struct {
   int32_t op;   /* nut_prog_op */
-  int32_t arg;  /* NUT_P_COL: column index; NUT_P_LOOKUP: table length; NUT_P_DATEPART: part */
-  int64_t v;    /* NUT_P_I64 / NUT_P_F64 constant; NUT_P_LOOKUP: table address */
+  int32_t arg;  /* NUT_P_COL: column index; NUT_P_LOOKUP / MAP: table length; NUT_P_DATEPART: part */
+  int64_t v;    /* NUT_P_I64 / NUT_P_F64 constant; NUT_P_LOOKUP / MAP: table address */
 } nut_prog_node;
 typedef struct {
   int32_t n;                  /* 0..NUT_MAX_PROG_NODES */

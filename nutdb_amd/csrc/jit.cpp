@@ -75,9 +75,9 @@ struct Gen {
       PVal a[3];
       const int op = nd.op;
       const int arity = op <= NUT_P_F64 ? 0 : (op == NUT_P_NOT || op == NUT_P_BITNOT || op == NUT_P_ABS ||
-                                                op == NUT_P_TO_F64 || op == NUT_P_LOOKUP || op == NUT_P_DATEPART) ? 1
+                                                op == NUT_P_TO_F64 || op == NUT_P_LOOKUP || op == NUT_P_DATEPART || op == NUT_P_MAP) ? 1
                                                                                          : op == NUT_P_IF ? 3 : 2;
-      if (op < 0 || op > NUT_P_DATEPART) return fail("unknown program op " + std::to_string(op));
+      if (op < 0 || op > NUT_P_MAP) return fail("unknown program op " + std::to_string(op));
       if (!pop(arity, a)) return fail("program stack underflow at node " + std::to_string(i));
       PVal r;
       const bool f = arity == 2 && (a[0].t == NUT_PT_F64 || a[1].t == NUT_PT_F64);
@@ -169,6 +169,13 @@ struct Gen {
           r = {NUT_PT_BOOL, "jlookup(" + as_i(a[0]) + ", " + konst((uint64_t)nd.v) + ", " +
                                 konst((uint64_t)(int64_t)nd.arg) + ")"};
           break;
+        case NUT_P_MAP:
+          if (a[0].t == NUT_PT_F64) return fail("MAP needs an integer operand");
+          if (nd.arg < 0) return fail("MAP table length is negative");
+          if (nd.arg > 0 && nd.v == 0) return fail("MAP table has no address");
+          r = {NUT_PT_I64, "jmap(" + as_i(a[0]) + ", " + konst((uint64_t)nd.v) + ", " +
+                               konst((uint64_t)(int64_t)nd.arg) + ")"};
+          break;
         case NUT_P_DATEPART:
           if (a[0].t == NUT_PT_F64) return fail("DATEPART needs an integer operand (days)");
           if (nd.arg < NUT_DP_YEAR || nd.arg > NUT_DP_YYYYMMDD) return fail("DATEPART: unknown part " + std::to_string(nd.arg));
@@ -214,6 +221,11 @@ __device__ __forceinline__ int64_t jabs(int64_t a) { return a < 0 ? (int64_t)(0 
 __device__ __forceinline__ bool jlookup(int64_t x, uint64_t t, uint64_t n) {
   if ((uint64_t)x >= n) return false;
   return ((const uint8_t *)t)[x] != 0;
+}
+// int64-table map (code -> code); outside the table: -1, which no dictionary string has
+__device__ __forceinline__ int64_t jmap(int64_t x, uint64_t t, uint64_t n) {
+  if ((uint64_t)x >= n) return -1;
+  return ((const int64_t *)t)[x];
 }
 // civil-from-days (proleptic Gregorian); P = nut_date_part.  d is clamped to +-2^40 days
 // first, so no intermediate overflows.

@@ -370,9 +370,10 @@ nut_status exec_groupby(nut_ctx *c, const nut_plan &p, const nut_column *const *
     if (o.kind == OUT_EXPR) {
       type = -1;  // below, once every other output is known
     } else if (o.kind == OUT_KEY) {
-      if (dicts && p.keys[o.a] >= 0 && dicts[p.keys[o.a]]) {
+      const int dc = key_dict_col(p, (size_t)o.a);
+      if (dicts && dc >= 0 && dicts[dc]) {
         type = NUT_T_STR;
-        out_dict[j] = dicts[p.keys[o.a]];
+        out_dict[j] = dicts[dc];
       }
       for (uint64_t i = 0; i < ng; ++i) col[i] = (uint64_t)keys[i * nk + o.a];
     } else if (o.kind == OUT_AGG) {

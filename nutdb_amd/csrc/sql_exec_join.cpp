@@ -109,7 +109,7 @@ bool mask_null_projections(nut_plan &q, const std::function<bool(int)> &nullable
     if (q.projs[j] >= 0) read.push_back(q.projs[j]);
     for (const PProg *pp : {&q.proj_val[j], &q.proj_mask[j]})
       for (const PNode &nd : *pp)
-        if (nd.op == NUT_P_COL || nd.op == P_LIKE || nd.op == P_ILIKE) read.push_back(nd.col);
+        if (reads_col(nd.op)) read.push_back(nd.col);
     std::vector<int> flags;
     for (int ci : read)
       if (nullable(ci)) {
@@ -226,7 +226,7 @@ nut_status exec_join(nut_ctx *c, const nut_plan &p, const nut_column *lc, int nl
   int bkey = side[k0] == ps ? k1 : k0, pkey = side[k0] == ps ? k0 : k1;
   auto in_prog = [](const PProg &pp, int i) {  // (LIKE leaves read their column too)
     for (const PNode &nd : pp)
-      if ((nd.op == NUT_P_COL || nd.op == P_LIKE || nd.op == P_ILIKE) && nd.col == i) return true;
+      if (reads_col(nd.op) && nd.col == i) return true;
     return false;
   };
   // read by plan q after the join: as a row decider, a projection (proj NULL: counted as a
@@ -285,7 +285,7 @@ nut_status exec_join(nut_ctx *c, const nut_plan &p, const nut_column *lc, int nl
     for (PProg &cj : conj) {
       int sd = -1;
       for (const PNode &nd : cj)
-        if (nd.op == NUT_P_COL || nd.op == P_LIKE || nd.op == P_ILIKE) sd = sd < 0 || sd == side[nd.col] ? side[nd.col] : 2;
+        if (reads_col(nd.op)) sd = sd < 0 || sd == side[nd.col] ? side[nd.col] : 2;
       (sd < 2 && pushable(sd) ? push[sd] : keep).push_back(std::move(cj));
     }
     p2.where = and_all(keep);
@@ -640,7 +640,7 @@ nut_status exec_joinn(nut_ctx *c, const nut_plan &p, const nut_column *const *ta
     if (!js.scope) {  // ON filters: conditions on the step's own table, applied before it joins
       for (PProg &cj : conj) {
         for (const PNode &nd : cj)
-          if ((nd.op == NUT_P_COL || nd.op == P_LIKE || nd.op == P_ILIKE) && side[nd.col] != t)
+          if (reads_col(nd.op) && side[nd.col] != t)
             return fail(NUT_ERR_PLAN, "JOIN " + std::to_string(t) + ": an ON condition beyond the key equality must read '" +
                                           tname[t] + "' alone (column '" + p.cols[nd.col] + "')");
         sub_push[t].push_back(std::move(cj));
@@ -650,7 +650,7 @@ nut_status exec_joinn(nut_ctx *c, const nut_plan &p, const nut_column *const *ta
     for (PProg &cj : conj) {
       bool inner = false, outer = false, later = false;
       for (const PNode &nd : cj)
-        if (nd.op == NUT_P_COL || nd.op == P_LIKE || nd.op == P_ILIKE) {
+        if (reads_col(nd.op)) {
           inner = inner || side[nd.col] == t;
           outer = outer || side[nd.col] < t;
           later = later || side[nd.col] > t;
@@ -700,7 +700,7 @@ nut_status exec_joinn(nut_ctx *c, const nut_plan &p, const nut_column *const *ta
   }
   auto in_prog = [](const PProg &pp, int i) {
     for (const PNode &nd : pp)
-      if ((nd.op == NUT_P_COL || nd.op == P_LIKE || nd.op == P_ILIKE) && nd.col == i) return true;
+      if (reads_col(nd.op) && nd.col == i) return true;
     return false;
   };
   // read by plan q after the joins: as a row decider / key, a projection, or inside an aggregate
@@ -759,7 +759,7 @@ nut_status exec_joinn(nut_ctx *c, const nut_plan &p, const nut_column *const *ta
     for (PProg &cj : conj) {
       int sd = -1;
       for (const PNode &nd : cj)
-        if (nd.op == NUT_P_COL || nd.op == P_LIKE || nd.op == P_ILIKE) sd = sd < 0 || sd == side[nd.col] ? side[nd.col] : nt;
+        if (reads_col(nd.op)) sd = sd < 0 || sd == side[nd.col] ? side[nd.col] : nt;
       (sd >= 0 && sd < nt ? push[sd] : keep).push_back(std::move(cj));
     }
     p2.where = and_all(keep);

@@ -131,7 +131,10 @@ nut_status exec_sort_rows(nut_ctx *c, const nut_plan &p, const nut_column *const
   std::vector<int> sdict(np, -1);
   for (size_t j = 0; j < np; ++j) {
     int dc = p.projs[j];
-    if (computed_proj(p, j)) dc = p.proj_val[j].size() == 1 && p.proj_val[j][0].op == NUT_P_COL ? p.proj_val[j][0].col : -1;
+    if (computed_proj(p, j))
+      dc = p.proj_val[j].size() == 1 && (p.proj_val[j][0].op == NUT_P_COL || p.proj_val[j][0].op == P_SUBSTR)
+               ? p.proj_val[j][0].col
+               : -1;
     if (dc >= 0 && dicts && dicts[dc]) sdict[j] = dc;
     r->names.push_back(p.outs[j].name);
     r->types.push_back(sdict[j] >= 0 ? NUT_T_STR : p.projs[j] >= 0 ? bound[p.projs[j]]->type : ctype[j]);
@@ -424,7 +427,7 @@ nut_status check_strings(const nut_plan &p, const PProg &pp, const Dict *const *
       a[i] = st.back();
       st.pop_back();
     }
-    if (op == NUT_P_COL) {
+    if (op == NUT_P_COL || op == P_SUBSTR) {  // (a substring: a code of its column's dictionary)
       st.push_back(dicts[n.col]);
       continue;
     }
@@ -444,6 +447,51 @@ nut_status check_strings(const nut_plan &p, const PProg &pp, const Dict *const *
   if (!st.empty() && st.back()) return fail(NUT_ERR_PLAN, std::string(what) + ": a string value (only count() takes strings)");
   return NUT_OK;
 }
+
+int key_dict_col(const nut_plan &p, size_t j) {
+  if (j < p.keys.size() && p.keys[j] >= 0) return p.keys[j];
+  if (j < p.key_progs.size() && p.key_progs[j].size() == 1 && p.key_progs[j][0].op == P_SUBSTR)
+    return p.key_progs[j][0].col;
+  return -1;
+}
+
+// substring(s, off, len), bytes (ClickHouse `substring`): the window starts at byte off - 1
+// (off >= 1) or |off| bytes before the end (off < 0), is len bytes long (len < 0: ends |len|
+// bytes before the end; no len, kHuge: at the end), and is clipped to the string — a window
+// starting before the string keeps only its part inside; off = 0 gives ''
+std::string substr_bytes(const std::string &s, int off, i128 len) {
+  const i128 sz = (i128)s.size();
+  if (off == 0) return std::string();
+  const i128 w0 = off > 0 ? (i128)off - 1 : sz + off;
+  const i128 w1 = len >= kHuge ? sz : len >= 0 ? w0 + len : sz + len;
+  const i128 b = std::max<i128>(0, std::min(w0, sz)), e = std::min(w1, sz);
+  return e > b ? s.substr((size_t)b, (size_t)(e - b)) : std::string();
+}
+
+namespace {
+// substring(col, off, len) over a dictionary (P_SUBSTR): the table code -> the code of its
+// substring in the same dictionary.  The dictionary gains the substrings it lacks — append
+// only, so every code already handed out (the table's columns, earlier results) keeps its
+// string — which lets a substring meet the column's own strings, string constants and
+// GROUP BY decoding exactly as a column does.  An Enum's declared dictionary cannot grow.
+nut_status substr_map(const Dict *cd, const std::string &cname, int off, i128 len, std::vector<int64_t> &map) {
+  if (!cd) return fail(NUT_ERR_PLAN, "substring needs a string column ('" + cname + "')");
+  if (cd->fixed) return fail(NUT_ERR_PLAN, "substring over the Enum column '" + cname + "' is not executed");
+  Dict *d = const_cast<Dict *>(cd);
+  const size_t n0 = d->strs.size();
+  map.resize(n0);
+  for (size_t i = 0; i < n0; ++i) {
+    std::string t = substr_bytes(d->strs[i], off, len);
+    auto it = d->codes.find(t);
+    if (it == d->codes.end()) {
+      it = d->codes.emplace(t, (int64_t)d->strs.size()).first;
+      d->strs.push_back(std::move(t));
+    }
+    map[i] = it->second;
+  }
+  return NUT_OK;
+}
+}  // namespace
 
 nut_status build_spec(const nut_plan &p, const nut_column *const *bound, const Dict *const *dicts, uint64_t n,
                       nut_agg_spec &s, ProgStore &store, std::vector<int> &agg_f64, GbExtra *gx) {
@@ -536,6 +584,45 @@ nut_status build_spec(const nut_plan &p, const nut_column *const *bound, const D
       v.push_back(lk);
       return NUT_OK;
     };
+    // substring maps, all built before any program binds a string constant (a constant
+    // compared with a substring may name a string only the substrings add)
+    std::map<std::tuple<int, int, i128>, nut_prog_node> smaps;
+    auto substr_node = [&](const PNode &n, nut_prog_node &out) -> nut_status {
+      const auto key = std::make_tuple(n.col, n.arg, n.c.v);
+      auto it = smaps.find(key);
+      if (it != smaps.end()) {
+        out = it->second;
+        return NUT_OK;
+      }
+      out = nut_prog_node{NUT_P_MAP, 0, 0};  // compile-only (no dictionaries): every row -1
+      if (dicts) {
+        std::vector<int64_t> map;
+        nut_status ms = substr_map(dicts[n.col], p.cols[n.col], n.arg, n.c.v, map);
+        if (ms) return ms;
+        if (map.size() > (size_t)INT32_MAX) return fail(NUT_ERR_PLAN, "substring over a dictionary of more than 2^31 strings");
+        if (!map.empty()) {
+          store.tables.emplace_back();
+          DevBuf &t = store.tables.back();
+          NUT_HIP(hipMalloc(&t.p, map.size() * 8));
+          NUT_HIP(hipMemcpy(t.p, map.data(), map.size() * 8, hipMemcpyHostToDevice));
+          out = nut_prog_node{NUT_P_MAP, (int32_t)map.size(), (int64_t)(uintptr_t)t.p};
+        }
+      }
+      smaps.emplace(key, out);
+      return NUT_OK;
+    };
+    {
+      std::vector<const PProg *> all{&p.where};
+      for (const PlanAgg &g : p.aggs) all.push_back(&g.val), all.push_back(&g.mask);
+      for (const PProg &k : p.key_progs) all.push_back(&k);
+      for (const PProg *pp : all)
+        for (const PNode &nd : *pp)
+          if (nd.op == P_SUBSTR) {
+            nut_prog_node tmp;
+            nut_status ss = substr_node(nd, tmp);
+            if (ss) return ss;
+          }
+    }
     auto resolve = [&](const PProg &pp, nut_prog &out, const char *what, int32_t *type,
                        bool str_ok = false) -> nut_status {
       store.nodes.emplace_back();
@@ -545,6 +632,15 @@ nut_status build_spec(const nut_plan &p, const nut_column *const *bound, const D
         if (n.op == P_LIKE || n.op == P_ILIKE) {
           nut_status ls = lower_like(n, v);
           if (ls) return ls;
+          continue;
+        }
+        if (n.op == P_SUBSTR) {  // COL, MAP (code -> the substring's code)
+          nut_prog_node col{NUT_P_COL, 0, 0}, mp;
+          nut_status bs = bind_col(n.col, col.arg);
+          if (!bs) bs = substr_node(n, mp);
+          if (bs) return bs;
+          v.push_back(col);
+          v.push_back(mp);
           continue;
         }
         if (n.op == NUT_P_COL) {
@@ -609,7 +705,10 @@ nut_status build_spec(const nut_plan &p, const nut_column *const *bound, const D
       if (gx) gx->slot[a] = k;
       s.agg_op[k] = g.op;
       if (g.op != NUT_AGG_COUNT) {
-        st = resolve(g.val, s.agg_val[k], "aggregate argument", &t);
+        // (a scan's computed projection may be a string: one column or substring of one)
+        const bool str_val = p.kind != NUT_PLAN_GROUPBY && g.val.size() == 1 &&
+                             (g.val[0].op == NUT_P_COL || g.val[0].op == P_SUBSTR);
+        st = resolve(g.val, s.agg_val[k], "aggregate argument", &t, str_val);
         agg_f64[a] = t == NUT_PT_F64;
       }
       if (!st && !g.mask.empty()) st = resolve(g.mask, s.agg_mask[k], "aggregate argument", &t);
@@ -617,7 +716,7 @@ nut_status build_spec(const nut_plan &p, const nut_column *const *bound, const D
     for (size_t j = 0; j < p.key_progs.size() && !st && keyprog && gx; ++j) {
       // a plain string column is a key of dictionary codes; computed keys are numbers
       gx->key.emplace_back();
-      st = resolve(p.key_progs[j], gx->key.back(), "GROUP BY key", &t, p.keys[j] >= 0);
+      st = resolve(p.key_progs[j], gx->key.back(), "GROUP BY key", &t, key_dict_col(p, j) >= 0);
       if (!st && t == NUT_PT_F64)
         st = fail(NUT_ERR_PLAN, "GROUP BY key '" + p.key_text[j] + "' is float64 (keys are integers)");
     }

@@ -266,7 +266,7 @@ int mirror(int op) { return op == NUT_LT ? NUT_GT : op == NUT_GT ? NUT_LT : op =
 
 
 int pnode_arity(int op) {
-  if (op == P_LIKE || op == P_ILIKE) return 0;
+  if (op == P_LIKE || op == P_ILIKE || op == P_SUBSTR) return 0;
   return op <= NUT_P_F64 ? 0 : (op == NUT_P_NOT || op == NUT_P_BITNOT || op == NUT_P_ABS ||
                                 op == NUT_P_TO_F64 || op == NUT_P_DATEPART) ? 1 : op == NUT_P_IF ? 3 : 2;
 }
@@ -527,7 +527,8 @@ bool is_null_lit(const Expr &e) { return e.k == EK::Literal && e.lit->k == LitKi
 // a string constant compared (= / != / IN / CASE x WHEN) with a column takes that
 // column's dictionary at execution
 void bind_str(PProg &a, const PProg &other) {
-  if (a.size() == 1 && a[0].op == NUT_P_I64 && a[0].c.is_str && other.size() == 1 && other[0].op == NUT_P_COL)
+  if (a.size() == 1 && a[0].op == NUT_P_I64 && a[0].c.is_str && other.size() == 1 &&
+      (other[0].op == NUT_P_COL || other[0].op == P_SUBSTR))  // (substrings: codes of the column's dictionary)
     a[0].col = other[0].col;
 }
 bool is_agg_name(sv n) {
@@ -740,9 +741,27 @@ bool lower_prog(nut_plan &p, const Expr &e, PProg &o, Lowering &L) {
         o.push_back(dp);
         return true;
       }
+      if ((ieq(n, "substring") || ieq(n, "substr") || ieq(n, "mid")) && (na == 2 || na == 3)) {
+        // substring(col, offset[, length]) of a string column, constant offset / length:
+        // a dictionary function (P_SUBSTR: the codes map to the substrings' codes)
+        sv cname;
+        CVal off, len;
+        len.v = kHuge;
+        if (!column_ref(p, e.kids[0], cname) || !const_eval(e.kids[1], off, L) || !off.is_int || off.is_str ||
+            off.param >= 0 || (na == 3 && (!const_eval(e.kids[2], len, L) || !len.is_int || len.is_str || len.param >= 0)))
+          return L.fail("substring takes a string column and integer constants ('" + expr_text(e) + "')");
+        if (off.v < INT32_MIN || off.v > INT32_MAX) return L.fail("substring offset out of range ('" + expr_text(e) + "')");
+        PNode sn;
+        sn.op = P_SUBSTR;
+        sn.col = col_index(p, cname);
+        sn.arg = (int)off.v;
+        sn.c = len;
+        o.push_back(sn);
+        return true;
+      }
       if (ieq(n, "todate")) return L.fail("toDate takes one 'YYYY-MM-DD' constant");
       return L.fail("function '" + std::string(n) + "' is not executed (executed: if, multiIf, abs, toFloat64, intDiv, "
-                    "modulo, toYear/getYear, toMonth, toDayOfMonth, toQuarter, toDayOfWeek, toDayOfYear, toYYYYMM, "
+                    "modulo, substring, toYear/getYear, toMonth, toDayOfMonth, toQuarter, toDayOfWeek, toDayOfYear, toYYYYMM, "
                     "toYYYYMMDD)");
     }
     default: return L.fail("'" + expr_text(e) + "' is not executed (parameters, collections, subqueries)");
@@ -960,7 +979,7 @@ bool lower_output(nut_plan &p, const Expr &e, PlanOut &o, Lowering &L) {
     if (!lower_nullable(p, e.kids[0], a.val, a.mask, nullable, L)) return false;
     for (const PProg *pp : {&a.val, &a.mask})
       for (const PNode &nd : *pp)
-        if (nd.op == NUT_P_COL || nd.op == P_LIKE || nd.op == P_ILIKE) a.refs.push_back(nd.col);
+        if (reads_col(nd.op)) a.refs.push_back(nd.col);
     std::sort(a.refs.begin(), a.refs.end());
     a.refs.erase(std::unique(a.refs.begin(), a.refs.end()), a.refs.end());
     a.op = NUT_AGG_COUNT;
@@ -982,7 +1001,7 @@ bool lower_output(nut_plan &p, const Expr &e, PlanOut &o, Lowering &L) {
     if (!star && !lower_nullable(p, e.kids[0], a.val, a.mask, nullable, L)) return false;
     for (const PProg *pp : {&a.val, &a.mask})
       for (const PNode &nd : *pp)
-        if (nd.op == NUT_P_COL || nd.op == P_LIKE || nd.op == P_ILIKE) a.refs.push_back(nd.col);
+        if (reads_col(nd.op)) a.refs.push_back(nd.col);
     std::sort(a.refs.begin(), a.refs.end());
     a.refs.erase(std::unique(a.refs.begin(), a.refs.end()), a.refs.end());
     if (op == NUT_AGG_COUNT) a.val.clear();  // count(x) counts the rows where x is not NULL
@@ -1972,7 +1991,8 @@ bool lower(const Statement &st, nut_plan &p, Lowering &L) {
 }
 
 // An uncorrelated scalar subquery in a value position: planned on its own (a global
-// aggregate with one output over the same table, no JOIN), executed before the plan; `c`
+// aggregate with one output over the plan's FROM table, no JOIN — in a JOIN plan too:
+// table 0 of the execution), executed before the plan; `c`
 // becomes a placeholder naming it (resolve_subqueries puts the value in at execution).
 bool scalar_subquery(nut_plan &p, const Expr &e, CVal &c, Lowering &L) {
   if (e.k != EK::Subquery || !e.q) return false;
@@ -1985,7 +2005,6 @@ bool scalar_subquery(nut_plan &p, const Expr &e, CVal &c, Lowering &L) {
     return L.fail("a scalar subquery executes as a global aggregate with one output (SELECT agg(..) FROM t ..)");
   if (sub->join >= 0 || !sub->subs.empty() || sub->star)
     return L.fail("a scalar subquery executes over one table, without JOIN or nested subqueries");
-  if (p.join >= 0) return L.fail("scalar subqueries execute in single-table plans (the query has a JOIN)");
   if (!p.table.empty() && !sub->table.empty() && !ieq(p.table, sub->table))
     return L.fail("scalar subquery over table '" + sub->table + "' (the query reads '" + p.table +
                   "'): subqueries execute over the same table");
@@ -2016,6 +2035,9 @@ std::string prog_text(const nut_plan &p, const PProg &pp) {
     };
     if (n.op == P_LIKE || n.op == P_ILIKE)
       st.push_back("(" + shown(p.cols[n.col]) + (n.op == P_LIKE ? " like " : " ilike ") + cval_str(n.c) + ")");
+    else if (n.op == P_SUBSTR)
+      st.push_back("substring(" + shown(p.cols[n.col]) + ", " + std::to_string(n.arg) +
+                   (n.c.v >= kHuge ? std::string() : ", " + i128_str(n.c.v)) + ")");
     else if (n.op == NUT_P_COL) st.push_back(shown(p.cols[n.col]));
     else if (n.op == NUT_P_I64 || n.op == NUT_P_F64) st.push_back(cval_str(n.c));
     else if (n.op == NUT_P_DATEPART) {

@@ -92,6 +92,7 @@ nut_status resolve_subqueries(const nut_plan &p, nut_plan &q,
   for (PProg &pp : q.proj_mask) prog(pp);
   for (PProg &pp : q.key_progs) prog(pp);
   for (PlanAgg &a : q.aggs) prog(a.val), prog(a.mask);
+  for (nut_plan::JoinStep &js : q.jn) prog(js.cond);
   std::function<void(HNode &)> hv = [&](HNode &h) {
     if (h.k == H_CONST && h.param >= 0) {
       if (null[h.param]) bad_null = true;
@@ -397,7 +398,13 @@ nut_status nut_plan_execute2(nut_ctx *c, const nut_plan *p, const nut_column *le
     return st ? st : run_over_derived(c, *p, r1, out);
   }
   if (p->join < 0) return nut_plan_execute(c, p, left, nleft, lrows, group_hint, out);
-  if (!p->subs.empty()) return fail(NUT_ERR_UNSUPPORTED, "scalar subqueries execute in single-table plans");
+  if (!p->subs.empty()) {  // scalar subqueries first, over the FROM table (left)
+    nut_plan q;
+    nut_status st = resolve_subqueries(*p, q, [&](const nut_plan *sp, nut_result **r) {
+      return nut_plan_execute(c, sp, left, nleft, lrows, 1, r);
+    });
+    return st ? st : nut_plan_execute2(c, &q, left, nleft, lrows, right, nright, rrows, group_hint, out);
+  }
   if (p->jn.size() == 1) {  // one JOIN run as a chain step (ON filters, EXISTS / IN)
     const nut_column *tabs[2] = {left, right};
     const int nc[2] = {nleft, nright};
@@ -458,7 +465,13 @@ nut_status nut_plan_executen(nut_ctx *c, const nut_plan *p, const nut_column *co
       return nut_plan_execute2(c, p, tables[0], ncols[0], nrows[0], tables[1], ncols[1], nrows[1], group_hint, out);
     return fail(NUT_ERR_INVALID_ARG, "nut_plan_executen: the plan joins fewer tables");
   }
-  if (!p->subs.empty()) return fail(NUT_ERR_UNSUPPORTED, "scalar subqueries execute in single-table plans");
+  if (!p->subs.empty()) {  // scalar subqueries first, over the FROM table (table 0)
+    nut_plan q;
+    nut_status st = resolve_subqueries(*p, q, [&](const nut_plan *sp, nut_result **r) {
+      return nut_plan_execute(c, sp, tables[0], ncols[0], nrows[0], 1, r);
+    });
+    return st ? st : nut_plan_executen(c, &q, tables, ncols, nrows, ntables, group_hint, out);
+  }
   *out = nullptr;
   DeviceGuard g(c->device);
   std::deque<HostStage> hs(ntables);
@@ -628,7 +641,13 @@ nut_status nut_table_execute2(nut_ctx *c, nut_table *left, nut_table *right, con
     nut_table *const tabs[2] = {left, right};
     return nut_table_executen(c, tabs, 2, p, group_hint, out);
   }
-  if (!p->subs.empty()) return fail(NUT_ERR_UNSUPPORTED, "scalar subqueries execute in single-table plans");
+  if (!p->subs.empty()) {  // scalar subqueries first, over the FROM table (left)
+    nut_plan q;
+    nut_status st = resolve_subqueries(*p, q, [&](const nut_plan *sp, nut_result **r) {
+      return nut_table_execute(c, left, sp, 1, r);
+    });
+    return st ? st : nut_table_execute2(c, left, right, &q, group_hint, out);
+  }
   *out = nullptr;
   std::vector<nut_column> cols[2];
   std::vector<const Dict *> dicts[2];
@@ -691,7 +710,13 @@ nut_status nut_table_executen(nut_ctx *c, nut_table *const *tables, int ntables,
     if (ntables == 2) return nut_table_execute2(c, tables[0], tables[1], p, group_hint, out);
     return fail(NUT_ERR_INVALID_ARG, "nut_table_executen: the plan joins fewer tables");
   }
-  if (!p->subs.empty()) return fail(NUT_ERR_UNSUPPORTED, "scalar subqueries execute in single-table plans");
+  if (!p->subs.empty()) {  // scalar subqueries first, over the FROM table (table 0)
+    nut_plan q;
+    nut_status st = resolve_subqueries(*p, q, [&](const nut_plan *sp, nut_result **r) {
+      return nut_table_execute(c, tables[0], sp, 1, r);
+    });
+    return st ? st : nut_table_executen(c, tables, ntables, &q, group_hint, out);
+  }
   *out = nullptr;
   std::vector<std::vector<nut_column>> cols(ntables);
   std::vector<std::vector<const Dict *>> dicts(ntables);

@@ -10,7 +10,9 @@
 #include <algorithm>
 #include <deque>
 #include <functional>
+#include <map>
 #include <memory>
+#include <tuple>
 
 #include "common.hpp"
 #include "sort.hpp"
@@ -55,7 +57,7 @@ struct PNode {
   int op = NUT_P_I64;
   int col = -1;  // NUT_P_COL: plan column
   CVal c;        // NUT_P_I64 / NUT_P_F64 constant
-  int arg = 0;   // NUT_P_DATEPART: nut_date_part
+  int arg = 0;   // NUT_P_DATEPART: nut_date_part; P_SUBSTR: the 1-based byte offset
 };
 using PProg = std::vector<PNode>;
 
@@ -209,8 +211,12 @@ namespace nut {
 namespace plan {
 
 // internal program leaves (never reach nut_prog): `col [I]LIKE 'pattern'` over a
-// dictionary column, lowered at execution to COL + LOOKUP in a per-code match table
-constexpr int P_LIKE = 1000, P_ILIKE = 1001;
+// dictionary column, lowered at execution to COL + LOOKUP in a per-code match table;
+// `substring(col, arg, c.v)` over one (c.v = kHuge: to the end), lowered at execution to
+// COL + MAP from the column's codes to its substrings' codes in the same dictionary
+constexpr int P_LIKE = 1000, P_ILIKE = 1001, P_SUBSTR = 1002;
+// a node that reads its plan column (col)
+inline bool reads_col(int op) { return op == NUT_P_COL || op == P_LIKE || op == P_ILIKE || op == P_SUBSTR; }
 // ------------------------------------------------------------------ predicate resolution
 enum Verdict { V_PRED, V_TRUE, V_FALSE };
 // a query-lifetime device buffer: stream-ordered (hipMallocAsync on the context's stream,
@@ -347,6 +353,11 @@ HVal having_val(const HNode &h, const std::vector<std::vector<uint64_t>> &cols, 
 bool having_true(const HNode &h, const std::vector<std::vector<uint64_t>> &cols, const std::vector<int> &types,
                  uint64_t g);
 nut_status check_strings(const nut_plan &p, const PProg &pp, const Dict *const *dicts, const char *what);
+// the plan column whose dictionary decodes GROUP BY key j (a plain string column, or one
+// substring of it), else -1
+int key_dict_col(const nut_plan &p, size_t j);
+// substring(s, off, len) with ClickHouse's byte semantics (P_SUBSTR)
+std::string substr_bytes(const std::string &s, int off, i128 len);
 
 // ---- groupby
 nut_prog and_prog(const nut_prog &a, const nut_prog &b, ProgStore &store);

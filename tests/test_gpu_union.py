@@ -107,4 +107,4 @@ def test_union_all_type_mismatch_is_a_plan_error(ex):
     a = torch.arange(10, dtype=torch.int64, device=ex.device)
     f = torch.arange(10, dtype=torch.float64, device=ex.device)
     with pytest.raises(NutError, match="UNION ALL: column 1"):
-        Plan("select a from t union all select f from u").execute_tables(ex, [{"a": a}, {"f": f}])
+        Plan("select sum(a) from t union all select sum(f) from u").execute_tables(ex, [{"a": a}, {"f": f}])

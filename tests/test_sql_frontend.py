@@ -603,3 +603,30 @@ def test_plan_union_all_and_view_body():
                       ("select a from t join u on t.x = u.x union all select a from v", "over one table")]:
         with pytest.raises(NutError, match=frag):
             Plan(sql)
+
+
+def test_plan_substring_dictionary_function():
+    """substring(col, off[, len]) over a string column (fixture 9, TPC-H Q22): a dictionary
+    function leaf of the program, in WHERE, as a GROUP BY key and as a projection; string
+    constants compared with it bind to its column's dictionary."""
+    d = Plan((SQL_DIR / "9.sql").read_text()).describe()
+    assert d["keys"] == ["substring(c_phone, 1, 2)"] and d["outputs"][0]["name"] == "cntrycode"
+    assert "(substring(c_phone, 1, 2) = '13')" in d["where_expr"] and "$subquery0" in d["where_expr"]
+    assert [j["type"] for j in d["joins"]] == ["anti"] and d["joins"][0]["table"] == "orders"
+    assert "substring(c_phone, 1, 2)" in d["subqueries"][0]["where_expr"]
+    d = Plan("select substr(s, -3) as t, count(*) from tb group by t order by t").describe()
+    assert d["keys"] == ["substr(s, -3)"]  # (the key as written)
+    d = Plan("select mid(s, 2, 4) from tb where substring(s, 1, 1) in ('a', 'b')").describe()
+    assert "substring(s, 1, 1) = 'a'" in d["where_expr"]
+
+
+@pytest.mark.parametrize("sql", [
+    "select substring(s, x) from tb",
+    "select substring(s + 1, 1) from tb",
+    "select substring(s, 1, y) from tb",
+    "select substring(s, 1.5) from tb",
+])
+def test_plan_substring_errors(sql):
+    with pytest.raises(NutError) as e:
+        Plan(sql)
+    assert e.value.status == 7 and "substring takes a string column and integer constants" in str(e.value)
