@@ -683,6 +683,7 @@ def main():
     gb_stats = ex.groupby_stats() if nd is None and args.workload in ("q1", "groupby", "q12expr", "q12join") else None
     if gb_stats is not None and gb_stats["path"] == "partitioned_ordered":
         gb_stats["overflow_rows"] = ex.groupby_overflow_rows()
+        gb_stats["heavy_keys"], gb_stats["heavy_rows"] = ex.groupby_heavy()
     if nd is not None:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -112,6 +112,9 @@ typedef enum {
   NUT_GB_DECLINE_TABLE = 5       /* a partition held more groups than its table */
 } nut_gb_decline;
 nut_status nut_ctx_groupby_overflow(nut_ctx *ctx, uint64_t *rows, uint32_t *declined);
+/* The last ordered nut_groupby_to_host's heavy-key split (NUT_OPT_GB_HEAVY): how many keys
+ * were aggregated in the streaming pass before the partition levels, and their rows. */
+nut_status nut_ctx_groupby_heavy(nut_ctx *ctx, uint32_t *keys, uint64_t *rows);
 /* The compiled Q1 kernel's launch shape on this context's device (NUT_OPT_PRIV_PROBE):
  * threads per workgroup and workgroups per CU the next launch takes, and the probe's best
  * kernel time per candidate shape {192 x 2, 128 x 3, 128 x 4} in ms (-1: not probed in
@@ -143,7 +146,8 @@ typedef enum {
   NUT_OPT_SORT_BD = 18,        /* sort, capped scatter levels: threads per workgroup 1024 (0, default) or 512 (two per CU) */
   NUT_OPT_GB_ORDERED = 19,     /* nut_groupby_to_host: the range-partitioned ordered path where it applies (1, default) or the hashed path + ordering (0) */
   NUT_OPT_PRIV_PROBE = 20,     /* 1 (default): the first compiled-Q1-shape group-by of >= 2^27 rows on a device times the kernel at 192 x 2, 128 x 3 and 128 x 4 threads x workgroups per CU on its first 2^28 rows (discarded) and keeps the fastest for that device (nut_ctx_priv_shape); 0: 192 x 2 */
-  NUT_OPT_COUNT = 21
+  NUT_OPT_GB_HEAVY = 21,       /* nut_groupby_to_host, ordered path: 1 (default) = keys the sample sees often (>= 5 % of it together) are aggregated in one streaming pass and split off before the partition levels; 0 = they take the overflow arenas */
+  NUT_OPT_COUNT = 22
 } nut_option;
 nut_status nut_ctx_set_option(nut_ctx *ctx, int option, int64_t value);
 nut_status nut_ctx_get_option(nut_ctx *ctx, int option, int64_t *value);

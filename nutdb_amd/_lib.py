@@ -135,6 +135,7 @@ SIGNATURES = {
     "nut_ctx_sort_stats": (_I32, [_P, C.POINTER(_U64), C.POINTER(C.c_uint32)]),
     "nut_ctx_groupby_stats": (_I32, [_P, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
     "nut_ctx_groupby_overflow": (_I32, [_P, C.POINTER(_U64), C.POINTER(C.c_uint32)]),
+    "nut_ctx_groupby_heavy": (_I32, [_P, C.POINTER(C.c_uint32), C.POINTER(_U64)]),
     "nut_ctx_priv_shape": (_I32, [_P, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_double)]),
     "nut_ctx_set_option": (_I32, [_P, _I32, _I64]),
     "nut_ctx_get_option": (_I32, [_P, _I32, C.POINTER(_I64)]),

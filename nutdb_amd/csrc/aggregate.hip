@@ -11,6 +11,7 @@
 
 #include "agg_kernel.hpp"
 #include "gpart.hpp"
+#include "heavy.hpp"
 #include "sort.hpp"
 #include "jit.hpp"
 #include "select_kernel.hpp"
@@ -1058,6 +1059,8 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
   const double lam = (double)group_hint / (double)(1 << (bits0 + bits1));
   c->gb_overflow_rows = 0;
   c->gb_decline = 0;
+  c->gb_heavy_keys = 0;
+  c->gb_heavy_rows = 0;
   // every NUT_ERR_UNSUPPORTED names its reason (nut_ctx_groupby_overflow): the caller then
   // runs the hashed path, with the same result
   auto decline = [c](uint32_t why) {
@@ -1156,11 +1159,91 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
     ~FreeArena() { (void)hipFreeAsync(p, s); }
   } free_arena{darena, st};
   NUT_HIP(hipMemsetAsync(darena, 0, 16, st));
+  // ---- heavy keys (heavy.hpp): a key the sample saw >= 3 times (>= ~1/22000 of the rows,
+  // more than a level-1 partition's share) would overflow its partition.  When such keys
+  // hold >= 5 % of the sample, the <= HK_MAX most frequent are aggregated in one streaming
+  // pass and the other rows, compacted into B2, are what the levels partition.
+  std::vector<int64_t> hkeys;
+  if (c->opt[NUT_OPT_GB_HEAVY] != 0) {
+    std::vector<int64_t> ss(smp);
+    std::sort(ss.begin(), ss.end());
+    std::vector<std::pair<uint32_t, int64_t>> cand;  // (sample count, key)
+    for (size_t i = 0; i < ss.size();) {
+      size_t j = i;
+      while (j < ss.size() && ss[j] == ss[i]) ++j;
+      if (j - i >= 3) cand.emplace_back((uint32_t)(j - i), ss[i]);
+      i = j;
+    }
+    std::sort(cand.begin(), cand.end(), [](const auto &x, const auto &y) { return x.first > y.first; });
+    const size_t hmax = std::min<size_t>(HK_MAX, HK_WORDS / na);
+    if (cand.size() > hmax) cand.resize(hmax);
+    uint64_t cover = 0;
+    for (const auto &x : cand) cover += x.first;
+    if (cover * 20 >= kSample) {
+      for (const auto &x : cand) hkeys.push_back(x.second);
+      std::sort(hkeys.begin(), hkeys.end());
+    }
+  }
+  uint64_t n0 = n;  // the rows the partition levels read
+  unsigned long long *dheavy = nullptr;  // [cursor, keys (h), aggregates (h x na)]
+  struct FreeHeavy {
+    unsigned long long *p = nullptr;
+    hipStream_t s;
+    ~FreeHeavy() {
+      if (p) (void)hipFreeAsync(p, s);
+    }
+  } free_heavy{nullptr, st};
+  const uint32_t nh = (uint32_t)hkeys.size();
+  if (nh) {
+    std::vector<uint64_t> init(1 + nh + (size_t)nh * na, 0);
+    memcpy(&init[1], hkeys.data(), (size_t)nh * 8);
+    for (uint32_t j = 0; j < nh; ++j)
+      for (int a = 0; a < na; ++a) init[1 + nh + (size_t)j * na + a] = agg_init(g->kinds[a]);
+    NUT_HIP(hipMallocAsync((void **)&dheavy, init.size() * 8, st));
+    free_heavy.p = dheavy;
+    NUT_HIP(hipMemcpyAsync(dheavy, init.data(), init.size() * 8, hipMemcpyHostToDevice, st));
+    HkArgs ha{};
+    ha.key = src[1];
+    ha.okey = B2[1];
+    ha.nv = nv;
+    for (int j = 0; j < NUT_MAX_VALS; ++j)
+      if (vmap[j] >= 0) {
+        ha.val[vmap[j]] = src[3 + vmap[j]];
+        ha.oval[vmap[j]] = B2[3 + vmap[j]];
+      }
+    ha.n = n;
+    ha.na = na;
+    for (int a = 0; a < na; ++a) {
+      ha.kind[a] = g->kinds[a];
+      ha.arg[a] = s->agg_op[a] == NUT_AGG_COUNT ? 0 : vmap[s->agg_arg[a][0]];
+    }
+    ha.hk = (const int64_t *)dheavy + 1;
+    ha.h = nh;
+    ha.hagg = (uint64_t *)dheavy + 1 + nh;
+    ha.cursor = dheavy;
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, hk_split_kernel, HK_THREADS, 0) != hipSuccess || per_cu < 1)
+      per_cu = 1;
+    const uint64_t ntiles = (n + HK_TILE - 1) / HK_TILE;
+    c->timer.begin(st, NUT_KERNEL_AGGREGATE);
+    hipLaunchKernelGGL(hk_split_kernel, dim3((unsigned)std::min<uint64_t>(ntiles, (uint64_t)c->num_cus * per_cu)),
+                       dim3(HK_THREADS), 0, st, ha);
+    c->timer.end(st);
+    NUT_HIP(hipGetLastError());
+    NUT_HIP(hipMemcpyAsync(c->host_pinned, dheavy, 8, hipMemcpyDeviceToHost, st));
+    NUT_HIP(hipStreamSynchronize(st));
+    n0 = c->host_pinned[0];
+    src[1] = B2[1];
+    for (int j = 0; j < NUT_MAX_VALS; ++j)
+      if (vmap[j] >= 0) src[3 + vmap[j]] = B2[3 + vmap[j]];
+  }
+  c->gb_heavy_keys = nh;
+  c->gb_heavy_rows = n - n0;
   // ---- level 0 (range digit = cell >> bits1): 1.5 x the even share per partition, the rest
   // of O (~n / 2 rows) its arena
   const uint64_t ocap = ((3 * rows / 2) >> bits0) & ~1ull;
   const uint64_t abase0 = ocap << bits0, acap0 = 2 * rows - abase0 - 2 * GP_TILE;
-  std::vector<GpSeg> segs{GpSeg{0, n, 0, 0}};
+  std::vector<GpSeg> segs{GpSeg{0, n0, 0, 0}};
   segs[0].ocap = ocap;
   std::vector<uint64_t> hist, p0;
   c->timer.begin(st, NUT_KERNEL_AGGREGATE);
@@ -1397,6 +1480,15 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
     if (e) return e;
     done = fold_sorted_groups(keys_h, aggs_h, done, cap, hk, hw, g->kinds, na, &over);
   }
+  if (nh && !over) {  // the heavy keys' groups (result words: f64 MIN / MAX back from the table order)
+    std::vector<uint64_t> hw((size_t)nh * na);
+    NUT_HIP(hipMemcpyAsync(hw.data(), dheavy + 1 + nh, hw.size() * 8, hipMemcpyDeviceToHost, st));
+    NUT_HIP(hipStreamSynchronize(st));
+    for (uint32_t j = 0; j < nh; ++j)
+      for (int a = 0; a < na; ++a)
+        if (g->kinds[a] == AK_MIN_F64 || g->kinds[a] == AK_MAX_F64) hw[(size_t)j * na + a] = ord_to_f64(hw[(size_t)j * na + a]);
+    done = fold_sorted_groups(keys_h, aggs_h, done, cap, hkeys, hw, g->kinds, na, &over);
+  }
   *n_out = done;
   if (over) return fail(NUT_ERR_CAPACITY, "nut_groupby_to_host: capacity " + std::to_string(cap) + " < " +
                                               std::to_string(done) + " groups");
@@ -1584,6 +1676,13 @@ nut_status nut_ctx_groupby_overflow(nut_ctx *c, uint64_t *rows, uint32_t *declin
   if (!c) return fail(NUT_ERR_INVALID_ARG, "nut_ctx_groupby_overflow: NULL context");
   if (rows) *rows = c->gb_overflow_rows;
   if (declined) *declined = c->gb_decline;
+  return NUT_OK;
+}
+
+nut_status nut_ctx_groupby_heavy(nut_ctx *c, uint32_t *keys, uint64_t *rows) {
+  if (!c) return fail(NUT_ERR_INVALID_ARG, "nut_ctx_groupby_heavy: NULL context");
+  if (keys) *keys = c->gb_heavy_keys;
+  if (rows) *rows = c->gb_heavy_rows;
   return NUT_OK;
 }
 

@@ -360,7 +360,7 @@ class Executor:
                "gb_dense": 9, "gb_l1_bits": 10,
                "topk": 11, "gb_l0_bits": 12, "stream_blocks": 13,
                "priv_bd": 14, "priv_blocks": 15, "agg_blocks": 16, "sel_blocks": 17, "sort_bd": 18,
-               "gb_ordered": 19, "priv_probe": 20}
+               "gb_ordered": 19, "priv_probe": 20, "gb_heavy": 21}
 
     def groupby_stats(self) -> dict:
         """The algorithm the last group-by on this context took (nut_ctx_groupby_stats)."""
@@ -377,6 +377,13 @@ class Executor:
         r, d = C.c_uint64(), C.c_uint32()
         check(lib.nut_ctx_groupby_overflow(self.ctx, C.byref(r), C.byref(d)), "nut_ctx_groupby_overflow")
         return r.value
+
+    def groupby_heavy(self) -> tuple:
+        """(keys, rows) the last ordered groupby_to_host aggregated in its heavy-key pass
+        before the partition levels (nut_ctx_groupby_heavy)."""
+        k, r = C.c_uint32(), C.c_uint64()
+        check(lib.nut_ctx_groupby_heavy(self.ctx, C.byref(k), C.byref(r)), "nut_ctx_groupby_heavy")
+        return k.value, r.value
 
     def groupby_declined(self) -> str:
         """Why the last groupby_to_host left the ordered path ("none" if it did not)."""

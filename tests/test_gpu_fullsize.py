@@ -113,8 +113,9 @@ def test_groupby_full_config3_large_groups(ex, orc, G, levels):
 def test_groupby_full_config3_ordered_to_host(ex, orc, skew):
     """Config 3 at G = 1e7 as the bench runs it (nut_groupby_to_host, the key-range ordered
     path) on 1e9 rows: uniform pool keys, and Zipf-like keys (GEN_SKEW_KEY: pool index i on
-    ~1/i of the rows, the top key ~6 %) whose heavy keys overflow their capped partitions
-    into the arenas — both bit-exact against the indexed oracle, both on the ordered path."""
+    ~1/i of the rows, the top key ~6 %) whose frequent keys go through the heavy-key pass
+    before the partition levels (heavy.hpp) — both bit-exact against the indexed oracle,
+    both on the ordered path."""
     import torch
     from nutdb_amd import Agg, AggQuery
     from nutdb_amd import _lib as L
@@ -126,11 +127,11 @@ def test_groupby_full_config3_ordered_to_host(ex, orc, skew):
     q = AggQuery(keys=[key], values=[val], aggs=[Agg("sum", "col", (0,)), Agg("count"), Agg("min", "col", (0,)),
                                                    Agg("max", "col", (0,))])
     gk, gw = ex.groupby_to_host(q, group_hint=G, out=out)
-    st, ovf = ex.groupby_stats(), ex.groupby_overflow_rows()
+    st, hv = ex.groupby_stats(), ex.groupby_heavy()
     gk, gw = gk.copy(), gw.copy()
     del key, val, out
     assert st["path"] == "partitioned_ordered", st
-    assert (ovf > 0) == skew, ovf
+    assert (hv[1] > n // 4) == skew and (hv[0] > 0) == skew, hv
     ok, ow = orc.groupby_pool_dyadic(G, n, key_seed=GB_KEY_SEED, val_seed=GB_VAL_SEED,
                                      kind=L.GEN_SKEW_KEY if skew else L.GEN_POOL_KEY)
     gc.collect()

@@ -4,7 +4,9 @@ host arrays chunk by chunk — must return exactly what nut_groupby + nut_groups
 return (the hashed path + device ordering), and the oracle's groups: keys, counts, MIN /
 MAX bit-exact, f64 sums within F64_SUM_RTOL (exact for dyadic values).  Shapes it does not
 take (clustered keys, pageable outputs, the option off) fall back and give the same result;
-heavy keys stay on it through the overflow arenas."""
+heavy keys stay on it: keys the sample sees often (together >= 5 % of it) are aggregated in
+the heavy-key pass before the partition levels (heavy.hpp), the excess of the others goes
+through the overflow arenas."""
 import numpy as np
 import pytest
 import torch
@@ -90,7 +92,29 @@ def test_ordered_extreme_keys(ex, orc):
     q = gb_query(dev(key, ex), dev(val, ex))
     k, w, path = run_to_host(ex, q, G)
     assert path == "partitioned_ordered"
-    assert ex.groupby_overflow_rows() > 0
+    assert ex.groupby_overflow_rows() > 0 and ex.groupby_heavy() == (0, 0)
+    ok, ow = orc.groupby([key], AGGS4, values=[val])
+    _, absum = orc.groupby([key], [(0, 0, (0,))], values=[np.abs(val)])
+    check_signed(k, w, ok, ow, absum)
+    assert k[0, 0] == I64_MIN and k[-1, 0] == I64_MAX
+
+
+def test_ordered_extreme_heavy_keys(ex, orc):
+    """INT64_MIN and INT64_MAX on 4 % of the rows each, signed values: both go through the
+    heavy-key pass (INT64_MIN is the hash tables' empty marker; the pass's set indexes its
+    keys instead), the rest through the levels."""
+    rng = np.random.default_rng(17)
+    pool = rng.integers(I64_MIN, I64_MAX, 2_000_000, dtype=np.int64)
+    key = pool[rng.integers(0, len(pool), N)]
+    key[::25] = I64_MIN
+    key[1::25] = I64_MAX
+    val = rng.standard_normal(N)
+    val[::97] = -0.0
+    q = gb_query(dev(key, ex), dev(val, ex))
+    k, w, path = run_to_host(ex, q, len(np.unique(key)))
+    assert path == "partitioned_ordered"
+    hk, hr = ex.groupby_heavy()
+    assert hk >= 2 and hr >= 2 * (N // 25)
     ok, ow = orc.groupby([key], AGGS4, values=[val])
     _, absum = orc.groupby([key], [(0, 0, (0,))], values=[np.abs(val)])
     check_signed(k, w, ok, ow, absum)
@@ -101,8 +125,9 @@ def test_ordered_extreme_keys(ex, orc):
 def test_ordered_heavy_key(ex, orc, share):
     """One key on `share` of the rows: 0.3 % passes level 0 and overflows its level-1 region
     (ADVICE r4: the aggregation must not read past the region, and the result must hold);
-    2 % and 10 % overflow level 0 too.  The excess is aggregated from the arenas and folded
-    into the ordered result — same groups as the oracle, ordered path kept."""
+    2 % overflows level 0 too — their excess is aggregated from the arenas and folded into
+    the ordered result; 10 % (>= 5 % of the sample) goes through the heavy-key pass.  Same
+    groups as the oracle, ordered path kept."""
     G = 2_000_000
     key = orc.gen_column(2, 0x6A, N, a=G)
     rng = np.random.default_rng(11)
@@ -112,15 +137,22 @@ def test_ordered_heavy_key(ex, orc, share):
     q = gb_query(dev(key, ex), dev(val, ex))
     k, w, path = run_to_host(ex, q, G)
     assert path == "partitioned_ordered"
-    assert ex.groupby_overflow_rows() > 0
+    if share >= 0.05:
+        assert ex.groupby_heavy() == (1, int((key == key[12345]).sum()))
+    else:
+        assert ex.groupby_overflow_rows() > 0 and ex.groupby_heavy() == (0, 0)
     ok, ow = orc.groupby([key], AGGS4, values=[val])
     check(k, w, ok, ow, sums_exact=True)
 
 
-def test_ordered_skew_generator(ex, orc):
+@pytest.mark.parametrize("heavy_pass", [1, 0])
+def test_ordered_skew_generator(ex, orc, opts, heavy_pass):
     """Zipf-like keys (GEN_SKEW_KEY: pool index i on ~1/i of the rows, the top key ~6 %)
-    on the ordered path vs the indexed oracle of the same generator."""
+    on the ordered path vs the indexed oracle of the same generator: with the heavy-key pass
+    (the default: the sample's frequent keys aggregated before the levels) and without it
+    (their excess through the overflow arenas)."""
     from nutdb_amd import _lib as L
+    opts(gb_heavy=heavy_pass)
     G = 4_000_000
     key = ex.gen_column(L.GEN_SKEW_KEY, 0x51, N, a=G)
     val = ex.gen_column(L.GEN_DYADIC, 0x52, N)
@@ -129,7 +161,11 @@ def test_ordered_skew_generator(ex, orc):
     k, w, path = run_to_host(ex, q, hint)
     ok, ow = orc.groupby_pool_dyadic(G, N, key_seed=0x51, val_seed=0x52, kind=7)
     assert path == "partitioned_ordered"
-    assert ex.groupby_overflow_rows() > 0
+    hk, hr = ex.groupby_heavy()
+    if heavy_pass:
+        assert hk > 100 and hr > N // 4
+    else:
+        assert (hk, hr) == (0, 0) and ex.groupby_overflow_rows() > 0
     assert np.array_equal(k, ok) and np.array_equal(w.view(np.uint64), ow)
 
 
