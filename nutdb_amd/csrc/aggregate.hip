@@ -564,7 +564,7 @@ uint32_t gp_tiles(std::vector<GpSeg> &segs, uint32_t tile, std::vector<uint32_t>
 void gp_capped_launch(nut_ctx *c, const GpArrays &ar, const GpSeg *dseg, const uint32_t *dts, uint32_t nst, int shift,
                       unsigned long long *dcur, uint64_t kx, uint64_t ovf, unsigned long long *dflag, int bits,
                       bool two_keys, const GpRange *rg, unsigned long long *acur = nullptr, uint64_t acap = 0,
-                      unsigned long long *acut = nullptr) {
+                      unsigned long long *acut = nullptr, int gather = 0) {
   if (!nst) return;
   const unsigned grid = std::min<unsigned>(nst, (unsigned)c->num_cus);
   using SK = void (*)(GpArrays, const GpSeg *, const uint32_t *, uint32_t, int, int, unsigned long long *, uint64_t,
@@ -575,8 +575,8 @@ void gp_capped_launch(nut_ctx *c, const GpArrays &ar, const GpSeg *dseg, const u
       {gp_scatter_kernel<1, 1024, 1, 6, true>, gp_scatter_kernel<1, 1024, 1, 7, true>,
        gp_scatter_kernel<1, 1024, 1, 8, true>}};
   const int kv = rg ? 2 : two_keys ? 1 : 0;
-  hipLaunchKernelGGL(kern[kv][bits - 6], dim3(grid), dim3(1024), 0, c->stream, ar, dseg, dts, nst, shift, 0, dcur, kx,
-                     ovf, dflag, rg ? *rg : GpRange{}, acur, acap, acut);
+  hipLaunchKernelGGL(kern[kv][bits - 6], dim3(grid), dim3(1024), 0, c->stream, ar, dseg, dts, nst, shift, gather, dcur,
+                     kx, ovf, dflag, rg ? *rg : GpRange{}, acur, acap, acut);
 }
 
 // one partition level: histogram + scatter of every segment; returns the 256 counts per
@@ -603,15 +603,19 @@ nut_status gp_level(nut_ctx *c, GpMeta &mm, std::vector<GpSeg> &segs, int shift,
     // (no message) if a digit outgrew its rows: nothing is usable, partition again with a
     // histogram.  With an overflow arena (acur) an overflowing run goes there instead and
     // its digit's rows end at the first such run (see gp_scatter_kernel).
-    // (bits: the digit width of this level, 6..8)
-    if (gather || have_hist || !parts || bits < 6 || bits > 8)
+    // (bits: the digit width of this level, 6..8).  Gather: every segment scatters into
+    // segment 0's regions (the segments must name the same obase / ocap).
+    if (have_hist || !parts || bits < 6 || bits > 8)
       return fail(NUT_ERR_INVALID_ARG, "gp_level: capped layout needs parts");
     const int nb = 1 << bits;
-    const size_t nc = segs.size() * nb;
+    const size_t nc = nh * nb;
     std::vector<uint64_t> cur(nc + 1, 0);  // + the overflow flag
     for (size_t i = 0; i < segs.size(); ++i) {
       if ((segs[i].obase | segs[i].ocap) & 1) return fail(NUT_ERR_INVALID_ARG, "gp_level: odd capped region");
-      for (int d = 0; d < nb; ++d) cur[i * nb + d] = segs[i].obase + (uint64_t)d * segs[i].ocap;
+      if (gather && (segs[i].obase != segs[0].obase || segs[i].ocap != segs[0].ocap))
+        return fail(NUT_ERR_INVALID_ARG, "gp_level: gathered capped segments name different regions");
+      if (i < nh)
+        for (int d = 0; d < nb; ++d) cur[i * nb + d] = segs[i].obase + (uint64_t)d * segs[i].ocap;
     }
     const uint32_t nst = gp_tiles(segs, 2 * GP_TILE, ts);
     s = mm.begin(GpMeta::al(segs.size() * sizeof(GpSeg)) + GpMeta::al(ts.size() * 4 + 1) + GpMeta::al(cur.size() * 8) +
@@ -632,7 +636,7 @@ nut_status gp_level(nut_ctx *c, GpMeta &mm, std::vector<GpSeg> &segs, int shift,
     ar.narr = narr;
     unsigned long long *dflag = (unsigned long long *)dcur + nc;
     gp_capped_launch(c, ar, dseg, dts, nst, shift, (unsigned long long *)dcur, kx, ovf, dflag, bits, src[2] != nullptr,
-                     rg, acur, acap, dcut);
+                     rg, acur, acap, dcut, gather ? 1 : 0);
     NUT_HIP(hipGetLastError());
     std::vector<uint64_t> back(cur.size()), cut(dcut ? nc : 0);
     NUT_HIP(hipMemcpyAsync(back.data(), dcur, back.size() * 8, hipMemcpyDeviceToHost, st));
@@ -979,8 +983,8 @@ bool host_pinned_ptr(const void *p) {
 // Fold groups sorted by key (hk, hw: result words, SELECT order) into a sorted host result
 // of n groups with room for cap: equal keys combine by kind (SUM f64 adds, SUM i64 / COUNT
 // wrap-add, MIN / MAX of f64 in the tables' total order: -0 < +0, NaN above +inf), the rest
-// are merged in by one backward pass.  Returns the new count; *over when it exceeds cap
-// (the result is then left as it was).
+// are merged in by one backward pass of block moves.  Returns the new count; *over when it
+// exceeds cap (the caller then fails the call: equal keys may already be combined).
 static uint64_t fold_sorted_groups(int64_t *keys, uint64_t *aggs, uint64_t n, uint64_t cap,
                                    const std::vector<int64_t> &hk, const std::vector<uint64_t> &hw,
                                    const int32_t *kinds, int na, bool *over) {
@@ -1007,36 +1011,40 @@ static uint64_t fold_sorted_groups(int64_t *keys, uint64_t *aggs, uint64_t n, ui
       }
     }
   };
-  uint64_t fresh = 0;  // keys not in the result yet
-  for (uint64_t i = 0, j = 0; j < m;) {
-    if (i < n && keys[i] < hk[j]) {
-      ++i;
-    } else if (i < n && keys[i] == hk[j]) {
-      ++i, ++j;
+  // each incoming key's place (hk ascending: a galloping search from the previous place, so
+  // dense and sparse folds both stay near linear), equal keys combined in place; only the
+  // keys not in the result yet move anything
+  std::vector<uint64_t> pos;
+  std::vector<uint32_t> fresh_j;
+  uint64_t lo = 0;
+  for (uint64_t j = 0; j < m; ++j) {
+    uint64_t step = 1;
+    while (lo + step < n && keys[lo + step] < hk[j]) step *= 2;
+    lo = (uint64_t)(std::lower_bound(keys + lo + step / 2, keys + std::min(n, lo + step + 1), hk[j]) - keys);
+    if (lo < n && keys[lo] == hk[j]) {
+      combine(aggs + lo * na, &hw[j * na]);
     } else {
-      ++fresh, ++j;
+      fresh_j.push_back((uint32_t)j);
+      pos.push_back(lo);
     }
   }
+  const uint64_t fresh = fresh_j.size();
   if (n + fresh > cap) {
     *over = true;
     return n + fresh;
   }
-  uint64_t i = n, j = m, w = n + fresh;  // backward merge: the write position never passes i
-  while (j > 0) {
-    if (i > 0 && keys[i - 1] > hk[j - 1]) {
-      --i, --w;
-      keys[w] = keys[i];
-      memmove(aggs + w * na, aggs + i * na, (size_t)na * 8);
-    } else if (i > 0 && keys[i - 1] == hk[j - 1]) {
-      --i, --j, --w;
-      keys[w] = keys[i];
-      memmove(aggs + w * na, aggs + i * na, (size_t)na * 8);
-      combine(aggs + w * na, &hw[j * na]);
-    } else {
-      --j, --w;
-      keys[w] = hk[j];
-      memcpy(aggs + w * na, &hw[j * na], (size_t)na * 8);
+  // backward: the block [p, end) of the rows after fresh key r's place moves up by the r + 1
+  // fresh keys at or before it, then the key goes in front of it
+  uint64_t end = n;
+  for (uint64_t r = fresh; r-- > 0;) {
+    const uint64_t p = pos[r], j = fresh_j[r];
+    if (end > p) {
+      memmove(keys + p + r + 1, keys + p, (end - p) * 8);
+      memmove(aggs + (p + r + 1) * na, aggs + p * na, (end - p) * 8 * (size_t)na);
     }
+    keys[p + r] = hk[j];
+    memcpy(aggs + (p + r) * na, &hw[j * na], (size_t)na * 8);
+    end = p;
   }
   return n + fresh;
 }
@@ -1159,8 +1167,8 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
     ~FreeArena() { (void)hipFreeAsync(p, s); }
   } free_arena{darena, st};
   NUT_HIP(hipMemsetAsync(darena, 0, 16, st));
-  // ---- heavy keys (heavy.hpp): a key the sample saw >= 3 times (>= ~1/22000 of the rows,
-  // more than a level-1 partition's share) would overflow its partition.  When such keys
+  // ---- heavy keys (heavy.hpp): a key the sample saw >= 4 times (>= ~1/16000 of the rows:
+  // a whole level-1 partition's share) would overflow its partition.  When such keys
   // hold >= 5 % of the sample, the <= HK_MAX most frequent are aggregated in one streaming
   // pass and the other rows, compacted into B2, are what the levels partition.
   std::vector<int64_t> hkeys;
@@ -1171,7 +1179,7 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
     for (size_t i = 0; i < ss.size();) {
       size_t j = i;
       while (j < ss.size() && ss[j] == ss[i]) ++j;
-      if (j - i >= 3) cand.emplace_back((uint32_t)(j - i), ss[i]);
+      if (j - i >= 4) cand.emplace_back((uint32_t)(j - i), ss[i]);
       i = j;
     }
     std::sort(cand.begin(), cand.end(), [](const auto &x, const auto &y) { return x.first > y.first; });
@@ -1185,7 +1193,9 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
     }
   }
   uint64_t n0 = n;  // the rows the partition levels read
-  unsigned long long *dheavy = nullptr;  // [cursor, keys (h), aggregates (h x na)]
+  std::vector<uint64_t> hcount;  // heavy pass: the rows each workgroup kept, at hchunk-row strides of B2
+  uint64_t hchunk = 0;
+  unsigned long long *dheavy = nullptr;
   struct FreeHeavy {
     unsigned long long *p = nullptr;
     hipStream_t s;
@@ -1195,10 +1205,17 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
   } free_heavy{nullptr, st};
   const uint32_t nh = (uint32_t)hkeys.size();
   if (nh) {
-    std::vector<uint64_t> init(1 + nh + (size_t)nh * na, 0);
-    memcpy(&init[1], hkeys.data(), (size_t)nh * 8);
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, hk_split_kernel, HK_THREADS, 0) != hipSuccess || per_cu < 1)
+      per_cu = 1;
+    const uint64_t ntiles = (n + HK_TILE - 1) / HK_TILE;
+    const uint64_t hgrid = std::min<uint64_t>(ntiles, (uint64_t)c->num_cus * per_cu);
+    const uint64_t chunk = (ntiles + hgrid - 1) / hgrid;
+    // [keys (h), aggregates (h x na), kept rows per workgroup (hgrid)]
+    std::vector<uint64_t> init(nh + (size_t)nh * na + hgrid, 0);
+    memcpy(&init[0], hkeys.data(), (size_t)nh * 8);
     for (uint32_t j = 0; j < nh; ++j)
-      for (int a = 0; a < na; ++a) init[1 + nh + (size_t)j * na + a] = agg_init(g->kinds[a]);
+      for (int a = 0; a < na; ++a) init[nh + (size_t)j * na + a] = agg_init(g->kinds[a]);
     NUT_HIP(hipMallocAsync((void **)&dheavy, init.size() * 8, st));
     free_heavy.p = dheavy;
     NUT_HIP(hipMemcpyAsync(dheavy, init.data(), init.size() * 8, hipMemcpyHostToDevice, st));
@@ -1217,22 +1234,21 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
       ha.kind[a] = g->kinds[a];
       ha.arg[a] = s->agg_op[a] == NUT_AGG_COUNT ? 0 : vmap[s->agg_arg[a][0]];
     }
-    ha.hk = (const int64_t *)dheavy + 1;
+    ha.hk = (const int64_t *)dheavy;
     ha.h = nh;
-    ha.hagg = (uint64_t *)dheavy + 1 + nh;
-    ha.cursor = dheavy;
-    int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, hk_split_kernel, HK_THREADS, 0) != hipSuccess || per_cu < 1)
-      per_cu = 1;
-    const uint64_t ntiles = (n + HK_TILE - 1) / HK_TILE;
+    ha.hagg = (uint64_t *)dheavy + nh;
+    ha.count = (uint64_t *)dheavy + nh + (size_t)nh * na;
+    ha.chunk = chunk;
     c->timer.begin(st, NUT_KERNEL_AGGREGATE);
-    hipLaunchKernelGGL(hk_split_kernel, dim3((unsigned)std::min<uint64_t>(ntiles, (uint64_t)c->num_cus * per_cu)),
-                       dim3(HK_THREADS), 0, st, ha);
+    hipLaunchKernelGGL(hk_split_kernel, dim3((unsigned)hgrid), dim3(HK_THREADS), 0, st, ha);
     c->timer.end(st);
     NUT_HIP(hipGetLastError());
-    NUT_HIP(hipMemcpyAsync(c->host_pinned, dheavy, 8, hipMemcpyDeviceToHost, st));
+    hcount.resize(hgrid);
+    NUT_HIP(hipMemcpyAsync(hcount.data(), ha.count, hgrid * 8, hipMemcpyDeviceToHost, st));
     NUT_HIP(hipStreamSynchronize(st));
-    n0 = c->host_pinned[0];
+    hchunk = chunk * HK_TILE;
+    n0 = 0;
+    for (uint64_t x : hcount) n0 += x;
     src[1] = B2[1];
     for (int j = 0; j < NUT_MAX_VALS; ++j)
       if (vmap[j] >= 0) src[3 + vmap[j]] = B2[3 + vmap[j]];
@@ -1243,11 +1259,19 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
   // of O (~n / 2 rows) its arena
   const uint64_t ocap = ((3 * rows / 2) >> bits0) & ~1ull;
   const uint64_t abase0 = ocap << bits0, acap0 = 2 * rows - abase0 - 2 * GP_TILE;
-  std::vector<GpSeg> segs{GpSeg{0, n0, 0, 0}};
-  segs[0].ocap = ocap;
+  std::vector<GpSeg> segs;
+  if (hcount.empty()) {
+    segs.push_back(GpSeg{0, n, 0, 0});
+  } else {  // the heavy pass's per-workgroup runs, gathered into one set of regions
+    for (size_t b = 0; b < hcount.size(); ++b)
+      if (hcount[b]) segs.push_back(GpSeg{b * hchunk, hcount[b], 0, 0});
+    if (segs.empty()) segs.push_back(GpSeg{0, 0, 0, 0});
+  }
+  for (GpSeg &sg : segs) sg.ocap = ocap;
   std::vector<uint64_t> hist, p0;
   c->timer.begin(st, NUT_KERNEL_AGGREGATE);
-  e = gp_level(c, mm, segs, bits1, src, O, narr, false, false, hist, &p0, 0, abase0, bits0, &rg, darena, acap0);
+  e = gp_level(c, mm, segs, bits1, src, O, narr, hcount.size() > 0, false, hist, &p0, 0, abase0, bits0, &rg, darena,
+               acap0);
   c->timer.end(st);
   if (e) return e == NUT_ERR_CAPACITY ? decline(NUT_GB_DECLINE_ARENA) : e;
   // ---- level-1 regions, as the hashed path sizes them
@@ -1317,11 +1341,29 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
   GpSeg *dseg;
   uint32_t *dts;
   uint64_t *dinit, *drend;
+  // each heavy key's partition (heavy pass): level-0 digit -> its index among the non-empty
+  // level-0 partitions (region d starts at row d * ocap), then the level-1 digit; -1: its
+  // level-0 partition holds no rows (the host folds that key's group)
+  std::vector<int64_t> hq(nh, -1);
+  if (nh) {
+    std::vector<int64_t> idx0((size_t)1 << bits0, -1);
+    for (uint32_t i = 0; i < np0; ++i) idx0[p0[2 * i] / ocap] = i;
+    for (uint32_t j = 0; j < nh; ++j) {
+      const uint32_t cell = rg.cell((uint64_t)hkeys[j]);
+      const int64_t i0 = idx0[cell >> bits1];
+      if (i0 >= 0) hq[j] = i0 * nb1 + (cell & (nb1 - 1));
+    }
+  }
   e = mm.begin(GpMeta::al(s2.size() * sizeof(GpSeg)) + GpMeta::al(tiles.size() * 4 + 1) + GpMeta::al(init.size() * 8) +
-               2 * GpMeta::al(init.size() * 8) + 4 * GpMeta::al(nparts * 8) + GpMeta::al(64));
+               2 * GpMeta::al(init.size() * 8) + 4 * GpMeta::al(nparts * 8) + GpMeta::al(64) +
+               2 * GpMeta::al((size_t)nh * 8 + 1));
   if (e) return e;
   if ((e = mm.up(s2, &dseg)) || (e = mm.up(tiles, &dts)) || (e = mm.up(init, &dinit)) || (e = mm.up(rend, &drend)))
     return e;
+  int64_t *dhq = nullptr;
+  if ((e = mm.up(hq, &dhq))) return e;
+  uint64_t *dmiss = (uint64_t *)mm.alloc((size_t)nh * 8 + 1);  // heavy keys whose partition's region was full
+  if (nh) NUT_HIP(hipMemsetAsync(dmiss, 0, (size_t)nh * 8, st));
   uint64_t *dend = (uint64_t *)mm.alloc(nparts * 8);  // partition ends, cut at their regions' ends
   unsigned long long *dcur = (unsigned long long *)mm.alloc(init.size() * 8);
   unsigned long long *dcount = (unsigned long long *)mm.alloc(nparts * 8);
@@ -1404,6 +1446,10 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
     nut_status e2 = launch_agg(g, &s3, per, g->kinds, &sg);
     c->stream = st;
     if (e2) return e2;
+    if (nh)  // the heavy keys' groups of this chunk's partitions join their regions before the ordering
+      hipLaunchKernelGGL(go_heavy_insert_kernel, dim3(1), dim3(1024), 0, ax, (const int64_t *)dheavy,
+                         (const uint64_t *)dheavy + nh, nh, na, (const int64_t *)dhq, q0, nq, dcount, g->gt.slot,
+                         g->gt.agg, g->gt.cap + 1, dregion, dmiss);
     c->timer.begin(ax, NUT_KERNEL_AGGREGATE);
     hipLaunchKernelGGL(go_scan_kernel, dim3(1), dim3(1024), 0, ax, (const unsigned long long *)dcount + q0, (uint32_t)nq,
                        doffs + q0, drun);
@@ -1480,14 +1526,24 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
     if (e) return e;
     done = fold_sorted_groups(keys_h, aggs_h, done, cap, hk, hw, g->kinds, na, &over);
   }
-  if (nh && !over) {  // the heavy keys' groups (result words: f64 MIN / MAX back from the table order)
-    std::vector<uint64_t> hw((size_t)nh * na);
-    NUT_HIP(hipMemcpyAsync(hw.data(), dheavy + 1 + nh, hw.size() * 8, hipMemcpyDeviceToHost, st));
+  if (nh && !over) {
+    // heavy keys that joined no region (their level-0 partition was empty, or the region
+    // was full): folded here (result words: f64 MIN / MAX back from the table order)
+    std::vector<uint64_t> miss(nh), hw((size_t)nh * na);
+    NUT_HIP(hipMemcpyAsync(miss.data(), dmiss, (size_t)nh * 8, hipMemcpyDeviceToHost, st));
+    NUT_HIP(hipMemcpyAsync(hw.data(), dheavy + nh, hw.size() * 8, hipMemcpyDeviceToHost, st));
     NUT_HIP(hipStreamSynchronize(st));
-    for (uint32_t j = 0; j < nh; ++j)
-      for (int a = 0; a < na; ++a)
-        if (g->kinds[a] == AK_MIN_F64 || g->kinds[a] == AK_MAX_F64) hw[(size_t)j * na + a] = ord_to_f64(hw[(size_t)j * na + a]);
-    done = fold_sorted_groups(keys_h, aggs_h, done, cap, hkeys, hw, g->kinds, na, &over);
+    std::vector<int64_t> fk;
+    std::vector<uint64_t> fw;
+    for (uint32_t j = 0; j < nh; ++j) {
+      if (hq[j] >= 0 && !miss[j]) continue;
+      fk.push_back(hkeys[j]);
+      for (int a = 0; a < na; ++a) {
+        const uint64_t x = hw[(size_t)j * na + a];
+        fw.push_back(g->kinds[a] == AK_MIN_F64 || g->kinds[a] == AK_MAX_F64 ? ord_to_f64(x) : x);
+      }
+    }
+    if (!fk.empty()) done = fold_sorted_groups(keys_h, aggs_h, done, cap, fk, fw, g->kinds, na, &over);
   }
   *n_out = done;
   if (over) return fail(NUT_ERR_CAPACITY, "nut_groupby_to_host: capacity " + std::to_string(cap) + " < " +

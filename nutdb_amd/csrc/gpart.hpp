@@ -326,6 +326,40 @@ __global__ void go_clamp_kernel(const unsigned long long *__restrict__ cursor, c
   if (q < n) end[q] = min((uint64_t)cursor[q], (uint64_t)cut[q]);
 }
 
+// The heavy-key pass's groups (heavy.hpp) into their partitions' dense regions after the
+// chunk's aggregation and before its ordering: hq[j] = heavy key j's partition (global
+// index; outside [q0, q0 + nq): another chunk's, or -1: none, the host folds it), appended
+// after the partition's own groups (hagg: table-encoded words, as the regions hold them).
+// One workgroup, so a region that fills up is cut back after every claim is made: the keys
+// that did not fit are flagged in miss[j] (the host folds them).
+__global__ __launch_bounds__(1024) void go_heavy_insert_kernel(const int64_t *__restrict__ hk,
+                                                               const uint64_t *__restrict__ hagg, uint32_t h, int na,
+                                                               const int64_t *__restrict__ hq, uint64_t q0, uint64_t nq,
+                                                               unsigned long long *__restrict__ cnt,
+                                                               uint64_t *__restrict__ slot, uint64_t *__restrict__ agg,
+                                                               uint64_t gstr, uint64_t dregion,
+                                                               uint64_t *__restrict__ miss) {
+  for (uint32_t j0 = 0; j0 < h; j0 += blockDim.x) {
+    const uint32_t j = j0 + threadIdx.x;
+    const int64_t q = j < h ? hq[j] : -1;
+    const bool mine = q >= (int64_t)q0 && q < (int64_t)(q0 + nq);
+    uint64_t idx = 0;
+    if (mine) {
+      idx = atomicAdd(&cnt[q], 1ull);
+      if (idx < dregion) {
+        const uint64_t at = (uint64_t)q * dregion + idx;
+        slot[at] = (uint64_t)hk[j];
+        for (int a = 0; a < na; ++a) agg[(uint64_t)a * gstr + at] = hagg[(uint64_t)j * na + a];
+      } else {
+        miss[j] = 1;
+      }
+    }
+    __syncthreads();
+    if (mine && idx >= dregion) atomicMin(&cnt[q], (unsigned long long)dregion);
+    __syncthreads();
+  }
+}
+
 // one workgroup: offs[p] = *run + the groups of the partitions before p, then *run += all
 // of them (each thread a run of ceil(np / 1024) consecutive partitions)
 __global__ __launch_bounds__(1024) void go_scan_kernel(const unsigned long long *__restrict__ cnt, uint32_t np,

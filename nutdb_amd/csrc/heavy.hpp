@@ -17,10 +17,10 @@
 namespace nut {
 
 constexpr int HK_THREADS = 256, HK_ITEMS = 8;
-constexpr uint32_t HK_TILE = HK_THREADS * HK_ITEMS;  // rows per tile (one cursor claim)
+constexpr uint32_t HK_TILE = HK_THREADS * HK_ITEMS;  // rows per tile
 constexpr int HK_MAX = 1024;                         // heavy keys at most
 constexpr int HK_SLOTS = 2048;                       // LDS hash set (load <= 1/2)
-constexpr int HK_WORDS = 4096;                       // heavy keys x aggregates at most (32 KB)
+constexpr int HK_WORDS = 2048;                       // heavy keys x aggregates at most (16 KB)
 
 struct HkArgs {
   const uint64_t *key;
@@ -28,13 +28,14 @@ struct HkArgs {
   uint64_t *okey;                     // compacted rows (every row whose key is not heavy)
   uint64_t *oval[NUT_MAX_VALS];
   uint64_t n;
+  uint64_t chunk;                     // tiles per workgroup: workgroup b reads tiles [b chunk, (b + 1) chunk)
   int nv, na;
   int32_t kind[NUT_MAX_AGGS];         // aggregate kinds (AggKind)
   int32_t arg[NUT_MAX_AGGS];          // value array of each aggregate (COUNT: unused)
   const int64_t *hk;                  // the heavy keys (h of them)
   uint32_t h;
   uint64_t *hagg;                     // [h x na] table-encoded words, initialised to agg_init
-  unsigned long long *cursor;         // compacted rows so far (output order: tile claims)
+  uint64_t *count;                    // [gridDim.x] rows each workgroup kept
 };
 
 __device__ __forceinline__ uint32_t hk_hash(uint64_t k) { return (uint32_t)(mix64(k) >> 40) & (HK_SLOTS - 1); }
@@ -50,14 +51,16 @@ __device__ __forceinline__ void combine_atomic(uint64_t *w, uint64_t x) {
   else atomicMax((long long *)w, (long long)x);
 }
 
-// Persistent: each workgroup claims tiles of HK_TILE rows in turn (grid stride); per tile
-// the kept rows of (item, wave) pairs get consecutive output runs from one cursor claim.
+// Workgroup b owns a contiguous chunk of tiles and compacts its kept rows to the start of
+// the same chunk of the output (no global cursor: the host reads the per-workgroup counts
+// and hands the level-0 scatter one segment per workgroup).  Within a tile the kept rows of
+// (item, wave) pairs get consecutive runs; the next tile's rows are loaded before this
+// tile's are looked up.
 __global__ __launch_bounds__(HK_THREADS) void hk_split_kernel(HkArgs a) {
   __shared__ uint16_t s_slot[HK_SLOTS];  // heavy key index + 1 (0: empty)
   __shared__ int64_t s_key[HK_MAX];
   __shared__ uint64_t s_acc[HK_WORDS];
-  __shared__ uint32_t s_off[HK_ITEMS * (HK_THREADS / 64)];
-  __shared__ uint64_t s_base;
+  __shared__ uint32_t s_off[2][HK_ITEMS * (HK_THREADS / 64)];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   constexpr int NW = HK_THREADS / 64;
   for (int i = tid; i < HK_SLOTS; i += HK_THREADS) s_slot[i] = 0;
@@ -73,28 +76,39 @@ __global__ __launch_bounds__(HK_THREADS) void hk_split_kernel(HkArgs a) {
   }
   __syncthreads();
   const uint64_t ntiles = (a.n + HK_TILE - 1) / HK_TILE;
-  for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-    const uint64_t base = t * HK_TILE;
-    uint64_t k[HK_ITEMS], v[HK_ITEMS][NUT_MAX_VALS];
+  const uint64_t t0 = (uint64_t)blockIdx.x * a.chunk, t1 = min(ntiles, t0 + a.chunk);
+  uint64_t out = t0 * HK_TILE;  // this workgroup's next output row
+  uint64_t k[HK_ITEMS], v[HK_ITEMS][NUT_MAX_VALS];
+  auto load = [&](uint64_t t) {
+#pragma unroll
+    for (int i = 0; i < HK_ITEMS; ++i) {
+      const uint64_t r = min(t * HK_TILE + (uint64_t)i * HK_THREADS + tid, a.n - 1);  // (clamped: unconditional loads)
+      k[i] = __builtin_nontemporal_load(a.key + r);
+#pragma unroll
+      for (int c = 0; c < NUT_MAX_VALS; ++c) v[i][c] = c < a.nv ? __builtin_nontemporal_load(a.val[c] + r) : 0;
+    }
+  };
+  if (t0 < t1) load(t0);
+  int buf = 0;
+  for (uint64_t t = t0; t < t1; ++t) {
+    uint64_t ck[HK_ITEMS], cv[HK_ITEMS][NUT_MAX_VALS];
+#pragma unroll
+    for (int i = 0; i < HK_ITEMS; ++i) {
+      ck[i] = k[i];
+#pragma unroll
+      for (int c = 0; c < NUT_MAX_VALS; ++c) cv[i][c] = v[i][c];
+    }
+    if (t + 1 < t1) load(t + 1);
     int hid[HK_ITEMS];
 #pragma unroll
     for (int i = 0; i < HK_ITEMS; ++i) {
-      const uint64_t r = base + (uint64_t)i * HK_THREADS + tid;
-      const bool ok = r < a.n;
-      k[i] = ok ? __builtin_nontemporal_load(a.key + r) : 0;
-#pragma unroll
-      for (int c = 0; c < NUT_MAX_VALS; ++c) v[i][c] = ok && c < a.nv ? __builtin_nontemporal_load(a.val[c] + r) : 0;
-      hid[i] = ok ? -1 : -2;  // -2: past the end
-    }
-    // heavy lookup + in-place aggregation
-#pragma unroll
-    for (int i = 0; i < HK_ITEMS; ++i) {
+      hid[i] = t * HK_TILE + (uint64_t)i * HK_THREADS + tid < a.n ? -1 : -2;  // -2: past the end
       if (hid[i] == -1) {
-        uint32_t q = hk_hash(k[i]);
+        uint32_t q = hk_hash(ck[i]);
         for (;;) {
           const uint32_t j = s_slot[q];
           if (!j) break;
-          if ((uint64_t)s_key[j - 1] == k[i]) {
+          if ((uint64_t)s_key[j - 1] == ck[i]) {
             hid[i] = (int)j - 1;
             break;
           }
@@ -105,7 +119,7 @@ __global__ __launch_bounds__(HK_THREADS) void hk_split_kernel(HkArgs a) {
         for (int g = 0; g < a.na; ++g) {
           uint64_t x = 0;
 #pragma unroll
-          for (int c = 0; c < NUT_MAX_VALS; ++c) x = a.arg[g] == c ? v[i][c] : x;
+          for (int c = 0; c < NUT_MAX_VALS; ++c) x = a.arg[g] == c ? cv[i][c] : x;
           with_kind(a.kind[g], [&](auto KC) {
             constexpr int K = decltype(KC)::value;
             fold_atomic<K>(&s_acc[hid[i] * a.na + g], x);
@@ -113,37 +127,37 @@ __global__ __launch_bounds__(HK_THREADS) void hk_split_kernel(HkArgs a) {
         }
       }
     }
-    // compaction: the kept rows of item i, wave w go to one run
+    // compaction: the kept rows of item i, wave w go to one run (offsets: an exclusive scan
+    // of the 32 counts, every thread reading them — no serial section)
     uint64_t m[HK_ITEMS];
 #pragma unroll
     for (int i = 0; i < HK_ITEMS; ++i) {
       m[i] = __ballot(hid[i] == -1);
-      if (lane == 0) s_off[i * NW + wave] = (uint32_t)__popcll(m[i]);
+      if (lane == 0) s_off[buf][i * NW + wave] = (uint32_t)__popcll(m[i]);
     }
     __syncthreads();
-    if (tid == 0) {
-      uint32_t run = 0;
-      for (int j = 0; j < HK_ITEMS * NW; ++j) {
-        const uint32_t c = s_off[j];
-        s_off[j] = run;
-        run += c;
-      }
-      s_base = run ? (uint64_t)atomicAdd(a.cursor, (unsigned long long)run) : 0;
+    uint32_t before[HK_ITEMS], total = 0;
+#pragma unroll
+    for (int j = 0; j < HK_ITEMS * NW; ++j) {
+      const uint32_t cj = s_off[buf][j];
+      if (j % NW == wave) before[j / NW] = total;
+      total += cj;
     }
-    __syncthreads();
-    const uint64_t ob = s_base;
 #pragma unroll
     for (int i = 0; i < HK_ITEMS; ++i) {
       if (hid[i] == -1) {
-        const uint64_t o = ob + s_off[i * NW + wave] + lane_rank(m[i]);
-        __builtin_nontemporal_store(k[i], a.okey + o);
+        const uint64_t o = out + before[i] + lane_rank(m[i]);
+        __builtin_nontemporal_store(ck[i], a.okey + o);
 #pragma unroll
         for (int c = 0; c < NUT_MAX_VALS; ++c)
-          if (c < a.nv) __builtin_nontemporal_store(v[i][c], a.oval[c] + o);
+          if (c < a.nv) __builtin_nontemporal_store(cv[i][c], a.oval[c] + o);
       }
     }
-    __syncthreads();  // (s_off / s_base are rewritten by the next tile)
+    out += total;
+    buf ^= 1;  // (the other half of s_off: the next tile's counts cannot overwrite these before every wave read them)
   }
+  if (tid == 0) a.count[blockIdx.x] = out - t0 * HK_TILE;
+  __syncthreads();
   // this workgroup's heavy accumulators into the device words
   for (uint32_t i = tid; i < a.h * (uint32_t)a.na; i += HK_THREADS) {
     const int g = (int)(i % a.na);

@@ -49,8 +49,9 @@ constexpr int MS_BINS = 1 << MS_BITS;               // 512: MS_TILE / 512 = 28 k
 static_assert(MS_BINS <= MS_THREADS, "one scan thread per digit");
 // local-sort classes: threads x max items per thread (ms_local_kernel), by segment size.
 // The segments of a 1.25e9-key sort (~4768 keys) take class 1: 256 threads x 20 keys, three
-// workgroups per CU (51 KB of LDS each) — scripts/tune/local_tune.hip, 262144 segments of
-// 4768 keys: 5.70 ms vs 6.65 for 512 x 12 at two per CU (profiles/r05/sort/)
+// workgroups per CU (51 KB of LDS each), one workgroup per segment — scripts/tune/
+// local_tune.hip, 262144 segments of 4768 keys: 5.14 ms vs 6.65 for round 4's persistent
+// 512 x 12 at two per CU (profiles/r05/sort/local_tune_sweep.log)
 constexpr int LS_NCLS = 4;
 constexpr int LS_S_THREADS = 256, LS_S_ITEMS = 8;     // class 0: <= 2048 keys
 constexpr int LS_M_THREADS = 256, LS_M_ITEMS = 20;    // class 1: <= 5120 keys, 3 workgroups per CU

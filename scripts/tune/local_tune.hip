@@ -146,8 +146,9 @@ int main(int argc, char **argv) {
     printf("%-28s                 %7.3f ms  %6.0f GB/s\n", "copy (HBM floor)", best, 16.0 * c.n / best / 1e6);
   }
   printf("segments %u x %u keys\n", c.nseg, c.seglen);
-  run<512, 12, 0, 0>(c, "default <512,12> (SB12 WS10)");
+  run<256, 20, 0, 0, false>(c, "product <256,20> 1 WG/segment");
   if (argc > 3) return 0;  // profiling runs: the product variant only
+  run<512, 12, 0, 0>(c, "round-4 <512,12> persistent");
   run<256, 20, 11, 10>(c, "<256,20> SB11 WS10");
   run<256, 20, 11, 10, false>(c, "<256,20> SB11 WS10 no prefetch");
   run<256, 20, 12, 10>(c, "<256,20> SB12 WS10");

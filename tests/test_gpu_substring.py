@@ -54,7 +54,7 @@ def test_fixture9_q22(ex):
     """TPC-H Q22 as written (tests/sql/9.sql): substring in the derived table's projection,
     its WHERE and the scalar subquery's WHERE; NOT EXISTS over orders; GROUP BY cntrycode."""
     rng = np.random.default_rng(9)
-    nc, no = 150_000, 600_000
+    nc, no = 150_000, 300_000
     cust = {"c_custkey": rng.permutation(nc * 2)[:nc].astype(np.int64), "c_phone": phones(rng, nc),
             "c_acctbal": np.round(rng.uniform(-999.99, 9999.99, nc), 2)}
     orders = {"o_custkey": rng.choice(cust["c_custkey"], no).astype(np.int64)}
