@@ -567,7 +567,9 @@ __global__ __launch_bounds__(BD) void agg_kernel(AggArgs p) {
   uint64_t rb = 0, nrows = p.n, gstride = (uint64_t)gridDim.x * BD, q = (uint64_t)blockIdx.x * BD + threadIdx.x;
   if (p.seg_off) {
     rb = p.seg_end ? p.seg_off[blockIdx.x] : p.seg_off[2 * blockIdx.x];
-    nrows = (p.seg_end ? p.seg_end[blockIdx.x] : p.seg_off[2 * blockIdx.x + 1]) - rb;
+    nrows = (p.seg_end ? (p.seg_cut ? min(p.seg_end[blockIdx.x], p.seg_cut[blockIdx.x]) : p.seg_end[blockIdx.x])
+                       : p.seg_off[2 * blockIdx.x + 1]) -
+            rb;
     gstride = BD;
     q = threadIdx.x;
   }

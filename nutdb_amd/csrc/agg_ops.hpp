@@ -61,6 +61,7 @@ struct AggArgs {
   // Segment mode (seg_off != 0): block b folds rows [seg_off[2b], seg_off[2b+1]) only.
   const uint64_t *seg_off;
   const uint64_t *seg_end;  // non-null: block b's rows are [seg_off[b], seg_end[b]) instead
+  const uint64_t *seg_cut;  // non-null (with seg_end): ... [seg_off[b], min(seg_end[b], seg_cut[b]))
   // dense (segment mode, one key, every segment a whole partition): a block's groups are
   // final, so they are appended to the table's first slots instead of hashed into it
   int32_t dense, pad_;

@@ -290,6 +290,7 @@ struct LaunchExtra {
   uint64_t blocks = 0, region = 0;         // out (spill): grid and per-block staging region
   const uint64_t *seg_off = nullptr;       // one block per segment: [start, end) pairs, even starts
   const uint64_t *seg_end = nullptr;       //   or starts in seg_off, ends here (AggArgs::seg_end)
+  const uint64_t *seg_cut = nullptr;       //   ... or at min(seg_end, seg_cut) (AggArgs::seg_cut)
   uint32_t nseg = 0;
   bool dense = false;                      // every segment a whole partition (AggArgs::dense)
   unsigned long long *dcount = nullptr;    // dense staging (AggArgs::dcount / dregion / dbase)
@@ -426,6 +427,7 @@ nut_status launch_agg(nut_groups *g, const nut_agg_spec *s, uint64_t group_hint,
   if (ex && ex->seg_off) {  // one block per segment (segments start at even rows)
     a.seg_off = ex->seg_off;
     a.seg_end = ex->seg_end;
+    a.seg_cut = ex->seg_cut;
     a.dense = ex->dense && g->nk == 1 ? 1 : 0;
     blocks = ex->nseg;
     if (ex->dcount) {  // dense staging: every region must hold a full block table
@@ -1133,11 +1135,40 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
     if (s->agg_op[a] != NUT_AGG_COUNT && vmap[s->agg_arg[a][0]] < 0) vmap[s->agg_arg[a][0]] = nv++;
   const int narr = 3 + nv, nstore = narr - 2;
   const uint64_t rows = (n + 2 * 65536 + 64 + 31) & ~31ull;
-  const double slack1 = 1.0 + 6.0 / sqrt(lam);
+  // ---- heavy keys (heavy.hpp): a key the sample saw >= 4 times (>= ~1/16000 of the rows:
+  // a whole level-1 partition's share) would overflow its partition.  When such keys
+  // hold >= 5 % of the sample, the <= HK_MAX most frequent are aggregated in one streaming
+  // pass and the other rows, compacted into B2, are what the levels partition.
+  std::vector<int64_t> hkeys;
+  if (c->opt[NUT_OPT_GB_HEAVY] != 0) {
+    std::vector<int64_t> ss(smp);
+    std::sort(ss.begin(), ss.end());
+    std::vector<std::pair<uint32_t, int64_t>> cand;  // (sample count, key)
+    for (size_t i = 0; i < ss.size();) {
+      size_t j = i;
+      while (j < ss.size() && ss[j] == ss[i]) ++j;
+      if (j - i >= 4) cand.emplace_back((uint32_t)(j - i), ss[i]);
+      i = j;
+    }
+    std::sort(cand.begin(), cand.end(), [](const auto &x, const auto &y) { return x.first > y.first; });
+    const size_t hmax = std::min<size_t>(HK_MAX, HK_WORDS / na);
+    if (cand.size() > hmax) cand.resize(hmax);
+    uint64_t cover = 0;
+    for (const auto &x : cand) cover += x.first;
+    if (cover * 20 >= kSample) {
+      for (const auto &x : cand) hkeys.push_back(x.second);
+      std::sort(hkeys.begin(), hkeys.end());
+    }
+  }
+  // level-1 regions: the even share x slack1 (six standard deviations of a Poisson count
+  // of lambda keys per partition); with heavy keys split off, the data is skewed below them
+  // too (Zipf-like: keys of ~1/2 to 2 partition shares remain), so their regions get 2.5 x
+  // (1e9-row Zipf G = 1e7: 62 M arena rows at 1.24 x)
+  const double slack1 = hkeys.empty() ? 1.0 + 6.0 / sqrt(lam) : 2.5;
   // B2: the level-1 regions (n x slack1 + per-region slack), then level 1's overflow arena
-  // (n / 2 rows: Zipf-like keys over 1e7 groups put ~1/3 of the rows there), then one tile
-  // of scratch for runs an exhausted arena cannot take
-  const uint64_t arena1 = (n / 2 + 31) & ~31ull;
+  // (n / 2 rows, n / 4 with the wider regions), then one tile of scratch for runs an
+  // exhausted arena cannot take
+  const uint64_t arena1 = ((hkeys.empty() ? n / 2 : n / 4) + 31) & ~31ull;
   const uint64_t b2rows =
       ((uint64_t)ceil(n * slack1) + (66ull << (bits0 + bits1)) + arena1 + 2 * GP_TILE + 64 + 31) & ~31ull;
   e = c->gp_data.reserve((2 * (size_t)nstore * rows + (size_t)nstore * b2rows) * 8 + 256);
@@ -1167,31 +1198,6 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
     ~FreeArena() { (void)hipFreeAsync(p, s); }
   } free_arena{darena, st};
   NUT_HIP(hipMemsetAsync(darena, 0, 16, st));
-  // ---- heavy keys (heavy.hpp): a key the sample saw >= 4 times (>= ~1/16000 of the rows:
-  // a whole level-1 partition's share) would overflow its partition.  When such keys
-  // hold >= 5 % of the sample, the <= HK_MAX most frequent are aggregated in one streaming
-  // pass and the other rows, compacted into B2, are what the levels partition.
-  std::vector<int64_t> hkeys;
-  if (c->opt[NUT_OPT_GB_HEAVY] != 0) {
-    std::vector<int64_t> ss(smp);
-    std::sort(ss.begin(), ss.end());
-    std::vector<std::pair<uint32_t, int64_t>> cand;  // (sample count, key)
-    for (size_t i = 0; i < ss.size();) {
-      size_t j = i;
-      while (j < ss.size() && ss[j] == ss[i]) ++j;
-      if (j - i >= 4) cand.emplace_back((uint32_t)(j - i), ss[i]);
-      i = j;
-    }
-    std::sort(cand.begin(), cand.end(), [](const auto &x, const auto &y) { return x.first > y.first; });
-    const size_t hmax = std::min<size_t>(HK_MAX, HK_WORDS / na);
-    if (cand.size() > hmax) cand.resize(hmax);
-    uint64_t cover = 0;
-    for (const auto &x : cand) cover += x.first;
-    if (cover * 20 >= kSample) {
-      for (const auto &x : cand) hkeys.push_back(x.second);
-      std::sort(hkeys.begin(), hkeys.end());
-    }
-  }
   uint64_t n0 = n;  // the rows the partition levels read
   std::vector<uint64_t> hcount;  // heavy pass: the rows each workgroup kept, at hchunk-row strides of B2
   uint64_t hchunk = 0;
@@ -1205,8 +1211,12 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
   } free_heavy{nullptr, st};
   const uint32_t nh = (uint32_t)hkeys.size();
   if (nh) {
+    using HK = void (*)(HkArgs);
+    static const HK hkern[NUT_MAX_VALS + 1] = {hk_split_kernel<0>, hk_split_kernel<1>, hk_split_kernel<2>,
+                                               hk_split_kernel<3>, hk_split_kernel<4>};
+    static_assert(NUT_MAX_VALS == 4, "one heavy-pass kernel per value-array count");
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, hk_split_kernel, HK_THREADS, 0) != hipSuccess || per_cu < 1)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, hkern[nv], HK_THREADS, 0) != hipSuccess || per_cu < 1)
       per_cu = 1;
     const uint64_t ntiles = (n + HK_TILE - 1) / HK_TILE;
     const uint64_t hgrid = std::min<uint64_t>(ntiles, (uint64_t)c->num_cus * per_cu);
@@ -1240,7 +1250,7 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
     ha.count = (uint64_t *)dheavy + nh + (size_t)nh * na;
     ha.chunk = chunk;
     c->timer.begin(st, NUT_KERNEL_AGGREGATE);
-    hipLaunchKernelGGL(hk_split_kernel, dim3((unsigned)hgrid), dim3(HK_THREADS), 0, st, ha);
+    hipLaunchKernelGGL(hkern[nv], dim3((unsigned)hgrid), dim3(HK_THREADS), 0, st, ha);
     c->timer.end(st);
     NUT_HIP(hipGetLastError());
     hcount.resize(hgrid);
@@ -1364,12 +1374,12 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
   if ((e = mm.up(hq, &dhq))) return e;
   uint64_t *dmiss = (uint64_t *)mm.alloc((size_t)nh * 8 + 1);  // heavy keys whose partition's region was full
   if (nh) NUT_HIP(hipMemsetAsync(dmiss, 0, (size_t)nh * 8, st));
-  uint64_t *dend = (uint64_t *)mm.alloc(nparts * 8);  // partition ends, cut at their regions' ends
   unsigned long long *dcur = (unsigned long long *)mm.alloc(init.size() * 8);
   unsigned long long *dcount = (unsigned long long *)mm.alloc(nparts * 8);
   uint64_t *doffs = (uint64_t *)mm.alloc(nparts * 8);
   unsigned long long *drun = (unsigned long long *)mm.alloc(64);
-  // the first overflowing run's start per partition (go_clamp_kernel), from the region ends
+  // the first overflowing run's start per partition (gp_scatter_kernel's acut), from the
+  // region ends: the aggregation ends each partition there (AggArgs::seg_cut)
   unsigned long long *dcut = (unsigned long long *)mm.alloc(nparts * 8);
   NUT_HIP(hipMemcpyAsync(dcut, drend, nparts * 8, hipMemcpyDeviceToDevice, st));
   NUT_HIP(hipMemcpyAsync(dcur, dinit, init.size() * 8, hipMemcpyDeviceToDevice, st));
@@ -1430,13 +1440,12 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
     NUT_HIP(hipEventRecord(ev1[j], st));
     NUT_HIP(hipStreamWaitEvent(ax, ev1[j], 0));
     // partition rows [first row, cursor after the scatter), cut at the first run that went
-    // to the arena (the rows after it are not the partition's)
-    hipLaunchKernelGGL(go_clamp_kernel, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, ax,
-                       (const unsigned long long *)dcur + q0, (const unsigned long long *)dcut + q0, (uint32_t)nq,
-                       dend + q0);
+    // to the arena (the rows after it are not the partition's): min(cursor, cut), read by
+    // the aggregation's blocks themselves
     LaunchExtra sg;
     sg.seg_off = dinit + q0;
-    sg.seg_end = (const uint64_t *)dend + q0;
+    sg.seg_end = (const uint64_t *)dcur + q0;
+    sg.seg_cut = (const uint64_t *)dcut + q0;
     sg.nseg = (uint32_t)nq;
     sg.dense = true;
     sg.dcount = dcount + q0;
@@ -1500,23 +1509,32 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
   if (used0 + used1 && !over) {
     // the arenas' rows (heavy keys' excess, mostly) aggregated on their own and folded
     // into the ordered host result
+    // (copied out of gp_data first — the arenas live there and the group-by may partition,
+    // which takes gp_data — then one group-by over both levels' rows, on whichever path its
+    // size picks)
+    const uint64_t ar_rows = used0 + used1;
+    uint64_t *ar = nullptr;
+    NUT_HIP(hipMallocAsync((void **)&ar, ar_rows * 8 * (1 + (size_t)nv), st));
+    struct FreeAr {
+      uint64_t *p;
+      hipStream_t s;
+      ~FreeAr() { (void)hipFreeAsync(p, s); }
+    } free_ar{ar, st};
+    for (int i = 1; i < narr; ++i) {
+      if (i == 2) continue;
+      uint64_t *dst = ar + (size_t)(i == 1 ? 0 : i - 2) * ar_rows;
+      if (used0) NUT_HIP(hipMemcpyAsync(dst, O[i] + abase0, used0 * 8, hipMemcpyDeviceToDevice, st));
+      if (used1) NUT_HIP(hipMemcpyAsync(dst + used0, B2[i] + ovf1, used1 * 8, hipMemcpyDeviceToDevice, st));
+    }
     nut_agg_spec sa = s3;
+    sa.n = ar_rows;
+    sa.keys[0] = (const int64_t *)ar;
+    for (int j = 0; j < NUT_MAX_VALS; ++j)
+      if (vmap[j] >= 0) sa.val_col[vmap[j]] = ar + (size_t)(1 + vmap[j]) * ar_rows;
     const uint32_t path = c->gb_path, lv = c->gb_levels, opt = c->gb_optimistic;
-    const int64_t part = c->opt[NUT_OPT_GB_PARTITION];
-    c->opt[NUT_OPT_GB_PARTITION] = 0;  // (the partitioned path would reuse gp_data, which holds the arenas)
     nut_groups *ga = nullptr;
     uint64_t na_groups = 0;
-    for (int lvl = 0; lvl < 2 && !e; ++lvl) {
-      const uint64_t rows_l = lvl ? used1 : used0, base = lvl ? ovf1 : abase0;
-      uint64_t *const *arr = lvl ? B2 : O;
-      if (!rows_l) continue;
-      sa.n = rows_l;
-      sa.keys[0] = (const int64_t *)(arr[1] + base);
-      for (int j = 0; j < NUT_MAX_VALS; ++j)
-        if (vmap[j] >= 0) sa.val_col[vmap[j]] = arr[3 + vmap[j]] + base;
-      e = ga ? nut_groupby_accumulate(c, &sa, ga) : nut_groupby(c, &sa, std::min<uint64_t>(rows_l, group_hint), &ga);
-    }
-    c->opt[NUT_OPT_GB_PARTITION] = part;
+    e = nut_groupby(c, &sa, std::min<uint64_t>(ar_rows, group_hint), &ga);
     c->gb_path = path, c->gb_levels = lv, c->gb_optimistic = opt;
     if (!e) e = nut_groups_size(ga, &na_groups);
     std::vector<int64_t> hk(na_groups);

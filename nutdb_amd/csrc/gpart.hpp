@@ -315,17 +315,6 @@ __global__ void go_sample_kernel(const int64_t *__restrict__ k, uint64_t n, uint
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) out[i] = k[i * step];
 }
 
-// end[q] = min(cursor[q], cut[q]): a capped level's partition ends.  When a run overflows
-// its region the cursor still advances by the whole run (the run itself goes to the
-// arena), so the raw cursor would send the aggregation past the region; cut[q] starts at
-// the region's end and the scatter lowers it to the first overflowing run's start
-// (gp_scatter_kernel's acut), below which every row was written.
-__global__ void go_clamp_kernel(const unsigned long long *__restrict__ cursor, const unsigned long long *__restrict__ cut,
-                                uint32_t n, uint64_t *__restrict__ end) {
-  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
-  if (q < n) end[q] = min((uint64_t)cursor[q], (uint64_t)cut[q]);
-}
-
 // The heavy-key pass's groups (heavy.hpp) into their partitions' dense regions after the
 // chunk's aggregation and before its ordering: hq[j] = heavy key j's partition (global
 // index; outside [q0, q0 + nq): another chunk's, or -1: none, the host folds it), appended

@@ -55,10 +55,12 @@ __device__ __forceinline__ void combine_atomic(uint64_t *w, uint64_t x) {
 // the same chunk of the output (no global cursor: the host reads the per-workgroup counts
 // and hands the level-0 scatter one segment per workgroup).  Within a tile the kept rows of
 // (item, wave) pairs get consecutive runs; the next tile's rows are loaded before this
-// tile's are looked up.
+// tile's are looked up.  NV: value arrays (registers for two tiles of them: a template, so
+// one value array takes ~80 VGPRs, not the 206 that four would).
+template <int NV>
 __global__ __launch_bounds__(HK_THREADS) void hk_split_kernel(HkArgs a) {
   __shared__ uint16_t s_slot[HK_SLOTS];  // heavy key index + 1 (0: empty)
-  __shared__ int64_t s_key[HK_MAX];
+  __shared__ uint64_t s_skey[HK_SLOTS];  // the slot's key (read with its index: one round trip per probe)
   __shared__ uint64_t s_acc[HK_WORDS];
   __shared__ uint32_t s_off[2][HK_ITEMS * (HK_THREADS / 64)];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -68,58 +70,76 @@ __global__ __launch_bounds__(HK_THREADS) void hk_split_kernel(HkArgs a) {
   __syncthreads();
   if (tid == 0) {  // (h <= HK_MAX keys into 2048 slots: linear probing always finds room)
     for (uint32_t j = 0; j < a.h; ++j) {
-      s_key[j] = a.hk[j];
       uint32_t q = hk_hash((uint64_t)a.hk[j]);
       while (s_slot[q]) q = (q + 1) & (HK_SLOTS - 1);
       s_slot[q] = (uint16_t)(j + 1);
+      s_skey[q] = (uint64_t)a.hk[j];
     }
   }
   __syncthreads();
   const uint64_t ntiles = (a.n + HK_TILE - 1) / HK_TILE;
   const uint64_t t0 = (uint64_t)blockIdx.x * a.chunk, t1 = min(ntiles, t0 + a.chunk);
   uint64_t out = t0 * HK_TILE;  // this workgroup's next output row
-  uint64_t k[HK_ITEMS], v[HK_ITEMS][NUT_MAX_VALS];
+  uint64_t k[HK_ITEMS], v[HK_ITEMS][NV];
   auto load = [&](uint64_t t) {
 #pragma unroll
     for (int i = 0; i < HK_ITEMS; ++i) {
       const uint64_t r = min(t * HK_TILE + (uint64_t)i * HK_THREADS + tid, a.n - 1);  // (clamped: unconditional loads)
       k[i] = __builtin_nontemporal_load(a.key + r);
 #pragma unroll
-      for (int c = 0; c < NUT_MAX_VALS; ++c) v[i][c] = c < a.nv ? __builtin_nontemporal_load(a.val[c] + r) : 0;
+      for (int c = 0; c < NV; ++c) v[i][c] = __builtin_nontemporal_load(a.val[c] + r);
     }
   };
   if (t0 < t1) load(t0);
   int buf = 0;
   for (uint64_t t = t0; t < t1; ++t) {
-    uint64_t ck[HK_ITEMS], cv[HK_ITEMS][NUT_MAX_VALS];
+    uint64_t ck[HK_ITEMS], cv[HK_ITEMS][NV];
 #pragma unroll
     for (int i = 0; i < HK_ITEMS; ++i) {
       ck[i] = k[i];
 #pragma unroll
-      for (int c = 0; c < NUT_MAX_VALS; ++c) cv[i][c] = v[i][c];
+      for (int c = 0; c < NV; ++c) cv[i][c] = v[i][c];
     }
     if (t + 1 < t1) load(t + 1);
+    // lookups in probe rounds over all items at once (each round's 8 LDS reads in flight
+    // together, instead of each item's probe chain one read after another)
     int hid[HK_ITEMS];
+    uint32_t q[HK_ITEMS];
+    bool act[HK_ITEMS];
 #pragma unroll
     for (int i = 0; i < HK_ITEMS; ++i) {
-      hid[i] = t * HK_TILE + (uint64_t)i * HK_THREADS + tid < a.n ? -1 : -2;  // -2: past the end
-      if (hid[i] == -1) {
-        uint32_t q = hk_hash(ck[i]);
-        for (;;) {
-          const uint32_t j = s_slot[q];
-          if (!j) break;
-          if ((uint64_t)s_key[j - 1] == ck[i]) {
-            hid[i] = (int)j - 1;
-            break;
-          }
-          q = (q + 1) & (HK_SLOTS - 1);
+      const bool in = t * HK_TILE + (uint64_t)i * HK_THREADS + tid < a.n;
+      hid[i] = in ? -1 : -2;  // -2: past the end
+      act[i] = in;
+      q[i] = hk_hash(ck[i]);
+    }
+    for (;;) {
+      bool any = false;
+#pragma unroll
+      for (int i = 0; i < HK_ITEMS; ++i) any = any || act[i];
+      if (!__any(any)) break;
+#pragma unroll
+      for (int i = 0; i < HK_ITEMS; ++i) {
+        if (!act[i]) continue;
+        const uint32_t j = s_slot[q[i]];
+        const uint64_t sk = s_skey[q[i]];
+        if (!j) {
+          act[i] = false;
+        } else if (sk == ck[i]) {
+          hid[i] = (int)j - 1;
+          act[i] = false;
+        } else {
+          q[i] = (q[i] + 1) & (HK_SLOTS - 1);
         }
       }
+    }
+#pragma unroll
+    for (int i = 0; i < HK_ITEMS; ++i) {
       if (hid[i] >= 0) {
         for (int g = 0; g < a.na; ++g) {
           uint64_t x = 0;
 #pragma unroll
-          for (int c = 0; c < NUT_MAX_VALS; ++c) x = a.arg[g] == c ? cv[i][c] : x;
+          for (int c = 0; c < NV; ++c) x = a.arg[g] == c ? cv[i][c] : x;
           with_kind(a.kind[g], [&](auto KC) {
             constexpr int K = decltype(KC)::value;
             fold_atomic<K>(&s_acc[hid[i] * a.na + g], x);
@@ -149,8 +169,7 @@ __global__ __launch_bounds__(HK_THREADS) void hk_split_kernel(HkArgs a) {
         const uint64_t o = out + before[i] + lane_rank(m[i]);
         __builtin_nontemporal_store(ck[i], a.okey + o);
 #pragma unroll
-        for (int c = 0; c < NUT_MAX_VALS; ++c)
-          if (c < a.nv) __builtin_nontemporal_store(cv[i][c], a.oval[c] + o);
+        for (int c = 0; c < NV; ++c) __builtin_nontemporal_store(cv[i][c], a.oval[c] + o);
       }
     }
     out += total;
