@@ -1099,24 +1099,29 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
   if (rg.span < (1ull << 16)) return decline(NUT_GB_DECLINE_SHAPE);  // (mul must fit 32 bits; tiny spans hash fine)
   rg.t = rg.span >> 32 ? 32 - __builtin_clzll(rg.span) : 0;
   rg.mul = (uint32_t)((1ull << 46) / ((rg.span >> rg.t) + 1));
+  // the sample's keys counted in an open-addressing table (2x the sample): distinct keys
+  // for the admission, repeated ones for the heavy-key split (a sort of the 64 Ki keys took
+  // milliseconds of host time ahead of every call's first kernel)
+  constexpr uint32_t kSlots = 2 * kSample;
+  std::vector<int64_t> tk(kSlots);
+  std::vector<uint32_t> tc(kSlots, 0);
+  for (int64_t k : smp) {
+    uint32_t q = (uint32_t)(mix64((uint64_t)k) >> 32) & (kSlots - 1);
+    while (tc[q] && tk[q] != k) q = (q + 1) & (kSlots - 1);
+    tk[q] = k;
+    ++tc[q];
+  }
   {  // admission: the sample's distinct keys spread over the level-0 partitions.  Keys
      // clustered inside the sampled range would overfill some partitions' tables (each
      // holds ~2x its share of groups) and send the call to the hashed path after all the
      // work; decline up front instead.  Repeated keys count once: a heavy key is rows,
-     // not groups, and its excess rows go to the overflow arenas below.
-    // (raw counts first — one pass; only a partition above the bound has its samples
-    // deduplicated, so uniform keys pay no sort)
+     // not groups (the heavy-key split or the overflow arenas below take its rows).
     const uint32_t np0 = 1u << bits0, bound = 2 * kSample / np0 + 16;
-    std::vector<uint32_t> raw(np0, 0);
-    for (int64_t k : smp) ++raw[rg.cell((uint64_t)k) >> bits1];
-    for (uint32_t p = 0; p < np0; ++p) {
-      if (raw[p] <= bound) continue;
-      std::vector<int64_t> ks;
-      for (int64_t k : smp)
-        if (rg.cell((uint64_t)k) >> bits1 == p) ks.push_back(k);
-      std::sort(ks.begin(), ks.end());
-      if ((uint64_t)(std::unique(ks.begin(), ks.end()) - ks.begin()) > bound) return decline(NUT_GB_DECLINE_CLUSTERED);
-    }
+    std::vector<uint32_t> distinct(np0, 0);
+    for (uint32_t q = 0; q < kSlots; ++q)
+      if (tc[q]) ++distinct[rg.cell((uint64_t)tk[q]) >> bits1];
+    for (uint32_t p = 0; p < np0; ++p)
+      if (distinct[p] > bound) return decline(NUT_GB_DECLINE_CLUSTERED);
   }
   // ---- partition buffers: level 0 capped over O (2 x rows per array), level 1 into B2
   nut_groups *g = new nut_groups();
@@ -1141,16 +1146,12 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
   // pass and the other rows, compacted into B2, are what the levels partition.
   std::vector<int64_t> hkeys;
   if (c->opt[NUT_OPT_GB_HEAVY] != 0) {
-    std::vector<int64_t> ss(smp);
-    std::sort(ss.begin(), ss.end());
     std::vector<std::pair<uint32_t, int64_t>> cand;  // (sample count, key)
-    for (size_t i = 0; i < ss.size();) {
-      size_t j = i;
-      while (j < ss.size() && ss[j] == ss[i]) ++j;
-      if (j - i >= 4) cand.emplace_back((uint32_t)(j - i), ss[i]);
-      i = j;
-    }
-    std::sort(cand.begin(), cand.end(), [](const auto &x, const auto &y) { return x.first > y.first; });
+    for (uint32_t q = 0; q < kSlots; ++q)
+      if (tc[q] >= 4) cand.emplace_back(tc[q], tk[q]);
+    std::sort(cand.begin(), cand.end(), [](const auto &x, const auto &y) {
+      return x.first > y.first || (x.first == y.first && x.second < y.second);
+    });
     const size_t hmax = std::min<size_t>(HK_MAX, HK_WORDS / na);
     if (cand.size() > hmax) cand.resize(hmax);
     uint64_t cover = 0;
@@ -1531,10 +1532,16 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
     sa.keys[0] = (const int64_t *)ar;
     for (int j = 0; j < NUT_MAX_VALS; ++j)
       if (vmap[j] >= 0) sa.val_col[vmap[j]] = ar + (size_t)(1 + vmap[j]) * ar_rows;
+    // (partitioned whatever its size: the rows are the tails of many keys — up to one group
+    // per row — and the streaming path's global table would take every one of them by
+    // atomics: 4 ms for 8.7 M arena rows of the 1e9-row Zipf step)
     const uint32_t path = c->gb_path, lv = c->gb_levels, opt = c->gb_optimistic;
+    const int64_t part = c->opt[NUT_OPT_GB_PARTITION];
+    c->opt[NUT_OPT_GB_PARTITION] = 1;
     nut_groups *ga = nullptr;
     uint64_t na_groups = 0;
     e = nut_groupby(c, &sa, std::min<uint64_t>(ar_rows, group_hint), &ga);
+    c->opt[NUT_OPT_GB_PARTITION] = part;
     c->gb_path = path, c->gb_levels = lv, c->gb_optimistic = opt;
     if (!e) e = nut_groups_size(ga, &na_groups);
     std::vector<int64_t> hk(na_groups);

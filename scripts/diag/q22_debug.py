@@ -1,10 +1,14 @@
 """Localise a fixture-9 (TPC-H Q22) mismatch: the substring WHERE alone, with the scalar
 subquery, with the NOT EXISTS step, and the whole fixture, each against pandas."""
+import os
+import sys
+
 import numpy as np
 import pandas as pd
 
-from nutdb_amd import Executor
-from nutdb_amd.table import Table
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", ".."))
+from nutdb_amd import Executor  # noqa: E402
+from nutdb_amd.table import Table  # noqa: E402
 
 ex = Executor()
 rng = np.random.default_rng(9)
