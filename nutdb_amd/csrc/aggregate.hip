@@ -1513,9 +1513,9 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
     // (copied out of gp_data first — the arenas live there and the group-by may partition,
     // which takes gp_data — then one group-by over both levels' rows, on whichever path its
     // size picks)
-    const uint64_t ar_rows = used0 + used1;
+    const uint64_t ar_rows = used0 + used1, ar_str = (ar_rows + 31) & ~31ull;  // (arrays 256-B aligned: vector loads)
     uint64_t *ar = nullptr;
-    NUT_HIP(hipMallocAsync((void **)&ar, ar_rows * 8 * (1 + (size_t)nv), st));
+    NUT_HIP(hipMallocAsync((void **)&ar, ar_str * 8 * (1 + (size_t)nv), st));
     struct FreeAr {
       uint64_t *p;
       hipStream_t s;
@@ -1523,7 +1523,7 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
     } free_ar{ar, st};
     for (int i = 1; i < narr; ++i) {
       if (i == 2) continue;
-      uint64_t *dst = ar + (size_t)(i == 1 ? 0 : i - 2) * ar_rows;
+      uint64_t *dst = ar + (size_t)(i == 1 ? 0 : i - 2) * ar_str;
       if (used0) NUT_HIP(hipMemcpyAsync(dst, O[i] + abase0, used0 * 8, hipMemcpyDeviceToDevice, st));
       if (used1) NUT_HIP(hipMemcpyAsync(dst + used0, B2[i] + ovf1, used1 * 8, hipMemcpyDeviceToDevice, st));
     }
@@ -1531,7 +1531,7 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
     sa.n = ar_rows;
     sa.keys[0] = (const int64_t *)ar;
     for (int j = 0; j < NUT_MAX_VALS; ++j)
-      if (vmap[j] >= 0) sa.val_col[vmap[j]] = ar + (size_t)(1 + vmap[j]) * ar_rows;
+      if (vmap[j] >= 0) sa.val_col[vmap[j]] = ar + (size_t)(1 + vmap[j]) * ar_str;
     // (partitioned whatever its size: the rows are the tails of many keys — up to one group
     // per row — and the streaming path's global table would take every one of them by
     // atomics: 4 ms for 8.7 M arena rows of the 1e9-row Zipf step)

@@ -930,6 +930,7 @@ nut_status exec_joinn(nut_ctx *c, const nut_plan &p, const nut_column *const *ta
     for (const PProg &pp : p2.proj_val) used = used || in_prog(pp, ci);
     for (const PProg &pp : p2.proj_mask) used = used || in_prog(pp, ci);
     for (int k2 : p2.keys) used = used || k2 == ci;
+    for (const PProg &kp : p2.key_progs) used = used || in_prog(kp, ci);  // computed GROUP BY keys
     for (const auto &sk : p2.sort_keys) used = used || sk.first == ci;
     for (const PlanPred &pr : p2.preds) used = used || pr.col == ci;
     for (int v : p2.vals) used = used || v == ci;

@@ -230,3 +230,20 @@ def test_subquery_after_join_and_empty_inner(ex):
     got = ex.sql("select count(*) as c from t where not exists (select * from u where uk = k and w > 100 and w < x)",
                  {**on_dev(ex, t), "x": torch.zeros(30_000, dtype=torch.int64, device=ex.device)}, right=[on_dev(ex, u)])
     assert got["c"].tolist() == [30_000]
+
+
+def test_computed_key_after_semi_join(ex):
+    """A computed GROUP BY key (`o_orderdate % 7`) over a plan with a SEMI step: the key's
+    column is gathered through the step's row ids like any other column it reads."""
+    rng = np.random.default_rng(22)
+    no, nl = 50_000, 150_000
+    okey = rng.permutation(no * 2)[:no].astype(np.int64)
+    orders = {"o_orderkey": okey, "o_orderdate": rng.integers(8000, 9000, no).astype(np.int64)}
+    lines = {"l_orderkey": rng.choice(np.concatenate([okey, okey + no * 3]), nl).astype(np.int64)}
+    got = ex.sql("select o_orderdate % 7 as wd, count(*) as n from orders where exists "
+                 "(select * from lineitem where l_orderkey = o_orderkey) group by wd order by wd",
+                 on_dev(ex, orders), right=[on_dev(ex, lines)])
+    do = pd.DataFrame(orders)
+    m = do[do.o_orderkey.isin(set(lines["l_orderkey"]))]
+    g = m.groupby(m.o_orderdate % 7).size()
+    assert got["wd"].tolist() == g.index.tolist() and got["n"].tolist() == g.tolist()
