@@ -1250,6 +1250,7 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
     ha.hagg = (uint64_t *)dheavy + nh;
     ha.count = (uint64_t *)dheavy + nh + (size_t)nh * na;
     ha.chunk = chunk;
+    ha.junk = n;  // (B2 holds n x slack1 + ... rows per array: the junk rows exist)
     c->timer.begin(st, NUT_KERNEL_AGGREGATE);
     hipLaunchKernelGGL(hkern[nv], dim3((unsigned)hgrid), dim3(HK_THREADS), 0, st, ha);
     c->timer.end(st);
@@ -1494,8 +1495,11 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
   // the capped level-1 flags (an exhausted arena), the arenas' fill and the aggregation's
   // control words
   NUT_HIP(hipStreamSynchronize(ax));
-  std::vector<uint64_t> flags(nch);
+  // (everything in gp_meta is read now: the arenas' group-by below may partition, and its
+  // own tables take gp_meta)
+  std::vector<uint64_t> flags(nch), miss(nh);
   NUT_HIP(hipMemcpyAsync(flags.data(), dcur + nparts, nch * 8, hipMemcpyDeviceToHost, st));
+  if (nh) NUT_HIP(hipMemcpyAsync(miss.data(), dmiss, (size_t)nh * 8, hipMemcpyDeviceToHost, st));
   uint32_t ctl[4];
   NUT_HIP(hipMemcpyAsync(c->host_pinned, g->gt.ctl, 16, hipMemcpyDeviceToHost, st));
   NUT_HIP(hipMemcpyAsync(c->host_pinned + 2, darena, 16, hipMemcpyDeviceToHost, st));
@@ -1554,8 +1558,7 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
   if (nh && !over) {
     // heavy keys that joined no region (their level-0 partition was empty, or the region
     // was full): folded here (result words: f64 MIN / MAX back from the table order)
-    std::vector<uint64_t> miss(nh), hw((size_t)nh * na);
-    NUT_HIP(hipMemcpyAsync(miss.data(), dmiss, (size_t)nh * 8, hipMemcpyDeviceToHost, st));
+    std::vector<uint64_t> hw((size_t)nh * na);
     NUT_HIP(hipMemcpyAsync(hw.data(), dheavy + nh, hw.size() * 8, hipMemcpyDeviceToHost, st));
     NUT_HIP(hipStreamSynchronize(st));
     std::vector<int64_t> fk;

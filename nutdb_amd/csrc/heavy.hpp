@@ -36,6 +36,7 @@ struct HkArgs {
   uint32_t h;
   uint64_t *hagg;                     // [h x na] table-encoded words, initialised to agg_init
   uint64_t *count;                    // [gridDim.x] rows each workgroup kept
+  uint64_t junk;                      // rows [junk, junk + gridDim.x) of the outputs: the dropped rows' stores
 };
 
 __device__ __forceinline__ uint32_t hk_hash(uint64_t k) { return (uint32_t)(mix64(k) >> 40) & (HK_SLOTS - 1); }
@@ -163,14 +164,15 @@ __global__ __launch_bounds__(HK_THREADS) void hk_split_kernel(HkArgs a) {
       if (j % NW == wave) before[j / NW] = total;
       total += cj;
     }
+    // every lane stores (a dropped row to this workgroup's junk row): a fixed number of
+    // stores per tile, so the next tile's loads are waited for by count, not by vmcnt(0)
+    // behind this tile's stores
 #pragma unroll
     for (int i = 0; i < HK_ITEMS; ++i) {
-      if (hid[i] == -1) {
-        const uint64_t o = out + before[i] + lane_rank(m[i]);
-        __builtin_nontemporal_store(ck[i], a.okey + o);
+      const uint64_t o = hid[i] == -1 ? out + before[i] + lane_rank(m[i]) : a.junk + blockIdx.x;
+      __builtin_nontemporal_store(ck[i], a.okey + o);
 #pragma unroll
-        for (int c = 0; c < NV; ++c) __builtin_nontemporal_store(cv[i][c], a.oval[c] + o);
-      }
+      for (int c = 0; c < NV; ++c) __builtin_nontemporal_store(cv[i][c], a.oval[c] + o);
     }
     out += total;
     buf ^= 1;  // (the other half of s_off: the next tile's counts cannot overwrite these before every wave read them)
