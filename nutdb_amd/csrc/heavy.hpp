@@ -119,34 +119,39 @@ __global__ __launch_bounds__(HK_THREADS) void hk_split_kernel(HkArgs a) {
 #pragma unroll
       for (int i = 0; i < HK_ITEMS; ++i) any = any || act[i];
       if (!__any(any)) break;
+      // every item's slot read, unconditionally (an inactive item re-reads its last slot),
+      // so the 16 LDS reads issue back to back and are waited for once; then the updates,
+      // branch-free
+      uint32_t sj[HK_ITEMS];
+      uint64_t sk[HK_ITEMS];
 #pragma unroll
       for (int i = 0; i < HK_ITEMS; ++i) {
-        if (!act[i]) continue;
-        const uint32_t j = s_slot[q[i]];
-        const uint64_t sk = s_skey[q[i]];
-        if (!j) {
-          act[i] = false;
-        } else if (sk == ck[i]) {
-          hid[i] = (int)j - 1;
-          act[i] = false;
-        } else {
-          q[i] = (q[i] + 1) & (HK_SLOTS - 1);
-        }
+        sj[i] = s_slot[q[i]];
+        sk[i] = s_skey[q[i]];
+      }
+#pragma unroll
+      for (int i = 0; i < HK_ITEMS; ++i) {
+        const bool hit = act[i] && sj[i] != 0 && sk[i] == ck[i];
+        hid[i] = hit ? (int)sj[i] - 1 : hid[i];
+        const bool more = act[i] && sj[i] != 0 && !hit;
+        q[i] = more ? (q[i] + 1) & (HK_SLOTS - 1) : q[i];
+        act[i] = more;
       }
     }
+    // the heavy rows into the accumulators: aggregate by aggregate (one kind dispatch per
+    // aggregate and tile), every item inside
+    for (int g = 0; g < a.na; ++g) {
+      const int ag = a.arg[g];
+      with_kind(a.kind[g], [&](auto KC) {
+        constexpr int K = decltype(KC)::value;
 #pragma unroll
-    for (int i = 0; i < HK_ITEMS; ++i) {
-      if (hid[i] >= 0) {
-        for (int g = 0; g < a.na; ++g) {
+        for (int i = 0; i < HK_ITEMS; ++i) {
           uint64_t x = 0;
 #pragma unroll
-          for (int c = 0; c < NV; ++c) x = a.arg[g] == c ? cv[i][c] : x;
-          with_kind(a.kind[g], [&](auto KC) {
-            constexpr int K = decltype(KC)::value;
-            fold_atomic<K>(&s_acc[hid[i] * a.na + g], x);
-          });
+          for (int c = 0; c < NV; ++c) x = ag == c ? cv[i][c] : x;
+          if (hid[i] >= 0) fold_atomic<K>(&s_acc[hid[i] * a.na + g], x);
         }
-      }
+      });
     }
     // compaction: the kept rows of item i, wave w go to one run (offsets: an exclusive scan
     // of the 32 counts, every thread reading them — no serial section)
