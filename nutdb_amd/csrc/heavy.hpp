@@ -57,8 +57,10 @@ __device__ __forceinline__ void combine_atomic(uint64_t *w, uint64_t x) {
 // and hands the level-0 scatter one segment per workgroup).  Within a tile the kept rows of
 // (item, wave) pairs get consecutive runs; the next tile's rows are loaded before this
 // tile's are looked up.  NV: value arrays (registers for two tiles of them: a template, so
-// one value array takes ~80 VGPRs, not the 206 that four would).
-template <int NV>
+// one value array takes ~80 VGPRs, not the 206 that four would).  VAR: tuning variants for
+// scripts/tune/hk_tune.hip (bit 0 no lookups, bit 1 no accumulator atomics, bit 2 no
+// stores); the product runs VAR = 0.
+template <int NV, int VAR = 0>
 __global__ __launch_bounds__(HK_THREADS) void hk_split_kernel(HkArgs a) {
   __shared__ uint16_t s_slot[HK_SLOTS];  // heavy key index + 1 (0: empty)
   __shared__ uint64_t s_skey[HK_SLOTS];  // the slot's key (read with its index: one round trip per probe)
@@ -111,7 +113,7 @@ __global__ __launch_bounds__(HK_THREADS) void hk_split_kernel(HkArgs a) {
     for (int i = 0; i < HK_ITEMS; ++i) {
       const bool in = t * HK_TILE + (uint64_t)i * HK_THREADS + tid < a.n;
       hid[i] = in ? -1 : -2;  // -2: past the end
-      act[i] = in;
+      act[i] = in && !(VAR & 1);
       q[i] = hk_hash(ck[i]);
     }
     for (;;) {
@@ -149,7 +151,7 @@ __global__ __launch_bounds__(HK_THREADS) void hk_split_kernel(HkArgs a) {
           uint64_t x = 0;
 #pragma unroll
           for (int c = 0; c < NV; ++c) x = ag == c ? cv[i][c] : x;
-          if (hid[i] >= 0) fold_atomic<K>(&s_acc[hid[i] * a.na + g], x);
+          if (!(VAR & 2) && hid[i] >= 0) fold_atomic<K>(&s_acc[hid[i] * a.na + g], x);
         }
       });
     }
@@ -173,7 +175,7 @@ __global__ __launch_bounds__(HK_THREADS) void hk_split_kernel(HkArgs a) {
     // stores per tile, so the next tile's loads are waited for by count, not by vmcnt(0)
     // behind this tile's stores
 #pragma unroll
-    for (int i = 0; i < HK_ITEMS; ++i) {
+    for (int i = 0; i < HK_ITEMS && !(VAR & 4); ++i) {
       const uint64_t o = hid[i] == -1 ? out + before[i] + lane_rank(m[i]) : a.junk + blockIdx.x;
       __builtin_nontemporal_store(ck[i], a.okey + o);
 #pragma unroll
