@@ -1145,6 +1145,8 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
   // hold >= 5 % of the sample, the <= HK_MAX most frequent are aggregated in one streaming
   // pass and the other rows, compacted into B2, are what the levels partition.
   std::vector<int64_t> hkeys;
+  std::vector<uint16_t> hslot;
+  uint64_t hseed1 = 0, hseed2 = 0;
   if (c->opt[NUT_OPT_GB_HEAVY] != 0) {
     std::vector<std::pair<uint32_t, int64_t>> cand;  // (sample count, key)
     for (uint32_t q = 0; q < kSlots; ++q)
@@ -1159,6 +1161,16 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
     if (cover * 20 >= kSample) {
       for (const auto &x : cand) hkeys.push_back(x.second);
       std::sort(hkeys.begin(), hkeys.end());
+      // the pass's lookup table: a cuckoo table (two slots per key) built here, so every
+      // lookup is two reads; new seeds if a key finds no place (at load <= 1/4, rare)
+      hslot.assign(HK_SLOTS, 0);
+      bool placed = false;
+      for (uint64_t attempt = 0; attempt < 8 && !placed; ++attempt) {
+        hseed1 = mix64(0x9E3779B97F4A7C15ull + 2 * attempt);
+        hseed2 = mix64(0x9E3779B97F4A7C15ull + 2 * attempt + 1);
+        placed = hk_cuckoo(hkeys.data(), (uint32_t)hkeys.size(), hseed1, hseed2, hslot.data());
+      }
+      if (!placed) hkeys.clear();  // (the overflow arenas take them)
     }
   }
   // level-1 regions: the even share x slack1 (six standard deviations of a Poisson count
@@ -1222,9 +1234,11 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
     const uint64_t ntiles = (n + HK_TILE - 1) / HK_TILE;
     const uint64_t hgrid = std::min<uint64_t>(ntiles, (uint64_t)c->num_cus * per_cu);
     const uint64_t chunk = (ntiles + hgrid - 1) / hgrid;
-    // [keys (h), aggregates (h x na), kept rows per workgroup (hgrid)]
-    std::vector<uint64_t> init(nh + (size_t)nh * na + hgrid, 0);
+    // [keys (h), aggregates (h x na), kept rows per workgroup (hgrid), cuckoo slots]
+    const size_t slot0 = nh + (size_t)nh * na + hgrid;
+    std::vector<uint64_t> init(slot0 + HK_SLOTS / 4, 0);
     memcpy(&init[0], hkeys.data(), (size_t)nh * 8);
+    memcpy(&init[slot0], hslot.data(), HK_SLOTS * 2);
     for (uint32_t j = 0; j < nh; ++j)
       for (int a = 0; a < na; ++a) init[nh + (size_t)j * na + a] = agg_init(g->kinds[a]);
     NUT_HIP(hipMallocAsync((void **)&dheavy, init.size() * 8, st));
@@ -1246,6 +1260,9 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
       ha.arg[a] = s->agg_op[a] == NUT_AGG_COUNT ? 0 : vmap[s->agg_arg[a][0]];
     }
     ha.hk = (const int64_t *)dheavy;
+    ha.slot = (const uint16_t *)((uint64_t *)dheavy + slot0);
+    ha.seed1 = hseed1;
+    ha.seed2 = hseed2;
     ha.h = nh;
     ha.hagg = (uint64_t *)dheavy + nh;
     ha.count = (uint64_t *)dheavy + nh + (size_t)nh * na;

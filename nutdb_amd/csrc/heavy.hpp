@@ -19,7 +19,7 @@ namespace nut {
 constexpr int HK_THREADS = 256, HK_ITEMS = 8;
 constexpr uint32_t HK_TILE = HK_THREADS * HK_ITEMS;  // rows per tile
 constexpr int HK_MAX = 1024;                         // heavy keys at most
-constexpr int HK_SLOTS = 2048;                       // LDS hash set (load <= 1/2)
+constexpr int HK_SLOTS = 4096;                       // cuckoo slots (load <= 1/4), host-built
 constexpr int HK_WORDS = 2048;                       // heavy keys x aggregates at most (16 KB)
 
 struct HkArgs {
@@ -33,13 +33,40 @@ struct HkArgs {
   int32_t kind[NUT_MAX_AGGS];         // aggregate kinds (AggKind)
   int32_t arg[NUT_MAX_AGGS];          // value array of each aggregate (COUNT: unused)
   const int64_t *hk;                  // the heavy keys (h of them)
+  const uint16_t *slot;               // [HK_SLOTS] cuckoo table: key index + 1 (0: empty), hk_slot1 / hk_slot2
+  uint64_t seed1, seed2;
   uint32_t h;
   uint64_t *hagg;                     // [h x na] table-encoded words, initialised to agg_init
   uint64_t *count;                    // [gridDim.x] rows each workgroup kept
   uint64_t junk;                      // rows [junk, junk + gridDim.x) of the outputs: the dropped rows' stores
 };
 
-__device__ __forceinline__ uint32_t hk_hash(uint64_t k) { return (uint32_t)(mix64(k) >> 40) & (HK_SLOTS - 1); }
+// a key's two cuckoo slots (the host places every heavy key in one of them: hk_cuckoo)
+__host__ __device__ __forceinline__ uint32_t hk_slot(uint64_t k, uint64_t seed) {
+  return (uint32_t)(mix64(k ^ seed) >> 52) & (HK_SLOTS - 1);
+}
+
+// host: a cuckoo table of the h keys (slot = key index + 1); false if some key found no
+// place (the caller retries with other seeds)
+inline bool hk_cuckoo(const int64_t *hk, uint32_t h, uint64_t s1, uint64_t s2, uint16_t *slot) {
+  for (int i = 0; i < HK_SLOTS; ++i) slot[i] = 0;
+  for (uint32_t j = 0; j < h; ++j) {
+    uint16_t cur = (uint16_t)(j + 1);
+    uint32_t pos = hk_slot((uint64_t)hk[j], s1);
+    int steps = 0;
+    for (;;) {
+      const uint16_t old = slot[pos];
+      slot[pos] = cur;
+      if (!old) break;
+      if (++steps > 1000) return false;
+      cur = old;  // the evicted key moves to its other slot
+      const uint64_t k = (uint64_t)hk[old - 1];
+      const uint32_t a = hk_slot(k, s1), b = hk_slot(k, s2);
+      pos = pos == a ? b : a;
+    }
+  }
+  return true;
+}
 
 // combine an accumulator word into a shared one (both table-encoded)
 template <int K>
@@ -62,23 +89,15 @@ __device__ __forceinline__ void combine_atomic(uint64_t *w, uint64_t x) {
 // stores); the product runs VAR = 0.
 template <int NV, int VAR = 0>
 __global__ __launch_bounds__(HK_THREADS) void hk_split_kernel(HkArgs a) {
-  __shared__ uint16_t s_slot[HK_SLOTS];  // heavy key index + 1 (0: empty)
-  __shared__ uint64_t s_skey[HK_SLOTS];  // the slot's key (read with its index: one round trip per probe)
+  __shared__ uint16_t s_slot[HK_SLOTS];  // cuckoo table: heavy key index + 1 (0: empty)
+  __shared__ uint64_t s_key[HK_MAX];
   __shared__ uint64_t s_acc[HK_WORDS];
   __shared__ uint32_t s_off[2][HK_ITEMS * (HK_THREADS / 64)];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   constexpr int NW = HK_THREADS / 64;
-  for (int i = tid; i < HK_SLOTS; i += HK_THREADS) s_slot[i] = 0;
+  for (int i = tid; i < HK_SLOTS; i += HK_THREADS) s_slot[i] = a.slot[i];
+  for (uint32_t i = tid; i < a.h; i += HK_THREADS) s_key[i] = (uint64_t)a.hk[i];
   for (uint32_t i = tid; i < a.h * (uint32_t)a.na; i += HK_THREADS) s_acc[i] = agg_init(a.kind[i % a.na]);
-  __syncthreads();
-  if (tid == 0) {  // (h <= HK_MAX keys into 2048 slots: linear probing always finds room)
-    for (uint32_t j = 0; j < a.h; ++j) {
-      uint32_t q = hk_hash((uint64_t)a.hk[j]);
-      while (s_slot[q]) q = (q + 1) & (HK_SLOTS - 1);
-      s_slot[q] = (uint16_t)(j + 1);
-      s_skey[q] = (uint64_t)a.hk[j];
-    }
-  }
   __syncthreads();
   const uint64_t ntiles = (a.n + HK_TILE - 1) / HK_TILE;
   const uint64_t t0 = (uint64_t)blockIdx.x * a.chunk, t1 = min(ntiles, t0 + a.chunk);
@@ -104,41 +123,20 @@ __global__ __launch_bounds__(HK_THREADS) void hk_split_kernel(HkArgs a) {
       for (int c = 0; c < NV; ++c) cv[i][c] = v[i][c];
     }
     if (t + 1 < t1) load(t + 1);
-    // lookups in probe rounds over all items at once (each round's 8 LDS reads in flight
-    // together, instead of each item's probe chain one read after another)
+    // lookups: a key's two cuckoo slots, then the keys they name — two rounds of 16 LDS
+    // reads for all 8 rows of a lane, no probe loop
     int hid[HK_ITEMS];
-    uint32_t q[HK_ITEMS];
-    bool act[HK_ITEMS];
+    uint32_t j1[HK_ITEMS], j2[HK_ITEMS];
 #pragma unroll
     for (int i = 0; i < HK_ITEMS; ++i) {
-      const bool in = t * HK_TILE + (uint64_t)i * HK_THREADS + tid < a.n;
-      hid[i] = in ? -1 : -2;  // -2: past the end
-      act[i] = in && !(VAR & 1);
-      q[i] = hk_hash(ck[i]);
+      j1[i] = (VAR & 1) ? 0u : s_slot[hk_slot(ck[i], a.seed1)];
+      j2[i] = (VAR & 1) ? 0u : s_slot[hk_slot(ck[i], a.seed2)];
     }
-    for (;;) {
-      bool any = false;
 #pragma unroll
-      for (int i = 0; i < HK_ITEMS; ++i) any = any || act[i];
-      if (!__any(any)) break;
-      // every item's slot read, unconditionally (an inactive item re-reads its last slot),
-      // so the 16 LDS reads issue back to back and are waited for once; then the updates,
-      // branch-free
-      uint32_t sj[HK_ITEMS];
-      uint64_t sk[HK_ITEMS];
-#pragma unroll
-      for (int i = 0; i < HK_ITEMS; ++i) {
-        sj[i] = s_slot[q[i]];
-        sk[i] = s_skey[q[i]];
-      }
-#pragma unroll
-      for (int i = 0; i < HK_ITEMS; ++i) {
-        const bool hit = act[i] && sj[i] != 0 && sk[i] == ck[i];
-        hid[i] = hit ? (int)sj[i] - 1 : hid[i];
-        const bool more = act[i] && sj[i] != 0 && !hit;
-        q[i] = more ? (q[i] + 1) & (HK_SLOTS - 1) : q[i];
-        act[i] = more;
-      }
+    for (int i = 0; i < HK_ITEMS; ++i) {
+      const uint64_t k1 = s_key[j1[i] ? j1[i] - 1 : 0], k2 = s_key[j2[i] ? j2[i] - 1 : 0];
+      const bool in = t * HK_TILE + (uint64_t)i * HK_THREADS + tid < a.n;
+      hid[i] = !in ? -2 : (j1[i] && k1 == ck[i]) ? (int)j1[i] - 1 : (j2[i] && k2 == ck[i]) ? (int)j2[i] - 1 : -1;
     }
     // the heavy rows into the accumulators: aggregate by aggregate (one kind dispatch per
     // aggregate and tile), every item inside

@@ -38,7 +38,8 @@ __global__ void copy2(const uint64_t *a, const uint64_t *b, uint64_t *c, uint64_
 }
 
 struct Ctx {
-  uint64_t n, *k, *v, *ok, *ov, *hk, *hagg, *cnt;
+  uint64_t n, *k, *v, *ok, *ov, *hk, *hagg, *cnt, s1, s2;
+  uint16_t *slot;
   uint32_t h;
   int ncu;
   hipEvent_t e0, e1;
@@ -63,6 +64,9 @@ static void run(Ctx &c, const char *name, uint32_t h) {
   a.kind[0] = nut::AK_SUM_F64;
   a.arg[0] = 0;
   a.hk = (const int64_t *)c.hk;
+  a.slot = c.slot;
+  a.seed1 = c.s1;
+  a.seed2 = c.s2;
   a.h = h;
   a.hagg = c.hagg;
   a.count = c.cnt;
@@ -97,6 +101,7 @@ int main(int argc, char **argv) {
   CK(hipMalloc(&c.hk, nut::HK_MAX * 8));
   CK(hipMalloc(&c.hagg, nut::HK_MAX * 8));
   CK(hipMalloc(&c.cnt, 65536 * 8));
+  CK(hipMalloc(&c.slot, nut::HK_SLOTS * 2));
   CK(hipEventCreate(&c.e0));
   CK(hipEventCreate(&c.e1));
   for (int skew = 1; skew >= 0; --skew) {
@@ -119,6 +124,11 @@ int main(int argc, char **argv) {
     std::sort(hk.begin(), hk.end(), [](uint64_t a, uint64_t b) { return (int64_t)a < (int64_t)b; });
     c.h = (uint32_t)hk.size();
     if (c.h) CK(hipMemcpy(c.hk, hk.data(), c.h * 8, hipMemcpyHostToDevice));
+    std::vector<uint16_t> slot(nut::HK_SLOTS);
+    c.s1 = nut::mix64(0x9E3779B97F4A7C15ull);
+    c.s2 = nut::mix64(0x9E3779B97F4A7C16ull);
+    if (!nut::hk_cuckoo((const int64_t *)hk.data(), c.h, c.s1, c.s2, slot.data())) printf("cuckoo build failed\n");
+    CK(hipMemcpy(c.slot, slot.data(), nut::HK_SLOTS * 2, hipMemcpyHostToDevice));
     printf("%s keys: %u heavy\n", skew ? "Zipf-like" : "uniform", c.h);
     float best = 1e9;
     for (int r = 0; r < 3; ++r) {
