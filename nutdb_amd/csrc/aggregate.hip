@@ -1266,8 +1266,7 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
     ha.h = nh;
     ha.hagg = (uint64_t *)dheavy + nh;
     ha.count = (uint64_t *)dheavy + nh + (size_t)nh * na;
-    ha.chunk = chunk;
-    ha.junk = n;  // (B2 holds n x slack1 + ... rows per array: the junk rows exist)
+    ha.chunk = chunk;  // (the chunks' regions end by n + chunk x HK_TILE rows: B2 holds n x slack1 + ...)
     c->timer.begin(st, NUT_KERNEL_AGGREGATE);
     hipLaunchKernelGGL(hkern[nv], dim3((unsigned)hgrid), dim3(HK_THREADS), 0, st, ha);
     c->timer.end(st);

@@ -38,7 +38,6 @@ struct HkArgs {
   uint32_t h;
   uint64_t *hagg;                     // [h x na] table-encoded words, initialised to agg_init
   uint64_t *count;                    // [gridDim.x] rows each workgroup kept
-  uint64_t junk;                      // rows [junk, junk + gridDim.x) of the outputs: the dropped rows' stores
 };
 
 // a key's two cuckoo slots (the host places every heavy key in one of them: hk_cuckoo)
@@ -92,7 +91,7 @@ __global__ __launch_bounds__(HK_THREADS) void hk_split_kernel(HkArgs a) {
   __shared__ uint16_t s_slot[HK_SLOTS];  // cuckoo table: heavy key index + 1 (0: empty)
   __shared__ uint64_t s_key[HK_MAX];
   __shared__ uint64_t s_acc[HK_WORDS];
-  __shared__ uint32_t s_off[2][HK_ITEMS * (HK_THREADS / 64)];
+  __shared__ uint32_t s_off[2][2][HK_ITEMS * (HK_THREADS / 64)];  // [buffer][kept, dropped][item x wave]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   constexpr int NW = HK_THREADS / 64;
   for (int i = tid; i < HK_SLOTS; i += HK_THREADS) s_slot[i] = a.slot[i];
@@ -101,7 +100,8 @@ __global__ __launch_bounds__(HK_THREADS) void hk_split_kernel(HkArgs a) {
   __syncthreads();
   const uint64_t ntiles = (a.n + HK_TILE - 1) / HK_TILE;
   const uint64_t t0 = (uint64_t)blockIdx.x * a.chunk, t1 = min(ntiles, t0 + a.chunk);
-  uint64_t out = t0 * HK_TILE;  // this workgroup's next output row
+  uint64_t out = t0 * HK_TILE;                 // this workgroup's next kept row (from the chunk's start)
+  uint64_t back = (t0 + a.chunk) * HK_TILE;    // ... and its next dropped row (down from the chunk's end)
   uint64_t k[HK_ITEMS], v[HK_ITEMS][NV];
   auto load = [&](uint64_t t) {
 #pragma unroll
@@ -153,32 +153,38 @@ __global__ __launch_bounds__(HK_THREADS) void hk_split_kernel(HkArgs a) {
         }
       });
     }
-    // compaction: the kept rows of item i, wave w go to one run (offsets: an exclusive scan
-    // of the 32 counts, every thread reading them — no serial section)
-    uint64_t m[HK_ITEMS];
+    // compaction: the kept rows of item i, wave w go to one run from the chunk's start, the
+    // dropped ones (heavy or past the end) to one run down from its end — every lane stores
+    // (a fixed number of stores per tile, so the next tile's loads are waited for by count),
+    // and no two lanes store to one address (one junk row for every dropped row had 1024
+    // workgroups writing the same lines: 21 vs 6 ms)
+    uint64_t m[HK_ITEMS], dm[HK_ITEMS];
 #pragma unroll
     for (int i = 0; i < HK_ITEMS; ++i) {
       m[i] = __ballot(hid[i] == -1);
-      if (lane == 0) s_off[buf][i * NW + wave] = (uint32_t)__popcll(m[i]);
+      dm[i] = __ballot(hid[i] != -1);
+      if (lane == 0) {
+        s_off[buf][0][i * NW + wave] = (uint32_t)__popcll(m[i]);
+        s_off[buf][1][i * NW + wave] = (uint32_t)__popcll(dm[i]);
+      }
     }
     __syncthreads();
-    uint32_t before[HK_ITEMS], total = 0;
+    uint32_t before[HK_ITEMS], dbefore[HK_ITEMS], total = 0, dtotal = 0;
 #pragma unroll
     for (int j = 0; j < HK_ITEMS * NW; ++j) {
-      const uint32_t cj = s_off[buf][j];
-      if (j % NW == wave) before[j / NW] = total;
+      const uint32_t cj = s_off[buf][0][j], dj = s_off[buf][1][j];
+      if (j % NW == wave) before[j / NW] = total, dbefore[j / NW] = dtotal;
       total += cj;
+      dtotal += dj;
     }
-    // every lane stores (a dropped row to this workgroup's junk row): a fixed number of
-    // stores per tile, so the next tile's loads are waited for by count, not by vmcnt(0)
-    // behind this tile's stores
 #pragma unroll
     for (int i = 0; i < HK_ITEMS && !(VAR & 4); ++i) {
-      const uint64_t o = hid[i] == -1 ? out + before[i] + lane_rank(m[i]) : a.junk + blockIdx.x;
+      const uint64_t o = hid[i] == -1 ? out + before[i] + lane_rank(m[i]) : back - 1 - dbefore[i] - lane_rank(dm[i]);
       __builtin_nontemporal_store(ck[i], a.okey + o);
 #pragma unroll
       for (int c = 0; c < NV; ++c) __builtin_nontemporal_store(cv[i][c], a.oval[c] + o);
     }
+    back -= dtotal;
     out += total;
     buf ^= 1;  // (the other half of s_off: the next tile's counts cannot overwrite these before every wave read them)
   }

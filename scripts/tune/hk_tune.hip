@@ -70,7 +70,6 @@ static void run(Ctx &c, const char *name, uint32_t h) {
   a.h = h;
   a.hagg = c.hagg;
   a.count = c.cnt;
-  a.junk = c.n;
   float best = 1e9;
   for (int r = 0; r < 3; ++r) {
     CK(hipEventRecord(c.e0));
@@ -96,8 +95,8 @@ int main(int argc, char **argv) {
   CK(hipDeviceGetAttribute(&c.ncu, hipDeviceAttributeMultiprocessorCount, 0));
   CK(hipMalloc(&c.k, c.n * 8));
   CK(hipMalloc(&c.v, c.n * 8));
-  CK(hipMalloc(&c.ok, (c.n + 4096) * 8));
-  CK(hipMalloc(&c.ov, (c.n + 4096) * 8));
+  CK(hipMalloc(&c.ok, (c.n + (8ull << 20)) * 8));
+  CK(hipMalloc(&c.ov, (c.n + (8ull << 20)) * 8));
   CK(hipMalloc(&c.hk, nut::HK_MAX * 8));
   CK(hipMalloc(&c.hagg, nut::HK_MAX * 8));
   CK(hipMalloc(&c.cnt, 65536 * 8));
