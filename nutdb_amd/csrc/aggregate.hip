@@ -1140,8 +1140,9 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
     if (s->agg_op[a] != NUT_AGG_COUNT && vmap[s->agg_arg[a][0]] < 0) vmap[s->agg_arg[a][0]] = nv++;
   const int narr = 3 + nv, nstore = narr - 2;
   const uint64_t rows = (n + 2 * 65536 + 64 + 31) & ~31ull;
-  // ---- heavy keys (heavy.hpp): a key the sample saw >= 4 times (>= ~1/16000 of the rows:
-  // a whole level-1 partition's share) would overflow its partition.  When such keys
+  // ---- heavy keys (heavy.hpp): a key the sample saw >= 3 times (expected rows >= ~1/22000
+  // of the rows, most of a level-1 partition's share; a key of twice that share is still
+  // sampled < 3 times one time in ten) would overflow its partition.  When such keys
   // hold >= 5 % of the sample, the <= HK_MAX most frequent are aggregated in one streaming
   // pass and the other rows, compacted into B2, are what the levels partition.
   std::vector<int64_t> hkeys;
@@ -1150,7 +1151,7 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
   if (c->opt[NUT_OPT_GB_HEAVY] != 0) {
     std::vector<std::pair<uint32_t, int64_t>> cand;  // (sample count, key)
     for (uint32_t q = 0; q < kSlots; ++q)
-      if (tc[q] >= 4) cand.emplace_back(tc[q], tk[q]);
+      if (tc[q] >= 3) cand.emplace_back(tc[q], tk[q]);
     std::sort(cand.begin(), cand.end(), [](const auto &x, const auto &y) {
       return x.first > y.first || (x.first == y.first && x.second < y.second);
     });

@@ -18,8 +18,8 @@ namespace nut {
 
 constexpr int HK_THREADS = 256, HK_ITEMS = 8;
 constexpr uint32_t HK_TILE = HK_THREADS * HK_ITEMS;  // rows per tile
-constexpr int HK_MAX = 1024;                         // heavy keys at most
-constexpr int HK_SLOTS = 4096;                       // cuckoo slots (load <= 1/4), host-built
+constexpr int HK_MAX = 2048;                         // heavy keys at most
+constexpr int HK_SLOTS = 8192;                       // cuckoo slots (load <= 1/4), host-built
 constexpr int HK_WORDS = 2048;                       // heavy keys x aggregates at most (16 KB)
 
 struct HkArgs {
@@ -42,7 +42,7 @@ struct HkArgs {
 
 // a key's two cuckoo slots (the host places every heavy key in one of them: hk_cuckoo)
 __host__ __device__ __forceinline__ uint32_t hk_slot(uint64_t k, uint64_t seed) {
-  return (uint32_t)(mix64(k ^ seed) >> 52) & (HK_SLOTS - 1);
+  return (uint32_t)(mix64(k ^ seed) >> 32) & (HK_SLOTS - 1);
 }
 
 // host: a cuckoo table of the h keys (slot = key index + 1); false if some key found no

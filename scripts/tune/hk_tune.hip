@@ -115,7 +115,7 @@ int main(int argc, char **argv) {
     }
     std::vector<std::pair<uint32_t, uint64_t>> cand;
     for (auto &kv : cnt)
-      if (kv.second >= 4) cand.emplace_back(kv.second, kv.first);
+      if (kv.second >= 3) cand.emplace_back(kv.second, kv.first);
     std::sort(cand.rbegin(), cand.rend());
     if (cand.size() > (size_t)nut::HK_MAX) cand.resize(nut::HK_MAX);
     std::vector<uint64_t> hk;
