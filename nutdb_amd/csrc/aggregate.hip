@@ -1235,6 +1235,7 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
     const uint64_t ntiles = (n + HK_TILE - 1) / HK_TILE;
     const uint64_t hgrid = std::min<uint64_t>(ntiles, (uint64_t)c->num_cus * per_cu);
     const uint64_t chunk = (ntiles + hgrid - 1) / hgrid;
+    if (chunk * HK_TILE * 8 >= (1ull << 32)) return decline(NUT_GB_DECLINE_CAPACITY);  // (a chunk's buffer resource)
     // [keys (h), aggregates (h x na), kept rows per workgroup (hgrid), cuckoo slots]
     const size_t slot0 = nh + (size_t)nh * na + hgrid;
     std::vector<uint64_t> init(slot0 + HK_SLOTS / 4, 0);
@@ -1267,7 +1268,7 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
     ha.h = nh;
     ha.hagg = (uint64_t *)dheavy + nh;
     ha.count = (uint64_t *)dheavy + nh + (size_t)nh * na;
-    ha.chunk = chunk;  // (the chunks' regions end by n + chunk x HK_TILE rows: B2 holds n x slack1 + ...)
+    ha.chunk = chunk;
     c->timer.begin(st, NUT_KERNEL_AGGREGATE);
     hipLaunchKernelGGL(hkern[nv], dim3((unsigned)hgrid), dim3(HK_THREADS), 0, st, ha);
     c->timer.end(st);

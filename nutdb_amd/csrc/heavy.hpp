@@ -67,6 +67,17 @@ inline bool hk_cuckoo(const int64_t *hk, uint32_t h, uint64_t s1, uint64_t s2, u
   return true;
 }
 
+// a raw buffer resource over `bytes` bytes from p (stride 0; stores past `bytes` are
+// discarded by the bounds check — how a dropped row's store writes nothing)
+typedef unsigned int hk_u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t hk_rsrc(void *p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(p, (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ void hk_store(uint64_t v, __amdgpu_buffer_rsrc_t r, uint32_t off) {
+  const hk_u32x2 w = {(uint32_t)v, (uint32_t)(v >> 32)};
+  __builtin_amdgcn_raw_buffer_store_b64(w, r, (int)off, 0, 2);  // (glc 0, slc 1: non-temporal)
+}
+
 // combine an accumulator word into a shared one (both table-encoded)
 template <int K>
 __device__ __forceinline__ void combine_atomic(uint64_t *w, uint64_t x) {
@@ -91,7 +102,7 @@ __global__ __launch_bounds__(HK_THREADS) void hk_split_kernel(HkArgs a) {
   __shared__ uint16_t s_slot[HK_SLOTS];  // cuckoo table: heavy key index + 1 (0: empty)
   __shared__ uint64_t s_key[HK_MAX];
   __shared__ uint64_t s_acc[HK_WORDS];
-  __shared__ uint32_t s_off[2][2][HK_ITEMS * (HK_THREADS / 64)];  // [buffer][kept, dropped][item x wave]
+  __shared__ uint32_t s_off[2][HK_ITEMS * (HK_THREADS / 64)];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   constexpr int NW = HK_THREADS / 64;
   for (int i = tid; i < HK_SLOTS; i += HK_THREADS) s_slot[i] = a.slot[i];
@@ -100,8 +111,13 @@ __global__ __launch_bounds__(HK_THREADS) void hk_split_kernel(HkArgs a) {
   __syncthreads();
   const uint64_t ntiles = (a.n + HK_TILE - 1) / HK_TILE;
   const uint64_t t0 = (uint64_t)blockIdx.x * a.chunk, t1 = min(ntiles, t0 + a.chunk);
-  uint64_t out = t0 * HK_TILE;                 // this workgroup's next kept row (from the chunk's start)
-  uint64_t back = (t0 + a.chunk) * HK_TILE;    // ... and its next dropped row (down from the chunk's end)
+  uint64_t out = 0;  // this workgroup's next kept row, from its chunk's start
+  // the chunk's output rows as buffer resources (< 2^32 bytes: the host checks)
+  const uint32_t cbytes = (uint32_t)(a.chunk * HK_TILE * 8);
+  const __amdgpu_buffer_rsrc_t rk = hk_rsrc(a.okey + t0 * HK_TILE, cbytes);
+  __amdgpu_buffer_rsrc_t rv[NV > 0 ? NV : 1];
+#pragma unroll
+  for (int c = 0; c < NV; ++c) rv[c] = hk_rsrc(a.oval[c] + t0 * HK_TILE, cbytes);
   uint64_t k[HK_ITEMS], v[HK_ITEMS][NV];
   auto load = [&](uint64_t t) {
 #pragma unroll
@@ -153,42 +169,35 @@ __global__ __launch_bounds__(HK_THREADS) void hk_split_kernel(HkArgs a) {
         }
       });
     }
-    // compaction: the kept rows of item i, wave w go to one run from the chunk's start, the
-    // dropped ones (heavy or past the end) to one run down from its end — every lane stores
-    // (a fixed number of stores per tile, so the next tile's loads are waited for by count),
-    // and no two lanes store to one address (one junk row for every dropped row had 1024
-    // workgroups writing the same lines: 21 vs 6 ms)
-    uint64_t m[HK_ITEMS], dm[HK_ITEMS];
+    // compaction: the kept rows of item i, wave w go to one run; every lane stores (a fixed
+    // number of stores per tile, so the next tile's loads are waited for by count, not by
+    // vmcnt(0) behind this tile's stores), a dropped row (heavy, or past the end) at an
+    // offset past the buffer, so its store writes nothing
+    uint64_t m[HK_ITEMS];
 #pragma unroll
     for (int i = 0; i < HK_ITEMS; ++i) {
       m[i] = __ballot(hid[i] == -1);
-      dm[i] = __ballot(hid[i] != -1);
-      if (lane == 0) {
-        s_off[buf][0][i * NW + wave] = (uint32_t)__popcll(m[i]);
-        s_off[buf][1][i * NW + wave] = (uint32_t)__popcll(dm[i]);
-      }
+      if (lane == 0) s_off[buf][i * NW + wave] = (uint32_t)__popcll(m[i]);
     }
     __syncthreads();
-    uint32_t before[HK_ITEMS], dbefore[HK_ITEMS], total = 0, dtotal = 0;
+    uint32_t before[HK_ITEMS], total = 0;
 #pragma unroll
     for (int j = 0; j < HK_ITEMS * NW; ++j) {
-      const uint32_t cj = s_off[buf][0][j], dj = s_off[buf][1][j];
-      if (j % NW == wave) before[j / NW] = total, dbefore[j / NW] = dtotal;
+      const uint32_t cj = s_off[buf][j];
+      if (j % NW == wave) before[j / NW] = total;
       total += cj;
-      dtotal += dj;
     }
 #pragma unroll
     for (int i = 0; i < HK_ITEMS && !(VAR & 4); ++i) {
-      const uint64_t o = hid[i] == -1 ? out + before[i] + lane_rank(m[i]) : back - 1 - dbefore[i] - lane_rank(dm[i]);
-      __builtin_nontemporal_store(ck[i], a.okey + o);
+      const uint32_t o = hid[i] == -1 ? (uint32_t)(out + before[i] + lane_rank(m[i])) * 8u : 0xFFFFFFF0u;
+      hk_store(ck[i], rk, o);
 #pragma unroll
-      for (int c = 0; c < NV; ++c) __builtin_nontemporal_store(cv[i][c], a.oval[c] + o);
+      for (int c = 0; c < NV; ++c) hk_store(cv[i][c], rv[c], o);
     }
-    back -= dtotal;
     out += total;
     buf ^= 1;  // (the other half of s_off: the next tile's counts cannot overwrite these before every wave read them)
   }
-  if (tid == 0) a.count[blockIdx.x] = out - t0 * HK_TILE;
+  if (tid == 0) a.count[blockIdx.x] = out;
   __syncthreads();
   // this workgroup's heavy accumulators into the device words
   for (uint32_t i = tid; i < a.h * (uint32_t)a.na; i += HK_THREADS) {
