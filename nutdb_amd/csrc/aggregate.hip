@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "agg_kernel.hpp"
@@ -987,6 +988,8 @@ bool host_pinned_ptr(const void *p) {
 // wrap-add, MIN / MAX of f64 in the tables' total order: -0 < +0, NaN above +inf), the rest
 // are merged in by one backward pass of block moves.  Returns the new count; *over when it
 // exceeds cap (the caller then fails the call: equal keys may already be combined).
+constexpr int kFoldThreads = 8;  // host threads of fold_sorted_groups' block moves
+
 static uint64_t fold_sorted_groups(int64_t *keys, uint64_t *aggs, uint64_t n, uint64_t cap,
                                    const std::vector<int64_t> &hk, const std::vector<uint64_t> &hw,
                                    const int32_t *kinds, int na, bool *over) {
@@ -1036,17 +1039,56 @@ static uint64_t fold_sorted_groups(int64_t *keys, uint64_t *aggs, uint64_t n, ui
     return n + fresh;
   }
   // backward: the block [p, end) of the rows after fresh key r's place moves up by the r + 1
-  // fresh keys at or before it, then the key goes in front of it
-  uint64_t end = n;
-  for (uint64_t r = fresh; r-- > 0;) {
-    const uint64_t p = pos[r], j = fresh_j[r];
-    if (end > p) {
-      memmove(keys + p + r + 1, keys + p, (end - p) * 8);
-      memmove(aggs + (p + r + 1) * na, aggs + p * na, (end - p) * 8 * (size_t)na);
+  // fresh keys at or before it, then the key goes in front of it.  Old row i moves by the
+  // count of fresh places <= i, so a fresh key near the front moves the whole result: the
+  // blocks go to up to kFoldThreads threads, each a run of consecutive fresh keys and the
+  // rows between them.  Group g's moves write over the first r0[g] rows of the next
+  // groups' ranges, so every group first saves those head rows (joined before any move)
+  // and takes them from the copy.
+  auto move_rows = [&](uint64_t from, uint64_t to, uint64_t cnt) {
+    memmove(keys + to, keys + from, cnt * 8);
+    memmove(aggs + to * na, aggs + from * na, cnt * 8 * (size_t)na);
+  };
+  const int T = (int)std::min<uint64_t>(fresh, n >= (1ull << 20) ? kFoldThreads : 1);
+  std::vector<uint64_t> r0(T + 1);
+  for (int g = 0; g <= T; ++g) r0[g] = fresh * (uint64_t)g / (uint64_t)std::max(T, 1);
+  auto start_of = [&](int g) { return g < T ? pos[r0[g]] : n; };
+  std::vector<std::vector<int64_t>> hk_save(T);
+  std::vector<std::vector<uint64_t>> hw_save(T);
+  auto save_head = [&](int g) {
+    const uint64_t a = start_of(g), h = std::min(r0[g], start_of(g + 1) - a);
+    hk_save[g].assign(keys + a, keys + a + h);
+    hw_save[g].assign(aggs + a * na, aggs + (a + h) * na);
+  };
+  auto run_group = [&](int g) {
+    const uint64_t a = start_of(g), h = hk_save[g].size();
+    uint64_t end = start_of(g + 1);
+    for (uint64_t r = r0[g + 1]; r-- > r0[g];) {
+      const uint64_t p = pos[r], j = fresh_j[r];
+      if (end > p) {
+        const uint64_t mem0 = std::max(p, a + h);  // rows [p, a + h) come from the saved head
+        if (end > mem0) move_rows(mem0, mem0 + r + 1, end - mem0);
+        for (uint64_t i = p; i < std::min(end, a + h); ++i) {
+          keys[i + r + 1] = hk_save[g][i - a];
+          memcpy(aggs + (i + r + 1) * na, &hw_save[g][(i - a) * na], (size_t)na * 8);
+        }
+      }
+      keys[p + r] = hk[j];
+      memcpy(aggs + (p + r) * na, &hw[j * na], (size_t)na * 8);
+      end = p;
     }
-    keys[p + r] = hk[j];
-    memcpy(aggs + (p + r) * na, &hw[j * na], (size_t)na * 8);
-    end = p;
+  };
+  if (T <= 1) {
+    hk_save.resize(1);
+    hw_save.resize(1);
+    if (T == 1) run_group(0);  // (group 0's head is never written by another group: no copy)
+  } else {
+    std::vector<std::thread> th;
+    for (int g = 1; g < T; ++g) th.emplace_back(save_head, g);
+    for (auto &t : th) t.join();
+    th.clear();
+    for (int g = 0; g < T; ++g) th.emplace_back(run_group, g);
+    for (auto &t : th) t.join();
   }
   return n + fresh;
 }
