@@ -1,6 +1,6 @@
 # the round-end checks the driver runs, in one call: every -m gpu test, smoke(), the default bench line
 cd $GRAFT_REPO_ROOT && export NUT_PREBUILT=1
-timeout -k 10 1500 python -u -m pytest tests -m gpu -x -q --timeout 400 --timeout-method thread > gpurun_out/t_all.log 2>&1; rc=$?
+timeout -k 10 1000 python -u -m pytest tests -m gpu -q --timeout 400 --timeout-method thread > gpurun_out/t_all.log 2>&1; rc=$?
 tail -4 gpurun_out/t_all.log
 [ $rc = 0 ] || exit $rc
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/smoke.log 2>&1 || { tail -5 gpurun_out/smoke.log; exit 1; }
