@@ -1124,8 +1124,13 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
   const uint64_t arena1 = ((hkeys.empty() ? n / 2 : n / 4) + 31) & ~31ull;
   const uint64_t b2rows =
       ((uint64_t)ceil(n * slack1) + (66ull << (bits0 + bits1)) + arena1 + 2 * GP_TILE + 64 + 31) & ~31ull;
-  e = c->gp_data.reserve((2 * (size_t)nstore * rows + (size_t)nstore * b2rows) * 8 + 256);
-  if (e) return e;
+  // (no growth margin; buffers that do not fit send the call to the hashed path, which
+  // needs less)
+  e = c->gp_data.reserve((2 * (size_t)nstore * rows + (size_t)nstore * b2rows) * 8 + 256, false);
+  if (e) {
+    (void)hipGetLastError();
+    return decline(NUT_GB_DECLINE_CAPACITY);
+  }
   uint64_t *O[GP_MAX_ARR] = {}, *B2[GP_MAX_ARR] = {};
   for (int i = 1, k = 0; i < narr; ++i) {
     if (i == 2) continue;

@@ -7,7 +7,8 @@ r=${1:?round tag}
 case "$2" in
   1) bash scripts/round_measure.sh $r q1 pmc --workload q1 || exit $?
      set -- "filter filter" "groupby1000 groupby --groups 1000" ;;
-  2) set -- "groupby1e5 groupby --groups 100000" "groupby1e7 groupby --groups 10000000" "sort sort" ;;
+  2) set -- "groupby1e5 groupby --groups 100000" "groupby1e7 groupby --groups 10000000" \
+       "groupby1e7zipf groupby --groups 10000000 --skew" "sort sort" ;;
   3) set -- "scanexpr scanexpr" "q12expr q12expr" "q12join q12join" "join join" ;;
   *) echo "part 1|2|3"; exit 2 ;;
 esac
