@@ -50,7 +50,8 @@ def main():
     (d / "summary.json").write_text(json.dumps(s, indent=1))
     (d / f"pmc_{name}.json").write_text(json.dumps({
         "workload": name, "rows": int(rows),
-        "groups": int(args[args.index("--groups") + 1]) if "--groups" in args else 1000, "kernel_match": match, "hbm_bytes_per_launch": traffic,
+        "groups": int(args[args.index("--groups") + 1]) if "--groups" in args else {"q1": 6, "groupby": 1000}.get(wl),
+        "kernel_match": match, "hbm_bytes_per_launch": traffic, "dispatches": s.get("dispatches"),
         "fetch_size_kb": c.get("FETCH_SIZE"), "write_size_kb": c.get("WRITE_SIZE"),
         "per": {"sort": "step (all ms_* kernels of one sort)", "join": "step (all hj_* kernels of one join)"}.get(
             wl, "launch of " + match),

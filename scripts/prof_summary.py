@@ -18,12 +18,19 @@ def summarize(d: Path, match: str = "agg_kernel", step_match: str = ""):
             out["kernels"].append({"name": row["Name"][:100], "calls": int(row["Calls"]),
                                    "avg_ns": float(row["AverageNs"]), "pct": float(row["Percentage"])})
     for f in glob.glob(str(d / "*" / "*_counter_collection.csv")):
-        vals = collections.defaultdict(list)
-        for row in csv.DictReader(open(f)):
+        # per dispatch (rows of one dispatch summed); the mean over the full-size dispatches
+        # only — those within half of the largest — so a workload's smaller launches of the
+        # same kernel (the Q1 launch-shape probe on 2^28 rows) do not dilute it
+        per = collections.defaultdict(lambda: collections.defaultdict(float))
+        for i, row in enumerate(csv.DictReader(open(f))):
             if match in row["Kernel_Name"]:
-                vals[row["Counter_Name"]].append(float(row["Counter_Value"]))
-        for k, v in vals.items():
-            out["counters"][k] = sum(v) / len(v)
+                per[row["Counter_Name"]][row.get("Dispatch_Id", i)] += float(row["Counter_Value"])
+        for k, byd in per.items():
+            v = list(byd.values())
+            full = [x for x in v if x >= 0.5 * max(v)] if v else []
+            if full:
+                out["counters"][k] = sum(full) / len(full)
+                out.setdefault("dispatches", {})[k] = {"kept": len(full), "of": len(v)}
     c = out["counters"]
     if step_match:
         # totals per step: every dispatch matching `match`, divided by the number of
