@@ -120,7 +120,7 @@ def test_groupby_pool_indexed_matches_hash_oracle(orc, groups, n, row0):
     assert int(iw[:, 1].sum()) == n
 
 
-@pytest.mark.parametrize("groups,nk,masked", [(100_000, 1, False), (1_000_000, 1, True), (300_000, 2, True),
+@pytest.mark.parametrize("groups,nk,masked", [(500_000, 1, False), (1_000_000, 1, True), (300_000, 2, True),
                                               (20_000, 1, False)])
 def test_groupby_partitioned_merge_is_bitwise_the_table_merge(orc, groups, nk, masked):
     """orc_groupby's key-range partitioned merge (large G: the CPU baseline's path) gives
