@@ -10,7 +10,9 @@ case "$2" in
   2) set -- "groupby1e5 groupby --groups 100000" "groupby1e7 groupby --groups 10000000" \
        "groupby1e7zipf groupby --groups 10000000 --skew" "sort sort" ;;
   3) set -- "scanexpr scanexpr" "q12expr q12expr" "q12join q12join" "join join" ;;
-  *) echo "part 1|2|3"; exit 2 ;;
+  4) bash scripts/round_measure.sh $r sort_pmc pmc --workload sort || exit $?
+     exit 0 ;;
+  *) echo "part 1|2|3|4"; exit 2 ;;
 esac
 for w in "$@"; do
   set -- $w
