@@ -240,3 +240,32 @@ def test_capacity_and_auto_size(ex, orc):
     k, w = ex.groupby_to_host(q, group_hint=G // 4)  # library-made arrays, resized once
     ok, ow = orc.groupby([key], AGGS4, values=[val])
     check(k, w, ok, ow, sums_exact=True)
+
+
+def test_ordered_heavy_pass_two_value_columns(ex, orc):
+    """The heavy-key pass with two value arrays (its NV = 2 kernel) and five aggregates —
+    SUM / MIN / MAX of an i64 column, SUM / MAX of an f64 column, COUNT — over Zipf-like
+    keys: heavy keys' i64 MIN / MAX and f64 MAX travel through its accumulators, the rest
+    through the levels; every word bit-exact (dyadic f64 values)."""
+    from nutdb_amd import Agg, AggQuery
+    from nutdb_amd import _lib as L
+    G = 3_000_000
+    key = ex.gen_column(L.GEN_SKEW_KEY, 0x71, N, a=G)
+    fv = ex.gen_column(L.GEN_DYADIC, 0x72, N)
+    rng = np.random.default_rng(72)
+    iv_h = rng.integers(-(1 << 40), 1 << 40, N, dtype=np.int64)
+    iv = dev(iv_h, ex)
+    q = AggQuery(keys=[key], values=[iv, fv],
+                 aggs=[Agg("sum", "col", (0,)), Agg("min", "col", (0,)), Agg("max", "col", (0,)),
+                       Agg("sum", "col", (1,)), Agg("max", "col", (1,)), Agg("count")])
+    kh = key.cpu().numpy()
+    hint = len(np.unique(kh))
+    out = (pinned(2 * hint, 1), pinned(2 * hint, 6))
+    k, w = ex.groupby_to_host(q, group_hint=hint, out=out)
+    k, w = k.copy(), w.copy()
+    assert ex.groupby_stats()["path"] == "partitioned_ordered"
+    hk, hr = ex.groupby_heavy()
+    assert hk > 50 and hr > N // 5
+    ok, ow = orc.groupby([kh], [(0, 0, (0,)), (2, 0, (0,)), (3, 0, (0,)), (0, 0, (1,)), (3, 0, (1,)), (1, 0, ())],
+                         values=[iv_h, fv.cpu().numpy()])
+    assert np.array_equal(k, ok) and np.array_equal(w.view(np.uint64), ow)
