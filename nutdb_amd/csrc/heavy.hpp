@@ -5,9 +5,10 @@
 // rows; a key with more rows than that (Zipf-like data: the top ~1000 keys of a 1e7-key pool
 // hold ~45 % of the rows) would push its excess through the overflow arenas and aggregate
 // on one workgroup.  Keys the host's sample saw often are instead aggregated here, in one
-// streaming pass over the input: an LDS hash set names them, their rows fold into LDS
-// accumulators (merged into device words once per workgroup), and every other row is
-// copied, compacted, to the arrays the partition levels then read.
+// streaming pass over the input: a host-built cuckoo table in LDS names them (two reads per
+// lookup), their rows fold into LDS accumulators (merged into device words once per
+// workgroup), and every other row is copied, compacted, to the arrays the partition levels
+// then read.  scripts/tune/hk_tune.hip times it against a copy of the same arrays.
 #pragma once
 
 #include "agg_ops.hpp"
