@@ -51,7 +51,8 @@ def main():
     (d / f"pmc_{name}.json").write_text(json.dumps({
         "workload": name, "rows": int(rows),
         "groups": int(args[args.index("--groups") + 1]) if "--groups" in args else {"q1": 6, "groupby": 1000}.get(wl),
-        "kernel_match": match, "hbm_bytes_per_launch": traffic, "dispatches": s.get("dispatches"),
+        "kernel_match": match, "hbm_bytes_per_launch": traffic,
+        "dispatches": None if wl in STEP_KERNEL else s.get("dispatches"),
         "fetch_size_kb": c.get("FETCH_SIZE"), "write_size_kb": c.get("WRITE_SIZE"),
         "per": {"sort": "step (all ms_* kernels of one sort)", "join": "step (all hj_* kernels of one join)"}.get(
             wl, "launch of " + match),
