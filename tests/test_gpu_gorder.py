@@ -249,7 +249,7 @@ def test_ordered_heavy_pass_two_value_columns(ex, orc):
     through the levels; every word bit-exact (dyadic f64 values)."""
     from nutdb_amd import Agg, AggQuery
     from nutdb_amd import _lib as L
-    G = 3_000_000
+    G = 6_000_000  # ~2.0e6 distinct keys: the ordered path needs >= 100 per range cell
     key = ex.gen_column(L.GEN_SKEW_KEY, 0x71, N, a=G)
     fv = ex.gen_column(L.GEN_DYADIC, 0x72, N)
     rng = np.random.default_rng(72)
@@ -263,7 +263,7 @@ def test_ordered_heavy_pass_two_value_columns(ex, orc):
     out = (pinned(2 * hint, 1), pinned(2 * hint, 6))
     k, w = ex.groupby_to_host(q, group_hint=hint, out=out)
     k, w = k.copy(), w.copy()
-    assert ex.groupby_stats()["path"] == "partitioned_ordered"
+    assert ex.groupby_stats()["path"] == "partitioned_ordered", ex.groupby_declined()
     hk, hr = ex.groupby_heavy()
     assert hk > 50 and hr > N // 5
     ok, ow = orc.groupby([kh], [(0, 0, (0,)), (2, 0, (0,)), (3, 0, (0,)), (0, 0, (1,)), (3, 0, (1,)), (1, 0, ())],
