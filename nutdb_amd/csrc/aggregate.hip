@@ -1113,15 +1113,20 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
       if (!placed) hkeys.clear();  // (the overflow arenas take them)
     }
   }
-  // level-1 regions: the even share x slack1 (six standard deviations of a Poisson count
-  // of lambda keys per partition); with heavy keys split off, the data is skewed below them
-  // too (Zipf-like: keys of ~1/2 to 2 partition shares remain), so their regions get 2.5 x
-  // (1e9-row Zipf G = 1e7: 62 M arena rows at 1.24 x)
-  const double slack1 = hkeys.empty() ? 1.0 + 6.0 / sqrt(lam) : 2.5;
+  // Exact layout (heavy keys split off): the data is skewed below the heavy keys too
+  // (Zipf-like: keys of ~1/2 to 2 partition shares remain), so the heavy pass's kept rows are
+  // counted per range cell (go_cell_hist_kernel, 8 B per kept row) and both levels' regions
+  // are laid out from the counts — no overflow, no arenas, no arena group-by or host fold.
+  // NUT_OPT_GB_HEAVY = 2 keeps the capped layout behind the heavy pass (A/B, tests).
+  const bool exact = !hkeys.empty() && c->opt[NUT_OPT_GB_HEAVY] != 2;
+  // capped level-1 regions: the even share x slack1 (six standard deviations of a Poisson
+  // count of lambda keys per partition); behind the heavy pass 2.5 x (1e9-row Zipf G = 1e7:
+  // 62 M arena rows at 1.24 x)
+  const double slack1 = exact ? 1.0 : hkeys.empty() ? 1.0 + 6.0 / sqrt(lam) : 2.5;
   // B2: the level-1 regions (n x slack1 + per-region slack), then level 1's overflow arena
-  // (n / 2 rows, n / 4 with the wider regions), then one tile of scratch for runs an
-  // exhausted arena cannot take
-  const uint64_t arena1 = ((hkeys.empty() ? n / 2 : n / 4) + 31) & ~31ull;
+  // (n / 2 rows, n / 4 with the wider regions, none exact), then one tile of scratch for
+  // runs an exhausted arena cannot take
+  const uint64_t arena1 = ((exact ? 0 : hkeys.empty() ? n / 2 : n / 4) + 31) & ~31ull;
   const uint64_t b2rows =
       ((uint64_t)ceil(n * slack1) + (66ull << (bits0 + bits1)) + arena1 + 2 * GP_TILE + 64 + 31) & ~31ull;
   // (no growth margin; buffers that do not fit send the call to the hashed path, which
@@ -1168,6 +1173,7 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
     }
   } free_heavy{nullptr, st};
   const uint32_t nh = (uint32_t)hkeys.size();
+  std::vector<uint64_t> cells;  // exact: kept rows per range cell
   if (nh) {
     using HK = void (*)(HkArgs);
     static const HK hkern[NUT_MAX_VALS + 1] = {hk_split_kernel<0>, hk_split_kernel<1>, hk_split_kernel<2>,
@@ -1180,9 +1186,10 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
     const uint64_t hgrid = std::min<uint64_t>(ntiles, (uint64_t)c->num_cus * per_cu);
     const uint64_t chunk = (ntiles + hgrid - 1) / hgrid;
     if (chunk * HK_TILE * 8 >= (1ull << 32)) return decline(NUT_GB_DECLINE_CAPACITY);  // (a chunk's buffer resource)
-    // [keys (h), aggregates (h x na), kept rows per workgroup (hgrid), cuckoo slots]
-    const size_t slot0 = nh + (size_t)nh * na + hgrid;
-    std::vector<uint64_t> init(slot0 + HK_SLOTS / 4, 0);
+    // [keys (h), aggregates (h x na), kept rows per workgroup (hgrid), cuckoo slots, exact:
+    // kept rows per range cell]
+    const size_t slot0 = nh + (size_t)nh * na + hgrid, cell0 = slot0 + HK_SLOTS / 4;
+    std::vector<uint64_t> init(cell0 + (exact ? GO_CELLS : 0), 0);
     memcpy(&init[0], hkeys.data(), (size_t)nh * 8);
     memcpy(&init[slot0], hslot.data(), HK_SLOTS * 2);
     for (uint32_t j = 0; j < nh; ++j)
@@ -1215,10 +1222,17 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
     ha.chunk = chunk;
     c->timer.begin(st, NUT_KERNEL_AGGREGATE);
     hipLaunchKernelGGL(hkern[nv], dim3((unsigned)hgrid), dim3(HK_THREADS), 0, st, ha);
+    if (exact)
+      hipLaunchKernelGGL(go_cell_hist_kernel, dim3((unsigned)hgrid), dim3(GO_HIST_THREADS), 0, st, ha.okey,
+                         (const uint64_t *)ha.count, chunk * HK_TILE, rg, (unsigned long long *)dheavy + cell0);
     c->timer.end(st);
     NUT_HIP(hipGetLastError());
     hcount.resize(hgrid);
     NUT_HIP(hipMemcpyAsync(hcount.data(), ha.count, hgrid * 8, hipMemcpyDeviceToHost, st));
+    if (exact) {
+      cells.resize(GO_CELLS);
+      NUT_HIP(hipMemcpyAsync(cells.data(), dheavy + cell0, GO_CELLS * 8, hipMemcpyDeviceToHost, st));
+    }
     NUT_HIP(hipStreamSynchronize(st));
     hchunk = chunk * HK_TILE;
     n0 = 0;
@@ -1243,20 +1257,51 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
   }
   for (GpSeg &sg : segs) sg.ocap = ocap;
   std::vector<uint64_t> hist, p0;
-  c->timer.begin(st, NUT_KERNEL_AGGREGATE);
-  e = gp_level(c, mm, segs, bits1, src, O, narr, hcount.size() > 0, false, hist, &p0, 0, abase0, bits0, &rg, darena,
-               acap0);
-  c->timer.end(st);
-  if (e) return e == NUT_ERR_CAPACITY ? decline(NUT_GB_DECLINE_ARENA) : e;
-  // ---- level-1 regions, as the hashed path sizes them
-  const uint32_t np0 = (uint32_t)(p0.size() / 2), nb1 = 1u << bits1;
+  std::vector<uint32_t> dig0;  // the level-0 digit of each non-empty level-0 partition
+  const uint32_t nb0 = 1u << bits0, nb1 = 1u << bits1;
+  // exact: level 0 is launched after the metadata upload below (its layout is known now)
+  std::vector<uint32_t> ts0;
+  std::vector<uint64_t> cur0;
+  if (!exact) {
+    c->timer.begin(st, NUT_KERNEL_AGGREGATE);
+    e = gp_level(c, mm, segs, bits1, src, O, narr, hcount.size() > 0, false, hist, &p0, 0, abase0, bits0, &rg, darena,
+                 acap0);
+    c->timer.end(st);
+    if (e) return e == NUT_ERR_CAPACITY ? decline(NUT_GB_DECLINE_ARENA) : e;
+    for (size_t i = 0; i < p0.size(); i += 2) dig0.push_back((uint32_t)(p0[i] / ocap));
+  } else {
+    // digit d's rows start at a 32-row boundary of O after digit d - 1's (256-B aligned)
+    cur0.assign(nb0 + 1, 0);  // + the (unused) overflow flag
+    uint64_t at = 0;
+    for (uint32_t d = 0; d < nb0; ++d) {
+      uint64_t cnt = 0;
+      for (uint32_t q = 0; q < nb1; ++q) cnt += cells[(d << bits1) | q];
+      cur0[d] = at;
+      if (cnt) {
+        p0.push_back(at);
+        p0.push_back(at + cnt);
+        dig0.push_back(d);
+      }
+      at = (at + cnt + 31) & ~31ull;
+    }
+    if (at + 2 * GP_TILE > 2 * rows) return decline(NUT_GB_DECLINE_CAPACITY);
+    for (GpSeg &sg : segs) sg.ocap = 0;
+    gp_tiles(segs, 2 * GP_TILE, ts0);
+  }
+  // ---- level-1 regions, as the hashed path sizes them (capped), or from the cell counts
+  const uint32_t np0 = (uint32_t)(p0.size() / 2);
   std::vector<GpSeg> s2;
   uint64_t ovf1 = 0;
   for (uint32_t i = 0; i < np0; ++i) {
     GpSeg sg{p0[2 * i], p0[2 * i + 1] - p0[2 * i], 0, 0};
     sg.obase = ovf1;
-    sg.ocap = ((uint64_t)ceil((double)sg.count / nb1 * slack1) + 64 + 1) & ~1ull;
-    ovf1 += sg.ocap << bits1;
+    if (exact) {
+      sg.ocap = 0;
+      for (uint32_t q = 0; q < nb1; ++q) ovf1 += (cells[(dig0[i] << bits1) | q] + 1) & ~1ull;
+    } else {
+      sg.ocap = ((uint64_t)ceil((double)sg.count / nb1 * slack1) + 64 + 1) & ~1ull;
+      ovf1 += sg.ocap << bits1;
+    }
     s2.push_back(sg);
   }
   if (ovf1 + 2 * GP_TILE > b2rows) return decline(NUT_GB_DECLINE_CAPACITY);
@@ -1281,11 +1326,21 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
     tiles.insert(tiles.end(), ts.begin(), ts.end());
   }
   std::vector<uint64_t> init(nparts + nch, 0), rend(nparts);  // + one overflow flag per chunk
-  for (uint32_t i = 0; i < np0; ++i)
+  for (uint32_t i = 0; i < np0; ++i) {
+    uint64_t at = s2[i].obase;  // (exact: digit d's rows after digit d - 1's, even starts)
     for (uint32_t d = 0; d < nb1; ++d) {
-      init[(uint64_t)i * nb1 + d] = s2[i].obase + (uint64_t)d * s2[i].ocap;
-      rend[(uint64_t)i * nb1 + d] = s2[i].obase + (uint64_t)(d + 1) * s2[i].ocap;
+      const uint64_t q = (uint64_t)i * nb1 + d;
+      if (exact) {
+        const uint64_t cnt = cells[(dig0[i] << bits1) | d];
+        init[q] = at;
+        rend[q] = at + cnt;
+        at += (cnt + 1) & ~1ull;
+      } else {
+        init[q] = s2[i].obase + (uint64_t)d * s2[i].ocap;
+        rend[q] = s2[i].obase + (uint64_t)(d + 1) * s2[i].ocap;
+      }
     }
+  }
   // the aggregation's table regions: every one holds a full block table (+ the special key)
   nut_agg_spec s3;
   memset(&s3, 0, sizeof(s3));
@@ -1321,7 +1376,7 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
   std::vector<int64_t> hq(nh, -1);
   if (nh) {
     std::vector<int64_t> idx0((size_t)1 << bits0, -1);
-    for (uint32_t i = 0; i < np0; ++i) idx0[p0[2 * i] / ocap] = i;
+    for (uint32_t i = 0; i < np0; ++i) idx0[dig0[i]] = i;
     for (uint32_t j = 0; j < nh; ++j) {
       const uint32_t cell = rg.cell((uint64_t)hkeys[j]);
       const int64_t i0 = idx0[cell >> bits1];
@@ -1330,10 +1385,30 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
   }
   e = mm.begin(GpMeta::al(s2.size() * sizeof(GpSeg)) + GpMeta::al(tiles.size() * 4 + 1) + GpMeta::al(init.size() * 8) +
                2 * GpMeta::al(init.size() * 8) + 4 * GpMeta::al(nparts * 8) + GpMeta::al(64) +
-               2 * GpMeta::al((size_t)nh * 8 + 1));
+               2 * GpMeta::al((size_t)nh * 8 + 1) +
+               (exact ? GpMeta::al(segs.size() * sizeof(GpSeg)) + GpMeta::al(ts0.size() * 4 + 1) +
+                            GpMeta::al(cur0.size() * 8)
+                      : 0));
   if (e) return e;
   if ((e = mm.up(s2, &dseg)) || (e = mm.up(tiles, &dts)) || (e = mm.up(init, &dinit)) || (e = mm.up(rend, &drend)))
     return e;
+  if (exact) {  // ---- level 0 into the exact regions (no overflow check: ovf = 0)
+    GpSeg *dseg0;
+    uint32_t *dts0;
+    uint64_t *dcur0;
+    if ((e = mm.up(segs, &dseg0)) || (e = mm.up(ts0, &dts0)) || (e = mm.up(cur0, &dcur0))) return e;
+    GpArrays a0;
+    for (int a = 0; a < GP_MAX_ARR; ++a) {
+      a0.src[a] = src[a];
+      a0.dst[a] = O[a];
+    }
+    a0.narr = narr;
+    c->timer.begin(st, NUT_KERNEL_AGGREGATE);
+    gp_capped_launch(c, a0, dseg0, dts0, (uint32_t)ts0.size(), bits1, (unsigned long long *)dcur0, 0, 0,
+                     (unsigned long long *)dcur0 + nb0, bits0, false, &rg, nullptr, 0, nullptr, 1);
+    c->timer.end(st);
+    NUT_HIP(hipGetLastError());
+  }
   int64_t *dhq = nullptr;
   if ((e = mm.up(hq, &dhq))) return e;
   uint64_t *dmiss = (uint64_t *)mm.alloc((size_t)nh * 8 + 1);  // heavy keys whose partition's region was full
@@ -1397,8 +1472,8 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
     const uint32_t a0 = cb[j], a1 = cb[j + 1];
     const uint64_t q0 = (uint64_t)a0 * nb1, nq = (uint64_t)(a1 - a0) * nb1;
     c->timer.begin(st, NUT_KERNEL_AGGREGATE);
-    gp_capped_launch(c, ar, dseg + a0, dts + tile0[j], ntile[j], 0, dcur + q0, 0, ovf1, dcur + nparts + j, bits1, false,
-                     &rg, darena + 1, acap1, dcut + q0);
+    gp_capped_launch(c, ar, dseg + a0, dts + tile0[j], ntile[j], 0, dcur + q0, 0, exact ? 0 : ovf1, dcur + nparts + j,
+                     bits1, false, &rg, exact ? nullptr : darena + 1, acap1, exact ? nullptr : dcut + q0);
     c->timer.end(st);
     NUT_HIP(hipGetLastError());
     NUT_HIP(hipEventRecord(ev1[j], st));

@@ -349,6 +349,36 @@ __global__ __launch_bounds__(1024) void go_heavy_insert_kernel(const int64_t *__
   }
 }
 
+// Rows per range cell (GpRange: 2^14 cells) of the heavy pass's kept rows: workgroup b
+// counts the count[b] rows at row b * chunk of k (heavy.hpp's compacted chunks).  With the
+// heavy keys split off, the rest of a skewed distribution still loads its cells unevenly
+// (keys of ~1/2 to 2 cell shares), so both levels then lay their regions out from these
+// exact counts — no capped regions, no overflow arenas — for 8 B per kept row.
+constexpr int GO_HIST_THREADS = 512;
+constexpr uint32_t GO_CELLS = 1u << 14;
+__global__ __launch_bounds__(GO_HIST_THREADS) void go_cell_hist_kernel(const uint64_t *__restrict__ k,
+                                                                       const uint64_t *__restrict__ count,
+                                                                       uint64_t chunk, GpRange rg,
+                                                                       unsigned long long *__restrict__ cells) {
+  __shared__ uint32_t h[GO_CELLS];
+  for (uint32_t i = threadIdx.x; i < GO_CELLS; i += GO_HIST_THREADS) h[i] = 0;
+  __syncthreads();
+  const uint64_t n = count[blockIdx.x];
+  const uint64_t *b = k + (uint64_t)blockIdx.x * chunk;
+  constexpr int L = 8;
+  for (uint64_t i = threadIdx.x; i < n; i += GO_HIST_THREADS * L) {
+    uint64_t a[L];  // (clamped loads, all in flight before the first count)
+#pragma unroll
+    for (int j = 0; j < L; ++j) a[j] = __builtin_nontemporal_load(b + min(i + (uint64_t)j * GO_HIST_THREADS, n - 1));
+#pragma unroll
+    for (int j = 0; j < L; ++j)
+      if (i + (uint64_t)j * GO_HIST_THREADS < n) atomicAdd(&h[rg.cell(a[j])], 1u);
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < GO_CELLS; i += GO_HIST_THREADS)
+    if (h[i]) atomicAdd(&cells[i], (unsigned long long)h[i]);
+}
+
 // one workgroup: offs[p] = *run + the groups of the partitions before p, then *run += all
 // of them (each thread a run of ceil(np / 1024) consecutive partitions)
 __global__ __launch_bounds__(1024) void go_scan_kernel(const unsigned long long *__restrict__ cnt, uint32_t np,

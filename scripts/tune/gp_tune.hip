@@ -9,6 +9,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <string>
 #include <vector>
 
 #include "../../nutdb_amd/csrc/gpart.hpp"
@@ -164,6 +165,20 @@ int main(int argc, char **argv) {
     printf("%-34s                   %7.3f ms  %6.0f GB/s\n", "copy 2 arrays (HBM floor)", best, 32.0 * c.n / best / 1e6);
   }
   printf("records %llu, groups %llu\n", (unsigned long long)c.n, (unsigned long long)groups);
+  if (argc > 3 && std::string(argv[3]) == "layout") {
+    // the product's output layout (aggregate.hip groupby_partitioned_direct: every array's
+    // regions in one gp_data allocation, array k at row k * 2 * rows) vs one allocation per
+    // array, interleaved on one box
+    uint64_t *joint = nullptr, *sep_k = c.dk, *sep_v = c.dv;
+    CK(hipMalloc(&joint, 4 * rows * 8 + 256));
+    for (int r = 0; r < 2; ++r) {
+      c.dk = sep_k, c.dv = sep_v;
+      run<1024, 1, 7>(c, "128 bins, separate allocations", true);
+      c.dk = joint, c.dv = joint + 2 * rows;
+      run<1024, 1, 7>(c, "128 bins, product layout (joint)", true);
+    }
+    return 0;
+  }
   run<1024, 1>(c, "product <1,1024> (nt stores)", true);
   if (argc > 3) return 0;  // profiling runs: the product variant only
   run<1024, 1, 7>(c, "<1,1024> nt, 128 bins (G = 1e5)", true);

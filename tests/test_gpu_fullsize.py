@@ -127,11 +127,12 @@ def test_groupby_full_config3_ordered_to_host(ex, orc, skew):
     q = AggQuery(keys=[key], values=[val], aggs=[Agg("sum", "col", (0,)), Agg("count"), Agg("min", "col", (0,)),
                                                    Agg("max", "col", (0,))])
     gk, gw = ex.groupby_to_host(q, group_hint=G, out=out)
-    st, hv = ex.groupby_stats(), ex.groupby_heavy()
+    st, hv, ovf = ex.groupby_stats(), ex.groupby_heavy(), ex.groupby_overflow_rows()
     gk, gw = gk.copy(), gw.copy()
     del key, val, out
     assert st["path"] == "partitioned_ordered", st
     assert (hv[1] > n // 4) == skew and (hv[0] > 0) == skew, hv
+    assert not skew or ovf == 0, ovf  # (behind the heavy pass the levels' regions are exact)
     ok, ow = orc.groupby_pool_dyadic(G, n, key_seed=GB_KEY_SEED, val_seed=GB_VAL_SEED,
                                      kind=L.GEN_SKEW_KEY if skew else L.GEN_POOL_KEY)
     gc.collect()

@@ -140,18 +140,21 @@ def test_ordered_heavy_key(ex, orc, share):
     if share >= 0.05:
         hk, hr = ex.groupby_heavy()  # (a key whose few rows the sample hit 4 times may join it)
         assert hk >= 1 and hr >= int((key == key[12345]).sum())
+        assert ex.groupby_overflow_rows() == 0  # (exact layout behind the heavy pass)
     else:
         assert ex.groupby_overflow_rows() > 0 and ex.groupby_heavy() == (0, 0)
     ok, ow = orc.groupby([key], AGGS4, values=[val])
     check(k, w, ok, ow, sums_exact=True)
 
 
-@pytest.mark.parametrize("heavy_pass", [1, 0])
+@pytest.mark.parametrize("heavy_pass", [1, 2, 0])
 def test_ordered_skew_generator(ex, orc, opts, heavy_pass):
     """Zipf-like keys (GEN_SKEW_KEY: pool index i on ~1/i of the rows, the top key ~6 %)
     on the ordered path vs the indexed oracle of the same generator: with the heavy-key pass
-    (the default: the sample's frequent keys aggregated before the levels) and without it
-    (their excess through the overflow arenas)."""
+    (the default: the sample's frequent keys aggregated before the levels, whose regions are
+    then laid out from exact per-cell counts — no overflow), with the pass but capped levels
+    (gb_heavy = 2: the rest's excess through the overflow arenas), and without it (every
+    excess through the arenas)."""
     from nutdb_amd import _lib as L
     opts(gb_heavy=heavy_pass)
     G = 4_000_000
@@ -165,6 +168,7 @@ def test_ordered_skew_generator(ex, orc, opts, heavy_pass):
     hk, hr = ex.groupby_heavy()
     if heavy_pass:
         assert hk > 100 and hr > N // 4
+        assert (ex.groupby_overflow_rows() == 0) == (heavy_pass == 1)
     else:
         assert (hk, hr) == (0, 0) and ex.groupby_overflow_rows() > 0
     assert np.array_equal(k, ok) and np.array_equal(w.view(np.uint64), ow)
