@@ -116,6 +116,29 @@ def test_join_any_order(ex, orc, how, passes):
         check(ex, orc, b.astype(np.int64), p.astype(np.int64), how, passes=passes, any_order=True)
 
 
+@pytest.mark.parametrize("match", [1, 0])
+@pytest.mark.parametrize("how", HOW)
+def test_join_ordered_one_vs_two_pass(ex, orc, opts, how, match):
+    """The ordered write with NUT_OPT_JOIN_MATCH on (default: walks into a match array, then
+    the ordered write-out from it, whenever no probe row can match two build rows) and off
+    (one ordered pass): unique keys (two passes), repeated keys (INNER / LEFT stay one pass;
+    SEMI / ANTI take two), a region-built table, extreme keys, tile-boundary sizes."""
+    opts(join_match=match)
+    rng = np.random.default_rng(88)
+    cases = [
+        (rng.permutation(np.arange(100_000, dtype=np.int64) * 7 - 1000), rng.integers(-2000, 700_000, 1_000_003)),
+        (rng.integers(0, 300, 20_000), rng.integers(-50, 350, 30_001)),
+        (rng.permutation(np.arange(2_100_000, dtype=np.int64) * 3), rng.integers(-100_000, 6_400_000, 3_000_001)),
+        (np.array([I64_MIN, I64_MAX, 0, -1], dtype=np.int64),
+         np.array([I64_MIN, I64_MAX, 0, -1, 1, 5], dtype=np.int64)[rng.integers(0, 6, 10_000)]),
+        (np.array([3], np.int64), np.array([3], np.int64)),
+        (rng.permutation(np.arange(5000, dtype=np.int64)), rng.integers(0, 10_000, 4096)),
+        (rng.permutation(np.arange(5000, dtype=np.int64)), rng.integers(0, 10_000, 4097)),
+    ]
+    for b, p in cases:
+        check(ex, orc, b.astype(np.int64), p.astype(np.int64), how)
+
+
 def test_join_large_property(ex, orc):
     """1e7 unique build keys, 2e8 probe keys (~90 % matching): count and a checksum of the
     pairs against numpy."""
