@@ -467,6 +467,14 @@ constexpr HjCfg hj_make() {
 }
 // the two-pass ordered probe's walk kernel: the unordered probe's default shape
 constexpr int HJ_MATCH_THREADS = 256, HJ_MATCH_ITEMS = 4;
+// its ordered write-out: 512 x 16 tiles (streaming, so the larger tile halves the look-back
+// chain; same box, 1e9 probe rows: join 41.04 ms vs 41.99 / 42.47 at 512 x 8,
+// profiles/r05/join/cfg_ab.txt).  Its tiles are larger than any ordered shape's, so the
+// status array sized at build holds them.
+const HjCfg &hj_emit_cfg() {
+  static const HjCfg c = hj_make<512, 16>();
+  return c;
+}
 // probe tile shapes (threads x rows per lane); NUT_OPT_JOIN_PROBE_CFG picks one for tuning
 // runs.  A join keeps the index it was built with (its status array is sized by the tile).
 const HjCfg &hj_cfg(int i) {
@@ -591,16 +599,18 @@ nut_status join_probe(nut_join *j, bool write, int64_t *pi, int64_t *bi, uint64_
                                                          (const uint32_t *)j->dup, j->prows, nullptr);
   } else if (write && j->two_pass) {
     // two passes (at most one build row per probe row): the walks, then the ordered write-out
+    const HjCfg &cf = hj_emit_cfg();
+    const uint64_t nt = (j->np + cf.tile - 1) / cf.tile;
+    if (nt > j->ntiles) return fail(NUT_ERR_UNSUPPORTED, "nut_join: write-out tiles exceed the status array");
     int32_t *match = nullptr;
     NUT_HIP(hipMallocAsync((void **)&match, j->np * 4, st));
     constexpr uint64_t mt = (uint64_t)HJ_MATCH_THREADS * HJ_MATCH_ITEMS;
     hipLaunchKernelGGL((hj_match_kernel<HJ_MATCH_THREADS, HJ_MATCH_ITEMS>), dim3((unsigned)((j->np + mt - 1) / mt)),
                        dim3(HJ_MATCH_THREADS), 0, st, j->t, j->probe, j->np, match);
-    NUT_HIP(hipMemsetAsync(j->ticket, 0, j->state_bytes, st));
-    const HjCfg &cf = hj_cfg(j->cfg);
-    cf.from_match<<<dim3((unsigned)j->ntiles), dim3(cf.threads), 0, st>>>(
-        j->t, j->probe, j->np, j->type, j->ticket, j->status, (uint32_t)j->ntiles, j->total, pi, bi, cap, j->err,
-        (const uint32_t *)j->dup, j->prows, match);
+    NUT_HIP(hipMemsetAsync(j->ticket, 0, 16 + nt * 8, st));
+    cf.from_match<<<dim3((unsigned)nt), dim3(cf.threads), 0, st>>>(j->t, j->probe, j->np, j->type, j->ticket,
+                                                                 j->status, (uint32_t)nt, j->total, pi, bi, cap,
+                                                                 j->err, (const uint32_t *)j->dup, j->prows, match);
     (void)hipFreeAsync(match, st);
   } else {
     NUT_HIP(hipMemsetAsync(j->ticket, 0, j->state_bytes, st));
