@@ -1739,11 +1739,14 @@ nut_status groupby_partitioned(nut_groups *g, const nut_agg_spec *s, uint64_t gr
 extern "C" {
 
 // NUT_OPT_PRIV_PROBE: before the first compiled-Q1-shape launch of >= 2^27 rows on a
-// device, time the kernel at each of kPrivShapes on the first 2^28 rows of the caller's
-// columns (two interleaved rounds, best of each; the kernel timer is paused, so no probe
-// launch is counted as the caller's work) and keep the fastest for the device.  The probe
-// launches fold into g's table, which is initialised again afterwards: the result is the
-// real launch's alone.
+// device, time the kernel at each of kPrivShapes over the caller's whole input (two
+// interleaved rounds, best of each; the kernel timer is paused, so no probe launch is
+// counted as the caller's work) and keep the fastest for the device — another shape than
+// the default 192 x 2 only if it is >= 0.5 % faster (the shapes lie within ~1 % of each other
+// and a 2^28-row slice had picked 128 x 3 where the full-size table, same box, had 192 x 2
+// ahead: 7.447 vs 7.502 ms, profiles/r05/q1/probe_full_size.txt).  The probe launches fold
+// into g's table, which is initialised again afterwards: the result is the real launch's
+// alone.
 static nut_status probe_priv_shape(nut_groups *g, const nut_agg_spec *s, uint64_t group_hint, uint64_t cap) {
   nut_ctx *c = g->ctx;
   if (!c->opt[NUT_OPT_PRIV_PROBE] || c->opt[NUT_OPT_PRIV_BD] || c->opt[NUT_OPT_PRIV_BLOCKS] || s->n < (1ull << 27) ||
@@ -1754,7 +1757,6 @@ static nut_status probe_priv_shape(nut_groups *g, const nut_agg_spec *s, uint64_
   nut_status st = launch_agg(g, s, group_hint, g->kinds, &dry);
   if (st || !dry.q1_fused) return st;
   nut_agg_spec s2 = *s;
-  s2.n = std::min<uint64_t>(s->n, 1ull << 28);
   hipEvent_t e0 = nullptr, e1 = nullptr;
   NUT_HIP(hipEventCreate(&e0));
   hipError_t he = hipEventCreate(&e1);
@@ -1784,7 +1786,7 @@ static nut_status probe_priv_shape(nut_groups *g, const nut_agg_spec *s, uint64_
   if (st) return st;
   int k = 0;
   for (int j = 1; j < 3; ++j)
-    if (best[j] < best[k]) k = j;
+    if (best[j] < best[k] && best[j] < 0.995 * best[0]) k = j;
   {
     std::lock_guard<std::mutex> lk(g_priv_mu);
     g_priv_shape[c->device].shape = k;
