@@ -12,7 +12,9 @@ case "$2" in
   3) set -- "scanexpr scanexpr" "q12expr q12expr" "q12join q12join" "join join" ;;
   4) bash scripts/round_measure.sh $r sort_pmc pmc --workload sort || exit $?
      exit 0 ;;
-  *) echo "part 1|2|3|4"; exit 2 ;;
+  5) bash scripts/round_measure.sh $r join_pmc pmc --workload join || exit $?
+     exit 0 ;;
+  *) echo "part 1|2|3|4|5"; exit 2 ;;
 esac
 for w in "$@"; do
   set -- $w
