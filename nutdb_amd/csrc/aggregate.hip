@@ -568,7 +568,7 @@ uint32_t gp_tiles(std::vector<GpSeg> &segs, uint32_t tile, std::vector<uint32_t>
 void gp_capped_launch(nut_ctx *c, const GpArrays &ar, const GpSeg *dseg, const uint32_t *dts, uint32_t nst, int shift,
                       unsigned long long *dcur, uint64_t kx, uint64_t ovf, unsigned long long *dflag, int bits,
                       bool two_keys, const GpRange *rg, unsigned long long *acur = nullptr, uint64_t acap = 0,
-                      unsigned long long *acut = nullptr, int gather = 0) {
+                      unsigned long long *acut = nullptr, int gather = 0, int threads = 1024) {
   if (!nst) return;
   const unsigned grid = std::min<unsigned>(nst, (unsigned)c->num_cus);
   using SK = void (*)(GpArrays, const GpSeg *, const uint32_t *, uint32_t, int, int, unsigned long long *, uint64_t,
@@ -578,9 +578,15 @@ void gp_capped_launch(nut_ctx *c, const GpArrays &ar, const GpSeg *dseg, const u
       {gp_scatter_kernel<2, 1024, 1, 6>, gp_scatter_kernel<2, 1024, 1, 7>, gp_scatter_kernel<2, 1024, 1, 8>},
       {gp_scatter_kernel<1, 1024, 1, 6, true>, gp_scatter_kernel<1, 1024, 1, 7, true>,
        gp_scatter_kernel<1, 1024, 1, 8, true>}};
+  // range digits at 512 threads (8 Ki-record tiles, ~75 KB of LDS): the ordered path's level
+  // 1 can then share each CU with an aggregation workgroup (NUT_OPT_GB_L1_THREADS)
+  static const SK kern512[3] = {gp_scatter_kernel<1, 512, 1, 6, true>, gp_scatter_kernel<1, 512, 1, 7, true>,
+                                gp_scatter_kernel<1, 512, 1, 8, true>};
   const int kv = rg ? 2 : two_keys ? 1 : 0;
-  hipLaunchKernelGGL(kern[kv][bits - 6], dim3(grid), dim3(1024), 0, c->stream, ar, dseg, dts, nst, shift, gather, dcur,
-                     kx, ovf, dflag, rg ? *rg : GpRange{}, acur, acap, acut);
+  const bool narrow = rg && threads == 512;
+  hipLaunchKernelGGL(narrow ? kern512[bits - 6] : kern[kv][bits - 6], dim3(grid), dim3(narrow ? 512 : 1024), 0,
+                     c->stream, ar, dseg, dts, nst, shift, gather, dcur, kx, ovf, dflag, rg ? *rg : GpRange{}, acur,
+                     acap, acut);
 }
 
 // one partition level: histogram + scatter of every segment; returns the 256 counts per
@@ -1316,11 +1322,12 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
     if (e1 > cb.back()) cb.push_back(e1);
   }
   const uint32_t nch = (uint32_t)cb.size() - 1;
+  const int l1_threads = c->opt[NUT_OPT_GB_L1_THREADS] == 512 ? 512 : 1024;  // level 1's scatter workgroup
   std::vector<uint32_t> tiles, tile0(nch + 1, 0), ntile(nch, 0);
   for (uint32_t j = 0; j < nch; ++j) {
     std::vector<GpSeg> sub(s2.begin() + cb[j], s2.begin() + cb[j + 1]);
     std::vector<uint32_t> ts;
-    ntile[j] = gp_tiles(sub, 2 * GP_TILE, ts);
+    ntile[j] = gp_tiles(sub, (uint32_t)l1_threads * GP_ITEMS, ts);
     for (uint32_t i = 0; i < sub.size(); ++i) s2[cb[j] + i].tile0 = sub[i].tile0;
     tile0[j] = (uint32_t)tiles.size();
     tiles.insert(tiles.end(), ts.begin(), ts.end());
@@ -1473,7 +1480,8 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
     const uint64_t q0 = (uint64_t)a0 * nb1, nq = (uint64_t)(a1 - a0) * nb1;
     c->timer.begin(st, NUT_KERNEL_AGGREGATE);
     gp_capped_launch(c, ar, dseg + a0, dts + tile0[j], ntile[j], 0, dcur + q0, 0, exact ? 0 : ovf1, dcur + nparts + j,
-                     bits1, false, &rg, exact ? nullptr : darena + 1, acap1, exact ? nullptr : dcut + q0);
+                     bits1, false, &rg, exact ? nullptr : darena + 1, acap1, exact ? nullptr : dcut + q0, 0,
+                     l1_threads);
     c->timer.end(st);
     NUT_HIP(hipGetLastError());
     NUT_HIP(hipEventRecord(ev1[j], st));

@@ -361,7 +361,7 @@ class Executor:
                "topk": 11, "gb_l0_bits": 12, "stream_blocks": 13,
                "priv_bd": 14, "priv_blocks": 15, "agg_blocks": 16, "sel_blocks": 17, "sort_bd": 18,
                "gb_ordered": 19, "priv_probe": 20, "gb_heavy": 21,
-               "join_match": 22}
+               "join_match": 22, "gb_l1_threads": 23}
 
     def groupby_stats(self) -> dict:
         """The algorithm the last group-by on this context took (nut_ctx_groupby_stats)."""

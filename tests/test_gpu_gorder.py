@@ -174,6 +174,22 @@ def test_ordered_skew_generator(ex, orc, opts, heavy_pass):
     assert np.array_equal(k, ok) and np.array_equal(w.view(np.uint64), ow)
 
 
+@pytest.mark.parametrize("skew", [False, True])
+def test_ordered_narrow_level1(ex, orc, opts, skew):
+    """Level 1 at 512-thread scatter workgroups (NUT_OPT_GB_L1_THREADS = 512: 8 Ki-record
+    tiles): the same groups, bit-exact, uniform pool keys and Zipf-like keys."""
+    from nutdb_amd import _lib as L
+    opts(gb_l1_threads=512)
+    G = 4_000_000
+    kind = L.GEN_SKEW_KEY if skew else L.GEN_POOL_KEY
+    key = ex.gen_column(kind, 0x53, N, a=G)
+    val = ex.gen_column(L.GEN_DYADIC, 0x54, N)
+    ok, ow = orc.groupby_pool_dyadic(G, N, key_seed=0x53, val_seed=0x54, kind=kind)
+    k, w, path = run_to_host(ex, gb_query(key, val), int(ok.shape[0]))
+    assert path == "partitioned_ordered"
+    assert np.array_equal(k, ok) and np.array_equal(w.view(np.uint64), ow)
+
+
 def test_ordered_i64_values(ex, orc):
     from nutdb_amd import Agg, AggQuery
     rng = np.random.default_rng(8)
