@@ -701,11 +701,14 @@ def main():
     # source file, its commit and date travel with the number as traffic_source)
     traffic, traffic_src = None, None
     pmc = ROOT / "profiles" / f"pmc_{w.name}.json"
+    if w.name == "groupby_i64_sum_f64":  # partitioned G: its own per-step file, if measured
+        pg = ROOT / "profiles" / f"pmc_{w.name}_g{args.groups}{'_skew' if args.skew else ''}.json"
+        pmc = pg if pg.exists() else pmc
     if pmc.exists():
         try:
             d = json.loads(pmc.read_text())
-            if int(d.get("rows", -1)) == rows and (w.name != "groupby_i64_sum_f64" or
-                                                    int(d.get("groups", 1000)) == args.groups):
+            if int(d.get("rows", -1)) == rows and (w.name != "groupby_i64_sum_f64" or (
+                    int(d.get("groups", 1000)) == args.groups and bool(d.get("skew", False)) == bool(args.skew))):
                 traffic = d.get("hbm_bytes_per_launch")
                 m = d.get("measured", {})
                 traffic_src = (f"profiles/{pmc.name}: {d.get('per', 'per launch')}, "

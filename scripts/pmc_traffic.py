@@ -36,7 +36,19 @@ def main():
                                                                            "join": 1e9, "scanexpr": 1e8,
                                                                            "q12join": 1e9}[wl]
     name, match = WORKLOAD_KERNEL[wl]
-    s = summarize(d, match, STEP_KERNEL.get(wl, ""))
+    groups = int(float(args[args.index("--groups") + 1])) if "--groups" in args else {"q1": 6, "groupby": 1000}.get(wl)
+    step_kernel, exclude, fname = STEP_KERNEL.get(wl, ""), "", name
+    per_desc = {"sort": "step (all ms_* kernels of one sort)", "join": "step (all hj_* kernels of one join)"}.get(
+        wl, "launch of " + match)
+    if wl == "groupby" and groups and groups >= 100000:
+        # partitioned group-by: every library kernel of one step (scatter levels, heavy-key
+        # pass, aggregation, ordering), column generation excluded; steps counted by a kernel
+        # that runs once per step (the one capped level at G = 1e5, the range sample above)
+        match, exclude = "nut::", "gen_column"
+        step_kernel = "go_sample_kernel" if groups >= 1000000 else "gp_scatter_kernel"
+        fname = f"{name}_g{groups}" + ("_skew" if "--skew" in args else "")
+        per_desc = "step (all nut:: kernels of one group-by step except column generation)"
+    s = summarize(d, match, step_kernel, exclude)
     c = s["counters"]
     traffic = None
     # join: the reads are dominated by random single-slot (64-B) requests, counted whole;
@@ -48,14 +60,12 @@ def main():
     s["rows"] = int(rows)
     s["hbm_bytes_per_launch"] = traffic
     (d / "summary.json").write_text(json.dumps(s, indent=1))
-    (d / f"pmc_{name}.json").write_text(json.dumps({
-        "workload": name, "rows": int(rows),
-        "groups": int(args[args.index("--groups") + 1]) if "--groups" in args else {"q1": 6, "groupby": 1000}.get(wl),
-        "kernel_match": match, "hbm_bytes_per_launch": traffic,
-        "dispatches": None if wl in STEP_KERNEL else s.get("dispatches"),
+    (d / f"pmc_{fname}.json").write_text(json.dumps({
+        "workload": name, "rows": int(rows), "groups": groups, "skew": "--skew" in args,
+        "kernel_match": match, "kernel_exclude": exclude or None, "hbm_bytes_per_launch": traffic,
+        "dispatches": None if step_kernel else s.get("dispatches"),
         "fetch_size_kb": c.get("FETCH_SIZE"), "write_size_kb": c.get("WRITE_SIZE"),
-        "per": {"sort": "step (all ms_* kernels of one sort)", "join": "step (all hj_* kernels of one join)"}.get(
-            wl, "launch of " + match),
+        "per": per_desc,
         "measured": {"tag": d.name, "commit": os.environ.get("NUT_COMMIT", "unknown"),
                      "date_utc": time.strftime("%Y-%m-%dT%H:%MZ", time.gmtime()),
                      "how": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, one pass each, over bench.py "

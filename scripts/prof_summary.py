@@ -11,7 +11,7 @@ import sys
 from pathlib import Path
 
 
-def summarize(d: Path, match: str = "agg_kernel", step_match: str = ""):
+def summarize(d: Path, match: str = "agg_kernel", step_match: str = "", exclude: str = ""):
     out = {"kernels": [], "counters": {}}
     for f in glob.glob(str(d / "trace" / "*_kernel_stats.csv")):
         for row in csv.DictReader(open(f)):
@@ -23,7 +23,7 @@ def summarize(d: Path, match: str = "agg_kernel", step_match: str = ""):
         # same kernel (the Q1 launch-shape probe on 2^28 rows) do not dilute it
         per = collections.defaultdict(lambda: collections.defaultdict(float))
         for i, row in enumerate(csv.DictReader(open(f))):
-            if match in row["Kernel_Name"]:
+            if match in row["Kernel_Name"] and not (exclude and exclude in row["Kernel_Name"]):
                 per[row["Counter_Name"]][row.get("Dispatch_Id", i)] += float(row["Counter_Value"])
         for k, byd in per.items():
             v = list(byd.values())
@@ -39,7 +39,7 @@ def summarize(d: Path, match: str = "agg_kernel", step_match: str = ""):
             tot = collections.defaultdict(float)
             steps = collections.defaultdict(set)
             for row in csv.DictReader(open(f)):
-                if match in row["Kernel_Name"]:
+                if match in row["Kernel_Name"] and not (exclude and exclude in row["Kernel_Name"]):
                     tot[row["Counter_Name"]] += float(row["Counter_Value"])
                 if step_match in row["Kernel_Name"]:
                     steps[row["Counter_Name"]].add(row.get("Dispatch_Id", row.get("Correlation_Id", len(steps))))
