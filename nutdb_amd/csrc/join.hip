@@ -32,6 +32,7 @@
 // see DESIGN.md §4.4 for the measured line rate.
 #include <algorithm>
 #include <new>
+#include <type_traits>
 
 #include "common.hpp"
 #include "lookback.hpp"
@@ -343,15 +344,17 @@ __global__ __launch_bounds__(HJ_THREADS, HJ_ITEMS <= 8 ? 4 : 1) void hj_probe_ke
       act = more ? act : (act & ~(1u << i));
     }
   }
-  // ranks inside the tile, rows ordered (item, wave, lane)
-  uint64_t ex[HJ_ITEMS];
+  // ranks inside the tile, rows ordered (item, wave, lane); in-wave exclusive ranks: with the match array every row has at most one pair, so 32
+  // bits hold them (and 16 fewer VGPRs at 16 rows per lane)
+  using Rank = typename std::conditional<FROM_MATCH, uint32_t, uint64_t>::type;
+  Rank ex[HJ_ITEMS];
 #pragma unroll
   for (int i = 0; i < HJ_ITEMS; ++i) {
-    const uint64_t c = base + (uint64_t)i * HJ_THREADS < n ? hj_out_count(m[i], type) : 0;
-    uint64_t incl = c;
+    const Rank c = base + (uint64_t)i * HJ_THREADS < n ? hj_out_count(m[i], type) : 0;
+    Rank incl = c;
 #pragma unroll
     for (int off = 1; off < kWave; off <<= 1) {
-      const uint64_t y = __shfl_up(incl, off, kWave);
+      const Rank y = __shfl_up(incl, off, kWave);
       if (lane >= off) incl += y;
     }
     ex[i] = incl - c;
