@@ -468,8 +468,22 @@ constexpr HjCfg hj_make() {
   return HjCfg{T, (uint32_t)(T * I), hj_probe_kernel<true, T, I>, hj_probe_kernel<false, T, I>,
                hj_probe_kernel<true, T, I, true>, hj_probe_kernel<true, T, I, false, true>};
 }
-// the two-pass ordered probe's walk kernel: the unordered probe's default shape
-constexpr int HJ_MATCH_THREADS = 256, HJ_MATCH_ITEMS = 4;
+// the two-pass ordered probe's walk kernel: threads x rows per lane, the unordered probe's
+// shapes (NUT_OPT_JOIN_ANY_CFG picks for both)
+struct HjMatchCfg {
+  int threads;
+  uint32_t tile;
+  void (*fn)(HjTable, const int64_t *, uint64_t, int32_t *);
+};
+template <int T, int I>
+constexpr HjMatchCfg hj_match_make() {
+  return HjMatchCfg{T, (uint32_t)(T * I), hj_match_kernel<T, I>};
+}
+const HjMatchCfg &hj_match_cfg(int i) {
+  static const HjMatchCfg cfgs[] = {hj_match_make<256, 4>(), hj_match_make<512, 8>(), hj_match_make<256, 8>(),
+                                    hj_match_make<512, 4>(), hj_match_make<128, 4>()};
+  return cfgs[i];
+}
 // its ordered write-out: 512 x 16 tiles (streaming, so the larger tile halves the look-back
 // chain; same box, 1e9 probe rows: join 41.04 ms vs 41.99 / 42.47 at 512 x 8,
 // profiles/r05/join/cfg_ab.txt).  Its tiles are larger than any ordered shape's, so the
@@ -607,9 +621,9 @@ nut_status join_probe(nut_join *j, bool write, int64_t *pi, int64_t *bi, uint64_
     if (nt > j->ntiles) return fail(NUT_ERR_UNSUPPORTED, "nut_join: write-out tiles exceed the status array");
     int32_t *match = nullptr;
     NUT_HIP(hipMallocAsync((void **)&match, j->np * 4, st));
-    constexpr uint64_t mt = (uint64_t)HJ_MATCH_THREADS * HJ_MATCH_ITEMS;
-    hipLaunchKernelGGL((hj_match_kernel<HJ_MATCH_THREADS, HJ_MATCH_ITEMS>), dim3((unsigned)((j->np + mt - 1) / mt)),
-                       dim3(HJ_MATCH_THREADS), 0, st, j->t, j->probe, j->np, match);
+    const HjMatchCfg &mc = hj_match_cfg(j->any_cfg);
+    hipLaunchKernelGGL(mc.fn, dim3((unsigned)((j->np + mc.tile - 1) / mc.tile)), dim3(mc.threads), 0, st, j->t,
+                       j->probe, j->np, match);
     NUT_HIP(hipMemsetAsync(j->ticket, 0, 16 + nt * 8, st));
     cf.from_match<<<dim3((unsigned)nt), dim3(cf.threads), 0, st>>>(j->t, j->probe, j->np, j->type, j->ticket,
                                                                  j->status, (uint32_t)nt, j->total, pi, bi, cap,
