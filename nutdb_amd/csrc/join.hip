@@ -148,7 +148,9 @@ __global__ __launch_bounds__(256) void hj_dupcheck_kernel(const int64_t *__restr
 // Region build: the table is cut into regions of HJ_RS slots (128 KB); a region's build
 // rows arrive contiguous (hash_partition16 by the home hash's top bits), one workgroup
 // builds the region in LDS with LDS atomics — runs wrap inside the region — checks it for
-// duplicate keys, and writes it out whole (the table needs no memset).
+// duplicate keys, and writes it out whole (the table needs no memset).  Persistent (one
+// workgroup per CU, nreg / grid regions each): the next region's records are loaded
+// before this region's write-out, so their latency hides behind its 128 KB of stores.
 constexpr uint32_t HJ_RS = 8192;
 constexpr int HJ_RTHREADS = 1024;
 
@@ -159,25 +161,29 @@ __global__ __launch_bounds__(HJ_RTHREADS) void hj_region_build_kernel(const int6
                                                                       const int64_t *__restrict__ rows,
                                                                       const uint64_t *__restrict__ region_off,
                                                                       HjTable t, int64_t row_base,
-                                                                      uint32_t *__restrict__ dup) {
+                                                                      uint32_t *__restrict__ dup, uint64_t nreg) {
   __shared__ int64_t s_key[HJ_RS];
   __shared__ unsigned long long s_row[HJ_RS];
   const int tid = threadIdx.x;
-  const uint64_t r = blockIdx.x;
-  const uint64_t lo = region_off[r], hi = region_off[r + 1];
-  // the region's records, all loads issued together (clamped: no per-record branch) and
+  // a region's records, all loads issued together (clamped: no per-record branch) and
   // kept in registers for the duplicate check
   int64_t k[HJ_RK];
   unsigned long long row[HJ_RK];
-  if (hi > lo) {
+  auto load = [&](uint64_t r, int64_t (&kk)[HJ_RK], unsigned long long (&rr)[HJ_RK]) {
+    const uint64_t lo = region_off[r], hi = region_off[r + 1];
+    if (hi <= lo) return;
 #pragma unroll
     for (int j = 0; j < HJ_RK; ++j) {
       const uint64_t i = lo + tid + (uint64_t)j * HJ_RTHREADS;
       const uint64_t ic = i < hi ? i : hi - 1;
-      k[j] = keys[ic];
-      row[j] = (unsigned long long)(rows[ic] + row_base);
+      kk[j] = keys[ic];
+      rr[j] = (unsigned long long)(rows[ic] + row_base);
     }
-  }
+  };
+  uint64_t r = blockIdx.x;
+  load(r, k, row);
+  for (;;) {
+  const uint64_t lo = region_off[r], hi = region_off[r + 1];
   for (uint32_t i = tid; i < HJ_RS; i += HJ_RTHREADS) s_row[i] = HJ_EMPTY;
   __syncthreads();
 #pragma unroll
@@ -206,8 +212,14 @@ __global__ __launch_bounds__(HJ_RTHREADS) void hj_region_build_kernel(const int6
     }
   }
   if (__any(found) && (tid & (kWave - 1)) == 0) atomicOr(dup, 1u);
+  const uint64_t rn = r + gridDim.x;
+  if (rn < nreg) load(rn, k, row);  // (the duplicate check above was this region's last use)
   i64x2 *out = t.slot + r * HJ_RS;
   for (uint32_t i = tid; i < HJ_RS; i += HJ_RTHREADS) out[i] = i64x2{s_key[i], (int64_t)s_row[i]};
+  if (rn >= nreg) break;
+  r = rn;
+  __syncthreads();  // every lane's write-out has read s_key / s_row before they are reset
+  }
 }
 
 // output pairs of one probe row with m matches
@@ -578,9 +590,9 @@ nut_status join_build(nut_ctx *c, nut_join *j, const int64_t *build, uint64_t nb
       NUT_HIP(hipMallocAsync((void **)&doff, (nreg + 1) * 8, st));
       NUT_HIP(hipMemcpyAsync(doff, off.data(), (nreg + 1) * 8, hipMemcpyHostToDevice, st));
       j->t.wmask = HJ_RS - 1;
-      hipLaunchKernelGGL(hj_region_build_kernel, dim3((unsigned)nreg), dim3(HJ_RTHREADS), 0, st,
-                         (const int64_t *)(tmp + 2 * nb), (const int64_t *)(tmp + 3 * nb), (const uint64_t *)doff,
-                         j->t, (int64_t)0, j->dup);
+      hipLaunchKernelGGL(hj_region_build_kernel, dim3((unsigned)std::min<uint64_t>(nreg, (uint64_t)c->num_cus)),
+                         dim3(HJ_RTHREADS), 0, st, (const int64_t *)(tmp + 2 * nb), (const int64_t *)(tmp + 3 * nb),
+                         (const uint64_t *)doff, j->t, (int64_t)0, j->dup, nreg);
       NUT_HIP(hipGetLastError());
       NUT_HIP(hipStreamSynchronize(st));  // `off` is host memory of this frame
       (void)hipFreeAsync(doff, st);
