@@ -14,7 +14,8 @@
 // it may stop at the first match (unique build keys: the PK-FK case) or must walk the run
 // to its empty slot.  SEMI / ANTI always stop at the first match.
 //
-// Probe: ONE pass in probe-row order.  A 512-thread workgroup takes a tile of 4096 probe
+// Probe, when a probe row can match several build rows (repeated build keys under INNER /
+// LEFT): ONE pass in probe-row order.  A 512-thread workgroup takes a tile of 4096 probe
 // rows by atomic ticket and loads its keys (striped, coalesced).  Runs are walked in
 // lock-step rounds: each round issues one slot load for every unfinished row of the lane
 // (8 random reads in flight per lane; finished rows issue nothing), then consumes them.
@@ -22,7 +23,10 @@
 // the wave totals) and the tile's global offset comes from decoupled look-back
 // (lookback.hpp).  A row with at most one match writes its pair from registers; rows with
 // several walk their run again while writing.  Rows come out in probe order with no
-// per-row or per-tile count array in HBM.  NUT_HJ_CFG selects another tile shape (tuning).
+// per-row or per-tile count array in HBM.  NUT_OPT_JOIN_PROBE_CFG selects another tile
+// shape (tuning).  Otherwise (unique build keys, SEMI / ANTI; NUT_OPT_JOIN_MATCH) in two
+// passes: the walks in launch order into a 4-B match array, then the ordered write-out
+// from it (hj_match_kernel, below).
 //   nut_join_i64 (+ nut_join_write): a count-only pass gives the pair count first, the
 //   write pass follows (two probe passes, caller-sized output);
 //   nut_join_i64_into: the write pass alone into caller arrays of a given capacity.
