@@ -618,6 +618,14 @@ int nut_plan_kind_of(const nut_plan *plan);
 /* JSON description of the plan (columns, predicates, aggregates, outputs); same
  * buffer convention as nut_stmt_dump */
 nut_status nut_plan_describe(const nut_plan *plan, char *buf, size_t cap, size_t *len);
+/* The executor route a single-table plan takes over columns of the given names and types
+ * (`data` may be NULL: host only, no device, nothing runs) — "fused-filter", "fused-sort",
+ * "expr-filter", "expr-sort", "expr-sort-f64-order" (float64 bits sorted as int64 words in
+ * the IEEE total order), "rowid-scan", "rerun-expression -> …", "fused-groupby",
+ * "expr-groupby", "packed-groupby" — or the NUT_ERR_PLAN nut_plan_execute would return.
+ * A test hook for the routing; same buffer convention as nut_stmt_dump. */
+nut_status nut_plan_route(const nut_plan *plan, const nut_column *cols, int ncols, char *buf, size_t cap,
+                          size_t *len);
 void nut_plan_free(nut_plan *plan);
 
 /* Compile an expression-mode plan's kernel now (hipRTC; no device needed) so the first

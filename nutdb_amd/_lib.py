@@ -191,6 +191,7 @@ SIGNATURES = {
     "nut_sql_plan": (_I32, [C.c_char_p, C.c_size_t, C.POINTER(_P)]),
     "nut_plan_kind_of": (_I32, [_P]),
     "nut_plan_describe": (_I32, [_P, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
+    "nut_plan_route": (_I32, [_P, _P, _I32, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
     "nut_plan_free": (None, [_P]),
     "nut_plan_execute": (_I32, [_P, _P, _P, _I32, _U64, _U64, C.POINTER(_P)]),
     "nut_plan_execute2": (_I32, [_P, _P, _P, _I32, _U64, _P, _I32, _U64, _U64, C.POINTER(_P)]),

@@ -1249,6 +1249,24 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
   }
   c->gb_heavy_keys = nh;
   c->gb_heavy_rows = n - n0;
+  if (nh && n0 == 0) {
+    // every row was a heavy key's (few distinct keys under a large group_hint): no row is
+    // left for the partition levels, and the heavy pass's groups are the whole result
+    // (hkeys ascending, every one seen in the data; f64 MIN / MAX back from the table order)
+    std::vector<uint64_t> hw((size_t)nh * na);
+    NUT_HIP(hipMemcpyAsync(hw.data(), dheavy + nh, hw.size() * 8, hipMemcpyDeviceToHost, st));
+    NUT_HIP(hipStreamSynchronize(st));
+    for (uint32_t j = 0; j < nh; ++j)
+      for (int a = 0; a < na; ++a) {
+        uint64_t &x = hw[(size_t)j * na + a];
+        if (g->kinds[a] == AK_MIN_F64 || g->kinds[a] == AK_MAX_F64) x = ord_to_f64(x);
+      }
+    bool over = false;
+    *n_out = fold_sorted_groups(keys_h, aggs_h, 0, cap, hkeys, hw, g->kinds, na, &over);
+    if (over) return fail(NUT_ERR_CAPACITY, "nut_groupby_to_host: capacity " + std::to_string(cap) + " < " +
+                                                std::to_string(nh) + " groups");
+    return NUT_OK;
+  }
   // ---- level 0 (range digit = cell >> bits1): 1.5 x the even share per partition, the rest
   // of O (~n / 2 rows) its arena
   const uint64_t ocap = ((3 * rows / 2) >> bits0) & ~1ull;
@@ -1313,6 +1331,7 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
   if (ovf1 + 2 * GP_TILE > b2rows) return decline(NUT_GB_DECLINE_CAPACITY);
   const uint64_t acap1 = b2rows - ovf1 - 2 * GP_TILE;  // level 1's arena: rows [ovf1, ovf1 + acap1) of B2
   const uint64_t nparts = (uint64_t)np0 * nb1;
+  if (nparts == 0) return decline(NUT_GB_DECLINE_CAPACITY);  // (no kept row reached level 0: not reached)
   // chunks of level-0 partitions (in key order) halving in size — 1/2, 1/4, 1/8, 1/16,
   // 1/16: a chunk's transfer (~0.4x its compute) hides behind the next, smaller chunk, and
   // only the last 1/16 crosses after the work; each launch costs a tail, so few chunks

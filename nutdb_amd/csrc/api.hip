@@ -360,6 +360,8 @@ nut_status nut_ctx_set_option(nut_ctx *c, int option, int64_t value) {
     return fail(NUT_ERR_INVALID_ARG, "nut_ctx_set_option: NUT_OPT_PRIV_BD takes 0, 128, 192 or 256");
   if (option == NUT_OPT_SORT_BD && value && value != 512 && value != 1024)
     return fail(NUT_ERR_INVALID_ARG, "nut_ctx_set_option: NUT_OPT_SORT_BD takes 0, 512 or 1024");
+  if (option == NUT_OPT_GB_L1_THREADS && value != 512 && value != 1024)
+    return fail(NUT_ERR_INVALID_ARG, "nut_ctx_set_option: NUT_OPT_GB_L1_THREADS takes 512 or 1024");
   c->opt[option] = value;
   return NUT_OK;
 }

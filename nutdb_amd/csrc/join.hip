@@ -245,7 +245,7 @@ __device__ __forceinline__ uint32_t hj_out_count(uint32_t m, int type) {
 // the ordered write-out is then a streaming pass over `match` (hj_probe_kernel<FROM_MATCH>).
 template <int HJ_THREADS, int HJ_ITEMS>
 __global__ __launch_bounds__(HJ_THREADS, 4) void hj_match_kernel(HjTable t, const int64_t *__restrict__ probe,
-                                                                 uint64_t n, int32_t *__restrict__ match) {
+                                                                 uint64_t n, uint32_t *__restrict__ match) {
   const uint64_t base = (uint64_t)blockIdx.x * (HJ_THREADS * HJ_ITEMS) + threadIdx.x;
   int64_t key[HJ_ITEMS];
   uint32_t s[HJ_ITEMS], first[HJ_ITEMS];
@@ -276,7 +276,7 @@ __global__ __launch_bounds__(HJ_THREADS, 4) void hj_match_kernel(HjTable t, cons
 #pragma unroll
   for (int i = 0; i < HJ_ITEMS; ++i) {
     const uint64_t r = base + (uint64_t)i * HJ_THREADS;
-    if (r < n) __builtin_nontemporal_store((int32_t)first[i], match + r);
+    if (r < n) __builtin_nontemporal_store(first[i], match + r);  // ~0u: no match
   }
 }
 
@@ -297,7 +297,7 @@ __global__ __launch_bounds__(HJ_THREADS, HJ_ITEMS <= 8 ? 4 : 1) void hj_probe_ke
                                                               uint32_t *__restrict__ err,
                                                               const uint32_t *__restrict__ dup,
                                                               const int64_t *__restrict__ prows,
-                                                              const int32_t *__restrict__ match) {
+                                                              const uint32_t *__restrict__ match) {
   static_assert(!FROM_MATCH || (WRITE && !ANY), "the match array feeds the ordered write pass");
   constexpr int HJ_WAVES = HJ_THREADS / kWave;
   constexpr uint32_t HJ_TILE = HJ_THREADS * HJ_ITEMS;
@@ -319,11 +319,11 @@ __global__ __launch_bounds__(HJ_THREADS, HJ_ITEMS <= 8 ? 4 : 1) void hj_probe_ke
   for (int i = 0; i < HJ_ITEMS; ++i) {
     const uint64_t r = base + (uint64_t)i * HJ_THREADS;
     if constexpr (FROM_MATCH) {
-      const int32_t b = __builtin_nontemporal_load(match + (r < n ? r : n - 1));
+      const uint32_t b = __builtin_nontemporal_load(match + (r < n ? r : n - 1));
       key[i] = 0;
       s[i] = 0;
-      m[i] = b >= 0 ? 1u : 0u;
-      first[i] = (uint32_t)b;
+      m[i] = b != ~0u ? 1u : 0u;
+      first[i] = b;
       continue;
     }
     // clamped, unconditional: a conditional load compiles to a branch and a wait per item
@@ -441,6 +441,17 @@ __global__ __launch_bounds__(HJ_THREADS, HJ_ITEMS <= 8 ? 4 : 1) void hj_probe_ke
   }
 }
 
+// the largest build row id a join carries (brows), as unsigned: the probe keeps a matched
+// build row in 32 bits (the match array, the one-pass `first`), so ids must stay < 2^32 - 1
+__global__ void max_row_kernel(const int64_t *__restrict__ rows, uint64_t n, unsigned long long *__restrict__ out) {
+  uint64_t m = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    m = max(m, (uint64_t)rows[i]);
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) m = max(m, (uint64_t)__shfl_xor(m, off, 64));
+  if ((threadIdx.x & 63) == 0 && m) atomicMax(out, (unsigned long long)m);
+}
+
 __global__ void matched_kernel(const int64_t *__restrict__ bi, uint64_t n, int64_t *__restrict__ out) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
     out[i] = bi[i] >= 0 ? 1 : 0;
@@ -473,7 +484,7 @@ namespace {
 
 using HjProbeFn = void (*)(HjTable, const int64_t *, uint64_t, int, uint32_t *, uint64_t *, uint32_t,
                            unsigned long long *, int64_t *, int64_t *, uint64_t, uint32_t *, const uint32_t *,
-                           const int64_t *, const int32_t *);
+                           const int64_t *, const uint32_t *);
 struct HjCfg {
   int threads;
   uint32_t tile;
@@ -489,7 +500,7 @@ constexpr HjCfg hj_make() {
 struct HjMatchCfg {
   int threads;
   uint32_t tile;
-  void (*fn)(HjTable, const int64_t *, uint64_t, int32_t *);
+  void (*fn)(HjTable, const int64_t *, uint64_t, uint32_t *);
 };
 template <int T, int I>
 constexpr HjMatchCfg hj_match_make() {
@@ -616,12 +627,24 @@ nut_status join_build(nut_ctx *c, nut_join *j, const int64_t *build, uint64_t nb
   return NUT_OK;
 }
 
+// the two-pass write's match array (4 B per probe row), or NULL when HBM has no room for it
+// (the caller then takes the one-pass ordered write, which needs none)
+uint32_t *match_buffer(nut_ctx *c, uint64_t np) {
+  uint32_t *m = nullptr;
+  if (hipMallocAsync((void **)&m, np * 4, c->stream) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  return m;
+}
+
 // one probe pass; WRITE: pairs below cap into (pi, bi).  Returns the pair count.
 nut_status join_probe(nut_join *j, bool write, int64_t *pi, int64_t *bi, uint64_t cap, uint64_t *npairs) {
   nut_ctx *c = j->ctx;
   hipStream_t st = c->stream;
   *npairs = 0;
   if (!j->ntiles) return NUT_OK;
+  uint32_t *match = nullptr;
   if (j->any_order && write) {
     NUT_HIP(hipMemsetAsync(j->ticket, 0, 16, st));
     const HjCfg &cf = hj_any_cfg(j->any_cfg);
@@ -630,13 +653,15 @@ nut_status join_probe(nut_join *j, bool write, int64_t *pi, int64_t *bi, uint64_
     cf.any<<<dim3((unsigned)nt), dim3(cf.threads), 0, st>>>(j->t, j->probe, j->np, j->type, j->ticket, j->status,
                                                          (uint32_t)nt, j->total, pi, bi, cap, j->err,
                                                          (const uint32_t *)j->dup, j->prows, nullptr);
-  } else if (write && j->two_pass) {
+  } else if (write && j->two_pass && (match = match_buffer(c, j->np)) != nullptr) {
     // two passes (at most one build row per probe row): the walks, then the ordered write-out
+    // (no room for the match array: the one-pass form below)
     const HjCfg &cf = hj_emit_cfg();
     const uint64_t nt = (j->np + cf.tile - 1) / cf.tile;
-    if (nt > j->ntiles) return fail(NUT_ERR_UNSUPPORTED, "nut_join: write-out tiles exceed the status array");
-    int32_t *match = nullptr;
-    NUT_HIP(hipMallocAsync((void **)&match, j->np * 4, st));
+    if (nt > j->ntiles) {
+      (void)hipFreeAsync(match, st);
+      return fail(NUT_ERR_UNSUPPORTED, "nut_join: write-out tiles exceed the status array");
+    }
     const HjMatchCfg &mc = hj_match_cfg(j->any_cfg);
     hipLaunchKernelGGL(mc.fn, dim3((unsigned)((j->np + mc.tile - 1) / mc.tile)), dim3(mc.threads), 0, st, j->t,
                        j->probe, j->np, match);
@@ -676,7 +701,25 @@ nut_status join_begin(nut_ctx *c, const int64_t *build, uint64_t nb, const int64
   j->any_order = any_order;
   j->brows = brows;
   j->prows = prows;
-  nut_status s = join_build(c, j, build, nb);
+  nut_status s = NUT_OK;
+  if (brows && nb) {  // build row ids must fit the probe's 32-bit match words (fail loudly, never truncate)
+    unsigned long long *mx = (unsigned long long *)c->host_pinned + 8;
+    unsigned long long *dmx = nullptr;
+    hipError_t e = hipMallocAsync((void **)&dmx, 8, c->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(dmx, 0, 8, c->stream);
+    if (e == hipSuccess) {
+      const unsigned g = (unsigned)std::min<uint64_t>((nb + 255) / 256, c->num_cus * 8ull);
+      hipLaunchKernelGGL(max_row_kernel, dim3(g), dim3(256), 0, c->stream, brows, nb, dmx);
+      e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(mx, dmx, 8, hipMemcpyDeviceToHost, c->stream);
+    if (dmx) (void)hipFreeAsync(dmx, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) s = hip_fail(e, who);
+    else if (*mx >= 0xFFFFFFFFull)
+      s = fail(NUT_ERR_UNSUPPORTED, std::string(who) + ": build row ids >= 2^32 - 1 (the probe keeps 32-bit build rows)");
+  }
+  if (!s) s = join_build(c, j, build, nb);
   // the ordered write in two passes when no probe row can have two build rows
   // (NUT_OPT_JOIN_MATCH; SEMI / ANTI always, INNER / LEFT when the build keys are unique)
   if (!s && !any_order && np && c->opt[NUT_OPT_JOIN_MATCH] != 0) {

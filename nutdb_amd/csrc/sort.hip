@@ -312,6 +312,31 @@ __global__ void sort_key_kernel(const uint64_t *__restrict__ in, int type, int d
   }
 }
 
+// f64 bit patterns <-> int64 words whose signed order is the IEEE total order (-NaN < -inf
+// < ... < -0 < +0 < ... < +inf < +NaN): a set sign bit flips the other 63 bits.  The map
+// is its own inverse, so the same launch maps the sorted words back.  `canon` (GROUP BY
+// keys): -0.0 is +0.0 and every NaN the quiet +NaN first, so equal values share one word.
+__global__ void f64_signed_order_kernel(const uint64_t *__restrict__ in, uint64_t *__restrict__ out, uint64_t n,
+                                        int canon) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t b = in[i];
+    if (canon) {
+      if ((b << 1) == 0) b = 0;                                           // -0.0 -> +0.0
+      if ((b & 0x7FFFFFFFFFFFFFFFull) > 0x7FF0000000000000ull) b = kF64CanonNaN;  // NaN -> +qNaN
+    }
+    out[i] = b ^ ((uint64_t)((int64_t)b >> 63) >> 1);
+  }
+}
+
+nut_status f64_signed_order(nut_ctx *c, const uint64_t *in, uint64_t *out, uint64_t n, bool canon) {
+  if (n == 0) return NUT_OK;
+  DeviceGuard g(c->device);
+  const unsigned gk = (unsigned)std::min<uint64_t>((n + 255) / 256, (uint64_t)c->num_cus * 16);
+  hipLaunchKernelGGL(f64_signed_order_kernel, dim3(gk), dim3(256), 0, c->stream, in, out, n, canon ? 1 : 0);
+  NUT_HIP(hipGetLastError());
+  return NUT_OK;
+}
+
 // Status granules for `ntiles` tiles, tagged with a fresh pass epoch.  The array is
 // cleared only when it is (re)allocated or the 8-bit epoch wraps.
 nut_status next_status(nut_ctx *c, uint64_t ntiles, uint64_t **status, uint32_t *epoch) {

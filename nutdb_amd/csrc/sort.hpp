@@ -15,6 +15,10 @@ nut_status msd_sort_i64(nut_ctx *c, const int64_t *in, int64_t *out, uint64_t n,
 // unstable range partition by <= 63 ascending splitters (the sample sort's send layout)
 nut_status partition_i64_ranges(nut_ctx *c, const int64_t *in, uint64_t n, const int64_t *spl, int ns, int64_t *out,
                                 uint64_t *counts_host);  // msd_sort.hip
+// f64 bits <-> int64 words in the IEEE total order (an involution; in == out allowed),
+// stream-ordered; canon: -0.0 -> +0.0 and NaN -> kF64CanonNaN first (GROUP BY keys)
+constexpr uint64_t kF64CanonNaN = 0x7FF8000000000000ull;
+nut_status f64_signed_order(nut_ctx *c, const uint64_t *in, uint64_t *out, uint64_t n, bool canon = false);  // sort.hip
 nut_status join_matched(nut_ctx *c, const int64_t *bi, uint64_t n, int64_t *out);                   // join.hip
 nut_status hash_partition16(nut_ctx *c, const int64_t *keys, uint64_t n, uint64_t kx, int64_t *tmpk,  // aggregate.hip
                             int64_t *tmpr, int64_t *outk, int64_t *outr, std::vector<uint64_t> &counts,

@@ -337,8 +337,9 @@ int xpr_type(const XNode &x, const std::vector<int> &types) {
   return t;
 }
 
-nut_status exec_groupby(nut_ctx *c, const nut_plan &p, const nut_column *const *bound, const Dict *const *dicts,
-                        uint64_t n, uint64_t hint, nut_result *r) {
+// fkey[j]: GROUP BY key j is a float64 column bound to its key words (exec_groupby)
+nut_status groupby_bound(nut_ctx *c, const nut_plan &p, const nut_column *const *bound, const Dict *const *dicts,
+                         uint64_t n, uint64_t hint, nut_result *r, const std::vector<char> &fkey) {
   nut_agg_spec s;
   ProgStore store;  // program nodes, alive until nut_groupby returns
   std::vector<int> agg_f64;
@@ -376,6 +377,10 @@ nut_status exec_groupby(nut_ctx *c, const nut_plan &p, const nut_column *const *
         out_dict[j] = dicts[dc];
       }
       for (uint64_t i = 0; i < ng; ++i) col[i] = (uint64_t)keys[i * nk + o.a];
+      if ((size_t)o.a < fkey.size() && fkey[o.a]) {  // key words -> the (canonical) float64 values
+        type = NUT_T_F64;
+        for (uint64_t &w : col) w ^= (uint64_t)((int64_t)w >> 63) >> 1;
+      }
     } else if (o.kind == OUT_AGG) {
       type = agg_f64[o.a] ? NUT_T_F64 : NUT_T_I64;
       for (uint64_t i = 0; i < ng; ++i) col[i] = words[i * na + o.a];
@@ -452,9 +457,9 @@ nut_status exec_groupby(nut_ctx *c, const nut_plan &p, const nut_column *const *
           const int c2 = str_of(ok.first, x).compare(str_of(ok.first, y));
           cmp = c2 < 0 ? -1 : c2 > 0 ? 1 : 0;
         } else if (r->types[ok.first] == NUT_T_F64) {
-          double a, b;
-          memcpy(&a, &col[x], 8);
-          memcpy(&b, &col[y], 8);
+          // the IEEE total order (-0.0 < +0.0, NaNs at the ends by sign), as the scans'
+          // ORDER BY: a strict weak order even over NaN
+          const uint64_t a = f64_to_ord(col[x]), b = f64_to_ord(col[y]);
           cmp = a < b ? -1 : a > b ? 1 : 0;
         } else {
           int64_t a = (int64_t)col[x], b = (int64_t)col[y];
@@ -491,6 +496,42 @@ nut_status exec_groupby(nut_ctx *c, const nut_plan &p, const nut_column *const *
   return NUT_OK;
 }
 
+// GROUP BY over float64 columns: each such key is grouped on a column of
+// int64 words of its own — the IEEE total order with -0.0 = +0.0 and every NaN one value
+// (f64_signed_order, canon; one 16 B/row pass per key) — so the group kernels, the packed
+// key fields and the key-tuple order are the int64 ones, and the outputs decode the words
+// back (+0.0 for the zeros, the quiet +NaN for the NaNs).  A WHERE or aggregate over the
+// same column still reads its float64 values.
+nut_status exec_groupby(nut_ctx *c, const nut_plan &p, const nut_column *const *bound, const Dict *const *dicts,
+                        uint64_t n, uint64_t hint, nut_result *r) {
+  std::vector<char> fkey(p.keys.size(), 0);
+  bool any = false;
+  for (size_t j = 0; j < p.keys.size(); ++j)
+    if (p.keys[j] >= 0 && bound[p.keys[j]]->type == NUT_T_F64 && !(dicts && dicts[p.keys[j]])) fkey[j] = 1, any = true;
+  if (!any) return groupby_bound(c, p, bound, dicts, n, hint, r, fkey);
+  nut_plan q = p;
+  std::vector<const nut_column *> b(bound, bound + p.cols.size());
+  std::vector<const Dict *> d(p.cols.size(), nullptr);
+  if (dicts) d.assign(dicts, dicts + p.cols.size());
+  std::deque<DevBuf> words;
+  std::deque<nut_column> wcols;
+  for (size_t j = 0; j < p.keys.size(); ++j) {
+    if (!fkey[j]) continue;
+    const nut_column *fc = bound[p.keys[j]];
+    words.emplace_back();
+    if (words.back().alloc(c, std::max<uint64_t>(n, 1) * 8) != hipSuccess) return fail(NUT_ERR_OOM, "hipMalloc (float64 keys)");
+    nut_status st = f64_signed_order(c, (const uint64_t *)fc->data, (uint64_t *)words.back().p, p.never ? 0 : n, true);
+    if (st) return st;
+    wcols.push_back(nut_column{fc->name, words.back().p, NUT_T_I64});
+    const int ci = (int)q.cols.size();
+    q.cols.push_back("\x1f" "f64key:" + p.cols[p.keys[j]]);
+    b.push_back(&wcols.back());
+    d.push_back(nullptr);
+    q.keys[j] = ci;
+    if (j < q.key_progs.size() && q.key_progs[j].size() == 1 && q.key_progs[j][0].op == NUT_P_COL) q.key_progs[j][0].col = ci;
+  }
+  return groupby_bound(c, q, b.data(), d.data(), n, hint, r, fkey);
+}
 
 }  // namespace plan
 }  // namespace nut

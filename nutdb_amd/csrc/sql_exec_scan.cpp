@@ -90,13 +90,7 @@ bool computed_proj(const nut_plan &p, size_t j) { return j < p.proj_val.size() &
 // projection's NULL mask fills the result's validity flags.
 nut_status exec_sort_rows(nut_ctx *c, const nut_plan &p, const nut_column *const *bound, const Dict *const *dicts,
                           uint64_t n, nut_result *r) {
-  for (const auto &k : p.sort_keys) {
-    if (dicts && dicts[k.first])
-      return fail(NUT_ERR_PLAN, "ORDER BY string column '" + p.cols[k.first] + "' is not executed (dictionary codes "
-                                "are in first-seen order)");
-    if (bound[k.first]->type != NUT_T_I64 && bound[k.first]->type != NUT_T_F64)
-      return fail(NUT_ERR_PLAN, "ORDER BY column '" + p.cols[k.first] + "' must be int64 or float64");
-  }
+  // (ORDER BY keys checked by scan_route: int64 or float64, no strings)
   const size_t np = p.projs.size();
   // computed projections: groups of <= NUT_MAX_AGGS programs, one eval spec each
   std::vector<size_t> comp;
@@ -237,16 +231,64 @@ nut_status exec_sort_rows(nut_ctx *c, const nut_plan &p, const nut_column *const
   return NUT_OK;
 }
 
-nut_status exec_scan(nut_ctx *c, const nut_plan &p, const nut_column *const *bound, const Dict *const *dicts,
-                     uint64_t n, nut_result *r) {
+// Which executor a FILTER / SORT plan takes over its bound columns (host only; also the
+// nut_plan_route test hook).  Fused scans compare and sort int64 words: a float64 column
+// (projected or compared) reruns in expression mode, where the WHERE is a program that
+// compares in f64 and a single-key sort maps the f64 bits to int64 words in the IEEE
+// total order first (S_EXPR_SORT_F64); string FILTER scans rerun the same way (codes
+// gathered, then decoded).  Several keys / projections and computed projections are
+// row-id scans (exec_sort_rows: nut_sort_pairs sorts f64 keys in the same total order).
+nut_status scan_route(const nut_plan &p, const nut_column *const *bound, const Dict *const *dicts, ScanRoute *route) {
   bool computed = false;
   for (size_t j = 0; j < p.projs.size(); ++j) computed = computed || computed_proj(p, j);
   if (computed || (p.kind == NUT_PLAN_SORT &&
-                   !(p.sort_keys.size() == 1 && p.projs.size() == 1 && p.sort_keys[0].first == p.proj)))
-    return exec_sort_rows(c, p, bound, dicts, n, r);
-  const nut_column *col = bound[p.proj];
-  if (!p.compiled && p.kind == NUT_PLAN_FILTER && dicts && dicts[p.proj]) {
-    // a string column: rerun as an expression-mode scan (codes gathered, then decoded)
+                   !(p.sort_keys.size() == 1 && p.projs.size() == 1 && p.sort_keys[0].first == p.proj))) {
+    for (const auto &k : p.sort_keys) {
+      if (dicts && dicts[k.first])
+        return fail(NUT_ERR_PLAN, "ORDER BY string column '" + p.cols[k.first] + "' is not executed (dictionary codes "
+                                  "are in first-seen order)");
+      if (bound[k.first]->type != NUT_T_I64 && bound[k.first]->type != NUT_T_F64)
+        return fail(NUT_ERR_PLAN, "ORDER BY column '" + p.cols[k.first] + "' must be int64 or float64");
+    }
+    *route = S_ROWID;
+    return NUT_OK;
+  }
+  bool f64 = false;
+  for (int pj : p.projs) f64 = f64 || bound[pj]->type == NUT_T_F64;
+  for (const PlanPred &pr : p.preds) f64 = f64 || bound[pr.col]->type == NUT_T_F64;
+  if (!p.compiled && (f64 || (p.kind == NUT_PLAN_FILTER && dicts && dicts[p.proj]))) {
+    *route = S_RERUN_EXPR;
+    return NUT_OK;
+  }
+  for (int pj : p.projs)
+    if (dicts && dicts[pj] && !(p.compiled && p.kind == NUT_PLAN_FILTER))
+      return fail(NUT_ERR_PLAN, "column '" + p.cols[pj] + "' holds strings: sorts and single-column fused scans of "
+                                "strings are not executed");
+  for (const PlanPred &pr : p.preds)
+    if (pr.c.is_str) return fail(NUT_ERR_PLAN, "string constant " + cval_str(pr.c) + " compared with an int64 column");
+  for (int pj : p.projs)
+    if (bound[pj]->type != NUT_T_I64 && !(p.compiled && bound[pj]->type == NUT_T_F64))
+      return fail(NUT_ERR_PLAN, "column '" + p.cols[pj] + "' must be int64 or float64 for this scan/sort");
+  if (p.compiled)
+    *route = p.kind == NUT_PLAN_FILTER ? S_EXPR_FILTER : f64 ? S_EXPR_SORT_F64 : S_EXPR_SORT;
+  else
+    *route = p.kind == NUT_PLAN_FILTER ? S_FUSED_FILTER : S_FUSED_SORT;
+  return NUT_OK;
+}
+
+const char *scan_route_name(ScanRoute r) {
+  static const char *const k[] = {"rowid-scan", "rerun-expression", "expr-filter", "expr-sort", "expr-sort-f64-order",
+                                  "fused-filter", "fused-sort"};
+  return k[r];
+}
+
+nut_status exec_scan(nut_ctx *c, const nut_plan &p, const nut_column *const *bound, const Dict *const *dicts,
+                     uint64_t n, nut_result *r) {
+  ScanRoute route;
+  nut_status rs = scan_route(p, bound, dicts, &route);
+  if (rs) return rs;
+  if (route == S_ROWID) return exec_sort_rows(c, p, bound, dicts, n, r);
+  if (route == S_RERUN_EXPR) {  // the WHERE as one program, then the expression-mode scan
     nut_plan q = p;
     std::vector<PProg> cs;
     for (const PlanPred &pr : p.preds) cs.push_back(pred_prog(pr));
@@ -255,17 +297,7 @@ nut_status exec_scan(nut_ctx *c, const nut_plan &p, const nut_column *const *bou
     q.where = and_all(cs);
     return exec_scan(c, q, bound, dicts, n, r);
   }
-  // string columns: expression-mode FILTER scans gather their codes and decode on output
-  for (int pj : p.projs)
-    if (dicts && dicts[pj] && !(p.compiled && p.kind == NUT_PLAN_FILTER))
-      return fail(NUT_ERR_PLAN, "column '" + p.cols[pj] + "' holds strings: sorts and single-column fused scans of "
-                                "strings are not executed");
-  for (const PlanPred &pr : p.preds)
-    if (pr.c.is_str) return fail(NUT_ERR_PLAN, "string constant " + cval_str(pr.c) + " compared with an int64 column");
-  // fused scans and sorts: int64; expression-mode FILTER scans: int64 or float64 columns
-  for (int pj : p.projs)
-    if (bound[pj]->type != NUT_T_I64 && !(p.compiled && p.kind == NUT_PLAN_FILTER && bound[pj]->type == NUT_T_F64))
-      return fail(NUT_ERR_PLAN, "column '" + p.cols[pj] + "' must be int64 for this scan/sort");
+  const nut_column *col = bound[p.proj];
   for (size_t j = 0; j < p.projs.size(); ++j) {
     r->names.push_back(p.outs[j].name);
     r->types.push_back(dicts && dicts[p.projs[j]] ? NUT_T_STR : bound[p.projs[j]]->type);
@@ -305,6 +337,10 @@ nut_status exec_scan(nut_ctx *c, const nut_plan &p, const nut_column *const *bou
       DevBuf vals, pos, cv;
       NUT_HIP(vals.alloc(c, std::max<uint64_t>(cnt, 1) * 8));
       s = nut_gather_u64(c, (const uint64_t *)col->data, (const int64_t *)rows.p, cnt, 0, (uint64_t *)vals.p);
+      // float64: the words sort (and top-k select) as int64 in the IEEE total order, and
+      // map back after the sort (-0.0 before +0.0, NaNs at the ends by sign)
+      const bool fo = route == S_EXPR_SORT_F64;
+      if (!s && fo) s = f64_signed_order(c, (const uint64_t *)vals.p, (uint64_t *)vals.p, cnt);
       uint64_t m2 = cnt;  // ORDER BY ... LIMIT: only the top-k candidates are sorted
       if (!s) s = topk_reduce(c, p, vals.p, NUT_T_I64, p.desc, cnt, pos, &m2);
       if (!s && m2 < cnt) {
@@ -315,6 +351,7 @@ nut_status exec_scan(nut_ctx *c, const nut_plan &p, const nut_column *const *bou
       }
       if (!s) s = p.desc ? nut_sort_i64_desc(c, (const int64_t *)vals.p, (int64_t *)r->dev, cnt)
                          : nut_sort_i64(c, (const int64_t *)vals.p, (int64_t *)r->dev, cnt);
+      if (!s && fo) s = f64_signed_order(c, (const uint64_t *)r->dev, (uint64_t *)r->dev, cnt);
     }
     if (!s) s = nut_ctx_sync(c);
     if (s) return s;
@@ -470,25 +507,18 @@ std::string substr_bytes(const std::string &s, int off, i128 len) {
 
 namespace {
 // substring(col, off, len) over a dictionary (P_SUBSTR): the table code -> the code of its
-// substring in the same dictionary.  The dictionary gains the substrings it lacks — append
-// only, so every code already handed out (the table's columns, earlier results) keeps its
-// string — which lets a substring meet the column's own strings, string constants and
-// GROUP BY decoding exactly as a column does.  An Enum's declared dictionary cannot grow.
+// substring.  The substrings the dictionary lacks get codes in the execution's overlay
+// (Dict::overlay, DictOverlays: the table's dictionary is only read), so a substring meets
+// the column's own strings, string constants and GROUP BY decoding exactly as a column
+// does, within the query.  An Enum's declared dictionary cannot grow.
 nut_status substr_map(const Dict *cd, const std::string &cname, int off, i128 len, std::vector<int64_t> &map) {
   if (!cd) return fail(NUT_ERR_PLAN, "substring needs a string column ('" + cname + "')");
   if (cd->fixed) return fail(NUT_ERR_PLAN, "substring over the Enum column '" + cname + "' is not executed");
-  Dict *d = const_cast<Dict *>(cd);
-  const size_t n0 = d->strs.size();
+  if (!cd->base) return fail(NUT_ERR_INVALID_ARG, "substring over '" + cname + "': no query-local dictionary");
+  Dict *d = const_cast<Dict *>(cd);  // (the execution's own overlay)
+  const size_t n0 = d->size();
   map.resize(n0);
-  for (size_t i = 0; i < n0; ++i) {
-    std::string t = substr_bytes(d->strs[i], off, len);
-    auto it = d->codes.find(t);
-    if (it == d->codes.end()) {
-      it = d->codes.emplace(t, (int64_t)d->strs.size()).first;
-      d->strs.push_back(std::move(t));
-    }
-    map[i] = it->second;
-  }
+  for (size_t i = 0; i < n0; ++i) map[i] = d->intern(substr_bytes(d->at(i), off, len));
   return NUT_OK;
 }
 }  // namespace
@@ -568,10 +598,10 @@ nut_status build_spec(const nut_plan &p, const nut_column *const *bound, const D
         table.assign((size_t)(hi + 1), 0);
         for (const auto &kv : d->codes) table[(size_t)kv.second] = like_match(kv.first, n.c.s, ci);
       } else {
-        if (d->strs.size() > (size_t)INT32_MAX)
+        if (d->size() > (size_t)INT32_MAX)
           return fail(NUT_ERR_PLAN, "LIKE over a dictionary of more than 2^31 strings");
-        table.resize(d->strs.size());
-        for (size_t i = 0; i < d->strs.size(); ++i) table[i] = like_match(d->strs[i], n.c.s, ci);
+        table.resize(d->size());
+        for (size_t i = 0; i < d->size(); ++i) table[i] = like_match(d->at(i), n.c.s, ci);
       }
       nut_prog_node lk{NUT_P_LOOKUP, (int32_t)table.size(), 0};
       if (!table.empty()) {

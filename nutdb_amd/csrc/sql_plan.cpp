@@ -310,6 +310,63 @@ nut_status nut_plan_describe(const nut_plan *p, char *buf, size_t cap, size_t *l
   return put_text(describe(*p), buf, cap, len);
 }
 
+nut_status nut_plan_route(const nut_plan *p, const nut_column *cols, int ncols, char *buf, size_t cap, size_t *len) {
+  if (!p || (ncols && !cols) || ncols < 0) return fail(NUT_ERR_INVALID_ARG, "nut_plan_route: NULL argument");
+  if (p->join >= 0 || p->inner || !p->uni.empty() || !p->subs.empty())
+    return fail(NUT_ERR_INVALID_ARG, "nut_plan_route: single-table plans without subqueries or UNION only");
+  nut_plan sq;
+  if (p->star) {
+    std::vector<std::string> names;
+    for (int i = 0; i < ncols; ++i)
+      if (cols[i].name) names.push_back(cols[i].name);
+    p = expand_star(*p, names, sq);
+  }
+  std::vector<const nut_column *> bound(p->cols.size());
+  for (size_t i = 0; i < p->cols.size(); ++i) {
+    bound[i] = bind(*p, (int)i, cols, ncols);
+    if (!bound[i]) return fail(NUT_ERR_INVALID_ARG, "nut_plan_route: column '" + p->cols[i] + "' is not bound");
+    if (bound[i]->type != NUT_T_I64 && bound[i]->type != NUT_T_F64)
+      return fail(NUT_ERR_INVALID_ARG, "nut_plan_route: column '" + p->cols[i] + "' has an unknown type");
+  }
+  std::string route;
+  if (p->kind == NUT_PLAN_GROUPBY) {
+    nut_agg_spec s;
+    ProgStore store;
+    std::vector<int> agg_f64;
+    GbExtra gx;
+    // float64 key columns are grouped on int64 key words (exec_groupby)
+    std::deque<nut_column> words;
+    int nf = 0;
+    for (int k : p->keys)
+      if (k >= 0 && bound[k]->type == NUT_T_F64) {
+        words.push_back(nut_column{bound[k]->name, nullptr, NUT_T_I64});
+        bound[k] = &words.back();
+        ++nf;
+      }
+    nut_status st = build_spec(*p, bound.data(), nullptr, 0, s, store, agg_f64, &gx);
+    if (st) return st;
+    route = gx.active ? "packed-groupby" : p->compiled ? "expr-groupby" : "fused-groupby";
+    if (nf) route += " (float64 key words)";
+  } else {
+    ScanRoute r;
+    nut_status st = scan_route(*p, bound.data(), nullptr, &r);
+    if (st) return st;
+    route = scan_route_name(r);
+    if (r == S_RERUN_EXPR) {  // and where the rerun lands
+      nut_plan q = *p;
+      std::vector<PProg> cs;
+      for (const PlanPred &pr : p->preds) cs.push_back(pred_prog(pr));
+      q.compiled = true;
+      q.preds.clear();
+      q.where = and_all(cs);
+      st = scan_route(q, bound.data(), nullptr, &r);
+      if (st) return st;
+      route += std::string(" -> ") + scan_route_name(r);
+    }
+  }
+  return put_text(route, buf, cap, len);
+}
+
 void nut_plan_free(nut_plan *p) { delete p; }
 
 nut_status nut_plan_execute(nut_ctx *c, const nut_plan *p, const nut_column *cols, int ncols, uint64_t nrows,
@@ -596,6 +653,7 @@ nut_status nut_table_execute(nut_ctx *c, nut_table *t, const nut_plan *p, uint64
   std::vector<nut_column> cols(p->cols.size());
   std::vector<const nut_column *> bound(p->cols.size());
   std::vector<const Dict *> dicts(p->cols.size(), nullptr);
+  DictOverlays ov;  // the query's own view of the table's dictionary (substring results)
   for (size_t i = 0; i < p->cols.size(); ++i) {
     const TCol *tc = nullptr;
     for (const TCol &x : t->cols)
@@ -606,7 +664,7 @@ nut_status nut_table_execute(nut_ctx *c, nut_table *t, const nut_plan *p, uint64
     if (!tc) return fail(NUT_ERR_PLAN, "table '" + t->name + "' has no column '" + p->cols[i] + "'");
     cols[i] = nut_column{tc->name.c_str(), tc->dev, tc->exec_type};
     bound[i] = &cols[i];
-    dicts[i] = tc->dict;
+    dicts[i] = ov.of(tc->dict);
   }
   nut_result *r = new (std::nothrow) nut_result;
   if (!r) return fail(NUT_ERR_OOM, "nut_table_execute: out of host memory");
@@ -651,6 +709,7 @@ nut_status nut_table_execute2(nut_ctx *c, nut_table *left, nut_table *right, con
   *out = nullptr;
   std::vector<nut_column> cols[2];
   std::vector<const Dict *> dicts[2];
+  DictOverlays ov;
   nut_table *t2[2] = {left, right};
   for (int k = 0; k < 2; ++k) {
     nut_table *t = t2[k];
@@ -659,7 +718,7 @@ nut_status nut_table_execute2(nut_ctx *c, nut_table *left, nut_table *right, con
       return fail(NUT_ERR_INVALID_ARG, "nut_table_execute2: table '" + t->name + "' lives on another device");
     for (const TCol &x : t->cols) {
       cols[k].push_back(nut_column{x.name.c_str(), x.dev, x.exec_type});
-      dicts[k].push_back(x.dict);
+      dicts[k].push_back(ov.of(x.dict));
     }
   }
   nut_result *r = new (std::nothrow) nut_result;
@@ -720,6 +779,7 @@ nut_status nut_table_executen(nut_ctx *c, nut_table *const *tables, int ntables,
   *out = nullptr;
   std::vector<std::vector<nut_column>> cols(ntables);
   std::vector<std::vector<const Dict *>> dicts(ntables);
+  DictOverlays ov;
   std::vector<const nut_column *> tabs(ntables);
   std::vector<const Dict *const *> tdicts(ntables);
   std::vector<int> ncols(ntables);
@@ -731,7 +791,7 @@ nut_status nut_table_executen(nut_ctx *c, nut_table *const *tables, int ntables,
       return fail(NUT_ERR_INVALID_ARG, "nut_table_executen: table '" + t->name + "' lives on another device");
     for (const TCol &x : t->cols) {
       cols[k].push_back(nut_column{x.name.c_str(), x.dev, x.exec_type});
-      dicts[k].push_back(x.dict);
+      dicts[k].push_back(ov.of(x.dict));
     }
     tabs[k] = cols[k].data();
     tdicts[k] = dicts[k].data();

@@ -346,6 +346,9 @@ nut_status topk_reduce(nut_ctx *c, const nut_plan &p, const void *keys, int type
 bool computed_proj(const nut_plan &p, size_t j);
 nut_status exec_sort_rows(nut_ctx *c, const nut_plan &p, const nut_column *const *bound, const Dict *const *dicts,
                           uint64_t n, nut_result *r);
+enum ScanRoute { S_ROWID, S_RERUN_EXPR, S_EXPR_FILTER, S_EXPR_SORT, S_EXPR_SORT_F64, S_FUSED_FILTER, S_FUSED_SORT };
+nut_status scan_route(const nut_plan &p, const nut_column *const *bound, const Dict *const *dicts, ScanRoute *route);
+const char *scan_route_name(ScanRoute r);
 nut_status exec_scan(nut_ctx *c, const nut_plan &p, const nut_column *const *bound, const Dict *const *dicts,
                      uint64_t n, nut_result *r);
 HVal having_val(const HNode &h, const std::vector<std::vector<uint64_t>> &cols, const std::vector<int> &types,

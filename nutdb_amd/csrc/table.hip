@@ -210,9 +210,7 @@ nut_status nut_table_append(nut_ctx *c, nut_table *t, int j, const void *data, c
       int64_t code = d.find(s);
       if (code < 0) {
         if (d.fixed) return fail(NUT_ERR_INVALID_ARG, "column '" + col.name + "': '" + s + "' is not a value of its Enum");
-        code = (int64_t)d.strs.size();
-        d.codes.emplace(s, code);
-        d.strs.push_back(std::move(s));
+        code = d.intern(std::move(s));
       }
       codes[i] = code;
     }

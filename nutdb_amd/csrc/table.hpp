@@ -15,6 +15,7 @@
 // codes are in first-seen order (no ordering), so strings support = / != / IN only.
 #pragma once
 
+#include <memory>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -24,12 +25,39 @@
 namespace nut {
 
 struct Dict {
-  std::vector<std::string> strs;                 // code -> string
+  std::vector<std::string> strs;                 // code -> string (an overlay: codes from base_n on)
   std::unordered_map<std::string, int64_t> codes;  // string -> code
   bool fixed = false;                            // Enum: the declaration is the dictionary
+  // A query-local overlay over a table's dictionary: strings a query derives
+  // (substring results) get codes after the base's, in the overlay only — the table's
+  // dictionary is never written during a query, so concurrent queries only read it and no
+  // query's strings leak into another's per-code tables.
+  const Dict *base = nullptr;
+  size_t base_n = 0;
+  static Dict overlay(const Dict *b) {
+    Dict o;
+    o.base = b;
+    o.base_n = b->strs.size();
+    return o;
+  }
+  size_t size() const { return base_n + strs.size(); }  // codes [0, size()) (not Enum)
+  const std::string &at(size_t c) const { return c < base_n ? base->strs[c] : strs[c - base_n]; }
   int64_t find(const std::string &s) const {
+    if (base) {
+      const int64_t b = base->find(s);
+      if (b >= 0) return b;
+    }
     auto it = codes.find(s);
     return it == codes.end() ? -1 : it->second;
+  }
+  // the code of s, appended to this dictionary if absent (overlays and table loads only)
+  int64_t intern(std::string s) {
+    const int64_t k = find(s);
+    if (k >= 0) return k;
+    const int64_t code = (int64_t)size();
+    codes.emplace(s, code);
+    strs.push_back(std::move(s));
+    return code;
   }
   const std::string *decode(int64_t c) const {
     if (fixed) {
@@ -37,7 +65,19 @@ struct Dict {
         if (kv.second == c) return &kv.first;
       return nullptr;
     }
-    return c >= 0 && (uint64_t)c < strs.size() ? &strs[(size_t)c] : nullptr;
+    return c >= 0 && (uint64_t)c < size() ? &at((size_t)c) : nullptr;
+  }
+};
+
+// the overlays of one execution: one per table dictionary it binds (Enums stay as they are)
+struct DictOverlays {
+  std::vector<std::pair<const Dict *, std::unique_ptr<Dict>>> o;
+  const Dict *of(const Dict *d) {
+    if (!d || d->fixed) return d;
+    for (auto &x : o)
+      if (x.first == d) return x.second.get();
+    o.emplace_back(d, std::unique_ptr<Dict>(new Dict(Dict::overlay(d))));
+    return o.back().second.get();
   }
 };
 

@@ -197,6 +197,20 @@ class Plan:
             arr[i].type = {"int64": T_I64, "float64": T_F64}[t]
         check(lib.nut_plan_prepare(self._h, arr, len(types)), "nut_plan_prepare")
 
+    def route(self, types: Dict[str, str]) -> str:
+        """The executor route over columns of these types (nut_plan_route: host only, no
+        GPU) — e.g. "fused-sort", "rerun-expression -> expr-sort-f64-order"; raises the
+        NutError execution would raise for a shape the executor rejects."""
+        arr = (NutColumn * max(len(types), 1))()
+        names = [k.encode() for k in types]
+        for i, (name, t) in enumerate(types.items()):
+            arr[i].name = names[i]
+            arr[i].data = None
+            arr[i].type = {"int64": T_I64, "float64": T_F64}[t]
+        fn = lambda h, buf, cap, ln: lib.nut_plan_route(h, arr, len(types), buf, cap, ln)  # noqa: E731
+        fn.__name__ = "nut_plan_route"
+        return _text(fn, self._h)
+
     def execute(self, ex, columns: Dict[str, "object"], nrows: Optional[int] = None,
                 group_hint: int = 0) -> Dict[str, np.ndarray]:
         """Run on the GPU of executor `ex` with `columns` = {name: 1-D int64/float64 CUDA

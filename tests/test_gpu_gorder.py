@@ -289,3 +289,26 @@ def test_ordered_heavy_pass_two_value_columns(ex, orc):
     ok, ow = orc.groupby([kh], [(0, 0, (0,)), (2, 0, (0,)), (3, 0, (0,)), (0, 0, (1,)), (3, 0, (1,)), (1, 0, ())],
                          values=[iv_h, fv.cpu().numpy()])
     assert np.array_equal(k, ok) and np.array_equal(w.view(np.uint64), ow)
+
+
+@pytest.mark.parametrize("nkeys", [1, 400])
+def test_ordered_all_rows_heavy(ex, orc, nkeys):
+    """few distinct keys under a large group_hint — every key is heavy
+    (<= 2048 / aggregates of them), the heavy pass takes every row and no row is left for
+    the partition levels (the division by the partition count that followed is gone): the
+    heavy groups are the result, as the oracle's."""
+    rng = np.random.default_rng(23)
+    n = 1 << 25
+    pool = rng.integers(I64_MIN, I64_MAX, max(nkeys, 2), dtype=np.int64)
+    pool[1] = pool[0] + (1 << 40)  # (the sampled key range must span >= 2^16)
+    key = pool[rng.integers(0, nkeys, n)] if nkeys > 1 else np.full(n, pool[0])
+    if nkeys == 1:
+        key[::2] = pool[1]
+    val = orc.gen_column(3, 0x6C, n)
+    q = gb_query(dev(key, ex), dev(val, ex))
+    k, w, path = run_to_host(ex, q, 1 << 21, rows=1 << 12)
+    ok, ow = orc.groupby([key], AGGS4, values=[val])
+    check(k, w, ok, ow, sums_exact=True)
+    if path == "partitioned_ordered":
+        hk, hr = ex.groupby_heavy()
+        assert hr == n and hk == len(ok)

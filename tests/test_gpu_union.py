@@ -102,9 +102,11 @@ def test_union_all_of_aggregates(ex):
     assert np.allclose(got["s"], want["s"].to_numpy(), rtol=1e-12, atol=0)
 
 
-def test_union_all_type_mismatch_is_a_plan_error(ex):
+@pytest.mark.parametrize("sql", ["select a from t union all select f from u",
+                                 "select sum(a) from t union all select sum(f) from u"])
+def test_union_all_type_mismatch_is_a_plan_error(ex, sql):
     from nutdb_amd import NutError
     a = torch.arange(10, dtype=torch.int64, device=ex.device)
     f = torch.arange(10, dtype=torch.float64, device=ex.device)
     with pytest.raises(NutError, match="UNION ALL: column 1"):
-        Plan("select sum(a) from t union all select sum(f) from u").execute_tables(ex, [{"a": a}, {"f": f}])
+        Plan(sql).execute_tables(ex, [{"a": a}, {"f": f}])
