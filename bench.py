@@ -145,9 +145,9 @@ class GroupBy:
             # (fresh pageable arrays cost ~10 ms of first-touch page faults at 1e7 groups)
             rows = max(2 * self.G, 1024)
             self.out = tuple(torch.empty((rows, 1), dtype=torch.int64, pin_memory=True).numpy() for _ in range(2))
-        q = AggQuery(keys=[self.key], values=[self.val], aggs=[Agg("sum", "col", (0,))])
+            self.q = AggQuery(keys=[self.key], values=[self.val], aggs=[Agg("sum", "col", (0,))])
         # views of the reused buffers: the last step's result stays
-        return self.ex.groupby_to_host(q, group_hint=self.G, out=self.out)
+        return self.ex.groupby_to_host(self.q, group_hint=self.G, out=self.out)
 
     @staticmethod
     def parity(gpu, cpu):  # dyadic values: the f64 sums are exact, so compare bits

@@ -2430,6 +2430,86 @@ nut_status nut_groups_to_host(nut_groups *g, int64_t *keys, uint64_t *aggs, uint
   return NUT_OK;
 }
 
+// Small results on the on-chip path (the table's slots <= kSmallTail): the aggregation,
+// the table's control words, the compaction and ONE copy of both into page-locked staging
+// are queued back to back and the host waits once (nut_groupby + nut_groups_to_host wait
+// three times and copy through pageable memory).  The compaction writes columns of the
+// table's slot count (an upper bound of the groups), so nothing waits for the group count.
+// *done = false: the table overflowed (more groups than hinted) or the shape takes another
+// path — the caller runs the general one.
+constexpr uint64_t kSmallTail = 1ull << 16;
+nut_status groupby_small_to_host(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hint, int64_t *keys,
+                                 uint64_t *aggs, uint64_t cap, uint64_t *n_out, bool *done) {
+  *done = false;
+  const int64_t gp = c->opt[NUT_OPT_GB_PARTITION];
+  if (s->nkeys == 0 || !s->n) return NUT_OK;
+  if (gp == 1 || (gp != 0 && group_hint >= kGpMinGroups && s->n >= 4 * group_hint)) return NUT_OK;
+  const uint64_t tcap = table_cap_for(group_hint ? group_hint : 8192);
+  if (tcap + 1 > kSmallTail) return NUT_OK;
+  nut_groups *g = new nut_groups();
+  struct Free {
+    nut_groups *g;
+    ~Free() { nut_groups_free(g); }
+  } free_g{g};
+  g->ctx = c;
+  g->nk = s->nkeys;
+  g->naggs = s->naggs;
+  for (int a = 0; a < s->naggs; ++a) g->kinds[a] = kind_of(s, a);
+  c->gb_path = NUT_GB_ONCHIP;
+  c->gb_levels = c->gb_optimistic = 0;
+  nut_status st = alloc_table(g, tcap);
+  if (!st) st = probe_priv_shape(g, s, group_hint, tcap);
+  if (!st) st = launch_agg(g, s, group_hint, g->kinds);
+  if (st) return st;
+  const int nk = g->nk, na = g->naggs, w = nk + na;
+  const uint64_t stride = g->gt.cap + 1;
+  for (auto &b : c->stage)
+    if (!b) NUT_HIP(hipHostMalloc((void **)&b, kStageBytes, hipHostMallocDefault));
+  if ((stride * w + 2) * 8 > kStageBytes) return NUT_OK;
+  uint64_t *dev = nullptr;
+  NUT_HIP(hipMallocAsync((void **)&dev, (size_t)stride * w * 8, c->stream));
+  struct FreeDev {
+    uint64_t *p;
+    hipStream_t s;
+    ~FreeDev() { (void)hipFreeAsync(p, s); }
+  } free_dev{dev, c->stream};
+  uint64_t *host = (uint64_t *)c->stage[0];
+  hipLaunchKernelGGL(gtable_sum_kernel, dim3(1), dim3(256), 0, c->stream, (const GTable *)g->dev_gt);
+  NUT_HIP(hipMemcpyAsync(host, g->gt.ctl, 16, hipMemcpyDeviceToHost, c->stream));
+  NUT_HIP(hipMemsetAsync(g->dev_cursors, 0, 64 * 8, c->stream));
+  const uint64_t blocks = std::min<uint64_t>((stride + GT_CHUNK - 1) / GT_CHUNK, (uint64_t)c->num_cus * 8);
+  hipLaunchKernelGGL(gtable_compact_kernel, dim3((unsigned)blocks), dim3(256), 0, c->stream, (const GTable *)g->dev_gt,
+                     nk, dev, stride, g->dev_cursors, 1, (const uint64_t *)nullptr);
+  NUT_HIP(hipGetLastError());
+  NUT_HIP(hipMemcpyAsync(host + 2, dev, (size_t)stride * w * 8, hipMemcpyDeviceToHost, c->stream));
+  NUT_HIP(hipStreamSynchronize(c->stream));
+  uint32_t ctl[4];
+  memcpy(ctl, host, 16);
+  if (ctl[1] & 2u) return fail(NUT_ERR_INVALID_ARG, "nut_groupby: division by zero in an expression");
+  if (ctl[1] & 1u) return NUT_OK;  // more groups than the table admits: the general path regrows it
+  const uint64_t n = (uint64_t)ctl[0] + (nk == 1 && ctl[2] ? 1 : 0);
+  *done = true;
+  *n_out = n;
+  if (n > cap)
+    return fail(NUT_ERR_CAPACITY, "nut_groupby_to_host: capacity " + std::to_string(cap) + " < " + std::to_string(n) +
+                                      " groups");
+  // key-tuple order, rows out of the column-major staging (columns of `stride` rows)
+  const uint64_t *h = host + 2;
+  std::vector<uint32_t> order(n);
+  for (uint64_t i = 0; i < n; ++i) order[i] = (uint32_t)i;
+  std::sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) {
+    const int64_t a0 = (int64_t)h[x], b0 = (int64_t)h[y];
+    if (a0 != b0) return a0 < b0;
+    return nk == 2 && (int64_t)h[stride + x] < (int64_t)h[stride + y];
+  });
+  for (uint64_t i = 0; i < n; ++i) {
+    const uint64_t src = order[i];
+    for (int j = 0; j < nk; ++j) keys[i * nk + j] = (int64_t)h[(size_t)j * stride + src];
+    for (int a = 0; a < na; ++a) aggs[i * na + a] = h[(size_t)(nk + a) * stride + src];
+  }
+  return NUT_OK;
+}
+
 nut_status nut_groupby_to_host(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hint, int64_t *keys, uint64_t *aggs,
                                uint64_t cap, uint64_t *n_out) {
   if (!c || !n_out) return fail(NUT_ERR_INVALID_ARG, "nut_groupby_to_host: NULL argument");
@@ -2440,6 +2520,11 @@ nut_status nut_groupby_to_host(nut_ctx *c, const nut_agg_spec *s, uint64_t group
   st = groupby_ordered(c, s, group_hint, keys, aggs, cap, n_out);
   if (st != NUT_ERR_UNSUPPORTED) return st;
   *n_out = 0;
+  bool done = false;
+  if (keys && (aggs || !s->naggs)) {
+    st = groupby_small_to_host(c, s, group_hint, keys, aggs, cap, n_out, &done);
+    if (st || done) return st;
+  }
   nut_groups *g = nullptr;
   st = nut_groupby(c, s, group_hint, &g);
   if (st) return st;

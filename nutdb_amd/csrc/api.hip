@@ -147,7 +147,6 @@ __global__ __launch_bounds__(256) void stream_probe_kernel(const u32x4 *__restri
 }
 
 // ------------------------------------------------------------ large D2H
-constexpr size_t kStageBytes = 32u << 20;  // per pinned chunk
 constexpr int kCopyThreads = 8;
 
 nut_status copy_to_host(nut_ctx *c, void *dst, const void *src, size_t bytes) {

@@ -144,6 +144,8 @@ nut_status copy_to_host(nut_ctx *c, void *dst, const void *src, size_t bytes);
 nut_status pool_take(nut_ctx *c, size_t bytes, void **p, size_t *got);
 void pool_give(nut_ctx *c, void *p, size_t bytes);
 
+constexpr size_t kStageBytes = 32u << 20;  // nut_ctx::stage: each pinned chunk
+
 // Device scratch that only grows; reused across calls (no malloc in steady state).
 struct Scratch {
   void *ptr = nullptr;

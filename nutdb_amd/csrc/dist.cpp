@@ -19,6 +19,7 @@
 
 #include <algorithm>
 #include <condition_variable>
+#include <functional>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -40,6 +41,8 @@ struct Rccl {
   decltype(&ncclAllGather) all_gather = nullptr;
   decltype(&ncclAllToAllv) all_to_allv = nullptr;
   decltype(&ncclGetErrorString) error_string = nullptr;
+  decltype(&ncclGroupStart) group_start = nullptr;
+  decltype(&ncclGroupEnd) group_end = nullptr;
   std::string load_error;
 };
 
@@ -65,7 +68,8 @@ const Rccl *rccl() {
     if (!bind(h, "ncclGetUniqueId", r.get_unique_id) || !bind(h, "ncclCommInitRank", r.comm_init_rank) ||
         !bind(h, "ncclCommInitAll", r.comm_init_all) || !bind(h, "ncclCommDestroy", r.comm_destroy) ||
         !bind(h, "ncclAllGather", r.all_gather) || !bind(h, "ncclAllToAllv", r.all_to_allv) ||
-        !bind(h, "ncclGetErrorString", r.error_string)) {
+        !bind(h, "ncclGetErrorString", r.error_string) || !bind(h, "ncclGroupStart", r.group_start) ||
+        !bind(h, "ncclGroupEnd", r.group_end)) {
       g_rccl.load_error = "librccl.so.1 lacks an entry point nut_dist needs";
       return;
     }
@@ -119,7 +123,8 @@ struct nut_dist {
     nut_ctx *ctx = nullptr;
     ncclComm_t comm = nullptr;
     Scratch hdr_dev;                  // headers: this rank's and the all-gathered ones
-    uint64_t *hdr_host = nullptr;     // pinned, kHdrBytes
+    uint64_t *hdr_host = nullptr;     // pinned, kHdrBytes: the all-gathered headers
+    uint64_t *hdr_send = nullptr;     // pinned, kHdrWords + kSamples words: this rank's header, sample positions
     Scratch buf[10];                  // send / receive / output buffers of the calls
   };
   std::vector<Member> m;
@@ -131,6 +136,7 @@ constexpr int kMaxRanks = 64;  // nut_groups_partition / nut_partition_i64 bound
 constexpr size_t kHdrWords = 2 + 2 * kMaxRanks;
 constexpr size_t kHdrBytes = kHdrWords * kMaxRanks * 8;
 constexpr int kSamples = 4096;  // sample sort: strided samples per rank
+constexpr uint64_t kSampleWords = 2 + kSamples;  // one rank's all-gathered [status, has keys, samples]
 constexpr uint64_t kSortFlip = 1ull << 63;  // int64 order -> unsigned order
 
 using Member = nut_dist::Member;
@@ -224,6 +230,51 @@ nut_status alltoallv(nut_dist *d, int l, const uint64_t *send, const size_t *sc,
   return e == hipSuccess ? NUT_OK : hip_fail(e, "nut_dist (virtual) all-to-all");
 }
 
+// Several all-to-alls as one exchange: RCCL runs them inside one ncclGroupStart / End
+// (every link carries all of them at once, one launch and one completion), in rounds in
+// which no (sender, receiver) pair moves more than kA2AChunk words over all of them
+// together (RCCL's per-transfer limit, above).  Virtual ranks run them one after another.
+struct A2A {
+  const uint64_t *send;
+  const size_t *sc, *sd;
+  uint64_t *recv;
+  const size_t *rc, *rd;
+};
+nut_status alltoallv_group(nut_dist *d, int l, const std::vector<A2A> &ops, size_t gmax) {
+  if (d->mode == nut_dist::kVirtual) {
+    for (const A2A &o : ops) {
+      nut_status st = alltoallv(d, l, o.send, o.sc, o.sd, o.recv, o.rc, o.rd, gmax);
+      if (st) return st;
+    }
+    return NUT_OK;
+  }
+  Member &mb = d->m[l];
+  hipStream_t s = mb.ctx->stream;
+  const int P = d->nranks;
+  const size_t chunk = kA2AChunk / std::max<size_t>(ops.size(), 1);
+  const size_t rounds = std::max<size_t>(1, (gmax + chunk - 1) / chunk);
+  std::vector<size_t> c1(P), d1(P), c2(P), d2(P);
+  for (size_t k = 0; k < rounds; ++k) {
+    const size_t o = k * chunk;
+    ncclResult_t e = d->r->group_start();
+    for (size_t i = 0; i < ops.size() && e == ncclSuccess; ++i) {
+      const A2A &a = ops[i];
+      for (int q = 0; q < P; ++q) {
+        c1[q] = a.sc[q] > o ? std::min(chunk, a.sc[q] - o) : 0;
+        d1[q] = a.sd[q] + o;
+        c2[q] = a.rc[q] > o ? std::min(chunk, a.rc[q] - o) : 0;
+        d2[q] = a.rd[q] + o;
+      }
+      e = d->r->all_to_allv(a.send, c1.data(), d1.data(), a.recv, c2.data(), d2.data(), ncclUint64, mb.comm, s);
+    }
+    const ncclResult_t e2 = d->r->group_end();
+    (void)hipGetLastError();
+    if (e != ncclSuccess) return rccl_fail(d->r, e, "ncclAllToAllv (grouped)");
+    if (e2 != ncclSuccess) return rccl_fail(d->r, e2, "ncclGroupEnd");
+  }
+  return NUT_OK;
+}
+
 // All-gather of a `w`-word host header whose word 0 is this rank's status.  On return
 // all[q * w + i] holds rank q's header; NUT_OK only if every rank reported NUT_OK.
 nut_status exchange_header(nut_dist *d, int l, nut_status mine, const std::vector<uint64_t> &hdr,
@@ -233,9 +284,12 @@ nut_status exchange_header(nut_dist *d, int l, nut_status mine, const std::vecto
   std::string my_error = mine ? nut_last_error() : "";
   uint64_t *dev = (uint64_t *)mb.hdr_dev.ptr;
   hipStream_t s = mb.ctx->stream;
-  std::vector<uint64_t> h = hdr;
-  h[0] = (uint64_t)mine;
-  NUT_HIP(hipMemcpyAsync(dev, h.data(), w * 8, hipMemcpyHostToDevice, s));
+  if (w > kHdrWords) return fail(NUT_ERR_INVALID_ARG, "nut_dist: header too wide");
+  // staged in page-locked memory: the copy is stream-ordered, no host wait before the
+  // all-gather (the one synchronization is the read-back below)
+  memcpy(mb.hdr_send, hdr.data(), w * 8);
+  mb.hdr_send[0] = (uint64_t)mine;
+  NUT_HIP(hipMemcpyAsync(dev, mb.hdr_send, w * 8, hipMemcpyHostToDevice, s));
   nut_status st = allgather(d, l, dev, dev + w, w);
   if (st) return st;
   NUT_HIP(hipMemcpyAsync(mb.hdr_host, dev + w, w * d->nranks * 8, hipMemcpyDeviceToHost, s));
@@ -252,6 +306,21 @@ nut_status exchange_header(nut_dist *d, int l, nut_status mine, const std::vecto
 nut_status agree(nut_dist *d, int l, nut_status mine) {
   std::vector<uint64_t> all;
   return exchange_header(d, l, mine, std::vector<uint64_t>(1, 0), all);
+}
+
+// A rank's receive buffers only grow (Scratch), so in steady state they already hold what
+// the next exchange brings and reserving them cannot fail.  Each header carries the rank's
+// capacities (words); after the header every rank knows every rank's needs, so all ranks
+// take the same decision: `agree` on the reservations only when some rank must grow one
+// (a failed hipMalloc then fails the call on every rank instead of leaving the others in
+// the all-to-all), else no second all-gather.
+uint64_t cap_words(const Member &mb, int i) { return mb.buf[i].bytes / 8; }
+bool any_growth(const std::vector<uint64_t> &all, size_t w, size_t cap0, int P, int ncap,
+                const std::function<uint64_t(int q, int k)> &need) {
+  for (int q = 0; q < P; ++q)
+    for (int k = 0; k < ncap; ++k)
+      if (std::max<uint64_t>(need(q, k), 1) > all[(size_t)q * w + cap0 + k]) return true;
+  return false;
 }
 
 // run f(l) for every local member: one host thread per member when there are several
@@ -290,8 +359,10 @@ nut_status member_init(nut_dist *d, Member &mb, int device) {
   st = mb.hdr_dev.reserve(kHdrBytes * 2);
   if (st) return st;
   NUT_HIP(hipHostMalloc((void **)&mb.hdr_host, kHdrBytes, hipHostMallocDefault));
-  (void)d;
-  return NUT_OK;
+  NUT_HIP(hipHostMalloc((void **)&mb.hdr_send, (kHdrWords + kSamples) * 8, hipHostMallocDefault));
+  // the sample sort's positions, own sample and pooled samples: reserved here, so the
+  // sample all-gather (which carries the status) never waits on an allocation
+  return reserve(mb, 3, kSamples + (uint64_t)(d->nranks + 1) * kSampleWords);
 }
 
 void member_free(Member &mb) {
@@ -302,7 +373,8 @@ void member_free(Member &mb) {
     for (auto &b : mb.buf) b.release();
     mb.hdr_dev.release();
     if (mb.hdr_host) (void)hipHostFree(mb.hdr_host);
-    mb.hdr_host = nullptr;
+    if (mb.hdr_send) (void)hipHostFree(mb.hdr_send);
+    mb.hdr_host = mb.hdr_send = nullptr;
   }
   nut_ctx_destroy(mb.ctx);
   mb.ctx = nullptr;
@@ -314,11 +386,19 @@ nut_status check_dist(nut_dist *d, const char *what) {
 }
 
 // ------------------------------------------------------------------ group-by
+// The owners' merged groups reach rank 0 in one all-to-all with no second header when they
+// are few: owner q holds at most bound_q = the partial groups it received (known to every
+// rank from the first header), so it sends a fixed 1 + W x bound_q words — its group count
+// first, then its groups column-major — and rank 0 reads the counts from the segments.
+// Above this many words the padding would cost more than a header: exact counts then.
+constexpr uint64_t kPaddedGather = 1ull << 20;
+
 nut_status groupby_member(nut_dist *d, int l, const nut_agg_spec *spec, uint64_t hint, nut_groups **out) {
   Member &mb = d->m[l];
   nut_ctx *c = mb.ctx;
   const int P = d->nranks, me = mb.rank;
   *out = nullptr;
+  if (P == 1) return nut_groupby(c, spec, hint, out);  // one rank: its groups are the result
   // 1. local pre-aggregation, partial groups partitioned by owner rank
   nut_groups *g = nullptr;
   uint64_t n = 0;
@@ -331,33 +411,61 @@ nut_status groupby_member(nut_dist *d, int l, const nut_agg_spec *spec, uint64_t
     st = reserve(mb, 0, (uint64_t)W * n);
   }
   if (!st) st = nut_groups_partition(g, P, buf(mb, 0), n, counts.data());
-  std::vector<uint64_t> hdr(2 + P, 0), all;
+  // header: [status, W, counts to each rank, capacity of buffers 1 and 2]
+  const size_t w = 4 + (size_t)P, cw = 2 + (size_t)P;
+  std::vector<uint64_t> hdr(w, 0), all;
   hdr[1] = (uint64_t)W;
   for (int q = 0; q < P; ++q) hdr[2 + q] = counts[q];
+  hdr[cw] = cap_words(mb, 1);
+  hdr[cw + 1] = cap_words(mb, 2);
   st = exchange_header(d, l, st, hdr, all);
   if (st) {
     nut_groups_free(g);
     return st;
   }
+  for (int q = 0; q < P; ++q)
+    if (all[(size_t)q * w + 1] != (uint64_t)W) {
+      nut_groups_free(g);
+      return fail(NUT_ERR_INVALID_ARG, "nut_dist_groupby: ranks passed specs of different shapes");
+    }
+  auto cnt = [&](int from, int to) { return all[(size_t)from * w + 2 + to]; };
+  // bound[q]: the partial groups owner q receives (>= its merged groups)
+  std::vector<uint64_t> bound(P, 0);
+  for (int q = 0; q < P; ++q)
+    for (int p = 0; p < P; ++p) bound[q] += cnt(p, q);
+  uint64_t gather_words = 0;
+  for (int q = 1; q < P; ++q) gather_words += 1 + (uint64_t)W * bound[q];
+  const bool padded = gather_words <= kPaddedGather;
+  // buffer 1: the partial groups received, and rank 0's gathered segments; buffer 2: owner
+  // q's padded segment (buffer 0 holds the partition until the exchange has sent it)
+  auto need = [&](int q, int k) -> uint64_t {
+    if (k == 0) return std::max<uint64_t>((uint64_t)W * bound[q], padded && q == 0 ? gather_words : 0);
+    return padded && q ? 1 + (uint64_t)W * bound[q] : 0;
+  };
+  if (any_growth(all, w, cw, P, 2, need)) {
+    st = reserve(mb, 1, need(me, 0));
+    if (!st) st = reserve(mb, 2, need(me, 1));
+    st = agree(d, l, st);
+    if (st) {
+      nut_groups_free(g);
+      return st;
+    }
+  }
   // 2. all-to-all of the partial groups (column-major segments of W words per group)
   std::vector<size_t> sc(P), sd(P), rc(P), rd(P);
   size_t stot = 0, rtot = 0;
   for (int q = 0; q < P; ++q) {
-    if (all[(size_t)q * (2 + P) + 1] != (uint64_t)W) {
-      nut_groups_free(g);
-      return fail(NUT_ERR_INVALID_ARG, "nut_dist_groupby: ranks passed specs of different shapes");
-    }
     sc[q] = (size_t)W * counts[q];
     sd[q] = stot;
     stot += sc[q];
-    rc[q] = (size_t)W * all[(size_t)q * (2 + P) + 2 + me];
+    rc[q] = (size_t)W * cnt(q, me);
     rd[q] = rtot;
     rtot += rc[q];
   }
-  st = agree(d, l, reserve(mb, 1, rtot));
-  if (!st)
-    st = alltoallv(d, l, buf(mb, 0), sc.data(), sd.data(), buf(mb, 1), rc.data(), rd.data(),
-                   max_cell(all, 2 + (size_t)P, 2, P, (size_t)W));
+  size_t gmax = 0;
+  for (int p = 0; p < P; ++p)
+    for (int q = 0; q < P; ++q) gmax = std::max<size_t>(gmax, (size_t)W * cnt(p, q));
+  st = alltoallv(d, l, buf(mb, 0), sc.data(), sd.data(), buf(mb, 1), rc.data(), rd.data(), gmax);
   // 3. the owner merges what it received
   nut_groups *own = nullptr;
   nut_prog_node nodes[NUT_MAX_AGGS];
@@ -372,32 +480,70 @@ nut_status groupby_member(nut_dist *d, int l, const nut_agg_spec *spec, uint64_t
   // 4. the owners' groups are gathered on rank 0, which folds them into its own
   uint64_t n_own = 0;
   if (!st) st = nut_groups_size(own, &n_own);
-  if (!st && me != 0) st = reserve(mb, 0, (uint64_t)W * n_own);
-  if (!st && me != 0) st = nut_groups_to_device(own, buf(mb, 0), n_own);
-  hdr.assign(2, 0);
-  hdr[1] = n_own;
-  st = exchange_header(d, l, st, hdr, all);
-  if (!st) {
-    std::fill(sc.begin(), sc.end(), 0);
-    std::fill(sd.begin(), sd.end(), 0);
-    std::fill(rc.begin(), rc.end(), 0);
+  std::vector<uint64_t> n_of(P, 0);  // rank 0: each owner's group count
+  std::fill(sc.begin(), sc.end(), 0);
+  std::fill(sd.begin(), sd.end(), 0);
+  std::fill(rc.begin(), rc.end(), 0);
+  if (padded) {
+    // fixed segments; a failed owner sends a count of ~0 in its segment (every rank still
+    // takes part in the all-to-all), and rank 0 fails the call on reading it
+    if (me != 0) {
+      uint64_t *seg = buf(mb, 2);
+      if (!st && n_own) st = nut_groups_to_device(own, seg + 1, n_own);
+      mb.hdr_send[0] = st ? ~0ull : n_own;
+      hipError_t e = hipMemcpyAsync(seg, mb.hdr_send, 8, hipMemcpyHostToDevice, c->stream);
+      if (e != hipSuccess && !st) st = hip_fail(e, "nut_dist_groupby");
+      sc[0] = 1 + (size_t)W * bound[me];
+    }
     rtot = 0;
     for (int q = 0; q < P; ++q) {
       rd[q] = rtot;
-      if (me == 0 && q != 0) rc[q] = (size_t)W * all[(size_t)q * 2 + 1];
+      if (me == 0 && q != 0) rc[q] = 1 + (size_t)W * bound[q];
       rtot += rc[q];
     }
-    if (me != 0) sc[0] = (size_t)W * n_own;
-    st = agree(d, l, reserve(mb, 1, rtot));
+    size_t pmax = 0;
+    for (int q = 1; q < P; ++q) pmax = std::max<size_t>(pmax, 1 + (size_t)W * bound[q]);
+    nut_status a2a = alltoallv(d, l, buf(mb, 2), sc.data(), sd.data(), buf(mb, 1), rc.data(), rd.data(), pmax);
+    if (!st) st = a2a;
+    if (me == 0 && !st) {
+      for (int q = 1; q < P && !st; ++q) {
+        hipError_t e = hipMemcpyAsync(mb.hdr_host + q, buf(mb, 1) + rd[q], 8, hipMemcpyDeviceToHost, c->stream);
+        if (e != hipSuccess) st = hip_fail(e, "nut_dist_groupby");
+      }
+      hipError_t e = st ? hipSuccess : hipStreamSynchronize(c->stream);
+      if (e != hipSuccess) st = hip_fail(e, "nut_dist_groupby");
+      for (int q = 1; q < P && !st; ++q) {
+        n_of[q] = mb.hdr_host[q];
+        if (n_of[q] == ~0ull) st = fail(NUT_ERR_HIP, "nut_dist: rank " + std::to_string(q) + " failed its owner merge");
+        else if (n_of[q] > bound[q]) st = fail(NUT_ERR_INVALID_ARG, "nut_dist_groupby: owner group count above its bound");
+        rd[q] += 1;  // the groups follow the count word
+      }
+    }
+  } else {
+    if (!st && me != 0) st = reserve(mb, 0, (uint64_t)W * n_own);
+    if (!st && me != 0) st = nut_groups_to_device(own, buf(mb, 0), n_own);
+    std::vector<uint64_t> h2(2, 0);
+    h2[1] = n_own;
+    st = exchange_header(d, l, st, h2, all);
+    if (!st) {
+      rtot = 0;
+      for (int q = 0; q < P; ++q) {
+        rd[q] = rtot;
+        n_of[q] = all[(size_t)q * 2 + 1];
+        if (me == 0 && q != 0) rc[q] = (size_t)W * n_of[q];
+        rtot += rc[q];
+      }
+      if (me != 0) sc[0] = (size_t)W * n_own;
+      st = agree(d, l, reserve(mb, 1, rtot));
+    }
+    size_t pmax = 0;
+    for (int q = 0; q < P && !st; ++q) pmax = std::max<size_t>(pmax, (size_t)W * n_of[q]);
+    if (!st) st = alltoallv(d, l, buf(mb, 0), sc.data(), sd.data(), buf(mb, 1), rc.data(), rd.data(), pmax);
   }
-  size_t gmax = 0;
-  for (int q = 0; q < P && !st; ++q) gmax = std::max<size_t>(gmax, (size_t)W * all[(size_t)q * 2 + 1]);
-  if (!st) st = alltoallv(d, l, buf(mb, 0), sc.data(), sd.data(), buf(mb, 1), rc.data(), rd.data(), gmax);
   if (!st && me == 0) {
     for (int q = 1; q < P && !st; ++q) {
-      const uint64_t cq = rc[q] / W;
-      if (!cq) continue;
-      groups_merge_spec(own, buf(mb, 1) + rd[q], cq, &ms, nodes);
+      if (!n_of[q]) continue;
+      groups_merge_spec(own, buf(mb, 1) + rd[q], n_of[q], &ms, nodes);
       st = nut_groupby_accumulate(c, &ms, own);
     }
   }
@@ -504,34 +650,58 @@ nut_status sort_member(nut_dist *d, int l, const int64_t *in, uint64_t n, const 
   nut_ctx *c = mb.ctx;
   const int P = d->nranks, me = mb.rank;
   hipStream_t s = c->stream;
-  // 1. a strided sample of the local keys, all-gathered; splitters at the pooled quantiles
-  nut_status st = reserve(mb, 3, 2 * (uint64_t)kSamples + (uint64_t)P * kSamples);
-  if (!st && n) {
-    std::vector<int64_t> idx(kSamples);
+  if (P == 1) {  // one rank: no samples, no partition, no exchange — the local sort of the input
+    nut_status st = reserve(mb, 2, n);
+    if (!st && n) {
+      DeviceGuard dg(c->device);
+      st = nut::msd_sort_i64(c, in, (int64_t *)buf(mb, 2), n, kSortFlip);
+    }
+    if (!st) st = nut_ctx_sync(c);
+    if (st) return st;
+    *out = (const int64_t *)buf(mb, 2);
+    *out_n = n;
+    return NUT_OK;
+  }
+  // 1. a strided sample of the local keys, all-gathered with its status and whether the
+  //    rank has keys (one all-gather, no header before it); splitters at the pooled quantiles
+  nut_status st = NUT_OK;
+  uint64_t *smp = buf(mb, 3) + kSamples;  // kSampleWords words (buffer 3: reserved at creation)
+  if (n) {
+    int64_t *idx = (int64_t *)mb.hdr_send;  // page-locked: the copy needs no host wait
     for (int i = 0; i < kSamples; ++i) idx[i] = (int64_t)(((unsigned __int128)i * n) / kSamples);
     int64_t *didx = (int64_t *)buf(mb, 3);
-    hipError_t e = hipMemcpyAsync(didx, idx.data(), kSamples * 8, hipMemcpyHostToDevice, s);
-    if (e == hipSuccess) e = hipStreamSynchronize(s);  // idx is pageable: complete before it goes
-    st = e == hipSuccess ? nut_gather_u64(c, (const uint64_t *)in, didx, kSamples, 0, buf(mb, 3) + kSamples)
+    hipError_t e = hipMemcpyAsync(didx, idx, kSamples * 8, hipMemcpyHostToDevice, s);
+    st = e == hipSuccess ? nut_gather_u64(c, (const uint64_t *)in, didx, kSamples, 0, smp + 2)
                          : hip_fail(e, "nut_dist_sort_i64 sample indices");
   }
-  std::vector<uint64_t> hdr(2, 0), all;
-  hdr[1] = n ? 1 : 0;
-  st = exchange_header(d, l, st, hdr, all);
-  if (st) return st;
-  uint64_t *pool_dev = buf(mb, 3) + 2 * kSamples;
-  // a local failure from here on travels in the next header (every rank returns together)
-  st = allgather(d, l, buf(mb, 3) + kSamples, pool_dev, kSamples);
-  std::vector<int64_t> pool((size_t)P * kSamples);
+  uint64_t *h2 = mb.hdr_send + kSamples;  // page-locked, after the positions
+  h2[0] = (uint64_t)st;
+  h2[1] = n ? 1 : 0;
+  NUT_HIP(hipMemcpyAsync(smp, h2, 16, hipMemcpyHostToDevice, s));
+  const std::string mine_err = st ? nut_last_error() : "";
+  constexpr uint64_t kSw = kSampleWords;
+  uint64_t *pool_dev = smp + kSw;
+  st = allgather(d, l, smp, pool_dev, kSw);
+  std::vector<uint64_t> pooled((size_t)P * kSw);
   if (!st) {
-    hipError_t e = hipMemcpyAsync(pool.data(), pool_dev, pool.size() * 8, hipMemcpyDeviceToHost, s);
+    hipError_t e = hipMemcpyAsync(pooled.data(), pool_dev, pooled.size() * 8, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) st = hip_fail(e, "nut_dist_sort_i64 sample copy");
   }
+  if (st) return st;
+  if (pooled[(size_t)me * kSw]) return fail((nut_status)pooled[(size_t)me * kSw], mine_err);
+  for (int q = 0; q < P; ++q)
+    if (pooled[(size_t)q * kSw])
+      return fail((nut_status)pooled[(size_t)q * kSw], "nut_dist: rank " + std::to_string(q) + " failed (status " +
+                                                           std::to_string(pooled[(size_t)q * kSw]) + ")");
+  std::vector<uint64_t> hdr, all;
+  std::vector<int64_t> pool((size_t)P * kSamples);
+  for (int q = 0; q < P; ++q)
+    memcpy(&pool[(size_t)q * kSamples], &pooled[(size_t)q * kSw + 2], kSamples * 8);
   std::vector<int64_t> live;
   live.reserve(pool.size());
   for (int q = 0; q < P; ++q)
-    if (all[(size_t)q * 2 + 1]) live.insert(live.end(), pool.begin() + (size_t)q * kSamples, pool.begin() + (size_t)(q + 1) * kSamples);
+    if (pooled[(size_t)q * kSw + 1]) live.insert(live.end(), pool.begin() + (size_t)q * kSamples, pool.begin() + (size_t)(q + 1) * kSamples);
   std::sort(live.begin(), live.end());
   std::vector<int64_t> spl(P - 1, 0);
   for (int i = 1; i < P; ++i) spl[i - 1] = live.empty() ? 0 : live[(live.size() * (size_t)i) / P];
@@ -550,8 +720,12 @@ nut_status sort_member(nut_dist *d, int l, const int64_t *in, uint64_t n, const 
     if (!st) st = nut::partition_i64_ranges(c, in, n, rg.e.data(), nb - 1, (int64_t *)buf(mb, 0), bcount.data());
   }
   for (int j = 0; j < nb; ++j) split_bucket(rg, (size_t)j, bcount[j], counts);
-  hdr.assign(1 + P, 0);
+  // header: [status, counts to each rank, capacity of buffers 1 and 2]
+  const size_t w = 3 + (size_t)P;
+  hdr.assign(w, 0);
   for (int q = 0; q < P; ++q) hdr[1 + q] = counts[q];
+  hdr[1 + P] = P == 1 ? ~0ull : cap_words(mb, 1);  // (one rank sorts its input in place of a copy)
+  hdr[2 + P] = cap_words(mb, 2);
   st = exchange_header(d, l, st, hdr, all);
   if (st) return st;
   std::vector<size_t> sc(P), sd(P), rc(P), rd(P);
@@ -560,20 +734,26 @@ nut_status sort_member(nut_dist *d, int l, const int64_t *in, uint64_t n, const 
     sc[q] = counts[q];
     sd[q] = stot;
     stot += sc[q];
-    rc[q] = all[(size_t)q * (1 + P) + 1 + me];
+    rc[q] = all[(size_t)q * w + 1 + me];
     rd[q] = rtot;
     rtot += rc[q];
   }
-  st = P == 1 ? NUT_OK : reserve(mb, 1, rtot);  // (one rank sorts its input in place of a copy)
-  if (!st) st = reserve(mb, 2, rtot);
-  st = agree(d, l, st);
+  auto need = [&](int q, int) {
+    uint64_t r = 0;
+    for (int p = 0; p < P; ++p) r += all[(size_t)p * w + 1 + q];
+    return r;
+  };
+  if (any_growth(all, w, 1 + (size_t)P, P, 2, need)) {
+    st = P == 1 ? NUT_OK : reserve(mb, 1, rtot);
+    if (!st) st = reserve(mb, 2, rtot);
+    st = agree(d, l, st);
+  }
   // 3. one all-to-all of keys, then the local radix sort of the received range
   const int64_t *sort_in = (const int64_t *)buf(mb, 1);
   if (P == 1)  // one rank: nothing to exchange, the local sort reads the input
     sort_in = in;
   else if (!st)
-    st = alltoallv(d, l, send, sc.data(), sd.data(), buf(mb, 1), rc.data(), rd.data(),
-                   max_cell(all, 1 + (size_t)P, 1, P, 1));
+    st = alltoallv(d, l, send, sc.data(), sd.data(), buf(mb, 1), rc.data(), rd.data(), max_cell(all, w, 1, P, 1));
   // this rank's key range from its buckets' splitters: the local sort's capped layout
   // spreads exactly that range, not the full 64-bit one
   uint64_t bnd[2] = {~0ull, 0};
@@ -627,11 +807,13 @@ nut_status join_member(nut_dist *d, int l, const int64_t *build, uint64_t nb, in
   if (!st) st = reserve(mb, 3, np);
   if (!st) st = nut_hash_partition_i64(c, build, nb, P, brow0, (int64_t *)buf(mb, 0), (int64_t *)buf(mb, 1), bc.data());
   if (!st) st = nut_hash_partition_i64(c, probe, np, P, prow0, (int64_t *)buf(mb, 2), (int64_t *)buf(mb, 3), pc.data());
-  std::vector<uint64_t> hdr(1 + 2 * P, 0), all;
+  // header: [status, build counts, probe counts, capacities of buffers 4..7]
+  const size_t w = 5 + 2 * (size_t)P;
+  std::vector<uint64_t> hdr(w, 0), all;
   for (int q = 0; q < P; ++q) hdr[1 + q] = bc[q], hdr[1 + P + q] = pc[q];
+  for (int k = 0; k < 4; ++k) hdr[1 + 2 * P + k] = cap_words(mb, 4 + k);
   st = exchange_header(d, l, st, hdr, all);
   if (st) return st;
-  const size_t w = 1 + 2 * (size_t)P;
   std::vector<size_t> bsc(P), bsd(P), brc(P), brd(P), psc(P), psd(P), prc(P), prd(P);
   size_t bs = 0, br = 0, ps = 0, pr = 0;
   for (int q = 0; q < P; ++q) {
@@ -640,16 +822,27 @@ nut_status join_member(nut_dist *d, int l, const int64_t *build, uint64_t nb, in
     brc[q] = all[q * w + 1 + me], brd[q] = br, br += brc[q];
     prc[q] = all[q * w + 1 + P + me], prd[q] = pr, pr += prc[q];
   }
-  st = reserve(mb, 4, br);
-  if (!st) st = reserve(mb, 5, br);
-  if (!st) st = reserve(mb, 6, pr);
-  if (!st) st = reserve(mb, 7, pr);
-  st = agree(d, l, st);
-  const size_t bmax = max_cell(all, w, 1, P, 1), pmax = max_cell(all, w, 1 + (size_t)P, P, 1);
-  if (!st) st = alltoallv(d, l, buf(mb, 0), bsc.data(), bsd.data(), buf(mb, 4), brc.data(), brd.data(), bmax);
-  if (!st) st = alltoallv(d, l, buf(mb, 1), bsc.data(), bsd.data(), buf(mb, 5), brc.data(), brd.data(), bmax);
-  if (!st) st = alltoallv(d, l, buf(mb, 2), psc.data(), psd.data(), buf(mb, 6), prc.data(), prd.data(), pmax);
-  if (!st) st = alltoallv(d, l, buf(mb, 3), psc.data(), psd.data(), buf(mb, 7), prc.data(), prd.data(), pmax);
+  auto need = [&](int q, int k) {  // buffers 4 / 5: build records received, 6 / 7: probe records
+    uint64_t r = 0;
+    for (int p = 0; p < P; ++p) r += all[(size_t)p * w + 1 + (k < 2 ? 0 : P) + q];
+    return r;
+  };
+  if (any_growth(all, w, 1 + 2 * (size_t)P, P, 4, need)) {
+    st = reserve(mb, 4, br);
+    if (!st) st = reserve(mb, 5, br);
+    if (!st) st = reserve(mb, 6, pr);
+    if (!st) st = reserve(mb, 7, pr);
+    st = agree(d, l, st);
+  }
+  const size_t gmax = std::max(max_cell(all, w, 1, P, 1), max_cell(all, w, 1 + (size_t)P, P, 1));
+  // the build and probe records (keys and row ids) in one grouped exchange
+  if (!st)
+    st = alltoallv_group(d, l,
+                         {A2A{buf(mb, 0), bsc.data(), bsd.data(), buf(mb, 4), brc.data(), brd.data()},
+                          A2A{buf(mb, 1), bsc.data(), bsd.data(), buf(mb, 5), brc.data(), brd.data()},
+                          A2A{buf(mb, 2), psc.data(), psd.data(), buf(mb, 6), prc.data(), prd.data()},
+                          A2A{buf(mb, 3), psc.data(), psd.data(), buf(mb, 7), prc.data(), prd.data()}},
+                         gmax);
   if (st) return st;
   // local join of what this rank owns; local pair indices -> global rows
   nut_join *j = nullptr;

@@ -89,9 +89,12 @@ def test_order_by_f64(ex, n, desc):
     f = column(max(n, 64), 3, nan=True)[:n]
     got = run(ex, "select f from t order by f" + (" desc" if desc else ""), f)
     assert bits_equal(got, total_sort(f, desc))
-    if n > 64:  # sanity: the zeros are split by sign, the infinities at the ends of the numbers
+    if n > 64:  # sanity: the numbers (NaNs aside) in order, the infinities at their ends
         num = got[~np.isnan(got)]
-        assert np.all(np.diff(num) <= 0) if desc else np.all(np.diff(num) >= 0)
+        fin = num[np.isfinite(num)]
+        assert np.all(np.diff(fin) <= 0) if desc else np.all(np.diff(fin) >= 0)
+        lo, hi = (num[-1], num[0]) if desc else (num[0], num[-1])
+        assert lo == -np.inf and hi == np.inf
 
 
 @pytest.mark.parametrize("limit", [1, 100, 5000])

@@ -120,16 +120,18 @@ def test_groupby_pool_indexed_matches_hash_oracle(orc, groups, n, row0):
     assert int(iw[:, 1].sum()) == n
 
 
-@pytest.mark.parametrize("groups,nk,masked", [(500_000, 1, False), (1_000_000, 1, True), (300_000, 2, True),
-                                              (20_000, 1, False)])
-def test_groupby_partitioned_merge_is_bitwise_the_table_merge(orc, groups, nk, masked):
+@pytest.mark.parametrize("groups,nk,masked,skew", [(500_000, 1, False, False), (1_000_000, 1, True, False),
+                                                   (300_000, 2, True, False), (20_000, 1, False, False),
+                                                   (1_000_000, 1, False, True), (1_000_000, 2, True, True)])
+def test_groupby_partitioned_merge_is_bitwise_the_table_merge(orc, groups, nk, masked, skew):
     """orc_groupby's key-range partitioned merge (large G: the CPU baseline's path) gives
     the per-thread-table merge's result bit for bit — keys, counts, i64 / f64 MIN / MAX and
     Neumaier f64 sums of non-dyadic values (the same per-group fold and merge order) —
-    with a WHERE, a row mask and two keys."""
+    with a WHERE, a row mask and two keys; Zipf-like keys (skew) through the heavy-tuple
+    split (keys holding >= 1/threads of the sample folded per thread chunk)."""
     n = (1 << 22) + 12345
     from nutdb_amd.workloads import groupby_cols
-    ks, _ = groupby_cols(groups, dyadic=True)
+    ks, _ = groupby_cols(groups, dyadic=True, skew=skew)
     key = orc.gen(ks, n)
     keys = [key] if nk == 1 else [key, orc.gen_column(5, 0x3A, n, a=-3, b=7)]
     v = orc.gen_column(4, 0x55, n)              # unit f64: sums round
@@ -141,4 +143,24 @@ def test_groupby_partitioned_merge_is_bitwise_the_table_merge(orc, groups, nk, m
     a = orc.groupby(keys, aggs, values=[v, iv], **kw)
     b = orc.groupby(keys, aggs, values=[v, iv], method="tables", **kw)
     assert len(a[0]) > 1000
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+
+
+@pytest.mark.parametrize("nthreads,share", [(16, 0.08), (8, 0.3), (4, 0.6)])
+def test_groupby_heavy_tuples_split_is_bitwise(orc, nthreads, share):
+    """Keys holding >= 1/threads of the rows: the range-partitioned
+    merge folds them per thread chunk and merges the chunks' groups in order — still the
+    per-thread-table merge's words bit for bit (non-dyadic f64 sums, i64 MIN / MAX, a WHERE)."""
+    n = (1 << 22) + 777
+    rng = np.random.default_rng(41)
+    key = orc.gen_column(2, 0x71, n, a=1_000_000)
+    hot = rng.random(n)
+    key[hot < share] = key[3]
+    key[(hot >= share) & (hot < 1.5 * share)] = key[99]  # a second, lighter heavy tuple
+    v = orc.gen_column(4, 0x72, n)
+    iv = orc.gen_column(0, 0x73, n) - (1 << 61)
+    aggs = [(0, 0, (0,)), (1, 0, ()), (2, 0, (1,)), (3, 0, (0,))]
+    kw = {"preds": [(iv, 0, 1 << 61)]}
+    a = orc.groupby([key], aggs, values=[v, iv], nthreads=nthreads, **kw)
+    b = orc.groupby([key], aggs, values=[v, iv], nthreads=nthreads, method="tables", **kw)
     assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
