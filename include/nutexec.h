@@ -149,7 +149,8 @@ typedef enum {
   NUT_OPT_GB_HEAVY = 21,       /* nut_groupby_to_host, ordered path: 1 (default) = keys the sample sees often (>= 5 % of it together) are aggregated in one streaming pass and split off before the partition levels, and the levels' regions are laid out from exact per-cell counts of the rest; 2 = the split with capped levels (their overflow through the arenas); 0 = no split (the arenas take every excess) */
   NUT_OPT_JOIN_MATCH = 22,     /* ordered join probe (nut_join_*): 1 (default) = in two passes when no probe row can match two build rows (SEMI / ANTI, or unique build keys): the run walks in launch order into a 4-B-per-row match array, then the ordered write-out from it; 0 = one ordered pass */
   NUT_OPT_GB_L1_THREADS = 23,  /* nut_groupby_to_host, ordered path: the level-1 scatter's workgroup, 1024 (default: 16 Ki-record tiles) or 512 (8 Ki-record tiles in ~75 KB of LDS, so an aggregation workgroup of the previous chunk fits beside it on a CU) */
-  NUT_OPT_COUNT = 24
+  NUT_OPT_AGG_SLOTS = 24,      /* streaming group-by, shared on-chip table: LDS slots per hinted group, 2..8 (4: load <= 1/4, a key almost always in its 4-slot home bucket); 2 halves the table so twice the workgroups fit a CU */
+  NUT_OPT_COUNT = 25
 } nut_option;
 nut_status nut_ctx_set_option(nut_ctx *ctx, int option, int64_t value);
 nut_status nut_ctx_get_option(nut_ctx *ctx, int option, int64_t *value);

@@ -325,7 +325,7 @@ constexpr size_t kAggLdsMax = 160 * 1024 - 2048;  // the kernel also holds stati
 uint32_t agg_lcap(nut_ctx *c, int nk, int na, uint64_t group_hint, bool seg) {
   // (32 slots = 8 buckets x 32 B = one pass over the 64 LDS banks: for <= 8 groups two
   // home buckets never conflict — distinct buckets hit distinct banks, equal ones broadcast)
-  const uint64_t want = group_hint ? (seg ? (uint64_t)c->opt[NUT_OPT_GB_SEG_SLOTS] * group_hint : 4 * group_hint) : 4096;
+  const uint64_t want = group_hint ? (uint64_t)c->opt[seg ? NUT_OPT_GB_SEG_SLOTS : NUT_OPT_AGG_SLOTS] * group_hint : 4096;
   uint32_t lcap = 32;
   while (lcap < want && lds_bytes(lcap * 2, nk, na, false, 0, kBdShared) <= kAggLdsMax) lcap *= 2;
   return group_hint > 8ull * lcap ? 0 : lcap;

@@ -61,6 +61,20 @@ class AggQuery:
     rows: int | None = None                     # row count when there is no column at all
 
     def to_spec(self, dev: torch.device) -> L.NutAggSpec:
+        # built once per device and column set: a query run step after step (the bench,
+        # a prepared statement) pays the ctypes marshalling once
+        cols = list(self.keys) + list(self.values) + [c for c, _, _ in self.preds]
+        lits = tuple((op, tuple(lit) if isinstance(lit, (list, tuple)) else lit) for _, op, lit in self.preds)
+        tag = (str(dev), tuple((t.data_ptr(), t.numel(), t.dtype) for t in cols), len(self.keys), len(self.values),
+               tuple((a.op, a.expr, tuple(a.args)) for a in self.aggs), lits, self.rows)
+        cached = self.__dict__.get("_spec")
+        if cached is not None and cached[0] == tag:
+            return cached[1]
+        s = self._build_spec(dev)
+        self.__dict__["_spec"] = (tag, s)
+        return s
+
+    def _build_spec(self, dev: torch.device) -> L.NutAggSpec:
         s = L.NutAggSpec()
         cols = list(self.keys) + list(self.values) + [c for c, _, _ in self.preds]
         n = int(cols[0].numel()) if cols else int(self.rows or 0)
@@ -361,7 +375,7 @@ class Executor:
                "topk": 11, "gb_l0_bits": 12, "stream_blocks": 13,
                "priv_bd": 14, "priv_blocks": 15, "agg_blocks": 16, "sel_blocks": 17, "sort_bd": 18,
                "gb_ordered": 19, "priv_probe": 20, "gb_heavy": 21,
-               "join_match": 22, "gb_l1_threads": 23}
+               "join_match": 22, "gb_l1_threads": 23, "agg_slots": 24}
 
     def groupby_stats(self) -> dict:
         """The algorithm the last group-by on this context took (nut_ctx_groupby_stats)."""

@@ -15,5 +15,28 @@ case "$1" in
       "200 g1000_b $B --workload groupby --groups 1000" \
       "300 g1000_trace rocprofv3 --kernel-trace --stats -d gpurun_out/g1000/trace -o trace --output-format csv -- $B --workload groupby --groups 1000 --steps 5 --warmup 1"
     ;;
+  s3)  # G = 1000: the shared table's slots per group x workgroups per CU
+    G="$B --workload groupby --groups 1000"
+    scripts/gpu_session.sh \
+      "200 g_def $G" "200 g_s2 $G --option agg_slots=2" "200 g_s2b3 $G --option agg_slots=2 --option agg_blocks=3" \
+      "200 g_s8 $G --option agg_slots=8" "200 g_def2 $G" "200 g_s2b $G --option agg_slots=2" \
+      "200 g_s2b2 $G --option agg_slots=2 --option agg_blocks=2"
+    ;;
+  s4)  # G = 1000 after the one-wait tail: plain runs, SQ / LDS counters of the agg kernel
+    mkdir -p gpurun_out/g1000
+    G="$B --workload groupby --groups 1000"
+    scripts/gpu_session.sh \
+      "200 g4_a $G" "200 g4_b $G" \
+      "120 g4_sq timeout -s KILL 110 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU -d gpurun_out/g1000/sq -o sq --output-format csv -- $G --steps 3 --warmup 1" \
+      "120 g4_sq2 timeout -s KILL 110 rocprofv3 --pmc SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_INSTS_VMEM_RD SQ_WAIT_INST_ANY SQ_LDS_ADDR_CONFLICT SQ_INST_CYCLES_VMEM_RD SQ_ACTIVE_INST_ANY -d gpurun_out/g1000/sq2 -o sq --output-format csv -- $G --steps 3 --warmup 1" \
+      "200 q1_a $B --workload q1"
+    ;;
+  s5)  # G = 1000: bucket vs own-slot LDS lookups, interleaved
+    G="$B --workload groupby --groups 1000"
+    scripts/gpu_session.sh \
+      "200 h0a $G" "200 h1a $G --option agg_home=1" "200 h0b $G" "200 h1b $G --option agg_home=1" \
+      "200 h1s8 $G --option agg_home=1 --option agg_slots=8" "200 h1s2 $G --option agg_home=1 --option agg_slots=2" \
+      "200 g1e5h1 $B --workload groupby --groups 100000 --option agg_home=1" "200 g1e5h0 $B --workload groupby --groups 100000"
+    ;;
   *) echo "unknown session $1"; exit 2 ;;
 esac
