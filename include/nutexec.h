@@ -120,6 +120,12 @@ nut_status nut_ctx_groupby_heavy(nut_ctx *ctx, uint32_t *keys, uint64_t *rows);
  * kernel time per candidate shape {192 x 2, 128 x 3, 128 x 4} in ms (-1: not probed in
  * this process). */
 nut_status nut_ctx_priv_shape(nut_ctx *ctx, int *threads, int *blocks_per_cu, double probe_ms[3]);
+/* First-call latency of the probe: the call that runs it (the first compiled-Q1-shape
+ * group-by of >= 2^27 rows on a device in the process) also times six full-size launches
+ * of the kernel (2 rounds x 3 shapes) over the caller's input — at 1e9 rows ~45 ms, about
+ * 7x that call's own kernel time — outside the kernel timers.  *ms = that wall time on this
+ * context's device (0: not probed in this process).  NUT_OPT_PRIV_PROBE = 0 skips it. */
+nut_status nut_ctx_priv_probe_cost(nut_ctx *ctx, double *ms);
 
 /* Algorithm options of one context, for tuning A/B runs and tests that drive a path at
  * a size where the planner would not pick it.  The defaults are the product choice;
@@ -150,7 +156,8 @@ typedef enum {
   NUT_OPT_JOIN_MATCH = 22,     /* ordered join probe (nut_join_*): 1 (default) = in two passes when no probe row can match two build rows (SEMI / ANTI, or unique build keys): the run walks in launch order into a 4-B-per-row match array, then the ordered write-out from it; 0 = one ordered pass */
   NUT_OPT_GB_L1_THREADS = 23,  /* nut_groupby_to_host, ordered path: the level-1 scatter's workgroup, 1024 (default: 16 Ki-record tiles) or 512 (8 Ki-record tiles in ~75 KB of LDS, so an aggregation workgroup of the previous chunk fits beside it on a CU) */
   NUT_OPT_AGG_SLOTS = 24,      /* streaming group-by, shared on-chip table: LDS slots per hinted group, 2..8 (4: load <= 1/4, a key almost always in its 4-slot home bucket); 2 halves the table so twice the workgroups fit a CU */
-  NUT_OPT_COUNT = 25
+  NUT_OPT_GB_L1_SPARE = 25,    /* nut_groupby_to_host, ordered path: CUs the level-1 scatter of chunks after the first leaves free for the previous chunk's aggregation, 0..128 (32: G = 1e7 step 20.6-20.8 vs 21.4 ms at 0, same box; 64: 20.5 vs 20.9) */
+  NUT_OPT_COUNT = 26
 } nut_option;
 nut_status nut_ctx_set_option(nut_ctx *ctx, int option, int64_t value);
 nut_status nut_ctx_get_option(nut_ctx *ctx, int option, int64_t *value);

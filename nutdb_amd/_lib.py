@@ -137,6 +137,7 @@ SIGNATURES = {
     "nut_ctx_groupby_overflow": (_I32, [_P, C.POINTER(_U64), C.POINTER(C.c_uint32)]),
     "nut_ctx_groupby_heavy": (_I32, [_P, C.POINTER(C.c_uint32), C.POINTER(_U64)]),
     "nut_ctx_priv_shape": (_I32, [_P, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_double)]),
+    "nut_ctx_priv_probe_cost": (_I32, [_P, C.POINTER(C.c_double)]),
     "nut_ctx_set_option": (_I32, [_P, _I32, _I64]),
     "nut_ctx_get_option": (_I32, [_P, _I32, C.POINTER(_I64)]),
     "nut_join_i64": (_I32, [_P, _P, _U64, _P, _U64, _I32, C.POINTER(_P), C.POINTER(_U64)]),

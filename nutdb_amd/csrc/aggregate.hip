@@ -6,6 +6,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -310,6 +311,7 @@ constexpr int kPrivShapes[3][2] = {{192, 2}, {128, 3}, {128, 4}};
 struct PrivShape {
   int shape = -1;  // index into kPrivShapes; -1: not probed (192 x 2)
   double ms[3] = {-1, -1, -1};
+  double cost_ms = 0;  // wall time the probe added to the call that ran it (nut_ctx_priv_probe_cost)
 };
 static PrivShape g_priv_shape[64];
 static std::mutex g_priv_mu;
@@ -568,9 +570,11 @@ uint32_t gp_tiles(std::vector<GpSeg> &segs, uint32_t tile, std::vector<uint32_t>
 void gp_capped_launch(nut_ctx *c, const GpArrays &ar, const GpSeg *dseg, const uint32_t *dts, uint32_t nst, int shift,
                       unsigned long long *dcur, uint64_t kx, uint64_t ovf, unsigned long long *dflag, int bits,
                       bool two_keys, const GpRange *rg, unsigned long long *acur = nullptr, uint64_t acap = 0,
-                      unsigned long long *acut = nullptr, int gather = 0, int threads = 1024) {
+                      unsigned long long *acut = nullptr, int gather = 0, int threads = 1024, int spare_cus = 0) {
   if (!nst) return;
-  const unsigned grid = std::min<unsigned>(nst, (unsigned)c->num_cus);
+  // persistent workgroups, one per CU — less `spare_cus`, CUs left to run other streams'
+  // kernels beside this launch (the ordered path's aggregation of the previous chunk)
+  const unsigned grid = std::min<unsigned>(nst, (unsigned)std::max(1, c->num_cus - spare_cus));
   using SK = void (*)(GpArrays, const GpSeg *, const uint32_t *, uint32_t, int, int, unsigned long long *, uint64_t,
                       uint64_t, unsigned long long *, GpRange, unsigned long long *, uint64_t, unsigned long long *);
   static const SK kern[3][3] = {
@@ -1458,14 +1462,14 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
     nut_ctx *c;
     hipStream_t st;
     uint64_t *res = nullptr;
-    std::vector<hipEvent_t> ev, ev1;
+    std::vector<hipEvent_t> ev, ev1, eva;
     ~Cleanup() {
       if (c->aux_stream) (void)hipStreamSynchronize(c->aux_stream);
+      if (c->order_stream) (void)hipStreamSynchronize(c->order_stream);
       (void)hipStreamSynchronize(c->copy_stream);
-      for (auto x : ev)
-        if (x) (void)hipEventDestroy(x);
-      for (auto x : ev1)
-        if (x) (void)hipEventDestroy(x);
+      for (auto *v : {&ev, &ev1, &eva})
+        for (auto x : *v)
+          if (x) (void)hipEventDestroy(x);
       c->stream = st;
       if (res) (void)hipFreeAsync(res, st);
     }
@@ -1485,22 +1489,27 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
     ar.dst[a] = B2[a];
   }
   ar.narr = narr;
-  // Three streams: level 1 of every chunk back to back on the context's stream; each
-  // chunk's aggregation and ordering on a second one as soon as its level 1 is done
-  // (they overlap the next chunk's level 1, so neither launch's tail idles the chip); its
-  // transfer on the third once the host has read the chunk's running total
+  // Four streams: level 1 of every chunk back to back on the context's stream; each
+  // chunk's aggregation on a second one as soon as its level 1 is done (it overlaps the
+  // next chunk's level 1, so neither launch's tail idles the chip); its ordering on a third
+  // as soon as its aggregation is done (beside the next chunk's aggregation: in one stream
+  // the orderings held every later aggregation back, ~1.5 ms for the first chunk's at
+  // G = 1e7); its transfer on the fourth once the host has read the chunk's running total
   if (!c->aux_stream) NUT_HIP(hipStreamCreateWithFlags(&c->aux_stream, hipStreamNonBlocking));
-  hipStream_t ax = c->aux_stream;
-  std::vector<hipEvent_t> &ev1 = cl.ev1;
+  if (!c->order_stream) NUT_HIP(hipStreamCreateWithFlags(&c->order_stream, hipStreamNonBlocking));
+  hipStream_t ax = c->aux_stream, ox = c->order_stream;
+  std::vector<hipEvent_t> &ev1 = cl.ev1, &eva = cl.eva;
   ev1.assign(nch, nullptr);
+  eva.assign(nch, nullptr);
   for (auto &x : ev1) NUT_HIP(hipEventCreateWithFlags(&x, hipEventDisableTiming));
+  for (auto &x : eva) NUT_HIP(hipEventCreateWithFlags(&x, hipEventDisableTiming));
   auto enqueue = [&](uint32_t j) -> nut_status {
     const uint32_t a0 = cb[j], a1 = cb[j + 1];
     const uint64_t q0 = (uint64_t)a0 * nb1, nq = (uint64_t)(a1 - a0) * nb1;
     c->timer.begin(st, NUT_KERNEL_AGGREGATE);
     gp_capped_launch(c, ar, dseg + a0, dts + tile0[j], ntile[j], 0, dcur + q0, 0, exact ? 0 : ovf1, dcur + nparts + j,
                      bits1, false, &rg, exact ? nullptr : darena + 1, acap1, exact ? nullptr : dcut + q0, 0,
-                     l1_threads);
+                     l1_threads, j ? (int)c->opt[NUT_OPT_GB_L1_SPARE] : 0);
     c->timer.end(st);
     NUT_HIP(hipGetLastError());
     NUT_HIP(hipEventRecord(ev1[j], st));
@@ -1525,17 +1534,19 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
       hipLaunchKernelGGL(go_heavy_insert_kernel, dim3(1), dim3(1024), 0, ax, (const int64_t *)dheavy,
                          (const uint64_t *)dheavy + nh, nh, na, (const int64_t *)dhq, q0, nq, dcount, g->gt.slot,
                          g->gt.agg, g->gt.cap + 1, dregion, dmiss);
-    c->timer.begin(ax, NUT_KERNEL_AGGREGATE);
-    hipLaunchKernelGGL(go_scan_kernel, dim3(1), dim3(1024), 0, ax, (const unsigned long long *)dcount + q0, (uint32_t)nq,
+    NUT_HIP(hipEventRecord(eva[j], ax));
+    NUT_HIP(hipStreamWaitEvent(ox, eva[j], 0));
+    c->timer.begin(ox, NUT_KERNEL_AGGREGATE);
+    hipLaunchKernelGGL(go_scan_kernel, dim3(1), dim3(1024), 0, ox, (const unsigned long long *)dcount + q0, (uint32_t)nq,
                        doffs + q0, drun);
-    hipLaunchKernelGGL(go_order_kernel, dim3((unsigned)nq), dim3(GO_ORDER_THREADS), (unsigned)go_order_lds(dregion), ax,
+    hipLaunchKernelGGL(go_order_kernel, dim3((unsigned)nq), dim3(GO_ORDER_THREADS), (unsigned)go_order_lds(dregion), ox,
                        (const uint64_t *)g->gt.slot, (const uint64_t *)g->gt.agg, g->gt.cap + 1, dregion, q0,
                        (const unsigned long long *)dcount + q0, (const uint64_t *)doffs + q0, na, g->gt.kinds, rk, ra,
                        rcap);
-    c->timer.end(ax);
+    c->timer.end(ox);
     NUT_HIP(hipGetLastError());
-    NUT_HIP(hipMemcpyAsync((void *)(runs + j), drun, 8, hipMemcpyDeviceToHost, ax));
-    NUT_HIP(hipEventRecord(ev[j], ax));
+    NUT_HIP(hipMemcpyAsync((void *)(runs + j), drun, 8, hipMemcpyDeviceToHost, ox));
+    NUT_HIP(hipEventRecord(ev[j], ox));
     return NUT_OK;
   };
   // every chunk queued (nothing waits for the host); chunk j crosses on the copy stream
@@ -1559,6 +1570,7 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
   // the capped level-1 flags (an exhausted arena), the arenas' fill and the aggregation's
   // control words
   NUT_HIP(hipStreamSynchronize(ax));
+  NUT_HIP(hipStreamSynchronize(ox));
   // (everything in gp_meta is read now: the arenas' group-by below may partition, and its
   // own tables take gp_meta)
   std::vector<uint64_t> flags(nch), miss(nh);
@@ -1793,6 +1805,7 @@ static nut_status probe_priv_shape(nut_groups *g, const nut_agg_spec *s, uint64_
   }
   const bool timing = c->timer.enabled;
   c->timer.enabled = false;
+  const auto t0 = std::chrono::steady_clock::now();
   double best[3] = {1e30, 1e30, 1e30};
   for (int rep = 0; rep < 2 && !st; ++rep)
     for (int k = 0; k < 3 && !st; ++k) {
@@ -1818,6 +1831,8 @@ static nut_status probe_priv_shape(nut_groups *g, const nut_agg_spec *s, uint64_
     std::lock_guard<std::mutex> lk(g_priv_mu);
     g_priv_shape[c->device].shape = k;
     for (int j = 0; j < 3; ++j) g_priv_shape[c->device].ms[j] = best[j];
+    g_priv_shape[c->device].cost_ms =
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   }
   return alloc_table(g, cap);  // the probe's partial groups are discarded
 }
@@ -1844,6 +1859,12 @@ nut_status nut_ctx_priv_shape(nut_ctx *c, int *threads, int *blocks_per_cu, doub
   if (blocks_per_cu) *blocks_per_cu = c->opt[NUT_OPT_PRIV_BLOCKS] ? (int)c->opt[NUT_OPT_PRIV_BLOCKS] : kPrivShapes[k][1];
   if (probe_ms)
     for (int j = 0; j < 3; ++j) probe_ms[j] = p.ms[j];
+  return NUT_OK;
+}
+
+nut_status nut_ctx_priv_probe_cost(nut_ctx *c, double *ms) {
+  if (!c || !ms) return fail(NUT_ERR_INVALID_ARG, "nut_ctx_priv_probe_cost: NULL argument");
+  *ms = priv_shape_of(c->device).cost_ms;
   return NUT_OK;
 }
 

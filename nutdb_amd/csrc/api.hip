@@ -299,6 +299,7 @@ void nut_ctx_destroy(nut_ctx *c) {
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
   if (c->aux_stream) (void)hipStreamDestroy(c->aux_stream);
+  if (c->order_stream) (void)hipStreamDestroy(c->order_stream);
   delete c;
 }
 
@@ -350,8 +351,8 @@ nut_status nut_ctx_groupby_stats(nut_ctx *c, uint32_t *path, uint32_t *levels, u
 
 nut_status nut_ctx_set_option(nut_ctx *c, int option, int64_t value) {
   if (!c || option < 0 || option >= NUT_OPT_COUNT) return fail(NUT_ERR_INVALID_ARG, "nut_ctx_set_option: bad option");
-  static const int64_t lo[NUT_OPT_COUNT] = {-1, 0, 0, 0, 1, 0, 0, 0, 1, 0, 6, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 512, 2},
-                       hi[NUT_OPT_COUNT] = {1, 2, 1, 1, 64, 1, 4, 4, 8, 1, 8, 1, 8, 32, 256, 16, 16, 16, 1024, 1, 1, 2, 1, 1024, 8};
+  static const int64_t lo[NUT_OPT_COUNT] = {-1, 0, 0, 0, 1, 0, 0, 0, 1, 0, 6, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 512, 2, 0},
+                       hi[NUT_OPT_COUNT] = {1, 2, 1, 1, 64, 1, 4, 4, 8, 1, 8, 1, 8, 32, 256, 16, 16, 16, 1024, 1, 1, 2, 1, 1024, 8, 128};
   if (value < lo[option] || value > hi[option])
     return fail(NUT_ERR_INVALID_ARG, "nut_ctx_set_option: value " + std::to_string(value) + " out of range [" +
                                          std::to_string(lo[option]) + ", " + std::to_string(hi[option]) + "]");

@@ -185,6 +185,7 @@ struct nut_ctx {
   hipStream_t stream = nullptr;
   hipStream_t copy_stream = nullptr;  // device -> host transfers beside the work (nut_groupby_to_host)
   hipStream_t aux_stream = nullptr;   // a second compute stream (nut_groupby_to_host's per-chunk aggregation)
+  hipStream_t order_stream = nullptr; //   and a third (its per-chunk ordering, beside the next chunk's aggregation)
   nut::Scratch filter_state;  // tile counter + look-back status words
   nut::Scratch sort_tmp;      // sort ping-pong + histograms
   nut::Scratch sort_tmp2;     // MSD sort, capped layout: the second level's regions
@@ -204,7 +205,7 @@ struct nut_ctx {
   size_t tbl_pool_bytes = 0;            //   hipMalloc / hipFree of a 10^7-group table cost ms
   nut::KernelTimer timer;
   // nut_ctx_set_option (tuning / tests; defaults = the product choice, nut_option order)
-  int64_t opt[NUT_OPT_COUNT] = {-1, 0, 1, 1, 8, 1, 0, 0, 2, 1, 6, 1, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 1024, 4};
+  int64_t opt[NUT_OPT_COUNT] = {-1, 0, 1, 1, 8, 1, 0, 0, 2, 1, 6, 1, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 1024, 4, 32};
   int priv_probe = -1;  // the compiled Q1 kernel's shape during the shape probe (aggregate.hip)
   uint32_t gb_path = 0, gb_levels = 0, gb_optimistic = 0;  // nut_ctx_groupby_stats
   uint64_t gb_overflow_rows = 0;  // nut_ctx_groupby_overflow (the ordered path's arenas)

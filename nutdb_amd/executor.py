@@ -357,9 +357,12 @@ class Executor:
         t, b = C.c_int(), C.c_int()
         ms = (C.c_double * 3)()
         check(lib.nut_ctx_priv_shape(self.ctx, C.byref(t), C.byref(b), ms), "nut_ctx_priv_shape")
+        cost = C.c_double()
+        check(lib.nut_ctx_priv_probe_cost(self.ctx, C.byref(cost)), "nut_ctx_priv_probe_cost")
         return {"threads": t.value, "blocks_per_cu": b.value,
                 "probe_ms": {f"{a}x{c}": (round(m, 4) if m >= 0 else None)
-                             for (a, c), m in zip(((192, 2), (128, 3), (128, 4)), ms)}}
+                             for (a, c), m in zip(((192, 2), (128, 3), (128, 4)), ms)},
+                "probe_first_call_cost_ms": round(cost.value, 3)}
 
     def sort_stats(self):
         """(algorithmic HBM bytes, scatter levels) of the last sort on this context."""
@@ -375,7 +378,7 @@ class Executor:
                "topk": 11, "gb_l0_bits": 12, "stream_blocks": 13,
                "priv_bd": 14, "priv_blocks": 15, "agg_blocks": 16, "sel_blocks": 17, "sort_bd": 18,
                "gb_ordered": 19, "priv_probe": 20, "gb_heavy": 21,
-               "join_match": 22, "gb_l1_threads": 23, "agg_slots": 24}
+               "join_match": 22, "gb_l1_threads": 23, "agg_slots": 24, "gb_l1_spare": 25}
 
     def groupby_stats(self) -> dict:
         """The algorithm the last group-by on this context took (nut_ctx_groupby_stats)."""

@@ -38,5 +38,25 @@ case "$1" in
       "200 h1s8 $G --option agg_home=1 --option agg_slots=8" "200 h1s2 $G --option agg_home=1 --option agg_slots=2" \
       "200 g1e5h1 $B --workload groupby --groups 100000 --option agg_home=1" "200 g1e5h0 $B --workload groupby --groups 100000"
     ;;
+  s6)  # G = 1e7 ordered: CUs the level-1 scatter leaves to the aggregation
+    G="$B --workload groupby --groups 10000000"
+    scripts/gpu_session.sh \
+      "200 e0a $G" "200 e16 $G --option gb_l1_spare=16" "200 e32 $G --option gb_l1_spare=32" \
+      "200 e64 $G --option gb_l1_spare=64" "200 e0b $G" "200 e32b $G --option gb_l1_spare=32" \
+      "200 e48 $G --option gb_l1_spare=48"
+    ;;
+  s7)  # G = 1e7 ordered: one step's timeline (kernels + copies)
+    mkdir -p gpurun_out/g1e7
+    scripts/gpu_session.sh \
+      "300 e_trace rocprofv3 --kernel-trace --memory-copy-trace -d gpurun_out/g1e7/trace -o trace --output-format csv -- $B --workload groupby --groups 10000000 --steps 3 --warmup 1 --no-copy-floor --option gb_l1_spare=32"
+    ;;
+  s8)  # G = 1e7 / Zipf with the ordering on its own stream; gorder tests first
+    G="$B --workload groupby --groups 10000000"
+    scripts/gpu_session.sh \
+      "400 t_gorder $T tests/test_gpu_gorder.py" \
+      "200 f0 $G" "200 f32 $G --option gb_l1_spare=32" "200 f0b $G" "200 f32b $G --option gb_l1_spare=32" \
+      "200 fz32 $G --skew --option gb_l1_spare=32" "200 fz0 $G --skew" \
+      "200 f1e5 $B --workload groupby --groups 100000"
+    ;;
   *) echo "unknown session $1"; exit 2 ;;
 esac
