@@ -781,6 +781,11 @@ nut_status filter_member(nut_dist *d, int l, const int64_t *col, uint64_t n, int
   Member &mb = d->m[l];
   uint64_t cnt = 0;
   nut_status st = nut_filter_i64(mb.ctx, col, n, cmp, k, out, &cnt);
+  if (d->nranks == 1) {  // one rank: its output starts at 0, no counts to exchange
+    *out_n = cnt;
+    *out_offset = 0;
+    return st;
+  }
   std::vector<uint64_t> hdr(2, 0), all;
   hdr[1] = cnt;
   st = exchange_header(d, l, st, hdr, all);
@@ -799,6 +804,28 @@ nut_status join_member(nut_dist *d, int l, const int64_t *build, uint64_t nb, in
   Member &mb = d->m[l];
   nut_ctx *c = mb.ctx;
   const int P = d->nranks, me = mb.rank;
+  if (P == 1 && brow0 == 0 && prow0 == 0) {
+    // one rank whose rows are the global rows: the local join's pairs are the result (no
+    // partition, exchange or row-id gathers)
+    // one pass into buffers of a pair per probe row (unique build keys), again at the exact
+    // size when build keys repeat
+    uint64_t cap = std::max<uint64_t>(np, 1), np2 = 0;
+    nut_status st = NUT_OK;
+    for (int attempt = 0; attempt < 2; ++attempt) {
+      st = reserve(mb, 8, cap);
+      if (!st) st = reserve(mb, 9, cap);
+      if (!st) st = nut_join_i64_into(c, build, nb, probe, np, type, (int64_t *)buf(mb, 8), (int64_t *)buf(mb, 9), cap,
+                                      &np2);
+      if (st != NUT_ERR_CAPACITY) break;
+      cap = np2;
+    }
+    if (!st) st = nut_ctx_sync(c);
+    if (st) return st;
+    *pout = (const int64_t *)buf(mb, 8);
+    *bout = (const int64_t *)buf(mb, 9);
+    *npairs = np2;
+    return NUT_OK;
+  }
   // buffers: 0/1 build keys/rows by part, 2/3 probe keys/rows by part, 4..7 received, 8/9 pairs
   std::vector<uint64_t> bc(P, 0), pc(P, 0);
   nut_status st = reserve(mb, 0, nb);

@@ -58,5 +58,18 @@ case "$1" in
       "200 fz32 $G --skew --option gb_l1_spare=32" "200 fz0 $G --skew" \
       "200 f1e5 $B --workload groupby --groups 100000"
     ;;
+  s9)  # the library's multi-GPU path at one RCCL rank (bench --dist) next to the plain lines
+    scripts/gpu_session.sh \
+      "200 d_q1 $B --workload q1 --dist" "200 p_q1 $B --workload q1" \
+      "200 d_g1000 $B --workload groupby --groups 1000 --dist" \
+      "200 d_g1e5 $B --workload groupby --groups 100000 --dist" \
+      "200 d_filter $B --workload filter --dist" "300 d_sort $B --workload sort --dist" \
+      "300 d_join $B --workload join --dist"
+    ;;
+  s10)  # dist tests after the P = 1 join / filter shortcuts, and their --dist lines
+    scripts/gpu_session.sh \
+      "500 t_dist $T tests/test_gpu_dist_native.py tests/test_gpu_join.py" \
+      "200 d_filter2 $B --workload filter --dist" "300 d_join2 $B --workload join --dist"
+    ;;
   *) echo "unknown session $1"; exit 2 ;;
 esac
