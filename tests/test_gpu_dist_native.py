@@ -284,3 +284,25 @@ def test_rccl_single_rank_large_sort_filter_join(ND, orc, mode):
         assert np.array_equal(pi[o], wp) and np.array_equal(bi[o], wb)
     finally:
         d.close()
+
+
+@pytest.mark.parametrize("mode", ["rank", "virtual"])
+def test_rccl_join_grouped_exchange_in_rounds(ND, orc, mode):
+    """The join's exchange as one grouped exchange (ncclGroupStart / End around the four
+    all-to-alls) in more than one round: row offsets keep one rank off the
+    P = 1 shortcut, and 3e7 probe records put each of the four transfers over the 2^24-word
+    share of a round (RCCL's 2^30-byte per-transfer limit split four ways)."""
+    nb, np_ = 4_000_000, 30_000_001
+    b = orc.gen_column(0, 0x81, nb)
+    sel = orc.gen_column(5, 0x82, np_, a=0, b=nb)
+    p = b[sel]
+    p[::7] ^= 1 << 62  # ~1/7 of the probe rows match nothing
+    d = ND.create_rank(1, 0, ND.unique_id(), 0) if mode == "rank" else ND.virtual(1)
+    try:
+        pi, bi = d.join_i64([dev(b)], [dev(p)], "inner", [1000], [7])[0]
+        pi, bi = pi.cpu().numpy(), bi.cpu().numpy()
+    finally:
+        d.close()
+    wp, wb = orc.join_i64(b, p, "inner")
+    o = np.lexsort((bi, pi))
+    assert np.array_equal(pi[o], wp + 7) and np.array_equal(bi[o], wb + 1000)
