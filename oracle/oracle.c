@@ -417,17 +417,7 @@ static uint64_t groupby_ranges(const orc_agg_spec *s, uint64_t cap, int64_t *out
   const uint64_t n = s->n, chunk = (n + (uint64_t)nt - 1) / (uint64_t)nt;
   const int nk = s->nkeys;
   if (nk < 1 || n < ((uint64_t)1 << 22)) return UINT64_MAX - 1;
-  /* ---- distinct groups: a k-minimum-values sketch over every key tuple (one hashing pass;
-   * ~3 % error at k = 1024).  The strided sample's Chao1 estimate it replaces is a lower
-   * bound that skew breaks: Zipf-like keys over 4.6 M groups estimated ~1.3e5 and went to
-   * the per-thread tables, whose serial merge of millions of groups ran 3x slower than the
-   * ranges (VERDICT r5 item 7). */
-  const double gest = kmv_distinct(s, nt);
-  if (gest < 262144) {  /* (per-thread tables of <= ~2^18 groups stay cache-resident and merge fast:
-                          G = 1e5 ran 3.1e8 rows/s there vs 1.3e8 through the ranges) */
-    return UINT64_MAX - 1;
-  }
-  /* a strided sample of the tuples: the heavy tuples and the splitters */
+  /* a strided sample of the tuples: the few-groups gate, the heavy tuples and the splitters */
   const uint64_t m = 65536;
   int64_t *smp = (int64_t *)malloc(m * 2 * sizeof(int64_t));
   for (uint64_t j = 0; j < m; ++j) {
@@ -437,6 +427,35 @@ static uint64_t groupby_ranges(const orc_agg_spec *s, uint64_t cap, int64_t *out
   }
   g_sort_nk = nk;
   qsort(smp, m, 2 * sizeof(int64_t), cmp_tuple);
+  /* few groups, seen in the sample: every sampled tuple occurs at least twice (no more than
+   * 1/64 of them once) and there are few of them — the per-thread tables, without the sketch
+   * (whose binary-search inserts never stop below k distinct hashes: G = 1000 ran 4x slower
+   * through it) */
+  {
+    uint64_t d = 0, f1 = 0;
+    for (uint64_t j = 0; j < m;) {
+      uint64_t e = j + 1;
+      while (e < m && cmp_tuple(&smp[2 * j], &smp[2 * e]) == 0) ++e;
+      ++d;
+      f1 += e - j == 1;
+      j = e;
+    }
+    if (f1 * 64 <= d && d * 16 <= m) {
+      free(smp);
+      return UINT64_MAX - 1;
+    }
+  }
+  /* ---- distinct groups: a k-minimum-values sketch over every key tuple (one hashing pass;
+   * ~3 % error at k = 1024).  The strided sample's Chao1 estimate it replaces is a lower
+   * bound that skew breaks: Zipf-like keys over 4.6 M groups estimated ~1.3e5 and went to
+   * the per-thread tables, whose serial merge of millions of groups ran 3x slower than the
+   * ranges (VERDICT r5 item 7). */
+  const double gest = kmv_distinct(s, nt);
+  if (gest < 262144) {  /* (per-thread tables of <= ~2^18 groups stay cache-resident and merge fast:
+                          G = 1e5 ran 3.1e8 rows/s there vs 1.3e8 through the ranges) */
+    free(smp);
+    return UINT64_MAX - 1;
+  }
   /* ---- heavy tuples: a sample run of >= 1/nt of the sample is more rows than one thread's
    * share, and a key range holding it would leave its partition on one thread (skewed keys
    * ran 5x slower than uniform ones).  Each thread folds its chunk's rows of such a tuple in
