@@ -1492,9 +1492,11 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
   // Four streams: level 1 of every chunk back to back on the context's stream; each
   // chunk's aggregation on a second one as soon as its level 1 is done (it overlaps the
   // next chunk's level 1, so neither launch's tail idles the chip); its ordering on a third
-  // as soon as its aggregation is done (beside the next chunk's aggregation: in one stream
-  // the orderings held every later aggregation back, ~1.5 ms for the first chunk's at
-  // G = 1e7); its transfer on the fourth once the host has read the chunk's running total
+  // as soon as its aggregation is done; its transfer on the fourth once the host has read
+  // the chunk's running total.  (With the runtime's four hardware queues the third stream
+  // lands on the aggregation's queue, so orderings and aggregations still alternate; the
+  // ordering on a high-priority stream, a queue of its own, ran beside them and stretched
+  // all three: 20.4 vs 19.3 ms per G = 1e7 step, profiles/r06/groupby1e7/ab_order_priority.txt)
   if (!c->aux_stream) NUT_HIP(hipStreamCreateWithFlags(&c->aux_stream, hipStreamNonBlocking));
   if (!c->order_stream) NUT_HIP(hipStreamCreateWithFlags(&c->order_stream, hipStreamNonBlocking));
   hipStream_t ax = c->aux_stream, ox = c->order_stream;
