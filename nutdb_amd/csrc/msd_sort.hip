@@ -48,13 +48,14 @@ constexpr int MS_BITS = 9;                          // digit width of a scatter 
 constexpr int MS_BINS = 1 << MS_BITS;               // 512: MS_TILE / 512 = 28 keys (224 B) per digit per stage
 static_assert(MS_BINS <= MS_THREADS, "one scan thread per digit");
 // local-sort classes: threads x max items per thread (ms_local_kernel), by segment size.
-// The segments of a 1.25e9-key sort (~4768 keys) take class 1: 256 threads x 20 keys, three
-// workgroups per CU (51 KB of LDS each), one workgroup per segment — scripts/tune/
-// local_tune.hip, 262144 segments of 4768 keys: 5.14 ms vs 6.65 for round 4's persistent
-// 512 x 12 at two per CU (profiles/r05/sort/local_tune_sweep.log)
+// The segments of a 1.25e9-key sort (~4768 keys) take class 1: 512 threads x 10 keys, three
+// workgroups per CU (51 KB of LDS each: 24 waves, 72 VGPRs), one workgroup per segment —
+// scripts/tune/local_tune.hip, 262144 segments of 4768 keys: 4.65-4.67 ms vs 5.13-5.18 for
+// round 5's 256 x 20 (12 waves per CU) on the same boxes (profiles/r06/sort/local_tune_*.log;
+// round 5: 5.14 vs 6.65 for round 4's persistent 512 x 12 at two per CU)
 constexpr int LS_NCLS = 4;
 constexpr int LS_S_THREADS = 256, LS_S_ITEMS = 8;     // class 0: <= 2048 keys
-constexpr int LS_M_THREADS = 256, LS_M_ITEMS = 20;    // class 1: <= 5120 keys, 3 workgroups per CU
+constexpr int LS_M_THREADS = 512, LS_M_ITEMS = 10;    // class 1: <= 5120 keys, 3 workgroups per CU
 constexpr int LS_M2_THREADS = 512, LS_M2_ITEMS = 12;  // class 2: <= 6144 keys, 2 workgroups per CU
 constexpr int LS_L_THREADS = 1024, LS_L_ITEMS = 24;   // class 3: <= 24576 keys
 constexpr uint64_t LS_S_CAP = LS_S_THREADS * LS_S_ITEMS;
@@ -612,17 +613,18 @@ __device__ unsigned long long g_ms_stamp[8];
 #endif
 
 // SB_ / WS_ = 0: the product defaults (bucket bits by capacity, window stride LS_WS)
-template <int THREADS, int MAXK, int SB_ = 0, int WS_ = 0>
+template <int THREADS, int MAXK, int SB_ = 0, int WS_ = 0, int LK_ = 0>
 struct LocalCfg {
   static constexpr int WAVES = THREADS / kWave;
   static constexpr int CAP = THREADS * MAXK;
-  static constexpr int LDS_KEYS = CAP < 16384 ? CAP : 16384;  // 8-B keys per round
+  static constexpr int LDS_KEYS = LK_ ? LK_ : (CAP < 16384 ? CAP : 16384);  // 8-B keys per round
   // bucket bits (~1-6 keys each) and window stride.  The M class (6144 keys) takes 4096
   // buckets and windows of ~10 keys: scripts/tune/local_tune.hip -DLT_PLAIN on 262144
   // segments of 4768 keys, two runs: 6.53-6.57 ms vs 6.81-6.85 for 2048 buckets / stride 12
   // (profiles/r04/sort/local_tune_plain.log)
-  // (256 x 20: 2048 buckets keep its LDS at 51 KB, three workgroups per CU)
-  static constexpr int SB = SB_ ? SB_ : (CAP > 4096 ? (THREADS >= 512 ? 12 : 11) : (CAP > 2048 ? 11 : 9));
+  // (<= 5120 keys: 2048 buckets keep the LDS at 51 KB, three workgroups per CU; 512 x 10 at
+  // 4096 buckets and two per CU took 6.03 vs 4.66 ms)
+  static constexpr int SB = SB_ ? SB_ : (CAP > 5120 ? 12 : CAP > 2048 ? 11 : 9);
   static constexpr int WS = WS_ ? WS_ : (CAP > 4096 && CAP <= 8192 ? 10 : LS_WS);
   static constexpr int NB = 1 << SB;
   static constexpr int BPT = NB / THREADS;  // buckets per thread in the scan
@@ -736,10 +738,18 @@ __device__ __forceinline__ void wave_bitonic32_multi(uint64_t (&v)[NR], int lane
   cx64<1, 1, NR>(v, lane);
 }
 
-template <int THREADS, int MAXK, bool PREFETCH, int SB_ = 0, int WS_ = 0>
-__global__ __launch_bounds__(THREADS, 4) void ms_local_kernel(MsBufs bf, const MsSeg *__restrict__ segs, uint32_t nseg,
+// waves per SIMD the register budget must allow: four, or as many as the workgroups that
+// LDS lets share a CU bring (at most eight) for the classes that run more than four
+template <int THREADS, int MAXK, int SB_, int WS_, int LK_>
+constexpr int ls_min_waves() {
+  using C = LocalCfg<THREADS, MAXK, SB_, WS_, LK_>;
+  constexpr int w = (163840 / C::BYTES) * C::WAVES / 4;
+  return (LK_ || (THREADS == 512 && MAXK <= 10) || (THREADS == 1024 && MAXK <= 5)) && w > 4 ? (w < 8 ? w : 8) : 4;
+}
+template <int THREADS, int MAXK, bool PREFETCH, int SB_ = 0, int WS_ = 0, int LK_ = 0>
+__global__ __launch_bounds__(THREADS, (ls_min_waves<THREADS, MAXK, SB_, WS_, LK_>())) void ms_local_kernel(MsBufs bf, const MsSeg *__restrict__ segs, uint32_t nseg,
                                                            uint64_t flip, uint32_t *__restrict__ fb) {
-  using C = LocalCfg<THREADS, MAXK, SB_, WS_>;
+  using C = LocalCfg<THREADS, MAXK, SB_, WS_, LK_>;
   constexpr int WAVES = C::WAVES, NB = C::NB, SB = C::SB, LS_WS = C::WS;
   __shared__ __attribute__((aligned(16))) char lds[C::BYTES];
   uint64_t *s_keys = (uint64_t *)lds;

@@ -67,9 +67,9 @@ struct Ctx {
   hipEvent_t e0, e1;
 };
 
-template <int T, int K, int SB, int WS, bool PF = true>
+template <int T, int K, int SB, int WS, bool PF = true, int LK = 0>
 static void run(Ctx &c, const char *name, int stop = 0) {
-  auto kern = nut::ms_local_kernel<T, K, PF, SB, WS>;
+  auto kern = nut::ms_local_kernel<T, K, PF, SB, WS, LK>;
   int per_cu = 1, ncu = 256;
   CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, T, 0));
   CK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
@@ -146,21 +146,12 @@ int main(int argc, char **argv) {
     printf("%-28s                 %7.3f ms  %6.0f GB/s\n", "copy (HBM floor)", best, 16.0 * c.n / best / 1e6);
   }
   printf("segments %u x %u keys\n", c.nseg, c.seglen);
-  run<256, 20, 0, 0, false>(c, "product <256,20> 1 WG/segment");
+  run<nut::LS_M_THREADS, nut::LS_M_ITEMS, 0, 0, false>(c, "product M class 1 WG/segment");
   if (argc > 3) return 0;  // profiling runs: the product variant only
-  run<512, 12, 0, 0>(c, "round-4 <512,12> persistent");
-  run<256, 20, 11, 10>(c, "<256,20> SB11 WS10");
-  run<256, 20, 11, 10, false>(c, "<256,20> SB11 WS10 no prefetch");
-  run<256, 20, 12, 10>(c, "<256,20> SB12 WS10");
-  run<256, 20, 11, 8>(c, "<256,20> SB11 WS8");
-  run<256, 20, 11, 12>(c, "<256,20> SB11 WS12");
-  run<256, 20, 11, 11>(c, "<256,20> SB11 WS11");
-  run<256, 24, 11, 10>(c, "<256,24> SB11 WS10");
-  run<256, 20, 10, 10>(c, "<256,20> SB10 WS10");
-  run<512, 12, 0, 0, false>(c, "<512,12> no prefetch, grid=nseg");
-  run<512, 10, 12, 10>(c, "<512,10> SB12 WS10");
-  run<256, 20, 11, 10>(c, "<256,20> SB11 WS10 again");
-  run<512, 12, 0, 0>(c, "default again (order check)");
+  run<256, 20, 11, 10, false>(c, "round-5 <256,20> SB11 WS10");
+  run<512, 10, 11, 10, false>(c, "<512,10> SB11 WS10 1 WG/seg");
+  run<1024, 5, 11, 10, false>(c, "<1024,5> SB11 WS10 1 WG/seg");
+  run<256, 20, 11, 10, false, 3072>(c, "<256,20> SB11 WS10 LK3072");
   return 0;
   run<512, 12, 0, 0>(c, "default: load only", 1);
   run<512, 12, 0, 0>(c, "default: + ranks/stage", 3);
