@@ -339,9 +339,11 @@ def test_sort_golden(golden, ex):
     assert pos_hash(out) == case["pos_hash"]
 
 
-@pytest.mark.parametrize("n", [0, 1, 2, 3, 63, 64, 65, 2048, 2049, 4095, 4096, 4097, 8192, 8193, 12289,
-                               32767, 32768, 32769, 65537, 1_000_003, 9_000_011])
+@pytest.mark.parametrize("n", [0, 1, 2, 3, 63, 64, 65, 2048, 2049, 4095, 4096, 4097, 5119, 5120, 5121, 6144, 6145,
+                               8192, 8193, 12289, 24576, 24577, 32767, 32768, 32769, 65537, 1_000_003, 9_000_011])
 def test_sort_sizes_vs_oracle(ex, orc, n):
+    """Every local-sort class edge (msd_sort.hip ls_class: S <= 2048, M <= 5120 as 512 x 10,
+    M2 <= 6144, L <= 24576 keys in one segment) and the multi-level sizes above them."""
     col = orc.gen_column(1, 0x50, n)
     got = host(ex.sort_i64(dev(col, ex)))
     assert np.array_equal(got, orc.sort_i64(col))
