@@ -164,3 +164,18 @@ def test_groupby_heavy_tuples_split_is_bitwise(orc, nthreads, share):
     a = orc.groupby([key], aggs, values=[v, iv], nthreads=nthreads, **kw)
     b = orc.groupby([key], aggs, values=[v, iv], nthreads=nthreads, method="tables", **kw)
     assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+
+
+@pytest.mark.parametrize("groups", [6, 1000, 4096, 50_000])
+def test_groupby_few_groups_gate_is_bitwise(orc, groups):
+    """The few-groups gate ahead of the k-minimum-values sketch (every sampled key seen at
+    least twice: the per-thread tables without hashing every row) and the sketch's path
+    just above it give the per-thread-table merge's words bit for bit."""
+    n = (1 << 22) + 5
+    key = orc.gen_column(2, 0x81, n, a=groups)
+    v = orc.gen_column(4, 0x82, n)
+    aggs = [(0, 0, (0,)), (1, 0, ())]
+    a = orc.groupby([key], aggs, values=[v], nthreads=4)
+    b = orc.groupby([key], aggs, values=[v], nthreads=4, method="tables")
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+    assert len(a[0]) <= groups
