@@ -1336,14 +1336,16 @@ nut_status groupby_ordered(nut_ctx *c, const nut_agg_spec *s, uint64_t group_hin
   const uint64_t acap1 = b2rows - ovf1 - 2 * GP_TILE;  // level 1's arena: rows [ovf1, ovf1 + acap1) of B2
   const uint64_t nparts = (uint64_t)np0 * nb1;
   if (nparts == 0) return decline(NUT_GB_DECLINE_CAPACITY);  // (no kept row reached level 0: not reached)
-  // chunks of level-0 partitions (in key order) shrinking — 3/8, 1/4, 3/16, 1/8, 1/16: a
-  // chunk's transfer (~0.4x its compute) hides behind the next, smaller chunk, and only the
-  // last 1/16 crosses after the work; each launch costs a tail, so few chunks.  The first
-  // chunk at 3/8 instead of 1/2 starts the transfers earlier: same-box A/Bs on two boxes,
-  // Zipf-like keys 17.88-17.90 vs 18.33-18.76 and 18.37-18.58 vs 19.12-19.22 ms, uniform
-  // 18.21-18.24 vs 18.34-18.62 and 20.75-21.16 vs 20.90 (profiles/r06/groupby1e7/ab_chunks.txt)
+  // chunks of level-0 partitions (in key order) shrinking — 3/8, 1/4, 3/16, 1/16, 1/16,
+  // 1/16: a chunk's transfer (~0.4x its compute) hides behind the next, smaller chunk, and
+  // only the last 1/16 crosses after the work; each launch costs a tail, so few chunks.
+  // The first chunk at 3/8 instead of 1/2 starts the transfers earlier: same-box A/Bs on two
+  // boxes, Zipf-like keys 17.88-17.90 vs 18.33-18.76 and 18.37-18.58 vs 19.12-19.22 ms,
+  // uniform 18.21-18.24 vs 18.34-18.62 and 20.75-21.16 vs 20.90; three 1/16 chunks at the
+  // end instead of 1/8 + 1/16, a third box: Zipf-like 18.42-18.56 vs 19.43-19.59, uniform
+  // 20.18 vs 20.18-20.23 (profiles/r06/groupby1e7/ab_chunks.txt)
   std::vector<uint32_t> cb{0};
-  for (uint32_t f : {6u, 10u, 13u, 15u, 16u}) {
+  for (uint32_t f : {6u, 10u, 13u, 14u, 15u, 16u}) {
     const uint32_t e1 = (uint32_t)((uint64_t)np0 * f / 16);
     if (e1 > cb.back()) cb.push_back(e1);
   }
